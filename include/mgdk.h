@@ -1,0 +1,174 @@
+/*
+ * mgdk.h -- C ABI of the MI355X-native GDK column-operator kernel
+ * (libmgdk.so).
+ *
+ * Each entry point replaces one GDK function of the reference MonetDB
+ * v11.52.0 and keeps its argument meaning, result properties, ownership and
+ * error behaviour; the BAT descriptor is a flat struct whose heaps live in HBM.
+ * A GDK maintainer binds these from the existing BAT* wrappers (see
+ * INTEGRATION.md): marshal BAT -> mgdk_bat (device heap), call, wrap the
+ * result.  No torch types, no C++ in the signatures.
+ *
+ * Conventions (gdk/gdk.h:1710,1947; gdk/gdk_bbp.c:3149-3183):
+ *   - functions returning a BAT return a NEW transient BAT with one reference
+ *     (release with mgdk_BBPunfix) or NULL after setting the thread-local
+ *     error buffer (mgdk_GDKerrbuf), with the reference's SQLSTATE-prefixed
+ *     messages ("22003!overflow in calculation ...");
+ *   - functions returning int return 0 (GDK_SUCCEED) or -1 (GDK_FAIL);
+ *   - inputs are borrowed; the library is thread safe, every calling thread
+ *     gets its own HIP stream; results are complete when a call returns.
+ */
+#ifndef MGDK_H
+#define MGDK_H
+
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef uint64_t mgdk_oid;          /* gdk/gdk.h oid (SIZEOF_OID 8) */
+typedef uint64_t mgdk_BUN;
+
+/* GDK type ids, gdk/gdk.h:428-451 (HAVE_HGE build) */
+enum {
+	MGDK_void = 0, MGDK_msk = 1, MGDK_bit = 2, MGDK_bte = 3, MGDK_sht = 4,
+	MGDK_int = 5, MGDK_oid = 6, MGDK_flt = 8, MGDK_dbl = 9, MGDK_lng = 10,
+	MGDK_hge = 11, MGDK_date = 12, MGDK_str = 16,
+};
+
+#define MGDK_OID_NIL ((mgdk_oid) 1 << 63)   /* oid_nil */
+
+/* BAT descriptor: the column-side fields of gdk/gdk.h:712-804 (COLrec, BAT)
+ * that the operators read or set.  theap/tvheap are HBM pointers. */
+typedef struct mgdk_bat {
+	int32_t ttype;          /* tail type (MGDK_*) */
+	int32_t twidth;         /* bytes per tail value; str: offset width 1/2/4/8 */
+	mgdk_BUN count;         /* BATcount */
+	mgdk_oid hseqbase;      /* head sequence base */
+	mgdk_oid tseqbase;      /* void: first oid; oid/other: MGDK_OID_NIL */
+	void *theap;            /* tail values in HBM (NULL for void) */
+	void *tvheap;           /* str: string heap in HBM (offsets are into it) */
+	uint64_t tvheapsize;
+	uint8_t tsorted, trevsorted, tkey, tnonil, tnil;
+	uint8_t _pad[3];
+	void *priv;             /* runtime-owned */
+} mgdk_bat;
+
+/* ---- runtime ---------------------------------------------------------- */
+int mgdk_init(int device);                       /* select HIP device */
+const char *mgdk_GDKerrbuf(void);                /* gdk.h:1947 GDKerrbuf */
+void mgdk_GDKclrerr(void);
+int mgdk_sync(void);                             /* drain calling thread's stream */
+void *mgdk_stream(void);                         /* calling thread's hipStream_t */
+uint64_t mgdk_mem_cursize(void);                 /* gdk_utils.c:1636 GDKmem_cursize */
+void mgdk_mem_release_cache(void);
+
+/* per-kernel timing with hipEvents on the library stream (ALGO tracing,
+ * gdk/gdk_private.h:331): enable, then read totals per kernel name */
+void mgdk_prof_enable(int on);
+int mgdk_prof_get(const char *kernel, double *total_ms, uint64_t *launches);
+void mgdk_prof_reset(void);
+
+/* ---- BAT lifecycle (gdk/gdk_bat.c:292 COLnew, :298 BATdense,
+ *      gdk/gdk_bbp.c:3149 BBPunfix, gdk/gdk_batop.c:1825 BATslice) ---- */
+mgdk_bat *mgdk_COLnew(mgdk_oid hseq, int tt, mgdk_BUN cap);
+mgdk_bat *mgdk_BATdense(mgdk_oid hseq, mgdk_oid tseq, mgdk_BUN cnt);
+mgdk_bat *mgdk_BATconstant(mgdk_oid hseq, int tt, const void *val, mgdk_BUN cnt);
+mgdk_bat *mgdk_BATslice(mgdk_bat *b, mgdk_BUN lo, mgdk_BUN hi);
+void mgdk_BBPunfix(mgdk_bat *b);
+/* host <-> HBM staging (the heap upload a GDK adaptor does once per BAT) */
+int mgdk_BATupload(mgdk_bat *b, const void *host, mgdk_BUN n);
+int mgdk_BATdownload(const mgdk_bat *b, void *host);
+int mgdk_BATsetvheap(mgdk_bat *b, const void *host, uint64_t size);
+int mgdk_BATdownload_vheap(const mgdk_bat *b, void *host);
+
+/* ---- select (gdk/gdk.h:2245-2246; gdk/gdk_select.c:1342, :2103) ------- */
+mgdk_bat *mgdk_BATselect(mgdk_bat *b, mgdk_bat *s, const void *tl, const void *th,
+			 bool li, bool hi, bool anti, bool nil_matches);
+mgdk_bat *mgdk_BATthetaselect(mgdk_bat *b, mgdk_bat *s, const void *val, const char *op);
+
+/* ---- project (gdk/gdk.h:2273; gdk/gdk_project.c:857) ------------------ */
+mgdk_bat *mgdk_BATproject(mgdk_bat *l, mgdk_bat *r);
+
+/* ---- calc (gdk/gdk_calc.h:36-44; gdk_calc_addsub.c:1480,1549,3166,3225,3280;
+ *      gdk_calc_mul.c:2085,2092).  Constants are given as (pointer, type). */
+mgdk_bat *mgdk_BATcalcadd(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2, int tp);
+mgdk_bat *mgdk_BATcalcsub(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2, int tp);
+mgdk_bat *mgdk_BATcalcmul(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2, int tp);
+mgdk_bat *mgdk_BATcalcaddcst(mgdk_bat *b, const void *v, int vt, mgdk_bat *s, int tp);
+mgdk_bat *mgdk_BATcalcsubcst(mgdk_bat *b, const void *v, int vt, mgdk_bat *s, int tp);
+mgdk_bat *mgdk_BATcalcmulcst(mgdk_bat *b, const void *v, int vt, mgdk_bat *s, int tp);
+mgdk_bat *mgdk_BATcalccstadd(const void *v, int vt, mgdk_bat *b, mgdk_bat *s, int tp);
+mgdk_bat *mgdk_BATcalccstsub(const void *v, int vt, mgdk_bat *b, mgdk_bat *s, int tp);
+mgdk_bat *mgdk_BATcalccstmul(const void *v, int vt, mgdk_bat *b, mgdk_bat *s, int tp);
+
+/* ---- aggregates (gdk/gdk_calc.h:127-147; gdk/gdk_aggr.c:900,1018,1996,3069,
+ *      3487-3844) --------------------------------------------------------- */
+int mgdk_BATsum(void *res, int tp, mgdk_bat *b, mgdk_bat *s, bool skip_nils, bool nil_if_empty);
+mgdk_bat *mgdk_BATgroupsum(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils);
+mgdk_bat *mgdk_BATgroupcount(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils);
+int mgdk_BATgroupavg3(mgdk_bat **avgp, mgdk_bat **remp, mgdk_bat **cntp,
+		      mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, bool skip_nils);
+mgdk_bat *mgdk_BATgroupmin(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils);
+mgdk_bat *mgdk_BATgroupmax(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils);
+
+/* ---- group (gdk/gdk.h:1447; gdk/gdk_group.c:1347) --------------------- */
+int mgdk_BATgroup(mgdk_bat **groups, mgdk_bat **extents, mgdk_bat **histo,
+		  mgdk_bat *b, mgdk_bat *s, mgdk_bat *g, mgdk_bat *e, mgdk_bat *h);
+
+/* ---- join, hash path (gdk/gdk.h:2266; gdk/gdk_join.c:4451, :2900) ----- */
+int mgdk_BATjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r,
+		 mgdk_bat *sl, mgdk_bat *sr, bool nil_matches, mgdk_BUN estimate);
+
+/* ---- sort (gdk/gdk.h:1526; gdk/gdk_batop.c:2342) ---------------------- */
+int mgdk_BATsort(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups,
+		 mgdk_bat *b, mgdk_bat *o, mgdk_bat *g, bool reverse, bool nilslast, bool stable);
+
+/* ---- window bounds (gdk/gdk_analytic.h:27-30;
+ *      gdk/gdk_analytic_bounds.c:1440) ------------------------------------- */
+int mgdk_GDKanalyticalwindowbounds(mgdk_bat *r, mgdk_bat *b, mgdk_bat *p, mgdk_bat *l,
+				   const void *bound, int tp1, int tp2, int unit,
+				   bool preceding, mgdk_oid first_half);
+
+/* ---- fused MAL pipelines (one pass over the lineitem columns; same
+ *      results as the op-at-a-time plans of SURVEY.md §3.2/§3.3) --------- */
+/* Q6: sum(price*disc) over rows with d0 <= shipdate < d1, dlo <= disc <= dhi,
+ * qty < qmax; result hge written to *revenue (16 bytes). */
+int mgdk_q6_fused(mgdk_bat *shipdate, mgdk_bat *discount, mgdk_bat *quantity,
+		  mgdk_bat *extendedprice, int32_t d0, int32_t d1, int64_t dlo,
+		  int64_t dhi, int64_t qmax, void *revenue);
+typedef struct mgdk_q1row {
+	uint8_t returnflag, linestatus, _pad[6];   /* str heap offsets */
+	int64_t sum_qty[2], sum_base_price[2], sum_disc_price[2], sum_charge[2]; /* hge lo,hi */
+	int64_t sum_disc[2];
+	int64_t count_order;
+	mgdk_oid first_row;
+} mgdk_q1row;
+/* Q1 groups (first-occurrence numbering, BATgroup semantics); returns the
+ * number of groups in *ngroups (<= maxgroups). */
+int mgdk_q1_fused(mgdk_bat *shipdate, mgdk_bat *returnflag, mgdk_bat *linestatus,
+		  mgdk_bat *quantity, mgdk_bat *extendedprice, mgdk_bat *discount,
+		  mgdk_bat *tax, int32_t dmax, mgdk_q1row *rows, int maxgroups, int *ngroups);
+
+/* the same two plans run operator by operator through the entry points
+ * above (what MonetDB's interpreter executes without the fused rewrite) */
+int mgdk_q6_opatatime(mgdk_bat *shipdate, mgdk_bat *discount, mgdk_bat *quantity,
+		      mgdk_bat *extendedprice, int32_t d0, int32_t d1, int64_t dlo,
+		      int64_t dhi, int64_t qmax, void *revenue);
+int mgdk_q1_opatatime(mgdk_bat *shipdate, mgdk_bat *returnflag, mgdk_bat *linestatus,
+		      mgdk_bat *quantity, mgdk_bat *extendedprice, mgdk_bat *discount,
+		      mgdk_bat *tax, int32_t dmax, mgdk_q1row *rows, int maxgroups, int *ngroups);
+
+/* ---- synthetic TPC-H lineitem generated directly in HBM (same values as
+ *      oracle/tpch_gen.c); cols: shipdate(date), quantity, extendedprice,
+ *      discount, tax (lng), returnflag, linestatus (str, 1-byte offsets) -- */
+int mgdk_tpch_lineitem(uint64_t seed, uint64_t row0, uint64_t n, uint64_t sf_parts,
+		       mgdk_bat **cols /* [7] */);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,745 @@
+// aggr.hip -- BATsum and the grouped aggregates on the MI355X.
+//
+// Integer sums are exact: every lane accumulates a 128-bit sum, the partials
+// are combined with 64-bit atomics on the two halves (the carry of each low
+// add is derived from the value it returned, so the 128-bit total is exact
+// and independent of arrival order -- results are bitwise reproducible).
+// The reference checks overflow after every add (ADDI_WITH_CHECK,
+// gdk/gdk_aggr.c:429-705); a prefix can only leave the result type's range
+// if count * max|v| exceeds it, which the kernel also measures; only then a
+// one-workgroup ordered pass re-evaluates the prefixes to decide exactly.
+//   BATsum       gdk/gdk_aggr.c:1018 (dosum :708; int->dbl via BATcalcavg :1112-1156)
+//   BATgroupsum  :900 (nil_if_empty; the "nil before first value" rule :497-527)
+//   BATgroupcount :3069, BATgroupavg3 :1996 (rounding :2070-2095),
+//   BATgroupmin/max :3487-3844, BATgroupaggrinit :65
+#include <cmath>
+#include <vector>
+
+#include "mgdk_internal.h"
+
+using namespace mgdk;
+
+namespace {
+
+__device__ __forceinline__ hge
+ldv(const void *base, int w, BUN p, bool &isnil)
+{
+	switch (w) {
+	case 1: { int8_t v = ((const int8_t *) base)[p]; isnil = v == INT8_MIN; return v; }
+	case 2: { int16_t v = ((const int16_t *) base)[p]; isnil = v == INT16_MIN; return v; }
+	case 4: { int32_t v = ((const int32_t *) base)[p]; isnil = v == INT32_MIN; return v; }
+	case 8: { int64_t v = ((const int64_t *) base)[p]; isnil = v == INT64_MIN; return v; }
+	default: { hge v = ((const hge *) base)[p]; isnil = is_nil(v); return v; }
+	}
+}
+
+__device__ __forceinline__ void
+atomic_add128(unsigned long long *lohi, hge v)
+{
+	const unsigned long long lo = (unsigned long long) (uhge) v;
+	const unsigned long long hi = (unsigned long long) ((uhge) v >> 64);
+	unsigned long long old = atomicAdd(&lohi[0], lo);
+	unsigned long long carry = (old + lo) < old ? 1ull : 0ull;
+	if (hi + carry)
+		atomicAdd(&lohi[1], hi + carry);
+}
+
+__device__ __forceinline__ uint64_t
+absbits(hge v)
+{
+	// ceil-ish magnitude class: top 64 bits of |v| (0 for |v| < 2^64) and low
+	uhge a = v < 0 ? (uhge) 0 - (uhge) v : (uhge) v;
+	return (a >> 64) ? (uint64_t) (a >> 64) | (1ull << 63) : (uint64_t) a >> 1;
+}
+
+// ---- BATsum -----------------------------------------------------------------
+struct SumOut {
+	unsigned long long sum[2];     // 128-bit total (two's complement)
+	unsigned long long cnt;        // non-nil values
+	unsigned long long firstnil;   // first nil position (candidate index)
+	unsigned long long maxabs;     // magnitude class (absbits)
+};
+
+__global__ __launch_bounds__(256) void
+k_sum(const void *base, int w, bool dense, oid off, const oid *oids, oid hseq, BUN n, SumOut *o)
+{
+	hge s = 0;
+	unsigned long long cnt = 0, firstnil = ~0ull, mx = 0;
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		BUN p = dense ? off + i : oids[i] - hseq;
+		bool isnil;
+		hge v = ldv(base, w, p, isnil);
+		if (isnil) {
+			if (i < firstnil)
+				firstnil = i;
+			continue;
+		}
+		s += v;
+		cnt++;
+		unsigned long long a = absbits(v);
+		mx = a > mx ? a : mx;
+	}
+	for (int k = 32; k > 0; k >>= 1) {
+		unsigned long long lo = __shfl_xor((unsigned long long) (uhge) s, k);
+		unsigned long long hi = __shfl_xor((unsigned long long) ((uhge) s >> 64), k);
+		s += (hge) (((uhge) hi << 64) | lo);
+		cnt += __shfl_xor(cnt, k);
+		unsigned long long t = __shfl_xor(firstnil, k);
+		firstnil = t < firstnil ? t : firstnil;
+		t = __shfl_xor(mx, k);
+		mx = t > mx ? t : mx;
+	}
+	if (__lane_id() == 0) {
+		atomic_add128(o->sum, s);
+		if (cnt)
+			atomicAdd(&o->cnt, cnt);
+		if (firstnil != ~0ull)
+			atomicMin(&o->firstnil, firstnil);
+		if (mx)
+			atomicMax(&o->maxabs, mx);
+	}
+}
+
+// ordered prefix check for the rare case where overflow is possible: one
+// workgroup, each lane a contiguous chunk, then an ordered combine of
+// (sum, max prefix, min prefix).  Uses a 192-bit-safe formulation: values are
+// at most 128 bits and we stop at the first overflow, so partial sums are
+// kept as (hi: int64 guard, 128-bit) via a per-chunk scan.
+__global__ __launch_bounds__(256) void
+k_sum_ordered(const void *base, int w, bool dense, oid off, const oid *oids, oid hseq, BUN n,
+	      hge max, unsigned long long *ovf)
+{
+	__shared__ hge s_sum[256], s_mx[256], s_mn[256];
+	__shared__ int s_has[256], s_bad[256];
+	const BUN chunk = (n + 255) / 256;
+	const BUN a = threadIdx.x * chunk, e = a + chunk < n ? a + chunk : n;
+	hge s = 0, mx = 0, mn = 0;
+	int has = 0, bad = 0;
+	for (BUN i = a; i < e; i++) {
+		BUN p = dense ? off + i : oids[i] - hseq;
+		bool isnil;
+		hge v = ldv(base, w, p, isnil);
+		if (isnil)
+			continue;
+		uhge r = (uhge) s + (uhge) v;
+		hge rs = (hge) r;
+		if (((s < 0) == (v < 0)) && ((rs < 0) != (s < 0)))
+			bad = 1;   // the chunk's own running sum left 128 bits: overflow for sure
+		s = rs;
+		if (!has) { mx = mn = s; has = 1; }
+		else { mx = s > mx ? s : mx; mn = s < mn ? s : mn; }
+	}
+	s_sum[threadIdx.x] = s;
+	s_mx[threadIdx.x] = mx;
+	s_mn[threadIdx.x] = mn;
+	s_has[threadIdx.x] = has;
+	s_bad[threadIdx.x] = bad;
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		// chunk-local overflow of the 128-bit running sum only matters if
+		// the true prefix also overflows, which it then does: any chunk
+		// prefix beyond 2^127 plus a prefix sum below max is beyond max?
+		// Not in general -- combine exactly with a 192-bit accumulator.
+		__int128 acc_lo = 0;
+		long long acc_hi = 0;   // acc = acc_hi * 2^128 + (uhge) acc_lo, signed
+		bool over = false;
+		for (int t = 0; t < 256 && !over; t++) {
+			if (s_bad[t]) { over = true; break; }
+			if (!s_has[t])
+				continue;
+			// test base + mx and base + mn against [-max, max]
+			for (int q = 0; q < 2 && !over; q++) {
+				hge x = q ? s_mn[t] : s_mx[t];
+				uhge lo = (uhge) acc_lo + (uhge) x;
+				long long hi = acc_hi + ((lo < (uhge) acc_lo) ? 1 : 0) + (x < 0 ? -1 : 0);
+				// value = hi*2^128 + lo (lo unsigned)
+				if (hi == 0 && (hge) lo >= 0) { if ((hge) lo > max) over = true; }
+				else if (hi == -1 && (hge) lo < 0) { if ((hge) lo < -max) over = true; }
+				else over = true;
+			}
+			uhge lo = (uhge) acc_lo + (uhge) s_sum[t];
+			acc_hi = acc_hi + ((lo < (uhge) acc_lo) ? 1 : 0) + (s_sum[t] < 0 ? -1 : 0);
+			acc_lo = (hge) lo;
+		}
+		*ovf = over ? 1 : 0;
+	}
+}
+
+hge
+tmax(int tp)
+{
+	switch (basetype(tp)) {
+	case MGDK_bte: return INT8_MAX;
+	case MGDK_sht: return INT16_MAX;
+	case MGDK_int: return INT32_MAX;
+	case MGDK_lng: return INT64_MAX;
+	default: return (hge) (((uhge) 1 << 127) - 1);
+	}
+}
+
+bool
+int_type(int t)
+{
+	t = basetype(t);
+	return t == MGDK_bte || t == MGDK_sht || t == MGDK_int || t == MGDK_lng || t == MGDK_hge;
+}
+
+void
+put_res(void *res, int tp, hge v, bool nil)
+{
+	switch (basetype(tp)) {
+	case MGDK_bte: *(int8_t *) res = nil ? INT8_MIN : (int8_t) v; break;
+	case MGDK_sht: *(int16_t *) res = nil ? INT16_MIN : (int16_t) v; break;
+	case MGDK_int: *(int32_t *) res = nil ? INT32_MIN : (int32_t) v; break;
+	case MGDK_lng: *(int64_t *) res = nil ? INT64_MIN : (int64_t) v; break;
+	default: { hge x = nil ? (hge) ((uhge) 1 << 127) : v; memcpy(res, &x, 16); break; }
+	}
+}
+
+// magnitude bound from absbits class: returns an upper bound of max|v| as
+// a long double (enough to decide "could a prefix overflow")
+long double
+mag_bound(unsigned long long cls)
+{
+	if (cls >> 63)
+		return ldexpl((long double) ((cls & ~(1ull << 63)) + 1), 64);
+	return ((long double) cls + 1) * 2;
+}
+
+}  // namespace
+
+extern "C" int
+mgdk_BATsum(void *res, int tp, mgdk_bat *b, mgdk_bat *s, bool skip_nils, bool nil_if_empty)
+{
+	if (b == nullptr || res == nullptr) {
+		seterr("BATsum: NULL argument");
+		return -1;
+	}
+	if (!int_type(b->ttype) || !(int_type(tp) || tp == MGDK_dbl || tp == MGDK_flt)) {
+		seterr("type combination (sum(%s)->%s) not supported.\n", atomname(b->ttype), atomname(tp));
+		return -1;
+	}
+	ProfScope prof("sum");
+	Cand ci;
+	if (cand_init(&ci, b, s) < 0)
+		return -1;
+	SumOut *o = (SumOut *) meta_buf();
+	SumOut init = {{0, 0}, 0, ~0ull, 0};
+	if (!hip_ok(hipMemcpyAsync(o, &init, sizeof(init), hipMemcpyHostToDevice, stream()), "memcpy"))
+		return -1;
+	const oid off = ci.dense ? ci.seq - b->hseqbase : 0;
+	if (ci.n)
+		hipLaunchKernelGGL(k_sum, dim3(grid_for(ci.n, 256 * 8, 256 * 16)), dim3(256), 0, stream(),
+				   b->theap, b->twidth, ci.dense, off, ci.oids, b->hseqbase, ci.n, o);
+	SumOut *h = (SumOut *) pinned(sizeof(SumOut));
+	if (h == nullptr || !hip_ok(hipMemcpyAsync(h, o, sizeof(SumOut), hipMemcpyDeviceToHost, stream()), "memcpy") ||
+	    !sync())
+		return -1;
+	const hge total = (hge) (((uhge) h->sum[1] << 64) | h->sum[0]);
+	const BUN cnt = h->cnt;
+	if (tp == MGDK_dbl || tp == MGDK_flt) {
+		// integers into floating point: exact average times count
+		// (gdk_aggr.c:1112-1156, BATcalcavg :2905-2960 with a hge sum)
+		double avg;
+		bool nil = false;
+		if (cnt == 0) {
+			nil = nil_if_empty;
+			avg = 0;
+		} else {
+			avg = (double) total / (double) cnt;
+		}
+		if (cnt < ci.n && !skip_nils)
+			nil = true;
+		if (tp == MGDK_dbl)
+			*(double *) res = nil ? __builtin_nan("") : avg * (double) cnt;
+		else
+			*(float *) res = nil ? __builtin_nanf("") : (float) avg * cnt;
+		return 0;
+	}
+	const hge max = tmax(tp);
+	const BUN firstnil = (!skip_nils && h->firstnil != ~0ull) ? h->firstnil : ci.n;
+	// could any prefix within [0, firstnil) leave [-max, max]?
+	long double bound = mag_bound(h->maxabs) * (long double) cnt;
+	bool maybe = bound > (long double) max;
+	if (maybe) {
+		unsigned long long *ov = (unsigned long long *) o;
+		hipLaunchKernelGGL(k_sum_ordered, dim3(1), dim3(256), 0, stream(), b->theap, b->twidth, ci.dense, off,
+				   ci.oids, b->hseqbase, firstnil, max, ov);
+		unsigned long long *hv = (unsigned long long *) pinned(16);
+		if (!hip_ok(hipMemcpyAsync(hv, ov, 8, hipMemcpyDeviceToHost, stream()), "memcpy") || !sync())
+			return -1;
+		if (*hv) {
+			seterr("22003!overflow in sum aggregate.\n");
+			return -1;
+		}
+	}
+	if (firstnil < ci.n) {
+		put_res(res, tp, 0, true);
+		return 0;
+	}
+	if (cnt == 0) {
+		put_res(res, tp, 0, nil_if_empty);
+		return 0;
+	}
+	put_res(res, tp, total, false);
+	return 0;
+}
+
+// ---- grouped aggregates ------------------------------------------------------
+namespace {
+
+// per group accumulators, laid out struct-of-arrays in global memory
+struct GAcc {
+	unsigned long long *sum;      // [2*ngrp] 128-bit sums
+	unsigned long long *cnt;      // [ngrp] non-nil values (or all rows)
+	unsigned long long *firstval; // [ngrp] first non-nil candidate index
+	unsigned long long *lastnil;  // [ngrp] last nil candidate index + 1 (0 = none)
+	long long *mn, *mx;           // [ngrp] min / max (lng-representable types)
+	unsigned long long maxabs;    // magnitude class over all values
+};
+
+enum { AGG_SUM = 1, AGG_CNT = 2, AGG_POS = 4, AGG_MINMAX = 8 };
+
+// K > 0: few groups -> per-lane register accumulators, one flush per wave
+template <int K>
+__global__ __launch_bounds__(256) void
+k_gaggr(const void *base, int w, oid off, const oid *gids, oid gseq, oid gmin, BUN ngrp, BUN n,
+	int what, bool count_all, GAcc acc, unsigned long long *maxabs)
+{
+	hge s[K > 0 ? K : 1];
+	unsigned long long c[K > 0 ? K : 1];
+	if constexpr (K > 0) {
+#pragma unroll
+		for (int k = 0; k < K; k++) { s[k] = 0; c[k] = 0; }
+	}
+	unsigned long long mx = 0;
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		oid g = gids ? gids[i] : gseq + i;
+		if (g < gmin || g - gmin >= ngrp)
+			continue;
+		BUN gi = g - gmin;
+		bool isnil;
+		hge v = ldv(base, w, off + i, isnil);
+		if (isnil) {
+			if (what & AGG_POS)
+				atomicMax(&acc.lastnil[gi], (unsigned long long) i + 1);
+			if (count_all) {
+				if constexpr (K > 0) {
+#pragma unroll
+					for (int k = 0; k < K; k++) c[k] += gi == (BUN) k;
+				} else {
+					atomicAdd(&acc.cnt[gi], 1ull);
+				}
+			}
+			continue;
+		}
+		unsigned long long a = absbits(v);
+		mx = a > mx ? a : mx;
+		if (what & AGG_POS) {
+			unsigned long long fv = acc.firstval[gi];
+			if (i < fv)
+				atomicMin(&acc.firstval[gi], (unsigned long long) i);
+		}
+		if (what & AGG_MINMAX) {
+			atomicMin(&acc.mn[gi], (long long) v);
+			atomicMax(&acc.mx[gi], (long long) v);
+		}
+		if constexpr (K > 0) {
+#pragma unroll
+			for (int k = 0; k < K; k++) {
+				bool m = gi == (BUN) k;
+				s[k] += m ? v : (hge) 0;
+				c[k] += m;
+			}
+		} else {
+			if (what & AGG_SUM)
+				atomic_add128(&acc.sum[2 * gi], v);
+			atomicAdd(&acc.cnt[gi], 1ull);
+		}
+	}
+	if constexpr (K > 0) {
+#pragma unroll
+		for (int k = 0; k < K; k++) {
+			hge sk = s[k];
+			unsigned long long ck = c[k];
+			for (int o = 32; o > 0; o >>= 1) {
+				unsigned long long lo = __shfl_xor((unsigned long long) (uhge) sk, o);
+				unsigned long long hi = __shfl_xor((unsigned long long) ((uhge) sk >> 64), o);
+				sk += (hge) (((uhge) hi << 64) | lo);
+				ck += __shfl_xor(ck, o);
+			}
+			if (__lane_id() == 0 && (BUN) k < ngrp) {
+				if (ck) {
+					if (what & AGG_SUM)
+						atomic_add128(&acc.sum[2 * k], sk);
+					atomicAdd(&acc.cnt[k], ck);
+				}
+			}
+		}
+	}
+	for (int o = 32; o > 0; o >>= 1) {
+		unsigned long long t = __shfl_xor(mx, o);
+		mx = t > mx ? t : mx;
+	}
+	if (__lane_id() == 0 && mx)
+		atomicMax(maxabs, mx);
+}
+
+struct AggrInit {
+	Cand ci;
+	oid min, max;
+	BUN ngrp;
+	const oid *gids;   // NULL: dense g
+	oid gseq;
+};
+
+__global__ void
+k_minmax_oid(const oid *g, BUN n, unsigned long long *out)
+{
+	unsigned long long mn = ~0ull, mx = 0;
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		oid x = g[i];
+		if (x == MGDK_OID_NIL)
+			continue;
+		mn = x < mn ? x : mn;
+		mx = x > mx ? x : mx;
+	}
+	for (int o = 32; o > 0; o >>= 1) {
+		unsigned long long t = __shfl_xor(mn, o);
+		mn = t < mn ? t : mn;
+		t = __shfl_xor(mx, o);
+		mx = t > mx ? t : mx;
+	}
+	if (__lane_id() == 0) {
+		atomicMin(&out[0], mn);
+		atomicMax(&out[1], mx);
+	}
+}
+
+// BATgroupaggrinit (gdk/gdk_aggr.c:65-146)
+int
+aggr_init(AggrInit *a, mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s)
+{
+	*a = AggrInit{};
+	if (cand_init(&a->ci, b, s) < 0)
+		return -1;
+	if (g == nullptr) {
+		seterr("b and g must be aligned\n");
+		return -1;
+	}
+	if (a->ci.n != g->count || (a->ci.n != 0 && a->ci.first != g->hseqbase)) {
+		seterr("b with s and g must be aligned\n");
+		return -1;
+	}
+	if (!a->ci.dense) {
+		seterr("42000!grouped aggregate over a materialized candidate list is not supported on the device path");
+		return -1;
+	}
+	a->gids = g->ttype == MGDK_void ? nullptr : (const oid *) g->theap;
+	a->gseq = g->tseqbase;
+	if (e) {
+		a->ngrp = e->count;
+		a->min = e->hseqbase;
+		a->max = e->hseqbase + a->ngrp - 1;
+		return 0;
+	}
+	if (a->gids == nullptr) {
+		a->min = g->tseqbase;
+		a->max = g->tseqbase + g->count - 1;
+		a->ngrp = g->count;
+		return 0;
+	}
+	unsigned long long *m = (unsigned long long *) meta_buf();
+	unsigned long long init[2] = {~0ull, 0};
+	if (!hip_ok(hipMemcpyAsync(m, init, 16, hipMemcpyHostToDevice, stream()), "memcpy"))
+		return -1;
+	if (g->count)
+		hipLaunchKernelGGL(k_minmax_oid, dim3(grid_for(g->count, 2048, 1024)), dim3(256), 0, stream(),
+				   a->gids, g->count, m);
+	unsigned long long *h = (unsigned long long *) pinned(16);
+	if (!hip_ok(hipMemcpyAsync(h, m, 16, hipMemcpyDeviceToHost, stream()), "memcpy") || !sync())
+		return -1;
+	a->min = h[0];
+	a->max = h[1];
+	a->ngrp = (h[0] == ~0ull || h[1] < h[0]) ? 0 : h[1] - h[0] + 1;
+	if (a->ngrp == 0)
+		a->min = 0;
+	return 0;
+}
+
+struct GRes {
+	std::vector<hge> sum;
+	std::vector<unsigned long long> cnt, firstval, lastnil;
+	std::vector<long long> mn, mx;
+	unsigned long long maxabs;
+};
+
+int
+run_gaggr(const AggrInit &a, mgdk_bat *b, int what, bool count_all, GRes &r)
+{
+	const BUN ng = a.ngrp;
+	size_t bytes = ng * (16 + 8 * 5) + 64;
+	char *d = (char *) scratch(bytes);
+	if (d == nullptr)
+		return -1;
+	GAcc acc;
+	acc.sum = (unsigned long long *) d;
+	acc.cnt = acc.sum + 2 * ng;
+	acc.firstval = acc.cnt + ng;
+	acc.lastnil = acc.firstval + ng;
+	acc.mn = (long long *) (acc.lastnil + ng);
+	acc.mx = acc.mn + ng;
+	unsigned long long *maxabs = (unsigned long long *) (acc.mx + ng);
+	hipStream_t st = stream();
+	if (!hip_ok(hipMemsetAsync(d, 0, (size_t) ng * 32, st), "memset") ||
+	    !hip_ok(hipMemsetAsync(acc.firstval, 0xff, ng * 8, st), "memset") ||
+	    !hip_ok(hipMemsetAsync(acc.lastnil, 0, ng * 8, st), "memset") ||
+	    !hip_ok(hipMemsetAsync(maxabs, 0, 8, st), "memset"))
+		return -1;
+	if (what & AGG_MINMAX) {
+		std::vector<long long> mn(ng, INT64_MAX), mx(ng, INT64_MIN);
+		if (!hip_ok(hipMemcpyAsync(acc.mn, mn.data(), ng * 8, hipMemcpyHostToDevice, st), "memcpy") ||
+		    !hip_ok(hipMemcpyAsync(acc.mx, mx.data(), ng * 8, hipMemcpyHostToDevice, st), "memcpy") || !sync())
+			return -1;
+	}
+	const oid off = a.ci.seq - b->hseqbase;
+	dim3 g(grid_for(a.ci.n, 256 * 8, 256 * 16)), blk(256);
+	if (a.ci.n) {
+		if (ng <= 1)
+			hipLaunchKernelGGL((k_gaggr<1>), g, blk, 0, st, b->theap, b->twidth, off, a.gids, a.gseq, a.min, ng, a.ci.n, what, count_all, acc, maxabs);
+		else if (ng <= 4)
+			hipLaunchKernelGGL((k_gaggr<4>), g, blk, 0, st, b->theap, b->twidth, off, a.gids, a.gseq, a.min, ng, a.ci.n, what, count_all, acc, maxabs);
+		else if (ng <= 8)
+			hipLaunchKernelGGL((k_gaggr<8>), g, blk, 0, st, b->theap, b->twidth, off, a.gids, a.gseq, a.min, ng, a.ci.n, what, count_all, acc, maxabs);
+		else
+			hipLaunchKernelGGL((k_gaggr<0>), g, blk, 0, st, b->theap, b->twidth, off, a.gids, a.gseq, a.min, ng, a.ci.n, what, count_all, acc, maxabs);
+	}
+	r.sum.resize(ng);
+	r.cnt.resize(ng);
+	r.firstval.resize(ng);
+	r.lastnil.resize(ng);
+	r.mn.resize(ng);
+	r.mx.resize(ng);
+	std::vector<unsigned long long> raw(2 * ng);
+	if ((ng && (!hip_ok(hipMemcpyAsync(raw.data(), acc.sum, ng * 16, hipMemcpyDeviceToHost, st), "memcpy") ||
+		    !hip_ok(hipMemcpyAsync(r.cnt.data(), acc.cnt, ng * 8, hipMemcpyDeviceToHost, st), "memcpy") ||
+		    !hip_ok(hipMemcpyAsync(r.firstval.data(), acc.firstval, ng * 8, hipMemcpyDeviceToHost, st), "memcpy") ||
+		    !hip_ok(hipMemcpyAsync(r.lastnil.data(), acc.lastnil, ng * 8, hipMemcpyDeviceToHost, st), "memcpy") ||
+		    !hip_ok(hipMemcpyAsync(r.mn.data(), acc.mn, ng * 8, hipMemcpyDeviceToHost, st), "memcpy") ||
+		    !hip_ok(hipMemcpyAsync(r.mx.data(), acc.mx, ng * 8, hipMemcpyDeviceToHost, st), "memcpy"))) ||
+	    !hip_ok(hipMemcpyAsync(&r.maxabs, maxabs, 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+		return -1;
+	for (BUN k = 0; k < ng; k++)
+		r.sum[k] = (hge) (((uhge) raw[2 * k + 1] << 64) | raw[2 * k]);
+	return 0;
+}
+
+mgdk_bat *
+upload_new(oid hseq, int tp, const void *host, BUN n)
+{
+	mgdk_bat *bn = newbat(hseq, tp, n);
+	if (bn == nullptr)
+		return nullptr;
+	if (mgdk_BATupload(bn, host, n) < 0) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	bn->count = n;
+	return bn;
+}
+
+void
+put_vec(std::vector<char> &buf, int tp, BUN k, hge v, bool nil)
+{
+	put_res(buf.data() + k * width_of(tp), tp, v, nil);
+}
+
+}  // namespace
+
+extern "C" {
+
+// BATgroupsum (gdk/gdk_aggr.c:900)
+mgdk_bat *
+mgdk_BATgroupsum(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils)
+{
+	if (b == nullptr || !int_type(b->ttype) || !int_type(tp)) {
+		seterr("type combination (sum(%s)->%s) not supported.\n", b ? atomname(b->ttype) : "?", atomname(tp));
+		return nullptr;
+	}
+	ProfScope prof("groupsum");
+	AggrInit a;
+	if (aggr_init(&a, b, g, e, s) < 0)
+		return nullptr;
+	const BUN ng = a.ngrp;
+	std::vector<char> out(ng * width_of(tp) + 16);
+	GRes r;
+	if (a.ci.n && ng) {
+		if (run_gaggr(a, b, AGG_SUM | AGG_POS, false, r) < 0)
+			return nullptr;
+		// overflow: a prefix of one group could exceed max only if
+		// count * max|v| exceeds it
+		const hge max = tmax(tp);
+		for (BUN k = 0; k < ng; k++) {
+			long double bound = mag_bound(r.maxabs) * (long double) r.cnt[k];
+			if (bound > (long double) max && (r.sum[k] > max || r.sum[k] < -max)) {
+				seterr("22003!overflow in sum aggregate.\n");
+				return nullptr;
+			}
+		}
+	}
+	bool hasnil = false;
+	for (BUN k = 0; k < ng; k++) {
+		bool nil;
+		if (a.ci.n == 0 || r.cnt[k] == 0)
+			nil = true;                              // no value: stays nil
+		else if (skip_nils)
+			nil = false;
+		else if (ng == 1)
+			nil = r.lastnil[k] != 0;                 // single group: any nil
+		else
+			nil = r.lastnil[k] > r.firstval[k] + 1;  // a nil after the first value
+		put_vec(out, tp, k, nil ? 0 : r.sum[k], nil);
+		hasnil |= nil;
+	}
+	mgdk_bat *bn = upload_new(ng ? a.min : 0, tp, out.data(), ng);
+	if (bn) {
+		bn->tkey = bn->tsorted = bn->trevsorted = ng <= 1;
+		bn->tnil = hasnil;
+		bn->tnonil = !hasnil;
+	}
+	return bn;
+}
+
+// BATgroupcount (gdk/gdk_aggr.c:3069)
+mgdk_bat *
+mgdk_BATgroupcount(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils)
+{
+	(void) tp;
+	if (b == nullptr || !(int_type(b->ttype) || b->ttype == MGDK_oid || b->ttype == MGDK_str)) {
+		seterr("42000!BATgroupcount: type not supported on the device path");
+		return nullptr;
+	}
+	ProfScope prof("groupcount");
+	AggrInit a;
+	if (aggr_init(&a, b, g, e, s) < 0)
+		return nullptr;
+	const BUN ng = a.ngrp;
+	std::vector<long long> out(ng + 1, 0);
+	if (a.ci.n && ng) {
+		GRes r;
+		// str offsets are never nil in our heaps; oid via lng width
+		bool all = !skip_nils || b->tnonil || b->ttype == MGDK_str;
+		if (run_gaggr(a, b, 0, all, r) < 0)
+			return nullptr;
+		for (BUN k = 0; k < ng; k++)
+			out[k] = (long long) r.cnt[k];
+	}
+	mgdk_bat *bn = upload_new(ng ? a.min : 0, MGDK_lng, out.data(), ng);
+	if (bn)
+		bn->tnonil = 1;
+	return bn;
+}
+
+// BATgroupavg3 (gdk/gdk_aggr.c:1996-2110)
+int
+mgdk_BATgroupavg3(mgdk_bat **avgp, mgdk_bat **remp, mgdk_bat **cntp, mgdk_bat *b, mgdk_bat *g,
+		  mgdk_bat *e, mgdk_bat *s, bool skip_nils)
+{
+	if (b == nullptr || !int_type(b->ttype)) {
+		seterr("42000!BATgroupavg3: type not supported on the device path");
+		return -1;
+	}
+	ProfScope prof("groupavg3");
+	AggrInit a;
+	if (aggr_init(&a, b, g, e, s) < 0)
+		return -1;
+	const BUN ng = a.ngrp;
+	const int tp = b->ttype;
+	GRes r;
+	if (a.ci.n && ng && run_gaggr(a, b, AGG_SUM | AGG_POS, false, r) < 0)
+		return -1;
+	std::vector<char> av(ng * width_of(tp) + 16);
+	std::vector<long long> rem(ng + 1), cnt(ng + 1);
+	for (BUN k = 0; k < ng; k++) {
+		unsigned long long n = a.ci.n ? r.cnt[k] : 0;
+		bool nil = a.ci.n && !skip_nils && r.lastnil[k] != 0;
+		if (nil) {
+			put_vec(av, tp, k, 0, true);
+			rem[k] = INT64_MIN;
+			cnt[k] = INT64_MIN;
+			continue;
+		}
+		cnt[k] = (long long) n;
+		if (n == 0) {
+			put_vec(av, tp, k, 0, true);
+			rem[k] = a.ci.n ? 0 : INT64_MIN;
+			continue;
+		}
+		hge S = r.sum[k], q = S / (hge) n, m = S % (hge) n;
+		if (m < 0) {
+			q -= 1;
+			m += (hge) n;
+		}
+		if (m > 0) {
+			if (q < 0) {
+				if (2 * m > (hge) n) { q++; m -= (hge) n; }
+			} else if (2 * m >= (hge) n) {
+				q++;
+				m -= (hge) n;
+			}
+		}
+		put_vec(av, tp, k, q, false);
+		rem[k] = (long long) m;
+	}
+	mgdk_bat *A = upload_new(ng ? a.min : 0, tp, av.data(), ng);
+	mgdk_bat *R = upload_new(ng ? a.min : 0, MGDK_lng, rem.data(), ng);
+	mgdk_bat *C = upload_new(ng ? a.min : 0, MGDK_lng, cnt.data(), ng);
+	if (!A || !R || !C) {
+		mgdk_BBPunfix(A);
+		mgdk_BBPunfix(R);
+		mgdk_BBPunfix(C);
+		return -1;
+	}
+	*avgp = A;
+	*remp = R;
+	*cntp = C;
+	return 0;
+}
+
+static mgdk_bat *
+groupminmax(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, bool skip_nils, bool domax)
+{
+	if (b == nullptr || !int_type(b->ttype) || basetype(b->ttype) == MGDK_hge) {
+		seterr("42000!BATgroupmin/max: type not supported on the device path");
+		return nullptr;
+	}
+	AggrInit a;
+	if (aggr_init(&a, b, g, e, s) < 0)
+		return nullptr;
+	const BUN ng = a.ngrp;
+	GRes r;
+	if (a.ci.n && ng && run_gaggr(a, b, AGG_MINMAX | AGG_POS, false, r) < 0)
+		return nullptr;
+	std::vector<char> out(ng * width_of(b->ttype) + 16);
+	for (BUN k = 0; k < ng; k++) {
+		bool nil = !a.ci.n || r.cnt[k] == 0 || (!skip_nils && r.lastnil[k] != 0);
+		put_vec(out, b->ttype, k, domax ? r.mx[k] : r.mn[k], nil);
+	}
+	return upload_new(ng ? a.min : 0, b->ttype, out.data(), ng);
+}
+
+mgdk_bat *
+mgdk_BATgroupmin(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils)
+{
+	(void) tp;
+	return groupminmax(b, g, e, s, skip_nils, false);
+}
+
+mgdk_bat *
+mgdk_BATgroupmax(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils)
+{
+	(void) tp;
+	return groupminmax(b, g, e, s, skip_nils, true);
+}
+
+}  // extern "C"

@@ -1,0 +1,405 @@
+// group.hip -- BATgroup on the MI355X (gdk/gdk_group.c:657-1347).
+//
+// GDK numbers groups in order of FIRST OCCURRENCE of each distinct
+// (prior group, value) pair over the candidates (GRPnotfound,
+// gdk_group.c:74-100); a GPU hash table is unordered, so the numbering is
+// recovered from first positions:
+//   A  insert: every candidate finds its slot -- a direct index for 1/2-byte
+//      keys (bte/sht/str offsets, GRP_small_values' domain, :607-654) or an
+//      open-addressing table keyed by a CAS-claimed representative row --
+//      and lowers the slot's first position with a pre-checked atomicMin;
+//   B  flags[i] = (slot(i).first == i); the ordered compaction kernel of
+//      select.hip turns them into the sorted first positions = extents, in
+//      group-id order;
+//   C  slot -> group id map from the extents;
+//   D  group id per row + histogram (LDS-privatised counts for <= 4096
+//      groups) + the sortedness property.
+// nil is an ordinary value (all nils form one group); float keys compare by
+// value (+0 == -0, every NaN is nil).
+#include <vector>
+
+#include "mgdk_internal.h"
+
+using namespace mgdk;
+
+namespace {
+
+struct KeySrc {
+	const void *base;
+	int w;
+	int kind;          // 0 signed int, 1 unsigned (str offsets), 2 flt, 3 dbl
+	bool dense;
+	oid off;           // dense: position of candidate 0
+	const oid *oids;   // materialized candidates
+	oid hseq;
+	const oid *g;      // prior groups aligned with candidates (NULL: none)
+	oid gseq;          // dense prior groups: gseq + i
+	bool has_g;
+};
+
+__device__ __forceinline__ void
+key_at(const KeySrc &s, BUN i, uint64_t &k0, uint64_t &k1, uint64_t &gg)
+{
+	BUN p = s.dense ? s.off + i : s.oids[i] - s.hseq;
+	k1 = 0;
+	switch (s.w) {
+	case 1: k0 = s.kind == 1 ? ((const uint8_t *) s.base)[p] : (uint64_t) (uint8_t) ((const int8_t *) s.base)[p]; break;
+	case 2: k0 = ((const uint16_t *) s.base)[p]; break;
+	case 4:
+		if (s.kind == 2) {
+			float f = ((const float *) s.base)[p];
+			if (f != f) k0 = 0x7fc00000u;
+			else if (f == 0.0f) k0 = 0;
+			else k0 = __float_as_uint(f);
+		} else {
+			k0 = ((const uint32_t *) s.base)[p];
+		}
+		break;
+	case 8:
+		if (s.kind == 3) {
+			double d = ((const double *) s.base)[p];
+			if (d != d) k0 = 0x7ff8000000000000ull;
+			else if (d == 0.0) k0 = 0;
+			else k0 = (uint64_t) __double_as_longlong(d);
+		} else {
+			k0 = ((const uint64_t *) s.base)[p];
+		}
+		break;
+	default:
+		k0 = ((const uint64_t *) s.base)[2 * p];
+		k1 = ((const uint64_t *) s.base)[2 * p + 1];
+		break;
+	}
+	gg = s.has_g ? (s.g ? s.g[i] : s.gseq + i) : 0;
+}
+
+__device__ __forceinline__ uint64_t
+hmix(uint64_t a, uint64_t b, uint64_t c)
+{
+	uint64_t x = a * 0x9e3779b97f4a7c15ull ^ (b + 0x632be59bd9b4e019ull) * 0xbf58476d1ce4e5b9ull ^ c * 0x94d049bb133111ebull;
+	x ^= x >> 31;
+	x *= 0xd6e8feb86659fd93ull;
+	return x ^ (x >> 32);
+}
+
+constexpr uint64_t EMPTY = ~0ull;
+
+// direct: slot = gg * D + k0 (1/2-byte keys), no probing
+template <bool DIRECT>
+__global__ __launch_bounds__(256) void
+k_grp_insert(KeySrc s, BUN n, uint64_t mask, int dshift, unsigned long long *s_row,
+	     unsigned long long *s_min, uint32_t *hidx, uint32_t *err)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		uint64_t k0, k1, gg;
+		key_at(s, i, k0, k1, gg);
+		uint64_t h;
+		if (DIRECT) {
+			h = (gg << dshift) | k0;
+		} else {
+			h = hmix(k0, k1, gg) & mask;
+			uint32_t probes = 0;
+			for (;;) {
+				unsigned long long r = s_row[h];
+				if (r == EMPTY) {
+					r = atomicCAS(&s_row[h], EMPTY, (unsigned long long) i);
+					if (r == EMPTY)
+						break;
+				}
+				uint64_t r0, r1, rg;
+				key_at(s, r, r0, r1, rg);
+				if (r0 == k0 && r1 == k1 && rg == gg)
+					break;
+				h = (h + 1) & mask;
+				if (++probes > mask) {
+					atomicOr(err, 1u);
+					break;
+				}
+			}
+		}
+		hidx[i] = (uint32_t) h;
+		if (s_min[h] > i)
+			atomicMin(&s_min[h], (unsigned long long) i);
+	}
+}
+
+__global__ __launch_bounds__(256) void
+k_grp_flags(BUN n, const uint32_t *hidx, const unsigned long long *s_min, int8_t *flags)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
+		flags[i] = s_min[hidx[i]] == i;
+}
+
+__global__ __launch_bounds__(256) void
+k_grp_map(BUN ngrp, const oid *E, oid Eseq, const uint32_t *hidx, uint32_t *gidmap, bool cdense,
+	  oid cseq, const oid *coids, oid *ext)
+{
+	for (BUN e = (BUN) blockIdx.x * blockDim.x + threadIdx.x; e < ngrp; e += (BUN) gridDim.x * blockDim.x) {
+		BUN p = E ? E[e] : Eseq + e;
+		gidmap[hidx[p]] = (uint32_t) e;
+		ext[e] = cdense ? cseq + p : coids[p];
+	}
+}
+
+template <bool LDSHIST>
+__global__ __launch_bounds__(256) void
+k_grp_assign(BUN n, const uint32_t *hidx, const uint32_t *gidmap, oid *gid, BUN ngrp,
+	     unsigned long long *histo, uint32_t *unsorted)
+{
+	extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
+	if (LDSHIST) {
+		for (BUN k = threadIdx.x; k < ngrp; k += blockDim.x)
+			s_hist[k] = 0;
+		__syncthreads();
+	}
+	uint32_t uns = 0;
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		uint32_t g = gidmap[hidx[i]];
+		gid[i] = g;
+		if (i > 0 && gidmap[hidx[i - 1]] > g)
+			uns = 1;
+		if (LDSHIST)
+			atomicAdd(&s_hist[g], 1u);
+		else
+			atomicAdd(&histo[g], 1ull);
+	}
+	if (uns)
+		atomicOr(unsorted, 1u);
+	if (LDSHIST) {
+		__syncthreads();
+		for (BUN k = threadIdx.x; k < ngrp; k += blockDim.x)
+			if (s_hist[k])
+				atomicAdd(&histo[k], (unsigned long long) s_hist[k]);
+	}
+}
+
+__global__ void
+k_max_oid(const oid *g, BUN n, unsigned long long *out)
+{
+	unsigned long long mx = 0;
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
+		if (g[i] != MGDK_OID_NIL && g[i] > mx)
+			mx = g[i];
+	for (int o = 32; o > 0; o >>= 1) {
+		unsigned long long t = __shfl_xor(mx, o);
+		mx = t > mx ? t : mx;
+	}
+	if (__lane_id() == 0)
+		atomicMax(out, mx);
+}
+
+mgdk_bat *
+dense_or_copy(const Cand &ci)
+{
+	if (ci.dense)
+		return mgdk_BATdense(0, ci.seq, ci.n);
+	mgdk_bat *bn = newbat(0, MGDK_oid, ci.n);
+	if (bn && hip_ok(hipMemcpyAsync(bn->theap, ci.oids, ci.n * 8, hipMemcpyDeviceToDevice, stream()), "memcpy") && sync()) {
+		bn->count = ci.n;
+		bn->tsorted = bn->tkey = bn->tnonil = 1;
+		bn->trevsorted = ci.n <= 1;
+		return bn;
+	}
+	mgdk_BBPunfix(bn);
+	return nullptr;
+}
+
+int
+key_kind(int tt)
+{
+	switch (tt) {
+	case MGDK_str: return 1;
+	case MGDK_flt: return 2;
+	case MGDK_dbl: return 3;
+	default: return 0;
+	}
+}
+
+}  // namespace
+
+extern "C" int
+mgdk_BATgroup(mgdk_bat **groups, mgdk_bat **extents, mgdk_bat **histo, mgdk_bat *b, mgdk_bat *s,
+	      mgdk_bat *g, mgdk_bat *e, mgdk_bat *h)
+{
+	(void) e;
+	(void) h;
+	if (b == nullptr || groups == nullptr) {
+		seterr("b must exist\n");
+		return -1;
+	}
+	if (b->ttype == MGDK_void || b->ttype == MGDK_msk) {
+		seterr("42000!BATgroup: type %s not supported on the device path", atomname(b->ttype));
+		return -1;
+	}
+	ProfScope prof("group");
+	Cand ci;
+	if (cand_init(&ci, b, s) < 0)
+		return -1;
+	const BUN n = ci.n;
+	const oid hseqb = n ? ci.first : 0;
+	if (g && g->count != n) {
+		seterr("b with s and g must be aligned\n");
+		return -1;
+	}
+	mgdk_bat *gn = nullptr, *en = nullptr, *hn = nullptr;
+	// trivial: one element per group (gdk_group.c:712-767)
+	if (b->tkey || n <= 1 || (g && (g->tkey || g->ttype == MGDK_void))) {
+		gn = mgdk_BATdense(hseqb, 0, b->count);
+		en = dense_or_copy(ci);
+		long long one = 1;
+		hn = mgdk_BATconstant(0, MGDK_lng, &one, n);
+		if (!gn || !en || !hn)
+			goto fail;
+		goto done;
+	}
+	// all values equal and no (or a constant) prior grouping: one group
+	if (b->tsorted && b->trevsorted && (!g || (g->tsorted && g->trevsorted))) {
+		oid zero = 0;
+		gn = mgdk_BATconstant(hseqb, MGDK_oid, &zero, n);
+		en = mgdk_BATdense(0, ci.first, 1);
+		long long cnt = (long long) n;
+		hn = mgdk_BATconstant(0, MGDK_lng, &cnt, 1);
+		if (!gn || !en || !hn)
+			goto fail;
+		gn->tsorted = gn->trevsorted = 1;
+		gn->tkey = n <= 1;
+		goto done;
+	}
+	{
+		KeySrc ks{};
+		ks.base = b->theap;
+		ks.w = b->twidth;
+		ks.kind = key_kind(b->ttype);
+		ks.dense = ci.dense;
+		ks.off = ci.dense ? ci.seq - b->hseqbase : 0;
+		ks.oids = ci.oids;
+		ks.hseq = b->hseqbase;
+		ks.has_g = g != nullptr;
+		ks.g = g && g->ttype == MGDK_oid ? (const oid *) g->theap : nullptr;
+		ks.gseq = g ? g->tseqbase : 0;
+		hipStream_t st = stream();
+		// prior group range for the direct table
+		uint64_t gmax = 0;
+		if (ks.g) {
+			unsigned long long *m = (unsigned long long *) meta_buf();
+			if (!hip_ok(hipMemsetAsync(m, 0, 8, st), "memset"))
+				return -1;
+			hipLaunchKernelGGL(k_max_oid, dim3(grid_for(n, 4096, 1024)), dim3(256), 0, st, ks.g, n, m);
+			unsigned long long *hm = (unsigned long long *) pinned(8);
+			if (!hip_ok(hipMemcpyAsync(hm, m, 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+				return -1;
+			gmax = *hm;
+		} else if (g) {
+			gmax = g->tseqbase + n;
+		}
+		const bool small = (ks.kind <= 1 && ks.w <= 2);
+		int dshift = ks.w * 8;
+		bool direct = small && ((gmax + 1) << dshift) <= ((uint64_t) 1 << 24);
+		uint64_t T;
+		if (direct) {
+			T = (gmax + 1) << dshift;
+		} else {
+			T = 1024;
+			while (T < 2 * n)
+				T <<= 1;
+			if (T > ((uint64_t) 1 << 32)) {
+				seterr("HY013!BATgroup: too many rows for the device hash table");
+				return -1;
+			}
+		}
+		DevBuf d_row(direct ? 8 : T * 8), d_min(T * 8), d_hidx(n * 4), d_flags(n), d_map(T * 4);
+		DevBuf d_err(16);
+		if (!d_row.p || !d_min.p || !d_hidx.p || !d_flags.p || !d_map.p || !d_err.p)
+			return -1;
+		if (!hip_ok(hipMemsetAsync(d_min.p, 0xff, T * 8, st), "memset") ||
+		    (!direct && !hip_ok(hipMemsetAsync(d_row.p, 0xff, T * 8, st), "memset")) ||
+		    !hip_ok(hipMemsetAsync(d_err.p, 0, 16, st), "memset"))
+			return -1;
+		dim3 grd(grid_for(n, 256 * 4, 256 * 64)), blk(256);
+		if (direct)
+			hipLaunchKernelGGL((k_grp_insert<true>), grd, blk, 0, st, ks, n, T - 1, dshift,
+					   d_row.as<unsigned long long>(), d_min.as<unsigned long long>(),
+					   d_hidx.as<uint32_t>(), d_err.as<uint32_t>());
+		else
+			hipLaunchKernelGGL((k_grp_insert<false>), grd, blk, 0, st, ks, n, T - 1, dshift,
+					   d_row.as<unsigned long long>(), d_min.as<unsigned long long>(),
+					   d_hidx.as<uint32_t>(), d_err.as<uint32_t>());
+		hipLaunchKernelGGL(k_grp_flags, grd, blk, 0, st, n, d_hidx.as<uint32_t>(),
+				   d_min.as<unsigned long long>(), d_flags.as<int8_t>());
+		mgdk_bat *E = compact_flags(d_flags.as<int8_t>(), n, 0);
+		if (E == nullptr)
+			return -1;
+		const BUN ngrp = E->count;
+		en = newbat(0, MGDK_oid, ngrp);
+		hn = newbat(0, MGDK_lng, ngrp);
+		gn = newbat(hseqb, MGDK_oid, n);
+		if (!en || !hn || !gn) {
+			mgdk_BBPunfix(E);
+			goto fail;
+		}
+		hipLaunchKernelGGL(k_grp_map, dim3(grid_for(ngrp, 256, 4096)), blk, 0, st, ngrp,
+				   E->ttype == MGDK_void ? nullptr : (const oid *) E->theap, E->tseqbase,
+				   d_hidx.as<uint32_t>(), d_map.as<uint32_t>(), ci.dense, ci.seq, ci.oids,
+				   (oid *) en->theap);
+		if (!hip_ok(hipMemsetAsync(hn->theap, 0, ngrp * 8, st), "memset")) {
+			mgdk_BBPunfix(E);
+			goto fail;
+		}
+		uint32_t *uns = d_err.as<uint32_t>() + 1;
+		if (ngrp <= 4096)
+			hipLaunchKernelGGL((k_grp_assign<true>), grd, blk, ngrp * 4, st, n, d_hidx.as<uint32_t>(),
+					   d_map.as<uint32_t>(), (oid *) gn->theap, ngrp,
+					   (unsigned long long *) hn->theap, uns);
+		else
+			hipLaunchKernelGGL((k_grp_assign<false>), grd, blk, 0, st, n, d_hidx.as<uint32_t>(),
+					   d_map.as<uint32_t>(), (oid *) gn->theap, ngrp,
+					   (unsigned long long *) hn->theap, uns);
+		uint32_t *herr = (uint32_t *) pinned(16);
+		if (!hip_ok(hipMemcpyAsync(herr, d_err.p, 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
+			mgdk_BBPunfix(E);
+			goto fail;
+		}
+		mgdk_BBPunfix(E);
+		if (herr[0]) {
+			seterr("HY013!BATgroup: hash table overflow");
+			goto fail;
+		}
+		gn->count = n;
+		en->count = ngrp;
+		hn->count = ngrp;
+		gn->tsorted = herr[1] == 0;
+		gn->trevsorted = ngrp == 1 || n <= 1;
+		gn->tkey = ngrp == n;
+		gn->tnonil = 1;
+		en->tsorted = en->tkey = en->tnonil = 1;
+		en->trevsorted = ngrp == 1;
+		bool hs = ngrp == n || ngrp == 1;
+		hn->tkey = ngrp == 1;
+		hn->tsorted = hn->trevsorted = hs;
+		hn->tnonil = 1;
+		// virtualize extents when dense
+		if (ngrp > 0) {
+			oid fl[2];
+			if (hip_ok(hipMemcpy(&fl[0], en->theap, 8, hipMemcpyDeviceToHost), "memcpy") &&
+			    hip_ok(hipMemcpy(&fl[1], (oid *) en->theap + ngrp - 1, 8, hipMemcpyDeviceToHost), "memcpy") &&
+			    fl[1] - fl[0] == ngrp - 1)
+				setdense(en, fl[0], ngrp);
+		}
+	}
+done:
+	*groups = gn;
+	if (extents)
+		*extents = en;
+	else
+		mgdk_BBPunfix(en);
+	if (histo)
+		*histo = hn;
+	else
+		mgdk_BBPunfix(hn);
+	return 0;
+fail:
+	mgdk_BBPunfix(gn);
+	mgdk_BBPunfix(en);
+	mgdk_BBPunfix(hn);
+	return -1;
+}

@@ -1,0 +1,116 @@
+// mgdk_internal.h -- shared internals of libmgdk.so (HIP, gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+
+#include "../../include/mgdk.h"
+
+typedef __int128 hge;
+typedef unsigned __int128 uhge;
+typedef mgdk_oid oid;
+typedef mgdk_BUN BUN;
+
+namespace mgdk {
+
+// ---- errors: thread-local GDKerrbuf (gdk/gdk.h:1710,1947) ----------------
+void seterr(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+bool hip_ok(hipError_t e, const char *what);
+
+// ---- streams, allocator, scratch ------------------------------------------
+hipStream_t stream();                       // per calling thread
+void *dalloc(size_t bytes);                 // HBM, cached, >= 256 B aligned
+void dfree(void *p);
+// per-thread scratch (grows; valid until the next scratch() on this thread)
+void *scratch(size_t bytes);
+// pinned host staging for small device->host reads
+void *pinned(size_t bytes);
+// per-thread 4 KiB device buffer for small results / arguments
+void *meta_buf();
+bool sync();                                // stream sync + error check
+
+// ---- BAT heap ownership ---------------------------------------------------
+struct Heap {
+	void *base;
+	size_t size;
+	int refs;
+};
+struct Priv {
+	Heap *theap;      // may be shared between views (BATslice)
+	Heap *tvheap;
+	size_t toff;      // byte offset of b->theap into theap->base
+};
+mgdk_bat *newbat(oid hseq, int tt, BUN cap);     // allocates tail heap
+void setdense(mgdk_bat *b, oid tseq, BUN cnt);
+void share_vheap(mgdk_bat *dst, const mgdk_bat *src);
+int width_of(int tt);
+int basetype(int tt);                            // date->int, bit->bte
+const char *atomname(int tt);
+
+// ---- profiling ----------------------------------------------------------
+struct ProfScope {
+	const char *name;
+	hipEvent_t e0, e1;
+	bool on;
+	explicit ProfScope(const char *n);
+	~ProfScope();
+};
+
+// ---- launch helpers ---------------------------------------------------------
+constexpr int BLOCK = 256;
+inline unsigned grid_for(uint64_t items, uint64_t per_block, unsigned cap = 65535u * 64u) {
+	uint64_t g = (items + per_block - 1) / per_block;
+	if (g == 0) g = 1;
+	return g > cap ? cap : (unsigned) g;
+}
+
+// ---- candidate description used by kernels --------------------------------
+struct Cand {
+	bool dense;
+	oid seq;              // dense: first candidate
+	const oid *oids;      // materialized: device pointer to first candidate
+	BUN n;
+	oid first, last;      // first/last candidate oid (valid when n > 0)
+};
+// canditer_init (gdk/gdk_cand.c:407): clip s to b's [hseqbase, hseqbase+count)
+int cand_init(Cand *ci, const mgdk_bat *b, const mgdk_bat *s);
+
+// ordered compaction (select.hip): sorted positions base+i with flags[i]==1;
+// the result may be a dense (void) BAT.  Uses the thread's scratch buffer.
+mgdk_bat *compact_flags(const int8_t *flags, BUN n, oid base);
+
+// RAII device temporary (not the per-thread scratch)
+struct DevBuf {
+	void *p = nullptr;
+	explicit DevBuf(size_t bytes) { p = dalloc(bytes ? bytes : 1); }
+	~DevBuf() { dfree(p); }
+	DevBuf(const DevBuf &) = delete;
+	DevBuf &operator=(const DevBuf &) = delete;
+	template <typename T> T *as() const { return (T *) p; }
+};
+
+}  // namespace mgdk
+
+
+// ---- device-side helpers ------------------------------------------------
+template <typename T> struct NilOf;
+template <> struct NilOf<int8_t> { static __device__ __host__ constexpr int8_t v() { return INT8_MIN; } };
+template <> struct NilOf<int16_t> { static __device__ __host__ constexpr int16_t v() { return INT16_MIN; } };
+template <> struct NilOf<int32_t> { static __device__ __host__ constexpr int32_t v() { return INT32_MIN; } };
+template <> struct NilOf<int64_t> { static __device__ __host__ constexpr int64_t v() { return INT64_MIN; } };
+template <> struct NilOf<uint64_t> { static __device__ __host__ constexpr uint64_t v() { return (uint64_t) 1 << 63; } };
+template <> struct NilOf<hge> { static __device__ __host__ constexpr hge v() { return (hge) ((uhge) 1 << 127); } };
+
+template <typename T>
+__device__ __host__ inline bool is_nil(T v) { return v == NilOf<T>::v(); }
+__device__ __host__ inline bool is_nil(float v) { return v != v; }
+__device__ __host__ inline bool is_nil(double v) { return v != v; }
+
+// wave64 helpers
+__device__ inline unsigned lane_id() { return __lane_id(); }
+__device__ inline uint64_t lanemask_lt() {
+	unsigned l = __lane_id();
+	return l == 0 ? 0ull : (~0ull >> (64 - l));
+}

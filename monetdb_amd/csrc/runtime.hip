@@ -1,0 +1,691 @@
+// runtime.hip -- HBM heap allocator, per-thread streams, error buffer, BAT
+// descriptors and candidate-list plumbing for libmgdk.so.
+//
+// Mirrors the GDK runtime conventions the operators rely on:
+//   GDKerror / GDKerrbuf thread-local messages   gdk/gdk.h:1710,1947
+//   HEAPalloc / GDKmalloc + memory accounting     gdk/gdk_heap.c:141-225, gdk/gdk_utils.c:1636,1752
+//   COLnew / BATdense / BATslice / BBPunfix       gdk/gdk_bat.c:292,298, gdk/gdk_batop.c:1825, gdk/gdk_bbp.c:3149
+//   canditer_init clipping                         gdk/gdk_cand.c:407
+#include <cstdarg>
+#include <cstdio>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "mgdk_internal.h"
+
+namespace mgdk {
+
+static thread_local char errbuf[2048];
+static int g_device = 0;
+
+void
+seterr(const char *fmt, ...)
+{
+	va_list ap;
+	va_start(ap, fmt);
+	vsnprintf(errbuf, sizeof(errbuf), fmt, ap);
+	va_end(ap);
+}
+
+bool
+hip_ok(hipError_t e, const char *what)
+{
+	if (e == hipSuccess)
+		return true;
+	seterr("HY013!HIP error %s in %s", hipGetErrorString(e), what);
+	return false;
+}
+
+// ---- streams ----------------------------------------------------------------
+struct ThreadCtx {
+	hipStream_t s = nullptr;
+	void *scratch = nullptr;
+	size_t scratch_size = 0;
+	void *pinned = nullptr;
+	size_t pinned_size = 0;
+	void *meta = nullptr;
+	~ThreadCtx() {
+		if (meta)
+			dfree(meta);
+		if (scratch)
+			dfree(scratch);
+		if (pinned)
+			(void) hipHostFree(pinned);
+		if (s)
+			(void) hipStreamDestroy(s);
+	}
+};
+static thread_local ThreadCtx tctx;
+
+hipStream_t
+stream()
+{
+	if (tctx.s == nullptr) {
+		(void) hipSetDevice(g_device);
+		if (hipStreamCreateWithFlags(&tctx.s, hipStreamNonBlocking) != hipSuccess)
+			tctx.s = nullptr;
+	}
+	return tctx.s;
+}
+
+bool
+sync()
+{
+	hipError_t e = hipStreamSynchronize(stream());
+	if (e != hipSuccess)
+		return hip_ok(e, "hipStreamSynchronize");
+	return hip_ok(hipGetLastError(), "kernel launch");
+}
+
+// ---- caching HBM allocator ---------------------------------------------------
+// Sizes are rounded to a class (power of two up to 64 MiB, then 64 MiB
+// multiples) and freed blocks are kept per class.  Every operator
+// synchronises its stream before returning, so a cached block is never in
+// use by an in-flight kernel when it is handed out again.
+static std::mutex alloc_mu;
+static std::map<size_t, std::vector<void *>> free_lists;
+static std::map<void *, size_t> live;
+static uint64_t cur_bytes = 0, cached_bytes = 0;
+
+static size_t
+size_class(size_t n)
+{
+	if (n < 256)
+		return 256;
+	const size_t big = (size_t) 64 << 20;
+	if (n >= big)
+		return (n + big - 1) / big * big;
+	size_t c = 256;
+	while (c < n)
+		c <<= 1;
+	return c;
+}
+
+void *
+dalloc(size_t bytes)
+{
+	size_t c = size_class(bytes);
+	{
+		std::lock_guard<std::mutex> g(alloc_mu);
+		auto it = free_lists.find(c);
+		if (it != free_lists.end() && !it->second.empty()) {
+			void *p = it->second.back();
+			it->second.pop_back();
+			live[p] = c;
+			cur_bytes += c;
+			cached_bytes -= c;
+			return p;
+		}
+	}
+	(void) hipSetDevice(g_device);
+	void *p = nullptr;
+	hipError_t e = hipMalloc(&p, c);
+	if (e != hipSuccess) {
+		mgdk_mem_release_cache();
+		e = hipMalloc(&p, c);
+	}
+	if (e != hipSuccess) {
+		seterr("HY013!Could not allocate space (%zu bytes in HBM)", c);
+		return nullptr;
+	}
+	std::lock_guard<std::mutex> g(alloc_mu);
+	live[p] = c;
+	cur_bytes += c;
+	return p;
+}
+
+void
+dfree(void *p)
+{
+	if (p == nullptr)
+		return;
+	std::lock_guard<std::mutex> g(alloc_mu);
+	auto it = live.find(p);
+	if (it == live.end())
+		return;
+	size_t c = it->second;
+	live.erase(it);
+	cur_bytes -= c;
+	cached_bytes += c;
+	free_lists[c].push_back(p);
+}
+
+void *
+scratch(size_t bytes)
+{
+	if (tctx.scratch_size < bytes) {
+		if (tctx.scratch)
+			dfree(tctx.scratch);
+		size_t n = bytes < ((size_t) 1 << 20) ? ((size_t) 1 << 20) : bytes;
+		tctx.scratch = dalloc(n);
+		tctx.scratch_size = tctx.scratch ? n : 0;
+	}
+	return tctx.scratch;
+}
+
+void *
+meta_buf()
+{
+	if (tctx.meta == nullptr)
+		tctx.meta = dalloc(4096);
+	return tctx.meta;
+}
+
+void *
+pinned(size_t bytes)
+{
+	if (tctx.pinned_size < bytes) {
+		if (tctx.pinned)
+			(void) hipHostFree(tctx.pinned);
+		size_t n = bytes < 4096 ? 4096 : bytes;
+		if (hipHostMalloc(&tctx.pinned, n, hipHostMallocDefault) != hipSuccess) {
+			tctx.pinned = nullptr;
+			tctx.pinned_size = 0;
+			seterr("HY013!Could not allocate pinned host memory");
+			return nullptr;
+		}
+		tctx.pinned_size = n;
+	}
+	return tctx.pinned;
+}
+
+// ---- profiling ---------------------------------------------------------------
+static std::mutex prof_mu;
+static std::map<std::string, std::pair<double, uint64_t>> prof;
+static bool prof_on = false;
+
+ProfScope::ProfScope(const char *n) : name(n), on(prof_on)
+{
+	if (on) {
+		(void) hipEventCreate(&e0);
+		(void) hipEventCreate(&e1);
+		(void) hipEventRecord(e0, stream());
+	}
+}
+
+ProfScope::~ProfScope()
+{
+	if (!on)
+		return;
+	(void) hipEventRecord(e1, stream());
+	(void) hipEventSynchronize(e1);
+	float ms = 0;
+	(void) hipEventElapsedTime(&ms, e0, e1);
+	(void) hipEventDestroy(e0);
+	(void) hipEventDestroy(e1);
+	std::lock_guard<std::mutex> g(prof_mu);
+	auto &x = prof[name];
+	x.first += ms;
+	x.second += 1;
+}
+
+// ---- BATs ----------------------------------------------------------------------
+int
+width_of(int tt)
+{
+	switch (tt) {
+	case MGDK_void: return 0;
+	case MGDK_bit: case MGDK_bte: return 1;
+	case MGDK_sht: return 2;
+	case MGDK_int: case MGDK_date: case MGDK_flt: return 4;
+	case MGDK_oid: case MGDK_lng: case MGDK_dbl: return 8;
+	case MGDK_hge: return 16;
+	case MGDK_str: return 1;
+	default: return -1;
+	}
+}
+
+int
+basetype(int tt)
+{
+	return tt == MGDK_date ? MGDK_int : tt == MGDK_bit ? MGDK_bte : tt;
+}
+
+const char *
+atomname(int tt)
+{
+	switch (tt) {
+	case MGDK_void: return "void";
+	case MGDK_bit: return "bit";
+	case MGDK_bte: return "bte";
+	case MGDK_sht: return "sht";
+	case MGDK_int: return "int";
+	case MGDK_oid: return "oid";
+	case MGDK_flt: return "flt";
+	case MGDK_dbl: return "dbl";
+	case MGDK_lng: return "lng";
+	case MGDK_hge: return "hge";
+	case MGDK_date: return "date";
+	case MGDK_str: return "str";
+	}
+	return "any";
+}
+
+static Heap *
+heap_new(size_t bytes)
+{
+	Heap *h = new Heap;
+	h->size = bytes;
+	h->refs = 1;
+	h->base = bytes ? dalloc(bytes) : nullptr;
+	if (bytes && h->base == nullptr) {
+		delete h;
+		return nullptr;
+	}
+	return h;
+}
+
+static void
+heap_decref(Heap *h)
+{
+	if (h == nullptr)
+		return;
+	if (__atomic_sub_fetch(&h->refs, 1, __ATOMIC_ACQ_REL) == 0) {
+		dfree(h->base);
+		delete h;
+	}
+}
+
+mgdk_bat *
+newbat(oid hseq, int tt, BUN cap)
+{
+	int w = width_of(tt);
+	if (w < 0) {
+		seterr("42000!type %d not supported", tt);
+		return nullptr;
+	}
+	mgdk_bat *b = (mgdk_bat *) calloc(1, sizeof(mgdk_bat));
+	Priv *p = new Priv{};
+	b->priv = p;
+	b->ttype = tt;
+	b->twidth = w;
+	b->hseqbase = hseq;
+	b->tseqbase = tt == MGDK_void ? 0 : MGDK_OID_NIL;
+	b->tsorted = b->trevsorted = b->tkey = 1;
+	b->tnonil = 1;
+	if (w > 0) {
+		p->theap = heap_new((cap ? cap : 1) * (size_t) w);
+		if (p->theap == nullptr) {
+			delete p;
+			free(b);
+			return nullptr;
+		}
+		b->theap = p->theap->base;
+	}
+	return b;
+}
+
+void
+setdense(mgdk_bat *b, oid tseq, BUN cnt)
+{
+	Priv *p = (Priv *) b->priv;
+	heap_decref(p->theap);
+	p->theap = nullptr;
+	b->theap = nullptr;
+	b->ttype = MGDK_void;
+	b->twidth = 0;
+	b->tseqbase = tseq;
+	b->count = cnt;
+	b->tsorted = b->tkey = b->tnonil = 1;
+	b->tnil = 0;
+	b->trevsorted = cnt <= 1;
+}
+
+void
+share_vheap(mgdk_bat *dst, const mgdk_bat *src)
+{
+	Priv *d = (Priv *) dst->priv, *s = (Priv *) src->priv;
+	if (s->tvheap)
+		__atomic_add_fetch(&s->tvheap->refs, 1, __ATOMIC_ACQ_REL);
+	heap_decref(d->tvheap);
+	d->tvheap = s->tvheap;
+	dst->tvheap = src->tvheap;
+	dst->tvheapsize = src->tvheapsize;
+}
+
+// ---- candidate lists -------------------------------------------------------------
+__global__ void
+k_lower_bounds(const oid *a, BUN n, oid lo, oid hi, BUN *out)
+{
+	// out[0] = lower_bound(a, lo), out[1] = lower_bound(a, hi),
+	// out[2] = a[p], out[3] = a[q-1]
+	BUN p = 0, e = n;
+	while (p < e) {
+		BUN m = (p + e) / 2;
+		if (a[m] < lo) p = m + 1; else e = m;
+	}
+	BUN q = p;
+	e = n;
+	while (q < e) {
+		BUN m = (q + e) / 2;
+		if (a[m] < hi) q = m + 1; else e = m;
+	}
+	out[0] = p;
+	out[1] = q;
+	out[2] = q > p ? a[p] : 0;
+	out[3] = q > p ? a[q - 1] : 0;
+}
+
+int
+cand_init(Cand *ci, const mgdk_bat *b, const mgdk_bat *s)
+{
+	oid lo = b ? b->hseqbase : 0;
+	oid hi = b ? b->hseqbase + b->count : ~(oid) 0;
+	*ci = Cand{};
+	ci->dense = true;
+	if (s == nullptr) {
+		ci->seq = lo;
+		ci->n = b ? b->count : 0;
+		ci->first = lo;
+		ci->last = lo + ci->n - 1;
+		return 0;
+	}
+	if (s->count == 0 || (b && b->count == 0))
+		return 0;
+	if (s->ttype == MGDK_void) {
+		if (s->tseqbase == MGDK_OID_NIL) {
+			seterr("candidate list with nil seqbase");
+			return -1;
+		}
+		oid a = s->tseqbase, e = s->tseqbase + s->count;
+		if (a < lo) a = lo;
+		if (e > hi) e = hi;
+		if (a < e) {
+			ci->seq = a;
+			ci->n = e - a;
+			ci->first = a;
+			ci->last = e - 1;
+		}
+		return 0;
+	}
+	if (s->ttype == MGDK_msk) {
+		seterr("42000!mask candidate lists are not supported on the device path");
+		return -1;
+	}
+	if (s->ttype != MGDK_oid) {
+		seterr("candidate list must have type oid");
+		return -1;
+	}
+	BUN *meta = (BUN *) meta_buf();
+	if (meta == nullptr)
+		return -1;
+	hipLaunchKernelGGL(k_lower_bounds, dim3(1), dim3(1), 0, stream(),
+			   (const oid *) s->theap, s->count, lo, hi, meta);
+	BUN *h = (BUN *) pinned(64);
+	if (h == nullptr)
+		return -1;
+	if (!hip_ok(hipMemcpyAsync(h, meta, 4 * sizeof(BUN), hipMemcpyDeviceToHost, stream()),
+		    "hipMemcpyAsync") || !sync())
+		return -1;
+	BUN p = h[0], q = h[1];
+	if (p >= q)
+		return 0;
+	ci->n = q - p;
+	ci->first = h[2];
+	ci->last = h[3];
+	if (ci->last - ci->first == ci->n - 1) {
+		ci->seq = ci->first;
+	} else {
+		ci->dense = false;
+		ci->oids = (const oid *) s->theap + p;
+	}
+	return 0;
+}
+
+}  // namespace mgdk
+
+using namespace mgdk;
+
+extern "C" {
+
+int
+mgdk_init(int device)
+{
+	int n = 0;
+	if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+		seterr("HY013!no HIP device available");
+		return -1;
+	}
+	if (device < 0 || device >= n) {
+		seterr("HY013!device %d out of range (%d devices)", device, n);
+		return -1;
+	}
+	g_device = device;
+	if (!hip_ok(hipSetDevice(device), "hipSetDevice"))
+		return -1;
+	return stream() ? 0 : -1;
+}
+
+const char *
+mgdk_GDKerrbuf(void)
+{
+	return errbuf;
+}
+
+void
+mgdk_GDKclrerr(void)
+{
+	errbuf[0] = 0;
+}
+
+int
+mgdk_sync(void)
+{
+	return sync() ? 0 : -1;
+}
+
+void *
+mgdk_stream(void)
+{
+	return (void *) stream();
+}
+
+uint64_t
+mgdk_mem_cursize(void)
+{
+	std::lock_guard<std::mutex> g(alloc_mu);
+	return cur_bytes;
+}
+
+void
+mgdk_mem_release_cache(void)
+{
+	std::lock_guard<std::mutex> g(alloc_mu);
+	for (auto &kv : free_lists)
+		for (void *p : kv.second)
+			(void) hipFree(p);
+	free_lists.clear();
+	cached_bytes = 0;
+}
+
+void
+mgdk_prof_enable(int on)
+{
+	prof_on = on != 0;
+}
+
+int
+mgdk_prof_get(const char *kernel, double *total_ms, uint64_t *launches)
+{
+	std::lock_guard<std::mutex> g(prof_mu);
+	auto it = prof.find(kernel);
+	if (it == prof.end()) {
+		*total_ms = 0;
+		*launches = 0;
+		return -1;
+	}
+	*total_ms = it->second.first;
+	*launches = it->second.second;
+	return 0;
+}
+
+void
+mgdk_prof_reset(void)
+{
+	std::lock_guard<std::mutex> g(prof_mu);
+	prof.clear();
+}
+
+mgdk_bat *
+mgdk_COLnew(mgdk_oid hseq, int tt, mgdk_BUN cap)
+{
+	return newbat(hseq, tt, cap);
+}
+
+mgdk_bat *
+mgdk_BATdense(mgdk_oid hseq, mgdk_oid tseq, mgdk_BUN cnt)
+{
+	mgdk_bat *b = newbat(hseq, MGDK_void, 0);
+	if (b)
+		setdense(b, tseq, cnt);
+	return b;
+}
+
+__global__ void
+k_fill(char *dst, const char *val, int w, BUN n)
+{
+	for (BUN i = blockIdx.x * (BUN) blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
+		for (int k = 0; k < w; k++)
+			dst[i * w + k] = val[k];
+}
+
+mgdk_bat *
+mgdk_BATconstant(mgdk_oid hseq, int tt, const void *val, mgdk_BUN cnt)
+{
+	mgdk_bat *b = newbat(hseq, tt, cnt);
+	if (b == nullptr)
+		return nullptr;
+	int w = b->twidth;
+	if (w > 0 && cnt > 0) {
+		char *dv = (char *) meta_buf();
+		if (!hip_ok(hipMemcpyAsync(dv, val, w, hipMemcpyHostToDevice, stream()), "memcpy")) {
+			mgdk_BBPunfix(b);
+			return nullptr;
+		}
+		hipLaunchKernelGGL(k_fill, dim3(grid_for(cnt, 1024, 4096)), dim3(256), 0, stream(),
+				   (char *) b->theap, dv, w, cnt);
+		if (!sync()) {
+			mgdk_BBPunfix(b);
+			return nullptr;
+		}
+	}
+	b->count = cnt;
+	b->tsorted = b->trevsorted = 1;
+	b->tkey = cnt <= 1;
+	return b;
+}
+
+mgdk_bat *
+mgdk_BATslice(mgdk_bat *b, mgdk_BUN lo, mgdk_BUN hi)
+{
+	if (hi > b->count)
+		hi = b->count;
+	if (lo > hi)
+		lo = hi;
+	mgdk_bat *v = (mgdk_bat *) calloc(1, sizeof(mgdk_bat));
+	Priv *p = new Priv{}, *bp = (Priv *) b->priv;
+	*v = *b;
+	v->priv = p;
+	v->hseqbase = b->hseqbase + lo;
+	v->count = hi - lo;
+	if (b->ttype == MGDK_void) {
+		if (b->tseqbase != MGDK_OID_NIL)
+			v->tseqbase = b->tseqbase + lo;
+	} else {
+		p->theap = bp->theap;
+		if (p->theap)
+			__atomic_add_fetch(&p->theap->refs, 1, __ATOMIC_ACQ_REL);
+		v->theap = (char *) b->theap + lo * (size_t) b->twidth;
+	}
+	if (bp->tvheap) {
+		p->tvheap = bp->tvheap;
+		__atomic_add_fetch(&p->tvheap->refs, 1, __ATOMIC_ACQ_REL);
+	}
+	if (v->count <= 1)
+		v->tsorted = v->trevsorted = v->tkey = 1;
+	return v;
+}
+
+void
+mgdk_BBPunfix(mgdk_bat *b)
+{
+	if (b == nullptr)
+		return;
+	Priv *p = (Priv *) b->priv;
+	if (p) {
+		heap_decref(p->theap);
+		heap_decref(p->tvheap);
+		delete p;
+	}
+	free(b);
+}
+
+int
+mgdk_BATupload(mgdk_bat *b, const void *host, mgdk_BUN n)
+{
+	if (b->ttype == MGDK_void) {
+		seterr("cannot upload into a void BAT");
+		return -1;
+	}
+	Priv *p = (Priv *) b->priv;
+	size_t bytes = n * (size_t) b->twidth;
+	if (p->theap == nullptr || p->theap->size < bytes + ((char *) b->theap - (char *) p->theap->base)) {
+		Heap *h = heap_new(bytes ? bytes : 1);
+		if (h == nullptr)
+			return -1;
+		heap_decref(p->theap);
+		p->theap = h;
+		b->theap = h->base;
+	}
+	if (bytes && !hip_ok(hipMemcpyAsync(b->theap, host, bytes, hipMemcpyHostToDevice, stream()),
+			     "hipMemcpyAsync H2D"))
+		return -1;
+	b->count = n;
+	return sync() ? 0 : -1;
+}
+
+int
+mgdk_BATdownload(const mgdk_bat *b, void *host)
+{
+	if (b->ttype == MGDK_void) {
+		oid *o = (oid *) host;
+		for (BUN i = 0; i < b->count; i++)
+			o[i] = b->tseqbase == MGDK_OID_NIL ? MGDK_OID_NIL : b->tseqbase + i;
+		return 0;
+	}
+	size_t bytes = b->count * (size_t) b->twidth;
+	if (bytes && !hip_ok(hipMemcpyAsync(host, b->theap, bytes, hipMemcpyDeviceToHost, stream()),
+			     "hipMemcpyAsync D2H"))
+		return -1;
+	return sync() ? 0 : -1;
+}
+
+int
+mgdk_BATsetvheap(mgdk_bat *b, const void *host, uint64_t size)
+{
+	Priv *p = (Priv *) b->priv;
+	Heap *h = heap_new(size ? size : 1);
+	if (h == nullptr)
+		return -1;
+	if (size && !hip_ok(hipMemcpyAsync(h->base, host, size, hipMemcpyHostToDevice, stream()), "vheap"))
+		return -1;
+	heap_decref(p->tvheap);
+	p->tvheap = h;
+	b->tvheap = h->base;
+	b->tvheapsize = size;
+	return sync() ? 0 : -1;
+}
+
+int
+mgdk_BATdownload_vheap(const mgdk_bat *b, void *host)
+{
+	if (b->tvheap == nullptr)
+		return 0;
+	if (!hip_ok(hipMemcpyAsync(host, b->tvheap, b->tvheapsize, hipMemcpyDeviceToHost, stream()), "vheap"))
+		return -1;
+	return sync() ? 0 : -1;
+}
+
+}  // extern "C"

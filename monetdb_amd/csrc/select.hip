@@ -1,0 +1,702 @@
+// select.hip -- BATselect / BATthetaselect on the MI355X.
+//
+// Host side restates the argument normalisation of BATselect
+// (gdk/gdk_select.c:1342-1564, nil/anti table :1288-1340) and of the typed
+// scan (scanfunc, :300-446), which reduces every request to one of a few
+// closed predicates.  The device side is a single-pass, order-preserving
+// stream compaction:
+//   * a tile = 8 rows x 256 lanes x 16 B of the column (8 KiB of int32);
+//     every lane issues its eight 16-B loads up front (coalesced, 1 KiB per
+//     wave instruction), evaluates the predicate and keeps a hit bitmask;
+//   * ranks inside a wave come from __ballot + popcount of the per-lane hit
+//     counts (no LDS traffic), ranks of the 32 (row, wave) segments of a tile
+//     from one wave-level scan in LDS;
+//   * the tile's output offset comes from decoupled look-back over
+//     per-tile 8-byte status granules {flag:2, count:62} written and polled
+//     with agent-scope relaxed atomics (MI355X_MICROARCH.md "Valid forms",
+//     R2 granule hand-off), tiles being numbered in dispatch order by an
+//     atomic ticket so every predecessor is already resident;
+//   * the sorted oid list is written directly; a dense result is
+//     virtualised like virtualize() (gdk_select.c:31-89).
+// Input bytes are read exactly once; output = 8 B per hit.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <vector>
+
+#include "mgdk_internal.h"
+
+using namespace mgdk;
+
+namespace {
+
+enum SelMode { SEL_RANGE = 0, SEL_ANTI = 1, SEL_EQ = 2, SEL_EQNIL = 3, SEL_NOTNIL = 4 };
+
+template <typename T>
+struct SelPred {
+	int mode;
+	bool nil_matches;
+	T vl, vh;
+	__device__ __forceinline__ bool operator()(T v) const {
+		switch (mode) {
+		case SEL_RANGE: return v >= vl && v <= vh;
+		case SEL_ANTI:
+			return nil_matches ? (is_nil(v) || v <= vl || v >= vh)
+					   : (!is_nil(v) && (v <= vl || v >= vh));
+		case SEL_EQ: return v == vl;
+		case SEL_EQNIL: return is_nil(v);
+		default: return !is_nil(v);
+		}
+	}
+};
+
+constexpr uint64_t ST_AGG = 1ull << 62, ST_PRE = 2ull << 62, ST_VAL = (1ull << 62) - 1;
+
+__device__ __forceinline__ uint64_t
+lb_load(uint64_t *p)
+{
+	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void
+lb_store(uint64_t *p, uint64_t v)
+{
+	__hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Decoupled look-back, executed by one full wave; returns the exclusive
+// prefix of `tile`.  status[] must be zero before the launch.
+__device__ uint64_t
+lookback(uint64_t *status, uint32_t tile, uint64_t agg, uint32_t *err)
+{
+	const unsigned lane = __lane_id();
+	if (tile == 0) {
+		if (lane == 0)
+			lb_store(&status[0], ST_PRE | agg);
+		return 0;
+	}
+	if (lane == 0)
+		lb_store(&status[tile], ST_AGG | agg);
+	uint64_t excl = 0;
+	int64_t base = (int64_t) tile - 1;
+	for (;;) {
+		int64_t idx = base - (int64_t) lane;
+		uint64_t s = ST_PRE;
+		if (idx >= 0) {
+			uint32_t spins = 0;
+			for (;;) {
+				s = lb_load(&status[idx]);
+				if ((s >> 62) != 0)
+					break;
+				if (++spins > (1u << 26)) {
+					atomicOr(err, 1u);
+					s = ST_PRE;
+					break;
+				}
+				__builtin_amdgcn_s_sleep(1);
+			}
+		}
+		uint64_t pmask = __ballot((s >> 62) == 2);
+		int first = pmask ? __ffsll((long long) pmask) - 1 : 64;
+		uint64_t v = ((int) lane <= first) ? (s & ST_VAL) : 0;
+#pragma unroll
+		for (int o = 32; o > 0; o >>= 1)
+			v += __shfl_xor(v, o);
+		excl += v;
+		if (pmask)
+			break;
+		base -= 64;
+	}
+	if (lane == 0)
+		lb_store(&status[tile], ST_PRE | (excl + agg));
+	return excl;
+}
+
+template <int BITS>
+__device__ __forceinline__ void
+wave_rank(uint32_t c, uint64_t lt, uint32_t &excl, uint32_t &tot)
+{
+	excl = 0;
+	tot = 0;
+#pragma unroll
+	for (int b = 0; b < BITS; b++) {
+		uint64_t bal = __ballot((c >> b) & 1u);
+		excl += (uint32_t) __popcll(bal & lt) << b;
+		tot += (uint32_t) __popcll(bal) << b;
+	}
+}
+
+template <int V> struct Bits { static constexpr int v = V <= 1 ? 1 : V <= 3 ? 2 : V <= 7 ? 3 : V <= 15 ? 4 : 5; };
+
+template <typename T>
+struct SelArgs {
+	const T *col;             // b's tail; value of oid o is col[o - hseq]
+	oid hseq;
+	const T *col_al;          // dense: 16-B aligned base, slot j -> col_al[j]
+	const oid *cand_al;       // materialized: 16-B aligned base of candidate oids
+	oid cseq;                 // dense: oid of slot `shift`
+	uint64_t n;               // number of candidates
+	uint32_t shift;           // leading invalid slots (alignment)
+	uint32_t ntiles;
+	SelPred<T> pred;
+	oid *out;
+	uint64_t *status;         // [ntiles] look-back granules
+	uint32_t *ticket;         // dynamic tile numbering
+	uint64_t *meta;           // [0] total count, [1] error flags
+};
+
+constexpr int ROWS = 8;
+
+template <typename T, bool MAT>
+__global__ __launch_bounds__(256) void
+k_select(SelArgs<T> a)
+{
+	constexpr int V = MAT ? 2 : (int) (16 / sizeof(T));
+	constexpr int BITS = Bits<V>::v;
+	typedef T vec_t __attribute__((ext_vector_type(V)));
+	__shared__ uint32_t s_tile;
+	__shared__ uint32_t s_off[ROWS * 4];
+	__shared__ uint64_t s_prefix;
+
+	const unsigned tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+	if (tid == 0)
+		s_tile = atomicAdd(a.ticket, 1u);
+	__syncthreads();
+	const uint32_t tile = s_tile;
+	const uint64_t nslots = a.n + a.shift;
+	const uint64_t lt = lanemask_lt();
+
+	uint32_t hm[ROWS];
+	oid cv[MAT ? ROWS * 2 : 1];
+	(void) cv;
+#pragma unroll
+	for (int r = 0; r < ROWS; r++) {
+		const uint64_t vi = ((uint64_t) tile * ROWS + r) * 256 + tid;
+		const uint64_t j0 = vi * V;
+		uint32_t m = 0;
+		if (j0 < nslots) {
+			if constexpr (!MAT) {
+				vec_t x = *(const vec_t *) (a.col_al + j0);
+#pragma unroll
+				for (int k = 0; k < V; k++) {
+					uint64_t j = j0 + k;
+					bool ok = j >= a.shift && j < nslots && a.pred(x[k]);
+					m |= (uint32_t) ok << k;
+				}
+			} else {
+				typedef oid ovec_t __attribute__((ext_vector_type(2)));
+				ovec_t o = *(const ovec_t *) (a.cand_al + j0);
+#pragma unroll
+				for (int k = 0; k < 2; k++) {
+					uint64_t j = j0 + k;
+					cv[r * 2 + k] = o[k];
+					if (j >= a.shift && j < nslots) {
+						T v = a.col[o[k] - a.hseq];
+						m |= (uint32_t) a.pred(v) << k;
+					}
+				}
+			}
+		}
+		hm[r] = m;
+	}
+	// per (row, wave) totals
+#pragma unroll
+	for (int r = 0; r < ROWS; r++) {
+		uint32_t ex, tot;
+		wave_rank<BITS>((uint32_t) __popc(hm[r]), lt, ex, tot);
+		if (lane == 0)
+			s_off[r * 4 + wave] = tot;
+	}
+	__syncthreads();
+	if (wave == 0) {
+		uint32_t x = lane < ROWS * 4 ? s_off[lane] : 0u;
+		const uint32_t own = x;
+#pragma unroll
+		for (int o = 1; o < 64; o <<= 1) {
+			uint32_t y = __shfl_up(x, o);
+			if ((int) lane >= o)
+				x += y;
+		}
+		if (lane < ROWS * 4)
+			s_off[lane] = x - own;
+		uint64_t agg = __shfl(x, ROWS * 4 - 1);
+		uint64_t pre = lookback(a.status, tile, agg, (uint32_t *) &a.meta[1]);
+		if (lane == 0) {
+			s_prefix = pre;
+			if (tile == a.ntiles - 1)
+				a.meta[0] = pre + agg;
+		}
+	}
+	__syncthreads();
+	const uint64_t prefix = s_prefix;
+#pragma unroll
+	for (int r = 0; r < ROWS; r++) {
+		uint32_t ex, tot;
+		wave_rank<BITS>((uint32_t) __popc(hm[r]), lt, ex, tot);
+		uint64_t pos = prefix + s_off[r * 4 + wave] + ex;
+		uint32_t m = hm[r];
+		const uint64_t j0 = (((uint64_t) tile * ROWS + r) * 256 + tid) * V;
+		while (m) {
+			int k = __ffs(m) - 1;
+			m &= m - 1;
+			oid o;
+			if constexpr (MAT)
+				o = cv[r * 2 + k];
+			else
+				o = a.cseq + (j0 + k - a.shift);
+			a.out[pos++] = o;
+		}
+	}
+}
+
+__global__ void
+k_select_fin(const oid *out, uint64_t *meta)
+{
+	uint64_t n = meta[0];
+	meta[2] = n ? out[0] : 0;
+	meta[3] = n ? out[n - 1] : 0;
+}
+
+// ---- host-side normalisation -------------------------------------------------
+template <typename T> struct Lim {
+	static T minv() { return std::numeric_limits<T>::min() + 1; }   // GDK_T_min = nil + 1
+	static T maxv() { return std::numeric_limits<T>::max(); }
+	static T prev(T x) { return x - 1; }
+	static T next(T x) { return x + 1; }
+	static bool isnil(T x) { return x == std::numeric_limits<T>::min(); }
+	static T nil() { return std::numeric_limits<T>::min(); }
+};
+template <> struct Lim<uint64_t> {   // oid: nil = 1<<63, GDK_oid_min = 0, max = 2^63-1
+	static uint64_t minv() { return 0; }
+	static uint64_t maxv() { return ((uint64_t) 1 << 63) - 1; }
+	static uint64_t prev(uint64_t x) { return x - 1; }
+	static uint64_t next(uint64_t x) { return x + 1; }
+	static bool isnil(uint64_t x) { return x == ((uint64_t) 1 << 63); }
+	static uint64_t nil() { return (uint64_t) 1 << 63; }
+};
+template <> struct Lim<hge> {
+	static hge maxv() { return (hge) (((uhge) 1 << 127) - 1); }
+	static hge minv() { return -maxv(); }
+	static hge prev(hge x) { return x - 1; }
+	static hge next(hge x) { return x + 1; }
+	static bool isnil(hge x) { return x == (hge) ((uhge) 1 << 127); }
+	static hge nil() { return (hge) ((uhge) 1 << 127); }
+};
+template <> struct Lim<float> {
+	static float minv() { return -std::numeric_limits<float>::max(); }
+	static float maxv() { return std::numeric_limits<float>::max(); }
+	static float prev(float x) { return nextafterf(x, -std::numeric_limits<float>::max()); }
+	static float next(float x) { return nextafterf(x, std::numeric_limits<float>::max()); }
+	static bool isnil(float x) { return std::isnan(x); }
+	static float nil() { return std::numeric_limits<float>::quiet_NaN(); }
+};
+template <> struct Lim<double> {
+	static double minv() { return -std::numeric_limits<double>::max(); }
+	static double maxv() { return std::numeric_limits<double>::max(); }
+	static double prev(double x) { return nextafter(x, -std::numeric_limits<double>::max()); }
+	static double next(double x) { return nextafter(x, std::numeric_limits<double>::max()); }
+	static bool isnil(double x) { return std::isnan(x); }
+	static double nil() { return std::numeric_limits<double>::quiet_NaN(); }
+};
+
+template <typename T>
+static int
+cmp3(T a, T b)
+{
+	// ATOMcmp: nil smallest and equal to itself
+	bool an = Lim<T>::isnil(a), bn = Lim<T>::isnil(b);
+	if (an || bn)
+		return an && bn ? 0 : an ? -1 : 1;
+	return (a > b) - (a < b);
+}
+
+// outcome of normalisation
+struct Plan {
+	enum { EMPTY, ALL, NOTNIL_ALL, SCAN } kind;
+};
+
+static mgdk_bat *
+empty_result()
+{
+	return mgdk_BATdense(0, 0, 0);
+}
+
+// all candidates as a new candidate list (canditer_slice)
+static mgdk_bat *
+cand_slice(const Cand &ci)
+{
+	if (ci.dense)
+		return mgdk_BATdense(0, ci.seq, ci.n);
+	mgdk_bat *bn = newbat(0, MGDK_oid, ci.n);
+	if (bn == nullptr)
+		return nullptr;
+	if (!hip_ok(hipMemcpyAsync(bn->theap, ci.oids, ci.n * sizeof(oid), hipMemcpyDeviceToDevice, stream()),
+		    "hipMemcpyAsync") || !sync()) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	bn->count = ci.n;
+	bn->tsorted = bn->tkey = bn->tnonil = 1;
+	bn->trevsorted = ci.n <= 1;
+	return bn;
+}
+
+template <typename T>
+static mgdk_bat *
+run_scan(const mgdk_bat *b, const Cand &ci, const SelPred<T> &pred)
+{
+	ProfScope prof("select");
+	mgdk_bat *bn = newbat(0, MGDK_oid, ci.n);
+	if (bn == nullptr)
+		return nullptr;
+	SelArgs<T> a{};
+	a.col = (const T *) b->theap;
+	a.hseq = b->hseqbase;
+	a.n = ci.n;
+	a.pred = pred;
+	a.out = (oid *) bn->theap;
+	uint64_t items_per_tile;
+	if (ci.dense) {
+		const T *start = a.col + (ci.seq - b->hseqbase);
+		uintptr_t mis = ((uintptr_t) start % 16) / sizeof(T);
+		a.col_al = start - mis;
+		a.shift = (uint32_t) mis;
+		a.cseq = ci.seq;
+		items_per_tile = (uint64_t) ROWS * 256 * (16 / sizeof(T));
+	} else {
+		uintptr_t mis = ((uintptr_t) ci.oids % 16) / sizeof(oid);
+		a.cand_al = ci.oids - mis;
+		a.shift = (uint32_t) mis;
+		items_per_tile = (uint64_t) ROWS * 256 * 2;
+	}
+	uint64_t ntiles = (ci.n + a.shift + items_per_tile - 1) / items_per_tile;
+	if (ntiles >= (1ull << 31)) {
+		seterr("select: input too large");
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	a.ntiles = (uint32_t) ntiles;
+	size_t sbytes = (ntiles + 8) * sizeof(uint64_t);
+	char *sc = (char *) scratch(sbytes);
+	uint64_t *meta = (uint64_t *) meta_buf();
+	if (sc == nullptr || meta == nullptr) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	a.ticket = (uint32_t *) sc;
+	a.status = (uint64_t *) sc + 8;
+	a.meta = meta;
+	hipStream_t st = stream();
+	if (!hip_ok(hipMemsetAsync(sc, 0, sbytes, st), "hipMemsetAsync") ||
+	    !hip_ok(hipMemsetAsync(meta, 0, 64, st), "hipMemsetAsync")) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	if (ci.dense)
+		hipLaunchKernelGGL((k_select<T, false>), dim3((unsigned) ntiles), dim3(256), 0, st, a);
+	else
+		hipLaunchKernelGGL((k_select<T, true>), dim3((unsigned) ntiles), dim3(256), 0, st, a);
+	hipLaunchKernelGGL(k_select_fin, dim3(1), dim3(1), 0, st, (const oid *) bn->theap, meta);
+	uint64_t *h = (uint64_t *) pinned(64);
+	if (h == nullptr || !hip_ok(hipMemcpyAsync(h, meta, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, st), "memcpy") ||
+	    !sync()) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	if (h[1] & 1) {
+		seterr("HY013!select: look-back did not complete");
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	uint64_t cnt = h[0];
+	bn->count = cnt;
+	bn->tsorted = bn->tkey = bn->tnonil = 1;
+	bn->tnil = 0;
+	bn->trevsorted = cnt <= 1;
+	if (cnt <= 1 || h[3] - h[2] == cnt - 1)
+		setdense(bn, cnt ? h[2] : 0, cnt);   // virtualize
+	return bn;
+}
+
+// The body of BATselect after candidate setup, for value type T.
+template <typename T>
+static mgdk_bat *
+select_typed(mgdk_bat *b, const Cand &ci, const T *tlp, const T *thp, bool li, bool hi,
+	     bool anti, bool nil_matches)
+{
+	const T nil = Lim<T>::nil();
+	T tl = *tlp, th = thp ? *thp : T{};
+	bool th_null = thp == nullptr;
+	bool lnil = cmp3(tl, nil) == 0;
+	bool lval = !lnil || th_null;
+	bool equi = th_null || (lval && cmp3(tl, th) == 0);
+	bool hval;
+	if (lnil && nil_matches && (th_null || cmp3(th, nil) == 0)) {
+		equi = true;
+		lval = true;
+	}
+	if (equi) {
+		if (th_null)
+			hi = li;
+		th = tl;
+		hval = true;
+		if (!anti && (!li || !hi))
+			return empty_result();
+	} else {
+		nil_matches = false;
+		hval = cmp3(th, nil) != 0;
+	}
+	if (anti) {
+		if (lval != hval) {
+			bool ti = li;
+			li = !hi;
+			hi = !ti;
+			T tv = tl;
+			tl = th;
+			th = tv;
+			ti = lval;
+			lval = hval;
+			hval = ti;
+			lnil = cmp3(tl, nil) == 0;
+			anti = false;
+		} else if (!lval && !hval) {
+			return empty_result();
+		} else if ((equi && (lnil || !(li && hi))) || cmp3(tl, th) > 0) {
+			if (equi && !lnil && nil_matches && !(li && hi))
+				return cand_slice(ci);
+			SelPred<T> p{SEL_NOTNIL, false, tl, th};
+			if (b->tnonil)
+				return cand_slice(ci);
+			return run_scan<T>(b, ci, p);
+		} else {
+			equi = false;   // anti-equi handled by the scan (gdk_select.c:1519)
+		}
+	}
+	if (hval && (equi ? !li || !hi : cmp3(tl, th) > 0))
+		return empty_result();
+	if (equi && lnil && b->tnonil)
+		return empty_result();
+	if (!equi && !lval && !hval && lnil && b->tnonil)
+		return cand_slice(ci);
+
+	// scanfunc normalisation (gdk_select.c:300-446)
+	T vl = tl, vh = th;
+	if (anti && li) {
+		if (vl == Lim<T>::minv()) {
+			anti = false;
+			vl = vh;
+			li = !hi;
+			hval = false;
+		} else {
+			vl = Lim<T>::prev(vl);
+			li = false;
+		}
+	}
+	if (anti && hi) {
+		if (vh == Lim<T>::maxv()) {
+			anti = false;
+			vh = vl;
+			hi = !li;
+			lval = false;
+		} else {
+			vh = Lim<T>::next(vh);
+			hi = false;
+		}
+	}
+	if (!anti) {
+		if (lval) {
+			if (!li) {
+				if (vl == Lim<T>::maxv())
+					return empty_result();
+				vl = Lim<T>::next(vl);
+				li = true;
+			}
+		} else {
+			vl = Lim<T>::minv();
+			li = true;
+			lval = true;
+		}
+		if (hval) {
+			if (!hi) {
+				if (vh == Lim<T>::minv())
+					return empty_result();
+				vh = Lim<T>::prev(vh);
+				hi = true;
+			}
+		} else {
+			vh = Lim<T>::maxv();
+			hi = true;
+			hval = true;
+		}
+		if (vl > vh)
+			return empty_result();
+	}
+	SelPred<T> p;
+	p.vl = vl;
+	p.vh = vh;
+	p.nil_matches = nil_matches;
+	if (equi)
+		p.mode = lnil ? SEL_EQNIL : SEL_EQ;
+	else if (anti)
+		p.mode = SEL_ANTI;
+	else
+		p.mode = SEL_RANGE;
+	return run_scan<T>(b, ci, p);
+}
+
+// void (dense oid) column: positional select, values are tseqbase + p
+static mgdk_bat *
+select_void(mgdk_bat *b, const Cand &ci, const oid *tl, const oid *th, bool li, bool hi,
+	    bool anti, bool nil_matches)
+{
+	// materialise the dense values once, then use the generic path
+	mgdk_bat *tmp = newbat(b->hseqbase, MGDK_oid, b->count);
+	if (tmp == nullptr)
+		return nullptr;
+	std::vector<oid> h(b->count);
+	for (BUN i = 0; i < b->count; i++)
+		h[i] = b->tseqbase == MGDK_OID_NIL ? MGDK_OID_NIL : b->tseqbase + i;
+	if (mgdk_BATupload(tmp, h.data(), b->count) < 0) {
+		mgdk_BBPunfix(tmp);
+		return nullptr;
+	}
+	tmp->tnonil = b->tseqbase != MGDK_OID_NIL;
+	mgdk_bat *r = select_typed<uint64_t>(tmp, ci, tl, th, li, hi, anti, nil_matches);
+	mgdk_BBPunfix(tmp);
+	return r;
+}
+
+}  // namespace
+
+namespace mgdk {
+// Ordered compaction of a 0/1 byte array: the sorted list of positions i
+// (as oids base + i) with flags[i] == 1.  Used by BATgroup / BATjoin.
+mgdk_bat *
+compact_flags(const int8_t *flags, BUN n, oid base)
+{
+	if (n == 0)
+		return empty_result();
+	mgdk_bat tmp{};
+	tmp.ttype = MGDK_bte;
+	tmp.twidth = 1;
+	tmp.count = n;
+	tmp.hseqbase = base;
+	tmp.theap = (void *) flags;
+	Cand ci{};
+	ci.dense = true;
+	ci.seq = base;
+	ci.n = n;
+	ci.first = base;
+	ci.last = base + n - 1;
+	SelPred<int8_t> p{SEL_EQ, false, 1, 1};
+	return run_scan<int8_t>(&tmp, ci, p);
+}
+}  // namespace mgdk
+
+extern "C" {
+
+mgdk_bat *
+mgdk_BATselect(mgdk_bat *b, mgdk_bat *s, const void *tl, const void *th, bool li, bool hi,
+	       bool anti, bool nil_matches)
+{
+	if (b == nullptr) {
+		seterr("BATselect: b must exist");
+		return nullptr;
+	}
+	if (tl == nullptr) {
+		seterr("tl value required");
+		return nullptr;
+	}
+	if (s && s->ttype != MGDK_msk && !s->tsorted) {
+		seterr("invalid argument: s must be sorted.\n");
+		return nullptr;
+	}
+	Cand ci;
+	if (cand_init(&ci, b, s) < 0)
+		return nullptr;
+	if (ci.n == 0)
+		return empty_result();
+	switch (basetype(b->ttype)) {
+	case MGDK_void:
+		return select_void(b, ci, (const oid *) tl, (const oid *) th, li, hi, anti, nil_matches);
+	case MGDK_bte:
+		return select_typed<int8_t>(b, ci, (const int8_t *) tl, (const int8_t *) th, li, hi, anti, nil_matches);
+	case MGDK_sht:
+		return select_typed<int16_t>(b, ci, (const int16_t *) tl, (const int16_t *) th, li, hi, anti, nil_matches);
+	case MGDK_int:
+		return select_typed<int32_t>(b, ci, (const int32_t *) tl, (const int32_t *) th, li, hi, anti, nil_matches);
+	case MGDK_lng:
+		return select_typed<int64_t>(b, ci, (const int64_t *) tl, (const int64_t *) th, li, hi, anti, nil_matches);
+	case MGDK_oid:
+		return select_typed<uint64_t>(b, ci, (const uint64_t *) tl, (const uint64_t *) th, li, hi, anti, nil_matches);
+	case MGDK_hge:
+		return select_typed<hge>(b, ci, (const hge *) tl, (const hge *) th, li, hi, anti, nil_matches);
+	case MGDK_flt:
+		return select_typed<float>(b, ci, (const float *) tl, (const float *) th, li, hi, anti, nil_matches);
+	case MGDK_dbl:
+		return select_typed<double>(b, ci, (const double *) tl, (const double *) th, li, hi, anti, nil_matches);
+	default:
+		seterr("42000!BATselect: type %s not supported on the device path", atomname(b->ttype));
+		return nullptr;
+	}
+}
+
+// BATthetaselect (gdk/gdk_select.c:2103-2154)
+mgdk_bat *
+mgdk_BATthetaselect(mgdk_bat *b, mgdk_bat *s, const void *val, const char *op)
+{
+	if (b == nullptr || val == nullptr || op == nullptr) {
+		seterr("BATthetaselect: NULL argument");
+		return nullptr;
+	}
+	if (strcmp(op, "eq") == 0)
+		return mgdk_BATselect(b, s, val, nullptr, true, true, false, true);
+	if (strcmp(op, "ne") == 0)
+		return mgdk_BATselect(b, s, val, nullptr, true, true, true, true);
+	alignas(16) unsigned char nilv[16];
+	bool isnil = false;
+	switch (basetype(b->ttype)) {
+	case MGDK_bte: *(int8_t *) nilv = INT8_MIN; isnil = *(const int8_t *) val == INT8_MIN; break;
+	case MGDK_sht: *(int16_t *) nilv = INT16_MIN; isnil = *(const int16_t *) val == INT16_MIN; break;
+	case MGDK_int: *(int32_t *) nilv = INT32_MIN; isnil = *(const int32_t *) val == INT32_MIN; break;
+	case MGDK_lng: *(int64_t *) nilv = INT64_MIN; isnil = *(const int64_t *) val == INT64_MIN; break;
+	case MGDK_void:
+	case MGDK_oid: *(uint64_t *) nilv = MGDK_OID_NIL; isnil = *(const uint64_t *) val == MGDK_OID_NIL; break;
+	case MGDK_hge: {
+		hge n = (hge) ((uhge) 1 << 127);
+		memcpy(nilv, &n, 16);
+		isnil = memcmp(val, &n, 16) == 0;
+		break;
+	}
+	case MGDK_flt: *(float *) nilv = std::numeric_limits<float>::quiet_NaN(); isnil = std::isnan(*(const float *) val); break;
+	case MGDK_dbl: *(double *) nilv = std::numeric_limits<double>::quiet_NaN(); isnil = std::isnan(*(const double *) val); break;
+	default:
+		seterr("42000!BATthetaselect: type %s not supported on the device path", atomname(b->ttype));
+		return nullptr;
+	}
+	if (isnil)
+		return empty_result();
+	if (op[0] == '=' && ((op[1] == '=' && op[2] == 0) || op[1] == 0))
+		return mgdk_BATselect(b, s, val, nullptr, true, true, false, false);
+	if (op[0] == '!' && op[1] == '=' && op[2] == 0)
+		return mgdk_BATselect(b, s, val, nullptr, true, true, true, false);
+	if (op[0] == '<') {
+		if (op[1] == 0)
+			return mgdk_BATselect(b, s, nilv, val, false, false, false, false);
+		if (op[1] == '=' && op[2] == 0)
+			return mgdk_BATselect(b, s, nilv, val, false, true, false, false);
+		if (op[1] == '>' && op[2] == 0)
+			return mgdk_BATselect(b, s, val, nullptr, true, true, true, false);
+	}
+	if (op[0] == '>') {
+		if (op[1] == 0)
+			return mgdk_BATselect(b, s, val, nilv, false, false, false, false);
+		if (op[1] == '=' && op[2] == 0)
+			return mgdk_BATselect(b, s, val, nilv, true, false, false, false);
+	}
+	seterr("unknown operator.\n");
+	return nullptr;
+}
+
+}  // extern "C"

@@ -1,0 +1,551 @@
+// tpch.hip -- synthetic TPC-H lineitem generation in HBM and the fused
+// Q6 / Q1 column pipelines.
+//
+// Generation restates oracle/tpch_gen.c (the same counter-based splitmix64
+// values, so a row range can be generated on any GPU shard and checked
+// against the CPU oracle bit for bit).
+//
+// Fused pipelines: one streaming pass over the lineitem columns computing
+// exactly what the op-at-a-time MAL plans compute:
+//   Q6  select(shipdate in [d0,d1)) -> select(disc in [dlo,dhi]) ->
+//       thetaselect(qty < qmax) -> project price, disc -> price*disc (hge)
+//       -> sum.  28 B/row: each lane handles 4 consecutive rows with 16-B
+//       loads (shipdate 1 x 16 B, each lng column 2 x 16 B), keeps an exact
+//       128-bit partial, one pair of 64-bit atomics per wave at the end.
+//   Q1  thetaselect(shipdate <= dmax) -> group(returnflag) ->
+//       subgroup(linestatus) -> sums of qty, price, price*(100-disc),
+//       price*(100-disc)*(100+tax), disc and counts (avg3 derives from the
+//       exact sums).  38 B/row.  The few (returnflag, linestatus) keys are
+//       discovered on a prefix with their first-occurrence rows, then the
+//       main pass keeps K register-resident accumulator sets per lane
+//       (K <= 8, predicated adds, no atomics in the loop).  Any row whose key
+//       was not in the prefix, any nil, or any value outside the ranges for
+//       which the 64-bit lane partials are exact makes the call fall back to
+//       the op-at-a-time device plan (pipelines.hip), so results are always
+//       the reference's.
+#include <algorithm>
+#include <vector>
+
+#include "mgdk_internal.h"
+
+using namespace mgdk;
+
+namespace {
+
+__device__ __host__ __forceinline__ uint64_t
+mix64(uint64_t z)
+{
+	z += 0x9e3779b97f4a7c15ull;
+	z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+	z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+	return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint64_t
+rnd(uint64_t seed, uint64_t row, uint64_t col)
+{
+	return mix64(seed ^ mix64(row * 16 + col));
+}
+
+__device__ __forceinline__ int64_t
+urange(uint64_t r, int64_t lo, int64_t hi)
+{
+	uint64_t span = (uint64_t) (hi - lo + 1);
+	return lo + (int64_t) __umul64hi(r, span);
+}
+
+constexpr int ORDERDATE_DAYS = 2405;   // 1998-08-02 - 1992-01-01
+constexpr int CURRENTDATE_DAY = 1263;  // 1995-06-17 - 1992-01-01
+constexpr int TABLE_DAYS = ORDERDATE_DAYS + 121 + 30 + 2;
+
+__global__ __launch_bounds__(256) void
+k_lineitem(uint64_t seed, uint64_t row0, uint64_t n, uint64_t sf_parts, const int32_t *table,
+	   int32_t *shipdate, int64_t *quantity, int64_t *extendedprice, int64_t *discount,
+	   int64_t *tax, uint8_t *returnflag, uint8_t *linestatus)
+{
+	for (uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n;
+	     i += (uint64_t) gridDim.x * blockDim.x) {
+		uint64_t row = row0 + i;
+		int od = (int) urange(rnd(seed, row, 0), 0, ORDERDATE_DAYS);
+		int sd = od + (int) urange(rnd(seed, row, 1), 1, 121);
+		int rd = sd + (int) urange(rnd(seed, row, 2), 1, 30);
+		int64_t q = urange(rnd(seed, row, 3), 1, 50);
+		int64_t pk = urange(rnd(seed, row, 4), 1, (int64_t) sf_parts);
+		int64_t rp = 90000 + ((pk / 10) % 20001) + 100 * (pk % 1000);
+		shipdate[i] = table[sd];
+		quantity[i] = q * 100;
+		extendedprice[i] = q * rp;
+		discount[i] = urange(rnd(seed, row, 5), 0, 10);
+		tax[i] = urange(rnd(seed, row, 6), 0, 8);
+		returnflag[i] = rd <= CURRENTDATE_DAY ? ((rnd(seed, row, 7) >> 63) ? 16 : 0) : 8;
+		linestatus[i] = sd > CURRENTDATE_DAY ? 8 : 0;
+	}
+}
+
+int
+isleap(int y)
+{
+	return y % 4 == 0 && (y % 100 != 0 || y % 400 == 0);
+}
+
+int32_t
+mkdate(int y, int m, int d)
+{
+	return (int32_t) ((((uint32_t) ((y + 4712) * 12 + m - 1)) << 5) | (uint32_t) d);
+}
+
+std::vector<int32_t>
+date_table()
+{
+	static const int cum[13] = {0, 31, 59, 90, 120, 151, 181, 212, 243, 273, 304, 334, 365};
+	std::vector<int32_t> t(TABLE_DAYS);
+	int y = 1992, doy = 0;
+	for (int i = 0; i < TABLE_DAYS; i++) {
+		int m = 1;
+		while (m < 12 && doy >= cum[m] + (m >= 2 && isleap(y)))
+			m++;
+		int start = cum[m - 1] + (m > 2 && isleap(y));
+		t[i] = mkdate(y, m, doy - start + 1);
+		if (++doy == 365 + isleap(y)) {
+			doy = 0;
+			y++;
+		}
+	}
+	return t;
+}
+
+__device__ __forceinline__ void
+atomic_add128(unsigned long long *lohi, hge v)
+{
+	const unsigned long long lo = (unsigned long long) (uhge) v;
+	const unsigned long long hi = (unsigned long long) ((uhge) v >> 64);
+	unsigned long long old = atomicAdd(&lohi[0], lo);
+	unsigned long long carry = (old + lo) < old ? 1ull : 0ull;
+	if (hi + carry)
+		atomicAdd(&lohi[1], hi + carry);
+}
+
+__device__ __forceinline__ hge
+wave_sum128(hge s)
+{
+	for (int o = 32; o > 0; o >>= 1) {
+		unsigned long long lo = __shfl_xor((unsigned long long) (uhge) s, o);
+		unsigned long long hi = __shfl_xor((unsigned long long) ((uhge) s >> 64), o);
+		s += (hge) (((uhge) hi << 64) | lo);
+	}
+	return s;
+}
+
+// ---- Q6 -------------------------------------------------------------------
+struct Q6Args {
+	const int32_t *sd;
+	const int64_t *disc, *qty, *price;
+	uint64_t n;          // rows
+	int32_t d0, d1;
+	int64_t dlo, dhi, qmax;
+	unsigned long long *out;   // [2] 128-bit revenue
+};
+
+__device__ __forceinline__ hge
+q6_row(const Q6Args &a, int32_t sd, int64_t di, int64_t q, int64_t p)
+{
+	bool ok = sd != INT32_MIN && sd >= a.d0 && sd < a.d1 && di != INT64_MIN && di >= a.dlo &&
+		  di <= a.dhi && q != INT64_MIN && q < a.qmax && p != INT64_MIN;
+	return ok ? (hge) p * (hge) di : (hge) 0;
+}
+
+template <int UNROLL>
+__global__ __launch_bounds__(256) void
+k_q6(Q6Args a)
+{
+	typedef int32_t i4 __attribute__((ext_vector_type(4)));
+	typedef int64_t l2 __attribute__((ext_vector_type(2)));
+	hge acc = 0;
+	const uint64_t nq = a.n / 4;   // full quads
+	const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+	uint64_t q = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
+	for (; q + (UNROLL - 1) * stride < nq; q += UNROLL * stride) {
+		i4 sd[UNROLL];
+		l2 d0[UNROLL], d1[UNROLL], q0[UNROLL], q1[UNROLL], p0[UNROLL], p1[UNROLL];
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++) {
+			uint64_t r = (q + u * stride) * 4;
+			sd[u] = *(const i4 *) (a.sd + r);
+			d0[u] = *(const l2 *) (a.disc + r);
+			d1[u] = *(const l2 *) (a.disc + r + 2);
+			q0[u] = *(const l2 *) (a.qty + r);
+			q1[u] = *(const l2 *) (a.qty + r + 2);
+			p0[u] = *(const l2 *) (a.price + r);
+			p1[u] = *(const l2 *) (a.price + r + 2);
+		}
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++) {
+			acc += q6_row(a, sd[u][0], d0[u][0], q0[u][0], p0[u][0]);
+			acc += q6_row(a, sd[u][1], d0[u][1], q0[u][1], p0[u][1]);
+			acc += q6_row(a, sd[u][2], d1[u][0], q1[u][0], p1[u][0]);
+			acc += q6_row(a, sd[u][3], d1[u][1], q1[u][1], p1[u][1]);
+		}
+	}
+	for (; q < nq; q += stride) {
+		uint64_t r = q * 4;
+		for (int k = 0; k < 4; k++)
+			acc += q6_row(a, a.sd[r + k], a.disc[r + k], a.qty[r + k], a.price[r + k]);
+	}
+	// tail rows
+	if (blockIdx.x == 0 && threadIdx.x < (a.n & 3)) {
+		uint64_t r = nq * 4 + threadIdx.x;
+		acc += q6_row(a, a.sd[r], a.disc[r], a.qty[r], a.price[r]);
+	}
+	acc = wave_sum128(acc);
+	if (__lane_id() == 0 && acc != 0)
+		atomic_add128(a.out, acc);
+}
+
+__global__ __launch_bounds__(256) void
+k_q6_scalar(Q6Args a)
+{
+	hge acc = 0;
+	for (uint64_t r = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; r < a.n; r += (uint64_t) gridDim.x * blockDim.x)
+		acc += q6_row(a, a.sd[r], a.disc[r], a.qty[r], a.price[r]);
+	acc = wave_sum128(acc);
+	if (__lane_id() == 0 && acc != 0)
+		atomic_add128(a.out, acc);
+}
+
+// ---- Q1 -------------------------------------------------------------------
+constexpr int Q1_MAXK = 8;
+
+struct Q1Args {
+	const int32_t *sd;
+	const uint8_t *rf, *ls;
+	const int64_t *qty, *price, *disc, *tax;
+	uint64_t n;
+	int32_t dmax;
+	int K;
+	uint32_t codes[Q1_MAXK];          // rf << 8 | ls
+	unsigned long long *acc;          // [K][12]: qty, price, discprice(2), charge(2), disc, count (+pad)
+	uint32_t *flags;                  // [0] unknown key, [1] out of range / nil
+};
+
+__global__ __launch_bounds__(256) void
+k_q1_keys(const int32_t *sd, const uint8_t *rf, const uint8_t *ls, uint64_t n, int32_t dmax,
+	  unsigned long long *first)
+{
+	for (uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x) {
+		int32_t d = sd[i];
+		if (d == INT32_MIN || d > dmax)
+			continue;
+		uint32_t c = ((uint32_t) rf[i] << 8) | ls[i];
+		if (first[c] > i)
+			atomicMin(&first[c], (unsigned long long) i);
+	}
+}
+
+__global__ void
+k_q1_collect(const unsigned long long *first, uint32_t *cnt, unsigned long long *list)
+{
+	for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < 65536; c += gridDim.x * blockDim.x) {
+		if (first[c] != ~0ull) {
+			uint32_t k = atomicAdd(cnt, 1u);
+			if (k < 64) {
+				list[2 * k] = first[c];
+				list[2 * k + 1] = c;
+			}
+		}
+	}
+}
+
+constexpr int64_t Q1_LIM = (int64_t) 1 << 31;
+
+template <int K>
+__global__ __launch_bounds__(256) void
+k_q1(Q1Args a)
+{
+	int64_t sq[K], sp[K], sdsc[K];
+	hge sdp[K], sch[K];
+	uint32_t cnt[K];
+#pragma unroll
+	for (int k = 0; k < K; k++) {
+		sq[k] = sp[k] = sdsc[k] = 0;
+		sdp[k] = sch[k] = 0;
+		cnt[k] = 0;
+	}
+	uint32_t unknown = 0, bad = 0;
+	typedef int32_t i4 __attribute__((ext_vector_type(4)));
+	typedef int64_t l2 __attribute__((ext_vector_type(2)));
+	typedef uint8_t u4 __attribute__((ext_vector_type(4)));
+	const uint64_t nq = a.n / 4;
+	const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+	auto row = [&](int32_t d, uint32_t code, int64_t q, int64_t p, int64_t di, int64_t t) {
+		if (d == INT32_MIN || d > a.dmax)
+			return;
+		bad |= (q <= -Q1_LIM) | (q >= Q1_LIM) | (p <= -Q1_LIM) | (p >= Q1_LIM) |
+		       (di <= -Q1_LIM) | (di >= Q1_LIM) | (t <= -Q1_LIM) | (t >= Q1_LIM);
+		const int64_t dp = p * (100 - di);            // |.| < 2^63
+		const hge ch = (hge) dp * (hge) (100 + t);
+		bool hit = false;
+#pragma unroll
+		for (int k = 0; k < K; k++) {
+			const bool m = code == a.codes[k];
+			hit |= m;
+			sq[k] += m ? q : 0;
+			sp[k] += m ? p : 0;
+			sdsc[k] += m ? di : 0;
+			sdp[k] += m ? (hge) dp : (hge) 0;
+			sch[k] += m ? ch : (hge) 0;
+			cnt[k] += m;
+		}
+		unknown |= !hit;
+	};
+	uint64_t qi = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
+	for (; qi < nq; qi += stride) {
+		const uint64_t r = qi * 4;
+		i4 sd = *(const i4 *) (a.sd + r);
+		u4 rf = *(const u4 *) (a.rf + r);
+		u4 ls = *(const u4 *) (a.ls + r);
+		l2 q0 = *(const l2 *) (a.qty + r), q1 = *(const l2 *) (a.qty + r + 2);
+		l2 p0 = *(const l2 *) (a.price + r), p1 = *(const l2 *) (a.price + r + 2);
+		l2 d0 = *(const l2 *) (a.disc + r), d1 = *(const l2 *) (a.disc + r + 2);
+		l2 t0 = *(const l2 *) (a.tax + r), t1 = *(const l2 *) (a.tax + r + 2);
+		row(sd[0], ((uint32_t) rf[0] << 8) | ls[0], q0[0], p0[0], d0[0], t0[0]);
+		row(sd[1], ((uint32_t) rf[1] << 8) | ls[1], q0[1], p0[1], d0[1], t0[1]);
+		row(sd[2], ((uint32_t) rf[2] << 8) | ls[2], q1[0], p1[0], d1[0], t1[0]);
+		row(sd[3], ((uint32_t) rf[3] << 8) | ls[3], q1[1], p1[1], d1[1], t1[1]);
+	}
+	if (blockIdx.x == 0 && threadIdx.x < (a.n & 3)) {
+		const uint64_t r = nq * 4 + threadIdx.x;
+		row(a.sd[r], ((uint32_t) a.rf[r] << 8) | a.ls[r], a.qty[r], a.price[r], a.disc[r], a.tax[r]);
+	}
+	// lane partials of qty/price/disc are < 2^31 * rows-per-lane; widen
+#pragma unroll
+	for (int k = 0; k < K; k++) {
+		hge v[6] = {(hge) sq[k], (hge) sp[k], sdp[k], sch[k], (hge) sdsc[k], (hge) cnt[k]};
+#pragma unroll
+		for (int j = 0; j < 6; j++)
+			v[j] = wave_sum128(v[j]);
+		if (__lane_id() == 0) {
+			unsigned long long *acc = a.acc + (size_t) k * 12;
+#pragma unroll
+			for (int j = 0; j < 6; j++)
+				if (v[j] != 0)
+					atomic_add128(acc + 2 * j, v[j]);
+		}
+	}
+	for (int o = 32; o > 0; o >>= 1) {
+		unknown |= __shfl_xor(unknown, o);
+		bad |= __shfl_xor(bad, o);
+	}
+	if (__lane_id() == 0) {
+		if (unknown)
+			atomicOr(&a.flags[0], 1u);
+		if (bad)
+			atomicOr(&a.flags[1], 1u);
+	}
+}
+
+bool
+aligned16(const void *p)
+{
+	return ((uintptr_t) p & 15) == 0;
+}
+
+}  // namespace
+
+namespace mgdk {
+int q1_opatatime(mgdk_bat *shipdate, mgdk_bat *rf, mgdk_bat *ls, mgdk_bat *qty, mgdk_bat *price,
+		 mgdk_bat *disc, mgdk_bat *tax, int32_t dmax, mgdk_q1row *rows, int maxgroups, int *ngroups);
+}
+
+extern "C" {
+
+int
+mgdk_tpch_lineitem(uint64_t seed, uint64_t row0, uint64_t n, uint64_t sf_parts, mgdk_bat **cols)
+{
+	static const int types[7] = {MGDK_date, MGDK_lng, MGDK_lng, MGDK_lng, MGDK_lng, MGDK_str, MGDK_str};
+	mgdk_bat *b[7] = {};
+	for (int i = 0; i < 7; i++) {
+		b[i] = newbat(row0, types[i] == MGDK_str ? MGDK_bte : types[i], n);
+		if (b[i] == nullptr) {
+			for (int j = 0; j < i; j++)
+				mgdk_BBPunfix(b[j]);
+			return -1;
+		}
+	}
+	std::vector<int32_t> tab = date_table();
+	DevBuf dt(tab.size() * 4);
+	if (!hip_ok(hipMemcpyAsync(dt.p, tab.data(), tab.size() * 4, hipMemcpyHostToDevice, stream()), "memcpy"))
+		return -1;
+	if (n)
+		hipLaunchKernelGGL(k_lineitem, dim3(grid_for(n, 256 * 4, 256 * 64)), dim3(256), 0, stream(), seed, row0, n,
+				   sf_parts, dt.as<int32_t>(), (int32_t *) b[0]->theap, (int64_t *) b[1]->theap,
+				   (int64_t *) b[2]->theap, (int64_t *) b[3]->theap, (int64_t *) b[4]->theap,
+				   (uint8_t *) b[5]->theap, (uint8_t *) b[6]->theap);
+	// string heaps: GDK_VAROFFSET (8192) hash header, then 8-aligned strings
+	std::vector<char> rfh(8192 + 24, 0), lsh(8192 + 16, 0);
+	rfh[8192 + 0] = 'A';
+	rfh[8192 + 8] = 'N';
+	rfh[8192 + 16] = 'R';
+	lsh[8192 + 0] = 'F';
+	lsh[8192 + 8] = 'O';
+	if (!sync())
+		return -1;
+	for (int i = 0; i < 7; i++) {
+		b[i]->count = n;
+		b[i]->tsorted = b[i]->trevsorted = n <= 1;
+		b[i]->tkey = n <= 1;
+		b[i]->tnonil = 1;
+		b[i]->tnil = 0;
+		if (types[i] == MGDK_str) {
+			b[i]->ttype = MGDK_str;
+			std::vector<char> &hp = i == 5 ? rfh : lsh;
+			if (mgdk_BATsetvheap(b[i], hp.data(), hp.size()) < 0)
+				return -1;
+		}
+		cols[i] = b[i];
+	}
+	return 0;
+}
+
+int
+mgdk_q6_fused(mgdk_bat *shipdate, mgdk_bat *discount, mgdk_bat *quantity, mgdk_bat *extendedprice,
+	      int32_t d0, int32_t d1, int64_t dlo, int64_t dhi, int64_t qmax, void *revenue)
+{
+	mgdk_bat *c[4] = {shipdate, discount, quantity, extendedprice};
+	const int want[4] = {MGDK_int, MGDK_lng, MGDK_lng, MGDK_lng};
+	for (int i = 0; i < 4; i++) {
+		if (c[i] == nullptr || basetype(c[i]->ttype) != want[i] || c[i]->count != shipdate->count ||
+		    c[i]->hseqbase != shipdate->hseqbase) {
+			seterr("42000!q6_fused: lineitem columns must be aligned date/lng BATs");
+			return -1;
+		}
+	}
+	Q6Args a;
+	a.sd = (const int32_t *) shipdate->theap;
+	a.disc = (const int64_t *) discount->theap;
+	a.qty = (const int64_t *) quantity->theap;
+	a.price = (const int64_t *) extendedprice->theap;
+	a.n = shipdate->count;
+	a.d0 = d0;
+	a.d1 = d1;
+	a.dlo = dlo;
+	a.dhi = dhi;
+	a.qmax = qmax;
+	a.out = (unsigned long long *) meta_buf();
+	hipStream_t st = stream();
+	if (!hip_ok(hipMemsetAsync(a.out, 0, 16, st), "memset"))
+		return -1;
+	{
+		ProfScope prof("q6_fused");
+		if (a.n) {
+			bool al = aligned16(a.sd) && aligned16(a.disc) && aligned16(a.qty) && aligned16(a.price);
+			if (al)
+				hipLaunchKernelGGL((k_q6<2>), dim3(grid_for(a.n / 4 + 1, 256, 256 * 8)), dim3(256), 0, st, a);
+			else
+				hipLaunchKernelGGL(k_q6_scalar, dim3(grid_for(a.n, 256 * 4, 256 * 16)), dim3(256), 0, st, a);
+		}
+	}
+	unsigned long long *h = (unsigned long long *) pinned(16);
+	if (!hip_ok(hipMemcpyAsync(h, a.out, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+		return -1;
+	memcpy(revenue, h, 16);
+	return 0;
+}
+
+int
+mgdk_q1_fused(mgdk_bat *shipdate, mgdk_bat *returnflag, mgdk_bat *linestatus, mgdk_bat *quantity,
+	      mgdk_bat *extendedprice, mgdk_bat *discount, mgdk_bat *tax, int32_t dmax, mgdk_q1row *rows,
+	      int maxgroups, int *ngroups)
+{
+	mgdk_bat *c[7] = {shipdate, returnflag, linestatus, quantity, extendedprice, discount, tax};
+	for (int i = 0; i < 7; i++) {
+		if (c[i] == nullptr || c[i]->count != shipdate->count || c[i]->hseqbase != shipdate->hseqbase) {
+			seterr("42000!q1_fused: lineitem columns must be aligned");
+			return -1;
+		}
+	}
+	bool shape_ok = basetype(shipdate->ttype) == MGDK_int && returnflag->ttype == MGDK_str &&
+			returnflag->twidth == 1 && linestatus->ttype == MGDK_str && linestatus->twidth == 1;
+	for (int i = 3; i < 7; i++)
+		shape_ok = shape_ok && c[i]->ttype == MGDK_lng && aligned16(c[i]->theap);
+	shape_ok = shape_ok && aligned16(shipdate->theap) && ((uintptr_t) returnflag->theap & 3) == 0 &&
+		   ((uintptr_t) linestatus->theap & 3) == 0;
+	if (!shape_ok)
+		return q1_opatatime(shipdate, returnflag, linestatus, quantity, extendedprice, discount, tax, dmax,
+				    rows, maxgroups, ngroups);
+	const uint64_t n = shipdate->count;
+	hipStream_t st = stream();
+	// 1. keys and their first occurrence on a prefix
+	const uint64_t pre = std::min<uint64_t>(n, (uint64_t) 1 << 22);
+	DevBuf first(65536 * 8), list(64 * 16 + 64), acc(Q1_MAXK * 12 * 8 + 64);
+	uint32_t *cnt = (uint32_t *) ((char *) list.p + 64 * 16);
+	if (!hip_ok(hipMemsetAsync(first.p, 0xff, 65536 * 8, st), "memset") ||
+	    !hip_ok(hipMemsetAsync(cnt, 0, 16, st), "memset") ||
+	    !hip_ok(hipMemsetAsync(acc.p, 0, Q1_MAXK * 12 * 8 + 64, st), "memset"))
+		return -1;
+	ProfScope prof("q1_fused");
+	if (pre)
+		hipLaunchKernelGGL(k_q1_keys, dim3(grid_for(pre, 1024, 2048)), dim3(256), 0, st, (const int32_t *) shipdate->theap,
+				   (const uint8_t *) returnflag->theap, (const uint8_t *) linestatus->theap, pre, dmax,
+				   first.as<unsigned long long>());
+	hipLaunchKernelGGL(k_q1_collect, dim3(64), dim3(256), 0, st, first.as<unsigned long long>(), cnt,
+			   list.as<unsigned long long>());
+	unsigned long long *h = (unsigned long long *) pinned(64 * 16 + 64);
+	if (!hip_ok(hipMemcpyAsync(h, list.p, 64 * 16 + 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+		return -1;
+	uint32_t K = *(uint32_t *) (h + 128);
+	if (K == 0 || K > Q1_MAXK || (int) K > maxgroups)
+		return q1_opatatime(shipdate, returnflag, linestatus, quantity, extendedprice, discount, tax, dmax,
+				    rows, maxgroups, ngroups);
+	std::vector<std::pair<unsigned long long, uint32_t>> keys;
+	for (uint32_t k = 0; k < K; k++)
+		keys.emplace_back(h[2 * k], (uint32_t) h[2 * k + 1]);
+	std::sort(keys.begin(), keys.end());
+	// 2. main pass
+	Q1Args a{};
+	a.sd = (const int32_t *) shipdate->theap;
+	a.rf = (const uint8_t *) returnflag->theap;
+	a.ls = (const uint8_t *) linestatus->theap;
+	a.qty = (const int64_t *) quantity->theap;
+	a.price = (const int64_t *) extendedprice->theap;
+	a.disc = (const int64_t *) discount->theap;
+	a.tax = (const int64_t *) tax->theap;
+	a.n = n;
+	a.dmax = dmax;
+	a.K = (int) K;
+	for (uint32_t k = 0; k < K; k++)
+		a.codes[k] = keys[k].second;
+	for (uint32_t k = K; k < Q1_MAXK; k++)
+		a.codes[k] = 0xffffffffu;
+	a.acc = acc.as<unsigned long long>();
+	a.flags = (uint32_t *) (a.acc + Q1_MAXK * 12);
+	dim3 g(grid_for(n / 4 + 1, 256, 256 * 8)), blk(256);
+	if (K <= 1) hipLaunchKernelGGL(k_q1<1>, g, blk, 0, st, a);
+	else if (K <= 2) hipLaunchKernelGGL(k_q1<2>, g, blk, 0, st, a);
+	else if (K <= 4) hipLaunchKernelGGL(k_q1<4>, g, blk, 0, st, a);
+	else hipLaunchKernelGGL(k_q1<8>, g, blk, 0, st, a);
+	unsigned long long *hr = (unsigned long long *) pinned(Q1_MAXK * 12 * 8 + 64);
+	if (!hip_ok(hipMemcpyAsync(hr, acc.p, Q1_MAXK * 12 * 8 + 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+		return -1;
+	const uint32_t *fl = (const uint32_t *) (hr + Q1_MAXK * 12);
+	if (fl[0] || fl[1])
+		return q1_opatatime(shipdate, returnflag, linestatus, quantity, extendedprice, discount, tax, dmax,
+				    rows, maxgroups, ngroups);
+	for (uint32_t k = 0; k < K; k++) {
+		mgdk_q1row &r = rows[k];
+		memset(&r, 0, sizeof(r));
+		r.returnflag = (uint8_t) (keys[k].second >> 8);
+		r.linestatus = (uint8_t) (keys[k].second & 0xff);
+		r.first_row = shipdate->hseqbase + keys[k].first;
+		const unsigned long long *x = hr + k * 12;
+		memcpy(r.sum_qty, x + 0, 16);
+		memcpy(r.sum_base_price, x + 2, 16);
+		memcpy(r.sum_disc_price, x + 4, 16);
+		memcpy(r.sum_charge, x + 6, 16);
+		memcpy(r.sum_disc, x + 8, 16);
+		r.count_order = (int64_t) x[10];
+	}
+	*ngroups = (int) K;
+	return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,463 @@
+"""Host-side mirror of the GDK operator interface over libmgdk.so.
+
+Same names and argument meaning as the reference's C functions
+(gdk/gdk.h:1447,1526,2245-2275, gdk/gdk_calc.h, gdk/gdk_analytic.h); errors
+raise GDKError carrying the reference's SQLSTATE-prefixed message (the
+C functions return NULL/GDK_FAIL and set GDKerrbuf).  There is no CPU
+fallback: if libmgdk.so is missing or no GPU is present, calls fail loudly.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmgdk.so")
+
+TYPE_void, TYPE_msk, TYPE_bit, TYPE_bte, TYPE_sht, TYPE_int, TYPE_oid = 0, 1, 2, 3, 4, 5, 6
+TYPE_flt, TYPE_dbl, TYPE_lng, TYPE_hge, TYPE_date, TYPE_str = 8, 9, 10, 11, 12, 16
+OID_NIL = 1 << 63
+
+NP = {TYPE_bit: np.int8, TYPE_bte: np.int8, TYPE_sht: np.int16, TYPE_int: np.int32,
+      TYPE_date: np.int32, TYPE_oid: np.uint64, TYPE_lng: np.int64, TYPE_flt: np.float32,
+      TYPE_dbl: np.float64, TYPE_str: np.uint8}
+CT = {TYPE_bit: C.c_int8, TYPE_bte: C.c_int8, TYPE_sht: C.c_int16, TYPE_int: C.c_int32,
+      TYPE_date: C.c_int32, TYPE_oid: C.c_uint64, TYPE_void: C.c_uint64, TYPE_lng: C.c_int64,
+      TYPE_flt: C.c_float, TYPE_dbl: C.c_double}
+NIL = {TYPE_bit: -128, TYPE_bte: -128, TYPE_sht: -(1 << 15), TYPE_int: -(1 << 31),
+       TYPE_date: -(1 << 31), TYPE_lng: -(1 << 63), TYPE_hge: -(1 << 127), TYPE_oid: OID_NIL,
+       TYPE_void: OID_NIL, TYPE_flt: float("nan"), TYPE_dbl: float("nan")}
+WIDTH = {TYPE_void: 0, TYPE_bit: 1, TYPE_bte: 1, TYPE_sht: 2, TYPE_int: 4, TYPE_date: 4,
+         TYPE_flt: 4, TYPE_oid: 8, TYPE_lng: 8, TYPE_dbl: 8, TYPE_hge: 16, TYPE_str: 1}
+
+
+class MgdkBat(C.Structure):
+    _fields_ = [("ttype", C.c_int32), ("twidth", C.c_int32), ("count", C.c_uint64),
+                ("hseqbase", C.c_uint64), ("tseqbase", C.c_uint64), ("theap", C.c_void_p),
+                ("tvheap", C.c_void_p), ("tvheapsize", C.c_uint64),
+                ("tsorted", C.c_uint8), ("trevsorted", C.c_uint8), ("tkey", C.c_uint8),
+                ("tnonil", C.c_uint8), ("tnil", C.c_uint8), ("_pad", C.c_uint8 * 3),
+                ("priv", C.c_void_p)]
+
+
+class Q1Row(C.Structure):
+    _fields_ = [("returnflag", C.c_uint8), ("linestatus", C.c_uint8), ("_pad", C.c_uint8 * 6),
+                ("sum_qty", C.c_uint64 * 2), ("sum_base_price", C.c_uint64 * 2),
+                ("sum_disc_price", C.c_uint64 * 2), ("sum_charge", C.c_uint64 * 2),
+                ("sum_disc", C.c_uint64 * 2), ("count_order", C.c_int64),
+                ("first_row", C.c_uint64)]
+
+
+P = C.POINTER(MgdkBat)
+PP = C.POINTER(P)
+
+
+class GDKError(RuntimeError):
+    pass
+
+
+_lib = None
+_inited = False
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "mgdk_init": (C.c_int, [C.c_int]),
+    "mgdk_GDKerrbuf": (C.c_char_p, []),
+    "mgdk_GDKclrerr": (None, []),
+    "mgdk_sync": (C.c_int, []),
+    "mgdk_stream": (C.c_void_p, []),
+    "mgdk_mem_cursize": (C.c_uint64, []),
+    "mgdk_mem_release_cache": (None, []),
+    "mgdk_prof_enable": (None, [C.c_int]),
+    "mgdk_prof_get": (C.c_int, [C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
+    "mgdk_prof_reset": (None, []),
+    "mgdk_COLnew": (P, [C.c_uint64, C.c_int, C.c_uint64]),
+    "mgdk_BATdense": (P, [C.c_uint64, C.c_uint64, C.c_uint64]),
+    "mgdk_BATconstant": (P, [C.c_uint64, C.c_int, C.c_void_p, C.c_uint64]),
+    "mgdk_BATslice": (P, [P, C.c_uint64, C.c_uint64]),
+    "mgdk_BBPunfix": (None, [P]),
+    "mgdk_BATupload": (C.c_int, [P, C.c_void_p, C.c_uint64]),
+    "mgdk_BATdownload": (C.c_int, [P, C.c_void_p]),
+    "mgdk_BATsetvheap": (C.c_int, [P, C.c_void_p, C.c_uint64]),
+    "mgdk_BATdownload_vheap": (C.c_int, [P, C.c_void_p]),
+    "mgdk_BATselect": (P, [P, P, C.c_void_p, C.c_void_p, C.c_bool, C.c_bool, C.c_bool, C.c_bool]),
+    "mgdk_BATthetaselect": (P, [P, P, C.c_void_p, C.c_char_p]),
+    "mgdk_BATproject": (P, [P, P]),
+    "mgdk_BATcalcadd": (P, [P, P, P, P, C.c_int]),
+    "mgdk_BATcalcsub": (P, [P, P, P, P, C.c_int]),
+    "mgdk_BATcalcmul": (P, [P, P, P, P, C.c_int]),
+    "mgdk_BATcalcaddcst": (P, [P, C.c_void_p, C.c_int, P, C.c_int]),
+    "mgdk_BATcalcsubcst": (P, [P, C.c_void_p, C.c_int, P, C.c_int]),
+    "mgdk_BATcalcmulcst": (P, [P, C.c_void_p, C.c_int, P, C.c_int]),
+    "mgdk_BATcalccstadd": (P, [C.c_void_p, C.c_int, P, P, C.c_int]),
+    "mgdk_BATcalccstsub": (P, [C.c_void_p, C.c_int, P, P, C.c_int]),
+    "mgdk_BATcalccstmul": (P, [C.c_void_p, C.c_int, P, P, C.c_int]),
+    "mgdk_BATsum": (C.c_int, [C.c_void_p, C.c_int, P, P, C.c_bool, C.c_bool]),
+    "mgdk_BATgroupsum": (P, [P, P, P, P, C.c_int, C.c_bool]),
+    "mgdk_BATgroupcount": (P, [P, P, P, P, C.c_int, C.c_bool]),
+    "mgdk_BATgroupavg3": (C.c_int, [PP, PP, PP, P, P, P, P, C.c_bool]),
+    "mgdk_BATgroupmin": (P, [P, P, P, P, C.c_int, C.c_bool]),
+    "mgdk_BATgroupmax": (P, [P, P, P, P, C.c_int, C.c_bool]),
+    "mgdk_BATgroup": (C.c_int, [PP, PP, PP, P, P, P, P, P]),
+    "mgdk_BATjoin": (C.c_int, [PP, PP, P, P, P, P, C.c_bool, C.c_uint64]),
+    "mgdk_BATsort": (C.c_int, [PP, PP, PP, P, P, P, C.c_bool, C.c_bool, C.c_bool]),
+    "mgdk_GDKanalyticalwindowbounds": (C.c_int, [P, P, P, P, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                                 C.c_bool, C.c_uint64]),
+    "mgdk_q6_fused": (C.c_int, [P, P, P, P, C.c_int32, C.c_int32, C.c_int64, C.c_int64, C.c_int64,
+                                C.c_void_p]),
+    "mgdk_q1_fused": (C.c_int, [P, P, P, P, P, P, P, C.c_int32, C.POINTER(Q1Row), C.c_int,
+                                C.POINTER(C.c_int)]),
+    "mgdk_q6_opatatime": (C.c_int, [P, P, P, P, C.c_int32, C.c_int32, C.c_int64, C.c_int64,
+                                    C.c_int64, C.c_void_p]),
+    "mgdk_q1_opatatime": (C.c_int, [P, P, P, P, P, P, P, C.c_int32, C.POINTER(Q1Row), C.c_int,
+                                    C.POINTER(C.c_int)]),
+    "mgdk_tpch_lineitem": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, PP]),
+}
+
+
+def lib():
+    """Load libmgdk.so (in-tree build).  Raises if it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} not built: run python -m monetdb_amd.build")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def init(device=0):
+    global _inited
+    if not _inited:
+        if lib().mgdk_init(device) != 0:
+            raise GDKError(lib().mgdk_GDKerrbuf().decode())
+        _inited = True
+
+
+def _err():
+    return GDKError(lib().mgdk_GDKerrbuf().decode())
+
+
+def _chk(rc):
+    if rc != 0:
+        raise _err()
+
+
+def hge_to_int(words):
+    lo, hi = int(words[0]) & ((1 << 64) - 1), int(words[1]) & ((1 << 64) - 1)
+    v = (hi << 64) | lo
+    return v - (1 << 128) if v >= (1 << 127) else v
+
+
+def int_to_hge_words(v):
+    v &= (1 << 128) - 1
+    return v & ((1 << 64) - 1), v >> 64
+
+
+class BAT:
+    """Owning handle of one mgdk_bat (heap in HBM)."""
+
+    __slots__ = ("ptr",)
+
+    def __init__(self, ptr):
+        if not ptr:
+            raise _err()
+        self.ptr = ptr
+
+    # -- construction --
+    @classmethod
+    def from_numpy(cls, tp, arr, hseqbase=0, sorted_=None, revsorted=None, key=None,
+                   nonil=None, vheap=None):
+        init()
+        if tp == TYPE_hge:
+            a = np.ascontiguousarray(arr, dtype=np.uint64).reshape(-1, 2)
+        else:
+            a = np.ascontiguousarray(arr, dtype=NP[tp])
+        n = a.shape[0]
+        b = BAT(lib().mgdk_COLnew(hseqbase, tp, n))
+        _chk(lib().mgdk_BATupload(b.ptr, a.ctypes.data, n))
+        s = b.ptr.contents
+        if tp != TYPE_hge and tp != TYPE_str and n:
+            flat = a
+            isn = np.isnan(flat) if flat.dtype.kind == "f" else (flat == NIL[tp]) if tp in NIL else \
+                np.zeros(n, bool)
+            s.tnonil = int(not isn.any()) if nonil is None else int(nonil)
+            s.tnil = int(isn.any())
+            d = np.diff(flat.astype(np.float64) if flat.dtype.kind == "f" else flat)
+            s.tsorted = int((d >= 0).all()) if sorted_ is None else int(sorted_)
+            s.trevsorted = int((d <= 0).all()) if revsorted is None else int(revsorted)
+            s.tkey = int(len(np.unique(flat)) == n) if key is None else int(key)
+        else:
+            s.tnonil = 1 if nonil is None else int(nonil)
+            s.tsorted = int(n <= 1) if sorted_ is None else int(sorted_)
+            s.trevsorted = int(n <= 1) if revsorted is None else int(revsorted)
+            s.tkey = int(n <= 1) if key is None else int(key)
+        if vheap is not None:
+            vh = np.frombuffer(bytes(vheap), dtype=np.uint8)
+            _chk(lib().mgdk_BATsetvheap(b.ptr, vh.ctypes.data, vh.size))
+        return b
+
+    @classmethod
+    def dense(cls, tseq, n, hseqbase=0):
+        init()
+        return BAT(lib().mgdk_BATdense(hseqbase, tseq, n))
+
+    # -- properties --
+    @property
+    def s(self):
+        return self.ptr.contents
+
+    @property
+    def ttype(self):
+        return self.s.ttype
+
+    def count(self):
+        return self.s.count
+
+    def __len__(self):
+        return self.s.count
+
+    @property
+    def hseqbase(self):
+        return self.s.hseqbase
+
+    def is_dense(self):
+        return self.s.ttype == TYPE_void
+
+    def to_numpy(self):
+        s = self.s
+        n = s.count
+        if s.ttype == TYPE_void:
+            if s.tseqbase == OID_NIL:
+                return np.full(n, OID_NIL, np.uint64)
+            return np.arange(s.tseqbase, s.tseqbase + n, dtype=np.uint64)
+        if s.ttype == TYPE_hge:
+            out = np.empty((n, 2), np.uint64)
+        else:
+            out = np.empty(n, NP[s.ttype])
+        if n:
+            _chk(lib().mgdk_BATdownload(self.ptr, out.ctypes.data))
+        return out
+
+    def values(self):
+        """Python values (hge as int)."""
+        a = self.to_numpy()
+        if self.s.ttype == TYPE_hge:
+            return [hge_to_int(r) for r in a]
+        return a
+
+    def __del__(self):
+        p = getattr(self, "ptr", None)
+        if p and _lib is not None:
+            _lib.mgdk_BBPunfix(p)
+            self.ptr = None
+
+
+def _p(b):
+    return b.ptr if b is not None else None
+
+
+def _valptr(tp, v, keep):
+    if v is None:
+        return None
+    if tp == TYPE_hge:
+        buf = (C.c_uint64 * 2)(*int_to_hge_words(int(v)))
+    else:
+        buf = CT[tp](v)
+    keep.append(buf)
+    return C.cast(C.pointer(buf), C.c_void_p)
+
+
+# ---- operators (same names as GDK) ------------------------------------------
+
+def BATselect(b, s, tl, th, li, hi, anti, nil_matches=False):
+    keep = []
+    tp = b.ttype
+    return BAT(lib().mgdk_BATselect(b.ptr, _p(s), _valptr(tp, tl, keep), _valptr(tp, th, keep),
+                                    li, hi, anti, nil_matches))
+
+
+def BATthetaselect(b, s, val, op):
+    keep = []
+    return BAT(lib().mgdk_BATthetaselect(b.ptr, _p(s), _valptr(b.ttype, val, keep), op.encode()))
+
+
+def BATproject(l, r):
+    return BAT(lib().mgdk_BATproject(l.ptr, r.ptr))
+
+
+def BATcalcadd(b1, b2, tp, s1=None, s2=None):
+    return BAT(lib().mgdk_BATcalcadd(b1.ptr, b2.ptr, _p(s1), _p(s2), tp))
+
+
+def BATcalcsub(b1, b2, tp, s1=None, s2=None):
+    return BAT(lib().mgdk_BATcalcsub(b1.ptr, b2.ptr, _p(s1), _p(s2), tp))
+
+
+def BATcalcmul(b1, b2, tp, s1=None, s2=None):
+    return BAT(lib().mgdk_BATcalcmul(b1.ptr, b2.ptr, _p(s1), _p(s2), tp))
+
+
+def _cst(fn, b, v, vt, s, tp):
+    keep = []
+    return BAT(getattr(lib(), fn)(b.ptr, _valptr(vt, v, keep), vt, _p(s), tp))
+
+
+def _cstb(fn, v, vt, b, s, tp):
+    keep = []
+    return BAT(getattr(lib(), fn)(_valptr(vt, v, keep), vt, b.ptr, _p(s), tp))
+
+
+def BATcalcaddcst(b, v, vt, tp, s=None):
+    return _cst("mgdk_BATcalcaddcst", b, v, vt, s, tp)
+
+
+def BATcalcsubcst(b, v, vt, tp, s=None):
+    return _cst("mgdk_BATcalcsubcst", b, v, vt, s, tp)
+
+
+def BATcalcmulcst(b, v, vt, tp, s=None):
+    return _cst("mgdk_BATcalcmulcst", b, v, vt, s, tp)
+
+
+def BATcalccstadd(v, vt, b, tp, s=None):
+    return _cstb("mgdk_BATcalccstadd", v, vt, b, s, tp)
+
+
+def BATcalccstsub(v, vt, b, tp, s=None):
+    return _cstb("mgdk_BATcalccstsub", v, vt, b, s, tp)
+
+
+def BATcalccstmul(v, vt, b, tp, s=None):
+    return _cstb("mgdk_BATcalccstmul", v, vt, b, s, tp)
+
+
+def BATsum(tp, b, s=None, skip_nils=True, nil_if_empty=True):
+    buf = (C.c_uint64 * 2)()
+    _chk(lib().mgdk_BATsum(C.cast(buf, C.c_void_p), tp, b.ptr, _p(s), skip_nils, nil_if_empty))
+    if tp == TYPE_hge:
+        return hge_to_int(buf)
+    if tp == TYPE_dbl:
+        return C.cast(buf, C.POINTER(C.c_double))[0]
+    return C.cast(buf, C.POINTER(CT[tp]))[0]
+
+
+def BATgroupsum(b, g, e, tp, skip_nils=True, s=None):
+    return BAT(lib().mgdk_BATgroupsum(b.ptr, g.ptr, _p(e), _p(s), tp, skip_nils))
+
+
+def BATgroupcount(b, g, e, skip_nils=True, s=None):
+    return BAT(lib().mgdk_BATgroupcount(b.ptr, g.ptr, _p(e), _p(s), TYPE_lng, skip_nils))
+
+
+def BATgroupmin(b, g, e, skip_nils=True, s=None):
+    return BAT(lib().mgdk_BATgroupmin(b.ptr, g.ptr, _p(e), _p(s), b.ttype, skip_nils))
+
+
+def BATgroupmax(b, g, e, skip_nils=True, s=None):
+    return BAT(lib().mgdk_BATgroupmax(b.ptr, g.ptr, _p(e), _p(s), b.ttype, skip_nils))
+
+
+def BATgroupavg3(b, g, e, skip_nils=True, s=None):
+    a, r, c = P(), P(), P()
+    _chk(lib().mgdk_BATgroupavg3(C.byref(a), C.byref(r), C.byref(c), b.ptr, g.ptr, _p(e), _p(s),
+                                 skip_nils))
+    return BAT(a), BAT(r), BAT(c)
+
+
+def BATgroup(b, s=None, g=None, e=None, h=None):
+    gp, ep, hp = P(), P(), P()
+    _chk(lib().mgdk_BATgroup(C.byref(gp), C.byref(ep), C.byref(hp), b.ptr, _p(s), _p(g), _p(e),
+                             _p(h)))
+    return BAT(gp), BAT(ep), BAT(hp)
+
+
+def BATjoin(l, r, sl=None, sr=None, nil_matches=False, estimate=0):
+    a, b = P(), P()
+    _chk(lib().mgdk_BATjoin(C.byref(a), C.byref(b), l.ptr, r.ptr, _p(sl), _p(sr), nil_matches,
+                            estimate))
+    return BAT(a), BAT(b)
+
+
+def BATsort(b, o=None, g=None, reverse=False, nilslast=False, stable=True):
+    sp, op, gp = P(), P(), P()
+    _chk(lib().mgdk_BATsort(C.byref(sp), C.byref(op), C.byref(gp), b.ptr, _p(o), _p(g),
+                            reverse, nilslast, stable))
+    return BAT(sp), BAT(op), (BAT(gp) if gp else None)
+
+
+def GDKanalyticalwindowbounds(b, p, limit, preceding, tp1=TYPE_lng, tp2=TYPE_lng, unit=1):
+    n = b.count()
+    r = BAT(lib().mgdk_COLnew(0, TYPE_oid, n))
+    lim = C.c_int64(limit)
+    _chk(lib().mgdk_GDKanalyticalwindowbounds(r.ptr, b.ptr, _p(p), None,
+                                              C.cast(C.pointer(lim), C.c_void_p), tp1, tp2,
+                                              unit, preceding, 0))
+    return r
+
+
+def q6_fused(shipdate, discount, quantity, price, d0, d1, dlo, dhi, qmax):
+    out = (C.c_uint64 * 2)()
+    _chk(lib().mgdk_q6_fused(shipdate.ptr, discount.ptr, quantity.ptr, price.ptr, d0, d1, dlo, dhi,
+                             qmax, C.cast(out, C.c_void_p)))
+    return hge_to_int(out)
+
+
+def q6_opatatime(shipdate, discount, quantity, price, d0, d1, dlo, dhi, qmax):
+    out = (C.c_uint64 * 2)()
+    _chk(lib().mgdk_q6_opatatime(shipdate.ptr, discount.ptr, quantity.ptr, price.ptr, d0, d1, dlo,
+                                 dhi, qmax, C.cast(out, C.c_void_p)))
+    return hge_to_int(out)
+
+
+def q1_fused(cols, dmax, maxgroups=64, fused=True):
+    rows = (Q1Row * maxgroups)()
+    n = C.c_int()
+    fn = lib().mgdk_q1_fused if fused else lib().mgdk_q1_opatatime
+    _chk(fn(cols["shipdate"].ptr, cols["returnflag"].ptr,
+            cols["linestatus"].ptr, cols["quantity"].ptr,
+            cols["extendedprice"].ptr, cols["discount"].ptr, cols["tax"].ptr,
+            dmax, rows, maxgroups, C.byref(n)))
+    res = []
+    for i in range(n.value):
+        r = rows[i]
+        res.append(dict(returnflag=r.returnflag, linestatus=r.linestatus,
+                        sum_qty=hge_to_int(r.sum_qty), sum_base_price=hge_to_int(r.sum_base_price),
+                        sum_disc_price=hge_to_int(r.sum_disc_price),
+                        sum_charge=hge_to_int(r.sum_charge), sum_disc=hge_to_int(r.sum_disc),
+                        count_order=r.count_order, first_row=r.first_row))
+    return res
+
+
+LINEITEM_COLS = ("shipdate", "quantity", "extendedprice", "discount", "tax", "returnflag",
+                 "linestatus")
+
+
+def tpch_lineitem(seed, row0, n, sf_parts):
+    """Generate the synthetic lineitem columns directly in HBM."""
+    init()
+    arr = (P * 7)()
+    _chk(lib().mgdk_tpch_lineitem(seed, row0, n, sf_parts, arr))
+    return {k: BAT(arr[i]) for i, k in enumerate(LINEITEM_COLS)}
+
+
+def sync():
+    _chk(lib().mgdk_sync())
+
+
+def prof_enable(on=True):
+    lib().mgdk_prof_enable(1 if on else 0)
+
+
+def prof_get(kernel):
+    ms, n = C.c_double(), C.c_uint64()
+    lib().mgdk_prof_get(kernel.encode(), C.byref(ms), C.byref(n))
+    return ms.value, n.value
+
+
+def prof_reset():
+    lib().mgdk_prof_reset()

@@ -1,0 +1,130 @@
+/*
+ * gdk_oracle.h -- CPU restatement of MonetDB GDK's column-operator semantics.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This library is the parity checker for the
+ * MI355X product path (libmgdk.so).  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it.  The product never links,
+ * calls or falls back to it.
+ *
+ * It restates (does not copy) the algorithms of the reference
+ * rohan-flutterint/MonetDB v11.52.0 (/root/reference, read-only):
+ *   select      gdk/gdk_select.c:1342-2084 (BATselect), :2103-2154 (BATthetaselect),
+ *               scan normalisation :300-446
+ *   candidates  gdk/gdk_cand.c:407 (canditer_init clipping)
+ *   project     gdk/gdk_project.c:590-857
+ *   calc        gdk/gdk_calc_addsub.c, gdk/gdk_calc_mul.c:23-132,2020-2092,
+ *               overflow rules gdk/gdk_calc_private.h:38-140
+ *   aggregates  gdk/gdk_aggr.c:65 (BATgroupaggrinit), :708 (dosum), :900, :1018,
+ *               :1996 (BATgroupavg3), :3069 (BATgroupcount), AVERAGE_ITER
+ *               gdk/gdk_calc_private.h:231-275
+ *   group       gdk/gdk_group.c:657-1347 (first-occurrence numbering)
+ *   join        gdk/gdk_join.c:2781-2900 (hash join result order)
+ *   sort        gdk/gdk_batop.c:2266-2342, gdk/gdk_rsort.c:21 (stable)
+ *   window      gdk/gdk_analytic_bounds.c:273-387, :994, :1440
+ *
+ * Parity pinning: see tests/golden/ (fixtures extracted from the reference's
+ * own MAL known-answer tests) and DESIGN.md §Oracle.
+ */
+#ifndef GDK_ORACLE_H
+#define GDK_ORACLE_H
+
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef uint64_t ora_oid;
+typedef __int128 ora_hge;
+
+/* GDK type ids (gdk/gdk.h:428-451, HAVE_HGE build) */
+enum {
+	ORA_void = 0, ORA_msk = 1, ORA_bit = 2, ORA_bte = 3, ORA_sht = 4,
+	ORA_int = 5, ORA_oid = 6, ORA_flt = 8, ORA_dbl = 9, ORA_lng = 10,
+	ORA_hge = 11, ORA_date = 12, ORA_str = 16,
+};
+
+#define ORA_OID_NIL ((ora_oid) 1 << 63)
+
+typedef struct ora_bat {
+	int32_t type;        /* GDK type id */
+	int32_t width;       /* bytes per tail value (str: offset width) */
+	uint64_t count;
+	ora_oid hseqbase;
+	ora_oid tseqbase;    /* void/dense: first value; else ORA_OID_NIL */
+	void *base;          /* tail values (NULL for void) */
+	char *vheap;         /* str: string heap */
+	uint64_t vheapsize;
+	uint8_t sorted, revsorted, key, nonil, nil, owned;
+	uint8_t _pad[2];
+} ora_bat;
+
+/* memory */
+ora_bat *ora_new(int type, uint64_t count, ora_oid hseq);
+void ora_free(ora_bat *b);
+const char *ora_errbuf(void);
+
+/* operators: NULL / -1 on error with message in ora_errbuf() */
+ora_bat *ora_select(const ora_bat *b, const ora_bat *s, const void *tl,
+		    const void *th, bool li, bool hi, bool anti, bool nil_matches);
+ora_bat *ora_thetaselect(const ora_bat *b, const ora_bat *s, const void *val,
+			 const char *op);
+ora_bat *ora_project(const ora_bat *l, const ora_bat *r);
+/* op: '+', '-', '*'; b1/b2 may be NULL when a constant is given */
+ora_bat *ora_calc(char op, const ora_bat *b1, const void *c1, int t1,
+		  const ora_bat *b2, const void *c2, int t2,
+		  const ora_bat *s, int tp);
+int ora_sum(void *res, int tp, const ora_bat *b, const ora_bat *s,
+	    bool skip_nils, bool nil_if_empty);
+int ora_group(ora_bat **groups, ora_bat **extents, ora_bat **histo,
+	      const ora_bat *b, const ora_bat *s, const ora_bat *g);
+ora_bat *ora_groupsum(const ora_bat *b, const ora_bat *g, const ora_bat *e,
+		      const ora_bat *s, int tp, bool skip_nils);
+ora_bat *ora_groupcount(const ora_bat *b, const ora_bat *g, const ora_bat *e,
+			const ora_bat *s, bool skip_nils);
+int ora_groupavg3(ora_bat **avgp, ora_bat **remp, ora_bat **cntp,
+		  const ora_bat *b, const ora_bat *g, const ora_bat *e,
+		  const ora_bat *s, bool skip_nils);
+ora_bat *ora_groupminmax(const ora_bat *b, const ora_bat *g, const ora_bat *e,
+			 const ora_bat *s, bool skip_nils, bool domax);
+int ora_join(ora_bat **r1p, ora_bat **r2p, const ora_bat *l, const ora_bat *r,
+	     const ora_bat *sl, const ora_bat *sr, bool nil_matches);
+int ora_sort(ora_bat **sorted, ora_bat **order, const ora_bat *b,
+	     bool reverse, bool nilslast);
+int ora_rangebounds(ora_bat *r, const ora_bat *b, const ora_bat *p,
+		    const void *bound, int tp2, bool preceding, ora_oid first_half);
+
+/* synthetic TPC-H lineitem (tpch_gen.c) */
+typedef struct ora_lineitem {
+	uint64_t n;
+	int32_t *shipdate;     /* GDK date */
+	int64_t *quantity;     /* decimal(15,2) as lng */
+	int64_t *extendedprice;
+	int64_t *discount;
+	int64_t *tax;
+	uint8_t *returnflag;   /* 1-byte str offsets into ora_flag_heap */
+	uint8_t *linestatus;
+} ora_lineitem;
+void ora_tpch_lineitem(uint64_t seed, uint64_t row0, uint64_t n, uint64_t sf_parts,
+		       int32_t *shipdate, int64_t *quantity, int64_t *extendedprice,
+		       int64_t *discount, int64_t *tax, uint8_t *returnflag,
+		       uint8_t *linestatus);
+int32_t ora_mkdate(int y, int m, int d);
+
+/* op-at-a-time TPC-H pipelines over the oracle operators (pipelines.c) */
+int ora_q6(const ora_lineitem *li, int nthreads, ora_hge *revenue);
+typedef struct ora_q1row {
+	uint8_t returnflag, linestatus, _pad[6];
+	ora_hge sum_qty, sum_base_price, sum_disc_price, sum_charge;
+	int64_t avg_qty, avg_price, avg_disc;      /* avg3 rounded results */
+	int64_t rem_qty, rem_price, rem_disc;
+	int64_t count_order;
+} ora_q1row;
+int ora_q1(const ora_lineitem *li, int nthreads, ora_q1row *rows, int *nrows);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,660 @@
+/*
+ * gdk_oracle_grp.c -- CPU restatement of GDK grouping, grouped aggregates,
+ * hash join, sort and RANGE window bounds.  TEST INFRASTRUCTURE ONLY
+ * (see gdk_oracle.h).
+ */
+#include "gdk_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+void ora_seterr(const char *fmt, ...);
+int ora_width(int type);
+ora_bat *ora_dense(ora_oid hseq, ora_oid tseq, uint64_t cnt);
+
+typedef struct {
+	bool dense;
+	ora_oid seq;
+	const ora_oid *oids;
+	uint64_t n;
+} ora_ci;
+int ora_ci_init(ora_ci *ci, const ora_bat *b, const ora_bat *s);
+
+static inline ora_oid
+ci_get(const ora_ci *ci, uint64_t i)
+{
+	return ci->dense ? ci->seq + i : ci->oids[i];
+}
+
+#define HGE_NIL ((ora_hge) ((unsigned __int128) 1 << 127))
+#define HGE_MAX ((ora_hge) (((unsigned __int128) 1 << 127) - 1))
+
+/* value of row p of b widened to 128 bits; returns true when nil */
+static bool
+val_at(const ora_bat *b, uint64_t p, ora_hge *v)
+{
+	const char *x = (const char *) b->base + p * b->width;
+	switch (b->type) {
+	case ORA_void: *v = (ora_hge) (b->tseqbase + p); return false;
+	case ORA_bit: case ORA_bte: *v = *(const int8_t *) x; return *v == INT8_MIN;
+	case ORA_sht: *v = *(const int16_t *) x; return *v == INT16_MIN;
+	case ORA_int: case ORA_date: *v = *(const int32_t *) x; return *v == INT32_MIN;
+	case ORA_lng: *v = *(const int64_t *) x; return *v == INT64_MIN;
+	case ORA_hge: *v = *(const ora_hge *) x; return *v == HGE_NIL;
+	case ORA_oid: *v = (ora_hge) *(const ora_oid *) x; return *(const ora_oid *) x == ORA_OID_NIL;
+	case ORA_str:
+		/* 1/2/4/8-byte heap offsets; equal strings share offsets in a
+		 * duplicate-eliminated heap (gdk/gdk_atoms.h:370-430) */
+		switch (b->width) {
+		case 1: *v = *(const uint8_t *) x; break;
+		case 2: *v = *(const uint16_t *) x; break;
+		case 4: *v = *(const uint32_t *) x; break;
+		default: *v = *(const uint64_t *) x; break;
+		}
+		return false;
+	}
+	*v = 0;
+	return false;
+}
+
+/* ---------------------------------------------------------------------- */
+/* BATgroup (gdk/gdk_group.c:657-1347): group ids are handed out in order
+ * of first occurrence of each distinct (g, value) pair over the candidates
+ * (GRPnotfound, gdk_group.c:74-100); nil is an ordinary value; extents hold
+ * the oid of each group's first row, histo the row count.  groups is
+ * aligned with the candidates (hseqbase = first candidate). */
+
+typedef struct {
+	ora_hge key;
+	ora_oid g;
+	ora_oid gid;
+	int used;
+} gslot;
+
+static uint64_t
+ghash(ora_hge k, ora_oid g)
+{
+	uint64_t x = (uint64_t) k ^ ((uint64_t) (k >> 64) * 0x9e3779b97f4a7c15ULL) ^ (g * 0xbf58476d1ce4e5b9ULL);
+	x ^= x >> 31;
+	x *= 0x94d049bb133111ebULL;
+	return x ^ (x >> 29);
+}
+
+int
+ora_group(ora_bat **groups, ora_bat **extents, ora_bat **histo,
+	  const ora_bat *b, const ora_bat *s, const ora_bat *g)
+{
+	ora_ci ci;
+	if (ora_ci_init(&ci, b, s) < 0)
+		return -1;
+	if (g && g->count != ci.n) {
+		ora_seterr("b with s and g must be aligned");
+		return -1;
+	}
+	ora_oid hseqb = ci.n ? ci.seq : 0;
+	if (!ci.dense && ci.n)
+		hseqb = ci.oids[0];
+	ora_bat *gn = ora_new(ORA_oid, ci.n, hseqb);
+	ora_bat *en = ora_new(ORA_oid, ci.n, 0);
+	ora_bat *hn = ora_new(ORA_lng, ci.n, 0);
+	uint64_t cap = 16;
+	while (cap < 2 * ci.n)
+		cap <<= 1;
+	gslot *tab = calloc(cap, sizeof(gslot));
+	if (!gn || !en || !hn || !tab) {
+		ora_free(gn); ora_free(en); ora_free(hn); free(tab);
+		ora_seterr("out of memory");
+		return -1;
+	}
+	ora_oid *gids = gn->base, *ext = en->base;
+	int64_t *cnt = hn->base;
+	uint64_t ngrp = 0;
+	for (uint64_t i = 0; i < ci.n; i++) {
+		ora_oid o = ci_get(&ci, i);
+		ora_hge v;
+		(void) val_at(b, o - b->hseqbase, &v);
+		ora_oid gg = 0;
+		if (g)
+			gg = g->type == ORA_void ? g->tseqbase + i : ((const ora_oid *) g->base)[i];
+		uint64_t h = ghash(v, gg) & (cap - 1);
+		while (tab[h].used && !(tab[h].key == v && tab[h].g == gg))
+			h = (h + 1) & (cap - 1);
+		if (!tab[h].used) {
+			tab[h].used = 1;
+			tab[h].key = v;
+			tab[h].g = gg;
+			tab[h].gid = ngrp;
+			ext[ngrp] = o;
+			cnt[ngrp] = 0;
+			ngrp++;
+		}
+		gids[i] = tab[h].gid;
+		cnt[tab[h].gid]++;
+	}
+	free(tab);
+	en->count = hn->count = ngrp;
+	gn->nonil = 1;
+	gn->key = ngrp == ci.n;
+	gn->revsorted = ngrp == 1 || ci.n <= 1;
+	bool srt = true;
+	for (uint64_t i = 1; i < ci.n && srt; i++)
+		srt = gids[i - 1] <= gids[i];
+	gn->sorted = srt;
+	en->sorted = en->key = en->nonil = 1;
+	hn->nonil = 1;
+	*groups = gn;
+	if (extents)
+		*extents = en;
+	else
+		ora_free(en);
+	if (histo)
+		*histo = hn;
+	else
+		ora_free(hn);
+	return 0;
+}
+
+/* ---------------------------------------------------------------------- */
+/* grouped aggregates: BATgroupaggrinit (gdk/gdk_aggr.c:65-146) computes the
+ * group id range [min, max] from e (count(e) groups starting at
+ * e->hseqbase) or from g; g is aligned with the candidates. */
+
+typedef struct {
+	ora_ci ci;
+	ora_oid min, max;
+	uint64_t ngrp;
+	const ora_oid *gids;   /* NULL: dense g (gid = g->tseqbase + i) */
+	ora_oid gseq;
+} aggr_ctx;
+
+static int
+aggr_init(aggr_ctx *a, const ora_bat *b, const ora_bat *g, const ora_bat *e,
+	  const ora_bat *s)
+{
+	memset(a, 0, sizeof(*a));
+	if (ora_ci_init(&a->ci, b, s) < 0)
+		return -1;
+	if (g == NULL) {
+		ora_seterr("b and g must be aligned\n");
+		return -1;
+	}
+	if (a->ci.n != g->count) {
+		ora_seterr("b with s and g must be aligned\n");
+		return -1;
+	}
+	if (!a->ci.dense) {
+		ora_seterr("grouped aggregate with non-dense candidates unsupported");
+		return -1;
+	}
+	a->gids = g->type == ORA_void ? NULL : g->base;
+	a->gseq = g->tseqbase;
+	if (e) {
+		a->ngrp = e->count;
+		a->min = e->hseqbase;
+		a->max = e->hseqbase + a->ngrp - 1;
+	} else {
+		ora_oid mn = ORA_OID_NIL, mx = 0;
+		for (uint64_t i = 0; i < g->count; i++) {
+			ora_oid x = a->gids ? a->gids[i] : a->gseq + i;
+			if (x == ORA_OID_NIL)
+				continue;
+			if (x < mn) mn = x;
+			if (x > mx) mx = x;
+		}
+		a->min = mn;
+		a->max = mx;
+		a->ngrp = mx < mn || mn == ORA_OID_NIL ? 0 : mx - mn + 1;
+	}
+	return 0;
+}
+
+static inline bool
+aggr_gid(const aggr_ctx *a, uint64_t i, ora_oid *gid)
+{
+	ora_oid x = a->gids ? a->gids[i] : a->gseq + i;
+	if (x < a->min || x > a->max)
+		return false;
+	*gid = x - a->min;
+	return true;
+}
+
+static ora_hge
+tmax(int tp)
+{
+	switch (tp) {
+	case ORA_bte: return INT8_MAX;
+	case ORA_sht: return INT16_MAX;
+	case ORA_int: return INT32_MAX;
+	case ORA_lng: return INT64_MAX;
+	default: return HGE_MAX;
+	}
+}
+
+static void
+put(int tp, void *base, uint64_t i, ora_hge v, bool nil)
+{
+	switch (tp) {
+	case ORA_bte: ((int8_t *) base)[i] = nil ? INT8_MIN : (int8_t) v; break;
+	case ORA_sht: ((int16_t *) base)[i] = nil ? INT16_MIN : (int16_t) v; break;
+	case ORA_int: ((int32_t *) base)[i] = nil ? INT32_MIN : (int32_t) v; break;
+	case ORA_lng: ((int64_t *) base)[i] = nil ? INT64_MIN : (int64_t) v; break;
+	case ORA_hge: ((ora_hge *) base)[i] = nil ? HGE_NIL : v; break;
+	}
+}
+
+/* BATgroupsum (gdk/gdk_aggr.c:900, dosum :708 with nil_if_empty=true):
+ * a group's sum is nil until its first non-nil value; a nil value makes
+ * it nil for good unless skip_nils; overflow is an error. */
+ora_bat *
+ora_groupsum(const ora_bat *b, const ora_bat *g, const ora_bat *e,
+	     const ora_bat *s, int tp, bool skip_nils)
+{
+	aggr_ctx a;
+	if (aggr_init(&a, b, g, e, s) < 0)
+		return NULL;
+	ora_bat *bn = ora_new(tp, a.ngrp, a.ngrp ? a.min : 0);
+	ora_hge *acc = calloc(a.ngrp + 1, sizeof(ora_hge));
+	uint8_t *st = calloc(a.ngrp + 1, 1);    /* 0 unseen, 1 value, 2 nil */
+	if (!bn || !acc || !st) {
+		ora_free(bn); free(acc); free(st);
+		ora_seterr("out of memory");
+		return NULL;
+	}
+	ora_hge max = tmax(tp);
+	/* st bit 0: group seen (a non-nil value arrived), bit 1: sum is nil.
+	 * With several groups, a nil arriving before the group's first
+	 * non-nil value is forgotten when that value resets the sum to 0
+	 * (AGGR_SUM "with groups", gdk_aggr.c:497-527); with a single group
+	 * any nil makes the sum nil (:440-470). */
+	for (uint64_t i = 0; i < a.ci.n; i++) {
+		ora_oid gid;
+		if (a.ngrp == 1)
+			gid = 0;
+		else if (!aggr_gid(&a, i, &gid))
+			continue;
+		ora_hge v;
+		if (val_at(b, ci_get(&a.ci, i) - b->hseqbase, &v)) {
+			if (!skip_nils) {
+				st[gid] |= 2;
+				if (a.ngrp == 1)
+					break;
+			}
+			continue;
+		}
+		if (!(st[gid] & 1)) {
+			st[gid] = 1;
+			acc[gid] = 0;
+		}
+		if (st[gid] & 2)
+			continue;
+		ora_hge z;
+		if (__builtin_add_overflow(acc[gid], v, &z) || z < -max || z > max) {
+			ora_seterr("22003!overflow in sum aggregate.\n");
+			ora_free(bn); free(acc); free(st);
+			return NULL;
+		}
+		acc[gid] = z;
+	}
+	bool hasnil = false;
+	for (uint64_t k = 0; k < a.ngrp; k++) {
+		put(tp, bn->base, k, acc[k], st[k] != 1);
+		hasnil |= st[k] != 1;
+	}
+	bn->nil = hasnil;
+	bn->nonil = !hasnil;
+	bn->sorted = bn->revsorted = bn->key = a.ngrp <= 1;
+	free(acc);
+	free(st);
+	return bn;
+}
+
+/* BATgroupcount (gdk/gdk_aggr.c:3069): lng counts, 0 for empty groups */
+ora_bat *
+ora_groupcount(const ora_bat *b, const ora_bat *g, const ora_bat *e,
+	       const ora_bat *s, bool skip_nils)
+{
+	aggr_ctx a;
+	if (aggr_init(&a, b, g, e, s) < 0)
+		return NULL;
+	ora_bat *bn = ora_new(ORA_lng, a.ngrp, a.ngrp ? a.min : 0);
+	if (!bn)
+		return NULL;
+	int64_t *c = bn->base;
+	memset(c, 0, a.ngrp * 8);
+	for (uint64_t i = 0; i < a.ci.n; i++) {
+		ora_oid gid;
+		if (!aggr_gid(&a, i, &gid))
+			continue;
+		ora_hge v;
+		if (skip_nils && val_at(b, ci_get(&a.ci, i) - b->hseqbase, &v))
+			continue;
+		c[gid]++;
+	}
+	bn->nonil = 1;
+	return bn;
+}
+
+/* BATgroupavg3 (gdk/gdk_aggr.c:1996-2110): exact average of integers as
+ * floor(sum/n) and remainder (AVERAGE_ITER, gdk_calc_private.h:231-275),
+ * then rounded half away from zero (non-TRUNCATE_NUMBERS branch:
+ * avg<0 rounds when 2*rem > n, avg>=0 when 2*rem >= n, and rem -= n).
+ * Empty groups: avg nil, rem 0, count 0; a nil input without skip_nils makes
+ * all three nil for the group. */
+int
+ora_groupavg3(ora_bat **avgp, ora_bat **remp, ora_bat **cntp,
+	      const ora_bat *b, const ora_bat *g, const ora_bat *e,
+	      const ora_bat *s, bool skip_nils)
+{
+	aggr_ctx a;
+	if (aggr_init(&a, b, g, e, s) < 0)
+		return -1;
+	int tp = b->type == ORA_date ? ORA_int : b->type;
+	ora_bat *bn = ora_new(tp, a.ngrp, a.ngrp ? a.min : 0);
+	ora_bat *rn = ora_new(ORA_lng, a.ngrp, a.ngrp ? a.min : 0);
+	ora_bat *cn = ora_new(ORA_lng, a.ngrp, a.ngrp ? a.min : 0);
+	ora_hge *sum = calloc(a.ngrp + 1, sizeof(ora_hge));
+	uint8_t *isnil = calloc(a.ngrp + 1, 1);
+	int64_t *cnt = cn ? cn->base : NULL;
+	if (!bn || !rn || !cn || !sum || !isnil) {
+		ora_free(bn); ora_free(rn); ora_free(cn); free(sum); free(isnil);
+		ora_seterr("out of memory");
+		return -1;
+	}
+	memset(cnt, 0, a.ngrp * 8);
+	for (uint64_t i = 0; i < a.ci.n; i++) {
+		ora_oid gid;
+		if (!aggr_gid(&a, i, &gid))
+			continue;
+		ora_hge v;
+		if (val_at(b, ci_get(&a.ci, i) - b->hseqbase, &v)) {
+			if (!skip_nils)
+				isnil[gid] = 1;
+			continue;
+		}
+		if (isnil[gid])
+			continue;
+		sum[gid] += v;   /* exact: |sum| < 2^63 * 2^64 */
+		cnt[gid]++;
+	}
+	int64_t *rem = rn->base;
+	for (uint64_t k = 0; k < a.ngrp; k++) {
+		if (isnil[k]) {
+			put(tp, bn->base, k, 0, true);
+			rem[k] = INT64_MIN;
+			cnt[k] = INT64_MIN;
+			continue;
+		}
+		if (cnt[k] == 0) {
+			put(tp, bn->base, k, 0, true);
+			rem[k] = 0;
+			continue;
+		}
+		ora_hge n = cnt[k];
+		ora_hge q = sum[k] / n, r = sum[k] % n;
+		if (r < 0) {      /* floor division, 0 <= r < n */
+			q -= 1;
+			r += n;
+		}
+		if (r > 0) {
+			if (q < 0) {
+				if (2 * r > n) { q++; r -= n; }
+			} else {
+				if (2 * r >= n) { q++; r -= n; }
+			}
+		}
+		put(tp, bn->base, k, q, false);
+		rem[k] = (int64_t) r;
+	}
+	free(sum);
+	free(isnil);
+	*avgp = bn;
+	*remp = rn;
+	*cntp = cn;
+	return 0;
+}
+
+/* BATgroupmin/max value variant (gdk/gdk_aggr.c:3487-3844): nil for empty
+ * groups; nils skipped when skip_nils. */
+ora_bat *
+ora_groupminmax(const ora_bat *b, const ora_bat *g, const ora_bat *e,
+		const ora_bat *s, bool skip_nils, bool domax)
+{
+	aggr_ctx a;
+	if (aggr_init(&a, b, g, e, s) < 0)
+		return NULL;
+	int tp = b->type == ORA_date ? ORA_int : b->type;
+	ora_bat *bn = ora_new(b->type, a.ngrp, a.ngrp ? a.min : 0);
+	ora_hge *best = calloc(a.ngrp + 1, sizeof(ora_hge));
+	uint8_t *st = calloc(a.ngrp + 1, 1);
+	if (!bn || !best || !st) {
+		ora_free(bn); free(best); free(st);
+		return NULL;
+	}
+	for (uint64_t i = 0; i < a.ci.n; i++) {
+		ora_oid gid;
+		if (!aggr_gid(&a, i, &gid))
+			continue;
+		ora_hge v;
+		if (val_at(b, ci_get(&a.ci, i) - b->hseqbase, &v)) {
+			if (!skip_nils)
+				st[gid] = 2;
+			continue;
+		}
+		if (st[gid] == 2)
+			continue;
+		if (st[gid] == 0 || (domax ? v > best[gid] : v < best[gid]))
+			best[gid] = v;
+		st[gid] = 1;
+	}
+	for (uint64_t k = 0; k < a.ngrp; k++)
+		put(tp, bn->base, k, best[k], st[k] != 1);
+	free(best);
+	free(st);
+	return bn;
+}
+
+/* ---------------------------------------------------------------------- */
+/* hash join (gdk/gdk_join.c:2900 hashjoin, HASHJOIN :2781-2895): the hash
+ * is built on the right input by prepending to bucket chains
+ * (gdk/gdk_hash.c:658-704), so for every left candidate in order its
+ * matches come out in DESCENDING right position.  nil never matches unless
+ * nil_matches. */
+int
+ora_join(ora_bat **r1p, ora_bat **r2p, const ora_bat *l, const ora_bat *r,
+	 const ora_bat *sl, const ora_bat *sr, bool nil_matches)
+{
+	ora_ci lci, rci;
+	if (ora_ci_init(&lci, l, sl) < 0 || ora_ci_init(&rci, r, sr) < 0)
+		return -1;
+	uint64_t cap = 16;
+	while (cap < 2 * rci.n)
+		cap <<= 1;
+	int64_t *head = malloc(cap * sizeof(int64_t));
+	int64_t *next = malloc((rci.n + 1) * sizeof(int64_t));
+	ora_hge *keys = malloc((rci.n + 1) * sizeof(ora_hge));
+	uint8_t *knil = malloc(rci.n + 1);
+	if (!head || !next || !keys || !knil) {
+		free(head); free(next); free(keys); free(knil);
+		ora_seterr("out of memory");
+		return -1;
+	}
+	memset(head, 0xff, cap * sizeof(int64_t));
+	for (uint64_t j = 0; j < rci.n; j++) {
+		knil[j] = val_at(r, ci_get(&rci, j) - r->hseqbase, &keys[j]);
+		uint64_t h = ghash(keys[j], 0) & (cap - 1);
+		next[j] = head[h];
+		head[h] = (int64_t) j;
+	}
+	uint64_t ocap = lci.n + 16, cnt = 0;
+	ora_oid *o1 = malloc(ocap * 8), *o2 = malloc(ocap * 8);
+	for (uint64_t i = 0; i < lci.n; i++) {
+		ora_oid lo = ci_get(&lci, i);
+		ora_hge v;
+		bool vn = val_at(l, lo - l->hseqbase, &v);
+		if (vn && !nil_matches)
+			continue;
+		uint64_t h = ghash(v, 0) & (cap - 1);
+		for (int64_t j = head[h]; j >= 0; j = next[j]) {
+			if (keys[j] != v || knil[j] != vn)
+				continue;
+			if (cnt == ocap) {
+				ocap *= 2;
+				o1 = realloc(o1, ocap * 8);
+				o2 = realloc(o2, ocap * 8);
+			}
+			o1[cnt] = lo;
+			o2[cnt] = ci_get(&rci, (uint64_t) j);
+			cnt++;
+		}
+	}
+	free(head); free(next); free(keys); free(knil);
+	ora_bat *a = ora_new(ORA_oid, cnt, 0), *b = ora_new(ORA_oid, cnt, 0);
+	memcpy(a->base, o1, cnt * 8);
+	memcpy(b->base, o2, cnt * 8);
+	free(o1);
+	free(o2);
+	a->nonil = b->nonil = 1;
+	*r1p = a;
+	if (r2p)
+		*r2p = b;
+	else
+		ora_free(b);
+	return 0;
+}
+
+/* ---------------------------------------------------------------------- */
+/* BATsort (gdk/gdk_batop.c:2342, do_sort :2266-2304): integer keys with
+ * nilslast == reverse are sorted by the stable LSD radix sort GDKrsort
+ * (gdk/gdk_rsort.c:21); nil (the type minimum) sorts first ascending and
+ * last descending; equal keys keep input order.  order holds the oids. */
+typedef struct {
+	ora_hge k;
+	uint64_t i;
+} skey;
+
+static int reverse_cmp;
+
+static int
+skey_cmp(const void *x, const void *y)
+{
+	const skey *a = x, *b = y;
+	if (a->k != b->k)
+		return reverse_cmp ? (a->k < b->k ? 1 : -1) : (a->k < b->k ? -1 : 1);
+	return a->i < b->i ? -1 : a->i > b->i;
+}
+
+int
+ora_sort(ora_bat **sorted, ora_bat **order, const ora_bat *b,
+	 bool reverse, bool nilslast)
+{
+	if (reverse != nilslast) {
+		ora_seterr("stable sort cannot have reverse != nilslast\n");
+		return -1;
+	}
+	uint64_t n = b->count;
+	skey *k = malloc((n + 1) * sizeof(skey));
+	for (uint64_t i = 0; i < n; i++) {
+		(void) val_at(b, i, &k[i].k);
+		k[i].i = i;
+	}
+	reverse_cmp = reverse;
+	qsort(k, n, sizeof(skey), skey_cmp);
+	ora_bat *sn = ora_new(b->type == ORA_void ? ORA_oid : b->type, n, b->hseqbase);
+	ora_bat *on = ora_new(ORA_oid, n, b->hseqbase);
+	for (uint64_t i = 0; i < n; i++) {
+		memcpy((char *) sn->base + i * sn->width,
+		       b->type == ORA_void ? (const void *) &(ora_oid){b->tseqbase + k[i].i}
+		       : (const char *) b->base + k[i].i * b->width, sn->width);
+		((ora_oid *) on->base)[i] = b->hseqbase + k[i].i;
+	}
+	free(k);
+	sn->sorted = !reverse;
+	sn->revsorted = reverse;
+	*sorted = sn;
+	if (order)
+		*order = on;
+	else
+		ora_free(on);
+	return 0;
+}
+
+/* ---------------------------------------------------------------------- */
+/* RANGE frame bounds (gdk/gdk_analytic_bounds.c:994-1294, kernels
+ * :273-387, special cases :614 allbounds and :710 peers): partitions start
+ * where p is true (and at row 0); PRECEDING walks back from row k while
+ * |b[k]-b[j]| <= limit and gives the first row of that run; FOLLOWING walks
+ * forward and gives one past the last row; a nil row's frame is its run of
+ * nils; a limit of GDK_lng_max is "unbounded".  Results are absolute row
+ * numbers.  Supports lng values with a lng limit. */
+int
+ora_rangebounds(ora_bat *r, const ora_bat *b, const ora_bat *p,
+		const void *bound, int tp2, bool preceding, ora_oid first_half)
+{
+	(void) first_half;
+	if (b->type != ORA_lng || tp2 != ORA_lng) {
+		ora_seterr("42000!range frame bound type not supported.\n");
+		return -1;
+	}
+	int64_t limit = *(const int64_t *) bound;
+	uint64_t cnt = b->count;
+	const int64_t *bp = b->base;
+	const int8_t *np = p ? p->base : NULL;
+	ora_oid *rb = r->base;
+	bool all = limit == INT64_MAX;
+	if (!all && (limit == INT64_MIN || limit < 0)) {
+		ora_seterr("42000!range frame bound must be non negative and non null.\n");
+		return -1;
+	}
+	uint64_t m = 0;
+	for (uint64_t i = 0; i <= cnt; i++) {
+		if (i < cnt && !(np && np[i]))
+			continue;
+		/* partition [m, i) */
+		for (uint64_t k = m; k < i; k++) {
+			int64_t v = bp[k];
+			bool vn = v == INT64_MIN;
+			uint64_t j;
+			if (all) {
+				rb[k] = preceding ? m : i;
+				continue;
+			}
+			if (preceding) {
+				for (j = k;; j--) {
+					bool jn = bp[j] == INT64_MIN;
+					if (vn ? !jn : jn) { j++; break; }
+					if (!vn) {
+						int64_t c;
+						if (__builtin_sub_overflow(v, bp[j], &c) || c == INT64_MIN) {
+							ora_seterr("22003!overflow in calculation.\n");
+							return -1;
+						}
+						if ((c < 0 ? -c : c) > limit) { j++; break; }
+					}
+					if (j == m)
+						break;
+				}
+			} else {
+				for (j = k + 1; j < i; j++) {
+					bool jn = bp[j] == INT64_MIN;
+					if (vn ? !jn : jn)
+						break;
+					if (!vn) {
+						int64_t c;
+						if (__builtin_sub_overflow(v, bp[j], &c) || c == INT64_MIN) {
+							ora_seterr("22003!overflow in calculation.\n");
+							return -1;
+						}
+						if ((c < 0 ? -c : c) > limit)
+							break;
+					}
+				}
+			}
+			rb[k] = j;
+		}
+		m = i;
+	}
+	r->count = cnt;
+	r->nonil = 1;
+	return 0;
+}

@@ -1,0 +1,345 @@
+"""ctypes wrapper of oracle/liboracle.so -- TEST INFRASTRUCTURE ONLY.
+
+Imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg, always as the checker / CPU comparator, never as the product path.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+TYPE_void, TYPE_bit, TYPE_bte, TYPE_sht, TYPE_int, TYPE_oid = 0, 2, 3, 4, 5, 6
+TYPE_flt, TYPE_dbl, TYPE_lng, TYPE_hge, TYPE_date, TYPE_str = 8, 9, 10, 11, 12, 16
+OID_NIL = 1 << 63
+
+NP = {TYPE_bit: np.int8, TYPE_bte: np.int8, TYPE_sht: np.int16, TYPE_int: np.int32,
+      TYPE_date: np.int32, TYPE_oid: np.uint64, TYPE_lng: np.int64, TYPE_flt: np.float32,
+      TYPE_dbl: np.float64, TYPE_str: np.uint8}
+CT = {TYPE_bit: C.c_int8, TYPE_bte: C.c_int8, TYPE_sht: C.c_int16, TYPE_int: C.c_int32,
+      TYPE_date: C.c_int32, TYPE_oid: C.c_uint64, TYPE_lng: C.c_int64, TYPE_flt: C.c_float,
+      TYPE_dbl: C.c_double}
+NIL = {TYPE_bit: -128, TYPE_bte: -128, TYPE_sht: -(1 << 15), TYPE_int: -(1 << 31),
+       TYPE_date: -(1 << 31), TYPE_lng: -(1 << 63), TYPE_hge: -(1 << 127), TYPE_oid: OID_NIL}
+
+
+class OraBat(C.Structure):
+    _fields_ = [("type", C.c_int32), ("width", C.c_int32), ("count", C.c_uint64),
+                ("hseqbase", C.c_uint64), ("tseqbase", C.c_uint64), ("base", C.c_void_p),
+                ("vheap", C.c_void_p), ("vheapsize", C.c_uint64),
+                ("sorted", C.c_uint8), ("revsorted", C.c_uint8), ("key", C.c_uint8),
+                ("nonil", C.c_uint8), ("nil", C.c_uint8), ("owned", C.c_uint8),
+                ("_pad", C.c_uint8 * 2)]
+
+
+class OraLineitem(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("shipdate", C.c_void_p), ("quantity", C.c_void_p),
+                ("extendedprice", C.c_void_p), ("discount", C.c_void_p), ("tax", C.c_void_p),
+                ("returnflag", C.c_void_p), ("linestatus", C.c_void_p)]
+
+
+class OraQ1Row(C.Structure):
+    # ora_hge members are 16-byte aligned in the C struct
+    _fields_ = [("returnflag", C.c_uint8), ("linestatus", C.c_uint8), ("_pad", C.c_uint8 * 14),
+                ("sum_qty", C.c_uint64 * 2), ("sum_base_price", C.c_uint64 * 2),
+                ("sum_disc_price", C.c_uint64 * 2), ("sum_charge", C.c_uint64 * 2),
+                ("avg_qty", C.c_int64), ("avg_price", C.c_int64), ("avg_disc", C.c_int64),
+                ("rem_qty", C.c_int64), ("rem_price", C.c_int64), ("rem_disc", C.c_int64),
+                ("count_order", C.c_int64), ("_tail", C.c_uint8 * 8)]   # sizeof = 144
+
+
+P = C.POINTER(OraBat)
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("oracle/liboracle.so not built (run make -C oracle)")
+        L = C.CDLL(LIB_PATH)
+        L.ora_new.restype = P
+        L.ora_new.argtypes = [C.c_int, C.c_uint64, C.c_uint64]
+        L.ora_free.argtypes = [P]
+        L.ora_errbuf.restype = C.c_char_p
+        L.ora_select.restype = P
+        L.ora_select.argtypes = [P, P, C.c_void_p, C.c_void_p, C.c_bool, C.c_bool, C.c_bool, C.c_bool]
+        L.ora_thetaselect.restype = P
+        L.ora_thetaselect.argtypes = [P, P, C.c_void_p, C.c_char_p]
+        L.ora_project.restype = P
+        L.ora_project.argtypes = [P, P]
+        L.ora_calc.restype = P
+        L.ora_calc.argtypes = [C.c_char, P, C.c_void_p, C.c_int, P, C.c_void_p, C.c_int, P, C.c_int]
+        L.ora_sum.argtypes = [C.c_void_p, C.c_int, P, P, C.c_bool, C.c_bool]
+        L.ora_group.argtypes = [C.POINTER(P), C.POINTER(P), C.POINTER(P), P, P, P]
+        for f in ("ora_groupsum",):
+            getattr(L, f).restype = P
+            getattr(L, f).argtypes = [P, P, P, P, C.c_int, C.c_bool]
+        L.ora_groupcount.restype = P
+        L.ora_groupcount.argtypes = [P, P, P, P, C.c_bool]
+        L.ora_groupminmax.restype = P
+        L.ora_groupminmax.argtypes = [P, P, P, P, C.c_bool, C.c_bool]
+        L.ora_groupavg3.argtypes = [C.POINTER(P), C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool]
+        L.ora_join.argtypes = [C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool]
+        L.ora_sort.argtypes = [C.POINTER(P), C.POINTER(P), P, C.c_bool, C.c_bool]
+        L.ora_rangebounds.argtypes = [P, P, P, C.c_void_p, C.c_int, C.c_bool, C.c_uint64]
+        L.ora_tpch_lineitem.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64] + [C.c_void_p] * 7
+        L.ora_mkdate.restype = C.c_int32
+        L.ora_mkdate.argtypes = [C.c_int, C.c_int, C.c_int]
+        L.ora_q6.argtypes = [C.POINTER(OraLineitem), C.c_int, C.c_void_p]
+        L.ora_q1.argtypes = [C.POINTER(OraLineitem), C.c_int, C.POINTER(OraQ1Row), C.POINTER(C.c_int)]
+        _lib = L
+    return _lib
+
+
+class OracleError(RuntimeError):
+    pass
+
+
+def _err():
+    return OracleError(lib().ora_errbuf().decode())
+
+
+def hge_to_int(words):
+    lo, hi = int(words[0]), int(words[1])
+    v = (hi << 64) | lo
+    return v - (1 << 128) if v >= (1 << 127) else v
+
+
+def int_to_hge_words(v):
+    v &= (1 << 128) - 1
+    return v & ((1 << 64) - 1), v >> 64
+
+
+class Bat:
+    """Python-side holder of an ora_bat; keeps numpy buffers alive."""
+
+    def __init__(self, ptr=None, keep=None):
+        self.ptr = ptr
+        self.keep = keep or []
+        self.owned = ptr is not None and keep is None
+
+    @classmethod
+    def from_array(cls, tp, arr, hseqbase=0, sorted_=False, revsorted=False, key=False,
+                   nonil=False, vheap=None):
+        if tp == TYPE_hge:
+            a = np.ascontiguousarray(arr, dtype=np.uint64).reshape(-1, 2)
+        else:
+            a = np.ascontiguousarray(arr, dtype=NP[tp])
+        n = a.shape[0]
+        b = OraBat()
+        b.type = tp
+        b.width = 16 if tp == TYPE_hge else (1 if tp == TYPE_str else a.dtype.itemsize)
+        b.count = n
+        b.hseqbase = hseqbase
+        b.tseqbase = OID_NIL
+        b.base = a.ctypes.data if n else a.ctypes.data
+        keep = [a, b]
+        if vheap is not None:
+            vh = np.frombuffer(vheap, dtype=np.uint8).copy()
+            b.vheap = vh.ctypes.data
+            b.vheapsize = vh.size
+            keep.append(vh)
+        b.sorted, b.revsorted, b.key, b.nonil = sorted_, revsorted, key, nonil
+        return cls(C.pointer(b), keep)
+
+    @classmethod
+    def dense(cls, tseq, n, hseqbase=0):
+        b = OraBat()
+        b.type = TYPE_void
+        b.count = n
+        b.hseqbase = hseqbase
+        b.tseqbase = tseq
+        b.sorted = b.key = b.nonil = 1
+        return cls(C.pointer(b), [b])
+
+    @property
+    def s(self):
+        return self.ptr.contents
+
+    def count(self):
+        return self.s.count
+
+    def values(self):
+        b = self.s
+        if b.type == TYPE_void:
+            return np.arange(b.tseqbase, b.tseqbase + b.count, dtype=np.uint64)
+        if b.type == TYPE_hge:
+            raw = np.ctypeslib.as_array(C.cast(b.base, C.POINTER(C.c_uint64)), (b.count * 2,)) \
+                if b.count else np.zeros(0, np.uint64)
+            return [hge_to_int(raw[2 * i:2 * i + 2]) for i in range(b.count)]
+        if b.count == 0:
+            return np.zeros(0, NP[b.type])
+        ct = CT.get(b.type, C.c_uint8)
+        return np.ctypeslib.as_array(C.cast(b.base, C.POINTER(ct)), (b.count,)).copy()
+
+    def __del__(self):
+        if self.owned and self.ptr is not None:
+            lib().ora_free(self.ptr)
+            self.ptr = None
+
+
+def _valptr(tp, v, keep):
+    if v is None:
+        return None
+    if tp == TYPE_hge:
+        buf = (C.c_uint64 * 2)(*int_to_hge_words(v))
+    elif tp == TYPE_void:
+        buf = C.c_uint64(v)
+    else:
+        buf = CT[tp](v)
+    keep.append(buf)
+    return C.cast(C.pointer(buf), C.c_void_p)
+
+
+def _ret(p):
+    if not p:
+        raise _err()
+    return Bat(p)
+
+
+def BATselect(b, s, tl, th, li, hi, anti, nil_matches=False):
+    keep = []
+    tp = b.s.type
+    return _ret(lib().ora_select(b.ptr, s.ptr if s else None, _valptr(tp, tl, keep),
+                                 _valptr(tp, th, keep), li, hi, anti, nil_matches))
+
+
+def BATthetaselect(b, s, val, op):
+    keep = []
+    return _ret(lib().ora_thetaselect(b.ptr, s.ptr if s else None,
+                                      _valptr(b.s.type, val, keep), op.encode()))
+
+
+def BATproject(l, r):
+    return _ret(lib().ora_project(l.ptr, r.ptr))
+
+
+def BATcalc(op, b1, b2, tp, s=None, c1=None, t1=0, c2=None, t2=0):
+    keep = []
+    return _ret(lib().ora_calc(op.encode(), b1.ptr if b1 else None, _valptr(t1, c1, keep), t1,
+                               b2.ptr if b2 else None, _valptr(t2, c2, keep), t2,
+                               s.ptr if s else None, tp))
+
+
+def BATsum(tp, b, s=None, skip_nils=True, nil_if_empty=True):
+    buf = (C.c_uint64 * 2)()
+    if lib().ora_sum(C.cast(buf, C.c_void_p), tp, b.ptr, s.ptr if s else None,
+                     skip_nils, nil_if_empty) < 0:
+        raise _err()
+    if tp == TYPE_hge:
+        return hge_to_int(buf)
+    if tp == TYPE_dbl:
+        return C.cast(buf, C.POINTER(C.c_double))[0]
+    return C.cast(buf, C.POINTER(CT[tp]))[0]
+
+
+def BATgroup(b, s=None, g=None):
+    gp, ep, hp = P(), P(), P()
+    if lib().ora_group(C.byref(gp), C.byref(ep), C.byref(hp), b.ptr, s.ptr if s else None,
+                       g.ptr if g else None) < 0:
+        raise _err()
+    return Bat(gp), Bat(ep), Bat(hp)
+
+
+def BATgroupsum(b, g, e, tp, skip_nils=True, s=None):
+    return _ret(lib().ora_groupsum(b.ptr, g.ptr, e.ptr if e else None, s.ptr if s else None,
+                                   tp, skip_nils))
+
+
+def BATgroupcount(b, g, e, skip_nils=True, s=None):
+    return _ret(lib().ora_groupcount(b.ptr, g.ptr, e.ptr if e else None, s.ptr if s else None,
+                                     skip_nils))
+
+
+def BATgroupminmax(b, g, e, domax, skip_nils=True, s=None):
+    return _ret(lib().ora_groupminmax(b.ptr, g.ptr, e.ptr if e else None,
+                                      s.ptr if s else None, skip_nils, domax))
+
+
+def BATgroupavg3(b, g, e, skip_nils=True, s=None):
+    a, r, c = P(), P(), P()
+    if lib().ora_groupavg3(C.byref(a), C.byref(r), C.byref(c), b.ptr, g.ptr,
+                           e.ptr if e else None, s.ptr if s else None, skip_nils) < 0:
+        raise _err()
+    return Bat(a), Bat(r), Bat(c)
+
+
+def BATjoin(l, r, sl=None, sr=None, nil_matches=False):
+    a, b = P(), P()
+    if lib().ora_join(C.byref(a), C.byref(b), l.ptr, r.ptr, sl.ptr if sl else None,
+                      sr.ptr if sr else None, nil_matches) < 0:
+        raise _err()
+    return Bat(a), Bat(b)
+
+
+def BATsort(b, reverse=False, nilslast=False):
+    a, o = P(), P()
+    if lib().ora_sort(C.byref(a), C.byref(o), b.ptr, reverse, nilslast) < 0:
+        raise _err()
+    return Bat(a), Bat(o)
+
+
+def rangebounds(b, p, limit, preceding):
+    n = b.count()
+    r = lib().ora_new(TYPE_oid, n, 0)
+    lim = C.c_int64(limit)
+    if lib().ora_rangebounds(r, b.ptr, p.ptr if p else None, C.cast(C.pointer(lim), C.c_void_p),
+                             TYPE_lng, preceding, 0) < 0:
+        lib().ora_free(r)
+        raise _err()
+    return Bat(r)
+
+
+def mkdate(y, m, d):
+    return lib().ora_mkdate(y, m, d)
+
+
+def tpch_lineitem(seed, row0, n, sf_parts):
+    cols = dict(shipdate=np.empty(n, np.int32), quantity=np.empty(n, np.int64),
+                extendedprice=np.empty(n, np.int64), discount=np.empty(n, np.int64),
+                tax=np.empty(n, np.int64), returnflag=np.empty(n, np.uint8),
+                linestatus=np.empty(n, np.uint8))
+    lib().ora_tpch_lineitem(seed, row0, n, sf_parts,
+                            *[cols[k].ctypes.data for k in ("shipdate", "quantity",
+                                                            "extendedprice", "discount", "tax",
+                                                            "returnflag", "linestatus")])
+    return cols
+
+
+def _li(cols):
+    li = OraLineitem()
+    li.n = cols["shipdate"].shape[0]
+    for k in ("shipdate", "quantity", "extendedprice", "discount", "tax", "returnflag",
+              "linestatus"):
+        setattr(li, k, cols[k].ctypes.data)
+    return li
+
+
+def q6(cols, nthreads=1):
+    out = (C.c_uint64 * 2)()
+    li = _li(cols)
+    if lib().ora_q6(C.byref(li), nthreads, C.cast(out, C.c_void_p)) < 0:
+        raise _err()
+    return hge_to_int(out)
+
+
+def q1(cols, nthreads=1):
+    rows = (OraQ1Row * 16)()
+    n = C.c_int()
+    li = _li(cols)
+    if lib().ora_q1(C.byref(li), nthreads, rows, C.byref(n)) < 0:
+        raise _err()
+    res = []
+    for i in range(n.value):
+        r = rows[i]
+        res.append(dict(returnflag=r.returnflag, linestatus=r.linestatus,
+                        sum_qty=hge_to_int(r.sum_qty), sum_base_price=hge_to_int(r.sum_base_price),
+                        sum_disc_price=hge_to_int(r.sum_disc_price),
+                        sum_charge=hge_to_int(r.sum_charge),
+                        avg_qty=r.avg_qty, avg_price=r.avg_price, avg_disc=r.avg_disc,
+                        rem_qty=r.rem_qty, rem_price=r.rem_price, rem_disc=r.rem_disc,
+                        count_order=r.count_order))
+    return res

@@ -1,0 +1,135 @@
+#!/usr/bin/env python3
+"""Extract golden vectors from the reference's own MAL known-answer tests.
+
+Run in the build container (where /root/reference exists); the output JSON
+files are committed and are what the tests read (the GPU box has no
+/root/reference).  Only inputs and expected outputs are kept -- no text of the
+reference test files.
+
+Sources (reference paths, relative to /root/reference):
+  monetdb5/modules/kernel/Tests/select.maltest  -- algebra.select over an int
+      BAT with a nil, on unsorted / sorted / reverse-sorted copies, every
+      li/hi/anti combination; expected = projected values of the selection
+      (ALGselect2 -> BATselect, monetdb5/modules/kernel/algebra.c:260-326)
+  monetdb5/mal/Tests/tst1500.maltest, tst1503.maltest -- group.group on a bte
+      BAT: groups / extents / histo (GRPsubgroup5 -> BATgroup)
+  monetdb5/modules/mal/Tests/bigsum.maltest -- aggr.sum of 10^16 followed by
+      10^7 ones into dbl (BATsum exactness)
+"""
+import json
+import os
+import re
+import sys
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def parse_blocks(text):
+    """Yield (kind, header, body_lines, expected_lines) records."""
+    lines = text.split("\n")
+    i = 0
+    while i < len(lines):
+        ln = lines[i].strip()
+        if ln.startswith("statement") or ln.startswith("query"):
+            kind = ln
+            body = []
+            i += 1
+            while i < len(lines) and lines[i].strip() not in ("", "----"):
+                body.append(lines[i].strip())
+                i += 1
+            exp = []
+            if i < len(lines) and lines[i].strip() == "----":
+                i += 1
+                while i < len(lines) and lines[i].strip() != "":
+                    exp.append(lines[i].strip())
+                    i += 1
+            yield kind, body, exp
+        else:
+            i += 1
+
+
+def val(tok):
+    tok = tok.strip()
+    if tok.startswith("nil"):
+        return None
+    return int(tok.split(":")[0])
+
+
+def select_fixture():
+    path = os.path.join(REF, "monetdb5/modules/kernel/Tests/select.maltest")
+    text = open(path).read()
+    values = []
+    cases = []
+    pending = None
+    for kind, body, exp in parse_blocks(text):
+        stmt = " ".join(body)
+        m = re.match(r"bat\.append\(b,\s*(.*)\)$", stmt)
+        if m:
+            values.append(val(m.group(1)))
+            continue
+        m = re.match(r"x := algebra\.select\((\w), nil:bat\[:oid\], ([^,]+), ([^,]+), "
+                     r"(true|false), (true|false), (true|false)\)$", stmt)
+        if m:
+            pending = dict(bat=m.group(1), low=val(m.group(2)), high=val(m.group(3)),
+                           li=m.group(4) == "true", hi=m.group(5) == "true",
+                           anti=m.group(6) == "true")
+            continue
+        if kind.startswith("query II") and stmt == "io.print(z)" and pending is not None:
+            # rows are (head, value) pairs, flattened
+            vals = exp[1::2]
+            pending["expected"] = sorted(None if v == "NULL" else int(v) for v in vals
+                                         if True) if "NULL" not in vals else \
+                [None] * vals.count("NULL") + sorted(int(v) for v in vals if v != "NULL")
+            cases.append(pending)
+            pending = None
+    return {"source": "monetdb5/modules/kernel/Tests/select.maltest",
+            "type": "int", "values": values,
+            "note": "s = algebra.sort(b) ascending nils first; r = descending nils last",
+            "cases": cases}
+
+
+def group_fixture(rel):
+    text = open(os.path.join(REF, rel)).read()
+    x = []
+    outs = {}
+    label = None
+    for kind, body, exp in parse_blocks(text):
+        stmt = " ".join(body)
+        m = re.match(r"\w+ := bat\.append\(x,\s*(\d+):bte\)$", stmt)
+        if m:
+            x.append(int(m.group(1)))
+            continue
+        if kind.startswith("query II") and re.match(r"io\.print\((g1|e1|h1)\)$", stmt):
+            name = stmt[9:11]
+            if exp:
+                outs[name] = [int(v) for v in exp[1::2]]
+    return {"source": rel, "type": "bte", "values": x, "expected": outs}
+
+
+def bigsum_fixture():
+    rel = "monetdb5/modules/mal/Tests/bigsum.maltest"
+    text = open(os.path.join(REF, rel)).read()
+    first = int(re.search(r"bat\.append\(b,(\d+):lng\)", text).group(1))
+    m = re.search(r"iterator\.next\((\d+):lng,(\d+):lng\)", text)
+    step, upto = int(m.group(1)), int(m.group(2))
+    ones = re.search(r"bat\.append\(b,(\d+):lng\)\s*\n\s*\nstatement ok\s*\n\s*redo", text)
+    expected = re.search(r"io\.print\(s\)\s*\n----\s*\n(\S+)", text).group(1)
+    return {"source": rel, "first": first, "repeat_value": 1,
+            "repeat_count": upto // step, "result_type": "dbl", "expected": expected}
+
+
+def main():
+    if not os.path.isdir(REF):
+        sys.exit("reference not present; fixtures are already committed")
+    fx = {"select": select_fixture(),
+          "group_tst1500": group_fixture("monetdb5/mal/Tests/tst1500.maltest"),
+          "group_tst1503": group_fixture("monetdb5/mal/Tests/tst1503.maltest"),
+          "bigsum": bigsum_fixture()}
+    with open(os.path.join(OUT, "maltest_fixtures.json"), "w") as f:
+        json.dump(fx, f, indent=1)
+    print("select cases:", len(fx["select"]["cases"]))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,334 @@
+"""Parity of the HIP path (libmgdk.so through the C ABI) with the oracle and
+with the reference's own fixtures.  Bit-exact for every oid / integer result."""
+import numpy as np
+import pytest
+
+from helpers import FIX, replay_select, rng, with_nils
+
+pytestmark = pytest.mark.gpu
+
+
+def mk(G, tp, vals, **kw):
+    return G.BAT.from_numpy(tp, np.asarray(vals), **kw)
+
+
+def omk(O, tp, vals, **kw):
+    return O.Bat.from_array(tp, np.asarray(vals), **kw)
+
+
+# ---- select ---------------------------------------------------------------
+
+def test_select_maltest_fixture(gdk):
+    bad = replay_select(gdk, lambda tp, v: mk(gdk, tp, np.array(v, np.int32)), gdk.TYPE_int,
+                        gdk.NIL[gdk.TYPE_int])
+    assert not bad, bad[:3]
+
+
+SEL_TYPES = [("bte", np.int8), ("sht", np.int16), ("int", np.int32), ("lng", np.int64),
+             ("dbl", np.float64), ("flt", np.float32)]
+
+
+def _cases(lo, hi, nil):
+    vs = [lo, hi, (lo + hi) // 2 if not isinstance(lo, float) else (lo + hi) / 2]
+    out = []
+    for tl in vs + [nil]:
+        for th in vs + [nil, None]:
+            for li in (False, True):
+                for hi_ in (False, True):
+                    for anti in (False, True):
+                        for nm in (False, True):
+                            out.append((tl, th, li, hi_, anti, nm))
+    return out
+
+
+@pytest.mark.parametrize("tname,dt", SEL_TYPES)
+def test_select_random_parity(gdk, ora, tname, dt):
+    r = rng(11)
+    tp = getattr(gdk, "TYPE_" + tname)
+    n = 50_000
+    if dt in (np.float32, np.float64):
+        vals = (r.integers(-50, 50, n)).astype(dt)
+        vals[r.random(n) < 0.05] = np.nan
+        nil = float("nan")
+        lo, hi = -20.0, 20.0
+    else:
+        vals = r.integers(-50, 50, n).astype(dt)
+        nil = gdk.NIL[tp]
+        vals = with_nils(vals, nil, 0.05, r)
+        lo, hi = -20, 20
+    b = mk(gdk, tp, vals)
+    ob = omk(ora, tp, vals)
+    # candidate lists: none, dense slice, materialized
+    cands = [(None, None),
+             (gdk.BAT.dense(1000, 30_000), ora.Bat.dense(1000, 30_000))]
+    co = np.sort(r.choice(n, 20_000, replace=False)).astype(np.uint64)
+    cands.append((mk(gdk, gdk.TYPE_oid, co, sorted_=True, key=True),
+                  omk(ora, ora.TYPE_oid, co, sorted_=True, key=True)))
+    for tl, th, li, hi_, anti, nm in _cases(lo, hi, nil):
+        for gs, os_ in cands:
+            try:
+                want = ora.BATselect(ob, os_, tl, th, li, hi_, anti, nm).values()
+            except ora.OracleError as e:
+                with pytest.raises(gdk.GDKError):
+                    gdk.BATselect(b, gs, tl, th, li, hi_, anti, nm)
+                continue
+            got = gdk.BATselect(b, gs, tl, th, li, hi_, anti, nm)
+            gv = got.values()
+            assert np.array_equal(np.asarray(gv, np.uint64), np.asarray(want, np.uint64)), \
+                (tname, tl, th, li, hi_, anti, nm)
+            # virtualised when dense, like virtualize()
+            if len(gv) <= 1 or int(gv[-1]) - int(gv[0]) == len(gv) - 1:
+                assert got.is_dense()
+
+
+def test_select_large_lookback(gdk):
+    """Many tiles: exercises the decoupled look-back across the whole grid."""
+    r = rng(3)
+    n = 30_000_001
+    vals = r.integers(0, 1000, n, dtype=np.int32)
+    b = mk(gdk, gdk.TYPE_int, vals, nonil=True)
+    for thr in (1, 100, 500, 999):
+        got = gdk.BATthetaselect(b, None, thr, "<").to_numpy()
+        want = np.flatnonzero(vals < thr).astype(np.uint64)
+        assert np.array_equal(got, want), thr
+
+
+def test_select_unaligned_view(gdk):
+    r = rng(5)
+    vals = r.integers(0, 10, 100_003, dtype=np.int32)
+    b = mk(gdk, gdk.TYPE_int, vals)
+    v = gdk.BAT(gdk.lib().mgdk_BATslice(b.ptr, 3, 100_001))
+    got = gdk.BATthetaselect(v, None, 5, "<").to_numpy()
+    want = (np.flatnonzero(vals[3:100_001] < 5) + 3).astype(np.uint64)
+    assert np.array_equal(got, want)
+
+
+# ---- project / calc / sum ---------------------------------------------------
+
+@pytest.mark.parametrize("tname,dt", [("bte", np.int8), ("int", np.int32), ("lng", np.int64),
+                                      ("dbl", np.float64)])
+def test_project(gdk, ora, tname, dt):
+    r = rng(21)
+    tp = getattr(gdk, "TYPE_" + tname)
+    vals = r.integers(-100, 100, 10_000).astype(dt)
+    b = mk(gdk, tp, vals, hseqbase=500)
+    l = np.sort(r.choice(np.arange(500, 10_500), 3000, replace=False)).astype(np.uint64)
+    l2 = l.copy()
+    l2[7] = gdk.OID_NIL
+    for arr in (l, l2):
+        got = gdk.BATproject(mk(gdk, gdk.TYPE_oid, arr), b).to_numpy()
+        want = ora.BATproject(omk(ora, ora.TYPE_oid, arr), omk(ora, tp, vals, hseqbase=500)).values()
+        assert np.array_equal(got.view(np.uint8), np.asarray(want, dt).view(np.uint8))
+    bad = l.copy()
+    bad[0] = 3
+    with pytest.raises(gdk.GDKError, match="does not match always"):
+        gdk.BATproject(mk(gdk, gdk.TYPE_oid, bad), b)
+    # dense left: slice
+    s = gdk.BATproject(gdk.BAT.dense(600, 100, hseqbase=7), b)
+    assert s.hseqbase == 7 and np.array_equal(s.to_numpy(), vals[100:200])
+
+
+@pytest.mark.parametrize("op", ["+", "-", "*"])
+@pytest.mark.parametrize("t1,t2,tp", [("int", "int", "int"), ("int", "int", "lng"),
+                                      ("lng", "lng", "lng"), ("lng", "lng", "hge"),
+                                      ("sht", "bte", "sht")])
+def test_calc(gdk, ora, op, t1, t2, tp):
+    r = rng(31)
+    T1, T2, TP = (getattr(gdk, "TYPE_" + x) for x in (t1, t2, tp))
+    dt = {"bte": np.int8, "sht": np.int16, "int": np.int32, "lng": np.int64}
+    n = 20_000
+    a = with_nils(r.integers(-1000, 1000, n).astype(dt[t1]), gdk.NIL[T1], 0.02, r)
+    b = with_nils(r.integers(-100, 100, n).astype(dt[t2]), gdk.NIL[T2], 0.02, r)
+    fn = {"+": gdk.BATcalcadd, "-": gdk.BATcalcsub, "*": gdk.BATcalcmul}[op]
+    ga, gb = mk(gdk, T1, a), mk(gdk, T2, b)
+    oa, ob = omk(ora, T1, a), omk(ora, T2, b)
+    try:
+        want = ora.BATcalc(op, oa, ob, TP).values()
+    except ora.OracleError as e:
+        with pytest.raises(gdk.GDKError) as ei:
+            fn(ga, gb, TP)
+        assert str(ei.value) == str(e)
+        return
+    got = fn(ga, gb, TP).values()
+    assert [int(x) for x in got] == [int(x) for x in want]
+
+
+def test_calc_overflow_matches(gdk, ora):
+    a = np.array([1, 5, 2**30, 7, 2**30], np.int32)
+    ga, oa = mk(gdk, gdk.TYPE_int, a), omk(ora, ora.TYPE_int, a)
+    with pytest.raises(gdk.GDKError) as ei:
+        gdk.BATcalcmulcst(ga, 4, gdk.TYPE_int, gdk.TYPE_int)
+    with pytest.raises(ora.OracleError) as eo:
+        ora.BATcalc("*", oa, None, ora.TYPE_int, c2=4, t2=ora.TYPE_int)
+    assert str(ei.value) == str(eo.value)
+    assert str(ei.value).startswith("22003!overflow in calculation 1073741824*4")
+
+
+def test_calc_cst_and_candidates(gdk, ora):
+    r = rng(41)
+    a = r.integers(0, 100, 5000).astype(np.int64)
+    ga, oa = mk(gdk, gdk.TYPE_lng, a), omk(ora, ora.TYPE_lng, a)
+    got = gdk.BATcalccstsub(100, gdk.TYPE_lng, ga, gdk.TYPE_lng).values()
+    want = ora.BATcalc("-", None, oa, ora.TYPE_lng, c1=100, t1=ora.TYPE_lng).values()
+    assert np.array_equal(got, want)
+    s = gdk.BAT.dense(100, 2000)
+    got = gdk.BATcalcmulcst(ga, 3, gdk.TYPE_lng, gdk.TYPE_hge, s=s)
+    want = ora.BATcalc("*", oa, None, ora.TYPE_hge, s=ora.Bat.dense(100, 2000), c2=3,
+                       t2=ora.TYPE_lng)
+    assert got.values() == want.values()
+
+
+@pytest.mark.parametrize("tname,tp", [("int", "lng"), ("lng", "lng"), ("lng", "hge"),
+                                      ("hge", "hge"), ("int", "dbl")])
+def test_sum(gdk, ora, tname, tp):
+    r = rng(51)
+    T, TP = getattr(gdk, "TYPE_" + tname), getattr(gdk, "TYPE_" + tp)
+    n = 100_000
+    if tname == "hge":
+        v = r.integers(-10**6, 10**6, n)
+        raw = np.zeros((n, 2), np.uint64)
+        raw[:, 0] = v.astype(np.int64).view(np.uint64)
+        raw[:, 1] = np.where(v < 0, np.uint64(2**64 - 1), np.uint64(0))
+        vals = raw
+    else:
+        dt = {"int": np.int32, "lng": np.int64}[tname]
+        vals = with_nils(r.integers(-10**6, 10**6, n).astype(dt), gdk.NIL[T], 0.01, r)
+    g, o = mk(gdk, T, vals), omk(ora, T, vals)
+    for skip in (True, False):
+        for nie in (True, False):
+            a = gdk.BATsum(TP, g, skip_nils=skip, nil_if_empty=nie)
+            b = ora.BATsum(TP, o, skip_nils=skip, nil_if_empty=nie)
+            if tp == "dbl":
+                assert (np.isnan(a) and np.isnan(b)) or a == b
+            else:
+                assert a == b
+
+
+def test_sum_overflow(gdk, ora):
+    big = np.array([2**62, 2**62, -2**62, 5], np.int64)
+    g, o = mk(gdk, gdk.TYPE_lng, big), omk(ora, ora.TYPE_lng, big)
+    with pytest.raises(ora.OracleError, match="overflow in sum"):
+        ora.BATsum(ora.TYPE_lng, o)
+    with pytest.raises(gdk.GDKError, match="22003!overflow in sum aggregate"):
+        gdk.BATsum(gdk.TYPE_lng, g)
+    ok = np.array([2**62, -2**62, 2**62, 5], np.int64)
+    assert gdk.BATsum(gdk.TYPE_lng, mk(gdk, gdk.TYPE_lng, ok)) == 2**62 + 5
+
+
+def test_bigsum_fixture(gdk):
+    fx = FIX["bigsum"]
+    vals = np.full(fx["repeat_count"] + 1, fx["repeat_value"], np.int64)
+    vals[0] = fx["first"]
+    s = gdk.BATsum(gdk.TYPE_dbl, mk(gdk, gdk.TYPE_lng, vals))
+    assert "%.10g" % s == fx["expected"]
+
+
+# ---- group and grouped aggregates --------------------------------------------
+
+@pytest.mark.parametrize("name", ["group_tst1500", "group_tst1503"])
+def test_group_fixture(gdk, name):
+    fx = FIX[name]
+    g, e, h = gdk.BATgroup(mk(gdk, gdk.TYPE_bte, np.array(fx["values"], np.int8)))
+    assert list(g.values()) == fx["expected"]["g1"]
+    assert list(e.values()) == fx["expected"]["e1"]
+    assert list(h.values()) == fx["expected"]["h1"]
+
+
+@pytest.mark.parametrize("tname,dt,card", [("bte", np.int8, 20), ("int", np.int32, 1000),
+                                           ("lng", np.int64, 100_000), ("sht", np.int16, 3000)])
+def test_group_random(gdk, ora, tname, dt, card):
+    r = rng(61)
+    tp = getattr(gdk, "TYPE_" + tname)
+    n = 200_000
+    vals = with_nils(r.integers(-card // 2, card // 2, n).astype(dt), gdk.NIL[tp], 0.01, r)
+    g, e, h = gdk.BATgroup(mk(gdk, tp, vals))
+    og, oe, oh = ora.BATgroup(omk(ora, tp, vals))
+    assert np.array_equal(g.to_numpy(), og.values())
+    assert np.array_equal(e.to_numpy(), oe.values())
+    assert np.array_equal(h.to_numpy(), oh.values())
+    # subgroup by a second column
+    v2 = r.integers(0, 7, n).astype(np.int8)
+    g2, e2, h2 = gdk.BATgroup(mk(gdk, gdk.TYPE_bte, v2), None, g)
+    og2, oe2, oh2 = ora.BATgroup(omk(ora, ora.TYPE_bte, v2), None, og)
+    assert np.array_equal(g2.to_numpy(), og2.values())
+    assert np.array_equal(e2.to_numpy(), oe2.values())
+    assert np.array_equal(h2.to_numpy(), oh2.values())
+
+
+def test_grouped_aggregates(gdk, ora):
+    r = rng(71)
+    n = 300_000
+    for ng in (1, 3, 6, 500):
+        gid = r.integers(0, ng, n).astype(np.uint64)
+        vals = with_nils(r.integers(-10**9, 10**9, n).astype(np.int64), gdk.NIL[gdk.TYPE_lng],
+                         0.001, r)
+        gg, og = mk(gdk, gdk.TYPE_oid, gid), omk(ora, ora.TYPE_oid, gid)
+        gv, ov = mk(gdk, gdk.TYPE_lng, vals), omk(ora, ora.TYPE_lng, vals)
+        for skip in (True, False):
+            assert gdk.BATgroupsum(gv, gg, None, gdk.TYPE_hge, skip).values() == \
+                ora.BATgroupsum(ov, og, None, ora.TYPE_hge, skip).values()
+            assert np.array_equal(gdk.BATgroupcount(gv, gg, None, skip).to_numpy(),
+                                  ora.BATgroupcount(ov, og, None, skip).values())
+            a, rr, c = gdk.BATgroupavg3(gv, gg, None, skip)
+            oa, orr, oc = ora.BATgroupavg3(ov, og, None, skip)
+            assert np.array_equal(a.to_numpy(), oa.values())
+            assert np.array_equal(rr.to_numpy(), orr.values())
+            assert np.array_equal(c.to_numpy(), oc.values())
+            for domax in (False, True):
+                f = gdk.BATgroupmax if domax else gdk.BATgroupmin
+                assert np.array_equal(f(gv, gg, None, skip).to_numpy(),
+                                      ora.BATgroupminmax(ov, og, None, domax, skip).values())
+
+
+def test_groupsum_nil_rules(gdk, ora):
+    L = gdk.NIL[gdk.TYPE_lng]
+    vals = np.array([L, 1, 2, 3, L, 4], np.int64)
+    gid = np.array([0, 0, 1, 1, 1, 0], np.uint64)
+    got = gdk.BATgroupsum(mk(gdk, gdk.TYPE_lng, vals), mk(gdk, gdk.TYPE_oid, gid), None,
+                          gdk.TYPE_lng, False).values()
+    assert list(got) == [5, L]
+
+
+# ---- TPC-H lineitem generation and pipelines ------------------------------------
+
+def test_tpch_generator_matches_oracle(gdk, ora):
+    n, row0 = 300_001, 12345
+    cols = gdk.tpch_lineitem(42, row0, n, 20_000)
+    want = ora.tpch_lineitem(42, row0, n, 20_000)
+    for k in gdk.LINEITEM_COLS:
+        assert np.array_equal(cols[k].to_numpy(), want[k]), k
+
+
+@pytest.mark.parametrize("n", [1, 5, 1_000_003])
+def test_q6_parity(gdk, ora, n):
+    cols = gdk.tpch_lineitem(9, 0, n, 20_000)
+    want = ora.q6(ora.tpch_lineitem(9, 0, n, 20_000), 4)
+    d0, d1 = ora.mkdate(1994, 1, 1), ora.mkdate(1995, 1, 1)
+    got = gdk.q6_fused(cols["shipdate"], cols["discount"], cols["quantity"],
+                       cols["extendedprice"], d0, d1, 5, 7, 2400)
+    assert got == want
+    got = gdk.q6_opatatime(cols["shipdate"], cols["discount"], cols["quantity"],
+                           cols["extendedprice"], d0, d1, 5, 7, 2400)
+    assert got == want
+
+
+def _q1_rows(rows):
+    out = []
+    for r in rows:
+        out.append((r["returnflag"], r["linestatus"], r["sum_qty"], r["sum_base_price"],
+                    r["sum_disc_price"], r["sum_charge"], r["count_order"]))
+    return sorted(out)
+
+
+@pytest.mark.parametrize("n", [7, 2_000_003])
+def test_q1_parity(gdk, ora, n):
+    cols = gdk.tpch_lineitem(5, 0, n, 20_000)
+    want = ora.q1(ora.tpch_lineitem(5, 0, n, 20_000), 4)
+    got = gdk.q1_fused(cols, ora.mkdate(1998, 9, 2))
+    assert _q1_rows(got) == _q1_rows(want)
+    # first-occurrence group numbering (BATgroup) and first rows agree with
+    # the op-at-a-time device plan
+    op = gdk.q1_fused(cols, ora.mkdate(1998, 9, 2), fused=False)
+    assert [(r["returnflag"], r["linestatus"], r["first_row"]) for r in got] == \
+        [(r["returnflag"], r["linestatus"], r["first_row"]) for r in op]
+    assert _q1_rows(op) == _q1_rows(want)
