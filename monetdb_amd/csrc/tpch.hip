@@ -154,7 +154,17 @@ q6_row(const Q6Args &a, int32_t sd, int64_t di, int64_t q, int64_t p)
 	return ok ? (hge) p * (hge) di : (hge) 0;
 }
 
-template <int UNROLL>
+template <bool NT, typename V>
+__device__ __forceinline__ V
+ldv(const V *p)
+{
+	if constexpr (NT)
+		return __builtin_nontemporal_load(p);
+	else
+		return *p;
+}
+
+template <int UNROLL, bool NT = false>
 __global__ __launch_bounds__(256) void
 k_q6(Q6Args a)
 {
@@ -170,13 +180,13 @@ k_q6(Q6Args a)
 #pragma unroll
 		for (int u = 0; u < UNROLL; u++) {
 			uint64_t r = (q + u * stride) * 4;
-			sd[u] = *(const i4 *) (a.sd + r);
-			d0[u] = *(const l2 *) (a.disc + r);
-			d1[u] = *(const l2 *) (a.disc + r + 2);
-			q0[u] = *(const l2 *) (a.qty + r);
-			q1[u] = *(const l2 *) (a.qty + r + 2);
-			p0[u] = *(const l2 *) (a.price + r);
-			p1[u] = *(const l2 *) (a.price + r + 2);
+			sd[u] = ldv<NT>((const i4 *) (a.sd + r));
+			d0[u] = ldv<NT>((const l2 *) (a.disc + r));
+			d1[u] = ldv<NT>((const l2 *) (a.disc + r + 2));
+			q0[u] = ldv<NT>((const l2 *) (a.qty + r));
+			q1[u] = ldv<NT>((const l2 *) (a.qty + r + 2));
+			p0[u] = ldv<NT>((const l2 *) (a.price + r));
+			p1[u] = ldv<NT>((const l2 *) (a.price + r + 2));
 		}
 #pragma unroll
 		for (int u = 0; u < UNROLL; u++) {
@@ -194,6 +204,59 @@ k_q6(Q6Args a)
 	// tail rows
 	if (blockIdx.x == 0 && threadIdx.x < (a.n & 3)) {
 		uint64_t r = nq * 4 + threadIdx.x;
+		acc += q6_row(a, a.sd[r], a.disc[r], a.qty[r], a.price[r]);
+	}
+	acc = wave_sum128(acc);
+	if (__lane_id() == 0 && acc != 0)
+		atomic_add128(a.out, acc);
+}
+
+// Contiguous-per-instruction variant: a wave owns a 256-row chunk; lane l
+// takes rows {2l, 2l+1, 128+2l, 128+2l+1}, so every load instruction of the
+// wave covers one contiguous range (512 B of shipdate, 1 KiB of each lng).
+template <int UNROLL, bool NT = false>
+__global__ __launch_bounds__(256) void
+k_q6c(Q6Args a)
+{
+	typedef int32_t i2 __attribute__((ext_vector_type(2)));
+	typedef int64_t l2 __attribute__((ext_vector_type(2)));
+	hge acc = 0;
+	const unsigned lane = __lane_id();
+	const uint64_t nch = a.n / 256;
+	const uint64_t nw = (uint64_t) gridDim.x * (blockDim.x / 64);
+	uint64_t c = ((uint64_t) blockIdx.x * blockDim.x + threadIdx.x) / 64;
+	for (; c + (UNROLL - 1) * nw < nch; c += UNROLL * nw) {
+		i2 s0[UNROLL], s1[UNROLL];
+		l2 d0[UNROLL], d1[UNROLL], q0[UNROLL], q1[UNROLL], p0[UNROLL], p1[UNROLL];
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++) {
+			const uint64_t r0 = (c + u * nw) * 256 + 2 * lane, r1 = r0 + 128;
+			s0[u] = ldv<NT>((const i2 *) (a.sd + r0));
+			s1[u] = ldv<NT>((const i2 *) (a.sd + r1));
+			d0[u] = ldv<NT>((const l2 *) (a.disc + r0));
+			d1[u] = ldv<NT>((const l2 *) (a.disc + r1));
+			q0[u] = ldv<NT>((const l2 *) (a.qty + r0));
+			q1[u] = ldv<NT>((const l2 *) (a.qty + r1));
+			p0[u] = ldv<NT>((const l2 *) (a.price + r0));
+			p1[u] = ldv<NT>((const l2 *) (a.price + r1));
+		}
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++) {
+			acc += q6_row(a, s0[u][0], d0[u][0], q0[u][0], p0[u][0]);
+			acc += q6_row(a, s0[u][1], d0[u][1], q0[u][1], p0[u][1]);
+			acc += q6_row(a, s1[u][0], d1[u][0], q1[u][0], p1[u][0]);
+			acc += q6_row(a, s1[u][1], d1[u][1], q1[u][1], p1[u][1]);
+		}
+	}
+	for (; c < nch; c += nw) {
+		const uint64_t r0 = c * 256 + 2 * lane, r1 = r0 + 128;
+		for (int k = 0; k < 2; k++) {
+			acc += q6_row(a, a.sd[r0 + k], a.disc[r0 + k], a.qty[r0 + k], a.price[r0 + k]);
+			acc += q6_row(a, a.sd[r1 + k], a.disc[r1 + k], a.qty[r1 + k], a.price[r1 + k]);
+		}
+	}
+	if (blockIdx.x == 0 && threadIdx.x < (a.n & 255)) {
+		const uint64_t r = nch * 256 + threadIdx.x;
 		acc += q6_row(a, a.sd[r], a.disc[r], a.qty[r], a.price[r]);
 	}
 	acc = wave_sum128(acc);
@@ -227,17 +290,32 @@ struct Q1Args {
 	uint32_t *flags;                  // [0] unknown key, [1] out of range / nil
 };
 
+// first qualifying row of every (returnflag, linestatus) code.  Lanes of a
+// wave hold consecutive rows, so per distinct code in the wave only its
+// lowest lane (= smallest row) competes for the global atomicMin.
 __global__ __launch_bounds__(256) void
 k_q1_keys(const int32_t *sd, const uint8_t *rf, const uint8_t *ls, uint64_t n, int32_t dmax,
 	  unsigned long long *first)
 {
-	for (uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x) {
-		int32_t d = sd[i];
-		if (d == INT32_MIN || d > dmax)
-			continue;
-		uint32_t c = ((uint32_t) rf[i] << 8) | ls[i];
-		if (first[c] > i)
-			atomicMin(&first[c], (unsigned long long) i);
+	const unsigned lane = __lane_id();
+	for (uint64_t base = (uint64_t) blockIdx.x * blockDim.x; base < n; base += (uint64_t) gridDim.x * blockDim.x) {
+		const uint64_t i = base + threadIdx.x;
+		bool valid = false;
+		uint32_t c = 0;
+		if (i < n) {
+			int32_t d = sd[i];
+			valid = d != INT32_MIN && d <= dmax;
+			c = ((uint32_t) rf[i] << 8) | ls[i];
+		}
+		uint64_t act = __ballot(valid);
+		while (act) {
+			const int leader = __ffsll((long long) act) - 1;
+			const uint32_t lc = __shfl(c, leader);
+			const uint64_t same = __ballot(valid && c == lc);
+			if ((int) lane == leader && first[lc] > i)
+				atomicMin(&first[lc], (unsigned long long) i);
+			act &= ~same;
+		}
 	}
 }
 
@@ -300,13 +378,13 @@ k_q1(Q1Args a)
 	uint64_t qi = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
 	for (; qi < nq; qi += stride) {
 		const uint64_t r = qi * 4;
-		i4 sd = *(const i4 *) (a.sd + r);
-		u4 rf = *(const u4 *) (a.rf + r);
-		u4 ls = *(const u4 *) (a.ls + r);
-		l2 q0 = *(const l2 *) (a.qty + r), q1 = *(const l2 *) (a.qty + r + 2);
-		l2 p0 = *(const l2 *) (a.price + r), p1 = *(const l2 *) (a.price + r + 2);
-		l2 d0 = *(const l2 *) (a.disc + r), d1 = *(const l2 *) (a.disc + r + 2);
-		l2 t0 = *(const l2 *) (a.tax + r), t1 = *(const l2 *) (a.tax + r + 2);
+		i4 sd = ldv<true>((const i4 *) (a.sd + r));
+		u4 rf = ldv<true>((const u4 *) (a.rf + r));
+		u4 ls = ldv<true>((const u4 *) (a.ls + r));
+		l2 q0 = ldv<true>((const l2 *) (a.qty + r)), q1 = ldv<true>((const l2 *) (a.qty + r + 2));
+		l2 p0 = ldv<true>((const l2 *) (a.price + r)), p1 = ldv<true>((const l2 *) (a.price + r + 2));
+		l2 d0 = ldv<true>((const l2 *) (a.disc + r)), d1 = ldv<true>((const l2 *) (a.disc + r + 2));
+		l2 t0 = ldv<true>((const l2 *) (a.tax + r)), t1 = ldv<true>((const l2 *) (a.tax + r + 2));
 		row(sd[0], ((uint32_t) rf[0] << 8) | ls[0], q0[0], p0[0], d0[0], t0[0]);
 		row(sd[1], ((uint32_t) rf[1] << 8) | ls[1], q0[1], p0[1], d0[1], t0[1]);
 		row(sd[2], ((uint32_t) rf[2] << 8) | ls[2], q1[0], p1[0], d1[0], t1[0]);
@@ -406,6 +484,43 @@ mgdk_tpch_lineitem(uint64_t seed, uint64_t row0, uint64_t n, uint64_t sf_parts, 
 	return 0;
 }
 
+// Q6 launch variants (tuning): variant = layout*3 + unroll_idx (+8: nt loads)
+//   layout 0: lane owns 4 consecutive rows (k_q6); 1: contiguous (k_q6c)
+//   unroll_idx 0,1,2 -> UNROLL 1,2,4;  bpc = workgroups per CU (256 CUs)
+// default from tools/q6_tune.py on MI355X (profiles/r01/q6_tune.log):
+// 4-row lanes, 2 iterations in flight, nontemporal loads, 16 WG/CU
+static int q6_variant = 9, q6_bpc = 16;
+
+static void
+launch_q6(const Q6Args &a, int variant, int bpc, hipStream_t st)
+{
+	const bool nt = (variant & 8) != 0;
+	const int v = variant & 7;
+	dim3 g(256u * (unsigned) bpc), blk(256);
+#define Q6L(K, U) do { if (nt) hipLaunchKernelGGL((K<U, true>), g, blk, 0, st, a); \
+			else hipLaunchKernelGGL((K<U, false>), g, blk, 0, st, a); } while (0)
+	switch (v) {
+	case 0: Q6L(k_q6, 1); break;
+	case 1: Q6L(k_q6, 2); break;
+	case 2: Q6L(k_q6, 4); break;
+	case 3: Q6L(k_q6c, 1); break;
+	case 4: Q6L(k_q6c, 2); break;
+	default: Q6L(k_q6c, 4); break;
+	}
+#undef Q6L
+}
+
+int mgdk_q6_fused(mgdk_bat *shipdate, mgdk_bat *discount, mgdk_bat *quantity, mgdk_bat *extendedprice,
+		  int32_t d0, int32_t d1, int64_t dlo, int64_t dhi, int64_t qmax, void *revenue);
+
+// select the Q6 launch variant for subsequent calls (tuning hook, not ABI)
+void
+mgdk_q6_set_variant(int variant, int blocks_per_cu)
+{
+	q6_variant = variant;
+	q6_bpc = blocks_per_cu > 0 ? blocks_per_cu : 8;
+}
+
 int
 mgdk_q6_fused(mgdk_bat *shipdate, mgdk_bat *discount, mgdk_bat *quantity, mgdk_bat *extendedprice,
 	      int32_t d0, int32_t d1, int64_t dlo, int64_t dhi, int64_t qmax, void *revenue)
@@ -439,7 +554,7 @@ mgdk_q6_fused(mgdk_bat *shipdate, mgdk_bat *discount, mgdk_bat *quantity, mgdk_b
 		if (a.n) {
 			bool al = aligned16(a.sd) && aligned16(a.disc) && aligned16(a.qty) && aligned16(a.price);
 			if (al)
-				hipLaunchKernelGGL((k_q6<2>), dim3(grid_for(a.n / 4 + 1, 256, 256 * 8)), dim3(256), 0, st, a);
+				launch_q6(a, q6_variant, q6_bpc, st);
 			else
 				hipLaunchKernelGGL(k_q6_scalar, dim3(grid_for(a.n, 256 * 4, 256 * 16)), dim3(256), 0, st, a);
 		}
@@ -475,7 +590,7 @@ mgdk_q1_fused(mgdk_bat *shipdate, mgdk_bat *returnflag, mgdk_bat *linestatus, mg
 	const uint64_t n = shipdate->count;
 	hipStream_t st = stream();
 	// 1. keys and their first occurrence on a prefix
-	const uint64_t pre = std::min<uint64_t>(n, (uint64_t) 1 << 22);
+	const uint64_t pre = std::min<uint64_t>(n, (uint64_t) 1 << 20);
 	DevBuf first(65536 * 8), list(64 * 16 + 64), acc(Q1_MAXK * 12 * 8 + 64);
 	uint32_t *cnt = (uint32_t *) ((char *) list.p + 64 * 16);
 	if (!hip_ok(hipMemsetAsync(first.p, 0xff, 65536 * 8, st), "memset") ||
@@ -518,7 +633,7 @@ mgdk_q1_fused(mgdk_bat *shipdate, mgdk_bat *returnflag, mgdk_bat *linestatus, mg
 		a.codes[k] = 0xffffffffu;
 	a.acc = acc.as<unsigned long long>();
 	a.flags = (uint32_t *) (a.acc + Q1_MAXK * 12);
-	dim3 g(grid_for(n / 4 + 1, 256, 256 * 8)), blk(256);
+	dim3 g(grid_for(n / 4 + 1, 256, 256 * 16)), blk(256);
 	if (K <= 1) hipLaunchKernelGGL(k_q1<1>, g, blk, 0, st, a);
 	else if (K <= 2) hipLaunchKernelGGL(k_q1<2>, g, blk, 0, st, a);
 	else if (K <= 4) hipLaunchKernelGGL(k_q1<4>, g, blk, 0, st, a);

@@ -1,0 +1,32 @@
+"""Q6 fused-kernel launch-variant sweep (interleaved rounds in one process)."""
+import ctypes as C
+import statistics
+import sys
+import time
+
+sys.path.insert(0, ".")
+from monetdb_amd import gdk
+
+gdk.init(0)
+rows = 600_121_500
+cols = gdk.tpch_lineitem(20241024, 0, rows, 20_000_000)
+mk = lambda y, m, d: (((y + 4712) * 12 + m - 1) << 5) | d
+args = (cols["shipdate"], cols["discount"], cols["quantity"], cols["extendedprice"],
+        mk(1994, 1, 1), mk(1995, 1, 1), 5, 7, 2400)
+L = gdk.lib()
+L.mgdk_q6_set_variant.argtypes = [C.c_int, C.c_int]
+ref = gdk.q6_fused(*args)
+variants = [(v, b) for v in (0, 1, 2, 3, 4, 5, 9, 12) for b in (4, 8, 16)]
+res = {k: [] for k in variants}
+gdk.prof_enable(True)
+for rnd in range(4):
+    for v, b in variants:
+        L.mgdk_q6_set_variant(v, b)
+        gdk.prof_reset()
+        for _ in range(5):
+            assert gdk.q6_fused(*args) == ref
+        ms, n = gdk.prof_get("q6_fused")
+        res[(v, b)].append(ms / n)
+for k in variants:
+    med = statistics.median(res[k])
+    print("variant %2d bpc %2d: %.4f ms  %.1f GB/s" % (k[0], k[1], med, rows * 28 / med / 1e6))
