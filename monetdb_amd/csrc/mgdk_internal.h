@@ -81,6 +81,17 @@ int cand_init(Cand *ci, const mgdk_bat *b, const mgdk_bat *s);
 // the result may be a dense (void) BAT.  Uses the thread's scratch buffer.
 mgdk_bat *compact_flags(const int8_t *flags, BUN n, oid base);
 
+// device-wide exclusive prefix sums (scan.hip); *total = sum of all inputs
+int exclusive_scan(const uint32_t *in, uint32_t *out, BUN n, uint64_t *total);
+int exclusive_scan(const uint32_t *in, uint64_t *out, BUN n, uint64_t *total);
+int exclusive_scan(const uint8_t *in, uint64_t *out, BUN n, uint64_t *total);
+
+// stable LSD radix sort of (key, payload) pairs in place (sort.hip); keys
+// are order-preserving unsigned images; `bits` = significant key bits.
+// Returns the buffers holding the result (the input pair or the spare).
+int radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32_t *vals_alt,
+		     BUN n, int bits, uint64_t **keys_out, uint32_t **vals_out);
+
 // RAII device temporary (not the per-thread scratch)
 struct DevBuf {
 	void *p = nullptr;

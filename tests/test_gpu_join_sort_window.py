@@ -1,0 +1,158 @@
+"""Parity of the device hash join, radix sort and RANGE window bounds with the
+oracle (bit-exact oid lists, permutations and bounds)."""
+import numpy as np
+import pytest
+
+from helpers import rng, with_nils
+
+pytestmark = pytest.mark.gpu
+
+
+def mk(G, tp, vals, **kw):
+    return G.BAT.from_numpy(tp, np.asarray(vals), **kw)
+
+
+def omk(O, tp, vals, **kw):
+    return O.Bat.from_array(tp, np.asarray(vals), **kw)
+
+
+# ---- hash join -----------------------------------------------------------------
+
+@pytest.mark.parametrize("tname,dt", [("int", np.int32), ("lng", np.int64), ("sht", np.int16)])
+@pytest.mark.parametrize("nil_matches", [False, True])
+def test_join_random(gdk, ora, tname, dt, nil_matches):
+    r = rng(81)
+    tp = getattr(gdk, "TYPE_" + tname)
+    nl, nr = 100_000, 30_000
+    lv = with_nils(r.integers(-5000, 5000, nl).astype(dt), gdk.NIL[tp], 0.01, r)
+    rv = with_nils(r.integers(-5000, 5000, nr).astype(dt), gdk.NIL[tp], 0.01, r)
+    a, b = gdk.BATjoin(mk(gdk, tp, lv, hseqbase=10), mk(gdk, tp, rv, hseqbase=7),
+                       nil_matches=nil_matches)
+    oa, ob = ora.BATjoin(omk(ora, tp, lv, hseqbase=10), omk(ora, tp, rv, hseqbase=7),
+                         nil_matches=nil_matches)
+    assert np.array_equal(a.to_numpy(), oa.values())
+    assert np.array_equal(b.to_numpy(), ob.values())
+
+
+def test_join_candidates_and_orders(gdk, ora):
+    r = rng(82)
+    nl, nr = 50_000, 20_000
+    # orders-like unique sparse keys, lineitem-like 1..7 lines per key, shuffled
+    okeys = np.arange(nr, dtype=np.int32) * 32 + (np.arange(nr) % 8)
+    r.shuffle(okeys)
+    lkeys = r.choice(okeys, nl).astype(np.int32)
+    sl = np.sort(r.choice(nl, 30_000, replace=False)).astype(np.uint64)
+    a, b = gdk.BATjoin(mk(gdk, gdk.TYPE_int, lkeys), mk(gdk, gdk.TYPE_int, okeys),
+                       sl=mk(gdk, gdk.TYPE_oid, sl), sr=gdk.BAT.dense(100, 15_000))
+    oa, ob = ora.BATjoin(omk(ora, ora.TYPE_int, lkeys), omk(ora, ora.TYPE_int, okeys),
+                         sl=omk(ora, ora.TYPE_oid, sl, sorted_=True), sr=ora.Bat.dense(100, 15_000))
+    assert np.array_equal(a.to_numpy(), oa.values())
+    assert np.array_equal(b.to_numpy(), ob.values())
+
+
+def test_join_duplicates_descending(gdk):
+    l = np.array([1, 2, 1], np.int32)
+    r = np.array([1, 1, 3, 1], np.int32)
+    a, b = gdk.BATjoin(mk(gdk, gdk.TYPE_int, l), mk(gdk, gdk.TYPE_int, r))
+    # per left row in order, right matches in descending position (chains prepend)
+    assert list(a.to_numpy()) == [0, 0, 0, 2, 2, 2]
+    assert list(b.to_numpy()) == [3, 1, 0, 3, 1, 0]
+
+
+# ---- sort -----------------------------------------------------------------------
+
+@pytest.mark.parametrize("tname,dt", [("bte", np.int8), ("int", np.int32), ("lng", np.int64)])
+@pytest.mark.parametrize("reverse", [False, True])
+def test_sort_int(gdk, ora, tname, dt, reverse):
+    r = rng(91)
+    tp = getattr(gdk, "TYPE_" + tname)
+    n = 200_001
+    vals = with_nils(r.integers(-100, 100, n).astype(dt), gdk.NIL[tp], 0.02, r)
+    s, o, g = gdk.BATsort(mk(gdk, tp, vals, hseqbase=3), reverse=reverse, nilslast=reverse)
+    os_, oo = ora.BATsort(omk(ora, tp, vals, hseqbase=3), reverse=reverse, nilslast=reverse)
+    assert np.array_equal(s.to_numpy(), os_.values())
+    assert np.array_equal(o.to_numpy(), oo.values())
+    sv = s.to_numpy()
+    want_g = np.concatenate([[0], np.cumsum(sv[1:] != sv[:-1])]).astype(np.uint64)
+    assert np.array_equal(g.to_numpy(), want_g)
+
+
+def test_sort_wide_range(gdk, ora):
+    r = rng(92)
+    vals = r.integers(-2**62, 2**62, 100_000).astype(np.int64)
+    s, o, _ = gdk.BATsort(mk(gdk, gdk.TYPE_lng, vals))
+    os_, oo = ora.BATsort(omk(ora, ora.TYPE_lng, vals))
+    assert np.array_equal(o.to_numpy(), oo.values())
+
+
+@pytest.mark.parametrize("dt,tname", [(np.float64, "dbl"), (np.float32, "flt")])
+def test_sort_float(gdk, dt, tname):
+    r = rng(93)
+    n = 50_000
+    vals = (r.integers(-50, 50, n) / 4).astype(dt)
+    vals[r.random(n) < 0.02] = np.nan
+    vals[r.random(n) < 0.01] = -0.0
+    tp = getattr(gdk, "TYPE_" + tname)
+    s, o, _ = gdk.BATsort(mk(gdk, tp, vals))
+    key = np.where(np.isnan(vals), -np.inf, vals)          # nil first
+    key = np.where(key == 0, 0.0, key)                      # -0 == +0
+    want = np.argsort(key, kind="stable").astype(np.uint64)
+    assert np.array_equal(o.to_numpy(), want)
+
+
+def test_sort_errors(gdk):
+    b = mk(gdk, gdk.TYPE_int, np.array([3, 1, 2], np.int32))
+    with pytest.raises(gdk.GDKError, match="stable sort cannot have reverse != nilslast"):
+        gdk.BATsort(b, reverse=True, nilslast=False, stable=True)
+
+
+# ---- RANGE window bounds ------------------------------------------------------------
+
+def _window_data(r, nparts, plen, desc=False, nil_frac=0.0, shuffle=False):
+    vals, bits = [], []
+    for _ in range(nparts):
+        gaps = r.integers(0, 5, plen)
+        v = np.cumsum(gaps).astype(np.int64) + r.integers(-1000, 1000)
+        nn = int(plen * nil_frac)
+        if desc:
+            v = v[::-1].copy()
+            if nn:
+                v[-nn:] = np.iinfo(np.int64).min
+        elif nn:
+            v[:nn] = np.iinfo(np.int64).min
+        if shuffle:
+            r.shuffle(v)
+        vals.append(v)
+        p = np.zeros(plen, np.int8)
+        p[0] = 1
+        bits.append(p)
+    return np.concatenate(vals), np.concatenate(bits)
+
+
+@pytest.mark.parametrize("desc,nil_frac,shuffle", [(False, 0.0, False), (False, 0.05, False),
+                                                   (True, 0.05, False), (False, 0.02, True)])
+@pytest.mark.parametrize("limit", [0, 3, 100, 2**63 - 1])
+@pytest.mark.parametrize("preceding", [True, False])
+def test_window_range_bounds(gdk, ora, desc, nil_frac, shuffle, limit, preceding):
+    r = rng(101)
+    vals, bits = _window_data(r, 37, 523, desc, nil_frac, shuffle)
+    got = gdk.GDKanalyticalwindowbounds(mk(gdk, gdk.TYPE_lng, vals), mk(gdk, gdk.TYPE_bit, bits),
+                                        limit, preceding).to_numpy()
+    want = ora.rangebounds(omk(ora, ora.TYPE_lng, vals), omk(ora, ora.TYPE_bit, bits), limit,
+                           preceding).values()
+    assert np.array_equal(got, want)
+
+
+def test_window_no_partitions_and_errors(gdk, ora):
+    r = rng(102)
+    vals = np.sort(r.integers(0, 10**6, 100_000)).astype(np.int64)
+    got = gdk.GDKanalyticalwindowbounds(mk(gdk, gdk.TYPE_lng, vals), None, 50, True).to_numpy()
+    want = ora.rangebounds(omk(ora, ora.TYPE_lng, vals), None, 50, True).values()
+    assert np.array_equal(got, want)
+    with pytest.raises(gdk.GDKError, match="non negative and non null"):
+        gdk.GDKanalyticalwindowbounds(mk(gdk, gdk.TYPE_lng, vals), None, -1, True)
+    big = np.array([-2**62 * 3 // 2, 2**62 * 3 // 2], np.int64)
+    with pytest.raises(gdk.GDKError, match="22003!overflow in calculation"):
+        gdk.GDKanalyticalwindowbounds(mk(gdk, gdk.TYPE_lng, big), None, 5, True)
+    with pytest.raises(ora.OracleError, match="22003!overflow in calculation"):
+        ora.rangebounds(omk(ora, ora.TYPE_lng, big), None, 5, True)
