@@ -167,6 +167,10 @@ int mgdk_q1_opatatime(mgdk_bat *shipdate, mgdk_bat *returnflag, mgdk_bat *linest
  *      discount, tax (lng), returnflag, linestatus (str, 1-byte offsets) -- */
 int mgdk_tpch_lineitem(uint64_t seed, uint64_t row0, uint64_t n, uint64_t sf_parts,
 		       mgdk_bat **cols /* [7] */);
+/* RANGE-window input of BASELINE config 5: n ascending lng values (gaps
+ * U[0,4]) and a partition-start bit column (one partition per plen rows) */
+int mgdk_gen_window_column(uint64_t seed, uint64_t n, uint64_t plen, mgdk_bat **vals,
+			   mgdk_bat **parts);
 
 #ifdef __cplusplus
 }

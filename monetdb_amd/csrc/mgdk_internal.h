@@ -79,7 +79,7 @@ int cand_init(Cand *ci, const mgdk_bat *b, const mgdk_bat *s);
 
 // ordered compaction (select.hip): sorted positions base+i with flags[i]==1;
 // the result may be a dense (void) BAT.  Uses the thread's scratch buffer.
-mgdk_bat *compact_flags(const int8_t *flags, BUN n, oid base);
+mgdk_bat *compact_flags(const int8_t *flags, BUN n, oid base, bool nonzero = false);
 
 // device-wide exclusive prefix sums (scan.hip); *total = sum of all inputs
 int exclusive_scan(const uint32_t *in, uint32_t *out, BUN n, uint64_t *total);

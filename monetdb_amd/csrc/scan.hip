@@ -13,7 +13,7 @@ using namespace mgdk;
 namespace {
 
 constexpr uint64_t ST_AGG = 1ull << 62, ST_PRE = 2ull << 62, ST_VAL = (1ull << 62) - 1;
-constexpr int ITEMS = 16;
+constexpr int ITEMS = 64;
 
 __device__ uint64_t
 lookback64(uint64_t *status, uint32_t tile, uint64_t agg, uint32_t *err)
@@ -60,11 +60,17 @@ lookback64(uint64_t *status, uint32_t tile, uint64_t agg, uint32_t *err)
 	return excl;
 }
 
+// a lane sums its ITEMS consecutive inputs with 16-byte loads (pass 1), the
+// tile is scanned, then the lane re-reads them (cache-resident) and writes
+// its outputs (pass 2); 64 items per lane keeps tile tickets to one per
+// 16 Ki items (a single ticket counter sustains ~88 atomics/us)
 template <typename TI, typename TO>
 __global__ __launch_bounds__(256) void
 k_scan(const TI *in, TO *out, BUN n, uint64_t *status, uint32_t *ticket, uint32_t ntiles,
        uint64_t *total, uint32_t *err)
 {
+	constexpr int VI = 16 / sizeof(TI);
+	typedef TI vec_t __attribute__((ext_vector_type(VI)));
 	__shared__ uint32_t s_tile;
 	__shared__ uint64_t s_wave[4];
 	__shared__ uint64_t s_prefix;
@@ -74,12 +80,20 @@ k_scan(const TI *in, TO *out, BUN n, uint64_t *status, uint32_t *ticket, uint32_
 	__syncthreads();
 	const uint32_t tile = s_tile;
 	const BUN base = ((BUN) tile * 256 + tid) * ITEMS;
-	uint64_t v[ITEMS];
+	const bool fullv = base + ITEMS <= n;
 	uint64_t sum = 0;
+	if (fullv) {
 #pragma unroll
-	for (int k = 0; k < ITEMS; k++) {
-		v[k] = base + k < n ? (uint64_t) in[base + k] : 0;
-		sum += v[k];
+		for (int k = 0; k < ITEMS; k += VI) {
+			vec_t x = *(const vec_t *) (in + base + k);
+#pragma unroll
+			for (int q = 0; q < VI; q++)
+				sum += (uint64_t) x[q];
+		}
+	} else {
+		for (int k = 0; k < ITEMS; k++)
+			if (base + k < n)
+				sum += (uint64_t) in[base + k];
 	}
 	// inclusive wave scan of lane sums
 	uint64_t x = sum;
@@ -108,11 +122,23 @@ k_scan(const TI *in, TO *out, BUN n, uint64_t *status, uint32_t *ticket, uint32_
 	}
 	__syncthreads();
 	uint64_t run = s_prefix + wpre + x - sum;
+	if (fullv) {
 #pragma unroll
-	for (int k = 0; k < ITEMS; k++) {
-		if (base + k < n)
-			out[base + k] = (TO) run;
-		run += v[k];
+		for (int k = 0; k < ITEMS; k += VI) {
+			vec_t xv = *(const vec_t *) (in + base + k);
+#pragma unroll
+			for (int q = 0; q < VI; q++) {
+				out[base + k + q] = (TO) run;
+				run += (uint64_t) xv[q];
+			}
+		}
+	} else {
+		for (int k = 0; k < ITEMS; k++) {
+			if (base + k < n) {
+				out[base + k] = (TO) run;
+				run += (uint64_t) in[base + k];
+			}
+		}
 	}
 }
 

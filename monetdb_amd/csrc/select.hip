@@ -38,18 +38,25 @@ struct SelPred {
 	int mode;
 	bool nil_matches;
 	T vl, vh;
-	__device__ __forceinline__ bool operator()(T v) const {
-		switch (mode) {
-		case SEL_RANGE: return v >= vl && v <= vh;
-		case SEL_ANTI:
-			return nil_matches ? (is_nil(v) || v <= vl || v >= vh)
-					   : (!is_nil(v) && (v <= vl || v >= vh));
-		case SEL_EQ: return v == vl;
-		case SEL_EQNIL: return is_nil(v);
-		default: return !is_nil(v);
-		}
-	}
 };
+
+// the predicate with the mode fixed at compile time (branch-free per value)
+template <int MODE, typename T>
+__device__ __forceinline__ bool
+sel_eval(const SelPred<T> &p, T v)
+{
+	if constexpr (MODE == SEL_RANGE)
+		return v >= p.vl && v <= p.vh;
+	else if constexpr (MODE == SEL_ANTI)
+		return p.nil_matches ? (is_nil(v) || v <= p.vl || v >= p.vh)
+				     : (!is_nil(v) && (v <= p.vl || v >= p.vh));
+	else if constexpr (MODE == SEL_EQ)
+		return v == p.vl;
+	else if constexpr (MODE == SEL_EQNIL)
+		return is_nil(v);
+	else
+		return !is_nil(v);
+}
 
 constexpr uint64_t ST_AGG = 1ull << 62, ST_PRE = 2ull << 62, ST_VAL = (1ull << 62) - 1;
 
@@ -146,15 +153,22 @@ struct SelArgs {
 	uint64_t *meta;           // [0] total count, [1] error flags
 };
 
-constexpr int ROWS = 8;
+// rows of 256 lanes x 16 B per tile: 32 for a dense scan (128 KiB of input per
+// tile, so one tile ticket per 128 KiB: a single counter sustains only ~88
+// atomics/us, MI355X_MICROARCH.md "dequeue"), 16 for candidate lists;
+// loads are issued in batches of 8 rows
+template <bool MAT> constexpr int sel_rows() { return MAT ? 16 : 32; }
+constexpr int BATCH = 8;
 
-template <typename T, bool MAT>
+template <typename T, bool MAT, int MODE>
 __global__ __launch_bounds__(256) void
 k_select(SelArgs<T> a)
 {
 	constexpr int V = MAT ? 2 : (int) (16 / sizeof(T));
+	constexpr int ROWS = sel_rows<MAT>();
 	constexpr int BITS = Bits<V>::v;
 	typedef T vec_t __attribute__((ext_vector_type(V)));
+	typedef oid ovec_t __attribute__((ext_vector_type(2)));
 	__shared__ uint32_t s_tile;
 	__shared__ uint32_t s_off[ROWS * 4];
 	__shared__ uint64_t s_prefix;
@@ -166,39 +180,79 @@ k_select(SelArgs<T> a)
 	const uint32_t tile = s_tile;
 	const uint64_t nslots = a.n + a.shift;
 	const uint64_t lt = lanemask_lt();
+	const uint64_t j_first = (uint64_t) tile * ROWS * 256 * V;
+	// interior tiles: every slot valid -> all loads issued before any use
+	const bool full = tile > 0 && j_first + (uint64_t) ROWS * 256 * V <= nslots;
 
 	uint32_t hm[ROWS];
 	oid cv[MAT ? ROWS * 2 : 1];
 	(void) cv;
+	if (full) {
 #pragma unroll
-	for (int r = 0; r < ROWS; r++) {
-		const uint64_t vi = ((uint64_t) tile * ROWS + r) * 256 + tid;
-		const uint64_t j0 = vi * V;
-		uint32_t m = 0;
-		if (j0 < nslots) {
+		for (int b0 = 0; b0 < ROWS; b0 += BATCH) {
 			if constexpr (!MAT) {
-				vec_t x = *(const vec_t *) (a.col_al + j0);
+				vec_t x[BATCH];
 #pragma unroll
-				for (int k = 0; k < V; k++) {
-					uint64_t j = j0 + k;
-					bool ok = j >= a.shift && j < nslots && a.pred(x[k]);
-					m |= (uint32_t) ok << k;
+				for (int r = 0; r < BATCH; r++)
+					x[r] = __builtin_nontemporal_load(
+						(const vec_t *) (a.col_al + (((uint64_t) tile * ROWS + b0 + r) * 256 + tid) * V));
+#pragma unroll
+				for (int r = 0; r < BATCH; r++) {
+					uint32_t m = 0;
+#pragma unroll
+					for (int k = 0; k < V; k++)
+						m |= (uint32_t) sel_eval<MODE>(a.pred, (T) x[r][k]) << k;
+					hm[b0 + r] = m;
 				}
 			} else {
-				typedef oid ovec_t __attribute__((ext_vector_type(2)));
-				ovec_t o = *(const ovec_t *) (a.cand_al + j0);
+				ovec_t o[BATCH];
 #pragma unroll
-				for (int k = 0; k < 2; k++) {
-					uint64_t j = j0 + k;
-					cv[r * 2 + k] = o[k];
-					if (j >= a.shift && j < nslots) {
-						T v = a.col[o[k] - a.hseq];
-						m |= (uint32_t) a.pred(v) << k;
+				for (int r = 0; r < BATCH; r++)
+					o[r] = *(const ovec_t *) (a.cand_al + (((uint64_t) tile * ROWS + b0 + r) * 256 + tid) * 2);
+				T v[BATCH * 2];
+#pragma unroll
+				for (int r = 0; r < BATCH; r++) {
+					cv[(b0 + r) * 2] = o[r][0];
+					cv[(b0 + r) * 2 + 1] = o[r][1];
+					v[r * 2] = a.col[o[r][0] - a.hseq];
+					v[r * 2 + 1] = a.col[o[r][1] - a.hseq];
+				}
+#pragma unroll
+				for (int r = 0; r < BATCH; r++)
+					hm[b0 + r] = (uint32_t) sel_eval<MODE>(a.pred, v[r * 2]) |
+						     ((uint32_t) sel_eval<MODE>(a.pred, v[r * 2 + 1]) << 1);
+			}
+		}
+	} else {
+#pragma unroll
+		for (int r = 0; r < ROWS; r++) {
+			const uint64_t vi = ((uint64_t) tile * ROWS + r) * 256 + tid;
+			const uint64_t j0 = vi * V;
+			uint32_t m = 0;
+			if (j0 < nslots) {
+				if constexpr (!MAT) {
+					vec_t x = *(const vec_t *) (a.col_al + j0);
+#pragma unroll
+					for (int k = 0; k < V; k++) {
+						uint64_t j = j0 + k;
+						bool ok = j >= a.shift && j < nslots && sel_eval<MODE>(a.pred, (T) x[k]);
+						m |= (uint32_t) ok << k;
+					}
+				} else {
+					ovec_t o = *(const ovec_t *) (a.cand_al + j0);
+#pragma unroll
+					for (int k = 0; k < 2; k++) {
+						uint64_t j = j0 + k;
+						cv[r * 2 + k] = o[k];
+						if (j >= a.shift && j < nslots) {
+							T v = a.col[o[k] - a.hseq];
+							m |= (uint32_t) sel_eval<MODE>(a.pred, v) << k;
+						}
 					}
 				}
 			}
+			hm[r] = m;
 		}
-		hm[r] = m;
 	}
 	// per (row, wave) totals
 #pragma unroll
@@ -210,17 +264,32 @@ k_select(SelArgs<T> a)
 	}
 	__syncthreads();
 	if (wave == 0) {
-		uint32_t x = lane < ROWS * 4 ? s_off[lane] : 0u;
-		const uint32_t own = x;
+		// exclusive scan of the ROWS*4 (row, wave) segment counts, in
+		// order; lane l owns entries [EPL*l, EPL*l + EPL)
+		constexpr int EPL = (ROWS * 4 + 63) / 64;
+		uint32_t e[EPL], own = 0;
+#pragma unroll
+		for (int q = 0; q < EPL; q++) {
+			const int idx = (int) lane * EPL + q;
+			e[q] = idx < ROWS * 4 ? s_off[idx] : 0u;
+			own += e[q];
+		}
+		uint32_t x = own;
 #pragma unroll
 		for (int o = 1; o < 64; o <<= 1) {
 			uint32_t y = __shfl_up(x, o);
 			if ((int) lane >= o)
 				x += y;
 		}
-		if (lane < ROWS * 4)
-			s_off[lane] = x - own;
-		uint64_t agg = __shfl(x, ROWS * 4 - 1);
+		uint32_t run = x - own;
+#pragma unroll
+		for (int q = 0; q < EPL; q++) {
+			const int idx = (int) lane * EPL + q;
+			if (idx < ROWS * 4)
+				s_off[idx] = run;
+			run += e[q];
+		}
+		uint64_t agg = __shfl(x, 63);
 		uint64_t pre = lookback(a.status, tile, agg, (uint32_t *) &a.meta[1]);
 		if (lane == 0) {
 			s_prefix = pre;
@@ -363,12 +432,12 @@ run_scan(const mgdk_bat *b, const Cand &ci, const SelPred<T> &pred)
 		a.col_al = start - mis;
 		a.shift = (uint32_t) mis;
 		a.cseq = ci.seq;
-		items_per_tile = (uint64_t) ROWS * 256 * (16 / sizeof(T));
+		items_per_tile = (uint64_t) sel_rows<false>() * 256 * (16 / sizeof(T));
 	} else {
 		uintptr_t mis = ((uintptr_t) ci.oids % 16) / sizeof(oid);
 		a.cand_al = ci.oids - mis;
 		a.shift = (uint32_t) mis;
-		items_per_tile = (uint64_t) ROWS * 256 * 2;
+		items_per_tile = (uint64_t) sel_rows<true>() * 256 * 2;
 	}
 	uint64_t ntiles = (ci.n + a.shift + items_per_tile - 1) / items_per_tile;
 	if (ntiles >= (1ull << 31)) {
@@ -393,10 +462,23 @@ run_scan(const mgdk_bat *b, const Cand &ci, const SelPred<T> &pred)
 		mgdk_BBPunfix(bn);
 		return nullptr;
 	}
-	if (ci.dense)
-		hipLaunchKernelGGL((k_select<T, false>), dim3((unsigned) ntiles), dim3(256), 0, st, a);
-	else
-		hipLaunchKernelGGL((k_select<T, true>), dim3((unsigned) ntiles), dim3(256), 0, st, a);
+	{
+		const dim3 g((unsigned) ntiles), blk(256);
+#define SELL(MAT, MODE) hipLaunchKernelGGL((k_select<T, MAT, MODE>), g, blk, 0, st, a)
+#define SELM(MAT) switch (pred.mode) { \
+		case SEL_RANGE: SELL(MAT, SEL_RANGE); break; \
+		case SEL_ANTI: SELL(MAT, SEL_ANTI); break; \
+		case SEL_EQ: SELL(MAT, SEL_EQ); break; \
+		case SEL_EQNIL: SELL(MAT, SEL_EQNIL); break; \
+		default: SELL(MAT, SEL_NOTNIL); break; }
+		if (ci.dense) {
+			SELM(false);
+		} else {
+			SELM(true);
+		}
+#undef SELM
+#undef SELL
+	}
 	hipLaunchKernelGGL(k_select_fin, dim3(1), dim3(1), 0, st, (const oid *) bn->theap, meta);
 	uint64_t *h = (uint64_t *) pinned(64);
 	if (h == nullptr || !hip_ok(hipMemcpyAsync(h, meta, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, st), "memcpy") ||
@@ -573,7 +655,7 @@ namespace mgdk {
 // Ordered compaction of a 0/1 byte array: the sorted list of positions i
 // (as oids base + i) with flags[i] == 1.  Used by BATgroup / BATjoin.
 mgdk_bat *
-compact_flags(const int8_t *flags, BUN n, oid base)
+compact_flags(const int8_t *flags, BUN n, oid base, bool nonzero)
 {
 	if (n == 0)
 		return empty_result();
@@ -590,6 +672,13 @@ compact_flags(const int8_t *flags, BUN n, oid base)
 	ci.first = base;
 	ci.last = base + n - 1;
 	SelPred<int8_t> p{SEL_EQ, false, 1, 1};
+	if (nonzero) {
+		// bit columns: any non-zero byte (true or nil) counts, like `if (np[i])`
+		p.mode = SEL_ANTI;
+		p.nil_matches = true;
+		p.vl = -1;
+		p.vh = 1;
+	}
 	return run_scan<int8_t>(&tmp, ci, p);
 }
 }  // namespace mgdk

@@ -436,6 +436,61 @@ int q1_opatatime(mgdk_bat *shipdate, mgdk_bat *rf, mgdk_bat *ls, mgdk_bat *qty, 
 
 extern "C" {
 
+// RANGE-window benchmark column (BASELINE config 5): n lng values ascending
+// by gaps U[0,4] (so every partition is ordered), partition bit every plen rows
+__global__ __launch_bounds__(256) void
+k_window_gaps(uint64_t seed, uint64_t n, uint64_t plen, uint8_t *gaps, int8_t *p)
+{
+	for (uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x) {
+		gaps[i] = (uint8_t) urange(rnd(seed, i, 9), 0, 4);
+		p[i] = i % plen == 0;
+	}
+}
+
+__global__ __launch_bounds__(256) void
+k_u64_to_lng(const uint64_t *in, uint64_t n, int64_t base, int64_t *out)
+{
+	for (uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x)
+		out[i] = base + (int64_t) in[i];
+}
+
+int
+mgdk_gen_window_column(uint64_t seed, uint64_t n, uint64_t plen, mgdk_bat **vals, mgdk_bat **parts)
+{
+	mgdk_bat *v = newbat(0, MGDK_lng, n), *p = newbat(0, MGDK_bit, n);
+	DevBuf gaps(n + 16), ex(n * 8 + 16);
+	if (!v || !p || !gaps.p || !ex.p) {
+		mgdk_BBPunfix(v);
+		mgdk_BBPunfix(p);
+		return -1;
+	}
+	if (n) {
+		hipLaunchKernelGGL(k_window_gaps, dim3(grid_for(n, 1024, 16384)), dim3(256), 0, stream(), seed, n,
+				   plen ? plen : n, gaps.as<uint8_t>(), (int8_t *) p->theap);
+		uint64_t tot;
+		if (exclusive_scan(gaps.as<uint8_t>(), ex.as<uint64_t>(), n, &tot) < 0) {
+			mgdk_BBPunfix(v);
+			mgdk_BBPunfix(p);
+			return -1;
+		}
+		hipLaunchKernelGGL(k_u64_to_lng, dim3(grid_for(n, 1024, 16384)), dim3(256), 0, stream(), ex.as<uint64_t>(),
+				   n, (int64_t) -1000000, (int64_t *) v->theap);
+	}
+	if (!sync()) {
+		mgdk_BBPunfix(v);
+		mgdk_BBPunfix(p);
+		return -1;
+	}
+	v->count = p->count = n;
+	v->tsorted = 1;
+	v->trevsorted = n <= 1;
+	v->tkey = 0;
+	p->tsorted = p->trevsorted = p->tkey = n <= 1;
+	*vals = v;
+	*parts = p;
+	return 0;
+}
+
 int
 mgdk_tpch_lineitem(uint64_t seed, uint64_t row0, uint64_t n, uint64_t sf_parts, mgdk_bat **cols)
 {

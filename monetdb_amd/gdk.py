@@ -112,6 +112,7 @@ _SIGS = {
     "mgdk_q1_opatatime": (C.c_int, [P, P, P, P, P, P, P, C.c_int32, C.POINTER(Q1Row), C.c_int,
                                     C.POINTER(C.c_int)]),
     "mgdk_tpch_lineitem": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, PP]),
+    "mgdk_gen_window_column": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, PP, PP]),
 }
 
 
@@ -443,6 +444,14 @@ def tpch_lineitem(seed, row0, n, sf_parts):
     arr = (P * 7)()
     _chk(lib().mgdk_tpch_lineitem(seed, row0, n, sf_parts, arr))
     return {k: BAT(arr[i]) for i, k in enumerate(LINEITEM_COLS)}
+
+
+def gen_window_column(seed, n, plen):
+    """Ascending lng column + partition bits generated in HBM (config 5)."""
+    init()
+    v, p = P(), P()
+    _chk(lib().mgdk_gen_window_column(seed, n, plen, C.byref(v), C.byref(p)))
+    return BAT(v), BAT(p)
 
 
 def sync():
