@@ -2,7 +2,7 @@
 """Benchmark: TPC-H Q6 (and Q1) column pipelines on MI355X, Grows/s + HBM roofline.
 
 One step = one pass of the fused Q6 pipeline over this GPU's lineitem shard
-(SF100 = 600,037,902 rows per GPU, columns resident in HBM): select(shipdate)
+(SF100 = 600,121,500 rows per GPU, columns resident in HBM): select(shipdate)
 -> select(discount) -> thetaselect(quantity) -> project -> price*discount (hge)
 -> sum, plus the exact combine of the per-GPU revenues.  Shards are independent
 row ranges (weak scaling); the only cross-GPU step is gathering the 16-byte
@@ -46,6 +46,7 @@ def parse():
     p.add_argument("--no-q1", action="store_true", help="skip the Q1 side measurement")
     p.add_argument("--cpu-sf", type=float, default=20.0, help="CPU baseline sample scale factor")
     p.add_argument("--cpu-threads", type=int, default=0)
+    p.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) or gloo (rehearsal)")
     return p.parse_args()
 
 
@@ -55,11 +56,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    dev = "cpu"
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        ndev = torch.cuda.device_count()
+        local = local % max(1, ndev)      # rehearsal: several ranks on one GPU (gloo)
+        if args.dist_backend == "nccl":
+            torch.cuda.set_device(local)
+            dev = "cuda:%d" % local
+        dist.init_process_group(args.dist_backend)
 
     from monetdb_amd import gdk
     gdk.init(local)
@@ -76,25 +82,18 @@ def main():
              d0, d1, 5, 7, 2400)
 
     def barrier():
-        gdk.sync()
+        gdk.sync()                       # the library's HIP stream
         if dist is not None:
-            import torch
-            torch.cuda.synchronize()
+            if dev != "cpu":
+                import torch
+                torch.cuda.synchronize()     # torch's stream (collectives)
             dist.barrier()
 
+    from monetdb_amd import dist as D
+
     def combine(rev):
-        if dist is None:
-            return rev
-        import torch
-        t = torch.tensor([rev & ((1 << 64) - 1), (rev >> 64) & ((1 << 64) - 1)],
-                         dtype=torch.uint64).view(torch.int64).cuda()
-        out = [torch.zeros_like(t) for _ in range(world)]
-        dist.all_gather(out, t)
-        tot = 0
-        for o in out:
-            w = o.cpu().view(torch.uint64).tolist()
-            tot += gdk.hge_to_int(w)
-        return tot
+        # exact 128-bit sum of the per-GPU partial revenues (all_gather of 16 B)
+        return D.combine_hge(rev, dist, dev)
 
     def step():
         return combine(gdk.q6_fused(*qargs))
@@ -109,7 +108,7 @@ def main():
     elapsed = time.perf_counter() - t
     if dist is not None:
         import torch
-        e = torch.tensor([elapsed], dtype=torch.float64).cuda()
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
 
@@ -124,21 +123,38 @@ def main():
     kern_ms = ms_total / max(1, launches)
 
     extra = {}
-    if not args.no_q1 and rank == 0:
+    if not args.no_q1:
+        # Q1 over the same shards: fused pass per GPU + exact merge of the
+        # per-GPU group partials (first-occurrence order over all rows)
         dmax = mkdate(1998, 9, 2)
         gdk.q1_fused(cols, dmax)
-        gdk.prof_reset()
-        gdk.prof_enable(True)
+        barrier()
         t = time.perf_counter()
         for _ in range(5):
-            q1 = gdk.q1_fused(cols, dmax)
-        q1_ms = (time.perf_counter() - t) / 5 * 1e3
+            q1 = D.combine_q1(gdk.q1_fused(cols, dmax), dist, dev)
+        barrier()
+        q1_s = time.perf_counter() - t
+        if dist is not None:
+            import torch
+            e = torch.tensor([q1_s], dtype=torch.float64, device=dev)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            q1_s = float(e.item())
+        q1_ms = q1_s / 5 * 1e3
+        gdk.prof_reset()
+        gdk.prof_enable(True)
+        for _ in range(3):
+            gdk.q1_fused(cols, dmax)
         q1k, q1n = gdk.prof_get("q1_fused")
         gdk.prof_enable(False)
-        extra["q1"] = {"ms_per_step": round(q1_ms, 3), "grows_per_s": round(rows / q1_ms / 1e6, 2),
+        extra["q1"] = {"ms_per_step": round(q1_ms, 3),
+                       "grows_per_s": round(rows * world / q1_ms / 1e6, 2),
                        "kernel_ms": round(q1k / max(1, q1n), 3),
-                       "hbm_gbs": round(rows * Q1_BYTES_PER_ROW / (q1k / max(1, q1n)) / 1e6, 1),
-                       "groups": len(q1)}
+                       "hbm_gbs_per_gpu": round(rows * Q1_BYTES_PER_ROW / (q1k / max(1, q1n)) / 1e6, 1),
+                       "roofline_frac": round(rows * Q1_BYTES_PER_ROW / (q1k / max(1, q1n)) / 1e6
+                                              / HBM_PEAK_GBS, 4),
+                       "groups": len(q1),
+                       "count_order": sum(r["count_order"] for r in q1)}
+    if not args.no_q1 and rank == 0:
         # the same Q6 plan operator by operator through the GDK C ABI
         r_op = gdk.q6_opatatime(*qargs)
         t = time.perf_counter()
@@ -176,7 +192,8 @@ def main():
                        "parallelism": "row-range shards x%d" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None, "kernel": "k_q6", "kernel_ms": round(kern_ms, 4),
+                         "traffic": pmc_traffic("k_q6", rows), "kernel": "k_q6",
+                         "kernel_ms": round(kern_ms, 4),
                          "bytes_per_launch": rows * Q6_BYTES_PER_ROW},
             "cpu_baseline": cpu,
             "revenue": str(revenue),
@@ -186,6 +203,19 @@ def main():
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def pmc_traffic(kernel, rows):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
+    summary (profiles/pmc_traffic.json, made by tools/pmc_summary.py from
+    separate --pmc FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled for
+    gfx950's half-counted wide streaming reads), scaled to this row count."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))[kernel]
+        return int(round(d["hbm_bytes_per_row"] * rows))
+    except Exception:  # noqa: BLE001
+        return None
 
 
 def cpu_baseline(args):

@@ -1,0 +1,47 @@
+"""Summarise rocprofv3 PMC passes into profiles/pmc_traffic.json.
+
+    python tools/pmc_summary.py FETCH_CSV WRITE_CSV ROWS_PER_LAUNCH [KERNEL ...]
+
+FETCH_SIZE / WRITE_SIZE are KiB per dispatch.  On gfx950 FETCH_SIZE counts
+exactly half of the bytes of a wide (16 B/lane) coalesced streaming read
+(MI355X_MICROARCH.md, HBM section), so it is doubled here; WRITE_SIZE is
+exact for 16-B stores and atomics.
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+
+def per_kernel(path, counter):
+    acc = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter:
+            acc[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main():
+    fetch, write, rows = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    kernels = sys.argv[4:] or None
+    f = per_kernel(fetch, "FETCH_SIZE")
+    w = per_kernel(write, "WRITE_SIZE")
+    out_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "profiles", "pmc_traffic.json")
+    out = json.load(open(out_path)) if os.path.exists(out_path) else {}
+    for k in f:
+        if kernels and k not in kernels:
+            continue
+        fb = f[k] * 1024 * 2
+        wb = w.get(k, 0.0) * 1024
+        out[k] = {"fetch_size_kib": round(f[k], 1), "write_size_kib": round(w.get(k, 0.0), 1),
+                  "hbm_bytes_per_launch": int(fb + wb), "rows_per_launch": rows,
+                  "hbm_bytes_per_row": (fb + wb) / rows,
+                  "source": [os.path.relpath(fetch), os.path.relpath(write)]}
+    json.dump(out, open(out_path, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
