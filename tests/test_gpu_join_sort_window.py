@@ -50,6 +50,44 @@ def test_join_candidates_and_orders(gdk, ora):
     assert np.array_equal(b.to_numpy(), ob.values())
 
 
+@pytest.mark.parametrize("tname,dt", [("int", np.int32), ("lng", np.int64)])
+def test_join_heavy_duplicates_fallback(gdk, ora, tname, dt):
+    # one key repeated 1500 times on the build side exceeds the open-addressing
+    # displacement bound -> CSR fallback; must give the same order
+    r = rng(83)
+    tp = getattr(gdk, "TYPE_" + tname)
+    rv = np.concatenate([np.full(1500, 7), r.integers(0, 3000, 5000)]).astype(dt)
+    r.shuffle(rv)
+    lv = r.integers(0, 3000, 20_000).astype(dt)
+    lv[::50] = 7
+    a, b = gdk.BATjoin(mk(gdk, tp, lv), mk(gdk, tp, rv, hseqbase=5))
+    oa, ob = ora.BATjoin(omk(ora, tp, lv), omk(ora, tp, rv, hseqbase=5))
+    assert np.array_equal(a.to_numpy(), oa.values())
+    assert np.array_equal(b.to_numpy(), ob.values())
+
+
+@pytest.mark.parametrize("tname,dt", [("int", np.int32), ("oid", np.uint64), ("bte", np.int8)])
+def test_join_unique_build(gdk, ora, tname, dt):
+    # FK -> PK shape: every probe row has at most one match (single-pass path)
+    r = rng(84)
+    tp = getattr(gdk, "TYPE_" + tname)
+    hi = 120 if tname == "bte" else 1 << 30
+    rv = r.choice(np.arange(0, hi), min(100_000, hi), replace=False).astype(dt)
+    lv = r.choice(np.arange(0, hi), 300_000).astype(dt)
+    a, b = gdk.BATjoin(mk(gdk, tp, lv, hseqbase=3), mk(gdk, tp, rv))
+    oa, ob = ora.BATjoin(omk(ora, tp, lv, hseqbase=3), omk(ora, tp, rv))
+    assert np.array_equal(a.to_numpy(), oa.values())
+    assert np.array_equal(b.to_numpy(), ob.values())
+
+
+def test_join_empty_sides(gdk):
+    e = mk(gdk, gdk.TYPE_int, np.zeros(0, np.int32))
+    x = mk(gdk, gdk.TYPE_int, np.arange(10, dtype=np.int32))
+    for l, rr in ((e, x), (x, e), (e, e)):
+        a, b = gdk.BATjoin(l, rr)
+        assert a.count() == 0 and b.count() == 0
+
+
 def test_join_duplicates_descending(gdk):
     l = np.array([1, 2, 1], np.int32)
     r = np.array([1, 1, 3, 1], np.int32)
