@@ -7,45 +7,21 @@
 // (FOLLOWING) while |b[k] - b[j]| <= limit, stopping at nils and at the
 // partition start/end: O(n * window).  Inside a partition ordered by the
 // window's ORDER BY (nils first ascending, last descending) that walk stops
-// exactly where a monotone predicate flips, so the device finds the same
-// row by galloping + binary search, and re-derives the only subtraction that
-// could have overflowed (the first violating pair) to raise the reference's
-// "22003!overflow in calculation." where it would.  A check kernel verifies
-// that order; when it does not hold, a per-row linear-walk kernel restates
-// the reference loop, so results always match.
-//
-// Ordered path (k_range_tile): a workgroup owns 2048 rows; it stages them
-// plus a 2048-row halo (before for PRECEDING, after for FOLLOWING) in LDS
-// with coalesced loads, and the (<= 128) partitions that overlap the staged
-// rows with their nil-run boundaries; every row then searches in LDS (global
-// memory only when a frame reaches past the halo) and its bound is stored
-// coalesced.  Partitions: the bit column p (row 0 always starts one).
+// exactly where a monotone predicate flips, and the row it stops at is
+// non-decreasing in k; the device therefore advances one pointer per lane
+// over consecutive rows (k_range_fast), and re-derives the only subtraction
+// that could have overflowed (the first violating pair) to raise the
+// reference's "22003!overflow in calculation." where it would.  The same
+// pass verifies the order; when neither ascending nor descending order holds
+// a per-row linear-walk kernel restates the reference loop, so results always
+// match.  Rows whose frame leaves the fast kernel's staged window are fixed
+// up by a global gallop + binary search (k_range_fix / k_range_tile) over the
+// partition starts S (compaction of p) and nil boundaries Z.
 #include "mgdk_internal.h"
 
 using namespace mgdk;
 
 namespace {
-
-// bit 0: violates ascending-nils-first, bit 1: violates descending-nils-last
-__global__ __launch_bounds__(256) void
-k_order_check(const int64_t *b, const int8_t *p, BUN n, uint32_t *flags)
-{
-	uint32_t v = 0;
-	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n; i += (BUN) gridDim.x * blockDim.x) {
-		if (p && p[i + 1] != 0)
-			continue;   // next row starts a new partition
-		const int64_t x = b[i], y = b[i + 1];
-		const bool xn = x == INT64_MIN, yn = y == INT64_MIN;
-		if (!xn && yn) v |= 1;
-		else if (!xn && !yn && x > y) v |= 1;
-		if (xn && !yn) v |= 2;
-		else if (!xn && !yn && x < y) v |= 2;
-	}
-	for (int o = 32; o > 0; o >>= 1)
-		v |= __shfl_xor(v, o);
-	if (__lane_id() == 0 && v)
-		atomicOr(flags, v);
-}
 
 struct WArgs {
 	const int64_t *b;
@@ -250,6 +226,538 @@ k_range_tile(WArgs a)
 		atomicOr(a.err, 1u);
 }
 
+// ---------------------------------------------------------------------------
+// Fast ordered path (k_range_fast).  Inside an ordered partition the bound of
+// row k is monotone non-decreasing in k (also across nil runs and partition
+// starts), so the bounds of a tile are a MERGE of the tile's rows with the
+// staged rows: staged row j precedes row k in the merge iff j lies before
+// k's bound.  Each lane walks a fixed number of merge steps from its own
+// diagonal (found by a binary search), so no lane waits on another's data
+// dependent loop: ~2 steps per row.  A workgroup owns FT rows and stages
+// them plus an FH-row halo (before for PRECEDING, after for FOLLOWING) and
+// the partition bits; partition membership inside the stage comes from a
+// block max-scan of partition starts, skipped when the stage holds none.
+// The same pass checks the order (both directions) so no separate check
+// kernel runs; rows whose frame reaches past the halo are listed for a
+// fix-up pass with the general machinery (S, Z, global search).  Reads b
+// once (+ halo), p once, writes the bound once (coalesced).
+// ---------------------------------------------------------------------------
+
+#ifndef MGDK_WIN_FR
+#define MGDK_WIN_FR 8
+#endif
+#ifndef MGDK_WIN_FH
+#define MGDK_WIN_FH 256
+#endif
+constexpr int FR = MGDK_WIN_FR;          // rows per lane
+constexpr int FT = 256 * FR;             // rows per tile
+constexpr int FH = MGDK_WIN_FH;          // halo rows
+constexpr int FS = FT + FH + 1;          // staged rows at most
+
+__device__ __forceinline__ int
+pidx(int i)
+{
+	return i;
+}
+
+struct FArgs {
+	const int64_t *b;
+	const int8_t *p;     // partition bits or NULL
+	bool p4;             // p is 4-byte aligned
+	BUN n;
+	int64_t limit;
+	bool preceding;
+	bool desc;
+	bool peers;
+	bool all;
+	oid *out;
+	uint32_t *flags;     // [0] overflow, [1] order violations (bit0 asc, bit1 desc), [2] unresolved rows,
+	                     // [3] a tile needs the wide kernel
+	oid *unres;          // unresolved row list
+	uint32_t unres_cap;
+};
+
+__global__ __launch_bounds__(256) void
+k_range_fast(FArgs a)
+{
+	__shared__ int64_t sv[FS];
+	__shared__ int16_t spst[FS];         // last partition start (stage index) <= i, -1: before the stage
+	__shared__ __attribute__((aligned(16))) uint8_t sp[FS + 4];   // partition start flags of the stage
+	__shared__ uint16_t sbd[FT];         // bound of every tile row (stage index)
+	__shared__ int32_t s_wmax[4];
+	__shared__ int s_hasb;
+	__shared__ uint32_t s_ord;
+	const int tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+	const BUN t0 = (BUN) blockIdx.x * FT;
+	const BUN t1 = t0 + FT < a.n ? t0 + FT : a.n;
+	const BUN lo = a.preceding ? (t0 > FH ? t0 - FH : 0) : t0;
+	const BUN hi = a.preceding ? (t1 + 1 < a.n ? t1 + 1 : a.n) : (t1 + FH < a.n ? t1 + FH : a.n);
+	const int S = (int) (hi - lo);
+	if (tid == 0) {
+		s_hasb = 0;
+		s_ord = 0;
+	}
+	{
+		// all loads of the stage in flight at once
+		constexpr int NB = (FS + 255) / 256;
+		int64_t tv[NB];
+#pragma unroll
+		for (int u = 0; u < NB; u++) {
+			const int i = tid + u * 256;
+			tv[u] = i < S ? a.b[lo + i] : 0;
+		}
+		constexpr int NW = (FS + 3 + 1023) / 1024;
+		uint32_t tw[NW];
+#pragma unroll
+		for (int u = 0; u < NW; u++) {
+			const int q = tid + u * 256;      // word q covers stage rows 4q .. 4q+3
+			tw[u] = 0;
+			if (a.p && 4 * q < S) {
+				if (a.p4 && lo + 4 * q + 3 < a.n) {
+					tw[u] = *(const uint32_t *) (a.p + lo + 4 * q);
+				} else {
+					for (int e = 0; e < 4 && lo + 4 * q + e < a.n; e++)
+						tw[u] |= (uint32_t) (uint8_t) a.p[lo + 4 * q + e] << (8 * e);
+				}
+			}
+		}
+#pragma unroll
+		for (int u = 0; u < NB; u++) {
+			const int i = tid + u * 256;
+			if (i < S)
+				sv[pidx(i)] = tv[u];
+		}
+		bool any = lo == 0;
+#pragma unroll
+		for (int u = 0; u < NW; u++) {
+			const int q = tid + u * 256;
+			if (4 * q < S) {
+				*(uint32_t *) &sp[4 * q] = tw[u];
+				any |= tw[u] != 0;
+			}
+		}
+		if (lo == 0 && tid == 0)
+			sp[0] = 1;                    // row 0 always starts a partition
+		__syncthreads();
+		if (__any(any) && lane == 0)
+			s_hasb = 1;
+		__syncthreads();
+	}
+	const bool hasb = s_hasb != 0;
+	if (hasb) {
+		// block max-scan of partition starts over per-thread chunks
+		const int C = (S + 255) / 256;
+		const int c0 = tid * C, c1 = c0 + C < S ? c0 + C : S;
+		int32_t m = -1;
+		for (int i = c0; i < c1; i++)
+			if (sp[i])
+				m = i;
+		int32_t incl = m;
+#pragma unroll
+		for (int o = 1; o < 64; o <<= 1) {
+			int32_t u = __shfl_up(incl, o);
+			if (lane >= o)
+				incl = u > incl ? u : incl;
+		}
+		if (lane == 63)
+			s_wmax[w] = incl;
+		__syncthreads();
+		int32_t ex = __shfl_up(incl, 1);
+		if (lane == 0)
+			ex = -1;
+		for (int q = 0; q < w; q++)
+			ex = s_wmax[q] > ex ? s_wmax[q] : ex;
+		m = ex;
+		for (int i = c0; i < c1; i++) {
+			if (sp[i])
+				m = i;
+			spst[i] = (int16_t) m;
+		}
+		__syncthreads();
+	}
+
+	const uint64_t lim = (uint64_t) a.limit;
+	const bool all = a.all, prec = a.preceding;
+	const int NA = (int) (t1 - t0), NB = S, xa = (int) (t0 - lo);
+	// ok: staged row j belongs to the frame of the row at stage index xk
+	auto ok = [&](int xk, int64_t vk, int j, int64_t vj) -> bool {
+		if (hasb && spst[xk] != spst[j])
+			return false;
+		if (all)
+			return true;
+		const bool vkn = vk == INT64_MIN, vjn = vj == INT64_MIN;
+		return vkn ? vjn : (!vjn && absdiff(vk, vj) <= lim);
+	};
+	// P(k, j): staged row j lies before the bound of tile row k.  Monotone:
+	// true then false in j, and the bound (#j with P) is non-decreasing in k
+	// inside ordered partitions -- a merge of the rows with the stage.
+	auto P = [&](int k, int j) -> bool {
+		if (j >= NB)
+			return false;
+		const int xk = xa + k;
+		if (prec) {
+			if (j >= xk)
+				return false;
+			return !ok(xk, sv[pidx(xk)], j, sv[pidx(j)]);
+		}
+		if (j <= xk)
+			return true;
+		return ok(xk, sv[pidx(xk)], j, sv[pidx(j)]);
+	};
+	{
+		// merge path: every lane walks L steps of the (rows x stage) merge
+		// from its diagonal; each step emits one bound or passes one row
+		const int T = NA + NB;
+		const int L = (T + 255) / 256;
+		const int d0 = tid * L < T ? tid * L : T;
+		int klo = d0 - NB > 0 ? d0 - NB : 0, khi = d0 < NA ? d0 : NA;
+		while (klo < khi) {
+			const int mid = (klo + khi + 1) >> 1;
+			if (!P(mid - 1, d0 - mid))
+				klo = mid;
+			else
+				khi = mid - 1;
+		}
+		int k = klo, j = d0 - klo;
+		for (int st = 0; st < L && k + j < T; st++) {
+			const bool pb = k >= NA || P(k, j);
+			if (!pb)
+				sbd[k] = (uint16_t) j;
+			k += pb ? 0 : 1;
+			j += pb ? 1 : 0;
+		}
+	}
+	__syncthreads();
+	// per row: unresolved frames, the overflow pair, the order of (k, k+1),
+	// coalesced result stores
+	uint32_t ovf = 0, ord = 0;
+	for (int i = tid; i < NA; i += 256) {
+		const int xk = xa + i;
+		const BUN k = t0 + (BUN) i;
+		const int bnd = sbd[i];
+		const int64_t vk = sv[pidx(xk)];
+		const bool vkn = vk == INT64_MIN;
+		if (k + 1 < a.n && !(hasb && spst[xk + 1] == xk + 1)) {
+			const int64_t y = sv[pidx(xk + 1)];
+			const bool yn = y == INT64_MIN;
+			if ((!vkn && yn) || (!vkn && !yn && vk > y))
+				ord |= 1;
+			if ((vkn && !yn) || (!vkn && !yn && vk < y))
+				ord |= 2;
+		}
+		const bool unres = prec ? (bnd == 0 && lo > 0) : (bnd == NB && hi < a.n);
+		if (unres) {
+			const uint32_t at = atomicAdd(&a.flags[2], 1u);
+			if (at < a.unres_cap)
+				a.unres[at] = k;
+		} else if (!all && !a.peers && !vkn) {
+			// the pair the reference subtracts last (first row outside the frame)
+			const int e = prec ? bnd - 1 : bnd;
+			if (e >= 0 && e < NB && !(hasb && spst[e] != spst[xk])) {
+				const int64_t vb = sv[pidx(e)];
+				if (vb != INT64_MIN && sub_ovf(vk, vb))
+					ovf = 1;
+			}
+		}
+		a.out[k] = lo + (BUN) bnd;
+	}
+	if (ovf)
+		atomicOr(&a.flags[0], 1u);
+	if (!all) {
+		// one flag update per workgroup, and only for bits not yet published:
+		// every tile of ascending data violates "descending", and a same-word
+		// atomic per wave would serialise the whole grid
+#pragma unroll
+		for (int o = 32; o > 0; o >>= 1)
+			ord |= __shfl_xor(ord, o);
+		if (lane == 0 && ord)
+			atomicOr(&s_ord, ord);
+		__syncthreads();
+		if (tid == 0 && s_ord) {
+			const uint32_t seen = __hip_atomic_load(&a.flags[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			if (s_ord & ~seen)
+				atomicOr(&a.flags[1], s_ord);
+		}
+	}
+}
+
+// ---------------------------------------------------------------------------
+// Narrow-key variant (k_range_keys), the common case.  When the non-nil
+// values staged by a tile span less than 2^32, every staged row becomes one
+// 64-bit key that is non-decreasing along ordered data:
+//     key = partition label (stage-relative) << 33 | flag << 32 | rel
+// with flag = "not nil" for ascending partitions (nils first) and "nil" for
+// descending ones (nils last), rel = v - min (ascending) or max - v
+// (descending), 0 for nils.  The frame edge of row k is then a key threshold
+// (partition start / nil run / rel -+ limit, clamped), so one merge step is a
+// single 64-bit compare, and no subtraction inside such a tile can overflow
+// (|v_k - v_j| < 2^32), so no overflow check is needed.  A tile whose values
+// span more sets flags[3]; the host then runs the wide kernel above.
+// ---------------------------------------------------------------------------
+
+constexpr uint64_t KMAXREL = 0xffffffffull;
+
+template <bool PREC, bool DESC, bool ALL>
+__global__ __launch_bounds__(256) void
+k_range_keys(FArgs a)
+{
+	__shared__ uint64_t sk[FS];
+	__shared__ __attribute__((aligned(16))) uint8_t spu[(FS + 4 > 2 * FT ? FS + 4 : 2 * FT)];  // partition flags, then bounds
+	__shared__ int64_t s_min[4], s_max[4];
+	__shared__ int s_hasb;
+	__shared__ uint32_t s_ord;
+	uint8_t *sp = spu;
+	uint16_t *sbd = (uint16_t *) spu;
+	const int tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+	const BUN t0 = (BUN) blockIdx.x * FT;
+	const BUN t1 = t0 + FT < a.n ? t0 + FT : a.n;
+	const BUN lo = PREC ? (t0 > FH ? t0 - FH : 0) : t0;
+	const BUN hi = PREC ? (t1 + 1 < a.n ? t1 + 1 : a.n) : (t1 + FH < a.n ? t1 + FH : a.n);
+	const int S = (int) (hi - lo);
+	if (tid == 0) {
+		s_hasb = 0;
+		s_ord = 0;
+	}
+	constexpr int NB = (FS + 255) / 256;
+	int64_t tv[NB];
+	int64_t vmin = INT64_MAX, vmax = INT64_MIN;
+	{
+#pragma unroll
+		for (int u = 0; u < NB; u++) {
+			const int i = tid + u * 256;
+			tv[u] = i < S ? a.b[lo + i] : INT64_MIN;
+		}
+		constexpr int NW = (FS + 3 + 1023) / 1024;
+		uint32_t tw[NW];
+#pragma unroll
+		for (int u = 0; u < NW; u++) {
+			const int q = tid + u * 256;
+			tw[u] = 0;
+			if (a.p && 4 * q < S) {
+				if (a.p4 && lo + 4 * q + 3 < a.n) {
+					tw[u] = *(const uint32_t *) (a.p + lo + 4 * q);
+				} else {
+					for (int e = 0; e < 4 && lo + 4 * q + e < a.n; e++)
+						tw[u] |= (uint32_t) (uint8_t) a.p[lo + 4 * q + e] << (8 * e);
+				}
+			}
+		}
+		bool any = lo == 0;
+#pragma unroll
+		for (int u = 0; u < NW; u++) {
+			const int q = tid + u * 256;
+			if (4 * q < S) {
+				*(uint32_t *) &sp[4 * q] = tw[u];
+				any |= tw[u] != 0;
+			}
+		}
+		if (lo == 0 && tid == 0)
+			sp[0] = 1;
+		if (!ALL) {
+#pragma unroll
+			for (int u = 0; u < NB; u++) {
+				if (tv[u] != INT64_MIN) {
+					vmin = tv[u] < vmin ? tv[u] : vmin;
+					vmax = tv[u] > vmax ? tv[u] : vmax;
+				}
+			}
+#pragma unroll
+			for (int o = 32; o > 0; o >>= 1) {
+				const int64_t x = __shfl_xor(vmin, o), y = __shfl_xor(vmax, o);
+				vmin = x < vmin ? x : vmin;
+				vmax = y > vmax ? y : vmax;
+			}
+			if (lane == 0) {
+				s_min[w] = vmin;
+				s_max[w] = vmax;
+			}
+		}
+		__syncthreads();
+		if (__any(any) && lane == 0)
+			s_hasb = 1;
+		__syncthreads();
+	}
+	const bool hasb = s_hasb != 0;
+	uint64_t base = 0;
+	if (!ALL) {
+		vmin = s_min[0];
+		vmax = s_max[0];
+		for (int q = 1; q < 4; q++) {
+			vmin = s_min[q] < vmin ? s_min[q] : vmin;
+			vmax = s_max[q] > vmax ? s_max[q] : vmax;
+		}
+		if (vmin <= vmax && (uint64_t) vmax - (uint64_t) vmin > KMAXREL) {
+			if (tid == 0)
+				atomicOr(&a.flags[3], 1u);          // wide tile: the host reruns k_range_fast
+			return;
+		}
+		base = DESC ? (uint64_t) vmax : (uint64_t) vmin;
+	}
+	auto mkkey = [&](uint64_t label, int64_t v) -> uint64_t {
+		if (ALL)
+			return label << 33;
+		const bool isnil = v == INT64_MIN;
+		const uint64_t flag = DESC ? (isnil ? 1 : 0) : (isnil ? 0 : 1);
+		const uint64_t rel = isnil ? 0 : (DESC ? base - (uint64_t) v : (uint64_t) v - base);
+		return (label << 33) | (flag << 32) | rel;
+	};
+	if (!hasb) {
+#pragma unroll
+		for (int u = 0; u < NB; u++) {
+			const int i = tid + u * 256;
+			if (i < S)
+				sk[i] = mkkey(0, tv[u]);
+		}
+		__syncthreads();
+	} else {
+#pragma unroll
+		for (int u = 0; u < NB; u++) {
+			const int i = tid + u * 256;
+			if (i < S)
+				sk[i] = (uint64_t) tv[u];
+		}
+		__syncthreads();
+		// partition labels: block max-scan of partition starts (per-thread chunks)
+		const int C = (S + 255) / 256;
+		const int c0 = tid * C, c1 = c0 + C < S ? c0 + C : S;
+		int32_t m = -1;
+		for (int i = c0; i < c1; i++)
+			if (sp[i])
+				m = i;
+		int32_t incl = m;
+#pragma unroll
+		for (int o = 1; o < 64; o <<= 1) {
+			int32_t u = __shfl_up(incl, o);
+			if (lane >= o)
+				incl = u > incl ? u : incl;
+		}
+		__shared__ int32_t s_wmax[4];
+		if (lane == 63)
+			s_wmax[w] = incl;
+		__syncthreads();
+		int32_t ex = __shfl_up(incl, 1);
+		if (lane == 0)
+			ex = -1;
+		for (int q = 0; q < w; q++)
+			ex = s_wmax[q] > ex ? s_wmax[q] : ex;
+		m = ex;
+		for (int i = c0; i < c1; i++) {
+			if (sp[i])
+				m = i;
+			sk[i] = mkkey((uint64_t) (m + 1), (int64_t) sk[i]);
+		}
+		__syncthreads();
+	}
+
+	const uint64_t lim32 = ALL ? 0 : ((uint64_t) a.limit < KMAXREL ? (uint64_t) a.limit : KMAXREL);
+	// frame threshold of the row with key kk
+	auto thr = [&](uint64_t kk) -> uint64_t {
+		const uint64_t lab = kk >> 33 << 33;
+		if (ALL)
+			return PREC ? lab : lab | ((1ull << 33) - 1);
+		const uint64_t flag = (kk >> 32) & 1, rel = kk & KMAXREL;
+		const bool valrow = DESC ? flag == 0 : flag == 1;
+		const uint64_t hd = lab | (flag << 32);
+		if (PREC)
+			return valrow ? hd | (rel > lim32 ? rel - lim32 : 0) : hd;
+		return valrow ? hd | (KMAXREL - rel > lim32 ? rel + lim32 : KMAXREL) : hd | KMAXREL;
+	};
+	const int NA = (int) (t1 - t0), NB2 = S, xa = (int) (t0 - lo);
+	// P(k, j): staged row j lies before the bound of tile row k
+	auto P = [&](int k, int j) -> bool {
+		if (j >= NB2)
+			return false;
+		const uint64_t t = thr(sk[xa + k]), kj = sk[j];
+		return PREC ? kj < t : kj <= t;
+	};
+	{
+		const int T = NA + NB2;
+		const int L = (T + 255) / 256;
+		const int d0 = tid * L < T ? tid * L : T;
+		int klo = d0 - NB2 > 0 ? d0 - NB2 : 0, khi = d0 < NA ? d0 : NA;
+		while (klo < khi) {
+			const int mid = (klo + khi + 1) >> 1;
+			if (!P(mid - 1, d0 - mid))
+				klo = mid;
+			else
+				khi = mid - 1;
+		}
+		int k = klo, j = d0 - klo;
+		uint64_t t = k < NA ? thr(sk[xa + k]) : 0;
+		for (int st = 0; st < L && k + j < T; st++) {
+			bool pb = true;
+			if (k < NA && j < NB2) {
+				const uint64_t kj = sk[j];
+				pb = PREC ? kj < t : kj <= t;
+			} else if (k < NA) {
+				pb = false;
+			}
+			if (!pb) {
+				sbd[k] = (uint16_t) j;
+				k++;
+				if (k < NA)
+					t = thr(sk[xa + k]);
+			} else {
+				j++;
+			}
+		}
+	}
+	__syncthreads();
+	uint32_t ord = 0;
+	for (int i = tid; i < NA; i += 256) {
+		const int xk = xa + i;
+		const BUN k = t0 + (BUN) i;
+		const int bnd = sbd[i];
+		if (!ALL && k + 1 < a.n) {
+			const uint64_t x = sk[xk], y = sk[xk + 1];
+			if ((x >> 33) == (y >> 33)) {        // same partition
+				if (y < x)
+					ord |= DESC ? 2u : 1u;
+				if (!DESC) {
+					const uint64_t fx = (x >> 32) & 1, fy = (y >> 32) & 1;
+					if ((fx == 0 && fy == 1) || (fx == 1 && fy == 1 && (y & KMAXREL) > (x & KMAXREL)))
+						ord |= 2u;
+				}
+			}
+		}
+		const bool unres = PREC ? (bnd == 0 && lo > 0) : (bnd == NB2 && hi < a.n);
+		if (unres) {
+			const uint32_t at = atomicAdd(&a.flags[2], 1u);
+			if (at < a.unres_cap)
+				a.unres[at] = k;
+		}
+		a.out[k] = lo + (BUN) bnd;
+	}
+	if (!ALL) {
+#pragma unroll
+		for (int o = 32; o > 0; o >>= 1)
+			ord |= __shfl_xor(ord, o);
+		if (lane == 0 && ord)
+			atomicOr(&s_ord, ord);
+		__syncthreads();
+		if (tid == 0 && s_ord) {
+			const uint32_t seen = __hip_atomic_load(&a.flags[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			if (s_ord & ~seen)
+				atomicOr(&a.flags[1], s_ord);
+		}
+	}
+}
+
+// fix-up of the rows k_range_fast could not resolve inside its stage
+__global__ __launch_bounds__(256) void
+k_range_fix(WArgs a, const oid *rows, uint32_t nrows)
+{
+	uint32_t ovf = 0;
+	Stage V{nullptr, 0, 0, a.b};
+	for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nrows; t += gridDim.x * blockDim.x) {
+		const BUN k = rows[t];
+		const BUN pi = partition_of(a, k);
+		a.out[k] = sorted_bound(a, V, k, pstart(a, pi), pend(a, pi), a.Z[pi], ovf);
+	}
+	if (ovf)
+		atomicOr(a.err, 1u);
+}
+
 // exact restatement of the reference walk for partitions that are not
 // ordered (or mixed); O(window) per row
 __global__ __launch_bounds__(256) void
@@ -304,6 +812,48 @@ k_first_oid(const oid *S, oid *out)
 
 }  // namespace
 
+// S (partition starts as an oid BAT), lead and m of the general machinery
+static int
+general_setup(WArgs &a, const mgdk_bat *p, BUN n, mgdk_bat **Sp)
+{
+	hipStream_t st = stream();
+	mgdk_bat *S = nullptr;
+	if (p) {
+		S = compact_flags((const int8_t *) p->theap, n, 0, true);
+		if (S == nullptr)
+			return -1;
+	}
+	if (S) {
+		a.S = S->ttype == MGDK_void ? nullptr : (const oid *) S->theap;
+		a.Sseq = S->tseqbase;
+		a.ns = S->count;
+	} else {
+		a.S = nullptr;
+		a.Sseq = 0;
+		a.ns = 0;
+	}
+	// does row 0 start a partition that S does not list?
+	bool first0 = false;
+	if (a.ns > 0) {
+		if (a.S == nullptr) {
+			first0 = a.Sseq == 0;
+		} else {
+			oid *d = (oid *) meta_buf();
+			hipLaunchKernelGGL(k_first_oid, dim3(1), dim3(1), 0, st, a.S, d);
+			oid *h = (oid *) pinned(8);
+			if (!hip_ok(hipMemcpyAsync(h, d, 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
+				mgdk_BBPunfix(S);
+				return -1;
+			}
+			first0 = *h == 0;
+		}
+	}
+	a.lead = !first0;
+	a.m = a.ns + (a.lead ? 1 : 0);
+	*Sp = S;
+	return 0;
+}
+
 extern "C" int
 mgdk_GDKanalyticalwindowbounds(mgdk_bat *r, mgdk_bat *b, mgdk_bat *p, mgdk_bat *l, const void *bound,
 			       int tp1, int tp2, int unit, bool preceding, mgdk_oid first_half)
@@ -356,82 +906,103 @@ mgdk_GDKanalyticalwindowbounds(mgdk_bat *r, mgdk_bat *b, mgdk_bat *p, mgdk_bat *
 		r->count = 0;
 		return 0;
 	}
-	// partition starts: the rows with p == 1 (ordered compaction), plus row 0
-	mgdk_bat *S = nullptr;
-	if (p) {
-		S = compact_flags((const int8_t *) p->theap, n, 0, true);
-		if (S == nullptr)
-			return -1;
-	}
-	DevBuf err(16);
-	if (!err.p || !hip_ok(hipMemsetAsync(err.p, 0, 16, st), "memset")) {
-		mgdk_BBPunfix(S);
-		return -1;
-	}
-	WArgs a{};
-	a.b = (const int64_t *) b->theap;
-	a.n = n;
-	if (S) {
-		a.S = S->ttype == MGDK_void ? nullptr : (const oid *) S->theap;
-		a.Sseq = S->tseqbase;
-		a.ns = S->count;
-	} else {
-		a.S = nullptr;
-		a.Sseq = 0;
-		a.ns = 0;
-	}
-	// does row 0 start a partition that S does not list?
-	bool first0 = false;
-	if (a.ns > 0) {
-		if (a.S == nullptr) {
-			first0 = a.Sseq == 0;
-		} else {
-			oid *d = (oid *) meta_buf();
-			hipLaunchKernelGGL(k_first_oid, dim3(1), dim3(1), 0, st, a.S, d);
-			oid *h = (oid *) pinned(8);
-			if (!hip_ok(hipMemcpyAsync(h, d, 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
-				mgdk_BBPunfix(S);
-				return -1;
-			}
-			first0 = *h == 0;
-		}
-	}
-	a.lead = !first0;
-	a.m = a.ns + (a.lead ? 1 : 0);
-	a.limit = limit;
-	a.preceding = preceding;
-	a.peers = limit == 0;
-	a.all = all;
-	a.out = (oid *) r->theap;
-	a.err = err.as<uint32_t>();
-	hipLaunchKernelGGL(k_order_check, dim3(grid_for(n, 2048, 4096)), dim3(256), 0, st, a.b,
-			   p ? (const int8_t *) p->theap : nullptr, n, err.as<uint32_t>() + 1);
-	uint32_t *h = (uint32_t *) pinned(16);
-	if (!hip_ok(hipMemcpyAsync(h, err.p, 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
-		mgdk_BBPunfix(S);
-		return -1;
-	}
-	const uint32_t order = h[1];
-	DevBuf Z((a.m + 1) * 8);
-	if (!Z.p) {
-		mgdk_BBPunfix(S);
-		return -1;
-	}
 	const dim3 blk(256);
-	if (all || !(order & 1) || !(order & 2)) {
-		a.desc = (order & 1) != 0;
-		a.Z = Z.as<oid>();
-		hipLaunchKernelGGL(k_part_nilbound, dim3(grid_for(a.m, 256, 8192)), blk, 0, st, a, Z.as<oid>());
-		hipLaunchKernelGGL(k_range_tile, dim3((unsigned) ((n + TT - 1) / TT)), blk, 0, st, a);
-	} else {
-		hipLaunchKernelGGL(k_range_walk, dim3(grid_for(n, 256 * 4, 256 * 64)), blk, 0, st, a);
-	}
-	if (!hip_ok(hipMemcpyAsync(h, err.p, 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
-		mgdk_BBPunfix(S);
+	// 1. fast ordered pass, ascending first (the SQL default), descending if
+	//    only that order holds
+	const uint32_t ucap = (uint32_t) (n / 32 > 65536 ? (n / 32 < (1u << 30) ? n / 32 : (1u << 30)) : 65536);
+	DevBuf fl(64), ul((size_t) ucap * 8);
+	uint32_t *h = (uint32_t *) pinned(64);
+	if (!fl.p || !ul.p || !h)
 		return -1;
+	FArgs f{};
+	f.b = (const int64_t *) b->theap;
+	f.p = p ? (const int8_t *) p->theap : nullptr;
+	f.p4 = ((uintptr_t) f.p & 3) == 0;
+	f.n = n;
+	f.limit = limit;
+	f.preceding = preceding;
+	f.peers = limit == 0;
+	f.all = all;
+	f.out = (oid *) r->theap;
+	f.flags = fl.as<uint32_t>();
+	f.unres = ul.as<oid>();
+	f.unres_cap = ucap;
+	const unsigned ftiles = (unsigned) ((n + FT - 1) / FT);
+	bool ordered = false;
+	for (int pass = 0; pass < 2; pass++) {
+		f.desc = pass == 1;
+		if (!hip_ok(hipMemsetAsync(fl.p, 0, 64, st), "memset"))
+			return -1;
+#define RK(P_, D_, A_) hipLaunchKernelGGL((k_range_keys<P_, D_, A_>), dim3(ftiles), blk, 0, st, f)
+		if (preceding) {
+			if (all) RK(true, false, true);
+			else if (f.desc) RK(true, true, false);
+			else RK(true, false, false);
+		} else {
+			if (all) RK(false, false, true);
+			else if (f.desc) RK(false, true, false);
+			else RK(false, false, false);
+		}
+#undef RK
+		if (!hip_ok(hipMemcpyAsync(h, fl.p, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+			return -1;
+		if (h[3]) {
+			// some tile spans >= 2^32: the wide kernel (with overflow checks)
+			if (!hip_ok(hipMemsetAsync(fl.p, 0, 64, st), "memset"))
+				return -1;
+			hipLaunchKernelGGL(k_range_fast, dim3(ftiles), blk, 0, st, f);
+			if (!hip_ok(hipMemcpyAsync(h, fl.p, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+				return -1;
+		}
+		const uint32_t viol = h[1];
+		if (all || !(viol & (f.desc ? 2u : 1u))) {
+			ordered = true;
+			break;
+		}
+		if (viol & 2u)
+			break;          // neither order holds
 	}
-	mgdk_BBPunfix(S);
-	if (h[0] & 1) {
+	uint32_t ovf = ordered ? (h[0] & 1) : 0;
+	const uint32_t nunres = ordered ? h[2] : 0;
+	if (!ordered || nunres > 0) {
+		// 2. general machinery: partition starts S, nil boundaries Z
+		WArgs a{};
+		a.b = (const int64_t *) b->theap;
+		a.n = n;
+		a.limit = limit;
+		a.preceding = preceding;
+		a.peers = limit == 0;
+		a.all = all;
+		a.desc = f.desc;
+		a.out = (oid *) r->theap;
+		a.err = fl.as<uint32_t>() + 4;
+		mgdk_bat *S = nullptr;
+		if (general_setup(a, p, n, &S) < 0)
+			return -1;
+		DevBuf Z((a.m + 1) * 8);
+		if (!Z.p || !hip_ok(hipMemsetAsync(a.err, 0, 4, st), "memset")) {
+			mgdk_BBPunfix(S);
+			return -1;
+		}
+		if (!ordered) {
+			hipLaunchKernelGGL(k_range_walk, dim3(grid_for(n, 256 * 4, 256 * 64)), blk, 0, st, a);
+		} else {
+			a.Z = Z.as<oid>();
+			hipLaunchKernelGGL(k_part_nilbound, dim3(grid_for(a.m, 256, 8192)), blk, 0, st, a, Z.as<oid>());
+			if (nunres <= ucap)
+				hipLaunchKernelGGL(k_range_fix, dim3(grid_for(nunres, 256, 8192)), blk, 0, st, a,
+						   (const oid *) ul.p, nunres);
+			else
+				hipLaunchKernelGGL(k_range_tile, dim3((unsigned) ((n + TT - 1) / TT)), blk, 0, st, a);
+		}
+		if (!hip_ok(hipMemcpyAsync(h, fl.p, 32, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
+			mgdk_BBPunfix(S);
+			return -1;
+		}
+		mgdk_BBPunfix(S);
+		ovf = ordered ? (ovf | (h[4] & 1)) : (h[4] & 1);
+	}
+	if (ovf) {
 		seterr("22003!overflow in calculation.\n");
 		return -1;
 	}

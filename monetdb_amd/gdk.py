@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmgdk.so")
+LIB_PATH = os.environ.get("MGDK_LIB") or os.path.join(HERE, "libmgdk.so")
 
 TYPE_void, TYPE_msk, TYPE_bit, TYPE_bte, TYPE_sht, TYPE_int, TYPE_oid = 0, 1, 2, 3, 4, 5, 6
 TYPE_flt, TYPE_dbl, TYPE_lng, TYPE_hge, TYPE_date, TYPE_str = 8, 9, 10, 11, 12, 16

@@ -181,6 +181,35 @@ def test_window_range_bounds(gdk, ora, desc, nil_frac, shuffle, limit, preceding
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("limit", [700, 3000, 10**7])
+@pytest.mark.parametrize("preceding", [True, False])
+@pytest.mark.parametrize("desc", [False, True])
+def test_window_long_frames(gdk, ora, limit, preceding, desc):
+    # frames longer than the fast kernel's halo: some rows (limit 700) or all
+    # rows (10**7 -> unresolved list overflows) go through the fix-up paths
+    r = rng(103)
+    vals, bits = _window_data(r, 6, 21_000, desc, 0.01, False)
+    got = gdk.GDKanalyticalwindowbounds(mk(gdk, gdk.TYPE_lng, vals), mk(gdk, gdk.TYPE_bit, bits),
+                                        limit, preceding).to_numpy()
+    want = ora.rangebounds(omk(ora, ora.TYPE_lng, vals), omk(ora, ora.TYPE_bit, bits), limit,
+                           preceding).values()
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("plen", [1, 2, 4095, 4097])
+def test_window_partition_sizes(gdk, ora, plen):
+    # partitions shorter than / straddling the fast kernel's tiles
+    r = rng(104)
+    nparts = max(3, 30_000 // plen)
+    vals, bits = _window_data(r, nparts, plen, False, 0.0, False)
+    for preceding in (True, False):
+        got = gdk.GDKanalyticalwindowbounds(mk(gdk, gdk.TYPE_lng, vals), mk(gdk, gdk.TYPE_bit, bits),
+                                            6, preceding).to_numpy()
+        want = ora.rangebounds(omk(ora, ora.TYPE_lng, vals), omk(ora, ora.TYPE_bit, bits), 6,
+                               preceding).values()
+        assert np.array_equal(got, want)
+
+
 def test_window_no_partitions_and_errors(gdk, ora):
     r = rng(102)
     vals = np.sort(r.integers(0, 10**6, 100_000)).astype(np.int64)
