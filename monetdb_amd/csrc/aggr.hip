@@ -79,18 +79,13 @@ k_sum(const void *base, int w, bool dense, oid off, const oid *oids, oid hseq, B
 		unsigned long long a = absbits(v);
 		mx = a > mx ? a : mx;
 	}
-	for (int k = 32; k > 0; k >>= 1) {
-		unsigned long long lo = __shfl_xor((unsigned long long) (uhge) s, k);
-		unsigned long long hi = __shfl_xor((unsigned long long) ((uhge) s >> 64), k);
-		s += (hge) (((uhge) hi << 64) | lo);
-		cnt += __shfl_xor(cnt, k);
-		unsigned long long t = __shfl_xor(firstnil, k);
-		firstnil = t < firstnil ? t : firstnil;
-		t = __shfl_xor(mx, k);
-		mx = t > mx ? t : mx;
-	}
-	if (__lane_id() == 0) {
-		atomic_add128(o->sum, s);
+	s = block_sum128(s);
+	cnt = block_reduce(cnt, [](unsigned long long x, unsigned long long y) { return x + y; });
+	firstnil = block_reduce(firstnil, [](unsigned long long x, unsigned long long y) { return x < y ? x : y; });
+	mx = block_reduce(mx, [](unsigned long long x, unsigned long long y) { return x > y ? x : y; });
+	if (threadIdx.x == 0) {
+		if (s)
+			atomic_add128(o->sum, s);
 		if (cnt)
 			atomicAdd(&o->cnt, cnt);
 		if (firstnil != ~0ull)
@@ -404,13 +399,9 @@ k_minmax_oid(const oid *g, BUN n, unsigned long long *out)
 		mn = x < mn ? x : mn;
 		mx = x > mx ? x : mx;
 	}
-	for (int o = 32; o > 0; o >>= 1) {
-		unsigned long long t = __shfl_xor(mn, o);
-		mn = t < mn ? t : mn;
-		t = __shfl_xor(mx, o);
-		mx = t > mx ? t : mx;
-	}
-	if (__lane_id() == 0) {
+	mn = block_reduce(mn, [](unsigned long long x, unsigned long long y) { return x < y ? x : y; });
+	mx = block_reduce(mx, [](unsigned long long x, unsigned long long y) { return x > y ? x : y; });
+	if (threadIdx.x == 0) {
 		atomicMin(&out[0], mn);
 		atomicMax(&out[1], mx);
 	}

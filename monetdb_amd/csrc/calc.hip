@@ -126,13 +126,10 @@ k_calc(Operand a, Operand b, void *out, int ow, hge max, BUN n, hge nilv,
 		}
 		st(out, ow, i, r);
 	}
-	// wave reduce then one atomic per wave
-	for (int o = 32; o > 0; o >>= 1) {
-		mynils += __shfl_xor(mynils, o);
-		unsigned long long t = __shfl_xor(myovf, o);
-		myovf = t < myovf ? t : myovf;
-	}
-	if (__lane_id() == 0) {
+	// block reduce then one atomic per workgroup
+	mynils = block_reduce(mynils, [](decltype(mynils) x, decltype(mynils) y) { return x + y; });
+	myovf = block_reduce(myovf, [](unsigned long long x, unsigned long long y) { return x < y ? x : y; });
+	if (threadIdx.x == 0) {
 		if (mynils)
 			atomicAdd(nils, mynils);
 		if (myovf != ~0ull)

@@ -163,8 +163,9 @@ k_grp_assign(BUN n, const uint32_t *hidx, const uint32_t *gidmap, oid *gid, BUN 
 		else
 			atomicAdd(&histo[g], 1ull);
 	}
-	if (uns)
-		atomicOr(unsorted, 1u);
+	uns = block_reduce(uns, [](uint32_t x, uint32_t y) { return x | y; });
+	if (threadIdx.x == 0)
+		publish_or(unsorted, uns);
 	if (LDSHIST) {
 		__syncthreads();
 		for (BUN k = threadIdx.x; k < ngrp; k += blockDim.x)
@@ -180,11 +181,8 @@ k_max_oid(const oid *g, BUN n, unsigned long long *out)
 	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
 		if (g[i] != MGDK_OID_NIL && g[i] > mx)
 			mx = g[i];
-	for (int o = 32; o > 0; o >>= 1) {
-		unsigned long long t = __shfl_xor(mx, o);
-		mx = t > mx ? t : mx;
-	}
-	if (__lane_id() == 0)
+	mx = block_reduce(mx, [](unsigned long long x, unsigned long long y) { return x > y ? x : y; });
+	if (threadIdx.x == 0)
 		atomicMax(out, mx);
 }
 

@@ -125,3 +125,59 @@ __device__ inline uint64_t lanemask_lt() {
 	unsigned l = __lane_id();
 	return l == 0 ? 0ull : (~0ull >> (64 - l));
 }
+
+// ---- block reductions (blockDim.x == 256, every thread calls) -------------
+// One global atomic per WORKGROUP, not per wave: same-word device atomics
+// serialise at ~88/us (MI355X_MICROARCH.md "fanin"/"dequeue"), so a grid of
+// thousands of waves each hitting one word would be bound by the atomic.
+// The result is valid in thread 0.
+template <typename T, typename F>
+__device__ __forceinline__ T
+block_reduce(T v, F op)
+{
+	__shared__ T s_red[4];
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1)
+		v = op(v, __shfl_xor(v, o));
+	__syncthreads();                 // s_red may still be read by a previous call
+	if (__lane_id() == 0)
+		s_red[threadIdx.x >> 6] = v;
+	__syncthreads();
+	if (threadIdx.x == 0)
+		v = op(op(s_red[0], s_red[1]), op(s_red[2], s_red[3]));
+	return v;
+}
+
+__device__ __forceinline__ hge
+block_sum128(hge s)
+{
+	unsigned long long lo = (unsigned long long) (uhge) s, hi = (unsigned long long) ((uhge) s >> 64);
+	__shared__ unsigned long long s_lo[4], s_hi[4];
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1) {
+		const unsigned long long l2 = __shfl_xor(lo, o), h2 = __shfl_xor(hi, o);
+		const uhge t = (((uhge) hi << 64) | lo) + (((uhge) h2 << 64) | l2);
+		lo = (unsigned long long) t;
+		hi = (unsigned long long) (t >> 64);
+	}
+	__syncthreads();
+	if (__lane_id() == 0) {
+		s_lo[threadIdx.x >> 6] = lo;
+		s_hi[threadIdx.x >> 6] = hi;
+	}
+	__syncthreads();
+	uhge t = 0;
+	if (threadIdx.x == 0)
+		for (int q = 0; q < 4; q++)
+			t += ((uhge) s_hi[q] << 64) | s_lo[q];
+	return (hge) t;
+}
+
+// thread 0 of a workgroup: set bits in a flag word, skipping the atomic when
+// they are already visible
+__device__ __forceinline__ void
+publish_or(uint32_t *flag, uint32_t bits)
+{
+	if (bits && (bits & ~__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
+		atomicOr(flag, bits);
+}

@@ -34,10 +34,12 @@ k_project(const oid *__restrict__ l, BUN n, const T *__restrict__ r, oid rseq, B
 		if (i + 1 < n)
 			out[i + 1] = v1;
 	}
-	if (bad)
-		atomicOr(&flags[0], 1u);
-	if (nil)
-		atomicOr(&flags[1], 1u);
+	bad = block_reduce(bad, [](uint32_t x, uint32_t y) { return x | y; });
+	nil = block_reduce(nil, [](uint32_t x, uint32_t y) { return x | y; });
+	if (threadIdx.x == 0) {
+		publish_or(&flags[0], bad);
+		publish_or(&flags[1], nil);
+	}
 }
 
 // r is a dense oid column: values are r.tseqbase + (o - rseq)
@@ -52,10 +54,12 @@ k_project_void(const oid *__restrict__ l, BUN n, oid rseq, BUN rcnt, oid rtseq,
 		else if (o - rseq >= rcnt) { out[i] = MGDK_OID_NIL; bad = 1; }
 		else out[i] = rtseq == MGDK_OID_NIL ? MGDK_OID_NIL : rtseq + (o - rseq);
 	}
-	if (bad)
-		atomicOr(&flags[0], 1u);
-	if (nil)
-		atomicOr(&flags[1], 1u);
+	bad = block_reduce(bad, [](uint32_t x, uint32_t y) { return x | y; });
+	nil = block_reduce(nil, [](uint32_t x, uint32_t y) { return x | y; });
+	if (threadIdx.x == 0) {
+		publish_or(&flags[0], bad);
+		publish_or(&flags[1], nil);
+	}
 }
 
 template <typename T>

@@ -4,16 +4,21 @@
 // stable LSD radix sort GDKrsort (gdk/gdk_rsort.c:21); stable float sorts use
 // the stable merge sort.  Both produce THE stable permutation, which is what
 // this stable LSD radix sort reproduces:
-//   key image: order-preserving unsigned 64-bit (sign bit flipped; IEEE
-//   floats folded; -0 == +0; nil placed first or last as requested; inverted
-//   for descending so ties keep input order);
+//   key image: order-preserving unsigned key (sign bit flipped; IEEE floats
+//   folded; -0 == +0; nil placed first or last as requested; inverted for
+//   descending so ties keep input order); 32-bit keys for types up to 4
+//   bytes (when nilslast == reverse, so nil keeps its natural image), 64-bit
+//   otherwise;
 //   passes: 8-bit digits, only digit positions that are not constant over
 //   the input (AND/OR reduction) are sorted;
 //   per pass: (1) per-tile digit histogram in LDS, (2) device scan of the
-//   digit-major counts, (3) stable scatter: 16 rows of 256 lanes per tile,
-//   wave peer groups from 8 bit-sliced ballots, per-wave digit counts in
-//   LDS, running per-digit bases -- a lane's destination is
-//   tile_base[d] + run[d] + earlier waves' count of d + rank in its wave.
+//   digit-major counts, (3) stable scatter of a 4096-key tile: each wave
+//   ranks its 16 rows of 64 keys with 8 bit-sliced ballots against per-wave
+//   running digit counters (no workgroup barrier per row), the tile is
+//   reordered by digit in LDS and written out in that order, so equal-digit
+//   runs leave as contiguous stores;
+//   the LAST pass writes the result columns directly: integer values decoded
+//   from the key image (no gather) and the order oids (hseqbase + position).
 #include <vector>
 
 #include "mgdk_internal.h"
@@ -22,89 +27,193 @@ using namespace mgdk;
 
 namespace {
 
-constexpr int SITEMS = 16;
-constexpr int STILE = 256 * SITEMS;
+constexpr int SROWS = 16;                  // rows of 64 keys per wave
+constexpr int STILE = 256 * SROWS;         // keys per tile
 
+template <typename K>
 __global__ __launch_bounds__(256) void
-k_rs_hist(const uint64_t *keys, BUN n, int shift, uint32_t *hist, uint32_t nblocks)
+k_rs_hist(const K *keys, BUN n, int shift, uint32_t *hist, uint32_t nblocks)
 {
 	__shared__ uint32_t h[256];
 	h[threadIdx.x] = 0;
 	__syncthreads();
 	const BUN base = (BUN) blockIdx.x * STILE;
+	K k[SROWS];
 #pragma unroll
-	for (int r = 0; r < SITEMS; r++) {
-		BUN i = base + r * 256 + threadIdx.x;
+	for (int r = 0; r < SROWS; r++) {
+		const BUN i = base + r * 256 + threadIdx.x;
+		k[r] = i < n ? keys[i] : 0;
+	}
+#pragma unroll
+	for (int r = 0; r < SROWS; r++) {
+		const BUN i = base + r * 256 + threadIdx.x;
 		if (i < n)
-			atomicAdd(&h[(keys[i] >> shift) & 255], 1u);
+			atomicAdd(&h[(uint32_t) (k[r] >> shift) & 255], 1u);
 	}
 	__syncthreads();
 	hist[(BUN) threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
 }
 
-__global__ __launch_bounds__(256) void
-k_rs_scatter(const uint64_t *keys, const uint32_t *vals, BUN n, int shift, const uint32_t *offs,
-	     uint32_t nblocks, uint64_t *keys_out, uint32_t *vals_out)
+// final pass outputs: decoded value column and order oids
+struct FinalOut {
+	void *sorted;       // NULL: not requested (or gathered separately)
+	int vw;             // value width in bytes (1, 2, 4, 8)
+	bool reverse;
+	bool is64;          // 64-bit key image of a signed/unsigned integer
+	bool uns;           // oid
+	oid *order;
+	oid hseq;
+};
+
+template <typename K>
+__device__ __forceinline__ void
+emit_final(const FinalOut &fo, BUN g, K key, uint32_t v)
 {
-	__shared__ uint32_t run[256], boff[256], wc[4][256];
-	const unsigned tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-	run[tid] = 0;
-	boff[tid] = offs[(BUN) tid * nblocks + blockIdx.x];
-	wc[0][tid] = wc[1][tid] = wc[2][tid] = wc[3][tid] = 0;
-	__syncthreads();
-	const uint64_t lt = lanemask_lt();
-	const BUN base = (BUN) blockIdx.x * STILE;
-	for (int r = 0; r < SITEMS; r++) {
-		const BUN i = base + r * 256 + tid;
-		const bool valid = i < n;
-		uint64_t k = valid ? keys[i] : 0;
-		uint32_t v = valid ? vals[i] : 0;
-		uint32_t d = (uint32_t) (k >> shift) & 255;
-		uint64_t peer = __ballot(valid);
-#pragma unroll
-		for (int b = 0; b < 8; b++) {
-			uint64_t bal = __ballot((d >> b) & 1);
-			peer &= ((d >> b) & 1) ? bal : ~bal;
+	if (fo.order)
+		fo.order[g] = fo.hseq + v;
+	if (fo.sorted) {
+		uint64_t u = (uint64_t) key;
+		if (fo.reverse)
+			u = ~u;
+		if (sizeof(K) == 4) {
+			const int32_t x = (int32_t) ((uint32_t) u ^ 0x80000000u);
+			switch (fo.vw) {
+			case 1: ((int8_t *) fo.sorted)[g] = (int8_t) x; break;
+			case 2: ((int16_t *) fo.sorted)[g] = (int16_t) x; break;
+			default: ((int32_t *) fo.sorted)[g] = x; break;
+			}
+		} else {
+			((uint64_t *) fo.sorted)[g] = fo.uns ? u : (u ^ (1ull << 63));
 		}
-		const uint32_t rank = (uint32_t) __popcll(peer & lt);
-		if (valid && (peer >> lane) == 1)   // highest lane of its peer group
-			wc[wave][d] = (uint32_t) __popcll(peer);
-		__syncthreads();
-		if (valid) {
-			uint32_t pos = boff[d] + run[d] + rank;
-			for (unsigned w = 0; w < wave; w++)
-				pos += wc[w][d];
-			keys_out[pos] = k;
-			vals_out[pos] = v;
-		}
-		__syncthreads();
-		run[tid] += wc[0][tid] + wc[1][tid] + wc[2][tid] + wc[3][tid];
-		wc[0][tid] = wc[1][tid] = wc[2][tid] = wc[3][tid] = 0;
-		__syncthreads();
 	}
 }
 
+template <typename K, bool FINAL>
 __global__ __launch_bounds__(256) void
-k_andor(const uint64_t *keys, BUN n, unsigned long long *out)
+k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32_t *offs, uint32_t nblocks,
+	     K *kout, uint32_t *vout, FinalOut fo)
+{
+	__shared__ K sk[STILE];
+	__shared__ uint32_t sv[STILE];
+	__shared__ uint32_t wcnt[4][256];     // per-wave running digit counts, then per-wave bases
+	__shared__ uint32_t tstart[256];      // digit start inside the reordered tile
+	__shared__ uint32_t gbase[256];       // digit start of this tile in the output
+	__shared__ uint32_t s_wt[4];
+	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+	wcnt[0][tid] = wcnt[1][tid] = wcnt[2][tid] = wcnt[3][tid] = 0;
+	gbase[tid] = offs[(BUN) tid * nblocks + blockIdx.x];
+	const BUN tbase = (BUN) blockIdx.x * STILE;
+	const BUN base = tbase + (BUN) w * (64 * SROWS);
+	K k[SROWS];
+	uint32_t v[SROWS];
+#pragma unroll
+	for (int r = 0; r < SROWS; r++) {
+		const BUN i = base + r * 64 + lane;
+		k[r] = i < n ? keys[i] : 0;
+		v[r] = i < n ? vals[i] : 0;
+	}
+	__syncthreads();
+	const uint64_t lt = lanemask_lt();
+	uint32_t rk[SROWS];
+#pragma unroll
+	for (int r = 0; r < SROWS; r++) {
+		const BUN i = base + r * 64 + lane;
+		const bool valid = i < n;
+		const uint32_t d = (uint32_t) (k[r] >> shift) & 255;
+		uint64_t peer = __ballot(valid);
+#pragma unroll
+		for (int b = 0; b < 8; b++) {
+			const uint64_t bal = __ballot((d >> b) & 1);
+			peer &= ((d >> b) & 1) ? bal : ~bal;
+		}
+		const uint32_t before = wcnt[w][d];
+		rk[r] = ((before + (uint32_t) __popcll(peer & lt)) << 8) | d;
+		if (valid && (peer >> lane) == 1)    // highest lane of its peer group
+			wcnt[w][d] = before + (uint32_t) __popcll(peer);
+	}
+	__syncthreads();
+	{
+		// digit d = tid: per-wave bases and the tile's digit prefix
+		const uint32_t c0 = wcnt[0][tid], c1 = wcnt[1][tid], c2 = wcnt[2][tid], c3 = wcnt[3][tid];
+		const uint32_t tot = c0 + c1 + c2 + c3;
+		uint32_t incl = tot;
+#pragma unroll
+		for (int o = 1; o < 64; o <<= 1) {
+			const uint32_t u = __shfl_up(incl, o);
+			if (lane >= (unsigned) o)
+				incl += u;
+		}
+		if (lane == 63)
+			s_wt[w] = incl;
+		wcnt[0][tid] = 0;
+		wcnt[1][tid] = c0;
+		wcnt[2][tid] = c0 + c1;
+		wcnt[3][tid] = c0 + c1 + c2;
+		__syncthreads();
+		uint32_t ex = incl - tot;
+		for (unsigned q = 0; q < w; q++)
+			ex += s_wt[q];
+		tstart[tid] = ex;
+	}
+	__syncthreads();
+#pragma unroll
+	for (int r = 0; r < SROWS; r++) {
+		const BUN i = base + r * 64 + lane;
+		if (i < n) {
+			const uint32_t d = rk[r] & 255;
+			const uint32_t lpos = tstart[d] + wcnt[w][d] + (rk[r] >> 8);
+			sk[lpos] = k[r];
+			sv[lpos] = v[r];
+		}
+	}
+	__syncthreads();
+	const uint32_t nt = (uint32_t) (n - tbase < (BUN) STILE ? n - tbase : (BUN) STILE);
+#pragma unroll
+	for (int u = 0; u < SROWS; u++) {
+		const uint32_t i = tid + u * 256;
+		if (i < nt) {
+			const K key = sk[i];
+			const uint32_t d = (uint32_t) (key >> shift) & 255;
+			const BUN g = (BUN) gbase[d] + (i - tstart[d]);
+			if (FINAL) {
+				emit_final<K>(fo, g, key, sv[i]);
+			} else {
+				kout[g] = key;
+				vout[g] = sv[i];
+			}
+		}
+	}
+}
+
+template <typename K>
+__global__ __launch_bounds__(256) void
+k_andor(const K *keys, BUN n, unsigned long long *out)
 {
 	unsigned long long a = ~0ull, o = 0;
 	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
-		a &= keys[i];
-		o |= keys[i];
+		a &= (unsigned long long) keys[i];
+		o |= (unsigned long long) keys[i];
 	}
-	for (int s = 32; s > 0; s >>= 1) {
-		a &= __shfl_xor(a, s);
-		o |= __shfl_xor(o, s);
-	}
-	if (__lane_id() == 0) {
+	a = block_reduce(a, [](unsigned long long x, unsigned long long y) { return x & y; });
+	o = block_reduce(o, [](unsigned long long x, unsigned long long y) { return x | y; });
+	if (threadIdx.x == 0) {
 		atomicAnd(&out[0], a);
 		atomicOr(&out[1], o);
 	}
 }
 
-// key image of row p
-template <typename T>
-__device__ __forceinline__ uint64_t
+// no radix pass needed (all keys equal): write the final outputs in place
+template <typename K>
+__global__ __launch_bounds__(256) void
+k_final_copy(const K *keys, const uint32_t *vals, BUN n, FinalOut fo)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
+		emit_final<K>(fo, i, keys[i], vals[i]);
+}
+
+// key image of a value
+template <typename T, typename K>
+__device__ __forceinline__ K
 keyimg(T v, bool reverse, bool nilslast)
 {
 	uint64_t u;
@@ -114,7 +223,7 @@ keyimg(T v, bool reverse, bool nilslast)
 		float f = v == 0 ? 0.0f : v;
 		uint32_t b = __float_as_uint(f);
 		b = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
-		u = (uint64_t) b << 32;
+		u = sizeof(K) == 4 ? (uint64_t) b : (uint64_t) b << 32;
 	} else if constexpr (sizeof(T) == 8 && (T) 0.5 != 0) {   // double
 		isnil = v != v;
 		double f = v == 0 ? 0.0 : v;
@@ -125,43 +234,53 @@ keyimg(T v, bool reverse, bool nilslast)
 		u = (uint64_t) v;
 	} else {
 		isnil = v == NilOf<T>::v();
-		u = (uint64_t) (int64_t) v ^ (1ull << 63);
+		u = sizeof(K) == 4 ? (uint64_t) ((uint32_t) (int32_t) v ^ 0x80000000u)
+				   : ((uint64_t) (int64_t) v ^ (1ull << 63));
 	}
+	const uint64_t all1 = sizeof(K) == 4 ? 0xffffffffull : ~0ull;
 	if (reverse)
-		u = ~u;
-	if (isnil)
-		u = nilslast ? ~0ull : 0ull;
-	return u;
+		u = ~u & all1;
+	// integer nil is the type minimum: with nilslast == reverse its natural
+	// image already sits at the requested end (and stays decodable)
+	constexpr bool is_int = !((T) 0.5 != 0);
+	if (isnil && !(is_int && reverse == nilslast))
+		u = nilslast ? all1 : 0ull;
+	return (K) u;
 }
 
-template <typename T>
+template <typename T, typename K>
 __global__ __launch_bounds__(256) void
-k_keys(const T *col, BUN n, bool reverse, bool nilslast, uint64_t *keys, uint32_t *idx)
+k_keys(const T *col, BUN n, bool reverse, bool nilslast, K *keys, uint32_t *idx)
 {
 	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
-		keys[i] = keyimg<T>(col[i], reverse, nilslast);
+		keys[i] = keyimg<T, K>(col[i], reverse, nilslast);
 		idx[i] = (uint32_t) i;
 	}
 }
 
 template <typename T>
 __global__ __launch_bounds__(256) void
-k_gather_sorted(const T *col, const uint32_t *idx, BUN n, oid hseq, T *sorted, oid *order)
+k_gather_sorted(const T *col, const oid *order, BUN n, oid hseq, T *sorted)
 {
-	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
-		uint32_t j = idx[i];
-		if (sorted)
-			sorted[i] = col[j];
-		if (order)
-			order[i] = hseq + j;
-	}
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
+		sorted[i] = col[order[i] - hseq];
 }
 
+template <typename K>
 __global__ __launch_bounds__(256) void
-k_newgrp(const uint64_t *keys, BUN n, uint8_t *flag)
+k_newgrp(const K *keys, BUN n, uint8_t *flag)
 {
 	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
 		flag[i] = i > 0 && keys[i] != keys[i - 1];
+}
+
+// float keys of the sorted order (for the groups of a float sort)
+template <typename T, typename K>
+__global__ __launch_bounds__(256) void
+k_keys_of_order(const T *col, const oid *order, BUN n, oid hseq, bool reverse, bool nilslast, K *keys)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
+		keys[i] = keyimg<T, K>(col[order[i] - hseq], reverse, nilslast);
 }
 
 __global__ __launch_bounds__(256) void
@@ -171,20 +290,126 @@ k_gid(const uint64_t *excl, const uint8_t *flag, BUN n, oid *gid)
 		gid[i] = excl[i] + flag[i];
 }
 
-template <typename T>
-void
-launch_keys(const mgdk_bat *b, bool reverse, bool nilslast, uint64_t *keys, uint32_t *idx)
+// stable LSD radix sort of (key, position) pairs; the final pass (when fo
+// is given) writes the result columns instead of the pairs
+template <typename K>
+int
+radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int bits, const FinalOut *fo,
+	   K **keys_out, uint32_t **vals_out)
 {
-	hipLaunchKernelGGL((k_keys<T>), dim3(grid_for(b->count, 1024, 8192)), dim3(256), 0, stream(),
+	*keys_out = keys;
+	*vals_out = vals;
+	hipStream_t st = stream();
+	if (n == 0)
+		return 0;
+	unsigned long long *ao = (unsigned long long *) meta_buf();
+	unsigned long long init[2] = {~0ull, 0ull};
+	if (!hip_ok(hipMemcpyAsync(ao, init, 16, hipMemcpyHostToDevice, st), "memcpy"))
+		return -1;
+	hipLaunchKernelGGL((k_andor<K>), dim3(grid_for(n, 8192, 1024)), dim3(256), 0, st, keys, n, ao);
+	unsigned long long *h = (unsigned long long *) pinned(16);
+	if (!hip_ok(hipMemcpyAsync(h, ao, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+		return -1;
+	const uint64_t diff = h[0] ^ h[1];
+	std::vector<int> shifts;
+	for (int shift = 0; shift < bits; shift += 8)
+		if ((diff >> shift) & 255)
+			shifts.push_back(shift);   // other digits are constant: identity passes
+	const uint32_t nblocks = (uint32_t) ((n + STILE - 1) / STILE);
+	DevBuf hist((size_t) 256 * nblocks * 4), offs((size_t) 256 * nblocks * 4);
+	if (!hist.p || !offs.p)
+		return -1;
+	K *kin = keys, *kout = keys_alt;
+	uint32_t *vin = vals, *vout = vals_alt;
+	FinalOut none{};
+	for (size_t s = 0; s < shifts.size(); s++) {
+		const int shift = shifts[s];
+		const bool fin = fo != nullptr && s + 1 == shifts.size();
+		hipLaunchKernelGGL((k_rs_hist<K>), dim3(nblocks), dim3(256), 0, st, kin, n, shift, hist.as<uint32_t>(),
+				   nblocks);
+		if (exclusive_scan(hist.as<uint32_t>(), offs.as<uint32_t>(), (BUN) 256 * nblocks, nullptr) < 0)
+			return -1;
+		if (fin)
+			hipLaunchKernelGGL((k_rs_scatter<K, true>), dim3(nblocks), dim3(256), 0, st, kin, vin, n, shift,
+					   offs.as<uint32_t>(), nblocks, kout, vout, *fo);
+		else
+			hipLaunchKernelGGL((k_rs_scatter<K, false>), dim3(nblocks), dim3(256), 0, st, kin, vin, n, shift,
+					   offs.as<uint32_t>(), nblocks, kout, vout, none);
+		std::swap(kin, kout);
+		std::swap(vin, vout);
+	}
+	if (fo != nullptr && shifts.empty())
+		hipLaunchKernelGGL((k_final_copy<K>), dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st, kin, vin, n, *fo);
+	if (!sync())
+		return -1;
+	*keys_out = kin;
+	*vals_out = vin;
+	return 0;
+}
+
+template <typename T, typename K>
+void
+launch_keys(const mgdk_bat *b, bool reverse, bool nilslast, K *keys, uint32_t *idx)
+{
+	hipLaunchKernelGGL((k_keys<T, K>), dim3(grid_for(b->count, 1024, 8192)), dim3(256), 0, stream(),
 			   (const T *) b->theap, b->count, reverse, nilslast, keys, idx);
 }
 
 template <typename T>
 void
-launch_gather(const mgdk_bat *b, const uint32_t *idx, void *sorted, oid *order)
+launch_gather(const mgdk_bat *b, const oid *order, void *sorted)
 {
 	hipLaunchKernelGGL((k_gather_sorted<T>), dim3(grid_for(b->count, 1024, 8192)), dim3(256), 0, stream(),
-			   (const T *) b->theap, idx, b->count, b->hseqbase, (T *) sorted, order);
+			   (const T *) b->theap, order, b->count, b->hseqbase, (T *) sorted);
+}
+
+// sort b's keys of type T with key width K; fills sn/on (either may be NULL)
+// and, for groups, returns the key images in sorted order in *keys (the
+// caller deletes it)
+template <typename T, typename K>
+int
+sort_typed(const mgdk_bat *b, bool reverse, bool nilslast, mgdk_bat *sn, mgdk_bat *on, bool want_keys,
+	   DevBuf **keys)
+{
+	const BUN n = b->count;
+	constexpr bool is_float = (T) 0.5 != 0;
+	DevBuf k0(n * sizeof(K)), k1(n * sizeof(K)), v0(n * 4), v1(n * 4), otmp(on ? 8 : n * 8);
+	if (!k0.p || !k1.p || !v0.p || !v1.p || !otmp.p)
+		return -1;
+	launch_keys<T, K>(b, reverse, nilslast, k0.as<K>(), v0.as<uint32_t>());
+	FinalOut fo{};
+	fo.vw = b->twidth;
+	fo.reverse = reverse;
+	fo.is64 = sizeof(K) == 8;
+	fo.uns = basetype(b->ttype) == MGDK_oid;
+	fo.hseq = b->hseqbase;
+	// floats (and reverse != nilslast images) are not decodable: gather by order
+	const bool decodable = !is_float && reverse == nilslast;
+	fo.sorted = decodable && sn ? sn->theap : nullptr;
+	fo.order = on ? (oid *) on->theap : otmp.as<oid>();
+	K *ks;
+	uint32_t *vs;
+	if (radix_sort<K>(k0.as<K>(), v0.as<uint32_t>(), k1.as<K>(), v1.as<uint32_t>(), n, 8 * (int) sizeof(K), &fo,
+			  &ks, &vs) < 0)
+		return -1;
+	if (sn && !decodable) {
+		switch (b->twidth) {
+		case 1: launch_gather<int8_t>(b, fo.order, sn->theap); break;
+		case 2: launch_gather<int16_t>(b, fo.order, sn->theap); break;
+		case 4: launch_gather<int32_t>(b, fo.order, sn->theap); break;
+		default: launch_gather<int64_t>(b, fo.order, sn->theap); break;
+		}
+	}
+	if (want_keys) {
+		// the key image of every sorted row, in sorted order
+		DevBuf *kb = new DevBuf(n * sizeof(K) + 8);
+		*keys = kb;
+		if (!kb->p)
+			return -1;
+		hipLaunchKernelGGL((k_keys_of_order<T, K>), dim3(grid_for(n, 1024, 8192)), dim3(256), 0, stream(),
+				   (const T *) b->theap, fo.order, n, b->hseqbase, reverse, nilslast, kb->as<K>());
+	}
+	return sync() ? 0 : -1;
 }
 
 }  // namespace
@@ -195,42 +420,7 @@ int
 radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32_t *vals_alt, BUN n, int bits,
 		 uint64_t **keys_out, uint32_t **vals_out)
 {
-	*keys_out = keys;
-	*vals_out = vals;
-	if (n <= 1)
-		return 0;
-	hipStream_t st = stream();
-	unsigned long long *ao = (unsigned long long *) meta_buf();
-	unsigned long long init[2] = {~0ull, 0ull};
-	if (!hip_ok(hipMemcpyAsync(ao, init, 16, hipMemcpyHostToDevice, st), "memcpy"))
-		return -1;
-	hipLaunchKernelGGL(k_andor, dim3(grid_for(n, 4096, 2048)), dim3(256), 0, st, keys, n, ao);
-	unsigned long long *h = (unsigned long long *) pinned(16);
-	if (!hip_ok(hipMemcpyAsync(h, ao, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
-		return -1;
-	const uint64_t diff = h[0] ^ h[1];
-	const uint32_t nblocks = (uint32_t) ((n + STILE - 1) / STILE);
-	DevBuf hist((size_t) 256 * nblocks * 4), offs((size_t) 256 * nblocks * 4);
-	if (!hist.p || !offs.p)
-		return -1;
-	uint64_t *kin = keys, *kout = keys_alt;
-	uint32_t *vin = vals, *vout = vals_alt;
-	for (int shift = 0; shift < bits; shift += 8) {
-		if (((diff >> shift) & 255) == 0)
-			continue;   // digit constant over all keys: identity pass
-		hipLaunchKernelGGL(k_rs_hist, dim3(nblocks), dim3(256), 0, st, kin, n, shift, hist.as<uint32_t>(), nblocks);
-		if (exclusive_scan(hist.as<uint32_t>(), offs.as<uint32_t>(), (BUN) 256 * nblocks, nullptr) < 0)
-			return -1;
-		hipLaunchKernelGGL(k_rs_scatter, dim3(nblocks), dim3(256), 0, st, kin, vin, n, shift, offs.as<uint32_t>(),
-				   nblocks, kout, vout);
-		std::swap(kin, kout);
-		std::swap(vin, vout);
-	}
-	if (!sync())
-		return -1;
-	*keys_out = kin;
-	*vals_out = vin;
-	return 0;
+	return radix_sort<uint64_t>(keys, vals, keys_alt, vals_alt, n, bits, nullptr, keys_out, vals_out);
 }
 
 }  // namespace mgdk
@@ -275,53 +465,57 @@ mgdk_BATsort(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b
 		goto done;
 	}
 	{
-		DevBuf k0(n * 8), k1(n * 8), v0(n * 4), v1(n * 4);
-		if (!k0.p || !k1.p || !v0.p || !v1.p)
-			return -1;
-		switch (tt) {
-		case MGDK_bte: launch_keys<int8_t>(b, reverse, nilslast, k0.as<uint64_t>(), v0.as<uint32_t>()); break;
-		case MGDK_sht: launch_keys<int16_t>(b, reverse, nilslast, k0.as<uint64_t>(), v0.as<uint32_t>()); break;
-		case MGDK_int: launch_keys<int32_t>(b, reverse, nilslast, k0.as<uint64_t>(), v0.as<uint32_t>()); break;
-		case MGDK_lng: launch_keys<int64_t>(b, reverse, nilslast, k0.as<uint64_t>(), v0.as<uint32_t>()); break;
-		case MGDK_oid: launch_keys<uint64_t>(b, reverse, nilslast, k0.as<uint64_t>(), v0.as<uint32_t>()); break;
-		case MGDK_flt: launch_keys<float>(b, reverse, nilslast, k0.as<uint64_t>(), v0.as<uint32_t>()); break;
-		case MGDK_dbl: launch_keys<double>(b, reverse, nilslast, k0.as<uint64_t>(), v0.as<uint32_t>()); break;
-		}
-		uint64_t *ks;
-		uint32_t *vs;
-		if (radix_sort_pairs(k0.as<uint64_t>(), v0.as<uint32_t>(), k1.as<uint64_t>(), v1.as<uint32_t>(), n, 64,
-				     &ks, &vs) < 0)
-			return -1;
 		sn = sorted ? newbat(b->hseqbase, b->ttype, n) : nullptr;
 		on = order ? newbat(b->hseqbase, MGDK_oid, n) : nullptr;
 		if ((sorted && !sn) || (order && !on))
 			goto fail;
-		switch (b->twidth) {
-		case 1: launch_gather<int8_t>(b, vs, sn ? sn->theap : nullptr, on ? (oid *) on->theap : nullptr); break;
-		case 2: launch_gather<int16_t>(b, vs, sn ? sn->theap : nullptr, on ? (oid *) on->theap : nullptr); break;
-		case 4: launch_gather<int32_t>(b, vs, sn ? sn->theap : nullptr, on ? (oid *) on->theap : nullptr); break;
-		default: launch_gather<int64_t>(b, vs, sn ? sn->theap : nullptr, on ? (oid *) on->theap : nullptr); break;
+		// 32-bit key images need nil at its natural end (nilslast == reverse)
+		const bool k32 = b->twidth <= 4 && reverse == nilslast;
+		DevBuf *keys = nullptr;
+		int rc = 0;
+		const bool wk = groups != nullptr;
+#define SORT(T, K) rc = sort_typed<T, K>(b, reverse, nilslast, sn, on, wk, &keys)
+		switch (tt) {
+		case MGDK_bte: if (k32) SORT(int8_t, uint32_t); else SORT(int8_t, uint64_t); break;
+		case MGDK_sht: if (k32) SORT(int16_t, uint32_t); else SORT(int16_t, uint64_t); break;
+		case MGDK_int: if (k32) SORT(int32_t, uint32_t); else SORT(int32_t, uint64_t); break;
+		case MGDK_flt: if (k32) SORT(float, uint32_t); else SORT(float, uint64_t); break;
+		case MGDK_lng: SORT(int64_t, uint64_t); break;
+		case MGDK_oid: SORT(uint64_t, uint64_t); break;
+		case MGDK_dbl: SORT(double, uint64_t); break;
+		}
+#undef SORT
+		if (rc < 0) {
+			delete keys;
+			goto fail;
 		}
 		if (groups) {
 			gn = newbat(b->hseqbase, MGDK_oid, n);
-			DevBuf fl(n), ex(n * 8);
-			if (!gn || !fl.p || !ex.p)
-				goto fail;
-			hipLaunchKernelGGL(k_newgrp, dim3(grid_for(n, 1024, 8192)), dim3(256), 0, stream(), ks, n,
-					   fl.as<uint8_t>());
+			DevBuf fl(n + 1), ex(n * 8 + 8);
 			uint64_t tot = 0;
-			if (exclusive_scan(fl.as<uint8_t>(), ex.as<uint64_t>(), n, &tot) < 0)
+			bool ok = gn && fl.p && ex.p;
+			if (ok) {
+				if (k32)
+					hipLaunchKernelGGL((k_newgrp<uint32_t>), dim3(grid_for(n, 1024, 8192)), dim3(256), 0,
+							   stream(), keys->as<uint32_t>(), n, fl.as<uint8_t>());
+				else
+					hipLaunchKernelGGL((k_newgrp<uint64_t>), dim3(grid_for(n, 1024, 8192)), dim3(256), 0,
+							   stream(), keys->as<uint64_t>(), n, fl.as<uint8_t>());
+				ok = exclusive_scan(fl.as<uint8_t>(), ex.as<uint64_t>(), n, &tot) >= 0;
+			}
+			if (ok)
+				hipLaunchKernelGGL(k_gid, dim3(grid_for(n, 1024, 8192)), dim3(256), 0, stream(),
+						   ex.as<uint64_t>(), fl.as<uint8_t>(), n, (oid *) gn->theap);
+			ok = ok && sync();
+			delete keys;
+			if (!ok)
 				goto fail;
-			hipLaunchKernelGGL(k_gid, dim3(grid_for(n, 1024, 8192)), dim3(256), 0, stream(), ex.as<uint64_t>(),
-					   fl.as<uint8_t>(), n, (oid *) gn->theap);
 			gn->count = n;
 			gn->tsorted = 1;
 			gn->trevsorted = tot == 0;
 			gn->tkey = tot + 1 == n || n <= 1;
 			gn->tnonil = 1;
 		}
-		if (!sync())
-			goto fail;
 		if (sn) {
 			sn->count = n;
 			sn->tsorted = !reverse || n <= 1;

@@ -138,6 +138,55 @@ def test_sort_float(gdk, dt, tname):
     assert np.array_equal(o.to_numpy(), want)
 
 
+def test_sort_float_groups(gdk):
+    r = rng(94)
+    vals = (r.integers(-20, 20, 30_000) / 2).astype(np.float64)
+    vals[r.random(30_000) < 0.05] = np.nan
+    vals[r.random(30_000) < 0.05] = -0.0
+    s, o, g = gdk.BATsort(mk(gdk, gdk.TYPE_dbl, vals))
+    key = np.where(np.isnan(vals), -np.inf, vals)
+    key = np.where(key == 0, 0.0, key)
+    perm = np.argsort(key, kind="stable")
+    assert np.array_equal(o.to_numpy(), perm.astype(np.uint64))
+    sv = s.to_numpy()
+    assert np.array_equal(sv.view(np.uint64), vals[perm].view(np.uint64))   # -0 kept bit-exact
+    ks = key[perm]
+    want_g = np.concatenate([[0], np.cumsum(ks[1:] != ks[:-1])]).astype(np.uint64)
+    assert np.array_equal(g.to_numpy(), want_g)
+
+
+@pytest.mark.parametrize("tname,dt", [("sht", np.int16), ("int", np.int32), ("lng", np.int64)])
+def test_sort_unstable_nils_other_end(gdk, tname, dt):
+    # reverse != nilslast (only without `stable`): nil keeps its requested end
+    r = rng(95)
+    tp = getattr(gdk, "TYPE_" + tname)
+    nil = gdk.NIL[tp]
+    vals = with_nils(r.integers(-1000, 1000, 50_000).astype(dt), nil, 0.03, r)
+    for reverse, nilslast in ((False, True), (True, False)):
+        s, o, _ = gdk.BATsort(mk(gdk, tp, vals), reverse=reverse, nilslast=nilslast, stable=False)
+        sv = s.to_numpy()
+        isn = sv == nil
+        k = int(isn.sum())
+        assert k == int((vals == nil).sum())
+        assert (isn[-k:].all() if nilslast else isn[:k].all())
+        nn = sv[~isn]
+        assert np.all(nn[:-1] >= nn[1:]) if reverse else np.all(nn[:-1] <= nn[1:])
+        assert np.array_equal(np.sort(vals[o.to_numpy().astype(np.int64)]), np.sort(vals))
+
+
+@pytest.mark.parametrize("n", [0, 1, 4095, 4097, 70_000])
+def test_sort_sizes_and_constant(gdk, ora, n):
+    r = rng(96)
+    for vals in (r.integers(-50, 50, n).astype(np.int32), np.full(n, 7, np.int32)):
+        s, o, g = gdk.BATsort(mk(gdk, gdk.TYPE_int, vals))
+        if n == 0:
+            assert s.count() == 0
+            continue
+        os_, oo = ora.BATsort(omk(ora, ora.TYPE_int, vals))
+        assert np.array_equal(s.to_numpy(), os_.values())
+        assert np.array_equal(o.to_numpy(), oo.values())
+
+
 def test_sort_errors(gdk):
     b = mk(gdk, gdk.TYPE_int, np.array([3, 1, 2], np.int32))
     with pytest.raises(gdk.GDKError, match="stable sort cannot have reverse != nilslast"):
