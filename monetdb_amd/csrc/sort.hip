@@ -57,6 +57,8 @@ k_rs_hist(const K *keys, BUN n, int shift, uint32_t *hist, uint32_t nblocks)
 // final pass outputs: decoded value column and order oids
 struct FinalOut {
 	void *sorted;       // NULL: not requested (or gathered separately)
+	void *keys;         // sorted key images (for groups), NULL: not requested
+	bool want_keys;
 	int vw;             // value width in bytes (1, 2, 4, 8)
 	bool reverse;
 	bool is64;          // 64-bit key image of a signed/unsigned integer
@@ -71,6 +73,8 @@ emit_final(const FinalOut &fo, BUN g, K key, uint32_t v)
 {
 	if (fo.order)
 		fo.order[g] = fo.hseq + v;
+	if (fo.keys)
+		((K *) fo.keys)[g] = key;
 	if (fo.sorted) {
 		uint64_t u = (uint64_t) key;
 		if (fo.reverse)
@@ -88,7 +92,7 @@ emit_final(const FinalOut &fo, BUN g, K key, uint32_t v)
 	}
 }
 
-template <typename K, bool FINAL>
+template <typename K, bool FINAL, bool IDV>
 __global__ __launch_bounds__(256) void
 k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32_t *offs, uint32_t nblocks,
 	     K *kout, uint32_t *vout, FinalOut fo)
@@ -110,7 +114,7 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 	for (int r = 0; r < SROWS; r++) {
 		const BUN i = base + r * 64 + lane;
 		k[r] = i < n ? keys[i] : 0;
-		v[r] = i < n ? vals[i] : 0;
+		v[r] = IDV ? (uint32_t) i : (i < n ? vals[i] : 0);   // first pass: positions
 	}
 	__syncthreads();
 	const uint64_t lt = lanemask_lt();
@@ -208,7 +212,7 @@ __global__ __launch_bounds__(256) void
 k_final_copy(const K *keys, const uint32_t *vals, BUN n, FinalOut fo)
 {
 	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
-		emit_final<K>(fo, i, keys[i], vals[i]);
+		emit_final<K>(fo, i, keys[i], vals ? vals[i] : (uint32_t) i);
 }
 
 // key image of a value
@@ -248,13 +252,23 @@ keyimg(T v, bool reverse, bool nilslast)
 	return (K) u;
 }
 
+// key images + their AND/OR (constant digits are skipped by the passes)
 template <typename T, typename K>
 __global__ __launch_bounds__(256) void
-k_keys(const T *col, BUN n, bool reverse, bool nilslast, K *keys, uint32_t *idx)
+k_keys(const T *col, BUN n, bool reverse, bool nilslast, K *keys, unsigned long long *andor)
 {
+	unsigned long long a = ~0ull, o = 0;
 	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
-		keys[i] = keyimg<T, K>(col[i], reverse, nilslast);
-		idx[i] = (uint32_t) i;
+		const K k = keyimg<T, K>(col[i], reverse, nilslast);
+		keys[i] = k;
+		a &= (unsigned long long) k;
+		o |= (unsigned long long) k;
+	}
+	a = block_reduce(a, [](unsigned long long x, unsigned long long y) { return x & y; });
+	o = block_reduce(o, [](unsigned long long x, unsigned long long y) { return x | y; });
+	if (threadIdx.x == 0) {
+		atomicAnd(&andor[0], a);
+		atomicOr(&andor[1], o);
 	}
 }
 
@@ -274,15 +288,6 @@ k_newgrp(const K *keys, BUN n, uint8_t *flag)
 		flag[i] = i > 0 && keys[i] != keys[i - 1];
 }
 
-// float keys of the sorted order (for the groups of a float sort)
-template <typename T, typename K>
-__global__ __launch_bounds__(256) void
-k_keys_of_order(const T *col, const oid *order, BUN n, oid hseq, bool reverse, bool nilslast, K *keys)
-{
-	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
-		keys[i] = keyimg<T, K>(col[order[i] - hseq], reverse, nilslast);
-}
-
 __global__ __launch_bounds__(256) void
 k_gid(const uint64_t *excl, const uint8_t *flag, BUN n, oid *gid)
 {
@@ -292,10 +297,13 @@ k_gid(const uint64_t *excl, const uint8_t *flag, BUN n, oid *gid)
 
 // stable LSD radix sort of (key, position) pairs; the final pass (when fo
 // is given) writes the result columns instead of the pairs
+// positions: the values are 0..n-1 and `vals` is uninitialised (the first
+// pass generates them); andor: the keys' AND/OR at meta_buf() are already
+// computed
 template <typename K>
 int
 radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int bits, const FinalOut *fo,
-	   K **keys_out, uint32_t **vals_out)
+	   bool positions, bool andor, K **keys_out, uint32_t **vals_out)
 {
 	*keys_out = keys;
 	*vals_out = vals;
@@ -303,10 +311,12 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 	if (n == 0)
 		return 0;
 	unsigned long long *ao = (unsigned long long *) meta_buf();
-	unsigned long long init[2] = {~0ull, 0ull};
-	if (!hip_ok(hipMemcpyAsync(ao, init, 16, hipMemcpyHostToDevice, st), "memcpy"))
-		return -1;
-	hipLaunchKernelGGL((k_andor<K>), dim3(grid_for(n, 8192, 1024)), dim3(256), 0, st, keys, n, ao);
+	if (!andor) {
+		unsigned long long init[2] = {~0ull, 0ull};
+		if (!hip_ok(hipMemcpyAsync(ao, init, 16, hipMemcpyHostToDevice, st), "memcpy"))
+			return -1;
+		hipLaunchKernelGGL((k_andor<K>), dim3(grid_for(n, 8192, 1024)), dim3(256), 0, st, keys, n, ao);
+	}
 	unsigned long long *h = (unsigned long long *) pinned(16);
 	if (!hip_ok(hipMemcpyAsync(h, ao, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
 		return -1;
@@ -325,34 +335,36 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 	for (size_t s = 0; s < shifts.size(); s++) {
 		const int shift = shifts[s];
 		const bool fin = fo != nullptr && s + 1 == shifts.size();
+		const bool idv = positions && s == 0;
 		hipLaunchKernelGGL((k_rs_hist<K>), dim3(nblocks), dim3(256), 0, st, kin, n, shift, hist.as<uint32_t>(),
 				   nblocks);
 		if (exclusive_scan(hist.as<uint32_t>(), offs.as<uint32_t>(), (BUN) 256 * nblocks, nullptr) < 0)
 			return -1;
-		if (fin)
-			hipLaunchKernelGGL((k_rs_scatter<K, true>), dim3(nblocks), dim3(256), 0, st, kin, vin, n, shift,
-					   offs.as<uint32_t>(), nblocks, kout, vout, *fo);
-		else
-			hipLaunchKernelGGL((k_rs_scatter<K, false>), dim3(nblocks), dim3(256), 0, st, kin, vin, n, shift,
-					   offs.as<uint32_t>(), nblocks, kout, vout, none);
+		FinalOut f2 = fin ? *fo : none;
+		if (fin && f2.want_keys)
+			f2.keys = kout;
+#define SCAT(F, I) hipLaunchKernelGGL((k_rs_scatter<K, F, I>), dim3(nblocks), dim3(256), 0, st, kin, vin, n, shift, \
+				      offs.as<uint32_t>(), nblocks, kout, vout, f2)
+		if (fin) {
+			if (idv) SCAT(true, true); else SCAT(true, false);
+		} else {
+			if (idv) SCAT(false, true); else SCAT(false, false);
+		}
+#undef SCAT
 		std::swap(kin, kout);
 		std::swap(vin, vout);
 	}
-	if (fo != nullptr && shifts.empty())
-		hipLaunchKernelGGL((k_final_copy<K>), dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st, kin, vin, n, *fo);
+	if (fo != nullptr && shifts.empty()) {
+		FinalOut f2 = *fo;
+		f2.keys = nullptr;            // keys already in order (kin)
+		hipLaunchKernelGGL((k_final_copy<K>), dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st, kin,
+				   positions ? nullptr : vin, n, f2);
+	}
 	if (!sync())
 		return -1;
 	*keys_out = kin;
 	*vals_out = vin;
 	return 0;
-}
-
-template <typename T, typename K>
-void
-launch_keys(const mgdk_bat *b, bool reverse, bool nilslast, K *keys, uint32_t *idx)
-{
-	hipLaunchKernelGGL((k_keys<T, K>), dim3(grid_for(b->count, 1024, 8192)), dim3(256), 0, stream(),
-			   (const T *) b->theap, b->count, reverse, nilslast, keys, idx);
 }
 
 template <typename T>
@@ -363,26 +375,30 @@ launch_gather(const mgdk_bat *b, const oid *order, void *sorted)
 			   (const T *) b->theap, order, b->count, b->hseqbase, (T *) sorted);
 }
 
-// sort b's keys of type T with key width K; fills sn/on (either may be NULL)
-// and, for groups, returns the key images in sorted order in *keys (the
-// caller deletes it)
+// sort b's keys of type T with key width K into sn / on / gn (any may be NULL)
 template <typename T, typename K>
 int
-sort_typed(const mgdk_bat *b, bool reverse, bool nilslast, mgdk_bat *sn, mgdk_bat *on, bool want_keys,
-	   DevBuf **keys)
+sort_typed(const mgdk_bat *b, bool reverse, bool nilslast, mgdk_bat *sn, mgdk_bat *on, mgdk_bat *gn)
 {
 	const BUN n = b->count;
 	constexpr bool is_float = (T) 0.5 != 0;
-	DevBuf k0(n * sizeof(K)), k1(n * sizeof(K)), v0(n * 4), v1(n * 4), otmp(on ? 8 : n * 8);
+	hipStream_t st = stream();
+	DevBuf k0(n * sizeof(K) + 8), k1(n * sizeof(K) + 8), v0(n * 4 + 4), v1(n * 4 + 4), otmp(on ? 8 : n * 8 + 8);
 	if (!k0.p || !k1.p || !v0.p || !v1.p || !otmp.p)
 		return -1;
-	launch_keys<T, K>(b, reverse, nilslast, k0.as<K>(), v0.as<uint32_t>());
+	unsigned long long *ao = (unsigned long long *) meta_buf();
+	unsigned long long init[2] = {~0ull, 0ull};
+	if (!hip_ok(hipMemcpyAsync(ao, init, 16, hipMemcpyHostToDevice, st), "memcpy"))
+		return -1;
+	hipLaunchKernelGGL((k_keys<T, K>), dim3(grid_for(n, 2048, 4096)), dim3(256), 0, st, (const T *) b->theap, n,
+			   reverse, nilslast, k0.as<K>(), ao);
 	FinalOut fo{};
 	fo.vw = b->twidth;
 	fo.reverse = reverse;
 	fo.is64 = sizeof(K) == 8;
 	fo.uns = basetype(b->ttype) == MGDK_oid;
 	fo.hseq = b->hseqbase;
+	fo.want_keys = gn != nullptr;
 	// floats (and reverse != nilslast images) are not decodable: gather by order
 	const bool decodable = !is_float && reverse == nilslast;
 	fo.sorted = decodable && sn ? sn->theap : nullptr;
@@ -390,7 +406,7 @@ sort_typed(const mgdk_bat *b, bool reverse, bool nilslast, mgdk_bat *sn, mgdk_ba
 	K *ks;
 	uint32_t *vs;
 	if (radix_sort<K>(k0.as<K>(), v0.as<uint32_t>(), k1.as<K>(), v1.as<uint32_t>(), n, 8 * (int) sizeof(K), &fo,
-			  &ks, &vs) < 0)
+			  true, true, &ks, &vs) < 0)
 		return -1;
 	if (sn && !decodable) {
 		switch (b->twidth) {
@@ -400,14 +416,24 @@ sort_typed(const mgdk_bat *b, bool reverse, bool nilslast, mgdk_bat *sn, mgdk_ba
 		default: launch_gather<int64_t>(b, fo.order, sn->theap); break;
 		}
 	}
-	if (want_keys) {
-		// the key image of every sorted row, in sorted order
-		DevBuf *kb = new DevBuf(n * sizeof(K) + 8);
-		*keys = kb;
-		if (!kb->p)
+	if (gn) {
+		// groups: a new group wherever the sorted key image changes
+		DevBuf fl(n + 1), ex(n * 8 + 8);
+		uint64_t tot = 0;
+		if (!fl.p || !ex.p)
 			return -1;
-		hipLaunchKernelGGL((k_keys_of_order<T, K>), dim3(grid_for(n, 1024, 8192)), dim3(256), 0, stream(),
-				   (const T *) b->theap, fo.order, n, b->hseqbase, reverse, nilslast, kb->as<K>());
+		hipLaunchKernelGGL((k_newgrp<K>), dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st, ks, n, fl.as<uint8_t>());
+		if (exclusive_scan(fl.as<uint8_t>(), ex.as<uint64_t>(), n, &tot) < 0)
+			return -1;
+		hipLaunchKernelGGL(k_gid, dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st, ex.as<uint64_t>(),
+				   fl.as<uint8_t>(), n, (oid *) gn->theap);
+		if (!sync())
+			return -1;
+		gn->count = n;
+		gn->tsorted = 1;
+		gn->trevsorted = tot == 0;
+		gn->tkey = tot + 1 == n || n <= 1;
+		gn->tnonil = 1;
 	}
 	return sync() ? 0 : -1;
 }
@@ -420,7 +446,8 @@ int
 radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32_t *vals_alt, BUN n, int bits,
 		 uint64_t **keys_out, uint32_t **vals_out)
 {
-	return radix_sort<uint64_t>(keys, vals, keys_alt, vals_alt, n, bits, nullptr, keys_out, vals_out);
+	return radix_sort<uint64_t>(keys, vals, keys_alt, vals_alt, n, bits, nullptr, false, false, keys_out,
+				    vals_out);
 }
 
 }  // namespace mgdk
@@ -471,10 +498,11 @@ mgdk_BATsort(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b
 			goto fail;
 		// 32-bit key images need nil at its natural end (nilslast == reverse)
 		const bool k32 = b->twidth <= 4 && reverse == nilslast;
-		DevBuf *keys = nullptr;
+		gn = groups ? newbat(b->hseqbase, MGDK_oid, n) : nullptr;
+		if (groups && !gn)
+			goto fail;
 		int rc = 0;
-		const bool wk = groups != nullptr;
-#define SORT(T, K) rc = sort_typed<T, K>(b, reverse, nilslast, sn, on, wk, &keys)
+#define SORT(T, K) rc = sort_typed<T, K>(b, reverse, nilslast, sn, on, gn)
 		switch (tt) {
 		case MGDK_bte: if (k32) SORT(int8_t, uint32_t); else SORT(int8_t, uint64_t); break;
 		case MGDK_sht: if (k32) SORT(int16_t, uint32_t); else SORT(int16_t, uint64_t); break;
@@ -485,37 +513,8 @@ mgdk_BATsort(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b
 		case MGDK_dbl: SORT(double, uint64_t); break;
 		}
 #undef SORT
-		if (rc < 0) {
-			delete keys;
+		if (rc < 0)
 			goto fail;
-		}
-		if (groups) {
-			gn = newbat(b->hseqbase, MGDK_oid, n);
-			DevBuf fl(n + 1), ex(n * 8 + 8);
-			uint64_t tot = 0;
-			bool ok = gn && fl.p && ex.p;
-			if (ok) {
-				if (k32)
-					hipLaunchKernelGGL((k_newgrp<uint32_t>), dim3(grid_for(n, 1024, 8192)), dim3(256), 0,
-							   stream(), keys->as<uint32_t>(), n, fl.as<uint8_t>());
-				else
-					hipLaunchKernelGGL((k_newgrp<uint64_t>), dim3(grid_for(n, 1024, 8192)), dim3(256), 0,
-							   stream(), keys->as<uint64_t>(), n, fl.as<uint8_t>());
-				ok = exclusive_scan(fl.as<uint8_t>(), ex.as<uint64_t>(), n, &tot) >= 0;
-			}
-			if (ok)
-				hipLaunchKernelGGL(k_gid, dim3(grid_for(n, 1024, 8192)), dim3(256), 0, stream(),
-						   ex.as<uint64_t>(), fl.as<uint8_t>(), n, (oid *) gn->theap);
-			ok = ok && sync();
-			delete keys;
-			if (!ok)
-				goto fail;
-			gn->count = n;
-			gn->tsorted = 1;
-			gn->trevsorted = tot == 0;
-			gn->tkey = tot + 1 == n || n <= 1;
-			gn->tnonil = 1;
-		}
 		if (sn) {
 			sn->count = n;
 			sn->tsorted = !reverse || n <= 1;
