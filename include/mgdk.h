@@ -172,6 +172,25 @@ int mgdk_tpch_lineitem(uint64_t seed, uint64_t row0, uint64_t n, uint64_t sf_par
 int mgdk_gen_window_column(uint64_t seed, uint64_t n, uint64_t plen, mgdk_bat **vals,
 			   mgdk_bat **parts);
 
+/* ---- multi-GPU exchange steps (SURVEY.md §8 e).  The reference shards a
+ *      plan by row ranges (opt_mitosis.c:150-230) and re-aggregates packed
+ *      partials (opt_mergetable.c:1496-1885); across GPUs the group / join
+ *      shuffles need a partitioning by VALUE and RCCL buffers: ----------- */
+/* order := positions of b (as oids, hseqbase-based) grouped by destination
+ * part hash(value) mod-scaled to [0, nparts), stable inside a part;
+ * counts[nparts] rows per part.  Integer types and void. */
+int mgdk_BAThashpartition(mgdk_bat **order, mgdk_bat *b, int nparts, uint64_t *counts);
+/* out[q] = number of rows of the run sorted by (keys, pos) that are below
+ * (qk[q], qp[q]); pos NULL: positions 0..n-1 (sample-sort splitters) */
+int mgdk_BATlowerbound2(const mgdk_bat *keys, const mgdk_bat *pos, const int64_t *qk, const uint64_t *qp,
+			int nq, uint64_t *out);
+/* gdk_batop.c:1011 BATappend: append the candidates s of n to b in place
+ * (fixed-width tails) */
+int mgdk_BATappend(mgdk_bat *b, mgdk_bat *n, mgdk_bat *s, bool force);
+/* device-to-device copies between a BAT tail and a device buffer (RCCL) */
+int mgdk_BATupload_device(mgdk_bat *b, const void *dev, mgdk_BUN n);
+int mgdk_BATdownload_device(const mgdk_bat *b, void *dev);
+
 #ifdef __cplusplus
 }
 #endif

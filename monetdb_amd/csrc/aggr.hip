@@ -187,6 +187,7 @@ put_res(void *res, int tp, hge v, bool nil)
 	case MGDK_sht: *(int16_t *) res = nil ? INT16_MIN : (int16_t) v; break;
 	case MGDK_int: *(int32_t *) res = nil ? INT32_MIN : (int32_t) v; break;
 	case MGDK_lng: *(int64_t *) res = nil ? INT64_MIN : (int64_t) v; break;
+	case MGDK_oid: *(uint64_t *) res = nil ? MGDK_OID_NIL : (uint64_t) v; break;
 	default: { hge x = nil ? (hge) ((uhge) 1 << 127) : v; memcpy(res, &x, 16); break; }
 	}
 }
@@ -700,7 +701,8 @@ mgdk_BATgroupavg3(mgdk_bat **avgp, mgdk_bat **remp, mgdk_bat **cntp, mgdk_bat *b
 static mgdk_bat *
 groupminmax(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, bool skip_nils, bool domax)
 {
-	if (b == nullptr || !int_type(b->ttype) || basetype(b->ttype) == MGDK_hge) {
+	// oids (< 2^63, nil = 2^63) order like their signed 64-bit images
+	if (b == nullptr || !(int_type(b->ttype) || b->ttype == MGDK_oid) || basetype(b->ttype) == MGDK_hge) {
 		seterr("42000!BATgroupmin/max: type not supported on the device path");
 		return nullptr;
 	}

@@ -42,6 +42,8 @@ struct Priv {
 	Heap *tvheap;
 	size_t toff;      // byte offset of b->theap into theap->base
 };
+Heap *heap_new(size_t bytes);                    // refs = 1
+void heap_decref(Heap *h);
 mgdk_bat *newbat(oid hseq, int tt, BUN cap);     // allocates tail heap
 void setdense(mgdk_bat *b, oid tseq, BUN cnt);
 void share_vheap(mgdk_bat *dst, const mgdk_bat *src);
@@ -91,6 +93,11 @@ int exclusive_scan(const uint8_t *in, uint64_t *out, BUN n, uint64_t *total);
 // Returns the buffers holding the result (the input pair or the spare).
 int radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32_t *vals_alt,
 		     BUN n, int bits, uint64_t **keys_out, uint32_t **vals_out);
+
+// stable sort of the positions 0..n-1 by 32-bit keys (sort.hip); when no
+// pass is needed (all keys equal) *perm is left NULL: identity
+int radix_sort_positions32(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, uint32_t *vals_alt, BUN n,
+			   int bits, uint32_t **perm);
 
 // RAII device temporary (not the per-thread scratch)
 struct DevBuf {

@@ -263,7 +263,7 @@ atomname(int tt)
 	return "any";
 }
 
-static Heap *
+Heap *
 heap_new(size_t bytes)
 {
 	Heap *h = new Heap;
@@ -277,7 +277,7 @@ heap_new(size_t bytes)
 	return h;
 }
 
-static void
+void
 heap_decref(Heap *h)
 {
 	if (h == nullptr)
@@ -689,3 +689,120 @@ mgdk_BATdownload_vheap(const mgdk_bat *b, void *host)
 }
 
 }  // extern "C"
+
+// BATappend (gdk/gdk_batop.c:1011 -> BATappend2 :674): append the candidates
+// s of n to b in place.  Fixed-width tails only (str would need heap
+// merging); a void b stays void while n continues its sequence.  The tail
+// heap grows geometrically; a heap shared with views is copied first.
+__global__ void
+k_fill_seq(oid *out, BUN n, oid seq)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
+		out[i] = seq == MGDK_OID_NIL ? MGDK_OID_NIL : seq + i;
+}
+
+extern "C" int
+mgdk_BATappend(mgdk_bat *b, mgdk_bat *n, mgdk_bat *s, bool force)
+{
+	(void) force;
+	if (b == nullptr || n == nullptr) {
+		seterr("BATappend: NULL argument");
+		return -1;
+	}
+	mgdk_bat *src = n, *proj = nullptr;
+	if (s) {
+		proj = mgdk_BATproject(s, n);
+		if (proj == nullptr)
+			return -1;
+		src = proj;
+	}
+	const BUN cnt = src->count;
+	int rc = -1;
+	if (cnt == 0) {
+		rc = 0;
+		goto out;
+	}
+	if (b->ttype == MGDK_str || src->ttype == MGDK_str) {
+		seterr("42000!BATappend: str tails are not supported on the device path");
+		goto out;
+	}
+	{
+		const int bt = basetype(b->ttype == MGDK_void ? MGDK_oid : b->ttype);
+		const int nt = basetype(src->ttype == MGDK_void ? MGDK_oid : src->ttype);
+		if (b->count > 0 && bt != nt) {
+			seterr("Incompatible operands (%s vs. %s).\n", atomname(b->ttype), atomname(src->ttype));
+			goto out;
+		}
+		if (b->count == 0 && b->ttype != src->ttype && b->ttype != MGDK_void && bt != nt) {
+			seterr("Incompatible operands (%s vs. %s).\n", atomname(b->ttype), atomname(src->ttype));
+			goto out;
+		}
+	}
+	// void + continuing dense sequence stays void
+	if (b->ttype == MGDK_void && src->ttype == MGDK_void &&
+	    (b->count == 0 || (b->tseqbase != MGDK_OID_NIL && src->tseqbase == b->tseqbase + b->count))) {
+		if (b->count == 0)
+			b->tseqbase = src->tseqbase;
+		b->count += cnt;
+		b->trevsorted = b->count <= 1;
+		rc = 0;
+		goto out;
+	}
+	{
+		Priv *p = (Priv *) b->priv;
+		hipStream_t st = stream();
+		const int tt = b->ttype == MGDK_void ? MGDK_oid : b->ttype;
+		const size_t w = (size_t) width_of(tt);
+		const BUN total = b->count + cnt;
+		const size_t used_off = p->theap ? (size_t) ((char *) b->theap - (char *) p->theap->base) : 0;
+		const bool fits = b->ttype != MGDK_void && p->theap && p->theap->refs == 1 &&
+				  p->theap->size >= used_off + total * w;
+		if (!fits) {
+			size_t cap = total * w;
+			if (p->theap && b->ttype != MGDK_void)
+				cap = cap < 2 * b->count * w ? 2 * b->count * w : cap;
+			Heap *h = heap_new(cap);
+			if (h == nullptr)
+				goto out;
+			if (b->count) {
+				if (b->ttype == MGDK_void)
+					hipLaunchKernelGGL(k_fill_seq, dim3(grid_for(b->count, 1024, 4096)), dim3(256), 0, st,
+							   (oid *) h->base, b->count, b->tseqbase);
+				else if (!hip_ok(hipMemcpyAsync(h->base, b->theap, b->count * w, hipMemcpyDeviceToDevice, st),
+						 "memcpy D2D")) {
+					heap_decref(h);
+					goto out;
+				}
+			}
+			heap_decref(p->theap);
+			p->theap = h;
+			b->theap = h->base;
+			if (b->ttype == MGDK_void) {
+				b->ttype = MGDK_oid;
+				b->twidth = 8;
+				b->tseqbase = MGDK_OID_NIL;
+			}
+		}
+		char *dst = (char *) b->theap + b->count * w;
+		if (src->ttype == MGDK_void)
+			hipLaunchKernelGGL(k_fill_seq, dim3(grid_for(cnt, 1024, 4096)), dim3(256), 0, st, (oid *) dst, cnt,
+					   src->tseqbase);
+		else if (!hip_ok(hipMemcpyAsync(dst, src->theap, cnt * w, hipMemcpyDeviceToDevice, st), "memcpy D2D"))
+			goto out;
+		if (!sync())
+			goto out;
+		const bool wasempty = b->count == 0;
+		b->count = total;
+		// properties the append cannot vouch for are cleared (BATappend2
+		// keeps them only after comparing the boundary values)
+		b->tnonil = (wasempty || b->tnonil) && src->tnonil;
+		b->tnil = (!wasempty && b->tnil) || src->tnil;
+		b->tsorted = wasempty ? src->tsorted : total <= 1;
+		b->trevsorted = wasempty ? src->trevsorted : total <= 1;
+		b->tkey = wasempty ? src->tkey : total <= 1;
+		rc = 0;
+	}
+out:
+	mgdk_BBPunfix(proj);
+	return rc;
+}

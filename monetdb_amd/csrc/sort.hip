@@ -363,7 +363,7 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 	if (!sync())
 		return -1;
 	*keys_out = kin;
-	*vals_out = vin;
+	*vals_out = positions && shifts.empty() ? nullptr : vin;   // NULL: identity
 	return 0;
 }
 
@@ -448,6 +448,18 @@ radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32_t *v
 {
 	return radix_sort<uint64_t>(keys, vals, keys_alt, vals_alt, n, bits, nullptr, false, false, keys_out,
 				    vals_out);
+}
+
+// stable counting sort of positions 0..n-1 by 32-bit keys (e.g. a
+// destination rank); *perm receives the buffer holding the permutation
+int
+radix_sort_positions32(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, uint32_t *vals_alt, BUN n, int bits,
+		       uint32_t **perm)
+{
+	uint32_t *ko;
+	if (radix_sort<uint32_t>(keys, vals, keys_alt, vals_alt, n, bits, nullptr, true, false, &ko, perm) < 0)
+		return -1;
+	return 0;
 }
 
 }  // namespace mgdk

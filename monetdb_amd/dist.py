@@ -1,12 +1,32 @@
-"""Multi-GPU plumbing for the row-range sharded pipelines.
+"""Multi-GPU plumbing: row-range shards and the exchange steps of SURVEY.md §8(e).
 
-One process per GPU (torchrun); rank r owns lineitem rows [r*N, (r+1)*N) in
-its own HBM -- the mitosis partitioning of opt_mitosis.c:150-230 -- and the
-per-rank partial aggregates are combined the way mergetable re-aggregates
-packed partials (opt_mergetable.c:1496-1670): exact 128-bit sums, counts, and
-group keys renumbered by global first occurrence.  The only collectives are
-all_gathers of a few dozen bytes (RCCL over xGMI with backend "nccl", or gloo
-on the CPU in tests).
+One process per GPU (torchrun); rank r owns a row range of every input in its
+own HBM -- the mitosis partitioning of opt_mitosis.c:150-230 -- and partial
+results are combined the way mergetable re-aggregates packed partials
+(opt_mergetable.c:1496-1885):
+
+  * select / calc / sum / Q6 / Q1: no data exchange; exact 128-bit partial
+    sums, counts and group keys all-gathered (combine_hge, combine_q1);
+  * group + aggregates: local BATgroup + BATgroupsum per rank, the partial
+    (key, first row, count, sums) rows hash-partitioned by key and shuffled
+    with ONE all_to_all, merged by a second BATgroup on the owner, and group
+    ids renumbered in global first-occurrence order (dist_group_aggr);
+  * hash join: both sides hash-partitioned by key and shuffled, joined on the
+    owner, the (l, r) pairs shuffled back to the left row's home rank and
+    restored to the reference order by a stable sort on l (dist_join);
+  * sort: local stable sort, (key, position) splitters from an all-gathered
+    sample, one all_to_all of the runs, stable merge sort per rank
+    (dist_sort);
+  * RANGE window bounds: shards re-cut at partition starts -- the rows before
+    a rank's first partition start move to the rank where that partition
+    began -- then bounds are local (dist_window_bounds).
+
+The algorithms are written once against a small backend interface: GdkBackend
+runs the local operators through libmgdk on this rank's GPU and exchanges
+device buffers with RCCL (torch.distributed backend "nccl"); the tests run the
+same code with an oracle backend over gloo on the CPU.  Exchanged columns are
+packed into one (rows, k) int64 tensor per shuffle (hge = two words), so each
+shuffle is a count exchange plus a single all_to_all_single.
 """
 
 MASK64 = (1 << 64) - 1
@@ -22,18 +42,37 @@ def _from_words(lo, hi):
     return v - (1 << 128) if v >= (1 << 127) else v
 
 
+def _s64(v):
+    v &= MASK64
+    return v - (1 << 64) if v >= (1 << 63) else v
+
+
 def shard(rows_per_rank, rank):
     """Row range [row0, row0 + n) of `rank` under weak scaling."""
     return rank * rows_per_rank, rows_per_rank
 
 
+def _world(dist):
+    if dist is None or not dist.is_initialized():
+        return 1, 0
+    return dist.get_world_size(), dist.get_rank()
+
+
 def _gather_int64(dist, device, vals):
     import torch
-    t = torch.tensor([v - (1 << 64) if v >= (1 << 63) else v for v in vals], dtype=torch.int64,
-                     device=device)
+    t = torch.tensor([_s64(v) for v in vals], dtype=torch.int64, device=device)
     out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(out, t)
     return [[int(x) & MASK64 for x in o.cpu().tolist()] for o in out]
+
+
+def _gather_var(dist, device, vals):
+    """all_gather of a variable-length list of int64 per rank."""
+    n = len(vals)
+    counts = [c[0] for c in _gather_int64(dist, device, [n])]
+    m = max(counts) if counts else 0
+    parts = _gather_int64(dist, device, list(vals) + [0] * (m - n))
+    return [[_s64(x) for x in p[:c]] for p, c in zip(parts, counts)]
 
 
 def combine_hge(value, dist=None, device="cpu"):
@@ -90,3 +129,320 @@ def avg3(total, count):
         elif 2 * r >= count:
             q, r = q + 1, r - count
     return q, r
+
+
+# ---------------------------------------------------------------------------
+# backend: libmgdk on this rank's GPU, RCCL on torch device buffers
+# ---------------------------------------------------------------------------
+
+class GdkBackend:
+    """Local operators of one rank through libmgdk (device BATs); packing
+    into / out of torch tensors on the same GPU for the collectives."""
+
+    def __init__(self, device):
+        from monetdb_amd import gdk
+        self.gdk = gdk
+        self.device = device
+
+    # -- columns -------------------------------------------------------------
+    def n(self, c):
+        return c.count()
+
+    def column(self, tp, values, hseq=0):
+        import numpy as np
+        return self.gdk.BAT.from_numpy(tp, np.asarray(values), hseqbase=hseq)
+
+    def values(self, c):
+        return c.values()          # numpy; hge as Python ints
+
+    def widen(self, c):
+        g = self.gdk
+        if c.ttype in (g.TYPE_lng, g.TYPE_oid):
+            return c
+        return g.BATcalcaddcst(c, 0, g.TYPE_lng, g.TYPE_lng)
+
+    def zeros_bit(self, n):
+        return self.gdk.BATconstant(self.gdk.TYPE_bit, 0, n)
+
+    def append(self, b, n):
+        return self.gdk.BATappend(b, n)
+
+    def copy(self, c):
+        g = self.gdk
+        return g.BATappend(g.BAT(g.lib().mgdk_COLnew(c.hseqbase, c.ttype, max(1, c.count()))), c)
+
+    def slice(self, c, lo, hi):
+        return self.gdk.BATslice(c, lo, hi)
+
+    # -- operators -----------------------------------------------------------
+    def hashpartition(self, c, nparts):
+        return self.gdk.BAThashpartition(c, nparts)
+
+    def project(self, order, c):
+        return self.gdk.BATproject(order, c)
+
+    def group(self, c):
+        return self.gdk.BATgroup(c)
+
+    def groupsum(self, c, g, e, tp):
+        return self.gdk.BATgroupsum(c, g, e, tp)
+
+    def groupmin(self, c, g, e):
+        return self.gdk.BATgroupmin(c, g, e)
+
+    def join(self, l, r):
+        return self.gdk.BATjoin(l, r)
+
+    def sort(self, c):
+        s, o, _ = self.gdk.BATsort(c)
+        return s, o
+
+    def lowerbound2(self, keys, pos, qk, qp):
+        return self.gdk.BATlowerbound2(keys, pos, qk, qp)
+
+    def rangebounds(self, vals, parts, limit, preceding):
+        return self.gdk.GDKanalyticalwindowbounds(vals, parts, limit, preceding)
+
+    def first_start(self, parts):
+        """first position with a partition start bit, or None"""
+        s = self.gdk.BATthetaselect(parts, None, 1, "==")
+        if s.count() == 0:
+            return None
+        return int(self.gdk.BATslice(s, 0, 1).to_numpy()[0]) - parts.hseqbase
+
+    # -- packing -------------------------------------------------------------
+    def pack(self, cols):
+        """(rows, k) int64 tensor of 8-byte and hge (2 words) columns, on the
+        GPU (RCCL) or staged through the host for a gloo rehearsal"""
+        import torch
+        g = self.gdk
+        n = cols[0].count() if cols else 0
+        if self.device == "cpu":
+            parts = []
+            for c in cols:
+                a = c.to_numpy()
+                parts.append(a.view("int64").reshape(n, 2) if c.ttype == g.TYPE_hge
+                             else a.astype("int64", copy=False).reshape(n, 1))
+            import numpy as np
+            return torch.from_numpy(np.ascontiguousarray(np.concatenate(parts, axis=1)))
+        width = sum(2 if c.ttype == g.TYPE_hge else 1 for c in cols)
+        out = torch.empty((width, n), dtype=torch.int64, device=self.device)
+        j = 0
+        for c in cols:
+            if c.ttype == g.TYPE_hge:
+                t = torch.empty((n, 2), dtype=torch.int64, device=self.device)
+                if n:
+                    g.BATdownload_device(c, t.data_ptr())
+                out[j:j + 2] = t.t()
+                j += 2
+            else:
+                if n:
+                    g.BATdownload_device(c, out[j].data_ptr())
+                j += 1
+        return out.t().contiguous()
+
+    def unpack(self, t, types, hseq=0):
+        import torch
+        g = self.gdk
+        n = t.shape[0]
+        cols, j = [], 0
+        if self.device == "cpu":
+            a = t.numpy()
+            for tp in types:
+                if tp == g.TYPE_hge:
+                    cols.append(g.BAT.from_numpy(tp, a[:, j:j + 2].view("uint64"), hseqbase=hseq))
+                    j += 2
+                else:
+                    cols.append(g.BAT.from_numpy(tp, a[:, j].astype(g.NP[tp]), hseqbase=hseq))
+                    j += 1
+            return cols
+        torch.cuda.current_stream(t.device).synchronize()   # collectives ran on torch's stream
+        for tp in types:
+            if tp == g.TYPE_hge:
+                src = t[:, j:j + 2].contiguous()
+                j += 2
+            else:
+                src = t[:, j].contiguous()
+                j += 1
+            b = g.BAT(g.lib().mgdk_COLnew(hseq, tp, max(n, 1)))
+            g.BATupload_device(b, src.data_ptr() if n else 0, n)
+            cols.append(b)
+        return cols
+
+
+def _exchange(dist, device, packed, send_counts):
+    """all_to_all of a (rows, k) int64 tensor whose rows are grouped by
+    destination rank (send_counts[d] rows for rank d)."""
+    import torch
+    sc = torch.tensor(send_counts, dtype=torch.int64, device=device)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc)
+    recv = [int(x) for x in rc.cpu().tolist()]
+    out = torch.empty((sum(recv), packed.shape[1]), dtype=torch.int64, device=device)
+    dist.all_to_all_single(out, packed, recv, list(send_counts))
+    return out, recv
+
+
+def _types(be):
+    g = getattr(be, "gdk", None) or be
+    return g.TYPE_lng, g.TYPE_oid, g.TYPE_hge
+
+
+# ---------------------------------------------------------------------------
+# group + aggregates
+# ---------------------------------------------------------------------------
+
+def dist_group_aggr(be, dist, keys, vals):
+    """GROUP BY keys with exact sums of `vals` (lng columns) and counts.
+
+    keys/vals: this rank's shard, hseqbase = the shard's first global row.
+    Returns the groups OWNED by this rank (hash of the key), as a list of
+    dicts {gid, key, first_row, count, sums} with gid = the group's number in
+    global first-occurrence order (what BATgroup over all rows would give).
+    """
+    TL, TO, TH = _types(be)
+    world, rank = _world(dist)
+    g, e, h = be.group(keys)
+    parts = [be.widen(be.project(e, keys)), e, h] + [be.groupsum(v, g, e, TH) for v in vals]
+    if world > 1:
+        order, counts = be.hashpartition(parts[0], world)
+        parts = [be.project(order, c) for c in parts]
+        recv, _ = _exchange(dist, be.device, be.pack(parts), counts)
+        parts = be.unpack(recv, [TL, TO, TL] + [TH] * len(vals))
+    rk, rfirst, rcount, rsums = parts[0], parts[1], parts[2], parts[3:]
+    if be.n(rk) == 0:
+        mine = []
+    else:
+        g2, e2, _ = be.group(rk)
+        mk = be.values(be.project(e2, rk))
+        mf = be.values(be.groupmin(rfirst, g2, e2))
+        mc = be.values(be.groupsum(rcount, g2, e2, TL))
+        ms = [be.values(be.groupsum(s, g2, e2, TH)) for s in rsums]
+        mine = [{"key": int(mk[i]), "first_row": int(mf[i]), "count": int(mc[i]),
+                 "sums": [int(s[i]) for s in ms]} for i in range(len(mk))]
+    # global first-occurrence numbering
+    firsts = [m["first_row"] for m in mine]
+    allf = sorted(x for part in (_gather_var(dist, be.device, firsts) if world > 1 else [firsts])
+                  for x in part)
+    pos = {f: i for i, f in enumerate(allf)}
+    for m in mine:
+        m["gid"] = pos[m["first_row"]]
+    return sorted(mine, key=lambda m: m["gid"])
+
+
+# ---------------------------------------------------------------------------
+# hash join
+# ---------------------------------------------------------------------------
+
+def dist_join(be, dist, lkeys, rkeys, lrows_per_rank):
+    """BATjoin(l, r) over sharded sides.  lkeys/rkeys have hseqbase = their
+    shard's first global row.  Returns this rank's (r1, r2) for the left rows
+    it owns, in the reference order (left order, matches of a left row in
+    descending right position); the concatenation over ranks is the global
+    result."""
+    TL, TO, _ = _types(be)
+    world, rank = _world(dist)
+    if world == 1:
+        return be.join(lkeys, rkeys)
+    sides = []
+    for c in (lkeys, rkeys):
+        w = be.widen(c)
+        order, counts = be.hashpartition(w, world)
+        packed = be.pack([be.project(order, w), order])
+        recv, _ = _exchange(dist, be.device, packed, counts)
+        sides.append(be.unpack(recv, [TL, TO]))
+    (lk, lo), (rk, ro) = sides
+    # sources arrive in rank order and keep their order: lo and ro ascend
+    j1, j2 = be.join(lk, rk)
+    r1, r2 = be.project(j1, lo), be.project(j2, ro)
+    # back to the left row's home rank; r1 ascends, so the split is by bounds
+    cuts = be.lowerbound2(r1, None, [d * lrows_per_rank for d in range(1, world)], [0] * (world - 1))
+    edges = [0] + cuts + [be.n(r1)]
+    counts = [edges[d + 1] - edges[d] for d in range(world)]
+    recv, _ = _exchange(dist, be.device, be.pack([r1, r2]), counts)
+    a, b = be.unpack(recv, [TO, TO])
+    # owners' runs interleave in l; a stable sort on l restores the order
+    # (all matches of one left row come from one owner, already descending)
+    _, order = be.sort(a)
+    return be.project(order, a), be.project(order, b)
+
+
+# ---------------------------------------------------------------------------
+# sort
+# ---------------------------------------------------------------------------
+
+def dist_sort(be, dist, keys, sample=64):
+    """Stable ascending sort of a sharded column (hseqbase = the shard's first
+    global row).  Returns this rank's slice of the global result: (sorted
+    keys widened to lng, order oids = global positions)."""
+    TL, TO, _ = _types(be)
+    world, rank = _world(dist)
+    w = be.widen(keys)
+    s, o = be.sort(w)
+    if world == 1:
+        return s, o
+    n = be.n(s)
+    sv, ov = be.values(s), be.values(o)
+    idx = [(i * n) // sample for i in range(sample)] if n else []
+    samp = []
+    for i in idx:
+        samp += [int(sv[i]), int(ov[i])]
+    allp = _gather_var(dist, be.device, samp)
+    pairs = sorted((p[i], p[i + 1]) for p in allp for i in range(0, len(p), 2))
+    spl = [pairs[(d * len(pairs)) // world] for d in range(1, world)] if pairs else []
+    cuts = be.lowerbound2(s, o, [k for k, _ in spl], [p for _, p in spl]) if spl else [n] * (world - 1)
+    edges = [0] + list(cuts) + [n]
+    counts = [edges[d + 1] - edges[d] for d in range(world)]
+    recv, _ = _exchange(dist, be.device, be.pack([s, o]), counts)
+    k2, p2 = be.unpack(recv, [TL, TO])
+    if be.n(k2) == 0:
+        return k2, p2
+    # runs arrive in rank order = ascending positions among equal keys, so
+    # a stable sort by key alone gives the global stable order
+    s3, o3 = be.sort(k2)
+    return s3, be.project(o3, p2)
+
+
+# ---------------------------------------------------------------------------
+# RANGE window bounds
+# ---------------------------------------------------------------------------
+
+def dist_window_bounds(be, dist, vals, parts, limit, preceding):
+    """GDKanalyticalwindowbounds over row-range shards.  The rows before a
+    rank's first partition start belong to a partition that began on an
+    earlier rank: they move to that rank (one all_to_all), so every rank
+    holds whole partitions and computes its bounds locally.  Returns
+    (first global row held, bounds as global row numbers) for the rows this
+    rank holds after the move."""
+    TL, TO, _ = _types(be)
+    world, rank = _world(dist)
+    row0 = vals.hseqbase
+    n = be.n(vals)
+    if world == 1:
+        b = be.rangebounds(vals, parts, limit, preceding)
+        return row0, be.values(b).astype("int64") + row0
+    fs = be.first_start(parts)
+    starts = [_s64(x[0]) for x in _gather_int64(dist, be.device, [fs if fs is not None else -1])]
+    lead = 0 if rank == 0 else (n if fs is None else fs)
+    owner = rank
+    if rank > 0:
+        owner = rank - 1
+        while owner > 0 and starts[owner] < 0:
+            owner -= 1
+    counts = [0] * world
+    counts[owner] = lead
+    w = be.widen(vals)
+    recv, _ = _exchange(dist, be.device, be.pack([be.slice(w, 0, lead)]), counts)
+    (rv,) = be.unpack(recv, [TL])
+    # kept rows [lead, n), then the leading rows of later ranks (they
+    # arrive in rank order and carry no partition start)
+    v2 = be.copy(be.slice(w, lead, n))
+    p2 = be.copy(be.slice(parts, lead, n))
+    if be.n(rv):
+        be.append(v2, rv)
+        be.append(p2, be.zeros_bit(be.n(rv)))
+    kept_first = row0 + lead
+    if be.n(v2) == 0:
+        return kept_first, be.values(v2).astype("int64")
+    b = be.rangebounds(v2, p2, limit, preceding)
+    return kept_first, be.values(b).astype("int64") + kept_first

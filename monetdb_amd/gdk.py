@@ -113,6 +113,12 @@ _SIGS = {
                                     C.POINTER(C.c_int)]),
     "mgdk_tpch_lineitem": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, PP]),
     "mgdk_gen_window_column": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, PP, PP]),
+    "mgdk_BAThashpartition": (C.c_int, [PP, C.c_void_p, C.c_int, C.c_void_p]),
+    "mgdk_BATlowerbound2": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                      C.c_void_p]),
+    "mgdk_BATupload_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
+    "mgdk_BATappend": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_bool]),
+    "mgdk_BATdownload_device": (C.c_int, [C.c_void_p, C.c_void_p]),
 }
 
 
@@ -470,3 +476,47 @@ def prof_get(kernel):
 
 def prof_reset():
     lib().mgdk_prof_reset()
+
+
+# ---- multi-GPU exchange helpers ------------------------------------------------
+
+def BAThashpartition(b, nparts):
+    """(order BAT, counts list): positions of b grouped by destination part."""
+    o = P()
+    cnt = (C.c_uint64 * nparts)()
+    _chk(lib().mgdk_BAThashpartition(C.byref(o), b.ptr, nparts, C.cast(cnt, C.c_void_p)))
+    return BAT(o), [int(c) for c in cnt]
+
+
+def BATlowerbound2(keys, pos, qk, qp):
+    nq = len(qk)
+    k = (C.c_int64 * max(1, nq))(*[int(x) for x in qk])
+    p = (C.c_uint64 * max(1, nq))(*[int(x) for x in qp])
+    out = (C.c_uint64 * max(1, nq))()
+    _chk(lib().mgdk_BATlowerbound2(keys.ptr, _p(pos), C.cast(k, C.c_void_p), C.cast(p, C.c_void_p), nq,
+                                   C.cast(out, C.c_void_p)))
+    return [int(x) for x in out[:nq]]
+
+
+def BATslice(b, lo, hi):
+    """View of rows [lo, hi) sharing b's heap (gdk_batop.c BATslice)."""
+    return BAT(lib().mgdk_BATslice(b.ptr, lo, hi))
+
+
+def BATconstant(tp, val, n, hseqbase=0):
+    keep = []
+    return BAT(lib().mgdk_BATconstant(hseqbase, tp, _valptr(tp, val, keep), n))
+
+
+def BATappend(b, n, s=None, force=False):
+    """Append (the candidates s of) n to b in place (gdk_batop.c:1011)."""
+    _chk(lib().mgdk_BATappend(b.ptr, n.ptr, _p(s), force))
+    return b
+
+
+def BATupload_device(b, dev_ptr, n):
+    _chk(lib().mgdk_BATupload_device(b.ptr, C.c_void_p(dev_ptr), n))
+
+
+def BATdownload_device(b, dev_ptr):
+    _chk(lib().mgdk_BATdownload_device(b.ptr, C.c_void_p(dev_ptr)))

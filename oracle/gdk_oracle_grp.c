@@ -235,11 +235,12 @@ static void
 put(int tp, void *base, uint64_t i, ora_hge v, bool nil)
 {
 	switch (tp) {
-	case ORA_bte: ((int8_t *) base)[i] = nil ? INT8_MIN : (int8_t) v; break;
+	case ORA_bit: case ORA_bte: ((int8_t *) base)[i] = nil ? INT8_MIN : (int8_t) v; break;
 	case ORA_sht: ((int16_t *) base)[i] = nil ? INT16_MIN : (int16_t) v; break;
 	case ORA_int: ((int32_t *) base)[i] = nil ? INT32_MIN : (int32_t) v; break;
 	case ORA_lng: ((int64_t *) base)[i] = nil ? INT64_MIN : (int64_t) v; break;
 	case ORA_hge: ((ora_hge *) base)[i] = nil ? HGE_NIL : v; break;
+	case ORA_oid: ((ora_oid *) base)[i] = nil ? ORA_OID_NIL : (ora_oid) v; break;
 	}
 }
 

@@ -81,3 +81,116 @@ def test_combine_single_process_is_identity():
     rows = [{"first_row": 5, "x": 1}, {"first_row": 2, "x": 2}]
     assert [r["first_row"] for r in D.combine_q1(rows)] == [2, 5]
     assert D.avg3(3, 2) == (2, -1) and D.avg3(-3, 2) == (-2, 1) and D.avg3(23, 3) == (8, -1)
+
+
+# ---- exchange steps (dist_group_aggr / dist_join / dist_sort / dist_window_bounds)
+
+def _exchange_worker(rank, world, port, out_dir, backend="oracle"):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import torch
+    import torch.distributed as dist
+
+    from dist_backends import OracleBackend
+    from monetdb_amd import dist as D
+    from oracle import pyoracle as ora
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    if backend == "gdk":
+        # the product operators on the GPU; shuffles staged through the host (gloo)
+        from monetdb_amd import gdk
+        gdk.init(0)
+        be = D.GdkBackend("cpu")
+    else:
+        be = OracleBackend()
+
+    def Col(tp, arr, hseq):     # noqa: N802 -- a column of the active backend
+        return be.column(tp, arr, hseq)
+    errs = []
+    r = np.random.default_rng(7)
+    per = 6_000
+    N = per * world
+    keys = r.integers(0, 700, N).astype(np.int32)
+    keys[r.random(N) < 0.02] = np.iinfo(np.int32).min           # nils group together
+    v1 = r.integers(-10**12, 10**12, N).astype(np.int64)
+    v2 = r.integers(0, 100, N).astype(np.int64)
+    lo, hi = rank * per, (rank + 1) * per
+
+    # group + sums
+    got = D.dist_group_aggr(be, dist, Col(ora.TYPE_int, keys[lo:hi], lo),
+                            [Col(ora.TYPE_lng, v1[lo:hi], lo), Col(ora.TYPE_lng, v2[lo:hi], lo)])
+    g, e, h = ora.BATgroup(ora.Bat.from_array(ora.TYPE_int, keys))
+    ev, hv = e.values().astype(np.int64), h.values()
+    s1 = ora.BATgroupsum(ora.Bat.from_array(ora.TYPE_lng, v1), g, e, ora.TYPE_hge).values()
+    s2 = ora.BATgroupsum(ora.Bat.from_array(ora.TYPE_lng, v2), g, e, ora.TYPE_hge).values()
+    for m in got:
+        i = m["gid"]
+        want = (int(keys[ev[i]]) if keys[ev[i]] != np.iinfo(np.int32).min else np.iinfo(np.int64).min,
+                int(ev[i]), int(hv[i]), [int(s1[i]), int(s2[i])])
+        if (m["key"], m["first_row"], m["count"], m["sums"]) != want:
+            errs.append("group %d: %r != %r" % (i, m, want))
+            break
+    tot = torch.tensor([len(got)])
+    dist.all_reduce(tot)
+    if int(tot) != len(ev):
+        errs.append("groups %d != %d" % (int(tot), len(ev)))
+
+    # hash join, duplicates on both sides
+    lk = r.integers(0, 3000, N).astype(np.int32)
+    rk = r.integers(0, 3000, N).astype(np.int32)
+    a, b = D.dist_join(be, dist, Col(ora.TYPE_int, lk[lo:hi], lo), Col(ora.TYPE_int, rk[lo:hi], lo), per)
+    wa, wb = ora.BATjoin(ora.Bat.from_array(ora.TYPE_int, lk), ora.Bat.from_array(ora.TYPE_int, rk))
+    wa, wb = wa.values(), wb.values()
+    sel = (wa >= lo) & (wa < hi)
+    if not (np.array_equal(be.values(a), wa[sel]) and np.array_equal(be.values(b), wb[sel])):
+        errs.append("join mismatch")
+
+    # stable sort
+    sk = r.integers(-50, 50, N).astype(np.int64)
+    s, o = D.dist_sort(be, dist, Col(ora.TYPE_lng, sk[lo:hi], lo), sample=16)
+    ws, wo = ora.BATsort(ora.Bat.from_array(ora.TYPE_lng, sk))
+    sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(sizes, torch.tensor([be.n(s)]))
+    off = sum(int(x) for x in sizes[:rank])
+    if not (np.array_equal(be.values(s), ws.values()[off:off + be.n(s)]) and
+            np.array_equal(be.values(o), wo.values()[off:off + be.n(s)])):
+        errs.append("sort mismatch")
+
+    # RANGE window bounds; partitions straddle shard edges, one shard has none
+    plen = [2500, 9000, 700, 4000, 1800]
+    bits = np.zeros(N, np.int8)
+    p, k = 0, 0
+    while p < N:
+        bits[p] = 1
+        p += plen[k % len(plen)]
+        k += 1
+    vals = np.concatenate([np.cumsum(r.integers(0, 5, 100)) for _ in range(N // 100)]).astype(np.int64)
+    order_ = np.zeros(N, np.int64)
+    starts = np.flatnonzero(bits)
+    for a0, a1 in zip(starts, list(starts[1:]) + [N]):
+        order_[a0:a1] = np.sort(vals[a0:a1])
+    for preceding in (True, False):
+        first, bnd = D.dist_window_bounds(be, dist, Col(ora.TYPE_lng, order_[lo:hi], lo),
+                                          Col(ora.TYPE_bit, bits[lo:hi], lo), 7, preceding)
+        want = ora.rangebounds(ora.Bat.from_array(ora.TYPE_lng, order_),
+                               ora.Bat.from_array(ora.TYPE_bit, bits), 7, preceding).values()
+        if not np.array_equal(bnd, want[first:first + len(bnd)].astype(np.int64)):
+            errs.append("window mismatch preceding=%s" % preceding)
+        cnt = torch.tensor([len(bnd)])
+        dist.all_reduce(cnt)
+        if int(cnt) != N:
+            errs.append("window rows %d != %d" % (int(cnt), N))
+    with open(os.path.join(out_dir, "rank%d.txt" % rank), "w") as f:
+        f.write("\n".join(errs) if errs else "ok")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_exchange_steps(tmp_path, world):
+    import torch.multiprocessing as mp
+    mp.spawn(_exchange_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for rk in range(world):
+        assert open(tmp_path / ("rank%d.txt" % rk)).read() == "ok", rk
