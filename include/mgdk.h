@@ -172,6 +172,18 @@ int mgdk_tpch_lineitem(uint64_t seed, uint64_t row0, uint64_t n, uint64_t sf_par
 int mgdk_gen_window_column(uint64_t seed, uint64_t n, uint64_t plen, mgdk_bat **vals,
 			   mgdk_bat **parts);
 
+/* gdk_analytic_func.c:1959 GDKanalyticalsum / :1626 GDKanalyticalcount
+ * (gdk_analytic.h:38-39): per-row aggregate over the row's frame.
+ * frame_type 3 = unbounded preceding .. current row (+ peers), 4 = current
+ * row (+ peers) .. unbounded following, 5 = whole partition, 6 = current
+ * row, otherwise [s[i], e[i]) from GDKanalyticalwindowbounds.  p / o: bit
+ * BATs of partition / peer-group starts.  r is caller-allocated (count(b)
+ * slots; tp2 = lng or hge for sums, lng for counts). */
+int mgdk_GDKanalyticalsum(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e,
+			  int tp1, int tp2, int frame_type);
+int mgdk_GDKanalyticalcount(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e,
+			    bool ignore_nils, int tpe, int frame_type);
+
 /* ---- multi-GPU exchange steps (SURVEY.md §8 e).  The reference shards a
  *      plan by row ranges (opt_mitosis.c:150-230) and re-aggregates packed
  *      partials (opt_mergetable.c:1496-1885); across GPUs the group / join

@@ -1,0 +1,659 @@
+// analytic_func.hip -- windowed SUM / COUNT over frames on the MI355X
+// (gdk/gdk_analytic_func.c:1959 GDKanalyticalsum, :1626 GDKanalyticalcount;
+// SURVEY.md §8(f) row 1, the direct consumer of the RANGE bounds of
+// analytic.hip).
+//
+// The reference walks every partition: running sums for the UNBOUNDED
+// frames (:1684-1745), and a fanout-16 segment tree per partition for
+// general frames (:1783-1815, gdk/gdk_analytic.h:52-130).  On the device
+// every frame is a row interval [lo, hi), so one exact 128-bit exclusive
+// prefix sum P of the non-nil values and one prefix count C of them give
+//     sum(frame) = P[hi] - P[lo],  nil when C[hi] - C[lo] == 0
+// for every frame kind at once (one reduce-then-scan over the column, one
+// per-row pass).  Frame intervals:
+//     3 unbounded preceding .. current row: [partition start, end of the
+//       row's peer group)             4 current row .. unbounded: [start of
+//       the peer group, partition end) 5 whole partition   6 the row
+//     other: [s[i], e[i]) from GDKanalyticalwindowbounds.
+// Overflow of a lng result is the reference's ADD_WITH_CHECK on every
+// partial: for the running frames the partials are exactly the partition's
+// prefix (3, 5) or suffix (4) sums, checked row by row from P; for the
+// segment-tree frames every tree node and query partial is a sum of a
+// subset of the partition, so a partition whose sum of |v| fits lng cannot
+// overflow -- such partitions are computed exactly, and a partition beyond
+// that bound (where the reference's answer depends on its tree's addition
+// order) fails loudly instead of guessing.  hge results of integer inputs
+// cannot overflow.
+#include "mgdk_internal.h"
+
+using namespace mgdk;
+
+namespace {
+
+constexpr int PF_ROWS = 8;                 // contiguous rows per lane
+constexpr int PF_TILE = 256 * PF_ROWS;
+
+template <typename T>
+__device__ __forceinline__ bool
+ldv(const T *b, BUN i, int64_t &v)
+{
+	const T x = b[i];
+	v = (int64_t) x;
+	return x == NilOf<T>::v();
+}
+
+__device__ __forceinline__ hge
+shfl_up128(hge v, int o)
+{
+	const unsigned long long lo = __shfl_up((unsigned long long) (uhge) v, o);
+	const unsigned long long hi = __shfl_up((unsigned long long) ((uhge) v >> 64), o);
+	return (hge) (((uhge) hi << 64) | lo);
+}
+
+// inclusive scans across a wave
+__device__ __forceinline__ hge
+wave_scan128(hge v)
+{
+	const unsigned lane = __lane_id();
+#pragma unroll
+	for (int o = 1; o < 64; o <<= 1) {
+		const hge u = shfl_up128(v, o);
+		if (lane >= (unsigned) o)
+			v += u;
+	}
+	return v;
+}
+
+__device__ __forceinline__ unsigned long long
+wave_scan64(unsigned long long v)
+{
+	const unsigned lane = __lane_id();
+#pragma unroll
+	for (int o = 1; o < 64; o <<= 1) {
+		const unsigned long long u = __shfl_up(v, o);
+		if (lane >= (unsigned) o)
+			v += u;
+	}
+	return v;
+}
+
+struct TileTot {
+	hge sum;
+	hge abs;
+	unsigned long long cnt;
+	unsigned long long pad;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void
+k_pf_tile(const T *b, BUN n, bool want_abs, TileTot *tot)
+{
+	const BUN base = (BUN) blockIdx.x * PF_TILE + (BUN) threadIdx.x * PF_ROWS;
+	hge s = 0, a = 0;
+	unsigned long long c = 0;
+#pragma unroll
+	for (int q = 0; q < PF_ROWS; q++) {
+		const BUN i = base + q;
+		int64_t v;
+		if (i < n && !ldv(b, i, v)) {
+			s += v;
+			c++;
+			if (want_abs)
+				a += v < 0 ? -(hge) v : (hge) v;
+		}
+	}
+	s = block_sum128(s);
+	if (want_abs)
+		a = block_sum128(a);
+	c = block_reduce(c, [](unsigned long long x, unsigned long long y) { return x + y; });
+	if (threadIdx.x == 0) {
+		tot[blockIdx.x].sum = s;
+		tot[blockIdx.x].abs = a;
+		tot[blockIdx.x].cnt = c;
+	}
+}
+
+// exclusive scan of up to 256 tile totals per workgroup, in place; the
+// workgroup's total goes to up[blockIdx.x] (a second level scans those)
+__global__ __launch_bounds__(256) void
+k_pf_scan256(TileTot *tot, BUN ntiles, TileTot *up)
+{
+	__shared__ hge w_s[4], w_a[4];
+	__shared__ unsigned long long w_c[4];
+	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+	const BUN t = (BUN) blockIdx.x * 256 + tid;
+	TileTot x{};
+	if (t < ntiles)
+		x = tot[t];
+	const hge is = wave_scan128(x.sum), ia = wave_scan128(x.abs);
+	const unsigned long long ic = wave_scan64(x.cnt);
+	if (lane == 63) {
+		w_s[w] = is;
+		w_a[w] = ia;
+		w_c[w] = ic;
+	}
+	__syncthreads();
+	hge es = is - x.sum, ea = ia - x.abs;
+	unsigned long long ec = ic - x.cnt;
+	for (unsigned q = 0; q < w; q++) {
+		es += w_s[q];
+		ea += w_a[q];
+		ec += w_c[q];
+	}
+	if (t < ntiles) {
+		tot[t].sum = es;
+		tot[t].abs = ea;
+		tot[t].cnt = ec;
+	}
+	if (up && tid == 255) {
+		up[blockIdx.x].sum = es + x.sum;
+		up[blockIdx.x].abs = ea + x.abs;
+		up[blockIdx.x].cnt = ec + x.cnt;
+	}
+}
+
+__global__ __launch_bounds__(256) void
+k_pf_addup(TileTot *tot, BUN ntiles, const TileTot *up)
+{
+	const BUN t = (BUN) blockIdx.x * 256 + threadIdx.x;
+	if (t < ntiles && blockIdx.x > 0) {
+		tot[t].sum += up[blockIdx.x].sum;
+		tot[t].abs += up[blockIdx.x].abs;
+		tot[t].cnt += up[blockIdx.x].cnt;
+	}
+}
+
+// P[i], C[i] (and A[i]) = sums over rows < i; entry n holds the totals.
+// Lanes own PF_ROWS consecutive rows (a thread-local running sum), the
+// results go through LDS so the stores are coalesced.  C may be NULL (no
+// nils: the count of [lo, hi) is hi - lo).
+template <typename T>
+__global__ __launch_bounds__(256) void
+k_pf_final(const T *b, BUN n, const TileTot *tot, hge *P, unsigned long long *Cn, hge *A)
+{
+	__shared__ hge w_s[4], w_a[4];
+	__shared__ unsigned long long w_c[4];
+	__shared__ hge sP[PF_TILE];
+	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+	const BUN tb = (BUN) blockIdx.x * PF_TILE;
+	const BUN base = tb + (BUN) tid * PF_ROWS;
+	int64_t v[PF_ROWS];
+	bool nl[PF_ROWS];
+	hge s = 0, a = 0;
+	unsigned long long c = 0;
+#pragma unroll
+	for (int q = 0; q < PF_ROWS; q++) {
+		const BUN i = base + q;
+		nl[q] = i >= n || ldv(b, i, v[q]);
+		if (!nl[q]) {
+			s += v[q];
+			c++;
+			if (A)
+				a += v[q] < 0 ? -(hge) v[q] : (hge) v[q];
+		}
+	}
+	const hge is = wave_scan128(s);
+	const hge ia = A ? wave_scan128(a) : 0;
+	const unsigned long long ic = wave_scan64(c);
+	if (lane == 63) {
+		w_s[w] = is;
+		w_a[w] = ia;
+		w_c[w] = ic;
+	}
+	__syncthreads();
+	hge es = is - s + tot[blockIdx.x].sum, ea = ia - a + tot[blockIdx.x].abs;
+	unsigned long long ec = ic - c + tot[blockIdx.x].cnt;
+	for (unsigned q = 0; q < w; q++) {
+		es += w_s[q];
+		ea += w_a[q];
+		ec += w_c[q];
+	}
+	const BUN nt = n - tb < (BUN) PF_TILE ? n - tb : (BUN) PF_TILE;
+	// sums
+#pragma unroll
+	for (int q = 0; q < PF_ROWS; q++) {
+		sP[tid * PF_ROWS + q] = es;
+		if (base + q == n - 1)
+			P[n] = es + (nl[q] ? 0 : v[q]);
+		if (!nl[q])
+			es += v[q];
+	}
+	__syncthreads();
+	for (unsigned i = tid; i < nt; i += 256)
+		P[tb + i] = sP[i];
+	if (Cn) {
+		__syncthreads();
+		unsigned long long *sC = (unsigned long long *) sP;
+#pragma unroll
+		for (int q = 0; q < PF_ROWS; q++) {
+			sC[tid * PF_ROWS + q] = ec;
+			if (base + q == n - 1)
+				Cn[n] = ec + (nl[q] ? 0 : 1);
+			if (!nl[q])
+				ec++;
+		}
+		__syncthreads();
+		for (unsigned i = tid; i < nt; i += 256)
+			Cn[tb + i] = sC[i];
+	}
+	if (A) {
+		__syncthreads();
+#pragma unroll
+		for (int q = 0; q < PF_ROWS; q++) {
+			sP[tid * PF_ROWS + q] = ea;
+			if (base + q == n - 1)
+				A[n] = ea + (nl[q] ? 0 : (v[q] < 0 ? -(hge) v[q] : (hge) v[q]));
+			if (!nl[q])
+				ea += v[q] < 0 ? -(hge) v[q] : (hge) v[q];
+		}
+		__syncthreads();
+		for (unsigned i = tid; i < nt; i += 256)
+			A[tb + i] = sP[i];
+	}
+}
+
+__global__ __launch_bounds__(256) void
+k_or_flags(const int8_t *p, const int8_t *o, BUN n, int8_t *f)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
+		f[i] = i == 0 || (p && p[i]) || (o && o[i]);
+}
+
+// sorted list of segment starts (row 0 always first)
+struct Starts {
+	const oid *L;        // NULL: dense Lseq + k
+	oid Lseq;
+	BUN m;               // entries, including a virtual row 0 when lead
+	bool lead;
+	BUN n;
+	__device__ __forceinline__ oid at(BUN k) const
+	{
+		if (lead) {
+			if (k == 0)
+				return 0;
+			k--;
+		}
+		return L ? L[k] : Lseq + k;
+	}
+	// [start, end) of the segment holding row i
+	__device__ __forceinline__ void seg(BUN i, BUN &s, BUN &e) const
+	{
+		BUN lo = 0, hi = m;
+		while (hi - lo > 1) {
+			const BUN mid = (lo + hi) / 2;
+			if (at(mid) <= i)
+				lo = mid;
+			else
+				hi = mid;
+		}
+		s = at(lo);
+		e = lo + 1 < m ? at(lo + 1) : n;
+	}
+};
+
+struct FArgs {
+	BUN n;
+	int frame;
+	bool other;          // frame given by s / e
+	bool lng_out;        // result lng (else hge)
+	bool count;          // GDKanalyticalcount
+	bool count_all;
+	Starts part, peer;
+	const oid *s, *e;
+	const hge *P, *A;
+	const unsigned long long *C;
+	void *out;
+	uint32_t *flags;     // [0] overflow, [1] beyond the exact bound, [2] nils in the result
+};
+
+__global__ __launch_bounds__(256) void
+k_frames(FArgs a)
+{
+	uint32_t ovf = 0, big = 0, hasnil = 0;
+	const hge MAXL = (hge) INT64_MAX;
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (BUN) gridDim.x * blockDim.x) {
+		BUN lo, hi, ps = 0, pe = 0;
+		if (a.frame == 3 || a.frame == 4 || a.frame == 5 || (a.other && a.A))
+			a.part.seg(i, ps, pe);
+		switch (a.frame) {
+		case 3: {
+			BUN gs, ge;
+			a.peer.seg(i, gs, ge);
+			lo = ps;
+			hi = ge;
+			break;
+		}
+		case 4: {
+			BUN gs, ge;
+			a.peer.seg(i, gs, ge);
+			lo = gs;
+			hi = pe;
+			break;
+		}
+		case 5: lo = ps; hi = pe; break;
+		case 6: lo = i; hi = i + 1; break;
+		default: lo = a.s[i]; hi = a.e[i]; break;
+		}
+		if (hi < lo)
+			hi = lo;
+		if (a.count) {
+			const long long c = a.count_all || !a.C ? (long long) (hi - lo) : (long long) (a.C[hi] - a.C[lo]);
+			((long long *) a.out)[i] = c;
+			continue;
+		}
+		const unsigned long long c = a.C ? a.C[hi] - a.C[lo] : hi - lo;
+		const hge sum = a.P[hi] - a.P[lo];
+		if (a.lng_out) {
+			// the reference's partials for this row's partition
+			if (a.frame == 3 || a.frame == 5) {
+				const hge q = a.P[i + 1] - a.P[ps];
+				ovf |= q > MAXL || q < -MAXL;
+			} else if (a.frame == 4) {
+				const hge q = a.P[pe] - a.P[i];
+				ovf |= q > MAXL || q < -MAXL;
+			} else if (a.other && a.A) {
+				big |= a.A[pe] - a.A[ps] > MAXL;
+			}
+			((long long *) a.out)[i] = c ? (long long) sum : INT64_MIN;
+		} else {
+			((hge *) a.out)[i] = c ? sum : NilOf<hge>::v();
+		}
+		hasnil |= c == 0;
+	}
+	ovf = block_reduce(ovf, [](uint32_t x, uint32_t y) { return x | y; });
+	big = block_reduce(big, [](uint32_t x, uint32_t y) { return x | y; });
+	hasnil = block_reduce(hasnil, [](uint32_t x, uint32_t y) { return x | y; });
+	if (threadIdx.x == 0) {
+		publish_or(&a.flags[0], ovf);
+		publish_or(&a.flags[1], big);
+		publish_or(&a.flags[2], hasnil);
+	}
+}
+
+// general frames [s[i], e[i]) into a hge result: 8 rows per lane with
+// every bound load, then every prefix load in flight (the generic kernel
+// above serialises two dependent loads per row)
+template <bool HASC>
+__global__ __launch_bounds__(256) void
+k_frames_other_hge(FArgs a)
+{
+	constexpr int R = 8;
+	const BUN base = (BUN) blockIdx.x * (256 * R) + threadIdx.x;
+	BUN lo[R], hi[R];
+#pragma unroll
+	for (int q = 0; q < R; q++) {
+		const BUN i = base + (BUN) q * 256;
+		lo[q] = hi[q] = 0;
+		if (i < a.n) {
+			lo[q] = a.s[i];
+			hi[q] = a.e[i];
+		}
+	}
+	hge pl[R], ph[R];
+	unsigned long long cl[R], ch[R];
+#pragma unroll
+	for (int q = 0; q < R; q++) {
+		if (hi[q] < lo[q])
+			hi[q] = lo[q];
+		pl[q] = a.P[lo[q]];
+		ph[q] = a.P[hi[q]];
+		if (HASC) {
+			cl[q] = a.C[lo[q]];
+			ch[q] = a.C[hi[q]];
+		}
+	}
+	uint32_t hasnil = 0;
+#pragma unroll
+	for (int q = 0; q < R; q++) {
+		const BUN i = base + (BUN) q * 256;
+		if (i < a.n) {
+			const unsigned long long c = HASC ? ch[q] - cl[q] : hi[q] - lo[q];
+			((hge *) a.out)[i] = c ? ph[q] - pl[q] : NilOf<hge>::v();
+			hasnil |= c == 0;
+		}
+	}
+	hasnil = block_reduce(hasnil, [](uint32_t x, uint32_t y) { return x | y; });
+	if (threadIdx.x == 0)
+		publish_or(&a.flags[2], hasnil);
+}
+
+__global__ void
+k_first(const oid *L, oid *out)
+{
+	*out = L[0];
+}
+
+// starts list from flags (nonzero = start); row 0 is always a start
+int
+make_starts(const int8_t *flags, BUN n, Starts &st, mgdk_bat **keep)
+{
+	st.n = n;
+	*keep = nullptr;
+	if (flags == nullptr) {
+		st.L = nullptr;
+		st.Lseq = 0;
+		st.m = 1;
+		st.lead = false;
+		return 0;
+	}
+	mgdk_bat *S = compact_flags(flags, n, 0, true);
+	if (S == nullptr)
+		return -1;
+	*keep = S;
+	st.L = S->ttype == MGDK_void ? nullptr : (const oid *) S->theap;
+	st.Lseq = S->tseqbase;
+	bool first0 = false;
+	if (S->count > 0) {
+		if (st.L == nullptr) {
+			first0 = st.Lseq == 0;
+		} else {
+			oid *d = (oid *) meta_buf();
+			hipLaunchKernelGGL(k_first, dim3(1), dim3(1), 0, stream(), st.L, d);
+			oid *h = (oid *) pinned(8);
+			if (!hip_ok(hipMemcpyAsync(h, d, 8, hipMemcpyDeviceToHost, stream()), "memcpy") || !sync())
+				return -1;
+			first0 = *h == 0;
+		}
+	}
+	st.lead = !first0;
+	st.m = S->count + (st.lead ? 1 : 0);
+	return 0;
+}
+
+bool
+sum_in_type(int t)
+{
+	t = basetype(t);
+	return t == MGDK_bte || t == MGDK_sht || t == MGDK_int || t == MGDK_lng;
+}
+
+int
+run_frames(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e, int frame_type,
+	   bool count, bool count_all, bool lng_out)
+{
+	const BUN n = b->count;
+	hipStream_t st = stream();
+	if (r->theap == nullptr && n) {
+		seterr("analytic: result BAT has no heap");
+		return -1;
+	}
+	if (n == 0) {
+		r->count = 0;
+		return 0;
+	}
+	if ((p && (p->count != n || width_of(p->ttype) != 1)) || (o && (o->count != n || width_of(o->ttype) != 1))) {
+		seterr("analytic: p and o must be bit BATs aligned with b");
+		return -1;
+	}
+	const bool frames = !(frame_type >= 3 && frame_type <= 6);
+	if (frames && (s == nullptr || e == nullptr || s->count < n || e->count < n || s->ttype != MGDK_oid ||
+		       e->ttype != MGDK_oid)) {
+		seterr("analytic: frame bounds s and e (oid BATs aligned with b) are required");
+		return -1;
+	}
+	if ((frame_type == 3 || frame_type == 4) && o == nullptr) {
+		seterr("analytic: the peer column o is required for this frame");
+		return -1;
+	}
+	// prefix sums / counts over the column
+	const bool need_prefix = !(count && count_all);
+	// without nils the count of [lo, hi) is hi - lo: no count prefix
+	const bool nonil = b->tnonil != 0;
+	const bool want_abs = !count && lng_out && frames;
+	const BUN ntiles = (n + PF_TILE - 1) / PF_TILE;
+	DevBuf tot(ntiles * sizeof(TileTot) + 64), P(need_prefix && !count ? (n + 1) * 16 : 16),
+		Cn(need_prefix ? (n + 1) * 8 : 8), A(want_abs ? (n + 1) * 16 : 16), fl(64);
+	if (!tot.p || !P.p || !Cn.p || !A.p || !fl.p)
+		return -1;
+	if (need_prefix) {
+		const dim3 g((unsigned) ntiles), blk(256);
+		hge *Pp = count ? nullptr : P.as<hge>();
+		DevBuf Pd(count ? (n + 1) * 16 : 16);   // sums are computed anyway; keep them apart for counts
+		if (!Pd.p)
+			return -1;
+		if (Pp == nullptr)
+			Pp = Pd.as<hge>();
+#define PF_TILE_K(T) hipLaunchKernelGGL((k_pf_tile<T>), g, blk, 0, st, (const T *) b->theap, n, want_abs, \
+					  tot.as<TileTot>())
+#define PF_FINAL_K(T) hipLaunchKernelGGL((k_pf_final<T>), g, blk, 0, st, (const T *) b->theap, n, tot.as<TileTot>(), \
+					   Pp, nonil ? nullptr : Cn.as<unsigned long long>(), want_abs ? A.as<hge>() : nullptr)
+		switch (b->twidth) {
+		case 1: PF_TILE_K(int8_t); break;
+		case 2: PF_TILE_K(int16_t); break;
+		case 4: PF_TILE_K(int32_t); break;
+		default: PF_TILE_K(int64_t); break;
+		}
+		// two-level exclusive scan of the tile totals
+		const BUN nb = (ntiles + 255) / 256;
+		if (nb > 256 * 256) {
+			seterr("analytic: input too large");
+			return -1;
+		}
+		DevBuf up(nb * sizeof(TileTot) + 64), up2(256 * sizeof(TileTot) + 64);
+		if (!up.p || !up2.p)
+			return -1;
+		hipLaunchKernelGGL(k_pf_scan256, dim3((unsigned) nb), blk, 0, st, tot.as<TileTot>(), ntiles, up.as<TileTot>());
+		if (nb > 1) {
+			const BUN nb2 = (nb + 255) / 256;
+			hipLaunchKernelGGL(k_pf_scan256, dim3((unsigned) nb2), blk, 0, st, up.as<TileTot>(), nb, up2.as<TileTot>());
+			if (nb2 > 1) {
+				hipLaunchKernelGGL(k_pf_scan256, dim3(1), blk, 0, st, up2.as<TileTot>(), nb2, (TileTot *) nullptr);
+				hipLaunchKernelGGL(k_pf_addup, dim3((unsigned) nb2), blk, 0, st, up.as<TileTot>(), nb, up2.as<TileTot>());
+			}
+			hipLaunchKernelGGL(k_pf_addup, dim3((unsigned) nb), blk, 0, st, tot.as<TileTot>(), ntiles, up.as<TileTot>());
+		}
+		switch (b->twidth) {
+		case 1: PF_FINAL_K(int8_t); break;
+		case 2: PF_FINAL_K(int16_t); break;
+		case 4: PF_FINAL_K(int32_t); break;
+		default: PF_FINAL_K(int64_t); break;
+		}
+#undef PF_TILE_K
+#undef PF_FINAL_K
+		if (!sync())
+			return -1;
+	}
+	// segments
+	mgdk_bat *Sp = nullptr, *Sg = nullptr;
+	FArgs a{};
+	a.n = n;
+	a.frame = frame_type;
+	a.other = frames;
+	a.lng_out = lng_out;
+	a.count = count;
+	a.count_all = count_all;
+	a.s = frames ? (const oid *) s->theap : nullptr;
+	a.e = frames ? (const oid *) e->theap : nullptr;
+	a.P = P.as<hge>();
+	a.A = want_abs ? A.as<hge>() : nullptr;
+	a.C = nonil ? nullptr : Cn.as<unsigned long long>();
+	a.out = r->theap;
+	a.flags = fl.as<uint32_t>();
+	int rc = -1;
+	DevBuf gf(n + 8);
+	if (!gf.p || make_starts(p ? (const int8_t *) p->theap : nullptr, n, a.part, &Sp) < 0)
+		goto out;
+	if (frame_type == 3 || frame_type == 4) {
+		hipLaunchKernelGGL(k_or_flags, dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st,
+				   p ? (const int8_t *) p->theap : nullptr, (const int8_t *) o->theap, n, gf.as<int8_t>());
+		if (make_starts(gf.as<int8_t>(), n, a.peer, &Sg) < 0)
+			goto out;
+	}
+	if (!hip_ok(hipMemsetAsync(fl.p, 0, 64, st), "memset"))
+		goto out;
+	if (frames && !count && !lng_out) {
+		const dim3 g((unsigned) ((n + 2047) / 2048));
+		if (a.C)
+			hipLaunchKernelGGL((k_frames_other_hge<true>), g, dim3(256), 0, st, a);
+		else
+			hipLaunchKernelGGL((k_frames_other_hge<false>), g, dim3(256), 0, st, a);
+	} else {
+		hipLaunchKernelGGL(k_frames, dim3(grid_for(n, 1024, 16384)), dim3(256), 0, st, a);
+	}
+	{
+		uint32_t *h = (uint32_t *) pinned(16);
+		if (!hip_ok(hipMemcpyAsync(h, fl.p, 12, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+			goto out;
+		if (h[0]) {
+			seterr("22003!overflow in calculation.\n");
+			goto out;
+		}
+		if (h[1]) {
+			seterr("42000!GDKanalyticalsum: a partition's sum of |values| exceeds lng; its lng frame sums "
+			       "depend on the segment tree's addition order -- not supported on the device path "
+			       "(use a hge result)");
+			goto out;
+		}
+		r->count = n;
+		r->tnil = h[2] != 0;
+		r->tnonil = h[2] == 0;
+		r->tsorted = r->trevsorted = r->tkey = n <= 1;
+		rc = 0;
+	}
+out:
+	mgdk_BBPunfix(Sp);
+	mgdk_BBPunfix(Sg);
+	return rc;
+}
+
+}  // namespace
+
+extern "C" int
+mgdk_GDKanalyticalsum(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e, int tp1,
+		      int tp2, int frame_type)
+{
+	if (r == nullptr || b == nullptr) {
+		seterr("GDKanalyticalsum: NULL argument");
+		return -1;
+	}
+	if (!sum_in_type(tp1) || basetype(b->ttype) != basetype(tp1) || !(tp2 == MGDK_lng || tp2 == MGDK_hge) ||
+	    r->ttype != tp2) {
+		seterr("42000!type combination (sum(%s)->%s) not supported.\n", atomname(tp1), atomname(tp2));
+		return -1;
+	}
+	ProfScope prof("analyticalsum");
+	return run_frames(r, p, o, b, s, e, frame_type, false, false, tp2 == MGDK_lng);
+}
+
+extern "C" int
+mgdk_GDKanalyticalcount(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e,
+			bool ignore_nils, int tpe, int frame_type)
+{
+	if (r == nullptr || b == nullptr) {
+		seterr("GDKanalyticalcount: NULL argument");
+		return -1;
+	}
+	(void) tpe;
+	if (r->ttype != MGDK_lng) {
+		seterr("GDKanalyticalcount: result must be a lng BAT");
+		return -1;
+	}
+	const bool count_all = !ignore_nils || b->tnonil;
+	if (!count_all && !sum_in_type(b->ttype)) {
+		seterr("42000!GDKanalyticalcount: nil-skipping count of %s not supported on the device path",
+		       atomname(b->ttype));
+		return -1;
+	}
+	ProfScope prof("analyticalcount");
+	return run_frames(r, p, o, b, s, e, frame_type, true, count_all, false);
+}

@@ -114,6 +114,8 @@ _SIGS = {
     "mgdk_tpch_lineitem": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, PP]),
     "mgdk_gen_window_column": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, PP, PP]),
     "mgdk_BAThashpartition": (C.c_int, [PP, C.c_void_p, C.c_int, C.c_void_p]),
+    "mgdk_GDKanalyticalsum": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_int, C.c_int]),
+    "mgdk_GDKanalyticalcount": (C.c_int, [C.c_void_p] * 6 + [C.c_bool, C.c_int, C.c_int]),
     "mgdk_BATlowerbound2": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
                                       C.c_void_p]),
     "mgdk_BATupload_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
@@ -404,6 +406,21 @@ def GDKanalyticalwindowbounds(b, p, limit, preceding, tp1=TYPE_lng, tp2=TYPE_lng
     _chk(lib().mgdk_GDKanalyticalwindowbounds(r.ptr, b.ptr, _p(p), None,
                                               C.cast(C.pointer(lim), C.c_void_p), tp1, tp2,
                                               unit, preceding, 0))
+    return r
+
+
+def GDKanalyticalsum(b, p, o, s, e, tp2, frame_type):
+    """Windowed sum per row over its frame (gdk_analytic_func.c:1959)."""
+    r = BAT(lib().mgdk_COLnew(0, tp2, max(1, b.count())))
+    _chk(lib().mgdk_GDKanalyticalsum(r.ptr, _p(p), _p(o), b.ptr, _p(s), _p(e), b.ttype, tp2, frame_type))
+    return r
+
+
+def GDKanalyticalcount(b, p, o, s, e, ignore_nils, frame_type):
+    """Windowed count per row over its frame (gdk_analytic_func.c:1626)."""
+    r = BAT(lib().mgdk_COLnew(0, TYPE_lng, max(1, b.count())))
+    _chk(lib().mgdk_GDKanalyticalcount(r.ptr, _p(p), _p(o), b.ptr, _p(s), _p(e), ignore_nils, b.ttype,
+                                       frame_type))
     return r
 
 

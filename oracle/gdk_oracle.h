@@ -21,6 +21,8 @@
  *   join        gdk/gdk_join.c:2781-2900 (hash join result order)
  *   sort        gdk/gdk_batop.c:2266-2342, gdk/gdk_rsort.c:21 (stable)
  *   window      gdk/gdk_analytic_bounds.c:273-387, :994, :1440
+ *   frames      gdk/gdk_analytic_func.c:1626 (count), :1959 (sum), segment
+ *               tree gdk/gdk_analytic.h:52-130
  *
  * Parity pinning: see tests/golden/ (fixtures extracted from the reference's
  * own MAL known-answer tests) and DESIGN.md §Oracle.
@@ -123,6 +125,13 @@ typedef struct ora_q1row {
 	int64_t count_order;
 } ora_q1row;
 int ora_q1(const ora_lineitem *li, int nthreads, ora_q1row *rows, int *nrows);
+
+/* windowed aggregates over frames (gdk_oracle_analytic.c); r is
+ * caller-allocated with count(b) slots of the result type */
+int ora_analyticalsum(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_bat *b,
+		      const ora_bat *s, const ora_bat *e, int tp1, int tp2, int frame_type);
+int ora_analyticalcount(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_bat *b,
+			const ora_bat *s, const ora_bat *e, bool ignore_nils, int frame_type);
 
 #ifdef __cplusplus
 }

@@ -85,6 +85,8 @@ def lib():
         L.ora_join.argtypes = [C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool]
         L.ora_sort.argtypes = [C.POINTER(P), C.POINTER(P), P, C.c_bool, C.c_bool]
         L.ora_rangebounds.argtypes = [P, P, P, C.c_void_p, C.c_int, C.c_bool, C.c_uint64]
+        L.ora_analyticalsum.argtypes = [P, P, P, P, P, P, C.c_int, C.c_int, C.c_int]
+        L.ora_analyticalcount.argtypes = [P, P, P, P, P, P, C.c_bool, C.c_int]
         L.ora_tpch_lineitem.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64] + [C.c_void_p] * 7
         L.ora_mkdate.restype = C.c_int32
         L.ora_mkdate.argtypes = [C.c_int, C.c_int, C.c_int]
@@ -288,6 +290,28 @@ def rangebounds(b, p, limit, preceding):
     lim = C.c_int64(limit)
     if lib().ora_rangebounds(r, b.ptr, p.ptr if p else None, C.cast(C.pointer(lim), C.c_void_p),
                              TYPE_lng, preceding, 0) < 0:
+        lib().ora_free(r)
+        raise _err()
+    return Bat(r)
+
+
+def analyticalsum(b, p, o, s, e, tp2, frame_type):
+    n = b.count()
+    r = lib().ora_new(tp2, n, 0)
+    if lib().ora_analyticalsum(r, p.ptr if p else None, o.ptr if o else None, b.ptr,
+                               s.ptr if s else None, e.ptr if e else None, b.s.type, tp2,
+                               frame_type) < 0:
+        lib().ora_free(r)
+        raise _err()
+    return Bat(r)
+
+
+def analyticalcount(b, p, o, s, e, ignore_nils, frame_type):
+    n = b.count()
+    r = lib().ora_new(TYPE_lng, n, 0)
+    if lib().ora_analyticalcount(r, p.ptr if p else None, o.ptr if o else None, b.ptr,
+                                 s.ptr if s else None, e.ptr if e else None, ignore_nils,
+                                 frame_type) < 0:
         lib().ora_free(r)
         raise _err()
     return Bat(r)

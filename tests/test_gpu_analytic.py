@@ -1,0 +1,123 @@
+"""Windowed SUM / COUNT over frames (GDKanalyticalsum / GDKanalyticalcount,
+gdk/gdk_analytic_func.c:1959 / :1626) against the oracle restatement, with
+frames from GDKanalyticalwindowbounds (the RANGE bounds of §8 a10)."""
+import numpy as np
+import pytest
+
+from helpers import rng
+
+pytestmark = pytest.mark.gpu
+
+NIL64 = np.iinfo(np.int64).min
+
+
+def _data(r, nparts=23, plen=517, nil_frac=0.05, tname="lng", lo=-10**6, hi=10**6):
+    dt = {"int": np.int32, "lng": np.int64, "sht": np.int16}[tname]
+    vals, bits, order = [], [], []
+    for _ in range(nparts):
+        n = int(r.integers(1, 2 * plen))
+        ob = np.sort(r.integers(0, n // 3 + 1, n))               # ORDER BY values -> peers
+        v = r.integers(lo, hi, n).astype(dt)
+        v[r.random(n) < nil_frac] = np.iinfo(dt).min
+        vals.append(v)
+        b = np.zeros(n, np.int8)
+        b[0] = 1
+        bits.append(b)
+        order.append(ob)
+    v = np.concatenate(vals)
+    p = np.concatenate(bits)
+    ob = np.concatenate(order).astype(np.int64)
+    o = np.ones(len(v), np.int8)
+    o[1:] = (ob[1:] != ob[:-1]) | (p[1:] != 0)
+    return v, p, o, ob
+
+
+def _bounds(gdk, ob, p, limit):
+    OB = gdk.BAT.from_numpy(gdk.TYPE_lng, ob)
+    P = gdk.BAT.from_numpy(gdk.TYPE_bit, p)
+    s = gdk.GDKanalyticalwindowbounds(OB, P, limit, True)
+    e = gdk.GDKanalyticalwindowbounds(OB, P, limit, False)
+    return s, e
+
+
+@pytest.mark.parametrize("tname", ["int", "lng"])
+@pytest.mark.parametrize("tp2", ["lng", "hge"])
+@pytest.mark.parametrize("frame", [3, 4, 5, 6, 1])
+def test_analytical_sum(gdk, ora, tname, tp2, frame):
+    r = rng(301)
+    v, p, o, ob = _data(r, tname=tname)
+    tp1 = getattr(gdk, "TYPE_" + tname)
+    T2 = getattr(gdk, "TYPE_" + tp2)
+    s = e = None
+    if frame == 1:
+        s, e = _bounds(gdk, ob, p, 3)
+    got = gdk.GDKanalyticalsum(gdk.BAT.from_numpy(tp1, v), gdk.BAT.from_numpy(gdk.TYPE_bit, p),
+                               gdk.BAT.from_numpy(gdk.TYPE_bit, o), s, e, T2, frame)
+    os_ = ora.Bat.from_array(ora.TYPE_oid, s.to_numpy()) if s else None
+    oe = ora.Bat.from_array(ora.TYPE_oid, e.to_numpy()) if e else None
+    want = ora.analyticalsum(ora.Bat.from_array(tp1, v), ora.Bat.from_array(ora.TYPE_bit, p),
+                             ora.Bat.from_array(ora.TYPE_bit, o), os_, oe, T2, frame)
+    g = got.values()
+    w = want.values()
+    assert list(g) == list(w)
+
+
+@pytest.mark.parametrize("ignore_nils", [True, False])
+@pytest.mark.parametrize("frame", [3, 4, 5, 6, 1])
+def test_analytical_count(gdk, ora, ignore_nils, frame):
+    r = rng(302)
+    v, p, o, ob = _data(r)
+    s = e = None
+    if frame == 1:
+        s, e = _bounds(gdk, ob, p, 5)
+    got = gdk.GDKanalyticalcount(gdk.BAT.from_numpy(gdk.TYPE_lng, v), gdk.BAT.from_numpy(gdk.TYPE_bit, p),
+                                 gdk.BAT.from_numpy(gdk.TYPE_bit, o), s, e, ignore_nils, frame)
+    os_ = ora.Bat.from_array(ora.TYPE_oid, s.to_numpy()) if s else None
+    oe = ora.Bat.from_array(ora.TYPE_oid, e.to_numpy()) if e else None
+    want = ora.analyticalcount(ora.Bat.from_array(ora.TYPE_lng, v), ora.Bat.from_array(ora.TYPE_bit, p),
+                               ora.Bat.from_array(ora.TYPE_bit, o), os_, oe, ignore_nils, frame)
+    assert np.array_equal(got.to_numpy(), want.values())
+
+
+@pytest.mark.parametrize("frame", [3, 4, 5])
+def test_analytical_sum_lng_overflow(gdk, ora, frame):
+    # running partials overflow lng in one partition: the reference's error
+    v = np.array([2**62, 2**62, 5, 7, 2**62, -(2**62), 1], np.int64)
+    p = np.array([0, 0, 0, 1, 1, 0, 0], np.int8)
+    o = np.ones(7, np.int8)
+    args = (gdk.BAT.from_numpy(gdk.TYPE_lng, v), gdk.BAT.from_numpy(gdk.TYPE_bit, p),
+            gdk.BAT.from_numpy(gdk.TYPE_bit, o), None, None)
+    with pytest.raises(ora.OracleError, match="22003!overflow in calculation"):
+        ora.analyticalsum(ora.Bat.from_array(ora.TYPE_lng, v), ora.Bat.from_array(ora.TYPE_bit, p),
+                          ora.Bat.from_array(ora.TYPE_bit, o), None, None, ora.TYPE_lng, frame)
+    with pytest.raises(gdk.GDKError, match="22003!overflow in calculation"):
+        gdk.GDKanalyticalsum(*args, gdk.TYPE_lng, frame)
+    # the same sums in hge are exact
+    got = gdk.GDKanalyticalsum(*args, gdk.TYPE_hge, frame).values()
+    want = ora.analyticalsum(ora.Bat.from_array(ora.TYPE_lng, v), ora.Bat.from_array(ora.TYPE_bit, p),
+                             ora.Bat.from_array(ora.TYPE_bit, o), None, None, ora.TYPE_hge, frame).values()
+    assert list(got) == list(want)
+
+
+def test_analytical_sum_frames_large_magnitude(gdk):
+    # |values| summing past lng in a partition: lng frame sums depend on the
+    # reference's segment-tree order -> refused loudly, hge is exact
+    v = np.array([2**62, -(2**62), 2**62, -(2**62), 3], np.int64)
+    V = gdk.BAT.from_numpy(gdk.TYPE_lng, v)
+    s = gdk.BAT.from_numpy(gdk.TYPE_oid, np.array([0, 0, 1, 2, 3], np.uint64))
+    e = gdk.BAT.from_numpy(gdk.TYPE_oid, np.array([1, 2, 3, 4, 5], np.uint64))
+    with pytest.raises(gdk.GDKError, match="not supported on the device path"):
+        gdk.GDKanalyticalsum(V, None, None, s, e, gdk.TYPE_lng, 1)
+    got = gdk.GDKanalyticalsum(V, None, None, s, e, gdk.TYPE_hge, 1).values()
+    assert list(got) == [2**62, 0, 0, 0, -(2**62) + 3]
+
+
+def test_analytical_sum_large(gdk, ora):
+    # multi-tile prefix scan (several 2048-row tiles and a ragged tail)
+    r = rng(303)
+    v, p, o, ob = _data(r, nparts=60, plen=3000)
+    got = gdk.GDKanalyticalsum(gdk.BAT.from_numpy(gdk.TYPE_lng, v), gdk.BAT.from_numpy(gdk.TYPE_bit, p),
+                               gdk.BAT.from_numpy(gdk.TYPE_bit, o), None, None, gdk.TYPE_hge, 3).values()
+    want = ora.analyticalsum(ora.Bat.from_array(ora.TYPE_lng, v), ora.Bat.from_array(ora.TYPE_bit, p),
+                             ora.Bat.from_array(ora.TYPE_bit, o), None, None, ora.TYPE_hge, 3).values()
+    assert list(got) == list(want)

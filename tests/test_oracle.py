@@ -104,3 +104,19 @@ def test_rangebounds_small(ora):
     fol = ora.rangebounds(b, p, 2, False)
     assert list(pre.values()) == [0, 0, 1, 3, 3, 5, 5]
     assert list(fol.values()) == [2, 3, 3, 5, 5, 7, 7]
+
+
+def test_analytical_sum_oracle_small(ora):
+    # hand-checked: partitions {0,1,2} {3..6}; peers {0,1} {2} {3} {4,5} {6}
+    v = np.array([1, 2, 3, -(2**63), 5, 6, 7], np.int64)
+    p = np.array([0, 0, 0, 1, 0, 0, 0], np.int8)
+    o = np.array([1, 0, 1, 1, 1, 0, 1], np.int8)
+    B, P, O = (ora.Bat.from_array(ora.TYPE_lng, v), ora.Bat.from_array(ora.TYPE_bit, p),
+               ora.Bat.from_array(ora.TYPE_bit, o))
+    NIL = -(2**127)
+    assert ora.analyticalsum(B, P, O, None, None, ora.TYPE_hge, 3).values() == [3, 3, 6, NIL, 11, 11, 18]
+    assert ora.analyticalsum(B, P, O, None, None, ora.TYPE_hge, 4).values() == [6, 6, 3, 18, 18, 18, 7]
+    assert list(ora.analyticalcount(B, P, O, None, None, True, 3).values()) == [2, 2, 3, 0, 2, 2, 3]
+    s = ora.Bat.from_array(ora.TYPE_oid, np.array([0, 0, 1, 3, 3, 4, 5], np.uint64))
+    e = ora.Bat.from_array(ora.TYPE_oid, np.array([2, 3, 3, 4, 6, 7, 7], np.uint64))
+    assert list(ora.analyticalsum(B, P, O, s, e, ora.TYPE_lng, 1).values()) == [3, 6, 5, -(2**63), 11, 18, 13]

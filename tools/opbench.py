@@ -112,7 +112,14 @@ def config5_window(n=1_000_000_000, plen=100_000, limit=100):
     v, p = gdk.gen_window_column(5, n, plen)
     res, wall, kms = timed(lambda: gdk.GDKanalyticalwindowbounds(v, p, limit, True), reps=3,
                            kernels=("windowbounds",))
-    return entry(n, 17 * n, wall, kms, partitions=n // plen, limit=limit)
+    out = entry(n, 17 * n, wall, kms, partitions=n // plen, limit=limit)
+    # the frame's SUM (RANGE BETWEEN limit PRECEDING AND limit FOLLOWING) over
+    # the same column, hge result: s, e bounds in, 8 B value + 16 B sum per row
+    e = gdk.GDKanalyticalwindowbounds(v, p, limit, False)
+    _, wall2, kms2 = timed(lambda: gdk.GDKanalyticalsum(v, p, None, res, e, gdk.TYPE_hge, 1), reps=3,
+                           kernels=("analyticalsum",))
+    out["frame_sum_hge"] = entry(n, n * (8 + 8 + 8 + 16), wall2, kms2)
+    return out
 
 
 def other_ops(n=100_000_000):
