@@ -126,6 +126,9 @@ int mgdk_BATjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r,
 /* ---- sort (gdk/gdk.h:1526; gdk/gdk_batop.c:2342) ---------------------- */
 int mgdk_BATsort(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups,
 		 mgdk_bat *b, mgdk_bat *o, mgdk_bat *g, bool reverse, bool nilslast, bool stable);
+/* gdk_unique.c:30 BATunique: candidate list of the first occurrence of
+ * every distinct value of b[s] */
+mgdk_bat *mgdk_BATunique(mgdk_bat *b, mgdk_bat *s);
 
 /* ---- window bounds (gdk/gdk_analytic.h:27-30;
  *      gdk/gdk_analytic_bounds.c:1440) ------------------------------------- */

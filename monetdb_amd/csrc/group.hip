@@ -401,3 +401,16 @@ fail:
 	mgdk_BBPunfix(hn);
 	return -1;
 }
+
+// BATunique (gdk/gdk_unique.c:30): the candidate list of the first
+// occurrence of every distinct value of b[s] -- the extents of BATgroup
+// (gdk_unique.c:18-22 says as much), so the same device path computes it.
+extern "C" mgdk_bat *
+mgdk_BATunique(mgdk_bat *b, mgdk_bat *s)
+{
+	mgdk_bat *g = nullptr, *e = nullptr;
+	if (mgdk_BATgroup(&g, &e, nullptr, b, s, nullptr, nullptr, nullptr) < 0)
+		return nullptr;
+	mgdk_BBPunfix(g);
+	return e;
+}

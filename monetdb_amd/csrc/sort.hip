@@ -438,6 +438,120 @@ sort_typed(const mgdk_bat *b, bool reverse, bool nilslast, mgdk_bat *sn, mgdk_ba
 	return sync() ? 0 : -1;
 }
 
+__global__ __launch_bounds__(256) void
+k_fill_ones(uint8_t *f, BUN n)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
+		f[i] = i > 0;
+}
+
+// ---- sub-sorting: BATsort with o (pre-order) and / or g (groups) ---------
+// (gdk/gdk_batop.c:2305-2340): b is first rearranged by o, then every run
+// of equal g is sorted.  g is sorted ascending, so "sort within runs" is a
+// stable sort on the composite (g, key image): LSD -- first by key image,
+// then (stably) by group id -- and the result oids are o[perm].
+
+template <typename T, typename K>
+__global__ __launch_bounds__(256) void
+k_subkeys(const T *col, const oid *o, oid oseq, oid hseq, BUN n, bool reverse, bool nilslast, K *keys)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
+		keys[i] = keyimg<T, K>(col[(o ? o[i] : oseq + i) - hseq], reverse, nilslast);
+}
+
+__global__ __launch_bounds__(256) void
+k_gather_gid(const oid *g, oid gseq, const uint32_t *perm, BUN n, uint64_t *out, uint32_t *idx)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		const uint32_t p = perm ? perm[i] : (uint32_t) i;
+		out[i] = g ? g[p] : gseq + p;
+		idx[i] = p;
+	}
+}
+
+template <typename T, typename K>
+__global__ __launch_bounds__(256) void
+k_final_sub(const T *col, const oid *o, oid oseq, oid hseq, const oid *g, oid gseq, const uint32_t *perm, BUN n,
+	    bool reverse, bool nilslast, T *sorted, oid *order, uint8_t *flag)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		const uint32_t p = perm ? perm[i] : (uint32_t) i;
+		const oid src = o ? o[p] : oseq + p;
+		if (order)
+			order[i] = src;
+		if (sorted)
+			sorted[i] = col[src - hseq];
+		if (flag) {
+			bool nw = i > 0;
+			if (nw) {
+				const uint32_t q = perm ? perm[i - 1] : (uint32_t) (i - 1);
+				const oid sq = o ? o[q] : oseq + q;
+				nw = (g && g[p] != g[q]) || keyimg<T, K>(col[src - hseq], reverse, nilslast) !=
+								    keyimg<T, K>(col[sq - hseq], reverse, nilslast);
+			}
+			flag[i] = nw;
+		}
+	}
+}
+
+template <typename T, typename K>
+int
+sort_sub(const mgdk_bat *b, const mgdk_bat *o, const mgdk_bat *g, bool reverse, bool nilslast, mgdk_bat *sn,
+	 mgdk_bat *on, mgdk_bat *gn)
+{
+	const BUN n = b->count;
+	hipStream_t st = stream();
+	const oid *op = o && o->ttype != MGDK_void ? (const oid *) o->theap : nullptr;
+	const oid oseq = o ? (o->ttype == MGDK_void ? o->tseqbase : 0) : b->hseqbase;
+	// g given as a dense (void) column means every row is its own group:
+	// nothing to sort inside the groups
+	const bool gdense = g && g->ttype == MGDK_void;
+	const oid *gp = g && !gdense ? (const oid *) g->theap : nullptr;
+	DevBuf k0(n * sizeof(K) + 8), k1(n * sizeof(K) + 8), v0(n * 4 + 4), v1(n * 4 + 4);
+	DevBuf g0(n * 8 + 8), g1(n * 8 + 8), w0(n * 4 + 4), w1(n * 4 + 4), fl(n + 8), ex(n * 8 + 8);
+	if (!k0.p || !k1.p || !v0.p || !v1.p || !g0.p || !g1.p || !w0.p || !w1.p || !fl.p || !ex.p)
+		return -1;
+	const dim3 grd(grid_for(n, 1024, 8192)), blk(256);
+	uint32_t *perm = nullptr;
+	if (!gdense) {
+		hipLaunchKernelGGL((k_subkeys<T, K>), grd, blk, 0, st, (const T *) b->theap, op, oseq, b->hseqbase, n, reverse,
+				   nilslast, k0.as<K>());
+		K *ks;
+		if (radix_sort<K>(k0.as<K>(), v0.as<uint32_t>(), k1.as<K>(), v1.as<uint32_t>(), n, 8 * (int) sizeof(K),
+				  nullptr, true, false, &ks, &perm) < 0)
+			return -1;
+		if (g) {
+			hipLaunchKernelGGL(k_gather_gid, grd, blk, 0, st, gp, g->tseqbase, perm, n, g0.as<uint64_t>(),
+					   w0.as<uint32_t>());
+			uint64_t *gs;
+			if (radix_sort<uint64_t>(g0.as<uint64_t>(), w0.as<uint32_t>(), g1.as<uint64_t>(), w1.as<uint32_t>(), n,
+						 64, nullptr, false, false, &gs, &perm) < 0)
+				return -1;
+		}
+	}
+	hipLaunchKernelGGL((k_final_sub<T, K>), grd, blk, 0, st, (const T *) b->theap, op, oseq, b->hseqbase,
+			   gdense ? nullptr : gp, g ? g->tseqbase : 0, perm, n, reverse, nilslast,
+			   sn ? (T *) sn->theap : nullptr, on ? (oid *) on->theap : nullptr,
+			   gn ? fl.as<uint8_t>() : nullptr);
+	if (gn) {
+		uint64_t tot = 0;
+		if (gdense) {
+			hipLaunchKernelGGL(k_fill_ones, grd, blk, 0, st, fl.as<uint8_t>(), n);
+		}
+		if (exclusive_scan(fl.as<uint8_t>(), ex.as<uint64_t>(), n, &tot) < 0)
+			return -1;
+		hipLaunchKernelGGL(k_gid, grd, blk, 0, st, ex.as<uint64_t>(), fl.as<uint8_t>(), n, (oid *) gn->theap);
+		if (!sync())
+			return -1;
+		gn->count = n;
+		gn->tsorted = 1;
+		gn->trevsorted = tot == 0;
+		gn->tkey = tot + 1 == n || n <= 1;
+		gn->tnonil = 1;
+	}
+	return sync() ? 0 : -1;
+}
+
 }  // namespace
 
 namespace mgdk {
@@ -476,10 +590,21 @@ mgdk_BATsort(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b
 		seterr("stable sort cannot have reverse != nilslast\n");
 		return -1;
 	}
-	if (o != nullptr || g != nullptr) {
-		seterr("42000!BATsort: sub-sorting (o/g) is not supported on the device path");
+	if (o != nullptr && (basetype(o->ttype) != MGDK_oid && o->ttype != MGDK_void)) {
+		seterr("o must have type oid and same size as b\n");
 		return -1;
 	}
+	if (o != nullptr && (o->count != b->count || (o->ttype == MGDK_void && o->count && o->tseqbase == MGDK_OID_NIL))) {
+		seterr("o must have type oid and same size as b\n");
+		return -1;
+	}
+	if (g != nullptr && ((basetype(g->ttype) != MGDK_oid && g->ttype != MGDK_void) || !g->tsorted ||
+			     g->count != b->count || (g->ttype == MGDK_void && g->count && g->tseqbase == MGDK_OID_NIL))) {
+		seterr("g must have type oid, sorted on the tail, and same size as b\n");
+		return -1;
+	}
+	if (g == nullptr && !stable)
+		o = nullptr;        // pre-ordering is meaningless for an unstable full sort
 	const int tt = basetype(b->ttype);
 	if (!(tt == MGDK_bte || tt == MGDK_sht || tt == MGDK_int || tt == MGDK_lng || tt == MGDK_oid ||
 	      tt == MGDK_flt || tt == MGDK_dbl || tt == MGDK_void)) {
@@ -493,6 +618,49 @@ mgdk_BATsort(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b
 	}
 	ProfScope prof("sort");
 	mgdk_bat *sn = nullptr, *on = nullptr, *gn = nullptr;
+	if (o != nullptr || g != nullptr) {
+		if (tt == MGDK_void) {
+			seterr("42000!BATsort: sub-sorting a void column is not supported on the device path");
+			return -1;
+		}
+		sn = sorted ? newbat(b->hseqbase, b->ttype, n) : nullptr;
+		on = order ? newbat(b->hseqbase, MGDK_oid, n) : nullptr;
+		gn = groups ? newbat(b->hseqbase, MGDK_oid, n) : nullptr;
+		if ((sorted && !sn) || (order && !on) || (groups && !gn))
+			goto fail;
+		const bool k32 = b->twidth <= 4 && reverse == nilslast;
+		int rc = 0;
+#define SUB(T, K) rc = sort_sub<T, K>(b, o, g, reverse, nilslast, sn, on, gn)
+		switch (tt) {
+		case MGDK_bte: if (k32) SUB(int8_t, uint32_t); else SUB(int8_t, uint64_t); break;
+		case MGDK_sht: if (k32) SUB(int16_t, uint32_t); else SUB(int16_t, uint64_t); break;
+		case MGDK_int: if (k32) SUB(int32_t, uint32_t); else SUB(int32_t, uint64_t); break;
+		case MGDK_flt: if (k32) SUB(float, uint32_t); else SUB(float, uint64_t); break;
+		case MGDK_lng: SUB(int64_t, uint64_t); break;
+		case MGDK_oid: SUB(uint64_t, uint64_t); break;
+		case MGDK_dbl: SUB(double, uint64_t); break;
+		}
+#undef SUB
+		if (rc < 0)
+			goto fail;
+		if (sn) {
+			sn->count = n;
+			sn->tsorted = (g == nullptr && !reverse) || n <= 1;
+			sn->trevsorted = (g == nullptr && reverse) || n <= 1;
+			sn->tkey = b->tkey;
+			sn->tnonil = b->tnonil;
+			sn->tnil = b->tnil;
+			if (b->ttype == MGDK_str)
+				share_vheap(sn, b);
+		}
+		if (on) {
+			on->count = n;
+			on->tkey = 1;
+			on->tnonil = 1;
+			on->tsorted = on->trevsorted = n <= 1;
+		}
+		goto done;
+	}
 	if (tt == MGDK_void) {
 		// dense column: sorted already (gdk_batop.c:2384-2392)
 		sn = mgdk_BATslice(b, 0, n);

@@ -114,6 +114,7 @@ _SIGS = {
     "mgdk_tpch_lineitem": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, PP]),
     "mgdk_gen_window_column": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, PP, PP]),
     "mgdk_BAThashpartition": (C.c_int, [PP, C.c_void_p, C.c_int, C.c_void_p]),
+    "mgdk_BATunique": (P, [C.c_void_p, C.c_void_p]),
     "mgdk_GDKanalyticalsum": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_int, C.c_int]),
     "mgdk_GDKanalyticalcount": (C.c_int, [C.c_void_p] * 6 + [C.c_bool, C.c_int, C.c_int]),
     "mgdk_BATlowerbound2": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
@@ -196,9 +197,10 @@ class BAT:
                 np.zeros(n, bool)
             s.tnonil = int(not isn.any()) if nonil is None else int(nonil)
             s.tnil = int(isn.any())
-            d = np.diff(flat.astype(np.float64) if flat.dtype.kind == "f" else flat)
-            s.tsorted = int((d >= 0).all()) if sorted_ is None else int(sorted_)
-            s.trevsorted = int((d <= 0).all()) if revsorted is None else int(revsorted)
+            cmpv = flat.astype(np.float64) if flat.dtype.kind == "f" else flat
+            # compare neighbours (np.diff wraps for unsigned oids)
+            s.tsorted = int(bool((cmpv[1:] >= cmpv[:-1]).all())) if sorted_ is None else int(sorted_)
+            s.trevsorted = int(bool((cmpv[1:] <= cmpv[:-1]).all())) if revsorted is None else int(revsorted)
             s.tkey = int(len(np.unique(flat)) == n) if key is None else int(key)
         else:
             s.tnonil = 1 if nonil is None else int(nonil)
@@ -397,6 +399,11 @@ def BATsort(b, o=None, g=None, reverse=False, nilslast=False, stable=True):
     _chk(lib().mgdk_BATsort(C.byref(sp), C.byref(op), C.byref(gp), b.ptr, _p(o), _p(g),
                             reverse, nilslast, stable))
     return BAT(sp), BAT(op), (BAT(gp) if gp else None)
+
+
+def BATunique(b, s=None):
+    """Candidate list of the first occurrence of each distinct value (gdk_unique.c:30)."""
+    return BAT(lib().mgdk_BATunique(b.ptr, _p(s)))
 
 
 def GDKanalyticalwindowbounds(b, p, limit, preceding, tp1=TYPE_lng, tp2=TYPE_lng, unit=1):

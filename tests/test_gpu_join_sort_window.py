@@ -272,3 +272,66 @@ def test_window_no_partitions_and_errors(gdk, ora):
         gdk.GDKanalyticalwindowbounds(mk(gdk, gdk.TYPE_lng, big), None, 5, True)
     with pytest.raises(ora.OracleError, match="22003!overflow in calculation"):
         ora.rangebounds(omk(ora, ora.TYPE_lng, big), None, 5, True)
+
+
+# ---- sub-sorting (o, g) and BATunique -----------------------------------------------
+
+def test_sort_multicolumn_chain(gdk):
+    # the reference's documented 3-column idiom (gdk_batop.c:2330-2334)
+    r = rng(97)
+    n = 60_000
+    c1 = r.integers(0, 20, n).astype(np.int32)
+    c2 = r.integers(-5, 5, n).astype(np.int64)
+    c3 = r.integers(0, 1000, n).astype(np.int16)
+    B1, B2, B3 = (mk(gdk, gdk.TYPE_int, c1, hseqbase=4), mk(gdk, gdk.TYPE_lng, c2, hseqbase=4),
+                  mk(gdk, gdk.TYPE_sht, c3, hseqbase=4))
+    s1, o1, g1 = gdk.BATsort(B1)
+    s2, o2, g2 = gdk.BATsort(B2, o=o1, g=g1)
+    s3, o3, g3 = gdk.BATsort(B3, o=o2, g=g2)
+    want = np.lexsort((c3, c2, c1))
+    assert np.array_equal(o3.to_numpy().astype(np.int64) - 4, want)
+    assert np.array_equal(s3.to_numpy(), c3[want])
+    key = np.stack([c1[want], c2[want], c3[want].astype(np.int64)], 1)
+    newg = np.concatenate([[0], np.cumsum(np.any(key[1:] != key[:-1], axis=1))]).astype(np.uint64)
+    assert np.array_equal(g3.to_numpy(), newg)
+
+
+def test_sort_with_order_only_and_reverse(gdk):
+    r = rng(98)
+    n = 30_000
+    a = r.integers(0, 100, n).astype(np.int32)
+    b = r.integers(0, 100, n).astype(np.int32)
+    _, oa, ga = gdk.BATsort(mk(gdk, gdk.TYPE_int, a))
+    # o only, stable: b ordered, ties in a-order
+    _, ob, _ = gdk.BATsort(mk(gdk, gdk.TYPE_int, b), o=oa, stable=True)
+    pa = np.argsort(a, kind="stable")
+    want = pa[np.argsort(b[pa], kind="stable")]
+    assert np.array_equal(ob.to_numpy().astype(np.int64), want)
+    # descending inside groups
+    _, od, _ = gdk.BATsort(mk(gdk, gdk.TYPE_int, b), o=oa, g=ga, reverse=True, nilslast=True)
+    want = np.lexsort((-b.astype(np.int64), a))
+    assert np.array_equal(od.to_numpy().astype(np.int64), want)
+
+
+def test_sort_sub_errors(gdk):
+    b = mk(gdk, gdk.TYPE_int, np.array([3, 1, 2], np.int32))
+    bad_g = mk(gdk, gdk.TYPE_oid, np.array([2, 1, 0], np.uint64))
+    with pytest.raises(gdk.GDKError, match="g must have type oid, sorted"):
+        gdk.BATsort(b, g=bad_g)
+    with pytest.raises(gdk.GDKError, match="o must have type oid"):
+        gdk.BATsort(b, o=mk(gdk, gdk.TYPE_oid, np.array([0, 1], np.uint64)))
+
+
+@pytest.mark.parametrize("tname,dt", [("int", np.int32), ("lng", np.int64), ("bte", np.int8)])
+def test_unique(gdk, tname, dt):
+    r = rng(99)
+    tp = getattr(gdk, "TYPE_" + tname)
+    v = r.integers(-40, 40, 50_000).astype(dt)
+    u = gdk.BATunique(mk(gdk, tp, v, hseqbase=7))
+    _, first = np.unique(v, return_index=True)
+    assert np.array_equal(u.to_numpy(), np.sort(first).astype(np.uint64) + 7)
+    s = np.sort(r.choice(50_000, 9_000, replace=False)).astype(np.uint64) + 7
+    u2 = gdk.BATunique(mk(gdk, tp, v, hseqbase=7), mk(gdk, gdk.TYPE_oid, s))
+    sv = v[(s - 7).astype(np.int64)]
+    _, f2 = np.unique(sv, return_index=True)
+    assert np.array_equal(u2.to_numpy(), s[np.sort(f2)])
