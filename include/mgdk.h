@@ -129,6 +129,13 @@ int mgdk_BATsort(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups,
 /* gdk_unique.c:30 BATunique: candidate list of the first occurrence of
  * every distinct value of b[s] */
 mgdk_bat *mgdk_BATunique(mgdk_bat *b, mgdk_bat *s);
+/* gdk_firstn.c:1280 BATfirstn: candidate list of the n first rows of b[s]
+ * in (g, b) order (asc / nilslast); gids != NULL or distinct: every row
+ * tied with the last one is included (as the reference); otherwise the
+ * first tied rows in candidate order (the reference: whichever its heap
+ * kept) */
+int mgdk_BATfirstn(mgdk_bat **topn, mgdk_bat **gids, mgdk_bat *b, mgdk_bat *s, mgdk_bat *g, mgdk_BUN n,
+		   bool asc, bool nilslast, bool distinct);
 
 /* ---- window bounds (gdk/gdk_analytic.h:27-30;
  *      gdk/gdk_analytic_bounds.c:1440) ------------------------------------- */

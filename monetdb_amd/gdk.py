@@ -115,6 +115,8 @@ _SIGS = {
     "mgdk_gen_window_column": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, PP, PP]),
     "mgdk_BAThashpartition": (C.c_int, [PP, C.c_void_p, C.c_int, C.c_void_p]),
     "mgdk_BATunique": (P, [C.c_void_p, C.c_void_p]),
+    "mgdk_BATfirstn": (C.c_int, [PP, PP, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_bool, C.c_bool,
+                                 C.c_bool]),
     "mgdk_GDKanalyticalsum": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_int, C.c_int]),
     "mgdk_GDKanalyticalcount": (C.c_int, [C.c_void_p] * 6 + [C.c_bool, C.c_int, C.c_int]),
     "mgdk_BATlowerbound2": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
@@ -404,6 +406,14 @@ def BATsort(b, o=None, g=None, reverse=False, nilslast=False, stable=True):
 def BATunique(b, s=None):
     """Candidate list of the first occurrence of each distinct value (gdk_unique.c:30)."""
     return BAT(lib().mgdk_BATunique(b.ptr, _p(s)))
+
+
+def BATfirstn(b, n, s=None, g=None, asc=True, nilslast=False, distinct=False, want_gids=False):
+    """(topn candidate list, gids or None) -- gdk_firstn.c:1280."""
+    t, gi = P(), P()
+    _chk(lib().mgdk_BATfirstn(C.byref(t), C.byref(gi) if want_gids else None, b.ptr, _p(s), _p(g), n,
+                              asc, nilslast, distinct))
+    return BAT(t), (BAT(gi) if want_gids else None)
 
 
 def GDKanalyticalwindowbounds(b, p, limit, preceding, tp1=TYPE_lng, tp2=TYPE_lng, unit=1):
