@@ -194,6 +194,18 @@ int mgdk_GDKanalyticalsum(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mg
 int mgdk_GDKanalyticalcount(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e,
 			    bool ignore_nils, int tpe, int frame_type);
 
+/* ---- compressed column inputs (sql/backends/monet5/dict.c, for.c):
+ *      a DICT column is codes o (bte/sht/int, read unsigned) + the
+ *      dictionary u of distinct values; a FOR column is bte/sht offsets
+ *      from one minimum.  Selections run on the codes. ---------------- */
+int mgdk_DICTcompress(mgdk_bat **o, mgdk_bat **u, mgdk_bat *b, bool ordered, bool smallest_type); /* dict.c:110 */
+mgdk_bat *mgdk_DICTdecompress(mgdk_bat *o, mgdk_bat *u);                                         /* dict.c:352 */
+mgdk_bat *mgdk_DICTselect(mgdk_bat *lo, mgdk_bat *lc, mgdk_bat *lv, const void *l, const void *h,
+			  bool li, bool hi, bool anti);                                         /* dict.c:926 */
+mgdk_bat *mgdk_DICTthetaselect(mgdk_bat *lo, mgdk_bat *lc, mgdk_bat *lv, const void *v, const char *op); /* dict.c:788 */
+mgdk_bat *mgdk_FORcompress(mgdk_bat *b, int64_t *minval);                                          /* for.c:148 */
+mgdk_bat *mgdk_FORdecompress(mgdk_bat *o, int64_t minval, int tp);                                 /* for.c:30 */
+
 /* ---- multi-GPU exchange steps (SURVEY.md §8 e).  The reference shards a
  *      plan by row ranges (opt_mitosis.c:150-230) and re-aggregates packed
  *      partials (opt_mergetable.c:1496-1885); across GPUs the group / join

@@ -115,6 +115,13 @@ _SIGS = {
     "mgdk_gen_window_column": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, PP, PP]),
     "mgdk_BAThashpartition": (C.c_int, [PP, C.c_void_p, C.c_int, C.c_void_p]),
     "mgdk_BATunique": (P, [C.c_void_p, C.c_void_p]),
+    "mgdk_DICTcompress": (C.c_int, [PP, PP, C.c_void_p, C.c_bool, C.c_bool]),
+    "mgdk_DICTdecompress": (P, [C.c_void_p, C.c_void_p]),
+    "mgdk_DICTselect": (P, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_bool, C.c_bool,
+                            C.c_bool]),
+    "mgdk_DICTthetaselect": (P, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_char_p]),
+    "mgdk_FORcompress": (P, [C.c_void_p, C.c_void_p]),
+    "mgdk_FORdecompress": (P, [C.c_void_p, C.c_int64, C.c_int]),
     "mgdk_BATfirstn": (C.c_int, [PP, PP, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_bool, C.c_bool,
                                  C.c_bool]),
     "mgdk_GDKanalyticalsum": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_int, C.c_int]),
@@ -414,6 +421,39 @@ def BATfirstn(b, n, s=None, g=None, asc=True, nilslast=False, distinct=False, wa
     _chk(lib().mgdk_BATfirstn(C.byref(t), C.byref(gi) if want_gids else None, b.ptr, _p(s), _p(g), n,
                               asc, nilslast, distinct))
     return BAT(t), (BAT(gi) if want_gids else None)
+
+
+def DICTcompress(b, ordered=True, smallest_type=True):
+    """(codes, dictionary) -- dict.c:110."""
+    o, u = P(), P()
+    _chk(lib().mgdk_DICTcompress(C.byref(o), C.byref(u), b.ptr, ordered, smallest_type))
+    return BAT(o), BAT(u)
+
+
+def DICTdecompress(o, u):
+    return BAT(lib().mgdk_DICTdecompress(o.ptr, u.ptr))
+
+
+def DICTselect(lo, lc, lv, low, high, li, hi, anti):
+    keep = []
+    return BAT(lib().mgdk_DICTselect(lo.ptr, _p(lc), lv.ptr, _valptr(lv.ttype, low, keep),
+                                     _valptr(lv.ttype, high, keep), li, hi, anti))
+
+
+def DICTthetaselect(lo, lc, lv, val, op):
+    keep = []
+    return BAT(lib().mgdk_DICTthetaselect(lo.ptr, _p(lc), lv.ptr, _valptr(lv.ttype, val, keep), op.encode()))
+
+
+def FORcompress(b):
+    """(offsets, minval) -- for.c:148."""
+    mn = C.c_int64()
+    o = BAT(lib().mgdk_FORcompress(b.ptr, C.byref(mn)))
+    return o, mn.value
+
+
+def FORdecompress(o, minval, tp):
+    return BAT(lib().mgdk_FORdecompress(o.ptr, minval, tp))
 
 
 def GDKanalyticalwindowbounds(b, p, limit, preceding, tp1=TYPE_lng, tp2=TYPE_lng, unit=1):
