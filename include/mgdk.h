@@ -206,6 +206,29 @@ mgdk_bat *mgdk_DICTthetaselect(mgdk_bat *lo, mgdk_bat *lc, mgdk_bat *lv, const v
 mgdk_bat *mgdk_FORcompress(mgdk_bat *b, int64_t *minval);                                          /* for.c:148 */
 mgdk_bat *mgdk_FORdecompress(mgdk_bat *o, int64_t minval, int tp);                                 /* for.c:30 */
 
+/* ---- persistent BAT heaps -> HBM (gdk_bbp.c:595-714 BBP.dir, gdk_heap.c:729
+ *      HEAPload): entries of a dbfarm's bat/BBP.dir, and one BAT's tail
+ *      (+ string heap) streamed into device memory ------------------------ */
+typedef struct mgdk_bbpentry {
+	int64_t batid;
+	char name[129];
+	char type[33];
+	int32_t tt;             /* MGDK_* id, -1: unknown type */
+	int32_t width;
+	int32_t var;            /* has a variable-size heap */
+	uint32_t props;         /* BBP.dir property bits (sorted 0x1, revsorted 0x80, key 0x100,
+	                           dense 0x200, nonil 0x400, nil 0x800) */
+	uint64_t count;
+	mgdk_oid hseqbase;
+	mgdk_oid tseqbase;
+	uint64_t free;          /* tail bytes */
+	uint64_t vfree;         /* string heap bytes */
+	char tail[256];         /* file names relative to the bat directory */
+	char theap[256];
+} mgdk_bbpentry;
+int mgdk_BBPreaddir(const char *bbp_dir_file, mgdk_bbpentry *out, int maxn, int *n);
+mgdk_bat *mgdk_BATload(const char *bat_dir, const mgdk_bbpentry *e);
+
 /* ---- multi-GPU exchange steps (SURVEY.md §8 e).  The reference shards a
  *      plan by row ranges (opt_mitosis.c:150-230) and re-aggregates packed
  *      partials (opt_mergetable.c:1496-1885); across GPUs the group / join

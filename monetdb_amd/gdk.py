@@ -115,6 +115,8 @@ _SIGS = {
     "mgdk_gen_window_column": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, PP, PP]),
     "mgdk_BAThashpartition": (C.c_int, [PP, C.c_void_p, C.c_int, C.c_void_p]),
     "mgdk_BATunique": (P, [C.c_void_p, C.c_void_p]),
+    "mgdk_BBPreaddir": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.POINTER(C.c_int)]),
+    "mgdk_BATload": (P, [C.c_char_p, C.c_void_p]),
     "mgdk_DICTcompress": (C.c_int, [PP, PP, C.c_void_p, C.c_bool, C.c_bool]),
     "mgdk_DICTdecompress": (P, [C.c_void_p, C.c_void_p]),
     "mgdk_DICTselect": (P, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_bool, C.c_bool,
@@ -175,6 +177,13 @@ def hge_to_int(words):
 def int_to_hge_words(v):
     v &= (1 << 128) - 1
     return v & ((1 << 64) - 1), v >> 64
+
+
+class BBPEntry(C.Structure):
+    _fields_ = [("batid", C.c_int64), ("name", C.c_char * 129), ("type", C.c_char * 33), ("tt", C.c_int32),
+                ("width", C.c_int32), ("var", C.c_int32), ("props", C.c_uint32), ("count", C.c_uint64),
+                ("hseqbase", C.c_uint64), ("tseqbase", C.c_uint64), ("free", C.c_uint64),
+                ("vfree", C.c_uint64), ("tail", C.c_char * 256), ("theap", C.c_char * 256)]
 
 
 class BAT:
@@ -421,6 +430,20 @@ def BATfirstn(b, n, s=None, g=None, asc=True, nilslast=False, distinct=False, wa
     _chk(lib().mgdk_BATfirstn(C.byref(t), C.byref(gi) if want_gids else None, b.ptr, _p(s), _p(g), n,
                               asc, nilslast, distinct))
     return BAT(t), (BAT(gi) if want_gids else None)
+
+
+def BBPreaddir(path):
+    """Entries of a dbfarm's bat/BBP.dir (gdk_bbp.c:595-714)."""
+    n = C.c_int()
+    _chk(lib().mgdk_BBPreaddir(path.encode(), None, 0, C.byref(n)))
+    arr = (BBPEntry * max(1, n.value))()
+    _chk(lib().mgdk_BBPreaddir(path.encode(), C.cast(arr, C.c_void_p), n.value, C.byref(n)))
+    return list(arr[:n.value])
+
+
+def BATload(bat_dir, entry):
+    """Stream one persistent BAT's heaps into HBM (gdk_heap.c:729 HEAPload)."""
+    return BAT(lib().mgdk_BATload(bat_dir.encode(), C.cast(C.pointer(entry), C.c_void_p)))
 
 
 def DICTcompress(b, ordered=True, smallest_type=True):
