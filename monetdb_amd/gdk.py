@@ -142,6 +142,14 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} not built: run python -m monetdb_amd.build")
+        # One HIP runtime per process: torch bundles its own libamdhip64.so.7
+        # (same soname as /opt/rocm's).  Whichever loads first is shared by
+        # both; if ours came first torch's device discovery fails, so let
+        # torch (the plumbing for collectives and device tensors) load first.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             f = getattr(L, name)
