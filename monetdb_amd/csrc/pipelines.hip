@@ -25,6 +25,7 @@ int
 q1_opatatime(mgdk_bat *shipdate, mgdk_bat *rf, mgdk_bat *ls, mgdk_bat *qty, mgdk_bat *price,
 	     mgdk_bat *disc, mgdk_bat *tax, int32_t dmax, mgdk_q1row *rows, int maxgroups, int *ngroups)
 {
+	ProfScope prof("q1_opatatime");
 	Bats t;
 	mgdk_bat *c1 = t.add(mgdk_BATthetaselect(shipdate, nullptr, &dmax, "<="));
 	if (!c1)

@@ -287,8 +287,165 @@ struct Q1Args {
 	int K;
 	uint32_t codes[Q1_MAXK];          // rf << 8 | ls
 	unsigned long long *acc;          // [K][12]: qty, price, discprice(2), charge(2), disc, count (+pad)
-	uint32_t *flags;                  // [0] unknown key, [1] out of range / nil
+	uint32_t *flags;                  // [0] unknown key, [1] out of range / nil, [2] outside narrow bounds
+	int64_t plim;                     // narrow pass: |qty|, |price| < plim
 };
+
+#ifndef MGDK_Q1_MODE
+#define MGDK_Q1_MODE 2
+#endif
+#ifndef MGDK_Q1_UNROLL
+#define MGDK_Q1_UNROLL 2
+#endif
+#ifndef MGDK_Q1_BLOCKS
+#define MGDK_Q1_BLOCKS 1024
+#endif
+// Narrow Q1 pass: when |qty|, |price| < plim and |disc|, |tax| < 2^12 every
+// per-lane partial fits 64 bits (plim = 2^37 / rows-per-lane, set by the
+// host), so a row costs 64-bit arithmetic only; hge appears at the wave
+// reduction.  A row outside the bounds raises flags[2] and the host reruns
+// the wide (hge) pass.  LDSACC keeps the five sums of each group in
+// lane-private LDS slots (one ds_add_u64 per sum per row, no per-group
+// predication); otherwise every group's registers take a predicated add.
+constexpr int64_t Q1_SMALL = (int64_t) 1 << 12;
+
+template <int K, bool LDSACC>
+__global__ __launch_bounds__(256) void
+k_q1n(Q1Args a)
+{
+	__shared__ unsigned long long lacc[LDSACC ? K * 5 * 256 : 1];
+	int64_t s[K][5];
+	uint32_t cnt[K];
+#pragma unroll
+	for (int k = 0; k < K; k++) {
+		cnt[k] = 0;
+#pragma unroll
+		for (int j = 0; j < 5; j++)
+			s[k][j] = 0;
+	}
+	if (LDSACC) {
+		for (int i = threadIdx.x; i < K * 5 * 256; i += 256)
+			lacc[i] = 0;
+		__syncthreads();
+	}
+	uint32_t unknown = 0, bad = 0;
+	typedef int32_t i4 __attribute__((ext_vector_type(4)));
+	typedef int64_t l2 __attribute__((ext_vector_type(2)));
+	typedef uint8_t u4 __attribute__((ext_vector_type(4)));
+	const uint64_t nq = a.n / 4;
+	const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+	const uint64_t pl = (uint64_t) a.plim;
+	auto row = [&](int32_t d, uint32_t code, int64_t q, int64_t p, int64_t di, int64_t t) {
+		if (d == INT32_MIN || d > a.dmax)
+			return;
+		bad |= ((uint64_t) (q + a.plim) >= 2 * pl) | ((uint64_t) (p + a.plim) >= 2 * pl) |
+		       ((uint64_t) (di + Q1_SMALL) >= 2 * Q1_SMALL) | ((uint64_t) (t + Q1_SMALL) >= 2 * Q1_SMALL);
+		const int64_t dp = p * (100 - di);
+		const int64_t ch = dp * (100 + t);
+		const int64_t v[5] = {q, p, dp, ch, di};
+		if (LDSACC) {
+			int g = 0;
+			bool hit = false;
+#pragma unroll
+			for (int k = 0; k < K; k++) {
+				const bool m = code == a.codes[k];
+				g = m ? k : g;
+				hit |= m;
+				cnt[k] += m;
+			}
+			unknown |= !hit;
+			unsigned long long *slot = lacc + (size_t) g * 5 * 256 + threadIdx.x;
+#pragma unroll
+			for (int j = 0; j < 5; j++)
+				__hip_atomic_fetch_add(slot + j * 256, (unsigned long long) v[j], __ATOMIC_RELAXED,
+						       __HIP_MEMORY_SCOPE_WORKGROUP);
+		} else {
+			bool hit = false;
+#pragma unroll
+			for (int k = 0; k < K; k++) {
+				const bool m = code == a.codes[k];
+				hit |= m;
+				cnt[k] += m;
+#pragma unroll
+				for (int j = 0; j < 5; j++)
+					s[k][j] += m ? v[j] : 0;
+			}
+			unknown |= !hit;
+		}
+	};
+	struct Quad {
+		i4 sd;
+		u4 rf, ls;
+		l2 q0, q1, p0, p1, d0, d1, t0, t1;
+	};
+	auto load = [&](uint64_t r, Quad &x) {
+		x.sd = ldv<true>((const i4 *) (a.sd + r));
+		x.rf = ldv<true>((const u4 *) (a.rf + r));
+		x.ls = ldv<true>((const u4 *) (a.ls + r));
+		x.q0 = ldv<true>((const l2 *) (a.qty + r)), x.q1 = ldv<true>((const l2 *) (a.qty + r + 2));
+		x.p0 = ldv<true>((const l2 *) (a.price + r)), x.p1 = ldv<true>((const l2 *) (a.price + r + 2));
+		x.d0 = ldv<true>((const l2 *) (a.disc + r)), x.d1 = ldv<true>((const l2 *) (a.disc + r + 2));
+		x.t0 = ldv<true>((const l2 *) (a.tax + r)), x.t1 = ldv<true>((const l2 *) (a.tax + r + 2));
+	};
+	auto rows4 = [&](const Quad &x) {
+		row(x.sd[0], ((uint32_t) x.rf[0] << 8) | x.ls[0], x.q0[0], x.p0[0], x.d0[0], x.t0[0]);
+		row(x.sd[1], ((uint32_t) x.rf[1] << 8) | x.ls[1], x.q0[1], x.p0[1], x.d0[1], x.t0[1]);
+		row(x.sd[2], ((uint32_t) x.rf[2] << 8) | x.ls[2], x.q1[0], x.p1[0], x.d1[0], x.t1[0]);
+		row(x.sd[3], ((uint32_t) x.rf[3] << 8) | x.ls[3], x.q1[1], x.p1[1], x.d1[1], x.t1[1]);
+	};
+	uint64_t qi = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
+#if MGDK_Q1_UNROLL > 1
+	// two quads in flight per lane
+	for (; qi + stride < nq; qi += 2 * stride) {
+		Quad x, y;
+		load(qi * 4, x);
+		load((qi + stride) * 4, y);
+		rows4(x);
+		rows4(y);
+	}
+#endif
+	for (; qi < nq; qi += stride) {
+		Quad x;
+		load(qi * 4, x);
+		rows4(x);
+	}
+	if (blockIdx.x == 0 && threadIdx.x < (a.n & 3)) {
+		const uint64_t r = nq * 4 + threadIdx.x;
+		row(a.sd[r], ((uint32_t) a.rf[r] << 8) | a.ls[r], a.qty[r], a.price[r], a.disc[r], a.tax[r]);
+	}
+	if (LDSACC) {
+		__syncthreads();
+#pragma unroll
+		for (int k = 0; k < K; k++)
+#pragma unroll
+			for (int j = 0; j < 5; j++)
+				s[k][j] = (int64_t) lacc[((size_t) k * 5 + j) * 256 + threadIdx.x];
+	}
+#pragma unroll
+	for (int k = 0; k < K; k++) {
+		hge v[6] = {(hge) s[k][0], (hge) s[k][1], (hge) s[k][2], (hge) s[k][3], (hge) s[k][4], (hge) cnt[k]};
+#pragma unroll
+		for (int j = 0; j < 6; j++)
+			v[j] = wave_sum128(v[j]);
+		if (__lane_id() == 0) {
+			unsigned long long *acc = a.acc + (size_t) k * 12;
+#pragma unroll
+			for (int j = 0; j < 6; j++)
+				if (v[j] != 0)
+					atomic_add128(acc + 2 * j, v[j]);
+		}
+	}
+	for (int o = 32; o > 0; o >>= 1) {
+		unknown |= __shfl_xor(unknown, o);
+		bad |= __shfl_xor(bad, o);
+	}
+	if (__lane_id() == 0) {
+		if (unknown)
+			atomicOr(&a.flags[0], 1u);
+		if (bad)
+			atomicOr(&a.flags[2], 1u);
+	}
+}
 
 // first qualifying row of every (returnflag, linestatus) code.  Lanes of a
 // wave hold consecutive rows, so per distinct code in the wave only its
@@ -688,14 +845,35 @@ mgdk_q1_fused(mgdk_bat *shipdate, mgdk_bat *returnflag, mgdk_bat *linestatus, mg
 		a.codes[k] = 0xffffffffu;
 	a.acc = acc.as<unsigned long long>();
 	a.flags = (uint32_t *) (a.acc + Q1_MAXK * 12);
-	dim3 g(grid_for(n / 4 + 1, 256, 256 * 16)), blk(256);
-	if (K <= 1) hipLaunchKernelGGL(k_q1<1>, g, blk, 0, st, a);
-	else if (K <= 2) hipLaunchKernelGGL(k_q1<2>, g, blk, 0, st, a);
-	else if (K <= 4) hipLaunchKernelGGL(k_q1<4>, g, blk, 0, st, a);
-	else hipLaunchKernelGGL(k_q1<8>, g, blk, 0, st, a);
+	dim3 g(grid_for(n / 4 + 1, 256, MGDK_Q1_MODE == 0 ? 4096 : MGDK_Q1_BLOCKS)), blk(256);
+	const uint64_t threads = (uint64_t) g.x * 256;
+	const uint64_t per_lane = 4 * ((n / 4 + threads - 1) / threads) + 3;
+	a.plim = std::min<int64_t>(Q1_LIM, (int64_t) (((uint64_t) 1 << 37) / per_lane));
+	const bool lds = MGDK_Q1_MODE == 2;
+	if (MGDK_Q1_MODE == 0)
+		;
+	else if (K <= 1) hipLaunchKernelGGL((lds ? k_q1n<1, true> : k_q1n<1, false>), g, blk, 0, st, a);
+	else if (K <= 2) hipLaunchKernelGGL((lds ? k_q1n<2, true> : k_q1n<2, false>), g, blk, 0, st, a);
+	else if (K <= 4) hipLaunchKernelGGL((lds ? k_q1n<4, true> : k_q1n<4, false>), g, blk, 0, st, a);
+	else hipLaunchKernelGGL((lds ? k_q1n<8, true> : k_q1n<8, false>), g, blk, 0, st, a);
 	unsigned long long *hr = (unsigned long long *) pinned(Q1_MAXK * 12 * 8 + 64);
-	if (!hip_ok(hipMemcpyAsync(hr, acc.p, Q1_MAXK * 12 * 8 + 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
-		return -1;
+	const size_t accb = Q1_MAXK * 12 * 8 + 16;
+	if (MGDK_Q1_MODE != 0) {
+		if (!hip_ok(hipMemcpyAsync(hr, acc.p, accb, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+			return -1;
+	}
+	if (MGDK_Q1_MODE == 0 || ((const uint32_t *) (hr + Q1_MAXK * 12))[2] != 0) {
+		// wide pass: values beyond the narrow bounds (or narrow pass disabled)
+		ProfScope profw("q1_wide");
+		if (!hip_ok(hipMemsetAsync(acc.p, 0, Q1_MAXK * 12 * 8 + 64, st), "memset"))
+			return -1;
+		if (K <= 1) hipLaunchKernelGGL(k_q1<1>, g, blk, 0, st, a);
+		else if (K <= 2) hipLaunchKernelGGL(k_q1<2>, g, blk, 0, st, a);
+		else if (K <= 4) hipLaunchKernelGGL(k_q1<4>, g, blk, 0, st, a);
+		else hipLaunchKernelGGL(k_q1<8>, g, blk, 0, st, a);
+		if (!hip_ok(hipMemcpyAsync(hr, acc.p, accb, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+			return -1;
+	}
 	const uint32_t *fl = (const uint32_t *) (hr + Q1_MAXK * 12);
 	if (fl[0] || fl[1])
 		return q1_opatatime(shipdate, returnflag, linestatus, quantity, extendedprice, discount, tax, dmax,

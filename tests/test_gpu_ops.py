@@ -332,3 +332,45 @@ def test_q1_parity(gdk, ora, n):
     assert [(r["returnflag"], r["linestatus"], r["first_row"]) for r in got] == \
         [(r["returnflag"], r["linestatus"], r["first_row"]) for r in op]
     assert _q1_rows(op) == _q1_rows(want)
+
+
+@pytest.mark.parametrize("case", ["none", "tax_wide", "disc_neg_wide", "price_beyond_wide", "qty_nil",
+                                  "price_lane_bound"])
+def test_q1_value_ranges(gdk, ora, case):
+    """The fused Q1 takes a 64-bit pass when every value is within narrow
+    bounds, reruns with 128-bit accumulation otherwise, and falls back to
+    the op-at-a-time plan beyond 2^31 or on nils; all must agree with the
+    oracle."""
+    # price_lane_bound: with ~80 rows per lane the narrow price bound
+    # (2^37 / rows-per-lane) drops below 2^31
+    n = 20_000_003 if case == "price_lane_bound" else 300_007
+    cols = gdk.tpch_lineitem(11, 0, n, 20_000)
+    host = ora.tpch_lineitem(11, 0, n, 20_000)
+    if case == "tax_wide":
+        host["tax"][::101] = 5000
+    elif case == "disc_neg_wide":
+        host["discount"][3::211] = -70000
+    elif case == "price_beyond_wide":
+        host["extendedprice"][::997] = (1 << 32) + 12345
+    elif case == "price_lane_bound":
+        host["extendedprice"][::99991] = 1_900_000_000
+    elif case == "qty_nil":
+        host["quantity"][5::1009] = np.iinfo(np.int64).min
+    for k in ("tax", "discount", "extendedprice", "quantity"):
+        cols[k] = gdk.BAT.from_numpy(gdk.TYPE_lng, host[k])
+    gdk.prof_reset()
+    gdk.prof_enable(True)
+    got = gdk.q1_fused(cols, ora.mkdate(1998, 9, 2))
+    gdk.prof_enable(False)
+    wide = gdk.prof_get("q1_wide")[1]
+    opat = gdk.prof_get("q1_opatatime")[1]
+    assert (wide, opat) == {"none": (0, 0), "tax_wide": (1, 0), "disc_neg_wide": (1, 0), "price_lane_bound": (1, 0),
+                            "price_beyond_wide": (1, 1), "qty_nil": (1, 1)}[case]
+    if case == "qty_nil":
+        # nil quantities: the reference's sum skips nils; the oracle's Q1 is
+        # the op-at-a-time restatement, so compare against the device plan
+        op = gdk.q1_fused(cols, ora.mkdate(1998, 9, 2), fused=False)
+        assert _q1_rows(got) == _q1_rows(op)
+        return
+    want = ora.q1(host, 4)
+    assert _q1_rows(got) == _q1_rows(want)
