@@ -12,7 +12,7 @@ partial revenues.
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 Rank 0 prints one JSON line.  The `roofline` object prices the dominant kernel
-(k_q6) from HIP events on the library stream; `cpu_baseline` times the CPU
+(k_q6c) from HIP events on the library stream; `cpu_baseline` times the CPU
 oracle (oracle/, a restatement of the reference GDK operators, op-at-a-time
 with mitosis-style threading) on a bounded sample of the same workload.
 """
@@ -112,7 +112,7 @@ def main():
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
 
-    # kernel time from HIP events around k_q6 on the library stream
+    # kernel time from HIP events around k_q6c on the library stream
     gdk.prof_reset()
     gdk.prof_enable(True)
     nprof = max(5, min(args.steps, 20))
@@ -152,6 +152,7 @@ def main():
                        "hbm_gbs_per_gpu": round(rows * Q1_BYTES_PER_ROW / (q1k / max(1, q1n)) / 1e6, 1),
                        "roofline_frac": round(rows * Q1_BYTES_PER_ROW / (q1k / max(1, q1n)) / 1e6
                                               / HBM_PEAK_GBS, 4),
+                       "kernel": "k_q1n", "traffic": pmc_traffic("k_q1n", rows),
                        "groups": len(q1),
                        "count_order": sum(r["count_order"] for r in q1)}
     if not args.no_q1 and rank == 0:
@@ -192,7 +193,7 @@ def main():
                        "parallelism": "row-range shards x%d" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": pmc_traffic("k_q6", rows), "kernel": "k_q6",
+                         "traffic": pmc_traffic("k_q6c", rows), "kernel": "k_q6c",
                          "kernel_ms": round(kern_ms, 4),
                          "bytes_per_launch": rows * Q6_BYTES_PER_ROW},
             "cpu_baseline": cpu,
@@ -236,10 +237,20 @@ def cpu_baseline(args):
         ora.q6(cols, threads)
         times.append(time.perf_counter() - t)
     med = statistics.median(times)
+    # the same sample on one core (the reference's MAL plan runs the GDK
+    # operators of one query single-threaded unless mitosis splits it)
+    t1 = []
+    for _ in range(3):
+        t = time.perf_counter()
+        ora.q6(cols, 1)
+        t1.append(time.perf_counter() - t)
+    med1 = statistics.median(t1)
     return {"value": round(n / med / 1e9, 4), "unit": "Grows/s", "cores": threads, "kind": "port",
             "sample": "TPC-H Q6 op-at-a-time (oracle GDK restatement), %d rows (SF%g), "
                       "%d threads, median of 5" % (n, args.cpu_sf, threads),
-            "ms": round(med * 1e3, 2)}
+            "ms": round(med * 1e3, 2),
+            "single_thread": {"value": round(n / med1 / 1e9, 4), "unit": "Grows/s", "cores": 1,
+                              "ms": round(med1 * 1e3, 2), "sample": "same rows, median of 3"}}
 
 
 if __name__ == "__main__":

@@ -298,18 +298,22 @@ struct Q1Args {
 #define MGDK_Q1_UNROLL 2
 #endif
 #ifndef MGDK_Q1_BLOCKS
-#define MGDK_Q1_BLOCKS 1024
+#define MGDK_Q1_BLOCKS 256
 #endif
-// Narrow Q1 pass: when |qty|, |price| < plim and |disc|, |tax| < 2^12 every
-// per-lane partial fits 64 bits (plim = 2^37 / rows-per-lane, set by the
-// host), so a row costs 64-bit arithmetic only; hge appears at the wave
+#ifndef MGDK_Q1_LAYOUT
+#define MGDK_Q1_LAYOUT 1
+#endif
+
+// Narrow Q1 pass: when |qty|, |price| < plim and |disc|, |tax| < 2^8 every
+// per-lane partial fits 64 bits (|charge| < plim * 2^18 per row, so
+// plim = 2^45 / rows-per-lane, capped at 2^31, set by the host), so a row costs 64-bit arithmetic only; hge appears at the wave
 // reduction.  A row outside the bounds raises flags[2] and the host reruns
 // the wide (hge) pass.  LDSACC keeps the five sums of each group in
 // lane-private LDS slots (one ds_add_u64 per sum per row, no per-group
 // predication); otherwise every group's registers take a predicated add.
-constexpr int64_t Q1_SMALL = (int64_t) 1 << 12;
+constexpr int64_t Q1_SMALL = (int64_t) 1 << 8;
 
-template <int K, bool LDSACC>
+template <int K, bool LDSACC, int LAYOUT>
 __global__ __launch_bounds__(256) void
 k_q1n(Q1Args a)
 {
@@ -340,8 +344,9 @@ k_q1n(Q1Args a)
 			return;
 		bad |= ((uint64_t) (q + a.plim) >= 2 * pl) | ((uint64_t) (p + a.plim) >= 2 * pl) |
 		       ((uint64_t) (di + Q1_SMALL) >= 2 * Q1_SMALL) | ((uint64_t) (t + Q1_SMALL) >= 2 * Q1_SMALL);
-		const int64_t dp = p * (100 - di);
-		const int64_t ch = dp * (100 + t);
+		// unsigned: wraps (harmlessly) only on rows that raise bad
+		const int64_t dp = (int64_t) ((uint64_t) p * (uint64_t) (100 - di));
+		const int64_t ch = (int64_t) ((uint64_t) dp * (uint64_t) (100 + t));
 		const int64_t v[5] = {q, p, dp, ch, di};
 		if (LDSACC) {
 			int g = 0;
@@ -393,6 +398,56 @@ k_q1n(Q1Args a)
 		row(x.sd[2], ((uint32_t) x.rf[2] << 8) | x.ls[2], x.q1[0], x.p1[0], x.d1[0], x.t1[0]);
 		row(x.sd[3], ((uint32_t) x.rf[3] << 8) | x.ls[3], x.q1[1], x.p1[1], x.d1[1], x.t1[1]);
 	};
+	if constexpr (LAYOUT == 1) {
+	// contiguous layout: a wave owns 256-row chunks; lane l takes rows
+	// 2l, 2l+1 and 128+2l, 128+2l+1 (each lng load covers 1 KiB)
+	typedef int32_t i2 __attribute__((ext_vector_type(2)));
+	typedef uint8_t u2 __attribute__((ext_vector_type(2)));
+	struct Chunk {
+		i2 s0, s1;
+		u2 f0, f1, l0, l1;
+		l2 q0, q1, p0, p1, d0, d1, t0, t1;
+	};
+	const unsigned lane = __lane_id();
+	auto cload = [&](uint64_t c, Chunk &x) {
+		const uint64_t r0 = c * 256 + 2 * lane, r1 = r0 + 128;
+		x.s0 = ldv<true>((const i2 *) (a.sd + r0)), x.s1 = ldv<true>((const i2 *) (a.sd + r1));
+		x.f0 = ldv<true>((const u2 *) (a.rf + r0)), x.f1 = ldv<true>((const u2 *) (a.rf + r1));
+		x.l0 = ldv<true>((const u2 *) (a.ls + r0)), x.l1 = ldv<true>((const u2 *) (a.ls + r1));
+		x.q0 = ldv<true>((const l2 *) (a.qty + r0)), x.q1 = ldv<true>((const l2 *) (a.qty + r1));
+		x.p0 = ldv<true>((const l2 *) (a.price + r0)), x.p1 = ldv<true>((const l2 *) (a.price + r1));
+		x.d0 = ldv<true>((const l2 *) (a.disc + r0)), x.d1 = ldv<true>((const l2 *) (a.disc + r1));
+		x.t0 = ldv<true>((const l2 *) (a.tax + r0)), x.t1 = ldv<true>((const l2 *) (a.tax + r1));
+	};
+	auto crows = [&](const Chunk &x) {
+		row(x.s0[0], ((uint32_t) x.f0[0] << 8) | x.l0[0], x.q0[0], x.p0[0], x.d0[0], x.t0[0]);
+		row(x.s0[1], ((uint32_t) x.f0[1] << 8) | x.l0[1], x.q0[1], x.p0[1], x.d0[1], x.t0[1]);
+		row(x.s1[0], ((uint32_t) x.f1[0] << 8) | x.l1[0], x.q1[0], x.p1[0], x.d1[0], x.t1[0]);
+		row(x.s1[1], ((uint32_t) x.f1[1] << 8) | x.l1[1], x.q1[1], x.p1[1], x.d1[1], x.t1[1]);
+	};
+	const uint64_t nch = a.n / 256;
+	const uint64_t nw = (uint64_t) gridDim.x * (blockDim.x / 64);
+	uint64_t c = ((uint64_t) blockIdx.x * blockDim.x + threadIdx.x) / 64;
+	// MGDK_Q1_UNROLL chunks in flight per wave
+	for (; c + (MGDK_Q1_UNROLL - 1) * nw < nch; c += MGDK_Q1_UNROLL * nw) {
+		Chunk x[MGDK_Q1_UNROLL];
+#pragma unroll
+		for (int u = 0; u < MGDK_Q1_UNROLL; u++)
+			cload(c + u * nw, x[u]);
+#pragma unroll
+		for (int u = 0; u < MGDK_Q1_UNROLL; u++)
+			crows(x[u]);
+	}
+	for (; c < nch; c += nw) {
+		Chunk x;
+		cload(c, x);
+		crows(x);
+	}
+	if (blockIdx.x == 0 && threadIdx.x < (a.n & 255)) {
+		const uint64_t r = nch * 256 + threadIdx.x;
+		row(a.sd[r], ((uint32_t) a.rf[r] << 8) | a.ls[r], a.qty[r], a.price[r], a.disc[r], a.tax[r]);
+	}
+	} else {
 	uint64_t qi = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
 #if MGDK_Q1_UNROLL > 1
 	// two quads in flight per lane
@@ -412,6 +467,7 @@ k_q1n(Q1Args a)
 	if (blockIdx.x == 0 && threadIdx.x < (a.n & 3)) {
 		const uint64_t r = nq * 4 + threadIdx.x;
 		row(a.sd[r], ((uint32_t) a.rf[r] << 8) | a.ls[r], a.qty[r], a.price[r], a.disc[r], a.tax[r]);
+	}
 	}
 	if (LDSACC) {
 		__syncthreads();
@@ -699,9 +755,13 @@ mgdk_tpch_lineitem(uint64_t seed, uint64_t row0, uint64_t n, uint64_t sf_parts, 
 // Q6 launch variants (tuning): variant = layout*3 + unroll_idx (+8: nt loads)
 //   layout 0: lane owns 4 consecutive rows (k_q6); 1: contiguous (k_q6c)
 //   unroll_idx 0,1,2 -> UNROLL 1,2,4;  bpc = workgroups per CU (256 CUs)
-// default from tools/q6_tune.py on MI355X (profiles/r01/q6_tune.log):
-// 4-row lanes, 2 iterations in flight, nontemporal loads, 16 WG/CU
-static int q6_variant = 9, q6_bpc = 16;
+// default from tools/q6_tune.py on MI355X (profiles/r01/q6_tune*.log):
+// contiguous 256-row chunks per wave (1 KiB per lng load instruction),
+// 4 chunks in flight, nontemporal loads, 12 WG/CU (odd WG/CU counts lose
+// 5-7 % with this layout)
+static int q6_variant = 14, q6_bpc = 12;
+// fused Q1 main pass (tools/q1_tune.py, profiles/r01/q1_tune.log)
+static int q1_layout = MGDK_Q1_LAYOUT, q1_blocks = MGDK_Q1_BLOCKS;
 
 static void
 launch_q6(const Q6Args &a, int variant, int bpc, hipStream_t st)
@@ -724,6 +784,15 @@ launch_q6(const Q6Args &a, int variant, int bpc, hipStream_t st)
 
 int mgdk_q6_fused(mgdk_bat *shipdate, mgdk_bat *discount, mgdk_bat *quantity, mgdk_bat *extendedprice,
 		  int32_t d0, int32_t d1, int64_t dlo, int64_t dhi, int64_t qmax, void *revenue);
+
+// select the fused Q1 main-pass layout (0: 4-row lanes, 1: 256-row chunks
+// per wave) and workgroup count (tuning hook, not ABI)
+void
+mgdk_q1_set_variant(int layout, int blocks)
+{
+	q1_layout = layout == 1 ? 1 : 0;
+	q1_blocks = blocks > 0 ? blocks : MGDK_Q1_BLOCKS;
+}
 
 // select the Q6 launch variant for subsequent calls (tuning hook, not ABI)
 void
@@ -845,17 +914,24 @@ mgdk_q1_fused(mgdk_bat *shipdate, mgdk_bat *returnflag, mgdk_bat *linestatus, mg
 		a.codes[k] = 0xffffffffu;
 	a.acc = acc.as<unsigned long long>();
 	a.flags = (uint32_t *) (a.acc + Q1_MAXK * 12);
-	dim3 g(grid_for(n / 4 + 1, 256, MGDK_Q1_MODE == 0 ? 4096 : MGDK_Q1_BLOCKS)), blk(256);
+	const int layout = q1_layout;
+	dim3 g(grid_for(n / 4 + 1, 256, MGDK_Q1_MODE == 0 ? 4096 : (unsigned) q1_blocks)), blk(256);
 	const uint64_t threads = (uint64_t) g.x * 256;
-	const uint64_t per_lane = 4 * ((n / 4 + threads - 1) / threads) + 3;
-	a.plim = std::min<int64_t>(Q1_LIM, (int64_t) (((uint64_t) 1 << 37) / per_lane));
-	const bool lds = MGDK_Q1_MODE == 2;
+	// rows one lane can see: quads (layout 0) or 4 rows per 256-row chunk
+	// per wave (layout 1), plus the tail rows
+	const uint64_t per_lane = layout == 1 ? 4 * ((n / 256 + threads / 64 - 1) / (threads / 64)) + 1
+					      : 4 * ((n / 4 + threads - 1) / threads) + 3;
+	a.plim = std::min<int64_t>(Q1_LIM, (int64_t) (((uint64_t) 1 << 45) / per_lane));
+	constexpr bool lds = MGDK_Q1_MODE == 2;
+#define Q1N(KK) do { if (layout == 1) hipLaunchKernelGGL((k_q1n<KK, lds, 1>), g, blk, 0, st, a); \
+		     else hipLaunchKernelGGL((k_q1n<KK, lds, 0>), g, blk, 0, st, a); } while (0)
 	if (MGDK_Q1_MODE == 0)
 		;
-	else if (K <= 1) hipLaunchKernelGGL((lds ? k_q1n<1, true> : k_q1n<1, false>), g, blk, 0, st, a);
-	else if (K <= 2) hipLaunchKernelGGL((lds ? k_q1n<2, true> : k_q1n<2, false>), g, blk, 0, st, a);
-	else if (K <= 4) hipLaunchKernelGGL((lds ? k_q1n<4, true> : k_q1n<4, false>), g, blk, 0, st, a);
-	else hipLaunchKernelGGL((lds ? k_q1n<8, true> : k_q1n<8, false>), g, blk, 0, st, a);
+	else if (K <= 1) Q1N(1);
+	else if (K <= 2) Q1N(2);
+	else if (K <= 4) Q1N(4);
+	else Q1N(8);
+#undef Q1N
 	unsigned long long *hr = (unsigned long long *) pinned(Q1_MAXK * 12 * 8 + 64);
 	const size_t accb = Q1_MAXK * 12 * 8 + 16;
 	if (MGDK_Q1_MODE != 0) {

@@ -341,8 +341,8 @@ def test_q1_value_ranges(gdk, ora, case):
     bounds, reruns with 128-bit accumulation otherwise, and falls back to
     the op-at-a-time plan beyond 2^31 or on nils; all must agree with the
     oracle."""
-    # price_lane_bound: with ~80 rows per lane the narrow price bound
-    # (2^37 / rows-per-lane) drops below 2^31
+    # price_lane_bound: on ONE workgroup (tuning hook) a lane sees ~78k rows,
+    # so the narrow price bound 2^45 / rows-per-lane drops to ~4.5e8
     n = 20_000_003 if case == "price_lane_bound" else 300_007
     cols = gdk.tpch_lineitem(11, 0, n, 20_000)
     host = ora.tpch_lineitem(11, 0, n, 20_000)
@@ -353,15 +353,23 @@ def test_q1_value_ranges(gdk, ora, case):
     elif case == "price_beyond_wide":
         host["extendedprice"][::997] = (1 << 32) + 12345
     elif case == "price_lane_bound":
-        host["extendedprice"][::99991] = 1_900_000_000
+        host["extendedprice"][::99991] = 600_000_000
     elif case == "qty_nil":
         host["quantity"][5::1009] = np.iinfo(np.int64).min
     for k in ("tax", "discount", "extendedprice", "quantity"):
         cols[k] = gdk.BAT.from_numpy(gdk.TYPE_lng, host[k])
+    import ctypes
+    tune = gdk.lib().mgdk_q1_set_variant
+    tune.argtypes = [ctypes.c_int, ctypes.c_int]
+    if case == "price_lane_bound":
+        tune(1, 1)
     gdk.prof_reset()
     gdk.prof_enable(True)
-    got = gdk.q1_fused(cols, ora.mkdate(1998, 9, 2))
-    gdk.prof_enable(False)
+    try:
+        got = gdk.q1_fused(cols, ora.mkdate(1998, 9, 2))
+    finally:
+        gdk.prof_enable(False)
+        tune(1, 0)
     wide = gdk.prof_get("q1_wide")[1]
     opat = gdk.prof_get("q1_opatatime")[1]
     assert (wide, opat) == {"none": (0, 0), "tax_wide": (1, 0), "disc_neg_wide": (1, 0), "price_lane_bound": (1, 0),
@@ -374,3 +382,23 @@ def test_q1_value_ranges(gdk, ora, case):
         return
     want = ora.q1(host, 4)
     assert _q1_rows(got) == _q1_rows(want)
+
+
+@pytest.mark.parametrize("case", ["none", "price_huge", "price_neg_nil"])
+def test_q6_value_ranges(gdk, ora, case):
+    """Q6 accumulates revenue in 128 bits: prices near 2^60 (products beyond
+    64 bits), negative prices and nil prices agree with the oracle."""
+    n = 400_009
+    cols = gdk.tpch_lineitem(13, 0, n, 20_000)
+    host = ora.tpch_lineitem(13, 0, n, 20_000)
+    if case == "price_huge":
+        host["extendedprice"][::61] = (1 << 60) + 7
+        host["extendedprice"][1::67] = -(1 << 60) - 3
+    elif case == "price_neg_nil":
+        host["extendedprice"][::13] *= -1
+        host["extendedprice"][5::29] = np.iinfo(np.int64).min
+    cols["extendedprice"] = gdk.BAT.from_numpy(gdk.TYPE_lng, host["extendedprice"])
+    d0, d1 = ora.mkdate(1994, 1, 1), ora.mkdate(1995, 1, 1)
+    got = gdk.q6_fused(cols["shipdate"], cols["discount"], cols["quantity"],
+                       cols["extendedprice"], d0, d1, 5, 7, 2400)
+    assert got == ora.q6(host, 4)

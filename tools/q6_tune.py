@@ -16,7 +16,9 @@ args = (cols["shipdate"], cols["discount"], cols["quantity"], cols["extendedpric
 L = gdk.lib()
 L.mgdk_q6_set_variant.argtypes = [C.c_int, C.c_int]
 ref = gdk.q6_fused(*args)
-variants = [(v, b) for v in (0, 1, 2, 3, 4, 5, 9, 12) for b in (4, 8, 16)]
+vs = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [0, 1, 2, 3, 4, 5, 9, 12]
+bs = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [4, 8, 16]
+variants = [(v, b) for v in vs for b in bs]
 res = {k: [] for k in variants}
 gdk.prof_enable(True)
 for rnd in range(4):
