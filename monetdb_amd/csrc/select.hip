@@ -98,8 +98,20 @@ struct SelArgs {
 // tile, so one tile ticket per 128 KiB: a single counter sustains only ~88
 // atomics/us, MI355X_MICROARCH.md "dequeue"), 16 for candidate lists;
 // loads are issued in batches of 8 rows
-template <bool MAT> constexpr int sel_rows() { return MAT ? 16 : 32; }
-constexpr int BATCH = 8;
+#ifndef MGDK_SEL_EXP
+#define MGDK_SEL_EXP 0
+#endif
+#ifndef MGDK_SEL_STREAM
+#define MGDK_SEL_STREAM 1
+#endif
+#ifndef MGDK_SEL_ROWS
+#define MGDK_SEL_ROWS 32
+#endif
+#ifndef MGDK_SEL_BATCH
+#define MGDK_SEL_BATCH 8
+#endif
+template <bool MAT> constexpr int sel_rows() { return MAT ? 16 : MGDK_SEL_ROWS; }
+constexpr int BATCH = MGDK_SEL_BATCH;
 
 template <typename T, bool MAT, int MODE>
 __global__ __launch_bounds__(256) void
@@ -116,7 +128,11 @@ k_select(SelArgs<T> a)
 
 	const unsigned tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 	if (tid == 0)
+#if MGDK_SEL_EXP & 1
+		s_tile = blockIdx.x;
+#else
 		s_tile = atomicAdd(a.ticket, 1u);
+#endif
 	__syncthreads();
 	const uint32_t tile = s_tile;
 	const uint64_t nslots = a.n + a.shift;
@@ -231,7 +247,11 @@ k_select(SelArgs<T> a)
 			run += e[q];
 		}
 		uint64_t agg = __shfl(x, 63);
+#if MGDK_SEL_EXP & 2
+		uint64_t pre = 0;
+#else
 		uint64_t pre = lookback(a.status, tile, agg, (uint32_t *) &a.meta[1]);
+#endif
 		if (lane == 0) {
 			s_prefix = pre;
 			if (tile == a.ntiles - 1)
@@ -257,6 +277,249 @@ k_select(SelArgs<T> a)
 				o = a.cseq + (j0 + k - a.shift);
 			a.out[pos++] = o;
 		}
+	}
+}
+
+// Dense-candidate scan in three launches, no look-back and no tickets:
+//   k_sel_count  streams the column once: a tile = SROWS rows x 256 lanes x
+//                16 B (64 KiB); the predicate bits go to a bitmap in slot
+//                order (bit j = candidate slot j: 1 bit per value, n/8 bytes)
+//                and the tile's hit count to counts[tile];
+//   k_sel_scan   one workgroup: exclusive prefix of the tile counts;
+//   k_sel_write  per tile: a workgroup scan of the bitmap words' popcounts
+//                ranks every hit; sparse tiles store from the owning lane,
+//                dense tiles go in rounds of 4096 slots whose hits are
+//                placed in LDS in order and stored as one contiguous run.
+// The column is read once; extra traffic is the bitmap twice (2 bits/value).
+constexpr int SROWS = 16;
+
+template <typename T> constexpr int sel_v() { return (int) (16 / sizeof(T)); }
+// bitmap words per tile and per lane of k_sel_write
+template <typename T> constexpr int sel_wpt() { return SROWS * 256 * sel_v<T>() / 32; }
+template <typename T> constexpr int sel_wpl() { return sel_wpt<T>() >= 256 ? sel_wpt<T>() / 256 : 1; }
+
+template <typename T, int MODE>
+__global__ __launch_bounds__(256) void
+k_sel_count(SelArgs<T> a, uint32_t *bits, uint32_t *counts)
+{
+	constexpr int V = sel_v<T>(), L = 32 / V;   // lanes per bitmap word
+	typedef T vec_t __attribute__((ext_vector_type(V)));
+	const unsigned tid = threadIdx.x, lane = tid & 63;
+	const uint32_t t = blockIdx.x;
+	const uint64_t nslots = a.n + a.shift;
+	const bool full = (t > 0 || a.shift == 0) && ((uint64_t) t + 1) * SROWS * 256 * V <= nslots;
+	vec_t x[SROWS];
+	if (full) {
+#pragma unroll
+		for (int r = 0; r < SROWS; r++)
+			x[r] = __builtin_nontemporal_load((const vec_t *) (a.col_al + (((uint64_t) t * SROWS + r) * 256 + tid) * V));
+	} else {
+#pragma unroll
+		for (int r = 0; r < SROWS; r++) {
+			const uint64_t j0 = (((uint64_t) t * SROWS + r) * 256 + tid) * V;
+			if (j0 < nslots)
+				x[r] = *(const vec_t *) (a.col_al + j0);
+		}
+	}
+	uint32_t cnt = 0;
+#pragma unroll
+	for (int r = 0; r < SROWS; r++) {
+		const uint64_t j0 = (((uint64_t) t * SROWS + r) * 256 + tid) * V;
+		uint32_t m = 0;
+		if (full) {
+#pragma unroll
+			for (int k = 0; k < V; k++)
+				m |= (uint32_t) sel_eval<MODE>(a.pred, (T) x[r][k]) << k;
+		} else if (j0 < nslots) {
+#pragma unroll
+			for (int k = 0; k < V; k++) {
+				const uint64_t j = j0 + k;
+				const bool ok = j >= a.shift && j < nslots && sel_eval<MODE>(a.pred, (T) x[r][k]);
+				m |= (uint32_t) ok << k;
+			}
+		}
+		cnt += __popc(m);
+		// gather the L lanes' V-bit pieces of one 32-bit word
+		uint32_t wv = m << ((lane % L) * V);
+#pragma unroll
+		for (int o = 1; o < L; o <<= 1)
+			wv |= __shfl_xor(wv, o);
+		if (lane % L == 0)
+			bits[j0 / 32] = wv;
+	}
+	cnt = block_reduce<uint32_t>(cnt, [](uint32_t p, uint32_t q) { return p + q; });
+	if (tid == 0)
+		counts[t] = cnt;
+}
+
+// exclusive prefix of counts[0..n) into pre[0..n), total into meta[0]; one
+// workgroup, thread i owns the consecutive run [i*P, (i+1)*P), all of whose
+// loads are issued before the first use (one memory latency in all)
+__global__ __launch_bounds__(1024) void
+k_sel_scan(const uint32_t *counts, uint64_t *pre, uint32_t n, uint64_t *meta)
+{
+	__shared__ uint64_t s_wave[16];
+	const unsigned tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+	const uint32_t P = (n + 1023) / 1024;
+	const uint64_t lo = (uint64_t) tid * P, hi = std::min<uint64_t>(lo + P, n);
+	uint64_t own = 0;
+	constexpr int B = 8;
+	for (uint64_t i = lo; i < hi; i += B) {
+		uint32_t v[B];
+#pragma unroll
+		for (int k = 0; k < B; k++)
+			v[k] = i + k < hi ? counts[i + k] : 0u;
+#pragma unroll
+		for (int k = 0; k < B; k++)
+			own += v[k];
+	}
+	uint64_t x = own;
+#pragma unroll
+	for (int o = 1; o < 64; o <<= 1) {
+		const uint64_t y = __shfl_up(x, o);
+		if ((int) lane >= o)
+			x += y;
+	}
+	if (lane == 63)
+		s_wave[wave] = x;
+	__syncthreads();
+	uint64_t run = x - own;
+	for (unsigned q = 0; q < wave; q++)
+		run += s_wave[q];
+	for (uint64_t i = lo; i < hi; i++) {
+		const uint32_t c = counts[i];   // cached from the first sweep
+		pre[i] = run;
+		run += c;
+	}
+	if (tid == 1023) {
+		uint64_t tot = 0;
+		for (int q = 0; q < 16; q++)
+			tot += s_wave[q];
+		meta[0] = tot;
+		meta[1] = 0;   // no look-back errors on this path
+	}
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void
+k_sel_write(SelArgs<T> a, const uint32_t *bits, const uint64_t *pre)
+{
+	constexpr int WPT = sel_wpt<T>(), WPL = sel_wpl<T>();
+	constexpr int SCH = 4096;   // slots per dense round (>= one tile of hge)
+	__shared__ oid s_stage[SCH];
+	__shared__ uint32_t s_words[WPT];
+	__shared__ uint32_t s_wave[4];
+	const unsigned tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+	const uint32_t t = blockIdx.x;
+	const uint64_t slot0 = (uint64_t) t * WPT * 32;
+	const bool active = tid * WPL < WPT;
+	uint32_t w[WPL], cnt = 0;
+#pragma unroll
+	for (int q = 0; q < WPL; q++) {
+		w[q] = active ? bits[(uint64_t) t * WPT + tid * WPL + q] : 0u;
+		cnt += __popc(w[q]);
+	}
+	// workgroup exclusive scan of the per-lane counts
+	uint32_t x = cnt;
+#pragma unroll
+	for (int o = 1; o < 64; o <<= 1) {
+		const uint32_t y = __shfl_up(x, o);
+		if ((int) lane >= o)
+			x += y;
+	}
+	if (lane == 63)
+		s_wave[wave] = x;
+	__syncthreads();
+	uint32_t ex = x - cnt;
+	for (unsigned q = 0; q < wave; q++)
+		ex += s_wave[q];
+	const uint32_t hits = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+	if (hits == 0)
+		return;
+	const uint64_t prefix = pre[t];
+	const oid base = a.cseq + slot0 - a.shift;
+	// first / last oid of the whole result (virtualisation test on the host)
+	if (cnt > 0 && (ex == 0 ? prefix == 0 : false)) {
+		int q = 0;
+		while (w[q] == 0)
+			q++;
+		a.meta[2] = base + ((uint64_t) (tid * WPL + q) * 32 + __ffs(w[q]) - 1);
+	}
+	if (cnt > 0 && ex + cnt == hits && prefix + hits == a.meta[0]) {
+		int q = WPL - 1;
+		while (w[q] == 0)
+			q--;
+		a.meta[3] = base + ((uint64_t) (tid * WPL + q) * 32 + 31 - __clz(w[q]));
+	}
+	if (hits < 1024) {
+		// sparse: the owning lane stores its hits
+		uint64_t pos = prefix + ex;
+#pragma unroll
+		for (int q = 0; q < WPL; q++) {
+			uint32_t m = w[q];
+			while (m) {
+				const int b = __ffs(m) - 1;
+				m &= m - 1;
+				a.out[pos++] = base + ((uint64_t) (tid * WPL + q) * 32 + b);
+			}
+		}
+		return;
+	}
+	if (hits <= (uint32_t) SCH) {
+		// all of the tile's hits fit the LDS stage: each lane places its
+		// own, then one contiguous store
+		uint32_t pos = ex;
+#pragma unroll
+		for (int q = 0; q < WPL; q++) {
+			uint32_t m = w[q];
+			while (m) {
+				const int b = __ffs(m) - 1;
+				m &= m - 1;
+				s_stage[pos++] = base + ((uint64_t) (tid * WPL + q) * 32 + b);
+			}
+		}
+		__syncthreads();
+		for (uint32_t i = tid; i < hits; i += 256)
+			a.out[prefix + i] = s_stage[i];
+		return;
+	}
+	// very dense: rounds of 4096 slots, lane i taking the 16 slots
+	// [16i, 16i+16) of the round; the round's hits are ranked by a workgroup
+	// scan, placed in LDS in order and stored as one run
+#pragma unroll
+	for (int q = 0; q < WPL; q++)
+		if (active)
+			s_words[tid * WPL + q] = w[q];
+	uint64_t obase = prefix;
+	for (int rd = 0; rd < WPT * 32 / SCH; rd++) {
+		__syncthreads();   // s_words written / previous round's s_wave, s_stage consumed
+		const uint32_t piece = (s_words[rd * (SCH / 32) + tid / 2] >> (16 * (tid & 1))) & 0xffffu;
+		const uint32_t pc = __popc(piece);
+		uint32_t y = pc;
+#pragma unroll
+		for (int o = 1; o < 64; o <<= 1) {
+			const uint32_t z = __shfl_up(y, o);
+			if ((int) lane >= o)
+				y += z;
+		}
+		if (lane == 63)
+			s_wave[wave] = y;
+		__syncthreads();
+		uint32_t pos = y - pc;
+		for (unsigned q = 0; q < wave; q++)
+			pos += s_wave[q];
+		const uint32_t rhits = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+		uint32_t mm = piece;
+		const oid rb = base + (uint64_t) rd * SCH + tid * 16;
+		while (mm) {
+			const int bb = __ffs(mm) - 1;
+			mm &= mm - 1;
+			s_stage[pos++] = rb + bb;
+		}
+		__syncthreads();
+		for (uint32_t i = tid; i < rhits; i += 256)
+			a.out[obase + i] = s_stage[i];
+		obase += rhits;
 	}
 }
 
@@ -373,7 +636,7 @@ run_scan(const mgdk_bat *b, const Cand &ci, const SelPred<T> &pred)
 		a.col_al = start - mis;
 		a.shift = (uint32_t) mis;
 		a.cseq = ci.seq;
-		items_per_tile = (uint64_t) sel_rows<false>() * 256 * (16 / sizeof(T));
+		items_per_tile = (uint64_t) (MGDK_SEL_STREAM ? SROWS : sel_rows<false>()) * 256 * (16 / sizeof(T));
 	} else {
 		uintptr_t mis = ((uintptr_t) ci.oids % 16) / sizeof(oid);
 		a.cand_al = ci.oids - mis;
@@ -398,14 +661,32 @@ run_scan(const mgdk_bat *b, const Cand &ci, const SelPred<T> &pred)
 	a.status = (uint64_t *) sc + 8;
 	a.meta = meta;
 	hipStream_t st = stream();
-	if (!hip_ok(hipMemsetAsync(sc, 0, sbytes, st), "hipMemsetAsync") ||
-	    !hip_ok(hipMemsetAsync(meta, 0, 64, st), "hipMemsetAsync")) {
+	const bool streamed = ci.dense && MGDK_SEL_STREAM;   // count / scan / write, no look-back
+	if (!streamed && (!hip_ok(hipMemsetAsync(sc, 0, sbytes, st), "hipMemsetAsync") ||
+			  !hip_ok(hipMemsetAsync(meta, 0, 64, st), "hipMemsetAsync"))) {
 		mgdk_BBPunfix(bn);
 		return nullptr;
 	}
+	// bitmap + counts + prefixes of the streamed scan; freed after the sync below
+	DevBuf sb(streamed ? ntiles * (4 * (size_t) sel_wpt<T>() + 4 + 8) + 64 : 8);
 	{
 		const dim3 g((unsigned) ntiles), blk(256);
-#define SELL(MAT, MODE) hipLaunchKernelGGL((k_select<T, MAT, MODE>), g, blk, 0, st, a)
+		uint32_t *bits = nullptr, *counts = nullptr;
+		uint64_t *pre = nullptr;
+		if (streamed) {
+			if (sb.p == nullptr) {
+				mgdk_BBPunfix(bn);
+				return nullptr;
+			}
+			pre = (uint64_t *) sb.p;
+			counts = (uint32_t *) (pre + ntiles);
+			bits = counts + ntiles + (ntiles & 1);
+		}
+#define SELS(MODE) do { hipLaunchKernelGGL((k_sel_count<T, MODE>), g, blk, 0, st, a, bits, counts); \
+			hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(1024), 0, st, counts, pre, (uint32_t) ntiles, a.meta); \
+			hipLaunchKernelGGL(k_sel_write<T>, g, blk, 0, st, a, bits, pre); } while (0)
+#define SELL(MAT, MODE) do { if (!(MAT) && MGDK_SEL_STREAM) SELS(MODE); \
+			     else hipLaunchKernelGGL((k_select<T, MAT, MODE>), g, blk, 0, st, a); } while (0)
 #define SELM(MAT) switch (pred.mode) { \
 		case SEL_RANGE: SELL(MAT, SEL_RANGE); break; \
 		case SEL_ANTI: SELL(MAT, SEL_ANTI); break; \
@@ -419,8 +700,10 @@ run_scan(const mgdk_bat *b, const Cand &ci, const SelPred<T> &pred)
 		}
 #undef SELM
 #undef SELL
+#undef SELS
 	}
-	hipLaunchKernelGGL(k_select_fin, dim3(1), dim3(1), 0, st, (const oid *) bn->theap, meta);
+	if (!streamed)
+		hipLaunchKernelGGL(k_select_fin, dim3(1), dim3(1), 0, st, (const oid *) bn->theap, meta);
 	uint64_t *h = (uint64_t *) pinned(64);
 	if (h == nullptr || !hip_ok(hipMemcpyAsync(h, meta, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, st), "memcpy") ||
 	    !sync()) {

@@ -88,9 +88,9 @@ static float timeit(void (*launch)(const u4 *, size_t, unsigned *), const u4 *p,
 #define REG(U, NT, BPC) [](const u4 *p, size_t n, unsigned *o) { hipLaunchKernelGGL((k_reg<U, NT>), dim3(256 * BPC), dim3(256), 0, 0, p, n / 16, o); }
 #define GLDS(S, AUX, WPB, BPC) [](const u4 *p, size_t n, unsigned *o) { hipLaunchKernelGGL((k_glds<S, AUX, WPB>), dim3(256 * BPC), dim3(64 * WPB), 0, 0, p, n / 1024, o); }
 
-int main()
+int main(int argc, char **argv)
 {
-	const size_t bytes = (size_t) 16 << 30;
+	const size_t bytes = argc > 1 ? (size_t) atoll(argv[1]) : (size_t) 16 << 30;
 	u4 *p;
 	unsigned *o;
 	if (hipMalloc(&p, bytes) != hipSuccess || hipMalloc(&o, 64) != hipSuccess) {
