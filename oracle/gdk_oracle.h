@@ -23,6 +23,7 @@
  *   window      gdk/gdk_analytic_bounds.c:273-387, :994, :1440
  *   frames      gdk/gdk_analytic_func.c:1626 (count), :1959 (sum), segment
  *               tree gdk/gdk_analytic.h:52-130
+ *   firstn      gdk/gdk_firstn.c:71-97 (heap), :211-1020, :1280
  *
  * Parity pinning: see tests/golden/ (fixtures extracted from the reference's
  * own MAL known-answer tests) and DESIGN.md §Oracle.
@@ -97,6 +98,10 @@ int ora_sort(ora_bat **sorted, ora_bat **order, const ora_bat *b,
 	     bool reverse, bool nilslast);
 int ora_rangebounds(ora_bat *r, const ora_bat *b, const ora_bat *p,
 		    const void *bound, int tp2, bool preceding, ora_oid first_half);
+/* plain first-N (no group ids, not distinct), heap semantics of
+ * gdk/gdk_firstn.c:211-1020 (gdk_oracle_firstn.c) */
+ora_bat *ora_firstn(const ora_bat *b, const ora_bat *s, const ora_bat *g, uint64_t n,
+		    bool asc, bool nilslast);
 
 /* synthetic TPC-H lineitem (tpch_gen.c) */
 typedef struct ora_lineitem {

@@ -84,6 +84,8 @@ def lib():
         L.ora_groupavg3.argtypes = [C.POINTER(P), C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool]
         L.ora_join.argtypes = [C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool]
         L.ora_sort.argtypes = [C.POINTER(P), C.POINTER(P), P, C.c_bool, C.c_bool]
+        L.ora_firstn.restype = P
+        L.ora_firstn.argtypes = [P, P, P, C.c_uint64, C.c_bool, C.c_bool]
         L.ora_rangebounds.argtypes = [P, P, P, C.c_void_p, C.c_int, C.c_bool, C.c_uint64]
         L.ora_analyticalsum.argtypes = [P, P, P, P, P, P, C.c_int, C.c_int, C.c_int]
         L.ora_analyticalcount.argtypes = [P, P, P, P, P, P, C.c_bool, C.c_int]
@@ -282,6 +284,11 @@ def BATsort(b, reverse=False, nilslast=False):
     if lib().ora_sort(C.byref(a), C.byref(o), b.ptr, reverse, nilslast) < 0:
         raise _err()
     return Bat(a), Bat(o)
+
+
+def BATfirstn(b, n, s=None, g=None, asc=True, nilslast=False):
+    """BATfirstn(&topn, NULL, b, s, g, n, asc, nilslast, false)"""
+    return _ret(lib().ora_firstn(b.ptr, s.ptr if s else None, g.ptr if g else None, n, asc, nilslast))
 
 
 def rangebounds(b, p, limit, preceding):

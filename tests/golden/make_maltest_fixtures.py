@@ -15,6 +15,11 @@ Sources (reference paths, relative to /root/reference):
       BAT: groups / extents / histo (GRPsubgroup5 -> BATgroup)
   monetdb5/modules/mal/Tests/bigsum.maltest -- aggr.sum of 10^16 followed by
       10^7 ones into dbl (BATsum exactness)
+  monetdb5/modules/mal/Tests/pqueue.maltest, pqueue2.maltest, pqueue3.maltest
+      -- algebra.firstn (ALGfirstn -> BATfirstn, algebra.c:937-990) on int
+      BATs: plain top-n (which of the tied rows the heap keeps), top-n with
+      group ids, and the two-column cascade (s, g from the previous step);
+      str columns are skipped (not on the device path)
 """
 import json
 import os
@@ -119,16 +124,66 @@ def bigsum_fixture():
             "repeat_count": upto // step, "result_type": "dbl", "expected": expected}
 
 
+def firstn_fixture(rel):
+    """Replay the bat.new / bat.append / algebra.firstn statements; every
+    io.print of a result gives the expected (head, tail) rows."""
+    text = open(os.path.join(REF, rel)).read()
+    bats, types = {}, {}
+    results = {}          # name -> expected tail values (from io.print)
+    cases = []
+    pending = []
+    for kind, body, exp in parse_blocks(text):
+        stmt = " ".join(body)
+        m = re.match(r"(\w+):= bat\.new\(:(\w+)\)$", stmt)
+        if m:
+            bats[m.group(1)] = []
+            types[m.group(1)] = m.group(2)
+            continue
+        m = re.match(r"bat\.append\((\w+),(.*)\)$", stmt)
+        if m:
+            bats[m.group(1)].append(m.group(2))
+            continue
+        m = re.match(r"(?:\((\w+),(\w+)\)|(\w+)):= algebra\.firstn\((\w+),(\w+(?::bat)?),(\w+(?::bat)?),"
+                     r"(\d+):lng,(true|false),(true|false),(true|false)\)$", stmt)
+        if m:
+            topn = m.group(1) or m.group(3)
+            gids = m.group(2)
+            b, sname, gname = m.group(4), m.group(5), m.group(6)
+            case = dict(b=b, type=types[b], values=None if types[b] != "int" else [int(v) for v in bats[b]],
+                        s=None if sname.startswith("nil") else sname,
+                        g=None if gname.startswith("nil") else gname,
+                        n=int(m.group(7)), asc=m.group(8) == "true", nilslast=m.group(9) == "true",
+                        distinct=m.group(10) == "true", topn=topn, gids=gids, expected={})
+            # s / g are the previous step's results, as the reference printed them
+            case["s_values"] = results.get(case["s"]) if case["s"] else None
+            case["g_values"] = results.get(case["g"]) if case["g"] else None
+            cases.append(case)
+            pending = [case]
+            continue
+        m = re.match(r"io\.print\((\w+)\)$", stmt)
+        if m and kind.startswith("query II"):
+            rows = sorted((int(exp[i]), int(exp[i + 1])) for i in range(0, len(exp), 2))
+            tail = [t for _, t in rows]
+            results[m.group(1)] = tail
+            for c in pending:
+                if m.group(1) in (c["topn"], c["gids"]):
+                    c["expected"]["gids" if m.group(1) == c["gids"] else "topn"] = tail
+    return {"source": rel, "cases": [c for c in cases if c["type"] == "int"]}
+
+
 def main():
     if not os.path.isdir(REF):
         sys.exit("reference not present; fixtures are already committed")
     fx = {"select": select_fixture(),
           "group_tst1500": group_fixture("monetdb5/mal/Tests/tst1500.maltest"),
           "group_tst1503": group_fixture("monetdb5/mal/Tests/tst1503.maltest"),
-          "bigsum": bigsum_fixture()}
+          "bigsum": bigsum_fixture(),
+          "firstn": [firstn_fixture("monetdb5/modules/mal/Tests/%s.maltest" % f)
+                     for f in ("pqueue", "pqueue2", "pqueue3")]}
     with open(os.path.join(OUT, "maltest_fixtures.json"), "w") as f:
         json.dump(fx, f, indent=1)
     print("select cases:", len(fx["select"]["cases"]))
+    print("firstn cases:", [len(f["cases"]) for f in fx["firstn"]])
 
 
 if __name__ == "__main__":

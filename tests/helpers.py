@@ -39,3 +39,12 @@ def with_nils(a, nil, frac, r):
         m = r.random(a.shape[0]) < frac
         a[m] = nil
     return a
+
+
+def firstn_cases(plain_only=False):
+    """algebra.firstn cases of pqueue*.maltest as (case, b values, s, g)."""
+    for fx in FIX["firstn"]:
+        for c in fx["cases"]:
+            if plain_only and (c["gids"] or c["distinct"]):
+                continue
+            yield fx["source"], c

@@ -120,3 +120,51 @@ def test_analytical_sum_oracle_small(ora):
     s = ora.Bat.from_array(ora.TYPE_oid, np.array([0, 0, 1, 3, 3, 4, 5], np.uint64))
     e = ora.Bat.from_array(ora.TYPE_oid, np.array([2, 3, 3, 4, 6, 7, 7], np.uint64))
     assert list(ora.analyticalsum(B, P, O, s, e, ora.TYPE_lng, 1).values()) == [3, 6, 5, -(2**63), 11, 18, 13]
+
+
+def test_firstn_maltest(ora):
+    """Plain top-n (no group ids): the rows the reference's heap keeps,
+    including its choice among tied rows (pqueue*.maltest)."""
+    from helpers import firstn_cases
+    n_checked = 0
+    for src, c in firstn_cases(plain_only=True):
+        b = ora.Bat.from_array(ora.TYPE_int, np.array(c["values"], np.int32))
+        s = g = None
+        if c["s"]:
+            s = ora.Bat.from_array(ora.TYPE_oid, np.array(c["s_values"], np.uint64))
+            g = ora.Bat.from_array(ora.TYPE_oid, np.array(c["g_values"], np.uint64))
+        t = ora.BATfirstn(b, c["n"], s=s, g=g, asc=c["asc"], nilslast=c["nilslast"])
+        assert [int(v) for v in t.values()] == c["expected"]["topn"], (src, c)
+        n_checked += 1
+    assert n_checked >= 27
+
+
+def test_firstn_oracle_sets(ora):
+    """Heap restatement: strictly-better rows always in, right count, the
+    rest tied with the n-th value; sorted inputs take the reference's slices."""
+    r = np.random.default_rng(11)
+    for trial in range(40):
+        N = int(r.integers(2, 400))
+        v = r.integers(-5, 5, N).astype(np.int32)
+        v[r.random(N) < 0.1] = -(1 << 31)
+        if trial % 5 == 0:
+            v = np.sort(v)
+        elif trial % 5 == 1:
+            v = np.sort(v)[::-1].copy()
+        for asc in (True, False):
+            for nilslast in (True, False):
+                n = int(r.integers(1, N + 1))
+                t = np.array(ora.BATfirstn(ora.Bat.from_array(ora.TYPE_int, v), n, asc=asc,
+                                           nilslast=nilslast).values(), np.int64)
+                assert len(t) == min(n, N)
+                assert np.all(np.diff(t) > 0)
+                if trial % 5 == 1 and nilslast == asc and (v == -(1 << 31)).any():
+                    continue        # reverse-sorted with nils: the reference's slice (see oracle)
+                x = v.astype(np.float64)
+                x[v == -(1 << 31)] = np.inf if nilslast else -np.inf
+                key = x if asc else -x
+                if not asc:
+                    key[v == -(1 << 31)] = np.inf if nilslast else -np.inf
+                kth = np.sort(key)[min(n, N) - 1]
+                assert np.all(np.isin(np.flatnonzero(key < kth), t))
+                assert np.all(key[t] <= kth)
