@@ -20,6 +20,15 @@ Sources (reference paths, relative to /root/reference):
       BATs: plain top-n (which of the tied rows the heap keeps), top-n with
       group ids, and the two-column cascade (s, g from the previous step);
       str columns are skipped (not on the device path)
+  sql/test/analytics/Tests/analytics03.test -- windowed SUM / COUNT over
+      RANGE / GROUPS frames that end at the current row's peers (frame
+      "unbounded preceding .. current row" and whole-partition frames); only
+      columns whose values are the same for every order among peers are
+      kept, so they pin GDKanalyticalsum / GDKanalyticalcount
+      (gdk_analytic_func.c:1626, :1959) independently of sort stability
+  monetdb5/modules/mal/Tests/orderidx00.maltest, orderidx04.maltest --
+      algebra.sort (ALGsort -> BATsort, algebra.c:1754-1831) of an int BAT:
+      sorted values, and the order oids of the stable variant
 """
 import json
 import os
@@ -171,6 +180,69 @@ def firstn_fixture(rel):
     return {"source": rel, "cases": [c for c in cases if c["type"] == "int"]}
 
 
+def sort_fixture(rel):
+    text = open(os.path.join(REF, rel)).read()
+    vals = []
+    cases = []
+    pending = None
+    for kind, body, exp in parse_blocks(text):
+        stmt = " ".join(body)
+        m = re.match(r"bat\.append\(bv,\s*(-?\d+)\s*\)$", stmt)
+        if m:
+            vals.append(int(m.group(1)))
+            continue
+        m = re.match(r"(?:\((\w+),(\w+)\)|(\w+)):= algebra\.sort\(bv,(\S+?),(\S+?),(\S+?)\)$", stmt)
+        if m:
+            flag = lambda t: t.startswith("1") or t == "true"
+            pending = dict(reverse=flag(m.group(4)), nilslast=flag(m.group(5)), stable=flag(m.group(6)),
+                           order=m.group(2) is not None, values=list(vals))
+            continue
+        if pending and kind.startswith("query I") and stmt.startswith("io.print("):
+            width = len(kind.split()[1])
+            rows = sorted(tuple(int(exp[i + k]) for k in range(width)) for i in range(0, len(exp), width))
+            pending["sorted"] = [r[1] for r in rows]
+            if width == 3:
+                pending["order_oids"] = [r[2] for r in rows]
+            cases.append(pending)
+            pending = None
+    return {"source": rel, "cases": cases}
+
+
+def analytics03_fixture():
+    rel = "sql/test/analytics/Tests/analytics03.test"
+    text = open(os.path.join(REF, rel)).read()
+    m = re.search(r"insert into rowsvsrangevsgroups values (.*)\n", text)
+    rows = [tuple(int(float(x)) for x in t.split(",")) for t in re.findall(r"\(([^)]*)\)", m.group(1))]
+    blocks = list(parse_blocks(text))
+    out = []
+    # (query prefix, columns kept: index -> (aggregate, partition col, order col, frame))
+    specs = [
+        ("select cast(sum(aa) over (rows unbounded preceding)",
+         {1: ("sum", None, None, "all"), 3: ("sum", None, "aa", "upto"), 4: ("sum", None, "aa", "upto"),
+          6: ("sum", "bb", "bb", "upto"), 7: ("sum", "bb", "bb", "upto")}, 8),
+        ("select cast(sum(aa) over (order by aa range between unbounded preceding and current row)",
+         {0: ("sum", None, "aa", "upto"), 2: ("count*", None, "aa", "upto"), 3: ("count", None, "aa", "upto")}, 8),
+    ]
+    deleted = False
+    for kind, body, exp in blocks:
+        stmt = " ".join(body)
+        if stmt.startswith("delete from rowsvsrangevsgroups where aa = 2"):
+            deleted = True
+            continue
+        for prefix, cols, width in specs:
+            if stmt.startswith(prefix) and kind.startswith("query"):
+                data = [r for r in rows if not (deleted and r[0] == 2)]
+                nrow = len(exp) // width
+                for ci, (agg, part, order, frame) in cols.items():
+                    out.append(dict(aa=[r[0] for r in data], bb=[r[1] for r in data], agg=agg, part=part,
+                                    order=order, frame=frame,
+                                    # query 1 prints its rows ordered by (bb, aa) -- the
+                                    # running sum of its first column is aa in that order
+                                    output_order="bb,aa" if "rows unbounded preceding)" in prefix else "sorted",
+                                    expected=[int(exp[i * width + ci]) for i in range(nrow)]))
+    return {"source": rel, "cases": out}
+
+
 def main():
     if not os.path.isdir(REF):
         sys.exit("reference not present; fixtures are already committed")
@@ -179,7 +251,10 @@ def main():
           "group_tst1503": group_fixture("monetdb5/mal/Tests/tst1503.maltest"),
           "bigsum": bigsum_fixture(),
           "firstn": [firstn_fixture("monetdb5/modules/mal/Tests/%s.maltest" % f)
-                     for f in ("pqueue", "pqueue2", "pqueue3")]}
+                     for f in ("pqueue", "pqueue2", "pqueue3")],
+          "window_frames": analytics03_fixture(),
+          "sort": [sort_fixture("monetdb5/modules/mal/Tests/%s.maltest" % f)
+                   for f in ("orderidx00", "orderidx04")]}
     with open(os.path.join(OUT, "maltest_fixtures.json"), "w") as f:
         json.dump(fx, f, indent=1)
     print("select cases:", len(fx["select"]["cases"]))

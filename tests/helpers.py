@@ -48,3 +48,38 @@ def firstn_cases(plain_only=False):
             if plain_only and (c["gids"] or c["distinct"]):
                 continue
             yield fx["source"], c
+
+
+def replay_window_frames(sumf, countf, make_bat, TYPE_int, TYPE_bit, TYPE_lng):
+    """Windowed SUM / COUNT cases of analytics03.test.  Rows are ordered by
+    (partition, order) keys; p / o mark partition and peer-group starts;
+    frame 3 = unbounded preceding .. current row's peers, 5 = partition.
+    sumf(b, p, o, tp2, frame) / countf(b, p, o, ignore_nils, frame) return
+    per-row values in sorted order.  Returns mismatches."""
+    bad = []
+    for c in FIX["window_frames"]["cases"]:
+        aa, bb = np.array(c["aa"], np.int32), np.array(c["bb"], np.int32)
+        cols = {"aa": aa, "bb": bb}
+        keys = [cols[k] for k in (c["order"], c["part"]) if k is not None]
+        perm = np.lexsort(keys) if keys else np.arange(len(aa))
+        part = cols[c["part"]][perm] if c["part"] else np.zeros(len(aa), np.int32)
+        order = cols[c["order"]][perm] if c["order"] else np.zeros(len(aa), np.int32)
+        p = np.zeros(len(aa), np.int8)
+        p[0] = 1
+        p[1:] = part[1:] != part[:-1]
+        o = p.copy()
+        o[1:] |= order[1:] != order[:-1]
+        frame = 5 if c["frame"] == "all" else 3
+        B, P, O = make_bat(TYPE_int, aa[perm]), make_bat(TYPE_bit, p), make_bat(TYPE_bit, o)
+        if c["agg"] == "sum":
+            got = sumf(B, P, O, TYPE_lng, frame)
+        else:
+            got = countf(B, P, O, c["agg"] == "count", frame)
+        got = np.asarray(got, np.int64)
+        if c["output_order"] == "bb,aa":
+            back = np.empty_like(got)
+            back[perm] = got
+            got = back[np.lexsort((aa, bb))]
+        if [int(x) for x in got] != c["expected"]:
+            bad.append((c, list(got)))
+    return bad

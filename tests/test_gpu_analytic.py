@@ -121,3 +121,14 @@ def test_analytical_sum_large(gdk, ora):
     want = ora.analyticalsum(ora.Bat.from_array(ora.TYPE_lng, v), ora.Bat.from_array(ora.TYPE_bit, p),
                              ora.Bat.from_array(ora.TYPE_bit, o), None, None, ora.TYPE_hge, 3).values()
     assert list(got) == list(want)
+
+
+def test_window_frames_sqltest(gdk):
+    """analytics03.test (the reference's own answers): windowed SUM / COUNT
+    over RANGE frames closed at the current row's peers, and whole partitions."""
+    from helpers import replay_window_frames
+    bad = replay_window_frames(
+        lambda b, p, o, tp2, f: gdk.GDKanalyticalsum(b, p, o, None, None, tp2, f).to_numpy(),
+        lambda b, p, o, ign, f: gdk.GDKanalyticalcount(b, p, o, None, None, ign, f).to_numpy(),
+        lambda tp, a: gdk.BAT.from_numpy(tp, a), gdk.TYPE_int, gdk.TYPE_bit, gdk.TYPE_lng)
+    assert not bad, bad

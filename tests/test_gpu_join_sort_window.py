@@ -335,3 +335,15 @@ def test_unique(gdk, tname, dt):
     sv = v[(s - 7).astype(np.int64)]
     _, f2 = np.unique(sv, return_index=True)
     assert np.array_equal(u2.to_numpy(), s[np.sort(f2)])
+
+
+def test_sort_maltest_fixture(gdk):
+    """algebra.sort of orderidx00 / orderidx04.maltest (the reference's answers)."""
+    from helpers import FIX
+    for fx in FIX["sort"]:
+        for c in fx["cases"]:
+            b = gdk.BAT.from_numpy(gdk.TYPE_int, np.array(c["values"], np.int32))
+            srt, order, _ = gdk.BATsort(b, reverse=c["reverse"], nilslast=c["nilslast"], stable=c["stable"])
+            assert [int(v) for v in srt.to_numpy()] == c["sorted"]
+            if c["order"]:
+                assert [int(v) for v in order.to_numpy()] == c["order_oids"]

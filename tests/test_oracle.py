@@ -168,3 +168,26 @@ def test_firstn_oracle_sets(ora):
                 kth = np.sort(key)[min(n, N) - 1]
                 assert np.all(np.isin(np.flatnonzero(key < kth), t))
                 assert np.all(key[t] <= kth)
+
+
+def test_sort_maltest(ora):
+    """algebra.sort of orderidx00 / orderidx04.maltest: sorted values and
+    (stable) order oids."""
+    from helpers import FIX
+    for fx in FIX["sort"]:
+        for c in fx["cases"]:
+            b = ora.Bat.from_array(ora.TYPE_int, np.array(c["values"], np.int32))
+            srt, order = ora.BATsort(b, reverse=c["reverse"], nilslast=c["nilslast"])
+            assert [int(v) for v in srt.values()] == c["sorted"]
+            if c["order"]:
+                assert [int(v) for v in order.values()] == c["order_oids"]
+
+
+def test_window_frames_sqltest(ora):
+    """analytics03.test windowed SUM / COUNT with peer-closed frames."""
+    from helpers import replay_window_frames
+    bad = replay_window_frames(
+        lambda b, p, o, tp2, f: ora.analyticalsum(b, p, o, None, None, tp2, f).values(),
+        lambda b, p, o, ign, f: ora.analyticalcount(b, p, o, None, None, ign, f).values(),
+        lambda tp, a: ora.Bat.from_array(tp, a), ora.TYPE_int, ora.TYPE_bit, ora.TYPE_lng)
+    assert not bad, bad
