@@ -636,6 +636,558 @@ join_csr(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_ba
 	return 0;
 }
 
+
+// ---------------------------------------------------------------------------
+// Radix-partitioned path (4-byte keys, unique build keys): the build side is
+// cut into P = 2^pbits hash partitions of <= ~8 Ki keys, each of which
+// becomes an LDS-resident open-addressing table (16 Ki slots, 128 KiB) in the
+// workgroup that probes it; the probe side is cut into the same partitions.
+// Both cuts are three passes over the side in 32 Ki-row subtiles: a
+// histogram per (subtile, partition), a column scan, and a scatter of
+// (key, row) entries whose slot comes from an LDS counter (no global
+// atomics; a subtile's entries of one partition form one contiguous run).
+// The probe workgroup rewrites each of its entries in place as
+// (match + 1, row).  The left order is restored per subtile: the restore
+// workgroup reads its subtile's run in every partition, drops each match
+// into an LDS array indexed by row, and compacts the matched rows in order
+// (output offset by decoupled look-back over the subtiles).  Every global
+// access is a stream or a short contiguous run; the only random accesses are
+// LDS ones.  Duplicate build keys (detected during the LDS build) or an
+// oversized partition send the join to the open-addressing path.
+// ---------------------------------------------------------------------------
+
+constexpr uint32_t PJ_SUBROWS = 32768;     // rows per subtile (the restore's LDS array)
+constexpr int PJ_SUBS = 1;                 // subtiles per histogram workgroup
+constexpr uint32_t PJ_SLOTS = 16384;       // LDS hash slots per build partition (128 KiB)
+constexpr uint32_t PJ_MAXFILL = 12288;     // largest build partition accepted
+constexpr int PJ_MAXPBITS = 11;            // <= 2048 partitions (LDS counters)
+
+// one 32-bit multiplicative (Fibonacci) hash per key: the partition is its
+// top pbits, the LDS home the next 14 bits.  A 64-bit mixer costs two
+// quarter-rate 64-bit multiplies per key, which bounded these passes;
+// skewed inputs are caught by the partition-size check (PJ_MAXFILL).
+__device__ __forceinline__ uint32_t
+pj_hash(uint32_t key)
+{
+	return key * 0x9E3779B1u;
+}
+
+__device__ __forceinline__ uint32_t
+pj_part32(uint32_t key, int pbits)
+{
+	return pj_hash(key) >> (32 - pbits);
+}
+
+__device__ __forceinline__ uint32_t
+pj_home(uint32_t key, int pbits)
+{
+	return (pj_hash(key) >> (32 - pbits - 14)) & (PJ_SLOTS - 1);
+}
+
+// 1024-thread workgroup reduction (16 waves); result valid in thread 0
+template <typename T, typename F>
+__device__ __forceinline__ T
+block_reduce16(T v, F op)
+{
+	__shared__ T s_r16[16];
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1)
+		v = op(v, __shfl_xor(v, o));
+	__syncthreads();
+	if (__lane_id() == 0)
+		s_r16[threadIdx.x >> 6] = v;
+	__syncthreads();
+	if (threadIdx.x == 0)
+		for (int q = 1; q < 16; q++)
+			v = op(v, s_r16[q]);
+	return v;
+}
+
+// 16 consecutive 4-byte keys of side s from candidate index i0 (vector loads
+// for a dense side with 16-byte aligned rows); ok[q] = exists and counts
+__device__ __forceinline__ void
+pj_keys16(const Side &s, BUN i0, BUN n, bool skipnil, uint32_t k[16], bool ok[16])
+{
+	if (s.dense && i0 + 16 <= n && ((s.off + i0) & 3) == 0) {
+		typedef int32_t i4 __attribute__((ext_vector_type(4)));
+		const i4 *src = (const i4 *) ((const int32_t *) s.base + s.off + i0);
+#pragma unroll
+		for (int q = 0; q < 4; q++) {
+			const i4 v = __builtin_nontemporal_load(src + q);
+			k[4 * q] = (uint32_t) v.x;
+			k[4 * q + 1] = (uint32_t) v.y;
+			k[4 * q + 2] = (uint32_t) v.z;
+			k[4 * q + 3] = (uint32_t) v.w;
+		}
+#pragma unroll
+		for (int q = 0; q < 16; q++)
+			ok[q] = !(skipnil && k[q] == 0x80000000u);
+		return;
+	}
+#pragma unroll
+	for (int q = 0; q < 16; q++) {
+		ok[q] = false;
+		k[q] = 0;
+		if (i0 + q < n) {
+			bool isnil;
+			k[q] = (uint32_t) key_of(s, i0 + q, isnil);
+			ok[q] = !(isnil && skipnil);
+		}
+	}
+}
+
+// histogram: cnt[sub][p] = rows of subtile sub in partition p
+__global__ __launch_bounds__(1024) void
+k_pj_hist(Side s, BUN n, int pbits, bool skipnil, uint32_t *cnt)
+{
+	__shared__ uint32_t c[1u << PJ_MAXPBITS];
+	const uint32_t P = 1u << pbits;
+	for (int k = 0; k < PJ_SUBS; k++) {
+		const BUN sub = (BUN) blockIdx.x * PJ_SUBS + k;
+		const BUN a = sub * PJ_SUBROWS;
+		if (a >= n)
+			break;
+		const BUN e = min(n, a + PJ_SUBROWS);
+		for (uint32_t p = threadIdx.x; p < P; p += blockDim.x)
+			c[p] = 0;
+		__syncthreads();
+		for (BUN i0 = a + (BUN) threadIdx.x * 16; i0 < e; i0 += (BUN) blockDim.x * 16) {
+			uint32_t k[16];
+			bool ok[16];
+			pj_keys16(s, i0, e, skipnil, k, ok);
+#pragma unroll
+			for (int q = 0; q < 16; q++)
+				if (ok[q])
+					atomicAdd(&c[pj_part32(k[q], pbits)], 1u);
+		}
+		__syncthreads();
+		for (uint32_t p = threadIdx.x; p < P; p += blockDim.x)
+			cnt[sub * P + p] = c[p];
+		__syncthreads();
+	}
+}
+
+// scatter of (key, row) entries: one workgroup per subtile, in halves of
+// 16 Ki rows that are counting-sorted by partition in LDS first, so each
+// partition's piece of the run is stored by consecutive lanes
+constexpr uint32_t PJ_HALF = PJ_SUBROWS / 2;
+constexpr int PJ_RPT = PJ_HALF / 1024;         // rows per thread per half
+
+__global__ __launch_bounds__(1024) void
+k_pj_scatter(Side s, BUN n, int pbits, bool skipnil, const uint32_t *off, const uint32_t *base, uint2 *ent)
+{
+	__shared__ uint2 stage[PJ_HALF];
+	__shared__ uint32_t hist[1u << PJ_MAXPBITS], start[1u << PJ_MAXPBITS], gcur[1u << PJ_MAXPBITS];
+	__shared__ uint32_t wsum[16];
+	const uint32_t P = 1u << pbits;
+	const unsigned tid = threadIdx.x;
+	const BUN sub = blockIdx.x;
+	const BUN a0 = sub * PJ_SUBROWS;
+	for (uint32_t p = tid; p < P; p += blockDim.x)
+		gcur[p] = base[p] + off[sub * P + p];
+	for (int half = 0; half < 2; half++) {
+		const BUN a = a0 + (BUN) half * PJ_HALF;
+		if (a >= n)
+			break;
+		for (uint32_t p = tid; p < P; p += blockDim.x)
+			hist[p] = 0;
+		__syncthreads();
+		static_assert(PJ_RPT == 16, "16 rows per thread");
+		uint32_t kk[PJ_RPT], pp[PJ_RPT], rk[PJ_RPT];
+		{
+			bool ok[16];
+			pj_keys16(s, a + (BUN) tid * 16, min(n, a + PJ_HALF), skipnil, kk, ok);
+#pragma unroll
+			for (int q = 0; q < PJ_RPT; q++)
+				pp[q] = ok[q] ? pj_part32(kk[q], pbits) : ~0u;
+		}
+#pragma unroll
+		for (int q = 0; q < PJ_RPT; q++)
+			if (pp[q] != ~0u)
+				rk[q] = atomicAdd(&hist[pp[q]], 1u);
+		__syncthreads();
+		// exclusive scan of hist[0..P) into start (P <= 4096: 4 per thread)
+		uint32_t loc[4], t = 0;
+		const uint32_t per = (P + 1023) / 1024;
+		for (uint32_t q = 0; q < per; q++) {
+			const uint32_t p = tid * per + q;
+			loc[q] = p < P ? hist[p] : 0;
+			t += loc[q];
+		}
+		uint32_t x = t;
+#pragma unroll
+		for (int o = 1; o < 64; o <<= 1) {
+			const uint32_t u = __shfl_up(x, o);
+			if (__lane_id() >= (unsigned) o)
+				x += u;
+		}
+		if (__lane_id() == 63)
+			wsum[tid >> 6] = x;
+		__syncthreads();
+		uint32_t pre = x - t, total = 0;
+		for (uint32_t w = 0; w < 16; w++) {
+			pre += w < (tid >> 6) ? wsum[w] : 0;
+			total += wsum[w];
+		}
+		for (uint32_t q = 0; q < per; q++) {
+			const uint32_t p = tid * per + q;
+			if (p < P)
+				start[p] = pre;
+			pre += loc[q];
+		}
+		__syncthreads();
+#pragma unroll
+		for (int q = 0; q < PJ_RPT; q++)
+			if (pp[q] != ~0u)
+				stage[start[pp[q]] + rk[q]] = make_uint2(kk[q], (uint32_t) (a + (BUN) tid * 16 + q));
+		__syncthreads();
+		for (uint32_t j = tid; j < total; j += blockDim.x) {
+			const uint2 en = stage[j];
+			const uint32_t p = pj_part32(en.x, pbits);
+			ent[gcur[p] + (j - start[p])] = en;
+		}
+		__syncthreads();
+		for (uint32_t p = tid; p < P; p += blockDim.x)
+			gcur[p] += hist[p];
+		__syncthreads();
+	}
+}
+
+// column-exclusive prefix of cnt[nsub][P] (64 columns x 16 row groups per
+// workgroup); tot[p] = column total
+__global__ __launch_bounds__(1024) void
+k_pj_colscan(const uint32_t *cnt, uint32_t nsub, uint32_t P, uint32_t *off, uint32_t *tot)
+{
+	__shared__ uint32_t part[16][64];
+	const uint32_t cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+	const uint32_t col = blockIdx.x * 64 + cl;
+	const uint32_t per = (nsub + 15) / 16;
+	const uint32_t r0 = min(nsub, grp * per), r1 = min(nsub, r0 + per);
+	uint32_t sum = 0;
+#pragma unroll 8
+	for (uint32_t r = r0; r < r1; r++)
+		sum += cnt[(size_t) r * P + col];
+	part[grp][cl] = sum;
+	__syncthreads();
+	uint32_t pre = 0;
+	for (uint32_t g = 0; g < grp; g++)
+		pre += part[g][cl];
+#pragma unroll 8
+	for (uint32_t r = r0; r < r1; r++) {
+		const uint32_t v = cnt[(size_t) r * P + col];
+		off[(size_t) r * P + col] = pre;
+		pre += v;
+	}
+	if (grp == 15)
+		tot[col] = pre;
+}
+
+// base[p] = exclusive prefix of tot (one workgroup; P <= 4096)
+__global__ __launch_bounds__(1024) void
+k_pj_base(const uint32_t *tot, uint32_t P, uint32_t *base, uint32_t *maxtot)
+{
+	__shared__ uint32_t wsum[16];
+	__shared__ uint32_t carry;
+	if (threadIdx.x == 0)
+		carry = 0;
+	uint32_t mx = 0;
+	for (uint32_t b = 0; b < P; b += 1024) {
+		__syncthreads();
+		const uint32_t p = b + threadIdx.x;
+		const uint32_t v = p < P ? tot[p] : 0;
+		mx = v > mx ? v : mx;
+		uint32_t x = v;
+#pragma unroll
+		for (int o = 1; o < 64; o <<= 1) {
+			const uint32_t u = __shfl_up(x, o);
+			if (__lane_id() >= (unsigned) o)
+				x += u;
+		}
+		if (__lane_id() == 63)
+			wsum[threadIdx.x >> 6] = x;
+		__syncthreads();
+		uint32_t wpre = 0;
+		for (uint32_t w = 0; w < (threadIdx.x >> 6); w++)
+			wpre += wsum[w];
+		if (p < P)
+			base[p] = carry + wpre + x - v;
+		__syncthreads();
+		if (threadIdx.x == 1023)
+			carry += wpre + x;
+	}
+	__syncthreads();
+	if (threadIdx.x == 0)
+		base[P] = carry;
+	mx = block_reduce16(mx, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
+	if (threadIdx.x == 0)
+		*maxtot = mx;
+}
+
+// one workgroup per partition: LDS table of the build entries, then each
+// probe entry of the partition rewritten in place as (match position + 1 or
+// 0, row)
+__global__ __launch_bounds__(1024) void
+k_pj_probe(const uint2 *bent, const uint32_t *bbase, uint2 *pent, const uint32_t *pbase, int pbits, uint32_t *dupflag)
+{
+	__shared__ unsigned long long tab[PJ_SLOTS];
+	const uint32_t p = blockIdx.x;
+	for (uint32_t i = threadIdx.x; i < PJ_SLOTS; i += blockDim.x)
+		tab[i] = 0ull;
+	__syncthreads();
+	const uint32_t b0 = bbase[p], b1 = bbase[p + 1];
+	bool dup = false;
+	for (uint32_t e = b0 + threadIdx.x; e < b1; e += blockDim.x) {
+		const uint2 en = bent[e];
+		const unsigned long long v = ((unsigned long long) (en.y + 1) << 32) | en.x;
+		uint32_t h = pj_home(en.x, pbits);
+		for (;;) {
+			const unsigned long long o = atomicCAS(&tab[h], 0ull, v);
+			if (o == 0ull)
+				break;
+			if ((uint32_t) o == en.x) {
+				dup = true;
+				break;
+			}
+			h = (h + 1) & (PJ_SLOTS - 1);
+		}
+	}
+	if (__any(dup) && __lane_id() == 0)
+		atomicOr(dupflag, 1u);
+	__syncthreads();
+	const uint32_t q0 = pbase[p], q1 = pbase[p + 1];
+	constexpr int U = 8;
+	for (uint32_t e0 = q0 + threadIdx.x; e0 < q1; e0 += U * blockDim.x) {
+		uint2 en[U];
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const uint32_t e = e0 + u * blockDim.x;
+			en[u] = e < q1 ? pent[e] : make_uint2(0, 0);
+		}
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			uint32_t h = pj_home(en[u].x, pbits), m = 0;
+			for (;;) {
+				const unsigned long long o = tab[h];
+				if (o == 0ull)
+					break;
+				if ((uint32_t) o == en[u].x) {
+					m = (uint32_t) (o >> 32);
+					break;
+				}
+				h = (h + 1) & (PJ_SLOTS - 1);
+			}
+			en[u].x = m;
+		}
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const uint32_t e = e0 + u * blockDim.x;
+			if (e < q1)
+				pent[e] = en[u];
+		}
+	}
+}
+
+// one workgroup per subtile (ticketed): matches back into row order
+__global__ __launch_bounds__(1024) void
+k_pj_restore(const uint2 *pent, const uint32_t *poff, const uint32_t *pbase, const uint32_t *offT, uint32_t P,
+	     uint64_t total, BUN n, uint32_t nsub, Side L, Side R, uint32_t *ticket, uint64_t *status, uint64_t *meta,
+	     oid *r1, oid *r2)
+{
+	// res[row + row / 32]: one pad word per 32 rows, so the 32-row runs of
+	// consecutive threads fall in different banks
+	__shared__ uint32_t res[PJ_SUBROWS + PJ_SUBROWS / 32];
+	__shared__ uint32_t fstart[(1u << PJ_MAXPBITS) + 1], src[1u << PJ_MAXPBITS];
+	__shared__ uint32_t wsum[16];
+	__shared__ uint32_t s_sub;
+	__shared__ uint64_t s_pre;
+	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+	if (tid == 0)
+		s_sub = atomicAdd(ticket, 1u);
+	for (uint32_t i = tid; i < PJ_SUBROWS + PJ_SUBROWS / 32; i += blockDim.x)
+		res[i] = 0;
+	__syncthreads();
+	const uint32_t sub = s_sub;
+	const BUN a = (BUN) sub * PJ_SUBROWS;
+	const uint32_t rows = (uint32_t) min((BUN) PJ_SUBROWS, n - a);
+	// the subtile's run of partition p starts at flat index fstart[p] (its
+	// subtile-major offset) and at pbase[p] + poff[sub][p] in the entries
+	const uint32_t f0 = offT[(size_t) sub * P];
+	const uint32_t f1 = sub + 1 < nsub ? offT[(size_t) (sub + 1) * P] : (uint32_t) total;
+	for (uint32_t q = tid; q < P; q += blockDim.x) {
+		fstart[q] = offT[(size_t) sub * P + q] - f0;
+		src[q] = pbase[q] + poff[(size_t) sub * P + q];
+	}
+	if (tid == 0)
+		fstart[P] = f1 - f0;
+	__syncthreads();
+	for (uint32_t j = tid; j < f1 - f0; j += blockDim.x) {
+		uint32_t lo = 0, hi = P;
+		while (hi - lo > 1) {
+			const uint32_t mid = (lo + hi) >> 1;
+			if (fstart[mid] <= j)
+				lo = mid;
+			else
+				hi = mid;
+		}
+		const uint2 en = pent[src[lo] + (j - fstart[lo])];
+		const uint32_t r = en.y - (uint32_t) a;
+		res[r + (r >> 5)] = en.x;
+	}
+	__syncthreads();
+	// thread tid counts the rows [32 tid, 32 tid + 32): a match mask and the
+	// run's exclusive offset, so the output pass below can walk the rows in
+	// order (consecutive lanes -> consecutive positions) without barriers
+	static_assert(PJ_SUBROWS == 32 * 1024, "32 rows per thread");
+	__shared__ uint32_t rmask[1024], rbase[1024];
+	const uint32_t r0 = tid * 32, rb = tid * 33;
+	uint32_t msk = 0;
+#pragma unroll
+	for (int k = 0; k < 32; k++)
+		msk |= (uint32_t) ((r0 + k < rows) && res[rb + k] != 0) << k;
+	const uint32_t c = __popc(msk);
+	uint32_t x = c;
+#pragma unroll
+	for (int o = 1; o < 64; o <<= 1) {
+		const uint32_t u = __shfl_up(x, o);
+		if (lane >= (unsigned) o)
+			x += u;
+	}
+	if (lane == 63)
+		wsum[w] = x;
+	__syncthreads();
+	uint32_t wpre = 0, tot = 0;
+	for (uint32_t q = 0; q < 16; q++) {
+		wpre += q < w ? wsum[q] : 0;
+		tot += wsum[q];
+	}
+	rmask[tid] = msk;
+	rbase[tid] = wpre + x - c;
+	if (w == 0) {
+		const uint64_t pre = lookback(status, sub, tot, (uint32_t *) &meta[1]);
+		if (lane == 0) {
+			s_pre = pre;
+			if (sub == nsub - 1)
+				meta[0] = pre + tot;
+		}
+	}
+	__syncthreads();
+	const uint64_t pre = s_pre;
+	for (uint32_t r = tid; r < rows; r += blockDim.x) {
+		const uint32_t run = r >> 5, bit = r & 31;
+		const uint32_t mk = rmask[run];
+		if ((mk >> bit) & 1) {
+			const uint64_t o = pre + rbase[run] + __popc(mk & ((1u << bit) - 1));
+			r1[o] = oid_of(L, a + r);
+			r2[o] = oid_of(R, res[r + run] - 1);
+		}
+	}
+}
+
+// one side cut into partitions: cnt/off matrices, partition bases, entries
+struct PjSide {
+	uint32_t nsub = 0;
+	DevBuf *cnt = nullptr, *off = nullptr, *tot = nullptr, *base = nullptr, *ent = nullptr;
+	~PjSide()
+	{
+		delete cnt;
+		delete off;
+		delete tot;
+		delete base;
+		delete ent;
+	}
+};
+
+int
+pj_cut(const Side &S, BUN n, int pbits, bool skipnil, PjSide &o, uint32_t *maxtot_dev)
+{
+	hipStream_t st = stream();
+	const uint32_t P = 1u << pbits;
+	o.nsub = (uint32_t) ((n + PJ_SUBROWS - 1) / PJ_SUBROWS);
+	const size_t m = (size_t) o.nsub * P * 4 + 64;
+	o.cnt = new DevBuf(m);
+	o.off = new DevBuf(m);
+	o.tot = new DevBuf(P * 4 + 64);
+	o.base = new DevBuf(P * 4 + 64);
+	o.ent = new DevBuf(n * 8 + 64);
+	if (!o.cnt->p || !o.off->p || !o.tot->p || !o.base->p || !o.ent->p)
+		return -1;
+	const unsigned grid = (o.nsub + PJ_SUBS - 1) / PJ_SUBS;
+	hipLaunchKernelGGL(k_pj_hist, dim3(grid), dim3(1024), 0, st, S, n, pbits, skipnil, o.cnt->as<uint32_t>());
+	hipLaunchKernelGGL(k_pj_colscan, dim3(P / 64), dim3(1024), 0, st, o.cnt->as<uint32_t>(), o.nsub, P,
+			   o.off->as<uint32_t>(), o.tot->as<uint32_t>());
+	hipLaunchKernelGGL(k_pj_base, dim3(1), dim3(1024), 0, st, o.tot->as<uint32_t>(), P, o.base->as<uint32_t>(),
+			   maxtot_dev);
+	hipLaunchKernelGGL(k_pj_scatter, dim3(o.nsub), dim3(1024), 0, st, S, n, pbits, skipnil, o.off->as<uint32_t>(),
+			   o.base->as<uint32_t>(), o.ent->as<uint2>());
+	return 0;
+}
+
+// returns 1 when not applicable (caller uses the open-addressing path)
+int
+join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_bat **ap, mgdk_bat **bp)
+{
+	static const int mode = getenv("MGDK_JOIN_PART") ? atoi(getenv("MGDK_JOIN_PART")) : 1;
+	if (mode == 0 || L.w != 4 || R.w != 4 || nr < 65536)
+		return 1;
+	int pbits = 6;
+	while (pbits < PJ_MAXPBITS && ((BUN) 8192 << pbits) < nr)
+		pbits++;
+	const uint32_t P = 1u << pbits;
+	if (nr / P > PJ_MAXFILL * 3 / 4)
+		return 1;
+	hipStream_t st = stream();
+	uint32_t *meta32 = (uint32_t *) meta_buf();
+	uint64_t *meta = (uint64_t *) meta32 + 4;          // [0] pairs, [1] look-back error
+	uint32_t *h = (uint32_t *) pinned(64);
+	if (!hip_ok(hipMemsetAsync(meta32, 0, 64, st), "memset"))
+		return -1;
+	PjSide B, Pr;
+	if (pj_cut(R, nr, pbits, !nil_matches, B, &meta32[0]) < 0)
+		return -1;
+	if (!hip_ok(hipMemcpyAsync(h, meta32, 4, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+		return -1;
+	if (h[0] > PJ_MAXFILL)
+		return 1;
+	if (pj_cut(L, nl, pbits, !nil_matches, Pr, &meta32[1]) < 0)
+		return -1;
+	// subtile-major offsets of the probe results
+	DevBuf offT((size_t) Pr.nsub * P * 4 + 64);
+	uint64_t total = 0;
+	if (!offT.p ||
+	    exclusive_scan(Pr.cnt->as<uint32_t>(), offT.as<uint32_t>(), (BUN) Pr.nsub * P, &total) < 0)
+		return -1;
+	hipLaunchKernelGGL(k_pj_probe, dim3(P), dim3(1024), 0, st, B.ent->as<uint2>(), B.base->as<uint32_t>(),
+			   Pr.ent->as<uint2>(), Pr.base->as<uint32_t>(), pbits, &meta32[2]);
+	if (!hip_ok(hipMemcpyAsync(h, meta32, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+		return -1;
+	if (h[2])
+		return 1;                                   // duplicate build keys
+	mgdk_bat *ra = newbat(0, MGDK_oid, nl), *rb = newbat(0, MGDK_oid, nl);
+	const size_t sbytes = (Pr.nsub + 8) * sizeof(uint64_t);
+	char *sc = (char *) scratch(sbytes);
+	if (!ra || !rb || !sc || !hip_ok(hipMemsetAsync(sc, 0, sbytes, st), "memset")) {
+		unfix2(ra, rb);
+		return -1;
+	}
+	hipLaunchKernelGGL(k_pj_restore, dim3(Pr.nsub), dim3(1024), 0, st, Pr.ent->as<uint2>(), Pr.off->as<uint32_t>(),
+			   Pr.base->as<uint32_t>(), offT.as<uint32_t>(), P, total, nl, Pr.nsub, L, R, (uint32_t *) sc,
+			   (uint64_t *) sc + 8, meta, (oid *) ra->theap, (oid *) rb->theap);
+	uint64_t *h64 = (uint64_t *) pinned(64);
+	if (!hip_ok(hipMemcpyAsync(h64, meta, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
+		unfix2(ra, rb);
+		return -1;
+	}
+	if (h64[1] & 1) {
+		seterr("HY013!BATjoin: look-back did not complete");
+		unfix2(ra, rb);
+		return -1;
+	}
+	ra->count = rb->count = h64[0];
+	*ap = ra;
+	*bp = rb;
+	return 0;
+}
+
 }  // namespace
 
 extern "C" int
@@ -677,8 +1229,10 @@ mgdk_BATjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk_bat 
 			return -1;
 		}
 	} else {
-		rc_ = l->twidth == 8 ? join_lp<8>(L, nl, R, nr, nil_matches, &a, &b)
-				     : join_lp<4>(L, nl, R, nr, nil_matches, &a, &b);
+		rc_ = l->twidth == 4 ? join_part(L, nl, R, nr, nil_matches, &a, &b) : 1;
+		if (rc_ > 0)
+			rc_ = l->twidth == 8 ? join_lp<8>(L, nl, R, nr, nil_matches, &a, &b)
+					     : join_lp<4>(L, nl, R, nr, nil_matches, &a, &b);
 		if (rc_ > 0)
 			rc_ = join_csr(L, nl, R, nr, nil_matches, &a, &b);
 		if (rc_ < 0)

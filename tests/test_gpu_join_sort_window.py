@@ -80,6 +80,35 @@ def test_join_unique_build(gdk, ora, tname, dt):
     assert np.array_equal(b.to_numpy(), ob.values())
 
 
+@pytest.mark.parametrize("nil_matches", [False, True])
+@pytest.mark.parametrize("case", ["plain", "cands", "dups", "date"])
+def test_join_partitioned(gdk, ora, nil_matches, case):
+    """Radix-partitioned LDS path (4-byte keys, >= 64 Ki unique build rows):
+    nils on both sides, candidate lists, a duplicate build key (falls back)."""
+    r = rng(85)
+    nr, nl = 700_001, 2_500_003
+    rv = r.choice(np.arange(-(1 << 30), 1 << 30, 7), nr, replace=False).astype(np.int32)
+    rv[123] = -(1 << 31)                                   # one nil (unique)
+    lv = r.choice(rv, nl).astype(np.int32)
+    lv[r.random(nl) < 0.05] = r.integers(-100, 100)        # misses
+    lv[::997] = -(1 << 31)
+    tp = gdk.TYPE_date if case == "date" else gdk.TYPE_int
+    otp = ora.TYPE_date if case == "date" else ora.TYPE_int
+    if case == "dups":
+        rv[5] = rv[6]
+    kw, okw = {}, {}
+    if case == "cands":
+        sl = np.sort(r.choice(nl, nl // 2, replace=False)).astype(np.uint64) + 11
+        sr = np.sort(r.choice(nr, nr - 1000, replace=False)).astype(np.uint64) + 4
+        kw = dict(sl=mk(gdk, gdk.TYPE_oid, sl), sr=mk(gdk, gdk.TYPE_oid, sr))
+        okw = dict(sl=omk(ora, ora.TYPE_oid, sl, sorted_=True), sr=omk(ora, ora.TYPE_oid, sr, sorted_=True))
+    a, b = gdk.BATjoin(mk(gdk, tp, lv, hseqbase=11), mk(gdk, tp, rv, hseqbase=4), nil_matches=nil_matches, **kw)
+    oa, ob = ora.BATjoin(omk(ora, otp, lv, hseqbase=11), omk(ora, otp, rv, hseqbase=4),
+                         nil_matches=nil_matches, **okw)
+    assert np.array_equal(a.to_numpy(), oa.values())
+    assert np.array_equal(b.to_numpy(), ob.values())
+
+
 def test_join_empty_sides(gdk):
     e = mk(gdk, gdk.TYPE_int, np.zeros(0, np.int32))
     x = mk(gdk, gdk.TYPE_int, np.arange(10, dtype=np.int32))

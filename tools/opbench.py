@@ -27,7 +27,9 @@ def timed(fn, reps=5, kernels=()):
     gdk.prof_reset()
     gdk.prof_enable(True)
     t = time.perf_counter()
+    out = None
     for _ in range(reps):
+        out = None          # release the previous result (its HBM returns to the cache)
         out = fn()
     wall = (time.perf_counter() - t) / reps * 1e3
     gdk.prof_enable(False)
