@@ -16,6 +16,7 @@
 //      groups) + the sortedness property.
 // nil is an ordinary value (all nils form one group); float keys compare by
 // value (+0 == -0, every NaN is nil).
+#include <cstdlib>
 #include <vector>
 
 #include "mgdk_internal.h"
@@ -186,6 +187,274 @@ k_max_oid(const oid *g, BUN n, unsigned long long *out)
 		atomicMax(out, mx);
 }
 
+
+// ---------------------------------------------------------------------------
+// Low-cardinality path (<= GL_MAXG groups; keys that fit one 64-bit image:
+// (prior group << 32 | key) for keys of <= 4 bytes, the key alone for 8-byte
+// keys without prior groups).  Three kernels, no per-row global atomics:
+//   first  each workgroup (64 Ki rows) builds an LDS table of its distinct
+//          keys with their first row, then merges it into a 4 Ki-slot
+//          global table (one CAS + one atomicMin per distinct key per tile);
+//   order  one workgroup sorts the occupied slots by first row (bitonic in
+//          LDS): rank = group id (first occurrence), extents;
+//   assign each workgroup copies the table + slot->id map into LDS and
+//          writes every row's group id, an LDS histogram and the order flag.
+// The image ~0 is kept in a slot of its own (GL_SLOTS).  Overflow of either
+// table (more distinct keys than fit) sends BATgroup to the global path.
+// ---------------------------------------------------------------------------
+
+constexpr uint32_t GL_SLOTS = 4096;
+constexpr uint32_t GL_MAXG = 3072;
+constexpr uint64_t GL_EMPTY = ~0ull;
+constexpr BUN GL_TILE = 65536;
+
+__device__ __forceinline__ uint64_t
+gl_key(const KeySrc &s, BUN i)
+{
+	uint64_t k0, k1, gg;
+	key_at(s, i, k0, k1, gg);
+	return s.has_g ? (gg << 32) | k0 : k0;
+}
+
+__device__ __forceinline__ uint32_t
+gl_hash(uint64_t k)
+{
+	return (uint32_t) ((k * 0x9E3779B97F4A7C15ull) >> 52);
+}
+
+__global__ __launch_bounds__(1024) void
+k_gl_first(KeySrc s, BUN n, unsigned long long *gkey, unsigned long long *gmin, uint32_t *err)
+{
+	__shared__ unsigned long long lkey[GL_SLOTS];
+	__shared__ uint32_t lmin[GL_SLOTS + 1];
+	const unsigned tid = threadIdx.x;
+	for (uint32_t q = tid; q < GL_SLOTS; q += blockDim.x) {
+		lkey[q] = GL_EMPTY;
+		lmin[q] = ~0u;
+	}
+	if (tid == 0)
+		lmin[GL_SLOTS] = ~0u;
+	__syncthreads();
+	const BUN a = (BUN) blockIdx.x * GL_TILE, e = min(n, a + GL_TILE);
+	bool ovf = false;
+	for (BUN i = a + tid; i < e; i += blockDim.x) {
+		const uint64_t k = gl_key(s, i);
+		const uint32_t r = (uint32_t) (i - a);
+		if (k == GL_EMPTY) {
+			atomicMin(&lmin[GL_SLOTS], r);
+			continue;
+		}
+		uint32_t h = gl_hash(k);
+		for (uint32_t pr = 0;; pr++) {
+			unsigned long long o = lkey[h];
+			if (o == GL_EMPTY)
+				o = atomicCAS(&lkey[h], GL_EMPTY, k);
+			if (o == GL_EMPTY || o == k) {
+				if (lmin[h] > r)
+					atomicMin(&lmin[h], r);
+				break;
+			}
+			h = (h + 1) & (GL_SLOTS - 1);
+			if (pr >= GL_SLOTS) {
+				ovf = true;
+				break;
+			}
+		}
+	}
+	if (__any(ovf) && __lane_id() == 0)
+		atomicOr(err, 1u);
+	__syncthreads();
+	for (uint32_t q = tid; q <= GL_SLOTS; q += blockDim.x) {
+		if (lmin[q] == ~0u)
+			continue;
+		const unsigned long long first = a + lmin[q];
+		if (q == GL_SLOTS) {
+			if (gmin[GL_SLOTS] > first)
+				atomicMin(&gmin[GL_SLOTS], first);
+			continue;
+		}
+		const uint64_t k = lkey[q];
+		uint32_t h = gl_hash(k);
+		for (uint32_t pr = 0;; pr++) {
+			unsigned long long o = gkey[h];
+			if (o == GL_EMPTY)
+				o = atomicCAS(&gkey[h], GL_EMPTY, k);
+			if (o == GL_EMPTY || o == k) {
+				if (gmin[h] > first)
+					atomicMin(&gmin[h], first);
+				break;
+			}
+			h = (h + 1) & (GL_SLOTS - 1);
+			if (pr >= GL_SLOTS) {
+				atomicOr(err, 1u);
+				break;
+			}
+		}
+	}
+}
+
+// one workgroup: occupied slots sorted by first row -> group ids, extents
+__global__ __launch_bounds__(1024) void
+k_gl_order(const unsigned long long *gmin, uint32_t *gmap, bool cdense, oid cseq, const oid *coids, oid *ext,
+	   uint32_t *ngrp)
+{
+	constexpr uint32_t NS = 2 * GL_SLOTS;          // power of two >= GL_SLOTS + 1
+	__shared__ unsigned long long sk[NS];
+	__shared__ uint32_t s_cnt;
+	const unsigned tid = threadIdx.x;
+	if (tid == 0)
+		s_cnt = 0;
+	for (uint32_t q = tid; q < NS; q += blockDim.x)
+		sk[q] = q <= GL_SLOTS && gmin[q] != ~0ull ? (gmin[q] << 13) | q : ~0ull;
+	__syncthreads();
+	for (uint32_t k = 2; k <= NS; k <<= 1) {
+		for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+			for (uint32_t i = tid; i < NS; i += blockDim.x) {
+				const uint32_t l = i ^ j;
+				if (l > i) {
+					const bool up = (i & k) == 0;
+					const unsigned long long x = sk[i], y = sk[l];
+					if ((x > y) == up) {
+						sk[i] = y;
+						sk[l] = x;
+					}
+				}
+			}
+			__syncthreads();
+		}
+	}
+	for (uint32_t r = tid; r < NS; r += blockDim.x) {
+		const unsigned long long v = sk[r];
+		if (v == ~0ull)
+			continue;
+		atomicAdd(&s_cnt, 1u);
+		const uint32_t slot = (uint32_t) (v & 8191);
+		const BUN first = (BUN) (v >> 13);
+		gmap[slot] = r;
+		ext[r] = cdense ? cseq + first : coids[first];
+	}
+	__syncthreads();
+	if (tid == 0)
+		*ngrp = s_cnt;
+}
+
+__device__ __forceinline__ uint32_t
+gl_lookup(const unsigned long long *lkey, const uint32_t *lmap, uint64_t k)
+{
+	if (k == GL_EMPTY)
+		return lmap[GL_SLOTS];
+	uint32_t h = gl_hash(k);
+	while (lkey[h] != k)
+		h = (h + 1) & (GL_SLOTS - 1);
+	return lmap[h];
+}
+
+__global__ __launch_bounds__(1024) void
+k_gl_assign(KeySrc s, BUN n, const unsigned long long *gkey, const uint32_t *gmap, uint32_t ngrp, oid *gid,
+	    unsigned long long *histo, uint32_t *unsorted)
+{
+	__shared__ unsigned long long lkey[GL_SLOTS];
+	__shared__ uint32_t lmap[GL_SLOTS + 1];
+	__shared__ uint32_t lh[GL_MAXG];
+	const unsigned tid = threadIdx.x, lane = __lane_id();
+	for (uint32_t q = tid; q < GL_SLOTS; q += blockDim.x) {
+		lkey[q] = gkey[q];
+		lmap[q] = gmap[q];
+	}
+	if (tid == 0)
+		lmap[GL_SLOTS] = gmap[GL_SLOTS];
+	for (uint32_t q = tid; q < ngrp; q += blockDim.x)
+		lh[q] = 0;
+	__syncthreads();
+	const BUN a = (BUN) blockIdx.x * GL_TILE, e = min(n, a + GL_TILE);
+	uint32_t uns = 0;
+	for (BUN i0 = a; i0 < e; i0 += blockDim.x) {
+		const BUN i = i0 + tid;
+		uint32_t g = 0;
+		if (i < e) {
+			g = gl_lookup(lkey, lmap, gl_key(s, i));
+			gid[i] = g;
+			atomicAdd(&lh[g], 1u);
+		}
+		uint32_t gp = __shfl_up(g, 1);
+		if (lane == 0 && i > 0 && i < e)
+			gp = gl_lookup(lkey, lmap, gl_key(s, i - 1));
+		if (i > 0 && i < e && gp > g)
+			uns = 1;
+	}
+	if (__any(uns) && lane == 0)
+		publish_or(unsorted, 1u);
+	__syncthreads();
+	for (uint32_t q = tid; q < ngrp; q += blockDim.x)
+		if (lh[q])
+			atomicAdd(&histo[q], (unsigned long long) lh[q]);
+}
+
+// returns 1 when the path does not apply (too many groups)
+int
+group_lds(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mgdk_bat **enp, mgdk_bat **hnp)
+{
+	hipStream_t st = stream();
+	DevBuf gkey((GL_SLOTS + 1) * 8), gmin((GL_SLOTS + 1) * 8), gmap((GL_SLOTS + 1) * 4), ext((GL_SLOTS + 1) * 8);
+	uint32_t *m = (uint32_t *) meta_buf();
+	uint32_t *h = (uint32_t *) pinned(16);
+	if (!gkey.p || !gmin.p || !gmap.p || !ext.p)
+		return -1;
+	if (!hip_ok(hipMemsetAsync(gkey.p, 0xff, (GL_SLOTS + 1) * 8, st), "memset") ||
+	    !hip_ok(hipMemsetAsync(gmin.p, 0xff, (GL_SLOTS + 1) * 8, st), "memset") ||
+	    !hip_ok(hipMemsetAsync(m, 0, 16, st), "memset"))
+		return -1;
+	const unsigned tiles = (unsigned) ((n + GL_TILE - 1) / GL_TILE);
+	hipLaunchKernelGGL(k_gl_first, dim3(tiles), dim3(1024), 0, st, ks, n, gkey.as<unsigned long long>(),
+			   gmin.as<unsigned long long>(), &m[0]);
+	hipLaunchKernelGGL(k_gl_order, dim3(1), dim3(1024), 0, st, gmin.as<unsigned long long>(), gmap.as<uint32_t>(),
+			   ci.dense, ci.seq, ci.oids, ext.as<oid>(), &m[1]);
+	if (!hip_ok(hipMemcpyAsync(h, m, 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+		return -1;
+	if (h[0] || h[1] > GL_MAXG)
+		return 1;
+	const uint32_t ngrp = h[1];
+	mgdk_bat *en = newbat(0, MGDK_oid, ngrp), *hn = newbat(0, MGDK_lng, ngrp), *gn = newbat(hseqb, MGDK_oid, n);
+	if (!en || !hn || !gn || !hip_ok(hipMemsetAsync(hn->theap, 0, ngrp * 8 + 8, st), "memset") ||
+	    !hip_ok(hipMemcpyAsync(en->theap, ext.p, ngrp * 8, hipMemcpyDeviceToDevice, st), "memcpy")) {
+		mgdk_BBPunfix(en);
+		mgdk_BBPunfix(hn);
+		mgdk_BBPunfix(gn);
+		return -1;
+	}
+	hipLaunchKernelGGL(k_gl_assign, dim3(tiles), dim3(1024), 0, st, ks, n, gkey.as<unsigned long long>(),
+			   gmap.as<uint32_t>(), ngrp, (oid *) gn->theap, (unsigned long long *) hn->theap, &m[2]);
+	oid fl[2] = {0, 0};
+	if (!hip_ok(hipMemcpyAsync(h, m, 12, hipMemcpyDeviceToHost, st), "memcpy") ||
+	    (ngrp > 0 && (!hip_ok(hipMemcpyAsync(&fl[0], ext.p, 8, hipMemcpyDeviceToHost, st), "memcpy") ||
+			  !hip_ok(hipMemcpyAsync(&fl[1], ext.as<oid>() + ngrp - 1, 8, hipMemcpyDeviceToHost, st),
+				  "memcpy"))) ||
+	    !sync()) {
+		mgdk_BBPunfix(en);
+		mgdk_BBPunfix(hn);
+		mgdk_BBPunfix(gn);
+		return -1;
+	}
+	gn->count = n;
+	en->count = ngrp;
+	hn->count = ngrp;
+	gn->tsorted = h[2] == 0;
+	gn->trevsorted = ngrp == 1 || n <= 1;
+	gn->tkey = ngrp == n;
+	gn->tnonil = 1;
+	en->tsorted = en->tkey = en->tnonil = 1;
+	en->trevsorted = ngrp == 1;
+	hn->tkey = ngrp == 1;
+	hn->tsorted = hn->trevsorted = ngrp == n || ngrp == 1;
+	hn->tnonil = 1;
+	if (ngrp > 0 && fl[1] - fl[0] == ngrp - 1)
+		setdense(en, fl[0], ngrp);
+	*gnp = gn;
+	*enp = en;
+	*hnp = hn;
+	return 0;
+}
+
 mgdk_bat *
 dense_or_copy(const Cand &ci)
 {
@@ -289,6 +558,15 @@ mgdk_BATgroup(mgdk_bat **groups, mgdk_bat **extents, mgdk_bat **histo, mgdk_bat 
 			gmax = *hm;
 		} else if (g) {
 			gmax = g->tseqbase + n;
+		}
+		// low-cardinality path first (falls through when it does not apply)
+		static const bool lds_on = getenv("MGDK_GROUP_LDS") ? atoi(getenv("MGDK_GROUP_LDS")) != 0 : true;
+		if (lds_on && ks.w <= 8 && (!ks.has_g || (ks.w <= 4 && gmax < 0xffffffffull)) && n < ((BUN) 1 << 50)) {
+			const int rc = group_lds(ks, n, ci, hseqb, &gn, &en, &hn);
+			if (rc < 0)
+				goto fail;
+			if (rc == 0)
+				goto done;
 		}
 		const bool small = (ks.kind <= 1 && ks.w <= 2);
 		int dshift = ks.w * 8;

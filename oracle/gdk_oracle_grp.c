@@ -30,6 +30,28 @@ ci_get(const ora_ci *ci, uint64_t i)
 #define HGE_NIL ((ora_hge) ((unsigned __int128) 1 << 127))
 #define HGE_MAX ((ora_hge) (((unsigned __int128) 1 << 127) - 1))
 
+/* grouping key of row p: values compare by equality as in GDK's group code
+ * (gdk_group.c, flt/dbl by value: -0 == +0, every NaN is the nil) */
+static bool val_at(const ora_bat *b, uint64_t p, ora_hge *v);
+static bool
+grp_key(const ora_bat *b, uint64_t p, ora_hge *v)
+{
+	if (b->type == ORA_flt || b->type == ORA_dbl) {
+		double d = b->type == ORA_flt ? (double) ((const float *) b->base)[p] : ((const double *) b->base)[p];
+		if (isnan(d)) {
+			*v = (ora_hge) 1 << 100;   /* outside every double image */
+			return true;
+		}
+		if (d == 0.0)
+			d = 0.0;
+		int64_t bits;
+		memcpy(&bits, &d, 8);
+		*v = bits;
+		return false;
+	}
+	return val_at(b, p, v);
+}
+
 /* value of row p of b widened to 128 bits; returns true when nil */
 static bool
 val_at(const ora_bat *b, uint64_t p, ora_hge *v)
@@ -113,7 +135,7 @@ ora_group(ora_bat **groups, ora_bat **extents, ora_bat **histo,
 	for (uint64_t i = 0; i < ci.n; i++) {
 		ora_oid o = ci_get(&ci, i);
 		ora_hge v;
-		(void) val_at(b, o - b->hseqbase, &v);
+		(void) grp_key(b, o - b->hseqbase, &v);
 		ora_oid gg = 0;
 		if (g)
 			gg = g->type == ORA_void ? g->tseqbase + i : ((const ora_oid *) g->base)[i];

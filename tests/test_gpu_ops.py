@@ -255,6 +255,32 @@ def test_group_random(gdk, ora, tname, dt, card):
     assert np.array_equal(h2.to_numpy(), oh2.values())
 
 
+@pytest.mark.parametrize("tname,dt", [("lng", np.int64), ("dbl", np.float64)])
+def test_group_low_cardinality_edges(gdk, ora, tname, dt):
+    """LDS path: the all-ones key image (lng -1), -0.0 == 0.0, NaN nils,
+    candidate lists and tiles of 64 Ki rows; > 3072 groups fall back."""
+    r = rng(62)
+    tp = getattr(gdk, "TYPE_" + tname)
+    n = 300_001
+    vals = r.integers(-3, 40, n).astype(dt)
+    if dt == np.float64:
+        vals[r.random(n) < 0.01] = np.nan
+        vals[r.random(n) < 0.01] = -0.0
+    cand = np.sort(r.choice(n, 200_000, replace=False)).astype(np.uint64)
+    for s in (None, cand):
+        S = mk(gdk, gdk.TYPE_oid, s) if s is not None else None
+        OS = omk(ora, ora.TYPE_oid, s, sorted_=True) if s is not None else None
+        g, e, h = gdk.BATgroup(mk(gdk, tp, vals), S)
+        og, oe, oh = ora.BATgroup(omk(ora, tp, vals), OS)
+        assert np.array_equal(g.to_numpy(), og.values())
+        assert np.array_equal(e.to_numpy(), oe.values())
+        assert np.array_equal(h.to_numpy(), oh.values())
+    wide = r.integers(0, 5000, n).astype(dt)
+    g, e, h = gdk.BATgroup(mk(gdk, tp, wide))
+    og, oe, oh = ora.BATgroup(omk(ora, tp, wide))
+    assert np.array_equal(g.to_numpy(), og.values()) and np.array_equal(h.to_numpy(), oh.values())
+
+
 def test_grouped_aggregates(gdk, ora):
     r = rng(71)
     n = 300_000
