@@ -293,49 +293,36 @@ k_gl_first(KeySrc s, BUN n, unsigned long long *gkey, unsigned long long *gmin, 
 	}
 }
 
-// one workgroup: occupied slots sorted by first row -> group ids, extents
+// one workgroup: occupied slots ranked by first row (counting ranks over
+// the compacted keys first << 13 | slot, all distinct) -> group ids, extents
 __global__ __launch_bounds__(1024) void
 k_gl_order(const unsigned long long *gmin, uint32_t *gmap, bool cdense, oid cseq, const oid *coids, oid *ext,
 	   uint32_t *ngrp)
 {
-	constexpr uint32_t NS = 2 * GL_SLOTS;          // power of two >= GL_SLOTS + 1
-	__shared__ unsigned long long sk[NS];
+	__shared__ unsigned long long sk[GL_SLOTS + 1];
 	__shared__ uint32_t s_cnt;
 	const unsigned tid = threadIdx.x;
 	if (tid == 0)
 		s_cnt = 0;
-	for (uint32_t q = tid; q < NS; q += blockDim.x)
-		sk[q] = q <= GL_SLOTS && gmin[q] != ~0ull ? (gmin[q] << 13) | q : ~0ull;
 	__syncthreads();
-	for (uint32_t k = 2; k <= NS; k <<= 1) {
-		for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-			for (uint32_t i = tid; i < NS; i += blockDim.x) {
-				const uint32_t l = i ^ j;
-				if (l > i) {
-					const bool up = (i & k) == 0;
-					const unsigned long long x = sk[i], y = sk[l];
-					if ((x > y) == up) {
-						sk[i] = y;
-						sk[l] = x;
-					}
-				}
-			}
-			__syncthreads();
-		}
+	for (uint32_t q = tid; q <= GL_SLOTS; q += blockDim.x) {
+		const unsigned long long f = gmin[q];
+		if (f != ~0ull)
+			sk[atomicAdd(&s_cnt, 1u)] = (f << 13) | q;
 	}
-	for (uint32_t r = tid; r < NS; r += blockDim.x) {
-		const unsigned long long v = sk[r];
-		if (v == ~0ull)
-			continue;
-		atomicAdd(&s_cnt, 1u);
+	__syncthreads();
+	const uint32_t c = s_cnt;
+	for (uint32_t i = tid; i < c; i += blockDim.x) {
+		const unsigned long long v = sk[i];
+		uint32_t r = 0;
+		for (uint32_t j = 0; j < c; j++)
+			r += sk[j] < v;
 		const uint32_t slot = (uint32_t) (v & 8191);
-		const BUN first = (BUN) (v >> 13);
 		gmap[slot] = r;
-		ext[r] = cdense ? cseq + first : coids[first];
+		ext[r] = cdense ? cseq + (BUN) (v >> 13) : coids[v >> 13];
 	}
-	__syncthreads();
 	if (tid == 0)
-		*ngrp = s_cnt;
+		*ngrp = c;
 }
 
 __device__ __forceinline__ uint32_t

@@ -288,6 +288,84 @@ k_newgrp(const K *keys, BUN n, uint8_t *flag)
 		flag[i] = i > 0 && keys[i] != keys[i - 1];
 }
 
+// group ids of a sorted key image: gid[i] = number of i' in [1, i] with
+// keys[i'] != keys[i'-1].  Two passes over 4096-key tiles (count, then
+// write with a workgroup scan) around a scan of the tile counts: 16 B/row.
+constexpr int GTILE = 4096;
+
+template <typename K>
+__global__ __launch_bounds__(256) void
+k_gid_count(const K *keys, BUN n, uint32_t *cnt)
+{
+	const BUN t0 = (BUN) blockIdx.x * GTILE;
+	uint32_t c = 0;
+#pragma unroll
+	for (int q = 0; q < GTILE / 256; q++) {
+		const BUN i = t0 + threadIdx.x + (BUN) q * 256;
+		if (i > 0 && i < n)
+			c += keys[i] != keys[i - 1];
+	}
+	c = block_reduce(c, [](uint32_t a, uint32_t b) { return a + b; });
+	if (threadIdx.x == 0)
+		cnt[blockIdx.x] = c;
+}
+
+template <typename K>
+__global__ __launch_bounds__(256) void
+k_gid_write(const K *keys, BUN n, const uint64_t *pre, oid *gid)
+{
+	// coalesced loads into LDS, a thread scans 16 consecutive keys, the ids
+	// go back through LDS to coalesced stores
+	constexpr int Q = GTILE / 256;
+	// one pad slot per 16 so a thread's 16-run starts in a different bank
+#define GPAD(j) ((j) + ((j) >> 4))
+	__shared__ K s_k[GPAD(GTILE + 1) + 1];
+	__shared__ oid s_g[GPAD(GTILE) + 1];
+	__shared__ uint32_t s_w[4];
+	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+	const BUN t0 = (BUN) blockIdx.x * GTILE;
+#pragma unroll
+	for (int q = 0; q < Q; q++) {
+		const BUN i = t0 + (BUN) q * 256 + tid;
+		s_k[GPAD(1 + q * 256 + tid)] = i < n ? keys[i] : K(0);
+	}
+	if (tid == 0)
+		s_k[GPAD(0)] = t0 > 0 ? keys[t0 - 1] : K(0);
+	__syncthreads();
+	uint32_t inc[Q], c = 0;
+#pragma unroll
+	for (int q = 0; q < Q; q++) {
+		const int j = tid * Q + q;
+		const BUN i = t0 + j;
+		c += (i > 0 && i < n && s_k[GPAD(j + 1)] != s_k[GPAD(j)]);
+		inc[q] = c;
+	}
+	uint32_t x = c;
+#pragma unroll
+	for (int o = 1; o < 64; o <<= 1) {
+		const uint32_t y = __shfl_up(x, o);
+		if (lane >= (unsigned) o)
+			x += y;
+	}
+	if (lane == 63)
+		s_w[w] = x;
+	__syncthreads();
+	uint64_t base = pre[blockIdx.x] + x - c;
+	for (unsigned q = 0; q < w; q++)
+		base += s_w[q];
+#pragma unroll
+	for (int q = 0; q < Q; q++)
+		s_g[GPAD(tid * Q + q)] = base + inc[q];
+	__syncthreads();
+#pragma unroll
+	for (int q = 0; q < Q; q++) {
+		const BUN i = t0 + (BUN) q * 256 + tid;
+		if (i < n)
+			gid[i] = s_g[GPAD(q * 256 + tid)];
+	}
+#undef GPAD
+}
+
 __global__ __launch_bounds__(256) void
 k_gid(const uint64_t *excl, const uint8_t *flag, BUN n, oid *gid)
 {
@@ -418,15 +496,19 @@ sort_typed(const mgdk_bat *b, bool reverse, bool nilslast, mgdk_bat *sn, mgdk_ba
 	}
 	if (gn) {
 		// groups: a new group wherever the sorted key image changes
-		DevBuf fl(n + 1), ex(n * 8 + 8);
+		const BUN nt = (n + GTILE - 1) / GTILE;
+		DevBuf cnt(nt * 4 + 4), pre(nt * 8 + 8);
 		uint64_t tot = 0;
-		if (!fl.p || !ex.p)
+		if (!cnt.p || !pre.p)
 			return -1;
-		hipLaunchKernelGGL((k_newgrp<K>), dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st, ks, n, fl.as<uint8_t>());
-		if (exclusive_scan(fl.as<uint8_t>(), ex.as<uint64_t>(), n, &tot) < 0)
-			return -1;
-		hipLaunchKernelGGL(k_gid, dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st, ex.as<uint64_t>(),
-				   fl.as<uint8_t>(), n, (oid *) gn->theap);
+		if (nt > 0) {
+			hipLaunchKernelGGL((k_gid_count<K>), dim3((unsigned) nt), dim3(256), 0, st, ks, n,
+					   cnt.as<uint32_t>());
+			if (exclusive_scan(cnt.as<uint32_t>(), pre.as<uint64_t>(), nt, &tot) < 0)
+				return -1;
+			hipLaunchKernelGGL((k_gid_write<K>), dim3((unsigned) nt), dim3(256), 0, st, ks, n,
+					   pre.as<uint64_t>(), (oid *) gn->theap);
+		}
 		if (!sync())
 			return -1;
 		gn->count = n;
