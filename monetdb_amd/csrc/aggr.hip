@@ -204,6 +204,8 @@ mag_bound(unsigned long long cls)
 
 }  // namespace
 
+int mgdk_fsum(void *res, int tp, mgdk_bat *b, mgdk_bat *s, bool skip_nils, bool nil_if_empty);   // fsum.hip
+
 extern "C" int
 mgdk_BATsum(void *res, int tp, mgdk_bat *b, mgdk_bat *s, bool skip_nils, bool nil_if_empty)
 {
@@ -211,6 +213,8 @@ mgdk_BATsum(void *res, int tp, mgdk_bat *b, mgdk_bat *s, bool skip_nils, bool ni
 		seterr("BATsum: NULL argument");
 		return -1;
 	}
+	if (b->ttype == MGDK_flt || b->ttype == MGDK_dbl)
+		return mgdk_fsum(res, tp, b, s, skip_nils, nil_if_empty);   // dofsum, gdk_aggr.c:183
 	if (!int_type(b->ttype) || !(int_type(tp) || tp == MGDK_dbl || tp == MGDK_flt)) {
 		seterr("type combination (sum(%s)->%s) not supported.\n", atomname(b->ttype), atomname(tp));
 		return -1;

@@ -783,6 +783,131 @@ ora_calc(char op, const ora_bat *b1, const void *c1, int t1,
  * integer sum into tp with overflow -> "22003!overflow in sum aggregate.";
  * nils are skipped when skip_nils, else make the result nil; an empty input
  * gives nil when nil_if_empty, else 0. */
+
+/* dofsum, gdk/gdk_aggr.c:183-427, one group: Shewchuk / msum partials with
+ * the reference's handling of intermediate overflow (twopow, infs) and its
+ * final correction step.  INFINITES_ALLOWED is not defined in the reference
+ * build, so infs counts overflows.  Returns -1 with the overflow message. */
+static void
+ora_twosum(volatile double *hi, volatile double *lo, double x, double y)
+{
+	volatile double yr;
+	*hi = x + y;
+	yr = *hi - x;
+	*lo = y - yr;
+}
+
+static bool
+ora_samesign(double x, double y)
+{
+	return (x >= 0) == (y >= 0);
+}
+
+static int
+ora_fsum(double *out, bool *isnil, const ora_bat *b, const ora_ci *ci, bool skip_nils, bool nil_if_empty)
+{
+	int npartials = 0, maxpartials = 2, infs = 0;
+	bool valseen = false;
+	double *partials = malloc(maxpartials * sizeof(double));
+	double x, y;
+	volatile double lo, hi;
+	const double twopow = pow(2.0, 1023.0);
+	*isnil = false;
+	for (uint64_t k = 0; k < ci->n; k++) {
+		uint64_t p = ci_get(ci, k) - b->hseqbase;
+		x = b->type == ORA_flt ? (double) ((const float *) b->base)[p] : ((const double *) b->base)[p];
+		if (isnan(x)) {
+			if (!skip_nils) {
+				*isnil = true;
+				free(partials);
+				return 0;
+			}
+			continue;
+		}
+		valseen = true;
+		int i = 0;
+		for (int pi = 0; pi < npartials; pi++) {
+			y = partials[pi];
+			if (fabs(x) < fabs(y)) { double t = x; x = y; y = t; }
+			ora_twosum(&hi, &lo, x, y);
+			if (isinf(hi)) {
+				int sign = hi > 0 ? 1 : -1;
+				hi = x - twopow * sign;
+				x = hi - twopow * sign;
+				infs += sign;
+				if (fabs(x) < fabs(y)) { double t = x; x = y; y = t; }
+				ora_twosum(&hi, &lo, x, y);
+			}
+			if (lo != 0)
+				partials[i++] = lo;
+			x = hi;
+		}
+		if (x != 0) {
+			if (i == maxpartials) {
+				maxpartials *= 2;
+				partials = realloc(partials, maxpartials * sizeof(double));
+			}
+			partials[i++] = x;
+		}
+		npartials = i;
+	}
+	if (!valseen) {
+		*isnil = nil_if_empty;
+		*out = 0;
+		free(partials);
+		return 0;
+	}
+	if ((infs == 1 || infs == -1) && npartials > 0 && !ora_samesign(infs, partials[npartials - 1])) {
+		ora_twosum(&hi, &lo, infs * twopow, partials[npartials - 1] / 2);
+		if (isinf(2 * hi)) {
+			y = 2 * lo;
+			x = hi + y;
+			x -= hi;
+			if (x == y && npartials > 1 && ora_samesign(lo, partials[npartials - 2])) {
+				*out = 2 * (hi + y);
+				free(partials);
+				return 0;
+			}
+		} else {
+			if (lo) {
+				if (npartials == maxpartials)
+					partials = realloc(partials, ++maxpartials * sizeof(double));
+				partials[npartials - 1] = 2 * lo;
+				partials[npartials++] = 2 * hi;
+			} else {
+				partials[npartials - 1] = 2 * hi;
+			}
+			infs = 0;
+		}
+	}
+	if (infs != 0) {
+		free(partials);
+		ora_seterr("22003!overflow in sum aggregate.\n");
+		return -1;
+	}
+	if (npartials == 0) {
+		*out = 0;
+		free(partials);
+		return 0;
+	}
+	hi = partials[--npartials];
+	while (npartials > 0) {
+		ora_twosum(&hi, &lo, hi, partials[--npartials]);
+		if (lo) {
+			partials[npartials++] = lo;
+			break;
+		}
+	}
+	if (npartials >= 2 && ora_samesign(partials[npartials - 1], partials[npartials - 2]) &&
+	    hi + 2 * partials[npartials - 1] - hi == 2 * partials[npartials - 1]) {
+		hi += 2 * partials[npartials - 1];
+		partials[npartials - 1] = -partials[npartials - 1];
+	}
+	free(partials);
+	*out = hi;
+	return 0;
+}
+
 int
 ora_sum(void *res, int tp, const ora_bat *b, const ora_bat *s,
 	bool skip_nils, bool nil_if_empty)
@@ -791,6 +916,23 @@ ora_sum(void *res, int tp, const ora_bat *b, const ora_bat *s,
 	if (ora_ci_init(&ci, b, s) < 0)
 		return -1;
 	int t = basetype(b->type);
+	if (t == ORA_flt || t == ORA_dbl) {
+		double d;
+		bool isnil;
+		if (ora_fsum(&d, &isnil, b, &ci, skip_nils, nil_if_empty) < 0)
+			return -1;
+		if (tp == ORA_dbl) {
+			*(double *) res = isnil ? nan("") : d;
+			return 0;
+		}
+		float f = (float) d;
+		if (!isnil && (isinf(f) || isnan(f))) {
+			ora_seterr("22003!overflow in sum aggregate.\n");
+			return -1;
+		}
+		*(float *) res = isnil ? nanf("") : f;
+		return 0;
+	}
 	if (tp == ORA_dbl) {
 		/* integers into dbl (gdk_aggr.c:1112-1156): the exact average
 		 * (BATcalcavg, sum in hge :2905-2960) times the count; any nil

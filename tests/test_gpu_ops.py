@@ -428,3 +428,53 @@ def test_q6_value_ranges(gdk, ora, case):
     got = gdk.q6_fused(cols["shipdate"], cols["discount"], cols["quantity"],
                        cols["extendedprice"], d0, d1, 5, 7, 2400)
     assert got == ora.q6(host, 4)
+
+
+@pytest.mark.parametrize("tname", ["dbl", "flt"])
+def test_fsum_exact(gdk, ora, tname):
+    """BATsum of flt / dbl (dofsum, gdk_aggr.c:183): bit-exact with the
+    oracle's msum restatement on wide ranges, cancellation, nils,
+    candidates, subnormal and intermediate-overflow cases."""
+    r = rng(92)
+    tp = getattr(gdk, "TYPE_" + tname)
+    dt = np.float64 if tname == "dbl" else np.float32
+    cases = []
+    for scale in ((1, 5, 20, 60) if tname == "dbl" else (1, 5, 20, 30)):
+        v = (r.standard_normal(300_000) * 10.0 ** r.integers(-scale, scale, 300_000)).astype(dt)
+        cases.append(v)
+    v = r.standard_normal(200_000).astype(dt)
+    cases.append(np.concatenate([v, -v[::-1], np.array([1e-3], dt)]))      # cancels to 1e-3
+    cases.append(np.array([2.0 ** -1070, 2.0 ** -1074, -(2.0 ** -1073)], np.float64).astype(dt))
+    cases.append(np.array([0.0, -0.0], dt))
+    if tname == "dbl":
+        cases.append(np.array([1e308, 1e308, -1e308, 1.0], np.float64))    # finite despite overflow
+        cases.append(np.array([1e16, 1.0, -1e16] * 1000, np.float64))
+    for v in cases:
+        B, OB = gdk.BAT.from_numpy(tp, v), ora.Bat.from_array(tp, v)
+        for rt in ((gdk.TYPE_dbl,) if tname == "dbl" else (gdk.TYPE_dbl, gdk.TYPE_flt)):
+            try:
+                want = ora.BATsum(rt, OB)
+            except ora.OracleError as e:
+                with pytest.raises(gdk.GDKError) as ei:
+                    gdk.BATsum(rt, B)
+                assert str(ei.value) == str(e)
+                continue
+            got = gdk.BATsum(rt, B)
+            assert np.array(got, np.float64).tobytes() == np.array(want, np.float64).tobytes(), (v[:4], rt)
+    # nils, empty, candidates
+    v = r.standard_normal(100_000).astype(dt)
+    v[::37] = np.nan
+    s = np.sort(r.choice(100_000, 50_000, replace=False)).astype(np.uint64)
+    B, OB = gdk.BAT.from_numpy(tp, v), ora.Bat.from_array(tp, v)
+    S, OS = gdk.BAT.from_numpy(gdk.TYPE_oid, s), ora.Bat.from_array(ora.TYPE_oid, s)
+    assert gdk.BATsum(gdk.TYPE_dbl, B, S) == ora.BATsum(ora.TYPE_dbl, OB, OS)
+    assert np.isnan(gdk.BATsum(gdk.TYPE_dbl, B, skip_nils=False))
+    E = gdk.BAT.from_numpy(tp, np.array([np.nan, np.nan], dt))
+    assert np.isnan(gdk.BATsum(gdk.TYPE_dbl, E)) and gdk.BATsum(gdk.TYPE_dbl, E, nil_if_empty=False) == 0.0
+
+
+def test_fsum_overflow(gdk):
+    with pytest.raises(gdk.GDKError, match="22003!overflow in sum aggregate"):
+        gdk.BATsum(gdk.TYPE_dbl, gdk.BAT.from_numpy(gdk.TYPE_dbl, np.array([1e308, 1e308])))
+    with pytest.raises(gdk.GDKError, match="22003!overflow in sum aggregate"):
+        gdk.BATsum(gdk.TYPE_flt, gdk.BAT.from_numpy(gdk.TYPE_flt, np.array([3e38, 3e38], np.float32)))

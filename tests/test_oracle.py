@@ -191,3 +191,23 @@ def test_window_frames_sqltest(ora):
         lambda b, p, o, ign, f: ora.analyticalcount(b, p, o, None, None, ign, f).values(),
         lambda tp, a: ora.Bat.from_array(tp, a), ora.TYPE_int, ora.TYPE_bit, ora.TYPE_lng)
     assert not bad, bad
+
+
+def test_fsum_oracle(ora):
+    """dofsum restatement (gdk_aggr.c:183-427) = the correctly rounded sum
+    (msum), checked against math.fsum; flt results are that double cast."""
+    r = np.random.default_rng(91)
+    for trial in range(30):
+        n = int(r.integers(1, 3000))
+        v = r.standard_normal(n) * 10.0 ** r.integers(-20, 20, n)
+        if trial % 3 == 0:
+            v = np.concatenate([v, -v[: n // 2]])
+        B = ora.Bat.from_array(ora.TYPE_dbl, v)
+        assert ora.BATsum(ora.TYPE_dbl, B) == math.fsum(v)
+        f = v.astype(np.float32)
+        assert np.float32(ora.BATsum(ora.TYPE_flt, ora.Bat.from_array(ora.TYPE_flt, f))) == \
+            np.float32(math.fsum(f.astype(np.float64)))
+    big = np.array([1e308, 1e308, -1e308], np.float64)         # intermediate overflow, finite result
+    assert ora.BATsum(ora.TYPE_dbl, ora.Bat.from_array(ora.TYPE_dbl, big)) == 1e308
+    with pytest.raises(ora.OracleError, match="overflow"):
+        ora.BATsum(ora.TYPE_dbl, ora.Bat.from_array(ora.TYPE_dbl, np.array([1e308, 1e308])))
