@@ -292,10 +292,14 @@ k_select(SelArgs<T> a)
 //                placed in LDS in order and stored as one contiguous run.
 // The column is read once; extra traffic is the bitmap twice (2 bits/value).
 constexpr int SROWS = 16;
+// rows of 16-B loads per lane: 1- and 2-byte types unpack 16 / 8 values per
+// load, so fewer rows keep the count kernel's registers (and occupancy) in
+// line with the 4- and 8-byte types (bte at 16 rows: 140 VGPRs, 0.8 TB/s)
+template <typename T> constexpr int sel_srows() { return sizeof(T) >= 4 ? SROWS : sizeof(T) == 2 ? SROWS / 2 : SROWS / 4; }
 
 template <typename T> constexpr int sel_v() { return (int) (16 / sizeof(T)); }
 // bitmap words per tile and per lane of k_sel_write
-template <typename T> constexpr int sel_wpt() { return SROWS * 256 * sel_v<T>() / 32; }
+template <typename T> constexpr int sel_wpt() { return sel_srows<T>() * 256 * sel_v<T>() / 32; }
 template <typename T> constexpr int sel_wpl() { return sel_wpt<T>() >= 256 ? sel_wpt<T>() / 256 : 1; }
 
 template <typename T, int MODE>
@@ -303,28 +307,29 @@ __global__ __launch_bounds__(256) void
 k_sel_count(SelArgs<T> a, uint32_t *bits, uint32_t *counts)
 {
 	constexpr int V = sel_v<T>(), L = 32 / V;   // lanes per bitmap word
+	constexpr int SR = sel_srows<T>();
 	typedef T vec_t __attribute__((ext_vector_type(V)));
 	const unsigned tid = threadIdx.x, lane = tid & 63;
 	const uint32_t t = blockIdx.x;
 	const uint64_t nslots = a.n + a.shift;
-	const bool full = (t > 0 || a.shift == 0) && ((uint64_t) t + 1) * SROWS * 256 * V <= nslots;
-	vec_t x[SROWS];
+	const bool full = (t > 0 || a.shift == 0) && ((uint64_t) t + 1) * SR * 256 * V <= nslots;
+	vec_t x[SR];
 	if (full) {
 #pragma unroll
-		for (int r = 0; r < SROWS; r++)
-			x[r] = __builtin_nontemporal_load((const vec_t *) (a.col_al + (((uint64_t) t * SROWS + r) * 256 + tid) * V));
+		for (int r = 0; r < SR; r++)
+			x[r] = __builtin_nontemporal_load((const vec_t *) (a.col_al + (((uint64_t) t * SR + r) * 256 + tid) * V));
 	} else {
 #pragma unroll
-		for (int r = 0; r < SROWS; r++) {
-			const uint64_t j0 = (((uint64_t) t * SROWS + r) * 256 + tid) * V;
+		for (int r = 0; r < SR; r++) {
+			const uint64_t j0 = (((uint64_t) t * SR + r) * 256 + tid) * V;
 			if (j0 < nslots)
 				x[r] = *(const vec_t *) (a.col_al + j0);
 		}
 	}
 	uint32_t cnt = 0;
 #pragma unroll
-	for (int r = 0; r < SROWS; r++) {
-		const uint64_t j0 = (((uint64_t) t * SROWS + r) * 256 + tid) * V;
+	for (int r = 0; r < SR; r++) {
+		const uint64_t j0 = (((uint64_t) t * SR + r) * 256 + tid) * V;
 		uint32_t m = 0;
 		if (full) {
 #pragma unroll
@@ -636,7 +641,7 @@ run_scan(const mgdk_bat *b, const Cand &ci, const SelPred<T> &pred)
 		a.col_al = start - mis;
 		a.shift = (uint32_t) mis;
 		a.cseq = ci.seq;
-		items_per_tile = (uint64_t) (MGDK_SEL_STREAM ? SROWS : sel_rows<false>()) * 256 * (16 / sizeof(T));
+		items_per_tile = (uint64_t) (MGDK_SEL_STREAM ? sel_srows<T>() : sel_rows<false>()) * 256 * (16 / sizeof(T));
 	} else {
 		uintptr_t mis = ((uintptr_t) ci.oids % 16) / sizeof(oid);
 		a.cand_al = ci.oids - mis;
