@@ -165,6 +165,19 @@ def main():
         assert r_op == gdk.q6_fused(*qargs)
         extra["q6_op_at_a_time"] = {"ms_per_step": round(op_ms, 3),
                                     "grows_per_s": round(rows / op_ms / 1e6, 2)}
+        # the Q1 MAL plan operator by operator (select, group/subgroup,
+        # projections, calc to hge, grouped sums / avg3 / count)
+        dmax = mkdate(1998, 9, 2)
+        q1_op = gdk.q1_fused(cols, dmax, fused=False)
+        t = time.perf_counter()
+        for _ in range(3):
+            q1_op = gdk.q1_fused(cols, dmax, fused=False)
+        op1_ms = (time.perf_counter() - t) / 3 * 1e3
+        key = lambda r: (r["returnflag"], r["linestatus"])
+        assert sorted((key(r), r["sum_charge"]) for r in q1_op) == \
+            sorted((key(r), r["sum_charge"]) for r in gdk.q1_fused(cols, dmax))
+        extra["q1_op_at_a_time"] = {"ms_per_step": round(op1_ms, 3),
+                                    "grows_per_s": round(rows / op1_ms / 1e6, 2)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

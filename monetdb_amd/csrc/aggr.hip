@@ -385,6 +385,115 @@ k_gaggr(const void *base, int w, oid off, const oid *gids, oid gseq, oid gmin, B
 		atomicMax(maxabs, mx);
 }
 
+// few groups (K <= 8): every per-group quantity in lane registers -- sums,
+// counts, first non-nil position, last nil position, min / max -- so the
+// loop has no global loads besides the gid and the value (U rows in flight
+// per lane); positions only grow along a lane, so "first" is the first one
+// seen and "last" the last one.  One flush of wave-reduced values per wave.
+template <int K, bool MM>
+__global__ __launch_bounds__(256) void
+k_gaggr_k(const void *base, int w, oid off, const oid *gids, oid gseq, oid gmin, BUN ngrp, BUN n, int what,
+	  bool count_all, GAcc acc, unsigned long long *maxabs)
+{
+	hge s[K];
+	unsigned long long c[K], fv[K], ln[K];
+	long long mn[K], mx[K];
+#pragma unroll
+	for (int k = 0; k < K; k++) {
+		s[k] = 0;
+		c[k] = 0;
+		fv[k] = ~0ull;
+		ln[k] = 0;
+		mn[k] = INT64_MAX;
+		mx[k] = INT64_MIN;
+	}
+	unsigned long long mxa = 0;
+	constexpr int U = 4;
+	const BUN stride = (BUN) gridDim.x * blockDim.x;
+	for (BUN i0 = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += stride * U) {
+		oid g[U];
+		hge v[U];
+		bool nil[U];
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const BUN i = i0 + (BUN) u * stride;
+			g[u] = i < n ? (gids ? gids[i] : gseq + i) : gmin + ngrp;
+			v[u] = i < n ? ldv(base, w, off + i, nil[u]) : (nil[u] = false, (hge) 0);
+		}
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const BUN i = i0 + (BUN) u * stride;
+			if (g[u] < gmin || g[u] - gmin >= ngrp)
+				continue;
+			const BUN gi = g[u] - gmin;
+			if (nil[u]) {
+#pragma unroll
+				for (int k = 0; k < K; k++) {
+					const bool m = gi == (BUN) k;
+					ln[k] = m ? i + 1 : ln[k];
+					c[k] += (m && count_all);
+				}
+				continue;
+			}
+			const unsigned long long a = absbits(v[u]);
+			mxa = a > mxa ? a : mxa;
+#pragma unroll
+			for (int k = 0; k < K; k++) {
+				const bool m = gi == (BUN) k;
+				s[k] += m ? v[u] : (hge) 0;
+				c[k] += m;
+				fv[k] = (m && fv[k] == ~0ull) ? i : fv[k];
+				if (MM) {
+					const long long x = (long long) v[u];
+					mn[k] = (m && x < mn[k]) ? x : mn[k];
+					mx[k] = (m && x > mx[k]) ? x : mx[k];
+				}
+			}
+		}
+	}
+#pragma unroll
+	for (int k = 0; k < K; k++) {
+		hge sk = s[k];
+		unsigned long long ck = c[k], fk = fv[k], lk = ln[k];
+		long long nk = mn[k], xk = mx[k];
+		for (int o = 32; o > 0; o >>= 1) {
+			const unsigned long long lo = __shfl_xor((unsigned long long) (uhge) sk, o);
+			const unsigned long long hi = __shfl_xor((unsigned long long) ((uhge) sk >> 64), o);
+			sk += (hge) (((uhge) hi << 64) | lo);
+			ck += __shfl_xor(ck, o);
+			const unsigned long long f2 = __shfl_xor(fk, o), l2 = __shfl_xor(lk, o);
+			fk = f2 < fk ? f2 : fk;
+			lk = l2 > lk ? l2 : lk;
+			if (MM) {
+				const long long n2 = __shfl_xor(nk, o), x2 = __shfl_xor(xk, o);
+				nk = n2 < nk ? n2 : nk;
+				xk = x2 > xk ? x2 : xk;
+			}
+		}
+		if (__lane_id() == 0 && (BUN) k < ngrp) {
+			if (ck) {
+				if (what & AGG_SUM)
+					atomic_add128(&acc.sum[2 * k], sk);
+				atomicAdd(&acc.cnt[k], ck);
+			}
+			if ((what & AGG_POS) && fk != ~0ull)
+				atomicMin(&acc.firstval[k], fk);
+			if ((what & AGG_POS) && lk)
+				atomicMax(&acc.lastnil[k], lk);
+			if (MM && (what & AGG_MINMAX) && fk != ~0ull) {
+				atomicMin(&acc.mn[k], nk);
+				atomicMax(&acc.mx[k], xk);
+			}
+		}
+	}
+	for (int o = 32; o > 0; o >>= 1) {
+		const unsigned long long t = __shfl_xor(mxa, o);
+		mxa = t > mxa ? t : mxa;
+	}
+	if (__lane_id() == 0 && mxa)
+		atomicMax(maxabs, mxa);
+}
+
 struct AggrInit {
 	Cand ci;
 	oid min, max;
@@ -501,12 +610,16 @@ run_gaggr(const AggrInit &a, mgdk_bat *b, int what, bool count_all, GRes &r)
 	const oid off = a.ci.seq - b->hseqbase;
 	dim3 g(grid_for(a.ci.n, 256 * 8, 256 * 16)), blk(256);
 	if (a.ci.n) {
+#define GK(K_) do { if (what & AGG_MINMAX) \
+		hipLaunchKernelGGL((k_gaggr_k<K_, true>), g, blk, 0, st, b->theap, b->twidth, off, a.gids, a.gseq, a.min, ng, a.ci.n, what, count_all, acc, maxabs); \
+	else \
+		hipLaunchKernelGGL((k_gaggr_k<K_, false>), g, blk, 0, st, b->theap, b->twidth, off, a.gids, a.gseq, a.min, ng, a.ci.n, what, count_all, acc, maxabs); } while (0)
 		if (ng <= 1)
-			hipLaunchKernelGGL((k_gaggr<1>), g, blk, 0, st, b->theap, b->twidth, off, a.gids, a.gseq, a.min, ng, a.ci.n, what, count_all, acc, maxabs);
+			GK(1);
 		else if (ng <= 4)
-			hipLaunchKernelGGL((k_gaggr<4>), g, blk, 0, st, b->theap, b->twidth, off, a.gids, a.gseq, a.min, ng, a.ci.n, what, count_all, acc, maxabs);
+			GK(4);
 		else if (ng <= 8)
-			hipLaunchKernelGGL((k_gaggr<8>), g, blk, 0, st, b->theap, b->twidth, off, a.gids, a.gseq, a.min, ng, a.ci.n, what, count_all, acc, maxabs);
+			GK(8);
 		else
 			hipLaunchKernelGGL((k_gaggr<0>), g, blk, 0, st, b->theap, b->twidth, off, a.gids, a.gseq, a.min, ng, a.ci.n, what, count_all, acc, maxabs);
 	}
