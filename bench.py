@@ -131,7 +131,7 @@ def main():
         barrier()
         t = time.perf_counter()
         for _ in range(5):
-            q1 = D.combine_q1(gdk.q1_fused(cols, dmax), dist, dev)
+            q1 = D.combine_q1(gdk.q1_fused(cols, dmax), dist, dev, rows_per_rank=rows, rank=rank)
         barrier()
         q1_s = time.perf_counter() - t
         if dist is not None:

@@ -96,7 +96,8 @@ def combine_q1(rows, dist=None, device="cpu", rows_per_rank=0, rank=0):
     for i in range(Q1_MAXG):
         if i < len(rows):
             r = rows[i]
-            flat += [r["returnflag"], r["linestatus"], r["first_row"], r["count_order"]]
+            # first rows are rank-local; the global row is rank * rows_per_rank + local
+            flat += [r["returnflag"], r["linestatus"], r["first_row"] + rank * rows_per_rank, r["count_order"]]
             for k in Q1_SUMS:
                 flat += _words(r[k])
         else:
