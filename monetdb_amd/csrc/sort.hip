@@ -27,7 +27,10 @@ using namespace mgdk;
 
 namespace {
 
-constexpr int SROWS = 16;                  // rows of 64 keys per wave
+#ifndef MGDK_SORT_ROWS
+#define MGDK_SORT_ROWS 32
+#endif
+constexpr int SROWS = MGDK_SORT_ROWS;      // rows of 64 keys per wave
 constexpr int STILE = 256 * SROWS;         // keys per tile
 
 template <typename K>
