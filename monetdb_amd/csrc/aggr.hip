@@ -205,6 +205,8 @@ mag_bound(unsigned long long cls)
 }  // namespace
 
 int mgdk_fsum(void *res, int tp, mgdk_bat *b, mgdk_bat *s, bool skip_nils, bool nil_if_empty);   // fsum.hip
+int mgdk_fgroupsum(const mgdk_bat *b, const Cand &ci, const oid *gids, oid gseq, oid gmin, BUN ngrp, bool skip_nils,
+		   int tp, void *res, bool *nils);                                                   // fsum.hip
 
 extern "C" int
 mgdk_BATsum(void *res, int tp, mgdk_bat *b, mgdk_bat *s, bool skip_nils, bool nil_if_empty)
@@ -671,6 +673,25 @@ extern "C" {
 mgdk_bat *
 mgdk_BATgroupsum(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils)
 {
+	if (b != nullptr && (b->ttype == MGDK_flt || b->ttype == MGDK_dbl)) {
+		// dofsum with groups (gdk_aggr.c:183), exact per group (fsum.hip)
+		ProfScope prof("groupsum");
+		AggrInit a;
+		if (aggr_init(&a, b, g, e, s) < 0)
+			return nullptr;
+		const BUN ng = a.ngrp;
+		std::vector<char> out(ng * 8 + 16);
+		bool nils = false;
+		if (ng && mgdk_fgroupsum(b, a.ci, a.gids, a.gseq, a.min, ng, skip_nils, tp, out.data(), &nils) < 0)
+			return nullptr;
+		mgdk_bat *bn = upload_new(ng ? a.min : 0, tp, out.data(), ng);
+		if (bn) {
+			bn->tkey = bn->tsorted = bn->trevsorted = ng <= 1;
+			bn->tnil = nils;
+			bn->tnonil = !nils;
+		}
+		return bn;
+	}
 	if (b == nullptr || !int_type(b->ttype) || !int_type(tp)) {
 		seterr("type combination (sum(%s)->%s) not supported.\n", b ? atomname(b->ttype) : "?", atomname(tp));
 		return nullptr;

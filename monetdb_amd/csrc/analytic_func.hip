@@ -417,6 +417,125 @@ k_frames_other_hge(FArgs a)
 		publish_or(&a.flags[2], hasnil);
 }
 
+// Fused general frames into a hge result: one workgroup per 2048-row tile
+// stages the values under the tile's frames -- [min s, max e), at most
+// FW_MAX rows -- in LDS, builds their exact prefix sums / non-nil counts
+// there and answers every row from LDS: the column is read about once and
+// no n-row prefix arrays are written or re-read.  A tile whose frames span
+// more (long or unbounded frames) raises flags[3]; the host then uses the
+// global-prefix path for the whole call.
+constexpr int FT_ROWS = 2048;
+constexpr int FW_MAX = 2560;
+constexpr int FW_PER = (FW_MAX + 255) / 256;   // staged values per lane
+
+template <typename T>
+__global__ __launch_bounds__(256) void
+k_frames_tile_hge(const T *b, BUN n, const oid *S, const oid *E, hge *out, uint32_t *flags)
+{
+	__shared__ hge sP[FW_MAX + 1];
+	__shared__ uint32_t sC[FW_MAX + 1];
+	__shared__ hge w_s[4];
+	__shared__ uint32_t w_c[4];
+	__shared__ unsigned long long s_lo, s_hi;
+	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+	const BUN t0 = (BUN) blockIdx.x * FT_ROWS;
+	constexpr int R = FT_ROWS / 256;
+	BUN lo[R], hi[R];
+	unsigned long long mn = ~0ull, mx = 0;
+#pragma unroll
+	for (int q = 0; q < R; q++) {
+		const BUN i = t0 + (BUN) q * 256 + tid;
+		lo[q] = hi[q] = 0;
+		if (i < n) {
+			lo[q] = S[i];
+			hi[q] = E[i];
+			if (hi[q] < lo[q])
+				hi[q] = lo[q];
+			mn = lo[q] < mn ? lo[q] : mn;
+			mx = hi[q] > mx ? hi[q] : mx;
+		}
+	}
+	if (tid == 0) {
+		s_lo = ~0ull;
+		s_hi = 0;
+	}
+	__syncthreads();
+	mn = block_reduce(mn, [](unsigned long long x, unsigned long long y) { return x < y ? x : y; });
+	if (tid == 0)
+		s_lo = mn;
+	mx = block_reduce(mx, [](unsigned long long x, unsigned long long y) { return x > y ? x : y; });
+	if (tid == 0)
+		s_hi = mx;
+	__syncthreads();
+	const BUN wlo = s_lo, whi = s_hi;
+	if (whi > wlo && whi - wlo > (BUN) FW_MAX) {
+		if (tid == 0)
+			publish_or(&flags[3], 1u);
+		return;
+	}
+	const int W = whi > wlo ? (int) (whi - wlo) : 0;
+	// thread tid stages the contiguous values [tid*FW_PER, ...) of the window
+	hge ls = 0;
+	uint32_t lc = 0;
+	int64_t v[FW_PER];
+	bool ok[FW_PER];
+#pragma unroll
+	for (int q = 0; q < FW_PER; q++) {
+		const int j = tid * FW_PER + q;
+		ok[q] = false;
+		v[q] = 0;
+		if (j < W) {
+			const T x = b[wlo + j];
+			ok[q] = !(x == NilOf<T>::v());
+			v[q] = ok[q] ? (int64_t) x : 0;
+		}
+		ls += v[q];
+		lc += ok[q];
+	}
+	const hge is = wave_scan128(ls);
+	const unsigned long long ic = wave_scan64(lc);
+	if (lane == 63) {
+		w_s[w] = is;
+		w_c[w] = (uint32_t) ic;
+	}
+	__syncthreads();
+	hge es = is - ls;
+	uint32_t ec = (uint32_t) ic - lc;
+	for (unsigned q = 0; q < w; q++) {
+		es += w_s[q];
+		ec += w_c[q];
+	}
+#pragma unroll
+	for (int q = 0; q < FW_PER; q++) {
+		const int j = tid * FW_PER + q;
+		if (j <= W) {
+			sP[j] = es;
+			sC[j] = ec;
+		}
+		es += v[q];
+		ec += ok[q];
+	}
+	if (tid == 255) {                // entry W (= FW_MAX: past every lane's range)
+		sP[W] = es;
+		sC[W] = ec;
+	}
+	__syncthreads();
+	uint32_t hasnil = 0;
+#pragma unroll
+	for (int q = 0; q < R; q++) {
+		const BUN i = t0 + (BUN) q * 256 + tid;
+		if (i < n) {
+			const int a0 = (int) (lo[q] - wlo), a1 = (int) (hi[q] - wlo);
+			const uint32_t c = sC[a1] - sC[a0];
+			out[i] = c ? sP[a1] - sP[a0] : NilOf<hge>::v();
+			hasnil |= c == 0;
+		}
+	}
+	hasnil = block_reduce(hasnil, [](uint32_t x, uint32_t y) { return x | y; });
+	if (tid == 0)
+		publish_or(&flags[2], hasnil);
+}
+
 __global__ void
 k_first(const oid *L, oid *out)
 {
@@ -494,6 +613,34 @@ run_frames(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk
 	if ((frame_type == 3 || frame_type == 4) && o == nullptr) {
 		seterr("analytic: the peer column o is required for this frame");
 		return -1;
+	}
+	// general frames into hge: the fused tile kernel when every tile's frames
+	// fit its LDS window
+	if (frames && !count && !lng_out && b->twidth <= 8 && basetype(b->ttype) != MGDK_flt &&
+	    basetype(b->ttype) != MGDK_dbl) {
+		DevBuf ff(64);
+		uint32_t *h = (uint32_t *) pinned(16);
+		if (!ff.p || !hip_ok(hipMemsetAsync(ff.p, 0, 64, st), "memset"))
+			return -1;
+		const dim3 g((unsigned) ((n + FT_ROWS - 1) / FT_ROWS)), blk(256);
+		const oid *S = (const oid *) s->theap, *E = (const oid *) e->theap;
+		hge *R = (hge *) r->theap;
+		switch (b->twidth) {
+		case 1: hipLaunchKernelGGL((k_frames_tile_hge<int8_t>), g, blk, 0, st, (const int8_t *) b->theap, n, S, E, R, ff.as<uint32_t>()); break;
+		case 2: hipLaunchKernelGGL((k_frames_tile_hge<int16_t>), g, blk, 0, st, (const int16_t *) b->theap, n, S, E, R, ff.as<uint32_t>()); break;
+		case 4: hipLaunchKernelGGL((k_frames_tile_hge<int32_t>), g, blk, 0, st, (const int32_t *) b->theap, n, S, E, R, ff.as<uint32_t>()); break;
+		default: hipLaunchKernelGGL((k_frames_tile_hge<int64_t>), g, blk, 0, st, (const int64_t *) b->theap, n, S, E, R, ff.as<uint32_t>()); break;
+		}
+		if (!hip_ok(hipMemcpyAsync(h, ff.p, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+			return -1;
+		if (h[3] == 0) {
+			r->count = n;
+			r->tnil = h[2] != 0;
+			r->tnonil = h[2] == 0;
+			r->tsorted = r->trevsorted = r->tkey = n <= 1;
+			return 0;
+		}
+		// some frame spans more than a tile's window: global prefix path below
 	}
 	// prefix sums / counts over the column
 	const bool need_prefix = !(count && count_all);

@@ -19,6 +19,7 @@
 // accumulator overflow, so it is reported as the reference's overflow
 // error.
 #include <cmath>
+#include <vector>
 
 #include "mgdk_internal.h"
 
@@ -462,4 +463,179 @@ mgdk_fsum(void *res, int tp, mgdk_bat *b, mgdk_bat *s, bool skip_nils, bool nil_
 	}
 	*(float *) res = nil ? __builtin_nanf("") : f;
 	return 0;
+}
+
+// ---- grouped: BATgroupsum of flt / dbl (dofsum with gids, gdk_aggr.c:183) --
+// Per group an exact fixed-point sum in 32-bit digits (weights 2^(32 d +
+// emin), int64 slots: 2^31 values of headroom), three signed chunks per
+// value; workgroup-private in LDS when the groups' digits fit, flushed with
+// one global atomic per non-zero digit, else global atomics directly.
+namespace {
+
+template <typename T, bool LDS>
+__global__ __launch_bounds__(256) void
+k_fgsum(const T *base, bool dense, oid off, const oid *oids, oid hseq, BUN n, const oid *gids, oid gseq, oid gmin,
+	BUN ngrp, int emin, int nd, long long *gdig, unsigned long long *gcnt, unsigned *gnil)
+{
+	extern __shared__ __attribute__((aligned(16))) long long sdig[];
+	long long *dig = gdig;
+	unsigned long long *cnt = gcnt;
+	unsigned *nil = gnil;
+	const BUN nslots = ngrp * (BUN) nd;
+	if (LDS) {
+		dig = sdig;
+		cnt = (unsigned long long *) (sdig + nslots);
+		nil = (unsigned *) (cnt + ngrp);
+		for (BUN q = threadIdx.x; q < nslots; q += blockDim.x)
+			dig[q] = 0;
+		for (BUN q = threadIdx.x; q < ngrp; q += blockDim.x) {
+			cnt[q] = 0;
+			nil[q] = 0;
+		}
+		__syncthreads();
+	}
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		const oid g = gids ? gids[i] : gseq + i;
+		if (g < gmin || g - gmin >= ngrp)
+			continue;
+		const BUN gi = g - gmin;
+		const T v = fval(base, dense, off, oids, hseq, i);
+		if (v != v) {
+			atomicOr(&nil[gi], 1u);
+			continue;
+		}
+		atomicAdd(&cnt[gi], 1ull);
+		bool neg;
+		uint64_t m;
+		int e;
+		if (isinf((double) v) || !fdecomp(v, neg, m, e))
+			continue;
+		const int pos = e - emin;
+		const int d = pos >> 5;
+		const uhge x = (uhge) m << (pos & 31);
+#pragma unroll
+		for (int k = 0; k < 3; k++) {
+			const long long c = (long long) (uint32_t) (x >> (32 * k));
+			if (c)
+				atomicAdd((unsigned long long *) &dig[gi * nd + d + k], (unsigned long long) (neg ? -c : c));
+		}
+	}
+	if (LDS) {
+		__syncthreads();
+		for (BUN q = threadIdx.x; q < nslots; q += blockDim.x)
+			if (dig[q])
+				atomicAdd((unsigned long long *) &gdig[q], (unsigned long long) dig[q]);
+		for (BUN q = threadIdx.x; q < ngrp; q += blockDim.x) {
+			if (cnt[q])
+				atomicAdd(&gcnt[q], cnt[q]);
+			if (nil[q])
+				atomicOr(&gnil[q], 1u);
+		}
+	}
+}
+
+template <typename T>
+int
+fgroupsum_typed(const mgdk_bat *b, const Cand &ci, const oid *gids, oid gseq, oid gmin, BUN ngrp, bool skip_nils,
+		int tp, void *res, bool *nils)
+{
+	hipStream_t st = stream();
+	FRange *r = (FRange *) meta_buf();
+	FRange init = {0, ~0ull, INT32_MAX, INT32_MIN, 0, 0};
+	if (!hip_ok(hipMemcpyAsync(r, &init, sizeof(init), hipMemcpyHostToDevice, st), "memcpy"))
+		return -1;
+	const oid off = ci.dense ? ci.seq - b->hseqbase : 0;
+	const T *base = (const T *) b->theap;
+	const unsigned grid = grid_for(ci.n, 256 * 16, 4096);
+	if (ci.n)
+		hipLaunchKernelGGL((k_fsum_range<T>), dim3(grid), dim3(256), 0, st, base, ci.dense, off, ci.oids,
+				   b->hseqbase, ci.n, r);
+	FRange *h = (FRange *) pinned(sizeof(FRange));
+	if (!hip_ok(hipMemcpyAsync(h, r, sizeof(FRange), hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+		return -1;
+	if (h->inf) {
+		seterr("22003!overflow in sum aggregate.\n");
+		return -1;
+	}
+	if (h->cnt >= ((unsigned long long) 1 << 31)) {
+		seterr("42000!BATgroupsum: more than 2^31 floating-point values are not supported on the device path");
+		return -1;
+	}
+	const int emin = h->etop == INT32_MIN ? 0 : h->emin;
+	const int nd = h->etop == INT32_MIN ? 4 : (h->etop - emin + 31) / 32 + 4;
+	const BUN nslots = ngrp * (BUN) nd;
+	DevBuf dig(nslots * 8 + 64), cnt(ngrp * 8 + 64), nilf(ngrp * 4 + 64);
+	if (!dig.p || !cnt.p || !nilf.p || !hip_ok(hipMemsetAsync(dig.p, 0, nslots * 8 + 64, st), "memset") ||
+	    !hip_ok(hipMemsetAsync(cnt.p, 0, ngrp * 8 + 64, st), "memset") ||
+	    !hip_ok(hipMemsetAsync(nilf.p, 0, ngrp * 4 + 64, st), "memset"))
+		return -1;
+	const size_t lds = nslots * 8 + ngrp * 12 + 16;
+	if (ci.n) {
+		if (lds <= 48 * 1024)
+			hipLaunchKernelGGL((k_fgsum<T, true>), dim3(grid), dim3(256), lds, st, base, ci.dense, off, ci.oids,
+					   b->hseqbase, ci.n, gids, gseq, gmin, ngrp, emin, nd, dig.as<long long>(),
+					   cnt.as<unsigned long long>(), nilf.as<unsigned>());
+		else
+			hipLaunchKernelGGL((k_fgsum<T, false>), dim3(grid), dim3(256), 0, st, base, ci.dense, off, ci.oids,
+					   b->hseqbase, ci.n, gids, gseq, gmin, ngrp, emin, nd, dig.as<long long>(),
+					   cnt.as<unsigned long long>(), nilf.as<unsigned>());
+	}
+	std::vector<long long> hd(nslots + 1);
+	std::vector<unsigned long long> hc(ngrp + 1);
+	std::vector<unsigned> hn(ngrp + 1);
+	if (!hip_ok(hipMemcpyAsync(hd.data(), dig.p, nslots * 8, hipMemcpyDeviceToHost, st), "memcpy") ||
+	    !hip_ok(hipMemcpyAsync(hc.data(), cnt.p, ngrp * 8, hipMemcpyDeviceToHost, st), "memcpy") ||
+	    !hip_ok(hipMemcpyAsync(hn.data(), nilf.p, ngrp * 4, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+		return -1;
+	*nils = false;
+	for (BUN k = 0; k < ngrp; k++) {
+		bool nil = (!skip_nils && hn[k]) || hc[k] == 0;      // dofsum :239-251, :304-312
+		double d = 0;
+		if (!nil) {
+			uint64_t limb[40] = {0};
+			const int nl = nd / 2 + 2;
+			hge carry = 0;
+			for (int q = 0; q < nl; q++) {
+				hge acc = carry;
+				for (int half = 0; half < 2; half++) {
+					const int j = 2 * q + half;
+					if (j < nd)
+						acc += (hge) hd[k * nd + j] << (32 * half);
+				}
+				limb[q] = (uint64_t) acc;
+				carry = acc >> 64;
+			}
+			if (!round_to_double(limb, nl, emin, &d)) {
+				seterr("22003!overflow in sum aggregate.\n");
+				return -1;
+			}
+		}
+		if (tp == MGDK_dbl) {
+			((double *) res)[k] = nil ? __builtin_nan("") : d;
+		} else {
+			const float f = (float) d;
+			if (!nil && std::isinf(f)) {
+				seterr("22003!overflow in sum aggregate.\n");
+				return -1;
+			}
+			((float *) res)[k] = nil ? __builtin_nanf("") : f;
+		}
+		*nils |= nil;
+	}
+	return 0;
+}
+
+}  // namespace
+
+// grouped float sums into res[0..ngrp) (called by mgdk_BATgroupsum, aggr.hip)
+int
+mgdk_fgroupsum(const mgdk_bat *b, const Cand &ci, const oid *gids, oid gseq, oid gmin, BUN ngrp, bool skip_nils,
+	       int tp, void *res, bool *nils)
+{
+	if (!(tp == MGDK_dbl || (tp == MGDK_flt && b->ttype == MGDK_flt))) {
+		seterr("type combination (sum(%s)->%s) not supported.\n", atomname(b->ttype), atomname(tp));
+		return -1;
+	}
+	return b->ttype == MGDK_flt ? fgroupsum_typed<float>(b, ci, gids, gseq, gmin, ngrp, skip_nils, tp, res, nils)
+				    : fgroupsum_typed<double>(b, ci, gids, gseq, gmin, ngrp, skip_nils, tp, res, nils);
 }

@@ -803,8 +803,10 @@ ora_samesign(double x, double y)
 	return (x >= 0) == (y >= 0);
 }
 
-static int
-ora_fsum(double *out, bool *isnil, const ora_bat *b, const ora_ci *ci, bool skip_nils, bool nil_if_empty)
+/* one group's values in input order (NaN = nil) */
+int ora_fsum_array(double *out, bool *isnil, const double *vals, uint64_t nv, bool skip_nils, bool nil_if_empty);
+int
+ora_fsum_array(double *out, bool *isnil, const double *vals, uint64_t nv, bool skip_nils, bool nil_if_empty)
 {
 	int npartials = 0, maxpartials = 2, infs = 0;
 	bool valseen = false;
@@ -813,9 +815,8 @@ ora_fsum(double *out, bool *isnil, const ora_bat *b, const ora_ci *ci, bool skip
 	volatile double lo, hi;
 	const double twopow = pow(2.0, 1023.0);
 	*isnil = false;
-	for (uint64_t k = 0; k < ci->n; k++) {
-		uint64_t p = ci_get(ci, k) - b->hseqbase;
-		x = b->type == ORA_flt ? (double) ((const float *) b->base)[p] : ((const double *) b->base)[p];
+	for (uint64_t k = 0; k < nv; k++) {
+		x = vals[k];
 		if (isnan(x)) {
 			if (!skip_nils) {
 				*isnil = true;
@@ -906,6 +907,19 @@ ora_fsum(double *out, bool *isnil, const ora_bat *b, const ora_ci *ci, bool skip
 	free(partials);
 	*out = hi;
 	return 0;
+}
+
+static int
+ora_fsum(double *out, bool *isnil, const ora_bat *b, const ora_ci *ci, bool skip_nils, bool nil_if_empty)
+{
+	double *vals = malloc((ci->n + 1) * sizeof(double));
+	for (uint64_t k = 0; k < ci->n; k++) {
+		uint64_t p = ci_get(ci, k) - b->hseqbase;
+		vals[k] = b->type == ORA_flt ? (double) ((const float *) b->base)[p] : ((const double *) b->base)[p];
+	}
+	int rc = ora_fsum_array(out, isnil, vals, ci->n, skip_nils, nil_if_empty);
+	free(vals);
+	return rc;
 }
 
 int

@@ -11,6 +11,7 @@
 
 void ora_seterr(const char *fmt, ...);
 int ora_width(int type);
+int ora_fsum_array(double *out, bool *isnil, const double *vals, uint64_t nv, bool skip_nils, bool nil_if_empty);
 ora_bat *ora_dense(ora_oid hseq, ora_oid tseq, uint64_t cnt);
 
 typedef struct {
@@ -276,6 +277,58 @@ ora_groupsum(const ora_bat *b, const ora_bat *g, const ora_bat *e,
 	aggr_ctx a;
 	if (aggr_init(&a, b, g, e, s) < 0)
 		return NULL;
+	if (b->type == ORA_flt || b->type == ORA_dbl) {
+		/* dofsum with groups (gdk_aggr.c:183-427): msum per group over its
+		 * values in candidate order; a nil makes the group nil unless
+		 * skip_nils, an empty group is nil */
+		ora_bat *bn = ora_new(tp, a.ngrp, a.ngrp ? a.min : 0);
+		uint64_t *cnt = calloc(a.ngrp + 1, sizeof(uint64_t)), *pos = calloc(a.ngrp + 1, sizeof(uint64_t));
+		double *vals = malloc((a.ci.n + 1) * sizeof(double));
+		ora_oid *gof = malloc((a.ci.n + 1) * sizeof(ora_oid));
+		for (uint64_t i = 0; i < a.ci.n; i++) {
+			ora_oid gid = 0;
+			if (a.ngrp != 1 && !aggr_gid(&a, i, &gid)) {
+				gof[i] = ORA_OID_NIL;
+				continue;
+			}
+			gof[i] = gid;
+			cnt[gid]++;
+		}
+		uint64_t acc = 0;
+		for (uint64_t k = 0; k < a.ngrp; k++) {
+			pos[k] = acc;
+			acc += cnt[k];
+		}
+		for (uint64_t i = 0; i < a.ci.n; i++) {
+			if (gof[i] == ORA_OID_NIL)
+				continue;
+			uint64_t p = ci_get(&a.ci, i) - b->hseqbase;
+			vals[pos[gof[i]]++] = b->type == ORA_flt ? (double) ((const float *) b->base)[p]
+								  : ((const double *) b->base)[p];
+		}
+		int rc = 0;
+		for (uint64_t k = 0; k < a.ngrp && rc == 0; k++) {
+			double d;
+			bool isnil;
+			rc = ora_fsum_array(&d, &isnil, vals + pos[k] - cnt[k], cnt[k], skip_nils, true);
+			if (tp == ORA_dbl) {
+				((double *) bn->base)[k] = isnil ? nan("") : d;
+			} else {
+				float f = (float) d;
+				if (!isnil && isinf(f)) {
+					ora_seterr("22003!overflow in sum aggregate.\n");
+					rc = -1;
+				}
+				((float *) bn->base)[k] = isnil ? nanf("") : f;
+			}
+		}
+		free(cnt); free(pos); free(vals); free(gof);
+		if (rc < 0) {
+			ora_free(bn);
+			return NULL;
+		}
+		return bn;
+	}
 	ora_bat *bn = ora_new(tp, a.ngrp, a.ngrp ? a.min : 0);
 	ora_hge *acc = calloc(a.ngrp + 1, sizeof(ora_hge));
 	uint8_t *st = calloc(a.ngrp + 1, 1);    /* 0 unseen, 1 value, 2 nil */

@@ -132,3 +132,21 @@ def test_window_frames_sqltest(gdk):
         lambda b, p, o, ign, f: gdk.GDKanalyticalcount(b, p, o, None, None, ign, f).to_numpy(),
         lambda tp, a: gdk.BAT.from_numpy(tp, a), gdk.TYPE_int, gdk.TYPE_bit, gdk.TYPE_lng)
     assert not bad, bad
+
+
+@pytest.mark.parametrize("limit", [0, 40, 3000, 10**9])
+@pytest.mark.parametrize("tname", ["int", "lng"])
+def test_analytical_sum_general_frames_hge(gdk, ora, limit, tname):
+    """RANGE frames [s, e) into hge: short frames take the fused tile kernel
+    (values staged in LDS), frames longer than a tile's window fall back to
+    the global prefix path; both equal the oracle, nils included."""
+    r = rng(304)
+    v, p, o, ob = _data(r, nparts=40, plen=4000, tname=tname)
+    s, e = _bounds(gdk, ob, p, limit)
+    tp1 = getattr(gdk, "TYPE_" + tname)
+    got = gdk.GDKanalyticalsum(gdk.BAT.from_numpy(tp1, v), gdk.BAT.from_numpy(gdk.TYPE_bit, p), None, s, e,
+                               gdk.TYPE_hge, 1).values()
+    want = ora.analyticalsum(ora.Bat.from_array(tp1, v), ora.Bat.from_array(ora.TYPE_bit, p), None,
+                             ora.Bat.from_array(ora.TYPE_oid, s.to_numpy()),
+                             ora.Bat.from_array(ora.TYPE_oid, e.to_numpy()), ora.TYPE_hge, 1).values()
+    assert list(got) == list(want)
