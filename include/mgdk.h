@@ -110,6 +110,10 @@ mgdk_bat *mgdk_BATcalccstmul(const void *v, int vt, mgdk_bat *b, mgdk_bat *s, in
 int mgdk_BATsum(void *res, int tp, mgdk_bat *b, mgdk_bat *s, bool skip_nils, bool nil_if_empty);
 mgdk_bat *mgdk_BATgroupsum(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils);
 mgdk_bat *mgdk_BATgroupcount(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils);
+/* BATgroupavg (gdk_calc.h:129, gdk_aggr.c:1801): dbl averages; tp must be
+ * MGDK_dbl; cntsp may be NULL; scale divides by 10^scale */
+int mgdk_BATgroupavg(mgdk_bat **bnp, mgdk_bat **cntsp, mgdk_bat *b, mgdk_bat *g, mgdk_bat *e,
+		     mgdk_bat *s, int tp, bool skip_nils, int scale);
 int mgdk_BATgroupavg3(mgdk_bat **avgp, mgdk_bat **remp, mgdk_bat **cntp,
 		      mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, bool skip_nils);
 mgdk_bat *mgdk_BATgroupmin(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils);

@@ -665,6 +665,133 @@ put_vec(std::vector<char> &buf, int tp, BUN k, hge v, bool nil)
 	put_res(buf.data() + k * width_of(tp), tp, v, nil);
 }
 
+
+// ---- BATgroupavg (gdk/gdk_aggr.c:1801) ----------------------------------
+
+// 128-bit integer -> double, round to nearest even: the top 64 significant
+// bits with a sticky bit below them convert exactly like the full value
+__device__ __forceinline__ double
+hge_to_dbl(hge v)
+{
+	if (v >= (hge) INT64_MIN && v <= (hge) INT64_MAX)
+		return (double) (long long) v;
+	const bool neg = v < 0;
+	const uhge u = neg ? (uhge) 0 - (uhge) v : (uhge) v;
+	const unsigned long long hi = (unsigned long long) (u >> 64);
+	const int shift = 64 - __builtin_clzll(hi);                 // 1..64
+	unsigned long long top = (unsigned long long) (u >> shift);
+	if (u & (((uhge) 1 << shift) - 1))
+		top |= 1;
+	const double d = ldexp((double) top, shift);
+	return neg ? -d : d;
+}
+
+// singleton groups: BATconvert(b, s, TYPE_dbl) (gdk_calc_convert.c:1415)
+__global__ void
+k_to_dbl(const void *base, int tp, int w, oid off, BUN n, double *out)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		double d;
+		if (tp == MGDK_flt) {
+			d = (double) ((const float *) base)[off + i];
+		} else if (tp == MGDK_dbl) {
+			d = ((const double *) base)[off + i];
+		} else {
+			bool nil;
+			const hge v = ldv(base, w, off + i, nil);
+			d = nil ? __builtin_nan("") : hge_to_dbl(v);
+		}
+		out[i] = d;
+	}
+}
+
+constexpr BUN AVG_LDS_BINS = 8192;
+
+// group key of each candidate row for the stable counting sort: gid - min,
+// or ngrp for rows whose group is out of range (sorted behind every group)
+__global__ __launch_bounds__(256) void
+k_avg_keys(const oid *gids, oid gseq, oid gmin, BUN ngrp, BUN n, uint32_t *key, uint32_t *cnt)
+{
+	// block-private counts in LDS when the groups fit (AVG_LDS_BINS)
+	extern __shared__ uint32_t s_cnt[];
+	const bool lds = ngrp < AVG_LDS_BINS;
+	if (lds)
+		for (BUN k = threadIdx.x; k <= ngrp; k += blockDim.x)
+			s_cnt[k] = 0;
+	__syncthreads();
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		const oid g = gids ? gids[i] : gseq + i;
+		const uint32_t k = (g < gmin || g - gmin >= ngrp) ? (uint32_t) ngrp : (uint32_t) (g - gmin);
+		key[i] = k;
+		atomicAdd(lds ? &s_cnt[k] : &cnt[k], 1u);
+	}
+	if (lds) {
+		__syncthreads();
+		for (BUN k = threadIdx.x; k <= ngrp; k += blockDim.x)
+			if (s_cnt[k])
+				atomicAdd(&cnt[k], s_cnt[k]);
+	}
+}
+
+// AVERAGE_ITER_FLOAT (gdk_calc_private.h:277-289) is order dependent and
+// not associative: one lane replays one group's rows in candidate order
+// (perm: rows grouped by the stable sort; NULL with one group: every row,
+// range-checked through gids).  Eight values are loaded ahead of the
+// dependent divisions.
+template <typename T>
+__global__ void
+k_favg_replay(const T *vals, oid off, const uint32_t *perm, const uint64_t *start, const oid *gids, oid gseq,
+	      oid gmin, BUN ngrp, BUN n, bool skip_nils, double fac, double *out, long long *cnt)
+{
+	const BUN k = (BUN) blockIdx.x * blockDim.x + threadIdx.x;
+	if (k >= ngrp)
+		return;
+	const BUN j0 = start ? start[k] : 0, j1 = start ? start[k + 1] : n;
+	double a = 0;
+	long long c = 0;
+	bool nil = false;
+	constexpr int U = 8;
+	for (BUN j = j0; j < j1 && !nil; j += U) {
+		double x[U];
+		bool ok[U];
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const BUN jj = j + u;
+			ok[u] = jj < j1;
+			BUN r = 0;
+			if (ok[u]) {
+				r = perm ? perm[jj] : jj;
+				if (!perm) {
+					const oid g = gids ? gids[r] : gseq + r;
+					ok[u] = g >= gmin && g - gmin < ngrp;
+				}
+			}
+			x[u] = ok[u] ? (double) vals[off + r] : 0.0;
+		}
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			if (!ok[u] || nil)
+				continue;
+			if (__builtin_isnan(x[u])) {
+				nil = !skip_nils;
+				continue;
+			}
+			const double nn = (double) ++c;
+			if ((a > 0) == (x[u] > 0))
+				a += (x[u] - a) / nn;
+			else
+				a = a - a / nn + x[u] / nn;
+		}
+	}
+	if (nil || c == 0) {
+		out[k] = __builtin_nan("");
+		cnt[k] = 0;
+	} else {
+		out[k] = fac != 1.0 ? a / fac : a;
+		cnt[k] = c;
+	}
+}
+
 }  // namespace
 
 extern "C" {
@@ -768,6 +895,198 @@ mgdk_BATgroupcount(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, b
 	if (bn)
 		bn->tnonil = 1;
 	return bn;
+}
+
+// BATgroupavg (gdk/gdk_aggr.c:1801-1984): trivial cases :1834-1873,
+// integers AGGR_AVG (:1717) as the exact floor average and remainder of the
+// group's 128-bit sum, flt/dbl AGGR_AVG_FLOAT (:1753) replayed per group
+int
+mgdk_BATgroupavg(mgdk_bat **bnp, mgdk_bat **cntsp, mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp,
+		 bool skip_nils, int scale)
+{
+	if (cntsp)
+		*cntsp = nullptr;
+	if (tp != MGDK_dbl) {
+		seterr("42000!BATgroupavg: result type must be dbl\n");
+		return -1;
+	}
+	if (b == nullptr) {
+		seterr("b and g must be aligned\n");
+		return -1;
+	}
+	const int bt = b->ttype;
+	const bool isf = bt == MGDK_flt || bt == MGDK_dbl;
+	if (!isf && bt != MGDK_bte && bt != MGDK_sht && bt != MGDK_int && bt != MGDK_lng && bt != MGDK_hge) {
+		seterr("type (%s) not supported.\n", atomname(bt));
+		return -1;
+	}
+	ProfScope prof("groupavg");
+	AggrInit a;
+	if (aggr_init(&a, b, g, e, s) < 0)
+		return -1;
+	const BUN ng = a.ngrp;
+	const oid hb = ng ? a.min : 0;
+	hipStream_t st = stream();
+	auto constant_lng = [&](long long v) -> mgdk_bat * {
+		std::vector<long long> c(ng + 1, v);
+		mgdk_bat *cn = upload_new(hb, MGDK_lng, c.data(), ng);
+		if (cn) {
+			cn->tnonil = 1;
+			cn->tkey = cn->tsorted = cn->trevsorted = ng <= 1;
+		}
+		return cn;
+	};
+	if (a.ci.n == 0 || ng == 0) {
+		std::vector<double> d(ng + 1, __builtin_nan(""));
+		mgdk_bat *bn = upload_new(hb, MGDK_dbl, d.data(), ng);
+		mgdk_bat *cn = cntsp ? constant_lng(0) : nullptr;
+		if (!bn || (cntsp && !cn)) {
+			mgdk_BBPunfix(bn);
+			mgdk_BBPunfix(cn);
+			return -1;
+		}
+		bn->tnil = ng > 0;
+		bn->tnonil = ng == 0;
+		*bnp = bn;
+		if (cntsp)
+			*cntsp = cn;
+		return 0;
+	}
+	const bool gdense = g->tseqbase != MGDK_OID_NIL;
+	const oid off = a.ci.seq - b->hseqbase;
+	if ((!skip_nils || cntsp == nullptr || b->tnonil) &&
+	    (e == nullptr || (e->count == a.ci.n && e->hseqbase == b->hseqbase)) && (gdense || (g->tkey && g->tnonil))) {
+		mgdk_bat *bn = newbat(s ? s->hseqbase : b->hseqbase, MGDK_dbl, a.ci.n);
+		mgdk_bat *cn = cntsp ? constant_lng(1) : nullptr;
+		if (!bn || (cntsp && !cn)) {
+			mgdk_BBPunfix(bn);
+			mgdk_BBPunfix(cn);
+			return -1;
+		}
+		hipLaunchKernelGGL(k_to_dbl, dim3(grid_for(a.ci.n, 1024, 8192)), dim3(256), 0, st, b->theap, bt, b->twidth,
+				   off, a.ci.n, (double *) bn->theap);
+		if (!sync()) {
+			mgdk_BBPunfix(bn);
+			mgdk_BBPunfix(cn);
+			return -1;
+		}
+		bn->count = a.ci.n;
+		*bnp = bn;
+		if (cntsp)
+			*cntsp = cn;
+		return 0;
+	}
+	const double fac = scale != 0 ? pow(10.0, (double) scale) : 1.0;
+	mgdk_bat *bn = nullptr, *cn = nullptr;
+	bool nils = false;
+	if (isf) {
+		if (a.ci.n >= 0xffffffffull || ng >= 0xffffffffull) {
+			seterr("42000!BATgroupavg: more than 2^32-1 rows on the device path\n");
+			return -1;
+		}
+		bn = newbat(hb, MGDK_dbl, ng);
+		cn = newbat(hb, MGDK_lng, ng);
+		DevBuf key(a.ci.n * 4 + 4), key2(a.ci.n * 4 + 4), v0(a.ci.n * 4 + 4), v1(a.ci.n * 4 + 4),
+			cnt((ng + 1) * 4), start((ng + 1) * 8);
+		if (!bn || !cn || !key.p || !key2.p || !v0.p || !v1.p || !cnt.p || !start.p) {
+			mgdk_BBPunfix(bn);
+			mgdk_BBPunfix(cn);
+			return -1;
+		}
+		const uint32_t *perm = nullptr;
+		const uint64_t *sp = nullptr;
+		bool ok = true;
+		if (ng > 1) {
+			ok = hip_ok(hipMemsetAsync(cnt.p, 0, (ng + 1) * 4, st), "memset");
+			if (ok) {
+				hipLaunchKernelGGL(k_avg_keys, dim3(grid_for(a.ci.n, 2048, 1024)), dim3(256),
+						   ng < AVG_LDS_BINS ? (ng + 1) * 4 : 0, st, a.gids,
+						   a.gseq, a.min, ng, a.ci.n, key.as<uint32_t>(), cnt.as<uint32_t>());
+				int bits = 0;
+				while (bits < 32 && (ng >> bits))
+					bits++;
+				uint32_t *pm = nullptr;
+				ok = exclusive_scan(cnt.as<uint32_t>(), start.as<uint64_t>(), ng + 1, nullptr) == 0 &&
+				     radix_sort_positions32(key.as<uint32_t>(), v0.as<uint32_t>(), key2.as<uint32_t>(),
+							    v1.as<uint32_t>(), a.ci.n, bits, &pm) == 0;
+				perm = pm;     // NULL: identity, rows already in group order
+				sp = start.as<uint64_t>();
+			}
+		}
+		if (ok) {
+			const dim3 grid((unsigned) ((ng + 63) / 64)), blk(64);
+			if (bt == MGDK_flt)
+				hipLaunchKernelGGL((k_favg_replay<float>), grid, blk, 0, st, (const float *) b->theap, off, perm,
+						   sp, a.gids, a.gseq, a.min, ng, a.ci.n, skip_nils, fac, (double *) bn->theap,
+						   (long long *) cn->theap);
+			else
+				hipLaunchKernelGGL((k_favg_replay<double>), grid, blk, 0, st, (const double *) b->theap, off,
+						   perm, sp, a.gids, a.gseq, a.min, ng, a.ci.n, skip_nils, fac,
+						   (double *) bn->theap, (long long *) cn->theap);
+			ok = sync();
+		}
+		if (!ok) {
+			mgdk_BBPunfix(bn);
+			mgdk_BBPunfix(cn);
+			return -1;
+		}
+		bn->count = cn->count = ng;
+		std::vector<long long> hc(ng);
+		if (!hip_ok(hipMemcpy(hc.data(), cn->theap, ng * 8, hipMemcpyDeviceToHost), "memcpy")) {
+			mgdk_BBPunfix(bn);
+			mgdk_BBPunfix(cn);
+			return -1;
+		}
+		for (BUN k = 0; k < ng; k++)
+			nils |= hc[k] == 0;
+	} else {
+		GRes r;
+		if (run_gaggr(a, b, AGG_SUM | AGG_POS, false, r) < 0)
+			return -1;
+		std::vector<double> d(ng + 1);
+		std::vector<long long> c(ng + 1);
+		for (BUN k = 0; k < ng; k++) {
+			const unsigned long long n = r.cnt[k];
+			if (n == 0 || (!skip_nils && r.lastnil[k] != 0)) {
+				d[k] = __builtin_nan("");
+				c[k] = 0;
+				nils = true;
+				continue;
+			}
+			if (bt == MGDK_hge && mag_bound(r.maxabs) * (long double) n >= ldexpl(1.0L, 127)) {
+				seterr("42000!BATgroupavg: hge group sum exceeds the 128-bit device accumulator\n");
+				return -1;
+			}
+			// AVERAGE_ITER's invariant: avg * n + rem == sum, 0 <= rem < n
+			hge q = r.sum[k] / (hge) n, m = r.sum[k] % (hge) n;
+			if (m < 0) {
+				q -= 1;
+				m += (hge) n;
+			}
+			d[k] = (double) q + (double) (long long) m / (double) (long long) n;
+			if (scale != 0)
+				d[k] /= fac;
+			c[k] = (long long) n;
+		}
+		bn = upload_new(hb, MGDK_dbl, d.data(), ng);
+		cn = upload_new(hb, MGDK_lng, c.data(), ng);
+		if (!bn || !cn) {
+			mgdk_BBPunfix(bn);
+			mgdk_BBPunfix(cn);
+			return -1;
+		}
+	}
+	bn->tkey = bn->tsorted = bn->trevsorted = ng <= 1;
+	bn->tnil = nils;
+	bn->tnonil = !nils;
+	cn->tkey = cn->tsorted = cn->trevsorted = ng <= 1;
+	cn->tnonil = 1;
+	*bnp = bn;
+	if (cntsp)
+		*cntsp = cn;
+	else
+		mgdk_BBPunfix(cn);
+	return 0;
 }
 
 // BATgroupavg3 (gdk/gdk_aggr.c:1996-2110)

@@ -95,6 +95,7 @@ _SIGS = {
     "mgdk_BATsum": (C.c_int, [C.c_void_p, C.c_int, P, P, C.c_bool, C.c_bool]),
     "mgdk_BATgroupsum": (P, [P, P, P, P, C.c_int, C.c_bool]),
     "mgdk_BATgroupcount": (P, [P, P, P, P, C.c_int, C.c_bool]),
+    "mgdk_BATgroupavg": (C.c_int, [PP, PP, P, P, P, P, C.c_int, C.c_bool, C.c_int]),
     "mgdk_BATgroupavg3": (C.c_int, [PP, PP, PP, P, P, P, P, C.c_bool]),
     "mgdk_BATgroupmin": (P, [P, P, P, P, C.c_int, C.c_bool]),
     "mgdk_BATgroupmax": (P, [P, P, P, P, C.c_int, C.c_bool]),
@@ -397,6 +398,15 @@ def BATgroupmin(b, g, e, skip_nils=True, s=None):
 
 def BATgroupmax(b, g, e, skip_nils=True, s=None):
     return BAT(lib().mgdk_BATgroupmax(b.ptr, g.ptr, _p(e), _p(s), b.ttype, skip_nils))
+
+
+def BATgroupavg(b, g, e, skip_nils=True, s=None, scale=0, want_counts=True):
+    """BATgroupavg(&bn, &cnts, b, g, e, s, TYPE_dbl, skip_nils, scale)
+    (gdk/gdk_aggr.c:1801); returns (averages, counts or None)."""
+    a, c = P(), P()
+    _chk(lib().mgdk_BATgroupavg(C.byref(a), C.byref(c) if want_counts else None, b.ptr, g.ptr, _p(e),
+                                _p(s), TYPE_dbl, skip_nils, scale))
+    return BAT(a), (BAT(c) if want_counts else None)
 
 
 def BATgroupavg3(b, g, e, skip_nils=True, s=None):

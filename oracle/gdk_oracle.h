@@ -15,13 +15,14 @@
  *   calc        gdk/gdk_calc_addsub.c, gdk/gdk_calc_mul.c:23-132,2020-2092,
  *               overflow rules gdk/gdk_calc_private.h:38-140
  *   aggregates  gdk/gdk_aggr.c:65 (BATgroupaggrinit), :708 (dosum), :900, :1018,
- *               :1996 (BATgroupavg3), :3069 (BATgroupcount), AVERAGE_ITER
+ *               :1801 (BATgroupavg), :1996 (BATgroupavg3), :3069 (BATgroupcount), AVERAGE_ITER
  *               gdk/gdk_calc_private.h:231-275
  *   group       gdk/gdk_group.c:657-1347 (first-occurrence numbering)
  *   join        gdk/gdk_join.c:2781-2900 (hash join result order)
  *   sort        gdk/gdk_batop.c:2266-2342, gdk/gdk_rsort.c:21 (stable)
  *   window      gdk/gdk_analytic_bounds.c:273-387, :994, :1440
- *   frames      gdk/gdk_analytic_func.c:1626 (count), :1959 (sum), segment
+ *   frames      gdk/gdk_analytic_func.c:1626 (count), :1959 (sum),
+ *               gdk/gdk_analytic_statistics.c:364 (avg), segment
  *               tree gdk/gdk_analytic.h:52-130
  *   firstn      gdk/gdk_firstn.c:71-97 (heap), :211-1020, :1280
  *
@@ -90,6 +91,8 @@ ora_bat *ora_groupcount(const ora_bat *b, const ora_bat *g, const ora_bat *e,
 int ora_groupavg3(ora_bat **avgp, ora_bat **remp, ora_bat **cntp,
 		  const ora_bat *b, const ora_bat *g, const ora_bat *e,
 		  const ora_bat *s, bool skip_nils);
+int ora_groupavg(ora_bat **bnp, ora_bat **cntp, const ora_bat *b, const ora_bat *g,
+		 const ora_bat *e, const ora_bat *s, bool skip_nils, int scale);
 ora_bat *ora_groupminmax(const ora_bat *b, const ora_bat *g, const ora_bat *e,
 			 const ora_bat *s, bool skip_nils, bool domax);
 int ora_join(ora_bat **r1p, ora_bat **r2p, const ora_bat *l, const ora_bat *r,
@@ -135,6 +138,8 @@ int ora_q1(const ora_lineitem *li, int nthreads, ora_q1row *rows, int *nrows);
  * caller-allocated with count(b) slots of the result type */
 int ora_analyticalsum(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_bat *b,
 		      const ora_bat *s, const ora_bat *e, int tp1, int tp2, int frame_type);
+int ora_analyticalavg(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_bat *b,
+		      const ora_bat *s, const ora_bat *e, int tpe, int frame_type);
 int ora_analyticalcount(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_bat *b,
 			const ora_bat *s, const ora_bat *e, bool ignore_nils, int frame_type);
 

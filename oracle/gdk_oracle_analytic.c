@@ -16,6 +16,7 @@
  * starts one); peers: o[i] != 0 starts a new peer group (ORDER BY value
  * change) -- the reference's np / op arrays.
  */
+#include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -342,5 +343,312 @@ ora_analyticalcount(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_ba
 		}
 	}
 	r->count = cnt;
+	return 0;
+}
+
+/* ---------------------------------------------------------------------- */
+/* GDKanalyticalavg (gdk/gdk_analytic_statistics.c:364-423).
+ * Integers (bte..lng): the running frames (3, 4, 5) divide the exact 128-bit
+ * sum by the count, (dbl) sum / n (ANALYTICAL_AVG_IMP_NUM_* :29-165; the
+ * AVERAGE_ITER overflow branch is unreachable below hge); the current row is
+ * (dbl) v; general frames walk a fanout-16 segment tree whose nodes are
+ * avg_num_deltas {a, n, rr} and whose combine step feeds each non-empty
+ * child's a into AVERAGE_ITER (:167-199) -- so an inner node counts its
+ * children, not its rows, and the result is a + (dbl) rr / n.
+ * flt/dbl: AVERAGE_ITER_FLOAT in the input type (TPE a, :201-316); frame 4
+ * never assigns its result, so every row is nil there (:224-246). */
+
+typedef struct {
+	int64_t a, n, rr;   /* integers */
+	double d;           /* dbl */
+	float f;            /* flt */
+} anode;
+
+/* AVERAGE_ITER (gdk/gdk_calc_private.h:231-275) in 64-bit arithmetic; for
+ * TYPE bte..lng no intermediate leaves TYPE's range */
+static void
+avg_iter_i(int64_t x, anode *c)
+{
+	const int64_t n = ++c->n;
+	int64_t an = c->a / n, xn = x / n, z1 = xn - an;
+	xn = x - xn * n;
+	an = c->a - an * n;
+	uint64_t z2;
+	if (xn >= an) {
+		z2 = (uint64_t) (xn - an);
+		while (z2 >= (uint64_t) n) {
+			z2 -= (uint64_t) n;
+			z1++;
+		}
+	} else {
+		z2 = (uint64_t) (an - xn);
+		for (;;) {
+			z1--;
+			if (z2 < (uint64_t) n) {
+				z2 = (uint64_t) n - z2;
+				break;
+			}
+			z2 -= (uint64_t) n;
+		}
+	}
+	c->a += z1;
+	c->rr += (int64_t) z2;
+	if (c->rr >= n) {
+		c->rr -= n;
+		c->a++;
+	}
+}
+
+/* AVERAGE_ITER_FLOAT (gdk_calc_private.h:277-289) in TPE arithmetic */
+static void
+avg_iter_f(float x, anode *c)
+{
+	c->n++;
+	const float n = (float) c->n;
+	if ((c->f > 0) == (x > 0))
+		c->f += (x - c->f) / n;
+	else
+		c->f = c->f - c->f / n + x / n;
+}
+
+static void
+avg_iter_d(double x, anode *c)
+{
+	c->n++;
+	const double n = (double) c->n;
+	if ((c->d > 0) == (x > 0))
+		c->d += (x - c->d) / n;
+	else
+		c->d = c->d - c->d / n + x / n;
+}
+
+/* fold a node into an accumulator (COMPUTE_LEVELN_AVG_NUM / _FP) */
+static void
+avg_fold(int tp, anode *acc, const anode *v)
+{
+	if (v->n == 0)
+		return;
+	if (tp == ORA_flt)
+		avg_iter_f(v->f, acc);
+	else if (tp == ORA_dbl)
+		avg_iter_d(v->d, acc);
+	else
+		avg_iter_i(v->a, acc);
+}
+
+static double
+avg_final(int tp, const anode *c, bool *has_nils)
+{
+	if (c->n == 0) {
+		*has_nils = true;
+		return nan("");
+	}
+	if (tp == ORA_flt)
+		return (double) c->f;
+	if (tp == ORA_dbl)
+		return c->d;
+	return (double) c->a + (double) c->rr / (double) c->n;
+}
+
+int
+ora_analyticalavg(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_bat *b, const ora_bat *s,
+		  const ora_bat *e, int tpe, int frame_type)
+{
+	const int tp = b->type;
+	if (!(tp == ORA_bte || tp == ORA_sht || tp == ORA_int || tp == ORA_lng || tp == ORA_flt || tp == ORA_dbl)) {
+		ora_seterr("42000!average of type %d to dbl unsupported.\n", tpe);
+		return -1;
+	}
+	const bool isf = tp == ORA_flt || tp == ORA_dbl;
+	const uint64_t cnt = b->count;
+	double *rb = r->base;
+	const ora_oid *start = s ? s->base : NULL, *end = e ? e->base : NULL;
+	bool has_nils = false;
+	anode *lv0 = calloc(cnt + 1, sizeof(anode));
+	if (!lv0)
+		return -1;
+	/* level-0 nodes: {v, 1} or {0} for nil (COMPUTE_LEVEL0_AVG_*) */
+	for (uint64_t i = 0; i < cnt; i++) {
+		if (isnil_any(b, i))
+			continue;
+		lv0[i].n = 1;
+		if (tp == ORA_flt)
+			lv0[i].f = ((const float *) b->base)[i];
+		else if (tp == ORA_dbl)
+			lv0[i].d = ((const double *) b->base)[i];
+		else {
+			ora_hge v;
+			ival(b, i, &v);
+			lv0[i].a = (int64_t) v;
+		}
+	}
+	uint64_t k = 0;
+	for (uint64_t i = 1; i <= cnt; i++) {
+		if (i < cnt && !bit_at(p, i))
+			continue;
+		/* partition [k, i) */
+		switch (frame_type) {
+		case 3:
+			if (isf) {
+				anode c = {0};
+				double cur = nan("");
+				while (k < i) {
+					uint64_t j = k;
+					do {
+						avg_fold(tp, &c, &lv0[k]);
+						k++;
+					} while (k < i && !bit_at(o, k));
+					if (c.n > 0)
+						cur = tp == ORA_flt ? (double) c.f : c.d;
+					else
+						has_nils = true;
+					for (; j < k; j++)
+						rb[j] = cur;
+				}
+			} else {
+				ora_hge sum = 0;
+				int64_t n = 0;
+				while (k < i) {
+					uint64_t j = k;
+					do {
+						if (lv0[k].n) {
+							sum += lv0[k].a;
+							n++;
+						}
+						k++;
+					} while (k < i && !bit_at(o, k));
+					double cur = n > 0 ? (double) sum / (double) n : nan("");
+					for (; j < k; j++)
+						rb[j] = cur;
+					has_nils |= n == 0;
+				}
+			}
+			break;
+		case 4: {
+			ora_hge sum = 0;
+			int64_t n = 0;
+			uint64_t l = i - 1;
+			for (uint64_t j = l;; j--) {
+				if (!isf && lv0[j].n) {
+					sum += lv0[j].a;
+					n++;
+				}
+				if (bit_at(o, j) || j == k) {
+					/* flt/dbl: curval is never assigned (nil) */
+					double cur = !isf && n > 0 ? (double) sum / (double) n : nan("");
+					for (;; l--) {
+						rb[l] = cur;
+						if (l == j)
+							break;
+					}
+					has_nils |= cur != cur;
+					if (j == k)
+						break;
+					l = j - 1;
+				}
+			}
+			k = i;
+			break;
+		}
+		case 5: {
+			double cur;
+			if (isf) {
+				anode c = {0};
+				for (uint64_t j = k; j < i; j++)
+					avg_fold(tp, &c, &lv0[j]);
+				cur = c.n > 0 ? (tp == ORA_flt ? (double) c.f : c.d) : nan("");
+			} else {
+				ora_hge sum = 0;
+				int64_t n = 0;
+				for (uint64_t j = k; j < i; j++)
+					if (lv0[j].n) {
+						sum += lv0[j].a;
+						n++;
+					}
+				cur = n > 0 ? (double) sum / (double) n : nan("");
+			}
+			has_nils |= cur != cur;
+			for (; k < i; k++)
+				rb[k] = cur;
+			break;
+		}
+		case 6:
+			for (; k < i; k++) {
+				rb[k] = lv0[k].n == 0 ? nan("")
+					: tp == ORA_flt ? (double) lv0[k].f : tp == ORA_dbl ? lv0[k].d : (double) lv0[k].a;
+				has_nils |= lv0[k].n == 0;
+			}
+			break;
+		default: {
+			/* populate_segment_tree / compute_on_segment_tree
+			 * (gdk_analytic.h:63-130) over avg nodes */
+			const uint64_t j = k, nc = i - k;
+			uint64_t total = nc, c = nc, nl = 1;
+			do {
+				c = (c + FANOUT - 1) / FANOUT;
+				total += c;
+				nl++;
+			} while (c > 1);
+			anode *tree = calloc(total, sizeof(anode));
+			uint64_t *off = malloc(nl * sizeof(uint64_t));
+			if (!tree || !off) {
+				free(tree);
+				free(off);
+				free(lv0);
+				return -1;
+			}
+			memcpy(tree, lv0 + j, nc * sizeof(anode));
+			uint64_t to = nc, lsize = nc, prev = 0, cur = 1;
+			off[0] = 0;
+			while (cur < nl) {
+				uint64_t prev_to = to;
+				off[cur++] = to;
+				for (uint64_t pos = 0; pos < lsize; pos += FANOUT) {
+					uint64_t pend = pos + FANOUT < lsize ? pos + FANOUT : lsize;
+					anode acc = {0};
+					for (uint64_t x = pos; x < pend; x++)
+						avg_fold(tp, &acc, &tree[prev + x]);
+					tree[to++] = acc;
+				}
+				prev = prev_to;
+				lsize = to - prev_to;
+			}
+			for (; k < i; k++) {
+				anode acc = {0};
+				uint64_t begin = start[k] - j, tend = end[k] - j;
+				if (begin < tend)
+					for (uint64_t level = 0; level < nl; level++) {
+						const anode *tl = tree + off[level];
+						uint64_t pb = begin / FANOUT, pe = tend / FANOUT;
+						if (pb == pe) {
+							for (uint64_t pos = begin; pos < tend; pos++)
+								avg_fold(tp, &acc, &tl[pos]);
+							break;
+						}
+						uint64_t gb = pb * FANOUT;
+						if (begin != gb) {
+							for (uint64_t pos = begin; pos < gb + FANOUT; pos++)
+								avg_fold(tp, &acc, &tl[pos]);
+							pb++;
+						}
+						uint64_t ge = pe * FANOUT;
+						if (tend != ge)
+							for (uint64_t pos = ge; pos < tend; pos++)
+								avg_fold(tp, &acc, &tl[pos]);
+						begin = pb;
+						tend = pe;
+					}
+				rb[k] = avg_final(tp, &acc, &has_nils);
+			}
+			free(tree);
+			free(off);
+			break;
+		}
+		}
+	}
+	free(lv0);
+	r->count = cnt;
+	r->nil = has_nils;
+	r->nonil = !has_nils;
 	return 0;
 }

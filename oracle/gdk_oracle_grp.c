@@ -490,6 +490,170 @@ ora_groupavg3(ora_bat **avgp, ora_bat **remp, ora_bat **cntp,
 	return 0;
 }
 
+/* BATgroupavg (gdk/gdk_aggr.c:1801-1984): average as dbl.
+ * Trivial cases first: no candidates or no groups -> all nil, counts 0
+ * (:1834-1853); singleton groups (g dense or key+nonil, e aligned) -> the
+ * values converted to dbl (BATconvert, no scale applied), counts 1
+ * (:1855-1873).  Otherwise integers run AVERAGE_ITER (gdk_calc_private.h:
+ * 231-275: floor average + remainder, exact) and give avg + (dbl) rem / cnt
+ * (AGGR_AVG :1717-1751); flt/dbl run the order-dependent AVERAGE_ITER_FLOAT
+ * (:277-289) in candidate order (AGGR_AVG_FLOAT :1753-1785).  A nil input
+ * without skip_nils makes the group nil for good; nil groups have count 0.
+ * scale != 0 divides non-nil averages by 10^scale (:1958-1964). */
+int
+ora_groupavg(ora_bat **bnp, ora_bat **cntp, const ora_bat *b, const ora_bat *g,
+	     const ora_bat *e, const ora_bat *s, bool skip_nils, int scale)
+{
+	aggr_ctx a;
+	if (cntp)
+		*cntp = NULL;
+	if (aggr_init(&a, b, g, e, s) < 0)
+		return -1;
+	const int tp = b->type;
+	const bool isf = tp == ORA_flt || tp == ORA_dbl;
+	if (!isf && tp != ORA_bte && tp != ORA_sht && tp != ORA_int && tp != ORA_lng && tp != ORA_hge) {
+		ora_seterr("type (%d) not supported.\n", tp);
+		return -1;
+	}
+	const uint64_t ng = a.ngrp;
+	const ora_oid hb = ng ? a.min : 0;
+	ora_bat *bn, *cn = NULL;
+	if (a.ci.n == 0 || ng == 0) {
+		bn = ora_new(ORA_dbl, ng, hb);
+		for (uint64_t k = 0; k < ng; k++)
+			((double *) bn->base)[k] = nan("");
+		if (cntp) {
+			cn = ora_new(ORA_lng, ng, hb);
+			memset(cn->base, 0, ng * 8);
+		}
+		*bnp = bn;
+		if (cntp)
+			*cntp = cn;
+		return 0;
+	}
+	const bool gdense = g->tseqbase != ORA_OID_NIL;
+	if ((!skip_nils || cntp == NULL || b->nonil) &&
+	    (e == NULL || (e->count == a.ci.n && e->hseqbase == b->hseqbase)) &&
+	    (gdense || (g->key && g->nonil))) {
+		bn = ora_new(ORA_dbl, a.ci.n, s ? s->hseqbase : b->hseqbase);
+		for (uint64_t i = 0; i < a.ci.n; i++) {
+			const uint64_t p = ci_get(&a.ci, i) - b->hseqbase;
+			double d;
+			if (isf) {
+				d = tp == ORA_flt ? (double) ((const float *) b->base)[p] : ((const double *) b->base)[p];
+			} else {
+				ora_hge v;
+				d = val_at(b, p, &v) ? nan("") : (double) v;
+			}
+			((double *) bn->base)[i] = d;
+		}
+		if (cntp) {
+			cn = ora_new(ORA_lng, ng, hb);
+			for (uint64_t k = 0; k < ng; k++)
+				((int64_t *) cn->base)[k] = 1;
+			*cntp = cn;
+		}
+		*bnp = bn;
+		return 0;
+	}
+	bn = ora_new(ORA_dbl, ng, hb);
+	cn = ora_new(ORA_lng, ng, hb);
+	ora_hge *avg = calloc(ng + 1, sizeof(ora_hge));
+	int64_t *rem = calloc(ng + 1, 8);
+	double *dbls = bn->base;
+	int64_t *cnts = cn->base;
+	memset(cnts, 0, ng * 8);
+	for (uint64_t k = 0; k < ng; k++)
+		dbls[k] = 0;
+	for (uint64_t i = 0; i < a.ci.n; i++) {
+		ora_oid gid;
+		if (!aggr_gid(&a, i, &gid))
+			continue;
+		const uint64_t p = ci_get(&a.ci, i) - b->hseqbase;
+		if (isf) {
+			double x = tp == ORA_flt ? (double) ((const float *) b->base)[p] : ((const double *) b->base)[p];
+			if (isnan(x)) {
+				if (!skip_nils)
+					cnts[gid] = INT64_MIN;
+				continue;
+			}
+			if (cnts[gid] == INT64_MIN)
+				continue;
+			double *av = &dbls[gid];
+			const double n = (double) ++cnts[gid];
+			if ((*av > 0) == (x > 0))
+				*av += (x - *av) / n;
+			else
+				*av = *av - *av / n + x / n;
+			continue;
+		}
+		ora_hge x;
+		if (val_at(b, p, &x)) {
+			if (!skip_nils)
+				cnts[gid] = INT64_MIN;
+			continue;
+		}
+		if (cnts[gid] == INT64_MIN)
+			continue;
+		/* AVERAGE_ITER: a + r/n is the running average, 0 <= r < n */
+		ora_hge *av = &avg[gid];
+		const int64_t n = ++cnts[gid];
+		ora_hge an = *av / n, xn = x / n, z1 = xn - an;
+		xn = x - xn * n;
+		an = *av - an * n;
+		unsigned __int128 z2;
+		if (xn >= an) {
+			z2 = (unsigned __int128) (xn - an);
+			while (z2 >= (unsigned __int128) n) {
+				z2 -= (unsigned __int128) n;
+				z1++;
+			}
+		} else {
+			z2 = (unsigned __int128) (an - xn);
+			for (;;) {
+				z1--;
+				if (z2 < (unsigned __int128) n) {
+					z2 = (unsigned __int128) n - z2;
+					break;
+				}
+				z2 -= (unsigned __int128) n;
+			}
+		}
+		*av += z1;
+		rem[gid] += (int64_t) z2;
+		if (rem[gid] >= n) {
+			rem[gid] -= n;
+			(*av)++;
+		}
+	}
+	bool nils = false;
+	for (uint64_t k = 0; k < ng; k++) {
+		if (cnts[k] == 0 || cnts[k] == INT64_MIN) {
+			dbls[k] = nan("");
+			cnts[k] = 0;
+			nils = true;
+		} else if (!isf) {
+			dbls[k] = (double) avg[k] + (double) rem[k] / cnts[k];
+		}
+	}
+	if (scale != 0) {
+		const double fac = pow(10.0, (double) scale);
+		for (uint64_t k = 0; k < ng; k++)
+			if (!isnan(dbls[k]))
+				dbls[k] /= fac;
+	}
+	bn->nil = nils;
+	bn->nonil = !nils;
+	free(avg);
+	free(rem);
+	*bnp = bn;
+	if (cntp)
+		*cntp = cn;
+	else
+		ora_free(cn);
+	return 0;
+}
+
 /* BATgroupmin/max value variant (gdk/gdk_aggr.c:3487-3844): nil for empty
  * groups; nils skipped when skip_nils. */
 ora_bat *

@@ -81,6 +81,7 @@ def lib():
         L.ora_groupcount.argtypes = [P, P, P, P, C.c_bool]
         L.ora_groupminmax.restype = P
         L.ora_groupminmax.argtypes = [P, P, P, P, C.c_bool, C.c_bool]
+        L.ora_groupavg.argtypes = [C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool, C.c_int]
         L.ora_groupavg3.argtypes = [C.POINTER(P), C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool]
         L.ora_join.argtypes = [C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool]
         L.ora_sort.argtypes = [C.POINTER(P), C.POINTER(P), P, C.c_bool, C.c_bool]
@@ -88,6 +89,7 @@ def lib():
         L.ora_firstn.argtypes = [P, P, P, C.c_uint64, C.c_bool, C.c_bool]
         L.ora_rangebounds.argtypes = [P, P, P, C.c_void_p, C.c_int, C.c_bool, C.c_uint64]
         L.ora_analyticalsum.argtypes = [P, P, P, P, P, P, C.c_int, C.c_int, C.c_int]
+        L.ora_analyticalavg.argtypes = [P, P, P, P, P, P, C.c_int, C.c_int]
         L.ora_analyticalcount.argtypes = [P, P, P, P, P, P, C.c_bool, C.c_int]
         L.ora_tpch_lineitem.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64] + [C.c_void_p] * 7
         L.ora_mkdate.restype = C.c_int32
@@ -263,6 +265,14 @@ def BATgroupminmax(b, g, e, domax, skip_nils=True, s=None):
                                       s.ptr if s else None, skip_nils, domax))
 
 
+def BATgroupavg(b, g, e, skip_nils=True, s=None, scale=0, want_counts=True):
+    a, c = P(), P()
+    if lib().ora_groupavg(C.byref(a), C.byref(c) if want_counts else None, b.ptr, g.ptr,
+                          e.ptr if e else None, s.ptr if s else None, skip_nils, scale) < 0:
+        raise _err()
+    return Bat(a), (Bat(c) if want_counts else None)
+
+
 def BATgroupavg3(b, g, e, skip_nils=True, s=None):
     a, r, c = P(), P(), P()
     if lib().ora_groupavg3(C.byref(a), C.byref(r), C.byref(c), b.ptr, g.ptr,
@@ -307,6 +317,16 @@ def analyticalsum(b, p, o, s, e, tp2, frame_type):
     r = lib().ora_new(tp2, n, 0)
     if lib().ora_analyticalsum(r, p.ptr if p else None, o.ptr if o else None, b.ptr,
                                s.ptr if s else None, e.ptr if e else None, b.s.type, tp2,
+                               frame_type) < 0:
+        lib().ora_free(r)
+        raise _err()
+    return Bat(r)
+
+
+def analyticalavg(b, p, o, s, e, frame_type):
+    r = lib().ora_new(TYPE_dbl, b.count(), 0)
+    if lib().ora_analyticalavg(r, p.ptr if p else None, o.ptr if o else None, b.ptr,
+                               s.ptr if s else None, e.ptr if e else None, b.s.type,
                                frame_type) < 0:
         lib().ora_free(r)
         raise _err()

@@ -509,3 +509,82 @@ def test_fgroupsum_exact(gdk, ora, ng):
         got = np.asarray(gdk.BATgroupsum(B, Gs, None, tr, True, s=S).values())
         want = np.asarray(ora.BATgroupsum(OB, OGs, None, tr, True, s=OS).values())
         assert got.tobytes() == want.tobytes()
+
+
+def _hge_pairs(v):
+    """int64 values (INT64_MIN = nil) as hge (lo, hi) uint64 pairs"""
+    lo = v.astype(np.uint64)
+    hi = np.where(v < 0, np.uint64(2**64 - 1), np.uint64(0)).astype(np.uint64)
+    nil = v == -(2**63)
+    lo[nil], hi[nil] = 0, np.uint64(1 << 63)
+    return np.stack([lo, hi], 1).reshape(-1)
+
+
+@pytest.mark.parametrize("tname", ["bte", "sht", "int", "lng", "hge", "flt", "dbl"])
+def test_groupavg(gdk, ora, tname):
+    """BATgroupavg (gdk_aggr.c:1801): integer averages from the exact floor
+    average + remainder, flt/dbl from the order-dependent AVERAGE_ITER_FLOAT
+    replay; bit-exact dbl results and counts against the oracle."""
+    r = rng(57)
+    n = 120_000
+    tp = getattr(gdk, "TYPE_" + tname)
+    if tname in ("flt", "dbl"):
+        v = r.standard_normal(n) * 10.0 ** r.integers(-3, 6, n)
+        v[r.random(n) < 0.002] = np.nan
+        v = v.astype(np.float32 if tname == "flt" else np.float64)
+        data = v
+    else:
+        bits = {"bte": 8, "sht": 16, "int": 32, "lng": 64, "hge": 64}[tname]
+        v = r.integers(-(2**(bits - 1)) + 1, 2**(bits - 1), n, dtype=np.int64)
+        v[r.random(n) < 0.002] = -(2**(bits - 1)) if bits < 64 else -(2**63)
+        data = _hge_pairs(v) if tname == "hge" else v.astype(gdk.NP[tp])
+    B = gdk.BAT.from_numpy(tp, data, nonil=False)
+    OB = ora.Bat.from_array(tp, data, nonil=False)
+    for ng in (1, 5, 700, 5000):
+        gid = r.integers(0, ng, n).astype(np.uint64)
+        if ng > 2:
+            gid[gid == 2] = 1                       # an empty group
+        G, OG = gdk.BAT.from_numpy(gdk.TYPE_oid, gid, key=False), ora.Bat.from_array(ora.TYPE_oid, gid)
+        for skip in (True, False):
+            for scale in (0, 2):
+                a, c = gdk.BATgroupavg(B, G, None, skip, scale=scale)
+                oa, oc = ora.BATgroupavg(OB, OG, None, skip, scale=scale)
+                assert np.asarray(a.values()).tobytes() == np.asarray(oa.values()).tobytes(), \
+                    (ng, skip, scale)
+                assert np.array_equal(c.to_numpy(), oc.values())
+    # dense candidate slice, g aligned with it
+    m = n // 3
+    S, OS = gdk.BAT.dense(500, m), ora.Bat.dense(500, m)
+    gid = r.integers(0, 9, m).astype(np.uint64)
+    G = gdk.BAT.from_numpy(gdk.TYPE_oid, gid, hseqbase=500, key=False)
+    OG = ora.Bat.from_array(ora.TYPE_oid, gid, hseqbase=500)
+    a, c = gdk.BATgroupavg(B, G, None, True, s=S)
+    oa, oc = ora.BATgroupavg(OB, OG, None, True, s=OS)
+    assert np.asarray(a.values()).tobytes() == np.asarray(oa.values()).tobytes()
+    assert np.array_equal(c.to_numpy(), oc.values())
+
+
+def test_groupavg_trivial_paths(gdk, ora):
+    """Singleton groups (g key + nonil) return the values converted to dbl
+    with counts 1 and no scale; no candidates -> nil averages, counts 0."""
+    r = rng(58)
+    n = 5000
+    v = r.integers(-2**62, 2**62, n).astype(np.int64)
+    v[::97] = gdk.NIL[gdk.TYPE_lng]
+    perm = r.permutation(n).astype(np.uint64)
+    B, OB = gdk.BAT.from_numpy(gdk.TYPE_lng, v), ora.Bat.from_array(ora.TYPE_lng, v)
+    G = gdk.BAT.from_numpy(gdk.TYPE_oid, perm, key=True, nonil=True)
+    OG = ora.Bat.from_array(ora.TYPE_oid, perm, key=True, nonil=True)
+    for skip, want_counts in ((False, True), (True, False)):
+        a, c = gdk.BATgroupavg(B, G, None, skip, scale=3, want_counts=want_counts)
+        oa, oc = ora.BATgroupavg(OB, OG, None, skip, scale=3, want_counts=want_counts)
+        assert np.asarray(a.values()).tobytes() == np.asarray(oa.values()).tobytes()
+        if want_counts:
+            assert np.array_equal(c.to_numpy(), oc.values())
+    f = r.standard_normal(n).astype(np.float32)
+    a, _ = gdk.BATgroupavg(gdk.BAT.from_numpy(gdk.TYPE_flt, f), G, None, False)
+    assert np.asarray(a.values()).tobytes() == f.astype(np.float64).tobytes()
+    S, OS = gdk.BAT.dense(0, 0), ora.Bat.dense(0, 0)
+    G0 = gdk.BAT.from_numpy(gdk.TYPE_oid, np.zeros(0, np.uint64))
+    a, c = gdk.BATgroupavg(B, G0, None, True, s=S)
+    assert a.count() == 0 and c.count() == 0

@@ -211,3 +211,44 @@ def test_fsum_oracle(ora):
     assert ora.BATsum(ora.TYPE_dbl, ora.Bat.from_array(ora.TYPE_dbl, big)) == 1e308
     with pytest.raises(ora.OracleError, match="overflow"):
         ora.BATsum(ora.TYPE_dbl, ora.Bat.from_array(ora.TYPE_dbl, np.array([1e308, 1e308])))
+
+
+def test_groupavg_oracle(ora):
+    """BATgroupavg (gdk_aggr.c:1801): integer averages are floor + remainder
+    (exact, checked against Fractions), flt/dbl replay AVERAGE_ITER_FLOAT
+    in row order (checked against the same recurrence in Python)."""
+    from fractions import Fraction
+    r = np.random.default_rng(5)
+    n, ng = 3000, 7
+    gid = r.integers(0, ng, n).astype(np.uint64)
+    G = ora.Bat.from_array(ora.TYPE_oid, gid)
+    v = r.integers(-2**62, 2**62, n).astype(np.int64)
+    v[r.random(n) < 0.05] = -(2**63)
+    for skip in (True, False):
+        a, c = ora.BATgroupavg(ora.Bat.from_array(ora.TYPE_lng, v), G, None, skip_nils=skip)
+        for k in range(ng):
+            x = v[gid == k]
+            if not skip and (x == -(2**63)).any():
+                assert math.isnan(a.values()[k]) and c.values()[k] == 0
+                continue
+            x = [int(t) for t in x if t != -(2**63)]
+            q, m = divmod(sum(x), len(x))
+            assert a.values()[k] == float(q) + float(m) / len(x)
+            assert c.values()[k] == len(x)
+    f = r.standard_normal(n) * 1e3
+    f[r.random(n) < 0.05] = np.nan
+    a, c = ora.BATgroupavg(ora.Bat.from_array(ora.TYPE_dbl, f), G, None, skip_nils=True, scale=2)
+    for k in range(ng):
+        av, cnt = 0.0, 0
+        for x in f[gid == k]:
+            if math.isnan(x):
+                continue
+            cnt += 1
+            av = av + (x - av) / cnt if (av > 0) == (x > 0) else av - av / cnt + x / cnt
+        assert a.values()[k] == av / 100.0 and c.values()[k] == cnt
+    # singleton groups: converted values, counts 1, no scale
+    Gd = ora.Bat.from_array(ora.TYPE_oid, np.arange(n, dtype=np.uint64)[::-1], key=True, nonil=True)
+    a, c = ora.BATgroupavg(ora.Bat.from_array(ora.TYPE_lng, v), Gd, None, skip_nils=False, scale=3)
+    want = np.where(v == -(2**63), np.nan, v.astype(np.float64))
+    np.testing.assert_array_equal(np.array(a.values()), want)
+    assert set(c.values()) == {1}
