@@ -197,6 +197,11 @@ int mgdk_GDKanalyticalsum(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mg
 			  int tp1, int tp2, int frame_type);
 int mgdk_GDKanalyticalcount(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e,
 			    bool ignore_nils, int tpe, int frame_type);
+/* gdk_analytic_statistics.c:364 GDKanalyticalavg (gdk_analytic.h:41): dbl
+ * average per row over its frame, frame kinds as above; r is a
+ * caller-allocated dbl BAT; tpe = type of b (bte..lng, flt, dbl) */
+int mgdk_GDKanalyticalavg(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e,
+			  int tpe, int frame_type);
 
 /* ---- compressed column inputs (sql/backends/monet5/dict.c, for.c):
  *      a DICT column is codes o (bte/sht/int, read unsigned) + the

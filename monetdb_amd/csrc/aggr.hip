@@ -668,24 +668,6 @@ put_vec(std::vector<char> &buf, int tp, BUN k, hge v, bool nil)
 
 // ---- BATgroupavg (gdk/gdk_aggr.c:1801) ----------------------------------
 
-// 128-bit integer -> double, round to nearest even: the top 64 significant
-// bits with a sticky bit below them convert exactly like the full value
-__device__ __forceinline__ double
-hge_to_dbl(hge v)
-{
-	if (v >= (hge) INT64_MIN && v <= (hge) INT64_MAX)
-		return (double) (long long) v;
-	const bool neg = v < 0;
-	const uhge u = neg ? (uhge) 0 - (uhge) v : (uhge) v;
-	const unsigned long long hi = (unsigned long long) (u >> 64);
-	const int shift = 64 - __builtin_clzll(hi);                 // 1..64
-	unsigned long long top = (unsigned long long) (u >> shift);
-	if (u & (((uhge) 1 << shift) - 1))
-		top |= 1;
-	const double d = ldexp((double) top, shift);
-	return neg ? -d : d;
-}
-
 // singleton groups: BATconvert(b, s, TYPE_dbl) (gdk_calc_convert.c:1415)
 __global__ void
 k_to_dbl(const void *base, int tp, int w, oid off, BUN n, double *out)

@@ -24,6 +24,8 @@
 // that bound (where the reference's answer depends on its tree's addition
 // order) fails loudly instead of guessing.  hge results of integer inputs
 // cannot overflow.
+#include <type_traits>
+
 #include "mgdk_internal.h"
 
 using namespace mgdk;
@@ -275,6 +277,20 @@ struct Starts {
 		}
 		return L ? L[k] : Lseq + k;
 	}
+	// index of the segment holding row i
+	__device__ __forceinline__ BUN idx(BUN i) const
+	{
+		BUN lo = 0, hi = m;
+		while (hi - lo > 1) {
+			const BUN mid = (lo + hi) / 2;
+			if (at(mid) <= i)
+				lo = mid;
+			else
+				hi = mid;
+		}
+		return lo;
+	}
+	__device__ __forceinline__ BUN end_of(BUN k) const { return k + 1 < m ? at(k + 1) : n; }
 	// [start, end) of the segment holding row i
 	__device__ __forceinline__ void seg(BUN i, BUN &s, BUN &e) const
 	{
@@ -298,6 +314,7 @@ struct FArgs {
 	bool lng_out;        // result lng (else hge)
 	bool count;          // GDKanalyticalcount
 	bool count_all;
+	bool avg;            // GDKanalyticalavg of integers: dbl sum / count
 	Starts part, peer;
 	const oid *s, *e;
 	const hge *P, *A;
@@ -343,6 +360,12 @@ k_frames(FArgs a)
 		}
 		const unsigned long long c = a.C ? a.C[hi] - a.C[lo] : hi - lo;
 		const hge sum = a.P[hi] - a.P[lo];
+		if (a.avg) {
+			// (dbl) sum / n of ANALYTICAL_AVG_IMP_NUM_* (gdk_analytic_statistics.c:55-165)
+			((double *) a.out)[i] = c ? hge_to_dbl(sum) / (double) (long long) c : __builtin_nan("");
+			hasnil |= c == 0;
+			continue;
+		}
 		if (a.lng_out) {
 			// the reference's partials for this row's partition
 			if (a.frame == 3 || a.frame == 5) {
@@ -588,7 +611,7 @@ sum_in_type(int t)
 
 int
 run_frames(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e, int frame_type,
-	   bool count, bool count_all, bool lng_out)
+	   bool count, bool count_all, bool lng_out, bool avg = false)
 {
 	const BUN n = b->count;
 	hipStream_t st = stream();
@@ -709,6 +732,7 @@ run_frames(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk
 	a.lng_out = lng_out;
 	a.count = count;
 	a.count_all = count_all;
+	a.avg = avg;
 	a.s = frames ? (const oid *) s->theap : nullptr;
 	a.e = frames ? (const oid *) e->theap : nullptr;
 	a.P = P.as<hge>();
@@ -763,6 +787,367 @@ out:
 	return rc;
 }
 
+
+// ---- GDKanalyticalavg (gdk/gdk_analytic_statistics.c:364-423) -----------
+//
+// Integer inputs over the running frames (3, 4, 5) are exact: the frame's
+// 128-bit sum from the prefix arrays above, (dbl) sum / n (k_frames, avg).
+// Everything else replays the reference's arithmetic, which is order
+// dependent:
+//   * flt / dbl over frames 3 and 5: AVERAGE_ITER_FLOAT in the input type,
+//     row by row through the partition -- one lane per partition
+//     (k_avg_replay); frame 4 of flt / dbl never assigns its result (:224-246),
+//     so every row is nil;
+//   * general frames: the reference's fanout-16 segment tree per partition
+//     (gdk_analytic.h:63-130) whose inner nodes fold their non-empty
+//     children's averages with AVERAGE_ITER / AVERAGE_ITER_FLOAT (a node
+//     counts children, not rows).  The device builds the same trees for
+//     every partition at once, one level per launch, and answers each row
+//     with the reference's query walk (k_avg_tree_query).
+// Level L >= 1 of partition k (start ps) is stored at
+//     lvl[L] + (ps >> 4L) + k + m,   m < ceil(nc / 16^L),
+// which never overlaps the next partition's nodes, so a level holds
+// (n >> 4L) + #partitions + 1 nodes and needs no per-partition offset scan.
+
+constexpr int AVG_MAX_LEVELS = 17;   // 16^16 = 2^64 rows
+
+// AVERAGE_ITER (gdk/gdk_calc_private.h:231-275) in 64-bit arithmetic: for
+// bte..lng inputs no intermediate leaves the input type's range
+__device__ __forceinline__ void
+avg_iter_int(long long x, long long &a, long long &rr, long long &n)
+{
+	n++;
+	long long an = a / n, xn = x / n, z1 = xn - an;
+	xn = x - xn * n;
+	an = a - an * n;
+	unsigned long long z2;
+	if (xn >= an) {
+		z2 = (unsigned long long) (xn - an);
+		while (z2 >= (unsigned long long) n) {
+			z2 -= (unsigned long long) n;
+			z1++;
+		}
+	} else {
+		z2 = (unsigned long long) (an - xn);
+		for (;;) {
+			z1--;
+			if (z2 < (unsigned long long) n) {
+				z2 = (unsigned long long) n - z2;
+				break;
+			}
+			z2 -= (unsigned long long) n;
+		}
+	}
+	a += z1;
+	rr += (long long) z2;
+	if (rr >= n) {
+		rr -= n;
+		a++;
+	}
+}
+
+// avg_num_deltas / avg_fp_deltas and their fold / finalize steps
+template <typename T, bool F = std::is_floating_point<T>::value>
+struct AvgNode;
+
+template <typename T>
+struct AvgNode<T, false> {
+	long long a, n, rr;
+	__device__ __forceinline__ void zero() { a = n = rr = 0; }
+	__device__ __forceinline__ void leaf(const T *b, BUN i)
+	{
+		const T v = b[i];
+		a = v == NilOf<T>::v() ? 0 : (long long) v;
+		n = v == NilOf<T>::v() ? 0 : 1;
+		rr = 0;
+	}
+	__device__ __forceinline__ void fold(const AvgNode &c)
+	{
+		if (c.n)
+			avg_iter_int(c.a, a, rr, n);
+	}
+	__device__ __forceinline__ double result() const
+	{
+		return (double) a + (double) rr / (double) n;
+	}
+};
+
+template <typename T>
+struct AvgNode<T, true> {
+	T a;
+	long long n;
+	__device__ __forceinline__ void zero() { a = 0; n = 0; }
+	__device__ __forceinline__ void leaf(const T *b, BUN i)
+	{
+		const T v = b[i];
+		a = v != v ? (T) 0 : v;
+		n = v != v ? 0 : 1;
+	}
+	// AVERAGE_ITER_FLOAT (gdk_calc_private.h:277-289) in T arithmetic
+	__device__ __forceinline__ void add(T x)
+	{
+		n++;
+		const T nn = (T) n;
+		if ((a > 0) == (x > 0))
+			a += (x - a) / nn;
+		else
+			a = a - a / nn + x / nn;
+	}
+	__device__ __forceinline__ void fold(const AvgNode &c)
+	{
+		if (c.n)
+			add(c.a);
+	}
+	__device__ __forceinline__ double result() const { return (double) a; }
+};
+
+struct AvgTree {
+	void *lvl[AVG_MAX_LEVELS];   // level L >= 1 node arrays
+	int nlev;                    // levels built above the rows
+};
+
+__global__ __launch_bounds__(256) void
+k_avg_pidx(Starts part, uint32_t *pidx)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < part.n; i += (BUN) gridDim.x * blockDim.x)
+		pidx[i] = (uint32_t) part.idx(i);
+}
+
+__global__ __launch_bounds__(256) void
+k_avg_maxlen(Starts part, unsigned long long *mx)
+{
+	unsigned long long v = 0;
+	for (BUN k = (BUN) blockIdx.x * blockDim.x + threadIdx.x; k < part.m; k += (BUN) gridDim.x * blockDim.x)
+		v = max(v, (unsigned long long) (part.end_of(k) - part.at(k)));
+	v = block_reduce(v, [](unsigned long long x, unsigned long long y) { return x > y ? x : y; });
+	if (threadIdx.x == 0 && v)
+		atomicMax(mx, v);
+}
+
+// populate_segment_tree, level L >= 1: the thread of the first row a node
+// covers folds the node's children (level L-1) in order
+template <typename T>
+__global__ __launch_bounds__(256) void
+k_avg_tree_level(const T *b, Starts part, const uint32_t *pidx, AvgTree t, int L)
+{
+	using N = AvgNode<T>;
+	const int sh = 4 * L, shc = sh - 4;
+	N *out = (N *) t.lvl[L];
+	const N *child = L > 1 ? (const N *) t.lvl[L - 1] : nullptr;
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < part.n; i += (BUN) gridDim.x * blockDim.x) {
+		const BUN k = pidx[i], ps = part.at(k);
+		const BUN rel = i - ps;
+		if (rel & (((BUN) 1 << sh) - 1))
+			continue;
+		const BUN nc = part.end_of(k) - ps;
+		const BUN ncl = (nc + ((BUN) 1 << shc) - 1) >> shc;     // nodes on level L-1
+		const BUN c0 = (rel >> sh) * 16, c1 = min(c0 + 16, ncl);
+		N acc;
+		acc.zero();
+		for (BUN c = c0; c < c1; c++) {
+			N x;
+			if (L == 1)
+				x.leaf(b, ps + c);
+			else
+				x = child[(ps >> shc) + k + c];
+			acc.fold(x);
+		}
+		out[(ps >> sh) + k + (rel >> sh)] = acc;
+	}
+}
+
+// compute_on_segment_tree (gdk_analytic.h:96-130) for [s[i], e[i])
+template <typename T>
+__global__ __launch_bounds__(256) void
+k_avg_tree_query(const T *b, Starts part, const uint32_t *pidx, AvgTree t, const oid *S, const oid *E,
+		 double *out, uint32_t *flags)
+{
+	using N = AvgNode<T>;
+	uint32_t hasnil = 0;
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < part.n; i += (BUN) gridDim.x * blockDim.x) {
+		const BUN k = pidx[i], ps = part.at(k), nc = part.end_of(k) - ps;
+		BUN begin = S[i] > ps ? min((BUN) S[i] - ps, nc) : 0;
+		BUN tend = E[i] > ps ? min((BUN) E[i] - ps, nc) : 0;
+		N acc;
+		acc.zero();
+		if (begin < tend) {
+			for (int L = 0; L <= t.nlev; L++) {
+				const N *lv = L ? (const N *) t.lvl[L] + ((ps >> (4 * L)) + k) : nullptr;
+				auto node = [&](BUN pos) {
+					N x;
+					if (L == 0)
+						x.leaf(b, ps + pos);
+					else
+						x = lv[pos];
+					return x;
+				};
+				BUN pb = begin / 16, pe = tend / 16;
+				if (pb == pe) {
+					for (BUN pos = begin; pos < tend; pos++)
+						acc.fold(node(pos));
+					break;
+				}
+				const BUN gb = pb * 16;
+				if (begin != gb) {
+					for (BUN pos = begin; pos < gb + 16; pos++)
+						acc.fold(node(pos));
+					pb++;
+				}
+				const BUN ge = pe * 16;
+				if (tend != ge)
+					for (BUN pos = ge; pos < tend; pos++)
+						acc.fold(node(pos));
+				begin = pb;
+				tend = pe;
+			}
+		}
+		if (acc.n == 0) {
+			out[i] = __builtin_nan("");
+			hasnil = 1;
+		} else {
+			out[i] = acc.result();
+		}
+	}
+	hasnil = block_reduce(hasnil, [](uint32_t x, uint32_t y) { return x | y; });
+	if (threadIdx.x == 0)
+		publish_or(flags, hasnil);
+}
+
+// flt / dbl, frames 3 (peer groups from o) and 5: one lane replays one
+// partition's rows in order (ANALYTICAL_AVG_IMP_FP_UNBOUNDED_TILL_CURRENT_ROW
+// / _ALL_ROWS, gdk_analytic_statistics.c:202-267)
+template <typename T>
+__global__ __launch_bounds__(64) void
+k_avg_replay(const T *b, Starts part, const int8_t *o, bool peers, double *out, uint32_t *flags)
+{
+	const BUN k = (BUN) blockIdx.x * blockDim.x + threadIdx.x;
+	uint32_t hasnil = 0;
+	if (k < part.m) {
+		const BUN ps = part.at(k), pe = part.end_of(k);
+		AvgNode<T> c;
+		c.zero();
+		double cur = __builtin_nan("");
+		BUN j = ps;
+		for (BUN r = ps; r < pe; r++) {
+			const T v = b[r];
+			if (v == v)
+				c.add(v);
+			if (r + 1 == pe || (peers && o[r + 1])) {
+				if (c.n > 0)
+					cur = (double) c.a;
+				else
+					hasnil = 1;
+				for (; j <= r; j++)
+					out[j] = cur;
+			}
+		}
+	}
+	if (hasnil)
+		publish_or(flags, 1);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void
+k_avg_row(const T *b, BUN n, bool nil_all, double *out, uint32_t *flags)
+{
+	uint32_t hasnil = nil_all && n;
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		const T v = b[i];
+		const bool nil = nil_all || is_nil(v);
+		out[i] = nil ? __builtin_nan("") : (double) v;
+		hasnil |= nil;
+	}
+	hasnil = block_reduce(hasnil, [](uint32_t x, uint32_t y) { return x | y; });
+	if (threadIdx.x == 0)
+		publish_or(flags, hasnil);
+}
+
+template <typename T>
+int
+run_avg(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e, int frame_type)
+{
+	constexpr bool isf = std::is_floating_point<T>::value;
+	const BUN n = b->count;
+	hipStream_t st = stream();
+	const T *bv = (const T *) b->theap;
+	double *out = (double *) r->theap;
+	const bool frames = !(frame_type >= 3 && frame_type <= 6);
+	DevBuf fl(64);
+	if (!fl.p || !hip_ok(hipMemsetAsync(fl.p, 0, 64, st), "memset"))
+		return -1;
+	mgdk_bat *Sp = nullptr;
+	int rc = -1;
+	if (frame_type == 6 || (isf && frame_type == 4)) {
+		hipLaunchKernelGGL((k_avg_row<T>), dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st, bv, n,
+				   frame_type == 4, out, fl.as<uint32_t>());
+	} else {
+		Starts part;
+		if (make_starts(p ? (const int8_t *) p->theap : nullptr, n, part, &Sp) < 0)
+			goto out;
+		if (!frames) {
+			// flt / dbl, frames 3 and 5 (integers take run_frames)
+			if constexpr (isf)
+				hipLaunchKernelGGL((k_avg_replay<T>), dim3((unsigned) ((part.m + 63) / 64)), dim3(64), 0, st, bv,
+						   part, frame_type == 3 ? (const int8_t *) o->theap : nullptr, frame_type == 3,
+						   out, fl.as<uint32_t>());
+		} else {
+			if (n >= 0xffffffffull) {
+				seterr("42000!GDKanalyticalavg: more than 2^32-1 rows on the device path\n");
+				goto out;
+			}
+			// levels: until one node covers the longest partition
+			unsigned long long *hm = (unsigned long long *) pinned(8);
+			DevBuf mx(64), pidx(n * 4 + 4);
+			if (!mx.p || !pidx.p || !hip_ok(hipMemsetAsync(mx.p, 0, 8, st), "memset"))
+				goto out;
+			hipLaunchKernelGGL(k_avg_maxlen, dim3(grid_for(part.m, 1024, 1024)), dim3(256), 0, st, part,
+					   mx.as<unsigned long long>());
+			hipLaunchKernelGGL(k_avg_pidx, dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st, part,
+					   pidx.as<uint32_t>());
+			if (!hip_ok(hipMemcpyAsync(hm, mx.p, 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+				goto out;
+			AvgTree t{};
+			// (nc - 1) >> 4L == 0 for every partition at the top level
+			int nlev = 1;
+			while (nlev < AVG_MAX_LEVELS - 1 && ((*hm - 1) >> (4 * nlev)) > 0)
+				nlev++;
+			t.nlev = nlev;
+			size_t tot = 0, offs[AVG_MAX_LEVELS] = {0};
+			for (int L = 1; L <= nlev; L++) {
+				offs[L] = tot;
+				tot += ((n >> (4 * L)) + part.m + 1) * sizeof(AvgNode<T>);
+				tot = (tot + 255) & ~(size_t) 255;
+			}
+			DevBuf tree(tot);
+			if (!tree.p)
+				goto out;
+			for (int L = 1; L <= nlev; L++)
+				t.lvl[L] = tree.as<char>() + offs[L];
+			for (int L = 1; L <= nlev; L++)
+				hipLaunchKernelGGL((k_avg_tree_level<T>), dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st, bv,
+						   part, pidx.as<uint32_t>(), t, L);
+			hipLaunchKernelGGL((k_avg_tree_query<T>), dim3(grid_for(n, 256, 16384)), dim3(256), 0, st, bv, part,
+					   pidx.as<uint32_t>(), t, (const oid *) s->theap, (const oid *) e->theap, out,
+					   fl.as<uint32_t>());
+			if (!sync())
+				goto out;
+		}
+	}
+	{
+		uint32_t *h = (uint32_t *) pinned(16);
+		if (!hip_ok(hipMemcpyAsync(h, fl.p, 4, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+			goto out;
+		r->count = n;
+		r->tnil = h[0] != 0;
+		r->tnonil = h[0] == 0;
+		r->tsorted = r->trevsorted = r->tkey = n <= 1;
+		rc = 0;
+	}
+out:
+	mgdk_BBPunfix(Sp);
+	return rc;
+}
+
 }  // namespace
 
 extern "C" int
@@ -803,4 +1188,66 @@ mgdk_GDKanalyticalcount(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk
 	}
 	ProfScope prof("analyticalcount");
 	return run_frames(r, p, o, b, s, e, frame_type, true, count_all, false);
+}
+
+// GDKanalyticalavg (gdk/gdk_analytic_statistics.c:364): r is a
+// caller-allocated dbl BAT of count(b) slots
+extern "C" int
+mgdk_GDKanalyticalavg(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e, int tpe,
+		      int frame_type)
+{
+	if (r == nullptr || b == nullptr) {
+		seterr("GDKanalyticalavg: NULL argument");
+		return -1;
+	}
+	const int bt = basetype(tpe);
+	if (!(bt == MGDK_bte || bt == MGDK_sht || bt == MGDK_int || bt == MGDK_lng || bt == MGDK_flt ||
+	      bt == MGDK_dbl)) {
+		if (bt == MGDK_hge)
+			seterr("42000!GDKanalyticalavg: average of hge is not supported on the device path\n");
+		else
+			seterr("42000!average of type %s to dbl unsupported.\n", atomname(tpe));
+		return -1;
+	}
+	if (basetype(b->ttype) != bt || r->ttype != MGDK_dbl) {
+		seterr("GDKanalyticalavg: b must be of type tpe and r a dbl BAT");
+		return -1;
+	}
+	const BUN n = b->count;
+	if (n && r->theap == nullptr) {
+		seterr("analytic: result BAT has no heap");
+		return -1;
+	}
+	if (n == 0) {
+		r->count = 0;
+		r->tnil = 0;
+		r->tnonil = 1;
+		return 0;
+	}
+	if ((p && (p->count != n || width_of(p->ttype) != 1)) || (o && (o->count != n || width_of(o->ttype) != 1))) {
+		seterr("analytic: p and o must be bit BATs aligned with b");
+		return -1;
+	}
+	const bool frames = !(frame_type >= 3 && frame_type <= 6);
+	if (frames && (s == nullptr || e == nullptr || s->count < n || e->count < n || s->ttype != MGDK_oid ||
+		       e->ttype != MGDK_oid)) {
+		seterr("analytic: frame bounds s and e (oid BATs aligned with b) are required");
+		return -1;
+	}
+	if ((frame_type == 3 || frame_type == 4) && o == nullptr) {
+		seterr("analytic: the peer column o is required for this frame");
+		return -1;
+	}
+	ProfScope prof("analyticalavg");
+	const bool isf = bt == MGDK_flt || bt == MGDK_dbl;
+	if (!isf && (frame_type == 3 || frame_type == 4 || frame_type == 5))
+		return run_frames(r, p, o, b, s, e, frame_type, false, false, false, true);
+	switch (bt) {
+	case MGDK_bte: return run_avg<int8_t>(r, p, o, b, s, e, frame_type);
+	case MGDK_sht: return run_avg<int16_t>(r, p, o, b, s, e, frame_type);
+	case MGDK_int: return run_avg<int32_t>(r, p, o, b, s, e, frame_type);
+	case MGDK_lng: return run_avg<int64_t>(r, p, o, b, s, e, frame_type);
+	case MGDK_flt: return run_avg<float>(r, p, o, b, s, e, frame_type);
+	default: return run_avg<double>(r, p, o, b, s, e, frame_type);
+	}
 }

@@ -188,3 +188,23 @@ publish_or(uint32_t *flag, uint32_t bits)
 	if (bits && (bits & ~__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
 		atomicOr(flag, bits);
 }
+
+// 128-bit integer -> double, round to nearest even: the top 64 significant
+// bits with a sticky bit below them convert exactly like the full value
+__device__ __forceinline__ double
+hge_to_dbl(hge v)
+{
+	if (v >= (hge) INT64_MIN && v <= (hge) INT64_MAX)
+		return (double) (long long) v;
+	const bool neg = v < 0;
+	const uhge u = neg ? (uhge) 0 - (uhge) v : (uhge) v;
+	const unsigned long long hi = (unsigned long long) (u >> 64);
+	if (hi == 0)
+		return neg ? -(double) (unsigned long long) u : (double) (unsigned long long) u;
+	const int shift = 64 - __builtin_clzll(hi);                 // 1..64
+	unsigned long long top = (unsigned long long) (u >> shift);
+	if (u & (((uhge) 1 << shift) - 1))
+		top |= 1;
+	const double d = ldexp((double) top, shift);
+	return neg ? -d : d;
+}

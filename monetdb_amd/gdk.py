@@ -129,6 +129,7 @@ _SIGS = {
                                  C.c_bool]),
     "mgdk_GDKanalyticalsum": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_int, C.c_int]),
     "mgdk_GDKanalyticalcount": (C.c_int, [C.c_void_p] * 6 + [C.c_bool, C.c_int, C.c_int]),
+    "mgdk_GDKanalyticalavg": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_int]),
     "mgdk_BATlowerbound2": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
                                       C.c_void_p]),
     "mgdk_BATupload_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
@@ -519,6 +520,14 @@ def GDKanalyticalcount(b, p, o, s, e, ignore_nils, frame_type):
     r = BAT(lib().mgdk_COLnew(0, TYPE_lng, max(1, b.count())))
     _chk(lib().mgdk_GDKanalyticalcount(r.ptr, _p(p), _p(o), b.ptr, _p(s), _p(e), ignore_nils, b.ttype,
                                        frame_type))
+    return r
+
+
+def GDKanalyticalavg(b, p, o, s, e, frame_type):
+    """Windowed dbl average per row over its frame
+    (gdk/gdk_analytic_statistics.c:364)."""
+    r = BAT(lib().mgdk_COLnew(0, TYPE_dbl, max(1, b.count())))
+    _chk(lib().mgdk_GDKanalyticalavg(r.ptr, _p(p), _p(o), b.ptr, _p(s), _p(e), b.ttype, frame_type))
     return r
 
 

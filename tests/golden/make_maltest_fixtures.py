@@ -243,6 +243,45 @@ def analytics03_fixture():
     return {"source": rel, "cases": out}
 
 
+def analytics03_avg_fixture():
+    """Windowed AVG cases of analytics03.test (GDKanalyticalavg,
+    gdk/gdk_analytic_statistics.c:364): avg(aa) / avg(cc) (cc real, equal to
+    aa in that table) over RANGE unbounded preceding .. current row, and the
+    overflowme table's int averages past the int range (floor printed)."""
+    rel = "sql/test/analytics/Tests/analytics03.test"
+    text = open(os.path.join(REF, rel)).read()
+    m = re.search(r"insert into rowsvsrangevsgroups values (.*)\n", text)
+    rows = [tuple(int(float(x)) for x in t.split(",")) for t in re.findall(r"\(([^)]*)\)", m.group(1))]
+    m = re.search(r"insert into overflowme values (.*)\n", text)
+    ovf = [tuple(int(x) for x in t.split(",")) for t in re.findall(r"\(([^)]*)\)", m.group(1))]
+    out = []
+    deleted = False
+    for kind, body, exp in parse_blocks(text):
+        stmt = " ".join(body)
+        if stmt.startswith("delete from rowsvsrangevsgroups where aa = 2"):
+            deleted = True
+            continue
+        if not kind.startswith("query"):
+            continue
+        if stmt.startswith("select cast(sum(aa) over (order by aa range between unbounded preceding and current row)"):
+            data = [r for r in rows if not (deleted and r[0] == 2)]
+            nrow = len(exp) // 8
+            for ci, agg in ((6, "avg"), (7, "avgf")):
+                out.append(dict(aa=[r[0] for r in data], bb=[r[1] for r in data], agg=agg, part=None,
+                                order="aa", frame="upto", floor=False,
+                                expected=[float(exp[i * 8 + ci]) for i in range(nrow)]))
+        elif stmt.startswith("select floor(avg(aa) over (rows between current row and unbounded following))"):
+            nrow = len(exp) // 6
+            # 1: range .. unbounded following, no order (one peer group);
+            # 3: order by bb range current row .. unbounded following;
+            # 5: partition by bb order by bb range unbounded preceding
+            for ci, part, order, frame in ((1, None, None, "from"), (3, None, "bb", "from"), (5, "bb", "bb", "upto")):
+                out.append(dict(aa=[r[0] for r in ovf], bb=[r[1] for r in ovf], agg="avg", part=part,
+                                order=order, frame=frame, floor=True,
+                                expected=[float(exp[i * 6 + ci]) for i in range(nrow)]))
+    return {"source": rel, "cases": out}
+
+
 def main():
     if not os.path.isdir(REF):
         sys.exit("reference not present; fixtures are already committed")
@@ -253,6 +292,7 @@ def main():
           "firstn": [firstn_fixture("monetdb5/modules/mal/Tests/%s.maltest" % f)
                      for f in ("pqueue", "pqueue2", "pqueue3")],
           "window_frames": analytics03_fixture(),
+          "window_avg": analytics03_avg_fixture(),
           "sort": [sort_fixture("monetdb5/modules/mal/Tests/%s.maltest" % f)
                    for f in ("orderidx00", "orderidx04")]}
     with open(os.path.join(OUT, "maltest_fixtures.json"), "w") as f:

@@ -83,3 +83,30 @@ def replay_window_frames(sumf, countf, make_bat, TYPE_int, TYPE_bit, TYPE_lng):
         if [int(x) for x in got] != c["expected"]:
             bad.append((c, list(got)))
     return bad
+
+
+def replay_window_avg(avgf, make_bat, TYPE_int, TYPE_flt, TYPE_bit):
+    """Windowed AVG cases of analytics03.test (frame 3 = unbounded preceding
+    .. current row's peers, 4 = current row's peers .. unbounded following).
+    avgf(b, p, o, frame) returns per-row dbl averages in sorted order; the
+    reference prints 3 decimals (or floor()).  Returns mismatches."""
+    bad = []
+    for c in FIX["window_avg"]["cases"]:
+        aa, bb = np.array(c["aa"], np.int32), np.array(c["bb"], np.int32)
+        cols = {"aa": aa, "bb": bb}
+        keys = [cols[k] for k in (c["order"], c["part"]) if k is not None]
+        perm = np.lexsort(keys) if keys else np.arange(len(aa))
+        part = cols[c["part"]][perm] if c["part"] else np.zeros(len(aa), np.int32)
+        order = cols[c["order"]][perm] if c["order"] else np.zeros(len(aa), np.int32)
+        p = np.zeros(len(aa), np.int8)
+        p[0] = 1
+        p[1:] = part[1:] != part[:-1]
+        o = p.copy()
+        o[1:] |= order[1:] != order[:-1]
+        frame = {"upto": 3, "from": 4, "all": 5}[c["frame"]]
+        b = make_bat(TYPE_flt, aa[perm].astype(np.float32)) if c["agg"] == "avgf" else make_bat(TYPE_int, aa[perm])
+        got = np.asarray(avgf(b, make_bat(TYPE_bit, p), make_bat(TYPE_bit, o), frame), np.float64)
+        got = np.floor(got) if c["floor"] else np.round(got, 3)
+        if list(got) != c["expected"]:
+            bad.append((c, list(got)))
+    return bad

@@ -150,3 +150,91 @@ def test_analytical_sum_general_frames_hge(gdk, ora, limit, tname):
                              ora.Bat.from_array(ora.TYPE_oid, s.to_numpy()),
                              ora.Bat.from_array(ora.TYPE_oid, e.to_numpy()), ora.TYPE_hge, 1).values()
     assert list(got) == list(want)
+
+
+def _avg_input(r, tname, n):
+    if tname in ("flt", "dbl"):
+        v = (r.standard_normal(n) * 10.0 ** r.integers(-2, 5, n)).astype(np.float32 if tname == "flt" else np.float64)
+        v[r.random(n) < 0.05] = np.nan
+        return v
+    dt = {"bte": np.int8, "sht": np.int16, "int": np.int32, "lng": np.int64}[tname]
+    info = np.iinfo(dt)
+    v = r.integers(info.min + 1, info.max, n, dtype=np.int64).astype(dt)
+    v[r.random(n) < 0.05] = info.min
+    return v
+
+
+@pytest.mark.parametrize("tname", ["bte", "sht", "int", "lng", "flt", "dbl"])
+@pytest.mark.parametrize("frame", [3, 4, 5, 6, 1])
+def test_analytical_avg(gdk, ora, tname, frame):
+    """GDKanalyticalavg (gdk_analytic_statistics.c:364) bit-exact against the
+    oracle: exact integer running frames, AVERAGE_ITER_FLOAT replay for
+    flt/dbl, and the reference's segment tree (averages of child averages)
+    for general frames."""
+    r = rng(311)
+    _, p, o, ob = _data(r, nparts=31, plen=900)
+    n = len(p)
+    v = _avg_input(r, tname, n)
+    tp = getattr(gdk, "TYPE_" + tname)
+    s = e = None
+    if frame == 1:
+        s, e = _bounds(gdk, ob, p, 40)
+    got = gdk.GDKanalyticalavg(gdk.BAT.from_numpy(tp, v), gdk.BAT.from_numpy(gdk.TYPE_bit, p),
+                               gdk.BAT.from_numpy(gdk.TYPE_bit, o), s, e, frame)
+    os_ = ora.Bat.from_array(ora.TYPE_oid, s.to_numpy()) if s else None
+    oe = ora.Bat.from_array(ora.TYPE_oid, e.to_numpy()) if e else None
+    want = ora.analyticalavg(ora.Bat.from_array(tp, v), ora.Bat.from_array(ora.TYPE_bit, p),
+                             ora.Bat.from_array(ora.TYPE_bit, o), os_, oe, frame)
+    assert np.asarray(got.values()).tobytes() == np.asarray(want.values()).tobytes()
+    assert bool(got.s.tnil) == bool(np.isnan(np.asarray(want.values())).any())
+
+
+@pytest.mark.parametrize("tname", ["int", "lng", "dbl"])
+def test_analytical_avg_deep_trees(gdk, ora, tname):
+    """General frames over long partitions (4-level trees, frames up to the
+    whole partition) and a single partition without p."""
+    r = rng(312)
+    n = 150_000
+    tp = getattr(gdk, "TYPE_" + tname)
+    v = _avg_input(r, tname, n)
+    for parts in (True, False):
+        p = np.zeros(n, np.int8)
+        p[0] = 1
+        if parts:
+            p[r.choice(n, 3, replace=False)] = 1
+        starts = np.flatnonzero(p)
+        ends = np.append(starts[1:], n)
+        pid = np.cumsum(p) - 1
+        i = np.arange(n)
+        s = np.maximum(starts[pid], i - r.integers(0, 70_000, n)).astype(np.uint64)
+        e = np.minimum(ends[pid], i + 1 + r.integers(0, 70_000, n)).astype(np.uint64)
+        P = gdk.BAT.from_numpy(gdk.TYPE_bit, p) if parts else None
+        OP = ora.Bat.from_array(ora.TYPE_bit, p) if parts else None
+        got = gdk.GDKanalyticalavg(gdk.BAT.from_numpy(tp, v), P, None, gdk.BAT.from_numpy(gdk.TYPE_oid, s),
+                                   gdk.BAT.from_numpy(gdk.TYPE_oid, e), 1)
+        want = ora.analyticalavg(ora.Bat.from_array(tp, v), OP, None, ora.Bat.from_array(ora.TYPE_oid, s),
+                                 ora.Bat.from_array(ora.TYPE_oid, e), 1)
+        assert np.asarray(got.values()).tobytes() == np.asarray(want.values()).tobytes()
+
+
+def test_window_avg_sqltest(gdk):
+    """analytics03.test's windowed AVG answers on the device."""
+    from helpers import replay_window_avg
+    bad = replay_window_avg(
+        lambda b, p, o, f: gdk.GDKanalyticalavg(b, p, o, None, None, f).values(),
+        lambda tp, a: gdk.BAT.from_numpy(tp, np.asarray(a)), gdk.TYPE_int, gdk.TYPE_flt, gdk.TYPE_bit)
+    assert not bad, bad
+
+
+def test_analytical_avg_edges(gdk):
+    """empty input; hge refused loudly; a frame with only nils is nil."""
+    E = gdk.BAT.from_numpy(gdk.TYPE_lng, np.zeros(0, np.int64))
+    assert gdk.GDKanalyticalavg(E, None, None, None, None, 5).count() == 0
+    H = gdk.BAT.from_numpy(gdk.TYPE_hge, np.zeros(8, np.uint64))
+    with pytest.raises(gdk.GDKError, match="not supported on the device path"):
+        gdk.GDKanalyticalavg(H, None, None, None, None, 5)
+    v = np.array([NIL64, NIL64, 4, NIL64], np.int64)
+    s = gdk.BAT.from_numpy(gdk.TYPE_oid, np.array([0, 0, 1, 3], np.uint64))
+    e = gdk.BAT.from_numpy(gdk.TYPE_oid, np.array([1, 2, 3, 4], np.uint64))
+    got = gdk.GDKanalyticalavg(gdk.BAT.from_numpy(gdk.TYPE_lng, v), None, None, s, e, 1).values()
+    assert np.isnan(got[0]) and np.isnan(got[1]) and got[2] == 4.0 and np.isnan(got[3])

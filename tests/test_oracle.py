@@ -252,3 +252,110 @@ def test_groupavg_oracle(ora):
     want = np.where(v == -(2**63), np.nan, v.astype(np.float64))
     np.testing.assert_array_equal(np.array(a.values()), want)
     assert set(c.values()) == {1}
+
+
+def test_window_avg_sqltest(ora):
+    """analytics03.test's windowed AVG answers (int and real inputs)."""
+    from helpers import replay_window_avg
+    bad = replay_window_avg(
+        lambda b, p, o, f: ora.analyticalavg(b, p, o, None, None, f).values(),
+        lambda tp, a: ora.Bat.from_array(tp, np.asarray(a)), ora.TYPE_int, ora.TYPE_flt, ora.TYPE_bit)
+    assert not bad, bad
+
+
+def _cdiv(a, b):
+    q = abs(a) // abs(b)
+    return q if (a >= 0) == (b > 0) else -q
+
+
+def _avg_iter(x, st):
+    """AVERAGE_ITER (gdk_calc_private.h:231-275) with C integer division"""
+    a, rr, n = st
+    n += 1
+    an, xn = _cdiv(a, n), _cdiv(x, n)
+    z1 = xn - an
+    xn, an = x - xn * n, a - an * n
+    if xn >= an:
+        z2 = xn - an
+        while z2 >= n:
+            z2 -= n
+            z1 += 1
+    else:
+        z2 = an - xn
+        while True:
+            z1 -= 1
+            if z2 < n:
+                z2 = n - z2
+                break
+            z2 -= n
+    a, rr = a + z1, rr + z2
+    if rr >= n:
+        rr, a = rr - n, a + 1
+    return [a, rr, n]
+
+
+def _tree_avg(vals, s, e):
+    """segment-tree AVG of one partition (gdk_analytic.h:63-130): nodes
+    [a, rr, n], inner nodes fold their non-empty children's a"""
+    levels = [[[v, 0, 1] if v is not None else [0, 0, 0] for v in vals]]
+    while len(levels[-1]) > 1 or len(levels) == 1:
+        prev, nxt = levels[-1], []
+        for pos in range(0, len(prev), 16):
+            acc = [0, 0, 0]
+            for c in prev[pos:pos + 16]:
+                if c[2]:
+                    acc = _avg_iter(c[0], acc)
+            nxt.append(acc)
+        levels.append(nxt)
+    out = []
+    for b, t in zip(s, e):
+        acc = [0, 0, 0]
+        if b < t:
+            for lv in levels:
+                pb, pe = b // 16, t // 16
+                if pb == pe:
+                    for x in lv[b:t]:
+                        if x[2]:
+                            acc = _avg_iter(x[0], acc)
+                    break
+                if b != pb * 16:
+                    for x in lv[b:pb * 16 + 16]:
+                        if x[2]:
+                            acc = _avg_iter(x[0], acc)
+                    pb += 1
+                for x in lv[pe * 16:t]:
+                    if x[2]:
+                        acc = _avg_iter(x[0], acc)
+                b, t = pb, pe
+        out.append(math.nan if acc[2] == 0 else acc[0] + acc[1] / acc[2])
+    return out
+
+
+def test_window_avg_tree_oracle(ora):
+    """The oracle's general-frame AVG replays the reference's segment tree
+    (average of child averages, not the exact frame average), checked against
+    an independent Python restatement on two partitions."""
+    r = np.random.default_rng(11)
+    sizes = [700, 300]
+    n = sum(sizes)
+    v = r.integers(-10**12, 10**12, n).astype(np.int64)
+    v[r.random(n) < 0.05] = -(2**63)
+    p = np.zeros(n, np.int8)
+    p[0] = 1
+    p[sizes[0]] = 1
+    s = np.empty(n, np.uint64)
+    e = np.empty(n, np.uint64)
+    k = 0
+    for sz in sizes:
+        for i in range(sz):
+            s[k + i] = k + max(0, i - int(r.integers(0, 300)))
+            e[k + i] = k + min(sz, i + 1 + int(r.integers(0, 300)))
+        k += sz
+    got = ora.analyticalavg(ora.Bat.from_array(ora.TYPE_lng, v), ora.Bat.from_array(ora.TYPE_bit, p), None,
+                            ora.Bat.from_array(ora.TYPE_oid, s), ora.Bat.from_array(ora.TYPE_oid, e), 1).values()
+    k = 0
+    for sz in sizes:
+        vals = [None if x == -(2**63) else int(x) for x in v[k:k + sz]]
+        want = _tree_avg(vals, [int(x) - k for x in s[k:k + sz]], [int(x) - k for x in e[k:k + sz]])
+        np.testing.assert_array_equal(np.array(got[k:k + sz]), np.array(want))
+        k += sz
