@@ -368,6 +368,80 @@ k_lower_bounds(const oid *a, BUN n, oid lo, oid hi, BUN *out)
 	out[3] = q > p ? a[q - 1] : 0;
 }
 
+// complex candidate lists (gdk/gdk_cand.h:23-38): a void BAT whose vheap
+// holds a ccand_t header {type:1, firstbit:48} and then either the
+// excluded oids (CAND_NEGOID, cand_except) or 32-bit mask words
+// (CAND_MSK, cand_mask).  cand_init (gdk_cand.c:455-490) materialises them
+// on the device into an ordered oid list (one flag pass + the ordered
+// compaction); the lists stay alive in a small per-thread ring until later
+// cand_init calls of the same thread replace them (operators synchronise
+// before returning, so a list is never replaced while a kernel reads it).
+__global__ void
+k_cand_negoid(int8_t *flags, BUN R)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < R; i += (BUN) gridDim.x * blockDim.x)
+		flags[i] = 1;
+}
+
+__global__ void
+k_cand_negoid_clear(int8_t *flags, BUN R, oid seq, const oid *exc, BUN nexc)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < nexc; i += (BUN) gridDim.x * blockDim.x) {
+		const oid x = exc[i];
+		if (x >= seq && x - seq < R)
+			flags[x - seq] = 0;
+	}
+}
+
+__global__ void
+k_cand_mask(int8_t *flags, BUN nbits, const uint32_t *mask)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < nbits; i += (BUN) gridDim.x * blockDim.x)
+		flags[i] = (int8_t) ((mask[i >> 5] >> (i & 31)) & 1);
+}
+
+static thread_local mgdk_bat *cand_ring[4];
+static thread_local unsigned cand_ring_next;
+
+static mgdk_bat *
+complex_cand(const mgdk_bat *s)
+{
+	uint64_t *hdr = (uint64_t *) pinned(64);
+	if (hdr == nullptr ||
+	    !hip_ok(hipMemcpyAsync(hdr, s->tvheap, 8, hipMemcpyDeviceToHost, stream()), "hipMemcpyAsync") || !sync())
+		return nullptr;
+	const bool msk = (*hdr & 1) != 0;
+	const oid firstbit = (*hdr >> 1) & ((1ull << 48) - 1);
+	const char *payload = (const char *) s->tvheap + 8;
+	const BUN bytes = s->tvheapsize - 8;
+	hipStream_t st = stream();
+	BUN R;
+	oid seq;
+	if (msk) {
+		// ci->seq = tseqbase - firstbit, bit i = candidate seq + i
+		seq = s->tseqbase - firstbit;
+		R = bytes / 4 * 32;
+		DevBuf f(R + 1);
+		if (!f.p)
+			return nullptr;
+		hipLaunchKernelGGL(k_cand_mask, dim3(grid_for(R, 1024, 8192)), dim3(256), 0, st, f.as<int8_t>(), R,
+				   (const uint32_t *) payload);
+		return compact_flags(f.as<int8_t>(), R, seq);
+	}
+	// candidates [tseqbase, tseqbase + count + nexc) minus the exceptions
+	const BUN nexc = bytes / 8;
+	seq = s->tseqbase;
+	R = s->count + nexc;
+	DevBuf f(R + 1);
+	if (!f.p)
+		return nullptr;
+	hipLaunchKernelGGL(k_cand_negoid, dim3(grid_for(R, 1024, 8192)), dim3(256), 0, st, f.as<int8_t>(), R);
+	if (nexc)
+		hipLaunchKernelGGL(k_cand_negoid_clear, dim3(grid_for(nexc, 1024, 8192)), dim3(256), 0, st,
+				   f.as<int8_t>(), R, seq, (const oid *) payload, nexc);
+	return compact_flags(f.as<int8_t>(), R, seq);
+}
+
 int
 cand_init(Cand *ci, const mgdk_bat *b, const mgdk_bat *s)
 {
@@ -384,6 +458,14 @@ cand_init(Cand *ci, const mgdk_bat *b, const mgdk_bat *s)
 	}
 	if (s->count == 0 || (b && b->count == 0))
 		return 0;
+	if (s->ttype == MGDK_void && s->tvheap != nullptr && s->tvheapsize > 8) {
+		mgdk_bat *m = complex_cand(s);
+		if (m == nullptr)
+			return -1;
+		mgdk_BBPunfix(cand_ring[cand_ring_next & 3]);
+		cand_ring[cand_ring_next++ & 3] = m;
+		return cand_init(ci, b, m);
+	}
 	if (s->ttype == MGDK_void) {
 		if (s->tseqbase == MGDK_OID_NIL) {
 			seterr("candidate list with nil seqbase");

@@ -245,6 +245,34 @@ class BAT:
         init()
         return BAT(lib().mgdk_BATdense(hseqbase, tseq, n))
 
+    @classmethod
+    def negoid_cand(cls, tseq, count, exceptions):
+        """A cand_except candidate list (gdk/gdk_cand.h:23-38): the dense
+        range [tseq, tseq + count + len(exceptions)) minus the sorted
+        exception oids, as a void BAT whose vheap holds ccand_t
+        {type = CAND_NEGOID} + the exceptions."""
+        b = cls.dense(tseq, count)
+        exc = np.asarray(exceptions, np.uint64)
+        buf = np.concatenate([np.zeros(1, np.uint64), exc]).tobytes()
+        _chk(lib().mgdk_BATsetvheap(b.ptr, buf, len(buf)))
+        return b
+
+    @classmethod
+    def mask_cand(cls, seq, bits):
+        """A cand_mask candidate list: candidate seq + i for every set bit i
+        of `bits` (bool array); ccand_t {type = CAND_MSK, firstbit} + 32-bit
+        words, tseqbase = the first candidate."""
+        bits = np.asarray(bits, bool)
+        nz = np.flatnonzero(bits)
+        first = int(nz[0]) if nz.size else 0
+        words = np.packbits(np.concatenate([bits, np.zeros((-len(bits)) % 32, bool)]),
+                            bitorder="little").view(np.uint32)
+        b = cls.dense(seq + first, int(nz.size))
+        hdr = np.array([1 | (first << 1)], np.uint64)
+        buf = hdr.tobytes() + words.tobytes()
+        _chk(lib().mgdk_BATsetvheap(b.ptr, buf, len(buf)))
+        return b
+
     # -- properties --
     @property
     def s(self):

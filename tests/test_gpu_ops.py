@@ -588,3 +588,47 @@ def test_groupavg_trivial_paths(gdk, ora):
     G0 = gdk.BAT.from_numpy(gdk.TYPE_oid, np.zeros(0, np.uint64))
     a, c = gdk.BATgroupavg(B, G0, None, True, s=S)
     assert a.count() == 0 and c.count() == 0
+
+
+def test_complex_candidate_lists(gdk, ora):
+    """cand_except / cand_mask candidate lists (gdk/gdk_cand.h:23-38,
+    gdk_cand.c:455-560): a void BAT whose vheap holds the exceptions or the
+    mask.  Every operator must see exactly the candidates the equivalent
+    materialised list holds -- checked on select, thetaselect, calc, sum,
+    groupsum and join against the oracle with the materialised list."""
+    r = rng(61)
+    n = 50_000
+    v = r.integers(-1000, 1000, n).astype(np.int32)
+    v[::53] = gdk.NIL[gdk.TYPE_int]
+    B, OB = gdk.BAT.from_numpy(gdk.TYPE_int, v, hseqbase=100), ora.Bat.from_array(ora.TYPE_int, v, hseqbase=100)
+    # except list over [150, 150 + 30000 + nexc) -- reaches past b's end
+    exc = np.sort(r.choice(np.arange(150, 150 + 30_000), 700, replace=False)).astype(np.uint64)
+    exc = np.unique(np.concatenate([exc, [150, 151]])).astype(np.uint64)   # pruned at the front
+    NEG = gdk.BAT.negoid_cand(150, 30_000, exc)
+    neg_oids = np.setdiff1d(np.arange(150, 150 + 30_000 + len(exc), dtype=np.uint64), exc)
+    # mask over rows 20..60000 (partly before and after b)
+    bits = r.random(60_000) < 0.3
+    MSK = gdk.BAT.mask_cand(20, bits)
+    msk_oids = (20 + np.flatnonzero(bits)).astype(np.uint64)
+    for S, oids in ((NEG, neg_oids), (MSK, msk_oids)):
+        OS = ora.Bat.from_array(ora.TYPE_oid, oids, sorted_=True, key=True, nonil=True)
+        got = gdk.BATselect(B, S, -100, 300, True, False, False).to_numpy()
+        want = np.asarray(ora.BATselect(OB, OS, -100, 300, True, False, False).values())
+        assert np.array_equal(got, want)
+        got = gdk.BATthetaselect(B, S, 0, ">=").to_numpy()
+        want = np.asarray(ora.BATthetaselect(OB, OS, 0, ">=").values())
+        assert np.array_equal(got, want)
+        assert gdk.BATsum(gdk.TYPE_lng, B, s=S) == ora.BATsum(ora.TYPE_lng, OB, s=OS)
+        c = gdk.BATcalcaddcst(B, 7, gdk.TYPE_int, gdk.TYPE_lng, s=S).to_numpy()
+        lo = np.clip(oids, 100, 100 + n).astype(np.int64)
+        keep = oids[(oids >= 100) & (oids < 100 + n)].astype(np.int64) - 100
+        want = np.where(v[keep] == gdk.NIL[gdk.TYPE_int], gdk.NIL[gdk.TYPE_lng], v[keep].astype(np.int64) + 7)
+        assert np.array_equal(c, want), lo.size
+        # join with a complex left candidate list
+        rk = r.permutation(2000).astype(np.int32) - 1000
+        R = gdk.BAT.from_numpy(gdk.TYPE_int, rk)
+        OR = ora.Bat.from_array(ora.TYPE_int, rk)
+        r1, r2 = gdk.BATjoin(B, R, sl=S)
+        o1, o2 = ora.BATjoin(OB, OR, sl=OS)
+        assert np.array_equal(r1.to_numpy(), np.asarray(o1.values()))
+        assert np.array_equal(r2.to_numpy(), np.asarray(o2.values()))
