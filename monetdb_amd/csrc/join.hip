@@ -661,6 +661,7 @@ constexpr int PJ_SUBS = 1;                 // subtiles per histogram workgroup
 constexpr uint32_t PJ_SLOTS = 16384;       // LDS hash slots per build partition (128 KiB)
 constexpr uint32_t PJ_MAXFILL = 12288;     // largest build partition accepted
 constexpr int PJ_MAXPBITS = 11;            // <= 2048 partitions (LDS counters)
+constexpr uint32_t PJ_LDS_SUBS = 4096;     // probe subtiles whose run offsets the probe stages in LDS
 
 // one 32-bit multiplicative (Fibonacci) hash per key: the partition is its
 // top pbits, the LDS home the next 14 bits.  A 64-bit mixer costs two
@@ -924,15 +925,23 @@ k_pj_base(const uint32_t *tot, uint32_t P, uint32_t *base, uint32_t *maxtot)
 }
 
 // one workgroup per partition: LDS table of the build entries, then each
-// probe entry of the partition rewritten in place as (match position + 1 or
-// 0, row)
+// probe entry of the partition is answered and stored, as (match position +
+// 1 or 0, row), at its subtile-major place in the flat array (the column of
+// run offsets deltaT[p][*] staged in LDS)
 __global__ __launch_bounds__(1024) void
-k_pj_probe(const uint2 *bent, const uint32_t *bbase, uint2 *pent, const uint32_t *pbase, int pbits, uint32_t *dupflag)
+k_pj_probe(const uint2 *bent, const uint32_t *bbase, const uint2 *pent, const uint32_t *pbase, int pbits,
+	   const uint32_t *deltaT, uint32_t nsub, uint2 *flat, uint32_t *dupflag)
 {
 	__shared__ unsigned long long tab[PJ_SLOTS];
+	__shared__ uint32_t sdelta[PJ_LDS_SUBS];
 	const uint32_t p = blockIdx.x;
 	for (uint32_t i = threadIdx.x; i < PJ_SLOTS; i += blockDim.x)
 		tab[i] = 0ull;
+	const uint32_t *dcol = deltaT + (size_t) p * nsub;
+	const bool ldsd = nsub <= PJ_LDS_SUBS;
+	if (ldsd)
+		for (uint32_t i = threadIdx.x; i < nsub; i += blockDim.x)
+			sdelta[i] = dcol[i];
 	__syncthreads();
 	const uint32_t b0 = bbase[p], b1 = bbase[p + 1];
 	bool dup = false;
@@ -981,22 +990,46 @@ k_pj_probe(const uint2 *bent, const uint32_t *bbase, uint2 *pent, const uint32_t
 #pragma unroll
 		for (int u = 0; u < U; u++) {
 			const uint32_t e = e0 + u * blockDim.x;
+			const uint32_t sub = en[u].y / PJ_SUBROWS;
 			if (e < q1)
-				pent[e] = en[u];
+				flat[e + (ldsd ? sdelta[sub] : dcol[sub])] = en[u];
 		}
 	}
 }
 
-// one workgroup per subtile (ticketed): matches back into row order
+// deltaT[p][sub] = (subtile-major start of the run of (sub, p)) - (its start
+// in the partition-major entries), mod 2^32: the probe stores entry e of
+// that run at e + delta, so each subtile's results end up contiguous for the
+// restore.  64 x 64 tiles transposed through LDS.
+__global__ __launch_bounds__(256) void
+k_pj_delta(const uint32_t *offT, const uint32_t *poff, const uint32_t *pbase, uint32_t nsub, uint32_t P,
+	   uint32_t *deltaT)
+{
+	__shared__ uint32_t t[64][65];
+	const uint32_t s0 = blockIdx.x * 64, p0 = blockIdx.y * 64;
+	for (uint32_t k = threadIdx.x; k < 64 * 64; k += blockDim.x) {
+		const uint32_t r = k / 64, c = k % 64, sub = s0 + r, p = p0 + c;
+		if (sub < nsub && p < P)
+			t[r][c] = offT[(size_t) sub * P + p] - pbase[p] - poff[(size_t) sub * P + p];
+	}
+	__syncthreads();
+	for (uint32_t k = threadIdx.x; k < 64 * 64; k += blockDim.x) {
+		const uint32_t r = k / 64, c = k % 64, p = p0 + r, sub = s0 + c;
+		if (sub < nsub && p < P)
+			deltaT[(size_t) p * nsub + sub] = t[c][r];
+	}
+}
+
+// one workgroup per subtile (ticketed): matches back into row order; the
+// subtile's probe results are the contiguous range [offT[sub][0],
+// offT[sub + 1][0]) of the flat array
 __global__ __launch_bounds__(1024) void
-k_pj_restore(const uint2 *pent, const uint32_t *poff, const uint32_t *pbase, const uint32_t *offT, uint32_t P,
-	     uint64_t total, BUN n, uint32_t nsub, Side L, Side R, uint32_t *ticket, uint64_t *status, uint64_t *meta,
-	     oid *r1, oid *r2)
+k_pj_restore(const uint2 *flat, const uint32_t *offT, uint32_t P, uint64_t total, BUN n, uint32_t nsub, Side L,
+	     Side R, uint32_t *ticket, uint64_t *status, uint64_t *meta, oid *r1, oid *r2)
 {
 	// res[row + row / 32]: one pad word per 32 rows, so the 32-row runs of
 	// consecutive threads fall in different banks
 	__shared__ uint32_t res[PJ_SUBROWS + PJ_SUBROWS / 32];
-	__shared__ uint32_t fstart[(1u << PJ_MAXPBITS) + 1], src[1u << PJ_MAXPBITS];
 	__shared__ uint32_t wsum[16];
 	__shared__ uint32_t s_sub;
 	__shared__ uint64_t s_pre;
@@ -1009,29 +1042,22 @@ k_pj_restore(const uint2 *pent, const uint32_t *poff, const uint32_t *pbase, con
 	const uint32_t sub = s_sub;
 	const BUN a = (BUN) sub * PJ_SUBROWS;
 	const uint32_t rows = (uint32_t) min((BUN) PJ_SUBROWS, n - a);
-	// the subtile's run of partition p starts at flat index fstart[p] (its
-	// subtile-major offset) and at pbase[p] + poff[sub][p] in the entries
 	const uint32_t f0 = offT[(size_t) sub * P];
 	const uint32_t f1 = sub + 1 < nsub ? offT[(size_t) (sub + 1) * P] : (uint32_t) total;
-	for (uint32_t q = tid; q < P; q += blockDim.x) {
-		fstart[q] = offT[(size_t) sub * P + q] - f0;
-		src[q] = pbase[q] + poff[(size_t) sub * P + q];
-	}
-	if (tid == 0)
-		fstart[P] = f1 - f0;
-	__syncthreads();
-	for (uint32_t j = tid; j < f1 - f0; j += blockDim.x) {
-		uint32_t lo = 0, hi = P;
-		while (hi - lo > 1) {
-			const uint32_t mid = (lo + hi) >> 1;
-			if (fstart[mid] <= j)
-				lo = mid;
-			else
-				hi = mid;
+	constexpr int U = 8;
+	for (uint32_t j0 = f0 + tid; j0 < f1; j0 += U * blockDim.x) {
+		uint2 en[U];
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const uint32_t j = j0 + u * blockDim.x;
+			en[u] = j < f1 ? flat[j] : make_uint2(0, (uint32_t) a);
 		}
-		const uint2 en = pent[src[lo] + (j - fstart[lo])];
-		const uint32_t r = en.y - (uint32_t) a;
-		res[r + (r >> 5)] = en.x;
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const uint32_t r = en[u].y - (uint32_t) a;
+			if (en[u].x)
+				res[r + (r >> 5)] = en[u].x;
+		}
 	}
 	__syncthreads();
 	// thread tid counts the rows [32 tid, 32 tid + 32): a match mask and the
@@ -1156,8 +1182,14 @@ join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_b
 	if (!offT.p ||
 	    exclusive_scan(Pr.cnt->as<uint32_t>(), offT.as<uint32_t>(), (BUN) Pr.nsub * P, &total) < 0)
 		return -1;
+	DevBuf deltaT((size_t) Pr.nsub * P * 4 + 64), flat((size_t) nl * 8 + 64);
+	if (!deltaT.p || !flat.p)
+		return -1;
+	hipLaunchKernelGGL(k_pj_delta, dim3((Pr.nsub + 63) / 64, (P + 63) / 64), dim3(256), 0, st, offT.as<uint32_t>(),
+			   Pr.off->as<uint32_t>(), Pr.base->as<uint32_t>(), Pr.nsub, P, deltaT.as<uint32_t>());
 	hipLaunchKernelGGL(k_pj_probe, dim3(P), dim3(1024), 0, st, B.ent->as<uint2>(), B.base->as<uint32_t>(),
-			   Pr.ent->as<uint2>(), Pr.base->as<uint32_t>(), pbits, &meta32[2]);
+			   Pr.ent->as<uint2>(), Pr.base->as<uint32_t>(), pbits, deltaT.as<uint32_t>(), Pr.nsub,
+			   flat.as<uint2>(), &meta32[2]);
 	if (!hip_ok(hipMemcpyAsync(h, meta32, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
 		return -1;
 	if (h[2])
@@ -1169,9 +1201,9 @@ join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_b
 		unfix2(ra, rb);
 		return -1;
 	}
-	hipLaunchKernelGGL(k_pj_restore, dim3(Pr.nsub), dim3(1024), 0, st, Pr.ent->as<uint2>(), Pr.off->as<uint32_t>(),
-			   Pr.base->as<uint32_t>(), offT.as<uint32_t>(), P, total, nl, Pr.nsub, L, R, (uint32_t *) sc,
-			   (uint64_t *) sc + 8, meta, (oid *) ra->theap, (oid *) rb->theap);
+	hipLaunchKernelGGL(k_pj_restore, dim3(Pr.nsub), dim3(1024), 0, st, flat.as<uint2>(), offT.as<uint32_t>(), P,
+			   total, nl, Pr.nsub, L, R, (uint32_t *) sc, (uint64_t *) sc + 8, meta, (oid *) ra->theap,
+			   (oid *) rb->theap);
 	uint64_t *h64 = (uint64_t *) pinned(64);
 	if (!hip_ok(hipMemcpyAsync(h64, meta, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
 		unfix2(ra, rb);
