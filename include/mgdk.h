@@ -92,6 +92,11 @@ mgdk_bat *mgdk_BATthetaselect(mgdk_bat *b, mgdk_bat *s, const void *val, const c
 
 /* ---- project (gdk/gdk.h:2273; gdk/gdk_project.c:857) ------------------ */
 mgdk_bat *mgdk_BATproject(mgdk_bat *l, mgdk_bat *r);
+/* BATproject2 (gdk.h:2274, gdk_project.c:590): l projected over r1 ++ r2
+ * (r2's head oids follow r1's); BATprojectchain (gdk.h:2275,
+ * gdk_project.c:879): NULL-terminated chain bats[0] . bats[1] . ... */
+mgdk_bat *mgdk_BATproject2(mgdk_bat *l, mgdk_bat *r1, mgdk_bat *r2);
+mgdk_bat *mgdk_BATprojectchain(mgdk_bat **bats);
 
 /* ---- calc (gdk/gdk_calc.h:36-44; gdk_calc_addsub.c:1480,1549,3166,3225,3280;
  *      gdk_calc_mul.c:2085,2092).  Constants are given as (pointer, type). */

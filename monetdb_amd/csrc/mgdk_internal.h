@@ -79,6 +79,11 @@ struct Cand {
 // canditer_init (gdk/gdk_cand.c:407): clip s to b's [hseqbase, hseqbase+count)
 int cand_init(Cand *ci, const mgdk_bat *b, const mgdk_bat *s);
 
+// a cand_except / cand_mask list (void BAT + ccand_t vheap) as a new ordered
+// oid list (BATunmask, gdk_cand.c); the caller owns the result
+mgdk_bat *unmask_cand(const mgdk_bat *s);
+inline bool is_complex_cand(const mgdk_bat *s) { return s->ttype == MGDK_void && s->tvheap && s->tvheapsize > 8; }
+
 // ordered compaction (select.hip): sorted positions base+i with flags[i]==1;
 // the result may be a dense (void) BAT.  Uses the thread's scratch buffer.
 mgdk_bat *compact_flags(const int8_t *flags, BUN n, oid base, bool nonzero = false);

@@ -74,6 +74,181 @@ launch(const oid *l, BUN n, const void *r, oid rseq, BUN rcnt, const void *nilp,
 			   nilv, (T *) out, flags);
 }
 
+
+// ---- BATproject2 / BATprojectchain (gdk/gdk_project.c:590, :879) --------
+//
+// One fused gather: every output row follows its oid through the chain of
+// oid columns (no intermediate is materialised) and then reads the value
+// from the last column -- or, for BATproject2, from whichever of r1 / r2
+// (r2 following r1 in head oids) holds it.
+
+constexpr int CHAIN_MAX = 8;
+
+struct ColRef {
+	const void *t;       // NULL: dense (void) column, value = tseq + (o - hlo)
+	oid hlo;
+	BUN cnt;
+	oid tseq;
+};
+
+struct Chain {
+	ColRef l0;           // the first (oid) column, read by position
+	ColRef lv[CHAIN_MAX];
+	int nl;              // intermediate oid columns
+	ColRef f[2];         // final value column(s)
+	int nf;
+};
+
+template <typename T>
+__device__ __forceinline__ T
+colval(const ColRef &c, oid off)
+{
+	if (c.t == nullptr)
+		return (T) (c.tseq == MGDK_OID_NIL ? MGDK_OID_NIL : c.tseq + off);
+	return ((const T *) c.t)[off];
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void
+k_project_chain(Chain c, BUN n, T nilv, T *out, uint32_t *flags)
+{
+	uint32_t bad = 0, nil = 0;
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		oid o = colval<oid>(c.l0, i);
+		bool isnil = false;
+		for (int k = 0; k < c.nl && !isnil; k++) {
+			if (o == MGDK_OID_NIL) {
+				isnil = true;
+				break;
+			}
+			if (o < c.lv[k].hlo || o - c.lv[k].hlo >= c.lv[k].cnt) {
+				bad = 1;
+				isnil = true;
+				break;
+			}
+			o = colval<oid>(c.lv[k], o - c.lv[k].hlo);
+		}
+		T v = nilv;
+		if (!isnil && o == MGDK_OID_NIL)
+			isnil = true;
+		if (!isnil) {
+			if (o >= c.f[0].hlo && o - c.f[0].hlo < c.f[0].cnt)
+				v = colval<T>(c.f[0], o - c.f[0].hlo);
+			else if (c.nf > 1 && o >= c.f[1].hlo && o - c.f[1].hlo < c.f[1].cnt)
+				v = colval<T>(c.f[1], o - c.f[1].hlo);
+			else
+				bad = 1;
+		}
+		nil |= isnil;
+		out[i] = v;
+	}
+	bad = block_reduce(bad, [](uint32_t x, uint32_t y) { return x | y; });
+	nil = block_reduce(nil, [](uint32_t x, uint32_t y) { return x | y; });
+	if (threadIdx.x == 0) {
+		publish_or(&flags[0], bad);
+		publish_or(&flags[1], nil);
+	}
+}
+
+ColRef
+colref(const mgdk_bat *b)
+{
+	ColRef c;
+	c.t = b->ttype == MGDK_void ? nullptr : b->theap;
+	c.hlo = b->hseqbase;
+	c.cnt = b->count;
+	c.tseq = b->tseqbase;
+	return c;
+}
+
+// run the fused gather; the value type comes from fin[0]
+mgdk_bat *
+run_chain(Chain &c, BUN n, oid hseq, const mgdk_bat *fin0, const mgdk_bat *fin1, bool *nil_seen)
+{
+	const int rt = fin0->ttype;
+	const int ot = rt == MGDK_void ? MGDK_oid : rt;
+	const int w = rt == MGDK_void ? 8 : fin0->twidth;
+	if (fin1 && ((fin1->ttype == MGDK_void ? 8 : fin1->twidth) != w ||
+		     (rt == MGDK_str && fin1->tvheap != fin0->tvheap) ||
+		     (basetype(fin1->ttype == MGDK_void ? MGDK_oid : fin1->ttype) != basetype(ot)))) {
+		seterr("42000!BATproject2: r1 and r2 must have the same type (and, for str, share their heap) on the "
+		       "device path");
+		return nullptr;
+	}
+	const int alloc_t = rt != MGDK_str ? ot : w == 1 ? MGDK_bte : w == 2 ? MGDK_sht : w == 4 ? MGDK_int : MGDK_lng;
+	mgdk_bat *bn = newbat(hseq, alloc_t, n);
+	if (bn == nullptr)
+		return nullptr;
+	if (rt == MGDK_str) {
+		bn->ttype = MGDK_str;
+		share_vheap(bn, fin0);
+	}
+	uint32_t *flags = (uint32_t *) meta_buf();
+	if (!hip_ok(hipMemsetAsync(flags, 0, 16, stream()), "memset")) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	const dim3 g(grid_for(n, 1024, 256 * 16)), blk(256);
+	hipStream_t st = stream();
+	alignas(16) unsigned char nilv[16] = {0};
+	const int bt = rt == MGDK_str ? -w : basetype(ot);
+	switch (bt) {
+	case MGDK_bte: *(int8_t *) nilv = INT8_MIN; hipLaunchKernelGGL((k_project_chain<int8_t>), g, blk, 0, st, c, n, *(int8_t *) nilv, (int8_t *) bn->theap, flags); break;
+	case MGDK_sht: *(int16_t *) nilv = INT16_MIN; hipLaunchKernelGGL((k_project_chain<int16_t>), g, blk, 0, st, c, n, *(int16_t *) nilv, (int16_t *) bn->theap, flags); break;
+	case MGDK_int: *(int32_t *) nilv = INT32_MIN; hipLaunchKernelGGL((k_project_chain<int32_t>), g, blk, 0, st, c, n, *(int32_t *) nilv, (int32_t *) bn->theap, flags); break;
+	case MGDK_flt: { const float f = __builtin_nanf(""); uint32_t u; memcpy(&u, &f, 4); hipLaunchKernelGGL((k_project_chain<uint32_t>), g, blk, 0, st, c, n, u, (uint32_t *) bn->theap, flags); break; }
+	case MGDK_lng: hipLaunchKernelGGL((k_project_chain<int64_t>), g, blk, 0, st, c, n, (int64_t) INT64_MIN, (int64_t *) bn->theap, flags); break;
+	case MGDK_oid: hipLaunchKernelGGL((k_project_chain<uint64_t>), g, blk, 0, st, c, n, (uint64_t) MGDK_OID_NIL, (uint64_t *) bn->theap, flags); break;
+	case MGDK_dbl: { const double d = __builtin_nan(""); uint64_t u; memcpy(&u, &d, 8); hipLaunchKernelGGL((k_project_chain<uint64_t>), g, blk, 0, st, c, n, u, (uint64_t *) bn->theap, flags); break; }
+	case MGDK_hge: hipLaunchKernelGGL((k_project_chain<hge>), g, blk, 0, st, c, n, NilOf<hge>::v(), (hge *) bn->theap, flags); break;
+	case -1: hipLaunchKernelGGL((k_project_chain<uint8_t>), g, blk, 0, st, c, n, (uint8_t) 0, (uint8_t *) bn->theap, flags); break;
+	case -2: hipLaunchKernelGGL((k_project_chain<uint16_t>), g, blk, 0, st, c, n, (uint16_t) 0, (uint16_t *) bn->theap, flags); break;
+	case -4: hipLaunchKernelGGL((k_project_chain<uint32_t>), g, blk, 0, st, c, n, (uint32_t) 0, (uint32_t *) bn->theap, flags); break;
+	case -8: hipLaunchKernelGGL((k_project_chain<uint64_t>), g, blk, 0, st, c, n, (uint64_t) 0, (uint64_t *) bn->theap, flags); break;
+	default:
+		seterr("42000!BATproject: type %s not supported on the device path", atomname(rt));
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	uint32_t *h = (uint32_t *) pinned(16);
+	if (h == nullptr || !hip_ok(hipMemcpyAsync(h, flags, 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	if (h[0]) {
+		seterr("does not match always\n");
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	if (h[1] && rt == MGDK_str) {
+		seterr("42000!BATproject: nil oid into a str column unsupported on the device path");
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	bn->count = n;
+	bn->tnil = h[1] != 0;
+	*nil_seen = h[1] != 0;
+	return bn;
+}
+
+// l as a ColRef (complex candidate lists materialised into *tmp)
+int
+left_ref(mgdk_bat *l, ColRef &c, mgdk_bat **tmp)
+{
+	*tmp = nullptr;
+	if (is_complex_cand(l)) {
+		mgdk_bat *m = unmask_cand(l);
+		if (m == nullptr)
+			return -1;
+		*tmp = m;
+		c = colref(m);
+		c.hlo = l->hseqbase;
+		return 0;
+	}
+	c = colref(l);
+	return 0;
+}
+
 }  // namespace
 
 extern "C" mgdk_bat *
@@ -86,6 +261,16 @@ mgdk_BATproject(mgdk_bat *l, mgdk_bat *r)
 	if (l->ttype != MGDK_void && l->ttype != MGDK_oid) {
 		seterr("BATproject: left must be oid");
 		return nullptr;
+	}
+	if (is_complex_cand(l)) {
+		// candidate list with exceptions or a bitmask (gdk_project.c:656-670)
+		mgdk_bat *m = unmask_cand(l);
+		if (m == nullptr)
+			return nullptr;
+		m->hseqbase = l->hseqbase;
+		mgdk_bat *bn = mgdk_BATproject(m, r);
+		mgdk_BBPunfix(m);
+		return bn;
 	}
 	ProfScope prof("project");
 	const BUN n = l->count;
@@ -186,5 +371,155 @@ mgdk_BATproject(mgdk_bat *l, mgdk_bat *r)
 	bn->tsorted = n <= 1 || (l->tsorted && r->tsorted) || (l->trevsorted && r->trevsorted) || r->count <= 1;
 	bn->trevsorted = n <= 1 || (l->tsorted && r->trevsorted) || (l->trevsorted && r->tsorted) || r->count <= 1;
 	bn->tkey = n <= 1 || (l->tkey && r->tkey);
+	return bn;
+}
+extern "C" mgdk_bat *
+mgdk_BATproject2(mgdk_bat *l, mgdk_bat *r1, mgdk_bat *r2)
+{
+	if (l == nullptr || r1 == nullptr) {
+		seterr("BATproject2: NULL argument");
+		return nullptr;
+	}
+	if (r2 == nullptr)
+		return mgdk_BATproject(l, r1);
+	if (r1->hseqbase + r1->count != r2->hseqbase) {
+		seterr("BATproject2: r2 must follow r1");
+		return nullptr;
+	}
+	if (r1->count == 0)        // gdk_project.c:613-620
+		return mgdk_BATproject(l, r2);
+	if (l->ttype == MGDK_void && !is_complex_cand(l) && l->count > 0 && l->tseqbase != MGDK_OID_NIL) {
+		// dense l: a slice of r1 or r2 when it lies inside one of them (:622-645)
+		const oid lo = l->tseqbase, hi = l->tseqbase + l->count;
+		if ((lo >= r1->hseqbase && hi <= r1->hseqbase + r1->count) || lo >= r2->hseqbase)
+			return mgdk_BATproject(l, lo >= r2->hseqbase ? r2 : r1);
+		if (lo < r1->hseqbase || hi > r2->hseqbase + r2->count) {
+			seterr("does not match always\n");
+			return nullptr;
+		}
+	}
+	if (l->ttype != MGDK_void && l->ttype != MGDK_oid) {
+		seterr("BATproject2: left must be oid");
+		return nullptr;
+	}
+	ProfScope prof("project2");
+	Chain c{};
+	mgdk_bat *tmp;
+	if (left_ref(l, c.l0, &tmp) < 0)
+		return nullptr;
+	const BUN n = tmp ? tmp->count : l->count;
+	c.nl = 0;
+	c.f[0] = colref(r1);
+	c.f[1] = colref(r2);
+	c.nf = 2;
+	bool nils = false;
+	mgdk_bat *bn = run_chain(c, n, l->hseqbase, r1, r2, &nils);
+	mgdk_BBPunfix(tmp);
+	if (bn) {
+		bn->tnonil = !nils && l->tnonil && r1->tnonil && r2->tnonil;
+		bn->tsorted = bn->trevsorted = bn->tkey = n <= 1;
+	}
+	return bn;
+}
+
+// BATprojectchain (gdk_project.c:879-1164): bats is NULL-terminated
+extern "C" mgdk_bat *
+mgdk_BATprojectchain(mgdk_bat **bats)
+{
+	int n = 0;
+	while (bats && bats[n])
+		n++;
+	if (n == 0) {
+		seterr("must have BAT arguments\n");
+		return nullptr;
+	}
+	mgdk_bat *b = bats[n - 1];
+	if (n == 1)
+		return mgdk_BATslice(b, 0, b->count);
+	// drop identity steps (dense, hseqbase == tseqbase == next hseqbase, same count)
+	mgdk_bat *keep[64];
+	int k = 0;
+	for (int i = 0; i < n; i++) {
+		mgdk_bat *x = bats[i];
+		if (i + 1 < n && x->ttype == MGDK_void && !is_complex_cand(x) && x->tseqbase != MGDK_OID_NIL &&
+		    x->hseqbase == x->tseqbase && x->tseqbase == bats[i + 1]->hseqbase && x->count == bats[i + 1]->count)
+			continue;
+		if (k == 64 || k - 1 > CHAIN_MAX) {
+			seterr("42000!BATprojectchain: chains longer than %d not supported on the device path", CHAIN_MAX + 2);
+			return nullptr;
+		}
+		keep[k++] = x;
+	}
+	if (k == 1)
+		return mgdk_BATslice(keep[0], 0, keep[0]->count);
+	if (k == 2)
+		return mgdk_BATproject(keep[0], keep[1]);
+	bool allnil = false, issorted = true, nonil = true;
+	for (int i = 0; i < k; i++) {
+		allnil |= keep[i]->ttype == MGDK_void && !is_complex_cand(keep[i]) && keep[i]->tseqbase == MGDK_OID_NIL;
+		issorted &= keep[i]->tsorted != 0;
+		if (i + 1 < k)
+			nonil &= keep[i]->tnonil != 0;
+	}
+	ProfScope prof("projectchain");
+	Chain c{};
+	mgdk_bat *tmp[CHAIN_MAX + 1] = {nullptr};
+	int ntmp = 0;
+	auto cleanup = [&]() {
+		for (int i = 0; i < ntmp; i++)
+			mgdk_BBPunfix(tmp[i]);
+	};
+	if (left_ref(keep[0], c.l0, &tmp[ntmp]) < 0)
+		return nullptr;
+	const BUN cnt = tmp[ntmp] ? tmp[ntmp]->count : keep[0]->count;
+	ntmp += tmp[ntmp] != nullptr;
+	if (allnil || cnt == 0) {
+		cleanup();
+		alignas(16) unsigned char nilv[16] = {0};
+		const int rt = b->ttype;
+		switch (basetype(rt)) {
+		case MGDK_bte: *(int8_t *) nilv = INT8_MIN; break;
+		case MGDK_sht: *(int16_t *) nilv = INT16_MIN; break;
+		case MGDK_int: *(int32_t *) nilv = INT32_MIN; break;
+		case MGDK_lng: *(int64_t *) nilv = INT64_MIN; break;
+		case MGDK_oid: case MGDK_void: *(uint64_t *) nilv = MGDK_OID_NIL; break;
+		case MGDK_hge: nilv[15] = 0x80; break;
+		case MGDK_flt: { const float f = __builtin_nanf(""); memcpy(nilv, &f, 4); break; }
+		case MGDK_dbl: { const double d = __builtin_nan(""); memcpy(nilv, &d, 8); break; }
+		default:
+			seterr("42000!BATprojectchain: nil projection of %s unsupported", atomname(rt));
+			return nullptr;
+		}
+		return mgdk_BATconstant(keep[0]->hseqbase, rt == MGDK_oid ? MGDK_void : rt, nilv, cnt);
+	}
+	c.nl = 0;
+	for (int i = 1; i + 1 < k; i++) {
+		if (keep[i]->ttype != MGDK_void && keep[i]->ttype != MGDK_oid) {
+			cleanup();
+			seterr("BATprojectchain: all but the last BAT must be oid");
+			return nullptr;
+		}
+		if (left_ref(keep[i], c.lv[c.nl], &tmp[ntmp]) < 0) {
+			cleanup();
+			return nullptr;
+		}
+		if (tmp[ntmp]) {
+			c.lv[c.nl].cnt = tmp[ntmp]->count;
+			ntmp++;
+		}
+		c.nl++;
+	}
+	c.f[0] = colref(b);
+	c.nf = 1;
+	bool nils = false;
+	mgdk_bat *bn = run_chain(c, cnt, keep[0]->hseqbase, b, nullptr, &nils);
+	cleanup();
+	if (bn) {
+		// gdk_project.c:1141-1146
+		bn->tsorted = cnt <= 1 || issorted;
+		bn->trevsorted = cnt <= 1;
+		bn->tnonil = nonil && b->tnonil && !nils;
+		bn->tkey = cnt <= 1;
+	}
 	return bn;
 }

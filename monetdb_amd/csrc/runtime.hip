@@ -403,8 +403,8 @@ k_cand_mask(int8_t *flags, BUN nbits, const uint32_t *mask)
 static thread_local mgdk_bat *cand_ring[4];
 static thread_local unsigned cand_ring_next;
 
-static mgdk_bat *
-complex_cand(const mgdk_bat *s)
+mgdk_bat *
+unmask_cand(const mgdk_bat *s)
 {
 	uint64_t *hdr = (uint64_t *) pinned(64);
 	if (hdr == nullptr ||
@@ -459,7 +459,7 @@ cand_init(Cand *ci, const mgdk_bat *b, const mgdk_bat *s)
 	if (s->count == 0 || (b && b->count == 0))
 		return 0;
 	if (s->ttype == MGDK_void && s->tvheap != nullptr && s->tvheapsize > 8) {
-		mgdk_bat *m = complex_cand(s);
+		mgdk_bat *m = unmask_cand(s);
 		if (m == nullptr)
 			return -1;
 		mgdk_BBPunfix(cand_ring[cand_ring_next & 3]);

@@ -83,6 +83,8 @@ _SIGS = {
     "mgdk_BATselect": (P, [P, P, C.c_void_p, C.c_void_p, C.c_bool, C.c_bool, C.c_bool, C.c_bool]),
     "mgdk_BATthetaselect": (P, [P, P, C.c_void_p, C.c_char_p]),
     "mgdk_BATproject": (P, [P, P]),
+    "mgdk_BATproject2": (P, [P, P, P]),
+    "mgdk_BATprojectchain": (P, [C.c_void_p]),
     "mgdk_BATcalcadd": (P, [P, P, P, P, C.c_int]),
     "mgdk_BATcalcsub": (P, [P, P, P, P, C.c_int]),
     "mgdk_BATcalcmul": (P, [P, P, P, P, C.c_int]),
@@ -351,6 +353,17 @@ def BATselect(b, s, tl, th, li, hi, anti, nil_matches=False):
 def BATthetaselect(b, s, val, op):
     keep = []
     return BAT(lib().mgdk_BATthetaselect(b.ptr, _p(s), _valptr(b.ttype, val, keep), op.encode()))
+
+
+def BATproject2(l, r1, r2):
+    """BATproject2(l, r1, r2) (gdk/gdk_project.c:590): l over r1 ++ r2."""
+    return BAT(lib().mgdk_BATproject2(l.ptr, r1.ptr, _p(r2)))
+
+
+def BATprojectchain(bats):
+    """BATprojectchain (gdk/gdk_project.c:879): bats[0] . bats[1] . ... in one pass."""
+    arr = (P * (len(bats) + 1))(*[b.ptr for b in bats], None)
+    return BAT(lib().mgdk_BATprojectchain(C.cast(arr, C.c_void_p)))
 
 
 def BATproject(l, r):

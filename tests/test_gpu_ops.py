@@ -632,3 +632,78 @@ def test_complex_candidate_lists(gdk, ora):
         o1, o2 = ora.BATjoin(OB, OR, sl=OS)
         assert np.array_equal(r1.to_numpy(), np.asarray(o1.values()))
         assert np.array_equal(r2.to_numpy(), np.asarray(o2.values()))
+
+
+def _same(got, want):
+    g, w = got.values(), want.values()
+    if isinstance(g, list) or isinstance(w, list):
+        return list(g) == list(w)
+    return np.asarray(g).tobytes() == np.asarray(w).tobytes()
+
+
+@pytest.mark.parametrize("tname", ["int", "lng", "hge", "dbl", "oid"])
+def test_projectchain_and_project2(gdk, ora, tname):
+    """BATprojectchain (gdk_project.c:879) = the sequence of BATproject calls
+    it stands for (its own definition), fused on the device; BATproject2
+    (gdk_project.c:590) = BATproject over r1 ++ r2.  Checked against the
+    oracle's BATproject; nil oids, dense steps, complex candidate lists and
+    the "does not match always" error included."""
+    r = rng(71)
+    tp = getattr(gdk, "TYPE_" + tname)
+    n3 = 40_000
+    if tname == "hge":
+        vals = r.integers(-2**62, 2**62, 2 * n3).astype(np.uint64)
+    elif tname == "dbl":
+        vals = r.standard_normal(n3)
+    elif tname == "oid":
+        vals = r.integers(0, 2**40, n3).astype(np.uint64)
+    else:
+        vals = r.integers(-10**6, 10**6, n3).astype(gdk.NP[tp])
+    V = gdk.BAT.from_numpy(tp, vals, hseqbase=1000)
+    OV = ora.Bat.from_array(tp, vals, hseqbase=1000)
+    # chain: a (oid into b's heads) . b (oid into V's heads) . V
+    b = (1000 + r.integers(0, n3, 30_000)).astype(np.uint64)
+    b[::97] = gdk.OID_NIL
+    a = r.integers(0, 30_000, 25_000).astype(np.uint64) + 50
+    A, B = gdk.BAT.from_numpy(gdk.TYPE_oid, a), gdk.BAT.from_numpy(gdk.TYPE_oid, b, hseqbase=50)
+    OA, OBb = ora.Bat.from_array(ora.TYPE_oid, a), ora.Bat.from_array(ora.TYPE_oid, b, hseqbase=50)
+    got = gdk.BATprojectchain([A, B, V])
+    want = ora.BATproject(ora.BATproject(OA, OBb), OV)
+    assert _same(got, want)
+    assert got.s.tnil
+    # an identity (dense) step is skipped; a dense first step
+    D = gdk.BAT.dense(50, 30_000, hseqbase=50)
+    got2 = gdk.BATprojectchain([A, D, B, V])
+    assert _same(got2, want)
+    C0 = gdk.BAT.dense(60, 1000)
+    got3 = gdk.BATprojectchain([C0, B, V])
+    want3 = ora.BATproject(ora.BATproject(ora.Bat.from_array(ora.TYPE_oid, np.arange(60, 1060, dtype=np.uint64)),
+                                          OBb), OV)
+    assert _same(got3, want3)
+    # complex candidate list as the first step
+    M = gdk.BAT.negoid_cand(60, 900, np.array([70, 500, 999], np.uint64))
+    keep = np.setdiff1d(np.arange(60, 963, dtype=np.uint64), [70, 500, 999])
+    got4 = gdk.BATprojectchain([M, B, V])
+    want4 = ora.BATproject(ora.BATproject(ora.Bat.from_array(ora.TYPE_oid, keep), OBb), OV)
+    assert _same(got4, want4)
+    bad = a.copy()
+    bad[7] = 10**9
+    with pytest.raises(gdk.GDKError, match="does not match always"):
+        gdk.BATprojectchain([gdk.BAT.from_numpy(gdk.TYPE_oid, bad), B, V])
+    # BATproject2: r1 = V[:m], r2 = V[m:]
+    m = n3 // 3
+    if tname == "hge":
+        v1, v2 = vals[:2 * m], vals[2 * m:]
+    else:
+        v1, v2 = vals[:m], vals[m:]
+    R1 = gdk.BAT.from_numpy(tp, v1, hseqbase=1000)
+    R2 = gdk.BAT.from_numpy(tp, v2, hseqbase=1000 + m)
+    got5 = gdk.BATproject2(B, R1, R2)
+    want5 = ora.BATproject(OBb, OV)
+    assert _same(got5, want5)
+    # dense l across the r1 / r2 boundary, and inside r2 (slice)
+    for lo, cnt in ((1000 + m - 5, 10), (1000 + m + 3, 100)):
+        L = gdk.BAT.dense(lo, cnt)
+        got6 = gdk.BATproject2(L, R1, R2)
+        want6 = ora.BATproject(ora.Bat.from_array(ora.TYPE_oid, np.arange(lo, lo + cnt, dtype=np.uint64)), OV)
+        assert _same(got6, want6)
