@@ -119,6 +119,10 @@ mgdk_bat *mgdk_BATgroupcount(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s,
  * MGDK_dbl; cntsp may be NULL; scale divides by 10^scale */
 int mgdk_BATgroupavg(mgdk_bat **bnp, mgdk_bat **cntsp, mgdk_bat *b, mgdk_bat *g, mgdk_bat *e,
 		     mgdk_bat *s, int tp, bool skip_nils, int scale);
+/* BATgroupavg3combine (gdk_calc.h, gdk_aggr.c:2634): combine per-row partial
+ * (avg, rem, cnt) triples of BATgroupavg3 into the rounded group averages */
+mgdk_bat *mgdk_BATgroupavg3combine(mgdk_bat *avg, mgdk_bat *rem, mgdk_bat *cnt, mgdk_bat *g, mgdk_bat *e,
+				   bool skip_nils);
 int mgdk_BATgroupavg3(mgdk_bat **avgp, mgdk_bat **remp, mgdk_bat **cntp,
 		      mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, bool skip_nils);
 mgdk_bat *mgdk_BATgroupmin(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils);

@@ -774,6 +774,35 @@ k_favg_replay(const T *vals, oid off, const uint32_t *perm, const uint64_t *star
 	}
 }
 
+
+// BATgroupavg3combine terms: t = avg * cnt + rem (the row's exact total),
+// c = cnt; both nil where avg is nil.  flags[0]: |avg * cnt| beyond 2^126
+template <typename T>
+__global__ void
+k_avg3c_terms(const T *avg, const long long *rem, const long long *cnt, oid off, BUN n, hge *t, long long *c,
+	      uint32_t *flags)
+{
+	uint32_t big = 0;
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		const T a = avg[off + i];
+		if (a == NilOf<T>::v()) {
+			t[i] = NilOf<hge>::v();
+			c[i] = INT64_MIN;
+			continue;
+		}
+		const long long k = cnt[off + i], r = rem[off + i];
+		const hge ha = (hge) a;
+		const uhge ua = (uhge) (ha < 0 ? -ha : ha), uk = (uhge) (k < 0 ? -(hge) k : (hge) k);
+		// |avg| * |cnt| < 2^126 so the group totals stay inside hge
+		if (ua && uk && ua > ((uhge) 1 << 126) / uk)
+			big = 1;
+		t[i] = ha * (hge) k + (hge) r;
+		c[i] = k;
+	}
+	if (big)
+		atomicOr(flags, 1u);
+}
+
 }  // namespace
 
 extern "C" {
@@ -1069,6 +1098,128 @@ mgdk_BATgroupavg(mgdk_bat **bnp, mgdk_bat **cntsp, mgdk_bat *b, mgdk_bat *g, mgd
 	else
 		mgdk_BBPunfix(cn);
 	return 0;
+}
+
+// BATgroupavg3combine (gdk/gdk_aggr.c:2634-2960): each group's state is
+// folded row by row with combine_averages_TYPE (:2402-2630), which keeps
+// avg * cnt + rem == the exact total; the device sums the rows' totals and
+// counts per group (order independent) and takes the floor average and its
+// remainder, rounded half away from zero (:2702-2716)
+mgdk_bat *
+mgdk_BATgroupavg3combine(mgdk_bat *avg, mgdk_bat *rem, mgdk_bat *cnt, mgdk_bat *g, mgdk_bat *e, bool skip_nils)
+{
+	if (avg == nullptr || rem == nullptr || cnt == nullptr || !int_type(avg->ttype)) {
+		seterr("42000!BATgroupavg3combine: type not supported on the device path");
+		return nullptr;
+	}
+	ProfScope prof("groupavg3combine");
+	AggrInit a;
+	if (aggr_init(&a, avg, g, e, nullptr) < 0)
+		return nullptr;
+	if (a.ci.n != rem->count || a.ci.n != cnt->count) {
+		seterr("input bats not aligned");
+		return nullptr;
+	}
+	const BUN n = a.ci.n, ng = a.ngrp;
+	const int tp = avg->ttype;
+	if (n == 0 || ng == 0) {
+		std::vector<char> nilv(ng * width_of(tp) + 16);
+		for (BUN k = 0; k < ng; k++)
+			put_vec(nilv, tp, k, 0, true);
+		mgdk_bat *bn = upload_new(ng == 0 ? 0 : a.min, tp, nilv.data(), ng);
+		if (bn) {
+			bn->tnil = ng > 0;
+			bn->tnonil = ng == 0;
+		}
+		return bn;
+	}
+	hipStream_t st = stream();
+	mgdk_bat *T = newbat(avg->hseqbase, MGDK_hge, n), *Cb = newbat(avg->hseqbase, MGDK_lng, n);
+	DevBuf fl(64);
+	mgdk_bat *S = nullptr, *C = nullptr, *bn = nullptr;
+	uint32_t *hf = (uint32_t *) pinned(16);
+	if (!T || !Cb || !fl.p || !hip_ok(hipMemsetAsync(fl.p, 0, 64, st), "memset"))
+		goto out;
+	{
+		const oid off = a.ci.seq - avg->hseqbase;
+		const dim3 gr(grid_for(n, 1024, 8192)), blk(256);
+		const long long *R = (const long long *) rem->theap, *K = (const long long *) cnt->theap;
+		switch (basetype(tp)) {
+		case MGDK_bte: hipLaunchKernelGGL((k_avg3c_terms<int8_t>), gr, blk, 0, st, (const int8_t *) avg->theap, R, K, off, n, (hge *) T->theap, (long long *) Cb->theap, fl.as<uint32_t>()); break;
+		case MGDK_sht: hipLaunchKernelGGL((k_avg3c_terms<int16_t>), gr, blk, 0, st, (const int16_t *) avg->theap, R, K, off, n, (hge *) T->theap, (long long *) Cb->theap, fl.as<uint32_t>()); break;
+		case MGDK_int: hipLaunchKernelGGL((k_avg3c_terms<int32_t>), gr, blk, 0, st, (const int32_t *) avg->theap, R, K, off, n, (hge *) T->theap, (long long *) Cb->theap, fl.as<uint32_t>()); break;
+		case MGDK_lng: hipLaunchKernelGGL((k_avg3c_terms<int64_t>), gr, blk, 0, st, (const int64_t *) avg->theap, R, K, off, n, (hge *) T->theap, (long long *) Cb->theap, fl.as<uint32_t>()); break;
+		default: hipLaunchKernelGGL((k_avg3c_terms<hge>), gr, blk, 0, st, (const hge *) avg->theap, R, K, off, n, (hge *) T->theap, (long long *) Cb->theap, fl.as<uint32_t>()); break;
+		}
+		if (!hip_ok(hipMemcpyAsync(hf, fl.p, 4, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+			goto out;
+		if (hf[0]) {
+			seterr("42000!BATgroupavg3combine: |avg * count| beyond 2^126 is not supported on the device path");
+			goto out;
+		}
+		T->count = Cb->count = n;
+		T->tnonil = Cb->tnonil = avg->tnonil;
+		T->tnil = Cb->tnil = !avg->tnonil;
+		// the group's rows in the same candidate order as avg: T / Cb are
+		// aligned with avg's candidates (hseqbase avg->hseqbase + off)
+		T->hseqbase = Cb->hseqbase = a.ci.seq;
+		// sums over the non-nil rows; without skip_nils a group with any nil
+		// avg is nil for good (counted apart: BATgroupsum's own nil rule
+		// differs, gdk_aggr.c:497-527)
+		S = mgdk_BATgroupsum(T, g, e, nullptr, MGDK_hge, true);
+		C = mgdk_BATgroupsum(Cb, g, e, nullptr, MGDK_hge, true);
+		if (!S || !C)
+			goto out;
+		std::vector<unsigned long long> hs(2 * ng), hc(2 * ng);
+		std::vector<long long> nall(ng), nnon(ng);
+		if (!skip_nils && !avg->tnonil) {
+			mgdk_bat *N1 = mgdk_BATgroupcount(avg, g, e, nullptr, MGDK_lng, false);
+			mgdk_bat *N2 = N1 ? mgdk_BATgroupcount(avg, g, e, nullptr, MGDK_lng, true) : nullptr;
+			bool ok = N1 && N2 &&
+				  hip_ok(hipMemcpyAsync(nall.data(), N1->theap, ng * 8, hipMemcpyDeviceToHost, st), "memcpy") &&
+				  hip_ok(hipMemcpyAsync(nnon.data(), N2->theap, ng * 8, hipMemcpyDeviceToHost, st), "memcpy") &&
+				  sync();
+			mgdk_BBPunfix(N1);
+			mgdk_BBPunfix(N2);
+			if (!ok)
+				goto out;
+		}
+		if (!hip_ok(hipMemcpyAsync(hs.data(), S->theap, ng * 16, hipMemcpyDeviceToHost, st), "memcpy") ||
+		    !hip_ok(hipMemcpyAsync(hc.data(), C->theap, ng * 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+			goto out;
+		std::vector<char> out(ng * width_of(tp) + 16);
+		bool nils = false;
+		const hge NIL = NilOf<hge>::v();
+		for (BUN k = 0; k < ng; k++) {
+			const hge sv = (hge) (((uhge) hs[2 * k + 1] << 64) | hs[2 * k]);
+			const hge cv = (hge) (((uhge) hc[2 * k + 1] << 64) | hc[2 * k]);
+			if (sv == NIL || cv == NIL || cv == 0 || nall[k] != nnon[k]) {
+				put_vec(out, tp, k, 0, true);
+				nils = true;
+				continue;
+			}
+			hge q = sv / cv, r = sv % cv;
+			if (r < 0) {
+				q -= 1;
+				r += cv;
+			}
+			if (r > 0 && (q < 0 ? 2 * r > cv : 2 * r >= cv))
+				q += 1;
+			put_vec(out, tp, k, q, false);
+		}
+		bn = upload_new(a.min, tp, out.data(), ng);
+		if (bn) {
+			bn->tnil = nils;
+			bn->tnonil = !nils;
+			bn->tkey = bn->tsorted = bn->trevsorted = ng <= 1;
+		}
+	}
+out:
+	mgdk_BBPunfix(T);
+	mgdk_BBPunfix(Cb);
+	mgdk_BBPunfix(S);
+	mgdk_BBPunfix(C);
+	return bn;
 }
 
 // BATgroupavg3 (gdk/gdk_aggr.c:1996-2110)

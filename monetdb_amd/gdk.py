@@ -98,6 +98,7 @@ _SIGS = {
     "mgdk_BATgroupsum": (P, [P, P, P, P, C.c_int, C.c_bool]),
     "mgdk_BATgroupcount": (P, [P, P, P, P, C.c_int, C.c_bool]),
     "mgdk_BATgroupavg": (C.c_int, [PP, PP, P, P, P, P, C.c_int, C.c_bool, C.c_int]),
+    "mgdk_BATgroupavg3combine": (P, [P, P, P, P, P, C.c_bool]),
     "mgdk_BATgroupavg3": (C.c_int, [PP, PP, PP, P, P, P, P, C.c_bool]),
     "mgdk_BATgroupmin": (P, [P, P, P, P, C.c_int, C.c_bool]),
     "mgdk_BATgroupmax": (P, [P, P, P, P, C.c_int, C.c_bool]),
@@ -449,6 +450,12 @@ def BATgroupavg(b, g, e, skip_nils=True, s=None, scale=0, want_counts=True):
     _chk(lib().mgdk_BATgroupavg(C.byref(a), C.byref(c) if want_counts else None, b.ptr, g.ptr, _p(e),
                                 _p(s), TYPE_dbl, skip_nils, scale))
     return BAT(a), (BAT(c) if want_counts else None)
+
+
+def BATgroupavg3combine(avg, rem, cnt, g, e, skip_nils=True):
+    """BATgroupavg3combine (gdk/gdk_aggr.c:2634): rounded group averages of
+    partial (avg, rem, cnt) rows."""
+    return BAT(lib().mgdk_BATgroupavg3combine(avg.ptr, rem.ptr, cnt.ptr, _p(g), _p(e), skip_nils))
 
 
 def BATgroupavg3(b, g, e, skip_nils=True, s=None):

@@ -15,7 +15,7 @@
  *   calc        gdk/gdk_calc_addsub.c, gdk/gdk_calc_mul.c:23-132,2020-2092,
  *               overflow rules gdk/gdk_calc_private.h:38-140
  *   aggregates  gdk/gdk_aggr.c:65 (BATgroupaggrinit), :708 (dosum), :900, :1018,
- *               :1801 (BATgroupavg), :1996 (BATgroupavg3), :3069 (BATgroupcount), AVERAGE_ITER
+ *               :1801 (BATgroupavg), :1996 (BATgroupavg3), :2634 (combine), :3069 (BATgroupcount), AVERAGE_ITER
  *               gdk/gdk_calc_private.h:231-275
  *   group       gdk/gdk_group.c:657-1347 (first-occurrence numbering)
  *   join        gdk/gdk_join.c:2781-2900 (hash join result order)
@@ -91,6 +91,8 @@ ora_bat *ora_groupcount(const ora_bat *b, const ora_bat *g, const ora_bat *e,
 int ora_groupavg3(ora_bat **avgp, ora_bat **remp, ora_bat **cntp,
 		  const ora_bat *b, const ora_bat *g, const ora_bat *e,
 		  const ora_bat *s, bool skip_nils);
+ora_bat *ora_groupavg3combine(const ora_bat *avg, const ora_bat *rem, const ora_bat *cnt,
+			       const ora_bat *g, const ora_bat *e, bool skip_nils);
 int ora_groupavg(ora_bat **bnp, ora_bat **cntp, const ora_bat *b, const ora_bat *g,
 		 const ora_bat *e, const ora_bat *s, bool skip_nils, int scale);
 ora_bat *ora_groupminmax(const ora_bat *b, const ora_bat *g, const ora_bat *e,

@@ -490,6 +490,83 @@ ora_groupavg3(ora_bat **avgp, ora_bat **remp, ora_bat **cntp,
 	return 0;
 }
 
+/* BATgroupavg3combine (gdk/gdk_aggr.c:2634-2960): each group's (avg, rem,
+ * cnt) state starts at 0 and folds every row in order with
+ * combine_averages_TYPE (:2402-2630): a row with rem < 0 is first
+ * normalised (avg--, rem += cnt); the new state is the floor average of
+ * the exact total avg1*cnt1 + rem1 + avg2*cnt2 + rem2 over cnt1 + cnt2
+ * (the hge branch reaches the same quotient through multdiv).  A nil avg
+ * without skip_nils makes the group nil for good; groups with count 0 are
+ * nil; the rest are rounded half away from zero (:2702-2716). */
+ora_bat *
+ora_groupavg3combine(const ora_bat *avg, const ora_bat *rem, const ora_bat *cnt, const ora_bat *g,
+		     const ora_bat *e, bool skip_nils)
+{
+	aggr_ctx a;
+	if (aggr_init(&a, avg, g, e, NULL) < 0)
+		return NULL;
+	if (a.ci.n != rem->count || a.ci.n != cnt->count) {
+		ora_seterr("input bats not aligned");
+		return NULL;
+	}
+	const int tp = avg->type;
+	ora_bat *bn = ora_new(tp, a.ngrp, a.ngrp ? a.min : 0);
+	ora_hge *av = calloc(a.ngrp + 1, sizeof(ora_hge));
+	int64_t *rm = calloc(a.ngrp + 1, 8), *ct = calloc(a.ngrp + 1, 8);
+	uint8_t *isnil = calloc(a.ngrp + 1, 1);
+	if (!bn || !av || !rm || !ct || !isnil) {
+		ora_free(bn); free(av); free(rm); free(ct); free(isnil);
+		ora_seterr("out of memory");
+		return NULL;
+	}
+	const int64_t *R = rem->base, *K = cnt->base;
+	for (uint64_t i = 0; i < a.ci.n; i++) {
+		ora_oid gid;
+		if (!aggr_gid(&a, i, &gid))
+			continue;
+		ora_hge v2;
+		if (val_at(avg, i, &v2)) {
+			if (!skip_nils)
+				isnil[gid] = 1;
+			continue;
+		}
+		if (isnil[gid])
+			continue;
+		int64_t rem2 = R[i], cnt2 = K[i];
+		if (rem2 < 0) {
+			v2--;
+			rem2 += cnt2;
+		}
+		const int64_t c = ct[gid] + cnt2;
+		ora_hge t = av[gid] * ct[gid] + rm[gid] + v2 * cnt2 + rem2;
+		ora_hge q = t / c, r = t % c;
+		if (r < 0) {
+			q--;
+			r += c;
+		}
+		av[gid] = q;
+		rm[gid] = (int64_t) r;
+		ct[gid] = c;
+	}
+	bool hasnil = false;
+	for (uint64_t k = 0; k < a.ngrp; k++) {
+		if (isnil[k] || ct[k] == 0) {
+			put(tp, bn->base, k, 0, true);
+			hasnil = true;
+			continue;
+		}
+		ora_hge q = av[k];
+		if (rm[k] > 0 && (q < 0 ? 2 * rm[k] > ct[k] : 2 * rm[k] >= ct[k]))
+			q++;
+		put(tp, bn->base, k, q, false);
+	}
+	bn->nil = hasnil;
+	bn->nonil = !hasnil;
+	bn->sorted = bn->revsorted = bn->key = a.ngrp <= 1;
+	free(av); free(rm); free(ct); free(isnil);
+	return bn;
+}
+
 /* BATgroupavg (gdk/gdk_aggr.c:1801-1984): average as dbl.
  * Trivial cases first: no candidates or no groups -> all nil, counts 0
  * (:1834-1853); singleton groups (g dense or key+nonil, e aligned) -> the

@@ -82,6 +82,8 @@ def lib():
         L.ora_groupminmax.restype = P
         L.ora_groupminmax.argtypes = [P, P, P, P, C.c_bool, C.c_bool]
         L.ora_groupavg.argtypes = [C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool, C.c_int]
+        L.ora_groupavg3combine.restype = P
+        L.ora_groupavg3combine.argtypes = [P, P, P, P, P, C.c_bool]
         L.ora_groupavg3.argtypes = [C.POINTER(P), C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool]
         L.ora_join.argtypes = [C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool]
         L.ora_sort.argtypes = [C.POINTER(P), C.POINTER(P), P, C.c_bool, C.c_bool]
@@ -271,6 +273,11 @@ def BATgroupavg(b, g, e, skip_nils=True, s=None, scale=0, want_counts=True):
                           e.ptr if e else None, s.ptr if s else None, skip_nils, scale) < 0:
         raise _err()
     return Bat(a), (Bat(c) if want_counts else None)
+
+
+def BATgroupavg3combine(avg, rem, cnt, g, e, skip_nils=True):
+    return _ret(lib().ora_groupavg3combine(avg.ptr, rem.ptr, cnt.ptr, g.ptr if g else None,
+                                           e.ptr if e else None, skip_nils))
 
 
 def BATgroupavg3(b, g, e, skip_nils=True, s=None):

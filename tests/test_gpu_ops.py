@@ -707,3 +707,40 @@ def test_projectchain_and_project2(gdk, ora, tname):
         got6 = gdk.BATproject2(L, R1, R2)
         want6 = ora.BATproject(ora.Bat.from_array(ora.TYPE_oid, np.arange(lo, lo + cnt, dtype=np.uint64)), OV)
         assert _same(got6, want6)
+
+
+@pytest.mark.parametrize("tname", ["bte", "sht", "int", "lng", "hge"])
+@pytest.mark.parametrize("skip", [True, False])
+def test_groupavg3combine(gdk, ora, tname, skip):
+    """BATgroupavg3combine (gdk_aggr.c:2634) bit-exact against the oracle's
+    row-by-row combine_averages replay: partials from BATgroupavg3 over
+    shards (negative remainders after rounding, empty and nil groups)."""
+    r = rng(81)
+    tp = getattr(gdk, "TYPE_" + tname)
+    bits = {"bte": 8, "sht": 16, "int": 32, "lng": 40, "hge": 40}[tname]
+    n, ng = 30_000, 700
+    v = r.integers(-(2**(bits - 1)) + 1, 2**(bits - 1), n, dtype=np.int64)
+    nilv = -(2**(bits - 1)) if tname in ("bte", "sht", "int") else -(2**63)
+    v[r.random(n) < 0.01] = nilv
+    gid = r.integers(0, ng, n).astype(np.uint64)
+    gid[gid == 5] = 6
+    dt = gdk.NP.get(tp, np.int64)
+    parts = []
+    for sh in np.array_split(np.arange(n), 5):
+        vv = v[sh]
+        data = _hge_pairs(vv) if tname == "hge" else vv.astype(dt)
+        a, rm, c = gdk.BATgroupavg3(gdk.BAT.from_numpy(tp, data, nonil=False),
+                                    gdk.BAT.from_numpy(gdk.TYPE_oid, gid[sh], key=False), None, skip)
+        parts.append((a.to_numpy(), rm.to_numpy(), c.to_numpy(), a.count()))
+    A = np.concatenate([p[0] for p in parts])
+    R = np.concatenate([p[1] for p in parts])
+    K = np.concatenate([p[2] for p in parts])
+    G = np.concatenate([np.arange(p[3], dtype=np.uint64) for p in parts])
+    Ad = A.reshape(-1) if tname == "hge" else A
+    got = gdk.BATgroupavg3combine(gdk.BAT.from_numpy(tp, Ad, nonil=False), gdk.BAT.from_numpy(gdk.TYPE_lng, R),
+                                  gdk.BAT.from_numpy(gdk.TYPE_lng, K), gdk.BAT.from_numpy(gdk.TYPE_oid, G, key=False),
+                                  None, skip)
+    want = ora.BATgroupavg3combine(ora.Bat.from_array(tp, Ad), ora.Bat.from_array(ora.TYPE_lng, R),
+                                   ora.Bat.from_array(ora.TYPE_lng, K), ora.Bat.from_array(ora.TYPE_oid, G),
+                                   None, skip)
+    assert _same(got, want)

@@ -359,3 +359,29 @@ def test_window_avg_tree_oracle(ora):
         want = _tree_avg(vals, [int(x) - k for x in s[k:k + sz]], [int(x) - k for x in e[k:k + sz]])
         np.testing.assert_array_equal(np.array(got[k:k + sz]), np.array(want))
         k += sz
+
+
+def test_groupavg3combine_oracle(ora):
+    """BATgroupavg3combine (gdk_aggr.c:2634) of per-shard BATgroupavg3
+    partials equals BATgroupavg3 over the whole input (its purpose in the
+    mitosis/mergetable plan), here checked on exact integers."""
+    r = np.random.default_rng(17)
+    n, ng, shards = 6000, 9, 4
+    v = r.integers(-10**9, 10**9, n).astype(np.int64)
+    v[r.random(n) < 0.03] = -(2**63)
+    gid = r.integers(0, ng, n).astype(np.uint64)
+    A, R, K, G = [], [], [], []
+    for sh in np.array_split(np.arange(n), shards):
+        a, rm, c = ora.BATgroupavg3(ora.Bat.from_array(ora.TYPE_lng, v[sh]),
+                                    ora.Bat.from_array(ora.TYPE_oid, gid[sh]), None, True)
+        A += list(a.values())
+        R += list(rm.values())
+        K += list(c.values())
+        G += list(range(ng))
+    comb = ora.BATgroupavg3combine(ora.Bat.from_array(ora.TYPE_lng, np.array(A, np.int64)),
+                                   ora.Bat.from_array(ora.TYPE_lng, np.array(R, np.int64)),
+                                   ora.Bat.from_array(ora.TYPE_lng, np.array(K, np.int64)),
+                                   ora.Bat.from_array(ora.TYPE_oid, np.array(G, np.uint64)), None, True)
+    full, _, _ = ora.BATgroupavg3(ora.Bat.from_array(ora.TYPE_lng, v), ora.Bat.from_array(ora.TYPE_oid, gid),
+                                  None, True)
+    assert list(comb.values()) == list(full.values())
