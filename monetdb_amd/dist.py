@@ -191,6 +191,12 @@ class GdkBackend:
     def groupmin(self, c, g, e):
         return self.gdk.BATgroupmin(c, g, e)
 
+    def groupavg3(self, c, g, e):
+        return self.gdk.BATgroupavg3(c, g, e, True)
+
+    def groupavg3combine(self, a, r, c, g, e):
+        return self.gdk.BATgroupavg3combine(a, r, c, g, e, True)
+
     def join(self, l, r):
         return self.gdk.BATjoin(l, r)
 
@@ -322,6 +328,47 @@ def dist_group_aggr(be, dist, keys, vals):
         mine = [{"key": int(mk[i]), "first_row": int(mf[i]), "count": int(mc[i]),
                  "sums": [int(s[i]) for s in ms]} for i in range(len(mk))]
     # global first-occurrence numbering
+    firsts = [m["first_row"] for m in mine]
+    allf = sorted(x for part in (_gather_var(dist, be.device, firsts) if world > 1 else [firsts])
+                  for x in part)
+    pos = {f: i for i, f in enumerate(allf)}
+    for m in mine:
+        m["gid"] = pos[m["first_row"]]
+    return sorted(mine, key=lambda m: m["gid"])
+
+
+# ---------------------------------------------------------------------------
+# group + exact average (the mergetable plan of AVG: opt_mergetable.c
+# mat_group_aggr turns avg into per-shard BATgroupavg3 and one
+# BATgroupavg3combine over the partials, gdk_aggr.c:1996 / :2634)
+# ---------------------------------------------------------------------------
+
+def dist_group_avg(be, dist, keys, vals):
+    """GROUP BY keys, AVG(vals) (lng), as BATgroupavg3 over all rows would
+    round it.  Each rank groups its shard and computes (avg, rem, cnt)
+    partials; the partial rows are hash-partitioned by key (ONE all_to_all)
+    and each owner combines its groups' partials with BATgroupavg3combine.
+    Returns this rank's owned groups {gid, key, first_row, avg}, gid in
+    global first-occurrence order."""
+    TL, TO, TH = _types(be)
+    world, rank = _world(dist)
+    g, e, _ = be.group(keys)
+    a, r, c = be.groupavg3(vals, g, e)
+    parts = [be.widen(be.project(e, keys)), e, a, r, c]
+    if world > 1:
+        order, counts = be.hashpartition(parts[0], world)
+        parts = [be.project(order, x) for x in parts]
+        recv, _ = _exchange(dist, be.device, be.pack(parts), counts)
+        parts = be.unpack(recv, [TL, TO, TL, TL, TL])
+    rk, rfirst, ra, rr, rc = parts
+    if be.n(rk) == 0:
+        mine = []
+    else:
+        g2, e2, _ = be.group(rk)
+        mk = be.values(be.project(e2, rk))
+        mf = be.values(be.groupmin(rfirst, g2, e2))
+        ma = be.values(be.groupavg3combine(ra, rr, rc, g2, e2))
+        mine = [{"key": int(mk[i]), "first_row": int(mf[i]), "avg": int(ma[i])} for i in range(len(mk))]
     firsts = [m["first_row"] for m in mine]
     allf = sorted(x for part in (_gather_var(dist, be.device, firsts) if world > 1 else [firsts])
                   for x in part)

@@ -96,6 +96,13 @@ class OracleBackend:
     def groupmin(self, c, g, e):
         return _from_ora(ora.BATgroupminmax(c.ora(), g.ora(), e.ora(), False))
 
+    def groupavg3(self, c, g, e):
+        a, r, k = ora.BATgroupavg3(c.ora(), g.ora(), e.ora(), True)
+        return _from_ora(a), _from_ora(r), _from_ora(k)
+
+    def groupavg3combine(self, a, r, c, g, e):
+        return _from_ora(ora.BATgroupavg3combine(a.ora(), r.ora(), c.ora(), g.ora(), e.ora(), True))
+
     def join(self, l, r):
         a, b = ora.BATjoin(l.ora(), r.ora())
         return _from_ora(a), _from_ora(b)

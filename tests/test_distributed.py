@@ -137,6 +137,22 @@ def _exchange_worker(rank, world, port, out_dir, backend="oracle"):
     if int(tot) != len(ev):
         errs.append("groups %d != %d" % (int(tot), len(ev)))
 
+    # group + AVG: per-shard BATgroupavg3 partials, one shuffle, BATgroupavg3combine
+    v3 = v1.copy()
+    v3[r.random(N) < 0.03] = np.iinfo(np.int64).min
+    gota = D.dist_group_avg(be, dist, Col(ora.TYPE_int, keys[lo:hi], lo), Col(ora.TYPE_lng, v3[lo:hi], lo))
+    av, _, _ = ora.BATgroupavg3(ora.Bat.from_array(ora.TYPE_lng, v3), g, e, True)
+    av = av.values()
+    for m in gota:
+        i = m["gid"]
+        if (m["first_row"], m["avg"]) != (int(ev[i]), int(av[i])):
+            errs.append("avg group %d: %r != %r" % (i, m, (int(ev[i]), int(av[i]))))
+            break
+    tot = torch.tensor([len(gota)])
+    dist.all_reduce(tot)
+    if int(tot) != len(ev):
+        errs.append("avg groups %d != %d" % (int(tot), len(ev)))
+
     # hash join, duplicates on both sides
     lk = r.integers(0, 3000, N).astype(np.int32)
     rk = r.integers(0, 3000, N).astype(np.int32)
