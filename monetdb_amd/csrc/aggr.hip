@@ -524,10 +524,43 @@ k_minmax_oid(const oid *g, BUN n, unsigned long long *out)
 }
 
 // BATgroupaggrinit (gdk/gdk_aggr.c:65-146)
+// b's values at a materialised candidate list, as a new BAT whose head
+// starts at the first candidate (so it is aligned with g, which has one
+// group id per candidate); kept alive in a small per-thread ring (nested
+// aggregate calls each take their own slot)
+static thread_local mgdk_bat *cv_ring[4];
+static thread_local unsigned cv_next;
+
+mgdk_bat *
+cand_values(mgdk_bat *b, const Cand &ci)
+{
+	mgdk_bat *l = newbat(0, MGDK_oid, ci.n);
+	if (l == nullptr)
+		return nullptr;
+	if (!hip_ok(hipMemcpyAsync(l->theap, ci.oids, ci.n * sizeof(oid), hipMemcpyDeviceToDevice, stream()), "memcpy")) {
+		mgdk_BBPunfix(l);
+		return nullptr;
+	}
+	l->count = ci.n;
+	l->tsorted = l->tkey = l->tnonil = 1;
+	l->trevsorted = ci.n <= 1;
+	mgdk_bat *v = mgdk_BATproject(l, b);
+	mgdk_BBPunfix(l);
+	if (v == nullptr)
+		return nullptr;
+	v->hseqbase = ci.first;
+	mgdk_BBPunfix(cv_ring[cv_next & 3]);
+	cv_ring[cv_next++ & 3] = v;
+	return v;
+}
+
+// BATgroupaggrinit (gdk/gdk_aggr.c:65); a materialised candidate list is
+// resolved once into a gathered value column (*bp is replaced by it)
 int
-aggr_init(AggrInit *a, mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s)
+aggr_init(AggrInit *a, mgdk_bat **bp, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s)
 {
 	*a = AggrInit{};
+	mgdk_bat *b = *bp;
 	if (cand_init(&a->ci, b, s) < 0)
 		return -1;
 	if (g == nullptr) {
@@ -539,8 +572,10 @@ aggr_init(AggrInit *a, mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s)
 		return -1;
 	}
 	if (!a->ci.dense) {
-		seterr("42000!grouped aggregate over a materialized candidate list is not supported on the device path");
-		return -1;
+		mgdk_bat *v = cand_values(b, a->ci);
+		if (v == nullptr || cand_init(&a->ci, v, nullptr) < 0)
+			return -1;
+		*bp = v;
 	}
 	a->gids = g->ttype == MGDK_void ? nullptr : (const oid *) g->theap;
 	a->gseq = g->tseqbase;
@@ -815,7 +850,7 @@ mgdk_BATgroupsum(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, boo
 		// dofsum with groups (gdk_aggr.c:183), exact per group (fsum.hip)
 		ProfScope prof("groupsum");
 		AggrInit a;
-		if (aggr_init(&a, b, g, e, s) < 0)
+		if (aggr_init(&a, &b, g, e, s) < 0)
 			return nullptr;
 		const BUN ng = a.ngrp;
 		std::vector<char> out(ng * 8 + 16);
@@ -836,7 +871,7 @@ mgdk_BATgroupsum(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, boo
 	}
 	ProfScope prof("groupsum");
 	AggrInit a;
-	if (aggr_init(&a, b, g, e, s) < 0)
+	if (aggr_init(&a, &b, g, e, s) < 0)
 		return nullptr;
 	const BUN ng = a.ngrp;
 	std::vector<char> out(ng * width_of(tp) + 16);
@@ -889,7 +924,7 @@ mgdk_BATgroupcount(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, b
 	}
 	ProfScope prof("groupcount");
 	AggrInit a;
-	if (aggr_init(&a, b, g, e, s) < 0)
+	if (aggr_init(&a, &b, g, e, s) < 0)
 		return nullptr;
 	const BUN ng = a.ngrp;
 	std::vector<long long> out(ng + 1, 0);
@@ -933,7 +968,7 @@ mgdk_BATgroupavg(mgdk_bat **bnp, mgdk_bat **cntsp, mgdk_bat *b, mgdk_bat *g, mgd
 	}
 	ProfScope prof("groupavg");
 	AggrInit a;
-	if (aggr_init(&a, b, g, e, s) < 0)
+	if (aggr_init(&a, &b, g, e, s) < 0)
 		return -1;
 	const BUN ng = a.ngrp;
 	const oid hb = ng ? a.min : 0;
@@ -1114,7 +1149,7 @@ mgdk_BATgroupavg3combine(mgdk_bat *avg, mgdk_bat *rem, mgdk_bat *cnt, mgdk_bat *
 	}
 	ProfScope prof("groupavg3combine");
 	AggrInit a;
-	if (aggr_init(&a, avg, g, e, nullptr) < 0)
+	if (aggr_init(&a, &avg, g, e, nullptr) < 0)
 		return nullptr;
 	if (a.ci.n != rem->count || a.ci.n != cnt->count) {
 		seterr("input bats not aligned");
@@ -1233,7 +1268,7 @@ mgdk_BATgroupavg3(mgdk_bat **avgp, mgdk_bat **remp, mgdk_bat **cntp, mgdk_bat *b
 	}
 	ProfScope prof("groupavg3");
 	AggrInit a;
-	if (aggr_init(&a, b, g, e, s) < 0)
+	if (aggr_init(&a, &b, g, e, s) < 0)
 		return -1;
 	const BUN ng = a.ngrp;
 	const int tp = b->ttype;
@@ -1297,7 +1332,7 @@ groupminmax(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, bool skip_nils, 
 		return nullptr;
 	}
 	AggrInit a;
-	if (aggr_init(&a, b, g, e, s) < 0)
+	if (aggr_init(&a, &b, g, e, s) < 0)
 		return nullptr;
 	const BUN ng = a.ngrp;
 	GRes r;

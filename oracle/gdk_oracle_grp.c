@@ -202,12 +202,10 @@ aggr_init(aggr_ctx *a, const ora_bat *b, const ora_bat *g, const ora_bat *e,
 		ora_seterr("b and g must be aligned\n");
 		return -1;
 	}
-	if (a->ci.n != g->count) {
+	/* BATgroupaggrinit (gdk_aggr.c:65-110): g has one group id per
+	 * candidate and its head starts at the first candidate */
+	if (a->ci.n != g->count || (a->ci.n != 0 && ci_get(&a->ci, 0) != g->hseqbase)) {
 		ora_seterr("b with s and g must be aligned\n");
-		return -1;
-	}
-	if (!a->ci.dense) {
-		ora_seterr("grouped aggregate with non-dense candidates unsupported");
 		return -1;
 	}
 	a->gids = g->type == ORA_void ? NULL : g->base;

@@ -744,3 +744,43 @@ def test_groupavg3combine(gdk, ora, tname, skip):
                                    ora.Bat.from_array(ora.TYPE_lng, K), ora.Bat.from_array(ora.TYPE_oid, G),
                                    None, skip)
     assert _same(got, want)
+
+
+def test_grouped_aggregates_candidate_lists(gdk, ora):
+    """BATgroupsum / count / min / max / avg3 / avg with a materialised (and a
+    cand_except) candidate list: g has one group id per candidate and its
+    head starts at the first candidate (BATgroupaggrinit, gdk_aggr.c:65)."""
+    r = rng(91)
+    n = 60_000
+    v = r.integers(-10**9, 10**9, n).astype(np.int64)
+    v[::41] = gdk.NIL[gdk.TYPE_lng]
+    B, OB = gdk.BAT.from_numpy(gdk.TYPE_lng, v, hseqbase=10), ora.Bat.from_array(ora.TYPE_lng, v, hseqbase=10)
+    oids = np.sort(r.choice(np.arange(10, 10 + n), 25_000, replace=False)).astype(np.uint64)
+    S = gdk.BAT.from_numpy(gdk.TYPE_oid, oids, sorted_=True, key=True, nonil=True)
+    OS = ora.Bat.from_array(ora.TYPE_oid, oids, sorted_=True, key=True, nonil=True)
+    gid = r.integers(0, 300, len(oids)).astype(np.uint64)
+    G = gdk.BAT.from_numpy(gdk.TYPE_oid, gid, hseqbase=int(oids[0]), key=False)
+    OG = ora.Bat.from_array(ora.TYPE_oid, gid, hseqbase=int(oids[0]))
+    for skip in (True, False):
+        assert _same(gdk.BATgroupsum(B, G, None, gdk.TYPE_hge, skip, s=S),
+                     ora.BATgroupsum(OB, OG, None, ora.TYPE_hge, skip, s=OS))
+        assert np.array_equal(gdk.BATgroupcount(B, G, None, skip, s=S).to_numpy(),
+                              np.asarray(ora.BATgroupcount(OB, OG, None, skip, s=OS).values()))
+        a, rm, c = gdk.BATgroupavg3(B, G, None, skip, s=S)
+        oa, orm, oc = ora.BATgroupavg3(OB, OG, None, skip, s=OS)
+        assert _same(a, oa) and _same(rm, orm) and _same(c, oc)
+        av, cn = gdk.BATgroupavg(B, G, None, skip, s=S)
+        oav, ocn = ora.BATgroupavg(OB, OG, None, skip, s=OS)
+        assert _same(av, oav) and _same(cn, ocn)
+    assert _same(gdk.BATgroupmin(B, G, None, s=S), ora.BATgroupminmax(OB, OG, None, False, s=OS))
+    assert _same(gdk.BATgroupmax(B, G, None, s=S), ora.BATgroupminmax(OB, OG, None, True, s=OS))
+    # cand_except list over the same BAT
+    exc = np.sort(r.choice(np.arange(100, 30_000), 500, replace=False)).astype(np.uint64)
+    NEG = gdk.BAT.negoid_cand(100, 29_900 - 500, exc)
+    keep = np.setdiff1d(np.arange(100, 30_000, dtype=np.uint64), exc)
+    gid2 = r.integers(0, 50, len(keep)).astype(np.uint64)
+    G2 = gdk.BAT.from_numpy(gdk.TYPE_oid, gid2, hseqbase=int(keep[0]), key=False)
+    OG2 = ora.Bat.from_array(ora.TYPE_oid, gid2, hseqbase=int(keep[0]))
+    OK = ora.Bat.from_array(ora.TYPE_oid, keep, sorted_=True, key=True, nonil=True)
+    assert _same(gdk.BATgroupsum(B, G2, None, gdk.TYPE_hge, True, s=NEG),
+                 ora.BATgroupsum(OB, OG2, None, ora.TYPE_hge, True, s=OK))
