@@ -11,8 +11,13 @@
 //   otherwise;
 //   passes: 8-bit digits, only digit positions that are not constant over
 //   the input (AND/OR reduction) are sorted;
-//   per pass: (1) per-tile digit histogram in LDS, (2) device scan of the
-//   digit-major counts, (3) stable scatter of a 4096-key tile: each wave
+//   the global digit counts of every pass come from ONE pass over the input
+//   (LSD passes permute the keys, the counts do not change);
+//   per pass: a stable scatter of an 8192-key tile whose output base per
+//   digit is the pass's digit start + a decoupled look-back over the
+//   tiles' digit counts (each tile publishes its counts before ranking, so
+//   the walk back is short; MGDK_SORT_LB=0 restores the per-pass histogram
+//   + scan); in the tile each wave
 //   ranks its 16 rows of 64 keys with 8 bit-sliced ballots against per-wave
 //   running digit counters (no workgroup barrier per row), the tile is
 //   reordered by digit in LDS and written out in that order, so equal-digit
@@ -21,6 +26,7 @@
 //   from the key image (no gather) and the order oids (hseqbase + position).
 #include <vector>
 
+#include "lookback.h"
 #include "mgdk_internal.h"
 
 using namespace mgdk;
@@ -55,6 +61,55 @@ k_rs_hist(const K *keys, BUN n, int shift, uint32_t *hist, uint32_t nblocks)
 	}
 	__syncthreads();
 	hist[(BUN) threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+}
+
+// digit histograms of every pass at once: LSD passes permute the keys, so
+// each pass's global digit counts are those of the input (one read)
+constexpr int RS_MAXP = 8;
+struct Shifts {
+	int s[RS_MAXP];
+	int n;
+};
+
+template <typename K>
+__global__ __launch_bounds__(256) void
+k_rs_dhist(const K *keys, BUN n, Shifts sh, uint32_t *out)
+{
+	__shared__ uint32_t h[RS_MAXP][256];
+	for (int p = 0; p < sh.n; p++)
+		h[p][threadIdx.x] = 0;
+	__syncthreads();
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		const K k = keys[i];
+		for (int p = 0; p < sh.n; p++)
+			atomicAdd(&h[p][(uint32_t) (k >> sh.s[p]) & 255], 1u);
+	}
+	__syncthreads();
+	for (int p = 0; p < sh.n; p++)
+		if (h[p][threadIdx.x])
+			atomicAdd(&out[p * 256 + threadIdx.x], h[p][threadIdx.x]);
+}
+
+// exclusive scan of each pass's 256 digit counts (one workgroup per pass)
+__global__ __launch_bounds__(256) void
+k_rs_dscan(const uint32_t *cnt, uint32_t *gdig)
+{
+	__shared__ uint32_t ws[4];
+	const uint32_t v = cnt[blockIdx.x * 256 + threadIdx.x];
+	const unsigned lane = __lane_id(), w = threadIdx.x >> 6;
+	uint32_t x = v;
+#pragma unroll
+	for (int o = 1; o < 64; o <<= 1) {
+		const uint32_t u = __shfl_up(x, o);
+		if (lane >= (unsigned) o)
+			x += u;
+	}
+	if (lane == 63)
+		ws[w] = x;
+	__syncthreads();
+	for (unsigned q = 0; q < w; q++)
+		x += ws[q];
+	gdig[blockIdx.x * 256 + threadIdx.x] = x - v;
 }
 
 // final pass outputs: decoded value column and order oids
@@ -95,10 +150,16 @@ emit_final(const FinalOut &fo, BUN g, K key, uint32_t v)
 	}
 }
 
-template <typename K, bool FINAL, bool IDV>
+// LB: the tile's output base per digit comes from a decoupled look-back
+// over the tiles' digit counts (tiles numbered by a ticket, so every
+// predecessor is resident) plus the pass's global digit start gdig -- no
+// per-pass histogram pass and scan.  Otherwise offs holds the digit-major
+// exclusive scan of k_rs_hist's counts.
+template <typename K, bool FINAL, bool IDV, bool LB>
 __global__ __launch_bounds__(256) void
 k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32_t *offs, uint32_t nblocks,
-	     K *kout, uint32_t *vout, FinalOut fo)
+	     K *kout, uint32_t *vout, FinalOut fo, uint32_t *ticket, uint64_t *status, const uint32_t *gdig,
+	     uint32_t *err)
 {
 	__shared__ K sk[STILE];
 	__shared__ uint32_t sv[STILE];
@@ -106,10 +167,21 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 	__shared__ uint32_t tstart[256];      // digit start inside the reordered tile
 	__shared__ uint32_t gbase[256];       // digit start of this tile in the output
 	__shared__ uint32_t s_wt[4];
+	__shared__ uint32_t s_tile;
 	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+	if (LB) {
+		if (tid == 0)
+			s_tile = atomicAdd(ticket, 1u);
+		__syncthreads();
+	}
+	const uint32_t blk = LB ? s_tile : blockIdx.x;
+	__shared__ uint32_t lh[256];          // LB: the tile's digit counts, published before ranking
+	if (LB)
+		lh[tid] = 0;
 	wcnt[0][tid] = wcnt[1][tid] = wcnt[2][tid] = wcnt[3][tid] = 0;
-	gbase[tid] = offs[(BUN) tid * nblocks + blockIdx.x];
-	const BUN tbase = (BUN) blockIdx.x * STILE;
+	if (!LB)
+		gbase[tid] = offs[(BUN) tid * nblocks + blk];
+	const BUN tbase = (BUN) blk * STILE;
 	const BUN base = tbase + (BUN) w * (64 * SROWS);
 	K k[SROWS];
 	uint32_t v[SROWS];
@@ -120,6 +192,16 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 		v[r] = IDV ? (uint32_t) i : (i < n ? vals[i] : 0);   // first pass: positions
 	}
 	__syncthreads();
+	if (LB) {
+		// publish this tile's digit counts as early as possible, so the
+		// look-back of later tiles rarely has to walk far
+#pragma unroll
+		for (int r = 0; r < SROWS; r++)
+			if (base + r * 64 + lane < n)
+				atomicAdd(&lh[(uint32_t) (k[r] >> shift) & 255], 1u);
+		__syncthreads();
+		mgdk_lb::lb_store(status + (size_t) blk * 256 + tid, (blk == 0 ? mgdk_lb::ST_PRE : mgdk_lb::ST_AGG) | lh[tid]);
+	}
 	const uint64_t lt = lanemask_lt();
 	uint32_t rk[SROWS];
 #pragma unroll
@@ -161,6 +243,34 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 		for (unsigned q = 0; q < w; q++)
 			ex += s_wt[q];
 		tstart[tid] = ex;
+		if (LB) {
+			using namespace mgdk_lb;
+			uint64_t *me = status + (size_t) blk * 256 + tid;
+			if (blk == 0) {
+				gbase[tid] = gdig[tid];
+			} else {
+				uint64_t excl = 0;
+				int64_t t = (int64_t) blk - 1;
+				uint32_t spins = 0;
+				while (t >= 0) {
+					const uint64_t sv = lb_load(status + (size_t) t * 256 + tid);
+					if ((sv >> 62) == 0) {
+						if (++spins > (1u << 24)) {
+							atomicOr(err, 1u);
+							break;
+						}
+						__builtin_amdgcn_s_sleep(1);
+						continue;
+					}
+					excl += sv & ST_VAL;
+					if (sv & ST_PRE)
+						break;
+					t--;
+				}
+				lb_store(me, ST_PRE | (excl + tot));
+				gbase[tid] = gdig[tid] + (uint32_t) excl;
+			}
+		}
 	}
 	__syncthreads();
 #pragma unroll
@@ -407,9 +517,25 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 		if ((diff >> shift) & 255)
 			shifts.push_back(shift);   // other digits are constant: identity passes
 	const uint32_t nblocks = (uint32_t) ((n + STILE - 1) / STILE);
-	DevBuf hist((size_t) 256 * nblocks * 4), offs((size_t) 256 * nblocks * 4);
-	if (!hist.p || !offs.p)
+	static const bool use_lb = getenv("MGDK_SORT_LB") ? atoi(getenv("MGDK_SORT_LB")) != 0 : true;
+	const bool lb = use_lb && !shifts.empty() && shifts.size() <= (size_t) RS_MAXP;
+	DevBuf hist(lb ? 64 : (size_t) 256 * nblocks * 4), offs(lb ? 64 : (size_t) 256 * nblocks * 4);
+	DevBuf status(lb ? (size_t) 256 * nblocks * 8 : 64), dcnt(RS_MAXP * 256 * 4 * 2 + 64), lbm(64);
+	if (!hist.p || !offs.p || !status.p || !dcnt.p || !lbm.p)
 		return -1;
+	uint32_t *gdig = dcnt.as<uint32_t>() + RS_MAXP * 256;
+	if (lb) {
+		Shifts sh{};
+		sh.n = (int) shifts.size();
+		for (int q = 0; q < sh.n; q++)
+			sh.s[q] = shifts[q];
+		if (!hip_ok(hipMemsetAsync(dcnt.p, 0, RS_MAXP * 256 * 4, st), "memset") ||
+		    !hip_ok(hipMemsetAsync(lbm.p, 0, 64, st), "memset"))
+			return -1;
+		hipLaunchKernelGGL((k_rs_dhist<K>), dim3(grid_for(n, 16384, 2048)), dim3(256), 0, st, keys, n, sh,
+				   dcnt.as<uint32_t>());
+		hipLaunchKernelGGL(k_rs_dscan, dim3(sh.n), dim3(256), 0, st, dcnt.as<uint32_t>(), gdig);
+	}
 	K *kin = keys, *kout = keys_alt;
 	uint32_t *vin = vals, *vout = vals_alt;
 	FinalOut none{};
@@ -417,19 +543,35 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 		const int shift = shifts[s];
 		const bool fin = fo != nullptr && s + 1 == shifts.size();
 		const bool idv = positions && s == 0;
-		hipLaunchKernelGGL((k_rs_hist<K>), dim3(nblocks), dim3(256), 0, st, kin, n, shift, hist.as<uint32_t>(),
-				   nblocks);
-		if (exclusive_scan(hist.as<uint32_t>(), offs.as<uint32_t>(), (BUN) 256 * nblocks, nullptr) < 0)
-			return -1;
+		if (lb) {
+			if (!hip_ok(hipMemsetAsync(status.p, 0, (size_t) 256 * nblocks * 8, st), "memset") ||
+			    !hip_ok(hipMemsetAsync(lbm.p, 0, 8, st), "memset"))
+				return -1;
+		} else {
+			hipLaunchKernelGGL((k_rs_hist<K>), dim3(nblocks), dim3(256), 0, st, kin, n, shift,
+					   hist.as<uint32_t>(), nblocks);
+			if (exclusive_scan(hist.as<uint32_t>(), offs.as<uint32_t>(), (BUN) 256 * nblocks, nullptr) < 0)
+				return -1;
+		}
 		FinalOut f2 = fin ? *fo : none;
 		if (fin && f2.want_keys)
 			f2.keys = kout;
-#define SCAT(F, I) hipLaunchKernelGGL((k_rs_scatter<K, F, I>), dim3(nblocks), dim3(256), 0, st, kin, vin, n, shift, \
-				      offs.as<uint32_t>(), nblocks, kout, vout, f2)
-		if (fin) {
-			if (idv) SCAT(true, true); else SCAT(true, false);
+		uint32_t *tk = lbm.as<uint32_t>(), *er = lbm.as<uint32_t>() + 4;
+		const uint32_t *gd = gdig + s * 256;
+#define SCAT(F, I, L) hipLaunchKernelGGL((k_rs_scatter<K, F, I, L>), dim3(nblocks), dim3(256), 0, st, kin, vin, n, \
+					 shift, offs.as<uint32_t>(), nblocks, kout, vout, f2, tk, status.as<uint64_t>(), gd, er)
+		if (lb) {
+			if (fin) {
+				if (idv) SCAT(true, true, true); else SCAT(true, false, true);
+			} else {
+				if (idv) SCAT(false, true, true); else SCAT(false, false, true);
+			}
 		} else {
-			if (idv) SCAT(false, true); else SCAT(false, false);
+			if (fin) {
+				if (idv) SCAT(true, true, false); else SCAT(true, false, false);
+			} else {
+				if (idv) SCAT(false, true, false); else SCAT(false, false, false);
+			}
 		}
 #undef SCAT
 		std::swap(kin, kout);
@@ -443,6 +585,15 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 	}
 	if (!sync())
 		return -1;
+	if (lb) {
+		uint32_t *he = (uint32_t *) pinned(16);
+		if (!hip_ok(hipMemcpyAsync(he, lbm.as<uint32_t>() + 4, 4, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+			return -1;
+		if (he[0]) {
+			seterr("HY013!BATsort: radix look-back did not complete");
+			return -1;
+		}
+	}
 	*keys_out = kin;
 	*vals_out = positions && shifts.empty() ? nullptr : vin;   // NULL: identity
 	return 0;
