@@ -943,6 +943,17 @@ k_pj_probe(const uint2 *bent, const uint32_t *bbase, const uint2 *pent, const ui
 		for (uint32_t i = threadIdx.x; i < nsub; i += blockDim.x)
 			sdelta[i] = dcol[i];
 	__syncthreads();
+	// the first batch of probe entries is loaded while the table is built
+	// (one workgroup per CU: nothing else would hide the build's latency),
+	// and every later batch while the previous one is answered
+	constexpr int U = 8;
+	const uint32_t q0 = pbase[p], q1 = pbase[p + 1];
+	uint2 cur[U];
+#pragma unroll
+	for (int u = 0; u < U; u++) {
+		const uint32_t e = q0 + threadIdx.x + u * blockDim.x;
+		cur[u] = e < q1 ? pent[e] : make_uint2(0, 0);
+	}
 	const uint32_t b0 = bbase[p], b1 = bbase[p + 1];
 	bool dup = false;
 	for (uint32_t e = b0 + threadIdx.x; e < b1; e += blockDim.x) {
@@ -963,14 +974,13 @@ k_pj_probe(const uint2 *bent, const uint32_t *bbase, const uint2 *pent, const ui
 	if (__any(dup) && __lane_id() == 0)
 		atomicOr(dupflag, 1u);
 	__syncthreads();
-	const uint32_t q0 = pbase[p], q1 = pbase[p + 1];
-	constexpr int U = 8;
 	for (uint32_t e0 = q0 + threadIdx.x; e0 < q1; e0 += U * blockDim.x) {
-		uint2 en[U];
+		uint2 en[U], nxt[U];
 #pragma unroll
 		for (int u = 0; u < U; u++) {
-			const uint32_t e = e0 + u * blockDim.x;
-			en[u] = e < q1 ? pent[e] : make_uint2(0, 0);
+			en[u] = cur[u];
+			const uint32_t e = e0 + (U + u) * blockDim.x;
+			nxt[u] = e < q1 ? pent[e] : make_uint2(0, 0);
 		}
 #pragma unroll
 		for (int u = 0; u < U; u++) {
@@ -994,6 +1004,9 @@ k_pj_probe(const uint2 *bent, const uint32_t *bbase, const uint2 *pent, const ui
 			if (e < q1)
 				flat[e + (ldsd ? sdelta[sub] : dcol[sub])] = en[u];
 		}
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			cur[u] = nxt[u];
 	}
 }
 
