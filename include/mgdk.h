@@ -211,6 +211,11 @@ int mgdk_GDKanalyticalcount(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, 
  * caller-allocated dbl BAT; tpe = type of b (bte..lng, flt, dbl) */
 int mgdk_GDKanalyticalavg(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e,
 			  int tpe, int frame_type);
+/* gdk_analytic_statistics.c:631 GDKanalyticalavginteger (gdk_analytic.h:42):
+ * the average in b's integer type (bte..lng), rounded half away from zero;
+ * r is a caller-allocated BAT of that type */
+int mgdk_GDKanalyticalavginteger(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e,
+				 int tpe, int frame_type);
 
 /* ---- compressed column inputs (sql/backends/monet5/dict.c, for.c):
  *      a DICT column is codes o (bte/sht/int, read unsigned) + the

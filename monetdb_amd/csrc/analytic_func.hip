@@ -315,6 +315,7 @@ struct FArgs {
 	bool count;          // GDKanalyticalcount
 	bool count_all;
 	bool avg;            // GDKanalyticalavg of integers: dbl sum / count
+	int avgint;          // GDKanalyticalavginteger: output width (0: off)
 	Starts part, peer;
 	const oid *s, *e;
 	const hge *P, *A;
@@ -360,6 +361,29 @@ k_frames(FArgs a)
 		}
 		const unsigned long long c = a.C ? a.C[hi] - a.C[lo] : hi - lo;
 		const hge sum = a.P[hi] - a.P[lo];
+		if (a.avgint) {
+			// AVERAGE_ITER's state of the frame = floor(sum / n), sum mod n;
+			// ANALYTICAL_AVERAGE_INT_CALC_FINALIZE (gdk_analytic_statistics.c:435-446)
+			long long q = 0;
+			if (c) {
+				hge hq = sum / (hge) c, hr = sum % (hge) c;
+				if (hr < 0) {
+					hq -= 1;
+					hr += (hge) c;
+				}
+				if (hr > 0 && (hq < 0 ? 2 * hr > (hge) c : 2 * hr >= (hge) c))
+					hq += 1;
+				q = (long long) hq;
+			}
+			switch (a.avgint) {
+			case 1: ((int8_t *) a.out)[i] = c ? (int8_t) q : INT8_MIN; break;
+			case 2: ((int16_t *) a.out)[i] = c ? (int16_t) q : INT16_MIN; break;
+			case 4: ((int32_t *) a.out)[i] = c ? (int32_t) q : INT32_MIN; break;
+			default: ((int64_t *) a.out)[i] = c ? (int64_t) q : INT64_MIN; break;
+			}
+			hasnil |= c == 0;
+			continue;
+		}
 		if (a.avg) {
 			// (dbl) sum / n of ANALYTICAL_AVG_IMP_NUM_* (gdk_analytic_statistics.c:55-165)
 			((double *) a.out)[i] = c ? hge_to_dbl(sum) / (double) (long long) c : __builtin_nan("");
@@ -611,7 +635,7 @@ sum_in_type(int t)
 
 int
 run_frames(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e, int frame_type,
-	   bool count, bool count_all, bool lng_out, bool avg = false)
+	   bool count, bool count_all, bool lng_out, bool avg = false, int avgint = 0)
 {
 	const BUN n = b->count;
 	hipStream_t st = stream();
@@ -733,6 +757,7 @@ run_frames(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk
 	a.count = count;
 	a.count_all = count_all;
 	a.avg = avg;
+	a.avgint = avgint;
 	a.s = frames ? (const oid *) s->theap : nullptr;
 	a.e = frames ? (const oid *) e->theap : nullptr;
 	a.P = P.as<hge>();
@@ -870,6 +895,14 @@ struct AvgNode<T, false> {
 	{
 		return (double) a + (double) rr / (double) n;
 	}
+	// ANALYTICAL_AVERAGE_INT_CALC_FINALIZE (gdk_analytic_statistics.c:435-446)
+	__device__ __forceinline__ long long rounded() const
+	{
+		long long q = a;
+		if (rr > 0 && (q < 0 ? 2 * rr > n : 2 * rr >= n))
+			q++;
+		return q;
+	}
 };
 
 template <typename T>
@@ -899,6 +932,7 @@ struct AvgNode<T, true> {
 			add(c.a);
 	}
 	__device__ __forceinline__ double result() const { return (double) a; }
+	__device__ __forceinline__ long long rounded() const { return 0; }
 };
 
 struct AvgTree {
@@ -957,10 +991,10 @@ k_avg_tree_level(const T *b, Starts part, const uint32_t *pidx, AvgTree t, int L
 }
 
 // compute_on_segment_tree (gdk_analytic.h:96-130) for [s[i], e[i])
-template <typename T>
+template <typename T, bool IOUT>
 __global__ __launch_bounds__(256) void
 k_avg_tree_query(const T *b, Starts part, const uint32_t *pidx, AvgTree t, const oid *S, const oid *E,
-		 double *out, uint32_t *flags)
+		 void *out, uint32_t *flags)
 {
 	using N = AvgNode<T>;
 	uint32_t hasnil = 0;
@@ -1001,11 +1035,14 @@ k_avg_tree_query(const T *b, Starts part, const uint32_t *pidx, AvgTree t, const
 				tend = pe;
 			}
 		}
-		if (acc.n == 0) {
-			out[i] = __builtin_nan("");
+		if constexpr (IOUT) {
+			((T *) out)[i] = acc.n == 0 ? NilOf<T>::v() : (T) acc.rounded();
+			hasnil |= acc.n == 0;
+		} else if (acc.n == 0) {
+			((double *) out)[i] = __builtin_nan("");
 			hasnil = 1;
 		} else {
-			out[i] = acc.result();
+			((double *) out)[i] = acc.result();
 		}
 	}
 	hasnil = block_reduce(hasnil, [](uint32_t x, uint32_t y) { return x | y; });
@@ -1062,7 +1099,23 @@ k_avg_row(const T *b, BUN n, bool nil_all, double *out, uint32_t *flags)
 		publish_or(flags, hasnil);
 }
 
+// integer copy of the values (frame 6 of GDKanalyticalavginteger)
 template <typename T>
+__global__ __launch_bounds__(256) void
+k_avg_copy(const T *b, BUN n, T *out, uint32_t *flags)
+{
+	uint32_t hasnil = 0;
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		const T v = b[i];
+		out[i] = v;
+		hasnil |= is_nil(v);
+	}
+	hasnil = block_reduce(hasnil, [](uint32_t x, uint32_t y) { return x | y; });
+	if (threadIdx.x == 0)
+		publish_or(flags, hasnil);
+}
+
+template <typename T, bool IOUT = false>
 int
 run_avg(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e, int frame_type)
 {
@@ -1070,16 +1123,19 @@ run_avg(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_ba
 	const BUN n = b->count;
 	hipStream_t st = stream();
 	const T *bv = (const T *) b->theap;
-	double *out = (double *) r->theap;
+	void *out = r->theap;
 	const bool frames = !(frame_type >= 3 && frame_type <= 6);
 	DevBuf fl(64);
 	if (!fl.p || !hip_ok(hipMemsetAsync(fl.p, 0, 64, st), "memset"))
 		return -1;
 	mgdk_bat *Sp = nullptr;
 	int rc = -1;
-	if (frame_type == 6 || (isf && frame_type == 4)) {
+	if (IOUT && frame_type == 6) {
+		hipLaunchKernelGGL((k_avg_copy<T>), dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st, bv, n, (T *) out,
+				   fl.as<uint32_t>());
+	} else if (frame_type == 6 || (isf && frame_type == 4)) {
 		hipLaunchKernelGGL((k_avg_row<T>), dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st, bv, n,
-				   frame_type == 4, out, fl.as<uint32_t>());
+				   frame_type == 4, (double *) out, fl.as<uint32_t>());
 	} else {
 		Starts part;
 		if (make_starts(p ? (const int8_t *) p->theap : nullptr, n, part, &Sp) < 0)
@@ -1089,7 +1145,7 @@ run_avg(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_ba
 			if constexpr (isf)
 				hipLaunchKernelGGL((k_avg_replay<T>), dim3((unsigned) ((part.m + 63) / 64)), dim3(64), 0, st, bv,
 						   part, frame_type == 3 ? (const int8_t *) o->theap : nullptr, frame_type == 3,
-						   out, fl.as<uint32_t>());
+						   (double *) out, fl.as<uint32_t>());
 		} else {
 			if (n >= 0xffffffffull) {
 				seterr("42000!GDKanalyticalavg: more than 2^32-1 rows on the device path\n");
@@ -1126,7 +1182,7 @@ run_avg(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_ba
 			for (int L = 1; L <= nlev; L++)
 				hipLaunchKernelGGL((k_avg_tree_level<T>), dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st, bv,
 						   part, pidx.as<uint32_t>(), t, L);
-			hipLaunchKernelGGL((k_avg_tree_query<T>), dim3(grid_for(n, 256, 16384)), dim3(256), 0, st, bv, part,
+			hipLaunchKernelGGL((k_avg_tree_query<T, IOUT>), dim3(grid_for(n, 256, 16384)), dim3(256), 0, st, bv, part,
 					   pidx.as<uint32_t>(), t, (const oid *) s->theap, (const oid *) e->theap, out,
 					   fl.as<uint32_t>());
 			if (!sync())
@@ -1249,5 +1305,64 @@ mgdk_GDKanalyticalavg(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_b
 	case MGDK_lng: return run_avg<int64_t>(r, p, o, b, s, e, frame_type);
 	case MGDK_flt: return run_avg<float>(r, p, o, b, s, e, frame_type);
 	default: return run_avg<double>(r, p, o, b, s, e, frame_type);
+	}
+}
+
+// GDKanalyticalavginteger (gdk/gdk_analytic_statistics.c:631): the average
+// in the input's integer type, rounded half away from zero; r is a
+// caller-allocated BAT of b's type
+extern "C" int
+mgdk_GDKanalyticalavginteger(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e, int tpe,
+			     int frame_type)
+{
+	if (r == nullptr || b == nullptr) {
+		seterr("GDKanalyticalavginteger: NULL argument");
+		return -1;
+	}
+	const int bt = basetype(tpe);
+	if (!(bt == MGDK_bte || bt == MGDK_sht || bt == MGDK_int || bt == MGDK_lng)) {
+		if (bt == MGDK_hge)
+			seterr("42000!GDKanalyticalavginteger: average of hge is not supported on the device path\n");
+		else
+			seterr("42000!average of type %s to int unsupported.\n", atomname(tpe));
+		return -1;
+	}
+	if (basetype(b->ttype) != bt || basetype(r->ttype) != bt) {
+		seterr("GDKanalyticalavginteger: b and r must be of type tpe");
+		return -1;
+	}
+	const BUN n = b->count;
+	if (n && r->theap == nullptr) {
+		seterr("analytic: result BAT has no heap");
+		return -1;
+	}
+	if (n == 0) {
+		r->count = 0;
+		r->tnil = 0;
+		r->tnonil = 1;
+		return 0;
+	}
+	if ((p && (p->count != n || width_of(p->ttype) != 1)) || (o && (o->count != n || width_of(o->ttype) != 1))) {
+		seterr("analytic: p and o must be bit BATs aligned with b");
+		return -1;
+	}
+	const bool frames = !(frame_type >= 3 && frame_type <= 6);
+	if (frames && (s == nullptr || e == nullptr || s->count < n || e->count < n || s->ttype != MGDK_oid ||
+		       e->ttype != MGDK_oid)) {
+		seterr("analytic: frame bounds s and e (oid BATs aligned with b) are required");
+		return -1;
+	}
+	if ((frame_type == 3 || frame_type == 4) && o == nullptr) {
+		seterr("analytic: the peer column o is required for this frame");
+		return -1;
+	}
+	ProfScope prof("analyticalavginteger");
+	if (frame_type == 3 || frame_type == 4 || frame_type == 5)
+		return run_frames(r, p, o, b, s, e, frame_type, false, false, false, false, width_of(bt));
+	switch (bt) {
+	case MGDK_bte: return run_avg<int8_t, true>(r, p, o, b, s, e, frame_type);
+	case MGDK_sht: return run_avg<int16_t, true>(r, p, o, b, s, e, frame_type);
+	case MGDK_int: return run_avg<int32_t, true>(r, p, o, b, s, e, frame_type);
+	default: return run_avg<int64_t, true>(r, p, o, b, s, e, frame_type);
 	}
 }

@@ -133,6 +133,7 @@ _SIGS = {
     "mgdk_GDKanalyticalsum": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_int, C.c_int]),
     "mgdk_GDKanalyticalcount": (C.c_int, [C.c_void_p] * 6 + [C.c_bool, C.c_int, C.c_int]),
     "mgdk_GDKanalyticalavg": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_int]),
+    "mgdk_GDKanalyticalavginteger": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_int]),
     "mgdk_BATlowerbound2": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
                                       C.c_void_p]),
     "mgdk_BATupload_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
@@ -576,6 +577,13 @@ def GDKanalyticalavg(b, p, o, s, e, frame_type):
     (gdk/gdk_analytic_statistics.c:364)."""
     r = BAT(lib().mgdk_COLnew(0, TYPE_dbl, max(1, b.count())))
     _chk(lib().mgdk_GDKanalyticalavg(r.ptr, _p(p), _p(o), b.ptr, _p(s), _p(e), b.ttype, frame_type))
+    return r
+
+
+def GDKanalyticalavginteger(b, p, o, s, e, frame_type):
+    """Windowed average in b's integer type (gdk/gdk_analytic_statistics.c:631)."""
+    r = BAT(lib().mgdk_COLnew(0, b.ttype, max(1, b.count())))
+    _chk(lib().mgdk_GDKanalyticalavginteger(r.ptr, _p(p), _p(o), b.ptr, _p(s), _p(e), b.ttype, frame_type))
     return r
 
 

@@ -22,7 +22,7 @@
  *   sort        gdk/gdk_batop.c:2266-2342, gdk/gdk_rsort.c:21 (stable)
  *   window      gdk/gdk_analytic_bounds.c:273-387, :994, :1440
  *   frames      gdk/gdk_analytic_func.c:1626 (count), :1959 (sum),
- *               gdk/gdk_analytic_statistics.c:364 (avg), segment
+ *               gdk/gdk_analytic_statistics.c:364 (avg), :428-700 (avginteger), segment
  *               tree gdk/gdk_analytic.h:52-130
  *   firstn      gdk/gdk_firstn.c:71-97 (heap), :211-1020, :1280
  *
@@ -142,6 +142,8 @@ int ora_analyticalsum(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_
 		      const ora_bat *s, const ora_bat *e, int tp1, int tp2, int frame_type);
 int ora_analyticalavg(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_bat *b,
 		      const ora_bat *s, const ora_bat *e, int tpe, int frame_type);
+int ora_analyticalavginteger(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_bat *b,
+			     const ora_bat *s, const ora_bat *e, int tpe, int frame_type);
 int ora_analyticalcount(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_bat *b,
 			const ora_bat *s, const ora_bat *e, bool ignore_nils, int frame_type);
 

@@ -652,3 +652,189 @@ ora_analyticalavg(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_bat 
 	r->nonil = !has_nils;
 	return 0;
 }
+
+/* ---------------------------------------------------------------------- */
+/* GDKanalyticalavginteger (gdk/gdk_analytic_statistics.c:428-700): the
+ * average in the input's integer type.  Every frame keeps AVERAGE_ITER's
+ * (avg, rem, ncnt) state -- row by row through the running frames
+ * (forward for 3 and 5, backward from the partition end for 4), over
+ * avg_int_deltas nodes of the same fanout-16 segment tree as
+ * GDKanalyticalavg for general frames -- and ends with
+ * ANALYTICAL_AVERAGE_INT_CALC_FINALIZE (:435-446, rounding half away from
+ * zero); no rows -> nil; frame 6 copies the values. */
+
+/* compute_on_segment_tree over one partition's tree (levels built by the
+ * caller as in ora_analyticalavg): the folded node of [begin, tend) */
+static anode
+avg_tree_query(int tp, anode *const *lvl, uint64_t nl, uint64_t begin, uint64_t tend)
+{
+	anode acc = {0};
+	if (begin < tend)
+		for (uint64_t level = 0; level < nl; level++) {
+			const anode *tl = lvl[level];
+			uint64_t pb = begin / FANOUT, pe = tend / FANOUT;
+			if (pb == pe) {
+				for (uint64_t pos = begin; pos < tend; pos++)
+					avg_fold(tp, &acc, &tl[pos]);
+				break;
+			}
+			uint64_t gb = pb * FANOUT;
+			if (begin != gb) {
+				for (uint64_t pos = begin; pos < gb + FANOUT; pos++)
+					avg_fold(tp, &acc, &tl[pos]);
+				pb++;
+			}
+			uint64_t ge = pe * FANOUT;
+			if (tend != ge)
+				for (uint64_t pos = ge; pos < tend; pos++)
+					avg_fold(tp, &acc, &tl[pos]);
+			begin = pb;
+			tend = pe;
+		}
+	return acc;
+}
+
+static void
+put_int(ora_bat *r, uint64_t k, int64_t v, bool nil)
+{
+	switch (r->width) {
+	case 1: ((int8_t *) r->base)[k] = nil ? INT8_MIN : (int8_t) v; break;
+	case 2: ((int16_t *) r->base)[k] = nil ? INT16_MIN : (int16_t) v; break;
+	case 4: ((int32_t *) r->base)[k] = nil ? INT32_MIN : (int32_t) v; break;
+	default: ((int64_t *) r->base)[k] = nil ? INT64_MIN : v; break;
+	}
+}
+
+/* ANALYTICAL_AVERAGE_INT_CALC_FINALIZE into slot k of r */
+static void
+avgint_put(ora_bat *r, uint64_t k, const anode *c, bool *has_nils)
+{
+	if (c->n == 0) {
+		*has_nils = true;
+		put_int(r, k, 0, true);
+		return;
+	}
+	int64_t avg = c->a;
+	if (c->rr > 0) {
+		if (avg < 0) {
+			if (2 * c->rr > c->n)
+				avg++;
+		} else if (2 * c->rr >= c->n) {
+			avg++;
+		}
+	}
+	put_int(r, k, avg, false);
+}
+
+int
+ora_analyticalavginteger(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_bat *b, const ora_bat *s,
+			 const ora_bat *e, int tpe, int frame_type)
+{
+	const int tp = b->type;
+	if (!(tp == ORA_bte || tp == ORA_sht || tp == ORA_int || tp == ORA_lng)) {
+		ora_seterr("42000!average of type %d to int unsupported.\n", tpe);
+		return -1;
+	}
+	const uint64_t cnt = b->count;
+	const ora_oid *start = s ? s->base : NULL, *end = e ? e->base : NULL;
+	bool has_nils = false;
+	anode *lv0 = calloc(cnt + 1, sizeof(anode));
+	if (!lv0)
+		return -1;
+	for (uint64_t i = 0; i < cnt; i++) {
+		if (isnil_any(b, i))
+			continue;
+		ora_hge v;
+		ival(b, i, &v);
+		lv0[i].n = 1;
+		lv0[i].a = (int64_t) v;
+	}
+	uint64_t k = 0;
+	for (uint64_t i = 1; i <= cnt; i++) {
+		if (i < cnt && !bit_at(p, i))
+			continue;
+		/* partition [k, i) */
+		if (frame_type == 3) {
+			anode c = {0};
+			while (k < i) {
+				uint64_t j = k;
+				do {
+					avg_fold(tp, &c, &lv0[k]);
+					k++;
+				} while (k < i && !bit_at(o, k));
+				for (; j < k; j++)
+					avgint_put(r, j, &c, &has_nils);
+			}
+		} else if (frame_type == 4) {
+			anode c = {0};
+			uint64_t l = i - 1;
+			for (uint64_t j = l;; j--) {
+				avg_fold(tp, &c, &lv0[j]);
+				if (bit_at(o, j) || j == k) {
+					for (;; l--) {
+						avgint_put(r, l, &c, &has_nils);
+						if (l == j)
+							break;
+					}
+					if (j == k)
+						break;
+					l = j - 1;
+				}
+			}
+			k = i;
+		} else if (frame_type == 5) {
+			anode c = {0};
+			for (uint64_t j = k; j < i; j++)
+				avg_fold(tp, &c, &lv0[j]);
+			for (; k < i; k++)
+				avgint_put(r, k, &c, &has_nils);
+		} else if (frame_type == 6) {
+			for (; k < i; k++) {
+				avgint_put(r, k, &lv0[k], &has_nils);
+			}
+		} else {
+			const uint64_t j = k, nc = i - k;
+			uint64_t total = nc, c = nc, nl = 1;
+			do {
+				c = (c + FANOUT - 1) / FANOUT;
+				total += c;
+				nl++;
+			} while (c > 1);
+			anode *tree = calloc(total, sizeof(anode));
+			anode **lvl = malloc(nl * sizeof(anode *));
+			if (!tree || !lvl) {
+				free(tree);
+				free(lvl);
+				free(lv0);
+				return -1;
+			}
+			memcpy(tree, lv0 + j, nc * sizeof(anode));
+			lvl[0] = tree;
+			uint64_t to = nc, lsize = nc, prev = 0;
+			for (uint64_t cur = 1; cur < nl; cur++) {
+				uint64_t prev_to = to;
+				lvl[cur] = tree + to;
+				for (uint64_t pos = 0; pos < lsize; pos += FANOUT) {
+					uint64_t pend = pos + FANOUT < lsize ? pos + FANOUT : lsize;
+					anode acc = {0};
+					for (uint64_t x = pos; x < pend; x++)
+						avg_fold(tp, &acc, &tree[prev + x]);
+					tree[to++] = acc;
+				}
+				prev = prev_to;
+				lsize = to - prev_to;
+			}
+			for (; k < i; k++) {
+				anode acc = avg_tree_query(tp, lvl, nl, start[k] - j, end[k] - j);
+				avgint_put(r, k, &acc, &has_nils);
+			}
+			free(tree);
+			free(lvl);
+		}
+	}
+	free(lv0);
+	r->count = cnt;
+	r->nil = has_nils;
+	r->nonil = !has_nils;
+	return 0;
+}

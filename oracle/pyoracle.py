@@ -92,6 +92,7 @@ def lib():
         L.ora_rangebounds.argtypes = [P, P, P, C.c_void_p, C.c_int, C.c_bool, C.c_uint64]
         L.ora_analyticalsum.argtypes = [P, P, P, P, P, P, C.c_int, C.c_int, C.c_int]
         L.ora_analyticalavg.argtypes = [P, P, P, P, P, P, C.c_int, C.c_int]
+        L.ora_analyticalavginteger.argtypes = [P, P, P, P, P, P, C.c_int, C.c_int]
         L.ora_analyticalcount.argtypes = [P, P, P, P, P, P, C.c_bool, C.c_int]
         L.ora_tpch_lineitem.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64] + [C.c_void_p] * 7
         L.ora_mkdate.restype = C.c_int32
@@ -335,6 +336,16 @@ def analyticalavg(b, p, o, s, e, frame_type):
     if lib().ora_analyticalavg(r, p.ptr if p else None, o.ptr if o else None, b.ptr,
                                s.ptr if s else None, e.ptr if e else None, b.s.type,
                                frame_type) < 0:
+        lib().ora_free(r)
+        raise _err()
+    return Bat(r)
+
+
+def analyticalavginteger(b, p, o, s, e, frame_type):
+    r = lib().ora_new(b.s.type, b.count(), 0)
+    if lib().ora_analyticalavginteger(r, p.ptr if p else None, o.ptr if o else None, b.ptr,
+                                      s.ptr if s else None, e.ptr if e else None, b.s.type,
+                                      frame_type) < 0:
         lib().ora_free(r)
         raise _err()
     return Bat(r)

@@ -238,3 +238,41 @@ def test_analytical_avg_edges(gdk):
     e = gdk.BAT.from_numpy(gdk.TYPE_oid, np.array([1, 2, 3, 4], np.uint64))
     got = gdk.GDKanalyticalavg(gdk.BAT.from_numpy(gdk.TYPE_lng, v), None, None, s, e, 1).values()
     assert np.isnan(got[0]) and np.isnan(got[1]) and got[2] == 4.0 and np.isnan(got[3])
+
+
+@pytest.mark.parametrize("tname", ["bte", "sht", "int", "lng"])
+@pytest.mark.parametrize("frame", [3, 4, 5, 6, 1])
+def test_analytical_avginteger(gdk, ora, tname, frame):
+    """GDKanalyticalavginteger (gdk_analytic_statistics.c:631) bit-exact
+    against the oracle's AVERAGE_ITER replay: rounded exact averages over
+    the running frames, the segment tree's state over general frames."""
+    r = rng(313)
+    _, p, o, ob = _data(r, nparts=31, plen=900)
+    n = len(p)
+    v = _avg_input(r, tname, n)
+    tp = getattr(gdk, "TYPE_" + tname)
+    s = e = None
+    if frame == 1:
+        s, e = _bounds(gdk, ob, p, 40)
+    got = gdk.GDKanalyticalavginteger(gdk.BAT.from_numpy(tp, v), gdk.BAT.from_numpy(gdk.TYPE_bit, p),
+                                      gdk.BAT.from_numpy(gdk.TYPE_bit, o), s, e, frame)
+    os_ = ora.Bat.from_array(ora.TYPE_oid, s.to_numpy()) if s else None
+    oe = ora.Bat.from_array(ora.TYPE_oid, e.to_numpy()) if e else None
+    want = ora.analyticalavginteger(ora.Bat.from_array(tp, v), ora.Bat.from_array(ora.TYPE_bit, p),
+                                    ora.Bat.from_array(ora.TYPE_bit, o), os_, oe, frame)
+    assert np.array_equal(got.to_numpy(), np.asarray(want.values()))
+    assert bool(got.s.tnil) == bool(want.s.nil)
+
+
+def test_analytical_avginteger_deep_tree(gdk, ora):
+    r = rng(314)
+    n = 120_000
+    v = _avg_input(r, "lng", n)
+    i = np.arange(n)
+    s = np.maximum(0, i - r.integers(0, 60_000, n)).astype(np.uint64)
+    e = np.minimum(n, i + 1 + r.integers(0, 60_000, n)).astype(np.uint64)
+    got = gdk.GDKanalyticalavginteger(gdk.BAT.from_numpy(gdk.TYPE_lng, v), None, None,
+                                      gdk.BAT.from_numpy(gdk.TYPE_oid, s), gdk.BAT.from_numpy(gdk.TYPE_oid, e), 1)
+    want = ora.analyticalavginteger(ora.Bat.from_array(ora.TYPE_lng, v), None, None,
+                                    ora.Bat.from_array(ora.TYPE_oid, s), ora.Bat.from_array(ora.TYPE_oid, e), 1)
+    assert np.array_equal(got.to_numpy(), np.asarray(want.values()))

@@ -294,7 +294,7 @@ def _avg_iter(x, st):
     return [a, rr, n]
 
 
-def _tree_avg(vals, s, e):
+def _tree_avg(vals, s, e, fin=None):
     """segment-tree AVG of one partition (gdk_analytic.h:63-130): nodes
     [a, rr, n], inner nodes fold their non-empty children's a"""
     levels = [[[v, 0, 1] if v is not None else [0, 0, 0] for v in vals]]
@@ -327,6 +327,9 @@ def _tree_avg(vals, s, e):
                     if x[2]:
                         acc = _avg_iter(x[0], acc)
                 b, t = pb, pe
+        if fin is not None:
+            out.append(fin(acc))
+            continue
         out.append(math.nan if acc[2] == 0 else acc[0] + acc[1] / acc[2])
     return out
 
@@ -385,3 +388,67 @@ def test_groupavg3combine_oracle(ora):
     full, _, _ = ora.BATgroupavg3(ora.Bat.from_array(ora.TYPE_lng, v), ora.Bat.from_array(ora.TYPE_oid, gid),
                                   None, True)
     assert list(comb.values()) == list(full.values())
+
+
+def _round_avg(a, rr, n):
+    """ANALYTICAL_AVERAGE_INT_CALC_FINALIZE: half away from zero"""
+    if rr > 0 and (2 * rr > n if a < 0 else 2 * rr >= n):
+        a += 1
+    return a
+
+
+def test_window_avginteger_oracle(ora):
+    """GDKanalyticalavginteger (gdk_analytic_statistics.c:428-700): running
+    frames give the exact average rounded half away from zero (checked with
+    Python integers); general frames the segment tree's folded state,
+    rounded the same way (checked with the Python tree restatement)."""
+    r = np.random.default_rng(13)
+    sizes = [500, 300, 1]
+    n = sum(sizes)
+    v = r.integers(-10**6, 10**6, n).astype(np.int32)
+    v[r.random(n) < 0.05] = -(2**31)
+    p = np.zeros(n, np.int8)
+    p[np.cumsum([0] + sizes[:-1])] = 1
+    ob = np.concatenate([np.sort(r.integers(0, sz // 4 + 1, sz)) for sz in sizes])
+    o = p.copy()
+    o[1:] |= (ob[1:] != ob[:-1]).astype(np.int8)
+    B, P, O = (ora.Bat.from_array(ora.TYPE_int, v), ora.Bat.from_array(ora.TYPE_bit, p),
+               ora.Bat.from_array(ora.TYPE_bit, o))
+    NIL = -(2**31)
+
+    def exact(xs):
+        xs = [int(x) for x in xs if x != NIL]
+        if not xs:
+            return NIL
+        q, m = divmod(sum(xs), len(xs))
+        return _round_avg(q, m, len(xs))
+    got5 = ora.analyticalavginteger(B, P, O, None, None, 5).values()
+    got3 = ora.analyticalavginteger(B, P, O, None, None, 3).values()
+    got4 = ora.analyticalavginteger(B, P, O, None, None, 4).values()
+    k = 0
+    for sz in sizes:
+        part = v[k:k + sz]
+        pstart = np.flatnonzero(o[k:k + sz])
+        pend = np.append(pstart[1:], sz)
+        for a, b_ in zip(pstart, pend):
+            assert all(got5[k + i] == exact(part) for i in range(a, b_))
+            assert all(got3[k + i] == exact(part[:b_]) for i in range(a, b_))
+            assert all(got4[k + i] == exact(part[a:]) for i in range(a, b_))
+        k += sz
+    s = np.empty(n, np.uint64)
+    e = np.empty(n, np.uint64)
+    k = 0
+    for sz in sizes:
+        for i in range(sz):
+            s[k + i] = k + max(0, i - int(r.integers(0, 200)))
+            e[k + i] = k + min(sz, i + 1 + int(r.integers(0, 200)))
+        k += sz
+    got = ora.analyticalavginteger(B, P, None, ora.Bat.from_array(ora.TYPE_oid, s),
+                                   ora.Bat.from_array(ora.TYPE_oid, e), 1).values()
+    k = 0
+    for sz in sizes:
+        vals = [None if x == NIL else int(x) for x in v[k:k + sz]]
+        want = _tree_avg(vals, [int(x) - k for x in s[k:k + sz]], [int(x) - k for x in e[k:k + sz]],
+                         fin=lambda acc: NIL if acc[2] == 0 else _round_avg(acc[0], acc[1], acc[2]))
+        assert list(got[k:k + sz]) == want
+        k += sz
