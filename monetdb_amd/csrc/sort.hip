@@ -87,15 +87,15 @@ k_rs_dhist(const K *keys, BUN n, Shifts sh, uint32_t *out)
 	__syncthreads();
 	for (int p = 0; p < sh.n; p++)
 		if (h[p][threadIdx.x])
-			atomicAdd(&out[p * 256 + threadIdx.x], h[p][threadIdx.x]);
+			atomicAdd(&out[(sh.s[p] / 8) * 256 + threadIdx.x], h[p][threadIdx.x]);
 }
 
 // exclusive scan of each pass's 256 digit counts (one workgroup per pass)
 __global__ __launch_bounds__(256) void
-k_rs_dscan(const uint32_t *cnt, uint32_t *gdig)
+k_rs_dscan(const uint32_t *cnt, Shifts sh, uint32_t *gdig)
 {
 	__shared__ uint32_t ws[4];
-	const uint32_t v = cnt[blockIdx.x * 256 + threadIdx.x];
+	const uint32_t v = cnt[(sh.s[blockIdx.x] / 8) * 256 + threadIdx.x];
 	const unsigned lane = __lane_id(), w = threadIdx.x >> 6;
 	uint32_t x = v;
 #pragma unroll
@@ -368,14 +368,33 @@ keyimg(T v, bool reverse, bool nilslast)
 // key images + their AND/OR (constant digits are skipped by the passes)
 template <typename T, typename K>
 __global__ __launch_bounds__(256) void
-k_keys(const T *col, BUN n, bool reverse, bool nilslast, K *keys, unsigned long long *andor)
+k_keys(const T *col, BUN n, bool reverse, bool nilslast, K *keys, unsigned long long *andor, uint32_t *dh)
 {
+	// dh: the digit counts of every byte position (row b = bits 8b..8b+7),
+	// for the radix passes' global digit starts (no separate read)
+	constexpr int NBYTES = (int) sizeof(K);
+	__shared__ uint32_t h[NBYTES][256];
+	if (dh) {
+		for (int q = 0; q < NBYTES; q++)
+			h[q][threadIdx.x] = 0;
+		__syncthreads();
+	}
 	unsigned long long a = ~0ull, o = 0;
 	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
 		const K k = keyimg<T, K>(col[i], reverse, nilslast);
 		keys[i] = k;
 		a &= (unsigned long long) k;
 		o |= (unsigned long long) k;
+		if (dh)
+#pragma unroll
+			for (int q = 0; q < NBYTES; q++)
+				atomicAdd(&h[q][(uint32_t) (k >> (8 * q)) & 255], 1u);
+	}
+	if (dh) {
+		__syncthreads();
+		for (int q = 0; q < NBYTES; q++)
+			if (h[q][threadIdx.x])
+				atomicAdd(&dh[q * 256 + threadIdx.x], h[q][threadIdx.x]);
 	}
 	a = block_reduce(a, [](unsigned long long x, unsigned long long y) { return x & y; });
 	o = block_reduce(o, [](unsigned long long x, unsigned long long y) { return x | y; });
@@ -494,7 +513,7 @@ k_gid(const uint64_t *excl, const uint8_t *flag, BUN n, oid *gid)
 template <typename K>
 int
 radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int bits, const FinalOut *fo,
-	   bool positions, bool andor, K **keys_out, uint32_t **vals_out)
+	   bool positions, bool andor, K **keys_out, uint32_t **vals_out, const uint32_t *digit_hist = nullptr)
 {
 	*keys_out = keys;
 	*vals_out = vals;
@@ -529,12 +548,17 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 		sh.n = (int) shifts.size();
 		for (int q = 0; q < sh.n; q++)
 			sh.s[q] = shifts[q];
-		if (!hip_ok(hipMemsetAsync(dcnt.p, 0, RS_MAXP * 256 * 4, st), "memset") ||
-		    !hip_ok(hipMemsetAsync(lbm.p, 0, 64, st), "memset"))
+		if (!hip_ok(hipMemsetAsync(lbm.p, 0, 64, st), "memset"))
 			return -1;
-		hipLaunchKernelGGL((k_rs_dhist<K>), dim3(grid_for(n, 16384, 2048)), dim3(256), 0, st, keys, n, sh,
-				   dcnt.as<uint32_t>());
-		hipLaunchKernelGGL(k_rs_dscan, dim3(sh.n), dim3(256), 0, st, dcnt.as<uint32_t>(), gdig);
+		const uint32_t *dh = digit_hist;
+		if (dh == nullptr) {
+			if (!hip_ok(hipMemsetAsync(dcnt.p, 0, RS_MAXP * 256 * 4, st), "memset"))
+				return -1;
+			hipLaunchKernelGGL((k_rs_dhist<K>), dim3(grid_for(n, 16384, 2048)), dim3(256), 0, st, keys, n, sh,
+					   dcnt.as<uint32_t>());
+			dh = dcnt.as<uint32_t>();
+		}
+		hipLaunchKernelGGL(k_rs_dscan, dim3(sh.n), dim3(256), 0, st, dh, sh, gdig);
 	}
 	K *kin = keys, *kout = keys_alt;
 	uint32_t *vin = vals, *vout = vals_alt;
@@ -622,8 +646,11 @@ sort_typed(const mgdk_bat *b, bool reverse, bool nilslast, mgdk_bat *sn, mgdk_ba
 	unsigned long long init[2] = {~0ull, 0ull};
 	if (!hip_ok(hipMemcpyAsync(ao, init, 16, hipMemcpyHostToDevice, st), "memcpy"))
 		return -1;
+	DevBuf dh(8 * 256 * 4);
+	if (!dh.p || !hip_ok(hipMemsetAsync(dh.p, 0, 8 * 256 * 4, st), "memset"))
+		return -1;
 	hipLaunchKernelGGL((k_keys<T, K>), dim3(grid_for(n, 2048, 4096)), dim3(256), 0, st, (const T *) b->theap, n,
-			   reverse, nilslast, k0.as<K>(), ao);
+			   reverse, nilslast, k0.as<K>(), ao, dh.as<uint32_t>());
 	FinalOut fo{};
 	fo.vw = b->twidth;
 	fo.reverse = reverse;
@@ -638,7 +665,7 @@ sort_typed(const mgdk_bat *b, bool reverse, bool nilslast, mgdk_bat *sn, mgdk_ba
 	K *ks;
 	uint32_t *vs;
 	if (radix_sort<K>(k0.as<K>(), v0.as<uint32_t>(), k1.as<K>(), v1.as<uint32_t>(), n, 8 * (int) sizeof(K), &fo,
-			  true, true, &ks, &vs) < 0)
+			  true, true, &ks, &vs, dh.as<uint32_t>()) < 0)
 		return -1;
 	if (sn && !decodable) {
 		switch (b->twidth) {
