@@ -1180,15 +1180,17 @@ join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_b
 	uint32_t *h = (uint32_t *) pinned(64);
 	if (!hip_ok(hipMemsetAsync(meta32, 0, 64, st), "memset"))
 		return -1;
+	// both sides are cut before the host looks at the build side's largest
+	// partition: one round trip instead of two (an oversized partition, rare,
+	// wastes the probe side's cut)
 	PjSide B, Pr;
-	if (pj_cut(R, nr, pbits, !nil_matches, B, &meta32[0]) < 0)
+	if (pj_cut(R, nr, pbits, !nil_matches, B, &meta32[0]) < 0 ||
+	    pj_cut(L, nl, pbits, !nil_matches, Pr, &meta32[1]) < 0)
 		return -1;
 	if (!hip_ok(hipMemcpyAsync(h, meta32, 4, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
 		return -1;
 	if (h[0] > PJ_MAXFILL)
 		return 1;
-	if (pj_cut(L, nl, pbits, !nil_matches, Pr, &meta32[1]) < 0)
-		return -1;
 	// subtile-major offsets of the probe results
 	DevBuf offT((size_t) Pr.nsub * P * 4 + 64);
 	uint64_t total = 0;
