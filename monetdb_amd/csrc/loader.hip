@@ -103,8 +103,11 @@ mgdk_BBPreaddir(const char *path, mgdk_bbpentry *out, int maxn, int *nout)
 		seterr("BBPreaddir: %s is not a BBP.dir", path);
 		goto out;
 	}
-	if (version < 061050U) {
-		seterr("BBPreaddir: BBP.dir version %o not supported (needs %o)", version, 061050U);
+	// gdk_bbp.c:990-998 refuses newer versions; older ones (which the
+	// reference upgrades in place) use other line formats than the one parsed here
+	if (version != 061050U) {
+		seterr("BBPreaddir: incompatible BBP version: expected 0%o, got 0%o (%s)", 061050U, version,
+		       version > 061050U ? "newer" : "too old");
 		goto out;
 	}
 	if (!fgets(buf, sizeof(buf), fp) || sscanf(buf, "%d %d %d", &szsize, &szoid, &szhge) != 3 || szoid != 8) {
@@ -200,28 +203,31 @@ mgdk_BATload(const char *bat_dir, const mgdk_bbpentry *e)
 	ProfScope prof("batload");
 	char path[1024];
 	snprintf(path, sizeof(path), "%s/%s", bat_dir, e->tail);
-	FILE *fp = fopen(path, "rb");
-	if (fp == nullptr) {
+	const size_t bytes = (size_t) e->count * (size_t) w;
+	// HEAPsave writes no file for an empty heap (gdk_heap.c:871-884) and
+	// HEAPload creates an empty one (:826-831): nothing to read then
+	FILE *fp = bytes ? fopen(path, "rb") : nullptr;
+	if (bytes && fp == nullptr) {
 		seterr("BATload: cannot open %s: %s", path, strerror(errno));
 		return nullptr;
 	}
 	// str: the tail holds heap offsets of e->width bytes
 	mgdk_bat *b = newbat(e->hseqbase, e->tt, e->tt == MGDK_str ? e->count * (BUN) w : e->count);
 	if (b == nullptr) {
-		fclose(fp);
+		if (fp)
+			fclose(fp);
 		return nullptr;
 	}
 	b->twidth = w;
-	const size_t bytes = (size_t) e->count * (size_t) w;
 	const size_t CH = (size_t) 64 << 20;
 	hipStream_t st = stream();
 	char *stage = nullptr;
-	if (!hip_ok(hipHostMalloc((void **) &stage, 2 * CH, hipHostMallocDefault), "hipHostMalloc"))
+	if (bytes && !hip_ok(hipHostMalloc((void **) &stage, 2 * CH, hipHostMallocDefault), "hipHostMalloc"))
 		stage = nullptr;
 	hipEvent_t ev[2];
 	bool okev = hip_ok(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming), "event") &&
 		    hip_ok(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming), "event");
-	bool ok = stage != nullptr && okev;
+	bool ok = (bytes == 0 || stage != nullptr) && okev;
 	bool used[2] = {false, false};
 	size_t off = 0;
 	int k = 0;
@@ -243,7 +249,8 @@ mgdk_BATload(const char *bat_dir, const mgdk_bbpentry *e)
 		off += len;
 		k ^= 1;
 	}
-	fclose(fp);
+	if (fp)
+		fclose(fp);
 	ok = ok && sync();
 	if (okev) {
 		(void) hipEventDestroy(ev[0]);
@@ -251,7 +258,9 @@ mgdk_BATload(const char *bat_dir, const mgdk_bbpentry *e)
 	}
 	if (stage)
 		(void) hipHostFree(stage);
-	if (ok && e->tt == MGDK_str && e->theap[0]) {
+	if (ok && e->tt == MGDK_str && e->theap[0] && e->vfree == 0) {
+		ok = mgdk_BATsetvheap(b, nullptr, 0) == 0;
+	} else if (ok && e->tt == MGDK_str && e->theap[0]) {
 		snprintf(path, sizeof(path), "%s/%s", bat_dir, e->theap);
 		FILE *vf = fopen(path, "rb");
 		std::vector<char> vh(e->vfree ? e->vfree : 1);

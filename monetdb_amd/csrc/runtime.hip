@@ -141,6 +141,13 @@ dfree(void *p)
 {
 	if (p == nullptr)
 		return;
+	// A block goes back to the shared cache only once the freeing thread's
+	// stream is idle: operators synchronise before they return, so this
+	// costs one query on the normal path, and an error path that leaves
+	// kernels in flight (reading or writing the block) drains them here
+	// before another thread can be handed the block.
+	if (tctx.s && hipStreamQuery(tctx.s) == hipErrorNotReady)
+		(void) hipStreamSynchronize(tctx.s);
 	std::lock_guard<std::mutex> g(alloc_mu);
 	auto it = live.find(p);
 	if (it == live.end())
@@ -713,7 +720,9 @@ mgdk_BATupload(mgdk_bat *b, const void *host, mgdk_BUN n)
 	}
 	Priv *p = (Priv *) b->priv;
 	size_t bytes = n * (size_t) b->twidth;
-	if (p->theap == nullptr || p->theap->size < bytes + ((char *) b->theap - (char *) p->theap->base)) {
+	// a heap shared with views (refs > 1) is never written in place
+	if (p->theap == nullptr || p->theap->refs != 1 ||
+	    p->theap->size < bytes + ((char *) b->theap - (char *) p->theap->base)) {
 		Heap *h = heap_new(bytes ? bytes : 1);
 		if (h == nullptr)
 			return -1;
@@ -751,8 +760,10 @@ mgdk_BATsetvheap(mgdk_bat *b, const void *host, uint64_t size)
 	Heap *h = heap_new(size ? size : 1);
 	if (h == nullptr)
 		return -1;
-	if (size && !hip_ok(hipMemcpyAsync(h->base, host, size, hipMemcpyHostToDevice, stream()), "vheap"))
+	if (size && !hip_ok(hipMemcpyAsync(h->base, host, size, hipMemcpyHostToDevice, stream()), "vheap")) {
+		heap_decref(h);
 		return -1;
+	}
 	heap_decref(p->tvheap);
 	p->tvheap = h;
 	b->tvheap = h->base;
@@ -800,6 +811,7 @@ mgdk_BATappend(mgdk_bat *b, mgdk_bat *n, mgdk_bat *s, bool force)
 	}
 	const BUN cnt = src->count;
 	int rc = -1;
+	Heap *old_heap = nullptr;
 	if (cnt == 0) {
 		rc = 0;
 		goto out;
@@ -856,7 +868,9 @@ mgdk_BATappend(mgdk_bat *b, mgdk_bat *n, mgdk_bat *s, bool force)
 					goto out;
 				}
 			}
-			heap_decref(p->theap);
+			// the old heap is still being read by the copy just queued:
+			// release it only after the stream has drained (below)
+			old_heap = p->theap;
 			p->theap = h;
 			b->theap = h->base;
 			if (b->ttype == MGDK_void) {
@@ -873,6 +887,8 @@ mgdk_BATappend(mgdk_bat *b, mgdk_bat *n, mgdk_bat *s, bool force)
 			goto out;
 		if (!sync())
 			goto out;
+		heap_decref(old_heap);
+		old_heap = nullptr;
 		const bool wasempty = b->count == 0;
 		b->count = total;
 		// properties the append cannot vouch for are cleared (BATappend2
@@ -885,6 +901,10 @@ mgdk_BATappend(mgdk_bat *b, mgdk_bat *n, mgdk_bat *s, bool force)
 		rc = 0;
 	}
 out:
+	if (old_heap) {
+		(void) hipStreamSynchronize(stream());   // error path: drain before release
+		heap_decref(old_heap);
+	}
 	mgdk_BBPunfix(proj);
 	return rc;
 }

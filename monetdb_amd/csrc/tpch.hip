@@ -26,6 +26,8 @@
 #include <algorithm>
 #include <vector>
 
+#include <atomic>
+
 #include "mgdk_internal.h"
 
 using namespace mgdk;
@@ -759,9 +761,11 @@ mgdk_tpch_lineitem(uint64_t seed, uint64_t row0, uint64_t n, uint64_t sf_parts, 
 // contiguous 256-row chunks per wave (1 KiB per lng load instruction),
 // 4 chunks in flight, nontemporal loads, 12 WG/CU (odd WG/CU counts lose
 // 5-7 % with this layout)
-static int q6_variant = 14, q6_bpc = 12;
+// tuning hooks: atomics, so a concurrent set/launch never tears (dataflow
+// workers call the library concurrently, SURVEY §8 b)
+static std::atomic<int> q6_variant{14}, q6_bpc{12};
 // fused Q1 main pass (tools/q1_tune.py, profiles/r01/q1_tune.log)
-static int q1_layout = MGDK_Q1_LAYOUT, q1_blocks = MGDK_Q1_BLOCKS;
+static std::atomic<int> q1_layout{MGDK_Q1_LAYOUT}, q1_blocks{MGDK_Q1_BLOCKS};
 
 static void
 launch_q6(const Q6Args &a, int variant, int bpc, hipStream_t st)
@@ -835,7 +839,7 @@ mgdk_q6_fused(mgdk_bat *shipdate, mgdk_bat *discount, mgdk_bat *quantity, mgdk_b
 		if (a.n) {
 			bool al = aligned16(a.sd) && aligned16(a.disc) && aligned16(a.qty) && aligned16(a.price);
 			if (al)
-				launch_q6(a, q6_variant, q6_bpc, st);
+				launch_q6(a, q6_variant.load(), q6_bpc.load(), st);
 			else
 				hipLaunchKernelGGL(k_q6_scalar, dim3(grid_for(a.n, 256 * 4, 256 * 16)), dim3(256), 0, st, a);
 		}
@@ -915,7 +919,7 @@ mgdk_q1_fused(mgdk_bat *shipdate, mgdk_bat *returnflag, mgdk_bat *linestatus, mg
 	a.acc = acc.as<unsigned long long>();
 	a.flags = (uint32_t *) (a.acc + Q1_MAXK * 12);
 	const int layout = q1_layout;
-	dim3 g(grid_for(n / 4 + 1, 256, MGDK_Q1_MODE == 0 ? 4096 : (unsigned) q1_blocks)), blk(256);
+	dim3 g(grid_for(n / 4 + 1, 256, MGDK_Q1_MODE == 0 ? 4096 : (unsigned) q1_blocks.load())), blk(256);
 	const uint64_t threads = (uint64_t) g.x * 256;
 	// rows one lane can see: quads (layout 0) or 4 rows per 256-row chunk
 	// per wave (layout 1), plus the tail rows

@@ -29,11 +29,11 @@ def props(sorted_=False, revsorted=False, key=False, dense=False, nonil=False, n
             | int(nil) << 11)
 
 
-def write_dbfarm(bat_dir, bats):
+def write_dbfarm(bat_dir, bats, version=GDKLIBRARY):
     """bats: list of dicts {id, name, type, values (numpy) | strings (list),
     hseqbase, props}"""
     os.makedirs(bat_dir, exist_ok=True)
-    lines = ["BBP.dir, GDKversion %d" % GDKLIBRARY, "8 8 16", "BBPsize=%d" % (max(b["id"] for b in bats) + 1),
+    lines = ["BBP.dir, GDKversion %d" % version, "8 8 16", "BBPsize=%d" % (max(b["id"] for b in bats) + 1),
              "BBPinfo=0"]
     for b in bats:
         phys = physical(b["id"])
@@ -70,8 +70,9 @@ def write_dbfarm(bat_dir, bats):
         else:
             v = np.ascontiguousarray(b["values"])
             w = TYPES[tp]
-            with open(os.path.join(bat_dir, phys + ".tail"), "wb") as f:
-                f.write(v.tobytes())
+            if len(v):      # HEAPsave writes no file for an empty heap (gdk_heap.c:871-884)
+                with open(os.path.join(bat_dir, phys + ".tail"), "wb") as f:
+                    f.write(v.tobytes())
             n = len(v)
             lines.append("%d %s %d %d %d %s %d 0 %d 0 0 0 0 %d %d %d %d" % (
                 b["id"], b["name"], 0, n, b.get("hseqbase", 0), tp, w, b.get("props", 0), 1 << 63, n * w,

@@ -23,6 +23,7 @@ def _farm(tmp_path):
         {"id": 0o123456, "name": "sys_lineitem_l_returnflag", "type": "str",
          "strings": [["A", "N", "R"][i % 3] for i in range(3001)]},
         {"id": 9, "name": "sys_dense", "type": "void", "count": 77, "tseqbase": 1000},
+        {"id": 10, "name": "sys_empty", "type": "lng", "values": np.zeros(0, np.int64), "props": 0},
     ]
     write_dbfarm(str(tmp_path), bats)
     return bats
@@ -40,6 +41,18 @@ def test_bbpdir_parse(tmp_path):
     assert ents[1].tail == b"12/1234.tail"
     assert ents[2].tail == b"12/34/123456.tail1" and ents[2].theap == b"12/34/123456.theap" and ents[2].var
     assert ents[3].type == b"void" and ents[3].tseqbase == 1000
+    assert ents[4].count == 0 and not (tmp_path / "12.tail").exists()
+
+
+def test_bbpdir_version(tmp_path):
+    # gdk_bbp.c:990-998: a BBP.dir of another library version is refused
+    from monetdb_amd import gdk
+    from dbfarm_writer import GDKLIBRARY
+    bats = [{"id": 3, "name": "x", "type": "lng", "values": np.arange(3, dtype=np.int64)}]
+    for v, word in ((GDKLIBRARY + 1, "newer"), (0o61047, "too old")):
+        write_dbfarm(str(tmp_path), bats, version=v)
+        with pytest.raises(gdk.GDKError, match=word):
+            gdk.BBPreaddir(str(tmp_path / "BBP.dir"))
 
 
 @pytest.mark.gpu
@@ -60,3 +73,6 @@ def test_batload(gdk, tmp_path):
     # a loaded column feeds the operators: thetaselect on the loaded lng
     sel = gdk.BATthetaselect(q, None, 2400, "<")
     assert sel.count() == int((bats[0]["values"] < 2400).sum())
+    # an empty persistent BAT has no tail file (HEAPsave wrote none)
+    z = gdk.BATload(str(tmp_path), ents[4])
+    assert z.count() == 0 and z.ttype == gdk.TYPE_lng
