@@ -20,7 +20,7 @@
  *   group       gdk/gdk_group.c:657-1347 (first-occurrence numbering)
  *   join        gdk/gdk_join.c:2781-2900 (hash join result order)
  *   sort        gdk/gdk_batop.c:2266-2342, gdk/gdk_rsort.c:21 (stable)
- *   window      gdk/gdk_analytic_bounds.c:273-387, :994, :1440
+ *   window      gdk/gdk_analytic_bounds.c:187-587, :855-1440 (gdk_oracle_bounds.c)
  *   frames      gdk/gdk_analytic_func.c:1626 (count), :1959 (sum),
  *               gdk/gdk_analytic_statistics.c:364 (avg), :428-700 (avginteger), segment
  *               tree gdk/gdk_analytic.h:52-130
@@ -47,7 +47,7 @@ typedef __int128 ora_hge;
 enum {
 	ORA_void = 0, ORA_msk = 1, ORA_bit = 2, ORA_bte = 3, ORA_sht = 4,
 	ORA_int = 5, ORA_oid = 6, ORA_flt = 8, ORA_dbl = 9, ORA_lng = 10,
-	ORA_hge = 11, ORA_date = 12, ORA_str = 16,
+	ORA_hge = 11, ORA_date = 12, ORA_daytime = 13, ORA_timestamp = 14, ORA_str = 16,
 };
 
 #define ORA_OID_NIL ((ora_oid) 1 << 63)
@@ -101,8 +101,15 @@ int ora_join(ora_bat **r1p, ora_bat **r2p, const ora_bat *l, const ora_bat *r,
 	     const ora_bat *sl, const ora_bat *sr, bool nil_matches);
 int ora_sort(ora_bat **sorted, ora_bat **order, const ora_bat *b,
 	     bool reverse, bool nilslast);
-int ora_rangebounds(ora_bat *r, const ora_bat *b, const ora_bat *p,
-		    const void *bound, int tp2, bool preceding, ora_oid first_half);
+/* GDKanalyticalwindowbounds, all units / types (gdk_oracle_bounds.c);
+ * r is caller-allocated with count(b) oid slots */
+int ora_windowbounds(ora_bat *r, const ora_bat *b, const ora_bat *p, const ora_bat *l, const void *bound,
+		     int tp1, int tp2, int unit, bool preceding, ora_oid second_half);
+int32_t ora_date_add_day(int32_t dt, int days);
+int32_t ora_date_add_month(int32_t dt, int months);
+int64_t ora_daytime_add_usec(int64_t t, int64_t usec);
+int64_t ora_timestamp_add_usec(int64_t ts, int64_t usec);
+int64_t ora_timestamp_add_month(int64_t ts, int m);
 /* plain first-N (no group ids, not distinct), heap semantics of
  * gdk/gdk_firstn.c:211-1020 (gdk_oracle_firstn.c) */
 ora_bat *ora_firstn(const ora_bat *b, const ora_bat *s, const ora_bat *g, uint64_t n,

@@ -902,74 +902,3 @@ ora_sort(ora_bat **sorted, ora_bat **order, const ora_bat *b,
  * forward and gives one past the last row; a nil row's frame is its run of
  * nils; a limit of GDK_lng_max is "unbounded".  Results are absolute row
  * numbers.  Supports lng values with a lng limit. */
-int
-ora_rangebounds(ora_bat *r, const ora_bat *b, const ora_bat *p,
-		const void *bound, int tp2, bool preceding, ora_oid first_half)
-{
-	(void) first_half;
-	if (b->type != ORA_lng || tp2 != ORA_lng) {
-		ora_seterr("42000!range frame bound type not supported.\n");
-		return -1;
-	}
-	int64_t limit = *(const int64_t *) bound;
-	uint64_t cnt = b->count;
-	const int64_t *bp = b->base;
-	const int8_t *np = p ? p->base : NULL;
-	ora_oid *rb = r->base;
-	bool all = limit == INT64_MAX;
-	if (!all && (limit == INT64_MIN || limit < 0)) {
-		ora_seterr("42000!range frame bound must be non negative and non null.\n");
-		return -1;
-	}
-	uint64_t m = 0;
-	for (uint64_t i = 0; i <= cnt; i++) {
-		if (i < cnt && !(np && np[i]))
-			continue;
-		/* partition [m, i) */
-		for (uint64_t k = m; k < i; k++) {
-			int64_t v = bp[k];
-			bool vn = v == INT64_MIN;
-			uint64_t j;
-			if (all) {
-				rb[k] = preceding ? m : i;
-				continue;
-			}
-			if (preceding) {
-				for (j = k;; j--) {
-					bool jn = bp[j] == INT64_MIN;
-					if (vn ? !jn : jn) { j++; break; }
-					if (!vn) {
-						int64_t c;
-						if (__builtin_sub_overflow(v, bp[j], &c) || c == INT64_MIN) {
-							ora_seterr("22003!overflow in calculation.\n");
-							return -1;
-						}
-						if ((c < 0 ? -c : c) > limit) { j++; break; }
-					}
-					if (j == m)
-						break;
-				}
-			} else {
-				for (j = k + 1; j < i; j++) {
-					bool jn = bp[j] == INT64_MIN;
-					if (vn ? !jn : jn)
-						break;
-					if (!vn) {
-						int64_t c;
-						if (__builtin_sub_overflow(v, bp[j], &c) || c == INT64_MIN) {
-							ora_seterr("22003!overflow in calculation.\n");
-							return -1;
-						}
-						if ((c < 0 ? -c : c) > limit)
-							break;
-					}
-				}
-			}
-			rb[k] = j;
-		}
-		m = i;
-	}
-	r->count = cnt;
-	r->nonil = 1;
-	return 0;
-}

@@ -13,14 +13,15 @@ LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 TYPE_void, TYPE_bit, TYPE_bte, TYPE_sht, TYPE_int, TYPE_oid = 0, 2, 3, 4, 5, 6
 TYPE_flt, TYPE_dbl, TYPE_lng, TYPE_hge, TYPE_date, TYPE_str = 8, 9, 10, 11, 12, 16
+TYPE_daytime, TYPE_timestamp = 13, 14
 OID_NIL = 1 << 63
 
 NP = {TYPE_bit: np.int8, TYPE_bte: np.int8, TYPE_sht: np.int16, TYPE_int: np.int32,
       TYPE_date: np.int32, TYPE_oid: np.uint64, TYPE_lng: np.int64, TYPE_flt: np.float32,
-      TYPE_dbl: np.float64, TYPE_str: np.uint8}
+      TYPE_dbl: np.float64, TYPE_str: np.uint8, TYPE_daytime: np.int64, TYPE_timestamp: np.int64}
 CT = {TYPE_bit: C.c_int8, TYPE_bte: C.c_int8, TYPE_sht: C.c_int16, TYPE_int: C.c_int32,
       TYPE_date: C.c_int32, TYPE_oid: C.c_uint64, TYPE_lng: C.c_int64, TYPE_flt: C.c_float,
-      TYPE_dbl: C.c_double}
+      TYPE_dbl: C.c_double, TYPE_daytime: C.c_int64, TYPE_timestamp: C.c_int64}
 NIL = {TYPE_bit: -128, TYPE_bte: -128, TYPE_sht: -(1 << 15), TYPE_int: -(1 << 31),
        TYPE_date: -(1 << 31), TYPE_lng: -(1 << 63), TYPE_hge: -(1 << 127), TYPE_oid: OID_NIL}
 
@@ -89,7 +90,8 @@ def lib():
         L.ora_sort.argtypes = [C.POINTER(P), C.POINTER(P), P, C.c_bool, C.c_bool]
         L.ora_firstn.restype = P
         L.ora_firstn.argtypes = [P, P, P, C.c_uint64, C.c_bool, C.c_bool]
-        L.ora_rangebounds.argtypes = [P, P, P, C.c_void_p, C.c_int, C.c_bool, C.c_uint64]
+        L.ora_windowbounds.argtypes = [P, P, P, P, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_bool,
+                                       C.c_uint64]
         L.ora_analyticalsum.argtypes = [P, P, P, P, P, P, C.c_int, C.c_int, C.c_int]
         L.ora_analyticalavg.argtypes = [P, P, P, P, P, P, C.c_int, C.c_int]
         L.ora_analyticalavginteger.argtypes = [P, P, P, P, P, P, C.c_int, C.c_int]
@@ -309,15 +311,25 @@ def BATfirstn(b, n, s=None, g=None, asc=True, nilslast=False):
     return _ret(lib().ora_firstn(b.ptr, s.ptr if s else None, g.ptr if g else None, n, asc, nilslast))
 
 
-def rangebounds(b, p, limit, preceding):
+def windowbounds(b, p, l, bound, tp1, tp2, unit, preceding, second_half=0):
+    """GDKanalyticalwindowbounds(r, b, p, l, bound, tp1, tp2, unit, preceding,
+    second_half) (gdk/gdk_analytic_bounds.c:1440); `bound` is the static
+    limit as a Python value of type tp2 (None when the per-row BAT l is
+    given).  Returns the bounds BAT (with the nonil / nil properties the
+    reference sets)."""
     n = b.count()
     r = lib().ora_new(TYPE_oid, n, 0)
-    lim = C.c_int64(limit)
-    if lib().ora_rangebounds(r, b.ptr, p.ptr if p else None, C.cast(C.pointer(lim), C.c_void_p),
-                             TYPE_lng, preceding, 0) < 0:
+    keep = []
+    bp = _valptr(tp2, bound, keep) if l is None else None
+    if lib().ora_windowbounds(r, b.ptr, p.ptr if p else None, l.ptr if l else None, bp, tp1, tp2, unit,
+                              preceding, second_half) < 0:
         lib().ora_free(r)
         raise _err()
     return Bat(r)
+
+
+def rangebounds(b, p, limit, preceding):
+    return windowbounds(b, p, None, limit, b.s.type, TYPE_lng, 1, preceding)
 
 
 def analyticalsum(b, p, o, s, e, tp2, frame_type):

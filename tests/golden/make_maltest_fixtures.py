@@ -282,6 +282,120 @@ def analytics03_avg_fixture():
     return {"source": rel, "cases": out}
 
 
+# ---- window frame bounds (GDKanalyticalwindowbounds) ---------------------
+def frame_spec(sql):
+    """(unit, start, end) of an OVER clause's frame text; a bound is
+    [kind, amount, unit_word] with kind PRECEDING / FOLLOWING / CURRENT /
+    UNBOUNDED and amount / unit_word as written (e.g. 100.0, None or 1,
+    'month').  `range unbounded preceding` abbreviates `range between
+    unbounded preceding and current row`."""
+    m = re.search(r"\b(rows|range|groups)\s+(between\s+(.*?)\s+and\s+(.*?)|unbounded preceding)\s*\)",
+                  sql, re.I | re.S)
+    unit = {"rows": 0, "range": 1, "groups": 2}[m.group(1).lower()]
+
+    def bound(t):
+        t = t.strip().lower()
+        if t == "current row":
+            return ["CURRENT", None, None]
+        if t.startswith("unbounded"):
+            return ["UNBOUNDED", None, None]
+        mm = re.match(r"interval\s+'(-?\d+)'\s+(\w+)\s+(preceding|following)", t)
+        if mm:
+            return [mm.group(3).upper(), int(mm.group(1)), mm.group(2)]
+        mm = re.match(r"(-?[\d.]+)\s+(preceding|following)", t)
+        return [mm.group(2).upper(), mm.group(1), None]
+    if m.group(3) is None:
+        return unit, ["UNBOUNDED", None, None], ["CURRENT", None, None]
+    return unit, bound(m.group(3)), bound(m.group(4))
+
+
+def window_functions_fixture():
+    """sql/test/Tests/window_functions.test: SUM(salary) over ROWS / GROUPS /
+    RANGE frames of the employee table (salary DECIMAL(7,2) = int at scale
+    2, PARTITION BY dep_name ORDER BY salary); expected sums per row in the
+    printed (partition, order) order."""
+    rel = "sql/test/Tests/window_functions.test"
+    text = open(os.path.join(REF, rel)).read()
+    emp = []
+    for m in re.finditer(r"INSERT INTO employee VALUES \(\s*(\d+),\s*'(\w+)',\s*'(\w+)',\s*(\d+),\s*(\d+)\)", text):
+        emp.append([int(m.group(1)), m.group(3), int(m.group(4)) * 100])
+    cases = []
+    for kind, body, exp in parse_blocks(text):
+        stmt = " ".join(body)
+        if not kind.startswith("query") or "SUM(salary)" not in stmt or "PARTITION BY dep_name ORDER BY salary" \
+                not in stmt:
+            continue
+        overs = re.findall(r"OVER\s*\((.*?\))\s*as", stmt, re.I)
+        width = 3 + len(overs)
+        nrow = len(exp) // width
+        if nrow * width != len(exp) or nrow != len(emp):
+            continue
+        for ci, over in enumerate(overs):
+            unit, st, en = frame_spec(over)
+            cases.append(dict(unit=unit, start=st, end=en,
+                              ids=[int(float(exp[i * width])) for i in range(nrow)],
+                              expected=[int(round(float(exp[i * width + 3 + ci]) * 100)) for i in range(nrow)]))
+    return {"source": rel, "employee": emp, "scale": 2, "cases": cases}
+
+
+def analytics07_fixture():
+    """sql/test/analytics/Tests/analytics07.test: count(*) over RANGE frames
+    with month / second intervals on date, timestamp and time columns, asc
+    and desc; count = frame end - frame start.  Values are kept as their
+    calendar / clock components; expected counts in printed order."""
+    rel = "sql/test/analytics/Tests/analytics07.test"
+    text = open(os.path.join(REF, rel)).read()
+    tables = {}
+    for m in re.finditer(r"insert into (testintervals\d?) values (.*?)\n\n", text, re.S):
+        vals = []
+        for t in re.findall(r"\((\w+) '([^']*)', (-?\d+)\)", m.group(2)):
+            vals.append([t[0], t[1]])
+        tables[m.group(1)] = vals
+    cases, errors = [], []
+    blocks = list(parse_blocks(text))
+    for kind, body, exp in blocks:
+        stmt = " ".join(body)
+        mt = re.search(r"from (testintervals\d?)\s*$", stmt)
+        if not mt or "count(*) over" not in stmt:
+            continue
+        overs = re.findall(r"over \((.*?\))", stmt)
+        if kind.startswith("statement error"):
+            for over in overs:
+                unit, st, en = frame_spec(over)
+                errors.append(dict(table=mt.group(1), desc=" desc " in over, unit=unit, start=st, end=en))
+            continue
+        width = len(overs)
+        nrow = len(exp) // width
+        for ci, over in enumerate(overs):
+            unit, st, en = frame_spec(over)
+            cases.append(dict(table=mt.group(1), desc=" desc " in over, unit=unit, start=st, end=en,
+                              expected=[int(exp[i * width + ci]) for i in range(nrow)]))
+    return {"source": rel, "tables": tables, "cases": cases, "errors": errors}
+
+
+# ---- batcalc (tst901 / tst906 / tst908) -------------------------------------
+def batcalc_fixture():
+    """monetdb5/mal/Tests/tst901.maltest, tst906.maltest: io.print of the BATs
+    of a batcalc +, +cst, (/cst,) *, ==, not sequence over 0..9, expected
+    as sqllogictest's rowsort md5 of the (oid, value) rows; tst908.maltest:
+    batcalc./(b, 1:lng) printed in full."""
+    out = {}
+    for name in ("tst901", "tst906"):
+        rel = "monetdb5/mal/Tests/%s.maltest" % name
+        text = open(os.path.join(REF, rel)).read()
+        m = re.search(r"bat\.new\(:(\w+)\)", text)
+        ops = re.findall(r"(\w) ?:= ?batcalc\.(\+|\*|/|==|not)\((\w+),\s*([\w:]+)", text)
+        h = re.search(r"(\d+) values hashing to ([0-9a-f]{32})", text)
+        out[name] = {"source": rel, "type": m.group(1), "n": 10,
+                     "ops": [list(o) for o in ops], "nvalues": int(h.group(1)), "md5": h.group(2)}
+    rel = "monetdb5/mal/Tests/tst908.maltest"
+    text = open(os.path.join(REF, rel)).read()
+    exp = [e for k, b, e in parse_blocks(text) if k.startswith("query")][0]
+    out["tst908"] = {"source": rel, "type": "lng", "divisor": 1,
+                     "expected": [[int(exp[i]), int(exp[i + 1])] for i in range(0, len(exp), 2)]}
+    return out
+
+
 def main():
     if not os.path.isdir(REF):
         sys.exit("reference not present; fixtures are already committed")
@@ -294,7 +408,10 @@ def main():
           "window_frames": analytics03_fixture(),
           "window_avg": analytics03_avg_fixture(),
           "sort": [sort_fixture("monetdb5/modules/mal/Tests/%s.maltest" % f)
-                   for f in ("orderidx00", "orderidx04")]}
+                   for f in ("orderidx00", "orderidx04")],
+          "window_bounds_employee": window_functions_fixture(),
+          "window_bounds_intervals": analytics07_fixture(),
+          "batcalc": batcalc_fixture()}
     with open(os.path.join(OUT, "maltest_fixtures.json"), "w") as f:
         json.dump(fx, f, indent=1)
     print("select cases:", len(fx["select"]["cases"]))

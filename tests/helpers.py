@@ -110,3 +110,133 @@ def replay_window_avg(avgf, make_bat, TYPE_int, TYPE_flt, TYPE_bit):
         if list(got) != c["expected"]:
             bad.append((c, list(got)))
     return bad
+
+
+# ---- window frame bounds fixtures (window_functions.test, analytics07.test) --
+INT_MAX, LNG_MAX = (1 << 31) - 1, (1 << 63) - 1
+TYPE_INT, TYPE_LNG, TYPE_BIT, TYPE_OID = 5, 10, 2, 6
+TYPE_DATE, TYPE_DAYTIME, TYPE_TIMESTAMP = 12, 13, 14
+MSEC = {"second": 1000, "minute": 60_000, "hour": 3_600_000, "day": 86_400_000}
+
+
+def mkdate(y, m, d):
+    """gdk_time.c:27 mkdate (packed (year + 4712) * 12 + month - 1, day)."""
+    return (((y + 4712) * 12 + m - 1) << 5) | d
+
+
+def mkdaytime(h, mi, s, us=0):
+    return ((h * 60 + mi) * 60 + s) * 1_000_000 + us
+
+
+def mktimestamp(d, t):
+    return (d << 37) | t
+
+
+def temporal_value(kind, text):
+    """Packed GDK value of a date / timestamp / time literal."""
+    if kind == "date":
+        y, m, d = (int(x) for x in text.split("-"))
+        return TYPE_DATE, mkdate(y, m, d)
+    if kind == "time":
+        h, mi, s = (int(x) for x in text.split(":"))
+        return TYPE_DAYTIME, mkdaytime(h, mi, s)
+    day, clock = text.split()
+    y, m, d = (int(x) for x in day.split("-"))
+    h, mi, s = (int(x) for x in clock.split(":"))
+    return TYPE_TIMESTAMP, mktimestamp(mkdate(y, m, d), mkdaytime(h, mi, s))
+
+
+def bound_args(unit, bnd, is_start, col_tp, scale=0):
+    """GDKanalyticalwindowbounds arguments (preceding, second_half, tp2,
+    limit) of one frame bound as the SQL layer builds them
+    (rel_select.c:4605-4710 generate_window_bound / calculate_window_bound,
+    sql_rank.c:124-130): ROWS / GROUPS limits are lng; RANGE limits have the
+    ORDER BY column's type (numeric) or are month (int) / msec (lng)
+    intervals (temporal); UNBOUNDED is the bound type's max, CURRENT ROW 0."""
+    kind, amount, word = bnd
+    code = {"PRECEDING": 0, "FOLLOWING": 1, "CURRENT": 4, "UNBOUNDED": 0}[kind]
+    if kind == "UNBOUNDED" and not is_start:
+        code = 1
+    if not is_start:
+        code = {0: 2, 1: 3, 4: 5}[code]
+    preceding = code % 2 == 0
+    second_half = 0 if (code < 2 or code == 4) else 1
+    temporal = col_tp in (TYPE_DATE, TYPE_DAYTIME, TYPE_TIMESTAMP)
+    if unit != 1 or temporal:
+        tp2 = TYPE_LNG
+        if kind == "UNBOUNDED":
+            return preceding, second_half, tp2, LNG_MAX
+        if kind == "CURRENT":
+            return preceding, second_half, tp2, 0
+        if word == "month":
+            return preceding, second_half, TYPE_INT, int(amount)
+        if word is not None:
+            return preceding, second_half, tp2, int(amount) * MSEC[word]
+        return preceding, second_half, tp2, int(float(amount))
+    tp2 = col_tp
+    if kind == "UNBOUNDED":
+        return preceding, second_half, tp2, INT_MAX
+    if kind == "CURRENT":
+        return preceding, second_half, tp2, 0
+    return preceding, second_half, tp2, int(round(float(amount) * 10 ** scale))
+
+
+def employee_frames():
+    """window_functions.test employee rows ordered by (dep_name, salary):
+    (ids, salary, partition bits, peer bits, cases)."""
+    fx = FIX["window_bounds_employee"]
+    emp = sorted(fx["employee"], key=lambda r: (r[1], r[2]))
+    ids = [r[0] for r in emp]
+    sal = np.array([r[2] for r in emp], np.int32)
+    dep = [r[1] for r in emp]
+    p = np.array([1] + [int(dep[i] != dep[i - 1]) for i in range(1, len(dep))], np.int8)
+    o = p.copy()
+    o[1:] |= (sal[1:] != sal[:-1]).astype(np.int8)
+    return ids, sal, p, o, fx["cases"]
+
+
+def replay_employee(bounds, make_bat):
+    """bounds(b, p, l=None, bound, tp1, tp2, unit, preceding, second_half) ->
+    numpy oid array.  Returns mismatches of the frame sums."""
+    ids, sal, p, o, cases = employee_frames()
+    B, P, O = make_bat(TYPE_INT, sal), make_bat(TYPE_BIT, p), make_bat(TYPE_BIT, o)
+    bad = []
+    for c in cases:
+        col = O if c["unit"] == 2 else B
+        coltp = TYPE_BIT if c["unit"] == 2 else TYPE_INT
+        res = []
+        for bnd, st in ((c["start"], True), (c["end"], False)):
+            pre, sh, tp2, lim = bound_args(c["unit"], bnd, st, TYPE_INT, scale=2)
+            res.append(np.asarray(bounds(col, P, None, lim, coltp, tp2, c["unit"], pre, sh), np.int64))
+        s, e = res
+        sums = [int(sal[s[i]:e[i]].sum()) for i in range(len(sal))]
+        if ids != c["ids"] or sums != c["expected"]:
+            bad.append((c, sums))
+    return bad
+
+
+def interval_cases(errors=False):
+    """analytics07.test cases: (case, column type, sorted packed values)."""
+    fx = FIX["window_bounds_intervals"]
+    for c in fx["errors" if errors else "cases"]:
+        vals = [temporal_value(k, t) for k, t in fx["tables"][c["table"]]]
+        tp = vals[0][0]
+        v = sorted(x[1] for x in vals)
+        if c["desc"]:
+            v = v[::-1]
+        yield c, tp, np.array(v, np.int32 if tp == TYPE_DATE else np.int64)
+
+
+def replay_intervals(bounds, make_bat):
+    """count(*) over the analytics07 frames = end - start."""
+    bad = []
+    for c, tp, v in interval_cases():
+        B = make_bat(tp, v)
+        res = []
+        for bnd, st in ((c["start"], True), (c["end"], False)):
+            pre, sh, tp2, lim = bound_args(1, bnd, st, tp)
+            res.append(np.asarray(bounds(B, None, None, lim, tp, tp2, 1, pre, sh), np.int64))
+        got = [int(x) for x in res[1] - res[0]]
+        if got != c["expected"]:
+            bad.append((c, got))
+    return bad

@@ -452,3 +452,40 @@ def test_window_avginteger_oracle(ora):
                          fin=lambda acc: NIL if acc[2] == 0 else _round_avg(acc[0], acc[1], acc[2]))
         assert list(got[k:k + sz]) == want
         k += sz
+
+
+# ---- window frame bounds pinned on the reference's SQL fixtures ------------
+def _ora_bounds(ora):
+    def f(b, p, l, lim, tp1, tp2, unit, pre, sh):
+        return ora.windowbounds(b, p, l, lim, tp1, tp2, unit, pre, sh).values()
+    return f
+
+
+def _ora_make(ora):
+    return lambda tp, a: ora.Bat.from_array(tp, a)
+
+
+def test_windowbounds_employee_fixture(ora):
+    """window_functions.test: SUM(salary) over ROWS / GROUPS / RANGE frames."""
+    from helpers import replay_employee
+    assert replay_employee(_ora_bounds(ora), _ora_make(ora)) == []
+
+
+def test_windowbounds_interval_fixture(ora):
+    """analytics07.test: RANGE frames with month / second intervals on
+    date, timestamp and time columns (asc and desc)."""
+    from helpers import replay_intervals
+    assert replay_intervals(_ora_bounds(ora), _ora_make(ora)) == []
+
+
+def test_windowbounds_interval_errors(ora):
+    from helpers import bound_args, interval_cases
+    n = 0
+    for c, tp, v in interval_cases(errors=True):
+        b = ora.Bat.from_array(tp, v)
+        with pytest.raises(ora.OracleError, match="42000!"):
+            for bnd, st in ((c["start"], True), (c["end"], False)):
+                pre, sh, tp2, lim = bound_args(1, bnd, st, tp)
+                ora.windowbounds(b, None, None, lim, tp, tp2, 1, pre, sh)
+        n += 1
+    assert n == 2
