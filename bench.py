@@ -240,7 +240,12 @@ def cpu_baseline(args):
     except Exception as e:  # noqa: BLE001
         return {"value": None, "unit": "Grows/s", "cores": 0, "kind": "port",
                 "sample": "oracle unavailable: %s" % e}
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    # every core this process may run on (the GPU box grants one GPU's
+    # share of the host; OMP_NUM_THREADS states that share there)
+    nproc = os.cpu_count() or 1
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = args.cpu_threads or (min(share, avail) if share > 0 else avail)
     n = int(round(args.cpu_sf * SF1_ROWS))
     cols = ora.tpch_lineitem(20241024, 0, n, max(1, int(args.cpu_sf * 200_000)))
     ora.q6(cols, threads)
@@ -259,6 +264,7 @@ def cpu_baseline(args):
         t1.append(time.perf_counter() - t)
     med1 = statistics.median(t1)
     return {"value": round(n / med / 1e9, 4), "unit": "Grows/s", "cores": threads, "kind": "port",
+            "nproc": nproc, "affinity_cpus": avail, "omp_num_threads": share or None,
             "sample": "TPC-H Q6 op-at-a-time (oracle GDK restatement), %d rows (SF%g), "
                       "%d threads, median of 5" % (n, args.cpu_sf, threads),
             "ms": round(med * 1e3, 2),
