@@ -36,7 +36,7 @@ typedef uint64_t mgdk_BUN;
 enum {
 	MGDK_void = 0, MGDK_msk = 1, MGDK_bit = 2, MGDK_bte = 3, MGDK_sht = 4,
 	MGDK_int = 5, MGDK_oid = 6, MGDK_flt = 8, MGDK_dbl = 9, MGDK_lng = 10,
-	MGDK_hge = 11, MGDK_date = 12, MGDK_str = 16,
+	MGDK_hge = 11, MGDK_date = 12, MGDK_daytime = 13, MGDK_timestamp = 14, MGDK_str = 16,
 };
 
 #define MGDK_OID_NIL ((mgdk_oid) 1 << 63)   /* oid_nil */

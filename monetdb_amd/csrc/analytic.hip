@@ -36,6 +36,7 @@ struct WArgs {
 	bool desc;          // partitions sorted descending (nils last)
 	bool peers;         // limit == 0: no overflow check (GDKanalyticalpeers)
 	bool all;           // unbounded
+	uint64_t tmax;      // max of the value type: |v - b[j]| > tmax overflows (SUB_WITH_CHECK)
 	const oid *Z;       // per partition nil-run boundary (ordered path)
 	oid *out;
 	uint32_t *err;      // bit 0: overflow
@@ -76,12 +77,6 @@ absdiff(int64_t x, int64_t y)
 	return x >= y ? (uint64_t) x - (uint64_t) y : (uint64_t) y - (uint64_t) x;
 }
 
-// true difference x - y overflows lng (SUB_WITH_CHECK, incl. == INT64_MIN)
-__device__ __forceinline__ bool
-sub_ovf(int64_t x, int64_t y)
-{
-	return absdiff(x, y) > (uint64_t) INT64_MAX;
-}
 
 // nil-run boundary of every partition: ascending -> first non-nil row,
 // descending -> first nil row
@@ -145,7 +140,7 @@ sorted_bound(const WArgs &a, const Stage &V, BUN k, BUN m, BUN e, BUN z0, uint32
 				BUN mid = bad + (good - bad) / 2;
 				if (absdiff(v, V(mid)) <= lim) good = mid; else bad = mid;
 			}
-			if (!a.peers && sub_ovf(v, V(bad)))
+			if (!a.peers && absdiff(v, V(bad)) > a.tmax)
 				ovf = 1;
 		}
 		return good;
@@ -161,7 +156,7 @@ sorted_bound(const WArgs &a, const Stage &V, BUN k, BUN m, BUN e, BUN z0, uint32
 		BUN mid = good + (bad - good) / 2;
 		if (absdiff(v, V(mid)) <= lim) good = mid; else bad = mid;
 	}
-	if (bad < vz && !a.peers && sub_ovf(v, V(bad)))
+	if (bad < vz && !a.peers && absdiff(v, V(bad)) > a.tmax)
 		ovf = 1;
 	return good + 1;
 }
@@ -262,6 +257,7 @@ pidx(int i)
 
 struct FArgs {
 	const int64_t *b;
+	uint64_t tmax;       // |v - b[j]| > tmax overflows (narrow value types widened to lng)
 	const int8_t *p;     // partition bits or NULL
 	bool p4;             // p is 4-byte aligned
 	BUN n;
@@ -455,7 +451,7 @@ k_range_fast(FArgs a)
 			const int e = prec ? bnd - 1 : bnd;
 			if (e >= 0 && e < NB && !(hasb && spst[e] != spst[xk])) {
 				const int64_t vb = sv[pidx(e)];
-				if (vb != INT64_MIN && sub_ovf(vk, vb))
+				if (vb != INT64_MIN && absdiff(vk, vb) > a.tmax)
 					ovf = 1;
 			}
 		}
@@ -703,7 +699,7 @@ k_range_keys(FArgs a)
 		}
 	}
 	__syncthreads();
-	uint32_t ord = 0;
+	uint32_t ord = 0, ovf = 0;
 	for (int i = tid; i < NA; i += 256) {
 		const int xk = xa + i;
 		const BUN k = t0 + (BUN) i;
@@ -725,9 +721,27 @@ k_range_keys(FArgs a)
 			const uint32_t at = atomicAdd(&a.flags[2], 1u);
 			if (at < a.unres_cap)
 				a.unres[at] = k;
+		} else if (!ALL && !a.peers && a.tmax < KMAXREL) {
+			// narrow value types: the pair the reference subtracts last (the
+			// first row outside the frame) may exceed the type's range even
+			// though the tile spans < 2^32
+			const int e = PREC ? bnd - 1 : bnd;
+			const uint64_t x = sk[xk];
+			const bool xval = DESC ? ((x >> 32) & 1) == 0 : ((x >> 32) & 1) == 1;
+			if (xval && e >= 0 && e < NB2) {
+				const uint64_t y = sk[e];
+				const bool yval = DESC ? ((y >> 32) & 1) == 0 : ((y >> 32) & 1) == 1;
+				if ((x >> 33) == (y >> 33) && yval) {
+					const uint64_t rx = x & KMAXREL, ry = y & KMAXREL;
+					if ((rx > ry ? rx - ry : ry - rx) > a.tmax)
+						ovf = 1;
+				}
+			}
 		}
 		a.out[k] = lo + (BUN) bnd;
 	}
+	if (ovf)
+		atomicOr(&a.flags[0], 1u);
 	if (!ALL) {
 #pragma unroll
 		for (int o = 32; o > 0; o >>= 1)
@@ -780,7 +794,7 @@ k_range_walk(WArgs a)
 				const bool jn = a.b[j] == INT64_MIN;
 				if (vn ? !jn : jn) { j++; break; }
 				if (!vn) {
-					if (!a.peers && sub_ovf(v, a.b[j])) { ovf = 1; break; }
+					if (!a.peers && absdiff(v, a.b[j]) > a.tmax) { ovf = 1; break; }
 					if (absdiff(v, a.b[j]) > lim) { j++; break; }
 				}
 				if (j == m)
@@ -792,7 +806,7 @@ k_range_walk(WArgs a)
 				if (vn ? !jn : jn)
 					break;
 				if (!vn) {
-					if (!a.peers && sub_ovf(v, a.b[j])) { ovf = 1; break; }
+					if (!a.peers && absdiff(v, a.b[j]) > a.tmax) { ovf = 1; break; }
 					if (absdiff(v, a.b[j]) > lim)
 						break;
 				}
@@ -854,58 +868,18 @@ general_setup(WArgs &a, const mgdk_bat *p, BUN n, mgdk_bat **Sp)
 	return 0;
 }
 
-extern "C" int
-mgdk_GDKanalyticalwindowbounds(mgdk_bat *r, mgdk_bat *b, mgdk_bat *p, mgdk_bat *l, const void *bound,
-			       int tp1, int tp2, int unit, bool preceding, mgdk_oid first_half)
+// RANGE bounds of integer values widened to lng (bte..lng), static limit:
+// the ordered fast path with its fix-ups and the unordered walk.  `limit`
+// is the effective limit min(limit, tmax) (a frame edge further away than
+// the type's max is the overflowing subtraction itself); `all` = unbounded.
+// Sets r's values; the caller sets the count and properties.
+int
+mgdk::range_bounds_int64(mgdk_bat *r, const int64_t *bvals, const mgdk_bat *p, BUN n, int64_t limit,
+			 uint64_t tmax, bool all, bool preceding)
 {
-	(void) first_half;
-	if (r == nullptr || b == nullptr) {
-		seterr("GDKanalyticalwindowbounds: NULL argument");
-		return -1;
-	}
-	if (unit != 1) {
-		seterr("42000!window bounds: unit %d (rows/groups) not supported on the device path", unit);
-		return -1;
-	}
-	if (l != nullptr || bound == nullptr) {
-		seterr("42000!window bounds: per-row (dynamic) bounds not supported on the device path");
-		return -1;
-	}
-	if (basetype(tp1) != MGDK_lng || basetype(b->ttype) != MGDK_lng) {
-		seterr("42000!type %s not supported for %s frame bound type.\n", atomname(tp1), atomname(tp2));
-		return -1;
-	}
-	if (tp2 != MGDK_lng) {
-		seterr("42000!range frame bound type %s not supported.\n", atomname(tp2));
-		return -1;
-	}
-	if (r->ttype != MGDK_oid) {
-		seterr("window bounds: result must be an oid BAT");
-		return -1;
-	}
-	const int64_t limit = *(const int64_t *) bound;
-	const bool all = limit == INT64_MAX;
-	if (!all && (limit == INT64_MIN || limit < 0)) {
-		seterr("42000!range frame bound must be non negative and non null.\n");
-		return -1;
-	}
-	ProfScope prof("windowbounds");
-	const BUN n = b->count;
-	if (p && (p->count != n || width_of(p->ttype) != 1)) {
-		seterr("window bounds: partition column must be a bit BAT aligned with b");
-		return -1;
-	}
-	// r is caller-allocated with room for count(b) oids (sql_rank.c:161
-	// allocates it with COLnew(..., BATcount(b), ...))
-	if (n > 0 && r->theap == nullptr) {
-		seterr("window bounds: result BAT has no heap");
-		return -1;
-	}
 	hipStream_t st = stream();
-	if (n == 0) {
-		r->count = 0;
+	if (n == 0)
 		return 0;
-	}
 	const dim3 blk(256);
 	// 1. fast ordered pass, ascending first (the SQL default), descending if
 	//    only that order holds
@@ -915,13 +889,14 @@ mgdk_GDKanalyticalwindowbounds(mgdk_bat *r, mgdk_bat *b, mgdk_bat *p, mgdk_bat *
 	if (!fl.p || !ul.p || !h)
 		return -1;
 	FArgs f{};
-	f.b = (const int64_t *) b->theap;
+	f.b = bvals;
+	f.tmax = tmax;
 	f.p = p ? (const int8_t *) p->theap : nullptr;
 	f.p4 = ((uintptr_t) f.p & 3) == 0;
 	f.n = n;
 	f.limit = limit;
 	f.preceding = preceding;
-	f.peers = limit == 0;
+	f.peers = false;
 	f.all = all;
 	f.out = (oid *) r->theap;
 	f.flags = fl.as<uint32_t>();
@@ -967,11 +942,12 @@ mgdk_GDKanalyticalwindowbounds(mgdk_bat *r, mgdk_bat *b, mgdk_bat *p, mgdk_bat *
 	if (!ordered || nunres > 0) {
 		// 2. general machinery: partition starts S, nil boundaries Z
 		WArgs a{};
-		a.b = (const int64_t *) b->theap;
+		a.b = bvals;
+		a.tmax = tmax;
 		a.n = n;
 		a.limit = limit;
 		a.preceding = preceding;
-		a.peers = limit == 0;
+		a.peers = false;
 		a.all = all;
 		a.desc = f.desc;
 		a.out = (oid *) r->theap;
@@ -1006,9 +982,5 @@ mgdk_GDKanalyticalwindowbounds(mgdk_bat *r, mgdk_bat *b, mgdk_bat *p, mgdk_bat *
 		seterr("22003!overflow in calculation.\n");
 		return -1;
 	}
-	r->count = n;
-	r->tnonil = 1;
-	r->tnil = 0;
-	r->tsorted = r->trevsorted = r->tkey = n <= 1;
 	return 0;
 }

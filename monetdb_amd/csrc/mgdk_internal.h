@@ -104,6 +104,12 @@ int radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32_
 int radix_sort_positions32(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, uint32_t *vals_alt, BUN n,
 			   int bits, uint32_t **perm);
 
+// RANGE bounds over lng images of bte..lng values with a static limit
+// (analytic.hip): ordered fast path + fix-ups + unordered walk; `limit` is
+// min(limit, tmax), overflow when |v - b[j]| of the stopping pair > tmax
+int range_bounds_int64(mgdk_bat *r, const int64_t *bvals, const mgdk_bat *p, BUN n, int64_t limit,
+		       uint64_t tmax, bool all, bool preceding);
+
 // RAII device temporary (not the per-thread scratch)
 struct DevBuf {
 	void *p = nullptr;

@@ -237,7 +237,7 @@ width_of(int tt)
 	case MGDK_bit: case MGDK_bte: return 1;
 	case MGDK_sht: return 2;
 	case MGDK_int: case MGDK_date: case MGDK_flt: return 4;
-	case MGDK_oid: case MGDK_lng: case MGDK_dbl: return 8;
+	case MGDK_oid: case MGDK_lng: case MGDK_dbl: case MGDK_daytime: case MGDK_timestamp: return 8;
 	case MGDK_hge: return 16;
 	case MGDK_str: return 1;
 	default: return -1;
@@ -247,7 +247,8 @@ width_of(int tt)
 int
 basetype(int tt)
 {
-	return tt == MGDK_date ? MGDK_int : tt == MGDK_bit ? MGDK_bte : tt;
+	return tt == MGDK_date ? MGDK_int : tt == MGDK_bit ? MGDK_bte :
+	       tt == MGDK_daytime || tt == MGDK_timestamp ? MGDK_lng : tt;
 }
 
 const char *
@@ -265,6 +266,8 @@ atomname(int tt)
 	case MGDK_lng: return "lng";
 	case MGDK_hge: return "hge";
 	case MGDK_date: return "date";
+	case MGDK_daytime: return "daytime";
+	case MGDK_timestamp: return "timestamp";
 	case MGDK_str: return "str";
 	}
 	return "any";

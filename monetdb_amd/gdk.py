@@ -16,19 +16,22 @@ LIB_PATH = os.environ.get("MGDK_LIB") or os.path.join(HERE, "libmgdk.so")
 
 TYPE_void, TYPE_msk, TYPE_bit, TYPE_bte, TYPE_sht, TYPE_int, TYPE_oid = 0, 1, 2, 3, 4, 5, 6
 TYPE_flt, TYPE_dbl, TYPE_lng, TYPE_hge, TYPE_date, TYPE_str = 8, 9, 10, 11, 12, 16
+TYPE_daytime, TYPE_timestamp = 13, 14
 OID_NIL = 1 << 63
 
 NP = {TYPE_bit: np.int8, TYPE_bte: np.int8, TYPE_sht: np.int16, TYPE_int: np.int32,
       TYPE_date: np.int32, TYPE_oid: np.uint64, TYPE_lng: np.int64, TYPE_flt: np.float32,
-      TYPE_dbl: np.float64, TYPE_str: np.uint8}
+      TYPE_dbl: np.float64, TYPE_str: np.uint8, TYPE_daytime: np.int64, TYPE_timestamp: np.int64}
 CT = {TYPE_bit: C.c_int8, TYPE_bte: C.c_int8, TYPE_sht: C.c_int16, TYPE_int: C.c_int32,
       TYPE_date: C.c_int32, TYPE_oid: C.c_uint64, TYPE_void: C.c_uint64, TYPE_lng: C.c_int64,
-      TYPE_flt: C.c_float, TYPE_dbl: C.c_double}
+      TYPE_flt: C.c_float, TYPE_dbl: C.c_double, TYPE_daytime: C.c_int64, TYPE_timestamp: C.c_int64}
 NIL = {TYPE_bit: -128, TYPE_bte: -128, TYPE_sht: -(1 << 15), TYPE_int: -(1 << 31),
        TYPE_date: -(1 << 31), TYPE_lng: -(1 << 63), TYPE_hge: -(1 << 127), TYPE_oid: OID_NIL,
-       TYPE_void: OID_NIL, TYPE_flt: float("nan"), TYPE_dbl: float("nan")}
+       TYPE_void: OID_NIL, TYPE_flt: float("nan"), TYPE_dbl: float("nan"), TYPE_daytime: -(1 << 63),
+       TYPE_timestamp: -(1 << 63)}
 WIDTH = {TYPE_void: 0, TYPE_bit: 1, TYPE_bte: 1, TYPE_sht: 2, TYPE_int: 4, TYPE_date: 4,
-         TYPE_flt: 4, TYPE_oid: 8, TYPE_lng: 8, TYPE_dbl: 8, TYPE_hge: 16, TYPE_str: 1}
+         TYPE_flt: 4, TYPE_oid: 8, TYPE_lng: 8, TYPE_dbl: 8, TYPE_hge: 16, TYPE_str: 1, TYPE_daytime: 8,
+         TYPE_timestamp: 8}
 
 
 class MgdkBat(C.Structure):
@@ -547,13 +550,17 @@ def FORdecompress(o, minval, tp):
     return BAT(lib().mgdk_FORdecompress(o.ptr, minval, tp))
 
 
-def GDKanalyticalwindowbounds(b, p, limit, preceding, tp1=TYPE_lng, tp2=TYPE_lng, unit=1):
+def GDKanalyticalwindowbounds(b, p, limit, preceding, tp1=None, tp2=TYPE_lng, unit=1, l=None, second_half=0):
+    """GDKanalyticalwindowbounds(r, b, p, l, bound, tp1, tp2, unit,
+    preceding, second_half) (gdk/gdk_analytic_bounds.c:1440) into a new
+    oid BAT r; `limit` is the static bound (a value of type tp2) unless the
+    per-row limit BAT l is given."""
     n = b.count()
     r = BAT(lib().mgdk_COLnew(0, TYPE_oid, n))
-    lim = C.c_int64(limit)
-    _chk(lib().mgdk_GDKanalyticalwindowbounds(r.ptr, b.ptr, _p(p), None,
-                                              C.cast(C.pointer(lim), C.c_void_p), tp1, tp2,
-                                              unit, preceding, 0))
+    keep = []
+    bp = _valptr(tp2, limit, keep) if l is None else None
+    _chk(lib().mgdk_GDKanalyticalwindowbounds(r.ptr, b.ptr, _p(p), _p(l), bp, b.ttype if tp1 is None else tp1,
+                                              tp2, unit, preceding, second_half))
     return r
 
 
