@@ -866,14 +866,16 @@ mgdk_GDKanalyticalwindowbounds(mgdk_bat *r, mgdk_bat *b, mgdk_bat *p, mgdk_bat *
 		if (special) {
 			rc = run_list_bounds(H, preceding, out);
 		} else if (n) {
+			// the peer-start list first: make_list / compact_flags use the
+			// thread's meta buffer that holds the error rows below
+			HostList G;
+			if (groups && make_list(G, (const int8_t *) b->theap, n, false) < 0)
+				return -1;
 			unsigned long long *err = (unsigned long long *) meta_buf();
 			unsigned long long *h = (unsigned long long *) pinned(64);
 			if (!err || !h || !hip_ok(hipMemsetAsync(err, 0xff, 16, stream()), "memset"))
 				return -1;
 			if (groups) {
-				HostList G;
-				if (make_list(G, (const int8_t *) b->theap, n, false) < 0)
-					return -1;
 				hipLaunchKernelGGL(k_rb_groups, dim3(grid_for(n, 256, 65536)), dim3(256), 0, stream(), H.P, G.P,
 						   L, preceding, out, err);
 				if (!hip_ok(hipMemcpyAsync(h, err, 16, hipMemcpyDeviceToHost, stream()), "memcpy") || !sync())
