@@ -40,6 +40,7 @@ enum {
 };
 
 #define MGDK_OID_NIL ((mgdk_oid) 1 << 63)   /* oid_nil */
+#define MGDK_BUN_NONE ((mgdk_BUN) INT64_MAX)  /* BUN_NONE, gdk/gdk.h:518 */
 
 /* BAT descriptor: the column-side fields of gdk/gdk.h:712-804 (COLrec, BAT)
  * that the operators read or set.  theap/tvheap are HBM pointers. */
@@ -55,6 +56,15 @@ typedef struct mgdk_bat {
 	uint8_t tsorted, trevsorted, tkey, tnonil, tnil;
 	uint8_t _pad[3];
 	void *priv;             /* runtime-owned */
+	/* knowledge kept with the column (gdk/gdk.h:721-726): positions proving
+	 * the column is not sorted / not reverse sorted (0: unknown), the
+	 * positions of its minimum / maximum (MGDK_BUN_NONE: unknown) and the
+	 * estimated number of distinct values (0: unknown).  Operators set them
+	 * on their results as the reference does and read them from inputs
+	 * (BATgroup's maximum group id, BATjoin's cost model). */
+	mgdk_BUN tnosorted, tnorevsorted;
+	mgdk_BUN tminpos, tmaxpos;
+	double tunique_est;
 } mgdk_bat;
 
 /* ---- runtime ---------------------------------------------------------- */

@@ -48,6 +48,7 @@ struct Side {
 	const oid *oids;   // materialized candidates
 	oid hseq;
 	oid cseq;          // dense: oid of candidate 0
+	oid tseq;          // void side (base == nullptr): value of position 0
 };
 
 __device__ __forceinline__ uint64_t
@@ -59,6 +60,10 @@ key_of(const Side &s, BUN i, bool &isnil)
 	case 2: { int16_t v = ((const int16_t *) s.base)[p]; isnil = v == INT16_MIN; return (uint64_t) (int64_t) v; }
 	case 4: { int32_t v = ((const int32_t *) s.base)[p]; isnil = v == INT32_MIN; return (uint64_t) (int64_t) v; }
 	default: {
+		if (s.base == nullptr) {        // void: dense oids (nil tseqbase: all nil)
+			isnil = s.tseq == MGDK_OID_NIL;
+			return isnil ? s.tseq : s.tseq + p;
+		}
 		uint64_t v = ((const uint64_t *) s.base)[p];
 		isnil = s.uns ? v == ((uint64_t) 1 << 63) : (int64_t) v == INT64_MIN;
 		return v;
@@ -449,19 +454,13 @@ k_probe(Side l, BUN n, uint64_t mask, const uint64_t *boff, const uint64_t *skey
 	}
 }
 
-bool
-join_type_ok(int t)
-{
-	t = basetype(t);
-	return t == MGDK_bte || t == MGDK_sht || t == MGDK_int || t == MGDK_lng || t == MGDK_oid;
-}
-
 void
 side_init(Side &s, const mgdk_bat *b, const Cand &c)
 {
-	s.base = b->theap;
-	s.w = b->twidth;
-	s.uns = basetype(b->ttype) == MGDK_oid;
+	s.base = b->ttype == MGDK_void ? nullptr : b->theap;
+	s.w = b->ttype == MGDK_void ? 8 : b->twidth;
+	s.uns = basetype(b->ttype) == MGDK_oid || b->ttype == MGDK_void;
+	s.tseq = b->tseqbase;
 	s.dense = c.dense;
 	s.off = c.dense ? c.seq - b->hseqbase : 0;
 	s.oids = c.oids;
@@ -1237,27 +1236,16 @@ join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_b
 
 }  // namespace
 
-extern "C" int
-mgdk_BATjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr,
-	     bool nil_matches, mgdk_BUN estimate)
+namespace mgdk {
+
+// hashjoin (gdk/gdk_join.c:2900-3335) over candidate lists already
+// initialised: per l candidate in order, the matches in r in DESCENDING
+// position.  The caller (joinalgo.hip) chose this algorithm and sets the
+// result properties.  *uniq_build: the r side had no duplicate key.
+int
+hash_join(const mgdk_bat *l, const mgdk_bat *r, const Cand &lc, const Cand &rc, bool nil_matches,
+	  mgdk_bat **ap, mgdk_bat **bp)
 {
-	(void) estimate;
-	if (l == nullptr || r == nullptr || r1p == nullptr) {
-		seterr("BATjoin: NULL argument");
-		return -1;
-	}
-	if (basetype(l->ttype) != basetype(r->ttype)) {
-		seterr("42000!BATjoin: type mismatch (%s, %s)", atomname(l->ttype), atomname(r->ttype));
-		return -1;
-	}
-	if (!join_type_ok(l->ttype)) {
-		seterr("42000!BATjoin: type %s not supported on the device path", atomname(l->ttype));
-		return -1;
-	}
-	ProfScope prof("join");
-	Cand lc, rc;
-	if (cand_init(&lc, l, sl) < 0 || cand_init(&rc, r, sr) < 0)
-		return -1;
 	const BUN nl = lc.n, nr = rc.n;
 	if (nr >= ((BUN) 1 << 32) - 1 || nl >= ((BUN) 1 << 32)) {
 		seterr("42000!BATjoin: more than 2^32 rows per side");
@@ -1266,35 +1254,14 @@ mgdk_BATjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk_bat 
 	Side L{}, R{};
 	side_init(L, l, lc);
 	side_init(R, r, rc);
-	mgdk_bat *a = nullptr, *b = nullptr;
-	int rc_ = 0;
-	if (nl == 0 || nr == 0) {
-		a = newbat(0, MGDK_oid, 0);
-		b = newbat(0, MGDK_oid, 0);
-		if (!a || !b) {
-			unfix2(a, b);
-			return -1;
-		}
-	} else {
-		rc_ = l->twidth == 4 ? join_part(L, nl, R, nr, nil_matches, &a, &b) : 1;
-		if (rc_ > 0)
-			rc_ = l->twidth == 8 ? join_lp<8>(L, nl, R, nr, nil_matches, &a, &b)
-					     : join_lp<4>(L, nl, R, nr, nil_matches, &a, &b);
-		if (rc_ > 0)
-			rc_ = join_csr(L, nl, R, nr, nil_matches, &a, &b);
-		if (rc_ < 0)
-			return -1;
-	}
-	const uint64_t nout = a->count;
-	a->tsorted = 1;                 // left candidates in order
-	a->trevsorted = nout <= 1;
-	a->tkey = nout <= 1;
-	a->tnonil = b->tnonil = 1;
-	b->tsorted = b->trevsorted = b->tkey = nout <= 1;
-	*r1p = a;
-	if (r2p)
-		*r2p = b;
-	else
-		mgdk_BBPunfix(b);
-	return 0;
+	const int w = L.w;
+	int rc_ = w == 4 ? join_part(L, nl, R, nr, nil_matches, ap, bp) : 1;
+	if (rc_ > 0)
+		rc_ = w == 8 ? join_lp<8>(L, nl, R, nr, nil_matches, ap, bp)
+			     : join_lp<4>(L, nl, R, nr, nil_matches, ap, bp);
+	if (rc_ > 0)
+		rc_ = join_csr(L, nl, R, nr, nil_matches, ap, bp);
+	return rc_ < 0 ? -1 : 0;
 }
+
+}  // namespace mgdk

@@ -315,6 +315,7 @@ newbat(oid hseq, int tt, BUN cap)
 	b->tseqbase = tt == MGDK_void ? 0 : MGDK_OID_NIL;
 	b->tsorted = b->trevsorted = b->tkey = 1;
 	b->tnonil = 1;
+	b->tminpos = b->tmaxpos = MGDK_BUN_NONE;
 	if (w > 0) {
 		p->theap = heap_new((cap ? cap : 1) * (size_t) w);
 		if (p->theap == nullptr) {
@@ -695,6 +696,10 @@ mgdk_BATslice(mgdk_bat *b, mgdk_BUN lo, mgdk_BUN hi)
 		p->tvheap = bp->tvheap;
 		__atomic_add_fetch(&p->tvheap->refs, 1, __ATOMIC_ACQ_REL);
 	}
+	// what is known of the parent's order holds for a slice, positions do not
+	v->tnosorted = v->tnorevsorted = 0;
+	v->tminpos = v->tmaxpos = MGDK_BUN_NONE;
+	v->tunique_est = 0;
 	if (v->count <= 1)
 		v->tsorted = v->trevsorted = v->tkey = 1;
 	return v;

@@ -40,7 +40,8 @@ class MgdkBat(C.Structure):
                 ("tvheap", C.c_void_p), ("tvheapsize", C.c_uint64),
                 ("tsorted", C.c_uint8), ("trevsorted", C.c_uint8), ("tkey", C.c_uint8),
                 ("tnonil", C.c_uint8), ("tnil", C.c_uint8), ("_pad", C.c_uint8 * 3),
-                ("priv", C.c_void_p)]
+                ("priv", C.c_void_p), ("tnosorted", C.c_uint64), ("tnorevsorted", C.c_uint64),
+                ("tminpos", C.c_uint64), ("tmaxpos", C.c_uint64), ("tunique_est", C.c_double)]
 
 
 class Q1Row(C.Structure):

@@ -240,7 +240,7 @@ cmp_val(int t, const void *a, const void *b)
 	case ORA_int: case ORA_date: CMP3(int32_t);
 	case ORA_lng: CMP3(int64_t);
 	case ORA_hge: CMP3(ora_hge);
-	case ORA_oid: CMP3(ora_oid);
+	case ORA_oid: CMP3(int64_t);   /* oid compares as its storage type lng */
 	case ORA_flt: {
 		float x = *(const float *) a, y = *(const float *) b;
 		if (isnan(x)) return isnan(y) ? 0 : -1;

@@ -18,7 +18,8 @@
  *               :1801 (BATgroupavg), :1996 (BATgroupavg3), :2634 (combine), :3069 (BATgroupcount), AVERAGE_ITER
  *               gdk/gdk_calc_private.h:231-275
  *   group       gdk/gdk_group.c:657-1347 (first-occurrence numbering)
- *   join        gdk/gdk_join.c:2781-2900 (hash join result order)
+ *   join        gdk/gdk_join.c:4451-4623 (BATjoin: algorithm choice, result
+ *               order and properties; gdk_oracle_join.c)
  *   sort        gdk/gdk_batop.c:2266-2342, gdk/gdk_rsort.c:21 (stable)
  *   window      gdk/gdk_analytic_bounds.c:187-587, :855-1440 (gdk_oracle_bounds.c)
  *   frames      gdk/gdk_analytic_func.c:1626 (count), :1959 (sum),
@@ -63,6 +64,7 @@ typedef struct ora_bat {
 	uint64_t vheapsize;
 	uint8_t sorted, revsorted, key, nonil, nil, owned;
 	uint8_t _pad[2];
+	double unique_est;   /* tunique_est (gdk/gdk.h:740): 0 = unknown */
 } ora_bat;
 
 /* memory */
@@ -97,8 +99,11 @@ int ora_groupavg(ora_bat **bnp, ora_bat **cntp, const ora_bat *b, const ora_bat 
 		 const ora_bat *e, const ora_bat *s, bool skip_nils, int scale);
 ora_bat *ora_groupminmax(const ora_bat *b, const ora_bat *g, const ora_bat *e,
 			 const ora_bat *s, bool skip_nils, bool domax);
-int ora_join(ora_bat **r1p, ora_bat **r2p, const ora_bat *l, const ora_bat *r,
+/* BATjoin with its algorithm choice (gdk_oracle_join.c); l and r receive
+ * the ordering / key flags the reference caches on them */
+int ora_join(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r,
 	     const ora_bat *sl, const ora_bat *sr, bool nil_matches);
+int ora_join_algo(ora_bat *l, ora_bat *r, const ora_bat *sl, const ora_bat *sr);
 int ora_sort(ora_bat **sorted, ora_bat **order, const ora_bat *b,
 	     bool reverse, bool nilslast);
 /* GDKanalyticalwindowbounds, all units / types (gdk_oracle_bounds.c);

@@ -770,73 +770,6 @@ ora_groupminmax(const ora_bat *b, const ora_bat *g, const ora_bat *e,
 }
 
 /* ---------------------------------------------------------------------- */
-/* hash join (gdk/gdk_join.c:2900 hashjoin, HASHJOIN :2781-2895): the hash
- * is built on the right input by prepending to bucket chains
- * (gdk/gdk_hash.c:658-704), so for every left candidate in order its
- * matches come out in DESCENDING right position.  nil never matches unless
- * nil_matches. */
-int
-ora_join(ora_bat **r1p, ora_bat **r2p, const ora_bat *l, const ora_bat *r,
-	 const ora_bat *sl, const ora_bat *sr, bool nil_matches)
-{
-	ora_ci lci, rci;
-	if (ora_ci_init(&lci, l, sl) < 0 || ora_ci_init(&rci, r, sr) < 0)
-		return -1;
-	uint64_t cap = 16;
-	while (cap < 2 * rci.n)
-		cap <<= 1;
-	int64_t *head = malloc(cap * sizeof(int64_t));
-	int64_t *next = malloc((rci.n + 1) * sizeof(int64_t));
-	ora_hge *keys = malloc((rci.n + 1) * sizeof(ora_hge));
-	uint8_t *knil = malloc(rci.n + 1);
-	if (!head || !next || !keys || !knil) {
-		free(head); free(next); free(keys); free(knil);
-		ora_seterr("out of memory");
-		return -1;
-	}
-	memset(head, 0xff, cap * sizeof(int64_t));
-	for (uint64_t j = 0; j < rci.n; j++) {
-		knil[j] = val_at(r, ci_get(&rci, j) - r->hseqbase, &keys[j]);
-		uint64_t h = ghash(keys[j], 0) & (cap - 1);
-		next[j] = head[h];
-		head[h] = (int64_t) j;
-	}
-	uint64_t ocap = lci.n + 16, cnt = 0;
-	ora_oid *o1 = malloc(ocap * 8), *o2 = malloc(ocap * 8);
-	for (uint64_t i = 0; i < lci.n; i++) {
-		ora_oid lo = ci_get(&lci, i);
-		ora_hge v;
-		bool vn = val_at(l, lo - l->hseqbase, &v);
-		if (vn && !nil_matches)
-			continue;
-		uint64_t h = ghash(v, 0) & (cap - 1);
-		for (int64_t j = head[h]; j >= 0; j = next[j]) {
-			if (keys[j] != v || knil[j] != vn)
-				continue;
-			if (cnt == ocap) {
-				ocap *= 2;
-				o1 = realloc(o1, ocap * 8);
-				o2 = realloc(o2, ocap * 8);
-			}
-			o1[cnt] = lo;
-			o2[cnt] = ci_get(&rci, (uint64_t) j);
-			cnt++;
-		}
-	}
-	free(head); free(next); free(keys); free(knil);
-	ora_bat *a = ora_new(ORA_oid, cnt, 0), *b = ora_new(ORA_oid, cnt, 0);
-	memcpy(a->base, o1, cnt * 8);
-	memcpy(b->base, o2, cnt * 8);
-	free(o1);
-	free(o2);
-	a->nonil = b->nonil = 1;
-	*r1p = a;
-	if (r2p)
-		*r2p = b;
-	else
-		ora_free(b);
-	return 0;
-}
 
 /* ---------------------------------------------------------------------- */
 /* BATsort (gdk/gdk_batop.c:2342, do_sort :2266-2304): integer keys with

@@ -1,0 +1,789 @@
+/*
+ * gdk_oracle_join.c -- CPU restatement of GDK's BATjoin, including its
+ * algorithm choice, result order and result properties.  TEST
+ * INFRASTRUCTURE ONLY (see gdk_oracle.h).
+ *
+ * BATjoin (gdk/gdk_join.c:4451-4623) picks one of five algorithms and the
+ * choice decides the ORDER of the (r1, r2) pairs:
+ *   selectjoin     one side is a single value (gdk_join.c:363-563):
+ *                  per driving candidate in order, the other side's matches
+ *                  ascending (a point BATselect);
+ *   mergejoin_void the other side is dense (gdk_join.c:571-1020): a range
+ *                  BATselect on the driving side, matches computed;
+ *   mergejoin      both sides sorted, or one sorted and binary search is
+ *                  cheaper than a hash (gdk_join.c:1023-1335, 1941-2780): per
+ *                  driving candidate in order, matches ascending;
+ *   hashjoin       otherwise (gdk_join.c:2900-3335): per driving candidate in
+ *                  order, matches in DESCENDING position (the hash chains are
+ *                  built by prepending, gdk/gdk_hash.c:658-704);
+ * and "swapped" variants drive from the right side (r2 then ascends).  The
+ * hash side is chosen by joincost (gdk_join.c:3586-3689) from the unique
+ * value estimates of guess_uniques (:3519-3576).
+ *
+ * The estimate samples 1000 rows with BATsample (gdk/gdk_sample.c:199),
+ * which is seeded from the clock; a BAT of <= 1000 rows is sampled whole, so
+ * the estimate -- and the algorithm choice -- is deterministic there.  For
+ * larger BATs this restatement (and the device) samples the rows at
+ * floor(i * n / 1000), i < 1000: the only place where the choice can differ
+ * from a given reference run, and only when the two costs are close.
+ * No BAT carries a prebuilt hash here (joincost's rhash / phash are false)
+ * and every BAT is transient (the hash-build cost is counted).
+ *
+ * BATordered / BATordered_rev (gdk/gdk_batop.c:2002-2262) are evaluated
+ * lazily in the reference's order and cache what they find in the input
+ * descriptors (tsorted, trevsorted, tkey), as the reference does: the cached
+ * flags feed later decisions and result properties.
+ */
+#include "gdk_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+void ora_seterr(const char *fmt, ...);
+ora_bat *ora_dense(ora_oid hseq, ora_oid tseq, uint64_t cnt);
+
+typedef struct {
+	bool dense;
+	ora_oid seq;
+	const ora_oid *oids;
+	uint64_t n;
+} ora_ci;
+int ora_ci_init(ora_ci *ci, const ora_bat *b, const ora_bat *s);
+
+static inline ora_oid
+ci_get(const ora_ci *ci, uint64_t i)
+{
+	return ci->dense ? ci->seq + i : ci->oids[i];
+}
+
+/* ---- values ---------------------------------------------------------- */
+
+/* value of position p sign-extended to 64 bits: every join type compares
+ * as a signed integer with its nil (the type minimum) smallest; oid
+ * compares like lng (its storage type, gdk/gdk_atoms.c:1720-1737) */
+static int64_t
+jv(const ora_bat *b, uint64_t p)
+{
+	switch (b->type) {
+	case ORA_void:
+		return b->tseqbase == ORA_OID_NIL ? INT64_MIN : (int64_t) (b->tseqbase + p);
+	case ORA_bte: case ORA_bit: return ((const int8_t *) b->base)[p];
+	case ORA_sht: return ((const int16_t *) b->base)[p];
+	case ORA_int: case ORA_date: return ((const int32_t *) b->base)[p];
+	default: return ((const int64_t *) b->base)[p];
+	}
+}
+
+static int64_t
+jnilv(int type)
+{
+	switch (type) {
+	case ORA_bte: case ORA_bit: return INT8_MIN;
+	case ORA_sht: return INT16_MIN;
+	case ORA_int: case ORA_date: return INT32_MIN;
+	default: return INT64_MIN;
+	}
+}
+
+static bool
+join_type_ok(int t)
+{
+	switch (t) {
+	case ORA_void: case ORA_bte: case ORA_sht: case ORA_int: case ORA_date:
+	case ORA_lng: case ORA_oid: case ORA_daytime: case ORA_timestamp:
+		return true;
+	}
+	return false;
+}
+
+/* ATOMtype: void joins as oid */
+static int
+atomtype(int t)
+{
+	return t == ORA_void ? ORA_oid : t;
+}
+
+/* BATtdense (gdk/gdk.h): a void or oid BAT with a tseqbase */
+static bool
+tdense(const ora_bat *b)
+{
+	return (b->type == ORA_void || b->type == ORA_oid) && b->tseqbase != ORA_OID_NIL;
+}
+
+/* ---- BATordered / BATordered_rev (gdk/gdk_batop.c:2002-2262) ------------- */
+
+static bool
+ordered(ora_bat *b)
+{
+	if (b->type == ORA_void || b->sorted || b->count == 0)
+		return true;
+	bool asc = false, eq = false;
+	for (uint64_t p = 1; p < b->count; p++) {
+		int64_t x = jv(b, p - 1), y = jv(b, p);
+		if (x > y)
+			return false;
+		if (x < y)
+			asc = true;
+		else
+			eq = true;
+	}
+	b->sorted = 1;
+	if (!asc)
+		b->revsorted = 1;
+	if (!eq)
+		b->key = 1;
+	return true;
+}
+
+static bool
+ordered_rev(ora_bat *b)
+{
+	if (b->count <= 1 || b->revsorted)
+		return true;
+	if (b->type == ORA_void)
+		return b->tseqbase == ORA_OID_NIL;
+	if (tdense(b))
+		return false;
+	for (uint64_t p = 1; p < b->count; p++)
+		if (jv(b, p - 1) < jv(b, p))
+			return false;
+	b->revsorted = 1;
+	return true;
+}
+
+/* ---- result builders --------------------------------------------------- */
+
+typedef struct {
+	ora_oid *a, *b;
+	uint64_t n, cap;
+} pairs;
+
+static int
+pairs_add(pairs *P, ora_oid x, ora_oid y)
+{
+	if (P->n == P->cap) {
+		uint64_t c = P->cap ? P->cap * 2 : 1024;
+		ora_oid *na = realloc(P->a, c * 8), *nb = realloc(P->b, c * 8);
+		if (na)
+			P->a = na;
+		if (nb)
+			P->b = nb;
+		if (!na || !nb) {
+			ora_seterr("out of memory");
+			return -1;
+		}
+		P->cap = c;
+	}
+	P->a[P->n] = x;
+	P->b[P->n] = y;
+	P->n++;
+	return 0;
+}
+
+static ora_bat *
+oidbat(const ora_oid *v, uint64_t n)
+{
+	ora_bat *bn = ora_new(ORA_oid, n, 0);
+	if (bn == NULL)
+		return NULL;
+	if (n)
+		memcpy(bn->base, v, n * 8);
+	bn->nonil = 1;
+	bn->nil = 0;
+	return bn;
+}
+
+/* properties of an oid column from its values */
+typedef struct {
+	bool asc, desc, eq, consec;   /* some adjacent pair <, >, ==; all +1 */
+} adj;
+
+static adj
+adjacent(const ora_oid *v, uint64_t n)
+{
+	adj r = {false, false, false, true};
+	for (uint64_t i = 1; i < n; i++) {
+		if (v[i - 1] < v[i])
+			r.asc = true;
+		else if (v[i - 1] > v[i])
+			r.desc = true;
+		else
+			r.eq = true;
+		if (v[i] != v[i - 1] + 1)
+			r.consec = false;
+	}
+	return r;
+}
+
+/* virtualize (gdk/gdk_select.c:31-89) of a sorted key oid column */
+static void
+virtualize(ora_bat *bn)
+{
+	if (bn->type != ORA_oid)
+		return;
+	const ora_oid *o = bn->base;
+	if (bn->count <= 1 || o[bn->count - 1] - o[0] == bn->count - 1) {
+		ora_oid seq = bn->count ? o[0] : 0;
+		free(bn->base);
+		bn->base = NULL;
+		bn->type = ORA_void;
+		bn->width = 0;
+		bn->tseqbase = seq;
+	}
+}
+
+/* BATsetcount (gdk/gdk_bat.c:2066-2082): counts <= 1 are ordered both ways */
+static void
+setcount_props(ora_bat *b)
+{
+	if (b->count <= 1)
+		b->sorted = b->revsorted = 1;
+}
+
+static void
+out2(ora_bat **r1p, ora_bat **r2p, ora_bat *a, ora_bat *b, bool swapped)
+{
+	if (swapped) {
+		ora_bat *t = a;
+		a = b;
+		b = t;
+	}
+	*r1p = a;
+	if (r2p)
+		*r2p = b;
+	else
+		ora_free(b);
+}
+
+/* nomatch (gdk_join.c:301-360) without nil_on_miss: two empty dense BATs */
+static int
+nomatch(ora_bat **r1p, ora_bat **r2p)
+{
+	ora_bat *a = ora_dense(0, 0, 0), *b = ora_dense(0, 0, 0);
+	if (!a || !b) {
+		ora_free(a);
+		ora_free(b);
+		return -1;
+	}
+	out2(r1p, r2p, a, b, false);
+	return 0;
+}
+
+/* ---- selectjoin (gdk_join.c:363-563) ------------------------------------ */
+
+static int
+selectjoin(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r, const ora_ci *lci,
+	   const ora_bat *sr, bool nil_matches, bool swapped)
+{
+	ora_oid o = ci_get(lci, 0);
+	int64_t v = jv(l, o - l->hseqbase);
+	if (!nil_matches && v == jnilv(l->type))
+		return nomatch(r1p, r2p);
+	/* bn = BATselect(r, sr, v, NULL, true, true, false, false) */
+	ora_bat *rr = r, *tmp = NULL;
+	if (r->type == ORA_void) {
+		/* the restated select reads stored values: materialise */
+		tmp = ora_new(ORA_oid, r->count, r->hseqbase);
+		if (tmp == NULL)
+			return -1;
+		for (uint64_t p = 0; p < r->count; p++)
+			((int64_t *) tmp->base)[p] = jv(r, p);
+		rr = tmp;
+	}
+	union { int8_t b; int16_t s; int32_t i; int64_t l; } val;
+	switch (rr->width) {
+	case 1: val.b = (int8_t) v; break;
+	case 2: val.s = (int16_t) v; break;
+	case 4: val.i = (int32_t) v; break;
+	default: val.l = v; break;
+	}
+	ora_bat *bn = ora_select(rr, sr, &val, NULL, true, true, false, false);
+	ora_free(tmp);
+	if (bn == NULL)
+		return -1;
+	uint64_t bnc = bn->count;
+	if (bnc == 0) {
+		ora_free(bn);
+		return nomatch(r1p, r2p);
+	}
+	uint64_t cnt = lci->n * bnc;
+	ora_bat *a = ora_new(ORA_oid, cnt, 0), *b = ora_new(ORA_oid, cnt, 0);
+	if (!a || !b) {
+		ora_free(a);
+		ora_free(b);
+		ora_free(bn);
+		return -1;
+	}
+	a->sorted = 1;
+	a->revsorted = lci->n == 1;
+	a->tseqbase = bnc == 1 && lci->dense ? o : ORA_OID_NIL;
+	a->key = bnc == 1;
+	a->nil = 0;
+	a->nonil = 1;
+	b->sorted = lci->n == 1 || bnc == 1;
+	b->revsorted = bnc == 1;
+	b->tseqbase = lci->n == 1 && tdense(bn) ? bn->tseqbase : ORA_OID_NIL;
+	b->key = lci->n == 1;
+	b->nil = 0;
+	b->nonil = 1;
+	ora_oid *A = a->base, *B = b->base;
+	for (uint64_t i = 0, k = 0; i < lci->n; i++) {
+		ora_oid lo = ci_get(lci, i);
+		for (uint64_t j = 0; j < bnc; j++, k++) {
+			A[k] = lo;
+			B[k] = bn->type == ORA_void ? bn->tseqbase + j : ((const ora_oid *) bn->base)[j];
+		}
+	}
+	ora_free(bn);
+	setcount_props(a);
+	setcount_props(b);
+	out2(r1p, r2p, a, b, swapped);
+	return 0;
+}
+
+/* ---- mergejoin_void (gdk_join.c:571-700, no nil_on_miss) ----------------- */
+
+static int
+mergejoin_void(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r, const ora_bat *sl,
+	       const ora_ci *rci, bool swapped)
+{
+	ora_oid lo = r->tseqbase, hi = lo + r->count;
+	if (rci->seq > r->hseqbase)
+		lo += rci->seq - r->hseqbase;
+	if (rci->seq + rci->n < r->hseqbase + r->count)
+		hi -= r->hseqbase + r->count - rci->seq - rci->n;
+	/* r1 = BATselect(l, sl, &lo, &hi, true, false, false, false) */
+	ora_bat *ll = l, *tmp = NULL;
+	if (l->type == ORA_void) {
+		tmp = ora_new(ORA_oid, l->count, l->hseqbase);
+		if (tmp == NULL)
+			return -1;
+		for (uint64_t p = 0; p < l->count; p++)
+			((int64_t *) tmp->base)[p] = jv(l, p);
+		ll = tmp;
+	}
+	ora_bat *a = ora_select(ll, sl, &lo, &hi, true, false, false, false);
+	ora_free(tmp);
+	if (a == NULL)
+		return -1;
+	ora_bat *b;
+	if (a->count == 0) {
+		b = ora_dense(0, 0, 0);
+	} else if (tdense(a) && tdense(l)) {
+		b = ora_dense(0, l->tseqbase + a->tseqbase - l->hseqbase + r->hseqbase - r->tseqbase, a->count);
+	} else {
+		b = ora_new(ORA_oid, a->count, 0);
+		if (b) {
+			for (uint64_t k = 0; k < a->count; k++) {
+				ora_oid o1 = a->type == ORA_void ? a->tseqbase + k : ((const ora_oid *) a->base)[k];
+				((ora_oid *) b->base)[k] = (ora_oid) jv(l, o1 - l->hseqbase) - r->tseqbase + r->hseqbase;
+			}
+			b->key = l->key;
+			b->sorted = l->sorted;
+			b->revsorted = l->revsorted;
+			b->nil = 0;
+			b->nonil = 1;
+			setcount_props(b);
+		}
+	}
+	if (b == NULL) {
+		ora_free(a);
+		return -1;
+	}
+	out2(r1p, r2p, a, b, swapped);
+	return 0;
+}
+
+/* ---- mergejoin (gdk_join.c:1941-2780; :1023-1335 mergejoin_int / _lng) ---- */
+
+/* the matches of one driving value: the candidate index range [lo, hi) of
+ * the sorted other side whose values equal v */
+static void
+equal_range(const ora_bat *r, const ora_ci *rci, bool rasc, int64_t v, uint64_t *lo, uint64_t *hi)
+{
+	uint64_t a = 0, b = rci->n;
+	while (a < b) {                 /* first index not "before" v */
+		uint64_t m = (a + b) / 2;
+		int64_t x = jv(r, ci_get(rci, m) - r->hseqbase);
+		if (rasc ? x < v : x > v)
+			a = m + 1;
+		else
+			b = m;
+	}
+	uint64_t c = a, d = rci->n;
+	while (c < d) {                 /* first index "after" v */
+		uint64_t m = (c + d) / 2;
+		int64_t x = jv(r, ci_get(rci, m) - r->hseqbase);
+		if (rasc ? x <= v : x >= v)
+			c = m + 1;
+		else
+			d = m;
+	}
+	*lo = a;
+	*hi = c;
+}
+
+static int
+mergejoin(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r, const ora_ci *lci,
+	  const ora_ci *rci, bool nil_matches, bool swapped)
+{
+	const int bt = atomtype(l->type);
+	const bool special = lci->dense && lci->n == l->count && rci->dense && rci->n == r->count &&
+		l->sorted && r->sorted && l->type != ORA_void &&
+		(bt == ORA_int || bt == ORA_date || bt == ORA_lng || bt == ORA_oid ||
+		 bt == ORA_daytime || bt == ORA_timestamp);
+	const bool lsorted = l->sorted || l->revsorted;   /* lscan > 0 */
+	const bool rasc = r->sorted;
+	const int64_t lnil = jnilv(l->type);
+	pairs P = {0};
+	uint64_t groups = 0;            /* matched runs of equal driving values */
+	bool nlmulti = false;           /* a matched run of several driving rows */
+	for (uint64_t i = 0; i < lci->n; i++) {
+		ora_oid lo_ = ci_get(lci, i);
+		int64_t v = jv(l, lo_ - l->hseqbase);
+		if (v == lnil && !nil_matches)
+			continue;
+		uint64_t a, b;
+		equal_range(r, rci, rasc, v, &a, &b);
+		if (a == b)
+			continue;
+		if (i == 0 || jv(l, ci_get(lci, i - 1) - l->hseqbase) != v)
+			groups++;
+		else
+			nlmulti = true;
+		for (uint64_t j = a; j < b; j++)
+			if (pairs_add(&P, lo_, ci_get(rci, j)) < 0) {
+				free(P.a);
+				free(P.b);
+				return -1;
+			}
+	}
+	ora_bat *A = oidbat(P.a, P.n), *B = oidbat(P.b, P.n);
+	free(P.a);
+	free(P.b);
+	if (!A || !B) {
+		ora_free(A);
+		ora_free(B);
+		return -1;
+	}
+	const uint64_t n = A->count;
+	adj a1 = adjacent(A->base, n), a2 = adjacent(B->base, n);
+	/* r1 ascends with the driving candidates: ordered, revsorted only when
+	 * all equal, key when no value has several matches */
+	A->sorted = 1;
+	A->revsorted = !a1.asc;
+	A->key = !a1.eq;
+	B->sorted = !a2.desc;
+	B->key = !a2.eq && !a2.desc;
+	if (special) {
+		/* mergejoin_int / _lng keep the dense oid columns as oid */
+		B->revsorted = !a2.asc;
+		B->key = !nlmulti;
+		A->tseqbase = n == 0 ? 0 : (A->key && a1.consec ? ((ora_oid *) A->base)[0] : ORA_OID_NIL);
+		B->tseqbase = n == 0 ? 0 : (B->key && !a2.desc && a2.consec ? ((ora_oid *) B->base)[0] : ORA_OID_NIL);
+		setcount_props(A);
+		setcount_props(B);
+	} else {
+		if (lsorted) {
+			/* every property the loop maintains is the column's own */
+			B->revsorted = !a2.asc;
+			B->key = !nlmulti;
+		} else {
+			/* l unsorted: r2 is flagged reverse sorted only within one run,
+			 * and key only while it ascends (or for two descending rows of two
+			 * runs) -- gdk_join.c:2587-2631 */
+			B->revsorted = !a2.asc && groups <= 1;
+			B->key = (!a2.desc && !a2.eq) ||
+				(n == 2 && ((ora_oid *) B->base)[0] > ((ora_oid *) B->base)[1]);
+		}
+		setcount_props(A);
+		setcount_props(B);
+		if (A->key)
+			virtualize(A);
+		if (n <= 1) {
+			B->key = 1;
+			virtualize(B);
+		}
+	}
+	out2(r1p, r2p, A, B, swapped);
+	return 0;
+}
+
+/* ---- hashjoin (gdk_join.c:2900-3335) --------------------------------------- */
+
+static int
+hashjoin(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r, const ora_ci *lci,
+	 const ora_ci *rci, bool nil_matches, bool swapped)
+{
+	uint64_t cap = 16;
+	while (cap < 2 * rci->n)
+		cap <<= 1;
+	int64_t *head = malloc(cap * sizeof(int64_t));
+	int64_t *next = malloc((rci->n + 1) * sizeof(int64_t));
+	int64_t *keys = malloc((rci->n + 1) * sizeof(int64_t));
+	if (!head || !next || !keys) {
+		free(head); free(next); free(keys);
+		ora_seterr("out of memory");
+		return -1;
+	}
+	memset(head, 0xff, cap * sizeof(int64_t));
+	/* chains by prepending (gdk_hash.c:658-704): DESCENDING position */
+	for (uint64_t j = 0; j < rci->n; j++) {
+		keys[j] = jv(r, ci_get(rci, j) - r->hseqbase);
+		uint64_t h = ((uint64_t) keys[j] * 0x9e3779b97f4a7c15ull) >> 20 & (cap - 1);
+		next[j] = head[h];
+		head[h] = (int64_t) j;
+	}
+	const int64_t lnil = jnilv(l->type);
+	pairs P = {0};
+	for (uint64_t i = 0; i < lci->n; i++) {
+		ora_oid lo_ = ci_get(lci, i);
+		int64_t v = jv(l, lo_ - l->hseqbase);
+		if (v == lnil && !nil_matches)
+			continue;
+		uint64_t h = ((uint64_t) v * 0x9e3779b97f4a7c15ull) >> 20 & (cap - 1);
+		for (int64_t j = head[h]; j >= 0; j = next[j])
+			if (keys[j] == v && pairs_add(&P, lo_, ci_get(rci, (uint64_t) j)) < 0) {
+				free(head); free(next); free(keys); free(P.a); free(P.b);
+				return -1;
+			}
+	}
+	free(head); free(next); free(keys);
+	ora_bat *A = oidbat(P.a, P.n), *B = oidbat(P.b, P.n);
+	free(P.a);
+	free(P.b);
+	if (!A || !B) {
+		ora_free(A);
+		ora_free(B);
+		return -1;
+	}
+	const uint64_t n = A->count;
+	adj a1 = adjacent(A->base, n);
+	A->sorted = 1;
+	A->revsorted = !a1.asc;
+	A->key = !a1.eq;
+	/* r1 keeps a tseqbase while the matched candidates are consecutive
+	 * (lskipped, gdk_join.c:3206-3230), only for a dense left candidate list */
+	A->tseqbase = lci->dense && A->key && a1.consec ? 0 : ORA_OID_NIL;
+	B->sorted = B->revsorted = 0;
+	B->key = l->key;
+	B->tseqbase = ORA_OID_NIL;
+	if (n <= 1) {
+		A->sorted = A->revsorted = A->key = 1;
+		A->tseqbase = 0;
+		B->sorted = B->revsorted = B->key = 1;
+		B->tseqbase = 0;
+	}
+	if (n > 0) {
+		if (A->tseqbase != ORA_OID_NIL)
+			A->tseqbase = ((ora_oid *) A->base)[0];
+		if (B->tseqbase != ORA_OID_NIL)
+			B->tseqbase = ((ora_oid *) B->base)[0];
+	}
+	double ue = l->unique_est < r->unique_est ? l->unique_est : r->unique_est;
+	A->unique_est = B->unique_est = ue;
+	out2(r1p, r2p, A, B, swapped);
+	return 0;
+}
+
+/* ---- cost model (gdk_join.c:3337-3689) ------------------------------------- */
+
+/* count_unique (gdk_join.c:3337-3516): distinct values among the first half
+ * and among all of the sampled positions s[0..ns) */
+static void
+count_unique(ora_bat *b, const ora_oid *s, uint64_t ns, uint64_t *cnt1, uint64_t *cnt2)
+{
+	uint64_t half = ns / 2;
+	if (b->key || ns <= 1 || tdense(b)) {
+		*cnt1 = half;
+		*cnt2 = ns;
+		return;
+	}
+	(void) ordered(b);
+	(void) ordered_rev(b);
+	if ((b->sorted && b->revsorted) || (b->type == ORA_void && b->tseqbase == ORA_OID_NIL)) {
+		*cnt1 = *cnt2 = 1;
+		return;
+	}
+	int64_t *seen = malloc((ns + 1) * sizeof(int64_t));
+	uint64_t ndist = 0;
+	*cnt1 = 0;
+	for (uint64_t i = 0; i < ns; i++) {
+		if (i == half)
+			*cnt1 = ndist;
+		int64_t v = jv(b, s[i] - b->hseqbase);
+		bool found = false;
+		for (uint64_t k = 0; k < ndist && !found; k++)
+			found = seen[k] == v;
+		if (!found)
+			seen[ndist++] = v;
+	}
+	*cnt2 = ndist;
+	free(seen);
+}
+
+/* the rows BATsample(b, 1000) stands for: all of them up to 1000 rows (the
+ * reference's own rule, gdk_sample.c:114-117), else 1000 evenly spaced */
+static uint64_t
+sample_positions(uint64_t cnt, uint64_t *pos)
+{
+	if (cnt <= 1000) {
+		for (uint64_t i = 0; i < cnt; i++)
+			pos[i] = i;
+		return cnt;
+	}
+	for (uint64_t i = 0; i < 1000; i++)
+		pos[i] = (uint64_t) ((unsigned __int128) i * cnt / 1000);
+	return 1000;
+}
+
+/* guess_uniques (gdk_join.c:3518-3576); s is the candidate BAT behind ci
+ * (NULL: all of b).  A candidate list is sampled whole (not clipped to b)
+ * and the sample projected through it, as BATsample + BATproject do. */
+static double
+guess_uniques(ora_bat *b, const ora_ci *ci, const ora_bat *s)
+{
+	if (b->key)
+		return (double) ci->n;
+	uint64_t pos[1000];
+	ora_oid s1[1000];
+	uint64_t n2;
+	const bool full = s == NULL || (ci->dense && ci->n == b->count);
+	if (full) {
+		if (b->unique_est != 0)
+			return b->unique_est;
+		n2 = sample_positions(b->count, pos);
+		for (uint64_t i = 0; i < n2; i++)
+			s1[i] = b->hseqbase + pos[i];
+	} else {
+		n2 = sample_positions(s->count, pos);
+		for (uint64_t i = 0; i < n2; i++)
+			s1[i] = s->type == ORA_void ? s->tseqbase + pos[i] : ((const ora_oid *) s->base)[pos[i]];
+	}
+	uint64_t n1 = n2 / 2, cnt1, cnt2;
+	/* count_unique iterates the sample as a candidate list of b (clipped) */
+	uint64_t lo = 0, hi = n2;
+	while (lo < hi && s1[lo] < b->hseqbase)
+		lo++;
+	while (hi > lo && s1[hi - 1] >= b->hseqbase + b->count)
+		hi--;
+	count_unique(b, s1 + lo, hi - lo, &cnt1, &cnt2);
+	double A = (double) (cnt2 - cnt1) / (n2 - n1);
+	double B = cnt1 - n1 * A;
+	B += A * ci->n;
+	if (full && b->unique_est == 0)
+		b->unique_est = B;
+	return B;
+}
+
+/* joincost (gdk_join.c:3586-3689) with no prebuilt hash */
+static double
+joincost(ora_bat *r, uint64_t lcount, const ora_ci *rci, const ora_bat *sr)
+{
+	double rcost = 1;
+	if (!rci->dense && rci->n > 0)
+		rcost += log2((double) rci->n);
+	rcost *= lcount;
+	const uint64_t cnt = r->count;
+	if (!tdense(r)) {
+		double ue = r->unique_est;
+		if (ue == 0) {
+			ora_ci all = {.dense = true, .seq = r->hseqbase, .n = r->count};
+			ue = guess_uniques(r, &all, NULL);
+		}
+		rcost *= 1.1 * ((double) cnt / ue);
+		rcost += cnt * 2.0;
+	}
+	if (rci->n != cnt) {
+		double ue = r->unique_est;
+		if (ue == 0)
+			ue = guess_uniques(r, rci, sr);
+		double rccost = 1.1 * ((double) cnt / ue);
+		rccost *= lcount;
+		rccost += rci->n * 2.0;
+		if (rccost < rcost)
+			rcost = rccost;
+	}
+	return rcost;
+}
+
+/* ---- BATjoin (gdk_join.c:4451-4623) ---------------------------------------- */
+
+int
+ora_join(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r,
+	 const ora_bat *sl, const ora_bat *sr, bool nil_matches)
+{
+	if (atomtype(l->type) != atomtype(r->type)) {
+		ora_seterr("BATjoin: inputs not compatible.");
+		return -1;
+	}
+	if (!join_type_ok(l->type) || !join_type_ok(r->type)) {
+		ora_seterr("BATjoin: type not restated");
+		return -1;
+	}
+	ora_ci lci, rci;
+	if (ora_ci_init(&lci, l, sl) < 0 || ora_ci_init(&rci, r, sr) < 0)
+		return -1;
+	if (lci.n == 0 || rci.n == 0)
+		return nomatch(r1p, r2p);
+	if (lci.n == 1 || (ordered(l) && ordered_rev(l)) ||
+	    (l->type == ORA_void && l->tseqbase == ORA_OID_NIL))
+		return selectjoin(r1p, r2p, l, r, &lci, sr, nil_matches, false);
+	if (rci.n == 1 || (ordered(r) && ordered_rev(r)) ||
+	    (r->type == ORA_void && r->tseqbase == ORA_OID_NIL))
+		return selectjoin(r1p, r2p, r, l, &rci, sl, nil_matches, true);
+	if (tdense(r) && rci.dense)
+		return mergejoin_void(r1p, r2p, l, r, sl, &rci, false);
+	if (tdense(l) && lci.dense)
+		return mergejoin_void(r1p, r2p, r, l, sr, &lci, true);
+	if ((ordered(l) || ordered_rev(l)) && (ordered(r) || ordered_rev(r)))
+		return mergejoin(r1p, r2p, l, r, &lci, &rci, nil_matches, false);
+	double lcost = joincost(l, rci.n, &lci, sl);
+	double rcost = joincost(r, lci.n, &rci, sr);
+	bool swap = lcost < rcost;
+	double best = swap ? lcost : rcost;
+	if ((ordered(r) || ordered_rev(r)) && lci.n * (log2((double) rci.n) + 1) < best)
+		return mergejoin(r1p, r2p, l, r, &lci, &rci, nil_matches, false);
+	if ((ordered(l) || ordered_rev(l)) && rci.n * (log2((double) lci.n) + 1) < best)
+		return mergejoin(r1p, r2p, r, l, &rci, &lci, nil_matches, true);
+	if (swap)
+		return hashjoin(r1p, r2p, r, l, &rci, &lci, nil_matches, true);
+	return hashjoin(r1p, r2p, l, r, &lci, &rci, nil_matches, false);
+}
+
+/* which algorithm ora_join takes (tests assert the branch they mean to
+ * cover): 0 nomatch, 1 selectjoin, 2 selectjoin swapped, 3 mergejoin_void,
+ * 4 mergejoin_void swapped, 5 mergejoin (both sorted), 6 mergejoin (r
+ * sorted, cheaper), 7 mergejoin swapped, 8 hashjoin swapped, 9 hashjoin.
+ * Evaluates the same conditions (and caches the same flags). */
+int
+ora_join_algo(ora_bat *l, ora_bat *r, const ora_bat *sl, const ora_bat *sr)
+{
+	ora_ci lci, rci;
+	if (ora_ci_init(&lci, l, sl) < 0 || ora_ci_init(&rci, r, sr) < 0)
+		return -1;
+	if (lci.n == 0 || rci.n == 0)
+		return 0;
+	if (lci.n == 1 || (ordered(l) && ordered_rev(l)) ||
+	    (l->type == ORA_void && l->tseqbase == ORA_OID_NIL))
+		return 1;
+	if (rci.n == 1 || (ordered(r) && ordered_rev(r)) ||
+	    (r->type == ORA_void && r->tseqbase == ORA_OID_NIL))
+		return 2;
+	if (tdense(r) && rci.dense)
+		return 3;
+	if (tdense(l) && lci.dense)
+		return 4;
+	if ((ordered(l) || ordered_rev(l)) && (ordered(r) || ordered_rev(r)))
+		return 5;
+	double lcost = joincost(l, rci.n, &lci, sl);
+	double rcost = joincost(r, lci.n, &rci, sr);
+	bool swap = lcost < rcost;
+	double best = swap ? lcost : rcost;
+	if ((ordered(r) || ordered_rev(r)) && lci.n * (log2((double) rci.n) + 1) < best)
+		return 6;
+	if ((ordered(l) || ordered_rev(l)) && rci.n * (log2((double) lci.n) + 1) < best)
+		return 7;
+	return swap ? 8 : 9;
+}

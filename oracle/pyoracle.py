@@ -32,7 +32,7 @@ class OraBat(C.Structure):
                 ("vheap", C.c_void_p), ("vheapsize", C.c_uint64),
                 ("sorted", C.c_uint8), ("revsorted", C.c_uint8), ("key", C.c_uint8),
                 ("nonil", C.c_uint8), ("nil", C.c_uint8), ("owned", C.c_uint8),
-                ("_pad", C.c_uint8 * 2)]
+                ("_pad", C.c_uint8 * 2), ("unique_est", C.c_double)]
 
 
 class OraLineitem(C.Structure):
@@ -87,6 +87,7 @@ def lib():
         L.ora_groupavg3combine.argtypes = [P, P, P, P, P, C.c_bool]
         L.ora_groupavg3.argtypes = [C.POINTER(P), C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool]
         L.ora_join.argtypes = [C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool]
+        L.ora_join_algo.argtypes = [P, P, P, P]
         L.ora_sort.argtypes = [C.POINTER(P), C.POINTER(P), P, C.c_bool, C.c_bool]
         L.ora_firstn.restype = P
         L.ora_firstn.argtypes = [P, P, P, C.c_uint64, C.c_bool, C.c_bool]
@@ -134,7 +135,7 @@ class Bat:
 
     @classmethod
     def from_array(cls, tp, arr, hseqbase=0, sorted_=False, revsorted=False, key=False,
-                   nonil=False, vheap=None):
+                   nonil=False, vheap=None, tseqbase=OID_NIL, unique_est=0.0):
         if tp == TYPE_hge:
             a = np.ascontiguousarray(arr, dtype=np.uint64).reshape(-1, 2)
         else:
@@ -145,7 +146,8 @@ class Bat:
         b.width = 16 if tp == TYPE_hge else (1 if tp == TYPE_str else a.dtype.itemsize)
         b.count = n
         b.hseqbase = hseqbase
-        b.tseqbase = OID_NIL
+        b.tseqbase = tseqbase
+        b.unique_est = unique_est
         b.base = a.ctypes.data if n else a.ctypes.data
         keep = [a, b]
         if vheap is not None:
@@ -297,6 +299,26 @@ def BATjoin(l, r, sl=None, sr=None, nil_matches=False):
                       sr.ptr if sr else None, nil_matches) < 0:
         raise _err()
     return Bat(a), Bat(b)
+
+
+JOIN_ALGOS = ["nomatch", "selectjoin", "selectjoin_swapped", "mergejoin_void", "mergejoin_void_swapped",
+              "mergejoin_sorted", "mergejoin", "mergejoin_swapped", "hashjoin_swapped", "hashjoin"]
+
+
+def join_algo(l, r, sl=None, sr=None):
+    """Name of the algorithm BATjoin(l, r, sl, sr) takes (gdk_join.c:4542-4618)."""
+    k = lib().ora_join_algo(l.ptr, r.ptr, sl.ptr if sl else None, sr.ptr if sr else None)
+    if k < 0:
+        raise _err()
+    return JOIN_ALGOS[k]
+
+
+def props(b):
+    """The result properties a parity test compares (gdk/gdk.h:712-740)."""
+    s = b.s
+    return dict(type="void" if s.type == TYPE_void else "oid" if s.type == TYPE_oid else s.type,
+                count=s.count, tseqbase=s.tseqbase, sorted=bool(s.sorted), revsorted=bool(s.revsorted),
+                key=bool(s.key), nonil=bool(s.nonil), nil=bool(s.nil))
 
 
 def BATsort(b, reverse=False, nilslast=False):

@@ -240,3 +240,128 @@ def replay_intervals(bounds, make_bat):
         if got != c["expected"]:
             bad.append((c, got))
     return bad
+
+
+# ---- BATjoin shapes covering every algorithm BATjoin chooses -------------------
+# (gdk_join.c:4542-4618).  Each case: l / r values with their GDK type, head
+# bases, optional candidate lists (sorted oid arrays or ("dense", seq, n)),
+# the flags the caller knows (both implementations start from the same
+# ones) and the algorithm the reference takes for it.
+
+def join_cases():
+    r = rng(4242)
+    I32, I64, U64 = np.int32, np.int64, np.uint64
+    NI = -(1 << 31)
+    cs = []
+
+    def add(name, tp, lv, rv, algo, lh=0, rh=0, sl=None, sr=None, nil_matches=False,
+            lflags=None, rflags=None, lvoid=None, rvoid=None):
+        cs.append(dict(name=name, tp=tp, lv=lv, rv=rv, algo=algo, lh=lh, rh=rh, sl=sl, sr=sr,
+                       nil_matches=nil_matches, lflags=lflags or {}, rflags=rflags or {},
+                       lvoid=lvoid, rvoid=rvoid))
+
+    # selectjoin: a single left candidate, an all-equal left, the same on the right
+    rv = r.integers(0, 50, 5000).astype(I32)
+    add("single_l", "int", np.array([7], I32), rv, "selectjoin", rh=3)
+    add("single_l_cand", "int", r.integers(0, 50, 300).astype(I32), rv, "selectjoin", lh=10,
+        sl=np.array([25], U64))
+    add("const_l", "int", np.full(40, 9, I32), rv, "selectjoin", lh=5)
+    add("const_l_nil", "int", np.full(30, NI, I32), np.where(rv < 3, NI, rv).astype(I32), "selectjoin",
+        nil_matches=True)
+    add("const_l_nil_nomatch", "int", np.full(30, NI, I32), np.where(rv < 3, NI, rv).astype(I32),
+        "selectjoin")
+    add("single_r", "int", r.integers(0, 50, 5000).astype(I32), np.array([11], I32), "selectjoin_swapped")
+    add("const_r", "lng", r.integers(0, 20, 3000).astype(I64), np.full(17, 4, I64), "selectjoin_swapped",
+        lh=2, rh=9)
+    # mergejoin_void: a dense right (or left) side
+    lo = r.integers(0, 3000, 8000).astype(U64)
+    lo[::97] = 1 << 63
+    add("dense_r", "oid", lo, None, "mergejoin_void", rvoid=(1000, 1500), rh=40)
+    add("dense_r_cand", "oid", lo, None, "mergejoin_void", rvoid=(1000, 1500), rh=40,
+        sr=("dense", 100, 700), sl=np.sort(r.choice(8000, 3000, replace=False)).astype(U64))
+    add("dense_l", "oid", None, r.integers(0, 900, 6000).astype(U64), "mergejoin_void_swapped",
+        lvoid=(200, 500), lh=7)
+    add("dense_both_sorted_l", "oid", np.sort(r.integers(0, 900, 6000)).astype(U64), None,
+        "mergejoin_void", rvoid=(100, 300))
+    # both sorted: full dense candidates (mergejoin_int / _lng) and general
+    ls = np.sort(r.integers(0, 4000, 20000)).astype(I32)
+    rs = np.sort(r.integers(0, 4000, 9000)).astype(I32)
+    add("sorted_int", "int", ls, rs, "mergejoin_sorted", lh=3, rh=11)
+    add("sorted_lng_nil", "lng", np.sort(np.where(r.random(5000) < .05, -(1 << 63),
+                                                  r.integers(0, 900, 5000))).astype(I64),
+        np.sort(np.where(r.random(3000) < .05, -(1 << 63), r.integers(0, 900, 3000))).astype(I64),
+        "mergejoin_sorted", nil_matches=True)
+    add("sorted_lng_nil_nomatch", "lng", np.sort(np.where(r.random(5000) < .05, -(1 << 63),
+                                                          r.integers(0, 900, 5000))).astype(I64),
+        np.sort(np.where(r.random(3000) < .05, -(1 << 63), r.integers(0, 900, 3000))).astype(I64),
+        "mergejoin_sorted")
+    add("sorted_key_dense", "int", np.arange(100, 2100, dtype=I32), np.arange(0, 5000, 2, dtype=I32),
+        "mergejoin_sorted")
+    add("sorted_consec", "int", np.arange(0, 3000, dtype=I32), np.arange(1000, 9000, dtype=I32),
+        "mergejoin_sorted", lh=50, rh=60)
+    add("sorted_cands", "int", ls, rs, "mergejoin_sorted",
+        sl=np.sort(r.choice(20000, 12000, replace=False)).astype(U64) + 3,
+        sr=np.sort(r.choice(9000, 6000, replace=False)).astype(U64) + 11, lh=3, rh=11)
+    add("sorted_sht", "sht", np.sort(r.integers(-300, 300, 6000)).astype(np.int16),
+        np.sort(r.integers(-300, 300, 2000)).astype(np.int16), "mergejoin_sorted")
+    add("ldesc_rasc", "int", ls[::-1].copy(), rs, "mergejoin_sorted", lh=3, rh=11)
+    add("lasc_rdesc", "int", ls, rs[::-1].copy(), "mergejoin_sorted")
+    add("both_desc", "lng", ls[::-1].astype(I64), rs[::-1].astype(I64), "mergejoin_sorted")
+    # one side sorted and binary search cheaper than a hash
+    rkey = np.sort(r.choice(1 << 20, 100_000, replace=False)).astype(I32)
+    add("small_l_sorted_r", "int", r.choice(rkey, 3000).astype(I32), rkey, "mergejoin", rh=5)
+    add("small_l_sorted_r_dups", "int", np.concatenate([r.integers(0, 5000, 1500),
+                                                        np.repeat(r.integers(0, 5000, 300), 3)]).astype(I32),
+        np.sort(r.integers(0, 5000, 60_000)).astype(I32), "mergejoin")
+    add("two_rows_desc", "int", np.array([30, 10, 99], I32), np.arange(40, dtype=I32), "mergejoin")
+    add("three_rows_desc", "int", np.array([30, 10, 5, 99], I32), np.arange(40, dtype=I32), "mergejoin")
+    add("runs_unsorted", "int", np.array([5, 5, 3, 3, 8, 1, 5], I32), np.sort(r.integers(0, 10, 200)).astype(I32),
+        "mergejoin")
+    add("small_r_sorted_l", "int", rkey, r.choice(rkey, 3000).astype(I32), "mergejoin_swapped", lh=8)
+    # hash joins: swapped (small left) and plain, duplicate build keys, nils
+    add("hash_swapped", "int", r.choice(1 << 20, 1000, replace=False).astype(I32),
+        r.integers(0, 1 << 20, 100_000).astype(I32), "hashjoin_swapped")
+    add("hash_swapped_tiny", "int", np.array([1, 2, 1], I32), np.array([1, 1, 3, 1], I32), "hashjoin_swapped")
+    add("hash_plain", "int", r.integers(0, 30_000, 100_000).astype(I32),
+        r.choice(30_000, 20_000, replace=False).astype(I32), "hashjoin", lh=4, rh=17)
+    add("hash_dups", "lng", r.integers(0, 3000, 50_000).astype(I64), r.integers(0, 3000, 9000).astype(I64),
+        "hashjoin")
+    add("hash_nils", "int", np.where(r.random(60_000) < .02, NI, r.integers(0, 9000, 60_000)).astype(I32),
+        np.where(r.random(12_000) < .02, NI, r.integers(0, 9000, 12_000)).astype(I32), "hashjoin",
+        nil_matches=True)
+    add("hash_cands", "int", r.integers(0, 30_000, 80_000).astype(I32),
+        r.choice(60_000, 30_000, replace=False).astype(I32), "hashjoin",
+        sl=np.sort(r.choice(80_000, 50_000, replace=False)).astype(U64),
+        sr=("dense", 2000, 20_000))
+    add("hash_key_flag", "int", r.integers(0, 30_000, 100_000).astype(I32),
+        r.choice(30_000, 20_000, replace=False).astype(I32), "hashjoin",
+        lflags=dict(key=False), rflags=dict(key=True))
+    add("hash_bte", "bte", r.integers(-100, 100, 40_000).astype(np.int8),
+        r.integers(-100, 100, 5_000).astype(np.int8), "hashjoin_swapped")
+    return cs
+
+
+def join_expected(c, lv, rv, lcand, rcand):
+    """The pairs BATjoin returns for algorithm c["algo"], from the order rule
+    of each algorithm (per driving candidate in order; matches ascending for
+    select / merge joins, descending for hash joins; swapped variants drive
+    from the right)."""
+    algo = c["algo"]
+    swapped = algo.endswith("swapped")
+    nm = c["nil_matches"]
+    dv, ov, dc, oc = (rv, lv, rcand, lcand) if swapped else (lv, rv, lcand, rcand)
+    dh, oh = (c["rh"], c["lh"]) if swapped else (c["lh"], c["rh"])
+    desc = algo.startswith("hashjoin")
+    from collections import defaultdict
+    pos = defaultdict(list)
+    for o in oc:
+        pos[ov[o - oh]].append(o)
+    out = []
+    for o in dc:
+        v = dv[o - dh]
+        if v is None and not nm:
+            continue
+        m = pos.get(v, [])
+        for x in (m[::-1] if desc else m):
+            out.append((x, o) if swapped else (o, x))
+    return out

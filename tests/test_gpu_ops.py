@@ -627,7 +627,7 @@ def test_complex_candidate_lists(gdk, ora):
         # join with a complex left candidate list
         rk = r.permutation(2000).astype(np.int32) - 1000
         R = gdk.BAT.from_numpy(gdk.TYPE_int, rk)
-        OR = ora.Bat.from_array(ora.TYPE_int, rk)
+        OR = ora.Bat.from_array(ora.TYPE_int, rk, key=True, nonil=True)
         r1, r2 = gdk.BATjoin(B, R, sl=S)
         o1, o2 = ora.BATjoin(OB, OR, sl=OS)
         assert np.array_equal(r1.to_numpy(), np.asarray(o1.values()))
