@@ -142,9 +142,16 @@ mgdk_bat *mgdk_BATgroupmax(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, i
 int mgdk_BATgroup(mgdk_bat **groups, mgdk_bat **extents, mgdk_bat **histo,
 		  mgdk_bat *b, mgdk_bat *s, mgdk_bat *g, mgdk_bat *e, mgdk_bat *h);
 
-/* ---- join, hash path (gdk/gdk.h:2266; gdk/gdk_join.c:4451, :2900) ----- */
+/* ---- join (gdk/gdk.h:2266; gdk/gdk_join.c:4451): the reference's choice
+ * of selectjoin / mergejoin_void / mergejoin / hashjoin (and swapped),
+ * which fixes the result order and properties ---------------------------- */
 int mgdk_BATjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r,
 		 mgdk_bat *sl, mgdk_bat *sr, bool nil_matches, mgdk_BUN estimate);
+/* gdk/gdk.h:1524-1525 (gdk_batop.c:2002, :2181): whether b is sorted /
+ * reverse sorted; what is found is recorded in b (tsorted, trevsorted,
+ * tkey, tnosorted, tnorevsorted) as the reference does */
+bool mgdk_BATordered(mgdk_bat *b);
+bool mgdk_BATordered_rev(mgdk_bat *b);
 
 /* ---- sort (gdk/gdk.h:1526; gdk/gdk_batop.c:2342) ---------------------- */
 int mgdk_BATsort(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups,

@@ -1033,3 +1033,17 @@ mgdk_BATjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk_bat 
 	return hashjoin(r1p, r2p, l, r, lc, rc, nil_matches, false);
 #undef ORD
 }
+
+extern "C" bool
+mgdk_BATordered(mgdk_bat *b)
+{
+	Ord o;
+	return b && ordered(b, o) > 0;
+}
+
+extern "C" bool
+mgdk_BATordered_rev(mgdk_bat *b)
+{
+	Ord o;
+	return b && ordered_rev(b, o) > 0;
+}

@@ -11,9 +11,11 @@ results are combined the way mergetable re-aggregates packed partials
     (key, first row, count, sums) rows hash-partitioned by key and shuffled
     with ONE all_to_all, merged by a second BATgroup on the owner, and group
     ids renumbered in global first-occurrence order (dist_group_aggr);
-  * hash join: both sides hash-partitioned by key and shuffled, joined on the
-    owner, the (l, r) pairs shuffled back to the left row's home rank and
-    restored to the reference order by a stable sort on l (dist_join);
+  * join: both sides hash-partitioned by key and shuffled, joined on the
+    owner, the (l, r) pairs shuffled back to the home rank of their driving
+    row and put in the order of the algorithm single-node BATjoin would take
+    (join_plan: the same tests and cost model over all-gathered order facts
+    and a 1000-value sample) by two stable sorts (dist_join);
   * sort: local stable sort, (key, position) splitters from an all-gathered
     sample, one all_to_all of the runs, stable merge sort per rank
     (dist_sort);
@@ -200,9 +202,24 @@ class GdkBackend:
     def join(self, l, r):
         return self.gdk.BATjoin(l, r)
 
-    def sort(self, c):
-        s, o, _ = self.gdk.BATsort(c)
+    def sort(self, c, reverse=False):
+        s, o, _ = self.gdk.BATsort(c, reverse=reverse, nilslast=reverse)
         return s, o
+
+    def order_info(self, c):
+        """(sorted, revsorted, key-if-sorted, first, last) of a widened column"""
+        g = self.gdk
+        srt, rev = g.BATordered(c), g.BATordered_rev(c)
+        n = c.count()
+        first = int(g.BATslice(c, 0, 1).to_numpy()[0])
+        last = int(g.BATslice(c, n - 1, n).to_numpy()[0])
+        return srt, rev, bool(c.s.tkey) and srt, first, last
+
+    def values_at(self, c, positions):
+        import numpy as np
+        g = self.gdk
+        o = g.BAT.from_numpy(g.TYPE_oid, np.asarray(positions, np.uint64) + c.hseqbase, sorted_=True, key=True)
+        return [int(v) for v in g.BATproject(o, c).to_numpy()]
 
     def lowerbound2(self, keys, pos, qk, qp):
         return self.gdk.BATlowerbound2(keys, pos, qk, qp)
@@ -382,16 +399,102 @@ def dist_group_avg(be, dist, keys, vals):
 # hash join
 # ---------------------------------------------------------------------------
 
-def dist_join(be, dist, lkeys, rkeys, lrows_per_rank):
+def _side_stats(be, dist, c, row0):
+    """What BATjoin's tests see of a sharded side (gdk_join.c:4542-4618):
+    global count, BATordered / BATordered_rev / the key BATordered records,
+    and the values at the positions BATsample(b, 1000) stands for (all rows
+    up to 1000, else floor(i * n / 1000)) in row order."""
+    n = be.n(c)
+    srt, rev, key, first, last = be.order_info(c) if n else (True, True, True, 0, 0)
+    parts = _gather_var(dist, be.device, [n, int(srt), int(rev), int(key), _s64(first), _s64(last)])
+    N = sum(p[0] for p in parts)
+    gs = gr = gk = True
+    prev = None
+    for p in parts:
+        if p[0] == 0:
+            continue
+        gs &= bool(p[1])
+        gr &= bool(p[2])
+        gk &= bool(p[3])
+        if prev is not None:
+            gs &= prev <= p[4]
+            gr &= prev >= p[4]
+            gk &= prev < p[4]
+        prev = p[5]
+    gk &= gs
+    pos = list(range(N)) if N <= 1000 else [i * N // 1000 for i in range(1000)]
+    mine = [q - row0 for q in pos if row0 <= q < row0 + n]
+    vals = be.values_at(c, mine) if mine else []
+    sample = [v for p in _gather_var(dist, be.device, [_s64(int(v)) for v in vals]) for v in p]
+    return dict(n=N, sorted=gs or N <= 1, revsorted=gr or N <= 1, key=gk or N <= 1, sample=sample)
+
+
+def _guess_uniques(st):
+    """guess_uniques / count_unique (gdk_join.c:3337-3576) over the sample."""
+    n = st["n"]
+    if st["key"]:
+        return float(n)
+    smp = st["sample"]
+    n2 = len(smp)
+    n1 = n2 // 2
+    if n2 <= 1:
+        c1, c2 = n1, n2
+    elif st["sorted"] and st["revsorted"]:
+        c1 = c2 = 1
+    else:
+        c1, c2 = len(set(smp[:n1])), len(set(smp))
+    A = (c2 - c1) / (n2 - n1)
+    B = c1 - n1 * A
+    return B + A * n
+
+
+def join_plan(be, dist, lkeys, rkeys, lrow0, rrow0):
+    """The algorithm single-node BATjoin takes on the whole (unsharded) sides
+    (gdk_join.c:4542-4618, no candidate lists, value columns) as (driving
+    side, matches descending): ("l", False) selectjoin / mergejoin, ("r",
+    False) their swapped forms, ("l", True) hashjoin, ("r", True) swapped
+    hashjoin; None when a side is empty."""
+    import math
+    L = _side_stats(be, dist, be.widen(lkeys), lrow0)
+    R = _side_stats(be, dist, be.widen(rkeys), rrow0)
+    if L["n"] == 0 or R["n"] == 0:
+        return None
+    if L["n"] == 1 or (L["sorted"] and L["revsorted"]):
+        return ("l", False)
+    if R["n"] == 1 or (R["sorted"] and R["revsorted"]):
+        return ("r", False)
+    lord = L["sorted"] or L["revsorted"]
+    rord = R["sorted"] or R["revsorted"]
+    if lord and rord:
+        return ("l", False)
+
+    def cost(b, other_n):          # joincost (gdk_join.c:3586-3689)
+        return other_n * 1.1 * (b["n"] / _guess_uniques(b)) + b["n"] * 2.0
+
+    lcost, rcost = cost(L, R["n"]), cost(R, L["n"])
+    swap = lcost < rcost
+    best = lcost if swap else rcost
+    if rord and L["n"] * (math.log2(R["n"]) + 1) < best:
+        return ("l", False)
+    if lord and R["n"] * (math.log2(L["n"]) + 1) < best:
+        return ("r", False)
+    return ("r", True) if swap else ("l", True)
+
+
+def dist_join(be, dist, lkeys, rkeys, lrows_per_rank, rrows_per_rank=None):
     """BATjoin(l, r) over sharded sides.  lkeys/rkeys have hseqbase = their
-    shard's first global row.  Returns this rank's (r1, r2) for the left rows
-    it owns, in the reference order (left order, matches of a left row in
-    descending right position); the concatenation over ranks is the global
-    result."""
+    shard's first global row.  Returns (r1, r2, driving): this rank's share of
+    the global result in the reference's order -- the pairs whose driving row
+    (l, or r for the swapped algorithms, `driving`) this rank owns; the
+    concatenation over ranks is the single-node BATjoin result."""
     TL, TO, _ = _types(be)
     world, rank = _world(dist)
+    if rrows_per_rank is None:
+        rrows_per_rank = lrows_per_rank
     if world == 1:
-        return be.join(lkeys, rkeys)
+        a, b = be.join(lkeys, rkeys)
+        return a, b, None
+    plan = join_plan(be, dist, lkeys, rkeys, lkeys.hseqbase, rkeys.hseqbase)
     sides = []
     for c in (lkeys, rkeys):
         w = be.widen(c)
@@ -400,19 +503,26 @@ def dist_join(be, dist, lkeys, rkeys, lrows_per_rank):
         recv, _ = _exchange(dist, be.device, packed, counts)
         sides.append(be.unpack(recv, [TL, TO]))
     (lk, lo), (rk, ro) = sides
-    # sources arrive in rank order and keep their order: lo and ro ascend
     j1, j2 = be.join(lk, rk)
     r1, r2 = be.project(j1, lo), be.project(j2, ro)
-    # back to the left row's home rank; r1 ascends, so the split is by bounds
-    cuts = be.lowerbound2(r1, None, [d * lrows_per_rank for d in range(1, world)], [0] * (world - 1))
-    edges = [0] + cuts + [be.n(r1)]
-    counts = [edges[d + 1] - edges[d] for d in range(world)]
-    recv, _ = _exchange(dist, be.device, be.pack([r1, r2]), counts)
-    a, b = be.unpack(recv, [TO, TO])
-    # owners' runs interleave in l; a stable sort on l restores the order
-    # (all matches of one left row come from one owner, already descending)
-    _, order = be.sort(a)
-    return be.project(order, a), be.project(order, b)
+    driving, desc = plan if plan is not None else ("l", False)
+    d, o = (r1, r2) if driving == "l" else (r2, r1)
+    per = lrows_per_rank if driving == "l" else rrows_per_rank
+    # to the driving row's home rank: sort by the driving oid, split by bounds
+    _, ordd = be.sort(d)
+    d, o = be.project(ordd, d), be.project(ordd, o)
+    cuts = be.lowerbound2(d, None, [k * per for k in range(1, world)], [0] * (world - 1))
+    edges = [0] + list(cuts) + [be.n(d)]
+    counts = [edges[k + 1] - edges[k] for k in range(world)]
+    recv, _ = _exchange(dist, be.device, be.pack([d, o]), counts)
+    d, o = be.unpack(recv, [TO, TO])
+    # the reference order: driving rows ascending, their matches ascending
+    # (select / merge joins) or descending (hash chains): two stable sorts
+    _, oo = be.sort(o, reverse=desc)
+    d, o = be.project(oo, d), be.project(oo, o)
+    _, od = be.sort(d)
+    d, o = be.project(od, d), be.project(od, o)
+    return (d, o, driving) if driving == "l" else (o, d, driving)
 
 
 # ---------------------------------------------------------------------------

@@ -108,6 +108,8 @@ _SIGS = {
     "mgdk_BATgroupmax": (P, [P, P, P, P, C.c_int, C.c_bool]),
     "mgdk_BATgroup": (C.c_int, [PP, PP, PP, P, P, P, P, P]),
     "mgdk_BATjoin": (C.c_int, [PP, PP, P, P, P, P, C.c_bool, C.c_uint64]),
+    "mgdk_BATordered": (C.c_bool, [P]),
+    "mgdk_BATordered_rev": (C.c_bool, [P]),
     "mgdk_BATsort": (C.c_int, [PP, PP, PP, P, P, P, C.c_bool, C.c_bool, C.c_bool]),
     "mgdk_GDKanalyticalwindowbounds": (C.c_int, [P, P, P, P, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                                  C.c_bool, C.c_uint64]),
@@ -482,6 +484,16 @@ def BATjoin(l, r, sl=None, sr=None, nil_matches=False, estimate=0):
     _chk(lib().mgdk_BATjoin(C.byref(a), C.byref(b), l.ptr, r.ptr, _p(sl), _p(sr), nil_matches,
                             estimate))
     return BAT(a), BAT(b)
+
+
+def BATordered(b):
+    """gdk_batop.c:2002: b sorted ascending (the finding is cached in b)."""
+    return bool(lib().mgdk_BATordered(b.ptr))
+
+
+def BATordered_rev(b):
+    """gdk_batop.c:2181: b sorted descending (cached in b)."""
+    return bool(lib().mgdk_BATordered_rev(b.ptr))
 
 
 def BATsort(b, o=None, g=None, reverse=False, nilslast=False, stable=True):

@@ -107,9 +107,18 @@ class OracleBackend:
         a, b = ora.BATjoin(l.ora(), r.ora())
         return _from_ora(a), _from_ora(b)
 
-    def sort(self, c):
-        s, o = ora.BATsort(c.ora())
+    def sort(self, c, reverse=False):
+        s, o = ora.BATsort(c.ora(), reverse=reverse, nilslast=reverse)
         return _from_ora(s, c.hseqbase), _from_ora(o, c.hseqbase)
+
+    def order_info(self, c):
+        a = c.arr.astype(np.int64)
+        d = np.diff(a)
+        srt, rev = bool((d >= 0).all()), bool((d <= 0).all())
+        return srt, rev, srt and bool((d > 0).all()), int(a[0]), int(a[-1])
+
+    def values_at(self, c, positions):
+        return [int(v) for v in c.arr.astype(np.int64)[np.asarray(positions, np.int64)]]
 
     def lowerbound2(self, keys, pos, qk, qp):
         k = keys.arr.astype(np.int64)

@@ -156,12 +156,20 @@ def _exchange_worker(rank, world, port, out_dir, backend="oracle"):
     # hash join, duplicates on both sides
     lk = r.integers(0, 3000, N).astype(np.int32)
     rk = r.integers(0, 3000, N).astype(np.int32)
-    a, b = D.dist_join(be, dist, Col(ora.TYPE_int, lk[lo:hi], lo), Col(ora.TYPE_int, rk[lo:hi], lo), per)
-    wa, wb = ora.BATjoin(ora.Bat.from_array(ora.TYPE_int, lk), ora.Bat.from_array(ora.TYPE_int, rk))
-    wa, wb = wa.values(), wb.values()
-    sel = (wa >= lo) & (wa < hi)
-    if not (np.array_equal(be.values(a), wa[sel]) and np.array_equal(be.values(b), wb[sel])):
-        errs.append("join mismatch")
+    # three shapes: plain hash join, swapped (small left), both sorted
+    for name, lkk, rkk in (("hash", lk, rk),
+                           ("swap", r.choice(1 << 20, world * 300, replace=False).astype(np.int32),
+                            r.integers(0, 1 << 20, N).astype(np.int32)),
+                           ("merge", np.sort(lk), np.sort(rk))):
+        lper, rper = len(lkk) // world, len(rkk) // world
+        a, b, drv = D.dist_join(be, dist, Col(ora.TYPE_int, lkk[rank * lper:(rank + 1) * lper], rank * lper),
+                                Col(ora.TYPE_int, rkk[rank * rper:(rank + 1) * rper], rank * rper), lper, rper)
+        wa, wb = ora.BATjoin(ora.Bat.from_array(ora.TYPE_int, lkk), ora.Bat.from_array(ora.TYPE_int, rkk))
+        wa, wb = wa.values(), wb.values()
+        dv, per_ = (wa, lper) if drv == "l" else (wb, rper)
+        sel = (dv >= rank * per_) & (dv < (rank + 1) * per_)
+        if not (np.array_equal(be.values(a), wa[sel]) and np.array_equal(be.values(b), wb[sel])):
+            errs.append("join mismatch " + name)
 
     # stable sort
     sk = r.integers(-50, 50, N).astype(np.int64)
