@@ -938,8 +938,13 @@ mgdk_BATgroupcount(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, b
 			out[k] = (long long) r.cnt[k];
 	}
 	mgdk_bat *bn = upload_new(ng ? a.min : 0, MGDK_lng, out.data(), ng);
-	if (bn)
+	if (bn) {
+		// gdk_aggr.c:3105-3106 (empty: BATconstant of 0), :3185-3190
 		bn->tnonil = 1;
+		bn->tnil = 0;
+		bn->tkey = ng <= 1;
+		bn->tsorted = bn->trevsorted = ng <= 1 || a.ci.n == 0;
+	}
 	return bn;
 }
 
@@ -1323,6 +1328,43 @@ mgdk_BATgroupavg3(mgdk_bat **avgp, mgdk_bat **remp, mgdk_bat **cntp, mgdk_bat *b
 	return 0;
 }
 
+// the rows holding each group's extreme value (target) and its first nil:
+// smallest candidate index of each (atomicMin, skipped when not smaller)
+__global__ __launch_bounds__(256) void
+k_gminmax_pos(const void *base, int w, oid off, const oid *gids, oid gseq, oid gmin, BUN ngrp, BUN n,
+	      bool skip_nils, const long long *target, unsigned long long *firstnil, unsigned long long *firstbest)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		const oid g = gids ? gids[i] : gseq + i;
+		if (g < gmin || g - gmin >= ngrp)
+			continue;
+		const BUN gi = g - gmin;
+		bool isnil;
+		const hge v = ldv(base, w, off + i, isnil);
+		unsigned long long *slot = isnil ? (skip_nils ? nullptr : &firstnil[gi])
+						 : ((long long) v == target[gi] ? &firstbest[gi] : nullptr);
+		if (slot && i < __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+			atomicMin(slot, (unsigned long long) i);
+	}
+}
+
+// group k's result: its first nil (no skip_nils), else its first extreme
+// row, else oid_nil; candidate index -> candidate oid
+__global__ void
+k_gminmax_out(BUN ngrp, const unsigned long long *firstnil, const unsigned long long *firstbest, bool dense,
+	      oid seq, const oid *oids, oid *out)
+{
+	for (BUN k = (BUN) blockIdx.x * blockDim.x + threadIdx.x; k < ngrp; k += (BUN) gridDim.x * blockDim.x) {
+		const unsigned long long p = firstnil[k] != ~0ull ? firstnil[k] : firstbest[k];
+		out[k] = p == ~0ull ? MGDK_OID_NIL : dense ? seq + p : oids[p];
+	}
+}
+
+// BATgroupmin / BATgroupmax (gdk/gdk_aggr.c:3487-3560, do_groupmin
+// :3247-3362): the POSITION (oid) of each group's minimum / maximum -- its
+// first row; without skip_nils the first nil of the group wins; groups
+// without a value give oid_nil.  MAL's aggr.min / aggr.max project b through
+// the result (monetdb5/modules/kernel/aggr.c:321-348).
 static mgdk_bat *
 groupminmax(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, bool skip_nils, bool domax)
 {
@@ -1331,19 +1373,71 @@ groupminmax(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, bool skip_nils, 
 		seterr("42000!BATgroupmin/max: type not supported on the device path");
 		return nullptr;
 	}
+	Cand c0;                         // the caller's candidates (positions)
+	if (cand_init(&c0, b, s) < 0)
+		return nullptr;
 	AggrInit a;
 	if (aggr_init(&a, &b, g, e, s) < 0)
 		return nullptr;
 	const BUN ng = a.ngrp;
-	GRes r;
-	if (a.ci.n && ng && run_gaggr(a, b, AGG_MINMAX | AGG_POS, false, r) < 0)
+	mgdk_bat *bn = newbat(ng ? a.min : 0, MGDK_oid, ng);
+	if (bn == nullptr)
 		return nullptr;
-	std::vector<char> out(ng * width_of(b->ttype) + 16);
-	for (BUN k = 0; k < ng; k++) {
-		bool nil = !a.ci.n || r.cnt[k] == 0 || (!skip_nils && r.lastnil[k] != 0);
-		put_vec(out, b->ttype, k, domax ? r.mx[k] : r.mn[k], nil);
+	bn->count = ng;
+	bn->tsorted = bn->trevsorted = bn->tkey = ng <= 1;
+	if (a.ci.n == 0 || ng == 0) {
+		// BATconstant(min, TYPE_oid, &oid_nil, ngrp)
+		std::vector<oid> nils(ng + 1, MGDK_OID_NIL);
+		if (ng && mgdk_BATupload(bn, nils.data(), ng) < 0) {
+			mgdk_BBPunfix(bn);
+			return nullptr;
+		}
+		bn->count = ng;
+		bn->tsorted = bn->trevsorted = 1;
+		bn->tnil = ng > 0;
+		bn->tnonil = ng == 0;
+		return bn;
 	}
-	return upload_new(ng ? a.min : 0, b->ttype, out.data(), ng);
+	GRes r;
+	if (run_gaggr(a, b, AGG_MINMAX, false, r) < 0) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	hipStream_t st = stream();
+	DevBuf tgt(ng * 8 + 8), fn(ng * 8 + 8), fb(ng * 8 + 8);
+	std::vector<long long> t(ng);
+	BUN nils = 0;
+	for (BUN k = 0; k < ng; k++)
+		t[k] = domax ? r.mx[k] : r.mn[k];
+	if (!tgt.p || !fn.p || !fb.p ||
+	    !hip_ok(hipMemcpyAsync(tgt.p, t.data(), ng * 8, hipMemcpyHostToDevice, st), "memcpy") ||
+	    !hip_ok(hipMemsetAsync(fn.p, 0xff, ng * 8, st), "memset") ||
+	    !hip_ok(hipMemsetAsync(fb.p, 0xff, ng * 8, st), "memset")) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	const oid off = a.ci.seq - b->hseqbase;
+	hipLaunchKernelGGL(k_gminmax_pos, dim3(grid_for(a.ci.n, 256 * 8, 256 * 16)), dim3(256), 0, st, b->theap,
+			   b->twidth, off, a.gids, a.gseq, a.min, ng, a.ci.n, skip_nils, tgt.as<long long>(),
+			   fn.as<unsigned long long>(), fb.as<unsigned long long>());
+	hipLaunchKernelGGL(k_gminmax_out, dim3(grid_for(ng, 256, 4096)), dim3(256), 0, st, ng,
+			   fn.as<unsigned long long>(), fb.as<unsigned long long>(), c0.dense, c0.seq, c0.oids,
+			   (oid *) bn->theap);
+	if (!sync()) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	// groups without a value: no non-nil row and (skip_nils or no nil row)
+	std::vector<unsigned long long> hn(ng);
+	if (!hip_ok(hipMemcpyAsync(hn.data(), fn.p, ng * 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	for (BUN k = 0; k < ng; k++)
+		nils += r.cnt[k] == 0 && hn[k] == ~0ull;
+	bn->tnil = nils != 0;
+	bn->tnonil = nils == 0;
+	return bn;
 }
 
 mgdk_bat *

@@ -287,7 +287,33 @@ calc(int op, mgdk_bat *b1, const void *v1, int t1, mgdk_bat *b2, const void *v2,
 	}
 	const BUN nils = h[1];
 	bn->count = n;
-	bn->tsorted = bn->trevsorted = n <= 1 || nils == n;
+	// result order (gdk_calc_addsub.c:1528-1531, 1590-1593, 1649-1652,
+	// 3208-3209, 3262-3265, 3318-3321; gdk_calc_mul.c:2068-2069, 2133-2138,
+	// 2194-2199): a constant operand keeps the BAT's order (a negative
+	// multiplier or cst - b reverses it), two sorted BATs add to a sorted
+	// result, anything else is unordered; only without nils
+	bool srt = false, rev = false;
+	if (nils == 0) {
+		if (b1 && b2) {
+			if (op == 0) {
+				srt = b1->tsorted && b2->tsorted;
+				rev = b1->trevsorted && b2->trevsorted;
+			}
+		} else {
+			int sign = 1;
+			if (op == 2) {
+				bool cn;
+				const hge c = cst_value(b1 ? v2 : v1, b1 ? t2 : t1, cn);
+				sign = c > 0 ? 1 : c < 0 ? -1 : 0;
+			} else if (op == 1 && !b1) {
+				sign = -1;
+			}
+			srt = (sign >= 0 && bb->tsorted) || (sign <= 0 && bb->trevsorted);
+			rev = (sign >= 0 && bb->trevsorted) || (sign <= 0 && bb->tsorted);
+		}
+	}
+	bn->tsorted = srt || n <= 1 || nils == n;
+	bn->trevsorted = rev || n <= 1 || nils == n;
 	bn->tkey = n <= 1;
 	bn->tnil = nils != 0;
 	bn->tnonil = nils == 0;

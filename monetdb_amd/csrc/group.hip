@@ -434,6 +434,9 @@ group_lds(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mg
 	hn->tkey = ngrp == 1;
 	hn->tsorted = hn->trevsorted = ngrp == n || ngrp == 1;
 	hn->tnonil = 1;
+	// tmaxpos: the row that started the last group (maxgrppos,
+	// gdk_group.c:99,1313)
+	gn->tmaxpos = ngrp > 0 ? cand_index(ci, fl[1]) : MGDK_BUN_NONE;
 	if (ngrp > 0 && fl[1] - fl[0] == ngrp - 1)
 		setdense(en, fl[0], ngrp);
 	*gnp = gn;
@@ -496,6 +499,7 @@ mgdk_BATgroup(mgdk_bat **groups, mgdk_bat **extents, mgdk_bat **histo, mgdk_bat 
 		return -1;
 	}
 	mgdk_bat *gn = nullptr, *en = nullptr, *hn = nullptr;
+	bool grouped = false;   // the general path ran (it sets the estimates)
 	// trivial: one element per group (gdk_group.c:712-767)
 	if (b->tkey || n <= 1 || (g && (g->tkey || g->ttype == MGDK_void))) {
 		gn = mgdk_BATdense(hseqb, 0, b->count);
@@ -507,7 +511,8 @@ mgdk_BATgroup(mgdk_bat **groups, mgdk_bat **extents, mgdk_bat **histo, mgdk_bat 
 		goto done;
 	}
 	// all values equal and no (or a constant) prior grouping: one group
-	if (b->tsorted && b->trevsorted && (!g || (g->tsorted && g->trevsorted))) {
+	// (gdk_group.c:768-770 evaluates BATordered / BATordered_rev on g)
+	if (b->tsorted && b->trevsorted && (!g || (mgdk_BATordered(g) && mgdk_BATordered_rev(g)))) {
 		oid zero = 0;
 		gn = mgdk_BATconstant(hseqb, MGDK_oid, &zero, n);
 		en = mgdk_BATdense(0, ci.first, 1);
@@ -519,6 +524,7 @@ mgdk_BATgroup(mgdk_bat **groups, mgdk_bat **extents, mgdk_bat **histo, mgdk_bat 
 		gn->tkey = n <= 1;
 		goto done;
 	}
+	grouped = true;
 	{
 		KeySrc ks{};
 		ks.base = b->theap;
@@ -534,7 +540,17 @@ mgdk_BATgroup(mgdk_bat **groups, mgdk_bat **extents, mgdk_bat **histo, mgdk_bat 
 		hipStream_t st = stream();
 		// prior group range for the direct table
 		uint64_t gmax = 0;
-		if (ks.g) {
+		oid gm = MGDK_OID_NIL;
+		// the largest prior group id without a scan when g says where it is
+		// (gdk_group.c:745-757: last / first row of an ordered g, tmaxpos)
+		if (ks.g && (g->tsorted || g->trevsorted || g->tmaxpos != MGDK_BUN_NONE)) {
+			const BUN p = g->tsorted ? n - 1 : g->trevsorted ? 0 : g->tmaxpos;
+			if (oid_at(g, p, &gm) < 0)
+				return -1;
+		}
+		if (ks.g && gm != MGDK_OID_NIL) {
+			gmax = gm;
+		} else if (ks.g) {
 			unsigned long long *m = (unsigned long long *) meta_buf();
 			if (!hip_ok(hipMemsetAsync(m, 0, 8, st), "memset"))
 				return -1;
@@ -640,16 +656,25 @@ mgdk_BATgroup(mgdk_bat **groups, mgdk_bat **extents, mgdk_bat **histo, mgdk_bat 
 		hn->tkey = ngrp == 1;
 		hn->tsorted = hn->trevsorted = hs;
 		hn->tnonil = 1;
-		// virtualize extents when dense
+		// tmaxpos (gdk_group.c:99,1313), extents virtualised when dense
 		if (ngrp > 0) {
 			oid fl[2];
-			if (hip_ok(hipMemcpy(&fl[0], en->theap, 8, hipMemcpyDeviceToHost), "memcpy") &&
-			    hip_ok(hipMemcpy(&fl[1], (oid *) en->theap + ngrp - 1, 8, hipMemcpyDeviceToHost), "memcpy") &&
-			    fl[1] - fl[0] == ngrp - 1)
+			if (oid_at(en, 0, &fl[0]) < 0 || oid_at(en, ngrp - 1, &fl[1]) < 0)
+				goto fail;
+			gn->tmaxpos = cand_index(ci, fl[1]);
+			if (fl[1] - fl[0] == ngrp - 1)
 				setdense(en, fl[0], ngrp);
 		}
 	}
 done:
+	if (grouped && en) {
+		// BATgroup's estimates (gdk_group.c:1291,1314-1318)
+		const BUN ngrp = en->count;
+		gn->tunique_est = (double) ngrp;
+		en->tunique_est = (double) ngrp;
+		if (!g && !e && !s)
+			b->tunique_est = (double) ngrp;
+	}
 	*groups = gn;
 	if (extents)
 		*extents = en;

@@ -78,6 +78,10 @@ struct Cand {
 };
 // canditer_init (gdk/gdk_cand.c:407): clip s to b's [hseqbase, hseqbase+count)
 int cand_init(Cand *ci, const mgdk_bat *b, const mgdk_bat *s);
+// index of candidate oid o in ci (canditer_search); BUN NONE-like ~0 on error
+BUN cand_index(const Cand &ci, oid o);
+// one oid of an oid / void column (host read)
+int oid_at(const mgdk_bat *b, BUN p, oid *v);
 
 // a cand_except / cand_mask list (void BAT + ccand_t vheap) as a new ordered
 // oid list (BATunmask, gdk_cand.c); the caller owns the result

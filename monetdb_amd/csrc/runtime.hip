@@ -453,6 +453,48 @@ unmask_cand(const mgdk_bat *s)
 	return compact_flags(f.as<int8_t>(), R, seq);
 }
 
+__global__ void
+k_cand_search(const oid *oids, BUN n, oid o, unsigned long long *out)
+{
+	BUN lo = 0, hi = n;
+	while (lo < hi) {
+		const BUN m = (lo + hi) >> 1;
+		if (oids[m] < o)
+			lo = m + 1;
+		else
+			hi = m;
+	}
+	*out = lo;
+}
+
+BUN
+cand_index(const Cand &ci, oid o)
+{
+	if (ci.dense)
+		return o - ci.seq;
+	unsigned long long *m = (unsigned long long *) meta_buf();
+	unsigned long long *h = (unsigned long long *) pinned(64);
+	hipLaunchKernelGGL(k_cand_search, dim3(1), dim3(1), 0, stream(), ci.oids, ci.n, o, m);
+	if (!hip_ok(hipMemcpyAsync(h, m, 8, hipMemcpyDeviceToHost, stream()), "memcpy") || !sync())
+		return ~(BUN) 0;
+	return h[0];
+}
+
+int
+oid_at(const mgdk_bat *b, BUN p, oid *v)
+{
+	if (b->ttype == MGDK_void) {
+		*v = b->tseqbase == MGDK_OID_NIL ? MGDK_OID_NIL : b->tseqbase + p;
+		return 0;
+	}
+	oid *h = (oid *) pinned(64);
+	if (!hip_ok(hipMemcpyAsync(h, (const oid *) b->theap + p, 8, hipMemcpyDeviceToHost, stream()), "memcpy") ||
+	    !sync())
+		return -1;
+	*v = h[0];
+	return 0;
+}
+
 int
 cand_init(Cand *ci, const mgdk_bat *b, const mgdk_bat *s)
 {

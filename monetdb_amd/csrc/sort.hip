@@ -920,7 +920,7 @@ mgdk_BATsort(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b
 			on->count = n;
 			on->tkey = 1;
 			on->tnonil = 1;
-			on->tsorted = on->trevsorted = n <= 1;
+			on->tsorted = on->trevsorted = 0;   // gdk_batop.c:2622-2624
 		}
 		goto done;
 	}
@@ -972,7 +972,7 @@ mgdk_BATsort(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b
 			on->count = n;
 			on->tkey = 1;
 			on->tnonil = 1;
-			on->tsorted = on->trevsorted = n <= 1;
+			on->tsorted = on->trevsorted = 0;   // gdk_batop.c:2622-2624
 		}
 	}
 done:

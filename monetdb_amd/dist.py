@@ -191,7 +191,8 @@ class GdkBackend:
         return self.gdk.BATgroupsum(c, g, e, tp)
 
     def groupmin(self, c, g, e):
-        return self.gdk.BATgroupmin(c, g, e)
+        # MAL aggr.min: the positions of BATgroupmin projected (aggr.c:321-333)
+        return self.gdk.BATproject(self.gdk.BATgroupmin(c, g, e), c)
 
     def groupavg3(self, c, g, e):
         return self.gdk.BATgroupavg3(c, g, e, True)

@@ -55,6 +55,7 @@ ora_new(int type, uint64_t count, ora_oid hseq)
 	b->count = count;
 	b->hseqbase = hseq;
 	b->tseqbase = type == ORA_void ? 0 : ORA_OID_NIL;
+	b->minpos = b->maxpos = ORA_BUN_NONE;
 	b->owned = 1;
 	if (b->width > 0) {
 		b->base = malloc(count * b->width + 16);
@@ -773,7 +774,34 @@ ora_calc(char op, const ora_bat *b1, const void *c1, int t1,
 	}
 	bn->nil = nils != 0;
 	bn->nonil = nils == 0;
-	bn->sorted = bn->revsorted = ci1.n <= 1 || nils == ci1.n;
+	/* result order (gdk_calc_addsub.c:1528-1531, 1590-1593, 1649-1652,
+	 * 3208-3209, 3262-3265, 3318-3321; gdk_calc_mul.c:2068-2069,
+	 * 2133-2138, 2194-2199): a constant operand keeps the BAT's order (a
+	 * negative multiplier or cst - b reverses it), two sorted BATs add to a
+	 * sorted result, anything else is unordered; only without nils */
+	bool srt = false, rev = false;
+	if (nils == 0) {
+		if (b1 && b2) {
+			if (op == '+') {
+				srt = b1->sorted && b2->sorted;
+				rev = b1->revsorted && b2->revsorted;
+			}
+		} else {
+			const ora_bat *b = b1 ? b1 : b2;
+			int sign = 1;
+			if (op == '*') {
+				ora_hge c;
+				get_hge(b1 ? t2 : t1, b1 ? c2 : c1, &c);
+				sign = c > 0 ? 1 : c < 0 ? -1 : 0;
+			} else if (op == '-' && !b1) {
+				sign = -1;
+			}
+			srt = (sign >= 0 && b->sorted) || (sign <= 0 && b->revsorted);
+			rev = (sign >= 0 && b->revsorted) || (sign <= 0 && b->sorted);
+		}
+	}
+	bn->sorted = srt || ci1.n <= 1 || nils == ci1.n;
+	bn->revsorted = rev || ci1.n <= 1 || nils == ci1.n;
 	bn->key = ci1.n <= 1;
 	return bn;
 }

@@ -65,7 +65,10 @@ typedef struct ora_bat {
 	uint8_t sorted, revsorted, key, nonil, nil, owned;
 	uint8_t _pad[2];
 	double unique_est;   /* tunique_est (gdk/gdk.h:740): 0 = unknown */
+	uint64_t minpos, maxpos;   /* tminpos / tmaxpos: ORA_BUN_NONE = unknown */
 } ora_bat;
+
+#define ORA_BUN_NONE ((uint64_t) INT64_MAX)
 
 /* memory */
 ora_bat *ora_new(int type, uint64_t count, ora_oid hseq);
@@ -85,7 +88,7 @@ ora_bat *ora_calc(char op, const ora_bat *b1, const void *c1, int t1,
 int ora_sum(void *res, int tp, const ora_bat *b, const ora_bat *s,
 	    bool skip_nils, bool nil_if_empty);
 int ora_group(ora_bat **groups, ora_bat **extents, ora_bat **histo,
-	      const ora_bat *b, const ora_bat *s, const ora_bat *g);
+	      ora_bat *b, const ora_bat *s, const ora_bat *g);
 ora_bat *ora_groupsum(const ora_bat *b, const ora_bat *g, const ora_bat *e,
 		      const ora_bat *s, int tp, bool skip_nils);
 ora_bat *ora_groupcount(const ora_bat *b, const ora_bat *g, const ora_bat *e,

@@ -104,9 +104,28 @@ ghash(ora_hge k, ora_oid g)
 	return x ^ (x >> 29);
 }
 
+static ora_bat *
+ora_constant(ora_oid hseq, int type, int64_t v, uint64_t n)
+{
+	/* BATconstant (gdk/gdk_batop.c:2832-2922) of an oid / lng value */
+	ora_bat *bn = ora_new(type, n, hseq);
+	if (bn == NULL)
+		return NULL;
+	for (uint64_t i = 0; i < n; i++)
+		((int64_t *) bn->base)[i] = v;
+	bn->sorted = bn->revsorted = 1;
+	bn->nil = 0;
+	bn->nonil = 1;
+	bn->key = n <= 1;
+	return bn;
+}
+
+/* BATgroup (gdk/gdk_group.c:657-1344): the one-element-per-group and
+ * single-group shortcuts (:712-800), else first-occurrence group ids with
+ * the result properties of :1284-1318 */
 int
 ora_group(ora_bat **groups, ora_bat **extents, ora_bat **histo,
-	  const ora_bat *b, const ora_bat *s, const ora_bat *g)
+	  ora_bat *b, const ora_bat *s, const ora_bat *g)
 {
 	ora_ci ci;
 	if (ora_ci_init(&ci, b, s) < 0)
@@ -115,12 +134,48 @@ ora_group(ora_bat **groups, ora_bat **extents, ora_bat **histo,
 		ora_seterr("b with s and g must be aligned");
 		return -1;
 	}
-	ora_oid hseqb = ci.n ? ci.seq : 0;
-	if (!ci.dense && ci.n)
-		hseqb = ci.oids[0];
-	ora_bat *gn = ora_new(ORA_oid, ci.n, hseqb);
-	ora_bat *en = ora_new(ORA_oid, ci.n, 0);
-	ora_bat *hn = ora_new(ORA_lng, ci.n, 0);
+	ora_oid hseqb = ci.n ? ci_get(&ci, 0) : 0;
+	ora_bat *gn, *en, *hn;
+	const bool gdense = g && (g->type == ORA_void || g->tseqbase != ORA_OID_NIL);
+	if (b->key || ci.n <= 1 || (g && (g->key || gdense))) {
+		/* trivial: one element per group; note the groups BAT has
+		 * BATcount(b) rows, as in the reference (:713) */
+		gn = ora_dense(hseqb, 0, b->count);
+		if (ci.dense || ci.n <= 1) {
+			en = ora_dense(0, ci.n ? ci_get(&ci, 0) : 0, ci.n);
+		} else {
+			en = ora_new(ORA_oid, ci.n, 0);
+			if (en) {
+				memcpy(en->base, ci.oids, ci.n * 8);
+				en->sorted = en->key = en->nonil = 1;
+				en->revsorted = ci.n <= 1;
+				en->minpos = 0;
+				en->maxpos = ci.n - 1;
+			}
+		}
+		hn = ora_constant(0, ORA_lng, 1, ci.n);
+		goto out;
+	}
+	bool gsame = !g;
+	if (g) {
+		bool asc = false, desc = false;
+		for (uint64_t i = 1; i < g->count; i++) {
+			ora_oid x = ((const ora_oid *) g->base)[i - 1], y = ((const ora_oid *) g->base)[i];
+			asc |= x < y;
+			desc |= x > y;
+		}
+		gsame = !asc && !desc;
+	}
+	if (b->sorted && b->revsorted && gsame) {
+		/* all values equal, one prior group: a single group 0 */
+		gn = ora_constant(hseqb, ORA_oid, 0, ci.n);
+		en = ora_dense(0, ci_get(&ci, 0), 1);
+		hn = ora_constant(0, ORA_lng, (int64_t) ci.n, 1);
+		goto out;
+	}
+	gn = ora_new(ORA_oid, ci.n, hseqb);
+	en = ora_new(ORA_oid, ci.n, 0);
+	hn = ora_new(ORA_lng, ci.n, 0);
 	uint64_t cap = 16;
 	while (cap < 2 * ci.n)
 		cap <<= 1;
@@ -132,7 +187,7 @@ ora_group(ora_bat **groups, ora_bat **extents, ora_bat **histo,
 	}
 	ora_oid *gids = gn->base, *ext = en->base;
 	int64_t *cnt = hn->base;
-	uint64_t ngrp = 0;
+	uint64_t ngrp = 0, maxgrppos = ORA_BUN_NONE;
 	for (uint64_t i = 0; i < ci.n; i++) {
 		ora_oid o = ci_get(&ci, i);
 		ora_hge v;
@@ -151,6 +206,7 @@ ora_group(ora_bat **groups, ora_bat **extents, ora_bat **histo,
 			ext[ngrp] = o;
 			cnt[ngrp] = 0;
 			ngrp++;
+			maxgrppos = i;
 		}
 		gids[i] = tab[h].gid;
 		cnt[tab[h].gid]++;
@@ -158,14 +214,44 @@ ora_group(ora_bat **groups, ora_bat **extents, ora_bat **histo,
 	free(tab);
 	en->count = hn->count = ngrp;
 	gn->nonil = 1;
+	gn->nil = 0;
 	gn->key = ngrp == ci.n;
 	gn->revsorted = ngrp == 1 || ci.n <= 1;
 	bool srt = true;
 	for (uint64_t i = 1; i < ci.n && srt; i++)
 		srt = gids[i - 1] <= gids[i];
 	gn->sorted = srt;
+	gn->maxpos = maxgrppos;
+	gn->unique_est = (double) ngrp;
 	en->sorted = en->key = en->nonil = 1;
+	en->nil = 0;
+	en->revsorted = ngrp == 1;
+	en->unique_est = (double) ngrp;
+	if (ngrp <= 1 || ext[ngrp - 1] - ext[0] == ngrp - 1) {
+		/* virtualize */
+		ora_oid seq = ngrp ? ext[0] : 0;
+		free(en->base);
+		en->base = NULL;
+		en->type = ORA_void;
+		en->width = 0;
+		en->tseqbase = seq;
+	}
+	if (ngrp == ci.n || ngrp == 1) {
+		hn->key = ngrp == 1;
+		hn->sorted = hn->revsorted = 1;
+	} else {
+		hn->key = hn->sorted = hn->revsorted = 0;
+	}
 	hn->nonil = 1;
+	hn->nil = 0;
+	if (!g && !s)
+		b->unique_est = (double) ngrp;
+out:
+	if (!gn || !en || !hn) {
+		ora_free(gn); ora_free(en); ora_free(hn);
+		ora_seterr("out of memory");
+		return -1;
+	}
 	*groups = gn;
 	if (extents)
 		*extents = en;
@@ -405,7 +491,11 @@ ora_groupcount(const ora_bat *b, const ora_bat *g, const ora_bat *e,
 			continue;
 		c[gid]++;
 	}
+	/* gdk_aggr.c:3105-3106 (empty: BATconstant of 0), :3185-3190 */
 	bn->nonil = 1;
+	bn->nil = 0;
+	bn->key = a.ngrp <= 1;
+	bn->sorted = bn->revsorted = a.ngrp <= 1 || a.ci.n == 0;
 	return bn;
 }
 
@@ -729,8 +819,12 @@ ora_groupavg(ora_bat **bnp, ora_bat **cntp, const ora_bat *b, const ora_bat *g,
 	return 0;
 }
 
-/* BATgroupmin/max value variant (gdk/gdk_aggr.c:3487-3844): nil for empty
- * groups; nils skipped when skip_nils. */
+/* BATgroupmin / BATgroupmax (gdk/gdk_aggr.c:3487-3560, do_groupmin
+ * :3247-3362, AGGR_CMP :3207-3240): the POSITION (oid) of each group's
+ * minimum / maximum -- the first row holding it; without skip_nils the
+ * first nil of the group wins; groups without a value give oid_nil.  MAL's
+ * aggr.min / aggr.max project b through it (monetdb5/modules/kernel/aggr.c:
+ * 321-348). */
 ora_bat *
 ora_groupminmax(const ora_bat *b, const ora_bat *g, const ora_bat *e,
 		const ora_bat *s, bool skip_nils, bool domax)
@@ -738,34 +832,45 @@ ora_groupminmax(const ora_bat *b, const ora_bat *g, const ora_bat *e,
 	aggr_ctx a;
 	if (aggr_init(&a, b, g, e, s) < 0)
 		return NULL;
-	int tp = b->type == ORA_date ? ORA_int : b->type;
-	ora_bat *bn = ora_new(b->type, a.ngrp, a.ngrp ? a.min : 0);
+	ora_bat *bn = ora_new(ORA_oid, a.ngrp, a.ngrp ? a.min : 0);
 	ora_hge *best = calloc(a.ngrp + 1, sizeof(ora_hge));
-	uint8_t *st = calloc(a.ngrp + 1, 1);
-	if (!bn || !best || !st) {
-		ora_free(bn); free(best); free(st);
+	uint8_t *isn = calloc(a.ngrp + 1, 1);
+	if (!bn || !best || !isn) {
+		ora_free(bn); free(best); free(isn);
 		return NULL;
 	}
+	ora_oid *oids = bn->base;
+	for (uint64_t k = 0; k < a.ngrp; k++)
+		oids[k] = ORA_OID_NIL;
 	for (uint64_t i = 0; i < a.ci.n; i++) {
 		ora_oid gid;
 		if (!aggr_gid(&a, i, &gid))
 			continue;
+		ora_oid o = ci_get(&a.ci, i);
 		ora_hge v;
-		if (val_at(b, ci_get(&a.ci, i) - b->hseqbase, &v)) {
-			if (!skip_nils)
-				st[gid] = 2;
+		bool vn = val_at(b, o - b->hseqbase, &v);
+		if (skip_nils && vn)
 			continue;
-		}
-		if (st[gid] == 2)
-			continue;
-		if (st[gid] == 0 || (domax ? v > best[gid] : v < best[gid]))
+		if (oids[gid] == ORA_OID_NIL) {
+			oids[gid] = o;
 			best[gid] = v;
-		st[gid] = 1;
+			isn[gid] = vn;
+		} else if (!isn[gid] && (vn || (domax ? v > best[gid] : v < best[gid]))) {
+			oids[gid] = o;
+			best[gid] = v;
+			isn[gid] = vn;
+		}
 	}
+	uint64_t nils = 0;
 	for (uint64_t k = 0; k < a.ngrp; k++)
-		put(tp, bn->base, k, best[k], st[k] != 1);
+		nils += oids[k] == ORA_OID_NIL;
+	bn->sorted = bn->revsorted = bn->key = a.ngrp <= 1;
+	if (a.ci.n == 0)          /* BATconstant(..., oid_nil, ngrp) */
+		bn->sorted = bn->revsorted = 1;
+	bn->nil = nils != 0;
+	bn->nonil = nils == 0;
 	free(best);
-	free(st);
+	free(isn);
 	return bn;
 }
 
@@ -817,8 +922,16 @@ ora_sort(ora_bat **sorted, ora_bat **order, const ora_bat *b,
 		((ora_oid *) on->base)[i] = b->hseqbase + k[i].i;
 	}
 	free(k);
+	/* sorted: a copy of b (COLcopy keeps key / nil / nonil) flagged
+	 * (rev)sorted; order: key, no nils, flagged unordered
+	 * (gdk_batop.c:2610-2630, 2749-2750) */
 	sn->sorted = !reverse;
 	sn->revsorted = reverse;
+	sn->key = b->key;
+	sn->nil = b->nil;
+	sn->nonil = b->nonil;
+	on->key = on->nonil = 1;
+	on->nil = on->sorted = on->revsorted = 0;
 	*sorted = sn;
 	if (order)
 		*order = on;

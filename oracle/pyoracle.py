@@ -32,7 +32,8 @@ class OraBat(C.Structure):
                 ("vheap", C.c_void_p), ("vheapsize", C.c_uint64),
                 ("sorted", C.c_uint8), ("revsorted", C.c_uint8), ("key", C.c_uint8),
                 ("nonil", C.c_uint8), ("nil", C.c_uint8), ("owned", C.c_uint8),
-                ("_pad", C.c_uint8 * 2), ("unique_est", C.c_double)]
+                ("_pad", C.c_uint8 * 2), ("unique_est", C.c_double),
+                ("minpos", C.c_uint64), ("maxpos", C.c_uint64)]
 
 
 class OraLineitem(C.Structure):
@@ -148,6 +149,7 @@ class Bat:
         b.hseqbase = hseqbase
         b.tseqbase = tseqbase
         b.unique_est = unique_est
+        b.minpos = b.maxpos = (1 << 63) - 1
         b.base = a.ctypes.data if n else a.ctypes.data
         keep = [a, b]
         if vheap is not None:
@@ -166,6 +168,8 @@ class Bat:
         b.hseqbase = hseqbase
         b.tseqbase = tseq
         b.sorted = b.key = b.nonil = 1
+        b.revsorted = n <= 1
+        b.minpos = b.maxpos = (1 << 63) - 1
         return cls(C.pointer(b), [b])
 
     @property

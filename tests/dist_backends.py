@@ -94,7 +94,8 @@ class OracleBackend:
         return _from_ora(ora.BATgroupsum(c.ora(), g.ora(), e.ora(), tp))
 
     def groupmin(self, c, g, e):
-        return _from_ora(ora.BATgroupminmax(c.ora(), g.ora(), e.ora(), False))
+        co = c.ora()
+        return _from_ora(ora.BATproject(ora.BATgroupminmax(co, g.ora(), e.ora(), False), co))
 
     def groupavg3(self, c, g, e):
         a, r, k = ora.BATgroupavg3(c.ora(), g.ora(), e.ora(), True)
