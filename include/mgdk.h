@@ -120,6 +120,54 @@ mgdk_bat *mgdk_BATcalccstadd(const void *v, int vt, mgdk_bat *b, mgdk_bat *s, in
 mgdk_bat *mgdk_BATcalccstsub(const void *v, int vt, mgdk_bat *b, mgdk_bat *s, int tp);
 mgdk_bat *mgdk_BATcalccstmul(const void *v, int vt, mgdk_bat *b, mgdk_bat *s, int tp);
 
+/* comparisons (gdk/gdk_calc.h:66-84; gdk/gdk_calc_compare.h:827-964): bit
+ * results (bte for cmp: -1/0/1), nil unless nil_matches (eq / ne) */
+mgdk_bat *mgdk_BATcalclt(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2);
+mgdk_bat *mgdk_BATcalcltcst(mgdk_bat *b, const void *v, int vt, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalccstlt(const void *v, int vt, mgdk_bat *b, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalcle(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2);
+mgdk_bat *mgdk_BATcalclecst(mgdk_bat *b, const void *v, int vt, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalccstle(const void *v, int vt, mgdk_bat *b, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalcgt(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2);
+mgdk_bat *mgdk_BATcalcgtcst(mgdk_bat *b, const void *v, int vt, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalccstgt(const void *v, int vt, mgdk_bat *b, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalcge(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2);
+mgdk_bat *mgdk_BATcalcgecst(mgdk_bat *b, const void *v, int vt, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalccstge(const void *v, int vt, mgdk_bat *b, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalceq(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2, bool nil_matches);
+mgdk_bat *mgdk_BATcalceqcst(mgdk_bat *b, const void *v, int vt, mgdk_bat *s, bool nil_matches);
+mgdk_bat *mgdk_BATcalccsteq(const void *v, int vt, mgdk_bat *b, mgdk_bat *s, bool nil_matches);
+mgdk_bat *mgdk_BATcalcne(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2, bool nil_matches);
+mgdk_bat *mgdk_BATcalcnecst(mgdk_bat *b, const void *v, int vt, mgdk_bat *s, bool nil_matches);
+mgdk_bat *mgdk_BATcalccstne(const void *v, int vt, mgdk_bat *b, mgdk_bat *s, bool nil_matches);
+mgdk_bat *mgdk_BATcalccmp(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2);
+mgdk_bat *mgdk_BATcalccmpcst(mgdk_bat *b, const void *v, int vt, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalccstcmp(const void *v, int vt, mgdk_bat *b, mgdk_bat *s);
+/* the same, op 0..6 = lt le gt ge eq ne cmp; b1 / b2 NULL take v1 / v2 */
+mgdk_bat *mgdk_BATcalccmp_op(int op, mgdk_bat *b1, const void *v1, int t1, mgdk_bat *b2, const void *v2,
+			     int t2, mgdk_bat *s1, mgdk_bat *s2, bool nil_matches);
+/* between (gdk/gdk_calc.h:85-88; gdk/gdk_calc.c:3968-4206); constants of type vt */
+mgdk_bat *mgdk_BATcalcbetween(mgdk_bat *b, mgdk_bat *lo, mgdk_bat *hi, mgdk_bat *s, mgdk_bat *slo, mgdk_bat *shi,
+			      bool symmetric, bool linc, bool hinc, bool nils_false, bool anti);
+mgdk_bat *mgdk_BATcalcbetweencstcst(mgdk_bat *b, const void *lo, const void *hi, int vt, mgdk_bat *s,
+				    bool symmetric, bool linc, bool hinc, bool nils_false, bool anti);
+mgdk_bat *mgdk_BATcalcbetweenbatcst(mgdk_bat *b, mgdk_bat *lo, const void *hi, int vt, mgdk_bat *s, mgdk_bat *slo,
+				    bool symmetric, bool linc, bool hinc, bool nils_false, bool anti);
+mgdk_bat *mgdk_BATcalcbetweencstbat(mgdk_bat *b, const void *lo, mgdk_bat *hi, int vt, mgdk_bat *s, mgdk_bat *shi,
+				    bool symmetric, bool linc, bool hinc, bool nils_false, bool anti);
+/* BATconvert (gdk/gdk_calc.h:118; gdk_calc_convert.c:1415): numeric, bit and
+ * oid types, DECIMAL rescaling (scale1 -> scale2) with the precision check */
+mgdk_bat *mgdk_BATconvert(mgdk_bat *b, mgdk_bat *s, int tp, uint8_t scale1, uint8_t scale2, uint8_t precision);
+/* BATcalcnot (gdk/gdk_calc.h:23; gdk_calc.c:41) */
+mgdk_bat *mgdk_BATcalcnot(mgdk_bat *b, mgdk_bat *s);
+/* division / modulo (gdk/gdk_calc.h:45-50; gdk_calc_div.c:1945, gdk_calc_mod.c:1179) */
+mgdk_bat *mgdk_BATcalcdiv(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2, int tp);
+mgdk_bat *mgdk_BATcalcdivcst(mgdk_bat *b, const void *v, int vt, mgdk_bat *s, int tp);
+mgdk_bat *mgdk_BATcalccstdiv(const void *v, int vt, mgdk_bat *b, mgdk_bat *s, int tp);
+mgdk_bat *mgdk_BATcalcmod(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2, int tp);
+mgdk_bat *mgdk_BATcalcmodcst(mgdk_bat *b, const void *v, int vt, mgdk_bat *s, int tp);
+mgdk_bat *mgdk_BATcalccstmod(const void *v, int vt, mgdk_bat *b, mgdk_bat *s, int tp);
+
 /* ---- aggregates (gdk/gdk_calc.h:127-147; gdk/gdk_aggr.c:900,1018,1996,3069,
  *      3487-3844) --------------------------------------------------------- */
 int mgdk_BATsum(void *res, int tp, mgdk_bat *b, mgdk_bat *s, bool skip_nils, bool nil_if_empty);

@@ -709,6 +709,28 @@ mgdk_BATconstant(mgdk_oid hseq, int tt, const void *val, mgdk_BUN cnt)
 	b->count = cnt;
 	b->tsorted = b->trevsorted = 1;
 	b->tkey = cnt <= 1;
+	// gdk_batop.c:2916-2920: tnil when the value is the type's nil
+	bool isnil = false;
+	if (val != nullptr && w > 0) {
+		const int bt = basetype(tt);
+		if (bt == MGDK_flt) {
+			float f;
+			memcpy(&f, val, 4);
+			isnil = f != f;
+		} else if (bt == MGDK_dbl) {
+			double d;
+			memcpy(&d, val, 8);
+			isnil = d != d;
+		} else if (bt != MGDK_str) {
+			unsigned char buf[16];
+			memcpy(buf, val, w);
+			isnil = buf[w - 1] == 0x80;   // little endian: the minimum has only the top bit set
+			for (int k = 0; k < w - 1 && isnil; k++)
+				isnil = buf[k] == 0;
+		}
+	}
+	b->tnil = cnt >= 1 && isnil;
+	b->tnonil = !b->tnil;
 	return b;
 }
 

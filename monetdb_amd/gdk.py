@@ -98,6 +98,19 @@ _SIGS = {
     "mgdk_BATcalccstadd": (P, [C.c_void_p, C.c_int, P, P, C.c_int]),
     "mgdk_BATcalccstsub": (P, [C.c_void_p, C.c_int, P, P, C.c_int]),
     "mgdk_BATcalccstmul": (P, [C.c_void_p, C.c_int, P, P, C.c_int]),
+    "mgdk_BATcalccmp_op": (P, [C.c_int, P, C.c_void_p, C.c_int, P, C.c_void_p, C.c_int, P, P, C.c_bool]),
+    "mgdk_BATcalcbetween": (P, [P, P, P, P, P, P] + [C.c_bool] * 5),
+    "mgdk_BATcalcbetweencstcst": (P, [P, C.c_void_p, C.c_void_p, C.c_int, P] + [C.c_bool] * 5),
+    "mgdk_BATcalcbetweenbatcst": (P, [P, P, C.c_void_p, C.c_int, P, P] + [C.c_bool] * 5),
+    "mgdk_BATcalcbetweencstbat": (P, [P, C.c_void_p, P, C.c_int, P, P] + [C.c_bool] * 5),
+    "mgdk_BATconvert": (P, [P, P, C.c_int, C.c_uint8, C.c_uint8, C.c_uint8]),
+    "mgdk_BATcalcnot": (P, [P, P]),
+    "mgdk_BATcalcdiv": (P, [P, P, P, P, C.c_int]),
+    "mgdk_BATcalcdivcst": (P, [P, C.c_void_p, C.c_int, P, C.c_int]),
+    "mgdk_BATcalccstdiv": (P, [C.c_void_p, C.c_int, P, P, C.c_int]),
+    "mgdk_BATcalcmod": (P, [P, P, P, P, C.c_int]),
+    "mgdk_BATcalcmodcst": (P, [P, C.c_void_p, C.c_int, P, C.c_int]),
+    "mgdk_BATcalccstmod": (P, [C.c_void_p, C.c_int, P, P, C.c_int]),
     "mgdk_BATsum": (C.c_int, [C.c_void_p, C.c_int, P, P, C.c_bool, C.c_bool]),
     "mgdk_BATgroupsum": (P, [P, P, P, P, C.c_int, C.c_bool]),
     "mgdk_BATgroupcount": (P, [P, P, P, P, C.c_int, C.c_bool]),
@@ -388,6 +401,55 @@ def BATcalcsub(b1, b2, tp, s1=None, s2=None):
 
 def BATcalcmul(b1, b2, tp, s1=None, s2=None):
     return BAT(lib().mgdk_BATcalcmul(b1.ptr, b2.ptr, _p(s1), _p(s2), tp))
+
+
+CMP_OPS = {"<": 0, "<=": 1, ">": 2, ">=": 3, "==": 4, "!=": 5, "cmp": 6}
+
+
+def BATcalccmp(op, b1, b2, s1=None, s2=None, c1=None, t1=0, c2=None, t2=0, nil_matches=False):
+    """BATcalc{lt,le,gt,ge,eq,ne,cmp} and their cst forms (gdk/gdk_calc.h:66-84):
+    op in CMP_OPS; b1 / b2 None takes the constant c1 / c2 of type t1 / t2."""
+    keep = []
+    return BAT(lib().mgdk_BATcalccmp_op(CMP_OPS[op], _p(b1), _valptr(t1, c1, keep), t1, _p(b2),
+                                        _valptr(t2, c2, keep), t2, _p(s1), _p(s2), nil_matches))
+
+
+def BATcalcbetween(b, lo, hi, s=None, slo=None, shi=None, clo=None, chi=None, ct=0, symmetric=False,
+                   linc=True, hinc=True, nils_false=False, anti=False):
+    """BATcalcbetween / -cstcst / -batcst / -cstbat (gdk/gdk_calc.c:3968-4206);
+    lo / hi None take the constants clo / chi of type ct."""
+    keep = []
+    f = (symmetric, linc, hinc, nils_false, anti)
+    L = lib()
+    if lo is not None and hi is not None:
+        return BAT(L.mgdk_BATcalcbetween(b.ptr, lo.ptr, hi.ptr, _p(s), _p(slo), _p(shi), *f))
+    if lo is None and hi is None:
+        return BAT(L.mgdk_BATcalcbetweencstcst(b.ptr, _valptr(ct, clo, keep), _valptr(ct, chi, keep), ct,
+                                               _p(s), *f))
+    if hi is None:
+        return BAT(L.mgdk_BATcalcbetweenbatcst(b.ptr, lo.ptr, _valptr(ct, chi, keep), ct, _p(s), _p(slo), *f))
+    return BAT(L.mgdk_BATcalcbetweencstbat(b.ptr, _valptr(ct, clo, keep), hi.ptr, ct, _p(s), _p(shi), *f))
+
+
+def BATconvert(b, s, tp, scale1=0, scale2=0, precision=0):
+    """BATconvert (gdk/gdk_calc_convert.c:1415)"""
+    return BAT(lib().mgdk_BATconvert(b.ptr, _p(s), tp, scale1, scale2, precision))
+
+
+def BATcalcnot(b, s=None):
+    return BAT(lib().mgdk_BATcalcnot(b.ptr, _p(s)))
+
+
+def BATcalcdivmod(op, b1, b2, tp, s1=None, s2=None, c1=None, t1=0, c2=None, t2=0):
+    """BATcalcdiv / BATcalcmod and their cst forms; op '/' or '%'"""
+    keep = []
+    nm = "div" if op == "/" else "mod"
+    L = lib()
+    if b1 is not None and b2 is not None:
+        return BAT(getattr(L, "mgdk_BATcalc" + nm)(b1.ptr, b2.ptr, _p(s1), _p(s2), tp))
+    if b2 is None:
+        return BAT(getattr(L, "mgdk_BATcalc%scst" % nm)(b1.ptr, _valptr(t2, c2, keep), t2, _p(s1), tp))
+    return BAT(getattr(L, "mgdk_BATcalccst" + nm)(_valptr(t1, c1, keep), t1, b2.ptr, _p(s1), tp))
 
 
 def _cst(fn, b, v, vt, s, tp):

@@ -2,7 +2,7 @@
  * gdk_oracle.c -- CPU restatement of the GDK select / project / calc / sum
  * semantics.  TEST INFRASTRUCTURE ONLY (see gdk_oracle.h).
  */
-#include "gdk_oracle.h"
+#include "gdk_oracle_private.h"
 
 #include <math.h>
 #include <stdarg.h>
@@ -18,7 +18,6 @@ ora_errbuf(void)
 	return errbuf;
 }
 
-void ora_seterr(const char *fmt, ...);
 void
 ora_seterr(const char *fmt, ...)
 {
@@ -28,7 +27,6 @@ ora_seterr(const char *fmt, ...)
 	va_end(ap);
 }
 
-int ora_width(int type);
 int
 ora_width(int type)
 {
@@ -79,7 +77,6 @@ ora_free(ora_bat *b)
 	free(b);
 }
 
-ora_bat *ora_dense(ora_oid hseq, ora_oid tseq, uint64_t cnt);
 ora_bat *
 ora_dense(ora_oid hseq, ora_oid tseq, uint64_t cnt)
 {
@@ -96,19 +93,6 @@ ora_dense(ora_oid hseq, ora_oid tseq, uint64_t cnt)
 /* candidate lists: gdk/gdk_cand.c:407 canditer_init; restated as an
  * explicit (seq, n) dense range or a clipped sorted oid array */
 
-typedef struct {
-	bool dense;
-	ora_oid seq;          /* dense: first candidate */
-	const ora_oid *oids;  /* materialized: first candidate */
-	uint64_t n;
-} ora_ci;
-
-static inline ora_oid
-ci_get(const ora_ci *ci, uint64_t i)
-{
-	return ci->dense ? ci->seq + i : ci->oids[i];
-}
-
 static uint64_t
 lower_bound_oid(const ora_oid *a, uint64_t n, ora_oid v)
 {
@@ -123,7 +107,6 @@ lower_bound_oid(const ora_oid *a, uint64_t n, ora_oid v)
 	return lo;
 }
 
-int ora_ci_init(ora_ci *ci, const ora_bat *b, const ora_bat *s);
 int
 ora_ci_init(ora_ci *ci, const ora_bat *b, const ora_bat *s)
 {

@@ -13,7 +13,8 @@
  *   candidates  gdk/gdk_cand.c:407 (canditer_init clipping)
  *   project     gdk/gdk_project.c:590-857
  *   calc        gdk/gdk_calc_addsub.c, gdk/gdk_calc_mul.c:23-132,2020-2092,
- *               overflow rules gdk/gdk_calc_private.h:38-140
+ *               overflow rules gdk/gdk_calc_private.h:38-140; compare, between,
+ *               convert, not, div, mod (gdk_oracle_calc.c)
  *   aggregates  gdk/gdk_aggr.c:65 (BATgroupaggrinit), :708 (dosum), :900, :1018,
  *               :1801 (BATgroupavg), :1996 (BATgroupavg3), :2634 (combine), :3069 (BATgroupcount), AVERAGE_ITER
  *               gdk/gdk_calc_private.h:231-275
@@ -85,6 +86,21 @@ ora_bat *ora_project(const ora_bat *l, const ora_bat *r);
 ora_bat *ora_calc(char op, const ora_bat *b1, const void *c1, int t1,
 		  const ora_bat *b2, const void *c2, int t2,
 		  const ora_bat *s, int tp);
+/* BATcalc{lt,le,gt,ge,eq,ne,cmp} (op 0..6; gdk/gdk_calc_compare.h), with
+ * constants as for ora_calc; s1 / s2 candidate lists of b1 / b2 */
+ora_bat *ora_calccmp(int op, const ora_bat *b1, const void *c1, int t1, const ora_bat *b2,
+		     const void *c2, int t2, const ora_bat *s1, const ora_bat *s2, bool nil_matches);
+/* BATcalcbetween / -cstcst / -batcst / -cstbat (gdk/gdk_calc.c:3968-4206) */
+ora_bat *ora_calcbetween(const ora_bat *b, const ora_bat *lo, const void *clo, const ora_bat *hi,
+			 const void *chi, int ct, const ora_bat *s, const ora_bat *slo,
+			 const ora_bat *shi, bool symmetric, bool linc, bool hinc, bool nils_false,
+			 bool anti);
+/* BATconvert (gdk/gdk_calc_convert.c:1415) for numeric / oid / bit types */
+ora_bat *ora_convert(const ora_bat *b, const ora_bat *s, int tp, int scale1, int scale2, int prec);
+ora_bat *ora_calcnot(const ora_bat *b, const ora_bat *s);
+/* BATcalcdiv / BATcalcmod (+cst variants): op '/' or '%' */
+ora_bat *ora_calcdivmod(char op, const ora_bat *b1, const void *c1, int t1, const ora_bat *b2,
+			const void *c2, int t2, const ora_bat *s1, const ora_bat *s2, int tp);
 int ora_sum(void *res, int tp, const ora_bat *b, const ora_bat *s,
 	    bool skip_nils, bool nil_if_empty);
 int ora_group(ora_bat **groups, ora_bat **extents, ora_bat **histo,

@@ -74,6 +74,16 @@ def lib():
         L.ora_project.argtypes = [P, P]
         L.ora_calc.restype = P
         L.ora_calc.argtypes = [C.c_char, P, C.c_void_p, C.c_int, P, C.c_void_p, C.c_int, P, C.c_int]
+        L.ora_calccmp.restype = P
+        L.ora_calccmp.argtypes = [C.c_int, P, C.c_void_p, C.c_int, P, C.c_void_p, C.c_int, P, P, C.c_bool]
+        L.ora_calcbetween.restype = P
+        L.ora_calcbetween.argtypes = [P, P, C.c_void_p, P, C.c_void_p, C.c_int, P, P, P] + [C.c_bool] * 5
+        L.ora_convert.restype = P
+        L.ora_convert.argtypes = [P, P, C.c_int, C.c_int, C.c_int, C.c_int]
+        L.ora_calcnot.restype = P
+        L.ora_calcnot.argtypes = [P, P]
+        L.ora_calcdivmod.restype = P
+        L.ora_calcdivmod.argtypes = [C.c_char, P, C.c_void_p, C.c_int, P, C.c_void_p, C.c_int, P, P, C.c_int]
         L.ora_sum.argtypes = [C.c_void_p, C.c_int, P, P, C.c_bool, C.c_bool]
         L.ora_group.argtypes = [C.POINTER(P), C.POINTER(P), C.POINTER(P), P, P, P]
         for f in ("ora_groupsum",):
@@ -239,6 +249,42 @@ def BATcalc(op, b1, b2, tp, s=None, c1=None, t1=0, c2=None, t2=0):
     return _ret(lib().ora_calc(op.encode(), b1.ptr if b1 else None, _valptr(t1, c1, keep), t1,
                                b2.ptr if b2 else None, _valptr(t2, c2, keep), t2,
                                s.ptr if s else None, tp))
+
+
+CMP_OPS = {"<": 0, "<=": 1, ">": 2, ">=": 3, "==": 4, "!=": 5, "cmp": 6}
+
+
+def _pp(b):
+    return b.ptr if b is not None else None
+
+
+def BATcalccmp(op, b1, b2, s1=None, s2=None, c1=None, t1=0, c2=None, t2=0, nil_matches=False):
+    """op in CMP_OPS; b1 / b2 None: the constant c1 / c2 of type t1 / t2"""
+    keep = []
+    return _ret(lib().ora_calccmp(CMP_OPS[op], _pp(b1), _valptr(t1, c1, keep), t1, _pp(b2),
+                                  _valptr(t2, c2, keep), t2, _pp(s1), _pp(s2), nil_matches))
+
+
+def BATcalcbetween(b, lo, hi, s=None, slo=None, shi=None, clo=None, chi=None, ct=0,
+                   symmetric=False, linc=True, hinc=True, nils_false=False, anti=False):
+    keep = []
+    return _ret(lib().ora_calcbetween(b.ptr, _pp(lo), _valptr(ct, clo, keep), _pp(hi),
+                                      _valptr(ct, chi, keep), ct, _pp(s), _pp(slo), _pp(shi),
+                                      symmetric, linc, hinc, nils_false, anti))
+
+
+def BATconvert(b, s, tp, scale1=0, scale2=0, precision=0):
+    return _ret(lib().ora_convert(b.ptr, _pp(s), tp, scale1, scale2, precision))
+
+
+def BATcalcnot(b, s=None):
+    return _ret(lib().ora_calcnot(b.ptr, _pp(s)))
+
+
+def BATcalcdivmod(op, b1, b2, tp, s1=None, s2=None, c1=None, t1=0, c2=None, t2=0):
+    keep = []
+    return _ret(lib().ora_calcdivmod(op.encode(), _pp(b1), _valptr(t1, c1, keep), t1, _pp(b2),
+                                     _valptr(t2, c2, keep), t2, _pp(s1), _pp(s2), tp))
 
 
 def BATsum(tp, b, s=None, skip_nils=True, nil_if_empty=True):
