@@ -234,6 +234,10 @@ typedef struct mgdk_q1row {
 	int64_t sum_disc[2];
 	int64_t count_order;
 	mgdk_oid first_row;
+	/* BATgroupavg3 of quantity, extendedprice, discount: the average rounded
+	 * half away from zero and its remainder (gdk_aggr.c:1996-2095) */
+	int64_t avg_qty, avg_price, avg_disc;
+	int64_t rem_qty, rem_price, rem_disc;
 } mgdk_q1row;
 /* Q1 groups (first-occurrence numbering, BATgroup semantics); returns the
  * number of groups in *ngroups (<= maxgroups). */

@@ -392,59 +392,124 @@ k_gaggr(const void *base, int w, oid off, const oid *gids, oid gseq, oid gmin, B
 // loop has no global loads besides the gid and the value (U rows in flight
 // per lane); positions only grow along a lane, so "first" is the first one
 // seen and "last" the last one.  One flush of wave-reduced values per wave.
-template <int K, bool MM>
+// GT: uint8_t reads the 1-byte group-id image BATgroup keeps with g (<= 255
+// groups), oid the 8-byte ids.  W16 = false: values of <= 8 bytes are summed
+// exactly as two 64-bit lane accumulators of their low 32 (unsigned) and high
+// 32 (signed) bits -- a lane sees < 2^31 rows -- instead of 128-bit adds.
+// POS: first non-nil / last nil positions are only tracked when wanted.
+template <int VW> struct VTy;
+template <> struct VTy<0> { typedef int64_t T; };   // COUNT(*): no values read
+template <> struct VTy<1> { typedef int8_t T; };
+template <> struct VTy<2> { typedef int16_t T; };
+template <> struct VTy<4> { typedef int32_t T; };
+template <> struct VTy<8> { typedef int64_t T; };
+template <> struct VTy<16> { typedef hge T; };
+
+// VW: value width, a template parameter so that the U loads of a step are
+// straight-line code (a runtime width switch puts every load in its own
+// block and the compiler then waits for each one before the next)
+template <int K, bool MM, bool POS, int VW, typename GT>
 __global__ __launch_bounds__(256) void
-k_gaggr_k(const void *base, int w, oid off, const oid *gids, oid gseq, oid gmin, BUN ngrp, BUN n, int what,
+k_gaggr_k(const void *base, int w, oid off, const GT *gids, oid gseq, oid gmin, BUN ngrp, BUN n, int what,
 	  bool count_all, GAcc acc, unsigned long long *maxabs)
 {
-	hge s[K];
-	unsigned long long c[K], fv[K], ln[K];
-	long long mn[K], mx[K];
+	constexpr bool W16 = VW == 16;
+	typedef typename VTy<VW>::T VT;
+	(void) w;
+	hge s[W16 ? K : 1];
+	unsigned long long slo[W16 ? 1 : K];
+	long long shi[W16 ? 1 : K];
+	unsigned c[K];
+	unsigned long long fv[POS ? K : 1], ln[POS ? K : 1];
+	long long mn[MM ? K : 1], mx[MM ? K : 1];
 #pragma unroll
 	for (int k = 0; k < K; k++) {
-		s[k] = 0;
+		if (W16)
+			s[k] = 0;
+		else
+			slo[k] = 0, shi[k] = 0;
 		c[k] = 0;
-		fv[k] = ~0ull;
-		ln[k] = 0;
-		mn[k] = INT64_MAX;
-		mx[k] = INT64_MIN;
+		if (POS)
+			fv[k] = ~0ull, ln[k] = 0;
+		if (MM)
+			mn[k] = INT64_MAX, mx[k] = INT64_MIN;
 	}
 	unsigned long long mxa = 0;
-	constexpr int U = 4;
-	const BUN stride = (BUN) gridDim.x * blockDim.x;
-	for (BUN i0 = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += stride * U) {
-		oid g[U];
+	// each wave streams 64 * U consecutive rows per step (row = chunk base +
+	// u * 64 + lane: every load instruction covers 64 consecutive values),
+	// U independent loads in flight per lane
+	constexpr int U = W16 ? 8 : 16;
+	constexpr BUN CH = 64 * U;
+	const uint32_t gm = (uint32_t) gmin;
+	const unsigned lane = __lane_id();
+	const BUN nwaves = (BUN) gridDim.x * (blockDim.x / 64);
+	for (BUN ch = (BUN) blockIdx.x * (blockDim.x / 64) + (threadIdx.x / 64); ch * CH < n; ch += nwaves) {
+		const BUN i0 = ch * CH + lane;
+		uint32_t gi[U];
 		hge v[U];
 		bool nil[U];
+		// every load is issued unconditionally (at a clamped index) and masked
+		// afterwards: a load under a divergent branch makes the compiler wait
+		// for it before the branch joins, which serialises the U loads
 #pragma unroll
 		for (int u = 0; u < U; u++) {
-			const BUN i = i0 + (BUN) u * stride;
-			g[u] = i < n ? (gids ? gids[i] : gseq + i) : gmin + ngrp;
-			v[u] = i < n ? ldv(base, w, off + i, nil[u]) : (nil[u] = false, (hge) 0);
+			const BUN i = i0 + (BUN) u * 64;
+			const bool ok = i < n;
+			const BUN ic = ok ? i : n - 1;
+			if (sizeof(GT) == 1) {
+				const uint32_t g = (uint32_t) gids[ic] - gm;
+				gi[u] = ok ? g : ~0u;
+			} else {
+				const oid g = gids ? (oid) gids[ic] : gseq + ic;
+				gi[u] = (!ok || g < gmin || g - gmin >= ngrp) ? ~0u : (uint32_t) (g - gmin);
+			}
+			// base NULL: COUNT(*) -- every row counts, no value is read
+			if constexpr (VW > 0) {
+				const VT x = ((const VT *) base)[off + ic];
+				v[u] = x;
+				nil[u] = is_nil(x);
+			} else {
+				v[u] = 0;
+				nil[u] = false;
+			}
 		}
 #pragma unroll
 		for (int u = 0; u < U; u++) {
-			const BUN i = i0 + (BUN) u * stride;
-			if (g[u] < gmin || g[u] - gmin >= ngrp)
+			const BUN i = i0 + (BUN) u * 64;
+			if (gi[u] >= (uint32_t) ngrp)
 				continue;
-			const BUN gi = g[u] - gmin;
 			if (nil[u]) {
 #pragma unroll
 				for (int k = 0; k < K; k++) {
-					const bool m = gi == (BUN) k;
-					ln[k] = m ? i + 1 : ln[k];
+					const bool m = gi[u] == (uint32_t) k;
+					if (POS)
+						ln[k] = m ? i + 1 : ln[k];
 					c[k] += (m && count_all);
 				}
 				continue;
 			}
-			const unsigned long long a = absbits(v[u]);
+			unsigned long long a;
+			if (W16) {
+				a = absbits(v[u]);
+			} else {
+				const long long x = (long long) v[u];
+				a = (unsigned long long) (x < 0 ? -x : x) >> 1;
+			}
 			mxa = a > mxa ? a : mxa;
+			const uint32_t lo32 = (uint32_t) (unsigned long long) v[u];
+			const int32_t hi32 = (int32_t) ((long long) v[u] >> 32);
 #pragma unroll
 			for (int k = 0; k < K; k++) {
-				const bool m = gi == (BUN) k;
-				s[k] += m ? v[u] : (hge) 0;
+				const bool m = gi[u] == (uint32_t) k;
+				if (W16) {
+					s[k] += m ? v[u] : (hge) 0;
+				} else {
+					slo[k] += m ? lo32 : 0u;
+					shi[k] += m ? hi32 : 0;
+				}
 				c[k] += m;
-				fv[k] = (m && fv[k] == ~0ull) ? i : fv[k];
+				if (POS)
+					fv[k] = (m && fv[k] == ~0ull) ? i : fv[k];
 				if (MM) {
 					const long long x = (long long) v[u];
 					mn[k] = (m && x < mn[k]) ? x : mn[k];
@@ -455,17 +520,19 @@ k_gaggr_k(const void *base, int w, oid off, const oid *gids, oid gseq, oid gmin,
 	}
 #pragma unroll
 	for (int k = 0; k < K; k++) {
-		hge sk = s[k];
-		unsigned long long ck = c[k], fk = fv[k], lk = ln[k];
-		long long nk = mn[k], xk = mx[k];
+		hge sk = W16 ? s[k] : (hge) shi[k] * ((hge) 1 << 32) + (hge) slo[k];
+		unsigned long long ck = c[k], fk = POS ? fv[k] : ~0ull, lk = POS ? ln[k] : 0;
+		long long nk = MM ? mn[k] : 0, xk = MM ? mx[k] : 0;
 		for (int o = 32; o > 0; o >>= 1) {
 			const unsigned long long lo = __shfl_xor((unsigned long long) (uhge) sk, o);
 			const unsigned long long hi = __shfl_xor((unsigned long long) ((uhge) sk >> 64), o);
 			sk += (hge) (((uhge) hi << 64) | lo);
 			ck += __shfl_xor(ck, o);
-			const unsigned long long f2 = __shfl_xor(fk, o), l2 = __shfl_xor(lk, o);
-			fk = f2 < fk ? f2 : fk;
-			lk = l2 > lk ? l2 : lk;
+			if (POS) {
+				const unsigned long long f2 = __shfl_xor(fk, o), l2 = __shfl_xor(lk, o);
+				fk = f2 < fk ? f2 : fk;
+				lk = l2 > lk ? l2 : lk;
+			}
 			if (MM) {
 				const long long n2 = __shfl_xor(nk, o), x2 = __shfl_xor(xk, o);
 				nk = n2 < nk ? n2 : nk;
@@ -478,11 +545,11 @@ k_gaggr_k(const void *base, int w, oid off, const oid *gids, oid gseq, oid gmin,
 					atomic_add128(&acc.sum[2 * k], sk);
 				atomicAdd(&acc.cnt[k], ck);
 			}
-			if ((what & AGG_POS) && fk != ~0ull)
+			if (POS && (what & AGG_POS) && fk != ~0ull)
 				atomicMin(&acc.firstval[k], fk);
-			if ((what & AGG_POS) && lk)
+			if (POS && (what & AGG_POS) && lk)
 				atomicMax(&acc.lastnil[k], lk);
-			if (MM && (what & AGG_MINMAX) && fk != ~0ull) {
+			if (MM && (what & AGG_MINMAX) && ck) {
 				atomicMin(&acc.mn[k], nk);
 				atomicMax(&acc.mx[k], xk);
 			}
@@ -501,6 +568,7 @@ struct AggrInit {
 	oid min, max;
 	BUN ngrp;
 	const oid *gids;   // NULL: dense g
+	const uint8_t *g8; // 1-byte image of gids kept by BATgroup (or NULL)
 	oid gseq;
 };
 
@@ -578,6 +646,7 @@ aggr_init(AggrInit *a, mgdk_bat **bp, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s)
 		*bp = v;
 	}
 	a->gids = g->ttype == MGDK_void ? nullptr : (const oid *) g->theap;
+	a->g8 = a->gids ? img8_get(g) : nullptr;
 	a->gseq = g->tseqbase;
 	if (e) {
 		a->ngrp = e->count;
@@ -646,14 +715,25 @@ run_gaggr(const AggrInit &a, mgdk_bat *b, int what, bool count_all, GRes &r)
 	}
 	const oid off = a.ci.seq - b->hseqbase;
 	dim3 g(grid_for(a.ci.n, 256 * 8, 256 * 16)), blk(256);
+	// COUNT(*) over few groups needs no values (k_gaggr_k's base == NULL)
+	const void *vbase = (what == 0 && count_all && ng <= 8) ? nullptr : b->theap;
 	if (a.ci.n) {
-#define GK(K_) do { if (what & AGG_MINMAX) \
-		hipLaunchKernelGGL((k_gaggr_k<K_, true>), g, blk, 0, st, b->theap, b->twidth, off, a.gids, a.gseq, a.min, ng, a.ci.n, what, count_all, acc, maxabs); \
-	else \
-		hipLaunchKernelGGL((k_gaggr_k<K_, false>), g, blk, 0, st, b->theap, b->twidth, off, a.gids, a.gseq, a.min, ng, a.ci.n, what, count_all, acc, maxabs); } while (0)
-		if (ng <= 1)
-			GK(1);
-		else if (ng <= 4)
+#define GK4(K_, MM_, POS_, VW_) do { \
+		if (a.g8 && a.min < 256 && a.min + ng <= 256) \
+			hipLaunchKernelGGL((k_gaggr_k<K_, MM_, POS_, VW_, uint8_t>), g, blk, 0, st, vbase, b->twidth, off, a.g8, a.gseq, a.min, ng, a.ci.n, what, count_all, acc, maxabs); \
+		else \
+			hipLaunchKernelGGL((k_gaggr_k<K_, MM_, POS_, VW_, oid>), g, blk, 0, st, vbase, b->twidth, off, a.gids, a.gseq, a.min, ng, a.ci.n, what, count_all, acc, maxabs); } while (0)
+#define GK3(K_, MM_, POS_) do { switch (vbase ? b->twidth : 0) { \
+		case 0: GK4(K_, MM_, POS_, 0); break; \
+		case 1: GK4(K_, MM_, POS_, 1); break; \
+		case 2: GK4(K_, MM_, POS_, 2); break; \
+		case 4: GK4(K_, MM_, POS_, 4); break; \
+		case 8: GK4(K_, MM_, POS_, 8); break; \
+		default: GK4(K_, MM_, POS_, 16); break; } } while (0)
+#define GK(K_) do { if (what & AGG_MINMAX) GK3(K_, true, true); \
+		else if (what & AGG_POS) GK3(K_, false, true); \
+		else GK3(K_, false, false); } while (0)
+		if (ng <= 4)
 			GK(4);
 		else if (ng <= 8)
 			GK(8);
@@ -877,7 +957,7 @@ mgdk_BATgroupsum(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, boo
 	std::vector<char> out(ng * width_of(tp) + 16);
 	GRes r;
 	if (a.ci.n && ng) {
-		if (run_gaggr(a, b, AGG_SUM | AGG_POS, false, r) < 0)
+		if (run_gaggr(a, b, AGG_SUM | (skip_nils ? 0 : AGG_POS), false, r) < 0)
 			return nullptr;
 		// overflow: a prefix of one group could exceed max only if
 		// count * max|v| exceeds it
@@ -1092,7 +1172,7 @@ mgdk_BATgroupavg(mgdk_bat **bnp, mgdk_bat **cntsp, mgdk_bat *b, mgdk_bat *g, mgd
 			nils |= hc[k] == 0;
 	} else {
 		GRes r;
-		if (run_gaggr(a, b, AGG_SUM | AGG_POS, false, r) < 0)
+		if (run_gaggr(a, b, AGG_SUM | (skip_nils ? 0 : AGG_POS), false, r) < 0)
 			return -1;
 		std::vector<double> d(ng + 1);
 		std::vector<long long> c(ng + 1);
@@ -1278,7 +1358,7 @@ mgdk_BATgroupavg3(mgdk_bat **avgp, mgdk_bat **remp, mgdk_bat **cntp, mgdk_bat *b
 	const BUN ng = a.ngrp;
 	const int tp = b->ttype;
 	GRes r;
-	if (a.ci.n && ng && run_gaggr(a, b, AGG_SUM | AGG_POS, false, r) < 0)
+	if (a.ci.n && ng && run_gaggr(a, b, AGG_SUM | (skip_nils ? 0 : AGG_POS), false, r) < 0)
 		return -1;
 	std::vector<char> av(ng * width_of(tp) + 16);
 	std::vector<long long> rem(ng + 1), cnt(ng + 1);

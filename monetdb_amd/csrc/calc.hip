@@ -99,34 +99,132 @@ st(void *base, int w, BUN i, hge v)
 	}
 }
 
-// OP: 0 add, 1 sub, 2 mul; CHECK: range/overflow check needed
+// OP: 0 add, 1 sub, 2 mul; CHECK: range/overflow check needed.  Each wave
+// streams 64 * U consecutive candidates per step (element = chunk base +
+// u * 64 + lane), all U operand pairs loaded before any is used.
 template <int OP, bool CHECK>
 __global__ __launch_bounds__(256) void
 k_calc(Operand a, Operand b, void *out, int ow, hge max, BUN n, hge nilv,
        unsigned long long *first_ovf, unsigned long long *nils)
 {
+	constexpr int U = 8;
+	constexpr BUN CH = 64 * U;
 	unsigned long long mynils = 0, myovf = ~0ull;
-	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
-		bool n1, n2;
-		hge x = operand(a, i, n1), y = operand(b, i, n2);
-		if (n1 || n2) {
-			st(out, ow, i, nilv);
-			mynils++;
-			continue;
+	const unsigned lane = __lane_id();
+	const BUN nwaves = (BUN) gridDim.x * (blockDim.x / 64);
+	for (BUN ch = (BUN) blockIdx.x * (blockDim.x / 64) + (threadIdx.x / 64); ch * CH < n; ch += nwaves) {
+		const BUN i0 = ch * CH + lane;
+		hge x[U], y[U];
+		bool n1[U], n2[U];
+		// loads at a clamped index, unconditionally (a load under a divergent
+		// branch is waited for before the branch joins)
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const BUN i = i0 + (BUN) u * 64;
+			const BUN ic = i < n ? i : n - 1;
+			x[u] = operand(a, ic, n1[u]);
+			y[u] = operand(b, ic, n2[u]);
 		}
-		hge r;
-		bool ovf;
-		if (OP == 0) ovf = add_ovf(x, y, r);
-		else if (OP == 1) ovf = sub_ovf(x, y, r);
-		else ovf = mul_ovf(x, y, r);
-		if (CHECK && (ovf || r < -max || r > max)) {
-			if (i < myovf)
-				myovf = i;
-			continue;
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const BUN i = i0 + (BUN) u * 64;
+			if (i >= n)
+				continue;
+			if (n1[u] || n2[u]) {
+				st(out, ow, i, nilv);
+				mynils++;
+				continue;
+			}
+			hge r;
+			bool ovf;
+			if (OP == 0) ovf = add_ovf(x[u], y[u], r);
+			else if (OP == 1) ovf = sub_ovf(x[u], y[u], r);
+			else ovf = mul_ovf(x[u], y[u], r);
+			if (CHECK && (ovf || r < -max || r > max)) {
+				if (i < myovf)
+					myovf = i;
+				continue;
+			}
+			st(out, ow, i, r);
 		}
-		st(out, ow, i, r);
 	}
 	// block reduce then one atomic per workgroup
+	mynils = block_reduce(mynils, [](decltype(mynils) x, decltype(mynils) y) { return x + y; });
+	myovf = block_reduce(myovf, [](unsigned long long x, unsigned long long y) { return x < y ? x : y; });
+	if (threadIdx.x == 0) {
+		if (mynils)
+			atomicAdd(nils, mynils);
+		if (myovf != ~0ull)
+			atomicMin(first_ovf, myovf);
+	}
+}
+
+// Width-generic load without branches: the 16-byte aligned word holding the
+// value is loaded and the value shifted out and sign-extended (heaps are at
+// least 16-byte aligned and padded, so the word never leaves the heap).  A
+// runtime width switch would put each load in its own block, and the
+// compiler waits for every such load before the block joins.
+__device__ __forceinline__ hge
+ld_any(const void *base, int w, BUN p, bool &isnil)
+{
+	const uintptr_t a = (uintptr_t) base + (uintptr_t) p * (uintptr_t) w;
+	const uint4 q = *(const uint4 *) (a & ~(uintptr_t) 15);
+	const unsigned sh = (unsigned) (a & 15) * 8;
+	uhge x = ((uhge) (((unsigned long long) q.w << 32) | q.z) << 64) | (((unsigned long long) q.y << 32) | q.x);
+	x >>= sh;
+	const unsigned bits = 8u * (unsigned) w;
+	const unsigned up = 128u - bits;
+	const hge v = up ? ((hge) (x << up) >> up) : (hge) x;
+	const hge nilv = up ? -((hge) 1 << (bits - 1)) : (hge) ((uhge) 1 << 127);
+	isnil = v == nilv;
+	return v;
+}
+
+// fast path: dense candidates (or constants: CA / CB), branch-free loads
+template <int OP, bool CHECK, bool CA, bool CB>
+__global__ __launch_bounds__(256) void
+k_calc_d(Operand a, Operand b, void *out, int ow, hge max, BUN n, hge nilv,
+	 unsigned long long *first_ovf, unsigned long long *nils)
+{
+	constexpr int U = 8;
+	constexpr BUN CH = 64 * U;
+	unsigned long long mynils = 0, myovf = ~0ull;
+	const unsigned lane = __lane_id();
+	const BUN nwaves = (BUN) gridDim.x * (blockDim.x / 64);
+	for (BUN ch = (BUN) blockIdx.x * (blockDim.x / 64) + (threadIdx.x / 64); ch * CH < n; ch += nwaves) {
+		const BUN i0 = ch * CH + lane;
+		hge x[U], y[U];
+		bool n1[U], n2[U];
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const BUN i = i0 + (BUN) u * 64;
+			const BUN ic = i < n ? i : n - 1;
+			if (CA) { x[u] = a.c; n1[u] = a.cnil; } else x[u] = ld_any(a.base, a.w, a.off + ic, n1[u]);
+			if (CB) { y[u] = b.c; n2[u] = b.cnil; } else y[u] = ld_any(b.base, b.w, b.off + ic, n2[u]);
+		}
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const BUN i = i0 + (BUN) u * 64;
+			if (i >= n)
+				continue;
+			if (n1[u] || n2[u]) {
+				st(out, ow, i, nilv);
+				mynils++;
+				continue;
+			}
+			hge r;
+			bool ovf;
+			if (OP == 0) ovf = add_ovf(x[u], y[u], r);
+			else if (OP == 1) ovf = sub_ovf(x[u], y[u], r);
+			else ovf = mul_ovf(x[u], y[u], r);
+			if (CHECK && (ovf || r < -max || r > max)) {
+				if (i < myovf)
+					myovf = i;
+				continue;
+			}
+			st(out, ow, i, r);
+		}
+	}
 	mynils = block_reduce(mynils, [](decltype(mynils) x, decltype(mynils) y) { return x + y; });
 	myovf = block_reduce(myovf, [](unsigned long long x, unsigned long long y) { return x < y ? x : y; });
 	if (threadIdx.x == 0) {
@@ -261,12 +359,18 @@ calc(int op, mgdk_bat *b1, const void *v1, int t1, mgdk_bat *b2, const void *v2,
 	case 4: nilv = INT32_MIN; break;
 	case 8: nilv = INT64_MIN; break;
 	}
-	dim3 g(grid_for(n, 256 * 4, 256 * 32)), blk(256);
-#define LAUNCH(OPC, CHK) hipLaunchKernelGGL((k_calc<OPC, CHK>), g, blk, 0, stream(), A, B, bn->theap, ow, max, n, nilv, m, m + 1)
+	dim3 g(grid_for(n, 256 * 8, 256 * 16)), blk(256);
+	const bool fast = (A.base == nullptr || A.dense) && (B.base == nullptr || B.dense);
+#define LAUNCHD(OPC, CHK, CA_, CB_) hipLaunchKernelGGL((k_calc_d<OPC, CHK, CA_, CB_>), g, blk, 0, stream(), A, B, bn->theap, ow, max, n, nilv, m, m + 1)
+#define LAUNCH(OPC, CHK) do { if (!fast) hipLaunchKernelGGL((k_calc<OPC, CHK>), g, blk, 0, stream(), A, B, bn->theap, ow, max, n, nilv, m, m + 1); \
+		else if (A.base == nullptr) LAUNCHD(OPC, CHK, true, false); \
+		else if (B.base == nullptr) LAUNCHD(OPC, CHK, false, true); \
+		else LAUNCHD(OPC, CHK, false, false); } while (0)
 	if (op == 0) { if (check) LAUNCH(0, true); else LAUNCH(0, false); }
 	else if (op == 1) { if (check) LAUNCH(1, true); else LAUNCH(1, false); }
 	else { if (check) LAUNCH(2, true); else LAUNCH(2, false); }
 #undef LAUNCH
+#undef LAUNCHD
 	unsigned long long *h = (unsigned long long *) pinned(64);
 	if (h == nullptr || !hip_ok(hipMemcpyAsync(h, m, 16, hipMemcpyDeviceToHost, stream()), "memcpy") || !sync()) {
 		mgdk_BBPunfix(bn);

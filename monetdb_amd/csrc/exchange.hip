@@ -116,6 +116,7 @@ mgdk_BATupload_device(mgdk_bat *b, const void *dev, mgdk_BUN n)
 	}
 	Priv *p = (Priv *) b->priv;
 	const size_t bytes = n * (size_t) b->twidth;
+	img8_drop(b);
 	if (p->theap == nullptr || p->theap->refs != 1 ||
 	    p->theap->size < bytes + ((char *) b->theap - (char *) p->theap->base)) {
 		Heap *h = heap_new(bytes ? bytes : 1);

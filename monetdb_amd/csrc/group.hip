@@ -34,6 +34,7 @@ struct KeySrc {
 	const oid *oids;   // materialized candidates
 	oid hseq;
 	const oid *g;      // prior groups aligned with candidates (NULL: none)
+	const uint8_t *g8; // their 1-byte image kept with g (NULL: none)
 	oid gseq;          // dense prior groups: gseq + i
 	bool has_g;
 };
@@ -71,7 +72,7 @@ key_at(const KeySrc &s, BUN i, uint64_t &k0, uint64_t &k1, uint64_t &gg)
 		k1 = ((const uint64_t *) s.base)[2 * p + 1];
 		break;
 	}
-	gg = s.has_g ? (s.g ? s.g[i] : s.gseq + i) : 0;
+	gg = s.has_g ? (s.g8 ? (uint64_t) s.g8[i] : s.g ? s.g[i] : s.gseq + i) : 0;
 }
 
 __device__ __forceinline__ uint64_t
@@ -338,7 +339,7 @@ gl_lookup(const unsigned long long *lkey, const uint32_t *lmap, uint64_t k)
 
 __global__ __launch_bounds__(1024) void
 k_gl_assign(KeySrc s, BUN n, const unsigned long long *gkey, const uint32_t *gmap, uint32_t ngrp, oid *gid,
-	    unsigned long long *histo, uint32_t *unsorted)
+	    uint8_t *img, unsigned long long *histo, uint32_t *unsorted)
 {
 	__shared__ unsigned long long lkey[GL_SLOTS];
 	__shared__ uint32_t lmap[GL_SLOTS + 1];
@@ -361,6 +362,8 @@ k_gl_assign(KeySrc s, BUN n, const unsigned long long *gkey, const uint32_t *gma
 		if (i < e) {
 			g = gl_lookup(lkey, lmap, gl_key(s, i));
 			gid[i] = g;
+			if (img)
+				img[i] = (uint8_t) g;
 			atomicAdd(&lh[g], 1u);
 		}
 		uint32_t gp = __shfl_up(g, 1);
@@ -409,8 +412,16 @@ group_lds(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mg
 		mgdk_BBPunfix(gn);
 		return -1;
 	}
+	uint8_t *img = nullptr;
+	gn->count = n;
+	if (ngrp <= 255 && (img = img8_new(gn)) == nullptr) {
+		mgdk_BBPunfix(en);
+		mgdk_BBPunfix(hn);
+		mgdk_BBPunfix(gn);
+		return -1;
+	}
 	hipLaunchKernelGGL(k_gl_assign, dim3(tiles), dim3(1024), 0, st, ks, n, gkey.as<unsigned long long>(),
-			   gmap.as<uint32_t>(), ngrp, (oid *) gn->theap, (unsigned long long *) hn->theap, &m[2]);
+			   gmap.as<uint32_t>(), ngrp, (oid *) gn->theap, img, (unsigned long long *) hn->theap, &m[2]);
 	oid fl[2] = {0, 0};
 	if (!hip_ok(hipMemcpyAsync(h, m, 12, hipMemcpyDeviceToHost, st), "memcpy") ||
 	    (ngrp > 0 && (!hip_ok(hipMemcpyAsync(&fl[0], ext.p, 8, hipMemcpyDeviceToHost, st), "memcpy") ||
@@ -436,6 +447,264 @@ group_lds(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mg
 	hn->tnonil = 1;
 	// tmaxpos: the row that started the last group (maxgrppos,
 	// gdk_group.c:99,1313)
+	gn->tmaxpos = ngrp > 0 ? cand_index(ci, fl[1]) : MGDK_BUN_NONE;
+	if (ngrp > 0 && fl[1] - fl[0] == ngrp - 1)
+		setdense(en, fl[0], ngrp);
+	*gnp = gn;
+	*enp = en;
+	*hnp = hn;
+	return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Direct path for 1-byte keys (bte / bit / str with 1-byte offsets) with at
+// most 32 prior groups -- GRP_small_values' domain (gdk_group.c:607-654):
+// slot = prior group * 256 + key, at most 8192 slots, so every table is a
+// plain LDS array (no hashing, no probing).
+//   first  each workgroup (64 Ki rows, 16 independent rows per lane in
+//          flight) records the first row of every slot it sees, merged into
+//          the global table with one atomicMin per occupied slot;
+//   order  one workgroup ranks the occupied slots by first row;
+//   assign writes each row's group id (and the 1-byte image for <= 255
+//          groups), counts per group in lane registers for <= 8 groups
+//          (LDS atomics otherwise) and the order flag.
+// ---------------------------------------------------------------------------
+constexpr uint32_t GS_MAXSLOTS = 8192;
+constexpr BUN GS_TILE = 65536;
+constexpr int GS_U = 16;
+
+// MODE 0: dense 1-byte keys; 1: dense keys + the prior groups' 1-byte image;
+// 2: anything else (key_at).  Modes 0 / 1 are straight-line loads (a
+// branchy loader makes the compiler wait for each load before the next).
+template <int MODE>
+__device__ __forceinline__ uint32_t
+gs_slot(const KeySrc &s, BUN i)
+{
+	if constexpr (MODE == 0) {
+		return ((const uint8_t *) s.base)[s.off + i];
+	} else if constexpr (MODE == 1) {
+		return ((uint32_t) s.g8[i] << 8) | ((const uint8_t *) s.base)[s.off + i];
+	} else {
+		uint64_t k0, k1, gg;
+		key_at(s, i, k0, k1, gg);
+		return (uint32_t) ((gg << 8) | (k0 & 0xff));
+	}
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void
+k_gs_first(KeySrc s, BUN n, uint32_t nslots, unsigned long long *gmin)
+{
+	extern __shared__ __attribute__((aligned(16))) uint32_t lmin[];   // [nslots]: LDS sized to the slots used
+	const unsigned tid = threadIdx.x;
+	for (uint32_t q = tid; q < nslots; q += blockDim.x)
+		lmin[q] = ~0u;
+	__syncthreads();
+	const BUN a = (BUN) blockIdx.x * GS_TILE, e = min(n, a + GS_TILE);
+	for (BUN i0 = a; i0 < e; i0 += (BUN) blockDim.x * GS_U) {
+		uint32_t sl[GS_U];
+#pragma unroll
+		for (int u = 0; u < GS_U; u++) {
+			const BUN i = i0 + (BUN) u * blockDim.x + tid;
+			const uint32_t x = gs_slot<MODE>(s, i < e ? i : e - 1);   // unconditional load, clamped
+			sl[u] = i < e ? x : ~0u;
+		}
+#pragma unroll
+		for (int u = 0; u < GS_U; u++) {
+			const uint32_t r = (uint32_t) (i0 - a) + (uint32_t) u * blockDim.x + tid;
+			if (sl[u] < nslots && lmin[sl[u]] > r)
+				atomicMin(&lmin[sl[u]], r);
+		}
+	}
+	__syncthreads();
+	for (uint32_t q = tid; q < nslots; q += blockDim.x)
+		if (lmin[q] != ~0u) {
+			const unsigned long long f = a + lmin[q];
+			if (gmin[q] > f)
+				atomicMin(&gmin[q], f);
+		}
+}
+
+__global__ __launch_bounds__(1024) void
+k_gs_order(const unsigned long long *gmin, uint32_t nslots, uint32_t *gmap, bool cdense, oid cseq, const oid *coids,
+	   oid *ext, uint32_t *ngrp)
+{
+	__shared__ unsigned long long sk[GS_MAXSLOTS];
+	__shared__ uint32_t s_cnt;
+	const unsigned tid = threadIdx.x;
+	if (tid == 0)
+		s_cnt = 0;
+	__syncthreads();
+	for (uint32_t q = tid; q < nslots; q += blockDim.x) {
+		const unsigned long long f = gmin[q];
+		if (f != ~0ull)
+			sk[atomicAdd(&s_cnt, 1u)] = (f << 13) | q;
+	}
+	__syncthreads();
+	const uint32_t c = s_cnt;
+	for (uint32_t i = tid; i < c; i += blockDim.x) {
+		const unsigned long long v = sk[i];
+		uint32_t r = 0;
+		for (uint32_t j = 0; j < c; j++)
+			r += sk[j] < v;
+		const uint32_t slot = (uint32_t) (v & 8191);
+		gmap[slot] = r;
+		ext[r] = cdense ? cseq + (BUN) (v >> 13) : coids[v >> 13];
+	}
+	if (tid == 0)
+		*ngrp = c;
+}
+
+template <int K, int MODE>
+__global__ __launch_bounds__(256) void
+k_gs_assign(KeySrc s, BUN n, const uint32_t *gmap, uint32_t nslots, uint32_t ngrp, oid *gid, uint8_t *img,
+	    unsigned long long *histo, uint32_t *unsorted)
+{
+	extern __shared__ __attribute__((aligned(16))) uint32_t lmap[];   // [nslots] + [ngrp] histogram (K == 0)
+	uint32_t *lh = lmap + nslots;
+	const unsigned tid = threadIdx.x, lane = __lane_id();
+	for (uint32_t q = tid; q < nslots; q += blockDim.x)
+		lmap[q] = gmap[q];
+	if (K == 0)
+		for (uint32_t q = tid; q < ngrp; q += blockDim.x)
+			lh[q] = 0;
+	__syncthreads();
+	uint32_t cnt[K > 0 ? K : 1];
+#pragma unroll
+	for (int k = 0; k < (K > 0 ? K : 1); k++)
+		cnt[k] = 0;
+	const BUN a = (BUN) blockIdx.x * GS_TILE, e = min(n, a + GS_TILE);
+	uint32_t uns = 0;
+	for (BUN i0 = a; i0 < e; i0 += (BUN) blockDim.x * GS_U) {
+		uint32_t sl[GS_U];
+#pragma unroll
+		for (int u = 0; u < GS_U; u++) {
+			const BUN i = i0 + (BUN) u * blockDim.x + tid;
+			const uint32_t x = gs_slot<MODE>(s, i < e ? i : e - 1);   // unconditional load, clamped
+			sl[u] = i < e ? x : ~0u;
+		}
+		uint32_t prev = 0;
+		if (lane == 0 && i0 + tid > 0 && i0 + tid < e)
+			prev = lmap[gs_slot<MODE>(s, i0 + tid - 1)];
+#pragma unroll
+		for (int u = 0; u < GS_U; u++) {
+			const BUN i = i0 + (BUN) u * blockDim.x + tid;
+			const uint32_t g = sl[u] < nslots ? lmap[sl[u]] : 0;
+			if (i < e) {
+				gid[i] = g;
+				if (img)
+					img[i] = (uint8_t) g;
+				if (K > 0) {
+#pragma unroll
+					for (int k = 0; k < K; k++)
+						cnt[k] += g == (uint32_t) k;
+				} else {
+					atomicAdd(&lh[g], 1u);
+				}
+			}
+			// order flag: the previous row is the previous lane's (lane 0:
+			// the last lane of the previous row group, looked up directly)
+			uint32_t gp = __shfl_up(g, 1);
+			if (lane == 0) {
+				if (u == 0)
+					gp = prev;
+				else if (i < e)     // rows past the tile end read nothing
+					gp = lmap[gs_slot<MODE>(s, i - 1)];
+			}
+			if (i > 0 && i < e && gp > g)
+				uns = 1;
+		}
+	}
+	if (__any(uns) && lane == 0)
+		publish_or(unsorted, 1u);
+	if (K > 0) {
+#pragma unroll
+		for (int k = 0; k < K; k++) {
+			uint32_t c = cnt[k];
+			for (int o = 32; o > 0; o >>= 1)
+				c += __shfl_xor(c, o);
+			if (lane == 0 && c && (uint32_t) k < ngrp)
+				atomicAdd(&histo[k], (unsigned long long) c);
+		}
+	} else {
+		__syncthreads();
+		for (uint32_t q = tid; q < ngrp; q += blockDim.x)
+			if (lh[q])
+				atomicAdd(&histo[q], (unsigned long long) lh[q]);
+	}
+}
+
+int
+group_small(const KeySrc &ks, BUN n, uint32_t nslots, const Cand &ci, oid hseqb, mgdk_bat **gnp, mgdk_bat **enp,
+	    mgdk_bat **hnp)
+{
+	hipStream_t st = stream();
+	DevBuf gmin(GS_MAXSLOTS * 8), gmap(GS_MAXSLOTS * 4), ext(GS_MAXSLOTS * 8);
+	uint32_t *m = (uint32_t *) meta_buf();
+	uint32_t *h = (uint32_t *) pinned(16);
+	if (!gmin.p || !gmap.p || !ext.p)
+		return -1;
+	if (!hip_ok(hipMemsetAsync(gmin.p, 0xff, nslots * 8, st), "memset") || !hip_ok(hipMemsetAsync(m, 0, 16, st), "memset"))
+		return -1;
+	const unsigned tiles = (unsigned) ((n + GS_TILE - 1) / GS_TILE);
+	const int mode = (ks.dense && !ks.has_g) ? 0 : (ks.dense && ks.g8) ? 1 : 2;
+	if (mode == 0)
+		hipLaunchKernelGGL((k_gs_first<0>), dim3(tiles), dim3(256), nslots * 4, st, ks, n, nslots, gmin.as<unsigned long long>());
+	else if (mode == 1)
+		hipLaunchKernelGGL((k_gs_first<1>), dim3(tiles), dim3(256), nslots * 4, st, ks, n, nslots, gmin.as<unsigned long long>());
+	else
+		hipLaunchKernelGGL((k_gs_first<2>), dim3(tiles), dim3(256), nslots * 4, st, ks, n, nslots, gmin.as<unsigned long long>());
+	hipLaunchKernelGGL(k_gs_order, dim3(1), dim3(1024), 0, st, gmin.as<unsigned long long>(), nslots, gmap.as<uint32_t>(),
+			   ci.dense, ci.seq, ci.oids, ext.as<oid>(), &m[1]);
+	if (!hip_ok(hipMemcpyAsync(h, m, 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+		return -1;
+	const uint32_t ngrp = h[1];
+	mgdk_bat *en = newbat(0, MGDK_oid, ngrp), *hn = newbat(0, MGDK_lng, ngrp), *gn = newbat(hseqb, MGDK_oid, n);
+	uint8_t *img = nullptr;
+	if (gn)
+		gn->count = n;
+	if (!en || !hn || !gn || !hip_ok(hipMemsetAsync(hn->theap, 0, ngrp * 8 + 8, st), "memset") ||
+	    !hip_ok(hipMemcpyAsync(en->theap, ext.p, ngrp * 8, hipMemcpyDeviceToDevice, st), "memcpy") ||
+	    (ngrp <= 255 && (img = img8_new(gn)) == nullptr)) {
+		mgdk_BBPunfix(en);
+		mgdk_BBPunfix(hn);
+		mgdk_BBPunfix(gn);
+		return -1;
+	}
+#define GSA2(K_, M_) hipLaunchKernelGGL((k_gs_assign<K_, M_>), dim3(tiles), dim3(256), (nslots + ((K_) == 0 ? ngrp : 0)) * 4, st, ks, n, gmap.as<uint32_t>(), nslots, ngrp, \
+				   (oid *) gn->theap, img, (unsigned long long *) hn->theap, &m[2])
+#define GSA(K_) do { if (mode == 0) GSA2(K_, 0); else if (mode == 1) GSA2(K_, 1); else GSA2(K_, 2); } while (0)
+	if (ngrp <= 1)
+		GSA(1);
+	else if (ngrp <= 4)
+		GSA(4);
+	else if (ngrp <= 8)
+		GSA(8);
+	else
+		GSA(0);
+#undef GSA
+#undef GSA2
+	oid fl[2] = {0, 0};
+	if (!hip_ok(hipMemcpyAsync(h, m, 12, hipMemcpyDeviceToHost, st), "memcpy") ||
+	    (ngrp > 0 && (!hip_ok(hipMemcpyAsync(&fl[0], ext.p, 8, hipMemcpyDeviceToHost, st), "memcpy") ||
+			  !hip_ok(hipMemcpyAsync(&fl[1], ext.as<oid>() + ngrp - 1, 8, hipMemcpyDeviceToHost, st), "memcpy"))) ||
+	    !sync()) {
+		mgdk_BBPunfix(en);
+		mgdk_BBPunfix(hn);
+		mgdk_BBPunfix(gn);
+		return -1;
+	}
+	en->count = ngrp;
+	hn->count = ngrp;
+	gn->tsorted = h[2] == 0;
+	gn->trevsorted = ngrp == 1 || n <= 1;
+	gn->tkey = ngrp == n;
+	gn->tnonil = 1;
+	en->tsorted = en->tkey = en->tnonil = 1;
+	en->trevsorted = ngrp == 1;
+	hn->tkey = ngrp == 1;
+	hn->tsorted = hn->trevsorted = ngrp == n || ngrp == 1;
+	hn->tnonil = 1;
 	gn->tmaxpos = ngrp > 0 ? cand_index(ci, fl[1]) : MGDK_BUN_NONE;
 	if (ngrp > 0 && fl[1] - fl[0] == ngrp - 1)
 		setdense(en, fl[0], ngrp);
@@ -536,6 +805,7 @@ mgdk_BATgroup(mgdk_bat **groups, mgdk_bat **extents, mgdk_bat **histo, mgdk_bat 
 		ks.hseq = b->hseqbase;
 		ks.has_g = g != nullptr;
 		ks.g = g && g->ttype == MGDK_oid ? (const oid *) g->theap : nullptr;
+		ks.g8 = ks.g ? img8_get(g) : nullptr;
 		ks.gseq = g ? g->tseqbase : 0;
 		hipStream_t st = stream();
 		// prior group range for the direct table
@@ -561,6 +831,14 @@ mgdk_BATgroup(mgdk_bat **groups, mgdk_bat **extents, mgdk_bat **histo, mgdk_bat 
 			gmax = *hm;
 		} else if (g) {
 			gmax = g->tseqbase + n;
+		}
+		// 1-byte keys under <= 32 prior groups: direct LDS tables
+		static const bool small_on = getenv("MGDK_GROUP_SMALL") ? atoi(getenv("MGDK_GROUP_SMALL")) != 0 : true;
+		if (small_on && ks.w == 1 && ks.kind <= 1 && (!ks.has_g || gmax < 32)) {
+			const uint32_t nslots = (uint32_t) ((ks.has_g ? gmax + 1 : 1) << 8);
+			if (group_small(ks, n, nslots, ci, hseqb, &gn, &en, &hn) < 0)
+				goto fail;
+			goto done;
 		}
 		// low-cardinality path first (falls through when it does not apply)
 		static const bool lds_on = getenv("MGDK_GROUP_LDS") ? atoi(getenv("MGDK_GROUP_LDS")) != 0 : true;

@@ -41,6 +41,13 @@ struct Priv {
 	Heap *theap;      // may be shared between views (BATslice)
 	Heap *tvheap;
 	size_t toff;      // byte offset of b->theap into theap->base
+	// accelerator kept with the column (as GDK keeps hashes / imprints /
+	// order indexes with a BAT): a 1-byte image of an oid tail whose values
+	// are all < 255 (BATgroup's group ids for <= 255 groups), read by the
+	// grouped aggregates and sub-grouping instead of the 8-byte ids; dropped
+	// whenever the tail is written
+	Heap *img8;
+	BUN img8_n;
 };
 Heap *heap_new(size_t bytes);                    // refs = 1
 void heap_decref(Heap *h);
@@ -48,6 +55,10 @@ mgdk_bat *newbat(oid hseq, int tt, BUN cap);     // allocates tail heap
 void setdense(mgdk_bat *b, oid tseq, BUN cnt);
 void share_vheap(mgdk_bat *dst, const mgdk_bat *src);
 int width_of(int tt);
+// the 1-byte image of b's oid tail, or NULL (see Priv::img8)
+const uint8_t *img8_get(const mgdk_bat *b);
+uint8_t *img8_new(mgdk_bat *b);     // allocate an image for b->count values
+void img8_drop(mgdk_bat *b);
 int basetype(int tt);                            // date->int, bit->bte
 const char *atomname(int tt);
 
@@ -113,6 +124,32 @@ int radix_sort_positions32(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, u
 // min(limit, tmax), overflow when |v - b[j]| of the stopping pair > tmax
 int range_bounds_int64(mgdk_bat *r, const int64_t *bvals, const mgdk_bat *p, BUN n, int64_t limit,
 		       uint64_t tmax, bool all, bool preceding);
+
+// BATgroupavg3's result for one group from its exact sum and count
+// (gdk_aggr.c:2070-2095): floor average and remainder, then rounded half
+// away from zero
+inline void
+avg3_of_sum(hge s, int64_t n, int64_t *avg, int64_t *rem)
+{
+	hge q = s / n, r = s % n;
+	if (r < 0) {
+		q -= 1;
+		r += n;
+	}
+	if (r > 0) {
+		if (q < 0) {
+			if (2 * r > n) {
+				q++;
+				r -= n;
+			}
+		} else if (2 * r >= n) {
+			q++;
+			r -= n;
+		}
+	}
+	*avg = (int64_t) q;
+	*rem = (int64_t) r;
+}
 
 // RAII device temporary (not the per-thread scratch)
 struct DevBuf {

@@ -3,7 +3,7 @@
 // calls them (algebra.select x2, thetaselect,
 // projection x2, batcalc.*, aggr.sum; §3.3 Q1: thetaselect, projection x6,
 // group.group, group.subgroup, batcalc.- + * + *, aggr.subsum x4 (+ disc),
-// aggr.subcount).  Used as the exact fallback of the fused kernels and as
+// aggr.subcount, aggr.subavg x3).  Used as the exact fallback of the fused kernels and as
 // the "drop-in" timing of the GDK boundary.
 #include <vector>
 
@@ -58,6 +58,14 @@ q1_opatatime(mgdk_bat *shipdate, mgdk_bat *rf, mgdk_bat *ls, mgdk_bat *qty, mgdk
 	mgdk_bat *s4 = t.add(mgdk_BATgroupsum(ch, g2, e2, nullptr, MGDK_hge, true));
 	mgdk_bat *s5 = t.add(mgdk_BATgroupsum(pd, g2, e2, nullptr, MGDK_hge, true));
 	mgdk_bat *cn = t.add(mgdk_BATgroupcount(pq, g2, e2, nullptr, MGDK_lng, false));
+	// aggr.subavg (3 outputs) of quantity, extendedprice, discount
+	mgdk_bat *av[3], *rm[3], *ac[3];
+	mgdk_bat *avin[3] = {pq, pp, pd};
+	for (int k = 0; k < 3; k++) {
+		if (mgdk_BATgroupavg3(&av[k], &rm[k], &ac[k], avin[k], g2, e2, nullptr, true) < 0)
+			return -1;
+		t.add(av[k]), t.add(rm[k]), t.add(ac[k]);
+	}
 	// extents are positions in the projected (filtered) columns
 	mgdk_bat *krf = t.add(mgdk_BATproject(e2, prf));
 	mgdk_bat *kls = t.add(mgdk_BATproject(e2, pls));
@@ -73,6 +81,13 @@ q1_opatatime(mgdk_bat *shipdate, mgdk_bat *rf, mgdk_bat *ls, mgdk_bat *qty, mgdk
 	std::vector<int64_t> vc(ng);
 	std::vector<oid> ve(ng);
 	std::vector<uint8_t> vr(ng), vl(ng);
+	std::vector<int64_t> va[3], vrm[3];
+	for (int k = 0; k < 3; k++) {
+		va[k].resize(ng);
+		vrm[k].resize(ng);
+		if (mgdk_BATdownload(av[k], va[k].data()) || mgdk_BATdownload(rm[k], vrm[k].data()))
+			return -1;
+	}
 	if (mgdk_BATdownload(s1, v1.data()) || mgdk_BATdownload(s2, v2.data()) || mgdk_BATdownload(s3, v3.data()) ||
 	    mgdk_BATdownload(s4, v4.data()) || mgdk_BATdownload(s5, v5.data()) || mgdk_BATdownload(cn, vc.data()) ||
 	    mgdk_BATdownload(krow, ve.data()) || mgdk_BATdownload(krf, vr.data()) || mgdk_BATdownload(kls, vl.data()))
@@ -89,6 +104,9 @@ q1_opatatime(mgdk_bat *shipdate, mgdk_bat *rf, mgdk_bat *ls, mgdk_bat *qty, mgdk
 		memcpy(r.sum_disc, &v5[k], 16);
 		r.count_order = vc[k];
 		r.first_row = ve[k];
+		r.avg_qty = va[0][k], r.rem_qty = vrm[0][k];
+		r.avg_price = va[1][k], r.rem_price = vrm[1][k];
+		r.avg_disc = va[2][k], r.rem_disc = vrm[2][k];
 	}
 	*ngroups = (int) ng;
 	return 0;

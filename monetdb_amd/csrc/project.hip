@@ -13,26 +13,45 @@ using namespace mgdk;
 
 namespace {
 
+// each wave streams 64 * U consecutive oids per step (element = chunk base
+// + u * 64 + lane): U oid loads in flight, then U independent gathers
 template <typename T>
 __global__ __launch_bounds__(256) void
 k_project(const oid *__restrict__ l, BUN n, const T *__restrict__ r, oid rseq, BUN rcnt, T nilv,
 	  T *__restrict__ out, uint32_t *__restrict__ flags)
 {
-	const BUN stride = (BUN) gridDim.x * blockDim.x * 2;
+	constexpr int U = 8;
+	constexpr BUN CH = 64 * U;
 	uint32_t bad = 0, nil = 0;
-	for (BUN i = ((BUN) blockIdx.x * blockDim.x + threadIdx.x) * 2; i < n; i += stride) {
-		oid o0 = l[i];
-		oid o1 = i + 1 < n ? l[i + 1] : rseq;
-		T v0, v1;
-		if (o0 == MGDK_OID_NIL) { v0 = nilv; nil = 1; }
-		else if (o0 - rseq >= rcnt) { v0 = nilv; bad = 1; }
-		else v0 = r[o0 - rseq];
-		if (o1 == MGDK_OID_NIL) { v1 = nilv; nil = 1; }
-		else if (o1 - rseq >= rcnt) { v1 = nilv; bad = 1; }
-		else v1 = r[o1 - rseq];
-		out[i] = v0;
-		if (i + 1 < n)
-			out[i + 1] = v1;
+	const unsigned lane = __lane_id();
+	const BUN nwaves = (BUN) gridDim.x * (blockDim.x / 64);
+	for (BUN ch = (BUN) blockIdx.x * (blockDim.x / 64) + (threadIdx.x / 64); ch * CH < n; ch += nwaves) {
+		const BUN i0 = ch * CH + lane;
+		oid o[U];
+		// unconditional loads at clamped indices, masked afterwards (a load
+		// under a divergent branch is waited for before the branch joins)
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const BUN i = i0 + (BUN) u * 64;
+			o[u] = l[i < n ? i : n - 1];
+		}
+		T v[U];
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const bool isnil = o[u] == MGDK_OID_NIL, out_of = !isnil && o[u] - rseq >= rcnt;
+			const BUN p = (isnil || out_of) ? 0 : o[u] - rseq;
+			v[u] = r[p];     // r has >= 1 readable element (the host passes a dummy for empty r)
+			if (isnil || out_of)
+				v[u] = nilv;
+			nil |= isnil;
+			bad |= out_of;
+		}
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const BUN i = i0 + (BUN) u * 64;
+			if (i < n)
+				out[i] = v[u];
+		}
 	}
 	bad = block_reduce(bad, [](uint32_t x, uint32_t y) { return x | y; });
 	nil = block_reduce(nil, [](uint32_t x, uint32_t y) { return x | y; });
@@ -69,7 +88,9 @@ launch(const oid *l, BUN n, const void *r, oid rseq, BUN rcnt, const void *nilp,
 {
 	T nilv;
 	memcpy(&nilv, nilp, sizeof(T));
-	unsigned g = grid_for(n, 512, 256 * 16);
+	if (rcnt == 0)
+		r = meta_buf();   // every non-nil oid is out of range; the gather still reads r[0]
+	unsigned g = grid_for(n, 256 * 8, 256 * 16);
 	hipLaunchKernelGGL((k_project<T>), dim3(g), dim3(256), 0, stream(), l, n, (const T *) r, rseq, rcnt,
 			   nilv, (T *) out, flags);
 }

@@ -328,10 +328,43 @@ newbat(oid hseq, int tt, BUN cap)
 	return b;
 }
 
+const uint8_t *
+img8_get(const mgdk_bat *b)
+{
+	const Priv *p = (const Priv *) b->priv;
+	if (p == nullptr || p->img8 == nullptr || b->ttype != MGDK_oid || p->img8_n != b->count)
+		return nullptr;
+	return (const uint8_t *) p->img8->base;
+}
+
+uint8_t *
+img8_new(mgdk_bat *b)
+{
+	Priv *p = (Priv *) b->priv;
+	img8_drop(b);
+	p->img8 = heap_new(b->count ? b->count : 1);
+	if (p->img8 == nullptr)
+		return nullptr;
+	p->img8_n = b->count;
+	return (uint8_t *) p->img8->base;
+}
+
+void
+img8_drop(mgdk_bat *b)
+{
+	Priv *p = (Priv *) b->priv;
+	if (p && p->img8) {
+		heap_decref(p->img8);
+		p->img8 = nullptr;
+		p->img8_n = 0;
+	}
+}
+
 void
 setdense(mgdk_bat *b, oid tseq, BUN cnt)
 {
 	Priv *p = (Priv *) b->priv;
+	img8_drop(b);
 	heap_decref(p->theap);
 	p->theap = nullptr;
 	b->theap = nullptr;
@@ -778,6 +811,7 @@ mgdk_BBPunfix(mgdk_bat *b)
 	if (p) {
 		heap_decref(p->theap);
 		heap_decref(p->tvheap);
+		heap_decref(p->img8);
 		delete p;
 	}
 	free(b);
@@ -792,6 +826,7 @@ mgdk_BATupload(mgdk_bat *b, const void *host, mgdk_BUN n)
 	}
 	Priv *p = (Priv *) b->priv;
 	size_t bytes = n * (size_t) b->twidth;
+	img8_drop(b);
 	// a heap shared with views (refs > 1) is never written in place
 	if (p->theap == nullptr || p->theap->refs != 1 ||
 	    p->theap->size < bytes + ((char *) b->theap - (char *) p->theap->base)) {
@@ -917,6 +952,7 @@ mgdk_BATappend(mgdk_bat *b, mgdk_bat *n, mgdk_bat *s, bool force)
 	{
 		Priv *p = (Priv *) b->priv;
 		hipStream_t st = stream();
+		img8_drop(b);
 		const int tt = b->ttype == MGDK_void ? MGDK_oid : b->ttype;
 		const size_t w = (size_t) width_of(tt);
 		const BUN total = b->count + cnt;

@@ -971,6 +971,14 @@ mgdk_q1_fused(mgdk_bat *shipdate, mgdk_bat *returnflag, mgdk_bat *linestatus, mg
 		memcpy(r.sum_charge, x + 6, 16);
 		memcpy(r.sum_disc, x + 8, 16);
 		r.count_order = (int64_t) x[10];
+		// aggr.subavg: BATgroupavg3 of the exact group sums
+		hge sq, sp, sd;
+		memcpy(&sq, x + 0, 16);
+		memcpy(&sp, x + 2, 16);
+		memcpy(&sd, x + 8, 16);
+		avg3_of_sum(sq, r.count_order, &r.avg_qty, &r.rem_qty);
+		avg3_of_sum(sp, r.count_order, &r.avg_price, &r.rem_price);
+		avg3_of_sum(sd, r.count_order, &r.avg_disc, &r.rem_disc);
 	}
 	*ngroups = (int) K;
 	return 0;

@@ -49,7 +49,9 @@ class Q1Row(C.Structure):
                 ("sum_qty", C.c_uint64 * 2), ("sum_base_price", C.c_uint64 * 2),
                 ("sum_disc_price", C.c_uint64 * 2), ("sum_charge", C.c_uint64 * 2),
                 ("sum_disc", C.c_uint64 * 2), ("count_order", C.c_int64),
-                ("first_row", C.c_uint64)]
+                ("first_row", C.c_uint64),
+                ("avg_qty", C.c_int64), ("avg_price", C.c_int64), ("avg_disc", C.c_int64),
+                ("rem_qty", C.c_int64), ("rem_price", C.c_int64), ("rem_disc", C.c_int64)]
 
 
 P = C.POINTER(MgdkBat)
@@ -698,7 +700,9 @@ def q1_fused(cols, dmax, maxgroups=64, fused=True):
                         sum_qty=hge_to_int(r.sum_qty), sum_base_price=hge_to_int(r.sum_base_price),
                         sum_disc_price=hge_to_int(r.sum_disc_price),
                         sum_charge=hge_to_int(r.sum_charge), sum_disc=hge_to_int(r.sum_disc),
-                        count_order=r.count_order, first_row=r.first_row))
+                        count_order=r.count_order, first_row=r.first_row,
+                        avg_qty=r.avg_qty, avg_price=r.avg_price, avg_disc=r.avg_disc,
+                        rem_qty=r.rem_qty, rem_price=r.rem_price, rem_disc=r.rem_disc))
     return res
 
 

@@ -342,7 +342,8 @@ def _q1_rows(rows):
     out = []
     for r in rows:
         out.append((r["returnflag"], r["linestatus"], r["sum_qty"], r["sum_base_price"],
-                    r["sum_disc_price"], r["sum_charge"], r["count_order"]))
+                    r["sum_disc_price"], r["sum_charge"], r["count_order"],
+                    r["avg_qty"], r["rem_qty"], r["avg_price"], r["rem_price"], r["avg_disc"], r["rem_disc"]))
     return sorted(out)
 
 
