@@ -408,10 +408,19 @@ template <> struct VTy<16> { typedef hge T; };
 // VW: value width, a template parameter so that the U loads of a step are
 // straight-line code (a runtime width switch puts every load in its own
 // block and the compiler then waits for each one before the next)
+// per-wave partial of one group (k_gaggr_k writes them, k_gaggr_fin sums
+// them): no same-word atomics from thousands of waves, which serialise at
+// the L2 (~88 per microsecond per word)
+struct GPart {
+	unsigned long long lo, hi, cnt, fv, ln;
+	long long mn, mx;
+	unsigned long long mxa;
+};
+
 template <int K, bool MM, bool POS, int VW, typename GT>
 __global__ __launch_bounds__(256) void
 k_gaggr_k(const void *base, int w, oid off, const GT *gids, oid gseq, oid gmin, BUN ngrp, BUN n, int what,
-	  bool count_all, GAcc acc, unsigned long long *maxabs)
+	  bool count_all, GPart *parts)
 {
 	constexpr bool W16 = VW == 16;
 	typedef typename VTy<VW>::T VT;
@@ -443,22 +452,46 @@ k_gaggr_k(const void *base, int w, oid off, const GT *gids, oid gseq, oid gmin, 
 	const uint32_t gm = (uint32_t) gmin;
 	const unsigned lane = __lane_id();
 	const BUN nwaves = (BUN) gridDim.x * (blockDim.x / 64);
+	// 1-byte ids: a lane takes U consecutive rows (one 16- or 8-byte load of
+	// ids, U consecutive values); 8-byte ids: row = chunk + u * 64 + lane
+	constexpr bool LC = sizeof(GT) == 1;
 	for (BUN ch = (BUN) blockIdx.x * (blockDim.x / 64) + (threadIdx.x / 64); ch * CH < n; ch += nwaves) {
-		const BUN i0 = ch * CH + lane;
+		const BUN i0 = LC ? ch * CH + (BUN) lane * U : ch * CH + lane;
+		const BUN du = LC ? 1 : 64;
 		uint32_t gi[U];
 		hge v[U];
 		bool nil[U];
+		if constexpr (LC) {
+			if (i0 + U <= n) {
+				uint32_t wds[U / 4];
+				if constexpr (U == 16) {
+					const uint4 q = *(const uint4 *) ((const uint8_t *) gids + i0);
+					wds[0] = q.x, wds[1] = q.y, wds[2] = q.z, wds[3] = q.w;
+				} else {
+					const uint2 q = *(const uint2 *) ((const uint8_t *) gids + i0);
+					wds[0] = q.x, wds[1] = q.y;
+				}
+#pragma unroll
+				for (int u = 0; u < U; u++)
+					gi[u] = ((wds[u / 4] >> (8 * (u % 4))) & 0xffu) - gm;
+			} else {
+#pragma unroll
+				for (int u = 0; u < U; u++) {
+					const BUN i = i0 + (BUN) u;
+					gi[u] = i < n ? (uint32_t) gids[i] - gm : ~0u;
+				}
+			}
+		}
 		// every load is issued unconditionally (at a clamped index) and masked
 		// afterwards: a load under a divergent branch makes the compiler wait
 		// for it before the branch joins, which serialises the U loads
 #pragma unroll
 		for (int u = 0; u < U; u++) {
-			const BUN i = i0 + (BUN) u * 64;
+			const BUN i = i0 + (BUN) u * du;
 			const bool ok = i < n;
 			const BUN ic = ok ? i : n - 1;
-			if (sizeof(GT) == 1) {
-				const uint32_t g = (uint32_t) gids[ic] - gm;
-				gi[u] = ok ? g : ~0u;
+			if (LC) {
+				;
 			} else {
 				const oid g = gids ? (oid) gids[ic] : gseq + ic;
 				gi[u] = (!ok || g < gmin || g - gmin >= ngrp) ? ~0u : (uint32_t) (g - gmin);
@@ -475,7 +508,7 @@ k_gaggr_k(const void *base, int w, oid off, const GT *gids, oid gseq, oid gmin, 
 		}
 #pragma unroll
 		for (int u = 0; u < U; u++) {
-			const BUN i = i0 + (BUN) u * 64;
+			const BUN i = i0 + (BUN) u * du;
 			if (gi[u] >= (uint32_t) ngrp)
 				continue;
 			if (nil[u]) {
@@ -539,28 +572,66 @@ k_gaggr_k(const void *base, int w, oid off, const GT *gids, oid gseq, oid gmin, 
 				xk = x2 > xk ? x2 : xk;
 			}
 		}
-		if (__lane_id() == 0 && (BUN) k < ngrp) {
-			if (ck) {
-				if (what & AGG_SUM)
-					atomic_add128(&acc.sum[2 * k], sk);
-				atomicAdd(&acc.cnt[k], ck);
-			}
-			if (POS && (what & AGG_POS) && fk != ~0ull)
-				atomicMin(&acc.firstval[k], fk);
-			if (POS && (what & AGG_POS) && lk)
-				atomicMax(&acc.lastnil[k], lk);
-			if (MM && (what & AGG_MINMAX) && ck) {
-				atomicMin(&acc.mn[k], nk);
-				atomicMax(&acc.mx[k], xk);
-			}
+		if (__lane_id() == 0) {
+			GPart pp;
+			pp.lo = (unsigned long long) (uhge) sk;
+			pp.hi = (unsigned long long) ((uhge) sk >> 64);
+			pp.cnt = ck;
+			pp.fv = fk;
+			pp.ln = lk;
+			pp.mn = MM ? nk : INT64_MAX;
+			pp.mx = MM ? xk : INT64_MIN;
+			pp.mxa = 0;
+			parts[((BUN) blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * K + k] = pp;
 		}
 	}
 	for (int o = 32; o > 0; o >>= 1) {
 		const unsigned long long t = __shfl_xor(mxa, o);
 		mxa = t > mxa ? t : mxa;
 	}
-	if (__lane_id() == 0 && mxa)
-		atomicMax(maxabs, mxa);
+	if (__lane_id() == 0)
+		parts[((BUN) blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * K].mxa = mxa;
+}
+
+// one workgroup per group: the sum of the per-wave partials into acc
+__global__ __launch_bounds__(256) void
+k_gaggr_fin(const GPart *parts, BUN nwaves, int K, BUN ngrp, GAcc acc, unsigned long long *maxabs)
+{
+	const int k = blockIdx.x;
+	uhge s = 0;
+	unsigned long long c = 0, fv = ~0ull, ln = 0, mxa = 0;
+	long long mn = INT64_MAX, mx = INT64_MIN;
+	for (BUN wv = threadIdx.x; wv < nwaves; wv += blockDim.x) {
+		const GPart &p = parts[wv * K + k];
+		s += ((uhge) p.hi << 64) | p.lo;
+		c += p.cnt;
+		fv = p.fv < fv ? p.fv : fv;
+		ln = p.ln > ln ? p.ln : ln;
+		mn = p.mn < mn ? p.mn : mn;
+		mx = p.mx > mx ? p.mx : mx;
+		if (k == 0)
+			mxa = p.mxa > mxa ? p.mxa : mxa;
+	}
+	s = (uhge) block_sum128((hge) s);
+	c = block_reduce(c, [](unsigned long long x, unsigned long long y) { return x + y; });
+	fv = block_reduce(fv, [](unsigned long long x, unsigned long long y) { return x < y ? x : y; });
+	ln = block_reduce(ln, [](unsigned long long x, unsigned long long y) { return x > y ? x : y; });
+	mn = block_reduce(mn, [](long long x, long long y) { return x < y ? x : y; });
+	mx = block_reduce(mx, [](long long x, long long y) { return x > y ? x : y; });
+	mxa = block_reduce(mxa, [](unsigned long long x, unsigned long long y) { return x > y ? x : y; });
+	if (threadIdx.x == 0) {
+		if ((BUN) k < ngrp) {
+			acc.sum[2 * k] = (unsigned long long) s;
+			acc.sum[2 * k + 1] = (unsigned long long) (s >> 64);
+			acc.cnt[k] = c;
+			acc.firstval[k] = fv;
+			acc.lastnil[k] = ln;
+			acc.mn[k] = mn;
+			acc.mx[k] = mx;
+		}
+		if (k == 0)
+			*maxabs = mxa;
+	}
 }
 
 struct AggrInit {
@@ -719,10 +790,11 @@ run_gaggr(const AggrInit &a, mgdk_bat *b, int what, bool count_all, GRes &r)
 	const void *vbase = (what == 0 && count_all && ng <= 8) ? nullptr : b->theap;
 	if (a.ci.n) {
 #define GK4(K_, MM_, POS_, VW_) do { \
+		kk = K_; \
 		if (a.g8 && a.min < 256 && a.min + ng <= 256) \
-			hipLaunchKernelGGL((k_gaggr_k<K_, MM_, POS_, VW_, uint8_t>), g, blk, 0, st, vbase, b->twidth, off, a.g8, a.gseq, a.min, ng, a.ci.n, what, count_all, acc, maxabs); \
+			hipLaunchKernelGGL((k_gaggr_k<K_, MM_, POS_, VW_, uint8_t>), g, blk, 0, st, vbase, b->twidth, off, a.g8, a.gseq, a.min, ng, a.ci.n, what, count_all, parts.as<GPart>()); \
 		else \
-			hipLaunchKernelGGL((k_gaggr_k<K_, MM_, POS_, VW_, oid>), g, blk, 0, st, vbase, b->twidth, off, a.gids, a.gseq, a.min, ng, a.ci.n, what, count_all, acc, maxabs); } while (0)
+			hipLaunchKernelGGL((k_gaggr_k<K_, MM_, POS_, VW_, oid>), g, blk, 0, st, vbase, b->twidth, off, a.gids, a.gseq, a.min, ng, a.ci.n, what, count_all, parts.as<GPart>()); } while (0)
 #define GK3(K_, MM_, POS_) do { switch (vbase ? b->twidth : 0) { \
 		case 0: GK4(K_, MM_, POS_, 0); break; \
 		case 1: GK4(K_, MM_, POS_, 1); break; \
@@ -733,10 +805,20 @@ run_gaggr(const AggrInit &a, mgdk_bat *b, int what, bool count_all, GRes &r)
 #define GK(K_) do { if (what & AGG_MINMAX) GK3(K_, true, true); \
 		else if (what & AGG_POS) GK3(K_, false, true); \
 		else GK3(K_, false, false); } while (0)
-		if (ng <= 4)
-			GK(4);
-		else if (ng <= 8)
-			GK(8);
+		if (ng <= 8) {
+			const BUN nw = (BUN) g.x * 4;
+			DevBuf parts(nw * 8 * sizeof(GPart));
+			if (parts.p == nullptr)
+				return -1;
+			int kk = 0;
+			if (ng <= 4)
+				GK(4);
+			else
+				GK(8);
+			hipLaunchKernelGGL(k_gaggr_fin, dim3(kk), dim3(256), 0, st, parts.as<GPart>(), nw, kk, ng, acc, maxabs);
+			if (!sync())
+				return -1;
+		}
 		else
 			hipLaunchKernelGGL((k_gaggr<0>), g, blk, 0, st, b->theap, b->twidth, off, a.gids, a.gseq, a.min, ng, a.ci.n, what, count_all, acc, maxabs);
 	}

@@ -618,20 +618,149 @@ k_gs_assign(KeySrc s, BUN n, const uint32_t *gmap, uint32_t nslots, uint32_t ngr
 	if (__any(uns) && lane == 0)
 		publish_or(unsorted, 1u);
 	if (K > 0) {
+		// per-workgroup counts to histo_part[tile][k] (summed by k_gs_hist):
+		// no same-word atomics from every wave
+		__shared__ uint32_t s_c[4][K > 0 ? K : 1];
 #pragma unroll
 		for (int k = 0; k < K; k++) {
 			uint32_t c = cnt[k];
 			for (int o = 32; o > 0; o >>= 1)
 				c += __shfl_xor(c, o);
-			if (lane == 0 && c && (uint32_t) k < ngrp)
-				atomicAdd(&histo[k], (unsigned long long) c);
+			if (lane == 0)
+				s_c[tid / 64][k] = c;
 		}
+		__syncthreads();
+		if (tid < (unsigned) K)
+			histo[(BUN) blockIdx.x * K + tid] = (unsigned long long) s_c[0][tid] + s_c[1][tid] + s_c[2][tid] + s_c[3][tid];
 	} else {
 		__syncthreads();
 		for (uint32_t q = tid; q < ngrp; q += blockDim.x)
 			if (lh[q])
 				atomicAdd(&histo[q], (unsigned long long) lh[q]);
 	}
+}
+
+// modes 0 / 1 with 16-byte aligned keys: a lane takes 16 consecutive rows
+// (one 16-byte load of keys and of prior ids, 16-byte stores of ids and of
+// the image), the order flag within the lane and across lanes by a shuffle
+template <int K, int MODE>
+__global__ __launch_bounds__(256) void
+k_gs_assign16(KeySrc s, BUN n, const uint32_t *gmap, uint32_t nslots, uint32_t ngrp, oid *gid, uint8_t *img,
+	      unsigned long long *histo, uint32_t *unsorted)
+{
+	extern __shared__ __attribute__((aligned(16))) uint32_t lmap[];   // [nslots] + [ngrp] histogram (K == 0)
+	uint32_t *lh = lmap + nslots;
+	const unsigned tid = threadIdx.x, lane = __lane_id();
+	for (uint32_t q = tid; q < nslots; q += blockDim.x)
+		lmap[q] = gmap[q];
+	if (K == 0)
+		for (uint32_t q = tid; q < ngrp; q += blockDim.x)
+			lh[q] = 0;
+	__syncthreads();
+	uint32_t cnt[K > 0 ? K : 1];
+#pragma unroll
+	for (int k = 0; k < (K > 0 ? K : 1); k++)
+		cnt[k] = 0;
+	const BUN a = (BUN) blockIdx.x * GS_TILE, e = min(n, a + GS_TILE);
+	uint32_t uns = 0;
+	const uint8_t *keys = (const uint8_t *) s.base + s.off;
+	for (BUN i0 = a + (BUN) tid * 16; i0 - (BUN) tid * 16 < e; i0 += (BUN) blockDim.x * 16) {
+		uint32_t g[16];
+		const bool full = i0 + 16 <= e;
+		if (full) {
+			const uint4 kq = *(const uint4 *) (keys + i0);
+			uint4 gq = make_uint4(0, 0, 0, 0);
+			if (MODE == 1)
+				gq = *(const uint4 *) (s.g8 + i0);
+			const uint32_t kw[4] = {kq.x, kq.y, kq.z, kq.w}, gw[4] = {gq.x, gq.y, gq.z, gq.w};
+#pragma unroll
+			for (int u = 0; u < 16; u++) {
+				const uint32_t k = (kw[u / 4] >> (8 * (u % 4))) & 0xffu;
+				const uint32_t pg = (gw[u / 4] >> (8 * (u % 4))) & 0xffu;
+				g[u] = lmap[(pg << 8) | k];
+			}
+			uint4 *go = (uint4 *) (gid + i0);
+#pragma unroll
+			for (int u = 0; u < 16; u += 2) {
+				go[u / 2] = make_uint4(g[u], 0, g[u + 1], 0);
+			}
+			if (img) {
+				uint32_t iw[4] = {0, 0, 0, 0};
+#pragma unroll
+				for (int u = 0; u < 16; u++)
+					iw[u / 4] |= (g[u] & 0xffu) << (8 * (u % 4));
+				*(uint4 *) (img + i0) = make_uint4(iw[0], iw[1], iw[2], iw[3]);
+			}
+		} else {
+#pragma unroll
+			for (int u = 0; u < 16; u++) {
+				const BUN i = i0 + u;
+				g[u] = 0;
+				if (i < e) {
+					g[u] = lmap[gs_slot<MODE>(s, i)];
+					gid[i] = g[u];
+					if (img)
+						img[i] = (uint8_t) g[u];
+				}
+			}
+		}
+#pragma unroll
+		for (int u = 0; u < 16; u++) {
+			const bool ok = i0 + u < e;
+			if (K > 0) {
+#pragma unroll
+				for (int k = 0; k < K; k++)
+					cnt[k] += ok && g[u] == (uint32_t) k;
+			} else if (ok) {
+				atomicAdd(&lh[g[u]], 1u);
+			}
+			if (u > 0 && ok && g[u - 1] > g[u])
+				uns = 1;
+		}
+		// the row before this lane's first: the previous lane's last row, or
+		// (lane 0) looked up directly
+		uint32_t gp = __shfl_up(g[15], 1);
+		if (lane == 0 && i0 > 0 && i0 < e)
+			gp = lmap[gs_slot<MODE>(s, i0 - 1)];
+		if (i0 > 0 && i0 < e && gp > g[0])
+			uns = 1;
+	}
+	if (__any(uns) && lane == 0)
+		publish_or(unsorted, 1u);
+	if (K > 0) {
+		// per-workgroup counts to histo_part[tile][k] (summed by k_gs_hist):
+		// no same-word atomics from every wave
+		__shared__ uint32_t s_c[4][K > 0 ? K : 1];
+#pragma unroll
+		for (int k = 0; k < K; k++) {
+			uint32_t c = cnt[k];
+			for (int o = 32; o > 0; o >>= 1)
+				c += __shfl_xor(c, o);
+			if (lane == 0)
+				s_c[tid / 64][k] = c;
+		}
+		__syncthreads();
+		if (tid < (unsigned) K)
+			histo[(BUN) blockIdx.x * K + tid] = (unsigned long long) s_c[0][tid] + s_c[1][tid] + s_c[2][tid] + s_c[3][tid];
+	} else {
+		__syncthreads();
+		for (uint32_t q = tid; q < ngrp; q += blockDim.x)
+			if (lh[q])
+				atomicAdd(&histo[q], (unsigned long long) lh[q]);
+	}
+}
+
+// histo[k] = the sum of the per-tile counts (one workgroup per group)
+__global__ __launch_bounds__(256) void
+k_gs_hist(const unsigned long long *part, BUN tiles, int K, BUN ngrp, unsigned long long *histo)
+{
+	const int k = blockIdx.x;
+	unsigned long long c = 0;
+	for (BUN t = threadIdx.x; t < tiles; t += blockDim.x)
+		c += part[t * K + k];
+	c = block_reduce(c, [](unsigned long long x, unsigned long long y) { return x + y; });
+	if (threadIdx.x == 0 && (BUN) k < ngrp)
+		histo[k] = c;
 }
 
 int
@@ -671,9 +800,22 @@ group_small(const KeySrc &ks, BUN n, uint32_t nslots, const Cand &ci, oid hseqb,
 		mgdk_BBPunfix(gn);
 		return -1;
 	}
+	DevBuf hpart((BUN) tiles * 8 * 8);
+	if (hpart.p == nullptr) {
+		mgdk_BBPunfix(en);
+		mgdk_BBPunfix(hn);
+		mgdk_BBPunfix(gn);
+		return -1;
+	}
+	unsigned long long *hdst = ngrp <= 8 ? hpart.as<unsigned long long>() : (unsigned long long *) hn->theap;
+	const int kk = ngrp <= 1 ? 1 : ngrp <= 4 ? 4 : 8;
 #define GSA2(K_, M_) hipLaunchKernelGGL((k_gs_assign<K_, M_>), dim3(tiles), dim3(256), (nslots + ((K_) == 0 ? ngrp : 0)) * 4, st, ks, n, gmap.as<uint32_t>(), nslots, ngrp, \
-				   (oid *) gn->theap, img, (unsigned long long *) hn->theap, &m[2])
-#define GSA(K_) do { if (mode == 0) GSA2(K_, 0); else if (mode == 1) GSA2(K_, 1); else GSA2(K_, 2); } while (0)
+				   (oid *) gn->theap, img, hdst, &m[2])
+#define GSA16(K_, M_) hipLaunchKernelGGL((k_gs_assign16<K_, M_>), dim3(tiles), dim3(256), (nslots + ((K_) == 0 ? ngrp : 0)) * 4, st, ks, n, gmap.as<uint32_t>(), nslots, ngrp, \
+				   (oid *) gn->theap, img, hdst, &m[2])
+	const bool al16 = (((uintptr_t) ks.base + ks.off) & 15) == 0;
+#define GSA(K_) do { if (mode == 0 && al16) GSA16(K_, 0); else if (mode == 1 && al16) GSA16(K_, 1); \
+		else if (mode == 0) GSA2(K_, 0); else if (mode == 1) GSA2(K_, 1); else GSA2(K_, 2); } while (0)
 	if (ngrp <= 1)
 		GSA(1);
 	else if (ngrp <= 4)
@@ -684,6 +826,10 @@ group_small(const KeySrc &ks, BUN n, uint32_t nslots, const Cand &ci, oid hseqb,
 		GSA(0);
 #undef GSA
 #undef GSA2
+#undef GSA16
+	if (ngrp <= 8 && ngrp > 0)
+		hipLaunchKernelGGL(k_gs_hist, dim3(kk), dim3(256), 0, st, hpart.as<unsigned long long>(), (BUN) tiles, kk, (BUN) ngrp,
+				   (unsigned long long *) hn->theap);
 	oid fl[2] = {0, 0};
 	if (!hip_ok(hipMemcpyAsync(h, m, 12, hipMemcpyDeviceToHost, st), "memcpy") ||
 	    (ngrp > 0 && (!hip_ok(hipMemcpyAsync(&fl[0], ext.p, 8, hipMemcpyDeviceToHost, st), "memcpy") ||
