@@ -26,6 +26,9 @@
 // cannot overflow.
 #include <type_traits>
 
+#include <cfloat>
+#include <cstdio>
+
 #include "mgdk_internal.h"
 
 using namespace mgdk;
@@ -1204,6 +1207,351 @@ out:
 	return rc;
 }
 
+// ---- GDKanalyticalsum over flt / dbl (gdk_analytic_func.c:1795-1817,
+// :1930-1950).  Float addition is not associative, so the order is the
+// reference's: frames 3 / 4 add row by row (one lane replays one partition),
+// general frames walk the reference's fanout-16 tree (built for every
+// partition at once, one launch per level) in its own order, every add with
+// ADD_WITH_CHECK in the result type T2 (gdk_calc_private.h:53-67); frame 5
+// is dofsum: the exact sum of the partition rounded once (the grouped exact
+// float sum with the partition as the group).
+template <typename T2>
+struct FSum {
+	T2 v;
+	int nil;
+	__device__ __forceinline__ void zero() { v = 0; nil = 1; }
+	// cur = x + cur (ADD_WITH_CHECK(x, cur, ...)); false on overflow
+	__device__ __forceinline__ bool fold(const FSum &x)
+	{
+		if (x.nil)
+			return true;
+		if (nil) {
+			v = x.v;
+			nil = 0;
+			return true;
+		}
+		const T2 mx = sizeof(T2) == 4 ? (T2) FLT_MAX : (T2) DBL_MAX;
+		if (v < 1) {
+			if (-mx - v > x.v)
+				return false;
+		} else if (mx - v < x.v) {
+			return false;
+		}
+		v = x.v + v;
+		return true;
+	}
+	template <typename T1>
+	__device__ __forceinline__ void leaf(const T1 *b, BUN i)
+	{
+		const T1 x = b[i];
+		nil = x != x;
+		v = nil ? (T2) 0 : (T2) x;
+	}
+};
+
+template <typename T1, typename T2>
+__global__ __launch_bounds__(64) void
+k_fsum_replay(const T1 *b, Starts part, const int8_t *o, bool forward, T2 *out, uint32_t *flags)
+{
+	const BUN k = (BUN) blockIdx.x * blockDim.x + threadIdx.x;
+	uint32_t fl = 0;
+	if (k < part.m) {
+		const BUN ps = part.at(k), pe = part.end_of(k);
+		FSum<T2> cur;
+		cur.zero();
+		if (forward) {
+			BUN j = ps;
+			for (BUN r = ps; r < pe && !(fl & 2); r++) {
+				FSum<T2> x;
+				x.leaf(b, r);
+				if (!cur.fold(x))
+					fl |= 2;
+				if (r + 1 == pe || o[r + 1]) {
+					const T2 w = cur.nil ? (T2) __builtin_nan("") : cur.v;
+					fl |= cur.nil;
+					for (; j <= r; j++)
+						out[j] = w;
+				}
+			}
+		} else if (pe > ps) {
+			BUN l = pe - 1;
+			for (BUN j = pe - 1;; j--) {
+				FSum<T2> x;
+				x.leaf(b, j);
+				if (!cur.fold(x)) {
+					fl |= 2;
+					break;
+				}
+				if (o[j] || j == ps) {
+					const T2 w = cur.nil ? (T2) __builtin_nan("") : cur.v;
+					fl |= cur.nil;
+					for (;; l--) {
+						out[l] = w;
+						if (l == j)
+							break;
+					}
+					if (j == ps)
+						break;
+					l = j - 1;
+				}
+			}
+		}
+	}
+	if (fl)
+		atomicOr(flags, fl);
+}
+
+template <typename T1, typename T2>
+__global__ __launch_bounds__(256) void
+k_fsum_row(const T1 *b, BUN n, T2 *out, uint32_t *flags)
+{
+	uint32_t hasnil = 0;
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		const T1 v = b[i];
+		out[i] = (T2) v;
+		hasnil |= v != v;
+	}
+	hasnil = block_reduce(hasnil, [](uint32_t x, uint32_t y) { return x | y; });
+	if (threadIdx.x == 0)
+		publish_or(flags, hasnil);
+}
+
+// frame 5: every row gets its partition's dofsum (psum: dbl per partition);
+// a flt result is the dbl sum rounded to flt (and an infinite one overflows)
+template <typename T2>
+__global__ __launch_bounds__(256) void
+k_fsum_bcast(const double *psum, const uint32_t *pidx, BUN n, T2 *out, uint32_t *flags)
+{
+	uint32_t fl = 0;
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		const double d = psum[pidx[i]];
+		const T2 w = (T2) d;
+		out[i] = w;
+		if (d != d)
+			fl |= 1;
+		else if (w - w != w - w)   // infinite after rounding
+			fl |= 4;
+	}
+	fl = block_reduce(fl, [](uint32_t x, uint32_t y) { return x | y; });
+	if (threadIdx.x == 0)
+		publish_or(flags, fl);
+}
+
+__global__ __launch_bounds__(256) void
+k_pidx_oid(const uint32_t *pidx, BUN n, oid *g)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
+		g[i] = pidx[i];
+}
+
+template <typename T1, typename T2>
+__global__ __launch_bounds__(256) void
+k_fsum_tree_level(const T1 *b, Starts part, const uint32_t *pidx, AvgTree t, int L, uint32_t *flags)
+{
+	using N = FSum<T2>;
+	const int sh = 4 * L, shc = sh - 4;
+	N *out = (N *) t.lvl[L];
+	const N *child = L > 1 ? (const N *) t.lvl[L - 1] : nullptr;
+	uint32_t fl = 0;
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < part.n; i += (BUN) gridDim.x * blockDim.x) {
+		const BUN k = pidx[i], ps = part.at(k);
+		const BUN rel = i - ps;
+		if (rel & (((BUN) 1 << sh) - 1))
+			continue;
+		const BUN nc = part.end_of(k) - ps;
+		const BUN ncl = (nc + ((BUN) 1 << shc) - 1) >> shc;
+		const BUN c0 = (rel >> sh) * 16, c1 = min(c0 + 16, ncl);
+		N acc;
+		acc.zero();
+		for (BUN c = c0; c < c1; c++) {
+			N x;
+			if (L == 1)
+				x.leaf(b, ps + c);
+			else
+				x = child[(ps >> shc) + k + c];
+			if (!acc.fold(x))
+				fl |= 2;
+		}
+		out[(ps >> sh) + k + (rel >> sh)] = acc;
+	}
+	fl = block_reduce(fl, [](uint32_t x, uint32_t y) { return x | y; });
+	if (threadIdx.x == 0)
+		publish_or(flags, fl);
+}
+
+template <typename T1, typename T2>
+__global__ __launch_bounds__(256) void
+k_fsum_tree_query(const T1 *b, Starts part, const uint32_t *pidx, AvgTree t, const oid *S, const oid *E, T2 *out,
+		  uint32_t *flags)
+{
+	using N = FSum<T2>;
+	uint32_t fl = 0;
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < part.n; i += (BUN) gridDim.x * blockDim.x) {
+		const BUN k = pidx[i], ps = part.at(k), nc = part.end_of(k) - ps;
+		BUN begin = S[i] > ps ? min((BUN) S[i] - ps, nc) : 0;
+		BUN tend = E[i] > ps ? min((BUN) E[i] - ps, nc) : 0;
+		N acc;
+		acc.zero();
+		if (begin < tend) {
+			for (int L = 0; L <= t.nlev; L++) {
+				const N *lv = L ? (const N *) t.lvl[L] + ((ps >> (4 * L)) + k) : nullptr;
+				auto node = [&](BUN pos) {
+					N x;
+					if (L == 0)
+						x.leaf(b, ps + pos);
+					else
+						x = lv[pos];
+					return x;
+				};
+				BUN pb = begin / 16, pe = tend / 16;
+				if (pb == pe) {
+					for (BUN pos = begin; pos < tend; pos++)
+						if (!acc.fold(node(pos)))
+							fl |= 2;
+					break;
+				}
+				const BUN gb = pb * 16;
+				if (begin != gb) {
+					for (BUN pos = begin; pos < gb + 16; pos++)
+						if (!acc.fold(node(pos)))
+							fl |= 2;
+					pb++;
+				}
+				const BUN ge = pe * 16;
+				if (tend != ge)
+					for (BUN pos = ge; pos < tend; pos++)
+						if (!acc.fold(node(pos)))
+							fl |= 2;
+				begin = pb;
+				tend = pe;
+			}
+		}
+		out[i] = acc.nil ? (T2) __builtin_nan("") : acc.v;
+		fl |= acc.nil;
+	}
+	fl = block_reduce(fl, [](uint32_t x, uint32_t y) { return x | y; });
+	if (threadIdx.x == 0)
+		publish_or(flags, fl);
+}
+
+template <typename T1, typename T2>
+int
+run_fsum(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e, int frame_type)
+{
+	const BUN n = b->count;
+	hipStream_t st = stream();
+	const T1 *bv = (const T1 *) b->theap;
+	T2 *out = (T2 *) r->theap;
+	const bool frames = !(frame_type >= 3 && frame_type <= 6);
+	DevBuf fl(64);
+	if (!fl.p || !hip_ok(hipMemsetAsync(fl.p, 0, 64, st), "memset"))
+		return -1;
+	mgdk_bat *Sp = nullptr;
+	int rc = -1;
+	if (frame_type == 6) {
+		hipLaunchKernelGGL((k_fsum_row<T1, T2>), dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st, bv, n, out,
+				   fl.as<uint32_t>());
+	} else {
+		Starts part;
+		if (make_starts(p ? (const int8_t *) p->theap : nullptr, n, part, &Sp) < 0)
+			goto out;
+		if (frame_type == 3 || frame_type == 4) {
+			hipLaunchKernelGGL((k_fsum_replay<T1, T2>), dim3((unsigned) ((part.m + 63) / 64)), dim3(64), 0, st, bv, part,
+					   (const int8_t *) o->theap, frame_type == 3, out, fl.as<uint32_t>());
+		} else {
+			if (n >= 0xffffffffull) {
+				seterr("42000!GDKanalyticalsum: more than 2^32-1 rows on the device path\n");
+				goto out;
+			}
+			DevBuf pidx(n * 4 + 4);
+			if (!pidx.p)
+				goto out;
+			hipLaunchKernelGGL(k_avg_pidx, dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st, part, pidx.as<uint32_t>());
+			if (frame_type == 5) {
+				// dofsum per partition: the exact grouped float sum, the
+				// partition index as the group id
+				mgdk_bat *g = newbat(0, MGDK_oid, n);
+				if (g == nullptr)
+					goto out;
+				g->count = n;
+				hipLaunchKernelGGL(k_pidx_oid, dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st, pidx.as<uint32_t>(), n,
+						   (oid *) g->theap);
+				mgdk_bat *en = mgdk_BATdense(0, 0, part.m);
+				mgdk_bat *ps = en ? mgdk_BATgroupsum(b, g, en, nullptr, MGDK_dbl, true) : nullptr;
+				mgdk_BBPunfix(g);
+				mgdk_BBPunfix(en);
+				if (ps == nullptr) {
+					// dofsum's message, then the analytic bailout's (GDKerror appends)
+					char m[512];
+					snprintf(m, sizeof(m), "%s42000!error while calculating floating-point sum\n", mgdk_GDKerrbuf());
+					seterr("%s", m);
+					goto out;
+				}
+				hipLaunchKernelGGL((k_fsum_bcast<T2>), dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st,
+						   (const double *) ps->theap, pidx.as<uint32_t>(), n, out, fl.as<uint32_t>());
+				const bool ok = sync();
+				mgdk_BBPunfix(ps);
+				if (!ok)
+					goto out;
+			} else {
+				unsigned long long *hm = (unsigned long long *) pinned(8);
+				DevBuf mx(64);
+				if (!mx.p || !hip_ok(hipMemsetAsync(mx.p, 0, 8, st), "memset"))
+					goto out;
+				hipLaunchKernelGGL(k_avg_maxlen, dim3(grid_for(part.m, 1024, 1024)), dim3(256), 0, st, part,
+						   mx.as<unsigned long long>());
+				if (!hip_ok(hipMemcpyAsync(hm, mx.p, 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+					goto out;
+				AvgTree t{};
+				int nlev = 1;
+				while (nlev < AVG_MAX_LEVELS - 1 && ((*hm - 1) >> (4 * nlev)) > 0)
+					nlev++;
+				t.nlev = nlev;
+				size_t tot = 0, offs[AVG_MAX_LEVELS] = {0};
+				for (int L = 1; L <= nlev; L++) {
+					offs[L] = tot;
+					tot += ((n >> (4 * L)) + part.m + 1) * sizeof(FSum<T2>);
+					tot = (tot + 255) & ~(size_t) 255;
+				}
+				DevBuf tree(tot);
+				if (!tree.p)
+					goto out;
+				for (int L = 1; L <= nlev; L++)
+					t.lvl[L] = tree.as<char>() + offs[L];
+				for (int L = 1; L <= nlev; L++)
+					hipLaunchKernelGGL((k_fsum_tree_level<T1, T2>), dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st, bv, part,
+							   pidx.as<uint32_t>(), t, L, fl.as<uint32_t>());
+				hipLaunchKernelGGL((k_fsum_tree_query<T1, T2>), dim3(grid_for(n, 256, 16384)), dim3(256), 0, st, bv, part,
+						   pidx.as<uint32_t>(), t, (const oid *) s->theap, (const oid *) e->theap, out,
+						   fl.as<uint32_t>());
+				if (!sync())
+					goto out;
+			}
+		}
+	}
+	{
+		uint32_t *h = (uint32_t *) pinned(16);
+		if (!hip_ok(hipMemcpyAsync(h, fl.p, 4, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+			goto out;
+		if (h[0] & 4) {
+			seterr("22003!overflow in sum aggregate.\n42000!error while calculating floating-point sum\n");
+			goto out;
+		}
+		if (h[0] & 2) {
+			seterr("22003!overflow in calculation.\n");
+			goto out;
+		}
+		r->count = n;
+		r->tnil = (h[0] & 1) != 0;
+		r->tnonil = (h[0] & 1) == 0;
+		r->tsorted = r->trevsorted = r->tkey = n <= 1;
+		rc = 0;
+	}
+out:
+	mgdk_BBPunfix(Sp);
+	return rc;
+}
+
 }  // namespace
 
 extern "C" int
@@ -1213,6 +1561,35 @@ mgdk_GDKanalyticalsum(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_b
 	if (r == nullptr || b == nullptr) {
 		seterr("GDKanalyticalsum: NULL argument");
 		return -1;
+	}
+	const bool fp = (tp1 == MGDK_flt && (tp2 == MGDK_flt || tp2 == MGDK_dbl)) || (tp1 == MGDK_dbl && tp2 == MGDK_dbl);
+	if (fp && basetype(b->ttype) == tp1 && r->ttype == tp2) {
+		const BUN n = b->count;
+		if (n == 0) {
+			r->count = 0;
+			r->tnil = 0;
+			r->tnonil = 1;
+			return 0;
+		}
+		if ((p && (p->count != n || width_of(p->ttype) != 1)) || (o && (o->count != n || width_of(o->ttype) != 1))) {
+			seterr("analytic: p and o must be bit BATs aligned with b");
+			return -1;
+		}
+		if (!(frame_type >= 3 && frame_type <= 6) &&
+		    (s == nullptr || e == nullptr || s->count < n || e->count < n || s->ttype != MGDK_oid || e->ttype != MGDK_oid)) {
+			seterr("analytic: frame bounds s and e (oid BATs aligned with b) are required");
+			return -1;
+		}
+		if ((frame_type == 3 || frame_type == 4) && o == nullptr) {
+			seterr("analytic: the peer column o is required for this frame");
+			return -1;
+		}
+		ProfScope prof("analyticalsum");
+		if (tp1 == MGDK_flt && tp2 == MGDK_flt)
+			return run_fsum<float, float>(r, p, o, b, s, e, frame_type);
+		if (tp1 == MGDK_flt)
+			return run_fsum<float, double>(r, p, o, b, s, e, frame_type);
+		return run_fsum<double, double>(r, p, o, b, s, e, frame_type);
 	}
 	if (!sum_in_type(tp1) || basetype(b->ttype) != basetype(tp1) || !(tp2 == MGDK_lng || tp2 == MGDK_hge) ||
 	    r->ttype != tp2) {

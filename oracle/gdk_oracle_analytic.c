@@ -16,14 +16,18 @@
  * starts one); peers: o[i] != 0 starts a new peer group (ORDER BY value
  * change) -- the reference's np / op arrays.
  */
+#include <float.h>
 #include <math.h>
+#include <stdbool.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "gdk_oracle.h"
 
 void ora_seterr(const char *fmt, ...);
+int ora_fsum_array(double *out, bool *isnil, const double *vals, uint64_t nv, bool skip_nils, bool nil_if_empty);
 
 #define FANOUT 16
 #define HGE_MAX ((ora_hge) (((unsigned __int128) 1 << 127) - 1))
@@ -167,10 +171,239 @@ bit_at(const ora_bat *b, uint64_t i)
 	return b && ((const int8_t *) b->base)[i] != 0;
 }
 
+/* ---- GDKanalyticalsum over flt / dbl (gdk_analytic_func.c:1795-1817,
+ * :1930-1950): frames 3 / 4 / 6 / segment-tree frames add in row order (or
+ * the tree's order) with ADD_WITH_CHECK in the result type
+ * (gdk_calc_private.h:53-67); frame 5 is dofsum (exact, rounded once). */
+typedef struct {
+	double v;   /* in the result type (a flt result is kept as its float value) */
+	int nil;
+	int isflt;
+	int ovf;
+} fsv;
+
+static double
+fround(const fsv *a, double x)
+{
+	return a->isflt ? (double) (float) x : x;
+}
+
+/* ADD_WITH_CHECK(lft, rgt, TPE2, dst, GDK_TPE2_max, overflow) with lft
+ * already converted to TPE2 (the comparisons promote it so) */
+static double
+fadd_check(fsv *a, double lft, double rgt)
+{
+	if (a->isflt) {
+		const float mx = FLT_MAX, l = (float) lft, r = (float) rgt;
+		if (r < 1) {
+			if (-mx - r > l) { a->ovf = 1; return rgt; }
+		} else if (mx - r < l) {
+			a->ovf = 1;
+			return rgt;
+		}
+		return (double) (float) (l + r);
+	}
+	const double mx = DBL_MAX;
+	if (rgt < 1) {
+		if (-mx - rgt > lft) { a->ovf = 1; return rgt; }
+	} else if (mx - rgt < lft) {
+		a->ovf = 1;
+		return rgt;
+	}
+	return lft + rgt;
+}
+
+/* COMPUTE_LEVELN_SUM_NUM / the sequential frames: cur = x + cur */
+static fsv
+fsadd(fsv *a, fsv cur, fsv x)
+{
+	if (x.nil)
+		return cur;
+	if (cur.nil) {
+		cur.v = x.v;
+		cur.nil = 0;
+		return cur;
+	}
+	cur.v = fadd_check(a, x.v, cur.v);
+	return cur;
+}
+
+static void
+put_fsum(ora_bat *r, int isflt, uint64_t k, fsv x)
+{
+	if (isflt)
+		((float *) r->base)[k] = x.nil ? nanf("") : (float) x.v;
+	else
+		((double *) r->base)[k] = x.nil ? nan("") : x.v;
+}
+
+static int
+fsum_frames(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_bat *b, const ora_bat *s, const ora_bat *e,
+	    int tp1, int tp2, int frame_type)
+{
+	const uint64_t cnt = b->count;
+	fsv a = {0, 0, tp2 == ORA_flt, 0};
+	fsv *lv0 = malloc((cnt + 1) * sizeof(fsv));
+	if (!lv0)
+		return -1;
+	for (uint64_t i = 0; i < cnt; i++) {
+		double x = tp1 == ORA_flt ? (double) ((const float *) b->base)[i] : ((const double *) b->base)[i];
+		lv0[i] = (fsv) {fround(&a, x), x != x, a.isflt, 0};
+	}
+	const ora_oid *start = s ? s->base : NULL, *end = e ? e->base : NULL;
+	int rc = 0, has_nils = 0;
+	uint64_t k = 0;
+	for (uint64_t i = 1; i <= cnt && !a.ovf && rc == 0; i++) {
+		if (i < cnt && !bit_at(p, i))
+			continue;
+		switch (frame_type) {
+		case 3: {
+			fsv cur = {0, 1, a.isflt, 0};
+			while (k < i) {
+				uint64_t j = k;
+				do {
+					cur = fsadd(&a, cur, lv0[k]);
+					k++;
+				} while (k < i && !bit_at(o, k));
+				for (; j < k; j++)
+					put_fsum(r, a.isflt, j, cur);
+				has_nils |= cur.nil;
+			}
+			break;
+		}
+		case 4: {
+			fsv cur = {0, 1, a.isflt, 0};
+			uint64_t l = i - 1;
+			for (uint64_t j = l;; j--) {
+				cur = fsadd(&a, cur, lv0[j]);
+				if (bit_at(o, j) || j == k) {
+					for (;; l--) {
+						put_fsum(r, a.isflt, l, cur);
+						if (l == j)
+							break;
+					}
+					has_nils |= cur.nil;
+					if (j == k)
+						break;
+					l = j - 1;
+				}
+			}
+			k = i;
+			break;
+		}
+		case 5: {   /* dofsum over the partition, nils skipped, nil if empty */
+			double *vals = malloc((i - k + 1) * sizeof(double));
+			for (uint64_t j = k; j < i; j++)
+				vals[j - k] = lv0[j].nil ? nan("") : (tp1 == ORA_flt ? (double) ((const float *) b->base)[j]
+											: ((const double *) b->base)[j]);
+			double d = 0;
+			bool isnil = false;
+			int frc = ora_fsum_array(&d, &isnil, vals, i - k, true, true);
+			free(vals);
+			if (frc < 0 || (!isnil && a.isflt && (isinf((float) d) || isnan((float) d)))) {
+				if (frc == 0)
+					ora_seterr("22003!overflow in sum aggregate.\n");
+				rc = -2;
+				break;
+			}
+			fsv cur = {a.isflt ? (double) (float) d : d, isnil, a.isflt, 0};
+			for (; k < i; k++)
+				put_fsum(r, a.isflt, k, cur);
+			has_nils |= isnil;
+			break;
+		}
+		case 6:
+			for (; k < i; k++) {
+				put_fsum(r, a.isflt, k, lv0[k]);
+				has_nils |= lv0[k].nil;
+			}
+			break;
+		default: {  /* the reference's tree over the partition, nodes in TPE2 */
+			const uint64_t j = k, n = i - k;
+			uint64_t total = n, c = n, nl = 1;
+			do {
+				c = (c + FANOUT - 1) / FANOUT;
+				total += c;
+				nl++;
+			} while (c > 1);
+			fsv *tree = malloc(total * sizeof(fsv));
+			uint64_t *off = malloc(nl * sizeof(uint64_t));
+			memcpy(tree, lv0 + j, n * sizeof(fsv));
+			uint64_t to = n, lsize = n, prev = 0, cl = 1;
+			off[0] = 0;
+			while (cl < nl) {
+				uint64_t prev_to = to;
+				off[cl++] = to;
+				for (uint64_t pos = 0; pos < lsize; pos += FANOUT) {
+					uint64_t en = pos + FANOUT < lsize ? pos + FANOUT : lsize;
+					fsv acc = {0, 1, a.isflt, 0};
+					for (uint64_t x = pos; x < en; x++)
+						acc = fsadd(&a, acc, tree[prev + x]);
+					tree[to++] = acc;
+				}
+				prev = prev_to;
+				lsize = to - prev_to;
+			}
+			for (; k < i && !a.ovf; k++) {
+				uint64_t begin = start[k] - j, tend = end[k] - j;
+				fsv acc = {0, 1, a.isflt, 0};
+				if (begin < tend)
+					for (uint64_t level = 0; level < nl; level++) {
+						const fsv *tl = tree + off[level];
+						uint64_t pb = begin / FANOUT, pe = tend / FANOUT;
+						if (pb == pe) {
+							for (uint64_t pos = begin; pos < tend; pos++)
+								acc = fsadd(&a, acc, tl[pos]);
+							break;
+						}
+						uint64_t gb = pb * FANOUT;
+						if (begin != gb) {
+							for (uint64_t pos = begin; pos < gb + FANOUT; pos++)
+								acc = fsadd(&a, acc, tl[pos]);
+							pb++;
+						}
+						uint64_t ge = pe * FANOUT;
+						if (tend != ge)
+							for (uint64_t pos = ge; pos < tend; pos++)
+								acc = fsadd(&a, acc, tl[pos]);
+						begin = pb;
+						tend = pe;
+					}
+				put_fsum(r, a.isflt, k, acc);
+				has_nils |= acc.nil;
+			}
+			free(tree);
+			free(off);
+			break;
+		}
+		}
+	}
+	free(lv0);
+	if (rc == -2) {
+		/* dofsum's message, then the analytic bailout's (GDKerror appends) */
+		char m[256];
+		snprintf(m, sizeof(m), "%s42000!error while calculating floating-point sum\n", ora_errbuf());
+		ora_seterr("%s", m);
+		return -1;
+	}
+	if (rc < 0)
+		return -1;
+	if (a.ovf) {
+		ora_seterr("22003!overflow in calculation.\n");
+		return -1;
+	}
+	r->count = cnt;
+	r->nil = has_nils;
+	r->nonil = !has_nils;
+	return 0;
+}
+
 int
 ora_analyticalsum(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_bat *b, const ora_bat *s,
 		  const ora_bat *e, int tp1, int tp2, int frame_type)
 {
+	if ((tp1 == ORA_flt && (tp2 == ORA_flt || tp2 == ORA_dbl)) || (tp1 == ORA_dbl && tp2 == ORA_dbl))
+		return fsum_frames(r, p, o, b, s, e, tp1, tp2, frame_type);
 	if (!((tp1 == ORA_bte || tp1 == ORA_sht || tp1 == ORA_int || tp1 == ORA_lng) &&
 	      (tp2 == ORA_lng || tp2 == ORA_hge))) {
 		ora_seterr("42000!type combination (sum(%d)->%d) not supported.\n", tp1, tp2);

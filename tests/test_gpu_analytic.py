@@ -276,3 +276,55 @@ def test_analytical_avginteger_deep_tree(gdk, ora):
     want = ora.analyticalavginteger(ora.Bat.from_array(ora.TYPE_lng, v), None, None,
                                     ora.Bat.from_array(ora.TYPE_oid, s), ora.Bat.from_array(ora.TYPE_oid, e), 1)
     assert np.array_equal(got.to_numpy(), np.asarray(want.values()))
+
+
+def _fdata(r, tname, nparts=23, plen=517, nil_frac=0.05):
+    dt = np.float32 if tname == "flt" else np.float64
+    v, p, o, ob = _data(r, nparts=nparts, plen=plen, nil_frac=0.0)
+    x = (r.standard_normal(len(v)) * 10.0 ** r.integers(-3, 6, len(v))).astype(dt)
+    x[r.random(len(v)) < nil_frac] = np.nan
+    return x, p, o, ob
+
+
+@pytest.mark.parametrize("t1,t2", [("flt", "flt"), ("flt", "dbl"), ("dbl", "dbl")])
+@pytest.mark.parametrize("frame", [3, 4, 5, 6, 1, 2])
+def test_analytical_sum_float(gdk, ora, t1, t2, frame):
+    """GDKanalyticalsum over flt / dbl: frames 3 / 4 add in row order, frame 5
+    is the partition's dofsum, frames from the bounds walk the reference's
+    segment tree -- all bit-identical to the oracle's restatement."""
+    r = rng(311 + frame)
+    v, p, o, ob = _fdata(r, t1)
+    tp1, T2 = getattr(gdk, "TYPE_" + t1), getattr(gdk, "TYPE_" + t2)
+    s = e = None
+    if frame in (1, 2):
+        s, e = _bounds(gdk, ob, p, 3 if frame == 1 else 40)
+    got = gdk.GDKanalyticalsum(gdk.BAT.from_numpy(tp1, v), gdk.BAT.from_numpy(gdk.TYPE_bit, p),
+                               gdk.BAT.from_numpy(gdk.TYPE_bit, o), s, e, T2, frame)
+    os_ = ora.Bat.from_array(ora.TYPE_oid, s.to_numpy()) if s else None
+    oe = ora.Bat.from_array(ora.TYPE_oid, e.to_numpy()) if e else None
+    want = ora.analyticalsum(ora.Bat.from_array(tp1, v), ora.Bat.from_array(ora.TYPE_bit, p),
+                             ora.Bat.from_array(ora.TYPE_bit, o), os_, oe, T2, frame)
+    g, w = got.to_numpy(), want.values()
+    assert g.dtype == w.dtype
+    assert np.array_equal(g.view(np.uint32 if g.dtype == np.float32 else np.uint64),
+                          w.view(np.uint32 if w.dtype == np.float32 else np.uint64))
+    assert bool(got.s.tnil) == bool(want.s.nil)
+
+
+@pytest.mark.parametrize("frame", [3, 4, 5, 1])
+def test_analytical_sum_float_overflow(gdk, ora, frame):
+    r = rng(5)
+    v, p, o, ob = _fdata(r, "flt", nparts=3, plen=40, nil_frac=0.0)
+    v[5:9] = 3e38
+    s = e = None
+    if frame == 1:
+        s, e = _bounds(gdk, ob, p, 10)
+    os_ = ora.Bat.from_array(ora.TYPE_oid, s.to_numpy()) if s else None
+    oe = ora.Bat.from_array(ora.TYPE_oid, e.to_numpy()) if e else None
+    with pytest.raises(ora.OracleError) as we:
+        ora.analyticalsum(ora.Bat.from_array(ora.TYPE_flt, v), ora.Bat.from_array(ora.TYPE_bit, p),
+                          ora.Bat.from_array(ora.TYPE_bit, o), os_, oe, ora.TYPE_flt, frame)
+    with pytest.raises(gdk.GDKError) as ge:
+        gdk.GDKanalyticalsum(gdk.BAT.from_numpy(gdk.TYPE_flt, v), gdk.BAT.from_numpy(gdk.TYPE_bit, p),
+                             gdk.BAT.from_numpy(gdk.TYPE_bit, o), s, e, gdk.TYPE_flt, frame)
+    assert str(ge.value) == str(we.value)
