@@ -76,6 +76,23 @@ void *mgdk_stream(void);                         /* calling thread's hipStream_t
 uint64_t mgdk_mem_cursize(void);                 /* gdk_utils.c:1636 GDKmem_cursize */
 void mgdk_mem_release_cache(void);
 
+/* query context (gdk/gdk_system.h:187-210 QryCtx, MT_thread_set_qry_ctx):
+ * endtime in microseconds of mgdk_usec() (0: none), or one of the negative
+ * codes a client sets (gdk/gdk.h:2325-2327).  Every operator of the calling
+ * thread tests it whenever it waits for its stream -- between its kernel
+ * launches -- and fails with the reference's message ("Timeout was
+ * reached!", "Query interrupted!", "Client is disconnected!"). */
+typedef struct mgdk_qryctx {
+	int64_t starttime;
+	int64_t endtime;
+} mgdk_qryctx;
+#define MGDK_QRY_TIMEOUT (-1)
+#define MGDK_QRY_INTERRUPT (-2)
+#define MGDK_QRY_DISCONNECT (-3)
+void mgdk_thread_set_qry_ctx(mgdk_qryctx *ctx);   /* NULL: no context */
+mgdk_qryctx *mgdk_thread_get_qry_ctx(void);
+int64_t mgdk_usec(void);                           /* GDKusec */
+
 /* per-kernel timing with hipEvents on the library stream (ALGO tracing,
  * gdk/gdk_private.h:331): enable, then read totals per kernel name */
 void mgdk_prof_enable(int on);

@@ -13,6 +13,8 @@
 #include <string>
 #include <vector>
 
+#include <ctime>
+
 #include "mgdk_internal.h"
 
 namespace mgdk {
@@ -70,13 +72,39 @@ stream()
 	return tctx.s;
 }
 
+// The calling thread's query context (MT_thread_set_qry_ctx,
+// gdk/gdk_system.h:187-210): the reference tests it every
+// CHECK_QRY_TIMEOUT_STEP iterations of its loops (TIMEOUT_LOOP, gdk.h:2420-
+// 2462); a device operator tests it whenever it waits for its stream, i.e.
+// between its launches, and fails the same way (GDK_FAIL / NULL with the
+// TIMEOUT_MESSAGE text, gdk.h:2321-2346).
+static thread_local mgdk_qryctx *qry_ctx;
+
+static bool
+qry_timed_out()
+{
+	mgdk_qryctx *qc = qry_ctx;
+	if (qc == nullptr)
+		return false;
+	if (qc->endtime >= 0 && qc->endtime && mgdk_usec() > qc->endtime)
+		qc->endtime = MGDK_QRY_TIMEOUT;
+	switch (qc->endtime) {
+	case MGDK_QRY_TIMEOUT: seterr("Timeout was reached!\n"); return true;
+	case MGDK_QRY_INTERRUPT: seterr("Query interrupted!\n"); return true;
+	case MGDK_QRY_DISCONNECT: seterr("Client is disconnected!\n"); return true;
+	default: return false;
+	}
+}
+
 bool
 sync()
 {
 	hipError_t e = hipStreamSynchronize(stream());
 	if (e != hipSuccess)
 		return hip_ok(e, "hipStreamSynchronize");
-	return hip_ok(hipGetLastError(), "kernel launch");
+	if (!hip_ok(hipGetLastError(), "kernel launch"))
+		return false;
+	return !qry_timed_out();
 }
 
 // ---- caching HBM allocator ---------------------------------------------------
@@ -624,6 +652,26 @@ mgdk_init(int device)
 	if (!hip_ok(hipSetDevice(device), "hipSetDevice"))
 		return -1;
 	return stream() ? 0 : -1;
+}
+
+int64_t
+mgdk_usec(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_REALTIME, &ts);
+	return (int64_t) ts.tv_sec * 1000000 + ts.tv_nsec / 1000;
+}
+
+void
+mgdk_thread_set_qry_ctx(mgdk_qryctx *ctx)
+{
+	qry_ctx = ctx;
+}
+
+mgdk_qryctx *
+mgdk_thread_get_qry_ctx(void)
+{
+	return qry_ctx;
 }
 
 const char *

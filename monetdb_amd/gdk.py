@@ -74,6 +74,9 @@ _SIGS = {
     "mgdk_stream": (C.c_void_p, []),
     "mgdk_mem_cursize": (C.c_uint64, []),
     "mgdk_mem_release_cache": (None, []),
+    "mgdk_thread_set_qry_ctx": (None, [C.c_void_p]),
+    "mgdk_thread_get_qry_ctx": (C.c_void_p, []),
+    "mgdk_usec": (C.c_int64, []),
     "mgdk_prof_enable": (None, [C.c_int]),
     "mgdk_prof_get": (C.c_int, [C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "mgdk_prof_reset": (None, []),
@@ -728,6 +731,24 @@ def gen_window_column(seed, n, plen):
 
 def sync():
     _chk(lib().mgdk_sync())
+
+
+class QryCtx(C.Structure):
+    """gdk/gdk_system.h:187 QryCtx (starttime, endtime in microseconds)."""
+    _fields_ = [("starttime", C.c_int64), ("endtime", C.c_int64)]
+
+
+QRY_TIMEOUT, QRY_INTERRUPT, QRY_DISCONNECT = -1, -2, -3
+
+
+def set_qry_ctx(ctx):
+    """MT_thread_set_qry_ctx for the calling thread (None clears it); the
+    caller keeps ctx alive while it is set."""
+    lib().mgdk_thread_set_qry_ctx(C.cast(C.pointer(ctx), C.c_void_p) if ctx is not None else None)
+
+
+def usec():
+    return lib().mgdk_usec()
 
 
 def prof_enable(on=True):

@@ -82,3 +82,34 @@ def test_concurrent_append_and_alloc(gdk):
     stop.set()
     ch.join()
     assert not errors, errors
+
+
+@pytest.mark.gpu
+def test_qry_ctx_timeout(gdk):
+    """QryCtx (gdk/gdk_system.h:187, TIMEOUT_TEST gdk.h:2367): an operator of a
+    thread whose query context has expired or was interrupted fails with the
+    reference's message; other threads are not affected."""
+    import threading
+    import time
+    b = gdk.BAT.from_numpy(gdk.TYPE_int, np.arange(100_000, dtype=np.int32))
+    ctx = gdk.QryCtx(0, gdk.QRY_INTERRUPT)
+    gdk.set_qry_ctx(ctx)
+    try:
+        with pytest.raises(gdk.GDKError, match="Query interrupted!"):
+            gdk.BATthetaselect(b, None, 10, "<")
+        ctx.endtime = gdk.usec() + 1
+        time.sleep(0.01)
+        with pytest.raises(gdk.GDKError, match="Timeout was reached!"):
+            gdk.BATthetaselect(b, None, 10, "<")
+        assert ctx.endtime == gdk.QRY_TIMEOUT
+        # another thread without a context runs normally meanwhile
+        out = []
+        t = threading.Thread(target=lambda: out.append(gdk.BATthetaselect(b, None, 10, "<").count()))
+        t.start()
+        t.join()
+        assert out == [10]
+        ctx.endtime = gdk.usec() + 60_000_000
+        assert gdk.BATthetaselect(b, None, 10, "<").count() == 10
+    finally:
+        gdk.set_qry_ctx(None)
+    assert gdk.BATthetaselect(b, None, 10, "<").count() == 10
