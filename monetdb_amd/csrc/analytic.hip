@@ -258,8 +258,9 @@ pidx(int i)
 struct FArgs {
 	const int64_t *b;
 	uint64_t tmax;       // |v - b[j]| > tmax overflows (narrow value types widened to lng)
-	const int8_t *p;     // partition bits or NULL
-	bool p4;             // p is 4-byte aligned
+	const int8_t *p;     // partition bits (4-byte aligned); a readable dummy without partitions
+	BUN pstep;           // 1, or 0 without partitions
+	uint32_t pmask;      // ~0, or 0 without partitions
 	BUN n;
 	int64_t limit;
 	bool preceding;
@@ -272,6 +273,26 @@ struct FArgs {
 	oid *unres;          // unresolved row list
 	uint32_t unres_cap;
 };
+
+// Partition-start flags of stage rows 4q .. 4q+3 as one little-endian word
+// (rows at or past the stage end read as 0).  The host hands over a 4-byte
+// aligned flag column (copying a misaligned view) and, without partitions,
+// a zero step and mask, so the word load is unconditional on a clamped
+// index -- heaps are allocated in >= 256-byte classes, so the aligned word
+// holding the last valid byte is always readable -- and the stage's loads
+// all stay in flight together instead of each waiting at a branch join.
+static_assert(FH % 4 == 0 && FT % 4 == 0, "stage starts must stay word aligned");
+
+__device__ __forceinline__ uint32_t
+flags_word(const FArgs &a, BUN lo, int q, int S)
+{
+	const bool in = 4 * q < S;
+	const BUN pos = lo + 4 * (BUN) (in ? q : 0);
+	const uint32_t x = *(const uint32_t *) (a.p + pos * a.pstep);
+	const BUN rem = a.n - pos;
+	const uint32_t m = rem >= 4 ? ~0u : (1u << (8 * rem)) - 1;
+	return in ? x & m & a.pmask : 0;
+}
 
 __global__ __launch_bounds__(256) void
 k_range_fast(FArgs a)
@@ -300,22 +321,15 @@ k_range_fast(FArgs a)
 #pragma unroll
 		for (int u = 0; u < NB; u++) {
 			const int i = tid + u * 256;
-			tv[u] = i < S ? a.b[lo + i] : 0;
+			const int64_t x = a.b[lo + (i < S ? i : 0)];   // clamped: every load in flight
+			tv[u] = i < S ? x : 0;
 		}
 		constexpr int NW = (FS + 3 + 1023) / 1024;
 		uint32_t tw[NW];
 #pragma unroll
 		for (int u = 0; u < NW; u++) {
 			const int q = tid + u * 256;      // word q covers stage rows 4q .. 4q+3
-			tw[u] = 0;
-			if (a.p && 4 * q < S) {
-				if (a.p4 && lo + 4 * q + 3 < a.n) {
-					tw[u] = *(const uint32_t *) (a.p + lo + 4 * q);
-				} else {
-					for (int e = 0; e < 4 && lo + 4 * q + e < a.n; e++)
-						tw[u] |= (uint32_t) (uint8_t) a.p[lo + 4 * q + e] << (8 * e);
-				}
-			}
+			tw[u] = flags_word(a, lo, q, S);
 		}
 #pragma unroll
 		for (int u = 0; u < NB; u++) {
@@ -521,22 +535,15 @@ k_range_keys(FArgs a)
 #pragma unroll
 		for (int u = 0; u < NB; u++) {
 			const int i = tid + u * 256;
-			tv[u] = i < S ? a.b[lo + i] : INT64_MIN;
+			const int64_t x = a.b[lo + (i < S ? i : 0)];
+			tv[u] = i < S ? x : INT64_MIN;
 		}
 		constexpr int NW = (FS + 3 + 1023) / 1024;
 		uint32_t tw[NW];
 #pragma unroll
 		for (int u = 0; u < NW; u++) {
 			const int q = tid + u * 256;
-			tw[u] = 0;
-			if (a.p && 4 * q < S) {
-				if (a.p4 && lo + 4 * q + 3 < a.n) {
-					tw[u] = *(const uint32_t *) (a.p + lo + 4 * q);
-				} else {
-					for (int e = 0; e < 4 && lo + 4 * q + e < a.n; e++)
-						tw[u] |= (uint32_t) (uint8_t) a.p[lo + 4 * q + e] << (8 * e);
-				}
-			}
+			tw[u] = flags_word(a, lo, q, S);
 		}
 		bool any = lo == 0;
 #pragma unroll
@@ -891,8 +898,16 @@ mgdk::range_bounds_int64(mgdk_bat *r, const int64_t *bvals, const mgdk_bat *p, B
 	FArgs f{};
 	f.b = bvals;
 	f.tmax = tmax;
-	f.p = p ? (const int8_t *) p->theap : nullptr;
-	f.p4 = ((uintptr_t) f.p & 3) == 0;
+	const bool mis = p && ((uintptr_t) p->theap & 3);
+	DevBuf pal(mis ? n : 0);
+	if (mis) {
+		// misaligned view of the partition column: an aligned copy
+		if (!pal.p || !hip_ok(hipMemcpyAsync(pal.p, p->theap, n, hipMemcpyDeviceToDevice, st), "memcpy"))
+			return -1;
+	}
+	f.p = !p ? (const int8_t *) fl.p : mis ? (const int8_t *) pal.p : (const int8_t *) p->theap;
+	f.pstep = p ? 1 : 0;
+	f.pmask = p ? ~0u : 0u;
 	f.n = n;
 	f.limit = limit;
 	f.preceding = preceding;
