@@ -177,6 +177,16 @@ class GdkBackend:
     def slice(self, c, lo, hi):
         return self.gdk.BATslice(c, lo, hi)
 
+    def dense(self, tseq, n):
+        return self.gdk.BAT.dense(tseq, n)
+
+    def addcst(self, c, v):
+        """c + v as lng (bounds oids to global row numbers)"""
+        g = self.gdk
+        if c.ttype != g.TYPE_lng:        # batcalc refuses oid arithmetic: convert first
+            c = g.BATconvert(c, None, g.TYPE_lng)
+        return g.BATcalcaddcst(c, v, g.TYPE_lng, g.TYPE_lng)
+
     # -- operators -----------------------------------------------------------
     def hashpartition(self, c, nparts):
         return self.gdk.BAThashpartition(c, nparts)
@@ -219,6 +229,8 @@ class GdkBackend:
     def values_at(self, c, positions):
         import numpy as np
         g = self.gdk
+        if len(positions) == 0:
+            return []
         o = g.BAT.from_numpy(g.TYPE_oid, np.asarray(positions, np.uint64) + c.hseqbase, sorted_=True, key=True)
         return [int(v) for v in g.BATproject(o, c).to_numpy()]
 
@@ -317,13 +329,56 @@ def _types(be):
 # group + aggregates
 # ---------------------------------------------------------------------------
 
+def _allgather_col(be, dist, c, tp):
+    """Concatenation over ranks (rank order) of one column, as a column of
+    this rank's backend (device BATs for GdkBackend): a size exchange and ONE
+    all_gather of the packed rows padded to the largest rank.  Returns
+    (column, this rank's offset in it)."""
+    import torch
+    world, rank = _world(dist)
+    if world == 1:
+        return c, 0
+    n = be.n(c)
+    sizes = [int(x[0]) for x in _gather_int64(dist, be.device, [n])]
+    width = 2 if tp == _types(be)[2] else 1
+    pad = torch.zeros((max(sizes), width), dtype=torch.int64, device=be.device)
+    if n:
+        pad[:n] = be.pack([c])
+    outs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(outs, pad)
+    (col,) = be.unpack(torch.cat([o[:k] for o, k in zip(outs, sizes)]), [tp])
+    return col, sum(sizes[:rank])
+
+
+def _global_ids(be, dist, firsts):
+    """Group ids in global first-occurrence order (what BATgroup over all
+    rows numbers them): the rank of each owned group's first row among the
+    first rows of every rank.  All on the backend's columns: the all-gathered
+    first rows sorted, the sort order sorted again (its inverse permutation),
+    this rank's slice of it."""
+    TL, TO, TH = _types(be)
+    allf, off = _allgather_col(be, dist, firsts, TO)
+    _, o = be.sort(allf)
+    _, inv = be.sort(o)
+    return be.project(be.dense(off, be.n(firsts)), inv)
+
+
+def _by_gid(be, gid, cols):
+    """The owned groups' columns put in ascending gid order."""
+    _, og = be.sort(gid)
+    return be.project(og, gid), [be.project(og, c) for c in cols]
+
+
 def dist_group_aggr(be, dist, keys, vals):
     """GROUP BY keys with exact sums of `vals` (lng columns) and counts.
 
     keys/vals: this rank's shard, hseqbase = the shard's first global row.
-    Returns the groups OWNED by this rank (hash of the key), as a list of
-    dicts {gid, key, first_row, count, sums} with gid = the group's number in
-    global first-occurrence order (what BATgroup over all rows would give).
+    Returns the groups OWNED by this rank (hash of the key) as columns of the
+    backend (device BATs with GdkBackend), in ascending gid order:
+    {"gid", "key" (lng), "first_row" (oid), "count" (lng), "sums" [hge]},
+    gid = the group's number in global first-occurrence order (what BATgroup
+    over all rows would give).  No per-group host objects: the merge, the
+    numbering and the ordering run as backend operators and collectives.
     """
     TL, TO, TH = _types(be)
     world, rank = _world(dist)
@@ -336,23 +391,15 @@ def dist_group_aggr(be, dist, keys, vals):
         parts = be.unpack(recv, [TL, TO, TL] + [TH] * len(vals))
     rk, rfirst, rcount, rsums = parts[0], parts[1], parts[2], parts[3:]
     if be.n(rk) == 0:
-        mine = []
+        mk, mf, mc, ms = rk, rfirst, rcount, list(rsums)
     else:
         g2, e2, _ = be.group(rk)
-        mk = be.values(be.project(e2, rk))
-        mf = be.values(be.groupmin(rfirst, g2, e2))
-        mc = be.values(be.groupsum(rcount, g2, e2, TL))
-        ms = [be.values(be.groupsum(s, g2, e2, TH)) for s in rsums]
-        mine = [{"key": int(mk[i]), "first_row": int(mf[i]), "count": int(mc[i]),
-                 "sums": [int(s[i]) for s in ms]} for i in range(len(mk))]
-    # global first-occurrence numbering
-    firsts = [m["first_row"] for m in mine]
-    allf = sorted(x for part in (_gather_var(dist, be.device, firsts) if world > 1 else [firsts])
-                  for x in part)
-    pos = {f: i for i, f in enumerate(allf)}
-    for m in mine:
-        m["gid"] = pos[m["first_row"]]
-    return sorted(mine, key=lambda m: m["gid"])
+        mk = be.project(e2, rk)
+        mf = be.groupmin(rfirst, g2, e2)
+        mc = be.groupsum(rcount, g2, e2, TL)
+        ms = [be.groupsum(s, g2, e2, TH) for s in rsums]
+    gid, cols = _by_gid(be, _global_ids(be, dist, mf), [mk, mf, mc] + ms)
+    return {"gid": gid, "key": cols[0], "first_row": cols[1], "count": cols[2], "sums": cols[3:]}
 
 
 # ---------------------------------------------------------------------------
@@ -366,8 +413,8 @@ def dist_group_avg(be, dist, keys, vals):
     round it.  Each rank groups its shard and computes (avg, rem, cnt)
     partials; the partial rows are hash-partitioned by key (ONE all_to_all)
     and each owner combines its groups' partials with BATgroupavg3combine.
-    Returns this rank's owned groups {gid, key, first_row, avg}, gid in
-    global first-occurrence order."""
+    Returns this rank's owned groups as backend columns in ascending gid
+    order: {"gid", "key", "first_row", "avg"}."""
     TL, TO, TH = _types(be)
     world, rank = _world(dist)
     g, e, _ = be.group(keys)
@@ -380,20 +427,14 @@ def dist_group_avg(be, dist, keys, vals):
         parts = be.unpack(recv, [TL, TO, TL, TL, TL])
     rk, rfirst, ra, rr, rc = parts
     if be.n(rk) == 0:
-        mine = []
+        mk, mf, ma = rk, rfirst, ra
     else:
         g2, e2, _ = be.group(rk)
-        mk = be.values(be.project(e2, rk))
-        mf = be.values(be.groupmin(rfirst, g2, e2))
-        ma = be.values(be.groupavg3combine(ra, rr, rc, g2, e2))
-        mine = [{"key": int(mk[i]), "first_row": int(mf[i]), "avg": int(ma[i])} for i in range(len(mk))]
-    firsts = [m["first_row"] for m in mine]
-    allf = sorted(x for part in (_gather_var(dist, be.device, firsts) if world > 1 else [firsts])
-                  for x in part)
-    pos = {f: i for i, f in enumerate(allf)}
-    for m in mine:
-        m["gid"] = pos[m["first_row"]]
-    return sorted(mine, key=lambda m: m["gid"])
+        mk = be.project(e2, rk)
+        mf = be.groupmin(rfirst, g2, e2)
+        ma = be.groupavg3combine(ra, rr, rc, g2, e2)
+    gid, cols = _by_gid(be, _global_ids(be, dist, mf), [mk, mf, ma])
+    return {"gid": gid, "key": cols[0], "first_row": cols[1], "avg": cols[2]}
 
 
 # ---------------------------------------------------------------------------
@@ -541,11 +582,10 @@ def dist_sort(be, dist, keys, sample=64):
     if world == 1:
         return s, o
     n = be.n(s)
-    sv, ov = be.values(s), be.values(o)
     idx = [(i * n) // sample for i in range(sample)] if n else []
     samp = []
-    for i in idx:
-        samp += [int(sv[i]), int(ov[i])]
+    for k, p in zip(be.values_at(s, idx), be.values_at(o, idx)):
+        samp += [int(k), int(p)]
     allp = _gather_var(dist, be.device, samp)
     pairs = sorted((p[i], p[i + 1]) for p in allp for i in range(0, len(p), 2))
     spl = [pairs[(d * len(pairs)) // world] for d in range(1, world)] if pairs else []
@@ -571,15 +611,14 @@ def dist_window_bounds(be, dist, vals, parts, limit, preceding):
     rank's first partition start belong to a partition that began on an
     earlier rank: they move to that rank (one all_to_all), so every rank
     holds whole partitions and computes its bounds locally.  Returns
-    (first global row held, bounds as global row numbers) for the rows this
-    rank holds after the move."""
+    (first global row held, bounds as global row numbers -- a lng column of
+    the backend) for the rows this rank holds after the move."""
     TL, TO, _ = _types(be)
     world, rank = _world(dist)
     row0 = vals.hseqbase
     n = be.n(vals)
     if world == 1:
-        b = be.rangebounds(vals, parts, limit, preceding)
-        return row0, be.values(b).astype("int64") + row0
+        return row0, be.addcst(be.rangebounds(vals, parts, limit, preceding), row0)
     fs = be.first_start(parts)
     starts = [_s64(x[0]) for x in _gather_int64(dist, be.device, [fs if fs is not None else -1])]
     lead = 0 if rank == 0 else (n if fs is None else fs)
@@ -602,6 +641,5 @@ def dist_window_bounds(be, dist, vals, parts, limit, preceding):
         be.append(p2, be.zeros_bit(be.n(rv)))
     kept_first = row0 + lead
     if be.n(v2) == 0:
-        return kept_first, be.values(v2).astype("int64")
-    b = be.rangebounds(v2, p2, limit, preceding)
-    return kept_first, be.values(b).astype("int64") + kept_first
+        return kept_first, v2
+    return kept_first, be.addcst(be.rangebounds(v2, p2, limit, preceding), kept_first)

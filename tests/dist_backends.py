@@ -76,6 +76,12 @@ class OracleBackend:
     def slice(self, c, lo, hi):
         return Col(c.tp, c.arr[lo:hi], c.hseqbase + lo)
 
+    def dense(self, tseq, n):
+        return Col(ora.TYPE_oid, np.arange(tseq, tseq + n, dtype=np.uint64))
+
+    def addcst(self, c, v):
+        return Col(ora.TYPE_lng, c.arr.astype(np.int64) + v, c.hseqbase)
+
     def hashpartition(self, c, nparts):
         d = _hash(c.arr.astype(np.int64), nparts)
         pos = np.argsort(d, kind="stable")

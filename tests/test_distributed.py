@@ -125,14 +125,21 @@ def _exchange_worker(rank, world, port, out_dir, backend="oracle"):
     ev, hv = e.values().astype(np.int64), h.values()
     s1 = ora.BATgroupsum(ora.Bat.from_array(ora.TYPE_lng, v1), g, e, ora.TYPE_hge).values()
     s2 = ora.BATgroupsum(ora.Bat.from_array(ora.TYPE_lng, v2), g, e, ora.TYPE_hge).values()
-    for m in got:
-        i = m["gid"]
-        want = (int(keys[ev[i]]) if keys[ev[i]] != np.iinfo(np.int32).min else np.iinfo(np.int64).min,
-                int(ev[i]), int(hv[i]), [int(s1[i]), int(s2[i])])
-        if (m["key"], m["first_row"], m["count"], m["sums"]) != want:
-            errs.append("group %d: %r != %r" % (i, m, want))
-            break
-    tot = torch.tensor([len(got)])
+    V = lambda c: np.asarray([int(x) for x in be.values(c)], dtype=object)   # noqa: E731
+    gid = V(got["gid"]).astype(np.int64)
+    if len(gid) and not (np.diff(gid) > 0).all():
+        errs.append("gids not ascending")
+    if len(gid):
+        ev_ = ev[gid]
+        kw = keys[ev_].astype(np.int64)
+        kw[keys[ev_] == np.iinfo(np.int32).min] = np.iinfo(np.int64).min
+        for name, have, want in (("key", V(got["key"]), kw), ("first", V(got["first_row"]), ev_),
+                                 ("count", V(got["count"]), hv[gid]),
+                                 ("sum1", V(got["sums"][0]), np.asarray(s1, dtype=object)[gid]),
+                                 ("sum2", V(got["sums"][1]), np.asarray(s2, dtype=object)[gid])):
+            if [int(x) for x in have] != [int(x) for x in want]:
+                errs.append("group column %s mismatch" % name)
+    tot = torch.tensor([len(gid)])
     dist.all_reduce(tot)
     if int(tot) != len(ev):
         errs.append("groups %d != %d" % (int(tot), len(ev)))
@@ -143,12 +150,11 @@ def _exchange_worker(rank, world, port, out_dir, backend="oracle"):
     gota = D.dist_group_avg(be, dist, Col(ora.TYPE_int, keys[lo:hi], lo), Col(ora.TYPE_lng, v3[lo:hi], lo))
     av, _, _ = ora.BATgroupavg3(ora.Bat.from_array(ora.TYPE_lng, v3), g, e, True)
     av = av.values()
-    for m in gota:
-        i = m["gid"]
-        if (m["first_row"], m["avg"]) != (int(ev[i]), int(av[i])):
-            errs.append("avg group %d: %r != %r" % (i, m, (int(ev[i]), int(av[i]))))
-            break
-    tot = torch.tensor([len(gota)])
+    gida = V(gota["gid"]).astype(np.int64)
+    if len(gida) and ([int(x) for x in V(gota["first_row"])] != [int(x) for x in ev[gida]] or
+                      [int(x) for x in V(gota["avg"])] != [int(x) for x in np.asarray(av, dtype=object)[gida]]):
+        errs.append("avg groups mismatch")
+    tot = torch.tensor([len(gida)])
     dist.all_reduce(tot)
     if int(tot) != len(ev):
         errs.append("avg groups %d != %d" % (int(tot), len(ev)))
@@ -200,6 +206,7 @@ def _exchange_worker(rank, world, port, out_dir, backend="oracle"):
                                           Col(ora.TYPE_bit, bits[lo:hi], lo), 7, preceding)
         want = ora.rangebounds(ora.Bat.from_array(ora.TYPE_lng, order_),
                                ora.Bat.from_array(ora.TYPE_bit, bits), 7, preceding).values()
+        bnd = np.asarray(be.values(bnd), dtype=np.int64)
         if not np.array_equal(bnd, want[first:first + len(bnd)].astype(np.int64)):
             errs.append("window mismatch preceding=%s" % preceding)
         cnt = torch.tensor([len(bnd)])
