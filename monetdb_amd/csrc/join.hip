@@ -479,7 +479,7 @@ unfix2(mgdk_bat *a, mgdk_bat *b)
 // falls back), 0 on success, -1 on error
 template <int KW>
 int
-join_lp(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_bat **ap, mgdk_bat **bp)
+join_lp(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_bat **ap, mgdk_bat **bp, bool *ukey)
 {
 	typedef typename Tab<KW>::slot_t slot_t;
 	hipStream_t st = stream();
@@ -561,6 +561,7 @@ join_lp(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_bat
 		const uint64_t nout = h[0];
 		if (nout <= ocap) {
 			ra->count = rb->count = nout;
+			*ukey = uniq;
 			*ap = ra;
 			*bp = rb;
 			return 0;
@@ -1162,7 +1163,7 @@ pj_cut(const Side &S, BUN n, int pbits, bool skipnil, PjSide &o, uint32_t *maxto
 
 // returns 1 when not applicable (caller uses the open-addressing path)
 int
-join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_bat **ap, mgdk_bat **bp)
+join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_bat **ap, mgdk_bat **bp, bool *ukey)
 {
 	static const int mode = getenv("MGDK_JOIN_PART") ? atoi(getenv("MGDK_JOIN_PART")) : 1;
 	if (mode == 0 || L.w != 4 || R.w != 4 || nr < 65536)
@@ -1229,6 +1230,7 @@ join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_b
 		return -1;
 	}
 	ra->count = rb->count = h64[0];
+	*ukey = true;                                       // unique build keys: one match per row
 	*ap = ra;
 	*bp = rb;
 	return 0;
@@ -1241,11 +1243,13 @@ namespace mgdk {
 // hashjoin (gdk/gdk_join.c:2900-3335) over candidate lists already
 // initialised: per l candidate in order, the matches in r in DESCENDING
 // position.  The caller (joinalgo.hip) chose this algorithm and sets the
-// result properties.  *uniq_build: the r side had no duplicate key.
+// result properties.  *ukey: the build side had no duplicate key, so no
+// probe row has two matches (r1 holds no repeated oid).
 int
 hash_join(const mgdk_bat *l, const mgdk_bat *r, const Cand &lc, const Cand &rc, bool nil_matches,
-	  mgdk_bat **ap, mgdk_bat **bp)
+	  mgdk_bat **ap, mgdk_bat **bp, bool *ukey)
 {
+	*ukey = false;
 	const BUN nl = lc.n, nr = rc.n;
 	if (nr >= ((BUN) 1 << 32) - 1 || nl >= ((BUN) 1 << 32)) {
 		seterr("42000!BATjoin: more than 2^32 rows per side");
@@ -1255,10 +1259,10 @@ hash_join(const mgdk_bat *l, const mgdk_bat *r, const Cand &lc, const Cand &rc, 
 	side_init(L, l, lc);
 	side_init(R, r, rc);
 	const int w = L.w;
-	int rc_ = w == 4 ? join_part(L, nl, R, nr, nil_matches, ap, bp) : 1;
+	int rc_ = w == 4 ? join_part(L, nl, R, nr, nil_matches, ap, bp, ukey) : 1;
 	if (rc_ > 0)
-		rc_ = w == 8 ? join_lp<8>(L, nl, R, nr, nil_matches, ap, bp)
-			     : join_lp<4>(L, nl, R, nr, nil_matches, ap, bp);
+		rc_ = w == 8 ? join_lp<8>(L, nl, R, nr, nil_matches, ap, bp, ukey)
+			     : join_lp<4>(L, nl, R, nr, nil_matches, ap, bp, ukey);
 	if (rc_ > 0)
 		rc_ = join_csr(L, nl, R, nr, nil_matches, ap, bp);
 	return rc_ < 0 ? -1 : 0;

@@ -30,7 +30,7 @@ using namespace mgdk;
 
 namespace mgdk {
 int hash_join(const mgdk_bat *l, const mgdk_bat *r, const Cand &lc, const Cand &rc, bool nil_matches,
-	      mgdk_bat **ap, mgdk_bat **bp);
+	      mgdk_bat **ap, mgdk_bat **bp, bool *ukey);
 }
 
 namespace {
@@ -701,12 +701,14 @@ hashjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, const Cand &l
 	 bool nil_matches, bool swapped)
 {
 	mgdk_bat *a = nullptr, *b = nullptr;
-	if (hash_join(l, r, lc, rc, nil_matches, &a, &b) < 0)
+	bool ukey = false;
+	if (hash_join(l, r, lc, rc, nil_matches, &a, &b, &ukey) < 0)
 		return -1;
 	const BUN n = a->count;
 	oid af, al, bf, bl;
 	uint32_t adj1 = 0;
-	if (first_last(a, &af, &al) < 0 || first_last(b, &bf, &bl) < 0 || oid_adj(a, &adj1) < 0) {
+	// with unique build keys r1 (ascending) cannot repeat an oid: no scan
+	if (first_last(a, &af, &al) < 0 || first_last(b, &bf, &bl) < 0 || (!ukey && oid_adj(a, &adj1) < 0)) {
 		unfix2(a, b);
 		return -1;
 	}
