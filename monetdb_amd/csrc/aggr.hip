@@ -452,36 +452,20 @@ k_gaggr_k(const void *base, int w, oid off, const GT *gids, oid gseq, oid gmin, 
 	const uint32_t gm = (uint32_t) gmin;
 	const unsigned lane = __lane_id();
 	const BUN nwaves = (BUN) gridDim.x * (blockDim.x / 64);
-	// 1-byte ids: a lane takes U consecutive rows (one 16- or 8-byte load of
-	// ids, U consecutive values); 8-byte ids: row = chunk + u * 64 + lane
+	// LC: 1-byte ids (the image BATgroup keeps), staged per wave in LDS
 	constexpr bool LC = sizeof(GT) == 1;
+	__shared__ uint32_t s_gid[4][LC ? 16 * U : 1];
 	for (BUN ch = (BUN) blockIdx.x * (blockDim.x / 64) + (threadIdx.x / 64); ch * CH < n; ch += nwaves) {
-		const BUN i0 = LC ? ch * CH + (BUN) lane * U : ch * CH + lane;
-		const BUN du = LC ? 1 : 64;
+		// row = chunk base + u * 64 + lane for the values, so every value load
+		// instruction covers 64 consecutive values (a lane-contiguous layout
+		// makes each instruction touch 64 cache lines).  1-byte ids are read
+		// lane-contiguously (one 16- or 8-byte load per lane covers the wave's
+		// chunk) and transposed through the wave's LDS slot.
+		const BUN i0 = ch * CH + lane;
+		constexpr BUN du = 64;
 		uint32_t gi[U];
 		hge v[U];
 		bool nil[U];
-		if constexpr (LC) {
-			if (i0 + U <= n) {
-				uint32_t wds[U / 4];
-				if constexpr (U == 16) {
-					const uint4 q = *(const uint4 *) ((const uint8_t *) gids + i0);
-					wds[0] = q.x, wds[1] = q.y, wds[2] = q.z, wds[3] = q.w;
-				} else {
-					const uint2 q = *(const uint2 *) ((const uint8_t *) gids + i0);
-					wds[0] = q.x, wds[1] = q.y;
-				}
-#pragma unroll
-				for (int u = 0; u < U; u++)
-					gi[u] = ((wds[u / 4] >> (8 * (u % 4))) & 0xffu) - gm;
-			} else {
-#pragma unroll
-				for (int u = 0; u < U; u++) {
-					const BUN i = i0 + (BUN) u;
-					gi[u] = i < n ? (uint32_t) gids[i] - gm : ~0u;
-				}
-			}
-		}
 		// every load is issued unconditionally (at a clamped index) and masked
 		// afterwards: a load under a divergent branch makes the compiler wait
 		// for it before the branch joins, which serialises the U loads
@@ -505,6 +489,39 @@ k_gaggr_k(const void *base, int w, oid off, const GT *gids, oid gseq, oid gmin, 
 				v[u] = 0;
 				nil[u] = false;
 			}
+		}
+		if constexpr (LC) {
+			// one aligned id block per lane at a clamped address (a lane past the
+			// end reads the last block; its rows are masked below): no branch
+			const BUN last = (n - 1) & ~(BUN) (U - 1);
+			const BUN ga = ch * CH + (BUN) lane * U;
+			const uint8_t *gp = (const uint8_t *) gids + (ga <= last ? ga : last);
+			uint32_t wds[U / 4];
+			if constexpr (U == 16) {
+				const uint4 q = *(const uint4 *) gp;
+				wds[0] = q.x, wds[1] = q.y, wds[2] = q.z, wds[3] = q.w;
+			} else {
+				const uint2 q = *(const uint2 *) gp;
+				wds[0] = q.x, wds[1] = q.y;
+			}
+			uint32_t *sw = s_gid[threadIdx.x / 64];
+#pragma unroll
+			for (int q = 0; q < U / 4; q++)
+				sw[lane * (U / 4) + q] = wds[q];
+			__builtin_amdgcn_wave_barrier();
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+			const uint8_t *sb = (const uint8_t *) sw;
+			uint32_t gb8[U];
+#pragma unroll
+			for (int u = 0; u < U; u++)
+				gb8[u] = sb[u * 64 + lane];
+#pragma unroll
+			for (int u = 0; u < U; u++) {
+				const BUN i = i0 + (BUN) u * 64;
+				gi[u] = i < n ? gb8[u] - gm : ~0u;
+			}
+			__builtin_amdgcn_wave_barrier();
 		}
 #pragma unroll
 		for (int u = 0; u < U; u++) {

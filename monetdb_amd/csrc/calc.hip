@@ -180,8 +180,27 @@ ld_any(const void *base, int w, BUN p, bool &isnil)
 	return v;
 }
 
+// typed load for the common 8- and 16-byte operands (one 8- or 16-byte load
+// per value instead of ld_any's 16-byte word), ld_any for the others (W = 0)
+template <int W>
+__device__ __forceinline__ hge
+ld_t(const void *base, int w, BUN p, bool &isnil)
+{
+	if constexpr (W == 8) {
+		const int64_t x = ((const int64_t *) base)[p];
+		isnil = x == INT64_MIN;
+		return x;
+	} else if constexpr (W == 16) {
+		const hge x = ((const hge *) base)[p];
+		isnil = x == (hge) ((uhge) 1 << 127);
+		return x;
+	} else {
+		return ld_any(base, w, p, isnil);
+	}
+}
+
 // fast path: dense candidates (or constants: CA / CB), branch-free loads
-template <int OP, bool CHECK, bool CA, bool CB>
+template <int OP, bool CHECK, bool CA, bool CB, int WA, int WB>
 __global__ __launch_bounds__(256) void
 k_calc_d(Operand a, Operand b, void *out, int ow, hge max, BUN n, hge nilv,
 	 unsigned long long *first_ovf, unsigned long long *nils)
@@ -199,8 +218,8 @@ k_calc_d(Operand a, Operand b, void *out, int ow, hge max, BUN n, hge nilv,
 		for (int u = 0; u < U; u++) {
 			const BUN i = i0 + (BUN) u * 64;
 			const BUN ic = i < n ? i : n - 1;
-			if (CA) { x[u] = a.c; n1[u] = a.cnil; } else x[u] = ld_any(a.base, a.w, a.off + ic, n1[u]);
-			if (CB) { y[u] = b.c; n2[u] = b.cnil; } else y[u] = ld_any(b.base, b.w, b.off + ic, n2[u]);
+			if (CA) { x[u] = a.c; n1[u] = a.cnil; } else x[u] = ld_t<WA>(a.base, a.w, a.off + ic, n1[u]);
+			if (CB) { y[u] = b.c; n2[u] = b.cnil; } else y[u] = ld_t<WB>(b.base, b.w, b.off + ic, n2[u]);
 		}
 #pragma unroll
 		for (int u = 0; u < U; u++) {
@@ -361,15 +380,24 @@ calc(int op, mgdk_bat *b1, const void *v1, int t1, mgdk_bat *b2, const void *v2,
 	}
 	dim3 g(grid_for(n, 256 * 8, 256 * 16)), blk(256);
 	const bool fast = (A.base == nullptr || A.dense) && (B.base == nullptr || B.dense);
-#define LAUNCHD(OPC, CHK, CA_, CB_) hipLaunchKernelGGL((k_calc_d<OPC, CHK, CA_, CB_>), g, blk, 0, stream(), A, B, bn->theap, ow, max, n, nilv, m, m + 1)
+	// operand widths with a typed loader (8 / 16 bytes), 0: generic
+	const int wa = A.base && (A.w == 8 || A.w == 16) ? A.w : 0;
+	const int wb = B.base && (B.w == 8 || B.w == 16) ? B.w : 0;
+#define LAUNCHD(OPC, CHK, CA_, CB_, WA_, WB_) hipLaunchKernelGGL((k_calc_d<OPC, CHK, CA_, CB_, WA_, WB_>), g, blk, 0, stream(), A, B, bn->theap, ow, max, n, nilv, m, m + 1)
+#define LW(OPC, CHK, CA_, CB_, WA_) do { if (wb == 8) LAUNCHD(OPC, CHK, CA_, CB_, WA_, 8); \
+		else if (wb == 16) LAUNCHD(OPC, CHK, CA_, CB_, WA_, 16); else LAUNCHD(OPC, CHK, CA_, CB_, WA_, 0); } while (0)
 #define LAUNCH(OPC, CHK) do { if (!fast) hipLaunchKernelGGL((k_calc<OPC, CHK>), g, blk, 0, stream(), A, B, bn->theap, ow, max, n, nilv, m, m + 1); \
-		else if (A.base == nullptr) LAUNCHD(OPC, CHK, true, false); \
-		else if (B.base == nullptr) LAUNCHD(OPC, CHK, false, true); \
-		else LAUNCHD(OPC, CHK, false, false); } while (0)
+		else if (A.base == nullptr) LW(OPC, CHK, true, false, 0); \
+		else if (B.base == nullptr) { if (wa == 8) LAUNCHD(OPC, CHK, false, true, 8, 0); \
+			else if (wa == 16) LAUNCHD(OPC, CHK, false, true, 16, 0); else LAUNCHD(OPC, CHK, false, true, 0, 0); } \
+		else if (wa == 8) LW(OPC, CHK, false, false, 8); \
+		else if (wa == 16) LW(OPC, CHK, false, false, 16); \
+		else LW(OPC, CHK, false, false, 0); } while (0)
 	if (op == 0) { if (check) LAUNCH(0, true); else LAUNCH(0, false); }
 	else if (op == 1) { if (check) LAUNCH(1, true); else LAUNCH(1, false); }
 	else { if (check) LAUNCH(2, true); else LAUNCH(2, false); }
 #undef LAUNCH
+#undef LW
 #undef LAUNCHD
 	unsigned long long *h = (unsigned long long *) pinned(64);
 	if (h == nullptr || !hip_ok(hipMemcpyAsync(h, m, 16, hipMemcpyDeviceToHost, stream()), "memcpy") || !sync()) {

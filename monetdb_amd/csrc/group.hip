@@ -640,9 +640,9 @@ k_gs_assign(KeySrc s, BUN n, const uint32_t *gmap, uint32_t nslots, uint32_t ngr
 	}
 }
 
-// modes 0 / 1 with 16-byte aligned keys: a lane takes 16 consecutive rows
-// (one 16-byte load of keys and of prior ids, 16-byte stores of ids and of
-// the image), the order flag within the lane and across lanes by a shuffle
+// modes 0 / 1 with 16-byte aligned keys: 16-byte key / prior-id loads per
+// lane, transposed through LDS so that the id and image stores coalesce; the
+// order flag across lanes by shuffles
 template <int K, int MODE>
 __global__ __launch_bounds__(256) void
 k_gs_assign16(KeySrc s, BUN n, const uint32_t *gmap, uint32_t nslots, uint32_t ngrp, oid *gid, uint8_t *img,
@@ -664,49 +664,46 @@ k_gs_assign16(KeySrc s, BUN n, const uint32_t *gmap, uint32_t nslots, uint32_t n
 	const BUN a = (BUN) blockIdx.x * GS_TILE, e = min(n, a + GS_TILE);
 	uint32_t uns = 0;
 	const uint8_t *keys = (const uint8_t *) s.base + s.off;
-	for (BUN i0 = a + (BUN) tid * 16; i0 - (BUN) tid * 16 < e; i0 += (BUN) blockDim.x * 16) {
+	// keys (and prior ids) are read lane-contiguously -- one 16-byte load per
+	// lane covers the wave's 1024 rows -- and transposed through the wave's
+	// LDS slot, so that row = wave base + u * 64 + lane and every id / image
+	// store instruction writes 64 consecutive rows (16-row runs per lane made
+	// each store touch 64 cache lines).  Block addresses are clamped to the
+	// last aligned block (rows past the tile end are masked), so no branch.
+	__shared__ uint4 s_kq[4][64], s_gq[4][MODE == 1 ? 64 : 1];
+	const unsigned w = tid / 64;
+	const BUN last = (n - 1) & ~(BUN) 15;
+	for (BUN wb = a + (BUN) w * 1024; wb < e; wb += (BUN) blockDim.x * 16) {
+		const BUN ga = wb + (BUN) lane * 16 <= last ? wb + (BUN) lane * 16 : last;
+		s_kq[w][lane] = *(const uint4 *) (keys + ga);
+		if (MODE == 1)
+			s_gq[w][lane] = *(const uint4 *) (s.g8 + ga);
+		__builtin_amdgcn_wave_barrier();
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+		const uint8_t *kb = (const uint8_t *) s_kq[w], *gb = (const uint8_t *) s_gq[w];
 		uint32_t g[16];
-		const bool full = i0 + 16 <= e;
-		if (full) {
-			const uint4 kq = *(const uint4 *) (keys + i0);
-			uint4 gq = make_uint4(0, 0, 0, 0);
-			if (MODE == 1)
-				gq = *(const uint4 *) (s.g8 + i0);
-			const uint32_t kw[4] = {kq.x, kq.y, kq.z, kq.w}, gw[4] = {gq.x, gq.y, gq.z, gq.w};
-#pragma unroll
-			for (int u = 0; u < 16; u++) {
-				const uint32_t k = (kw[u / 4] >> (8 * (u % 4))) & 0xffu;
-				const uint32_t pg = (gw[u / 4] >> (8 * (u % 4))) & 0xffu;
-				g[u] = lmap[(pg << 8) | k];
-			}
-			uint4 *go = (uint4 *) (gid + i0);
-#pragma unroll
-			for (int u = 0; u < 16; u += 2) {
-				go[u / 2] = make_uint4(g[u], 0, g[u + 1], 0);
-			}
-			if (img) {
-				uint32_t iw[4] = {0, 0, 0, 0};
-#pragma unroll
-				for (int u = 0; u < 16; u++)
-					iw[u / 4] |= (g[u] & 0xffu) << (8 * (u % 4));
-				*(uint4 *) (img + i0) = make_uint4(iw[0], iw[1], iw[2], iw[3]);
-			}
-		} else {
-#pragma unroll
-			for (int u = 0; u < 16; u++) {
-				const BUN i = i0 + u;
-				g[u] = 0;
-				if (i < e) {
-					g[u] = lmap[gs_slot<MODE>(s, i)];
-					gid[i] = g[u];
-					if (img)
-						img[i] = (uint8_t) g[u];
-				}
-			}
-		}
 #pragma unroll
 		for (int u = 0; u < 16; u++) {
-			const bool ok = i0 + u < e;
+			const uint32_t k = kb[u * 64 + lane];
+			const uint32_t pg = MODE == 1 ? gb[u * 64 + lane] : 0u;
+			const uint32_t sl = (pg << 8) | k;     // bytes past n (masked rows) may hold anything
+			g[u] = lmap[sl < nslots ? sl : 0];
+		}
+		__builtin_amdgcn_wave_barrier();
+		// the row before the wave base: looked up directly (lane 0)
+		uint32_t gprev = 0;
+		if (lane == 0 && wb > 0)
+			gprev = lmap[gs_slot<MODE>(s, wb - 1)];
+#pragma unroll
+		for (int u = 0; u < 16; u++) {
+			const BUN i = wb + (BUN) u * 64 + lane;
+			const bool ok = i < e;
+			if (ok) {
+				gid[i] = g[u];
+				if (img)
+					img[i] = (uint8_t) g[u];
+			}
 			if (K > 0) {
 #pragma unroll
 				for (int k = 0; k < K; k++)
@@ -714,16 +711,14 @@ k_gs_assign16(KeySrc s, BUN n, const uint32_t *gmap, uint32_t nslots, uint32_t n
 			} else if (ok) {
 				atomicAdd(&lh[g[u]], 1u);
 			}
-			if (u > 0 && ok && g[u - 1] > g[u])
+			// previous row: lane - 1 of this step; for lane 0 lane 63 of the
+			// step before (or the looked-up row before the wave base)
+			const uint32_t up = __shfl_up(g[u], 1);
+			const uint32_t l63 = __shfl(g[u > 0 ? u - 1 : 0], 63);
+			const uint32_t gp = lane ? up : u == 0 ? gprev : l63;
+			if (ok && i > 0 && gp > g[u])
 				uns = 1;
 		}
-		// the row before this lane's first: the previous lane's last row, or
-		// (lane 0) looked up directly
-		uint32_t gp = __shfl_up(g[15], 1);
-		if (lane == 0 && i0 > 0 && i0 < e)
-			gp = lmap[gs_slot<MODE>(s, i0 - 1)];
-		if (i0 > 0 && i0 < e && gp > g[0])
-			uns = 1;
 	}
 	if (__any(uns) && lane == 0)
 		publish_or(unsorted, 1u);

@@ -72,6 +72,25 @@ q1_opatatime(mgdk_bat *shipdate, mgdk_bat *rf, mgdk_bat *ls, mgdk_bat *qty, mgdk
 	mgdk_bat *krow = t.add(mgdk_BATproject(e2, c1));   // lineitem oid of each group's first row
 	if (!s1 || !s2 || !s3 || !s4 || !s5 || !cn || !krf || !kls || !krow)
 		return -1;
+	// ORDER BY l_returnflag, l_linestatus: algebra.sort on the first key,
+	// the subsort of the second within its groups, every output column
+	// projected through the final order (the plan's leftfetchjoins)
+	{
+		mgdk_bat *sa, *oa, *ga, *sb, *ob, *gb;
+		if (mgdk_BATsort(&sa, &oa, &ga, krf, nullptr, nullptr, false, false, false) < 0)
+			return -1;
+		t.add(sa), t.add(oa), t.add(ga);
+		if (mgdk_BATsort(&sb, &ob, &gb, kls, oa, ga, false, false, false) < 0)
+			return -1;
+		t.add(sb), t.add(ob);
+		if (gb)
+			t.add(gb);
+		mgdk_bat **outs[] = {&s1, &s2, &s3, &s4, &s5, &cn, &krf, &kls, &krow,
+				     &av[0], &av[1], &av[2], &rm[0], &rm[1], &rm[2]};
+		for (mgdk_bat **o : outs)
+			if (!(*o = t.add(mgdk_BATproject(ob, *o))))
+				return -1;
+	}
 	const BUN ng = e2->count;
 	if ((int) ng > maxgroups) {
 		seterr("q1: more groups (%llu) than room for results", (unsigned long long) ng);

@@ -815,6 +815,76 @@ sort_sub(const mgdk_bat *b, const mgdk_bat *o, const mgdk_bat *g, bool reverse, 
 	return sync() ? 0 : -1;
 }
 
+
+// ---- str columns (strCmp, gdk_atoms.h:414: nil first, then strcmp order) ----
+// A string sorts as a sequence of 64-bit chunk keys: chunk k holds its bytes
+// [7k, 7k + 7) big-endian (0 after the terminator) under a 0x01 tag byte, so
+// every non-nil key is positive and compares like strcmp's unsigned bytes;
+// the nil string gets lng nil, so the lng sort places it exactly as the
+// reference places nil.  Chunk 0 is sorted, each further chunk sub-sorts the
+// groups of equal prefixes.
+__device__ __forceinline__ const uint8_t *
+str_at(const void *offs, int w, const char *vh, BUN i)
+{
+	size_t o;
+	switch (w) {
+	case 1: o = (size_t) ((const uint8_t *) offs)[i] + 8192; break;
+	case 2: o = (size_t) ((const uint16_t *) offs)[i] + 8192; break;
+	case 4: o = (size_t) ((const uint32_t *) offs)[i]; break;
+	default: o = (size_t) ((const uint64_t *) offs)[i]; break;
+	}
+	return (const uint8_t *) vh + o;
+}
+
+__device__ __forceinline__ bool
+str_isnil(const uint8_t *s)
+{
+	return s[0] == 0x80 && s[1] == 0;
+}
+
+__global__ __launch_bounds__(256) void
+k_str_maxlen(const void *offs, int w, const char *vh, BUN n, unsigned long long *maxlen)
+{
+	unsigned long long m = 0;
+	const BUN stride = (BUN) gridDim.x * blockDim.x;
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+		const uint8_t *p = str_at(offs, w, vh, i);
+		if (str_isnil(p))
+			continue;
+		unsigned long long l = 0;
+		while (p[l])
+			l++;
+		m = l > m ? l : m;
+	}
+	m = block_reduce(m, [](unsigned long long a, unsigned long long b) { return a > b ? a : b; });
+	if (threadIdx.x == 0 && m)
+		atomicMax(maxlen, m);
+}
+
+__global__ __launch_bounds__(256) void
+k_str_chunk(const void *offs, int w, const char *vh, BUN n, int k, int64_t *key)
+{
+	const BUN stride = (BUN) gridDim.x * blockDim.x;
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+		const uint8_t *p = str_at(offs, w, vh, i);
+		if (str_isnil(p)) {
+			key[i] = INT64_MIN;
+			continue;
+		}
+		int j = 0;
+		while (j < 7 * k && p[j])
+			j++;
+		uint64_t v = 1;
+		bool end = j < 7 * k;
+		for (int q = 0; q < 7; q++) {
+			const uint8_t c = end ? 0 : p[j + q];
+			end |= c == 0;
+			v = (v << 8) | c;
+		}
+		key[i] = (int64_t) v;
+	}
+}
+
 }  // namespace
 
 namespace mgdk {
@@ -840,6 +910,76 @@ radix_sort_positions32(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, uint3
 }
 
 }  // namespace mgdk
+
+// BATsort of a str column through its chunk keys (see k_str_chunk)
+static int
+sort_str(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b, mgdk_bat *o, mgdk_bat *g,
+	 bool reverse, bool nilslast, bool stable)
+{
+	const BUN n = b->count;
+	hipStream_t st = stream();
+	unsigned long long *m = (unsigned long long *) meta_buf(), *h = (unsigned long long *) pinned(64);
+	if (!hip_ok(hipMemsetAsync(m, 0, 8, st), "memset"))
+		return -1;
+	if (n)
+		hipLaunchKernelGGL(k_str_maxlen, dim3(grid_for(n, 256, 8192)), dim3(256), 0, st, (const void *) b->theap, (int) b->twidth,
+				   (const char *) b->tvheap, n, m);
+	if (!hip_ok(hipMemcpyAsync(h, m, 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+		return -1;
+	const int nch = h[0] > 7 ? (int) ((h[0] + 6) / 7) : 1;
+	mgdk_bat *co = o, *cg = g, *on = nullptr, *gn = nullptr;
+	int rc = 0;
+	for (int k = 0; k < nch && rc == 0; k++) {
+		mgdk_bat *key = newbat(b->hseqbase, MGDK_lng, n);
+		if (!key) {
+			rc = -1;
+			break;
+		}
+		if (n)
+			hipLaunchKernelGGL(k_str_chunk, dim3(grid_for(n, 256, 8192)), dim3(256), 0, st, (const void *) b->theap,
+					   (int) b->twidth, (const char *) b->tvheap, n, k, (int64_t *) key->theap);
+		key->count = n;
+		key->tsorted = key->trevsorted = n <= 1;
+		key->tkey = n <= 1;
+		key->tnonil = b->tnonil;
+		key->tnil = b->tnil;
+		const bool wantg = k + 1 < nch || groups != nullptr;
+		on = gn = nullptr;
+		rc = mgdk_BATsort(nullptr, &on, wantg ? &gn : nullptr, key, co, cg, reverse, nilslast, stable);
+		mgdk_BBPunfix(key);
+		if (co != o)
+			mgdk_BBPunfix(co);
+		if (cg != g)
+			mgdk_BBPunfix(cg);
+		co = on;
+		cg = gn;
+	}
+	if (rc != 0) {
+		if (co != o)
+			mgdk_BBPunfix(co);
+		if (cg != g)
+			mgdk_BBPunfix(cg);
+		return -1;
+	}
+	mgdk_bat *sn = nullptr;
+	if (sorted) {
+		sn = mgdk_BATproject(co, b);
+		if (!sn) {
+			mgdk_BBPunfix(co);
+			mgdk_BBPunfix(cg);
+			return -1;
+		}
+		sn->tsorted = (g == nullptr && !reverse) || n <= 1;
+		sn->trevsorted = (g == nullptr && reverse) || n <= 1;
+		sn->tkey = b->tkey;
+		sn->tnonil = b->tnonil;
+		sn->tnil = b->tnil;
+		*sorted = sn;
+	}
+	if (order) *order = co; else mgdk_BBPunfix(co);
+	if (groups) *groups = cg; else mgdk_BBPunfix(cg);
+	return 0;
+}
 
 extern "C" int
 mgdk_BATsort(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b, mgdk_bat *o, mgdk_bat *g,
@@ -868,6 +1008,10 @@ mgdk_BATsort(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b
 	}
 	if (g == nullptr && !stable)
 		o = nullptr;        // pre-ordering is meaningless for an unstable full sort
+	if (b->ttype == MGDK_str) {
+		ProfScope prof("sort");
+		return sort_str(sorted, order, groups, b, o, g, reverse, nilslast, stable);
+	}
 	const int tt = basetype(b->ttype);
 	if (!(tt == MGDK_bte || tt == MGDK_sht || tt == MGDK_int || tt == MGDK_lng || tt == MGDK_oid ||
 	      tt == MGDK_flt || tt == MGDK_dbl || tt == MGDK_void)) {
