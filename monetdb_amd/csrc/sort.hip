@@ -816,6 +816,101 @@ sort_sub(const mgdk_bat *b, const mgdk_bat *o, const mgdk_bat *g, bool reverse, 
 }
 
 
+// ---- small inputs (n <= 1024): one workgroup, one kernel ------------------
+// every row's rank in the stable order of (group, key image, position) by
+// counting in LDS, then the outputs and the group ids (a workgroup scan of
+// the new-group flags).  Replaces the radix machinery's dozen launches and
+// round trips when a plan sorts a handful of rows (e.g. Q1's ORDER BY).
+constexpr BUN SMALL_SORT = 1024;
+
+template <typename T>
+__global__ __launch_bounds__(1024) void
+k_small_sort(const T *col, const oid *o, oid oseq, oid hseq, const oid *g, oid gseq, bool hasg, uint32_t n,
+	     bool reverse, bool nilslast, T *sorted, oid *order, oid *gid, uint32_t *ngrp)
+{
+	__shared__ uint64_t sk[SMALL_SORT], sg[SMALL_SORT];
+	__shared__ uint32_t sidx[SMALL_SORT], wsum[16];
+	const uint32_t i = threadIdx.x, lane = __lane_id(), w = i >> 6;
+	if (i < n) {
+		const oid src = o ? o[i] : oseq + i;
+		sk[i] = keyimg<T, uint64_t>(col[src - hseq], reverse, nilslast);
+		sg[i] = hasg ? (g ? g[i] : gseq + i) : 0;
+	}
+	__syncthreads();
+	if (i < n) {
+		const uint64_t ki = sk[i], gi = sg[i];
+		uint32_t r = 0;
+		for (uint32_t j = 0; j < n; j++) {
+			const uint64_t kj = sk[j], gj = sg[j];
+			r += gj < gi || (gj == gi && (kj < ki || (kj == ki && j < i)));
+		}
+		sidx[r] = i;
+	}
+	__syncthreads();
+	uint32_t f = 0;
+	if (i < n) {
+		const uint32_t q = sidx[i];
+		const oid src = o ? o[q] : oseq + q;
+		if (order)
+			order[i] = src;
+		if (sorted)
+			sorted[i] = col[src - hseq];
+		if (i > 0) {
+			const uint32_t q0 = sidx[i - 1];
+			f = sg[q] != sg[q0] || sk[q] != sk[q0];
+		}
+	}
+	// inclusive scan of the flags: group id of position i
+	uint32_t x = f;
+#pragma unroll
+	for (int d = 1; d < 64; d <<= 1) {
+		const uint32_t u = __shfl_up(x, d);
+		if (lane >= (unsigned) d)
+			x += u;
+	}
+	if (lane == 63)
+		wsum[w] = x;
+	__syncthreads();
+	uint32_t pre = 0;
+	for (uint32_t q = 0; q < w; q++)
+		pre += wsum[q];
+	if (i < n && gid)
+		gid[i] = pre + x;
+	if (i == n - 1)
+		*ngrp = pre + x;
+}
+
+template <typename T>
+int
+sort_small(const mgdk_bat *b, const mgdk_bat *o, const mgdk_bat *g, bool reverse, bool nilslast, mgdk_bat *sn,
+	   mgdk_bat *on, mgdk_bat *gn)
+{
+	const BUN n = b->count;
+	hipStream_t st = stream();
+	const oid *op = o && o->ttype != MGDK_void ? (const oid *) o->theap : nullptr;
+	const oid oseq = o ? (o->ttype == MGDK_void ? o->tseqbase : 0) : b->hseqbase;
+	const oid *gp = g && g->ttype != MGDK_void ? (const oid *) g->theap : nullptr;
+	uint32_t *m = (uint32_t *) meta_buf(), *h = (uint32_t *) pinned(64);
+	if (!hip_ok(hipMemsetAsync(m, 0, 4, st), "memset"))
+		return -1;
+	if (n)
+		hipLaunchKernelGGL((k_small_sort<T>), dim3(1), dim3(1024), 0, st, (const T *) b->theap, op, oseq, b->hseqbase,
+				   gp, g ? g->tseqbase : 0, g != nullptr, (uint32_t) n, reverse, nilslast,
+				   sn ? (T *) sn->theap : nullptr, on ? (oid *) on->theap : nullptr,
+				   gn ? (oid *) gn->theap : nullptr, m);
+	if (!hip_ok(hipMemcpyAsync(h, m, 4, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+		return -1;
+	if (gn) {
+		const uint64_t tot = h[0];
+		gn->count = n;
+		gn->tsorted = 1;
+		gn->trevsorted = tot == 0;
+		gn->tkey = tot + 1 == n || n <= 1;
+		gn->tnonil = 1;
+	}
+	return 0;
+}
+
 // ---- str columns (strCmp, gdk_atoms.h:414: nil first, then strcmp order) ----
 // A string sorts as a sequence of 64-bit chunk keys: chunk k holds its bytes
 // [7k, 7k + 7) big-endian (0 after the terminator) under a 0x01 tag byte, so
@@ -1025,6 +1120,42 @@ mgdk_BATsort(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b
 	}
 	ProfScope prof("sort");
 	mgdk_bat *sn = nullptr, *on = nullptr, *gn = nullptr;
+	if (n <= SMALL_SORT && tt != MGDK_void) {
+		sn = sorted ? newbat(b->hseqbase, b->ttype, n) : nullptr;
+		on = order ? newbat(b->hseqbase, MGDK_oid, n) : nullptr;
+		gn = groups ? newbat(b->hseqbase, MGDK_oid, n) : nullptr;
+		if ((sorted && !sn) || (order && !on) || (groups && !gn))
+			goto fail;
+		int rc = 0;
+#define SMALL(T) rc = sort_small<T>(b, o, g, reverse, nilslast, sn, on, gn)
+		switch (tt) {
+		case MGDK_bte: SMALL(int8_t); break;
+		case MGDK_sht: SMALL(int16_t); break;
+		case MGDK_int: SMALL(int32_t); break;
+		case MGDK_flt: SMALL(float); break;
+		case MGDK_lng: SMALL(int64_t); break;
+		case MGDK_oid: SMALL(uint64_t); break;
+		case MGDK_dbl: SMALL(double); break;
+		}
+#undef SMALL
+		if (rc < 0)
+			goto fail;
+		if (sn) {
+			sn->count = n;
+			sn->tsorted = (g == nullptr && !reverse) || n <= 1;
+			sn->trevsorted = (g == nullptr && reverse) || n <= 1;
+			sn->tkey = b->tkey;
+			sn->tnonil = b->tnonil;
+			sn->tnil = b->tnil;
+		}
+		if (on) {
+			on->count = n;
+			on->tkey = 1;
+			on->tnonil = 1;
+			on->tsorted = on->trevsorted = 0;   // gdk_batop.c:2622-2624
+		}
+		goto done;
+	}
 	if (o != nullptr || g != nullptr) {
 		if (tt == MGDK_void) {
 			seterr("42000!BATsort: sub-sorting a void column is not supported on the device path");
