@@ -48,6 +48,27 @@ struct Priv {
 	// whenever the tail is written
 	Heap *img8;
 	BUN img8_n;
+	// accelerator of a select result (an oid list from a dense candidate
+	// scan): the scan's predicate bitmap (1 bit per candidate slot) and its
+	// per-tile hit prefixes, so a projection through the list streams the
+	// projected column in row order instead of reading the 8-byte oids and
+	// gathering (see SelMap); dropped with img8 whenever the tail is written
+	Heap *smap;
+	BUN smap_n;
+	uint32_t smap_wpt;       // bitmap words per tile
+	uint64_t smap_ntiles;
+	uint64_t smap_nslots;    // candidate slots covered (incl. the alignment shift)
+	int64_t smap_base;       // oid of slot 0
+	size_t smap_bits_off;    // byte offset of the bitmap in the heap (the prefixes are at 0)
+	oid smap_lo, smap_hi;    // first / last oid of the list
+};
+struct SelMap {
+	const uint32_t *bits;
+	const uint64_t *pre;
+	uint32_t wpt;
+	uint64_t ntiles, nslots;
+	int64_t base;
+	oid lo, hi;
 };
 Heap *heap_new(size_t bytes);                    // refs = 1
 void heap_decref(Heap *h);
@@ -58,7 +79,9 @@ int width_of(int tt);
 // the 1-byte image of b's oid tail, or NULL (see Priv::img8)
 const uint8_t *img8_get(const mgdk_bat *b);
 uint8_t *img8_new(mgdk_bat *b);     // allocate an image for b->count values
-void img8_drop(mgdk_bat *b);
+void img8_drop(mgdk_bat *b);        // drops every accelerator of the tail (img8, smap)
+bool smap_get(const mgdk_bat *b, SelMap *m);
+void smap_set(mgdk_bat *b, Heap *h, const SelMap &m);   // takes a reference on h
 int basetype(int tt);                            // date->int, bit->bte
 const char *atomname(int tt);
 

@@ -95,6 +95,102 @@ launch(const oid *l, BUN n, const void *r, oid rseq, BUN rcnt, const void *nilp,
 			   nilv, (T *) out, flags);
 }
 
+// l carries its select scan's bitmap (Priv::smap): one workgroup per scan
+// tile streams the projected column over the tile's candidate slots in row
+// order (row = slot base + u * 256 + lane: every load covers 256 consecutive
+// values), and each hit goes to the tile's hit prefix + its rank among the
+// tile's set bits (LDS prefix of the word popcounts).  Reads the column once
+// plus n/8 bytes of bitmap instead of 8-byte oids and a gather.
+constexpr uint32_t PB_MAXW = 512;     // bitmap words per tile at most (select's sel_wpt)
+
+template <typename T>
+__global__ __launch_bounds__(256) void
+k_project_bits(const uint32_t *__restrict__ bits, const uint64_t *__restrict__ pre, uint32_t wpt, uint64_t nslots,
+	       int64_t rowbase, BUN rcnt, const T *__restrict__ r, T *__restrict__ out)
+{
+	__shared__ uint32_t s_w[PB_MAXW], s_pre[PB_MAXW];
+	__shared__ uint32_t s_wave[4];
+	const unsigned tid = threadIdx.x, lane = __lane_id(), wave = tid >> 6;
+	const uint64_t t = blockIdx.x;
+	// words of the tile (<= 2 per thread) and their exclusive popcount prefix
+	uint32_t w0 = 0, w1 = 0;
+	if (tid < wpt)
+		w0 = bits[t * wpt + tid];
+	if (tid + 256 < wpt)
+		w1 = bits[t * wpt + tid + 256];
+	// scan in word order: thread tid owns words tid and tid + 256
+	const uint32_t c0 = __popc(w0), c1 = __popc(w1);
+	uint32_t x = c0;
+#pragma unroll
+	for (int o = 1; o < 64; o <<= 1) {
+		const uint32_t y = __shfl_up(x, o);
+		if ((int) lane >= o)
+			x += y;
+	}
+	if (lane == 63)
+		s_wave[wave] = x;
+	__syncthreads();
+	uint32_t ex = x - c0, tot0 = 0;
+	for (unsigned q = 0; q < 4; q++) {
+		ex += q < wave ? s_wave[q] : 0;
+		tot0 += s_wave[q];
+	}
+	__syncthreads();
+	uint32_t x1 = c1;
+#pragma unroll
+	for (int o = 1; o < 64; o <<= 1) {
+		const uint32_t y = __shfl_up(x1, o);
+		if ((int) lane >= o)
+			x1 += y;
+	}
+	if (lane == 63)
+		s_wave[wave] = x1;
+	__syncthreads();
+	uint32_t ex1 = tot0 + x1 - c1;
+	for (unsigned q = 0; q < wave; q++)
+		ex1 += s_wave[q];
+	if (tid < wpt) {
+		s_w[tid] = w0;
+		s_pre[tid] = ex;
+	}
+	if (tid + 256 < wpt) {
+		s_w[tid + 256] = w1;
+		s_pre[tid + 256] = ex1;
+	}
+	__syncthreads();
+	const uint64_t obase = pre[t];
+	const uint64_t s0 = t * (uint64_t) wpt * 32;
+	const uint32_t tslots = wpt * 32;
+	constexpr int U = 16;
+	for (uint32_t r0 = 0; r0 < tslots; r0 += 256 * U) {
+		T v[U];
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const uint64_t j = s0 + r0 + (uint32_t) u * 256 + tid;
+			int64_t row = rowbase + (int64_t) j;
+			row = row < 0 ? 0 : row >= (int64_t) rcnt ? (int64_t) rcnt - 1 : row;   // clamped, masked below
+			v[u] = r[row];
+		}
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const uint32_t sl = r0 + (uint32_t) u * 256 + tid;
+			if (sl >= tslots || s0 + sl >= nslots)
+				continue;
+			const uint32_t wv = s_w[sl >> 5], bit = sl & 31;
+			if ((wv >> bit) & 1)
+				out[obase + s_pre[sl >> 5] + __popc(wv & ((1u << bit) - 1))] = v[u];
+		}
+	}
+}
+
+template <typename T>
+static void
+launch_bits(const SelMap &m, const mgdk_bat *r, void *out)
+{
+	hipLaunchKernelGGL((k_project_bits<T>), dim3((unsigned) m.ntiles), dim3(256), 0, stream(), m.bits, m.pre, m.wpt,
+			   m.nslots, m.base - (int64_t) r->hseqbase, r->count, (const T *) r->theap, (T *) out);
+}
+
 
 // ---- BATproject2 / BATprojectchain (gdk/gdk_project.c:590, :879) --------
 //
@@ -347,7 +443,20 @@ mgdk_BATproject(mgdk_bat *l, mgdk_bat *r)
 	}
 	const oid *lo = (const oid *) l->theap;
 	alignas(16) unsigned char nilv[16] = {0};
-	if (rt == MGDK_void) {
+	SelMap sm;
+	// a select result with its bitmap, all of whose oids lie in r (no nil,
+	// no "does not match"): stream r in row order
+	const bool bits = rt != MGDK_void && smap_get(l, &sm) && sm.wpt <= PB_MAXW && sm.lo >= r->hseqbase &&
+			  sm.hi - r->hseqbase < r->count && r->count > 0;
+	if (bits) {
+		switch (rt == MGDK_str ? r->twidth : width_of(rt)) {
+		case 1: launch_bits<uint8_t>(sm, r, bn->theap); break;
+		case 2: launch_bits<uint16_t>(sm, r, bn->theap); break;
+		case 4: launch_bits<uint32_t>(sm, r, bn->theap); break;
+		case 8: launch_bits<uint64_t>(sm, r, bn->theap); break;
+		default: launch_bits<hge>(sm, r, bn->theap); break;
+		}
+	} else if (rt == MGDK_void) {
 		hipLaunchKernelGGL(k_project_void, dim3(grid_for(n, 256, 256 * 16)), dim3(256), 0, stream(), lo, n,
 				   r->hseqbase, r->count, r->tseqbase, (oid *) bn->theap, flags);
 	} else {

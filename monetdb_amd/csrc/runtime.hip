@@ -386,6 +386,45 @@ img8_drop(mgdk_bat *b)
 		p->img8 = nullptr;
 		p->img8_n = 0;
 	}
+	if (p && p->smap) {
+		heap_decref(p->smap);
+		p->smap = nullptr;
+		p->smap_n = 0;
+	}
+}
+
+bool
+smap_get(const mgdk_bat *b, SelMap *m)
+{
+	const Priv *p = (const Priv *) b->priv;
+	if (p == nullptr || p->smap == nullptr || b->ttype != MGDK_oid || p->smap_n != b->count)
+		return false;
+	m->pre = (const uint64_t *) p->smap->base;
+	m->bits = (const uint32_t *) ((const char *) p->smap->base + p->smap_bits_off);
+	m->wpt = p->smap_wpt;
+	m->ntiles = p->smap_ntiles;
+	m->nslots = p->smap_nslots;
+	m->base = p->smap_base;
+	m->lo = p->smap_lo;
+	m->hi = p->smap_hi;
+	return true;
+}
+
+void
+smap_set(mgdk_bat *b, Heap *h, const SelMap &m)
+{
+	Priv *p = (Priv *) b->priv;
+	img8_drop(b);
+	__atomic_add_fetch(&h->refs, 1, __ATOMIC_ACQ_REL);
+	p->smap = h;
+	p->smap_n = b->count;
+	p->smap_wpt = m.wpt;
+	p->smap_ntiles = m.ntiles;
+	p->smap_nslots = m.nslots;
+	p->smap_base = m.base;
+	p->smap_bits_off = (size_t) ((const char *) m.bits - (const char *) h->base);
+	p->smap_lo = m.lo;
+	p->smap_hi = m.hi;
 }
 
 void
@@ -860,6 +899,7 @@ mgdk_BBPunfix(mgdk_bat *b)
 		heap_decref(p->theap);
 		heap_decref(p->tvheap);
 		heap_decref(p->img8);
+		heap_decref(p->smap);
 		delete p;
 	}
 	free(b);

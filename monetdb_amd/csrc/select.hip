@@ -292,6 +292,8 @@ k_select(SelArgs<T> a)
 //                placed in LDS in order and stored as one contiguous run.
 // The column is read once; extra traffic is the bitmap twice (2 bits/value).
 constexpr int SROWS = 16;
+// results of at least this many oids keep the scan's bitmap (Priv::smap)
+constexpr uint64_t SMAP_MIN = 1 << 20;
 // rows of 16-B loads per lane: 1- and 2-byte types unpack 16 / 8 values per
 // load, so fewer rows keep the count kernel's registers (and occupancy) in
 // line with the 4- and 8-byte types (bte at 16 rows: 140 VGPRs, 0.8 TB/s)
@@ -672,8 +674,14 @@ run_scan(const mgdk_bat *b, const Cand &ci, const SelPred<T> &pred)
 		mgdk_BBPunfix(bn);
 		return nullptr;
 	}
-	// bitmap + counts + prefixes of the streamed scan; freed after the sync below
-	DevBuf sb(streamed ? ntiles * (4 * (size_t) sel_wpt<T>() + 4 + 8) + 64 : 8);
+	// bitmap + counts + prefixes of the streamed scan: kept with the result
+	// as its projection accelerator (Priv::smap) when it stays a list
+	struct HeapRef {
+		Heap *h;
+		~HeapRef() { heap_decref(h); }
+	} sbh{streamed ? heap_new(ntiles * (4 * (size_t) sel_wpt<T>() + 4 + 8) + 64) : nullptr};
+	struct { void *p; } sb{sbh.h ? sbh.h->base : nullptr};
+	uint32_t *smap_bits = nullptr;
 	{
 		const dim3 g((unsigned) ntiles), blk(256);
 		uint32_t *bits = nullptr, *counts = nullptr;
@@ -686,6 +694,7 @@ run_scan(const mgdk_bat *b, const Cand &ci, const SelPred<T> &pred)
 			pre = (uint64_t *) sb.p;
 			counts = (uint32_t *) (pre + ntiles);
 			bits = counts + ntiles + (ntiles & 1);
+			smap_bits = bits;
 		}
 #define SELS(MODE) do { hipLaunchKernelGGL((k_sel_count<T, MODE>), g, blk, 0, st, a, bits, counts); \
 			hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(1024), 0, st, counts, pre, (uint32_t) ntiles, a.meta); \
@@ -725,8 +734,20 @@ run_scan(const mgdk_bat *b, const Cand &ci, const SelPred<T> &pred)
 	bn->tsorted = bn->tkey = bn->tnonil = 1;
 	bn->tnil = 0;
 	bn->trevsorted = cnt <= 1;
-	if (cnt <= 1 || h[3] - h[2] == cnt - 1)
+	if (cnt <= 1 || h[3] - h[2] == cnt - 1) {
 		setdense(bn, cnt ? h[2] : 0, cnt);   // virtualize
+	} else if (streamed && cnt >= SMAP_MIN) {
+		SelMap m{};
+		m.pre = (const uint64_t *) sbh.h->base;
+		m.bits = smap_bits;
+		m.wpt = (uint32_t) sel_wpt<T>();
+		m.ntiles = ntiles;
+		m.nslots = ci.n + a.shift;
+		m.base = (int64_t) (a.cseq - a.shift);
+		m.lo = h[2];
+		m.hi = h[3];
+		smap_set(bn, sbh.h, m);
+	}
 	return bn;
 }
 

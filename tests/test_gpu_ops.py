@@ -787,3 +787,42 @@ def test_grouped_aggregates_candidate_lists(gdk, ora):
     OK = ora.Bat.from_array(ora.TYPE_oid, keep, sorted_=True, key=True, nonil=True)
     assert _same(gdk.BATgroupsum(B, G2, None, gdk.TYPE_hge, True, s=NEG),
                  ora.BATgroupsum(OB, OG2, None, ora.TYPE_hge, True, s=OK))
+
+
+@pytest.mark.parametrize("sel_t", ["int", "lng", "bte"])
+@pytest.mark.parametrize("sel", [0.98, 0.5, 0.02])
+def test_project_through_select_bitmap(gdk, sel_t, sel):
+    """A select result of >= 1M oids keeps its scan bitmap (Priv::smap) and
+    BATproject through it streams the projected column: same values as the
+    oid gather, for every value width (1, 2, 4, 8, 16 B and str offsets),
+    unaligned scan starts (a sliced column), candidate oids offset by the
+    head base, and an r that does not cover the list (the error)."""
+    r = rng(91)
+    n = 3_000_017
+    dt = {"int": np.int32, "lng": np.int64, "bte": np.int8}[sel_t]
+    tp = getattr(gdk, "TYPE_" + sel_t)
+    lim = {"bte": 100, "int": 1_000_000, "lng": 1_000_000}[sel_t]
+    col = r.integers(0, lim, n).astype(dt)
+    thr = int(lim * sel)
+    B = gdk.BAT.from_numpy(tp, col, hseqbase=77)
+    for lo in (0, 3):                       # 3: a view whose data is not 16-B aligned
+        S = gdk.BATslice(B, lo, n) if lo else B
+        c = gdk.BATthetaselect(S, None, thr, "<")
+        want_idx = np.flatnonzero(col[lo:] < thr) + lo
+        assert np.array_equal(c.to_numpy().astype(np.int64), want_idx + 77)
+        for vt, vals in ((gdk.TYPE_lng, r.integers(-2**62, 2**62, n)),
+                         (gdk.TYPE_int, r.integers(-2**30, 2**30, n).astype(np.int32)),
+                         (gdk.TYPE_sht, r.integers(-2**14, 2**14, n).astype(np.int16)),
+                         (gdk.TYPE_bte, r.integers(-100, 100, n).astype(np.int8)),
+                         (gdk.TYPE_dbl, r.standard_normal(n)),
+                         (gdk.TYPE_hge, r.integers(0, 2**63, 2 * n).astype(np.uint64))):
+            V = gdk.BAT.from_numpy(vt, vals, hseqbase=77)
+            got = gdk.BATproject(c, V).to_numpy()
+            want = vals.reshape(n, 2)[want_idx] if vt == gdk.TYPE_hge else vals[want_idx]
+            assert np.array_equal(got.view(np.uint8), np.ascontiguousarray(want).view(np.uint8)), vt
+    # r shorter than the list's range: "does not match always" as with the gather
+    c = gdk.BATthetaselect(B, None, thr, "<")
+    short = gdk.BAT.from_numpy(gdk.TYPE_lng, np.arange(n - 5, dtype=np.int64), hseqbase=77)
+    if want_idx[-1] >= n - 5:
+        with pytest.raises(gdk.GDKError, match="does not match always"):
+            gdk.BATproject(c, short)
