@@ -28,6 +28,7 @@
 //   two-pass count/scan/write probe that walks each bucket backwards.
 // nil never matches unless nil_matches.  Integer key types (bte..lng, date,
 // oid).
+#include <cmath>
 #include <cstdlib>
 #include <vector>
 
@@ -468,6 +469,15 @@ side_init(Side &s, const mgdk_bat *b, const Cand &c)
 	s.cseq = c.seq;
 }
 
+// error return after launches: the stream drains before the caller's
+// buffers go back to the shared allocator cache
+int
+sync_fail()
+{
+	(void) sync();
+	return -1;
+}
+
 void
 unfix2(mgdk_bat *a, mgdk_bat *b)
 {
@@ -768,40 +778,70 @@ k_pj_hist(Side s, BUN n, int pbits, bool skipnil, uint32_t *cnt)
 	}
 }
 
+// XCD-aware remap (cdna_hip_programming.md T1, bijective form): workgroups
+// are dealt round-robin to the 8 XCDs; XCD x gets the contiguous index block
+// [x q + min(x, r), ...) of the G = 8 q + r indices, so neighbouring runs of
+// one partition (written by neighbouring subtiles / partitions) are stored
+// through the same L2, where their partial lines merge
+__device__ __forceinline__ uint32_t
+xcd_block(uint32_t b, uint32_t G)
+{
+	const uint32_t x = b & 7, k = b >> 3, q = G >> 3, r = G & 7;
+	return x * q + (x < r ? x : r) + k;
+}
+
 // scatter of (key, row) entries: one workgroup per subtile, in halves of
 // 16 Ki rows that are counting-sorted by partition in LDS first, so each
-// partition's piece of the run is stored by consecutive lanes
+// partition's piece of the run is stored by consecutive lanes.  Both halves'
+// keys are loaded before the first is ranked (straight-line loads on a full,
+// aligned dense subtile), so the second half's loads are in flight while the
+// first half is staged and stored.
 constexpr uint32_t PJ_HALF = PJ_SUBROWS / 2;
 constexpr int PJ_RPT = PJ_HALF / 1024;         // rows per thread per half
 
-__global__ __launch_bounds__(1024) void
-k_pj_scatter(Side s, BUN n, int pbits, bool skipnil, const uint32_t *off, const uint32_t *base, uint2 *ent)
+template <bool FULL>
+__device__ __forceinline__ void
+pj_scatter_sub(const Side &s, BUN n, int pbits, bool skipnil, BUN a0, uint2 *ent, uint2 *stage, uint32_t *hist,
+	       uint32_t *start, uint32_t *gcur, uint32_t *wsum)
 {
-	__shared__ uint2 stage[PJ_HALF];
-	__shared__ uint32_t hist[1u << PJ_MAXPBITS], start[1u << PJ_MAXPBITS], gcur[1u << PJ_MAXPBITS];
-	__shared__ uint32_t wsum[16];
 	const uint32_t P = 1u << pbits;
 	const unsigned tid = threadIdx.x;
-	const BUN sub = blockIdx.x;
-	const BUN a0 = sub * PJ_SUBROWS;
-	for (uint32_t p = tid; p < P; p += blockDim.x)
-		gcur[p] = base[p] + off[sub * P + p];
+	static_assert(PJ_RPT == 16, "16 rows per thread");
+	uint32_t kk[2][PJ_RPT];
+	bool ok[2][PJ_RPT];
+#pragma unroll
+	for (int half = 0; half < 2; half++) {
+		const BUN i0 = a0 + (BUN) half * PJ_HALF + (BUN) tid * 16;
+		if constexpr (FULL) {
+			typedef int32_t i4 __attribute__((ext_vector_type(4)));
+			const i4 *src = (const i4 *) ((const int32_t *) s.base + s.off + i0);
+#pragma unroll
+			for (int q = 0; q < 4; q++) {
+				const i4 v = __builtin_nontemporal_load(src + q);
+				kk[half][4 * q] = (uint32_t) v.x;
+				kk[half][4 * q + 1] = (uint32_t) v.y;
+				kk[half][4 * q + 2] = (uint32_t) v.z;
+				kk[half][4 * q + 3] = (uint32_t) v.w;
+			}
+#pragma unroll
+			for (int q = 0; q < 16; q++)
+				ok[half][q] = !(skipnil && kk[half][q] == 0x80000000u);
+		} else {
+			pj_keys16(s, i0, min(n, a0 + (BUN) (half + 1) * PJ_HALF), skipnil, kk[half], ok[half]);
+		}
+	}
+#pragma unroll
 	for (int half = 0; half < 2; half++) {
 		const BUN a = a0 + (BUN) half * PJ_HALF;
-		if (a >= n)
+		if (!FULL && a >= n)
 			break;
 		for (uint32_t p = tid; p < P; p += blockDim.x)
 			hist[p] = 0;
 		__syncthreads();
-		static_assert(PJ_RPT == 16, "16 rows per thread");
-		uint32_t kk[PJ_RPT], pp[PJ_RPT], rk[PJ_RPT];
-		{
-			bool ok[16];
-			pj_keys16(s, a + (BUN) tid * 16, min(n, a + PJ_HALF), skipnil, kk, ok);
+		uint32_t pp[PJ_RPT], rk[PJ_RPT];
 #pragma unroll
-			for (int q = 0; q < PJ_RPT; q++)
-				pp[q] = ok[q] ? pj_part32(kk[q], pbits) : ~0u;
-		}
+		for (int q = 0; q < PJ_RPT; q++)
+			pp[q] = ok[half][q] ? pj_part32(kk[half][q], pbits) : ~0u;
 #pragma unroll
 		for (int q = 0; q < PJ_RPT; q++)
 			if (pp[q] != ~0u)
@@ -840,7 +880,7 @@ k_pj_scatter(Side s, BUN n, int pbits, bool skipnil, const uint32_t *off, const 
 #pragma unroll
 		for (int q = 0; q < PJ_RPT; q++)
 			if (pp[q] != ~0u)
-				stage[start[pp[q]] + rk[q]] = make_uint2(kk[q], (uint32_t) (a + (BUN) tid * 16 + q));
+				stage[start[pp[q]] + rk[q]] = make_uint2(kk[half][q], (uint32_t) (a + (BUN) tid * 16 + q));
 		__syncthreads();
 		for (uint32_t j = tid; j < total; j += blockDim.x) {
 			const uint2 en = stage[j];
@@ -852,6 +892,23 @@ k_pj_scatter(Side s, BUN n, int pbits, bool skipnil, const uint32_t *off, const 
 			gcur[p] += hist[p];
 		__syncthreads();
 	}
+}
+
+__global__ __launch_bounds__(1024) void
+k_pj_scatter(Side s, BUN n, int pbits, bool skipnil, const uint32_t *off, const uint32_t *base, uint2 *ent)
+{
+	__shared__ uint2 stage[PJ_HALF];
+	__shared__ uint32_t hist[1u << PJ_MAXPBITS], start[1u << PJ_MAXPBITS], gcur[1u << PJ_MAXPBITS];
+	__shared__ uint32_t wsum[16];
+	const uint32_t P = 1u << pbits;
+	const BUN sub = xcd_block(blockIdx.x, gridDim.x);
+	const BUN a0 = sub * PJ_SUBROWS;
+	for (uint32_t p = threadIdx.x; p < P; p += blockDim.x)
+		gcur[p] = base[p] + off[sub * P + p];
+	if (s.dense && a0 + PJ_SUBROWS <= n && ((s.off + a0) & 3) == 0)
+		pj_scatter_sub<true>(s, n, pbits, skipnil, a0, ent, stage, hist, start, gcur, wsum);
+	else
+		pj_scatter_sub<false>(s, n, pbits, skipnil, a0, ent, stage, hist, start, gcur, wsum);
 }
 
 // column-exclusive prefix of cnt[nsub][P] (64 columns x 16 row groups per
@@ -934,7 +991,7 @@ k_pj_probe(const uint2 *bent, const uint32_t *bbase, const uint2 *pent, const ui
 {
 	__shared__ unsigned long long tab[PJ_SLOTS];
 	__shared__ uint32_t sdelta[PJ_LDS_SUBS];
-	const uint32_t p = blockIdx.x;
+	const uint32_t p = xcd_block(blockIdx.x, gridDim.x);
 	for (uint32_t i = threadIdx.x; i < PJ_SLOTS; i += blockDim.x)
 		tab[i] = 0ull;
 	const uint32_t *dcol = deltaT + (size_t) p * nsub;
@@ -1185,8 +1242,10 @@ join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_b
 	// wastes the probe side's cut)
 	PjSide B, Pr;
 	if (pj_cut(R, nr, pbits, !nil_matches, B, &meta32[0]) < 0 ||
-	    pj_cut(L, nl, pbits, !nil_matches, Pr, &meta32[1]) < 0)
+	    pj_cut(L, nl, pbits, !nil_matches, Pr, &meta32[1]) < 0) {
+		(void) sync();                              // launched cuts still use the buffers
 		return -1;
+	}
 	if (!hip_ok(hipMemcpyAsync(h, meta32, 4, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
 		return -1;
 	if (h[0] > PJ_MAXFILL)
@@ -1196,10 +1255,10 @@ join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_b
 	uint64_t total = 0;
 	if (!offT.p ||
 	    exclusive_scan(Pr.cnt->as<uint32_t>(), offT.as<uint32_t>(), (BUN) Pr.nsub * P, &total) < 0)
-		return -1;
+		return sync_fail();
 	DevBuf deltaT((size_t) Pr.nsub * P * 4 + 64), flat((size_t) nl * 8 + 64);
 	if (!deltaT.p || !flat.p)
-		return -1;
+		return sync_fail();
 	hipLaunchKernelGGL(k_pj_delta, dim3((Pr.nsub + 63) / 64, (P + 63) / 64), dim3(256), 0, st, offT.as<uint32_t>(),
 			   Pr.off->as<uint32_t>(), Pr.base->as<uint32_t>(), Pr.nsub, P, deltaT.as<uint32_t>());
 	hipLaunchKernelGGL(k_pj_probe, dim3(P), dim3(1024), 0, st, B.ent->as<uint2>(), B.base->as<uint32_t>(),
@@ -1214,7 +1273,7 @@ join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_b
 	char *sc = (char *) scratch(sbytes);
 	if (!ra || !rb || !sc || !hip_ok(hipMemsetAsync(sc, 0, sbytes, st), "memset")) {
 		unfix2(ra, rb);
-		return -1;
+		return sync_fail();
 	}
 	hipLaunchKernelGGL(k_pj_restore, dim3(Pr.nsub), dim3(1024), 0, st, flat.as<uint2>(), offT.as<uint32_t>(), P,
 			   total, nl, Pr.nsub, L, R, (uint32_t *) sc, (uint64_t *) sc + 8, meta, (oid *) ra->theap,
@@ -1231,6 +1290,283 @@ join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_b
 	}
 	ra->count = rb->count = h64[0];
 	*ukey = true;                                       // unique build keys: one match per row
+	*ap = ra;
+	*bp = rb;
+	return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Global-table path (4-byte keys, unique build keys, build side <= ~20M
+// rows): only the build side is cut (the pj_cut passes above).  One
+// workgroup per partition builds the partition's table in LDS and stores it
+// whole as region p of ONE global table -- P regions of nbp 16-byte buckets
+// (2 slots of key image + position + 1), linear probing inside the region,
+// no global atomics.  At load <= 3/4 the table of 15M keys is ~170 MB, which
+// stays resident in the 256 MB Infinity Cache while the probe streams past
+// it (MI355X_MICROARCH.md "Infinity Cache": table + bytes moved between two
+// uses of a line <= 256 MiB).  The probe is ONE ordered pass over the left
+// side: per row a 4-byte key load and (almost always) one 16-byte bucket
+// load served on-die, matches ranked per tile and placed by decoupled
+// look-back, so r1 comes out in left order with no probe-side cut, no
+// partition-major intermediate and no restore pass.  Duplicate build keys or
+// an overfull region are found by the build, after which the probe's result
+// is dropped and the caller falls back.
+// ---------------------------------------------------------------------------
+
+constexpr uint32_t GT_MAXB = PJ_SLOTS / 2;         // buckets per region (the LDS build table)
+
+__device__ __forceinline__ uint32_t
+gt_home(uint32_t hk, int pbits, uint32_t nbp)
+{
+	return __umulhi(hk << pbits, nbp);
+}
+
+// flags[0] |= 1: duplicate build key; flags[1] |= 1: a partition does not
+// fit its region
+__global__ __launch_bounds__(1024) void
+k_gt_build(const uint2 *bent, const uint32_t *bbase, int pbits, uint32_t nbp, ulonglong2 *gtab, uint32_t *flags)
+{
+	__shared__ unsigned long long tab[PJ_SLOTS];
+	const uint32_t p = blockIdx.x, ns = 2 * nbp;
+	for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x)
+		tab[i] = 0ull;
+	__syncthreads();
+	const uint32_t b0 = bbase[p], b1 = bbase[p + 1];
+	// an empty slot must remain so that every probe ends
+	const bool fits = b1 - b0 < ns;
+	bool dup = false;
+	if (fits)
+		for (uint32_t e = b0 + threadIdx.x; e < b1; e += blockDim.x) {
+			const uint2 en = bent[e];
+			const unsigned long long v = ((unsigned long long) (en.y + 1) << 32) | en.x;
+			uint32_t s = 2 * gt_home(pj_hash(en.x), pbits, nbp);
+			// every slot passed over is observed with its final content,
+			// so of two equal keys the later one always sees the earlier
+			for (;;) {
+				const unsigned long long o = atomicCAS(&tab[s], 0ull, v);
+				if (o == 0ull)
+					break;
+				if ((uint32_t) o == en.x) {
+					dup = true;
+					break;
+				}
+				s = s + 1 == ns ? 0 : s + 1;
+			}
+		}
+	if (__any(dup) && __lane_id() == 0)
+		atomicOr(&flags[0], 1u);
+	if (!fits && threadIdx.x == 0)
+		atomicOr(&flags[1], 1u);
+	__syncthreads();
+	ulonglong2 *dst = gtab + (size_t) p * nbp;
+	for (uint32_t i = threadIdx.x; i < nbp; i += blockDim.x)
+		dst[i] = make_ulonglong2(tab[2 * i], tab[2 * i + 1]);
+}
+
+struct GtArgs {
+	Side l, r;
+	BUN n;
+	int pbits;
+	uint32_t nbp;
+	bool nil_matches;
+	uint32_t *ticket;
+	uint64_t *status;
+	uint32_t ntiles;
+	uint64_t *meta;       // [0] total pairs, [1] look-back error
+	oid *r1, *r2;
+};
+
+constexpr int GT_JR = 8;                           // rows per lane in a probe tile
+
+// match position + 1 of key k in its region (0: none); the first bucket is
+// already loaded
+__device__ __forceinline__ uint32_t
+gt_find(const ulonglong2 *t, uint32_t k, ulonglong2 s, uint32_t reg, uint32_t b, uint32_t nbp)
+{
+	for (uint32_t d = 0;; d++) {
+		if (s.x == 0ull)
+			return 0;
+		if ((uint32_t) s.x == k)
+			return (uint32_t) (s.x >> 32);
+		if (s.y == 0ull)
+			return 0;
+		if ((uint32_t) s.y == k)
+			return (uint32_t) (s.y >> 32);
+		if (d >= nbp)
+			return 0;                      // (cannot happen: a region keeps an empty slot)
+		b = b + 1 == nbp ? 0 : b + 1;
+		s = t[(size_t) reg * nbp + b];
+	}
+}
+
+template <bool DENSE>
+__global__ __launch_bounds__(256) void
+k_gt_probe(GtArgs a, const ulonglong2 *t)
+{
+	constexpr int JR = GT_JR, JTILE = 256 * JR;
+	__shared__ uint32_t s_tot[64];     // [r][wave]
+	__shared__ uint64_t s_off[64];
+	__shared__ uint32_t s_tile;
+	__shared__ uint64_t s_pre;
+	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+	if (tid == 0)
+		s_tile = atomicAdd(a.ticket, 1u);
+	if (JR * 4 < 64 && tid < 64)
+		s_tot[tid] = 0;
+	__syncthreads();
+	const uint32_t tile = s_tile;
+	const BUN base = (BUN) tile * JTILE + tid;
+	const int32_t *kb = (const int32_t *) a.l.base;
+
+	// every load unconditional (clamped row): a load under a branch is
+	// waited for before the branch joins
+	uint32_t key[JR];
+	bool ok[JR];
+#pragma unroll
+	for (int r = 0; r < JR; r++) {
+		const BUN i = base + (BUN) r * 256;
+		const BUN ic = i < a.n ? i : a.n - 1;
+		key[r] = (uint32_t) (DENSE ? __builtin_nontemporal_load(&kb[a.l.off + ic]) : kb[a.l.oids[ic] - a.l.hseq]);
+		ok[r] = i < a.n && (key[r] != 0x80000000u || a.nil_matches);
+	}
+	uint32_t reg[JR], bk[JR];
+	ulonglong2 sv[JR];
+#pragma unroll
+	for (int r = 0; r < JR; r++) {
+		const uint32_t h = pj_hash(key[r]);
+		reg[r] = h >> (32 - a.pbits);
+		bk[r] = gt_home(h, a.pbits, a.nbp);
+		sv[r] = t[(size_t) reg[r] * a.nbp + bk[r]];
+	}
+	uint32_t m[JR];
+#pragma unroll
+	for (int r = 0; r < JR; r++)
+		m[r] = ok[r] ? gt_find(t, key[r], sv[r], reg[r], bk[r], a.nbp) : 0;
+	// ranks: one ballot per row slot r, then a 32-entry scan over (r, wave)
+	uint32_t ex[JR];
+#pragma unroll
+	for (int r = 0; r < JR; r++) {
+		const uint64_t bal = __ballot(m[r] != 0);
+		ex[r] = __popcll(bal & ((1ull << lane) - 1));
+		if (lane == 0)
+			s_tot[r * 4 + w] = __popcll(bal);
+	}
+	__syncthreads();
+	if (w == 0) {
+		uint64_t v = s_tot[lane];
+		const uint64_t own = v;
+#pragma unroll
+		for (int o = 1; o < 64; o <<= 1) {
+			const uint64_t u = __shfl_up(v, o);
+			if (lane >= (unsigned) o)
+				v += u;
+		}
+		s_off[lane] = v - own;
+		const uint64_t agg = __shfl(v, 63);
+		const uint64_t pre = lookback(a.status, tile, agg, (uint32_t *) &a.meta[1]);
+		if (lane == 0) {
+			s_pre = pre;
+			if (tile == a.ntiles - 1)
+				a.meta[0] = pre + agg;
+		}
+	}
+	__syncthreads();
+	const uint64_t pre = s_pre;
+#pragma unroll
+	for (int r = 0; r < JR; r++) {
+		if (m[r] == 0)
+			continue;
+		const uint64_t pos = pre + s_off[r * 4 + w] + ex[r];
+		const BUN i = base + (BUN) r * 256;
+		__builtin_nontemporal_store(oid_of(a.l, i), &a.r1[pos]);
+		__builtin_nontemporal_store(oid_of(a.r, m[r] - 1), &a.r2[pos]);
+	}
+}
+
+// returns 1 when not applicable (caller tries the next path)
+int
+join_gt(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_bat **ap, mgdk_bat **bp, bool *ukey)
+{
+	static const int mode = getenv("MGDK_JOIN_GT") ? atoi(getenv("MGDK_JOIN_GT")) : 1;
+	static const int lfpct = getenv("MGDK_JOIN_GT_LF") ? atoi(getenv("MGDK_JOIN_GT_LF")) : 72;
+	// the probe's bucket loads pull whole 128-B lines: past ~2M build rows
+	// (a ~25 MB table) they cost more than cutting the probe side too
+	// (tools/join_sweep.py: 0.18 vs 0.25 ms at 600 K, 0.26 vs 0.27 at 1.5 M,
+	// 0.47 vs 0.42 at 4 M build rows); MGDK_JOIN_GT=2 forces the path
+	if (mode == 0 || L.w != 4 || R.w != 4 || nr < 65536 || nl == 0 || (mode == 1 && nr > 2000000))
+		return 1;
+	int pbits = 6;
+	while (pbits < PJ_MAXPBITS && ((BUN) 8192 << pbits) < nr)
+		pbits++;
+	const uint32_t P = 1u << pbits;
+	// region size from the expected largest partition (mean + 6 sigma): no
+	// round trip to read the real one; a partition that does not fit is
+	// reported by the build and sends the join down the partitioned path
+	const double mean = (double) nr / P;
+	const double mx = mean + 6.0 * sqrt(mean) + 64.0;
+	uint64_t nbp = (uint64_t) (mx * 100.0 / (2.0 * (lfpct < 40 ? 40 : lfpct > 90 ? 90 : lfpct))) + 1;
+	if (nbp > GT_MAXB)
+		return 1;
+	const uint64_t jtile = 256 * GT_JR;
+	const uint64_t ntiles = (nl + jtile - 1) / jtile;
+	if (ntiles >= (1ull << 31))
+		return 1;
+	hipStream_t st = stream();
+	uint32_t *meta32 = (uint32_t *) meta_buf();
+	uint64_t *meta = (uint64_t *) meta32 + 4;          // [0] pairs, [1] look-back error
+	if (!hip_ok(hipMemsetAsync(meta32, 0, 64, st), "memset"))
+		return -1;
+	PjSide B;
+	DevBuf gtab((size_t) P * nbp * 16 + 64);
+	mgdk_bat *ra = newbat(0, MGDK_oid, nl), *rb = newbat(0, MGDK_oid, nl);
+	const size_t sbytes = (ntiles + 8) * sizeof(uint64_t);
+	char *sc = (char *) scratch(sbytes);
+	if (!gtab.p || !ra || !rb || !sc || pj_cut(R, nr, pbits, !nil_matches, B, &meta32[3]) < 0) {
+		(void) sync();                              // kernels may still read B's buffers
+		unfix2(ra, rb);
+		return -1;
+	}
+	hipLaunchKernelGGL(k_gt_build, dim3(P), dim3(1024), 0, st, B.ent->as<uint2>(), B.base->as<uint32_t>(), pbits,
+			   (uint32_t) nbp, gtab.as<ulonglong2>(), &meta32[0]);
+	GtArgs a{};
+	a.l = L;
+	a.r = R;
+	a.n = nl;
+	a.pbits = pbits;
+	a.nbp = (uint32_t) nbp;
+	a.nil_matches = nil_matches;
+	a.ticket = (uint32_t *) sc;
+	a.status = (uint64_t *) sc + 8;
+	a.ntiles = (uint32_t) ntiles;
+	a.meta = meta;
+	a.r1 = (oid *) ra->theap;
+	a.r2 = (oid *) rb->theap;
+	if (!hip_ok(hipMemsetAsync(sc, 0, sbytes, st), "memset")) {
+		(void) sync();
+		unfix2(ra, rb);
+		return -1;
+	}
+	if (L.dense)
+		hipLaunchKernelGGL(k_gt_probe<true>, dim3((unsigned) ntiles), dim3(256), 0, st, a, gtab.as<ulonglong2>());
+	else
+		hipLaunchKernelGGL(k_gt_probe<false>, dim3((unsigned) ntiles), dim3(256), 0, st, a, gtab.as<ulonglong2>());
+	uint32_t *h = (uint32_t *) pinned(64);
+	if (!hip_ok(hipMemcpyAsync(h, meta32, 64, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
+		unfix2(ra, rb);
+		return -1;
+	}
+	if (h[0] || h[1]) {                                 // duplicate build keys / region overflow
+		unfix2(ra, rb);
+		return 1;
+	}
+	const uint64_t *h64 = (const uint64_t *) h + 4;   // = meta
+	if (h64[1] & 1) {
+		seterr("HY013!BATjoin: look-back did not complete");
+		unfix2(ra, rb);
+		return -1;
+	}
+	ra->count = rb->count = h64[0];
+	*ukey = true;
 	*ap = ra;
 	*bp = rb;
 	return 0;
@@ -1259,7 +1595,9 @@ hash_join(const mgdk_bat *l, const mgdk_bat *r, const Cand &lc, const Cand &rc, 
 	side_init(L, l, lc);
 	side_init(R, r, rc);
 	const int w = L.w;
-	int rc_ = w == 4 ? join_part(L, nl, R, nr, nil_matches, ap, bp, ukey) : 1;
+	int rc_ = w == 4 ? join_gt(L, nl, R, nr, nil_matches, ap, bp, ukey) : 1;
+	if (rc_ > 0 && w == 4)
+		rc_ = join_part(L, nl, R, nr, nil_matches, ap, bp, ukey);
 	if (rc_ > 0)
 		rc_ = w == 8 ? join_lp<8>(L, nl, R, nr, nil_matches, ap, bp, ukey)
 			     : join_lp<4>(L, nl, R, nr, nil_matches, ap, bp, ukey);

@@ -84,13 +84,25 @@ def test_join_unique_build(gdk, ora, tname, dt):
 
 
 @pytest.mark.parametrize("nil_matches", [False, True])
-@pytest.mark.parametrize("case", ["plain", "cands", "dups", "date"])
+@pytest.mark.parametrize("case", ["plain", "cands", "dups", "date", "skew", "big"])
 def test_join_partitioned(gdk, ora, nil_matches, case):
-    """Radix-partitioned LDS path (4-byte keys, >= 64 Ki unique build rows):
-    nils on both sides, candidate lists, a duplicate build key (falls back)."""
+    """4-byte keys, >= 64 Ki unique build rows: the global-table path (build
+    side cut into per-partition LDS tables stored as one table, one ordered
+    probe pass), nils on both sides, candidate lists, a duplicate build key
+    (falls back), and a skewed build side whose largest partition overflows
+    its global-table region (-> the radix-partitioned path)."""
     r = rng(85)
-    nr, nl = 700_001, 2_500_003
+    # "big": more than 2M build rows take the radix-partitioned path
+    nr, nl = (2_100_003, 3_000_001) if case == "big" else (700_001, 2_500_003)
     rv = r.choice(np.arange(-(1 << 30), 1 << 30, 7), nr, replace=False).astype(np.int32)
+    if case == "skew":
+        # 9000 keys whose multiplicative hash (key * 0x9E3779B1, top 7 bits =
+        # partition of 700K build rows) lands in partition 0
+        cinv = pow(0x9E3779B1, -1, 1 << 32)
+        t = r.choice(1 << 25, 9000, replace=False).astype(np.uint64)
+        sk = ((t * np.uint64(cinv)) & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.int32)
+        sk = sk[(sk != -(1 << 31)) & ~np.isin(sk, rv)]
+        rv[: sk.size] = sk
     rv[123] = -(1 << 31)                                   # one nil (unique)
     lv = r.choice(rv, nl).astype(np.int32)
     lv[r.random(nl) < 0.05] = r.integers(-100, 100)        # misses
