@@ -695,6 +695,14 @@ pj_home(uint32_t key, int pbits)
 	return (pj_hash(key) >> (32 - pbits - 14)) & (PJ_SLOTS - 1);
 }
 
+// home bucket of a key in a table of nbp buckets: the hash bits below the
+// partition bits, scaled
+__device__ __forceinline__ uint32_t
+gt_home(uint32_t hk, int pbits, uint32_t nbp)
+{
+	return __umulhi(hk << pbits, nbp);
+}
+
 // 1024-thread workgroup reduction (16 waves); result valid in thread 0
 template <typename T, typename F>
 __device__ __forceinline__ T
@@ -984,24 +992,27 @@ k_pj_base(const uint32_t *tot, uint32_t P, uint32_t *base, uint32_t *maxtot)
 // one workgroup per partition: LDS table of the build entries, then each
 // probe entry of the partition is answered and stored, as (match position +
 // 1 or 0, row), at its subtile-major place in the flat array (the column of
-// run offsets deltaT[p][*] staged in LDS)
+// run offsets deltaT[p][*] staged in LDS).  The table is nbp 16-byte buckets
+// (2 slots, linear probing over slots from an even home slot) sized from the
+// largest build partition, in dynamic LDS together with the offsets column:
+// at ~80 % load a 15M-row build side needs < 80 KiB, so two workgroups share
+// a CU and one's table build overlaps the other's probe.
 __global__ __launch_bounds__(1024) void
 k_pj_probe(const uint2 *bent, const uint32_t *bbase, const uint2 *pent, const uint32_t *pbase, int pbits,
-	   const uint32_t *deltaT, uint32_t nsub, uint2 *flat, uint32_t *dupflag)
+	   uint32_t nbp, const uint32_t *deltaT, uint32_t nsub, bool ldsd, uint2 *flat, uint32_t *dupflag)
 {
-	__shared__ unsigned long long tab[PJ_SLOTS];
-	__shared__ uint32_t sdelta[PJ_LDS_SUBS];
-	const uint32_t p = xcd_block(blockIdx.x, gridDim.x);
-	for (uint32_t i = threadIdx.x; i < PJ_SLOTS; i += blockDim.x)
+	extern __shared__ __attribute__((aligned(16))) unsigned long long dyn[];
+	unsigned long long *tab = dyn;
+	uint32_t *sdelta = (uint32_t *) (dyn + 2 * nbp);
+	const uint32_t p = xcd_block(blockIdx.x, gridDim.x), ns = 2 * nbp;
+	for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x)
 		tab[i] = 0ull;
 	const uint32_t *dcol = deltaT + (size_t) p * nsub;
-	const bool ldsd = nsub <= PJ_LDS_SUBS;
 	if (ldsd)
 		for (uint32_t i = threadIdx.x; i < nsub; i += blockDim.x)
 			sdelta[i] = dcol[i];
 	__syncthreads();
-	// the first batch of probe entries is loaded while the table is built
-	// (one workgroup per CU: nothing else would hide the build's latency),
+	// the first batch of probe entries is loaded while the table is built,
 	// and every later batch while the previous one is answered
 	constexpr int U = 8;
 	const uint32_t q0 = pbase[p], q1 = pbase[p + 1];
@@ -1009,14 +1020,14 @@ k_pj_probe(const uint2 *bent, const uint32_t *bbase, const uint2 *pent, const ui
 #pragma unroll
 	for (int u = 0; u < U; u++) {
 		const uint32_t e = q0 + threadIdx.x + u * blockDim.x;
-		cur[u] = e < q1 ? pent[e] : make_uint2(0, 0);
+		cur[u] = pent[e < q1 ? e : q0];
 	}
 	const uint32_t b0 = bbase[p], b1 = bbase[p + 1];
 	bool dup = false;
 	for (uint32_t e = b0 + threadIdx.x; e < b1; e += blockDim.x) {
 		const uint2 en = bent[e];
 		const unsigned long long v = ((unsigned long long) (en.y + 1) << 32) | en.x;
-		uint32_t h = pj_home(en.x, pbits);
+		uint32_t h = 2 * gt_home(pj_hash(en.x), pbits, nbp);
 		for (;;) {
 			const unsigned long long o = atomicCAS(&tab[h], 0ull, v);
 			if (o == 0ull)
@@ -1025,32 +1036,39 @@ k_pj_probe(const uint2 *bent, const uint32_t *bbase, const uint2 *pent, const ui
 				dup = true;
 				break;
 			}
-			h = (h + 1) & (PJ_SLOTS - 1);
+			h = h + 1 == ns ? 0 : h + 1;
 		}
 	}
 	if (__any(dup) && __lane_id() == 0)
 		atomicOr(dupflag, 1u);
 	__syncthreads();
+	const ulonglong2 *bk = (const ulonglong2 *) tab;
 	for (uint32_t e0 = q0 + threadIdx.x; e0 < q1; e0 += U * blockDim.x) {
 		uint2 en[U], nxt[U];
 #pragma unroll
 		for (int u = 0; u < U; u++) {
 			en[u] = cur[u];
 			const uint32_t e = e0 + (U + u) * blockDim.x;
-			nxt[u] = e < q1 ? pent[e] : make_uint2(0, 0);
+			nxt[u] = pent[e < q1 ? e : q0];
 		}
 #pragma unroll
 		for (int u = 0; u < U; u++) {
-			uint32_t h = pj_home(en[u].x, pbits), m = 0;
+			uint32_t b = gt_home(pj_hash(en[u].x), pbits, nbp), m = 0;
 			for (;;) {
-				const unsigned long long o = tab[h];
-				if (o == 0ull)
+				const ulonglong2 sl = bk[b];
+				if (sl.x == 0ull)
 					break;
-				if ((uint32_t) o == en[u].x) {
-					m = (uint32_t) (o >> 32);
+				if ((uint32_t) sl.x == en[u].x) {
+					m = (uint32_t) (sl.x >> 32);
 					break;
 				}
-				h = (h + 1) & (PJ_SLOTS - 1);
+				if (sl.y == 0ull)
+					break;
+				if ((uint32_t) sl.y == en[u].x) {
+					m = (uint32_t) (sl.y >> 32);
+					break;
+				}
+				b = b + 1 == nbp ? 0 : b + 1;
 			}
 			en[u].x = m;
 		}
@@ -1261,9 +1279,22 @@ join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_b
 		return sync_fail();
 	hipLaunchKernelGGL(k_pj_delta, dim3((Pr.nsub + 63) / 64, (P + 63) / 64), dim3(256), 0, st, offT.as<uint32_t>(),
 			   Pr.off->as<uint32_t>(), Pr.base->as<uint32_t>(), Pr.nsub, P, deltaT.as<uint32_t>());
-	hipLaunchKernelGGL(k_pj_probe, dim3(P), dim3(1024), 0, st, B.ent->as<uint2>(), B.base->as<uint32_t>(),
-			   Pr.ent->as<uint2>(), Pr.base->as<uint32_t>(), pbits, deltaT.as<uint32_t>(), Pr.nsub,
-			   flat.as<uint2>(), &meta32[2]);
+	// table: ~80 % load on the largest build partition (an empty slot always
+	// remains); LDS = table + the probe's offsets column when it fits
+	static const int lfpct = getenv("MGDK_PJ_LF") ? atoi(getenv("MGDK_PJ_LF")) : 80;
+	uint32_t nbp = (uint32_t) ((uint64_t) h[0] * 100 / (2 * (uint64_t) (lfpct < 40 ? 40 : lfpct > 95 ? 95 : lfpct))) + 1;
+	if (2 * nbp <= h[0])
+		nbp = h[0] / 2 + 1;
+	nbp = nbp < PJ_SLOTS / 2 ? nbp : PJ_SLOTS / 2;    // (h[0] <= PJ_MAXFILL keeps load < 3/4)
+	const bool ldsd = Pr.nsub <= PJ_LDS_SUBS;
+	const size_t lds = (size_t) nbp * 16 + (ldsd ? (size_t) Pr.nsub * 4 : 0);
+	static const bool lds_attr = hipFuncSetAttribute((const void *) k_pj_probe,
+							 hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) == hipSuccess;
+	(void) lds_attr;
+	(void) hipGetLastError();
+	hipLaunchKernelGGL(k_pj_probe, dim3(P), dim3(1024), lds, st, B.ent->as<uint2>(), B.base->as<uint32_t>(),
+			   Pr.ent->as<uint2>(), Pr.base->as<uint32_t>(), pbits, nbp, deltaT.as<uint32_t>(), Pr.nsub,
+			   ldsd, flat.as<uint2>(), &meta32[2]);
 	if (!hip_ok(hipMemcpyAsync(h, meta32, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
 		return -1;
 	if (h[2])
@@ -1314,12 +1345,6 @@ join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_b
 // ---------------------------------------------------------------------------
 
 constexpr uint32_t GT_MAXB = PJ_SLOTS / 2;         // buckets per region (the LDS build table)
-
-__device__ __forceinline__ uint32_t
-gt_home(uint32_t hk, int pbits, uint32_t nbp)
-{
-	return __umulhi(hk << pbits, nbp);
-}
 
 // flags[0] |= 1: duplicate build key; flags[1] |= 1: a partition does not
 // fit its region
