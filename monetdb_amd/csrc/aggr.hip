@@ -766,6 +766,24 @@ aggr_init(AggrInit *a, mgdk_bat **bp, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s)
 	return 0;
 }
 
+// accumulator block of run_gaggr: sums and counts 0, first positions ~0,
+// last-nil 0, min / max at their identities, the magnitude class 0
+__global__ __launch_bounds__(256) void
+k_gacc_init(GAcc acc, BUN ng, unsigned long long *maxabs)
+{
+	for (BUN k = (BUN) blockIdx.x * blockDim.x + threadIdx.x; k < ng; k += (BUN) gridDim.x * blockDim.x) {
+		acc.sum[2 * k] = 0;
+		acc.sum[2 * k + 1] = 0;
+		acc.cnt[k] = 0;
+		acc.firstval[k] = ~0ull;
+		acc.lastnil[k] = 0;
+		acc.mn[k] = INT64_MAX;
+		acc.mx[k] = INT64_MIN;
+	}
+	if (blockIdx.x == 0 && threadIdx.x == 0)
+		*maxabs = 0;
+}
+
 struct GRes {
 	std::vector<hge> sum;
 	std::vector<unsigned long long> cnt, firstval, lastnil;
@@ -790,17 +808,10 @@ run_gaggr(const AggrInit &a, mgdk_bat *b, int what, bool count_all, GRes &r)
 	acc.mx = acc.mn + ng;
 	unsigned long long *maxabs = (unsigned long long *) (acc.mx + ng);
 	hipStream_t st = stream();
-	if (!hip_ok(hipMemsetAsync(d, 0, (size_t) ng * 32, st), "memset") ||
-	    !hip_ok(hipMemsetAsync(acc.firstval, 0xff, ng * 8, st), "memset") ||
-	    !hip_ok(hipMemsetAsync(acc.lastnil, 0, ng * 8, st), "memset") ||
-	    !hip_ok(hipMemsetAsync(maxabs, 0, 8, st), "memset"))
-		return -1;
-	if (what & AGG_MINMAX) {
-		std::vector<long long> mn(ng, INT64_MAX), mx(ng, INT64_MIN);
-		if (!hip_ok(hipMemcpyAsync(acc.mn, mn.data(), ng * 8, hipMemcpyHostToDevice, st), "memcpy") ||
-		    !hip_ok(hipMemcpyAsync(acc.mx, mx.data(), ng * 8, hipMemcpyHostToDevice, st), "memcpy") || !sync())
-			return -1;
-	}
+	// one init launch, one read-back of the whole accumulator block and one
+	// wait: the operator's host round trips, not its kernels, dominated
+	// small-group aggregates
+	hipLaunchKernelGGL(k_gacc_init, dim3(grid_for(ng + 1, 256, 1024)), dim3(256), 0, st, acc, ng, maxabs);
 	const oid off = a.ci.seq - b->hseqbase;
 	dim3 g(grid_for(a.ci.n, 256 * 8, 256 * 16)), blk(256);
 	// COUNT(*) over few groups needs no values (k_gaggr_k's base == NULL)
@@ -833,8 +844,6 @@ run_gaggr(const AggrInit &a, mgdk_bat *b, int what, bool count_all, GRes &r)
 			else
 				GK(8);
 			hipLaunchKernelGGL(k_gaggr_fin, dim3(kk), dim3(256), 0, st, parts.as<GPart>(), nw, kk, ng, acc, maxabs);
-			if (!sync())
-				return -1;
 		}
 		else
 			hipLaunchKernelGGL((k_gaggr<0>), g, blk, 0, st, b->theap, b->twidth, off, a.gids, a.gseq, a.min, ng, a.ci.n, what, count_all, acc, maxabs);
@@ -845,27 +854,37 @@ run_gaggr(const AggrInit &a, mgdk_bat *b, int what, bool count_all, GRes &r)
 	r.lastnil.resize(ng);
 	r.mn.resize(ng);
 	r.mx.resize(ng);
-	std::vector<unsigned long long> raw(2 * ng);
-	if ((ng && (!hip_ok(hipMemcpyAsync(raw.data(), acc.sum, ng * 16, hipMemcpyDeviceToHost, st), "memcpy") ||
-		    !hip_ok(hipMemcpyAsync(r.cnt.data(), acc.cnt, ng * 8, hipMemcpyDeviceToHost, st), "memcpy") ||
-		    !hip_ok(hipMemcpyAsync(r.firstval.data(), acc.firstval, ng * 8, hipMemcpyDeviceToHost, st), "memcpy") ||
-		    !hip_ok(hipMemcpyAsync(r.lastnil.data(), acc.lastnil, ng * 8, hipMemcpyDeviceToHost, st), "memcpy") ||
-		    !hip_ok(hipMemcpyAsync(r.mn.data(), acc.mn, ng * 8, hipMemcpyDeviceToHost, st), "memcpy") ||
-		    !hip_ok(hipMemcpyAsync(r.mx.data(), acc.mx, ng * 8, hipMemcpyDeviceToHost, st), "memcpy"))) ||
-	    !hip_ok(hipMemcpyAsync(&r.maxabs, maxabs, 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+	const size_t nblk = (size_t) ng * (16 + 8 * 5) + 8;
+	unsigned long long *hb = (unsigned long long *) pinned(nblk);
+	if (hb == nullptr || !hip_ok(hipMemcpyAsync(hb, d, nblk, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
 		return -1;
-	for (BUN k = 0; k < ng; k++)
-		r.sum[k] = (hge) (((uhge) raw[2 * k + 1] << 64) | raw[2 * k]);
+	const unsigned long long *hs = hb, *hc = hb + 2 * ng, *hf = hc + ng, *hl = hf + ng;
+	const long long *hmn = (const long long *) (hl + ng), *hmx = hmn + ng;
+	for (BUN k = 0; k < ng; k++) {
+		r.sum[k] = (hge) (((uhge) hs[2 * k + 1] << 64) | hs[2 * k]);
+		r.cnt[k] = hc[k];
+		r.firstval[k] = hf[k];
+		r.lastnil[k] = hl[k];
+		r.mn[k] = hmn[k];
+		r.mx[k] = hmx[k];
+	}
+	r.maxabs = hb[7 * ng];
 	return 0;
 }
 
+// wait = false: the copy is queued from the pinned arena and the caller
+// waits once after its last upload (sync())
 mgdk_bat *
-upload_new(oid hseq, int tp, const void *host, BUN n)
+upload_new(oid hseq, int tp, const void *host, BUN n, bool wait = true)
 {
 	mgdk_bat *bn = newbat(hseq, tp, n);
 	if (bn == nullptr)
 		return nullptr;
-	if (mgdk_BATupload(bn, host, n) < 0) {
+	const size_t bytes = n * (size_t) bn->twidth;
+	const void *src = bytes ? stage_host(host, bytes) : nullptr;
+	if ((bytes && (src == nullptr || !hip_ok(hipMemcpyAsync(bn->theap, src, bytes, hipMemcpyHostToDevice, stream()),
+						     "hipMemcpyAsync H2D"))) ||
+	    (wait && !sync())) {
 		mgdk_BBPunfix(bn);
 		return nullptr;
 	}
@@ -1492,9 +1511,9 @@ mgdk_BATgroupavg3(mgdk_bat **avgp, mgdk_bat **remp, mgdk_bat **cntp, mgdk_bat *b
 		put_vec(av, tp, k, q, false);
 		rem[k] = (long long) m;
 	}
-	mgdk_bat *A = upload_new(ng ? a.min : 0, tp, av.data(), ng);
-	mgdk_bat *R = upload_new(ng ? a.min : 0, MGDK_lng, rem.data(), ng);
-	mgdk_bat *C = upload_new(ng ? a.min : 0, MGDK_lng, cnt.data(), ng);
+	mgdk_bat *A = upload_new(ng ? a.min : 0, tp, av.data(), ng, false);
+	mgdk_bat *R = A ? upload_new(ng ? a.min : 0, MGDK_lng, rem.data(), ng, false) : nullptr;
+	mgdk_bat *C = R ? upload_new(ng ? a.min : 0, MGDK_lng, cnt.data(), ng) : nullptr;
 	if (!A || !R || !C) {
 		mgdk_BBPunfix(A);
 		mgdk_BBPunfix(R);

@@ -27,6 +27,9 @@ void dfree(void *p);
 void *scratch(size_t bytes);
 // pinned host staging for small device->host reads
 void *pinned(size_t bytes);
+// copy of `bytes` of host data in the thread's pinned upload arena (valid
+// until its next sync(): queue the H2D copy, then wait once)
+void *stage_host(const void *src, size_t bytes);
 // per-thread 4 KiB device buffer for small results / arguments
 void *meta_buf();
 bool sync();                                // stream sync + error check

@@ -5,6 +5,7 @@
 // group.group, group.subgroup, batcalc.- + * + *, aggr.subsum x4 (+ disc),
 // aggr.subcount, aggr.subavg x3).  Used as the exact fallback of the fused kernels and as
 // the "drop-in" timing of the GDK boundary.
+#include <cstring>
 #include <vector>
 
 #include "mgdk_internal.h"
@@ -16,6 +17,47 @@ struct Bats {
 	std::vector<mgdk_bat *> v;
 	mgdk_bat *add(mgdk_bat *b) { v.push_back(b); return b; }
 	~Bats() { for (mgdk_bat *b : v) mgdk_BBPunfix(b); }
+};
+// the plan's result columns read back with one wait (the result export of
+// the MAL plan), through the thread's pinned buffer
+struct Readback {
+	std::vector<std::pair<const mgdk_bat *, void *>> v;
+	void add(const mgdk_bat *b, void *host) { v.emplace_back(b, host); }
+	int run()
+	{
+		size_t tot = 16;
+		for (auto &x : v)
+			if (x.first->ttype != MGDK_void)
+				tot += (x.first->count * (size_t) x.first->twidth + 15) & ~(size_t) 15;
+		char *h = (char *) pinned(tot);
+		if (h == nullptr)
+			return -1;
+		size_t o = 0;
+		for (auto &x : v) {
+			const mgdk_bat *b = x.first;
+			const size_t bytes = b->count * (size_t) b->twidth;
+			if (b->ttype == MGDK_void || bytes == 0)
+				continue;
+			if (!hip_ok(hipMemcpyAsync(h + o, b->theap, bytes, hipMemcpyDeviceToHost, stream()), "memcpy"))
+				return -1;
+			o += (bytes + 15) & ~(size_t) 15;
+		}
+		if (!sync())
+			return -1;
+		o = 0;
+		for (auto &x : v) {
+			const mgdk_bat *b = x.first;
+			if (b->ttype == MGDK_void) {
+				if (mgdk_BATdownload(b, x.second) < 0)
+					return -1;
+				continue;
+			}
+			const size_t bytes = b->count * (size_t) b->twidth;
+			memcpy(x.second, h + o, bytes);
+			o += (bytes + 15) & ~(size_t) 15;
+		}
+		return 0;
+	}
 };
 }  // namespace
 
@@ -101,15 +143,17 @@ q1_opatatime(mgdk_bat *shipdate, mgdk_bat *rf, mgdk_bat *ls, mgdk_bat *qty, mgdk
 	std::vector<oid> ve(ng);
 	std::vector<uint8_t> vr(ng), vl(ng);
 	std::vector<int64_t> va[3], vrm[3];
+	Readback rb;
 	for (int k = 0; k < 3; k++) {
 		va[k].resize(ng);
 		vrm[k].resize(ng);
-		if (mgdk_BATdownload(av[k], va[k].data()) || mgdk_BATdownload(rm[k], vrm[k].data()))
-			return -1;
+		rb.add(av[k], va[k].data());
+		rb.add(rm[k], vrm[k].data());
 	}
-	if (mgdk_BATdownload(s1, v1.data()) || mgdk_BATdownload(s2, v2.data()) || mgdk_BATdownload(s3, v3.data()) ||
-	    mgdk_BATdownload(s4, v4.data()) || mgdk_BATdownload(s5, v5.data()) || mgdk_BATdownload(cn, vc.data()) ||
-	    mgdk_BATdownload(krow, ve.data()) || mgdk_BATdownload(krf, vr.data()) || mgdk_BATdownload(kls, vl.data()))
+	rb.add(s1, v1.data()), rb.add(s2, v2.data()), rb.add(s3, v3.data()), rb.add(s4, v4.data());
+	rb.add(s5, v5.data()), rb.add(cn, vc.data()), rb.add(krow, ve.data()), rb.add(krf, vr.data());
+	rb.add(kls, vl.data());
+	if (rb.run() < 0)
 		return -1;
 	for (BUN k = 0; k < ng; k++) {
 		mgdk_q1row &r = rows[k];

@@ -48,7 +48,11 @@ struct ThreadCtx {
 	void *pinned = nullptr;
 	size_t pinned_size = 0;
 	void *meta = nullptr;
+	void *stage = nullptr;          // pinned upload arena, reclaimed at sync()
+	size_t stage_size = 0, stage_used = 0;
 	~ThreadCtx() {
+		if (stage)
+			(void) hipHostFree(stage);
 		if (meta)
 			dfree(meta);
 		if (scratch)
@@ -100,6 +104,7 @@ bool
 sync()
 {
 	hipError_t e = hipStreamSynchronize(stream());
+	tctx.stage_used = 0;                // every staged upload has been read
 	if (e != hipSuccess)
 		return hip_ok(e, "hipStreamSynchronize");
 	if (!hip_ok(hipGetLastError(), "kernel launch"))
@@ -224,6 +229,36 @@ pinned(size_t bytes)
 		tctx.pinned_size = n;
 	}
 	return tctx.pinned;
+}
+
+// Pinned staging for host->device copies that are not waited for one by
+// one: an operator stages its small result columns, queues their copies and
+// waits once.  The arena is reclaimed at the thread's next sync(); a request
+// that does not fit waits for the queued copies first.
+void *
+stage_host(const void *src, size_t bytes)
+{
+	const size_t need = (bytes + 255) & ~(size_t) 255;
+	if (tctx.stage_used + need > tctx.stage_size) {
+		if (tctx.stage_used && !sync())
+			return nullptr;
+		if (need > tctx.stage_size) {
+			if (tctx.stage)
+				(void) hipHostFree(tctx.stage);
+			size_t n = need < ((size_t) 1 << 20) ? ((size_t) 1 << 20) : need;
+			if (hipHostMalloc(&tctx.stage, n, hipHostMallocDefault) != hipSuccess) {
+				tctx.stage = nullptr;
+				tctx.stage_size = 0;
+				seterr("HY013!Could not allocate pinned host memory");
+				return nullptr;
+			}
+			tctx.stage_size = n;
+		}
+	}
+	char *d = (char *) tctx.stage + tctx.stage_used;
+	tctx.stage_used += need;
+	memcpy(d, src, bytes);
+	return d;
 }
 
 // ---- profiling ---------------------------------------------------------------
@@ -925,8 +960,9 @@ mgdk_BATupload(mgdk_bat *b, const void *host, mgdk_BUN n)
 		p->theap = h;
 		b->theap = h->base;
 	}
-	if (bytes && !hip_ok(hipMemcpyAsync(b->theap, host, bytes, hipMemcpyHostToDevice, stream()),
-			     "hipMemcpyAsync H2D"))
+	const void *src = bytes && bytes <= ((size_t) 16 << 20) ? stage_host(host, bytes) : host;
+	if (bytes && (src == nullptr ||
+		      !hip_ok(hipMemcpyAsync(b->theap, src, bytes, hipMemcpyHostToDevice, stream()), "hipMemcpyAsync H2D")))
 		return -1;
 	b->count = n;
 	return sync() ? 0 : -1;
