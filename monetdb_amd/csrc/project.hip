@@ -103,22 +103,18 @@ launch(const oid *l, BUN n, const void *r, oid rseq, BUN rcnt, const void *nilp,
 // plus n/8 bytes of bitmap instead of 8-byte oids and a gather.
 constexpr uint32_t PB_MAXW = 512;     // bitmap words per tile at most (select's sel_wpt)
 
-template <typename T>
-__global__ __launch_bounds__(256) void
-k_project_bits(const uint32_t *__restrict__ bits, const uint64_t *__restrict__ pre, uint32_t wpt, uint64_t nslots,
-	       int64_t rowbase, BUN rcnt, const T *__restrict__ r, T *__restrict__ out)
+// the tile's bitmap words in LDS with their exclusive popcount prefix
+// (thread tid owns words tid and tid + 256)
+__device__ __forceinline__ void
+pb_prefix(const uint32_t *__restrict__ bits, uint64_t t, uint32_t wpt, uint32_t *s_w, uint32_t *s_pre,
+	  uint32_t *s_wave)
 {
-	__shared__ uint32_t s_w[PB_MAXW], s_pre[PB_MAXW];
-	__shared__ uint32_t s_wave[4];
 	const unsigned tid = threadIdx.x, lane = __lane_id(), wave = tid >> 6;
-	const uint64_t t = blockIdx.x;
-	// words of the tile (<= 2 per thread) and their exclusive popcount prefix
 	uint32_t w0 = 0, w1 = 0;
 	if (tid < wpt)
 		w0 = bits[t * wpt + tid];
 	if (tid + 256 < wpt)
 		w1 = bits[t * wpt + tid + 256];
-	// scan in word order: thread tid owns words tid and tid + 256
 	const uint32_t c0 = __popc(w0), c1 = __popc(w1);
 	uint32_t x = c0;
 #pragma unroll
@@ -158,6 +154,18 @@ k_project_bits(const uint32_t *__restrict__ bits, const uint64_t *__restrict__ p
 		s_pre[tid + 256] = ex1;
 	}
 	__syncthreads();
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void
+k_project_bits(const uint32_t *__restrict__ bits, const uint64_t *__restrict__ pre, uint32_t wpt, uint64_t nslots,
+	       int64_t rowbase, BUN rcnt, const T *__restrict__ r, T *__restrict__ out)
+{
+	__shared__ uint32_t s_w[PB_MAXW], s_pre[PB_MAXW];
+	__shared__ uint32_t s_wave[4];
+	const unsigned tid = threadIdx.x;
+	const uint64_t t = blockIdx.x;
+	pb_prefix(bits, t, wpt, s_w, s_pre, s_wave);
 	const uint64_t obase = pre[t];
 	const uint64_t s0 = t * (uint64_t) wpt * 32;
 	const uint32_t tslots = wpt * 32;
@@ -183,12 +191,112 @@ k_project_bits(const uint32_t *__restrict__ bits, const uint64_t *__restrict__ p
 	}
 }
 
+// vector form (1/2/4/8-byte values, the tile's first row a multiple of
+// V = 16 / sizeof(T)): a lane loads V consecutive values with one 16-byte
+// nontemporal load, so each wave load instruction covers 1 KiB of the
+// column; the chunk's hits are compacted into LDS at their rank and stored
+// from there by consecutive lanes (per-lane runs of V values written
+// straight to HBM are partial lines: 2x slower).  Rows past the last whole
+// vector of r (< V of them, last tile only) are read by single loads after
+// the main loop.
+template <typename T>
+__global__ __launch_bounds__(256) void
+k_project_bits_v(const uint32_t *__restrict__ bits, const uint64_t *__restrict__ pre, uint32_t wpt,
+		 uint64_t nslots, int64_t rowbase, BUN rcnt, const T *__restrict__ r, T *__restrict__ out)
+{
+	constexpr int V = 16 / sizeof(T), U = 8;
+	constexpr uint32_t CH = 256 * V * U;                 // slots per chunk
+	typedef uint32_t vec_t __attribute__((ext_vector_type(4)));
+	__shared__ uint32_t s_w[PB_MAXW], s_pre[PB_MAXW];
+	__shared__ uint32_t s_wave[4];
+	__shared__ T stage[CH];
+	const unsigned tid = threadIdx.x;
+	const uint64_t t = blockIdx.x;
+	pb_prefix(bits, t, wpt, s_w, s_pre, s_wave);
+	const uint64_t obase = pre[t];
+	const uint64_t s0 = t * (uint64_t) wpt * 32;
+	const uint32_t tslots = wpt * 32;
+	const int64_t nvec = (int64_t) (rcnt / V);           // whole vectors of r
+	const vec_t *rv = (const vec_t *) r;
+	for (uint32_t r0 = 0; r0 < tslots; r0 += CH) {
+		vec_t v[U];
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const uint32_t sl = r0 + ((uint32_t) u * 256 + tid) * V;
+			int64_t vi = (rowbase + (int64_t) (s0 + sl)) / V;
+			vi = vi < 0 ? 0 : vi >= nvec ? nvec - 1 : vi;      // clamped, masked below
+			v[u] = __builtin_nontemporal_load(rv + vi);
+		}
+		// the chunk's hits are the output range [c0, c1) of the tile
+		const uint32_t c0 = s_pre[r0 >> 5];
+		const uint32_t re = min(r0 + CH, tslots);
+		const uint32_t c1 = re < tslots ? s_pre[re >> 5] : s_pre[(tslots >> 5) - 1] + __popc(s_w[(tslots >> 5) - 1]);
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const uint32_t sl = r0 + ((uint32_t) u * 256 + tid) * V;
+			if (sl >= tslots)
+				continue;
+			const int64_t row0 = rowbase + (int64_t) (s0 + sl);
+			const uint32_t wv = s_w[sl >> 5], b0 = sl & 31;
+			uint32_t msk = (wv >> b0) & ((1u << V) - 1);
+			// slots past nslots or rows past the whole vectors are not here
+			const int64_t lim = min((int64_t) (nslots - (s0 + sl)), nvec * V - row0);
+			if (lim < V)
+				msk &= lim <= 0 ? 0u : ((1u << lim) - 1);
+			uint32_t o = s_pre[sl >> 5] + __popc(wv & ((1u << b0) - 1)) - c0;
+			T e[V];
+			__builtin_memcpy(e, &v[u], 16);
+#pragma unroll
+			for (int q = 0; q < V; q++)
+				if ((msk >> q) & 1)
+					stage[o++] = e[q];
+		}
+		__syncthreads();
+		// the hits the lane masks dropped (past nslots / the whole vectors)
+		// leave their stage places unwritten; those places are not stored
+		const uint32_t nst = c1 - c0;
+		uint32_t valid = nst;
+		{
+			const int64_t lastrow = nvec * V - 1 - rowbase - (int64_t) s0;   // last slot with a whole-vector row
+			const int64_t lastsl = min(lastrow, (int64_t) (nslots - s0) - 1);
+			if (lastsl < (int64_t) re - 1) {
+				if (lastsl < (int64_t) r0)
+					valid = 0;
+				else {
+					const uint32_t ls = (uint32_t) lastsl, wv = s_w[ls >> 5], bit = ls & 31;
+					valid = s_pre[ls >> 5] + __popc(wv & (bit == 31 ? ~0u : ((2u << bit) - 1))) - c0;
+				}
+			}
+		}
+		for (uint32_t j = tid; j < valid; j += 256)
+			out[obase + c0 + j] = stage[j];
+		__syncthreads();
+	}
+	// rows of r after its last whole vector
+	const int64_t tail0 = nvec * V;
+	if (tail0 < (int64_t) rcnt && tid < V) {
+		const int64_t row = tail0 + tid;
+		const int64_t sl64 = row - rowbase - (int64_t) s0;
+		if (row < (int64_t) rcnt && sl64 >= 0 && sl64 < (int64_t) tslots && s0 + (uint64_t) sl64 < nslots) {
+			const uint32_t sl = (uint32_t) sl64, wv = s_w[sl >> 5], bit = sl & 31;
+			if ((wv >> bit) & 1)
+				out[obase + s_pre[sl >> 5] + __popc(wv & ((1u << bit) - 1))] = r[row];
+		}
+	}
+}
+
 template <typename T>
 static void
 launch_bits(const SelMap &m, const mgdk_bat *r, void *out)
 {
-	hipLaunchKernelGGL((k_project_bits<T>), dim3((unsigned) m.ntiles), dim3(256), 0, stream(), m.bits, m.pre, m.wpt,
-			   m.nslots, m.base - (int64_t) r->hseqbase, r->count, (const T *) r->theap, (T *) out);
+	const int64_t rowbase = m.base - (int64_t) r->hseqbase;
+	constexpr int V = 16 / sizeof(T);
+	if (V > 1 && rowbase % V == 0 && ((uintptr_t) r->theap & 15) == 0 && r->count >= (BUN) V)
+		hipLaunchKernelGGL((k_project_bits_v<T>), dim3((unsigned) m.ntiles), dim3(256), 0, stream(), m.bits,
+				   m.pre, m.wpt, m.nslots, rowbase, r->count, (const T *) r->theap, (T *) out);
+	else
+		hipLaunchKernelGGL((k_project_bits<T>), dim3((unsigned) m.ntiles), dim3(256), 0, stream(), m.bits,
+				   m.pre, m.wpt, m.nslots, rowbase, r->count, (const T *) r->theap, (T *) out);
 }
 
 

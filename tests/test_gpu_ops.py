@@ -820,6 +820,12 @@ def test_project_through_select_bitmap(gdk, sel_t, sel):
             got = gdk.BATproject(c, V).to_numpy()
             want = vals.reshape(n, 2)[want_idx] if vt == gdk.TYPE_hge else vals[want_idx]
             assert np.array_equal(got.view(np.uint8), np.ascontiguousarray(want).view(np.uint8)), vt
+        # r longer than the scanned range (its last rows are no candidate
+        # slot; the 16-byte vector path must not take them for tail hits)
+        for vt, dtv in ((gdk.TYPE_lng, np.int64), (gdk.TYPE_bte, np.int8)):
+            vals = r.integers(-100, 100, n + 29).astype(dtv)
+            got = gdk.BATproject(c, gdk.BAT.from_numpy(vt, vals, hseqbase=77)).to_numpy()
+            assert np.array_equal(got, vals[want_idx]), vt
     # r shorter than the list's range: "does not match always" as with the gather
     c = gdk.BATthetaselect(B, None, thr, "<")
     short = gdk.BAT.from_numpy(gdk.TYPE_lng, np.arange(n - 5, dtype=np.int64), hseqbase=77)
