@@ -178,6 +178,44 @@ def test_calc_cst_and_candidates(gdk, ora):
     assert got.values() == want.values()
 
 
+@pytest.mark.parametrize("n", [1, 2, 7, 100_003])
+def test_calc_pair_path(gdk, ora, n):
+    """The paired kernel (two elements per lane, 16-byte loads / stores) for
+    dense 8 / 16-byte operands: odd counts, sliced operands (element 0 on an
+    8-byte boundary -> the single-element kernel), hge x lng -> hge (Q1's
+    charge), constants, nils, and an overflow at an odd position."""
+    r = rng(43)
+    a = with_nils(r.integers(-10**6, 10**6, n + 3).astype(np.int64), gdk.NIL[gdk.TYPE_lng], 0.03, r)
+    b = with_nils(r.integers(-10**6, 10**6, n + 3).astype(np.int64), gdk.NIL[gdk.TYPE_lng], 0.03, r)
+    ga, gb = mk(gdk, gdk.TYPE_lng, a), mk(gdk, gdk.TYPE_lng, b)
+    oa, ob = omk(ora, ora.TYPE_lng, a), omk(ora, ora.TYPE_lng, b)
+    for lo in (0, 1, 2):
+        sa, sb = gdk.BATslice(ga, lo, lo + n), gdk.BATslice(gb, lo, lo + n)
+        wa, wb = omk(ora, ora.TYPE_lng, a[lo:lo + n]), omk(ora, ora.TYPE_lng, b[lo:lo + n])
+        for tp in (gdk.TYPE_lng, gdk.TYPE_hge):
+            got = gdk.BATcalcmul(sa, sb, tp)
+            want = ora.BATcalc("*", wa, wb, tp)
+            assert [int(x) for x in got.values()] == [int(x) for x in want.values()]
+            assert (got.s.tnonil, got.s.tnil, got.count()) == (want.s.nonil, want.s.nil, want.s.count)
+        dp = gdk.BATcalcmul(sa, sb, gdk.TYPE_hge)
+        odp = ora.BATcalc("*", wa, wb, ora.TYPE_hge)
+        got = gdk.BATcalcmul(dp, sb, gdk.TYPE_hge).values()
+        want = ora.BATcalc("*", odp, wb, ora.TYPE_hge).values()
+        assert [int(x) for x in got] == [int(x) for x in want]
+        got = gdk.BATcalccstsub(100, gdk.TYPE_lng, sa, gdk.TYPE_lng).values()
+        want = ora.BATcalc("-", None, wa, ora.TYPE_lng, c1=100, t1=ora.TYPE_lng).values()
+        assert [int(x) for x in got] == [int(x) for x in want]
+    if n >= 7:
+        big = np.arange(n, dtype=np.int64)
+        big[5] = 2**62
+        g, o = mk(gdk, gdk.TYPE_lng, big), omk(ora, ora.TYPE_lng, big)
+        with pytest.raises(gdk.GDKError) as ei:
+            gdk.BATcalcmulcst(g, 4, gdk.TYPE_lng, gdk.TYPE_lng)
+        with pytest.raises(ora.OracleError) as eo:
+            ora.BATcalc("*", o, None, ora.TYPE_lng, c2=4, t2=ora.TYPE_lng)
+        assert str(ei.value) == str(eo.value)
+
+
 @pytest.mark.parametrize("tname,tp", [("int", "lng"), ("lng", "lng"), ("lng", "hge"),
                                       ("hge", "hge"), ("int", "dbl")])
 def test_sum(gdk, ora, tname, tp):
