@@ -245,6 +245,11 @@ int mgdk_GDKanalyticalwindowbounds(mgdk_bat *r, mgdk_bat *b, mgdk_bat *p, mgdk_b
 int mgdk_q6_fused(mgdk_bat *shipdate, mgdk_bat *discount, mgdk_bat *quantity,
 		  mgdk_bat *extendedprice, int32_t d0, int32_t d1, int64_t dlo,
 		  int64_t dhi, int64_t qmax, void *revenue);
+/* 128-byte lines of discount / quantity / extendedprice the calling thread's
+ * last mgdk_q6_fused read (its predicate cascade reads a column's line only
+ * when one of the line's rows passed the earlier predicates; shipdate is
+ * read whole).  0 after a full-read launch variant.  Measurement only. */
+unsigned long long mgdk_q6_last_sectors(void);
 typedef struct mgdk_q1row {
 	uint8_t returnflag, linestatus, _pad[6];   /* str heap offsets */
 	int64_t sum_qty[2], sum_base_price[2], sum_disc_price[2], sum_charge[2]; /* hge lo,hi */

@@ -23,6 +23,7 @@
 //       which the 64-bit lane partials are exact makes the call fall back to
 //       the op-at-a-time device plan (pipelines.hip), so results are always
 //       the reference's.
+#include <mutex>
 #include <algorithm>
 #include <vector>
 
@@ -264,6 +265,126 @@ k_q6c(Q6Args a)
 	acc = wave_sum128(acc);
 	if (__lane_id() == 0 && acc != 0)
 		atomic_add128(a.out, acc);
+}
+
+// Predicate-cascade variant (late materialisation inside one pass): the
+// same 256-row chunks as k_q6c, but a column is read only for the rows
+// still qualifying -- shipdate for every row, discount where the date
+// holds, quantity where date and discount hold, extendedprice where all
+// three do -- as the reference's candidate lists do (each
+// select / projection only touches the previous candidates).  A lane whose
+// two rows are both out points its load at one shared zero line (an L2
+// hit, no HBM traffic), so every load stays unconditional and in flight; a
+// 128-B line of a column is fetched only when one of its 16 rows is still
+// in.  sect[0] counts those lines (the roofline's byte count).  The
+// zero lines are spread over 64 KiB (one 16-B slot per lane of 64 waves):
+// every inactive lane of the chip on ONE line serialised on its L2 channel.
+constexpr uint32_t Q6_ZBYTES = 65536;
+template <int UNROLL>
+__global__ __launch_bounds__(256) void
+k_q6s(Q6Args a, const int64_t *zline, unsigned long long *sect)
+{
+	typedef int32_t i2 __attribute__((ext_vector_type(2)));
+	typedef int64_t l2 __attribute__((ext_vector_type(2)));
+	hge acc = 0;
+	uint32_t nsect = 0;
+	const unsigned lane = __lane_id();
+	const uint64_t nch = a.n / 256;
+	const uint64_t nw = (uint64_t) gridDim.x * (blockDim.x / 64);
+	const l2 *z = (const l2 *) zline + ((((uint64_t) blockIdx.x * blockDim.x + threadIdx.x)) & (Q6_ZBYTES / 16 - 1));
+	// 128-B lines (8 lanes x 16 B) with at least one active lane in a ballot
+	auto sectors = [](uint64_t b) -> uint32_t {
+		b |= b >> 1;
+		b |= b >> 2;
+		b |= b >> 4;
+		return (uint32_t) __popcll(b & 0x0101010101010101ull);
+	};
+	uint64_t c = ((uint64_t) blockIdx.x * blockDim.x + threadIdx.x) / 64;
+	for (; c + (UNROLL - 1) * nw < nch; c += UNROLL * nw) {
+		i2 s0[UNROLL], s1[UNROLL];
+		l2 v0[UNROLL], v1[UNROLL], d0[UNROLL], d1[UNROLL];
+		bool m[UNROLL][4];
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++) {
+			const uint64_t r0 = (c + u * nw) * 256 + 2 * lane, r1 = r0 + 128;
+			s0[u] = __builtin_nontemporal_load((const i2 *) (a.sd + r0));
+			s1[u] = __builtin_nontemporal_load((const i2 *) (a.sd + r1));
+		}
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++) {
+			const int32_t sd[4] = {s0[u][0], s0[u][1], s1[u][0], s1[u][1]};
+#pragma unroll
+			for (int k = 0; k < 4; k++)
+				m[u][k] = sd[k] != INT32_MIN && sd[k] >= a.d0 && sd[k] < a.d1;
+		}
+		// discount where the date holds
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++) {
+			const uint64_t r0 = (c + u * nw) * 256 + 2 * lane, r1 = r0 + 128;
+			const bool a0 = m[u][0] || m[u][1], a1 = m[u][2] || m[u][3];
+			nsect += sectors(__ballot(a0)) + sectors(__ballot(a1));
+			d0[u] = __builtin_nontemporal_load(a0 ? (const l2 *) (a.disc + r0) : z);
+			d1[u] = __builtin_nontemporal_load(a1 ? (const l2 *) (a.disc + r1) : z);
+		}
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++) {
+			const int64_t di[4] = {d0[u][0], d0[u][1], d1[u][0], d1[u][1]};
+#pragma unroll
+			for (int k = 0; k < 4; k++)
+				m[u][k] = m[u][k] && di[k] != INT64_MIN && di[k] >= a.dlo && di[k] <= a.dhi;
+		}
+		// quantity where date and discount hold
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++) {
+			const uint64_t r0 = (c + u * nw) * 256 + 2 * lane, r1 = r0 + 128;
+			const bool a0 = m[u][0] || m[u][1], a1 = m[u][2] || m[u][3];
+			nsect += sectors(__ballot(a0)) + sectors(__ballot(a1));
+			v0[u] = __builtin_nontemporal_load(a0 ? (const l2 *) (a.qty + r0) : z);
+			v1[u] = __builtin_nontemporal_load(a1 ? (const l2 *) (a.qty + r1) : z);
+		}
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++) {
+			const int64_t q[4] = {v0[u][0], v0[u][1], v1[u][0], v1[u][1]};
+#pragma unroll
+			for (int k = 0; k < 4; k++)
+				m[u][k] = m[u][k] && q[k] != INT64_MIN && q[k] < a.qmax;
+		}
+		// extendedprice where all three hold
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++) {
+			const uint64_t r0 = (c + u * nw) * 256 + 2 * lane, r1 = r0 + 128;
+			const bool a0 = m[u][0] || m[u][1], a1 = m[u][2] || m[u][3];
+			nsect += sectors(__ballot(a0)) + sectors(__ballot(a1));
+			v0[u] = __builtin_nontemporal_load(a0 ? (const l2 *) (a.price + r0) : z);
+			v1[u] = __builtin_nontemporal_load(a1 ? (const l2 *) (a.price + r1) : z);
+		}
+#pragma unroll
+		for (int u = 0; u < UNROLL; u++) {
+			const int64_t p[4] = {v0[u][0], v0[u][1], v1[u][0], v1[u][1]};
+			const int64_t di[4] = {d0[u][0], d0[u][1], d1[u][0], d1[u][1]};
+#pragma unroll
+			for (int k = 0; k < 4; k++)
+				if (m[u][k] && p[k] != INT64_MIN)
+					acc += (hge) p[k] * (hge) di[k];
+		}
+	}
+	for (; c < nch; c += nw) {
+		const uint64_t r0 = c * 256 + 2 * lane, r1 = r0 + 128;
+		for (int k = 0; k < 2; k++) {
+			acc += q6_row(a, a.sd[r0 + k], a.disc[r0 + k], a.qty[r0 + k], a.price[r0 + k]);
+			acc += q6_row(a, a.sd[r1 + k], a.disc[r1 + k], a.qty[r1 + k], a.price[r1 + k]);
+		}
+		nsect += 3 * 16;                         // counted as fully read
+	}
+	if (blockIdx.x == 0 && threadIdx.x < (a.n & 255)) {
+		const uint64_t r = nch * 256 + threadIdx.x;
+		acc += q6_row(a, a.sd[r], a.disc[r], a.qty[r], a.price[r]);
+	}
+	acc = wave_sum128(acc);
+	if (__lane_id() == 0 && acc != 0)
+		atomic_add128(a.out, acc);
+	if (sect && __lane_id() == 0 && nsect)
+		atomicAdd(sect, (unsigned long long) nsect);
 }
 
 __global__ __launch_bounds__(256) void
@@ -763,13 +884,40 @@ mgdk_tpch_lineitem(uint64_t seed, uint64_t row0, uint64_t n, uint64_t sf_parts, 
 // 5-7 % with this layout)
 // tuning hooks: atomics, so a concurrent set/launch never tears (dataflow
 // workers call the library concurrently, SURVEY §8 b)
-static std::atomic<int> q6_variant{14}, q6_bpc{12};
+// round 2: the predicate cascade k_q6s (variant 17: 2 chunks in flight,
+// 16 WG/CU; profiles/r02/q6_cascade_tune.log: 1.92 ms against 2.70-2.81 ms
+// for the full-read k_q6c on the same box)
+static std::atomic<int> q6_variant{17}, q6_bpc{16};
+static thread_local unsigned long long q6_sectors = 0;
 // fused Q1 main pass (tools/q1_tune.py, profiles/r01/q1_tune.log)
 static std::atomic<int> q1_layout{MGDK_Q1_LAYOUT}, q1_blocks{MGDK_Q1_BLOCKS};
 
 static void
 launch_q6(const Q6Args &a, int variant, int bpc, hipStream_t st)
 {
+	if (variant >= 16) {                 // predicate cascade (k_q6s)
+		dim3 g(256u * (unsigned) bpc), blk(256);
+		unsigned long long *sect = (unsigned long long *) a.out + 2;
+		static std::once_flag once;
+		static void *zbuf = nullptr;
+		std::call_once(once, [] {
+			zbuf = dalloc(Q6_ZBYTES);
+			if (zbuf && (hipMemset(zbuf, 0, Q6_ZBYTES) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
+				zbuf = nullptr;
+		});
+		if (zbuf == nullptr) {
+			variant = 14;
+			goto full;
+		}
+		const int64_t *z = (const int64_t *) zbuf;
+		switch (variant) {
+		case 17: hipLaunchKernelGGL((k_q6s<2>), g, blk, 0, st, a, z, sect); break;
+		case 18: hipLaunchKernelGGL((k_q6s<1>), g, blk, 0, st, a, z, sect); break;
+		default: hipLaunchKernelGGL((k_q6s<4>), g, blk, 0, st, a, z, sect); break;
+		}
+		return;
+	}
+full:
 	const bool nt = (variant & 8) != 0;
 	const int v = variant & 7;
 	dim3 g(256u * (unsigned) bpc), blk(256);
@@ -832,7 +980,8 @@ mgdk_q6_fused(mgdk_bat *shipdate, mgdk_bat *discount, mgdk_bat *quantity, mgdk_b
 	a.qmax = qmax;
 	a.out = (unsigned long long *) meta_buf();
 	hipStream_t st = stream();
-	if (!hip_ok(hipMemsetAsync(a.out, 0, 16, st), "memset"))
+	// out: [0..1] revenue, [2] sectors read by the cascade, [8..15] a zero line
+	if (!hip_ok(hipMemsetAsync(a.out, 0, 128, st), "memset"))
 		return -1;
 	{
 		ProfScope prof("q6_fused");
@@ -844,11 +993,21 @@ mgdk_q6_fused(mgdk_bat *shipdate, mgdk_bat *discount, mgdk_bat *quantity, mgdk_b
 				hipLaunchKernelGGL(k_q6_scalar, dim3(grid_for(a.n, 256 * 4, 256 * 16)), dim3(256), 0, st, a);
 		}
 	}
-	unsigned long long *h = (unsigned long long *) pinned(16);
-	if (!hip_ok(hipMemcpyAsync(h, a.out, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+	unsigned long long *h = (unsigned long long *) pinned(32);
+	if (!hip_ok(hipMemcpyAsync(h, a.out, 24, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
 		return -1;
 	memcpy(revenue, h, 16);
+	q6_sectors = h[2];
 	return 0;
+}
+
+// 128-B column lines the calling thread's last fused Q6 read beyond
+// shipdate (cascade variant; 0 for the full-read variants), for the bench's
+// byte count
+extern "C" unsigned long long
+mgdk_q6_last_sectors(void)
+{
+	return q6_sectors;
 }
 
 int

@@ -681,6 +681,20 @@ def q6_fused(shipdate, discount, quantity, price, d0, d1, dlo, dhi, qmax):
     return hge_to_int(out)
 
 
+def q6_last_lines():
+    """128-B column lines the last q6_fused on this thread read beyond shipdate
+    (0 for a full-read variant)."""
+    f = lib().mgdk_q6_last_sectors
+    f.restype = C.c_ulonglong
+    return int(f())
+
+
+def q6_set_variant(variant, blocks_per_cu):
+    """Launch variant of the fused Q6 (tuning / tests): 14 = full read (k_q6c),
+    16 / 17 / 18 = predicate cascade (k_q6s) with 4 / 2 / 1 chunks in flight."""
+    lib().mgdk_q6_set_variant(C.c_int(variant), C.c_int(blocks_per_cu))
+
+
 def q6_opatatime(shipdate, discount, quantity, price, d0, d1, dlo, dhi, qmax):
     out = (C.c_uint64 * 2)()
     _chk(lib().mgdk_q6_opatatime(shipdate.ptr, discount.ptr, quantity.ptr, price.ptr, d0, d1, dlo,

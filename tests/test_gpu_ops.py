@@ -451,6 +451,35 @@ def test_q1_value_ranges(gdk, ora, case):
     assert _q1_rows(got) == _q1_rows(want)
 
 
+@pytest.mark.parametrize("n", [255, 256, 70_001, 2_000_129])
+def test_q6_variants(gdk, ora, n):
+    """Every fused-Q6 launch variant (full read k_q6 / k_q6c, predicate
+    cascade k_q6s) gives the oracle's revenue, with nils in every column; the
+    cascade reads fewer column lines than the full read."""
+    r = rng(61)
+    host = ora.tpch_lineitem(17, 0, n, 20_000)
+    for k, nilv in (("shipdate", np.iinfo(np.int32).min), ("discount", np.iinfo(np.int64).min),
+                    ("quantity", np.iinfo(np.int64).min), ("extendedprice", np.iinfo(np.int64).min)):
+        host[k][r.random(n) < 0.01] = nilv
+    cols = {k: gdk.BAT.from_numpy(gdk.TYPE_int if k == "shipdate" else gdk.TYPE_lng, host[k])
+            for k in ("shipdate", "discount", "quantity", "extendedprice")}
+    d0, d1 = ora.mkdate(1994, 1, 1), ora.mkdate(1995, 1, 1)
+    want = ora.q6(host, 4)
+    try:
+        for v, b in ((14, 12), (5, 8), (2, 8), (16, 16), (17, 16), (18, 8)):
+            gdk.q6_set_variant(v, b)
+            got = gdk.q6_fused(cols["shipdate"], cols["discount"], cols["quantity"],
+                               cols["extendedprice"], d0, d1, 5, 7, 2400)
+            assert got == want, (v, b)
+            lines = gdk.q6_last_lines()
+            if v >= 16 and n >= 70_000:
+                assert 0 < lines * 128 < 3 * 8 * n, lines
+            elif v < 16:
+                assert lines == 0
+    finally:
+        gdk.q6_set_variant(17, 16)
+
+
 @pytest.mark.parametrize("case", ["none", "price_huge", "price_neg_nil"])
 def test_q6_value_ranges(gdk, ora, case):
     """Q6 accumulates revenue in 128 bits: prices near 2^60 (products beyond

@@ -11,14 +11,21 @@ import collections
 import csv
 import json
 import os
+import re
 import sys
+
+
+def short(name):
+    """k_xxx of a demangled kernel name (template arguments dropped)"""
+    m = re.search(r"\bk_\w+", name)
+    return m.group(0) if m else name
 
 
 def per_kernel(path, counter):
     acc = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == counter:
-            acc[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+            acc[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
 

@@ -29,6 +29,12 @@ for rnd in range(4):
             assert gdk.q6_fused(*args) == ref
         ms, n = gdk.prof_get("q6_fused")
         res[(v, b)].append(ms / n)
+L.mgdk_q6_last_sectors.restype = C.c_ulonglong
 for k in variants:
+    L.mgdk_q6_set_variant(*k)
+    gdk.q6_fused(*args)
+    sect = L.mgdk_q6_last_sectors()
+    nbytes = rows * 28 if sect == 0 else rows * 4 + sect * 128   # bytes the variant reads
     med = statistics.median(res[k])
-    print("variant %2d bpc %2d: %.4f ms  %.1f GB/s" % (k[0], k[1], med, rows * 28 / med / 1e6))
+    print("variant %2d bpc %2d: %.4f ms  %.1f GB/s read (%.2f GB)  %.1f Grows/s" % (
+        k[0], k[1], med, nbytes / med / 1e6, nbytes / 1e9, rows / med / 1e6))
