@@ -217,12 +217,48 @@ gl_key(const KeySrc &s, BUN i)
 	return s.has_g ? (gg << 32) | k0 : k0;
 }
 
+// typed key image for dense candidates over integer keys (W = 1, 2, 4, 8
+// bytes, zero-extended as key_at does for kinds 0 / 1) and prior groups
+// G = 0 none, 1 the 1-byte image, 2 an oid column, 3 dense; W == 0 takes
+// the generic key_at.  No branch on the width: a load under a runtime
+// switch is waited for before the switch joins (DESIGN §4 lesson).
+template <int W, int G>
+__device__ __forceinline__ uint64_t
+gl_key_t(const KeySrc &s, BUN i)
+{
+	if constexpr (W == 0) {
+		return gl_key(s, i);
+	} else {
+		const BUN p = s.off + i;
+		uint64_t k;
+		if constexpr (W == 1)
+			k = ((const uint8_t *) s.base)[p];
+		else if constexpr (W == 2)
+			k = ((const uint16_t *) s.base)[p];
+		else if constexpr (W == 4)
+			k = ((const uint32_t *) s.base)[p];
+		else
+			k = ((const uint64_t *) s.base)[p];
+		if constexpr (G == 1)
+			return ((uint64_t) s.g8[i] << 32) | k;
+		else if constexpr (G == 2)
+			return ((uint64_t) s.g[i] << 32) | k;
+		else if constexpr (G == 3)
+			return ((uint64_t) (s.gseq + i) << 32) | k;
+		else
+			return k;
+	}
+}
+
+constexpr int GL_U = 8;                   // rows per thread in flight
+
 __device__ __forceinline__ uint32_t
 gl_hash(uint64_t k)
 {
 	return (uint32_t) ((k * 0x9E3779B97F4A7C15ull) >> 52);
 }
 
+template <int W, int G>
 __global__ __launch_bounds__(1024) void
 k_gl_first(KeySrc s, BUN n, unsigned long long *gkey, unsigned long long *gmin, uint32_t *err)
 {
@@ -238,27 +274,39 @@ k_gl_first(KeySrc s, BUN n, unsigned long long *gkey, unsigned long long *gmin, 
 	__syncthreads();
 	const BUN a = (BUN) blockIdx.x * GL_TILE, e = min(n, a + GL_TILE);
 	bool ovf = false;
-	for (BUN i = a + tid; i < e; i += blockDim.x) {
-		const uint64_t k = gl_key(s, i);
-		const uint32_t r = (uint32_t) (i - a);
-		if (k == GL_EMPTY) {
-			atomicMin(&lmin[GL_SLOTS], r);
-			continue;
+	for (BUN i0 = a + tid; i0 < e; i0 += (BUN) GL_U * blockDim.x) {
+		uint64_t kk[GL_U];
+#pragma unroll
+		for (int u = 0; u < GL_U; u++) {
+			const BUN i = i0 + (BUN) u * blockDim.x;
+			kk[u] = gl_key_t<W, G>(s, i < e ? i : e - 1);       // clamped, all in flight
 		}
-		uint32_t h = gl_hash(k);
-		for (uint32_t pr = 0;; pr++) {
-			unsigned long long o = lkey[h];
-			if (o == GL_EMPTY)
-				o = atomicCAS(&lkey[h], GL_EMPTY, k);
-			if (o == GL_EMPTY || o == k) {
-				if (lmin[h] > r)
-					atomicMin(&lmin[h], r);
-				break;
+#pragma unroll
+		for (int u = 0; u < GL_U; u++) {
+			const BUN i = i0 + (BUN) u * blockDim.x;
+			if (i >= e)
+				continue;
+			const uint64_t k = kk[u];
+			const uint32_t r = (uint32_t) (i - a);
+			if (k == GL_EMPTY) {
+				atomicMin(&lmin[GL_SLOTS], r);
+				continue;
 			}
-			h = (h + 1) & (GL_SLOTS - 1);
-			if (pr >= GL_SLOTS) {
-				ovf = true;
-				break;
+			uint32_t h = gl_hash(k);
+			for (uint32_t pr = 0;; pr++) {
+				unsigned long long o = lkey[h];
+				if (o == GL_EMPTY)
+					o = atomicCAS(&lkey[h], GL_EMPTY, k);
+				if (o == GL_EMPTY || o == k) {
+					if (lmin[h] > r)
+						atomicMin(&lmin[h], r);
+					break;
+				}
+				h = (h + 1) & (GL_SLOTS - 1);
+				if (pr >= GL_SLOTS) {
+					ovf = true;
+					break;
+				}
 			}
 		}
 	}
@@ -337,6 +385,7 @@ gl_lookup(const unsigned long long *lkey, const uint32_t *lmap, uint64_t k)
 	return lmap[h];
 }
 
+template <int W, int G>
 __global__ __launch_bounds__(1024) void
 k_gl_assign(KeySrc s, BUN n, const unsigned long long *gkey, const uint32_t *gmap, uint32_t ngrp, oid *gid,
 	    uint8_t *img, unsigned long long *histo, uint32_t *unsorted)
@@ -356,21 +405,32 @@ k_gl_assign(KeySrc s, BUN n, const unsigned long long *gkey, const uint32_t *gma
 	__syncthreads();
 	const BUN a = (BUN) blockIdx.x * GL_TILE, e = min(n, a + GL_TILE);
 	uint32_t uns = 0;
-	for (BUN i0 = a; i0 < e; i0 += blockDim.x) {
-		const BUN i = i0 + tid;
-		uint32_t g = 0;
-		if (i < e) {
-			g = gl_lookup(lkey, lmap, gl_key(s, i));
-			gid[i] = g;
-			if (img)
-				img[i] = (uint8_t) g;
-			atomicAdd(&lh[g], 1u);
+	for (BUN i0 = a + tid; i0 < e; i0 += (BUN) GL_U * blockDim.x) {
+		uint64_t kk[GL_U], kp[GL_U];
+#pragma unroll
+		for (int u = 0; u < GL_U; u++) {
+			const BUN i = i0 + (BUN) u * blockDim.x, ic = i < e ? i : e - 1;
+			kk[u] = gl_key_t<W, G>(s, ic);
+			// lane 0's predecessor lies in the previous wave's rows
+			kp[u] = lane == 0 && ic > 0 ? gl_key_t<W, G>(s, ic - 1) : 0;
 		}
-		uint32_t gp = __shfl_up(g, 1);
-		if (lane == 0 && i > 0 && i < e)
-			gp = gl_lookup(lkey, lmap, gl_key(s, i - 1));
-		if (i > 0 && i < e && gp > g)
-			uns = 1;
+#pragma unroll
+		for (int u = 0; u < GL_U; u++) {
+			const BUN i = i0 + (BUN) u * blockDim.x;
+			uint32_t g = 0;
+			if (i < e) {
+				g = gl_lookup(lkey, lmap, kk[u]);
+				gid[i] = g;
+				if (img)
+					img[i] = (uint8_t) g;
+				atomicAdd(&lh[g], 1u);
+			}
+			uint32_t gp = __shfl_up(g, 1);
+			if (lane == 0 && i > 0 && i < e)
+				gp = gl_lookup(lkey, lmap, kp[u]);
+			if (i > 0 && i < e && gp > g)
+				uns = 1;
+		}
 	}
 	if (__any(uns) && lane == 0)
 		publish_or(unsorted, 1u);
@@ -395,8 +455,31 @@ group_lds(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mg
 	    !hip_ok(hipMemsetAsync(m, 0, 16, st), "memset"))
 		return -1;
 	const unsigned tiles = (unsigned) ((n + GL_TILE - 1) / GL_TILE);
-	hipLaunchKernelGGL(k_gl_first, dim3(tiles), dim3(1024), 0, st, ks, n, gkey.as<unsigned long long>(),
-			   gmin.as<unsigned long long>(), &m[0]);
+	// typed fast path: dense candidates, integer keys of 1-8 bytes
+	const int fw = ks.dense && ks.kind <= 1 && ks.w <= 8 ? ks.w : 0;
+	const int fg = !ks.has_g ? 0 : ks.g8 ? 1 : ks.g ? 2 : 3;
+#define GL_LAUNCH(K, ...) do { \
+		switch (fw * 4 + fg) { \
+		case 4: hipLaunchKernelGGL((K<1, 0>), __VA_ARGS__); break; \
+		case 5: hipLaunchKernelGGL((K<1, 1>), __VA_ARGS__); break; \
+		case 6: hipLaunchKernelGGL((K<1, 2>), __VA_ARGS__); break; \
+		case 7: hipLaunchKernelGGL((K<1, 3>), __VA_ARGS__); break; \
+		case 8: hipLaunchKernelGGL((K<2, 0>), __VA_ARGS__); break; \
+		case 9: hipLaunchKernelGGL((K<2, 1>), __VA_ARGS__); break; \
+		case 10: hipLaunchKernelGGL((K<2, 2>), __VA_ARGS__); break; \
+		case 11: hipLaunchKernelGGL((K<2, 3>), __VA_ARGS__); break; \
+		case 16: hipLaunchKernelGGL((K<4, 0>), __VA_ARGS__); break; \
+		case 17: hipLaunchKernelGGL((K<4, 1>), __VA_ARGS__); break; \
+		case 18: hipLaunchKernelGGL((K<4, 2>), __VA_ARGS__); break; \
+		case 19: hipLaunchKernelGGL((K<4, 3>), __VA_ARGS__); break; \
+		case 32: hipLaunchKernelGGL((K<8, 0>), __VA_ARGS__); break; \
+		case 33: hipLaunchKernelGGL((K<8, 1>), __VA_ARGS__); break; \
+		case 34: hipLaunchKernelGGL((K<8, 2>), __VA_ARGS__); break; \
+		case 35: hipLaunchKernelGGL((K<8, 3>), __VA_ARGS__); break; \
+		default: hipLaunchKernelGGL((K<0, 0>), __VA_ARGS__); break; \
+		} } while (0)
+	GL_LAUNCH(k_gl_first, dim3(tiles), dim3(1024), 0, st, ks, n, gkey.as<unsigned long long>(),
+		  gmin.as<unsigned long long>(), &m[0]);
 	hipLaunchKernelGGL(k_gl_order, dim3(1), dim3(1024), 0, st, gmin.as<unsigned long long>(), gmap.as<uint32_t>(),
 			   ci.dense, ci.seq, ci.oids, ext.as<oid>(), &m[1]);
 	if (!hip_ok(hipMemcpyAsync(h, m, 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
@@ -420,8 +503,9 @@ group_lds(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mg
 		mgdk_BBPunfix(gn);
 		return -1;
 	}
-	hipLaunchKernelGGL(k_gl_assign, dim3(tiles), dim3(1024), 0, st, ks, n, gkey.as<unsigned long long>(),
-			   gmap.as<uint32_t>(), ngrp, (oid *) gn->theap, img, (unsigned long long *) hn->theap, &m[2]);
+	GL_LAUNCH(k_gl_assign, dim3(tiles), dim3(1024), 0, st, ks, n, gkey.as<unsigned long long>(),
+		  gmap.as<uint32_t>(), ngrp, (oid *) gn->theap, img, (unsigned long long *) hn->theap, &m[2]);
+#undef GL_LAUNCH
 	oid fl[2] = {0, 0};
 	if (!hip_ok(hipMemcpyAsync(h, m, 12, hipMemcpyDeviceToHost, st), "memcpy") ||
 	    (ngrp > 0 && (!hip_ok(hipMemcpyAsync(&fl[0], ext.p, 8, hipMemcpyDeviceToHost, st), "memcpy") ||
