@@ -30,6 +30,10 @@ void *pinned(size_t bytes);
 // copy of `bytes` of host data in the thread's pinned upload arena (valid
 // until its next sync(): queue the H2D copy, then wait once)
 void *stage_host(const void *src, size_t bytes);
+// 64 KiB of device zeros (created once): the load target of lanes whose
+// rows are all filtered out, spread so no single line is hammered
+constexpr size_t ZERO_REGION = 65536;
+const void *zero_region();
 // per-thread 4 KiB device buffer for small results / arguments
 void *meta_buf();
 bool sync();                                // stream sync + error check
@@ -112,6 +116,7 @@ struct Cand {
 	const oid *oids;      // materialized: device pointer to first candidate
 	BUN n;
 	oid first, last;      // first/last candidate oid (valid when n > 0)
+	const mgdk_bat *src;  // materialized: the list itself (its accelerators)
 };
 // canditer_init (gdk/gdk_cand.c:407): clip s to b's [hseqbase, hseqbase+count)
 int cand_init(Cand *ci, const mgdk_bat *b, const mgdk_bat *s);

@@ -261,6 +261,21 @@ stage_host(const void *src, size_t bytes)
 	return d;
 }
 
+const void *
+zero_region()
+{
+	static std::once_flag once;
+	static void *z = nullptr;
+	std::call_once(once, [] {
+		void *p = dalloc(ZERO_REGION);
+		if (p && hipMemset(p, 0, ZERO_REGION) == hipSuccess && hipDeviceSynchronize() == hipSuccess)
+			z = p;
+	});
+	if (z == nullptr)
+		seterr("HY013!could not allocate the zero region");
+	return z;
+}
+
 // ---- profiling ---------------------------------------------------------------
 static std::mutex prof_mu;
 static std::map<std::string, std::pair<double, uint64_t>> prof;
@@ -700,6 +715,7 @@ cand_init(Cand *ci, const mgdk_bat *b, const mgdk_bat *s)
 	} else {
 		ci->dense = false;
 		ci->oids = (const oid *) s->theap + p;
+		ci->src = s;
 	}
 	return 0;
 }

@@ -359,6 +359,60 @@ k_sel_count(SelArgs<T> a, uint32_t *bits, uint32_t *counts)
 		counts[t] = cnt;
 }
 
+// k_sel_count over a candidate list that carries its select scan's bitmap
+// (Priv::smap) in the same slot space (slot j = oid cseq + j, 16-B aligned in
+// b): a value's predicate bit is ANDed with its candidate bit, and a lane
+// whose V slots hold no candidate loads from the zero region instead, so a
+// column line is fetched only when it holds a candidate.  The candidate
+// oids themselves are never read.
+template <typename T, int MODE>
+__global__ __launch_bounds__(256) void
+k_sel_count_c(SelArgs<T> a, const uint32_t *cbits, const void *zero, uint32_t *bits, uint32_t *counts)
+{
+	constexpr int V = sel_v<T>(), L = 32 / V;
+	constexpr int SR = sel_srows<T>();
+	typedef T vec_t __attribute__((ext_vector_type(V)));
+	const unsigned tid = threadIdx.x, lane = tid & 63;
+	const uint32_t t = blockIdx.x;
+	const uint64_t nslots = a.n;
+	const uint32_t vmask = V == 32 ? ~0u : ((1u << V) - 1);
+	const vec_t *z = (const vec_t *) zero + (((uint64_t) t * 256 + tid) & (ZERO_REGION / 16 - 1));
+	uint32_t cw[SR];
+#pragma unroll
+	for (int r = 0; r < SR; r++) {
+		const uint64_t j0 = (((uint64_t) t * SR + r) * 256 + tid) * V;
+		cw[r] = cbits[(j0 < nslots ? j0 : 0) / 32];
+	}
+	vec_t x[SR];
+	uint32_t cp[SR];
+#pragma unroll
+	for (int r = 0; r < SR; r++) {
+		const uint64_t j0 = (((uint64_t) t * SR + r) * 256 + tid) * V;
+		cp[r] = j0 < nslots ? (cw[r] >> (j0 % 32)) & vmask : 0u;
+		x[r] = __builtin_nontemporal_load(cp[r] ? (const vec_t *) (a.col_al + j0) : z);
+	}
+	uint32_t cnt = 0;
+#pragma unroll
+	for (int r = 0; r < SR; r++) {
+		const uint64_t j0 = (((uint64_t) t * SR + r) * 256 + tid) * V;
+		uint32_t m = 0;
+#pragma unroll
+		for (int k = 0; k < V; k++)
+			m |= (uint32_t) sel_eval<MODE>(a.pred, (T) x[r][k]) << k;
+		m &= cp[r];
+		cnt += __popc(m);
+		uint32_t wv = m << ((lane % L) * V);
+#pragma unroll
+		for (int o = 1; o < L; o <<= 1)
+			wv |= __shfl_xor(wv, o);
+		if (lane % L == 0)
+			bits[j0 / 32] = wv;             // zero past the last slot: the write pass reads whole tiles
+	}
+	cnt = block_reduce<uint32_t>(cnt, [](uint32_t p, uint32_t q) { return p + q; });
+	if (tid == 0)
+		counts[t] = cnt;
+}
+
 // exclusive prefix of counts[0..n) into pre[0..n), total into meta[0]; one
 // workgroup, thread i owns the consecutive run [i*P, (i+1)*P), all of whose
 // loads are issued before the first use (one memory latency in all)
@@ -623,9 +677,19 @@ cand_slice(const Cand &ci)
 }
 
 template <typename T>
+static mgdk_bat *run_scan_bits(const mgdk_bat *b, const Cand &ci, const SelPred<T> &pred, const SelMap &cm);
+
+template <typename T>
 static mgdk_bat *
 run_scan(const mgdk_bat *b, const Cand &ci, const SelPred<T> &pred)
 {
+	// a candidate list that is a whole select result with its scan bitmap,
+	// 16-B aligned against b in the same slot space: stream b through it
+	SelMap cm;
+	if (MGDK_SEL_STREAM && !ci.dense && ci.src && ci.n == ci.src->count && ci.n > 0 && smap_get(ci.src, &cm) &&
+	    cm.base >= (int64_t) b->hseqbase && cm.lo >= b->hseqbase && cm.hi < b->hseqbase + b->count &&
+	    (((uintptr_t) b->theap + (uintptr_t) (cm.base - (int64_t) b->hseqbase) * sizeof(T)) & 15) == 0)
+		return run_scan_bits<T>(b, ci, pred, cm);
 	ProfScope prof("select");
 	mgdk_bat *bn = newbat(0, MGDK_oid, ci.n);
 	if (bn == nullptr)
@@ -744,6 +808,90 @@ run_scan(const mgdk_bat *b, const Cand &ci, const SelPred<T> &pred)
 		m.ntiles = ntiles;
 		m.nslots = ci.n + a.shift;
 		m.base = (int64_t) (a.cseq - a.shift);
+		m.lo = h[2];
+		m.hi = h[3];
+		smap_set(bn, sbh.h, m);
+	}
+	return bn;
+}
+
+template <typename T>
+static mgdk_bat *
+run_scan_bits(const mgdk_bat *b, const Cand &ci, const SelPred<T> &pred, const SelMap &cm)
+{
+	ProfScope prof("select");
+	const uint64_t p0 = (uint64_t) (cm.base - (int64_t) b->hseqbase);      // b's position of slot 0
+	const uint64_t nslots = std::min<uint64_t>(cm.nslots, b->count - p0);
+	mgdk_bat *bn = newbat(0, MGDK_oid, ci.n);
+	const void *zero = zero_region();
+	if (bn == nullptr || zero == nullptr) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	SelArgs<T> a{};
+	a.col = (const T *) b->theap;
+	a.hseq = b->hseqbase;
+	a.col_al = a.col + p0;
+	a.shift = 0;
+	a.cseq = (oid) cm.base;
+	a.n = nslots;
+	a.pred = pred;
+	a.out = (oid *) bn->theap;
+	const uint64_t items_per_tile = (uint64_t) sel_srows<T>() * 256 * (16 / sizeof(T));
+	const uint64_t ntiles = (nslots + items_per_tile - 1) / items_per_tile;
+	if (ntiles >= (1ull << 31)) {
+		seterr("select: input too large");
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	a.ntiles = (uint32_t) ntiles;
+	uint64_t *meta = (uint64_t *) meta_buf();
+	a.meta = meta;
+	struct HeapRef {
+		Heap *h;
+		~HeapRef() { heap_decref(h); }
+	} sbh{heap_new(ntiles * (4 * (size_t) sel_wpt<T>() + 4 + 8) + 64)};
+	if (sbh.h == nullptr || meta == nullptr) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	uint64_t *pre = (uint64_t *) sbh.h->base;
+	uint32_t *counts = (uint32_t *) (pre + ntiles);
+	uint32_t *bits = counts + ntiles + (ntiles & 1);
+	hipStream_t st = stream();
+	const dim3 g((unsigned) ntiles), blk(256);
+#define SELC(MODE) do { hipLaunchKernelGGL((k_sel_count_c<T, MODE>), g, blk, 0, st, a, cm.bits, zero, bits, counts); \
+			hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(1024), 0, st, counts, pre, (uint32_t) ntiles, a.meta); \
+			hipLaunchKernelGGL(k_sel_write<T>, g, blk, 0, st, a, bits, pre); } while (0)
+	switch (pred.mode) {
+	case SEL_RANGE: SELC(SEL_RANGE); break;
+	case SEL_ANTI: SELC(SEL_ANTI); break;
+	case SEL_EQ: SELC(SEL_EQ); break;
+	case SEL_EQNIL: SELC(SEL_EQNIL); break;
+	default: SELC(SEL_NOTNIL); break;
+	}
+#undef SELC
+	uint64_t *h = (uint64_t *) pinned(64);
+	if (h == nullptr || !hip_ok(hipMemcpyAsync(h, meta, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, st), "memcpy") ||
+	    !sync()) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	const uint64_t cnt = h[0];
+	bn->count = cnt;
+	bn->tsorted = bn->tkey = bn->tnonil = 1;
+	bn->tnil = 0;
+	bn->trevsorted = cnt <= 1;
+	if (cnt <= 1 || h[3] - h[2] == cnt - 1) {
+		setdense(bn, cnt ? h[2] : 0, cnt);   // virtualize
+	} else if (cnt >= SMAP_MIN) {
+		SelMap m{};
+		m.pre = pre;
+		m.bits = bits;
+		m.wpt = (uint32_t) sel_wpt<T>();
+		m.ntiles = ntiles;
+		m.nslots = nslots;
+		m.base = cm.base;
 		m.lo = h[2];
 		m.hi = h[3];
 		smap_set(bn, sbh.h, m);

@@ -81,6 +81,60 @@ def test_select_random_parity(gdk, ora, tname, dt):
                 assert got.is_dense()
 
 
+@pytest.mark.parametrize("tname,dt", SEL_TYPES)
+def test_select_through_candidate_bitmap(gdk, ora, tname, dt):
+    """A candidate list that is a select result of >= 1M oids keeps its scan
+    bitmap; BATselect through it streams b and ANDs the candidate bits (no
+    oid reads, lines without a candidate not fetched).  Every predicate form
+    against the oracle with the same list as an ordinary oid list, chained
+    selects (the Q6 shape), a head-offset b and an unaligned view (the oid
+    path)."""
+    r = rng(12)
+    n = 3_000_017
+    tp = getattr(gdk, "TYPE_" + tname)
+    key = r.integers(0, 100, n).astype(np.int32)
+    K = mk(gdk, gdk.TYPE_int, key, nonil=True, hseqbase=40)
+    s1 = gdk.BATthetaselect(K, None, 60, "<")            # ~1.8M oids -> bitmap kept
+    s1v = s1.to_numpy()
+    assert s1v.size >= 1 << 20
+    if dt in (np.float32, np.float64):
+        vals = r.integers(-50, 50, n).astype(dt)
+        vals[r.random(n) < 0.05] = np.nan
+        nil, lo, hi = float("nan"), -20.0, 20.0
+    else:
+        vals = with_nils(r.integers(-50, 50, n).astype(dt), gdk.NIL[tp], 0.05, r)
+        nil, lo, hi = gdk.NIL[tp], -20, 20
+    b = mk(gdk, tp, vals, hseqbase=40)
+    ob = omk(ora, tp, vals, hseqbase=40)
+    os1 = omk(ora, ora.TYPE_oid, s1v, sorted_=True, key=True)
+    for tl, th, li, hi_, anti, nm in _cases(lo, hi, nil):
+        try:
+            want = ora.BATselect(ob, os1, tl, th, li, hi_, anti, nm).values()
+        except ora.OracleError:
+            with pytest.raises(gdk.GDKError):
+                gdk.BATselect(b, s1, tl, th, li, hi_, anti, nm)
+            continue
+        got = gdk.BATselect(b, s1, tl, th, li, hi_, anti, nm).values()
+        assert np.array_equal(np.asarray(got, np.uint64), np.asarray(want, np.uint64)), \
+            (tname, tl, th, li, hi_, anti, nm)
+    # chain: the result of a bitmap select keeps its own bitmap
+    s2 = gdk.BATselect(b, s1, type(lo)(-45), type(hi)(45), True, True, False)   # ~1.5M oids
+    assert s2.count() >= 1 << 20
+    k2 = gdk.BATthetaselect(K, s2, 30, "<").to_numpy()
+    want2 = s2.to_numpy()[key[s2.to_numpy().astype(np.int64) - 40] < 30]
+    assert np.array_equal(k2, want2)
+    # a view of b three rows in: candidate slots no longer 16-B aligned
+    # against it -> the oid-list path, same answer
+    v = gdk.BAT(gdk.lib().mgdk_BATslice(b.ptr, 3, n))
+    got = gdk.BATselect(v, s1, lo, hi, True, True, False).to_numpy()
+    sel = s1v[s1v >= 43]
+    vv = vals[sel.astype(np.int64) - 40]
+    keep = (vv >= lo) & (vv <= hi) if dt not in (np.float32, np.float64) else (vv >= lo) & (vv <= hi)
+    if dt not in (np.float32, np.float64):
+        keep &= vv != nil
+    assert np.array_equal(got, sel[keep])
+
+
 def test_select_large_lookback(gdk):
     """Many tiles: exercises the decoupled look-back across the whole grid."""
     r = rng(3)

@@ -23,18 +23,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sizes", nargs="*", type=int,
                     default=[70_000, 150_000, 300_000, 600_000, 1_500_000, 4_000_000, 15_000_000])
+    ap.add_argument("--lng", action="store_true", help="8-byte keys (the open-addressing path)")
     a = ap.parse_args()
+    dt, tp = (np.int64, gdk.TYPE_lng) if a.lng else (np.int32, gdk.TYPE_int)
     gdk.init(0)
     out = {}
     for nr in a.sizes:
         r = np.random.default_rng(3)
         i = np.arange(nr, dtype=np.int64)
-        okeys = ((i // 8) * 32 + (i % 8) + 1).astype(np.int32)
+        okeys = ((i // 8) * 32 + (i % 8) + 1).astype(dt)
         r.shuffle(okeys)
-        lkeys = np.repeat(okeys, r.integers(1, 8, nr)).astype(np.int32)
+        lkeys = np.repeat(okeys, r.integers(1, 8, nr)).astype(dt)
         r.shuffle(lkeys)
-        L = gdk.BAT.from_numpy(gdk.TYPE_int, lkeys, sorted_=False, revsorted=False, key=False, nonil=True)
-        R = gdk.BAT.from_numpy(gdk.TYPE_int, okeys, sorted_=False, revsorted=False, key=True, nonil=True)
+        L = gdk.BAT.from_numpy(tp, lkeys, sorted_=False, revsorted=False, key=False, nonil=True)
+        R = gdk.BAT.from_numpy(tp, okeys, sorted_=False, revsorted=False, key=True, nonil=True)
         _, wall, kms = timed(lambda: gdk.BATjoin(L, R), reps=5, kernels=("join",))
         out[nr] = {"probe_rows": int(lkeys.size), "wall_ms": round(wall, 4), "kernel_ms": round(kms, 4)}
         del L, R

@@ -8,8 +8,9 @@ sys.path.insert(0, ".")
 from monetdb_amd import gdk
 
 gdk.init(0)
-rows = 600_121_500
-cols = gdk.tpch_lineitem(20241024, 0, rows, 20_000_000)
+import os
+rows = int(os.environ.get("Q6_ROWS", "600121500"))
+cols = gdk.tpch_lineitem(20241024, 0, rows, max(1, rows // 30))
 mk = lambda y, m, d: (((y + 4712) * 12 + m - 1) << 5) | d
 args = (cols["shipdate"], cols["discount"], cols["quantity"], cols["extendedprice"],
         mk(1994, 1, 1), mk(1995, 1, 1), 5, 7, 2400)
