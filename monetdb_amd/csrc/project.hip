@@ -202,7 +202,8 @@ k_project_bits(const uint32_t *__restrict__ bits, const uint64_t *__restrict__ p
 template <typename T>
 __global__ __launch_bounds__(256) void
 k_project_bits_v(const uint32_t *__restrict__ bits, const uint64_t *__restrict__ pre, uint32_t wpt,
-		 uint64_t nslots, int64_t rowbase, BUN rcnt, const T *__restrict__ r, T *__restrict__ out)
+		 uint64_t nslots, int64_t rowbase, BUN rcnt, const T *__restrict__ r, T *__restrict__ out,
+		 const void *zero)
 {
 	constexpr int V = 16 / sizeof(T), U = 8;
 	constexpr uint32_t CH = 256 * V * U;                 // slots per chunk
@@ -218,6 +219,9 @@ k_project_bits_v(const uint32_t *__restrict__ bits, const uint64_t *__restrict__
 	const uint32_t tslots = wpt * 32;
 	const int64_t nvec = (int64_t) (rcnt / V);           // whole vectors of r
 	const vec_t *rv = (const vec_t *) r;
+	// lanes without a hit in their V slots load from the zero region: a
+	// column line is fetched only when it holds a hit (sparse lists)
+	const vec_t *z = (const vec_t *) zero + (((uint64_t) t * 256 + tid) & (ZERO_REGION / 16 - 1));
 	for (uint32_t r0 = 0; r0 < tslots; r0 += CH) {
 		vec_t v[U];
 #pragma unroll
@@ -225,7 +229,8 @@ k_project_bits_v(const uint32_t *__restrict__ bits, const uint64_t *__restrict__
 			const uint32_t sl = r0 + ((uint32_t) u * 256 + tid) * V;
 			int64_t vi = (rowbase + (int64_t) (s0 + sl)) / V;
 			vi = vi < 0 ? 0 : vi >= nvec ? nvec - 1 : vi;      // clamped, masked below
-			v[u] = __builtin_nontemporal_load(rv + vi);
+			const uint32_t hit = sl < tslots ? (s_w[sl >> 5] >> (sl & 31)) & ((1u << V) - 1) : 0u;
+			v[u] = __builtin_nontemporal_load(hit ? rv + vi : z);
 		}
 		// the chunk's hits are the output range [c0, c1) of the tile
 		const uint32_t c0 = s_pre[r0 >> 5];
@@ -291,9 +296,10 @@ launch_bits(const SelMap &m, const mgdk_bat *r, void *out)
 {
 	const int64_t rowbase = m.base - (int64_t) r->hseqbase;
 	constexpr int V = 16 / sizeof(T);
-	if (V > 1 && rowbase % V == 0 && ((uintptr_t) r->theap & 15) == 0 && r->count >= (BUN) V)
+	const void *zero = zero_region();
+	if (V > 1 && zero && rowbase % V == 0 && ((uintptr_t) r->theap & 15) == 0 && r->count >= (BUN) V)
 		hipLaunchKernelGGL((k_project_bits_v<T>), dim3((unsigned) m.ntiles), dim3(256), 0, stream(), m.bits,
-				   m.pre, m.wpt, m.nslots, rowbase, r->count, (const T *) r->theap, (T *) out);
+				   m.pre, m.wpt, m.nslots, rowbase, r->count, (const T *) r->theap, (T *) out, zero);
 	else
 		hipLaunchKernelGGL((k_project_bits<T>), dim3((unsigned) m.ntiles), dim3(256), 0, stream(), m.bits,
 				   m.pre, m.wpt, m.nslots, rowbase, r->count, (const T *) r->theap, (T *) out);
