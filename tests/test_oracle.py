@@ -97,6 +97,46 @@ def test_q1_threads_agree(ora):
     assert sum(r["count_order"] for r in a) <= 200_000
 
 
+def _avg3(s, n):
+    """BATgroupavg3's average / remainder of an exact sum (floor, then half
+    away from zero; gdk_aggr.c:2070-2095)"""
+    q, r = divmod(s, n)
+    if r > 0:
+        if q < 0:
+            if 2 * r > n:
+                q, r = q + 1, r - n
+        elif 2 * r >= n:
+            q, r = q + 1, r - n
+    return q, r
+
+
+def test_q1_nils_numpy(ora):
+    """The oracle's Q1 with nil quantities / prices / discounts: sums skip
+    nils, the three averages divide by each column's non-nil count, count(*)
+    counts every row -- checked against Python integers."""
+    n = 60_013
+    cols = ora.tpch_lineitem(23, 0, n, 2000)
+    nil = np.iinfo(np.int64).min
+    cols["quantity"][3::97] = nil
+    cols["extendedprice"][5::101] = nil
+    cols["discount"][7::89] = nil
+    got = {(r["returnflag"], r["linestatus"]): r for r in ora.q1(cols, 2)}
+    sel = cols["shipdate"] <= ora.mkdate(1998, 9, 2)
+    keys = set(zip(cols["returnflag"][sel].tolist(), cols["linestatus"][sel].tolist()))
+    assert set(got) == keys
+    for rf, ls in keys:
+        m = sel & (cols["returnflag"] == rf) & (cols["linestatus"] == ls)
+        r = got[(rf, ls)]
+        assert r["count_order"] == int(m.sum())
+        for col, sk, ak, rk in (("quantity", "sum_qty", "avg_qty", "rem_qty"),
+                                ("extendedprice", "sum_base_price", "avg_price", "rem_price"),
+                                ("discount", None, "avg_disc", "rem_disc")):
+            v = [int(x) for x in cols[col][m] if x != nil]
+            if sk:
+                assert r[sk] == sum(v), sk
+            assert (r[ak], r[rk]) == _avg3(sum(v), len(v)), ak
+
+
 def test_rangebounds_small(ora):
     b = ora.Bat.from_array(ora.TYPE_lng, np.array([1, 2, 4, 8, 9, 1, 3], np.int64))
     p = ora.Bat.from_array(ora.TYPE_bit, np.array([1, 0, 0, 0, 0, 1, 0], np.int8))
