@@ -17,6 +17,7 @@
 // match.  Rows whose frame leaves the fast kernel's staged window are fixed
 // up by a global gallop + binary search (k_range_fix / k_range_tile) over the
 // partition starts S (compaction of p) and nil boundaries Z.
+#include <cstdlib>
 #include "mgdk_internal.h"
 
 using namespace mgdk;
@@ -272,6 +273,8 @@ struct FArgs {
 	                     // [3] a tile needs the wide kernel
 	oid *unres;          // unresolved row list
 	uint32_t unres_cap;
+	const uint32_t *tiles;   // k_range_keys<uint64_t>: the tiles to run (NULL: every tile)
+	uint32_t *relist;        // k_range_keys<uint32_t>: tiles it leaves to the 64-bit kernel (count in flags[4])
 };
 
 // Partition-start flags of stage rows 4q .. 4q+3 as one little-endian word
@@ -507,11 +510,19 @@ k_range_fast(FArgs a)
 
 constexpr uint64_t KMAXREL = 0xffffffffull;
 
-template <bool PREC, bool DESC, bool ALL>
+// KT = uint32_t: the common tile -- no partition start in its stage and
+// values spanning < 2^31 -- with 32-bit keys flag << 31 | rel, half the key
+// LDS (13.8 KiB a workgroup: 8 workgroups per CU instead of 6 with 64-bit
+// keys).  Any other tile is listed in a.relist (count flags[4]) and rerun
+// by the 64-bit kernel over that list (a.tiles).
+template <bool PREC, bool DESC, bool ALL, typename KT = uint64_t>
 __global__ __launch_bounds__(256) void
 k_range_keys(FArgs a)
 {
-	__shared__ uint64_t sk[FS];
+	constexpr bool K32 = sizeof(KT) == 4;
+	constexpr int FB = K32 ? 31 : 32;                    // nil-flag bit
+	constexpr KT RMASK = (KT) ((((uint64_t) 1) << FB) - 1);
+	__shared__ KT sk[FS];
 	__shared__ __attribute__((aligned(16))) uint8_t spu[(FS + 4 > 2 * FT ? FS + 4 : 2 * FT)];  // partition flags, then bounds
 	__shared__ int64_t s_min[4], s_max[4];
 	__shared__ int s_hasb;
@@ -519,7 +530,8 @@ k_range_keys(FArgs a)
 	uint8_t *sp = spu;
 	uint16_t *sbd = (uint16_t *) spu;
 	const int tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
-	const BUN t0 = (BUN) blockIdx.x * FT;
+	const uint32_t tile = (!K32 && a.tiles) ? a.tiles[blockIdx.x] : blockIdx.x;
+	const BUN t0 = (BUN) tile * FT;
 	const BUN t1 = t0 + FT < a.n ? t0 + FT : a.n;
 	const BUN lo = PREC ? (t0 > FH ? t0 - FH : 0) : t0;
 	const BUN hi = PREC ? (t1 + 1 < a.n ? t1 + 1 : a.n) : (t1 + FH < a.n ? t1 + FH : a.n);
@@ -589,20 +601,29 @@ k_range_keys(FArgs a)
 			vmin = s_min[q] < vmin ? s_min[q] : vmin;
 			vmax = s_max[q] > vmax ? s_max[q] : vmax;
 		}
-		if (vmin <= vmax && (uint64_t) vmax - (uint64_t) vmin > KMAXREL) {
-			if (tid == 0)
-				atomicOr(&a.flags[3], 1u);          // wide tile: the host reruns k_range_fast
+		if (vmin <= vmax && (uint64_t) vmax - (uint64_t) vmin > (uint64_t) RMASK) {
+			if (tid == 0) {
+				if (K32)
+					a.relist[atomicAdd(&a.flags[4], 1u)] = tile;   // the 64-bit kernel takes it
+				else
+					atomicOr(&a.flags[3], 1u);          // wide tile: the host reruns k_range_fast
+			}
 			return;
 		}
 		base = DESC ? (uint64_t) vmax : (uint64_t) vmin;
 	}
-	auto mkkey = [&](uint64_t label, int64_t v) -> uint64_t {
+	if (K32 && hasb) {
+		if (tid == 0)
+			a.relist[atomicAdd(&a.flags[4], 1u)] = tile;       // partition labels need 64-bit keys
+		return;
+	}
+	auto mkkey = [&](uint64_t label, int64_t v) -> KT {
 		if (ALL)
-			return label << 33;
+			return (KT) (label << 33);
 		const bool isnil = v == INT64_MIN;
 		const uint64_t flag = DESC ? (isnil ? 1 : 0) : (isnil ? 0 : 1);
 		const uint64_t rel = isnil ? 0 : (DESC ? base - (uint64_t) v : (uint64_t) v - base);
-		return (label << 33) | (flag << 32) | rel;
+		return (KT) ((label << 33) | (flag << FB) | rel);
 	};
 	if (!hasb) {
 #pragma unroll
@@ -617,7 +638,7 @@ k_range_keys(FArgs a)
 		for (int u = 0; u < NB; u++) {
 			const int i = tid + u * 256;
 			if (i < S)
-				sk[i] = (uint64_t) tv[u];
+				sk[i] = (KT) tv[u];             // (64-bit keys only: 32-bit tiles left above)
 		}
 		__syncthreads();
 		// partition labels: block max-scan of partition starts (per-thread chunks)
@@ -652,18 +673,19 @@ k_range_keys(FArgs a)
 		__syncthreads();
 	}
 
-	const uint64_t lim32 = ALL ? 0 : ((uint64_t) a.limit < KMAXREL ? (uint64_t) a.limit : KMAXREL);
+	constexpr uint64_t RM = (uint64_t) RMASK;
+	const uint64_t lim32 = ALL ? 0 : ((uint64_t) a.limit < RM ? (uint64_t) a.limit : RM);
 	// frame threshold of the row with key kk
 	auto thr = [&](uint64_t kk) -> uint64_t {
-		const uint64_t lab = kk >> 33 << 33;
+		const uint64_t lab = K32 ? 0 : kk >> 33 << 33;
 		if (ALL)
-			return PREC ? lab : lab | ((1ull << 33) - 1);
-		const uint64_t flag = (kk >> 32) & 1, rel = kk & KMAXREL;
+			return PREC ? lab : lab | (K32 ? 0xffffffffull : ((1ull << 33) - 1));
+		const uint64_t flag = (kk >> FB) & 1, rel = kk & RM;
 		const bool valrow = DESC ? flag == 0 : flag == 1;
-		const uint64_t hd = lab | (flag << 32);
+		const uint64_t hd = lab | (flag << FB);
 		if (PREC)
 			return valrow ? hd | (rel > lim32 ? rel - lim32 : 0) : hd;
-		return valrow ? hd | (KMAXREL - rel > lim32 ? rel + lim32 : KMAXREL) : hd | KMAXREL;
+		return valrow ? hd | (RM - rel > lim32 ? rel + lim32 : RM) : hd | RM;
 	};
 	const int NA = (int) (t1 - t0), NB2 = S, xa = (int) (t0 - lo);
 	// P(k, j): staged row j lies before the bound of tile row k
@@ -717,8 +739,8 @@ k_range_keys(FArgs a)
 				if (y < x)
 					ord |= DESC ? 2u : 1u;
 				if (!DESC) {
-					const uint64_t fx = (x >> 32) & 1, fy = (y >> 32) & 1;
-					if ((fx == 0 && fy == 1) || (fx == 1 && fy == 1 && (y & KMAXREL) > (x & KMAXREL)))
+					const uint64_t fx = (x >> FB) & 1, fy = (y >> FB) & 1;
+					if ((fx == 0 && fy == 1) || (fx == 1 && fy == 1 && (y & RM) > (x & RM)))
 						ord |= 2u;
 				}
 			}
@@ -734,12 +756,12 @@ k_range_keys(FArgs a)
 			// though the tile spans < 2^32
 			const int e = PREC ? bnd - 1 : bnd;
 			const uint64_t x = sk[xk];
-			const bool xval = DESC ? ((x >> 32) & 1) == 0 : ((x >> 32) & 1) == 1;
+			const bool xval = DESC ? ((x >> FB) & 1) == 0 : ((x >> FB) & 1) == 1;
 			if (xval && e >= 0 && e < NB2) {
 				const uint64_t y = sk[e];
-				const bool yval = DESC ? ((y >> 32) & 1) == 0 : ((y >> 32) & 1) == 1;
+				const bool yval = DESC ? ((y >> FB) & 1) == 0 : ((y >> FB) & 1) == 1;
 				if ((x >> 33) == (y >> 33) && yval) {
-					const uint64_t rx = x & KMAXREL, ry = y & KMAXREL;
+					const uint64_t rx = x & RM, ry = y & RM;
 					if ((rx > ry ? rx - ry : ry - rx) > a.tmax)
 						ovf = 1;
 				}
@@ -918,22 +940,41 @@ mgdk::range_bounds_int64(mgdk_bat *r, const int64_t *bvals, const mgdk_bat *p, B
 	f.unres = ul.as<oid>();
 	f.unres_cap = ucap;
 	const unsigned ftiles = (unsigned) ((n + FT - 1) / FT);
+	static const bool narrow = getenv("MGDK_WIN_K32") ? atoi(getenv("MGDK_WIN_K32")) != 0 : true;
+	DevBuf rl((size_t) ftiles * 4 + 64);
+	if (!rl.p)
+		return -1;
 	bool ordered = false;
 	for (int pass = 0; pass < 2; pass++) {
 		f.desc = pass == 1;
 		if (!hip_ok(hipMemsetAsync(fl.p, 0, 64, st), "memset"))
 			return -1;
-#define RK(P_, D_, A_) hipLaunchKernelGGL((k_range_keys<P_, D_, A_>), dim3(ftiles), blk, 0, st, f)
-		if (preceding) {
-			if (all) RK(true, false, true);
-			else if (f.desc) RK(true, true, false);
-			else RK(true, false, false);
+		// 32-bit-key tiles first; the tiles they leave (a partition start in
+		// the stage, or values spanning >= 2^31) rerun with 64-bit keys
+		f.tiles = nullptr;
+		f.relist = rl.as<uint32_t>();
+#define RK(KT, G_, P_, D_, A_) hipLaunchKernelGGL((k_range_keys<P_, D_, A_, KT>), dim3(G_), blk, 0, st, f)
+#define RKA(KT, G_) do { if (preceding) { \
+			if (all) RK(KT, G_, true, false, true); \
+			else if (f.desc) RK(KT, G_, true, true, false); \
+			else RK(KT, G_, true, false, false); \
+		} else { \
+			if (all) RK(KT, G_, false, false, true); \
+			else if (f.desc) RK(KT, G_, false, true, false); \
+			else RK(KT, G_, false, false, false); } } while (0)
+		if (narrow) {
+			RKA(uint32_t, ftiles);
+			if (!hip_ok(hipMemcpyAsync(h, fl.p, 32, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+				return -1;
+			f.tiles = rl.as<uint32_t>();
+			if (h[4])
+				RKA(uint64_t, h[4]);
 		} else {
-			if (all) RK(false, false, true);
-			else if (f.desc) RK(false, true, false);
-			else RK(false, false, false);
+			RKA(uint64_t, ftiles);
 		}
+#undef RKA
 #undef RK
+		f.tiles = nullptr;
 		if (!hip_ok(hipMemcpyAsync(h, fl.p, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
 			return -1;
 		if (h[3]) {
