@@ -50,6 +50,7 @@ struct Side {
 	oid hseq;
 	oid cseq;          // dense: oid of candidate 0
 	oid tseq;          // void side (base == nullptr): value of position 0
+	uint32_t *nofit;   // partitioned paths, 8-byte keys: set when a value has no 4-byte image
 };
 
 __device__ __forceinline__ uint64_t
@@ -722,12 +723,31 @@ block_reduce16(T v, F op)
 	return v;
 }
 
-// 16 consecutive 4-byte keys of side s from candidate index i0 (vector loads
-// for a dense side with 16-byte aligned rows); ok[q] = exists and counts
+// 8-byte key as the 4-byte key image of the partitioned paths: values in
+// [INT32_MIN + 1, INT32_MAX] keep their bits, nil becomes the 4-byte nil
+// image; any other value does not fit (*fits = false).  The image is
+// injective on the values that fit, so equal images mean equal keys.
+__device__ __forceinline__ uint32_t
+narrow_key(const Side &s, uint64_t v, bool isnil, bool &fits)
+{
+	if (isnil) {
+		fits = true;
+		return 0x80000000u;
+	}
+	const int64_t x = (int64_t) v;
+	fits = s.uns ? v <= 0x7fffffffull : (x > (int64_t) INT32_MIN && x <= (int64_t) INT32_MAX);
+	return (uint32_t) x;
+}
+
+// 16 consecutive keys of side s from candidate index i0 as 4-byte images
+// (vector loads for a dense side with 16-byte aligned rows); ok[q] = exists,
+// counts and (8-byte keys) has a 4-byte image -- a value without one is
+// flagged in s.nofit (the build side then falls back; a probe value without
+// one cannot match a build side whose values all fit)
 __device__ __forceinline__ void
 pj_keys16(const Side &s, BUN i0, BUN n, bool skipnil, uint32_t k[16], bool ok[16])
 {
-	if (s.dense && i0 + 16 <= n && ((s.off + i0) & 3) == 0) {
+	if (s.w == 4 && s.dense && i0 + 16 <= n && ((s.off + i0) & 3) == 0) {
 		typedef int32_t i4 __attribute__((ext_vector_type(4)));
 		const i4 *src = (const i4 *) ((const int32_t *) s.base + s.off + i0);
 #pragma unroll
@@ -743,16 +763,40 @@ pj_keys16(const Side &s, BUN i0, BUN n, bool skipnil, uint32_t k[16], bool ok[16
 			ok[q] = !(skipnil && k[q] == 0x80000000u);
 		return;
 	}
+	bool bad = false;
+	if (s.w == 8 && s.base && s.dense && i0 + 16 <= n && ((s.off + i0) & 1) == 0) {
+		typedef long long l2 __attribute__((ext_vector_type(2)));
+		const l2 *src = (const l2 *) ((const int64_t *) s.base + s.off + i0);
+		const uint64_t nilv = s.uns ? (1ull << 63) : (uint64_t) INT64_MIN;
 #pragma unroll
-	for (int q = 0; q < 16; q++) {
-		ok[q] = false;
-		k[q] = 0;
-		if (i0 + q < n) {
-			bool isnil;
-			k[q] = (uint32_t) key_of(s, i0 + q, isnil);
-			ok[q] = !(isnil && skipnil);
+		for (int q = 0; q < 8; q++) {
+			const l2 v = __builtin_nontemporal_load(src + q);
+#pragma unroll
+			for (int e = 0; e < 2; e++) {
+				const uint64_t x = (uint64_t) (e ? v.y : v.x);
+				bool fits;
+				const bool isnil = x == nilv;
+				k[2 * q + e] = narrow_key(s, x, isnil, fits);
+				ok[2 * q + e] = fits && !(isnil && skipnil);
+				bad |= !fits;
+			}
+		}
+	} else {
+#pragma unroll
+		for (int q = 0; q < 16; q++) {
+			ok[q] = false;
+			k[q] = 0;
+			if (i0 + q < n) {
+				bool isnil, fits = true;
+				const uint64_t v = key_of(s, i0 + q, isnil);
+				k[q] = s.w == 8 ? narrow_key(s, v, isnil, fits) : (uint32_t) v;
+				ok[q] = fits && !(isnil && skipnil);
+				bad |= !fits;
+			}
 		}
 	}
+	if (bad && s.nofit)
+		atomicOr(s.nofit, 1u);
 }
 
 // histogram: cnt[sub][p] = rows of subtile sub in partition p
@@ -913,7 +957,7 @@ k_pj_scatter(Side s, BUN n, int pbits, bool skipnil, const uint32_t *off, const 
 	const BUN a0 = sub * PJ_SUBROWS;
 	for (uint32_t p = threadIdx.x; p < P; p += blockDim.x)
 		gcur[p] = base[p] + off[sub * P + p];
-	if (s.dense && a0 + PJ_SUBROWS <= n && ((s.off + a0) & 3) == 0)
+	if (s.w == 4 && s.dense && a0 + PJ_SUBROWS <= n && ((s.off + a0) & 3) == 0)
 		pj_scatter_sub<true>(s, n, pbits, skipnil, a0, ent, stage, hist, start, gcur, wsum);
 	else
 		pj_scatter_sub<false>(s, n, pbits, skipnil, a0, ent, stage, hist, start, gcur, wsum);
@@ -1241,7 +1285,8 @@ int
 join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_bat **ap, mgdk_bat **bp, bool *ukey)
 {
 	static const int mode = getenv("MGDK_JOIN_PART") ? atoi(getenv("MGDK_JOIN_PART")) : 1;
-	if (mode == 0 || L.w != 4 || R.w != 4 || nr < 65536)
+	const bool w4 = L.w == 4 && R.w == 4, w8 = L.w == 8 && R.w == 8 && L.base && R.base;
+	if (mode == 0 || !(w4 || w8) || nr < 65536)
 		return 1;
 	int pbits = 6;
 	while (pbits < PJ_MAXPBITS && ((BUN) 8192 << pbits) < nr)
@@ -1259,15 +1304,17 @@ join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_b
 	// partition: one round trip instead of two (an oversized partition, rare,
 	// wastes the probe side's cut)
 	PjSide B, Pr;
-	if (pj_cut(R, nr, pbits, !nil_matches, B, &meta32[0]) < 0 ||
+	Side Rn = R;
+	Rn.nofit = &meta32[5];
+	if (pj_cut(Rn, nr, pbits, !nil_matches, B, &meta32[0]) < 0 ||
 	    pj_cut(L, nl, pbits, !nil_matches, Pr, &meta32[1]) < 0) {
 		(void) sync();                              // launched cuts still use the buffers
 		return -1;
 	}
-	if (!hip_ok(hipMemcpyAsync(h, meta32, 4, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+	if (!hip_ok(hipMemcpyAsync(h, meta32, 32, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
 		return -1;
-	if (h[0] > PJ_MAXFILL)
-		return 1;
+	if (h[0] > PJ_MAXFILL || h[5])
+		return 1;                                   // oversized partition / build value without a 4-byte image
 	// subtile-major offsets of the probe results
 	DevBuf offT((size_t) Pr.nsub * P * 4 + 64);
 	uint64_t total = 0;
@@ -1424,7 +1471,7 @@ gt_find(const ulonglong2 *t, uint32_t k, ulonglong2 s, uint32_t reg, uint32_t b,
 	}
 }
 
-template <bool DENSE>
+template <bool DENSE, int W>
 __global__ __launch_bounds__(256) void
 k_gt_probe(GtArgs a, const ulonglong2 *t)
 {
@@ -1441,8 +1488,6 @@ k_gt_probe(GtArgs a, const ulonglong2 *t)
 	__syncthreads();
 	const uint32_t tile = s_tile;
 	const BUN base = (BUN) tile * JTILE + tid;
-	const int32_t *kb = (const int32_t *) a.l.base;
-
 	// every load unconditional (clamped row): a load under a branch is
 	// waited for before the branch joins
 	uint32_t key[JR];
@@ -1451,8 +1496,19 @@ k_gt_probe(GtArgs a, const ulonglong2 *t)
 	for (int r = 0; r < JR; r++) {
 		const BUN i = base + (BUN) r * 256;
 		const BUN ic = i < a.n ? i : a.n - 1;
-		key[r] = (uint32_t) (DENSE ? __builtin_nontemporal_load(&kb[a.l.off + ic]) : kb[a.l.oids[ic] - a.l.hseq]);
-		ok[r] = i < a.n && (key[r] != 0x80000000u || a.nil_matches);
+		if constexpr (W == 4) {
+			const int32_t *kb = (const int32_t *) a.l.base;
+			key[r] = (uint32_t) (DENSE ? __builtin_nontemporal_load(&kb[a.l.off + ic]) : kb[a.l.oids[ic] - a.l.hseq]);
+			ok[r] = i < a.n && (key[r] != 0x80000000u || a.nil_matches);
+		} else {
+			// 8-byte keys by their 4-byte image; a value without one matches nothing
+			const uint64_t *kb = (const uint64_t *) a.l.base;
+			const uint64_t v = DENSE ? __builtin_nontemporal_load(&kb[a.l.off + ic]) : kb[a.l.oids[ic] - a.l.hseq];
+			const bool isnil = v == (a.l.uns ? (1ull << 63) : (uint64_t) INT64_MIN);
+			bool fits;
+			key[r] = narrow_key(a.l, v, isnil, fits);
+			ok[r] = i < a.n && fits && (!isnil || a.nil_matches);
+		}
 	}
 	uint32_t reg[JR], bk[JR];
 	ulonglong2 sv[JR];
@@ -1518,7 +1574,10 @@ join_gt(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_bat
 	// (a ~25 MB table) they cost more than cutting the probe side too
 	// (tools/join_sweep.py: 0.18 vs 0.25 ms at 600 K, 0.26 vs 0.27 at 1.5 M,
 	// 0.47 vs 0.42 at 4 M build rows); MGDK_JOIN_GT=2 forces the path
-	if (mode == 0 || L.w != 4 || R.w != 4 || nr < 65536 || nl == 0 || (mode == 1 && nr > 2000000))
+	// 4-byte keys, or 8-byte keys by their 4-byte images (the build side's
+	// values must all have one: checked while it is cut)
+	const bool w4 = L.w == 4 && R.w == 4, w8 = L.w == 8 && R.w == 8 && L.base && R.base;
+	if (mode == 0 || !(w4 || w8) || nr < 65536 || nl == 0 || (mode == 1 && nr > 2000000))
 		return 1;
 	int pbits = 6;
 	while (pbits < PJ_MAXPBITS && ((BUN) 8192 << pbits) < nr)
@@ -1546,7 +1605,9 @@ join_gt(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_bat
 	mgdk_bat *ra = newbat(0, MGDK_oid, nl), *rb = newbat(0, MGDK_oid, nl);
 	const size_t sbytes = (ntiles + 8) * sizeof(uint64_t);
 	char *sc = (char *) scratch(sbytes);
-	if (!gtab.p || !ra || !rb || !sc || pj_cut(R, nr, pbits, !nil_matches, B, &meta32[3]) < 0) {
+	Side Rn = R;
+	Rn.nofit = &meta32[2];
+	if (!gtab.p || !ra || !rb || !sc || pj_cut(Rn, nr, pbits, !nil_matches, B, &meta32[3]) < 0) {
 		(void) sync();                              // kernels may still read B's buffers
 		unfix2(ra, rb);
 		return -1;
@@ -1571,16 +1632,22 @@ join_gt(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_bat
 		unfix2(ra, rb);
 		return -1;
 	}
-	if (L.dense)
-		hipLaunchKernelGGL(k_gt_probe<true>, dim3((unsigned) ntiles), dim3(256), 0, st, a, gtab.as<ulonglong2>());
-	else
-		hipLaunchKernelGGL(k_gt_probe<false>, dim3((unsigned) ntiles), dim3(256), 0, st, a, gtab.as<ulonglong2>());
+	if (L.w == 8) {
+		if (L.dense)
+			hipLaunchKernelGGL((k_gt_probe<true, 8>), dim3((unsigned) ntiles), dim3(256), 0, st, a, gtab.as<ulonglong2>());
+		else
+			hipLaunchKernelGGL((k_gt_probe<false, 8>), dim3((unsigned) ntiles), dim3(256), 0, st, a, gtab.as<ulonglong2>());
+	} else if (L.dense) {
+		hipLaunchKernelGGL((k_gt_probe<true, 4>), dim3((unsigned) ntiles), dim3(256), 0, st, a, gtab.as<ulonglong2>());
+	} else {
+		hipLaunchKernelGGL((k_gt_probe<false, 4>), dim3((unsigned) ntiles), dim3(256), 0, st, a, gtab.as<ulonglong2>());
+	}
 	uint32_t *h = (uint32_t *) pinned(64);
 	if (!hip_ok(hipMemcpyAsync(h, meta32, 64, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
 		unfix2(ra, rb);
 		return -1;
 	}
-	if (h[0] || h[1]) {                                 // duplicate build keys / region overflow
+	if (h[0] || h[1] || h[2]) {                         // duplicate build keys / region overflow / no 4-byte image
 		unfix2(ra, rb);
 		return 1;
 	}
@@ -1620,8 +1687,8 @@ hash_join(const mgdk_bat *l, const mgdk_bat *r, const Cand &lc, const Cand &rc, 
 	side_init(L, l, lc);
 	side_init(R, r, rc);
 	const int w = L.w;
-	int rc_ = w == 4 ? join_gt(L, nl, R, nr, nil_matches, ap, bp, ukey) : 1;
-	if (rc_ > 0 && w == 4)
+	int rc_ = w == 4 || w == 8 ? join_gt(L, nl, R, nr, nil_matches, ap, bp, ukey) : 1;
+	if (rc_ > 0 && (w == 4 || w == 8))
 		rc_ = join_part(L, nl, R, nr, nil_matches, ap, bp, ukey);
 	if (rc_ > 0)
 		rc_ = w == 8 ? join_lp<8>(L, nl, R, nr, nil_matches, ap, bp, ukey)

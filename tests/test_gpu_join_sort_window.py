@@ -124,6 +124,38 @@ def test_join_partitioned(gdk, ora, nil_matches, case):
     assert np.array_equal(b.to_numpy(), ob.values())
 
 
+@pytest.mark.parametrize("tname", ["lng", "oid"])
+@pytest.mark.parametrize("case", ["gt", "part", "probe_wide", "build_wide"])
+def test_join_8byte_keys(gdk, ora, tname, case):
+    """8-byte keys run the global-table / partitioned paths by their 4-byte
+    images when every build value has one: nils (nil_matches both ways),
+    probe values beyond 32 bits (no match), and a build value beyond 32 bits
+    (falls back to the open-addressing path) -- all bit-exact with the
+    oracle."""
+    r = rng(86)
+    nr, nl = (2_100_003, 3_000_001) if case == "part" else (700_001, 2_500_003)
+    tp = getattr(gdk, "TYPE_" + tname)
+    otp = getattr(ora, "TYPE_" + tname)
+    if tname == "lng":
+        rv = r.choice(np.arange(-(1 << 30), 1 << 30, 7), nr, replace=False).astype(np.int64)
+        nil = np.iinfo(np.int64).min
+    else:
+        rv = r.choice(np.arange(0, 1 << 31, 7), nr, replace=False).astype(np.uint64)
+        nil = np.uint64(1 << 63)
+    rv[123] = nil
+    lv = r.choice(rv, nl)
+    lv[::997] = nil
+    if case == "probe_wide":
+        lv[5::1013] = (1 << 40) + 3 if tname == "oid" else -(1 << 40) - 3
+    if case == "build_wide":
+        rv[77] = (1 << 33) + 5
+    for nm in (False, True):
+        a, b = gdk.BATjoin(mk(gdk, tp, lv, hseqbase=11), mk(gdk, tp, rv, hseqbase=4), nil_matches=nm)
+        oa, ob = ora.BATjoin(omk(ora, otp, lv, hseqbase=11), omk(ora, otp, rv, hseqbase=4), nil_matches=nm)
+        assert np.array_equal(a.to_numpy(), oa.values()), nm
+        assert np.array_equal(b.to_numpy(), ob.values()), nm
+
+
 def test_join_empty_sides(gdk):
     e = mk(gdk, gdk.TYPE_int, np.zeros(0, np.int32))
     x = mk(gdk, gdk.TYPE_int, np.arange(10, dtype=np.int32))
