@@ -223,6 +223,7 @@ struct ProbeArgs {
 	BUN n;
 	uint64_t cap;
 	uint32_t maxd;
+	const uint32_t *maxd_dev;   // non-NULL: the build's largest displacement, read on the device
 	bool nil_matches;
 	uint32_t *ticket;
 	uint64_t *status;
@@ -255,6 +256,7 @@ k_lp_probe(ProbeArgs a, const typename Tab<KW>::slot_t *t)
 	__syncthreads();
 	const uint32_t tile = s_tile;
 	const BUN base = (BUN) tile * JTILE + tid;
+	const uint32_t maxd = a.maxd_dev ? min(*a.maxd_dev, DMAX) : a.maxd;
 
 	uint64_t key[JR];
 	bool ok[JR];
@@ -306,7 +308,7 @@ k_lp_probe(ProbeArgs a, const typename Tab<KW>::slot_t *t)
 						break;
 					}
 				}
-				if (d >= a.maxd) {
+				if (d >= maxd) {
 					stop = true;
 					break;
 				}
@@ -386,7 +388,7 @@ k_lp_probe(ProbeArgs a, const typename Tab<KW>::slot_t *t)
 					break;
 				if (TB::same(s, key[r]) && p1 < prev && p1 > nb)
 					nb = p1;
-				if (d >= a.maxd)
+				if (d >= maxd)
 					break;
 			}
 			pos++;
@@ -512,12 +514,22 @@ join_lp(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_bat
 	if (KW == 8)
 		hipLaunchKernelGGL(k_lp_dupcheck, dim3(grid_for(nr, 1024, 16384)), dim3(256), 0, st, R, nr, cap,
 				   nil_matches, (const Slot16 *) tab.p, (uint32_t *) &meta[3]);
-	if (!hip_ok(hipMemcpyAsync(h, meta, 32, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
-		return -1;
-	const uint32_t maxd = (uint32_t) h[2];
-	const bool uniq = h[3] == 0;
-	if (maxd > DMAX || (!uniq && maxd > DMAX_DUP))
-		return 1;
+	// small build sides: no host round trip between build and probe -- the
+	// probe reads the displacement bound on the device and handles
+	// duplicates (the general probe is exact for unique keys too); the
+	// build's outcome is checked with the probe's, and a bad one discards
+	// the probe (a round trip costs more than the probe of a small join)
+	const bool onesync = nr < 65536;
+	uint32_t maxd = DMAX;
+	bool uniq = false;
+	if (!onesync) {
+		if (!hip_ok(hipMemcpyAsync(h, meta, 32, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+			return -1;
+		maxd = (uint32_t) h[2];
+		uniq = h[3] == 0;
+		if (maxd > DMAX || (!uniq && maxd > DMAX_DUP))
+			return 1;
+	}
 
 	const uint64_t jtile = 256 * jrows<KW>();
 	const uint64_t ntiles = (nl + jtile - 1) / jtile;
@@ -531,6 +543,7 @@ join_lp(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_bat
 	a.n = nl;
 	a.cap = cap;
 	a.maxd = maxd;
+	a.maxd_dev = onesync ? (const uint32_t *) &meta[2] : nullptr;
 	a.nil_matches = nil_matches;
 	a.nt = nt;
 	a.ntiles = (uint32_t) ntiles;
@@ -550,7 +563,7 @@ join_lp(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_bat
 		a.r2 = (oid *) rb->theap;
 		a.ocap = ocap;
 		if (!hip_ok(hipMemsetAsync(sc, 0, sbytes, st), "memset") ||
-		    !hip_ok(hipMemsetAsync(meta, 0, 16, st), "memset")) {
+		    !hip_ok(hipMemsetAsync(meta, 0, 16, st), "memset")) {   // [0], [1]: the build's [2], [3] stay
 			unfix2(ra, rb);
 			return -1;
 		}
@@ -560,9 +573,13 @@ join_lp(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_bat
 		else
 			hipLaunchKernelGGL((k_lp_probe<KW, false>), dim3((unsigned) ntiles), dim3(256), 0, st, a,
 					   (const slot_t *) tab.p);
-		if (!hip_ok(hipMemcpyAsync(h, meta, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
+		if (!hip_ok(hipMemcpyAsync(h, meta, 32, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
 			unfix2(ra, rb);
 			return -1;
+		}
+		if (onesync && ((uint32_t) h[2] > DMAX || (h[3] != 0 && (uint32_t) h[2] > DMAX_DUP))) {
+			unfix2(ra, rb);
+			return 1;                       // the build overflowed: the CSR path
 		}
 		if (h[1] & 1) {
 			seterr("HY013!BATjoin: look-back did not complete");
@@ -572,7 +589,7 @@ join_lp(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_bat
 		const uint64_t nout = h[0];
 		if (nout <= ocap) {
 			ra->count = rb->count = nout;
-			*ukey = uniq;
+			*ukey = onesync ? h[3] == 0 : uniq;
 			*ap = ra;
 			*bp = rb;
 			return 0;
