@@ -28,6 +28,7 @@
 //   two-pass count/scan/write probe that walks each bucket backwards.
 // nil never matches unless nil_matches.  Integer key types (bte..lng, date,
 // oid).
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <vector>
@@ -1681,6 +1682,214 @@ join_gt(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_bat
 	return 0;
 }
 
+// ---------------------------------------------------------------------------
+// Broadcast path (small unique build side, <= BJ_MAXR rows; 4-byte keys or
+// 8-byte keys with 4-byte images): every workgroup builds the whole build
+// side's table in its LDS (the build column stays in L2) and then claims
+// probe tiles by ticket, answering them from LDS and placing the matches by
+// decoupled look-back -- one launch and one host round trip, instead of a
+// global-table build (device-scope CAS chains) followed by a probe.  The
+// grid is at most two workgroups per CU, so the tables are built a bounded
+// number of times however long the probe side is.
+// ---------------------------------------------------------------------------
+
+constexpr uint32_t BJ_SLOTS = 8192;           // 64 KiB of LDS: two workgroups per CU
+constexpr uint32_t BJ_MAXR = 6144;            // load <= 3/4
+
+template <int W, bool DENSE>
+__global__ __launch_bounds__(256) void
+k_bj(Side L, BUN nl, Side R, uint32_t nr, bool nil_matches, uint32_t ntiles, uint32_t *ticket, uint64_t *status,
+     uint64_t *meta, uint32_t *flags, oid *r1, oid *r2)
+{
+	constexpr int JR = GT_JR, JTILE = 256 * JR;
+	__shared__ unsigned long long tab[BJ_SLOTS];
+	__shared__ uint32_t s_tot[64];
+	__shared__ uint64_t s_off[64];
+	__shared__ uint32_t s_tile;
+	__shared__ uint64_t s_pre;
+	__shared__ int s_bad;
+	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+	for (uint32_t i = tid; i < BJ_SLOTS; i += 256)
+		tab[i] = 0ull;
+	if (tid == 0)
+		s_bad = 0;
+	if (tid < 64)
+		s_tot[tid] = 0;
+	__syncthreads();
+	// the build side: 4-byte images, nil only when nil_matches
+	bool bad = false;
+	for (uint32_t j = tid; j < nr; j += 256) {
+		bool isnil, fits = true;
+		const uint64_t v = key_of(R, j, isnil);
+		const uint32_t k = W == 8 ? narrow_key(R, v, isnil, fits) : (uint32_t) v;
+		if (!fits) {
+			bad = true;                          // the host falls back
+			continue;
+		}
+		if (isnil && !nil_matches)
+			continue;
+		const unsigned long long e = ((unsigned long long) (j + 1) << 32) | k;
+		uint32_t h = pj_hash(k) >> (32 - 13);
+		for (;;) {
+			const unsigned long long o = atomicCAS(&tab[h], 0ull, e);
+			if (o == 0ull)
+				break;
+			if ((uint32_t) o == k) {
+				bad = true;                  // duplicate key: the general path
+				break;
+			}
+			h = (h + 1) & (BJ_SLOTS - 1);
+		}
+	}
+	if (__any(bad) && lane == 0)
+		atomicOr(&s_bad, 1);
+	__syncthreads();
+	if (s_bad) {
+		if (tid == 0)
+			atomicOr(flags, 1u);
+		// still take (and complete) tickets so the look-back of any tile
+		// already claimed by another workgroup finishes
+	}
+	const bool skip = s_bad != 0;
+	for (;;) {
+		__syncthreads();
+		if (tid == 0)
+			s_tile = atomicAdd(ticket, 1u);
+		__syncthreads();
+		const uint32_t tile = s_tile;
+		if (tile >= ntiles)
+			break;
+		const BUN base = (BUN) tile * JTILE + tid;
+		// typed, unconditional loads of the tile's keys (clamped rows)
+		uint64_t kv[JR];
+#pragma unroll
+		for (int r = 0; r < JR; r++) {
+			const BUN i = base + (BUN) r * 256, ic = i < nl ? i : nl - 1;
+			const BUN p = DENSE ? L.off + ic : L.oids[ic] - L.hseq;
+			kv[r] = W == 8 ? ((const uint64_t *) L.base)[p] : (uint64_t) (uint32_t) ((const int32_t *) L.base)[p];
+		}
+		uint32_t m[JR];
+#pragma unroll
+		for (int r = 0; r < JR; r++) {
+			const BUN i = base + (BUN) r * 256;
+			m[r] = 0;
+			if (i < nl && !skip) {
+				bool fits = true;
+				const uint64_t v = kv[r];
+				const bool isnil = W == 8 ? v == (L.uns ? (1ull << 63) : (uint64_t) INT64_MIN) : (uint32_t) v == 0x80000000u;
+				const uint32_t k = W == 8 ? narrow_key(L, v, isnil, fits) : (uint32_t) v;
+				if (fits && (!isnil || nil_matches)) {
+					uint32_t h = pj_hash(k) >> (32 - 13);
+					for (;;) {
+						const unsigned long long o = tab[h];
+						if (o == 0ull)
+							break;
+						if ((uint32_t) o == k) {
+							m[r] = (uint32_t) (o >> 32);
+							break;
+						}
+						h = (h + 1) & (BJ_SLOTS - 1);
+					}
+				}
+			}
+		}
+		uint32_t ex[JR];
+#pragma unroll
+		for (int r = 0; r < JR; r++) {
+			const uint64_t bal = __ballot(m[r] != 0);
+			ex[r] = __popcll(bal & ((1ull << lane) - 1));
+			if (lane == 0)
+				s_tot[r * 4 + w] = __popcll(bal);
+		}
+		__syncthreads();
+		if (w == 0) {
+			uint64_t v = s_tot[lane];
+			const uint64_t own = v;
+#pragma unroll
+			for (int o = 1; o < 64; o <<= 1) {
+				const uint64_t u = __shfl_up(v, o);
+				if (lane >= (unsigned) o)
+					v += u;
+			}
+			s_off[lane] = v - own;
+			const uint64_t agg = __shfl(v, 63);
+			const uint64_t pre = lookback(status, tile, agg, (uint32_t *) &meta[1]);
+			if (lane == 0) {
+				s_pre = pre;
+				if (tile == ntiles - 1)
+					meta[0] = pre + agg;
+			}
+		}
+		__syncthreads();
+		const uint64_t pre = s_pre;
+#pragma unroll
+		for (int r = 0; r < JR; r++) {
+			if (m[r] == 0)
+				continue;
+			const uint64_t pos = pre + s_off[r * 4 + w] + ex[r];
+			const BUN i = base + (BUN) r * 256;
+			r1[pos] = oid_of(L, i);
+			r2[pos] = oid_of(R, m[r] - 1);
+		}
+	}
+}
+
+// returns 1 when not applicable or the build side has duplicates / values
+// without a 4-byte image (the caller takes the next path)
+int
+join_bj(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_bat **ap, mgdk_bat **bp, bool *ukey)
+{
+	static const int mode = getenv("MGDK_JOIN_BJ") ? atoi(getenv("MGDK_JOIN_BJ")) : 1;
+	const bool w4 = L.w == 4 && R.w == 4, w8 = L.w == 8 && R.w == 8 && L.base && R.base;
+	if (mode == 0 || !(w4 || w8) || nr == 0 || nr > BJ_MAXR || nl == 0)
+		return 1;
+	const uint64_t jtile = 256 * GT_JR;
+	const uint64_t ntiles = (nl + jtile - 1) / jtile;
+	if (ntiles >= (1ull << 31))
+		return 1;
+	hipStream_t st = stream();
+	uint32_t *meta32 = (uint32_t *) meta_buf();
+	uint64_t *meta = (uint64_t *) meta32 + 4;
+	mgdk_bat *ra = newbat(0, MGDK_oid, nl), *rb = newbat(0, MGDK_oid, nl);
+	const size_t sbytes = (ntiles + 8) * sizeof(uint64_t);
+	char *sc = (char *) scratch(sbytes);
+	if (!ra || !rb || !sc || !hip_ok(hipMemsetAsync(meta32, 0, 64, st), "memset") ||
+	    !hip_ok(hipMemsetAsync(sc, 0, sbytes, st), "memset")) {
+		unfix2(ra, rb);
+		return -1;
+	}
+	const unsigned grid = (unsigned) std::min<uint64_t>(ntiles, 512);
+#define BJ(W_, D_) hipLaunchKernelGGL((k_bj<W_, D_>), dim3(grid), dim3(256), 0, st, L, nl, R, (uint32_t) nr, \
+				   nil_matches, (uint32_t) ntiles, (uint32_t *) sc, (uint64_t *) sc + 8, meta, &meta32[0], \
+				   (oid *) ra->theap, (oid *) rb->theap)
+	if (w8) {
+		if (L.dense) BJ(8, true); else BJ(8, false);
+	} else {
+		if (L.dense) BJ(4, true); else BJ(4, false);
+	}
+#undef BJ
+	uint32_t *h = (uint32_t *) pinned(64);
+	if (!hip_ok(hipMemcpyAsync(h, meta32, 64, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
+		unfix2(ra, rb);
+		return -1;
+	}
+	if (h[0]) {
+		unfix2(ra, rb);
+		return 1;
+	}
+	const uint64_t *h64 = (const uint64_t *) h + 4;
+	if (h64[1] & 1) {
+		seterr("HY013!BATjoin: look-back did not complete");
+		unfix2(ra, rb);
+		return -1;
+	}
+	ra->count = rb->count = h64[0];
+	*ukey = true;
+	*ap = ra;
+	*bp = rb;
+	return 0;
+}
+
 }  // namespace
 
 namespace mgdk {
@@ -1704,7 +1913,9 @@ hash_join(const mgdk_bat *l, const mgdk_bat *r, const Cand &lc, const Cand &rc, 
 	side_init(L, l, lc);
 	side_init(R, r, rc);
 	const int w = L.w;
-	int rc_ = w == 4 || w == 8 ? join_gt(L, nl, R, nr, nil_matches, ap, bp, ukey) : 1;
+	int rc_ = w == 4 || w == 8 ? join_bj(L, nl, R, nr, nil_matches, ap, bp, ukey) : 1;
+	if (rc_ > 0 && (w == 4 || w == 8))
+		rc_ = join_gt(L, nl, R, nr, nil_matches, ap, bp, ukey);
 	if (rc_ > 0 && (w == 4 || w == 8))
 		rc_ = join_part(L, nl, R, nr, nil_matches, ap, bp, ukey);
 	if (rc_ > 0)

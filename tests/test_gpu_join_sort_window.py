@@ -156,6 +156,39 @@ def test_join_8byte_keys(gdk, ora, tname, case):
         assert np.array_equal(b.to_numpy(), ob.values()), nm
 
 
+@pytest.mark.parametrize("tname", ["int", "lng", "oid", "date"])
+@pytest.mark.parametrize("case", ["plain", "cands", "dup", "one_tile"])
+def test_join_broadcast_small_build(gdk, ora, tname, case):
+    """Build sides of <= 6144 unique keys: every workgroup builds the table
+    in LDS and claims probe tiles (one launch): nils both ways, candidate
+    lists on both sides, a probe of one tile, a duplicate build key (falls
+    back) -- bit-exact with the oracle."""
+    r = rng(87)
+    nr, nl = 5000, (1500 if case == "one_tile" else 400_003)
+    tp, otp = getattr(gdk, "TYPE_" + tname), getattr(ora, "TYPE_" + tname)
+    dt = {"int": np.int32, "date": np.int32, "lng": np.int64, "oid": np.uint64}[tname]
+    lo = 0 if tname == "oid" else -(1 << 30)
+    rv = r.choice(np.arange(lo, 1 << 30, 3), nr, replace=False).astype(dt)
+    nil = {np.int32: np.iinfo(np.int32).min, np.int64: np.iinfo(np.int64).min, np.uint64: np.uint64(1 << 63)}[dt]
+    rv[17] = nil
+    if case == "dup":
+        rv[3] = rv[4]
+    lv = r.choice(rv, nl)
+    lv[r.random(nl) < 0.1] = rv[0] + 1                       # misses (not a multiple of 3 apart)
+    lv[::331] = nil
+    kw, okw = {}, {}
+    if case == "cands":
+        sl = np.sort(r.choice(nl, nl // 3, replace=False)).astype(np.uint64) + 9
+        sr = np.sort(r.choice(nr, nr - 300, replace=False)).astype(np.uint64) + 2
+        kw = dict(sl=mk(gdk, gdk.TYPE_oid, sl), sr=mk(gdk, gdk.TYPE_oid, sr))
+        okw = dict(sl=omk(ora, ora.TYPE_oid, sl, sorted_=True), sr=omk(ora, ora.TYPE_oid, sr, sorted_=True))
+    for nm in (False, True):
+        a, b = gdk.BATjoin(mk(gdk, tp, lv, hseqbase=9), mk(gdk, tp, rv, hseqbase=2), nil_matches=nm, **kw)
+        oa, ob = ora.BATjoin(omk(ora, otp, lv, hseqbase=9), omk(ora, otp, rv, hseqbase=2), nil_matches=nm, **okw)
+        assert np.array_equal(a.to_numpy(), oa.values()), nm
+        assert np.array_equal(b.to_numpy(), ob.values()), nm
+
+
 def test_join_empty_sides(gdk):
     e = mk(gdk, gdk.TYPE_int, np.zeros(0, np.int32))
     x = mk(gdk, gdk.TYPE_int, np.arange(10, dtype=np.int32))
