@@ -60,38 +60,94 @@ struct SumOut {
 	unsigned long long maxabs;     // magnitude class (absbits)
 };
 
-__global__ __launch_bounds__(256) void
-k_sum(const void *base, int w, bool dense, oid off, const oid *oids, oid hseq, BUN n, SumOut *o)
+// one workgroup's share of a BATsum, summed by k_sum_fin: a same-address
+// atomic from every workgroup serialised at one L2 channel
+struct SumPart {
+	unsigned long long lo, hi, cnt, firstnil, maxabs, pad[3];
+};
+
+template <int W>
+__device__ __forceinline__ hge
+ldw(const void *base, BUN p, bool &isnil)
 {
+	if constexpr (W == 1) { const int8_t v = ((const int8_t *) base)[p]; isnil = v == INT8_MIN; return v; }
+	else if constexpr (W == 2) { const int16_t v = ((const int16_t *) base)[p]; isnil = v == INT16_MIN; return v; }
+	else if constexpr (W == 4) { const int32_t v = ((const int32_t *) base)[p]; isnil = v == INT32_MIN; return v; }
+	else if constexpr (W == 8) { const int64_t v = ((const int64_t *) base)[p]; isnil = v == INT64_MIN; return v; }
+	else { const hge v = ((const hge *) base)[p]; isnil = is_nil(v); return v; }
+}
+
+// W: value width as a template parameter and U rows per thread loaded
+// before any is added (a runtime width switch waits for each load)
+template <int W, bool DENSE>
+__global__ __launch_bounds__(256) void
+k_sum(const void *base, oid off, const oid *oids, oid hseq, BUN n, SumPart *parts)
+{
+	constexpr int U = 8;
 	hge s = 0;
 	unsigned long long cnt = 0, firstnil = ~0ull, mx = 0;
-	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
-		BUN p = dense ? off + i : oids[i] - hseq;
-		bool isnil;
-		hge v = ldv(base, w, p, isnil);
-		if (isnil) {
-			if (i < firstnil)
-				firstnil = i;
-			continue;
+	const BUN stride = (BUN) gridDim.x * blockDim.x;
+	for (BUN i0 = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += U * stride) {
+		hge v[U];
+		bool nl[U];
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const BUN i = i0 + (BUN) u * stride, ic = i < n ? i : n - 1;
+			v[u] = ldw<W>(base, DENSE ? off + ic : oids[ic] - hseq, nl[u]);
 		}
-		s += v;
-		cnt++;
-		unsigned long long a = absbits(v);
-		mx = a > mx ? a : mx;
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const BUN i = i0 + (BUN) u * stride;
+			if (i >= n)
+				continue;
+			if (nl[u]) {
+				firstnil = i < firstnil ? i : firstnil;
+				continue;
+			}
+			s += v[u];
+			cnt++;
+			const unsigned long long a = absbits(v[u]);
+			mx = a > mx ? a : mx;
+		}
 	}
 	s = block_sum128(s);
 	cnt = block_reduce(cnt, [](unsigned long long x, unsigned long long y) { return x + y; });
 	firstnil = block_reduce(firstnil, [](unsigned long long x, unsigned long long y) { return x < y ? x : y; });
 	mx = block_reduce(mx, [](unsigned long long x, unsigned long long y) { return x > y ? x : y; });
 	if (threadIdx.x == 0) {
-		if (s)
-			atomic_add128(o->sum, s);
-		if (cnt)
-			atomicAdd(&o->cnt, cnt);
-		if (firstnil != ~0ull)
-			atomicMin(&o->firstnil, firstnil);
-		if (mx)
-			atomicMax(&o->maxabs, mx);
+		SumPart p;
+		p.lo = (unsigned long long) (uhge) s;
+		p.hi = (unsigned long long) ((uhge) s >> 64);
+		p.cnt = cnt;
+		p.firstnil = firstnil;
+		p.maxabs = mx;
+		p.pad[0] = p.pad[1] = p.pad[2] = 0;
+		parts[blockIdx.x] = p;
+	}
+}
+
+__global__ __launch_bounds__(256) void
+k_sum_fin(const SumPart *parts, uint32_t np, SumOut *o)
+{
+	hge s = 0;
+	unsigned long long cnt = 0, firstnil = ~0ull, mx = 0;
+	for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) {
+		const SumPart p = parts[i];
+		s += (hge) (((uhge) p.hi << 64) | p.lo);
+		cnt += p.cnt;
+		firstnil = p.firstnil < firstnil ? p.firstnil : firstnil;
+		mx = p.maxabs > mx ? p.maxabs : mx;
+	}
+	s = block_sum128(s);
+	cnt = block_reduce(cnt, [](unsigned long long x, unsigned long long y) { return x + y; });
+	firstnil = block_reduce(firstnil, [](unsigned long long x, unsigned long long y) { return x < y ? x : y; });
+	mx = block_reduce(mx, [](unsigned long long x, unsigned long long y) { return x > y ? x : y; });
+	if (threadIdx.x == 0) {
+		o->sum[0] = (unsigned long long) (uhge) s;
+		o->sum[1] = (unsigned long long) ((uhge) s >> 64);
+		o->cnt = cnt;
+		o->firstnil = firstnil;
+		o->maxabs = mx;
 	}
 }
 
@@ -226,13 +282,29 @@ mgdk_BATsum(void *res, int tp, mgdk_bat *b, mgdk_bat *s, bool skip_nils, bool ni
 	if (cand_init(&ci, b, s) < 0)
 		return -1;
 	SumOut *o = (SumOut *) meta_buf();
-	SumOut init = {{0, 0}, 0, ~0ull, 0};
-	if (!hip_ok(hipMemcpyAsync(o, &init, sizeof(init), hipMemcpyHostToDevice, stream()), "memcpy"))
-		return -1;
 	const oid off = ci.dense ? ci.seq - b->hseqbase : 0;
-	if (ci.n)
-		hipLaunchKernelGGL(k_sum, dim3(grid_for(ci.n, 256 * 8, 256 * 16)), dim3(256), 0, stream(),
-				   b->theap, b->twidth, ci.dense, off, ci.oids, b->hseqbase, ci.n, o);
+	if (ci.n) {
+		const unsigned g = grid_for(ci.n, 256 * 8, 2048);
+		SumPart *parts = (SumPart *) scratch((size_t) g * sizeof(SumPart));
+		if (parts == nullptr)
+			return -1;
+		const dim3 gd(g), blk(256);
+#define KS(W_) do { if (ci.dense) hipLaunchKernelGGL((k_sum<W_, true>), gd, blk, 0, stream(), b->theap, off, ci.oids, b->hseqbase, ci.n, parts); \
+		else hipLaunchKernelGGL((k_sum<W_, false>), gd, blk, 0, stream(), b->theap, off, ci.oids, b->hseqbase, ci.n, parts); } while (0)
+		switch (b->twidth) {
+		case 1: KS(1); break;
+		case 2: KS(2); break;
+		case 4: KS(4); break;
+		case 8: KS(8); break;
+		default: KS(16); break;
+		}
+#undef KS
+		hipLaunchKernelGGL(k_sum_fin, dim3(1), dim3(256), 0, stream(), parts, g, o);
+	} else {
+		SumOut init = {{0, 0}, 0, ~0ull, 0};
+		if (!hip_ok(hipMemcpyAsync(o, &init, sizeof(init), hipMemcpyHostToDevice, stream()), "memcpy"))
+			return -1;
+	}
 	SumOut *h = (SumOut *) pinned(sizeof(SumOut));
 	if (h == nullptr || !hip_ok(hipMemcpyAsync(h, o, sizeof(SumOut), hipMemcpyDeviceToHost, stream()), "memcpy") ||
 	    !sync())
