@@ -442,60 +442,52 @@ k_gid_count(const K *keys, BUN n, uint32_t *cnt)
 		cnt[blockIdx.x] = c;
 }
 
+// group ids of sorted keys: element j of the tile (= q * 256 + thread) is a
+// group start when its key differs from its predecessor's (read straight
+// from memory: the same lines, shifted by one key); its id is the tile's
+// prefix + the starts before it, ranked by one ballot per row and a 16 x 4
+// LDS table of row / wave totals, and stored where it is (coalesced) -- no
+// LDS image of the keys or ids, so the tile needs 256 B of LDS instead of
+// 52 KiB (3 workgroups per CU before)
 template <typename K>
 __global__ __launch_bounds__(256) void
 k_gid_write(const K *keys, BUN n, const uint64_t *pre, oid *gid)
 {
-	// coalesced loads into LDS, a thread scans 16 consecutive keys, the ids
-	// go back through LDS to coalesced stores
 	constexpr int Q = GTILE / 256;
-	// one pad slot per 16 so a thread's 16-run starts in a different bank
-#define GPAD(j) ((j) + ((j) >> 4))
-	__shared__ K s_k[GPAD(GTILE + 1) + 1];
-	__shared__ oid s_g[GPAD(GTILE) + 1];
-	__shared__ uint32_t s_w[4];
+	__shared__ uint32_t s_cnt[Q][4];
 	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
 	const BUN t0 = (BUN) blockIdx.x * GTILE;
+	K cur[Q], prv[Q];
+#pragma unroll
+	for (int q = 0; q < Q; q++) {
+		const BUN i = t0 + (BUN) q * 256 + tid, ic = i < n ? i : n - 1;
+		cur[q] = keys[ic];
+		prv[q] = keys[ic > 0 ? ic - 1 : 0];
+	}
+	const uint64_t lt = (1ull << lane) - 1;
+	uint64_t bal[Q];
 #pragma unroll
 	for (int q = 0; q < Q; q++) {
 		const BUN i = t0 + (BUN) q * 256 + tid;
-		s_k[GPAD(1 + q * 256 + tid)] = i < n ? keys[i] : K(0);
+		bal[q] = __ballot(i > 0 && i < n && cur[q] != prv[q]);
+		if (lane == 0)
+			s_cnt[q][w] = (uint32_t) __popcll(bal[q]);
 	}
-	if (tid == 0)
-		s_k[GPAD(0)] = t0 > 0 ? keys[t0 - 1] : K(0);
 	__syncthreads();
-	uint32_t inc[Q], c = 0;
-#pragma unroll
-	for (int q = 0; q < Q; q++) {
-		const int j = tid * Q + q;
-		const BUN i = t0 + j;
-		c += (i > 0 && i < n && s_k[GPAD(j + 1)] != s_k[GPAD(j)]);
-		inc[q] = c;
-	}
-	uint32_t x = c;
-#pragma unroll
-	for (int o = 1; o < 64; o <<= 1) {
-		const uint32_t y = __shfl_up(x, o);
-		if (lane >= (unsigned) o)
-			x += y;
-	}
-	if (lane == 63)
-		s_w[w] = x;
-	__syncthreads();
-	uint64_t base = pre[blockIdx.x] + x - c;
-	for (unsigned q = 0; q < w; q++)
-		base += s_w[q];
-#pragma unroll
-	for (int q = 0; q < Q; q++)
-		s_g[GPAD(tid * Q + q)] = base + inc[q];
-	__syncthreads();
+	uint64_t run = pre[blockIdx.x];
 #pragma unroll
 	for (int q = 0; q < Q; q++) {
 		const BUN i = t0 + (BUN) q * 256 + tid;
+		uint32_t before = 0, row = 0;
+#pragma unroll
+		for (unsigned v = 0; v < 4; v++) {
+			before += v < w ? s_cnt[q][v] : 0;
+			row += s_cnt[q][v];
+		}
 		if (i < n)
-			gid[i] = s_g[GPAD(q * 256 + tid)];
+			gid[i] = run + before + (uint32_t) __popcll(bal[q] & lt) + (uint32_t) ((bal[q] >> lane) & 1);
+		run += row;
 	}
-#undef GPAD
 }
 
 __global__ __launch_bounds__(256) void
