@@ -430,12 +430,20 @@ __global__ __launch_bounds__(256) void
 k_gid_count(const K *keys, BUN n, uint32_t *cnt)
 {
 	const BUN t0 = (BUN) blockIdx.x * GTILE;
+	constexpr int Q = GTILE / 256;
+	K cur[Q], prv[Q];
+#pragma unroll
+	for (int q = 0; q < Q; q++) {
+		// unconditional loads at clamped rows, all in flight
+		const BUN i = t0 + threadIdx.x + (BUN) q * 256, ic = i < n ? i : n - 1;
+		cur[q] = keys[ic];
+		prv[q] = keys[ic > 0 ? ic - 1 : 0];
+	}
 	uint32_t c = 0;
 #pragma unroll
-	for (int q = 0; q < GTILE / 256; q++) {
+	for (int q = 0; q < Q; q++) {
 		const BUN i = t0 + threadIdx.x + (BUN) q * 256;
-		if (i > 0 && i < n)
-			c += keys[i] != keys[i - 1];
+		c += i > 0 && i < n && cur[q] != prv[q];
 	}
 	c = block_reduce(c, [](uint32_t a, uint32_t b) { return a + b; });
 	if (threadIdx.x == 0)
