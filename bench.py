@@ -117,7 +117,7 @@ def main():
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
 
-    # kernel time from HIP events around k_q6c on the library stream
+    # kernel time from HIP events around the fused Q6 (k_q6s) on the library stream
     gdk.prof_reset()
     gdk.prof_enable(True)
     nprof = max(5, min(args.steps, 20))
