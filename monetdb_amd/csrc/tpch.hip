@@ -346,24 +346,25 @@ k_q6c(Q6Args a)
 // two rows are both out points its load at one shared zero line (an L2
 // hit, no HBM traffic), so every load stays unconditional and in flight; a
 // 128-B line of a column is fetched only when one of its 16 rows is still
-// in.  sect[0] counts those lines (the roofline's byte count).  The
+// in.  The workgroup partials carry the count of those lines (the
+// roofline's byte count, summed by k_q6_fin into out[2]).  The
 // zero lines are spread over 64 KiB (one 16-B slot per lane of 64 waves):
 // every inactive lane of the chip on ONE line serialised on its L2 channel.
 constexpr uint32_t Q6_ZBYTES = ZERO_REGION;
 template <int UNROLL>
 __global__ __launch_bounds__(256) void
-k_q6s(Q6Args a, const int64_t *zline, unsigned long long *sect)
+k_q6s(Q6Args a, const int64_t *zline)
 {
 	typedef int32_t i2 __attribute__((ext_vector_type(2)));
 	typedef int64_t l2 __attribute__((ext_vector_type(2)));
 	hge acc = 0;
-	uint32_t nsect = 0;
+	uint32_t nlines = 0;
 	const unsigned lane = __lane_id();
 	const uint64_t nch = a.n / 256;
 	const uint64_t nw = (uint64_t) gridDim.x * (blockDim.x / 64);
 	const l2 *z = (const l2 *) zline + ((((uint64_t) blockIdx.x * blockDim.x + threadIdx.x)) & (Q6_ZBYTES / 16 - 1));
 	// 128-B lines (8 lanes x 16 B) with at least one active lane in a ballot
-	auto sectors = [](uint64_t b) -> uint32_t {
+	auto lines = [](uint64_t b) -> uint32_t {
 		b |= b >> 1;
 		b |= b >> 2;
 		b |= b >> 4;
@@ -392,7 +393,7 @@ k_q6s(Q6Args a, const int64_t *zline, unsigned long long *sect)
 		for (int u = 0; u < UNROLL; u++) {
 			const uint64_t r0 = (c + u * nw) * 256 + 2 * lane, r1 = r0 + 128;
 			const bool a0 = m[u][0] || m[u][1], a1 = m[u][2] || m[u][3];
-			nsect += sectors(__ballot(a0)) + sectors(__ballot(a1));
+			nlines += lines(__ballot(a0)) + lines(__ballot(a1));
 			d0[u] = __builtin_nontemporal_load(a0 ? (const l2 *) (a.disc + r0) : z);
 			d1[u] = __builtin_nontemporal_load(a1 ? (const l2 *) (a.disc + r1) : z);
 		}
@@ -408,7 +409,7 @@ k_q6s(Q6Args a, const int64_t *zline, unsigned long long *sect)
 		for (int u = 0; u < UNROLL; u++) {
 			const uint64_t r0 = (c + u * nw) * 256 + 2 * lane, r1 = r0 + 128;
 			const bool a0 = m[u][0] || m[u][1], a1 = m[u][2] || m[u][3];
-			nsect += sectors(__ballot(a0)) + sectors(__ballot(a1));
+			nlines += lines(__ballot(a0)) + lines(__ballot(a1));
 			v0[u] = __builtin_nontemporal_load(a0 ? (const l2 *) (a.qty + r0) : z);
 			v1[u] = __builtin_nontemporal_load(a1 ? (const l2 *) (a.qty + r1) : z);
 		}
@@ -424,7 +425,7 @@ k_q6s(Q6Args a, const int64_t *zline, unsigned long long *sect)
 		for (int u = 0; u < UNROLL; u++) {
 			const uint64_t r0 = (c + u * nw) * 256 + 2 * lane, r1 = r0 + 128;
 			const bool a0 = m[u][0] || m[u][1], a1 = m[u][2] || m[u][3];
-			nsect += sectors(__ballot(a0)) + sectors(__ballot(a1));
+			nlines += lines(__ballot(a0)) + lines(__ballot(a1));
 			v0[u] = __builtin_nontemporal_load(a0 ? (const l2 *) (a.price + r0) : z);
 			v1[u] = __builtin_nontemporal_load(a1 ? (const l2 *) (a.price + r1) : z);
 		}
@@ -444,14 +445,13 @@ k_q6s(Q6Args a, const int64_t *zline, unsigned long long *sect)
 			acc += q6_row(a, a.sd[r0 + k], a.disc[r0 + k], a.qty[r0 + k], a.price[r0 + k]);
 			acc += q6_row(a, a.sd[r1 + k], a.disc[r1 + k], a.qty[r1 + k], a.price[r1 + k]);
 		}
-		nsect += 3 * 16;                         // counted as fully read
+		nlines += 3 * 16;                        // counted as fully read
 	}
 	if (blockIdx.x == 0 && threadIdx.x < (a.n & 255)) {
 		const uint64_t r = nch * 256 + threadIdx.x;
 		acc += q6_row(a, a.sd[r], a.disc[r], a.qty[r], a.price[r]);
 	}
-	(void) sect;
-	q6_publish(a, acc, nsect);
+	q6_publish(a, acc, nlines);
 }
 
 __global__ __launch_bounds__(256) void
@@ -955,7 +955,7 @@ mgdk_tpch_lineitem(uint64_t seed, uint64_t row0, uint64_t n, uint64_t sf_parts, 
 // 16 WG/CU; profiles/r02/q6_cascade_tune.log: 1.92 ms against 2.70-2.81 ms
 // for the full-read k_q6c on the same box)
 static std::atomic<int> q6_variant{17}, q6_bpc{16};
-static thread_local unsigned long long q6_sectors = 0;
+static thread_local unsigned long long q6_lines = 0;
 // fused Q1 main pass (tools/q1_tune.py, profiles/r01/q1_tune.log)
 static std::atomic<int> q1_layout{MGDK_Q1_LAYOUT}, q1_blocks{MGDK_Q1_BLOCKS};
 
@@ -971,7 +971,6 @@ launch_q6(Q6Args a, int variant, int bpc, hipStream_t st)
 	}
 	if (variant >= 16) {                 // predicate cascade (k_q6s)
 		dim3 g(256u * (unsigned) bpc), blk(256);
-		unsigned long long *sect = (unsigned long long *) a.out + 2;
 		const void *zbuf = zero_region();
 		if (zbuf == nullptr) {
 			variant = 14;
@@ -979,9 +978,9 @@ launch_q6(Q6Args a, int variant, int bpc, hipStream_t st)
 		}
 		const int64_t *z = (const int64_t *) zbuf;
 		switch (variant) {
-		case 17: hipLaunchKernelGGL((k_q6s<2>), g, blk, 0, st, a, z, sect); break;
-		case 18: hipLaunchKernelGGL((k_q6s<1>), g, blk, 0, st, a, z, sect); break;
-		default: hipLaunchKernelGGL((k_q6s<4>), g, blk, 0, st, a, z, sect); break;
+		case 17: hipLaunchKernelGGL((k_q6s<2>), g, blk, 0, st, a, z); break;
+		case 18: hipLaunchKernelGGL((k_q6s<1>), g, blk, 0, st, a, z); break;
+		default: hipLaunchKernelGGL((k_q6s<4>), g, blk, 0, st, a, z); break;
 		}
 		hipLaunchKernelGGL(k_q6_fin, dim3(1), dim3(1024), 0, st, a.parts, g.x, a.out);
 		return;
@@ -1052,7 +1051,7 @@ mgdk_q6_fused(mgdk_bat *shipdate, mgdk_bat *discount, mgdk_bat *quantity, mgdk_b
 	a.out = (unsigned long long *) meta_buf();
 	a.parts = nullptr;
 	hipStream_t st = stream();
-	// out: [0..1] revenue, [2] sectors read by the cascade, [8..15] a zero line
+	// out: [0..1] revenue, [2] column lines read by the cascade
 	if (!hip_ok(hipMemsetAsync(a.out, 0, 128, st), "memset"))
 		return -1;
 	{
@@ -1069,7 +1068,7 @@ mgdk_q6_fused(mgdk_bat *shipdate, mgdk_bat *discount, mgdk_bat *quantity, mgdk_b
 	if (!hip_ok(hipMemcpyAsync(h, a.out, 24, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
 		return -1;
 	memcpy(revenue, h, 16);
-	q6_sectors = h[2];
+	q6_lines = h[2];
 	return 0;
 }
 
@@ -1079,7 +1078,7 @@ mgdk_q6_fused(mgdk_bat *shipdate, mgdk_bat *discount, mgdk_bat *quantity, mgdk_b
 extern "C" unsigned long long
 mgdk_q6_last_sectors(void)
 {
-	return q6_sectors;
+	return q6_lines;
 }
 
 int
