@@ -7,6 +7,7 @@
 // outside r is the reference's "does not match always" error.  str columns
 // gather their heap offsets and share the string heap (the "stringtrick",
 // gdk_project.c:681-718).
+#include <type_traits>
 #include "mgdk_internal.h"
 
 using namespace mgdk;
@@ -273,8 +274,34 @@ k_project_bits_v(const uint32_t *__restrict__ bits, const uint64_t *__restrict__
 				}
 			}
 		}
-		for (uint32_t j = tid; j < valid; j += 256)
-			out[obase + c0 + j] = stage[j];
+		T *dst = out + obase + c0;
+		if constexpr (sizeof(T) < 4) {
+			// 1- and 2-byte values leave as 4-byte words (a store per value
+			// wrote 64 B per wave instruction): the unaligned head and the
+			// tail by single stores, every word wholly inside this chunk's
+			// output range
+			constexpr uint32_t E = 4 / sizeof(T);
+			typedef typename std::conditional<sizeof(T) == 1, uint8_t, uint16_t>::type U;
+			const uint32_t mis = (uint32_t) (((uintptr_t) dst & 3) / sizeof(T));
+			const uint32_t head = mis ? min(valid, E - mis) : 0u;
+			if (tid < head)
+				dst[tid] = stage[tid];
+			const uint32_t nw = (valid - head) / E;
+			uint32_t *dw = (uint32_t *) (dst + head);
+			for (uint32_t j = tid; j < nw; j += 256) {
+				uint32_t wv = 0;
+#pragma unroll
+				for (uint32_t e = 0; e < E; e++)
+					wv |= (uint32_t) (U) stage[head + j * E + e] << (8 * sizeof(T) * e);
+				dw[j] = wv;
+			}
+			const uint32_t done = head + nw * E;
+			if (tid < valid - done)
+				dst[done + tid] = stage[done + tid];
+		} else {
+			for (uint32_t j = tid; j < valid; j += 256)
+				dst[j] = stage[j];
+		}
 		__syncthreads();
 	}
 	// rows of r after its last whole vector
