@@ -351,7 +351,31 @@ k_q6c(Q6Args a)
 // zero lines are spread over 64 KiB (one 16-B slot per lane of 64 waves):
 // every inactive lane of the chip on ONE line serialised on its L2 channel.
 constexpr uint32_t Q6_ZBYTES = ZERO_REGION;
-template <int UNROLL>
+// BUF: the discount / quantity / extendedprice loads are raw buffer loads
+// through a per-chunk descriptor (wave-uniform base, 2 KiB range); a lane
+// with no live row passes an out-of-range offset, which the descriptor's
+// range check turns into zeros with no memory access at all
+// (cdna_hip_programming.md T15 recipe) -- instead of a zero-region load
+typedef unsigned int q6u4 __attribute__((ext_vector_type(4)));
+template <bool BUF>
+__device__ __forceinline__ void
+q6_ld(const int64_t *col, uint64_t chunk, uint64_t r, unsigned boff, bool live, const void *z, long long *out)
+{
+	typedef long long l2 __attribute__((ext_vector_type(2)));
+	if constexpr (BUF) {
+		__amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *) (col + chunk * 256), (short) 0, 2048,
+									      0x00020000);
+		const q6u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, live ? boff : 0x80000000u, 0, 0);
+		out[0] = (long long) (((unsigned long long) v.y << 32) | v.x);
+		out[1] = (long long) (((unsigned long long) v.w << 32) | v.z);
+	} else {
+		const l2 v = __builtin_nontemporal_load(live ? (const l2 *) (col + r) : (const l2 *) z);
+		out[0] = v.x;
+		out[1] = v.y;
+	}
+}
+
+template <int UNROLL, bool BUF = false>
 __global__ __launch_bounds__(256) void
 k_q6s(Q6Args a, const int64_t *zline)
 {
@@ -394,8 +418,15 @@ k_q6s(Q6Args a, const int64_t *zline)
 			const uint64_t r0 = (c + u * nw) * 256 + 2 * lane, r1 = r0 + 128;
 			const bool a0 = m[u][0] || m[u][1], a1 = m[u][2] || m[u][3];
 			nlines += lines(__ballot(a0)) + lines(__ballot(a1));
-			d0[u] = __builtin_nontemporal_load(a0 ? (const l2 *) (a.disc + r0) : z);
-			d1[u] = __builtin_nontemporal_load(a1 ? (const l2 *) (a.disc + r1) : z);
+			{
+				long long t0[2], t1[2];
+				q6_ld<BUF>(a.disc, c + u * nw, r0, 16u * lane, a0, z, t0);
+				q6_ld<BUF>(a.disc, c + u * nw, r1, 1024u + 16u * lane, a1, z, t1);
+				d0[u].x = t0[0];
+				d0[u].y = t0[1];
+				d1[u].x = t1[0];
+				d1[u].y = t1[1];
+			}
 		}
 #pragma unroll
 		for (int u = 0; u < UNROLL; u++) {
@@ -410,8 +441,15 @@ k_q6s(Q6Args a, const int64_t *zline)
 			const uint64_t r0 = (c + u * nw) * 256 + 2 * lane, r1 = r0 + 128;
 			const bool a0 = m[u][0] || m[u][1], a1 = m[u][2] || m[u][3];
 			nlines += lines(__ballot(a0)) + lines(__ballot(a1));
-			v0[u] = __builtin_nontemporal_load(a0 ? (const l2 *) (a.qty + r0) : z);
-			v1[u] = __builtin_nontemporal_load(a1 ? (const l2 *) (a.qty + r1) : z);
+			{
+				long long t0[2], t1[2];
+				q6_ld<BUF>(a.qty, c + u * nw, r0, 16u * lane, a0, z, t0);
+				q6_ld<BUF>(a.qty, c + u * nw, r1, 1024u + 16u * lane, a1, z, t1);
+				v0[u].x = t0[0];
+				v0[u].y = t0[1];
+				v1[u].x = t1[0];
+				v1[u].y = t1[1];
+			}
 		}
 #pragma unroll
 		for (int u = 0; u < UNROLL; u++) {
@@ -426,8 +464,15 @@ k_q6s(Q6Args a, const int64_t *zline)
 			const uint64_t r0 = (c + u * nw) * 256 + 2 * lane, r1 = r0 + 128;
 			const bool a0 = m[u][0] || m[u][1], a1 = m[u][2] || m[u][3];
 			nlines += lines(__ballot(a0)) + lines(__ballot(a1));
-			v0[u] = __builtin_nontemporal_load(a0 ? (const l2 *) (a.price + r0) : z);
-			v1[u] = __builtin_nontemporal_load(a1 ? (const l2 *) (a.price + r1) : z);
+			{
+				long long t0[2], t1[2];
+				q6_ld<BUF>(a.price, c + u * nw, r0, 16u * lane, a0, z, t0);
+				q6_ld<BUF>(a.price, c + u * nw, r1, 1024u + 16u * lane, a1, z, t1);
+				v0[u].x = t0[0];
+				v0[u].y = t0[1];
+				v1[u].x = t1[0];
+				v1[u].y = t1[1];
+			}
 		}
 #pragma unroll
 		for (int u = 0; u < UNROLL; u++) {
@@ -951,10 +996,11 @@ mgdk_tpch_lineitem(uint64_t seed, uint64_t row0, uint64_t n, uint64_t sf_parts, 
 // 5-7 % with this layout)
 // tuning hooks: atomics, so a concurrent set/launch never tears (dataflow
 // workers call the library concurrently, SURVEY §8 b)
-// round 2: the predicate cascade k_q6s (variant 17: 2 chunks in flight,
-// 16 WG/CU; profiles/r02/q6_cascade_tune.log: 1.92 ms against 2.70-2.81 ms
-// for the full-read k_q6c on the same box)
-static std::atomic<int> q6_variant{17}, q6_bpc{16};
+// round 2: the predicate cascade k_q6s with buffer loads (variant 19: 2
+// chunks in flight, 16 WG/CU; profiles/r02/q6_cascade/tune_buf*.log: 1.79 ms
+// at SF100 against 1.89 with zero-region loads (variant 17) and 2.57-2.81 ms
+// for the full-read k_q6c)
+static std::atomic<int> q6_variant{19}, q6_bpc{16};
 static thread_local unsigned long long q6_lines = 0;
 // fused Q1 main pass (tools/q1_tune.py, profiles/r01/q1_tune.log)
 static std::atomic<int> q1_layout{MGDK_Q1_LAYOUT}, q1_blocks{MGDK_Q1_BLOCKS};
@@ -980,6 +1026,8 @@ launch_q6(Q6Args a, int variant, int bpc, hipStream_t st)
 		switch (variant) {
 		case 17: hipLaunchKernelGGL((k_q6s<2>), g, blk, 0, st, a, z); break;
 		case 18: hipLaunchKernelGGL((k_q6s<1>), g, blk, 0, st, a, z); break;
+		case 19: hipLaunchKernelGGL((k_q6s<2, true>), g, blk, 0, st, a, z); break;
+		case 20: hipLaunchKernelGGL((k_q6s<4, true>), g, blk, 0, st, a, z); break;
 		default: hipLaunchKernelGGL((k_q6s<4>), g, blk, 0, st, a, z); break;
 		}
 		hipLaunchKernelGGL(k_q6_fin, dim3(1), dim3(1024), 0, st, a.parts, g.x, a.out);

@@ -691,7 +691,8 @@ def q6_last_lines():
 
 def q6_set_variant(variant, blocks_per_cu):
     """Launch variant of the fused Q6 (tuning / tests): 14 = full read (k_q6c),
-    16 / 17 / 18 = predicate cascade (k_q6s) with 4 / 2 / 1 chunks in flight."""
+    16 / 17 / 18 = predicate cascade (k_q6s) with 4 / 2 / 1 chunks in flight, 19 / 20 = the
+    cascade with buffer loads (2 / 4 chunks; the default is 19 at 16 workgroups per CU)."""
     lib().mgdk_q6_set_variant(C.c_int(variant), C.c_int(blocks_per_cu))
 
 

@@ -519,7 +519,7 @@ def test_q6_variants(gdk, ora, n):
     d0, d1 = ora.mkdate(1994, 1, 1), ora.mkdate(1995, 1, 1)
     want = ora.q6(host, 4)
     try:
-        for v, b in ((14, 12), (5, 8), (2, 8), (16, 16), (17, 16), (18, 8)):
+        for v, b in ((14, 12), (5, 8), (2, 8), (16, 16), (17, 16), (18, 8), (19, 16), (20, 8)):
             gdk.q6_set_variant(v, b)
             got = gdk.q6_fused(cols["shipdate"], cols["discount"], cols["quantity"],
                                cols["extendedprice"], d0, d1, 5, 7, 2400)
@@ -530,7 +530,7 @@ def test_q6_variants(gdk, ora, n):
             elif v < 16:
                 assert lines == 0
     finally:
-        gdk.q6_set_variant(17, 16)
+        gdk.q6_set_variant(19, 16)
 
 
 @pytest.mark.parametrize("case", ["none", "price_huge", "price_neg_nil"])
