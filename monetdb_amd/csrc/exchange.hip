@@ -134,7 +134,10 @@ mgdk_BATupload_device(mgdk_bat *b, const void *dev, mgdk_BUN n)
 	b->tsorted = b->trevsorted = b->tkey = n <= 1;
 	b->tnonil = n == 0;
 	b->tnil = 0;
-	return sync() ? 0 : -1;
+	b->tnosorted = b->tnorevsorted = 0;
+	b->tminpos = b->tmaxpos = MGDK_BUN_NONE;
+	b->tunique_est = 0;
+	return sync_data() ? 0 : -1;
 }
 
 extern "C" int
@@ -152,7 +155,7 @@ mgdk_BATdownload_device(const mgdk_bat *b, void *dev)
 	else if (!hip_ok(hipMemcpyAsync(dev, b->theap, b->count * (size_t) b->twidth, hipMemcpyDeviceToDevice, stream()),
 			 "memcpy D2D"))
 		return -1;
-	return sync() ? 0 : -1;
+	return sync_data() ? 0 : -1;
 }
 
 extern "C" int

@@ -968,11 +968,12 @@ key_kind(int tt)
 
 }  // namespace
 
-extern "C" int
-mgdk_BATgroup(mgdk_bat **groups, mgdk_bat **extents, mgdk_bat **histo, mgdk_bat *b, mgdk_bat *s,
-	      mgdk_bat *g, mgdk_bat *e, mgdk_bat *h)
+// BATgroup by the storage value (for str: by heap offset, exact when the
+// heap is duplicate eliminated)
+static int
+group_core(mgdk_bat **groups, mgdk_bat **extents, mgdk_bat **histo, mgdk_bat *b, mgdk_bat *s,
+	   mgdk_bat *g, mgdk_bat *e, mgdk_bat *h)
 {
-	(void) e;
 	(void) h;
 	if (b == nullptr || groups == nullptr) {
 		seterr("b must exist\n");
@@ -1193,6 +1194,299 @@ fail:
 	mgdk_BBPunfix(en);
 	mgdk_BBPunfix(hn);
 	return -1;
+}
+
+// ---- str columns whose heap is not duplicate eliminated -------------------
+// GDK groups strings by their offsets only when the heap is fully duplicate
+// eliminated, i.e. smaller than GDK_ELIMLIMIT = 64 KiB (gdk_group.c:897-919,
+// GDK_ELIMDOUBLES gdk_atoms.h:373-375); larger heaps keep equal strings at
+// different offsets and the reference compares contents (strCmp, its hash
+// path :1118-1282).  On the device:
+//   1  group by (prior group, offset) -- a refinement of the content
+//      grouping, numbered by first occurrence;
+//   2  per offset group: the string of its first row and its prior group;
+//      a 64-bit content hash of that string;
+//   3  group the offset groups (in id order = first-occurrence order) by
+//      (prior group, hash): first-occurrence numbering of the content
+//      classes, because an offset group's first row precedes another's iff
+//      its id is smaller;
+//   4  every offset group's string is compared byte for byte with its
+//      class representative's (a hash collision reruns with another seed);
+//   5  row ids through the id map, extents through the representatives,
+//      histogram = grouped sum of the offset groups' counts.
+namespace {
+
+constexpr uint64_t ELIMLIMIT = (uint64_t) 1 << 16;
+
+struct OidSrc {
+	const oid *p;     // NULL: dense
+	oid seq;
+	__device__ __forceinline__ oid at(BUN i) const { return p ? p[i] : seq + i; }
+};
+
+OidSrc
+oid_src(const mgdk_bat *b)
+{
+	return OidSrc{b->ttype == MGDK_void ? nullptr : (const oid *) b->theap, b->tseqbase};
+}
+
+// VarHeapVal (gdk_atoms.h:421-436): 1- and 2-byte offsets are relative to
+// GDK_VAROFFSET = 1024 * sizeof(var_t)
+__device__ __forceinline__ const uint8_t *
+str_ptr(const void *offs, int w, const char *vh, BUN p)
+{
+	size_t o;
+	switch (w) {
+	case 1: o = (size_t) ((const uint8_t *) offs)[p] + 8192; break;
+	case 2: o = (size_t) ((const uint16_t *) offs)[p] + 8192; break;
+	case 4: o = (size_t) ((const uint32_t *) offs)[p]; break;
+	default: o = (size_t) ((const uint64_t *) offs)[p]; break;
+	}
+	return (const uint8_t *) vh + o;
+}
+
+// step 2: the b position and prior group of every offset group's first row
+__global__ __launch_bounds__(256) void
+k_sg_rep(BUN n, OidSrc gid0, OidSrc ext0, bool cdense, oid cseq, const oid *coids, oid bhseq,
+	 const oid *g, uint64_t *rep_pos, oid *rep_g)
+{
+	const BUN stride = (BUN) gridDim.x * blockDim.x;
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+		const oid k = gid0.at(i);
+		const oid o = cdense ? cseq + i : coids[i];
+		if (ext0.at(k) == o) {
+			rep_pos[k] = o - bhseq;
+			if (rep_g)
+				rep_g[k] = g[i];
+		}
+	}
+}
+
+__global__ __launch_bounds__(256) void
+k_sg_hash(BUN K, const uint64_t *rep_pos, const void *offs, int w, const char *vh, uint64_t seed, int64_t *h)
+{
+	const BUN stride = (BUN) gridDim.x * blockDim.x;
+	for (BUN k = (BUN) blockIdx.x * blockDim.x + threadIdx.x; k < K; k += stride) {
+		const uint8_t *s = str_ptr(offs, w, vh, rep_pos[k]);
+		uint64_t x = seed ^ 0xcbf29ce484222325ULL;
+		for (; *s; s++)
+			x = (x ^ *s) * 0x100000001b3ULL;
+		x ^= x >> 31;
+		x *= 0x94d049bb133111ebULL;
+		x ^= x >> 29;
+		h[k] = (int64_t) x;
+	}
+}
+
+// step 4: 1 in *bad when an offset group's string differs from its class
+// representative's
+__global__ __launch_bounds__(256) void
+k_sg_verify(BUN K, OidSrc gid1, OidSrc ext1, const uint64_t *rep_pos, const void *offs, int w, const char *vh,
+	    uint32_t *bad)
+{
+	uint32_t diff = 0;
+	const BUN stride = (BUN) gridDim.x * blockDim.x;
+	for (BUN k = (BUN) blockIdx.x * blockDim.x + threadIdx.x; k < K; k += stride) {
+		const oid r = ext1.at(gid1.at(k));
+		if (r == k)
+			continue;
+		const uint8_t *a = str_ptr(offs, w, vh, rep_pos[k]), *c = str_ptr(offs, w, vh, rep_pos[r]);
+		size_t j = 0;
+		while (a[j] && a[j] == c[j])
+			j++;
+		diff |= a[j] != c[j];
+	}
+	diff = block_reduce(diff, [](uint32_t x, uint32_t y) { return x | y; });
+	if (threadIdx.x == 0)
+		publish_or(bad, diff);
+}
+
+// step 5: row ids through the map; bit 0 of *flags: a row's id is below its
+// predecessor's (the ids are not sorted)
+__global__ __launch_bounds__(256) void
+k_sg_final(BUN n, OidSrc gid0, OidSrc gid1, oid *gn, uint32_t *flags)
+{
+	uint32_t down = 0;
+	const BUN stride = (BUN) gridDim.x * blockDim.x;
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+		const oid v = gid1.at(gid0.at(i));
+		gn[i] = v;
+		if (i > 0)
+			down |= gid1.at(gid0.at(i - 1)) > v;
+	}
+	down = block_reduce(down, [](uint32_t x, uint32_t y) { return x | y; });
+	if (threadIdx.x == 0)
+		publish_or(flags, down);
+}
+
+__global__ __launch_bounds__(256) void
+k_sg_extents(BUN K1, OidSrc ext0, OidSrc ext1, oid *en)
+{
+	const BUN stride = (BUN) gridDim.x * blockDim.x;
+	for (BUN c = (BUN) blockIdx.x * blockDim.x + threadIdx.x; c < K1; c += stride)
+		en[c] = ext0.at(ext1.at(c));
+}
+
+// a scratch column of n rows whose properties are all unknown
+mgdk_bat *
+plain_col(int tt, BUN n)
+{
+	mgdk_bat *b = newbat(0, tt, n);
+	if (b) {
+		b->count = n;
+		b->tsorted = b->trevsorted = b->tkey = b->tnonil = b->tnil = 0;
+	}
+	return b;
+}
+
+int
+group_str_content(mgdk_bat **groups, mgdk_bat **extents, mgdk_bat **histo, mgdk_bat *b, mgdk_bat *s,
+		  mgdk_bat *g, const Cand &ci)
+{
+	const BUN n = ci.n;
+	const oid hseqb = n ? ci.first : 0;
+	const double est_b = b->tunique_est;
+	mgdk_bat *gn0 = nullptr, *en0 = nullptr, *hn0 = nullptr;
+	if (group_core(&gn0, &en0, &hn0, b, s, g, nullptr, nullptr) < 0)
+		return -1;
+	b->tunique_est = est_b;
+	const BUN K = en0->count;
+	mgdk_bat *gn = nullptr, *en = nullptr, *hn = nullptr;
+	mgdk_bat *H = nullptr, *G = nullptr, *g1 = nullptr, *e1 = nullptr;
+	hipStream_t st = stream();
+	int rc = -1;
+	BUN K1 = 0;
+	{
+		DevBuf d_pos(K * 8), d_flag(16);
+		if (!d_pos.p || !d_flag.p)
+			goto out;
+		H = plain_col(MGDK_lng, K);
+		if (H == nullptr || (g && (G = plain_col(MGDK_oid, K)) == nullptr))
+			goto out;
+		hipLaunchKernelGGL(k_sg_rep, dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st, n, oid_src(gn0),
+				   oid_src(en0), ci.dense, ci.seq, ci.oids, b->hseqbase,
+				   g ? (const oid *) g->theap : nullptr, d_pos.as<uint64_t>(),
+				   G ? (oid *) G->theap : nullptr);
+		for (uint64_t seed = 0;; seed++) {
+			if (seed == 4) {
+				seterr("HY013!BATgroup: string hash collisions");
+				goto out;
+			}
+			hipLaunchKernelGGL(k_sg_hash, dim3(grid_for(K, 256, 8192)), dim3(256), 0, st, K,
+					   d_pos.as<uint64_t>(), b->theap, b->twidth, (const char *) b->tvheap,
+					   seed * 0x9e3779b97f4a7c15ULL, (int64_t *) H->theap);
+			if (!sync() || group_core(&g1, &e1, nullptr, H, nullptr, G, nullptr, nullptr) < 0)
+				goto out;
+			uint32_t *hf = (uint32_t *) pinned(16);
+			if (!hip_ok(hipMemsetAsync(d_flag.p, 0, 16, st), "memset"))
+				goto out;
+			hipLaunchKernelGGL(k_sg_verify, dim3(grid_for(K, 256, 8192)), dim3(256), 0, st, K, oid_src(g1),
+					   oid_src(e1), d_pos.as<uint64_t>(), b->theap, b->twidth,
+					   (const char *) b->tvheap, d_flag.as<uint32_t>());
+			if (!hip_ok(hipMemcpyAsync(hf, d_flag.p, 4, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+				goto out;
+			if (hf[0] == 0)
+				break;
+			mgdk_BBPunfix(g1);
+			mgdk_BBPunfix(e1);
+			g1 = e1 = nullptr;
+		}
+		K1 = e1->count;
+		gn = newbat(hseqb, MGDK_oid, n);
+		en = newbat(0, MGDK_oid, K1);
+		if (gn == nullptr || en == nullptr || !hip_ok(hipMemsetAsync(d_flag.p, 0, 16, st), "memset"))
+			goto out;
+		hipLaunchKernelGGL(k_sg_final, dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st, n, oid_src(gn0),
+				   oid_src(g1), (oid *) gn->theap, d_flag.as<uint32_t>());
+		hipLaunchKernelGGL(k_sg_extents, dim3(grid_for(K1, 256, 8192)), dim3(256), 0, st, K1, oid_src(en0),
+				   oid_src(e1), (oid *) en->theap);
+		uint32_t *hf = (uint32_t *) pinned(16);
+		if (!hip_ok(hipMemcpyAsync(hf, d_flag.p, 4, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+			goto out;
+		gn->count = n;
+		gn->tsorted = hf[0] == 0;
+		gn->trevsorted = K1 == 1 || n <= 1;
+		gn->tkey = K1 == n;
+		gn->tnonil = 1;
+		gn->tnil = 0;
+		en->count = K1;
+		en->tsorted = en->tkey = en->tnonil = 1;
+		en->trevsorted = K1 == 1;
+		hn = mgdk_BATgroupsum(hn0, g1, e1, nullptr, MGDK_lng, true);
+		if (hn == nullptr)
+			goto out;
+		hn->tkey = K1 == 1;
+		hn->tsorted = hn->trevsorted = K1 == n || K1 == 1;
+		hn->tnonil = 1;
+		hn->tnil = 0;
+		hn->tminpos = hn->tmaxpos = MGDK_BUN_NONE;
+		hn->tunique_est = 0;
+		if (K1 > 0) {
+			oid fl[2];
+			if (oid_at(en, 0, &fl[0]) < 0 || oid_at(en, K1 - 1, &fl[1]) < 0)
+				goto out;
+			gn->tmaxpos = cand_index(ci, fl[1]);
+			if (fl[1] - fl[0] == K1 - 1)
+				setdense(en, fl[0], K1);
+		}
+		gn->tunique_est = en->tunique_est = (double) K1;
+		rc = 0;
+	}
+out:
+	mgdk_BBPunfix(gn0);
+	mgdk_BBPunfix(en0);
+	mgdk_BBPunfix(hn0);
+	mgdk_BBPunfix(H);
+	mgdk_BBPunfix(G);
+	mgdk_BBPunfix(g1);
+	mgdk_BBPunfix(e1);
+	if (rc < 0) {
+		mgdk_BBPunfix(gn);
+		mgdk_BBPunfix(en);
+		mgdk_BBPunfix(hn);
+		return -1;
+	}
+	*groups = gn;
+	if (extents)
+		*extents = en;
+	else
+		mgdk_BBPunfix(en);
+	if (histo)
+		*histo = hn;
+	else
+		mgdk_BBPunfix(hn);
+	return 0;
+}
+
+}  // namespace
+
+extern "C" int
+mgdk_BATgroup(mgdk_bat **groups, mgdk_bat **extents, mgdk_bat **histo, mgdk_bat *b, mgdk_bat *s,
+	      mgdk_bat *g, mgdk_bat *e, mgdk_bat *h)
+{
+	if (b != nullptr && groups != nullptr && b->ttype == MGDK_str && b->tvheap != nullptr &&
+	    b->tvheapsize >= ELIMLIMIT) {
+		Cand ci;
+		if (cand_init(&ci, b, s) < 0)
+			return -1;
+		if (g && g->count != ci.n) {
+			seterr("b with s and g must be aligned\n");
+			return -1;
+		}
+		// the shortcuts of gdk_group.c:712-802 hold by content (tkey and
+		// the order properties of a str column are about its strings)
+		const bool trivial = b->tkey || ci.n <= 1 || (g && (g->tkey || g->ttype == MGDK_void));
+		const bool single = b->tsorted && b->trevsorted &&
+				    (!g || (mgdk_BATordered(g) && mgdk_BATordered_rev(g)));
+		if (!trivial && !single) {
+			ProfScope prof("group_str");
+			const int rc = group_str_content(groups, extents, histo, b, s, g, ci);
+			if (rc == 0 && !g && !e && !s)
+				b->tunique_est = (*groups)->tunique_est;
+			return rc;
+		}
+	}
+	return group_core(groups, extents, histo, b, s, g, e, h);
 }
 
 // BATunique (gdk/gdk_unique.c:30): the candidate list of the first

@@ -36,7 +36,8 @@ constexpr size_t ZERO_REGION = 65536;
 const void *zero_region();
 // per-thread 4 KiB device buffer for small results / arguments
 void *meta_buf();
-bool sync();                                // stream sync + error check
+bool sync();                                // stream sync + error check + query context
+bool sync_data();                           // stream sync + error check (data transfers)
 
 // ---- BAT heap ownership ---------------------------------------------------
 struct Heap {

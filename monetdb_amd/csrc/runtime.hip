@@ -100,16 +100,24 @@ qry_timed_out()
 	}
 }
 
+// stream drain of a data transfer (upload / download / a host read of one
+// value): the reference tests the query context only inside operator loops,
+// so a client can still read back or clean up after a timeout
 bool
-sync()
+sync_data()
 {
 	hipError_t e = hipStreamSynchronize(stream());
 	tctx.stage_used = 0;                // every staged upload has been read
 	if (e != hipSuccess)
 		return hip_ok(e, "hipStreamSynchronize");
-	if (!hip_ok(hipGetLastError(), "kernel launch"))
-		return false;
-	return !qry_timed_out();
+	return hip_ok(hipGetLastError(), "kernel launch");
+}
+
+// stream drain between an operator's launches: also tests the query context
+bool
+sync()
+{
+	return sync_data() && !qry_timed_out();
 }
 
 // ---- caching HBM allocator ---------------------------------------------------
@@ -240,7 +248,7 @@ stage_host(const void *src, size_t bytes)
 {
 	const size_t need = (bytes + 255) & ~(size_t) 255;
 	if (tctx.stage_used + need > tctx.stage_size) {
-		if (tctx.stage_used && !sync())
+		if (tctx.stage_used && !sync_data())
 			return nullptr;
 		if (need > tctx.stage_size) {
 			if (tctx.stage)
@@ -264,13 +272,19 @@ stage_host(const void *src, size_t bytes)
 const void *
 zero_region()
 {
-	static std::once_flag once;
-	static void *z = nullptr;
-	std::call_once(once, [] {
+	// created on first use; a failed allocation is retried by the next call
+	static std::mutex mu;
+	static void *volatile z = nullptr;
+	if (z != nullptr)
+		return z;
+	std::lock_guard<std::mutex> g(mu);
+	if (z == nullptr) {
 		void *p = dalloc(ZERO_REGION);
 		if (p && hipMemset(p, 0, ZERO_REGION) == hipSuccess && hipDeviceSynchronize() == hipSuccess)
 			z = p;
-	});
+		else
+			dfree(p);
+	}
 	if (z == nullptr)
 		seterr("HY013!could not allocate the zero region");
 	return z;
@@ -625,7 +639,7 @@ cand_index(const Cand &ci, oid o)
 	unsigned long long *m = (unsigned long long *) meta_buf();
 	unsigned long long *h = (unsigned long long *) pinned(64);
 	hipLaunchKernelGGL(k_cand_search, dim3(1), dim3(1), 0, stream(), ci.oids, ci.n, o, m);
-	if (!hip_ok(hipMemcpyAsync(h, m, 8, hipMemcpyDeviceToHost, stream()), "memcpy") || !sync())
+	if (!hip_ok(hipMemcpyAsync(h, m, 8, hipMemcpyDeviceToHost, stream()), "memcpy") || !sync_data())
 		return ~(BUN) 0;
 	return h[0];
 }
@@ -639,7 +653,7 @@ oid_at(const mgdk_bat *b, BUN p, oid *v)
 	}
 	oid *h = (oid *) pinned(64);
 	if (!hip_ok(hipMemcpyAsync(h, (const oid *) b->theap + p, 8, hipMemcpyDeviceToHost, stream()), "memcpy") ||
-	    !sync())
+	    !sync_data())
 		return -1;
 	*v = h[0];
 	return 0;
@@ -779,7 +793,7 @@ mgdk_GDKclrerr(void)
 int
 mgdk_sync(void)
 {
-	return sync() ? 0 : -1;
+	return sync_data() ? 0 : -1;
 }
 
 void *
@@ -981,7 +995,11 @@ mgdk_BATupload(mgdk_bat *b, const void *host, mgdk_BUN n)
 		      !hip_ok(hipMemcpyAsync(b->theap, src, bytes, hipMemcpyHostToDevice, stream()), "hipMemcpyAsync H2D")))
 		return -1;
 	b->count = n;
-	return sync() ? 0 : -1;
+	// the new values carry no known positions or estimates
+	b->tnosorted = b->tnorevsorted = 0;
+	b->tminpos = b->tmaxpos = MGDK_BUN_NONE;
+	b->tunique_est = 0;
+	return sync_data() ? 0 : -1;
 }
 
 int
@@ -997,7 +1015,7 @@ mgdk_BATdownload(const mgdk_bat *b, void *host)
 	if (bytes && !hip_ok(hipMemcpyAsync(host, b->theap, bytes, hipMemcpyDeviceToHost, stream()),
 			     "hipMemcpyAsync D2H"))
 		return -1;
-	return sync() ? 0 : -1;
+	return sync_data() ? 0 : -1;
 }
 
 int
@@ -1015,7 +1033,7 @@ mgdk_BATsetvheap(mgdk_bat *b, const void *host, uint64_t size)
 	p->tvheap = h;
 	b->tvheap = h->base;
 	b->tvheapsize = size;
-	return sync() ? 0 : -1;
+	return sync_data() ? 0 : -1;
 }
 
 int
@@ -1025,7 +1043,7 @@ mgdk_BATdownload_vheap(const mgdk_bat *b, void *host)
 		return 0;
 	if (!hip_ok(hipMemcpyAsync(host, b->tvheap, b->tvheapsize, hipMemcpyDeviceToHost, stream()), "vheap"))
 		return -1;
-	return sync() ? 0 : -1;
+	return sync_data() ? 0 : -1;
 }
 
 }  // extern "C"
@@ -1039,6 +1057,57 @@ k_fill_seq(oid *out, BUN n, oid seq)
 {
 	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
 		out[i] = seq == MGDK_OID_NIL ? MGDK_OID_NIL : seq + i;
+}
+
+// atomcmp of two values of base type bt (host), nil smallest as in GDK
+static int
+atom_cmp(int bt, const void *x, const void *y)
+{
+#define CMP3(T) { T a, c; memcpy(&a, x, sizeof(T)); memcpy(&c, y, sizeof(T)); return (a > c) - (a < c); }
+	switch (bt) {
+	case MGDK_bte: CMP3(int8_t)
+	case MGDK_sht: CMP3(int16_t)
+	case MGDK_int: CMP3(int32_t)
+	case MGDK_lng: CMP3(int64_t)
+	case MGDK_hge: CMP3(hge)
+	case MGDK_oid: {
+		oid a, c;
+		memcpy(&a, x, 8);
+		memcpy(&c, y, 8);
+		// oid_nil compares smallest (gdk_atoms.c oidCmp via lngCmp on the
+		// signed image)
+		return ((int64_t) a > (int64_t) c) - ((int64_t) a < (int64_t) c);
+	}
+	case MGDK_flt: {
+		float a, c;
+		memcpy(&a, x, 4);
+		memcpy(&c, y, 4);
+		return a != a ? -(c == c) : c != c ? 1 : (a > c) - (a < c);
+	}
+	case MGDK_dbl: {
+		double a, c;
+		memcpy(&a, x, 8);
+		memcpy(&c, y, 8);
+		return a != a ? -(c == c) : c != c ? 1 : (a > c) - (a < c);
+	}
+	default: CMP3(int64_t)
+	}
+#undef CMP3
+}
+
+// value at position p of a fixed-width column (host read; void: its oid)
+static bool
+value_at(const mgdk_bat *b, BUN p, void *out)
+{
+	if (b->ttype == MGDK_void) {
+		oid v = b->tseqbase == MGDK_OID_NIL ? MGDK_OID_NIL : b->tseqbase + p;
+		memcpy(out, &v, 8);
+		return true;
+	}
+	void *h = pinned(16);
+	return h && hip_ok(hipMemcpyAsync(h, (const char *) b->theap + p * (size_t) b->twidth, b->twidth,
+					  hipMemcpyDeviceToHost, stream()), "memcpy") && sync_data() &&
+	       memcpy(out, h, b->twidth);
 }
 
 extern "C" int
@@ -1078,6 +1147,36 @@ mgdk_BATappend(mgdk_bat *b, mgdk_bat *n, mgdk_bat *s, bool force)
 			seterr("Incompatible operands (%s vs. %s).\n", atomname(b->ttype), atomname(src->ttype));
 			goto out;
 		}
+	}
+	// the extremes' positions and the distinct-value estimate
+	// (gdk_batop.c:762-792): kept when the appended part's extreme is known
+	// and no candidate list renumbers it, else unknown
+	{
+		const int vt = basetype(b->ttype == MGDK_void ? MGDK_oid : b->ttype);
+		const BUN bc = b->count;
+		char x[16], y[16];
+		BUN *pos[2] = {&b->tmaxpos, &b->tminpos};
+		const BUN npos[2] = {n->tmaxpos, n->tminpos};
+		for (int k = 0; k < 2; k++) {
+			if (bc != 0 && *pos[k] == MGDK_BUN_NONE)
+				continue;
+			if (npos[k] == MGDK_BUN_NONE) {
+				*pos[k] = MGDK_BUN_NONE;
+				continue;
+			}
+			int c = -1;
+			if (bc != 0) {
+				if (!value_at(b, *pos[k], x) || !value_at(n, npos[k], y))
+					goto out;
+				c = atom_cmp(vt, x, y);
+				if (k == 1)
+					c = -c;
+			}
+			if (c < 0)
+				*pos[k] = s == nullptr ? bc + npos[k] : MGDK_BUN_NONE;
+		}
+		if (cnt > bc / 1000)   // GDK_UNIQUE_ESTIMATE_KEEP_FRACTION, gdk_private.h:439
+			b->tunique_est = 0;
 	}
 	// void + continuing dense sequence stays void
 	if (b->ttype == MGDK_void && src->ttype == MGDK_void &&

@@ -363,6 +363,12 @@ q6_ld(const int64_t *col, uint64_t chunk, uint64_t r, unsigned boff, bool live, 
 {
 	typedef long long l2 __attribute__((ext_vector_type(2)));
 	if constexpr (BUF) {
+		// dword3 0x00020000 is the gfx950 (CDNA3/4) descriptor layout whose
+		// range check returns zeros for the dead lanes' out-of-range offset;
+		// other families lay the word out differently
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__) && !defined(__gfx942__)
+#error "q6_ld<BUF>: buffer descriptor word 3 is laid out for gfx942 / gfx950 only"
+#endif
 		__amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *) (col + chunk * 256), (short) 0, 2048,
 									      0x00020000);
 		const q6u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, live ? boff : 0x80000000u, 0, 0);

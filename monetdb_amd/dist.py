@@ -495,7 +495,13 @@ def join_plan(be, dist, lkeys, rkeys, lrow0, rrow0):
     (gdk_join.c:4542-4618, no candidate lists, value columns) as (driving
     side, matches descending): ("l", False) selectjoin / mergejoin, ("r",
     False) their swapped forms, ("l", True) hashjoin, ("r", True) swapped
-    hashjoin; None when a side is empty."""
+    hashjoin; None when a side is empty.
+
+    The estimate is always taken from the 1000-value sample (guess_uniques):
+    single-node BATjoin uses a side's tunique_est instead when one is set
+    (e.g. by an earlier BATgroup on that column, joinalgo.hip / gdk_join.c
+    :3600-3620) and mergejoin_void for a dense side; the pairs' order then
+    equals the single-node result only for sides without those properties."""
     import math
     L = _side_stats(be, dist, be.widen(lkeys), lrow0)
     R = _side_stats(be, dist, be.widen(rkeys), rrow0)
@@ -641,5 +647,7 @@ def dist_window_bounds(be, dist, vals, parts, limit, preceding):
         be.append(p2, be.zeros_bit(be.n(rv)))
     kept_first = row0 + lead
     if be.n(v2) == 0:
-        return kept_first, v2
+        # no rows left: an empty lng column (widen's type), the type every
+        # other rank's bounds have
+        return kept_first, be.copy(be.slice(w, 0, 0))
     return kept_first, be.addcst(be.rangebounds(v2, p2, limit, preceding), kept_first)

@@ -241,12 +241,21 @@ class BAT:
         init()
         if tp == TYPE_hge:
             a = np.ascontiguousarray(arr, dtype=np.uint64).reshape(-1, 2)
+        elif tp == TYPE_str:
+            # heap offsets of 1, 2, 4 or 8 bytes (the width follows the array)
+            a = np.ascontiguousarray(arr)
+            if a.dtype not in (np.uint8, np.uint16, np.uint32, np.uint64):
+                a = a.astype(np.uint8)
         else:
             a = np.ascontiguousarray(arr, dtype=NP[tp])
         n = a.shape[0]
-        b = BAT(lib().mgdk_COLnew(hseqbase, tp, n))
+        ctp = {1: TYPE_bte, 2: TYPE_sht, 4: TYPE_int, 8: TYPE_lng}[a.dtype.itemsize] if tp == TYPE_str else tp
+        b = BAT(lib().mgdk_COLnew(hseqbase, ctp, n))
         _chk(lib().mgdk_BATupload(b.ptr, a.ctypes.data, n))
         s = b.ptr.contents
+        if tp == TYPE_str:
+            s.ttype = TYPE_str
+            s.twidth = a.dtype.itemsize
         if tp != TYPE_hge and tp != TYPE_str and n:
             flat = a
             isn = np.isnan(flat) if flat.dtype.kind == "f" else (flat == NIL[tp]) if tp in NIL else \
@@ -332,6 +341,8 @@ class BAT:
             return np.arange(s.tseqbase, s.tseqbase + n, dtype=np.uint64)
         if s.ttype == TYPE_hge:
             out = np.empty((n, 2), np.uint64)
+        elif s.ttype == TYPE_str:
+            out = np.empty(n, {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[s.twidth])
         else:
             out = np.empty(n, NP[s.ttype])
         if n:

@@ -92,8 +92,45 @@ typedef struct {
 	ora_hge key;
 	ora_oid g;
 	ora_oid gid;
+	uint64_t pos;      /* b position of the group's first row (str content) */
 	int used;
 } gslot;
+
+/* a str column whose heap is not duplicate eliminated (GDK_ELIMDOUBLES,
+ * gdk/gdk_atoms.h:373-375: heap free >= GDK_ELIMLIMIT = 64 KiB): BATgroup then
+ * compares string contents, not offsets (gdk/gdk_group.c:897-919, the hash
+ * path :1118-1282 with ATOMcompare = strCmp) */
+#define ORA_ELIMLIMIT ((uint64_t) 1 << 16)
+static bool
+str_by_content(const ora_bat *b)
+{
+	return b->type == ORA_str && b->vheap != NULL && b->vheapsize >= ORA_ELIMLIMIT;
+}
+
+/* the string of row p (VarHeapVal, gdk/gdk_atoms.h:421-436: 1- and 2-byte
+ * offsets are relative to GDK_VAROFFSET = 1024 * sizeof(var_t)) */
+static const char *
+str_of(const ora_bat *b, uint64_t p)
+{
+	const char *x = (const char *) b->base + p * b->width;
+	uint64_t o;
+	switch (b->width) {
+	case 1: o = *(const uint8_t *) x + 8192u; break;
+	case 2: o = *(const uint16_t *) x + 8192u; break;
+	case 4: o = *(const uint32_t *) x; break;
+	default: o = *(const uint64_t *) x; break;
+	}
+	return b->vheap + o;
+}
+
+static uint64_t
+str_hash(const char *s)
+{
+	uint64_t h = 0xcbf29ce484222325ULL;   /* FNV-1a over the bytes */
+	for (; *s; s++)
+		h = (h ^ (uint8_t) *s) * 0x100000001b3ULL;
+	return h;
+}
 
 static uint64_t
 ghash(ora_hge k, ora_oid g)
@@ -188,19 +225,26 @@ ora_group(ora_bat **groups, ora_bat **extents, ora_bat **histo,
 	ora_oid *gids = gn->base, *ext = en->base;
 	int64_t *cnt = hn->base;
 	uint64_t ngrp = 0, maxgrppos = ORA_BUN_NONE;
+	const bool content = str_by_content(b);
 	for (uint64_t i = 0; i < ci.n; i++) {
 		ora_oid o = ci_get(&ci, i);
+		const uint64_t p = o - b->hseqbase;
 		ora_hge v;
-		(void) grp_key(b, o - b->hseqbase, &v);
+		if (content)
+			v = (ora_hge) str_hash(str_of(b, p));   /* equal strings, equal keys */
+		else
+			(void) grp_key(b, p, &v);
 		ora_oid gg = 0;
 		if (g)
 			gg = g->type == ORA_void ? g->tseqbase + i : ((const ora_oid *) g->base)[i];
 		uint64_t h = ghash(v, gg) & (cap - 1);
-		while (tab[h].used && !(tab[h].key == v && tab[h].g == gg))
+		while (tab[h].used && !(tab[h].key == v && tab[h].g == gg &&
+					(!content || strcmp(str_of(b, tab[h].pos), str_of(b, p)) == 0)))
 			h = (h + 1) & (cap - 1);
 		if (!tab[h].used) {
 			tab[h].used = 1;
 			tab[h].key = v;
+			tab[h].pos = p;
 			tab[h].g = gg;
 			tab[h].gid = ngrp;
 			ext[ngrp] = o;

@@ -149,12 +149,17 @@ class Bat:
                    nonil=False, vheap=None, tseqbase=OID_NIL, unique_est=0.0):
         if tp == TYPE_hge:
             a = np.ascontiguousarray(arr, dtype=np.uint64).reshape(-1, 2)
+        elif tp == TYPE_str:
+            # heap offsets of 1, 2, 4 or 8 bytes (the width follows the array)
+            a = np.ascontiguousarray(arr)
+            if a.dtype not in (np.uint8, np.uint16, np.uint32, np.uint64):
+                a = a.astype(np.uint8)
         else:
             a = np.ascontiguousarray(arr, dtype=NP[tp])
         n = a.shape[0]
         b = OraBat()
         b.type = tp
-        b.width = 16 if tp == TYPE_hge else (1 if tp == TYPE_str else a.dtype.itemsize)
+        b.width = 16 if tp == TYPE_hge else a.dtype.itemsize
         b.count = n
         b.hseqbase = hseqbase
         b.tseqbase = tseqbase

@@ -68,6 +68,40 @@ def test_append(gdk, tname, dt):
         gdk.BATappend(b, gdk.BAT.from_numpy(gdk.TYPE_dbl, np.zeros(3)))
 
 
+def test_append_keeps_extreme_positions(gdk, ora):
+    """BATappend maintains tmaxpos / tminpos / tunique_est
+    (gdk_batop.c:762-792).  BATgroup reads g's tmaxpos for the largest prior
+    group id: a group-id column that grew larger ids by an append must be
+    regrouped with those ids, exactly as the oracle does."""
+    r = rng(204)
+    v = r.integers(0, 4, 20_000).astype(np.int32)
+    g, _, _ = gdk.BATgroup(gdk.BAT.from_numpy(gdk.TYPE_int, v))
+    assert g.s.tmaxpos != (1 << 63) - 1
+    more = r.integers(4, 60, 5_000).astype(np.uint64)          # larger ids
+    gdk.BATappend(g, gdk.BAT.from_numpy(gdk.TYPE_oid, more))
+    gids = g.to_numpy()
+    mp = g.s.tmaxpos
+    assert mp == (1 << 63) - 1 or gids[mp] == gids.max()
+    assert g.s.tunique_est == 0
+    w = r.integers(0, 3, len(gids)).astype(np.int8)
+    gd, ed, hd = gdk.BATgroup(gdk.BAT.from_numpy(gdk.TYPE_bte, w), None, g)
+    og, oe, oh = ora.BATgroup(ora.Bat.from_array(ora.TYPE_bte, w),
+                              None, ora.Bat.from_array(ora.TYPE_oid, gids))
+    assert np.array_equal(gd.to_numpy(), og.values())
+    assert np.array_equal(ed.to_numpy(), oe.values())
+    assert np.array_equal(hd.to_numpy(), oh.values())
+    # a value known to be the maximum: its position moves with the append
+    b = gdk.BAT.from_numpy(gdk.TYPE_lng, np.array([5, 9, 1], np.int64))
+    b.s.tmaxpos, b.s.tminpos = 1, 2
+    n = gdk.BAT.from_numpy(gdk.TYPE_lng, np.array([3, 12, 0, 2], np.int64))
+    n.s.tmaxpos, n.s.tminpos = 1, 2
+    gdk.BATappend(b, n)
+    assert (b.s.tmaxpos, b.s.tminpos) == (4, 5)
+    n2 = gdk.BAT.from_numpy(gdk.TYPE_lng, np.array([4], np.int64))   # extremes unknown
+    gdk.BATappend(b, n2)
+    assert b.s.tmaxpos == b.s.tminpos == (1 << 63) - 1
+
+
 def test_append_void(gdk):
     v = gdk.BAT.dense(10, 5)
     gdk.BATappend(v, gdk.BAT.dense(15, 3))                          # continues: stays dense

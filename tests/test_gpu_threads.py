@@ -102,6 +102,10 @@ def test_qry_ctx_timeout(gdk):
         with pytest.raises(gdk.GDKError, match="Timeout was reached!"):
             gdk.BATthetaselect(b, None, 10, "<")
         assert ctx.endtime == gdk.QRY_TIMEOUT
+        # data transfers still work after the timeout (the reference tests
+        # the context only inside operator loops): read back, upload
+        assert b.to_numpy()[5] == 5
+        assert gdk.BAT.from_numpy(gdk.TYPE_int, np.arange(10, dtype=np.int32)).to_numpy()[9] == 9
         # another thread without a context runs normally meanwhile
         out = []
         t = threading.Thread(target=lambda: out.append(gdk.BATthetaselect(b, None, 10, "<").count()))
