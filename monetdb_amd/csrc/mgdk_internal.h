@@ -5,6 +5,8 @@
 
 #include <cstdint>
 #include <cstring>
+#include <utility>
+#include <vector>
 
 #include "../../include/mgdk.h"
 
@@ -145,6 +147,10 @@ int exclusive_scan(const uint8_t *in, uint64_t *out, BUN n, uint64_t *total);
 // Returns the buffers holding the result (the input pair or the spare).
 int radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32_t *vals_alt,
 		     BUN n, int bits, uint64_t **keys_out, uint32_t **vals_out);
+
+// GDKqsort's permutation (qsort.hip) of every segment (start, len) of the
+// rows (rank, pay): ranks are the rows' dense ranks in the requested order
+int qsort_replay(uint32_t *rank, uint64_t *pay, BUN n, const std::vector<std::pair<uint64_t, uint32_t>> &segs);
 
 // stable sort of the positions 0..n-1 by 32-bit keys (sort.hip); when no
 // pass is needed (all keys equal) *perm is left NULL: identity

@@ -1006,10 +1006,14 @@ radix_sort_positions32(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, uint3
 
 }  // namespace mgdk
 
-// BATsort of a str column through its chunk keys (see k_str_chunk)
+static int sort_core(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b, mgdk_bat *o,
+		     mgdk_bat *g, bool reverse, bool nilslast);
+
+// stable BATsort of a str column through its chunk keys (see k_str_chunk):
+// each chunk sub-sorts the runs of equal prefixes stably
 static int
 sort_str(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b, mgdk_bat *o, mgdk_bat *g,
-	 bool reverse, bool nilslast, bool stable)
+	 bool reverse, bool nilslast)
 {
 	const BUN n = b->count;
 	hipStream_t st = stream();
@@ -1040,7 +1044,7 @@ sort_str(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b, mg
 		key->tnil = b->tnil;
 		const bool wantg = k + 1 < nch || groups != nullptr;
 		on = gn = nullptr;
-		rc = mgdk_BATsort(nullptr, &on, wantg ? &gn : nullptr, key, co, cg, reverse, nilslast, stable);
+		rc = sort_core(nullptr, &on, wantg ? &gn : nullptr, key, co, cg, reverse, nilslast);
 		mgdk_BBPunfix(key);
 		if (co != o)
 			mgdk_BBPunfix(co);
@@ -1076,36 +1080,15 @@ sort_str(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b, mg
 	return 0;
 }
 
-extern "C" int
-mgdk_BATsort(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b, mgdk_bat *o, mgdk_bat *g,
-	     bool reverse, bool nilslast, bool stable)
+// the stable sort: sorted values, order oids and group ids of b rearranged
+// by o and sorted within the runs of g (ties in input order)
+static int
+sort_core(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b, mgdk_bat *o, mgdk_bat *g,
+	  bool reverse, bool nilslast)
 {
-	if (b == nullptr) {
-		seterr("b must exist\n");
-		return -1;
-	}
-	if (stable && reverse != nilslast) {
-		seterr("stable sort cannot have reverse != nilslast\n");
-		return -1;
-	}
-	if (o != nullptr && (basetype(o->ttype) != MGDK_oid && o->ttype != MGDK_void)) {
-		seterr("o must have type oid and same size as b\n");
-		return -1;
-	}
-	if (o != nullptr && (o->count != b->count || (o->ttype == MGDK_void && o->count && o->tseqbase == MGDK_OID_NIL))) {
-		seterr("o must have type oid and same size as b\n");
-		return -1;
-	}
-	if (g != nullptr && ((basetype(g->ttype) != MGDK_oid && g->ttype != MGDK_void) || !g->tsorted ||
-			     g->count != b->count || (g->ttype == MGDK_void && g->count && g->tseqbase == MGDK_OID_NIL))) {
-		seterr("g must have type oid, sorted on the tail, and same size as b\n");
-		return -1;
-	}
-	if (g == nullptr && !stable)
-		o = nullptr;        // pre-ordering is meaningless for an unstable full sort
 	if (b->ttype == MGDK_str) {
 		ProfScope prof("sort");
-		return sort_str(sorted, order, groups, b, o, g, reverse, nilslast, stable);
+		return sort_str(sorted, order, groups, b, o, g, reverse, nilslast);
 	}
 	const int tt = basetype(b->ttype);
 	if (!(tt == MGDK_bte || tt == MGDK_sht || tt == MGDK_int || tt == MGDK_lng || tt == MGDK_oid ||
@@ -1248,6 +1231,368 @@ mgdk_BATsort(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b
 			on->tkey = 1;
 			on->tnonil = 1;
 			on->tsorted = on->trevsorted = 0;   // gdk_batop.c:2622-2624
+		}
+	}
+done:
+	if (sorted) *sorted = sn; else mgdk_BBPunfix(sn);
+	if (order) *order = on; else mgdk_BBPunfix(on);
+	if (groups) *groups = gn; else mgdk_BBPunfix(gn);
+	return 0;
+fail:
+	mgdk_BBPunfix(sn);
+	mgdk_BBPunfix(on);
+	mgdk_BBPunfix(gn);
+	return -1;
+}
+
+// ---- BATsort (gdk/gdk_batop.c:2342-2827): the reference's control flow ----
+// around the stable engine above, and GDKqsort's order of equal values
+// (qsort.hip) wherever do_sort (gdk_batop.c:2266-2304) picks the quicksort:
+// an unstable sort of a type the radix sort does not take (bit, oid, flt,
+// dbl, str), of nils at the unnatural end (reverse != nilslast), or of a run
+// of at most 100 rows.
+namespace {
+
+struct OSrc {
+	const oid *p;
+	oid seq;
+	__device__ __forceinline__ oid at(BUN i) const { return p ? p[i] : seq + i; }
+};
+
+OSrc
+osrc(const mgdk_bat *b)
+{
+	return OSrc{b && b->ttype != MGDK_void ? (const oid *) b->theap : nullptr, b ? b->tseqbase : 0};
+}
+
+__global__ __launch_bounds__(256) void
+k_qs_ranks(BUN n, OSrc order1, oid h0, OSrc grp1, uint32_t *rank)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
+		rank[order1.at(i) - h0] = (uint32_t) grp1.at(i);
+}
+
+__global__ __launch_bounds__(256) void
+k_qs_pay(BUN n, OSrc o, bool has_o, oid hseq, uint64_t *pay)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
+		pay[i] = has_o ? o.at(i) : hseq + i;
+}
+
+__global__ __launch_bounds__(256) void
+k_run_starts(BUN n, OSrc g, int8_t *fl)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
+		fl[i] = i == 0 || g.at(i) != g.at(i - 1);
+}
+
+__global__ __launch_bounds__(256) void
+k_qs_mark_runs(const uint64_t *st, const uint32_t *len, uint32_t nseg, uint8_t *mark)
+{
+	const uint32_t k = blockIdx.x;
+	if (k >= nseg)
+		return;
+	for (uint32_t i = threadIdx.x; i < len[k]; i += blockDim.x)
+		mark[st[k] + i] = 1;
+}
+
+// order oids: the replayed payload in quicksort runs, the stable order
+// (through o) elsewhere
+__global__ __launch_bounds__(256) void
+k_qs_order(BUN n, const uint8_t *mark, const uint64_t *pay, OSrc order1, oid h0, OSrc o, bool has_o, oid hseq,
+	   oid *out)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		if (mark[i]) {
+			out[i] = pay[i];
+		} else {
+			const oid p = order1.at(i) - h0;
+			out[i] = has_o ? o.at(p) : hseq + p;
+		}
+	}
+}
+
+__global__ __launch_bounds__(256) void
+k_seq_oids(BUN n, oid hseq, oid *out)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
+		out[i] = hseq + i;
+}
+
+bool
+radix_type(int tt)
+{
+	switch (tt) {
+	case MGDK_bte: case MGDK_sht: case MGDK_int: case MGDK_lng: case MGDK_hge:
+	case MGDK_date: case MGDK_daytime: case MGDK_timestamp:
+		return true;
+	default:
+		return false;   // bit, oid, flt, dbl, str: GDKssort / GDKqsort
+	}
+}
+
+// runs of equal consecutive g (the sub-sorts of gdk_batop.c:2687-2711) as
+// (start, length); whole column without g
+int
+sort_runs(const mgdk_bat *g, BUN n, std::vector<std::pair<uint64_t, uint32_t>> &runs)
+{
+	runs.clear();
+	if (n == 0)
+		return 0;
+	if (g == nullptr) {
+		runs.emplace_back(0, (uint32_t) n);
+		return 0;
+	}
+	DevBuf fl(n + 8);
+	if (!fl.p)
+		return -1;
+	hipLaunchKernelGGL(k_run_starts, dim3(grid_for(n, 1024, 8192)), dim3(256), 0, stream(), n, osrc(g),
+			   fl.as<int8_t>());
+	mgdk_bat *S = compact_flags(fl.as<int8_t>(), n, 0);
+	if (S == nullptr)
+		return -1;
+	std::vector<oid> st(S->count);
+	const int rc = mgdk_BATdownload(S, st.data());
+	mgdk_BBPunfix(S);
+	if (rc < 0)
+		return -1;
+	for (size_t k = 0; k < st.size(); k++)
+		runs.emplace_back(st[k], (uint32_t) ((k + 1 < st.size() ? st[k + 1] : n) - st[k]));
+	return 0;
+}
+
+// a materialised order column hseq, hseq + 1, ... (gdk_batop.c:2611-2620)
+mgdk_bat *
+seq_order(oid hseq, BUN n)
+{
+	mgdk_bat *on = newbat(hseq, MGDK_oid, n);
+	if (on == nullptr)
+		return nullptr;
+	if (n)
+		hipLaunchKernelGGL(k_seq_oids, dim3(grid_for(n, 1024, 8192)), dim3(256), 0, stream(), n, hseq,
+				   (oid *) on->theap);
+	if (!sync()) {
+		mgdk_BBPunfix(on);
+		return nullptr;
+	}
+	on->count = n;
+	on->tkey = on->tnonil = 1;
+	on->tsorted = 1;
+	on->trevsorted = n <= 1;
+	return on;
+}
+
+// GDKqsort's order for the quicksort runs: stable-sort b (rearranged by o)
+// for the ranks, replay the quicksort on those runs, keep the stable order
+// in the others
+int
+sort_qsort(mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b, mgdk_bat *o, mgdk_bat *g, bool reverse,
+	   bool nilslast, const std::vector<std::pair<uint64_t, uint32_t>> &qruns)
+{
+	const BUN n = b->count;
+	hipStream_t st = stream();
+	mgdk_bat *bn = o ? mgdk_BATproject(o, b) : b;
+	if (bn == nullptr)
+		return -1;
+	mgdk_bat *o1 = nullptr, *g1 = nullptr, *on = nullptr;
+	int rc = -1;
+	{
+		if (sort_core(nullptr, &o1, &g1, bn, nullptr, g, reverse, nilslast) < 0)
+			goto out;
+		DevBuf rank(n * 4 + 4), pay(n * 8 + 8), mark(n + 8);
+		if (!rank.p || !pay.p || !mark.p)
+			goto out;
+		const dim3 grd(grid_for(n, 1024, 8192)), blk(256);
+		hipLaunchKernelGGL(k_qs_ranks, grd, blk, 0, st, n, osrc(o1), bn->hseqbase, osrc(g1), rank.as<uint32_t>());
+		hipLaunchKernelGGL(k_qs_pay, grd, blk, 0, st, n, osrc(o), o != nullptr, b->hseqbase, pay.as<uint64_t>());
+		if (qsort_replay(rank.as<uint32_t>(), pay.as<uint64_t>(), n, qruns) < 0)
+			goto out;
+		// mark the replayed runs
+		if (!hip_ok(hipMemsetAsync(mark.p, 0, n, st), "memset"))
+			goto out;
+		if (!qruns.empty()) {
+			std::vector<uint64_t> hs(qruns.size());
+			std::vector<uint32_t> hl(qruns.size());
+			for (size_t k = 0; k < qruns.size(); k++) {
+				hs[k] = qruns[k].first;
+				hl[k] = qruns[k].second;
+			}
+			DevBuf ds(hs.size() * 8), dl(hl.size() * 4);
+			if (!ds.p || !dl.p ||
+			    !hip_ok(hipMemcpyAsync(ds.p, hs.data(), hs.size() * 8, hipMemcpyHostToDevice, st), "memcpy") ||
+			    !hip_ok(hipMemcpyAsync(dl.p, hl.data(), hl.size() * 4, hipMemcpyHostToDevice, st), "memcpy"))
+				goto out;
+			hipLaunchKernelGGL(k_qs_mark_runs, dim3((unsigned) qruns.size()), dim3(256), 0, st, ds.as<uint64_t>(),
+					   dl.as<uint32_t>(), (uint32_t) qruns.size(), mark.as<uint8_t>());
+			if (!sync())
+				goto out;
+		}
+		on = newbat(b->hseqbase, MGDK_oid, n);
+		if (on == nullptr)
+			goto out;
+		hipLaunchKernelGGL(k_qs_order, grd, blk, 0, st, n, mark.as<uint8_t>(), pay.as<uint64_t>(), osrc(o1),
+				   bn->hseqbase, osrc(o), o != nullptr, b->hseqbase, (oid *) on->theap);
+		if (!sync())
+			goto out;
+		on->count = n;
+		on->tkey = o ? o->tkey : 1;
+		on->tnonil = 1;
+		on->tsorted = on->trevsorted = 0;
+		*order = on;
+		on = nullptr;
+		if (groups) {
+			*groups = g1;
+			g1 = nullptr;
+		}
+		rc = 0;
+	}
+out:
+	if (bn != b)
+		mgdk_BBPunfix(bn);
+	mgdk_BBPunfix(o1);
+	mgdk_BBPunfix(g1);
+	mgdk_BBPunfix(on);
+	return rc;
+}
+
+}  // namespace
+
+extern "C" int
+mgdk_BATsort(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b, mgdk_bat *o, mgdk_bat *g,
+	     bool reverse, bool nilslast, bool stable)
+{
+	if (sorted) *sorted = nullptr;
+	if (order) *order = nullptr;
+	if (groups) *groups = nullptr;
+	if (b == nullptr) {
+		seterr("b must exist\n");
+		return -1;
+	}
+	if (stable && reverse != nilslast) {
+		seterr("stable sort cannot have reverse != nilslast\n");
+		return -1;
+	}
+	const BUN n = b->count;
+	if (b->ttype == MGDK_void) {
+		b->tsorted = 1;
+		b->trevsorted = b->tseqbase == MGDK_OID_NIL || n <= 1;
+		b->tkey = b->tseqbase != MGDK_OID_NIL || n <= 1;
+	} else if (n <= 1) {
+		b->tsorted = b->trevsorted = 1;
+	}
+	if (o != nullptr && ((basetype(o->ttype) != MGDK_oid && o->ttype != MGDK_void) || o->count != n ||
+			     (o->ttype == MGDK_void && o->count && o->tseqbase == MGDK_OID_NIL))) {
+		seterr("o must have type oid and same size as b\n");
+		return -1;
+	}
+	if (g != nullptr && ((basetype(g->ttype) != MGDK_oid && g->ttype != MGDK_void) || !g->tsorted ||
+			     g->count != n || (g->ttype == MGDK_void && g->count && g->tseqbase == MGDK_OID_NIL))) {
+		seterr("g must have type oid, sorted on the tail, and same size as b\n");
+		return -1;
+	}
+	if (sorted == nullptr && order == nullptr) {
+		seterr("no place to put the result.\n");
+		return -1;
+	}
+	if (n >= ((BUN) 1 << 32)) {
+		seterr("42000!BATsort: more than 2^32 rows");
+		return -1;
+	}
+	if (g == nullptr && !stable)
+		o = nullptr;        // pre-ordering is meaningless for an unstable full sort (:2410-2414)
+	if (b->tnonil)
+		nilslast = reverse;  // no nils: their placement does not matter (:2415-2420)
+	ProfScope prof("BATsort");
+	mgdk_bat *sn = nullptr, *on = nullptr, *gn = nullptr;
+	// trivially (sub)sorted (:2422-2472)
+	if (n <= 1 || (reverse == nilslast && (reverse ? b->trevsorted : b->tsorted) && o == nullptr && g == nullptr &&
+		       (groups == nullptr || b->tkey || (reverse ? b->tsorted : b->trevsorted)))) {
+		if (sorted && (sn = mgdk_BATslice(b, 0, n)) == nullptr)
+			goto fail;
+		if (order && (on = mgdk_BATdense(b->hseqbase, b->hseqbase, n)) == nullptr)
+			goto fail;
+		if (groups) {
+			oid zero = 0;
+			gn = b->tkey ? mgdk_BATdense(b->hseqbase, 0, n) : mgdk_BATconstant(b->hseqbase, MGDK_oid, &zero, n);
+			if (gn == nullptr)
+				goto fail;
+		}
+		goto done;
+	}
+	// every group a single row: nothing to sort (:2633-2686)
+	if (g && (g->tkey || g->ttype == MGDK_void)) {
+		if (sorted && (sn = o ? mgdk_BATproject(o, b) : mgdk_BATslice(b, 0, n)) == nullptr)
+			goto fail;
+		if (order) {
+			if (o) {
+				on = mgdk_BATslice(o, 0, n);
+				if (on == nullptr)
+					goto fail;
+				on->hseqbase = b->hseqbase;
+				on->tsorted = o->tsorted;
+				on->trevsorted = o->trevsorted;
+			} else if ((on = seq_order(b->hseqbase, n)) == nullptr) {
+				goto fail;
+			}
+			if (n <= 1)
+				on->tsorted = on->trevsorted = 1;
+		}
+		if (groups) {
+			gn = mgdk_BATslice(g, 0, n);
+			if (gn == nullptr)
+				goto fail;
+		}
+		goto done;
+	}
+	{
+		// the runs do_sort sorts with GDKqsort
+		std::vector<std::pair<uint64_t, uint32_t>> runs, qruns;
+		bool single_run = g == nullptr;
+		if (!stable) {
+			const bool rx = radix_type(b->ttype);
+			if (sort_runs(g, n, runs) < 0)
+				goto fail;
+			single_run = runs.size() <= 1;
+			for (auto &r : runs)
+				if (r.second > 1 && (!rx || reverse != nilslast || r.second <= 100))
+					qruns.push_back(r);
+			// without g, a column already in the requested order is left as it
+			// is (:2735-2736)
+			if (g == nullptr && reverse == nilslast && (reverse ? b->trevsorted : b->tsorted))
+				qruns.clear();
+		} else if (g) {
+			single_run = mgdk_BATordered_rev(g);
+		}
+		if (!qruns.empty()) {
+			if (sort_qsort(&on, groups ? &gn : nullptr, b, o, g, reverse, nilslast, qruns) < 0)
+				goto fail;
+			if (sorted && (sn = mgdk_BATproject(on, b)) == nullptr)
+				goto fail;
+			if (!order) {
+				mgdk_BBPunfix(on);
+				on = nullptr;
+			}
+		} else {
+			if (sort_core(sorted ? &sn : nullptr, &on, groups ? &gn : nullptr, b, o, g, reverse, nilslast) < 0)
+				goto fail;
+			if (!order) {
+				mgdk_BBPunfix(on);
+				on = nullptr;
+			}
+		}
+		if (sn) {
+			// gdk_batop.c:2712-2715, 2749-2750, 2772-2776
+			sn->tsorted = single_run && !reverse && !nilslast;
+			sn->trevsorted = single_run && reverse && nilslast;
+			if (n <= 1)
+				sn->tsorted = sn->trevsorted = 1;
+			sn->tkey = o ? (o->tkey && b->tkey) : b->tkey;
+			sn->tnonil = b->tnonil;
+			sn->tnil = b->tnil;
+			sn->tnosorted = sn->tnorevsorted = 0;
+			sn->tminpos = sn->tmaxpos = MGDK_BUN_NONE;
+			if (gn && gn->tkey && (g == nullptr || (g->tsorted && g->trevsorted)))
+				sn->tkey = 1;
 		}
 	}
 done:

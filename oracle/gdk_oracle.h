@@ -21,7 +21,8 @@
  *   group       gdk/gdk_group.c:657-1347 (first-occurrence numbering)
  *   join        gdk/gdk_join.c:4451-4623 (BATjoin: algorithm choice, result
  *               order and properties; gdk_oracle_join.c)
- *   sort        gdk/gdk_batop.c:2266-2342, gdk/gdk_rsort.c:21 (stable)
+ *   sort        gdk/gdk_batop.c:2266-2827 (BATsort, do_sort), gdk/gdk_rsort.c:21 (stable),
+ *               gdk/gdk_qsort.c + gdk_qsort_impl.h (GDKqsort; gdk_oracle_sort.c)
  *   window      gdk/gdk_analytic_bounds.c:187-587, :855-1440 (gdk_oracle_bounds.c)
  *   frames      gdk/gdk_analytic_func.c:1626 (count), :1959 (sum),
  *               gdk/gdk_analytic_statistics.c:364 (avg), :428-700 (avginteger), segment
@@ -103,6 +104,11 @@ ora_bat *ora_calcdivmod(char op, const ora_bat *b1, const void *c1, int t1, cons
 			const void *c2, int t2, const ora_bat *s1, const ora_bat *s2, int tp);
 int ora_sum(void *res, int tp, const ora_bat *b, const ora_bat *s,
 	    bool skip_nils, bool nil_if_empty);
+/* BATsort (gdk/gdk_batop.c:2342) with do_sort's choice per run: stable sorts
+ * and an exact restatement of GDKqsort (gdk_oracle_sort.c) */
+int ora_BATsort(ora_bat **sorted, ora_bat **order, ora_bat **groups, ora_bat *b, const ora_bat *o,
+		const ora_bat *g, bool reverse, bool nilslast, bool stable);
+void ora_GDKqsort(const ora_bat *v, uint64_t *h, ora_oid *t, uint64_t n, bool reverse, bool nilslast);
 int ora_group(ora_bat **groups, ora_bat **extents, ora_bat **histo,
 	      ora_bat *b, const ora_bat *s, const ora_bat *g);
 ora_bat *ora_groupsum(const ora_bat *b, const ora_bat *g, const ora_bat *e,
@@ -123,8 +129,6 @@ ora_bat *ora_groupminmax(const ora_bat *b, const ora_bat *g, const ora_bat *e,
 int ora_join(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r,
 	     const ora_bat *sl, const ora_bat *sr, bool nil_matches);
 int ora_join_algo(ora_bat *l, ora_bat *r, const ora_bat *sl, const ora_bat *sr);
-int ora_sort(ora_bat **sorted, ora_bat **order, const ora_bat *b,
-	     bool reverse, bool nilslast);
 /* GDKanalyticalwindowbounds, all units / types (gdk_oracle_bounds.c);
  * r is caller-allocated with count(b) oid slots */
 int ora_windowbounds(ora_bat *r, const ora_bat *b, const ora_bat *p, const ora_bat *l, const void *bound,

@@ -920,69 +920,6 @@ ora_groupminmax(const ora_bat *b, const ora_bat *g, const ora_bat *e,
 
 /* ---------------------------------------------------------------------- */
 
-/* ---------------------------------------------------------------------- */
-/* BATsort (gdk/gdk_batop.c:2342, do_sort :2266-2304): integer keys with
- * nilslast == reverse are sorted by the stable LSD radix sort GDKrsort
- * (gdk/gdk_rsort.c:21); nil (the type minimum) sorts first ascending and
- * last descending; equal keys keep input order.  order holds the oids. */
-typedef struct {
-	ora_hge k;
-	uint64_t i;
-} skey;
-
-static int reverse_cmp;
-
-static int
-skey_cmp(const void *x, const void *y)
-{
-	const skey *a = x, *b = y;
-	if (a->k != b->k)
-		return reverse_cmp ? (a->k < b->k ? 1 : -1) : (a->k < b->k ? -1 : 1);
-	return a->i < b->i ? -1 : a->i > b->i;
-}
-
-int
-ora_sort(ora_bat **sorted, ora_bat **order, const ora_bat *b,
-	 bool reverse, bool nilslast)
-{
-	if (reverse != nilslast) {
-		ora_seterr("stable sort cannot have reverse != nilslast\n");
-		return -1;
-	}
-	uint64_t n = b->count;
-	skey *k = malloc((n + 1) * sizeof(skey));
-	for (uint64_t i = 0; i < n; i++) {
-		(void) val_at(b, i, &k[i].k);
-		k[i].i = i;
-	}
-	reverse_cmp = reverse;
-	qsort(k, n, sizeof(skey), skey_cmp);
-	ora_bat *sn = ora_new(b->type == ORA_void ? ORA_oid : b->type, n, b->hseqbase);
-	ora_bat *on = ora_new(ORA_oid, n, b->hseqbase);
-	for (uint64_t i = 0; i < n; i++) {
-		memcpy((char *) sn->base + i * sn->width,
-		       b->type == ORA_void ? (const void *) &(ora_oid){b->tseqbase + k[i].i}
-		       : (const char *) b->base + k[i].i * b->width, sn->width);
-		((ora_oid *) on->base)[i] = b->hseqbase + k[i].i;
-	}
-	free(k);
-	/* sorted: a copy of b (COLcopy keeps key / nil / nonil) flagged
-	 * (rev)sorted; order: key, no nils, flagged unordered
-	 * (gdk_batop.c:2610-2630, 2749-2750) */
-	sn->sorted = !reverse;
-	sn->revsorted = reverse;
-	sn->key = b->key;
-	sn->nil = b->nil;
-	sn->nonil = b->nonil;
-	on->key = on->nonil = 1;
-	on->nil = on->sorted = on->revsorted = 0;
-	*sorted = sn;
-	if (order)
-		*order = on;
-	else
-		ora_free(on);
-	return 0;
-}
 
 /* ---------------------------------------------------------------------- */
 /* RANGE frame bounds (gdk/gdk_analytic_bounds.c:994-1294, kernels

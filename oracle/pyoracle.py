@@ -99,7 +99,9 @@ def lib():
         L.ora_groupavg3.argtypes = [C.POINTER(P), C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool]
         L.ora_join.argtypes = [C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool]
         L.ora_join_algo.argtypes = [P, P, P, P]
-        L.ora_sort.argtypes = [C.POINTER(P), C.POINTER(P), P, C.c_bool, C.c_bool]
+        L.ora_BATsort.argtypes = [C.POINTER(P), C.POINTER(P), C.POINTER(P), P, P, P, C.c_bool, C.c_bool,
+                                  C.c_bool]
+        L.ora_GDKqsort.argtypes = [P, C.c_void_p, C.c_void_p, C.c_uint64, C.c_bool, C.c_bool]
         L.ora_firstn.restype = P
         L.ora_firstn.argtypes = [P, P, P, C.c_uint64, C.c_bool, C.c_bool]
         L.ora_windowbounds.argtypes = [P, P, P, P, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_bool,
@@ -376,11 +378,34 @@ def props(b):
                 key=bool(s.key), nonil=bool(s.nonil), nil=bool(s.nil))
 
 
-def BATsort(b, reverse=False, nilslast=False):
-    a, o = P(), P()
-    if lib().ora_sort(C.byref(a), C.byref(o), b.ptr, reverse, nilslast) < 0:
+def BATsort(b, reverse=False, nilslast=False, stable=None):
+    """(sorted, order) of BATsort without o / g; stable unless the nil
+    placement asks for an unstable sort (reverse != nilslast)"""
+    s, o, _ = BATsort_full(b, reverse=reverse, nilslast=nilslast,
+                           stable=(reverse == nilslast) if stable is None else stable, want_groups=False)
+    return s, o
+
+
+def BATsort_full(b, o=None, g=None, reverse=False, nilslast=False, stable=True, want_groups=True):
+    """BATsort(&sorted, &order, &groups, b, o, g, reverse, nilslast, stable)
+    (gdk/gdk_batop.c:2342) with do_sort's choice per run, GDKqsort included
+    (gdk_oracle_sort.c).  Returns (sorted, order, groups or None)."""
+    a, od, gp = P(), P(), P()
+    if lib().ora_BATsort(C.byref(a), C.byref(od), C.byref(gp) if want_groups else None, b.ptr,
+                         o.ptr if o else None, g.ptr if g else None, reverse, nilslast, stable) < 0:
         raise _err()
-    return Bat(a), Bat(o)
+    return Bat(a), Bat(od), (Bat(gp) if want_groups else None)
+
+
+def GDKqsort(b, reverse=False, nilslast=False):
+    """GDKqsort (gdk/gdk_qsort.c:358) of b's values with positions as payload:
+    returns the permutation (positions in sorted order)."""
+    n = b.s.count
+    h = np.arange(n, dtype=np.uint64)
+    t = np.arange(n, dtype=np.uint64)
+    lib().ora_GDKqsort(b.ptr, h.ctypes.data, t.ctypes.data, n, reverse, nilslast)
+    assert np.array_equal(h, t)
+    return h
 
 
 def BATfirstn(b, n, s=None, g=None, asc=True, nilslast=False):
