@@ -52,6 +52,11 @@ def parse():
     p.add_argument("--cpu-sf", type=float, default=20.0, help="CPU baseline sample scale factor")
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) or gloo (rehearsal)")
+    p.add_argument("--no-dist-legs", action="store_true",
+                   help="skip the config-4 (l_orderkey group, all_to_all) and config-5 (RANGE bounds) legs")
+    p.add_argument("--window-rows", type=int, default=1_000_000_000,
+                   help="config 5: rows of the window column over ALL ranks (strong scaling)")
+    p.add_argument("--leg-steps", type=int, default=3)
     return p.parse_args()
 
 
@@ -189,9 +194,17 @@ def main():
         extra["q1_op_at_a_time"] = {"ms_per_step": round(op1_ms, 3),
                                     "grows_per_s": round(rows / op1_ms / 1e6, 2)}
 
+    if not args.no_dist_legs:
+        extra["config4_orderkey_group"] = leg_orderkey_group(args, gdk, D, dist, dev, cols, rows, row0, world,
+                                                             barrier)
+        del cols, qargs
+        gdk.lib().mgdk_mem_release_cache()
+        extra["config5_window_bounds"] = leg_window(args, gdk, D, dist, dev, rank, world, barrier)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args)
+        extra["cpu_baselines"] = cpu_baselines_other(args)
 
     if rank == 0:
         ms = elapsed / args.steps * 1e3
@@ -228,6 +241,91 @@ def main():
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _max_over_ranks(dist, dev, vals):
+    if dist is None:
+        return vals
+    import torch
+    t = torch.tensor(vals, dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t.cpu().tolist()]
+
+
+def leg_orderkey_group(args, gdk, D, dist, dev, cols, rows, row0, world, barrier):
+    """Config 4 with its exchange: GROUP BY an l_orderkey-shaped key (4
+    lines per order, orders clustered as lineitem is) with exact sums of
+    l_quantity and l_extendedprice, over the same SF100-per-GPU shards:
+    local BATgroup + BATgroupsum, the partial rows hash-partitioned by key
+    and shuffled with ONE RCCL all_to_all per column, merged on the owner,
+    numbered in global first-occurrence order (opt_mergetable.c:1496-1885
+    mat_group / mat_group_aggr).  Weak scaling (rows per GPU fixed)."""
+    okey = gdk.BATconvert(gdk.BAT.dense(row0, rows, hseqbase=row0), None, gdk.TYPE_lng)
+    okey = gdk.BATcalcdivmod("/", okey, None, gdk.TYPE_lng, c2=4, t2=gdk.TYPE_lng)
+    okey.s.hseqbase = row0
+    okey.s.tsorted, okey.s.trevsorted, okey.s.tkey, okey.s.tnonil = 1, 0, 0, 1
+    vals = [cols["quantity"], cols["extendedprice"]]
+    be = D.GdkBackend(dev)
+    out = D.dist_group_aggr(be, dist, okey, vals)           # warm-up
+    ngroups_local = out["gid"].count()
+    del out
+    barrier()
+    D.STATS["exchange_s"] = 0.0
+    t = time.perf_counter()
+    for _ in range(args.leg_steps):
+        out = D.dist_group_aggr(be, dist, okey, vals)
+        del out
+    barrier()
+    tot = (time.perf_counter() - t) / args.leg_steps
+    exch = D.STATS["exchange_s"] / args.leg_steps
+    tot, exch, comp = _max_over_ranks(dist, dev, [tot, exch, tot - exch])
+    ng = _gather_sum(dist, dev, ngroups_local)
+    return {"ms_per_step": round(tot * 1e3, 3), "grows_per_s": round(rows * world / tot / 1e9, 3),
+            "unit": "Grows/s", "exchange_ms": round(exch * 1e3, 3), "local_ms": round(comp * 1e3, 3),
+            "groups": ng, "rows_per_gpu": rows, "scaling": "weak",
+            "workload": "GROUP BY l_orderkey (4 lines/order) SUM(l_quantity), SUM(l_extendedprice): "
+                        "dist_group_aggr, one all_to_all per partial column"}
+
+
+def _gather_sum(dist, dev, v):
+    if dist is None:
+        return int(v)
+    import torch
+    t = torch.tensor([float(v)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t)
+    return int(t.item())
+
+
+def leg_window(args, gdk, D, dist, dev, rank, world, barrier, limit=100, plen=100_000):
+    """Config 5: GDKanalyticalwindowbounds (RANGE 100 PRECEDING) over ONE
+    column of --window-rows rows (1B) range-partitioned over the ranks
+    (strong scaling); shards start at partition boundaries, so the move of
+    rows to the partition's owner is empty and every rank computes its
+    bounds locally (dist_window_bounds)."""
+    n = args.window_rows // world
+    v, p = gdk.gen_window_column(5 + rank, n, plen)
+    v.s.hseqbase = p.s.hseqbase = rank * n
+    be = D.GdkBackend(dev)
+    r = D.dist_window_bounds(be, dist, v, p, limit, True)
+    del r
+    barrier()
+    gdk.prof_reset()
+    gdk.prof_enable(True)
+    t = time.perf_counter()
+    for _ in range(args.leg_steps):
+        r = D.dist_window_bounds(be, dist, v, p, limit, True)
+        del r
+    barrier()
+    tot = (time.perf_counter() - t) / args.leg_steps
+    kms, kn = gdk.prof_get("windowbounds")
+    gdk.prof_enable(False)
+    kern = kms / max(1, kn) * 1e-3
+    tot, kern = _max_over_ranks(dist, dev, [tot, kern])
+    total_rows = n * world
+    return {"ms_per_step": round(tot * 1e3, 3), "grows_per_s": round(total_rows / tot / 1e9, 3),
+            "unit": "Grows/s", "kernel_ms": round(kern * 1e3, 3), "rows_total": total_rows,
+            "rows_per_gpu": n, "partitions": total_rows // plen, "limit": limit, "scaling": "strong",
+            "roofline_frac_kernel": round(17 * n / kern / 1e9 / HBM_PEAK_GBS, 4) if kern > 0 else None}
 
 
 def pmc_traffic(kernel, rows):
@@ -281,6 +379,77 @@ def cpu_baseline(args):
             "ms": round(med * 1e3, 2),
             "single_thread": {"value": round(n / med1 / 1e9, 4), "unit": "Grows/s", "cores": 1,
                               "ms": round(med1 * 1e3, 2), "sample": "same rows, median of 3"}}
+
+
+def _cpu_quota():
+    """The cgroup CPU quota of this process (cgroup v2 cpu.max), in CPUs."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except Exception:  # noqa: BLE001
+        return None
+
+
+def cpu_baselines_other(args):
+    """CPU comparators (the oracle's restatement of the reference operators)
+    for configs 3, 4 and 5 on bounded samples of the same workloads."""
+    try:
+        import numpy as np
+        from oracle import pyoracle as ora
+        ora.lib()
+    except Exception as e:  # noqa: BLE001
+        return {"error": "oracle unavailable: %s" % e}
+    out = {"cgroup_cpu_quota": _cpu_quota(), "nproc": os.cpu_count()}
+    r = np.random.default_rng(3)
+    # config 3: BATjoin (hash path) lineitem x orders at SF1, single thread
+    # (the reference's hashjoin is one thread per call)
+    no = 1_500_000
+    i = np.arange(no, dtype=np.int64)
+    ok = ((i // 8) * 32 + (i % 8) + 1).astype(np.int32)
+    r.shuffle(ok)
+    lk = np.repeat(ok, r.integers(1, 8, no)).astype(np.int32)
+    r.shuffle(lk)
+    L = ora.Bat.from_array(ora.TYPE_int, lk, nonil=True)
+    R = ora.Bat.from_array(ora.TYPE_int, ok, nonil=True, key=True)
+    ts = []
+    for _ in range(3):
+        t = time.perf_counter()
+        ora.BATjoin(L, R)
+        ts.append(time.perf_counter() - t)
+    med = statistics.median(ts)
+    out["config3_hashjoin"] = {"value": round(len(lk) / med / 1e9, 5), "unit": "Grows/s", "cores": 1,
+                               "kind": "port", "ms": round(med * 1e3, 1),
+                               "sample": "SF1: %d probe x %d unique shuffled build rows, median of 3"
+                                         % (len(lk), no)}
+    # config 4: Q1 op-at-a-time over an SF2 sample on the box's CPU share
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    n4 = 2 * SF1_ROWS
+    cols = ora.tpch_lineitem(20241024, 0, n4, 400_000)
+    ora.q1(cols, share)
+    ts = []
+    for _ in range(3):
+        t = time.perf_counter()
+        ora.q1(cols, share)
+        ts.append(time.perf_counter() - t)
+    med = statistics.median(ts)
+    out["config4_q1"] = {"value": round(n4 / med / 1e9, 5), "unit": "Grows/s", "cores": share, "kind": "port",
+                         "ms": round(med * 1e3, 1),
+                         "sample": "TPC-H Q1 op-at-a-time (oracle), SF2 = %d rows, %d threads, median of 3"
+                                   % (n4, share)}
+    # config 5: RANGE 100 PRECEDING bounds (the reference's walk), 2M rows
+    n5 = 2_000_000
+    v = np.cumsum(r.integers(0, 5, n5)).astype(np.int64)
+    pb = np.zeros(n5, np.int8)
+    pb[::100_000] = 1
+    V = ora.Bat.from_array(ora.TYPE_lng, v, nonil=True, sorted_=True)
+    P = ora.Bat.from_array(ora.TYPE_bit, pb)
+    t = time.perf_counter()
+    ora.rangebounds(V, P, 100, True)
+    med = time.perf_counter() - t
+    out["config5_rangebounds"] = {"value": round(n5 / med / 1e9, 5), "unit": "Grows/s", "cores": 1,
+                                  "kind": "port", "ms": round(med * 1e3, 1),
+                                  "sample": "%d rows, 20 partitions, limit 100, one run" % n5}
+    return out
 
 
 if __name__ == "__main__":

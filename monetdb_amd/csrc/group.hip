@@ -955,6 +955,106 @@ dense_or_copy(const Cand &ci)
 	return nullptr;
 }
 
+// ---- ordered keys: GRP_compare_consecutive_values (gdk_group.c:103-175,
+// chosen at :940-975 when b is sorted or reverse sorted and g is ordered):
+// a new group wherever the (prior group, value) pair differs from the row
+// before, so ids are a running count of those starts
+__global__ __launch_bounds__(256) void
+k_grp_seq_flags(KeySrc s, BUN n, uint8_t *fl)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		uint64_t a0, a1, ag, b0, b1, bg;
+		key_at(s, i, a0, a1, ag);
+		bool nw = i == 0;
+		if (!nw) {
+			key_at(s, i - 1, b0, b1, bg);
+			nw = a0 != b0 || a1 != b1 || ag != bg;
+		}
+		fl[i] = nw;
+	}
+}
+
+__global__ __launch_bounds__(256) void
+k_grp_seq_ids(BUN n, const uint8_t *fl, const uint64_t *ex, oid *gid, uint64_t *spos)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		const uint64_t k = ex[i] + fl[i] - 1;
+		gid[i] = k;
+		if (fl[i])
+			spos[k] = i;
+	}
+}
+
+__global__ __launch_bounds__(256) void
+k_grp_seq_ext(BUN ngrp, BUN n, const uint64_t *spos, bool cdense, oid cseq, const oid *coids, oid *en,
+	      int64_t *hn)
+{
+	for (BUN k = (BUN) blockIdx.x * blockDim.x + threadIdx.x; k < ngrp; k += (BUN) gridDim.x * blockDim.x) {
+		const uint64_t p = spos[k];
+		en[k] = cdense ? cseq + p : coids[p];
+		hn[k] = (int64_t) ((k + 1 < ngrp ? spos[k + 1] : n) - p);
+	}
+}
+
+int
+group_ordered(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mgdk_bat **enp,
+	      mgdk_bat **hnp)
+{
+	hipStream_t st = stream();
+	DevBuf fl(n + 8), ex(n * 8 + 8), spos(n * 8 + 8);
+	if (!fl.p || !ex.p || !spos.p)
+		return -1;
+	const dim3 grd(grid_for(n, 1024, 8192)), blk(256);
+	hipLaunchKernelGGL(k_grp_seq_flags, grd, blk, 0, st, ks, n, fl.as<uint8_t>());
+	uint64_t ngrp = 0;
+	if (exclusive_scan(fl.as<uint8_t>(), ex.as<uint64_t>(), n, &ngrp) < 0)
+		return -1;
+	mgdk_bat *gn = newbat(hseqb, MGDK_oid, n), *en = newbat(0, MGDK_oid, ngrp), *hn = newbat(0, MGDK_lng, ngrp);
+	if (!gn || !en || !hn) {
+		mgdk_BBPunfix(gn);
+		mgdk_BBPunfix(en);
+		mgdk_BBPunfix(hn);
+		return -1;
+	}
+	hipLaunchKernelGGL(k_grp_seq_ids, grd, blk, 0, st, n, fl.as<uint8_t>(), ex.as<uint64_t>(), (oid *) gn->theap,
+			   spos.as<uint64_t>());
+	hipLaunchKernelGGL(k_grp_seq_ext, dim3(grid_for(ngrp, 1024, 8192)), blk, 0, st, ngrp, n, spos.as<uint64_t>(),
+			   ci.dense, ci.seq, ci.oids, (oid *) en->theap, (int64_t *) hn->theap);
+	uint64_t *hl = (uint64_t *) pinned(16);
+	if (!hip_ok(hipMemcpyAsync(hl, spos.as<uint64_t>() + ngrp - 1, 8, hipMemcpyDeviceToHost, st), "memcpy") ||
+	    !sync()) {
+		mgdk_BBPunfix(gn);
+		mgdk_BBPunfix(en);
+		mgdk_BBPunfix(hn);
+		return -1;
+	}
+	gn->count = n;
+	gn->tsorted = 1;
+	gn->trevsorted = ngrp == 1 || n <= 1;
+	gn->tkey = ngrp == n;
+	gn->tnonil = 1;
+	gn->tmaxpos = hl[0];
+	en->count = hn->count = ngrp;
+	en->tsorted = en->tkey = en->tnonil = 1;
+	en->trevsorted = ngrp == 1;
+	hn->tkey = ngrp == 1;
+	hn->tsorted = hn->trevsorted = ngrp == n || ngrp == 1;
+	hn->tnonil = 1;
+	oid fl2[2];
+	if (oid_at(en, 0, &fl2[0]) < 0 || oid_at(en, ngrp - 1, &fl2[1]) < 0) {
+		mgdk_BBPunfix(gn);
+		mgdk_BBPunfix(en);
+		mgdk_BBPunfix(hn);
+		return -1;
+	}
+	if (fl2[1] - fl2[0] == ngrp - 1)
+		setdense(en, fl2[0], ngrp);
+	*gnp = gn;
+	*enp = en;
+	*hnp = hn;
+	return 0;
+}
+
 int
 key_kind(int tt)
 {
@@ -1057,6 +1157,14 @@ group_core(mgdk_bat **groups, mgdk_bat **extents, mgdk_bat **histo, mgdk_bat *b,
 			gmax = *hm;
 		} else if (g) {
 			gmax = g->tseqbase + n;
+		}
+		// ordered keys (and ordered prior groups): consecutive comparison
+		// (gdk_group.c:940-975); 1- and 2-byte keys keep the table paths
+		if (ks.w >= 4 && (b->tsorted || b->trevsorted) &&
+		    (!g || mgdk_BATordered(g) || mgdk_BATordered_rev(g))) {
+			if (group_ordered(ks, n, ci, hseqb, &gn, &en, &hn) < 0)
+				goto fail;
+			goto done;
 		}
 		// 1-byte keys under <= 32 prior groups: direct LDS tables
 		static const bool small_on = getenv("MGDK_GROUP_SMALL") ? atoi(getenv("MGDK_GROUP_SMALL")) != 0 : true;

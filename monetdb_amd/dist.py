@@ -247,6 +247,47 @@ class GdkBackend:
             return None
         return int(self.gdk.BATslice(s, 0, 1).to_numpy()[0]) - parts.hseqbase
 
+    # -- zero-copy exchange (RCCL) ---------------------------------------------
+    def tensor(self, c):
+        """c's tail as a torch tensor on the rank's GPU WITHOUT a copy (the
+        CUDA array interface over the BAT's heap); hge as (n, 2) int64.  A
+        dense (void) column is materialised first."""
+        import torch
+        g = self.gdk
+        if c.ttype == g.TYPE_void:
+            m = g.BAT(g.lib().mgdk_COLnew(c.hseqbase, g.TYPE_oid, max(1, c.count())))
+            g.BATappend(m, c)
+            c = m
+        return torch.as_tensor(_HeapView(c, g), device=self.device)
+
+    def exchange_cols(self, dist, cols, types, send_counts):
+        """all_to_all of columns whose rows are grouped by destination rank
+        (send_counts[d] rows for rank d): ONE collective per column straight
+        from the BAT heaps into the new BATs' heaps (no packing, no host
+        staging).  Returns (received columns in rank order, recv counts)."""
+        import torch
+        g = self.gdk
+        sc = torch.tensor(send_counts, dtype=torch.int64, device=self.device)
+        rc = torch.empty_like(sc)
+        dist.all_to_all_single(rc, sc)
+        recv = [int(x) for x in rc.cpu().tolist()]
+        tot = sum(recv)
+        g.sync()                              # the library stream wrote the sources
+        out, keep = [], []
+        for c, tp in zip(cols, types):
+            b = g.BAT(g.lib().mgdk_COLnew(0, tp, max(1, tot)))
+            b.s.count = tot
+            b.s.tsorted = b.s.trevsorted = b.s.tkey = int(tot <= 1)
+            b.s.tnonil = int(tot == 0)
+            b.s.tnil = 0
+            src = self.tensor(c)
+            dst = self.tensor(b)
+            keep += [src, c]
+            dist.all_to_all_single(dst, src, recv, list(send_counts))
+            out.append(b)
+        torch.cuda.current_stream(torch.device(self.device)).synchronize()
+        return out, recv
+
     # -- packing -------------------------------------------------------------
     def pack(self, cols):
         """(rows, k) int64 tensor of 8-byte and hge (2 words) columns, on the
@@ -305,6 +346,40 @@ class GdkBackend:
             g.BATupload_device(b, src.data_ptr() if n else 0, n)
             cols.append(b)
         return cols
+
+
+class _HeapView:
+    """A BAT tail under the CUDA array interface (torch.as_tensor wraps it
+    without copying); keeps the BAT alive as long as the tensor."""
+
+    def __init__(self, b, g):
+        self.b = b
+        n = b.count()
+        w = b.s.twidth
+        shape = (n, 2) if b.ttype == g.TYPE_hge else (n,)
+        typestr = "<i8" if b.ttype == g.TYPE_hge else {1: "|i1", 2: "<i2", 4: "<i4", 8: "<i8"}[w]
+        ptr = b.s.theap or 0
+        self.__cuda_array_interface__ = {"shape": shape, "typestr": typestr, "data": (ptr, False),
+                                         "version": 2, "strides": None}
+
+
+# time spent in the shuffles (exchange below), for the bench's split of a
+# step into local operators and exchange
+STATS = {"exchange_s": 0.0}
+
+
+def exchange(be, dist, cols, types, send_counts):
+    """Columns shuffled by destination: per-column RCCL all_to_all from the
+    heaps when the backend lives on a GPU, else packed rows over gloo."""
+    import time
+    t = time.perf_counter()
+    if getattr(be, "device", "cpu") != "cpu" and hasattr(be, "exchange_cols"):
+        out = be.exchange_cols(dist, cols, types, send_counts)[0]
+    else:
+        recv, _ = _exchange(dist, be.device, be.pack(cols), send_counts)
+        out = be.unpack(recv, types)
+    STATS["exchange_s"] += time.perf_counter() - t
+    return out
 
 
 def _exchange(dist, device, packed, send_counts):
@@ -387,8 +462,7 @@ def dist_group_aggr(be, dist, keys, vals):
     if world > 1:
         order, counts = be.hashpartition(parts[0], world)
         parts = [be.project(order, c) for c in parts]
-        recv, _ = _exchange(dist, be.device, be.pack(parts), counts)
-        parts = be.unpack(recv, [TL, TO, TL] + [TH] * len(vals))
+        parts = exchange(be, dist, parts, [TL, TO, TL] + [TH] * len(vals), counts)
     rk, rfirst, rcount, rsums = parts[0], parts[1], parts[2], parts[3:]
     if be.n(rk) == 0:
         mk, mf, mc, ms = rk, rfirst, rcount, list(rsums)
@@ -423,8 +497,7 @@ def dist_group_avg(be, dist, keys, vals):
     if world > 1:
         order, counts = be.hashpartition(parts[0], world)
         parts = [be.project(order, x) for x in parts]
-        recv, _ = _exchange(dist, be.device, be.pack(parts), counts)
-        parts = be.unpack(recv, [TL, TO, TL, TL, TL])
+        parts = exchange(be, dist, parts, [TL, TO, TL, TL, TL], counts)
     rk, rfirst, ra, rr, rc = parts
     if be.n(rk) == 0:
         mk, mf, ma = rk, rfirst, ra
@@ -547,9 +620,7 @@ def dist_join(be, dist, lkeys, rkeys, lrows_per_rank, rrows_per_rank=None):
     for c in (lkeys, rkeys):
         w = be.widen(c)
         order, counts = be.hashpartition(w, world)
-        packed = be.pack([be.project(order, w), order])
-        recv, _ = _exchange(dist, be.device, packed, counts)
-        sides.append(be.unpack(recv, [TL, TO]))
+        sides.append(exchange(be, dist, [be.project(order, w), order], [TL, TO], counts))
     (lk, lo), (rk, ro) = sides
     j1, j2 = be.join(lk, rk)
     r1, r2 = be.project(j1, lo), be.project(j2, ro)
@@ -562,8 +633,7 @@ def dist_join(be, dist, lkeys, rkeys, lrows_per_rank, rrows_per_rank=None):
     cuts = be.lowerbound2(d, None, [k * per for k in range(1, world)], [0] * (world - 1))
     edges = [0] + list(cuts) + [be.n(d)]
     counts = [edges[k + 1] - edges[k] for k in range(world)]
-    recv, _ = _exchange(dist, be.device, be.pack([d, o]), counts)
-    d, o = be.unpack(recv, [TO, TO])
+    d, o = exchange(be, dist, [d, o], [TO, TO], counts)
     # the reference order: driving rows ascending, their matches ascending
     # (select / merge joins) or descending (hash chains): two stable sorts
     _, oo = be.sort(o, reverse=desc)
@@ -598,8 +668,7 @@ def dist_sort(be, dist, keys, sample=64):
     cuts = be.lowerbound2(s, o, [k for k, _ in spl], [p for _, p in spl]) if spl else [n] * (world - 1)
     edges = [0] + list(cuts) + [n]
     counts = [edges[d + 1] - edges[d] for d in range(world)]
-    recv, _ = _exchange(dist, be.device, be.pack([s, o]), counts)
-    k2, p2 = be.unpack(recv, [TL, TO])
+    k2, p2 = exchange(be, dist, [s, o], [TL, TO], counts)
     if be.n(k2) == 0:
         return k2, p2
     # runs arrive in rank order = ascending positions among equal keys, so
@@ -636,8 +705,7 @@ def dist_window_bounds(be, dist, vals, parts, limit, preceding):
     counts = [0] * world
     counts[owner] = lead
     w = be.widen(vals)
-    recv, _ = _exchange(dist, be.device, be.pack([be.slice(w, 0, lead)]), counts)
-    (rv,) = be.unpack(recv, [TL])
+    (rv,) = exchange(be, dist, [be.slice(w, 0, lead)], [TL], counts)
     # kept rows [lead, n), then the leading rows of later ranks (they
     # arrive in rank order and carry no partition start)
     v2 = be.copy(be.slice(w, lead, n))

@@ -146,3 +146,56 @@ def test_gpu_group_aggr_high_cardinality_device_backend():
     errs = []
     _check_groups(got, _hicard_expect(keys, vals), errs)
     assert not errs, errs
+
+
+def test_gdk_backend_rccl_exchange_cols_world1():
+    """GdkBackend.exchange_cols -- the RCCL path of every dist_* shuffle: one
+    all_to_all per column straight from the BAT heaps (CUDA array interface
+    views, no packing) into new BATs.  World 1 over RCCL on the box's GPU:
+    the collective runs for real; the received columns equal the sent ones
+    (lng, oid, hge, a dense column, an empty exchange)."""
+    import os
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from monetdb_amd import dist as D
+    from monetdb_amd import gdk
+    from test_distributed import _free_port
+    gdk.init(0)
+    torch.cuda.set_device(0)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        be = D.GdkBackend("cuda:0")
+        r = np.random.default_rng(4)
+        n = 200_003
+        lv = r.integers(-2**63, 2**63 - 1, n, dtype=np.int64)
+        ov = r.integers(0, 2**40, n).astype(np.uint64)
+        hw = r.integers(0, 2**63, (n, 2)).astype(np.uint64)
+        cols = [gdk.BAT.from_numpy(gdk.TYPE_lng, lv), gdk.BAT.from_numpy(gdk.TYPE_oid, ov),
+                gdk.BAT.from_numpy(gdk.TYPE_hge, hw), gdk.BAT.dense(1000, n)]
+        types = [gdk.TYPE_lng, gdk.TYPE_oid, gdk.TYPE_hge, gdk.TYPE_oid]
+        out, recv = be.exchange_cols(dist, cols, types, [n])
+        assert recv == [n]
+        assert np.array_equal(out[0].to_numpy(), lv)
+        assert np.array_equal(out[1].to_numpy(), ov)
+        assert np.array_equal(out[2].to_numpy(), hw)
+        assert np.array_equal(out[3].to_numpy(), np.arange(1000, 1000 + n, dtype=np.uint64))
+        # a slice (view) as the source, and nothing to send
+        s = gdk.BATslice(cols[0], 10, 110)
+        out, _ = be.exchange_cols(dist, [s], [gdk.TYPE_lng], [100])
+        assert np.array_equal(out[0].to_numpy(), lv[10:110])
+        out, _ = be.exchange_cols(dist, [gdk.BATslice(cols[0], 0, 0)], [gdk.TYPE_lng], [0])
+        assert out[0].count() == 0
+        # the whole high-cardinality group + sum through the RCCL path
+        keys, vals = _hicard(0, 1, 50_000)
+        got = D.dist_group_aggr(be, dist, gdk.BAT.from_numpy(gdk.TYPE_lng, keys),
+                                [gdk.BAT.from_numpy(gdk.TYPE_lng, vals)])
+        errs = []
+        _check_groups(got, _hicard_expect(keys, vals), errs)
+        assert not errs, errs
+    finally:
+        dist.destroy_process_group()
