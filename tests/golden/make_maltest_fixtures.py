@@ -29,6 +29,11 @@ Sources (reference paths, relative to /root/reference):
   monetdb5/modules/mal/Tests/orderidx00.maltest, orderidx04.maltest --
       algebra.sort (ALGsort -> BATsort, algebra.c:1754-1831) of an int BAT:
       sorted values, and the order oids of the stable variant
+  monetdb5/mal/Tests/tst033.maltest, tst034.maltest,
+  monetdb5/modules/mal/Tests/orderidx02.maltest -- algebra.projection of
+      algebra.select results (every li/hi/anti combination, nil bounds, a
+      slice view): the printed (head, value) / (head, oid, value) rows; and
+      orderidx02's bat.orderidx order (a stable sort's order oids)
 """
 import json
 import os
@@ -206,6 +211,66 @@ def sort_fixture(rel):
             cases.append(pending)
             pending = None
     return {"source": rel, "cases": cases}
+
+
+def project_fixture(rel):
+    """algebra.select + algebra.projection (ALGprojection -> BATproject,
+    algebra.c:1040-1060) over int BATs built with bat.append (optionally
+    algebra.slice views), expected = the printed (head, [oid,] value) rows;
+    the order index of bat.orderidx / bat.getorderidx becomes a sort case"""
+    text = open(os.path.join(REF, rel)).read()
+    bats, sels, projs = {}, {}, {}
+    cases, sorts = [], []
+    pending = None
+    for kind, body, exp in parse_blocks(text):
+        stmt = " ".join(body)
+        m = re.match(r"(\w+)\s*:=\s*bat\.new\(:int\)$", stmt)
+        if m:
+            bats[m.group(1)] = []
+            continue
+        m = re.match(r"bat\.append\((\w+),\s*(-?\d+)\s*\)$", stmt)
+        if m and m.group(1) in bats:
+            bats[m.group(1)].append(int(m.group(2)))
+            continue
+        m = re.match(r"(\w+)\s*:=\s*algebra\.slice\((\w+),(\d+),(\d+)\)$", stmt)
+        if m:
+            bats[m.group(1)] = bats[m.group(2)][int(m.group(3)):int(m.group(4)) + 1]
+            continue
+        m = re.match(r"(\w+)\s*:=\s*algebra\.select\((\w+),nil:bat\[:oid\],([^,]+),([^,]+),"
+                     r"(true|false),(true|false),(true|false)\)$", stmt)
+        if m:
+            sels[m.group(1)] = dict(bat=m.group(2), low=val(m.group(3)), high=val(m.group(4)),
+                                    li=m.group(5) == "true", hi=m.group(6) == "true", anti=m.group(7) == "true")
+            continue
+        m = re.match(r"(\w+)\s*:=\s*algebra\.projection\((\w+),(\w+)\)$", stmt)
+        if m:
+            projs[m.group(1)] = (m.group(2), m.group(3))
+            continue
+        m = re.match(r"(\w+)\s*:=\s*bat\.getorderidx\((\w+)\)$", stmt)
+        if m:
+            pending = ("orderidx", m.group(2))
+            continue
+        m = re.match(r"io\.print\((\w+)(?:,(\w+))?\)$", stmt)
+        if m and kind.startswith("query I"):
+            width = len(kind.split()[1])
+            rows = sorted(tuple(int(exp[i + k]) for k in range(width)) for i in range(0, len(exp), width))
+            a, b = m.group(1), m.group(2)
+            if pending and pending[0] == "orderidx" and b == pending[1]:
+                sorts.append(dict(reverse=False, nilslast=False, stable=True, order=True,
+                                  values=list(bats[b]), sorted=sorted(bats[b]),
+                                  order_oids=[r[1] for r in rows]))
+                pending = None
+                continue
+            if b is None and a in projs:
+                sname, bname = projs[a]
+                sel = sels[sname]
+                if sel["bat"] != bname:
+                    continue
+                cases.append(dict(sel, values=list(bats[bname]), expected_rows=[list(r) for r in rows]))
+            elif b is not None and a in sels and b in projs:
+                sel = sels[a]
+                cases.append(dict(sel, values=list(bats[sel["bat"]]), expected_rows=[list(r) for r in rows]))
+    return {"source": rel, "cases": cases}, sorts
 
 
 def analytics03_fixture():
@@ -412,6 +477,13 @@ def main():
           "window_bounds_employee": window_functions_fixture(),
           "window_bounds_intervals": analytics07_fixture(),
           "batcalc": batcalc_fixture()}
+    fx["project"] = []
+    for rel in ("monetdb5/mal/Tests/tst033.maltest", "monetdb5/mal/Tests/tst034.maltest",
+                "monetdb5/modules/mal/Tests/orderidx02.maltest"):
+        proj, sorts = project_fixture(rel)
+        fx["project"].append(proj)
+        if sorts:
+            fx["sort"].append({"source": rel, "cases": sorts})
     with open(os.path.join(OUT, "maltest_fixtures.json"), "w") as f:
         json.dump(fx, f, indent=1)
     print("select cases:", len(fx["select"]["cases"]))

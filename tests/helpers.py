@@ -29,6 +29,26 @@ def replay_select(G, make_bat, TYPE_int, NIL):
     return bad
 
 
+def replay_project(G, make_bat, TYPE_int, NIL):
+    """algebra.select + algebra.projection cases of tst033 / tst034 /
+    orderidx02.maltest: the printed (head, value) or (head, oid, value) rows,
+    row-sorted as the tests print them.  Returns mismatches."""
+    from monetdb_amd import mal
+    bad = []
+    for fx in FIX["project"]:
+        for c in fx["cases"]:
+            b = make_bat(TYPE_int, [NIL if v is None else v for v in c["values"]])
+            s = mal.ALGselect2(G, b, None, c["low"], c["high"], c["li"], c["hi"], c["anti"], nil=NIL)
+            z = [int(v) for v in np.asarray(G.BATproject(s, b).values())]
+            oids = [int(v) for v in np.asarray(s.values())]
+            width = len(c["expected_rows"][0]) if c["expected_rows"] else 2
+            rows = [[i, v] for i, v in enumerate(z)] if width == 2 else \
+                [[i, o, v] for i, (o, v) in enumerate(zip(oids, z))]
+            if sorted(rows) != c["expected_rows"]:
+                bad.append((fx["source"], c, rows))
+    return bad
+
+
 def rng(seed):
     return np.random.default_rng(seed)
 

@@ -3,7 +3,7 @@ with the reference's own fixtures.  Bit-exact for every oid / integer result."""
 import numpy as np
 import pytest
 
-from helpers import FIX, replay_select, rng, with_nils
+from helpers import FIX, replay_project, replay_select, rng, with_nils
 
 pytestmark = pytest.mark.gpu
 
@@ -316,6 +316,14 @@ def test_bigsum_fixture(gdk):
 
 
 # ---- group and grouped aggregates --------------------------------------------
+
+def test_project_maltest_fixture(gdk):
+    """algebra.projection of algebra.select results (tst033 / tst034 /
+    orderidx02.maltest) on the device"""
+    bad = replay_project(gdk, lambda tp, v: mk(gdk, tp, np.array(v, np.int32)), gdk.TYPE_int,
+                         gdk.NIL[gdk.TYPE_int])
+    assert not bad, bad[:3]
+
 
 @pytest.mark.parametrize("name", ["group_tst1500", "group_tst1503"])
 def test_group_fixture(gdk, name):

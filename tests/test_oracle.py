@@ -7,7 +7,7 @@ import math
 import numpy as np
 import pytest
 
-from helpers import FIX, replay_select
+from helpers import FIX, replay_project, replay_select
 
 
 def test_select_maltest(ora):
@@ -529,3 +529,12 @@ def test_windowbounds_interval_errors(ora):
                 ora.windowbounds(b, None, None, lim, tp, tp2, 1, pre, sh)
         n += 1
     assert n == 2
+
+
+def test_project_maltest(ora):
+    """algebra.projection of algebra.select results: tst033 / tst034 /
+    orderidx02.maltest (20 cases)"""
+    mk = lambda tp, v: ora.Bat.from_array(tp, np.array(v, np.int32))
+    assert sum(len(f["cases"]) for f in FIX["project"]) == 20
+    bad = replay_project(ora, mk, ora.TYPE_int, ora.NIL[ora.TYPE_int])
+    assert not bad, bad[:3]
