@@ -730,7 +730,185 @@ struct AggrInit {
 	const oid *gids;   // NULL: dense g
 	const uint8_t *g8; // 1-byte image of gids kept by BATgroup (or NULL)
 	oid gseq;
+	bool gsorted;      // g non-decreasing: every group a run of rows
 };
+
+// ---- many groups, g sorted (every group a run of consecutive rows, as
+// BATgroup numbers ordered keys, a sub-grouping of them or a clustered
+// column): a wave owns a range of 64 * GS_U rows, reduces each 64-row chunk
+// with a segmented scan over the runs, carries the open run from chunk to
+// chunk, and stores every run that starts and ends inside its range with
+// plain stores -- no other wave holds that group.  Only the range's first
+// run (it may have begun in the previous range) and its last (it may go on)
+// are added with atomics.
+constexpr int GS_U = 16;
+
+template <int VW, bool MM, bool POS>
+__global__ __launch_bounds__(256) void
+k_gaggr_sorted(const void *base, oid off, const oid *gids, oid gseq, oid gmin, BUN ngrp, BUN n, bool do_sum,
+	       bool count_all, GAcc acc, unsigned long long *maxabs)
+{
+	typedef typename VTy<VW>::T T;
+	const int lane = __lane_id();
+	const BUN nwaves = (BUN) gridDim.x * (blockDim.x / 64);
+	const BUN wid = (BUN) blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+	unsigned long long mxa = 0;
+	constexpr BUN RW = 64 * GS_U;
+	auto flush = [&](bool atomic, BUN gi, uhge sv, unsigned long long c, unsigned long long fv,
+			 unsigned long long ln, long long mn, long long mx) {
+		if (atomic) {
+			if (do_sum && sv)
+				atomic_add128(&acc.sum[2 * gi], (hge) sv);
+			if (c)
+				atomicAdd(&acc.cnt[gi], c);
+			if (POS && fv != ~0ull)
+				atomicMin(&acc.firstval[gi], fv);
+			if (POS && ln)
+				atomicMax(&acc.lastnil[gi], ln);
+			if (MM && c) {
+				atomicMin(&acc.mn[gi], mn);
+				atomicMax(&acc.mx[gi], mx);
+			}
+		} else {
+			if (do_sum) {
+				acc.sum[2 * gi] = (unsigned long long) sv;
+				acc.sum[2 * gi + 1] = (unsigned long long) (sv >> 64);
+			}
+			acc.cnt[gi] = c;
+			if (POS) {
+				acc.firstval[gi] = fv;
+				acc.lastnil[gi] = ln;
+			}
+			if (MM) {
+				acc.mn[gi] = mn;
+				acc.mx[gi] = mx;
+			}
+		}
+	};
+	for (BUN r0 = wid * RW; r0 < n; r0 += nwaves * RW) {
+		const BUN r1 = r0 + RW < n ? r0 + RW : n;
+		// the open run carried between chunks (the same in every lane)
+		bool have = false, cval = false, cshared = true;
+		oid cg = 0;
+		uhge cs = 0;
+		unsigned long long cc = 0, cfv = ~0ull, cln = 0;
+		long long cmn = INT64_MAX, cmx = INT64_MIN;
+		for (BUN b = r0; b < r1; b += 64) {
+			const BUN i = b + lane;
+			const bool in = i < r1;
+			const BUN ic = in ? i : r1 - 1;
+			const oid g = gids ? gids[ic] : gseq + ic;
+			bool isnil = false;
+			hge v = 0;
+			if constexpr (VW > 0) {
+				const T x = ((const T *) base)[off + ic];
+				isnil = is_nil(x);
+				v = (hge) x;
+			}
+			const bool valid = in && g >= gmin && g - gmin < ngrp;
+			// this row's contribution
+			uhge s = valid && !isnil ? (uhge) v : 0;
+			unsigned long long c = valid && (!isnil || count_all) ? 1 : 0;
+			unsigned long long fv = valid && !isnil ? (unsigned long long) i : ~0ull;
+			unsigned long long ln = valid && isnil ? (unsigned long long) i + 1 : 0;
+			long long mn = valid && !isnil ? (long long) v : INT64_MAX, mx = valid && !isnil ? (long long) v : INT64_MIN;
+			if (valid && !isnil) {
+				const unsigned long long a = absbits(v);
+				mxa = a > mxa ? a : mxa;
+			}
+			const oid gp = __shfl_up(g, 1);
+			const bool inp = __shfl_up((int) in, 1) != 0;
+			// lane 0 of the range's first chunk continues the (empty) carry:
+			// its run is the range's first, possibly shared with the previous
+			const bool head = !in || (lane == 0 ? (have && g != cg) : (!inp || g != gp));
+			if (have && __shfl((int) head, 0)) {
+				// the carried run ended with the previous chunk
+				if (cval && lane == 0)
+					flush(cshared, cg - gmin, cs, cc, cfv, cln, cmn, cmx);
+				cs = 0;
+				cc = 0;
+				cfv = ~0ull;
+				cln = 0;
+				cmn = INT64_MAX;
+				cmx = INT64_MIN;
+				cshared = false;
+			}
+			// segmented inclusive scan over the runs
+			bool f = head;
+#pragma unroll
+			for (int d = 1; d < 64; d <<= 1) {
+				const unsigned long long tlo = __shfl_up((unsigned long long) s, d);
+				const unsigned long long thi = __shfl_up((unsigned long long) (s >> 64), d);
+				const unsigned long long tc = __shfl_up(c, d);
+				const unsigned long long tfv = POS ? __shfl_up(fv, d) : 0;
+				const unsigned long long tln = POS ? __shfl_up(ln, d) : 0;
+				const long long tmn = MM ? __shfl_up(mn, d) : 0, tmx = MM ? __shfl_up(mx, d) : 0;
+				const bool tf = __shfl_up((int) f, d) != 0;
+				if (lane >= d) {
+					if (!f) {
+						s += ((uhge) thi << 64) | tlo;
+						c += tc;
+						if (POS) {
+							fv = tfv < fv ? tfv : fv;
+							ln = tln > ln ? tln : ln;
+						}
+						if (MM) {
+							mn = tmn < mn ? tmn : mn;
+							mx = tmx > mx ? tmx : mx;
+						}
+					}
+					f |= tf;
+				}
+			}
+			// the chunk's first run continues the carried one (identity before
+			// the first chunk)
+			if (!f) {
+				s += cs;
+				c += cc;
+				if (POS) {
+					fv = cfv < fv ? cfv : fv;
+					ln = cln > ln ? cln : ln;
+				}
+				if (MM) {
+					mn = cmn < mn ? cmn : mn;
+					mx = cmx > mx ? cmx : mx;
+				}
+			}
+			const bool nexthead = __shfl_down((int) head, 1) != 0;
+			if (lane < 63 && nexthead && valid) {
+				// a run ends here: shared only if it is the range's first run
+				const bool shared = !f && cshared;
+				flush(shared, g - gmin, s, c, fv, ln, mn, mx);
+			}
+			// the new carry: lane 63's run
+			const bool f63 = __shfl((int) f, 63) != 0;
+			const bool v63 = __shfl((int) valid, 63) != 0;
+			cshared = f63 ? false : cshared;
+			have = true;
+			cval = v63;
+			cg = __shfl(g, 63);
+			cs = ((uhge) __shfl((unsigned long long) (s >> 64), 63) << 64) | __shfl((unsigned long long) s, 63);
+			cc = __shfl(c, 63);
+			if (POS) {
+				cfv = __shfl(fv, 63);
+				cln = __shfl(ln, 63);
+			}
+			if (MM) {
+				cmn = __shfl(mn, 63);
+				cmx = __shfl(mx, 63);
+			}
+		}
+		// the range's last run may continue in the next range: added
+		if (have && cval && lane == 0)
+			flush(true, cg - gmin, cs, cc, cfv, cln, cmn, cmx);
+	}
+	for (int o = 32; o > 0; o >>= 1) {
+		const unsigned long long t = __shfl_xor(mxa, o);
+		mxa = t > mxa ? t : mxa;
+	}
+	if (lane == 0 && mxa)
+		atomicMax(maxabs, mxa);
+}
 
 __global__ void
 k_minmax_oid(const oid *g, BUN n, unsigned long long *out)
@@ -808,6 +986,7 @@ aggr_init(AggrInit *a, mgdk_bat **bp, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s)
 	a->gids = g->ttype == MGDK_void ? nullptr : (const oid *) g->theap;
 	a->g8 = a->gids ? img8_get(g) : nullptr;
 	a->gseq = g->tseqbase;
+	a->gsorted = g->ttype == MGDK_void || g->tsorted;
 	if (e) {
 		a->ngrp = e->count;
 		a->min = e->hseqbase;
@@ -863,15 +1042,16 @@ struct GRes {
 	unsigned long long maxabs;
 };
 
+// the grouped accumulators on the device (the thread's scratch buffer:
+// valid until its next scratch() user), no read-back
 int
-run_gaggr(const AggrInit &a, mgdk_bat *b, int what, bool count_all, GRes &r)
+gaggr_device(const AggrInit &a, mgdk_bat *b, int what, bool count_all, GAcc &acc, unsigned long long *&maxabs_out)
 {
 	const BUN ng = a.ngrp;
 	size_t bytes = ng * (16 + 8 * 5) + 64;
 	char *d = (char *) scratch(bytes);
 	if (d == nullptr)
 		return -1;
-	GAcc acc;
 	acc.sum = (unsigned long long *) d;
 	acc.cnt = acc.sum + 2 * ng;
 	acc.firstval = acc.cnt + ng;
@@ -917,9 +1097,43 @@ run_gaggr(const AggrInit &a, mgdk_bat *b, int what, bool count_all, GRes &r)
 				GK(8);
 			hipLaunchKernelGGL(k_gaggr_fin, dim3(kk), dim3(256), 0, st, parts.as<GPart>(), nw, kk, ng, acc, maxabs);
 		}
-		else
+		else if (a.gsorted && (what & ~(AGG_SUM | AGG_POS | AGG_MINMAX)) == 0) {
+			// groups are runs of rows: segmented reduction (k_gaggr_sorted)
+			const BUN nw = (a.ci.n + 64 * GS_U - 1) / (64 * GS_U);
+			const dim3 gs(grid_for(nw, 4, 65535u * 16u));
+			const bool sum = (what & AGG_SUM) != 0;
+			const void *vb = (what == 0 && count_all) ? nullptr : b->theap;
+#define GS3(VW_, MM_, POS_) hipLaunchKernelGGL((k_gaggr_sorted<VW_, MM_, POS_>), gs, blk, 0, st, vb, off, a.gids, a.gseq, a.min, ng, a.ci.n, sum, count_all, acc, maxabs)
+#define GS2(VW_) do { if (what & AGG_MINMAX) GS3(VW_, true, false); \
+			else if (what & AGG_POS) GS3(VW_, false, true); \
+			else GS3(VW_, false, false); } while (0)
+			switch (vb ? b->twidth : 0) {
+			case 0: GS2(0); break;
+			case 1: GS2(1); break;
+			case 2: GS2(2); break;
+			case 4: GS2(4); break;
+			case 8: GS2(8); break;
+			default: GS2(16); break;
+			}
+#undef GS2
+#undef GS3
+		} else
 			hipLaunchKernelGGL((k_gaggr<0>), g, blk, 0, st, b->theap, b->twidth, off, a.gids, a.gseq, a.min, ng, a.ci.n, what, count_all, acc, maxabs);
 	}
+	maxabs_out = maxabs;
+	return 0;
+}
+
+int
+run_gaggr(const AggrInit &a, mgdk_bat *b, int what, bool count_all, GRes &r)
+{
+	const BUN ng = a.ngrp;
+	GAcc acc;
+	unsigned long long *maxabs;
+	if (gaggr_device(a, b, what, count_all, acc, maxabs) < 0)
+		return -1;
+	const char *d = (const char *) acc.sum;
+	hipStream_t st = stream();
 	r.sum.resize(ng);
 	r.cnt.resize(ng);
 	r.firstval.resize(ng);
@@ -942,6 +1156,199 @@ run_gaggr(const AggrInit &a, mgdk_bat *b, int what, bool count_all, GRes &r)
 	}
 	r.maxabs = hb[7 * ng];
 	return 0;
+}
+
+// ---- results finished on the device (no per-group host loop: a
+// high-cardinality GROUP BY has as many groups as rows / 4) --------------
+__device__ __forceinline__ void
+put_res_d(void *base, int bt, BUN k, hge v, bool nil)
+{
+	switch (bt) {
+	case MGDK_bte: ((int8_t *) base)[k] = nil ? INT8_MIN : (int8_t) v; break;
+	case MGDK_sht: ((int16_t *) base)[k] = nil ? INT16_MIN : (int16_t) v; break;
+	case MGDK_int: ((int32_t *) base)[k] = nil ? INT32_MIN : (int32_t) v; break;
+	case MGDK_lng: ((int64_t *) base)[k] = nil ? INT64_MIN : (int64_t) v; break;
+	case MGDK_oid: ((uint64_t *) base)[k] = nil ? MGDK_OID_NIL : (uint64_t) v; break;
+	default: ((hge *) base)[k] = nil ? NilOf<hge>::v() : v; break;
+	}
+}
+
+__device__ __forceinline__ hge
+acc_sum(const GAcc &acc, BUN k)
+{
+	return (hge) (((uhge) acc.sum[2 * k + 1] << 64) | acc.sum[2 * k]);
+}
+
+__device__ __forceinline__ void
+or_flags(uint32_t *flags, uint32_t f)
+{
+	f = block_reduce(f, [](uint32_t x, uint32_t y) { return x | y; });
+	if (threadIdx.x == 0)
+		publish_or(flags, f);
+}
+
+// BATgroupsum per group (gdk_aggr.c:429-705): nil without a value, and
+// without skip_nils when a nil came after the first value (one group: any
+// nil); flags bit 0: a group's sum -- itself a prefix -- beyond the type's
+// range (overflow), bit 1: a nil result
+__global__ __launch_bounds__(256) void
+k_gsum_out(GAcc acc, BUN ng, bool empty, int bt, bool skip_nils, hge max, void *out, uint32_t *flags)
+{
+	uint32_t f = 0;
+	for (BUN k = (BUN) blockIdx.x * blockDim.x + threadIdx.x; k < ng; k += (BUN) gridDim.x * blockDim.x) {
+		const hge sv = acc_sum(acc, k);
+		const unsigned long long c = acc.cnt[k];
+		if (sv > max || sv < -max)
+			f |= 1;
+		bool nil;
+		if (empty || c == 0)
+			nil = true;
+		else if (skip_nils)
+			nil = false;
+		else if (ng == 1)
+			nil = acc.lastnil[k] != 0;
+		else
+			nil = acc.lastnil[k] > acc.firstval[k] + 1;
+		put_res_d(out, bt, k, nil ? 0 : sv, nil);
+		f |= nil ? 2u : 0u;
+	}
+	or_flags(flags, f);
+}
+
+__global__ __launch_bounds__(256) void
+k_gcount_out(GAcc acc, BUN ng, long long *out)
+{
+	for (BUN k = (BUN) blockIdx.x * blockDim.x + threadIdx.x; k < ng; k += (BUN) gridDim.x * blockDim.x)
+		out[k] = (long long) acc.cnt[k];
+}
+
+// BATgroupavg3 per group (gdk_aggr.c:1996-2110, rounding :2070-2095)
+// flags bit 1: a nil average, bit 2: a nil remainder / count
+__global__ __launch_bounds__(256) void
+k_gavg3_out(GAcc acc, BUN ng, bool empty, int bt, bool skip_nils, void *avg, long long *rem, long long *cnt,
+	    uint32_t *flags)
+{
+	uint32_t f = 0;
+	for (BUN k = (BUN) blockIdx.x * blockDim.x + threadIdx.x; k < ng; k += (BUN) gridDim.x * blockDim.x) {
+		const unsigned long long n = empty ? 0 : acc.cnt[k];
+		if (!empty && !skip_nils && acc.lastnil[k] != 0) {
+			put_res_d(avg, bt, k, 0, true);
+			rem[k] = INT64_MIN;
+			cnt[k] = INT64_MIN;
+			f |= 6;
+			continue;
+		}
+		cnt[k] = (long long) n;
+		if (n == 0) {
+			put_res_d(avg, bt, k, 0, true);
+			rem[k] = empty ? INT64_MIN : 0;
+			f |= 2;
+			continue;
+		}
+		hge q = acc_sum(acc, k) / (hge) n, m = acc_sum(acc, k) % (hge) n;
+		if (m < 0) {
+			q -= 1;
+			m += (hge) n;
+		}
+		if (m > 0) {
+			if (q < 0) {
+				if (2 * m > (hge) n) { q++; m -= (hge) n; }
+			} else if (2 * m >= (hge) n) {
+				q++;
+				m -= (hge) n;
+			}
+		}
+		put_res_d(avg, bt, k, q, false);
+		rem[k] = (long long) m;
+	}
+	or_flags(flags, f);
+}
+
+// BATgroupavg of integers (AGGR_AVG, gdk_aggr.c:1717): floor average + its
+// remainder as a dbl; flags bit 0: an hge group sum may exceed the 128-bit
+// accumulator, bit 1: a nil result
+__global__ __launch_bounds__(256) void
+k_gavg_out(GAcc acc, BUN ng, bool skip_nils, bool hgein, const unsigned long long *maxabs, double fac,
+	   double *out, long long *cnt, uint32_t *flags)
+{
+	uint32_t f = 0;
+	const unsigned long long cls = *maxabs;
+	for (BUN k = (BUN) blockIdx.x * blockDim.x + threadIdx.x; k < ng; k += (BUN) gridDim.x * blockDim.x) {
+		const unsigned long long n = acc.cnt[k];
+		if (n == 0 || (!skip_nils && acc.lastnil[k] != 0)) {
+			out[k] = __builtin_nan("");
+			cnt[k] = 0;
+			f |= 2;
+			continue;
+		}
+		if (hgein) {
+			// mag_bound(cls) * n >= 2^127, in exact integers
+			const bool big = (cls >> 63) ? (uhge) ((cls & ~(1ull << 63)) + 1) * n >= ((uhge) 1 << 63)
+						     : (uhge) (cls + 1) * n >= ((uhge) 1 << 126);
+			f |= big ? 1u : 0u;
+		}
+		hge q = acc_sum(acc, k) / (hge) n, m = acc_sum(acc, k) % (hge) n;
+		if (m < 0) {
+			q -= 1;
+			m += (hge) n;
+		}
+		double d = hge_to_dbl(q) + (double) (long long) m / (double) (long long) n;
+		if (fac != 1.0)
+			d /= fac;
+		out[k] = d;
+		cnt[k] = (long long) n;
+	}
+	or_flags(flags, f);
+}
+
+// BATgroupavg3combine's result per group from the grouped exact totals and
+// counts (gdk_aggr.c:2702-2716); nall / nnon: rows and non-nil rows per
+// group (NULL: equal); flags bit 1: a nil result
+__global__ __launch_bounds__(256) void
+k_avg3c_out(BUN ng, const hge *S, const hge *C, const long long *nall, const long long *nnon, int bt, void *out,
+	    uint32_t *flags)
+{
+	uint32_t f = 0;
+	const hge NIL = NilOf<hge>::v();
+	for (BUN k = (BUN) blockIdx.x * blockDim.x + threadIdx.x; k < ng; k += (BUN) gridDim.x * blockDim.x) {
+		const hge sv = S[k], cv = C[k];
+		if (sv == NIL || cv == NIL || cv == 0 || (nall && nall[k] != nnon[k])) {
+			put_res_d(out, bt, k, 0, true);
+			f |= 2;
+			continue;
+		}
+		hge q = sv / cv, r = sv % cv;
+		if (r < 0) {
+			q -= 1;
+			r += cv;
+		}
+		if (r > 0 && (q < 0 ? 2 * r > cv : 2 * r >= cv))
+			q += 1;
+		put_res_d(out, bt, k, q, false);
+	}
+	or_flags(flags, f);
+}
+
+// groups of BATgroupmin / max without a value: no non-nil row and no nil
+// row that counts (flags bit 1)
+__global__ __launch_bounds__(256) void
+k_gminmax_nils(GAcc acc, BUN ng, const unsigned long long *firstnil, uint32_t *flags)
+{
+	uint32_t f = 0;
+	for (BUN k = (BUN) blockIdx.x * blockDim.x + threadIdx.x; k < ng; k += (BUN) gridDim.x * blockDim.x)
+		f |= (acc.cnt[k] == 0 && firstnil[k] == ~0ull) ? 2u : 0u;
+	or_flags(flags, f);
+}
+
+// read a 4-byte flag word after the stream has drained
+bool
+read_flags(const void *dev, uint32_t *out)
+{
+	uint32_t *h = (uint32_t *) pinned(16);
+	if (h == nullptr || !hip_ok(hipMemcpyAsync(h, dev, 4, hipMemcpyDeviceToHost, stream()), "memcpy") || !sync())
+		return false;
+	*out = h[0];
+	return true;
 }
 
 // wait = false: the copy is queued from the pinned arena and the caller
@@ -1144,42 +1551,38 @@ mgdk_BATgroupsum(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, boo
 	if (aggr_init(&a, &b, g, e, s) < 0)
 		return nullptr;
 	const BUN ng = a.ngrp;
-	std::vector<char> out(ng * width_of(tp) + 16);
-	GRes r;
-	if (a.ci.n && ng) {
-		if (run_gaggr(a, b, AGG_SUM | (skip_nils ? 0 : AGG_POS), false, r) < 0)
+	mgdk_bat *bn = newbat(ng ? a.min : 0, tp, ng);
+	DevBuf fl(16);
+	if (bn == nullptr || fl.p == nullptr || !hip_ok(hipMemsetAsync(fl.p, 0, 16, stream()), "memset")) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	uint32_t hf = 0;
+	if (ng) {
+		GAcc acc;
+		unsigned long long *mx;
+		if (gaggr_device(a, b, AGG_SUM | (skip_nils ? 0 : AGG_POS), false, acc, mx) < 0) {
+			mgdk_BBPunfix(bn);
 			return nullptr;
-		// overflow: a prefix of one group could exceed max only if
-		// count * max|v| exceeds it
-		const hge max = tmax(tp);
-		for (BUN k = 0; k < ng; k++) {
-			long double bound = mag_bound(r.maxabs) * (long double) r.cnt[k];
-			if (bound > (long double) max && (r.sum[k] > max || r.sum[k] < -max)) {
-				seterr("22003!overflow in sum aggregate.\n");
-				return nullptr;
-			}
+		}
+		hipLaunchKernelGGL(k_gsum_out, dim3(grid_for(ng, 1024, 8192)), dim3(256), 0, stream(), acc, ng, a.ci.n == 0,
+				   basetype(tp), skip_nils, tmax(tp), bn->theap, fl.as<uint32_t>());
+		if (!read_flags(fl.p, &hf)) {
+			mgdk_BBPunfix(bn);
+			return nullptr;
+		}
+		if (hf & 1) {
+			// a prefix of a group could exceed the range only if its final sum
+			// does (the final sum is the last prefix)
+			seterr("22003!overflow in sum aggregate.\n");
+			mgdk_BBPunfix(bn);
+			return nullptr;
 		}
 	}
-	bool hasnil = false;
-	for (BUN k = 0; k < ng; k++) {
-		bool nil;
-		if (a.ci.n == 0 || r.cnt[k] == 0)
-			nil = true;                              // no value: stays nil
-		else if (skip_nils)
-			nil = false;
-		else if (ng == 1)
-			nil = r.lastnil[k] != 0;                 // single group: any nil
-		else
-			nil = r.lastnil[k] > r.firstval[k] + 1;  // a nil after the first value
-		put_vec(out, tp, k, nil ? 0 : r.sum[k], nil);
-		hasnil |= nil;
-	}
-	mgdk_bat *bn = upload_new(ng ? a.min : 0, tp, out.data(), ng);
-	if (bn) {
-		bn->tkey = bn->tsorted = bn->trevsorted = ng <= 1;
-		bn->tnil = hasnil;
-		bn->tnonil = !hasnil;
-	}
+	bn->count = ng;
+	bn->tkey = bn->tsorted = bn->trevsorted = ng <= 1;
+	bn->tnil = (hf & 2) != 0;
+	bn->tnonil = !bn->tnil;
 	return bn;
 }
 
@@ -1197,18 +1600,27 @@ mgdk_BATgroupcount(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, b
 	if (aggr_init(&a, &b, g, e, s) < 0)
 		return nullptr;
 	const BUN ng = a.ngrp;
-	std::vector<long long> out(ng + 1, 0);
-	if (a.ci.n && ng) {
-		GRes r;
+	mgdk_bat *bn = newbat(ng ? a.min : 0, MGDK_lng, ng);
+	if (bn == nullptr)
+		return nullptr;
+	if (ng) {
 		// str offsets are never nil in our heaps; oid via lng width
 		bool all = !skip_nils || b->tnonil || b->ttype == MGDK_str;
-		if (run_gaggr(a, b, 0, all, r) < 0)
+		GAcc acc;
+		unsigned long long *mx;
+		if (gaggr_device(a, b, 0, all, acc, mx) < 0) {
+			mgdk_BBPunfix(bn);
 			return nullptr;
-		for (BUN k = 0; k < ng; k++)
-			out[k] = (long long) r.cnt[k];
+		}
+		hipLaunchKernelGGL(k_gcount_out, dim3(grid_for(ng, 1024, 8192)), dim3(256), 0, stream(), acc, ng,
+				   (long long *) bn->theap);
+		if (!sync()) {
+			mgdk_BBPunfix(bn);
+			return nullptr;
+		}
 	}
-	mgdk_bat *bn = upload_new(ng ? a.min : 0, MGDK_lng, out.data(), ng);
-	if (bn) {
+	bn->count = ng;
+	{
 		// gdk_aggr.c:3105-3106 (empty: BATconstant of 0), :3185-3190
 		bn->tnonil = 1;
 		bn->tnil = 0;
@@ -1361,41 +1773,32 @@ mgdk_BATgroupavg(mgdk_bat **bnp, mgdk_bat **cntsp, mgdk_bat *b, mgdk_bat *g, mgd
 		for (BUN k = 0; k < ng; k++)
 			nils |= hc[k] == 0;
 	} else {
-		GRes r;
-		if (run_gaggr(a, b, AGG_SUM | (skip_nils ? 0 : AGG_POS), false, r) < 0)
-			return -1;
-		std::vector<double> d(ng + 1);
-		std::vector<long long> c(ng + 1);
-		for (BUN k = 0; k < ng; k++) {
-			const unsigned long long n = r.cnt[k];
-			if (n == 0 || (!skip_nils && r.lastnil[k] != 0)) {
-				d[k] = __builtin_nan("");
-				c[k] = 0;
-				nils = true;
-				continue;
-			}
-			if (bt == MGDK_hge && mag_bound(r.maxabs) * (long double) n >= ldexpl(1.0L, 127)) {
-				seterr("42000!BATgroupavg: hge group sum exceeds the 128-bit device accumulator\n");
-				return -1;
-			}
-			// AVERAGE_ITER's invariant: avg * n + rem == sum, 0 <= rem < n
-			hge q = r.sum[k] / (hge) n, m = r.sum[k] % (hge) n;
-			if (m < 0) {
-				q -= 1;
-				m += (hge) n;
-			}
-			d[k] = (double) q + (double) (long long) m / (double) (long long) n;
-			if (scale != 0)
-				d[k] /= fac;
-			c[k] = (long long) n;
+		// AVERAGE_ITER's invariant: avg * n + rem == sum, 0 <= rem < n
+		bn = newbat(hb, MGDK_dbl, ng);
+		cn = newbat(hb, MGDK_lng, ng);
+		DevBuf fl(16);
+		GAcc acc;
+		unsigned long long *mx = nullptr;
+		uint32_t hf = 0;
+		bool ok = bn && cn && fl.p && hip_ok(hipMemsetAsync(fl.p, 0, 16, st), "memset") &&
+			  gaggr_device(a, b, AGG_SUM | (skip_nils ? 0 : AGG_POS), false, acc, mx) == 0;
+		if (ok) {
+			hipLaunchKernelGGL(k_gavg_out, dim3(grid_for(ng, 1024, 8192)), dim3(256), 0, st, acc, ng, skip_nils,
+					   bt == MGDK_hge, mx, scale != 0 ? fac : 1.0, (double *) bn->theap,
+					   (long long *) cn->theap, fl.as<uint32_t>());
+			ok = read_flags(fl.p, &hf);
 		}
-		bn = upload_new(hb, MGDK_dbl, d.data(), ng);
-		cn = upload_new(hb, MGDK_lng, c.data(), ng);
-		if (!bn || !cn) {
+		if (ok && (hf & 1)) {
+			seterr("42000!BATgroupavg: hge group sum exceeds the 128-bit device accumulator\n");
+			ok = false;
+		}
+		if (!ok) {
 			mgdk_BBPunfix(bn);
 			mgdk_BBPunfix(cn);
 			return -1;
 		}
+		bn->count = cn->count = ng;
+		nils = (hf & 2) != 0;
 	}
 	bn->tkey = bn->tsorted = bn->trevsorted = ng <= 1;
 	bn->tnil = nils;
@@ -1480,49 +1883,37 @@ mgdk_BATgroupavg3combine(mgdk_bat *avg, mgdk_bat *rem, mgdk_bat *cnt, mgdk_bat *
 		C = mgdk_BATgroupsum(Cb, g, e, nullptr, MGDK_hge, true);
 		if (!S || !C)
 			goto out;
-		std::vector<unsigned long long> hs(2 * ng), hc(2 * ng);
-		std::vector<long long> nall(ng), nnon(ng);
+		mgdk_bat *N1 = nullptr, *N2 = nullptr;
 		if (!skip_nils && !avg->tnonil) {
-			mgdk_bat *N1 = mgdk_BATgroupcount(avg, g, e, nullptr, MGDK_lng, false);
-			mgdk_bat *N2 = N1 ? mgdk_BATgroupcount(avg, g, e, nullptr, MGDK_lng, true) : nullptr;
-			bool ok = N1 && N2 &&
-				  hip_ok(hipMemcpyAsync(nall.data(), N1->theap, ng * 8, hipMemcpyDeviceToHost, st), "memcpy") &&
-				  hip_ok(hipMemcpyAsync(nnon.data(), N2->theap, ng * 8, hipMemcpyDeviceToHost, st), "memcpy") &&
-				  sync();
-			mgdk_BBPunfix(N1);
-			mgdk_BBPunfix(N2);
-			if (!ok)
+			N1 = mgdk_BATgroupcount(avg, g, e, nullptr, MGDK_lng, false);
+			N2 = N1 ? mgdk_BATgroupcount(avg, g, e, nullptr, MGDK_lng, true) : nullptr;
+			if (!N1 || !N2) {
+				mgdk_BBPunfix(N1);
+				mgdk_BBPunfix(N2);
 				goto out;
+			}
 		}
-		if (!hip_ok(hipMemcpyAsync(hs.data(), S->theap, ng * 16, hipMemcpyDeviceToHost, st), "memcpy") ||
-		    !hip_ok(hipMemcpyAsync(hc.data(), C->theap, ng * 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+		bn = newbat(a.min, tp, ng);
+		uint32_t hf = 0;
+		bool ok = bn && hip_ok(hipMemsetAsync(fl.p, 0, 16, st), "memset");
+		if (ok) {
+			hipLaunchKernelGGL(k_avg3c_out, dim3(grid_for(ng, 1024, 8192)), dim3(256), 0, st, ng,
+					   (const hge *) S->theap, (const hge *) C->theap,
+					   N1 ? (const long long *) N1->theap : nullptr,
+					   N2 ? (const long long *) N2->theap : nullptr, basetype(tp), bn->theap, fl.as<uint32_t>());
+			ok = read_flags(fl.p, &hf);
+		}
+		mgdk_BBPunfix(N1);
+		mgdk_BBPunfix(N2);
+		if (!ok) {
+			mgdk_BBPunfix(bn);
+			bn = nullptr;
 			goto out;
-		std::vector<char> out(ng * width_of(tp) + 16);
-		bool nils = false;
-		const hge NIL = NilOf<hge>::v();
-		for (BUN k = 0; k < ng; k++) {
-			const hge sv = (hge) (((uhge) hs[2 * k + 1] << 64) | hs[2 * k]);
-			const hge cv = (hge) (((uhge) hc[2 * k + 1] << 64) | hc[2 * k]);
-			if (sv == NIL || cv == NIL || cv == 0 || nall[k] != nnon[k]) {
-				put_vec(out, tp, k, 0, true);
-				nils = true;
-				continue;
-			}
-			hge q = sv / cv, r = sv % cv;
-			if (r < 0) {
-				q -= 1;
-				r += cv;
-			}
-			if (r > 0 && (q < 0 ? 2 * r > cv : 2 * r >= cv))
-				q += 1;
-			put_vec(out, tp, k, q, false);
 		}
-		bn = upload_new(a.min, tp, out.data(), ng);
-		if (bn) {
-			bn->tnil = nils;
-			bn->tnonil = !nils;
-			bn->tkey = bn->tsorted = bn->trevsorted = ng <= 1;
-		}
+		bn->count = ng;
+		bn->tnil = (hf & 2) != 0;
+		bn->tnonil = !bn->tnil;
+		bn->tkey = bn->tsorted = bn->trevsorted = ng <= 1;
 	}
 out:
 	mgdk_BBPunfix(T);
@@ -1547,51 +1938,40 @@ mgdk_BATgroupavg3(mgdk_bat **avgp, mgdk_bat **remp, mgdk_bat **cntp, mgdk_bat *b
 		return -1;
 	const BUN ng = a.ngrp;
 	const int tp = b->ttype;
-	GRes r;
-	if (a.ci.n && ng && run_gaggr(a, b, AGG_SUM | (skip_nils ? 0 : AGG_POS), false, r) < 0)
-		return -1;
-	std::vector<char> av(ng * width_of(tp) + 16);
-	std::vector<long long> rem(ng + 1), cnt(ng + 1);
-	for (BUN k = 0; k < ng; k++) {
-		unsigned long long n = a.ci.n ? r.cnt[k] : 0;
-		bool nil = a.ci.n && !skip_nils && r.lastnil[k] != 0;
-		if (nil) {
-			put_vec(av, tp, k, 0, true);
-			rem[k] = INT64_MIN;
-			cnt[k] = INT64_MIN;
-			continue;
+	const oid hb = ng ? a.min : 0;
+	mgdk_bat *A = newbat(hb, tp, ng), *R = newbat(hb, MGDK_lng, ng), *C = newbat(hb, MGDK_lng, ng);
+	DevBuf fl(16);
+	uint32_t hf = 0;
+	bool ok = A && R && C && fl.p && hip_ok(hipMemsetAsync(fl.p, 0, 16, stream()), "memset");
+	if (ok && ng) {
+		GAcc acc;
+		unsigned long long *mx;
+		ok = gaggr_device(a, b, AGG_SUM | (skip_nils ? 0 : AGG_POS), false, acc, mx) == 0;
+		if (ok) {
+			hipLaunchKernelGGL(k_gavg3_out, dim3(grid_for(ng, 1024, 8192)), dim3(256), 0, stream(), acc, ng,
+					   a.ci.n == 0, basetype(tp), skip_nils, A->theap, (long long *) R->theap,
+					   (long long *) C->theap, fl.as<uint32_t>());
+			ok = read_flags(fl.p, &hf);
 		}
-		cnt[k] = (long long) n;
-		if (n == 0) {
-			put_vec(av, tp, k, 0, true);
-			rem[k] = a.ci.n ? 0 : INT64_MIN;
-			continue;
-		}
-		hge S = r.sum[k], q = S / (hge) n, m = S % (hge) n;
-		if (m < 0) {
-			q -= 1;
-			m += (hge) n;
-		}
-		if (m > 0) {
-			if (q < 0) {
-				if (2 * m > (hge) n) { q++; m -= (hge) n; }
-			} else if (2 * m >= (hge) n) {
-				q++;
-				m -= (hge) n;
-			}
-		}
-		put_vec(av, tp, k, q, false);
-		rem[k] = (long long) m;
 	}
-	mgdk_bat *A = upload_new(ng ? a.min : 0, tp, av.data(), ng, false);
-	mgdk_bat *R = A ? upload_new(ng ? a.min : 0, MGDK_lng, rem.data(), ng, false) : nullptr;
-	mgdk_bat *C = R ? upload_new(ng ? a.min : 0, MGDK_lng, cnt.data(), ng) : nullptr;
-	if (!A || !R || !C) {
+	if (!ok) {
 		mgdk_BBPunfix(A);
 		mgdk_BBPunfix(R);
 		mgdk_BBPunfix(C);
 		return -1;
 	}
+	A->count = R->count = C->count = ng;
+	// gdk_aggr.c:2012-2027 (no candidates: constants nil / nil / 0), :2298-2303
+	const bool empty = a.ci.n == 0;
+	A->tnil = (hf & 2) != 0;
+	R->tnil = empty ? ng > 0 : (hf & 4) != 0;
+	C->tnil = !empty && (hf & 4) != 0;
+	A->tnonil = !A->tnil;
+	R->tnonil = !R->tnil;
+	C->tnonil = !C->tnil;
+	A->tkey = R->tkey = C->tkey = empty ? ng <= 1 : ng == 1;
+	A->tsorted = R->tsorted = C->tsorted = empty || ng == 1;
+	A->trevsorted = R->trevsorted = C->trevsorted = empty || ng == 1;
 	*avgp = A;
 	*remp = R;
 	*cntp = C;
@@ -1668,19 +2048,16 @@ groupminmax(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, bool skip_nils, 
 		bn->tnonil = ng == 0;
 		return bn;
 	}
-	GRes r;
-	if (run_gaggr(a, b, AGG_MINMAX, false, r) < 0) {
+	GAcc acc;
+	unsigned long long *mxa;
+	if (gaggr_device(a, b, AGG_MINMAX, false, acc, mxa) < 0) {
 		mgdk_BBPunfix(bn);
 		return nullptr;
 	}
 	hipStream_t st = stream();
-	DevBuf tgt(ng * 8 + 8), fn(ng * 8 + 8), fb(ng * 8 + 8);
-	std::vector<long long> t(ng);
-	BUN nils = 0;
-	for (BUN k = 0; k < ng; k++)
-		t[k] = domax ? r.mx[k] : r.mn[k];
-	if (!tgt.p || !fn.p || !fb.p ||
-	    !hip_ok(hipMemcpyAsync(tgt.p, t.data(), ng * 8, hipMemcpyHostToDevice, st), "memcpy") ||
+	DevBuf fn(ng * 8 + 8), fb(ng * 8 + 8), fl(16);
+	const long long *tgt = domax ? acc.mx : acc.mn;     // each group's extreme value
+	if (!fn.p || !fb.p || !fl.p || !hip_ok(hipMemsetAsync(fl.p, 0, 16, st), "memset") ||
 	    !hip_ok(hipMemsetAsync(fn.p, 0xff, ng * 8, st), "memset") ||
 	    !hip_ok(hipMemsetAsync(fb.p, 0xff, ng * 8, st), "memset")) {
 		mgdk_BBPunfix(bn);
@@ -1688,7 +2065,7 @@ groupminmax(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, bool skip_nils, 
 	}
 	const oid off = a.ci.seq - b->hseqbase;
 	hipLaunchKernelGGL(k_gminmax_pos, dim3(grid_for(a.ci.n, 256 * 8, 256 * 16)), dim3(256), 0, st, b->theap,
-			   b->twidth, off, a.gids, a.gseq, a.min, ng, a.ci.n, skip_nils, tgt.as<long long>(),
+			   b->twidth, off, a.gids, a.gseq, a.min, ng, a.ci.n, skip_nils, tgt,
 			   fn.as<unsigned long long>(), fb.as<unsigned long long>());
 	hipLaunchKernelGGL(k_gminmax_out, dim3(grid_for(ng, 256, 4096)), dim3(256), 0, st, ng,
 			   fn.as<unsigned long long>(), fb.as<unsigned long long>(), c0.dense, c0.seq, c0.oids,
@@ -1698,15 +2075,15 @@ groupminmax(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, bool skip_nils, 
 		return nullptr;
 	}
 	// groups without a value: no non-nil row and (skip_nils or no nil row)
-	std::vector<unsigned long long> hn(ng);
-	if (!hip_ok(hipMemcpyAsync(hn.data(), fn.p, ng * 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
+	hipLaunchKernelGGL(k_gminmax_nils, dim3(grid_for(ng, 1024, 8192)), dim3(256), 0, st, acc, ng,
+			   fn.as<unsigned long long>(), fl.as<uint32_t>());
+	uint32_t hf = 0;
+	if (!read_flags(fl.p, &hf)) {
 		mgdk_BBPunfix(bn);
 		return nullptr;
 	}
-	for (BUN k = 0; k < ng; k++)
-		nils += r.cnt[k] == 0 && hn[k] == ~0ull;
-	bn->tnil = nils != 0;
-	bn->tnonil = nils == 0;
+	bn->tnil = (hf & 2) != 0;
+	bn->tnonil = !bn->tnil;
 	return bn;
 }
 

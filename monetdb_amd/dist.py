@@ -181,10 +181,18 @@ class GdkBackend:
         return self.gdk.BAT.dense(tseq, n)
 
     def addcst(self, c, v):
-        """c + v as lng (bounds oids to global row numbers)"""
+        """c + v as lng (bounds oids to global row numbers).  An oid column
+        of row numbers (< 2^63, no nils) has the bits of the same lng values:
+        it is relabelled through a view of its heap, not converted, and v == 0
+        needs no pass at all."""
         g = self.gdk
-        if c.ttype != g.TYPE_lng:        # batcalc refuses oid arithmetic: convert first
+        if c.ttype == g.TYPE_oid and c.s.tnonil:
+            c = g.BATslice(c, 0, c.count())
+            c.s.ttype = g.TYPE_lng
+        elif c.ttype != g.TYPE_lng:      # batcalc refuses oid arithmetic: convert first
             c = g.BATconvert(c, None, g.TYPE_lng)
+        if v == 0:
+            return c
         return g.BATcalcaddcst(c, v, g.TYPE_lng, g.TYPE_lng)
 
     # -- operators -----------------------------------------------------------
@@ -214,7 +222,14 @@ class GdkBackend:
         return self.gdk.BATjoin(l, r)
 
     def sort(self, c, reverse=False):
-        s, o, _ = self.gdk.BATsort(c, reverse=reverse, nilslast=reverse)
+        # an ordered column is found out first (one read; BATordered records
+        # it) so BATsort takes its trivial path (gdk_batop.c:2422-2472):
+        # the exchange steps often sort what is sorted already
+        if reverse:
+            self.gdk.BATordered_rev(c)
+        else:
+            self.gdk.BATordered(c)
+        s, o, _ = self.gdk.BATsort(c, reverse=reverse, nilslast=reverse, groups=False)
         return s, o
 
     def order_info(self, c):

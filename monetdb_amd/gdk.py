@@ -574,9 +574,9 @@ def BATordered_rev(b):
     return bool(lib().mgdk_BATordered_rev(b.ptr))
 
 
-def BATsort(b, o=None, g=None, reverse=False, nilslast=False, stable=True):
+def BATsort(b, o=None, g=None, reverse=False, nilslast=False, stable=True, groups=True):
     sp, op, gp = P(), P(), P()
-    _chk(lib().mgdk_BATsort(C.byref(sp), C.byref(op), C.byref(gp), b.ptr, _p(o), _p(g),
+    _chk(lib().mgdk_BATsort(C.byref(sp), C.byref(op), C.byref(gp) if groups else None, b.ptr, _p(o), _p(g),
                             reverse, nilslast, stable))
     return BAT(sp), BAT(op), (BAT(gp) if gp else None)
 
