@@ -1019,17 +1019,25 @@ aggr_init(AggrInit *a, mgdk_bat **bp, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s)
 
 // accumulator block of run_gaggr: sums and counts 0, first positions ~0,
 // last-nil 0, min / max at their identities, the magnitude class 0
+// (only the quantities `what` asks for: with as many groups as rows / 4 the
+// block is as large as the column)
 __global__ __launch_bounds__(256) void
-k_gacc_init(GAcc acc, BUN ng, unsigned long long *maxabs)
+k_gacc_init(GAcc acc, BUN ng, unsigned long long *maxabs, int what)
 {
 	for (BUN k = (BUN) blockIdx.x * blockDim.x + threadIdx.x; k < ng; k += (BUN) gridDim.x * blockDim.x) {
-		acc.sum[2 * k] = 0;
-		acc.sum[2 * k + 1] = 0;
+		if (what & AGG_SUM) {
+			acc.sum[2 * k] = 0;
+			acc.sum[2 * k + 1] = 0;
+		}
 		acc.cnt[k] = 0;
-		acc.firstval[k] = ~0ull;
-		acc.lastnil[k] = 0;
-		acc.mn[k] = INT64_MAX;
-		acc.mx[k] = INT64_MIN;
+		if (what & AGG_POS) {
+			acc.firstval[k] = ~0ull;
+			acc.lastnil[k] = 0;
+		}
+		if (what & AGG_MINMAX) {
+			acc.mn[k] = INT64_MAX;
+			acc.mx[k] = INT64_MIN;
+		}
 	}
 	if (blockIdx.x == 0 && threadIdx.x == 0)
 		*maxabs = 0;
@@ -1045,7 +1053,8 @@ struct GRes {
 // the grouped accumulators on the device (the thread's scratch buffer:
 // valid until its next scratch() user), no read-back
 int
-gaggr_device(const AggrInit &a, mgdk_bat *b, int what, bool count_all, GAcc &acc, unsigned long long *&maxabs_out)
+gaggr_device(const AggrInit &a, mgdk_bat *b, int what, bool count_all, GAcc &acc, unsigned long long *&maxabs_out,
+	     bool full_init = false)
 {
 	const BUN ng = a.ngrp;
 	size_t bytes = ng * (16 + 8 * 5) + 64;
@@ -1063,7 +1072,10 @@ gaggr_device(const AggrInit &a, mgdk_bat *b, int what, bool count_all, GAcc &acc
 	// one init launch, one read-back of the whole accumulator block and one
 	// wait: the operator's host round trips, not its kernels, dominated
 	// small-group aggregates
-	hipLaunchKernelGGL(k_gacc_init, dim3(grid_for(ng + 1, 256, 1024)), dim3(256), 0, st, acc, ng, maxabs);
+	// the host read-back (run_gaggr) copies the whole block: all of it
+	// initialised there
+	hipLaunchKernelGGL(k_gacc_init, dim3(grid_for(ng + 1, 1024, 8192)), dim3(256), 0, st, acc, ng, maxabs,
+			   full_init ? (AGG_SUM | AGG_POS | AGG_MINMAX) : what);
 	const oid off = a.ci.seq - b->hseqbase;
 	dim3 g(grid_for(a.ci.n, 256 * 8, 256 * 16)), blk(256);
 	// COUNT(*) over few groups needs no values (k_gaggr_k's base == NULL)
@@ -1130,7 +1142,7 @@ run_gaggr(const AggrInit &a, mgdk_bat *b, int what, bool count_all, GRes &r)
 	const BUN ng = a.ngrp;
 	GAcc acc;
 	unsigned long long *maxabs;
-	if (gaggr_device(a, b, what, count_all, acc, maxabs) < 0)
+	if (gaggr_device(a, b, what, count_all, acc, maxabs, true) < 0)
 		return -1;
 	const char *d = (const char *) acc.sum;
 	hipStream_t st = stream();

@@ -245,6 +245,12 @@ k_range_tile(WArgs a)
 #ifndef MGDK_WIN_FH
 #define MGDK_WIN_FH 256
 #endif
+#ifndef MGDK_WIN_NT
+#define MGDK_WIN_NT 0
+#endif
+#ifndef MGDK_WIN_XCD
+#define MGDK_WIN_XCD 1
+#endif
 constexpr int FR = MGDK_WIN_FR;          // rows per lane
 constexpr int FT = 256 * FR;             // rows per tile
 constexpr int FH = MGDK_WIN_FH;          // halo rows
@@ -786,6 +792,148 @@ k_range_keys(FArgs a)
 	}
 }
 
+// ---------------------------------------------------------------------------
+// Lean kernel for the common tile of wide values (lng, tmax >= 2^32): no
+// nil and no partition start after the stage's first row, values within
+// 2^31 of the stage's first value (else the tile is listed for the 64-bit
+// kernel).  The general kernels above issue ~2.4 VALU wave-instructions per
+// row (PMC: 2.44e9 for 1e9 rows = 4.0 ms of VALU issue on 1024 SIMDs -- the
+// whole kernel time).  Here each row's bound is one BRANCHLESS binary search
+// over the whole stage, padded to a power of two with keys above every
+// threshold: a fixed number of steps, each an LDS read at an immediate
+// offset, a compare and a select -- no divergent loop and its exec-mask
+// SALU traffic (a per-lane walk measured 1.9e9 SALU + 1.5e9 VALU and was
+// slower).  On ordered keys the search over the whole stage equals the
+// frame bound (the row's own key satisfies its threshold); on unordered
+// keys the result is discarded because the order flags send the column to
+// the walk.  Rows map to lanes consecutively, so key reads and bound
+// writes are conflict-free and coalesced.
+// ---------------------------------------------------------------------------
+constexpr int FSP = FS <= 2048 ? 2048 : FS <= 4096 ? 4096 : 8192;   // padded stage
+static_assert(FS < FSP, "the stage needs one pad key");
+
+template <bool PREC, bool DESC>
+__global__ __launch_bounds__(256) void
+k_range_k32(FArgs a)
+{
+	__shared__ __attribute__((aligned(16))) uint32_t sk[FSP];
+	__shared__ uint32_t s_ord;
+	const int tid = threadIdx.x, lane = __lane_id();
+#if MGDK_WIN_XCD
+	// XCD-aware order: workgroups go round-robin over the 8 XCDs, so XCD x
+	// gets a consecutive run of tiles and a tile's halo was staged by the
+	// previous workgroup on the same L2
+	const uint32_t per = gridDim.x / 8, rem = gridDim.x % 8, x = blockIdx.x % 8;
+	const uint32_t tile = x * per + (x < rem ? x : rem) + blockIdx.x / 8;
+#else
+	const uint32_t tile = blockIdx.x;
+#endif
+	const BUN t0 = (BUN) tile * FT;
+	const BUN t1 = t0 + FT < a.n ? t0 + FT : a.n;
+	const BUN lo = PREC ? (t0 > FH ? t0 - FH : 0) : t0;
+	const BUN hi = PREC ? (t1 + 1 < a.n ? t1 + 1 : a.n) : (t1 + FH < a.n ? t1 + FH : a.n);
+	const int S = (int) (hi - lo);
+	if (tid == 0)
+		s_ord = 0;
+	const int64_t base = a.b[lo];
+	constexpr int NB = (FS + 255) / 256;
+	int64_t tv[NB];
+#pragma unroll
+	for (int u = 0; u < NB; u++) {
+		const int i = tid + u * 256;
+		tv[u] = a.b[lo + (i < S ? i : S - 1)];
+	}
+	constexpr int NW = (FS + 3 + 1023) / 1024;
+	uint32_t tw[NW];
+#pragma unroll
+	for (int u = 0; u < NW; u++)
+		tw[u] = flags_word(a, lo, tid + u * 256, S);
+	bool bad = false;
+#pragma unroll
+	for (int u = 0; u < NB; u++) {
+		const int i = tid + u * 256;
+		const uint64_t d = DESC ? (uint64_t) base - (uint64_t) tv[u] : (uint64_t) tv[u] - (uint64_t) base;
+		bad |= i < S && (tv[u] == INT64_MIN || d >= 0x80000000ull);
+		if (i < S)
+			sk[i] = (uint32_t) d;
+	}
+	for (int i = S + tid; i < FSP; i += 256)
+		sk[i] = 0xffffffffu;                // above every threshold
+#pragma unroll
+	for (int u = 0; u < NW; u++)
+		bad |= (tw[u] & (tid + u * 256 == 0 ? ~0xffu : ~0u)) != 0;   // a start after row 0
+	if (__syncthreads_or(bad)) {
+		if (tid == 0)
+			a.relist[atomicAdd(&a.flags[4], 1u)] = tile;
+		return;
+	}
+	const int NA = (int) (t1 - t0), xa = (int) (t0 - lo);
+	// thresholds stay below the pad key: valid keys are < 2^31
+	const uint32_t lim = (uint64_t) a.limit < 0xfffffffeull ? (uint32_t) a.limit : 0xfffffffeu;
+	// the FR searches of a lane run interleaved (independent LDS reads in
+	// flight); rows past the tile's end search a clamped row and store nothing
+	uint32_t key[FR], t[FR], pos[FR];
+#pragma unroll
+	for (int u = 0; u < FR; u++) {
+		const int r = tid + u * 256;
+		key[u] = sk[xa + (r < NA ? r : NA - 1)];
+		if (PREC)
+			t[u] = key[u] > lim ? key[u] - lim : 0u;
+		else
+			t[u] = 0xfffffffeu - key[u] > lim ? key[u] + lim : 0xfffffffeu;
+		pos[u] = 0;
+	}
+#pragma unroll
+	for (int h = FSP / 2; h >= 1; h >>= 1) {
+#pragma unroll
+		for (int u = 0; u < FR; u++) {
+			const uint32_t v = sk[pos[u] + h - 1];
+			// PREC: lower bound (first j with sk[j] >= key - limit);
+			// else upper bound (first j with sk[j] > key + limit)
+			pos[u] += (PREC ? v < t[u] : v <= t[u]) ? h : 0;
+		}
+	}
+	uint32_t ord = 0;
+#pragma unroll
+	for (int u = 0; u < FR; u++) {
+		const int r = tid + u * 256;
+		if (r >= NA)
+			break;
+		const int xk = xa + r;
+		const int b = (int) pos[u];
+		const BUN row = t0 + (BUN) r;
+		const bool unres = PREC ? (b == 0 && lo > 0) : (b >= S && hi < a.n);
+		if (unres) {
+			const uint32_t at = atomicAdd(&a.flags[2], 1u);
+			if (at < a.unres_cap)
+				a.unres[at] = row;
+		}
+#if MGDK_WIN_NT
+		__builtin_nontemporal_store(lo + (BUN) (b < S ? b : S), &a.out[row]);
+#else
+		a.out[row] = lo + (BUN) (b < S ? b : S);
+#endif
+		if (row + 1 < a.n) {
+			const uint32_t y = sk[xk + 1];
+			if (y < key[u])
+				ord |= DESC ? 2u : 1u;
+			if (!DESC && y > key[u])
+				ord |= 2u;
+		}
+	}
+#pragma unroll
+	for (int q = 32; q > 0; q >>= 1)
+		ord |= __shfl_xor(ord, q);
+	if (lane == 0 && ord)
+		atomicOr(&s_ord, ord);
+	__syncthreads();
+	if (tid == 0 && s_ord) {
+		const uint32_t seen = __hip_atomic_load(&a.flags[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		if (s_ord & ~seen)
+			atomicOr(&a.flags[1], s_ord);
+	}
+}
+
 // fix-up of the rows k_range_fast could not resolve inside its stage
 __global__ __launch_bounds__(256) void
 k_range_fix(WArgs a, const oid *rows, uint32_t nrows)
@@ -962,7 +1110,26 @@ mgdk::range_bounds_int64(mgdk_bat *r, const int64_t *bvals, const mgdk_bat *p, B
 			if (all) RK(KT, G_, false, false, true); \
 			else if (f.desc) RK(KT, G_, false, true, false); \
 			else RK(KT, G_, false, false, false); } } while (0)
-		if (narrow) {
+		static const bool lean = getenv("MGDK_WIN_LEAN") ? atoi(getenv("MGDK_WIN_LEAN")) != 0 : true;
+		if (narrow && lean && !all && tmax >= KMAXREL) {
+			// wide values (lng): the lean kernel, its left-over tiles below
+			if (preceding) {
+				if (f.desc)
+					hipLaunchKernelGGL((k_range_k32<true, true>), dim3(ftiles), blk, 0, st, f);
+				else
+					hipLaunchKernelGGL((k_range_k32<true, false>), dim3(ftiles), blk, 0, st, f);
+			} else {
+				if (f.desc)
+					hipLaunchKernelGGL((k_range_k32<false, true>), dim3(ftiles), blk, 0, st, f);
+				else
+					hipLaunchKernelGGL((k_range_k32<false, false>), dim3(ftiles), blk, 0, st, f);
+			}
+			if (!hip_ok(hipMemcpyAsync(h, fl.p, 32, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+				return -1;
+			f.tiles = rl.as<uint32_t>();
+			if (h[4])
+				RKA(uint64_t, h[4]);
+		} else if (narrow) {
 			RKA(uint32_t, ftiles);
 			if (!hip_ok(hipMemcpyAsync(h, fl.p, 32, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
 				return -1;
