@@ -246,7 +246,7 @@ k_range_tile(WArgs a)
 #define MGDK_WIN_FH 256
 #endif
 #ifndef MGDK_WIN_NT
-#define MGDK_WIN_NT 0
+#define MGDK_WIN_NT 1
 #endif
 #ifndef MGDK_WIN_XCD
 #define MGDK_WIN_XCD 1
