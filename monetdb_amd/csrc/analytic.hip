@@ -794,9 +794,8 @@ k_range_keys(FArgs a)
 
 // ---------------------------------------------------------------------------
 // Lean kernel for the common tile of wide values (lng, tmax >= 2^32): no
-// nil and no partition start after the stage's first row, values within
-// 2^31 of the stage's first value (else the tile is listed for the 64-bit
-// kernel).  The general kernels above issue ~2.4 VALU wave-instructions per
+// nil, at most 16 partition starts in the stage, values within 2^31 of the
+// stage's first value (else the tile is listed for the 64-bit kernel).  The general kernels above issue ~2.4 VALU wave-instructions per
 // row (PMC: 2.44e9 for 1e9 rows = 4.0 ms of VALU issue on 1024 SIMDs -- the
 // whole kernel time).  Here each row's bound is one BRANCHLESS binary search
 // over the whole stage, padded to a power of two with keys above every
@@ -816,8 +815,11 @@ template <bool PREC, bool DESC>
 __global__ __launch_bounds__(256) void
 k_range_k32(FArgs a)
 {
+	constexpr int LST = 16;
 	__shared__ __attribute__((aligned(16))) uint32_t sk[FSP];
 	__shared__ uint32_t s_ord;
+	__shared__ int s_nst;
+	__shared__ int s_st[LST];
 	const int tid = threadIdx.x, lane = __lane_id();
 #if MGDK_WIN_XCD
 	// XCD-aware order: workgroups go round-robin over the 8 XCDs, so XCD x
@@ -859,10 +861,32 @@ k_range_k32(FArgs a)
 	}
 	for (int i = S + tid; i < FSP; i += 256)
 		sk[i] = 0xffffffffu;                // above every threshold
-#pragma unroll
-	for (int u = 0; u < NW; u++)
-		bad |= (tw[u] & (tid + u * 256 == 0 ? ~0xffu : ~0u)) != 0;   // a start after row 0
+	if (tid == 0)
+		s_nst = 0;
 	if (__syncthreads_or(bad)) {
+		if (tid == 0)
+			a.relist[atomicAdd(&a.flags[4], 1u)] = tile;
+		return;
+	}
+	// partition starts after the stage's first row: at most LST of them are
+	// listed; a row's search is then confined to its partition
+#pragma unroll
+	for (int u = 0; u < NW; u++) {
+		uint32_t wd = tw[u] & (tid + u * 256 == 0 ? ~0xffu : ~0u);
+		while (wd) {
+			const int by = __builtin_ctz(wd) >> 3;
+			const int pos = 4 * (tid + u * 256) + by;
+			if (pos < S) {
+				const int at = atomicAdd(&s_nst, 1);
+				if (at < LST)
+					s_st[at] = pos;
+			}
+			wd &= ~(0xffu << (8 * by));
+		}
+	}
+	__syncthreads();
+	const int nst = s_nst;
+	if (nst > LST) {
 		if (tid == 0)
 			a.relist[atomicAdd(&a.flags[4], 1u)] = tile;
 		return;
@@ -883,14 +907,47 @@ k_range_k32(FArgs a)
 			t[u] = 0xfffffffeu - key[u] > lim ? key[u] + lim : 0xfffffffeu;
 		pos[u] = 0;
 	}
+	// the row's partition within the stage: [ps, pe)
+	int ps[FR], pe[FR];
 #pragma unroll
-	for (int h = FSP / 2; h >= 1; h >>= 1) {
+	for (int u = 0; u < FR; u++) {
+		ps[u] = 0;
+		pe[u] = S;
+	}
+	if (nst == 0) {
+#pragma unroll
+		for (int h = FSP / 2; h >= 1; h >>= 1) {
+#pragma unroll
+			for (int u = 0; u < FR; u++) {
+				const uint32_t v = sk[pos[u] + h - 1];
+				// PREC: lower bound (first j with sk[j] >= key - limit);
+				// else upper bound (first j with sk[j] > key + limit)
+				pos[u] += (PREC ? v < t[u] : v <= t[u]) ? h : 0;
+			}
+		}
+	} else {
 #pragma unroll
 		for (int u = 0; u < FR; u++) {
-			const uint32_t v = sk[pos[u] + h - 1];
-			// PREC: lower bound (first j with sk[j] >= key - limit);
-			// else upper bound (first j with sk[j] > key + limit)
-			pos[u] += (PREC ? v < t[u] : v <= t[u]) ? h : 0;
+			const int r = tid + u * 256;
+			const int xk = xa + (r < NA ? r : NA - 1);
+			for (int i = 0; i < nst; i++) {
+				const int st = s_st[i];
+				if (st <= xk)
+					ps[u] = st > ps[u] ? st : ps[u];
+				else
+					pe[u] = st < pe[u] ? st : pe[u];
+			}
+		}
+		// the predicate is true before ps and false from pe on
+#pragma unroll
+		for (int h = FSP / 2; h >= 1; h >>= 1) {
+#pragma unroll
+			for (int u = 0; u < FR; u++) {
+				const int j = (int) pos[u] + h - 1;
+				const uint32_t v = sk[j];
+				const bool c = j < ps[u] || (j < pe[u] && (PREC ? v < t[u] : v <= t[u]));
+				pos[u] += c ? h : 0;
+			}
 		}
 	}
 	uint32_t ord = 0;
@@ -902,7 +959,7 @@ k_range_k32(FArgs a)
 		const int xk = xa + r;
 		const int b = (int) pos[u];
 		const BUN row = t0 + (BUN) r;
-		const bool unres = PREC ? (b == 0 && lo > 0) : (b >= S && hi < a.n);
+		const bool unres = PREC ? (b == 0 && ps[u] == 0 && lo > 0) : (b >= S && pe[u] == S && hi < a.n);
 		if (unres) {
 			const uint32_t at = atomicAdd(&a.flags[2], 1u);
 			if (at < a.unres_cap)
@@ -913,7 +970,7 @@ k_range_k32(FArgs a)
 #else
 		a.out[row] = lo + (BUN) (b < S ? b : S);
 #endif
-		if (row + 1 < a.n) {
+		if (row + 1 < a.n && xk + 1 < pe[u]) {
 			const uint32_t y = sk[xk + 1];
 			if (y < key[u])
 				ord |= DESC ? 2u : 1u;

@@ -370,6 +370,30 @@ def test_window_partition_sizes(gdk, ora, plen):
         assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("desc", [False, True])
+@pytest.mark.parametrize("limit", [0, 5, 300])
+def test_window_ragged_partitions_global_order(gdk, ora, desc, limit):
+    # one ordered column cut into partitions of 1..3000 rows (config 5's
+    # shape): stages with 0, a few or more than 16 partition starts
+    r = rng(105)
+    n = 200_000
+    vals = np.cumsum(r.integers(0, 5, n)).astype(np.int64) - 10**5
+    if desc:
+        vals = vals[::-1].copy()
+    bits = np.zeros(n, np.int8)
+    at, k = 0, 0
+    while at < n:
+        bits[at] = 1
+        at += int(r.integers(1, 40)) if k % 7 == 3 else int(r.integers(1, 3000))
+        k += 1
+    for preceding in (True, False):
+        got = gdk.GDKanalyticalwindowbounds(mk(gdk, gdk.TYPE_lng, vals), mk(gdk, gdk.TYPE_bit, bits),
+                                            limit, preceding).to_numpy()
+        want = ora.rangebounds(omk(ora, ora.TYPE_lng, vals), omk(ora, ora.TYPE_bit, bits), limit,
+                               preceding).values()
+        assert np.array_equal(got, want)
+
+
 def test_window_no_partitions_and_errors(gdk, ora):
     r = rng(102)
     vals = np.sort(r.integers(0, 10**6, 100_000)).astype(np.int64)
