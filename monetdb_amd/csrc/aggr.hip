@@ -456,7 +456,7 @@ k_gaggr(const void *base, int w, oid off, const oid *gids, oid gseq, oid gmin, B
 		mx = t > mx ? t : mx;
 	}
 	if (__lane_id() == 0 && mx)
-		atomicMax(maxabs, mx);
+		publish_max(maxabs, mx);
 }
 
 // few groups (K <= 8): every per-group quantity in lane registers -- sums,
@@ -735,179 +735,338 @@ struct AggrInit {
 
 // ---- many groups, g sorted (every group a run of consecutive rows, as
 // BATgroup numbers ordered keys, a sub-grouping of them or a clustered
-// column): a wave owns a range of 64 * GS_U rows, reduces each 64-row chunk
-// with a segmented scan over the runs, carries the open run from chunk to
-// chunk, and stores every run that starts and ends inside its range with
-// plain stores -- no other wave holds that group.  Only the range's first
-// run (it may have begun in the previous range) and its last (it may go on)
-// are added with atomics.
+// column): a wave owns a range of 64 * GS_U rows and a lane GS_U CONSECUTIVE
+// rows of it, all loaded before any is used.  A lane reduces its rows in
+// order and stores every run that starts and ends inside them with plain
+// stores (no other lane or wave holds that group); only the lane's first and
+// last runs meet the neighbouring lanes, through ONE segmented scan over the
+// 64 lanes per range.  The range's first run (it may have begun in the
+// previous range) and its last (it may go on) are added with atomics.
+// (Round 2's one-row-per-lane version ran a 64-lane segmented scan per 64
+// rows with one chunk's loads in flight: 7.9 ms for 600M rows.)
 constexpr int GS_U = 16;
+constexpr int GS_US = 8;   // rows per lane when the groups are staged in LDS
+
+struct GRun {
+	uhge s;
+	unsigned long long c, fv, ln;
+	long long mn, mx;
+	__device__ void clear()
+	{
+		s = 0;
+		c = 0;
+		fv = ~0ull;
+		ln = 0;
+		mn = INT64_MAX;
+		mx = INT64_MIN;
+	}
+	template <bool MM, bool POS>
+	__device__ void add(const GRun &o)
+	{
+		s += o.s;
+		c += o.c;
+		if (POS) {
+			fv = o.fv < fv ? o.fv : fv;
+			ln = o.ln > ln ? o.ln : ln;
+		}
+		if (MM) {
+			mn = o.mn < mn ? o.mn : mn;
+			mx = o.mx > mx ? o.mx : mx;
+		}
+	}
+	template <bool MM, bool POS>
+	__device__ GRun shfl_up(int d) const
+	{
+		GRun t;
+		t.s = ((uhge) __shfl_up((unsigned long long) (s >> 64), d) << 64) | __shfl_up((unsigned long long) s, d);
+		t.c = __shfl_up(c, d);
+		t.fv = POS ? __shfl_up(fv, d) : ~0ull;
+		t.ln = POS ? __shfl_up(ln, d) : 0;
+		t.mn = MM ? __shfl_up(mn, d) : INT64_MAX;
+		t.mx = MM ? __shfl_up(mx, d) : INT64_MIN;
+		return t;
+	}
+};
+
+// the groups k_gaggr_sorted adds to with atomics: those of every range's
+// first and last row
+__global__ __launch_bounds__(256) void
+k_gacc_edges(const oid *gids, oid gseq, oid gmin, BUN ngrp, BUN n, BUN RW, GAcc acc, int what)
+{
+	const BUN nr = (n + RW - 1) / RW;
+	for (BUN k = (BUN) blockIdx.x * blockDim.x + threadIdx.x; k < nr; k += (BUN) gridDim.x * blockDim.x) {
+		const BUN rows[2] = {k * RW, (k + 1) * RW < n ? (k + 1) * RW - 1 : n - 1};
+		for (int e = 0; e < 2; e++) {
+			const oid g = gids ? gids[rows[e]] : gseq + rows[e];
+			if (g < gmin || g - gmin >= ngrp)
+				continue;
+			const BUN gi = g - gmin;
+			if (what & AGG_SUM) {
+				acc.sum[2 * gi] = 0;
+				acc.sum[2 * gi + 1] = 0;
+			}
+			acc.cnt[gi] = 0;
+			if (what & AGG_POS) {
+				acc.firstval[gi] = ~0ull;
+				acc.lastnil[gi] = 0;
+			}
+		}
+	}
+}
 
 template <int VW, bool MM, bool POS>
 __global__ __launch_bounds__(256) void
 k_gaggr_sorted(const void *base, oid off, const oid *gids, oid gseq, oid gmin, BUN ngrp, BUN n, bool do_sum,
-	       bool count_all, GAcc acc, unsigned long long *maxabs)
+	       bool count_all, bool vec, bool gapinit, bool stage, GAcc acc, unsigned long long *maxabs)
 {
 	typedef typename VTy<VW>::T T;
-	const int lane = __lane_id();
+	// sums / counts only: a range's complete groups (a contiguous id
+	// interval) are staged in LDS and stored as contiguous runs -- stored
+	// from the lanes that finish them, the 8-byte pieces of neighbouring
+	// groups left partial lines behind (PMC: 9.3 GB written for 3.6 GB of
+	// accumulators at 150M groups)
+	constexpr bool STAGE = !MM && !POS;
+	constexpr int U = STAGE ? GS_US : GS_U;
+	constexpr BUN RW = 64 * U;
+	__shared__ unsigned long long s_lo[STAGE ? 4 : 1][STAGE ? RW : 1], s_hi[STAGE ? 4 : 1][STAGE ? RW : 1],
+		s_c[STAGE ? 4 : 1][STAGE ? RW : 1];
+	const int lane = __lane_id(), wv = threadIdx.x >> 6;
 	const BUN nwaves = (BUN) gridDim.x * (blockDim.x / 64);
 	const BUN wid = (BUN) blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
 	unsigned long long mxa = 0;
-	constexpr BUN RW = 64 * GS_U;
-	auto flush = [&](bool atomic, BUN gi, uhge sv, unsigned long long c, unsigned long long fv,
-			 unsigned long long ln, long long mn, long long mx) {
-		if (atomic) {
-			if (do_sum && sv)
-				atomic_add128(&acc.sum[2 * gi], (hge) sv);
-			if (c)
-				atomicAdd(&acc.cnt[gi], c);
-			if (POS && fv != ~0ull)
-				atomicMin(&acc.firstval[gi], fv);
-			if (POS && ln)
-				atomicMax(&acc.lastnil[gi], ln);
-			if (MM && c) {
-				atomicMin(&acc.mn[gi], mn);
-				atomicMax(&acc.mx[gi], mx);
+	oid sbase = 0, send = 0;     // staged ids: (sbase, send)
+	auto flush = [&](bool atomic, BUN gi, const GRun &r) {
+		if (STAGE && !atomic && gi + gmin > sbase && gi + gmin < send) {
+			const BUN k = gi + gmin - sbase;
+			if (do_sum) {
+				s_lo[wv][k] = (unsigned long long) r.s;
+				s_hi[wv][k] = (unsigned long long) (r.s >> 64);
+			}
+			s_c[wv][k] = r.c;
+		} else if (atomic) {
+			if (do_sum && r.s)
+				atomic_add128(&acc.sum[2 * gi], (hge) r.s);
+			if (r.c)
+				atomicAdd(&acc.cnt[gi], r.c);
+			if (POS && r.fv != ~0ull)
+				atomicMin(&acc.firstval[gi], r.fv);
+			if (POS && r.ln)
+				atomicMax(&acc.lastnil[gi], r.ln);
+			if (MM && r.c) {
+				atomicMin(&acc.mn[gi], r.mn);
+				atomicMax(&acc.mx[gi], r.mx);
 			}
 		} else {
 			if (do_sum) {
-				acc.sum[2 * gi] = (unsigned long long) sv;
-				acc.sum[2 * gi + 1] = (unsigned long long) (sv >> 64);
+				acc.sum[2 * gi] = (unsigned long long) r.s;
+				acc.sum[2 * gi + 1] = (unsigned long long) (r.s >> 64);
 			}
-			acc.cnt[gi] = c;
+			acc.cnt[gi] = r.c;
 			if (POS) {
-				acc.firstval[gi] = fv;
-				acc.lastnil[gi] = ln;
+				acc.firstval[gi] = r.fv;
+				acc.lastnil[gi] = r.ln;
 			}
 			if (MM) {
-				acc.mn[gi] = mn;
-				acc.mx[gi] = mx;
+				acc.mn[gi] = r.mn;
+				acc.mx[gi] = r.mx;
 			}
+		}
+	};
+	auto valid = [&](oid g) { return g >= gmin && g - gmin < ngrp; };
+	// gapinit: the accumulators were not initialised (k_gacc_edges set the
+	// groups the atomics add to); groups with no row, i.e. the gaps between
+	// consecutive ids and before / after them, get the identity here
+	// the groups strictly between ids prev and next (prev < next, sorted)
+	auto gap = [&](oid prev, oid hi) {
+		if (!gapinit || prev >= gmin + ngrp)
+			return;
+		oid lo = prev + 1;
+		lo = lo > gmin ? lo : gmin;
+		hi = hi < gmin + ngrp ? hi : gmin + ngrp;
+		for (oid h = lo; h < hi; h++) {
+			GRun e;
+			e.clear();
+			flush(false, h - gmin, e);
 		}
 	};
 	for (BUN r0 = wid * RW; r0 < n; r0 += nwaves * RW) {
 		const BUN r1 = r0 + RW < n ? r0 + RW : n;
-		// the open run carried between chunks (the same in every lane)
-		bool have = false, cval = false, cshared = true;
-		oid cg = 0;
-		uhge cs = 0;
-		unsigned long long cc = 0, cfv = ~0ull, cln = 0;
-		long long cmn = INT64_MAX, cmx = INT64_MIN;
-		for (BUN b = r0; b < r1; b += 64) {
-			const BUN i = b + lane;
-			const bool in = i < r1;
-			const BUN ic = in ? i : r1 - 1;
-			const oid g = gids ? gids[ic] : gseq + ic;
-			bool isnil = false;
-			hge v = 0;
-			if constexpr (VW > 0) {
-				const T x = ((const T *) base)[off + ic];
-				isnil = is_nil(x);
-				v = (hge) x;
-			}
-			const bool valid = in && g >= gmin && g - gmin < ngrp;
-			// this row's contribution
-			uhge s = valid && !isnil ? (uhge) v : 0;
-			unsigned long long c = valid && (!isnil || count_all) ? 1 : 0;
-			unsigned long long fv = valid && !isnil ? (unsigned long long) i : ~0ull;
-			unsigned long long ln = valid && isnil ? (unsigned long long) i + 1 : 0;
-			long long mn = valid && !isnil ? (long long) v : INT64_MAX, mx = valid && !isnil ? (long long) v : INT64_MIN;
-			if (valid && !isnil) {
-				const unsigned long long a = absbits(v);
-				mxa = a > mxa ? a : mxa;
-			}
-			const oid gp = __shfl_up(g, 1);
-			const bool inp = __shfl_up((int) in, 1) != 0;
-			// lane 0 of the range's first chunk continues the (empty) carry:
-			// its run is the range's first, possibly shared with the previous
-			const bool head = !in || (lane == 0 ? (have && g != cg) : (!inp || g != gp));
-			if (have && __shfl((int) head, 0)) {
-				// the carried run ended with the previous chunk
-				if (cval && lane == 0)
-					flush(cshared, cg - gmin, cs, cc, cfv, cln, cmn, cmx);
-				cs = 0;
-				cc = 0;
-				cfv = ~0ull;
-				cln = 0;
-				cmn = INT64_MAX;
-				cmx = INT64_MIN;
-				cshared = false;
-			}
-			// segmented inclusive scan over the runs
-			bool f = head;
+		const BUN l0 = r0 + (BUN) lane * U;
+		oid g[U];
+		T x[U];
+		constexpr bool VEC_OK = VW == 0 || (U * VW) % 16 == 0;
+		if (VEC_OK && vec && l0 + U <= r1) {
+			// 16-byte loads (the host checked the alignment)
+			if (gids) {
+				const uint4 *p = (const uint4 *) (gids + l0);
+				uint4 q[U / 2];
 #pragma unroll
-			for (int d = 1; d < 64; d <<= 1) {
-				const unsigned long long tlo = __shfl_up((unsigned long long) s, d);
-				const unsigned long long thi = __shfl_up((unsigned long long) (s >> 64), d);
-				const unsigned long long tc = __shfl_up(c, d);
-				const unsigned long long tfv = POS ? __shfl_up(fv, d) : 0;
-				const unsigned long long tln = POS ? __shfl_up(ln, d) : 0;
-				const long long tmn = MM ? __shfl_up(mn, d) : 0, tmx = MM ? __shfl_up(mx, d) : 0;
-				const bool tf = __shfl_up((int) f, d) != 0;
-				if (lane >= d) {
-					if (!f) {
-						s += ((uhge) thi << 64) | tlo;
-						c += tc;
-						if (POS) {
-							fv = tfv < fv ? tfv : fv;
-							ln = tln > ln ? tln : ln;
-						}
-						if (MM) {
-							mn = tmn < mn ? tmn : mn;
-							mx = tmx > mx ? tmx : mx;
-						}
-					}
-					f |= tf;
-				}
+				for (int u = 0; u < U / 2; u++)
+					q[u] = p[u];
+				__builtin_memcpy(g, q, sizeof g);
+			} else {
+#pragma unroll
+				for (int u = 0; u < U; u++)
+					g[u] = gseq + l0 + u;
 			}
-			// the chunk's first run continues the carried one (identity before
-			// the first chunk)
-			if (!f) {
-				s += cs;
-				c += cc;
-				if (POS) {
-					fv = cfv < fv ? cfv : fv;
-					ln = cln > ln ? cln : ln;
-				}
-				if (MM) {
-					mn = cmn < mn ? cmn : mn;
-					mx = cmx > mx ? cmx : mx;
-				}
+			if constexpr (VW > 0 && VEC_OK) {
+				constexpr int NQ = U * VW / 16;
+				const uint4 *p = (const uint4 *) ((const T *) base + off + l0);
+				uint4 q[NQ];
+#pragma unroll
+				for (int u = 0; u < NQ; u++)
+					q[u] = p[u];
+				__builtin_memcpy(x, q, sizeof x);
 			}
-			const bool nexthead = __shfl_down((int) head, 1) != 0;
-			if (lane < 63 && nexthead && valid) {
-				// a run ends here: shared only if it is the range's first run
-				const bool shared = !f && cshared;
-				flush(shared, g - gmin, s, c, fv, ln, mn, mx);
-			}
-			// the new carry: lane 63's run
-			const bool f63 = __shfl((int) f, 63) != 0;
-			const bool v63 = __shfl((int) valid, 63) != 0;
-			cshared = f63 ? false : cshared;
-			have = true;
-			cval = v63;
-			cg = __shfl(g, 63);
-			cs = ((uhge) __shfl((unsigned long long) (s >> 64), 63) << 64) | __shfl((unsigned long long) s, 63);
-			cc = __shfl(c, 63);
-			if (POS) {
-				cfv = __shfl(fv, 63);
-				cln = __shfl(ln, 63);
-			}
-			if (MM) {
-				cmn = __shfl(mn, 63);
-				cmx = __shfl(mx, 63);
+		} else {
+			// rows past r1 repeat the range's last row: they extend its run
+			// and contribute nothing
+#pragma unroll
+			for (int u = 0; u < U; u++) {
+				const BUN ic = l0 + u < r1 ? l0 + u : r1 - 1;
+				g[u] = gids ? gids[ic] : gseq + ic;
+				if constexpr (VW > 0)
+					x[u] = ((const T *) base)[off + ic];
 			}
 		}
-		// the range's last run may continue in the next range: added
-		if (have && cval && lane == 0)
-			flush(true, cg - gmin, cs, cc, cfv, cln, cmn, cmx);
+		// the lane's rows in order: P = its first run, cur = the open run
+		GRun P, cur;
+		P.clear();
+		cur.clear();
+		bool single = true;
+		const oid gF = g[0];
+		oid cg = g[0];
+		if (STAGE && stage) {
+			// the range's first and last ids: groups strictly between them
+			// are complete (or empty) in this range; staged when they fit
+			const oid a0 = __shfl(g[0], 0), a1 = __shfl(g[U - 1], 63);
+			sbase = a0;
+			send = a1 - a0 <= RW ? a1 : a0;
+			// empty groups keep the identity (also when nothing writes them)
+			for (BUN k = lane; k < RW; k += 64) {
+				s_lo[wv][k] = 0;
+				s_hi[wv][k] = 0;
+				s_c[wv][k] = 0;
+			}
+			__builtin_amdgcn_wave_barrier();
+		}
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			if (g[u] != cg) {
+				if (single)
+					P = cur;
+				else if (valid(cg))
+					flush(false, cg - gmin, cur);     // a run inside the lane
+				if (g[u] > cg + 1)
+					gap(cg, g[u]);
+				single = false;
+				cur.clear();
+				cg = g[u];
+			}
+			const BUN i = l0 + u;
+			if (i < r1 && valid(g[u])) {
+				bool isnil = false;
+				hge v = 0;
+				if constexpr (VW > 0) {
+					isnil = is_nil(x[u]);
+					v = (hge) x[u];
+				}
+				if (!isnil) {
+					cur.s += (uhge) v;
+					cur.c++;
+					if (POS)
+						cur.fv = i < cur.fv ? i : cur.fv;
+					if (MM) {
+						cur.mn = (long long) v < cur.mn ? (long long) v : cur.mn;
+						cur.mx = (long long) v > cur.mx ? (long long) v : cur.mx;
+					}
+					const unsigned long long ab = absbits(v);
+					mxa = ab > mxa ? ab : mxa;
+				} else {
+					if (count_all)
+						cur.c++;
+					if (POS)
+						cur.ln = i + 1 > cur.ln ? i + 1 : cur.ln;
+				}
+			}
+		}
+		const oid gL = cg;
+		// the lanes' boundary runs
+		const oid gLprev = __shfl_up(gL, 1), gFnext = __shfl_down(gF, 1);
+		const bool connects = lane > 0 && gLprev == gF;           // my first run began to my left
+		const bool nextconn = lane < 63 && gFnext == gL;         // my last run goes on to my right
+		const unsigned long long chain = __ballot(single && (lane == 0 || connects));
+		const unsigned long long below = (1ull << lane) - 1;
+		// my first run is the range's first (it may have begun in the previous range)
+		const bool rfirst = lane == 0 || (connects && (~chain & below) == 0);
+		// segmented inclusive scan of the last runs: a lane that is one run
+		// and continues its left neighbour's run extends it
+		GRun t = cur;
+		bool f = !(single && connects);
+#pragma unroll
+		for (int d = 1; d < 64; d <<= 1) {
+			const GRun o = t.shfl_up<MM, POS>(d);
+			const bool tf = __shfl_up((int) f, d) != 0;
+			if (lane >= d) {
+				if (!f)
+					t.add<MM, POS>(o);
+				f |= tf;
+			}
+		}
+		// t = the run ending at my last row, from its start
+		const GRun cin = t.shfl_up<MM, POS>(1);
+		if (gapinit) {
+			if (lane < 63 && gFnext > gL + 1)
+				gap(gL, gFnext);
+			if (lane == 0) {
+				if (r0 == 0) {
+					if (gF > gmin && gmin + ngrp > gmin)
+						for (oid h = gmin; h < gF && h < gmin + ngrp; h++) {
+							GRun e;
+							e.clear();
+							flush(false, h - gmin, e);
+						}
+				} else {
+					const oid gp = gids ? gids[r0 - 1] : gseq + r0 - 1;
+					if (gF > gp + 1)
+						gap(gp, gF);
+				}
+			}
+			if (lane == 63 && r1 == n)
+				gap(gL, gmin + ngrp);
+		}
+		if (!single) {
+			if (connects)
+				P.add<MM, POS>(cin);
+			if (valid(gF))
+				flush(rfirst, gF - gmin, P);
+			if (!nextconn && valid(gL))
+				flush(lane == 63, gL - gmin, cur);
+		} else if (!nextconn && valid(gL)) {
+			flush(lane == 63 || rfirst, gL - gmin, t);
+		}
+		if (STAGE && send > sbase + 1) {
+			// the staged groups (sbase, send) out as contiguous runs
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+			__builtin_amdgcn_wave_barrier();
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+			const oid lo = sbase + 1 > gmin ? sbase + 1 : gmin;
+			const oid hi = send < gmin + ngrp ? send : gmin + ngrp;
+			for (oid h = lo + lane; h < hi; h += 64) {
+				const BUN k = h - sbase, gi = h - gmin;
+				if (do_sum)
+					*(ulonglong2 *) &acc.sum[2 * gi] = ulonglong2{s_lo[wv][k], s_hi[wv][k]};
+				acc.cnt[gi] = s_c[wv][k];
+			}
+			__builtin_amdgcn_wave_barrier();
+		}
 	}
 	for (int o = 32; o > 0; o >>= 1) {
 		const unsigned long long t = __shfl_xor(mxa, o);
 		mxa = t > mxa ? t : mxa;
 	}
 	if (lane == 0 && mxa)
-		atomicMax(maxabs, mxa);
+		publish_max(maxabs, mxa);
 }
 
 __global__ void
@@ -1074,8 +1233,22 @@ gaggr_device(const AggrInit &a, mgdk_bat *b, int what, bool count_all, GAcc &acc
 	// small-group aggregates
 	// the host read-back (run_gaggr) copies the whole block: all of it
 	// initialised there
-	hipLaunchKernelGGL(k_gacc_init, dim3(grid_for(ng + 1, 1024, 8192)), dim3(256), 0, st, acc, ng, maxabs,
-			   full_init ? (AGG_SUM | AGG_POS | AGG_MINMAX) : what);
+	// sorted ids over rows (sums / counts / positions): k_gaggr_sorted
+	// initialises the groups itself (gaps) and k_gacc_edges the ones it adds
+	// to atomically, so the accumulators are written once instead of twice
+	const bool sorted_path = a.ci.n && ng > 8 && a.gsorted && (what & ~(AGG_SUM | AGG_POS | AGG_MINMAX)) == 0;
+	static const bool gapinit_on = getenv("MGDK_GAGGR_GAPINIT") ? atoi(getenv("MGDK_GAGGR_GAPINIT")) != 0 : true;
+	const bool gapinit = gapinit_on && sorted_path && !full_init && !(what & AGG_MINMAX);
+	if (gapinit) {
+		if (!hip_ok(hipMemsetAsync(maxabs, 0, 8, st), "memset"))
+			return -1;
+		const BUN rw = 64 * ((what & (AGG_POS | AGG_MINMAX)) ? GS_U : GS_US);
+		hipLaunchKernelGGL(k_gacc_edges, dim3(grid_for((a.ci.n + rw - 1) / rw, 256, 8192)), dim3(256),
+				   0, st, a.gids, a.gseq, a.min, ng, a.ci.n, rw, acc, what);
+	} else {
+		hipLaunchKernelGGL(k_gacc_init, dim3(grid_for(ng + 1, 1024, 8192)), dim3(256), 0, st, acc, ng, maxabs,
+				   full_init ? (AGG_SUM | AGG_POS | AGG_MINMAX) : what);
+	}
 	const oid off = a.ci.seq - b->hseqbase;
 	dim3 g(grid_for(a.ci.n, 256 * 8, 256 * 16)), blk(256);
 	// COUNT(*) over few groups needs no values (k_gaggr_k's base == NULL)
@@ -1111,11 +1284,16 @@ gaggr_device(const AggrInit &a, mgdk_bat *b, int what, bool count_all, GAcc &acc
 		}
 		else if (a.gsorted && (what & ~(AGG_SUM | AGG_POS | AGG_MINMAX)) == 0) {
 			// groups are runs of rows: segmented reduction (k_gaggr_sorted)
-			const BUN nw = (a.ci.n + 64 * GS_U - 1) / (64 * GS_U);
+			const BUN rw = 64 * ((what & (AGG_POS | AGG_MINMAX)) ? GS_U : GS_US);
+			const BUN nw = (a.ci.n + rw - 1) / rw;
+			static const bool stage = getenv("MGDK_GS_STAGE") ? atoi(getenv("MGDK_GS_STAGE")) != 0 : true;
 			const dim3 gs(grid_for(nw, 4, 65535u * 16u));
 			const bool sum = (what & AGG_SUM) != 0;
 			const void *vb = (what == 0 && count_all) ? nullptr : b->theap;
-#define GS3(VW_, MM_, POS_) hipLaunchKernelGGL((k_gaggr_sorted<VW_, MM_, POS_>), gs, blk, 0, st, vb, off, a.gids, a.gseq, a.min, ng, a.ci.n, sum, count_all, acc, maxabs)
+			// 16-byte loads when a lane's rows start 16-byte aligned
+			const bool vec = ((uintptr_t) a.gids & 15) == 0 &&
+				(!vb || (((uintptr_t) vb + (uintptr_t) off * b->twidth) & 15) == 0);
+#define GS3(VW_, MM_, POS_) hipLaunchKernelGGL((k_gaggr_sorted<VW_, MM_, POS_>), gs, blk, 0, st, vb, off, a.gids, a.gseq, a.min, ng, a.ci.n, sum, count_all, vec, gapinit, stage, acc, maxabs)
 #define GS2(VW_) do { if (what & AGG_MINMAX) GS3(VW_, true, false); \
 			else if (what & AGG_POS) GS3(VW_, false, true); \
 			else GS3(VW_, false, false); } while (0)

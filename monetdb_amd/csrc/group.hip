@@ -996,28 +996,219 @@ k_grp_seq_ext(BUN ngrp, BUN n, const uint64_t *spos, bool cdense, oid cseq, cons
 	}
 }
 
+// Dense candidates: the same starts in two passes over the keys instead of
+// flags -> 8-byte scan -> ids (three passes and 8 B of scan per row): a
+// count of the starts per 2048-row tile, a scan of the tile counts, then
+// the starts again, ranked in the tile by one ballot per 64 rows and a
+// 32-entry LDS scan, the ids stored where the rows are.  Key width, float
+// normalisation and the prior-group source are template parameters, so
+// every key load of a lane is in flight before the first compare.
+constexpr int SQU = 8;
+constexpr BUN SQT = 256 * SQU;
+
+template <int W, bool FL>
+__device__ __forceinline__ void
+keyw(const void *base, BUN p, uint64_t &k0, uint64_t &k1)
+{
+	k1 = 0;
+	if constexpr (W == 1) {
+		k0 = ((const uint8_t *) base)[p];
+	} else if constexpr (W == 2) {
+		k0 = ((const uint16_t *) base)[p];
+	} else if constexpr (W == 4) {
+		const uint32_t u = ((const uint32_t *) base)[p];
+		if (FL) {
+			const float f = __uint_as_float(u);
+			k0 = f != f ? 0x7fc00000u : f == 0.0f ? 0 : u;
+		} else {
+			k0 = u;
+		}
+	} else if constexpr (W == 8) {
+		const uint64_t u = ((const uint64_t *) base)[p];
+		if (FL) {
+			const double d = __longlong_as_double((long long) u);
+			k0 = d != d ? 0x7ff8000000000000ull : d == 0.0 ? 0 : u;
+		} else {
+			k0 = u;
+		}
+	} else {
+		k0 = ((const uint64_t *) base)[2 * p];
+		k1 = ((const uint64_t *) base)[2 * p + 1];
+	}
+}
+
+// GK: 0 no prior groups, 1 their 1-byte image, 2 oid ids, 3 dense ids
+template <int GK>
+__device__ __forceinline__ uint64_t
+gval(const KeySrc &s, BUN i)
+{
+	if constexpr (GK == 0)
+		return 0;
+	else if constexpr (GK == 1)
+		return s.g8[i];
+	else if constexpr (GK == 2)
+		return s.g[i];
+	else
+		return s.gseq + i;
+}
+
+// start flags of the tile's rows t0 + u * 256 + tid (row 0 starts)
+template <int W, bool FL, int GK>
+__device__ __forceinline__ void
+sq_starts(const KeySrc &s, BUN n, BUN t0, bool st[SQU])
+{
+	uint64_t a0[SQU], a1[SQU], ag[SQU], b0[SQU], b1[SQU], bg[SQU];
+#pragma unroll
+	for (int u = 0; u < SQU; u++) {
+		const BUN i = t0 + (BUN) u * 256 + threadIdx.x;
+		const BUN ic = i < n ? i : n - 1, ip = ic ? ic - 1 : 0;
+		keyw<W, FL>(s.base, s.off + ic, a0[u], a1[u]);
+		keyw<W, FL>(s.base, s.off + ip, b0[u], b1[u]);
+		ag[u] = gval<GK>(s, ic);
+		bg[u] = gval<GK>(s, ip);
+	}
+#pragma unroll
+	for (int u = 0; u < SQU; u++) {
+		const BUN i = t0 + (BUN) u * 256 + threadIdx.x;
+		st[u] = i < n && (i == 0 || a0[u] != b0[u] || a1[u] != b1[u] || ag[u] != bg[u]);
+	}
+}
+
+template <int W, bool FL, int GK>
+__global__ __launch_bounds__(256) void
+k_sq_count(KeySrc s, BUN n, uint32_t *tcnt)
+{
+	bool st[SQU];
+	sq_starts<W, FL, GK>(s, n, (BUN) blockIdx.x * SQT, st);
+	uint32_t c = 0;
+#pragma unroll
+	for (int u = 0; u < SQU; u++)
+		c += st[u];
+	c = block_reduce(c, [](uint32_t x, uint32_t y) { return x + y; });
+	if (threadIdx.x == 0)
+		tcnt[blockIdx.x] = c;
+}
+
+template <int W, bool FL, int GK>
+__global__ __launch_bounds__(256) void
+k_sq_write(KeySrc s, BUN n, const uint64_t *tpre, oid *gid, uint64_t *spos)
+{
+	__shared__ uint32_t tab[SQU * 4];
+	const int lane = __lane_id(), w = threadIdx.x >> 6;
+	const BUN t0 = (BUN) blockIdx.x * SQT;
+	bool st[SQU];
+	sq_starts<W, FL, GK>(s, n, t0, st);
+	unsigned long long bal[SQU];
+#pragma unroll
+	for (int u = 0; u < SQU; u++) {
+		bal[u] = __ballot(st[u]);
+		if (lane == 0)
+			tab[u * 4 + w] = (uint32_t) __popcll(bal[u]);
+	}
+	__syncthreads();
+	if (threadIdx.x < 64) {
+		// exclusive scan of the (row group, wave) counts in row order
+		uint32_t v = threadIdx.x < SQU * 4 ? tab[threadIdx.x] : 0, x = v;
+#pragma unroll
+		for (int d = 1; d < 64; d <<= 1) {
+			const uint32_t t = __shfl_up(x, d);
+			if (lane >= d)
+				x += t;
+		}
+		if (threadIdx.x < SQU * 4)
+			tab[threadIdx.x] = x - v;
+	}
+	__syncthreads();
+	const uint64_t base = tpre[blockIdx.x];
+	const unsigned long long lt = (1ull << lane) - 1;
+#pragma unroll
+	for (int u = 0; u < SQU; u++) {
+		const BUN i = t0 + (BUN) u * 256 + threadIdx.x;
+		if (i < n) {
+			// starts up to and including row i, minus one
+			const uint64_t k = base + tab[u * 4 + w] + (uint64_t) __popcll(bal[u] & lt) + st[u] - 1;
+			gid[i] = k;
+			if (st[u])
+				spos[k] = i;
+		}
+	}
+}
+
+template <int W, bool FL, int GK>
+static int
+sq_ids(const KeySrc &ks, BUN n, DevBuf &tc, DevBuf &tp, oid *gid, uint64_t *spos, uint64_t *ngrp, bool write)
+{
+	hipStream_t st = stream();
+	const BUN nt = (n + SQT - 1) / SQT;
+	if (!write) {
+		hipLaunchKernelGGL((k_sq_count<W, FL, GK>), dim3(nt), dim3(256), 0, st, ks, n, tc.as<uint32_t>());
+		return exclusive_scan(tc.as<uint32_t>(), tp.as<uint64_t>(), nt, ngrp);
+	}
+	hipLaunchKernelGGL((k_sq_write<W, FL, GK>), dim3(nt), dim3(256), 0, st, ks, n, tp.as<uint64_t>(), gid, spos);
+	return 0;
+}
+
+template <int W, bool FL>
+static int
+sq_ids_g(const KeySrc &ks, BUN n, DevBuf &tc, DevBuf &tp, oid *gid, uint64_t *spos, uint64_t *ngrp, bool write)
+{
+	if (!ks.has_g)
+		return sq_ids<W, FL, 0>(ks, n, tc, tp, gid, spos, ngrp, write);
+	if (ks.g8)
+		return sq_ids<W, FL, 1>(ks, n, tc, tp, gid, spos, ngrp, write);
+	if (ks.g)
+		return sq_ids<W, FL, 2>(ks, n, tc, tp, gid, spos, ngrp, write);
+	return sq_ids<W, FL, 3>(ks, n, tc, tp, gid, spos, ngrp, write);
+}
+
+static int
+sq_dispatch(const KeySrc &ks, BUN n, DevBuf &tc, DevBuf &tp, oid *gid, uint64_t *spos, uint64_t *ngrp, bool write)
+{
+	switch (ks.w) {
+	case 1: return sq_ids_g<1, false>(ks, n, tc, tp, gid, spos, ngrp, write);
+	case 2: return sq_ids_g<2, false>(ks, n, tc, tp, gid, spos, ngrp, write);
+	case 4: return ks.kind == 2 ? sq_ids_g<4, true>(ks, n, tc, tp, gid, spos, ngrp, write)
+				    : sq_ids_g<4, false>(ks, n, tc, tp, gid, spos, ngrp, write);
+	case 8: return ks.kind == 3 ? sq_ids_g<8, true>(ks, n, tc, tp, gid, spos, ngrp, write)
+				    : sq_ids_g<8, false>(ks, n, tc, tp, gid, spos, ngrp, write);
+	default: return sq_ids_g<16, false>(ks, n, tc, tp, gid, spos, ngrp, write);
+	}
+}
+
 int
 group_ordered(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mgdk_bat **enp,
 	      mgdk_bat **hnp)
 {
 	hipStream_t st = stream();
-	DevBuf fl(n + 8), ex(n * 8 + 8), spos(n * 8 + 8);
-	if (!fl.p || !ex.p || !spos.p)
-		return -1;
 	const dim3 grd(grid_for(n, 1024, 8192)), blk(256);
-	hipLaunchKernelGGL(k_grp_seq_flags, grd, blk, 0, st, ks, n, fl.as<uint8_t>());
-	uint64_t ngrp = 0;
-	if (exclusive_scan(fl.as<uint8_t>(), ex.as<uint64_t>(), n, &ngrp) < 0)
+	static const bool two = getenv("MGDK_GROUP_SEQ2") ? atoi(getenv("MGDK_GROUP_SEQ2")) != 0 : true;
+	const bool fast = two && ks.dense && n > 0;
+	const BUN nt = (n + SQT - 1) / SQT;
+	DevBuf fl(fast ? 0 : n + 8), ex(fast ? 0 : n * 8 + 8), tc(fast ? nt * 4 + 8 : 0), tp(fast ? nt * 8 + 8 : 0);
+	if ((!fast && (!fl.p || !ex.p)) || (fast && (!tc.p || !tp.p)))
 		return -1;
+	uint64_t ngrp = 0;
+	if (fast) {
+		if (sq_dispatch(ks, n, tc, tp, nullptr, nullptr, &ngrp, false) < 0)
+			return -1;
+	} else {
+		hipLaunchKernelGGL(k_grp_seq_flags, grd, blk, 0, st, ks, n, fl.as<uint8_t>());
+		if (exclusive_scan(fl.as<uint8_t>(), ex.as<uint64_t>(), n, &ngrp) < 0)
+			return -1;
+	}
+	DevBuf spos(ngrp * 8 + 8);
 	mgdk_bat *gn = newbat(hseqb, MGDK_oid, n), *en = newbat(0, MGDK_oid, ngrp), *hn = newbat(0, MGDK_lng, ngrp);
-	if (!gn || !en || !hn) {
+	if (!gn || !en || !hn || !spos.p) {
 		mgdk_BBPunfix(gn);
 		mgdk_BBPunfix(en);
 		mgdk_BBPunfix(hn);
 		return -1;
 	}
-	hipLaunchKernelGGL(k_grp_seq_ids, grd, blk, 0, st, n, fl.as<uint8_t>(), ex.as<uint64_t>(), (oid *) gn->theap,
-			   spos.as<uint64_t>());
+	if (fast)
+		sq_dispatch(ks, n, tc, tp, (oid *) gn->theap, spos.as<uint64_t>(), nullptr, true);
+	else
+		hipLaunchKernelGGL(k_grp_seq_ids, grd, blk, 0, st, n, fl.as<uint8_t>(), ex.as<uint64_t>(), (oid *) gn->theap,
+				   spos.as<uint64_t>());
 	hipLaunchKernelGGL(k_grp_seq_ext, dim3(grid_for(ngrp, 1024, 8192)), blk, 0, st, ngrp, n, spos.as<uint64_t>(),
 			   ci.dense, ci.seq, ci.oids, (oid *) en->theap, (int64_t *) hn->theap);
 	uint64_t *hl = (uint64_t *) pinned(16);

@@ -279,6 +279,16 @@ publish_or(uint32_t *flag, uint32_t bits)
 		atomicOr(flag, bits);
 }
 
+// raise a device-wide maximum, skipping the atomic when a value at least as
+// large is already visible: one same-word atomic per wave of a large grid
+// serialises at the L2 (~88 per microsecond)
+__device__ __forceinline__ void
+publish_max(unsigned long long *m, unsigned long long v)
+{
+	if (v > __hip_atomic_load(m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+		atomicMax(m, v);
+}
+
 // 128-bit integer -> double, round to nearest even: the top 64 significant
 // bits with a sticky bit below them convert exactly like the full value
 __device__ __forceinline__ double

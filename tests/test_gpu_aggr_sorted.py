@@ -94,3 +94,42 @@ def test_sorted_groupsum_cands_extents_and_narrow(gdk, ora):
     (B, OB), (G2, _) = _cols(gdk, ora, "lng", big, gids)
     with pytest.raises(gdk.GDKError, match="22003!overflow in sum aggregate"):
         gdk.BATgroupsum(B, G2, None, gdk.TYPE_lng, True)
+
+
+@pytest.mark.parametrize("shift", [1, 3])
+def test_sorted_groupsum_unaligned_views(gdk, ora, shift):
+    """values and group ids as slices starting off a 16-byte boundary (the
+    kernel's scalar-load path), runs spanning lanes and ranges"""
+    r = rng(820 + shift)
+    n = 150_011
+    gids = _runs(r, n + shift, 37)
+    vals = r.integers(-10**9, 10**9, n + shift).astype(np.int64)
+    vals[r.random(n + shift) < 0.01] = NIL64
+    (V, OV), (G, OG) = _cols(gdk, ora, "lng", vals, gids)
+    Vs, Gs = gdk.BATslice(V, shift, n + shift), gdk.BATslice(G, shift, n + shift)
+    OVs = ora.Bat.from_array(ora.TYPE_lng, vals[shift:], hseqbase=shift, sorted_=False, revsorted=False,
+                             key=False, nonil=False)
+    OGs = ora.Bat.from_array(ora.TYPE_oid, gids[shift:], hseqbase=shift, sorted_=True, nonil=True)
+    _eq(gdk.BATgroupsum(Vs, Gs, None, gdk.TYPE_hge, True), ora.BATgroupsum(OVs, OGs, None, ora.TYPE_hge, True))
+    _eq(gdk.BATgroupcount(Vs, Gs, None, False), ora.BATgroupcount(OVs, OGs, None, False))
+    _eq(gdk.BATgroupmax(Vs, Gs, None, True), ora.BATgroupminmax(OVs, OGs, None, True, True))
+
+
+def test_sorted_groupsum_empty_groups(gdk, ora):
+    """groups without rows: ids starting above 0, gaps between runs (inside a
+    lane, between lanes and between ranges), groups after the last id"""
+    r = rng(830)
+    n = 100_003
+    gids = _runs(r, n, 9)
+    gids = gids * 3 + 5 + (gids // 700) * 50
+    vals = r.integers(-10**6, 10**6, n).astype(np.int64)
+    (V, OV), (G, OG) = _cols(gdk, ora, "lng", vals, gids)
+    ne = int(gids.max()) + 77
+    E, OE = gdk.BAT.dense(0, ne), ora.Bat.dense(0, ne)
+    for skip in (True, False):
+        _eq(gdk.BATgroupsum(V, G, E, gdk.TYPE_lng, skip), ora.BATgroupsum(OV, OG, OE, ora.TYPE_lng, skip))
+        _eq(gdk.BATgroupcount(V, G, E, skip), ora.BATgroupcount(OV, OG, OE, skip))
+        a, rm, c = gdk.BATgroupavg3(V, G, E, skip)
+        oa, orm, oc = ora.BATgroupavg3(OV, OG, OE, skip)
+        for d, o in ((a, oa), (rm, orm), (c, oc)):
+            assert np.array_equal(np.asarray(d.values()), np.asarray(o.values()))
