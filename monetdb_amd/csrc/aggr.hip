@@ -788,6 +788,36 @@ struct GRun {
 	}
 };
 
+__device__ __forceinline__ void put_res_d(void *base, int bt, BUN k, hge v, bool nil);
+
+// BATgroupsum straight into its result column (sums with skip_nils or
+// without nils: a group's result is nil only when it has no value): the
+// per-group accumulators, their initialisation and the finishing pass go
+// away; the groups a range shares with its neighbours leave their partial
+// in `edges` (two per range, in range order, so a group's partials are
+// consecutive) for k_gedge_sum instead of being added with atomics
+struct SOut {
+	void *out;
+	int bt;
+	hge max;
+	uint32_t *flags;
+	bool on;
+};
+
+struct GEdge {
+	oid g;
+	unsigned long long lo, hi, c;
+};
+
+__device__ __forceinline__ uint32_t
+sout_put(const SOut &so, BUN gi, uhge s, unsigned long long c)
+{
+	const hge sv = (hge) s;
+	const bool nil = c == 0;
+	put_res_d(so.out, so.bt, gi, nil ? 0 : sv, nil);
+	return (sv > so.max || sv < -so.max ? 1u : 0u) | (nil ? 2u : 0u);
+}
+
 // the groups k_gaggr_sorted adds to with atomics: those of every range's
 // first and last row
 __global__ __launch_bounds__(256) void
@@ -817,7 +847,8 @@ k_gacc_edges(const oid *gids, oid gseq, oid gmin, BUN ngrp, BUN n, BUN RW, GAcc 
 template <int VW, bool MM, bool POS>
 __global__ __launch_bounds__(256) void
 k_gaggr_sorted(const void *base, oid off, const oid *gids, oid gseq, oid gmin, BUN ngrp, BUN n, bool do_sum,
-	       bool count_all, bool vec, bool gapinit, bool stage, GAcc acc, unsigned long long *maxabs)
+	       bool count_all, bool vec, bool gapinit, bool stage, GAcc acc, unsigned long long *maxabs, SOut so,
+	       GEdge *edges)
 {
 	typedef typename VTy<VW>::T T;
 	// sums / counts only: a range's complete groups (a contiguous id
@@ -835,7 +866,12 @@ k_gaggr_sorted(const void *base, oid off, const oid *gids, oid gseq, oid gmin, B
 	const BUN wid = (BUN) blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
 	unsigned long long mxa = 0;
 	oid sbase = 0, send = 0;     // staged ids: (sbase, send)
+	uint32_t sof = 0;            // SOut flags
 	auto flush = [&](bool atomic, BUN gi, const GRun &r) {
+		if (!atomic && so.on && !(STAGE && stage && gi + gmin > sbase && gi + gmin < send)) {
+			sof |= sout_put(so, gi, r.s, r.c);
+			return;
+		}
 		if (STAGE && !atomic && gi + gmin > sbase && gi + gmin < send) {
 			const BUN k = gi + gmin - sbase;
 			if (do_sum) {
@@ -1035,7 +1071,48 @@ k_gaggr_sorted(const void *base, oid off, const oid *gids, oid gseq, oid gmin, B
 			if (lane == 63 && r1 == n)
 				gap(gL, gmin + ngrp);
 		}
-		if (!single) {
+		if (edges) {
+			// the range's shared groups: slot 0 = its first row's group when
+			// that group ends inside the range, slot 1 = its last row's group
+			bool e0 = false;
+			GRun r0run;
+			if (!single) {
+				if (connects)
+					P.add<MM, POS>(cin);
+				if (valid(gF)) {
+					if (rfirst) {
+						e0 = true;
+						r0run = P;
+					} else {
+						flush(false, gF - gmin, P);
+					}
+				}
+				if (!nextconn && valid(gL) && lane < 63)
+					flush(false, gL - gmin, cur);
+			} else if (!nextconn && valid(gL) && lane < 63) {
+				if (rfirst) {
+					e0 = true;
+					r0run = t;
+				} else {
+					flush(false, gL - gmin, t);
+				}
+			}
+			const BUN rk = r0 / RW;
+			const unsigned long long b0 = __ballot(e0);
+			if (e0 || (b0 == 0 && lane == 0)) {
+				if (!e0)
+					r0run.clear();
+				edges[2 * rk] = GEdge{gF, (unsigned long long) r0run.s, (unsigned long long) (r0run.s >> 64),
+						      r0run.c};
+			}
+			if (lane == 63) {
+				GRun r1run = single ? t : cur;
+				if (!valid(gL))
+					r1run.clear();
+				edges[2 * rk + 1] = GEdge{gL, (unsigned long long) r1run.s, (unsigned long long) (r1run.s >> 64),
+							  r1run.c};
+			}
+		} else if (!single) {
 			if (connects)
 				P.add<MM, POS>(cin);
 			if (valid(gF))
@@ -1054,6 +1131,10 @@ k_gaggr_sorted(const void *base, oid off, const oid *gids, oid gseq, oid gmin, B
 			const oid hi = send < gmin + ngrp ? send : gmin + ngrp;
 			for (oid h = lo + lane; h < hi; h += 64) {
 				const BUN k = h - sbase, gi = h - gmin;
+				if (so.on) {
+					sof |= sout_put(so, gi, ((uhge) s_hi[wv][k] << 64) | s_lo[wv][k], s_c[wv][k]);
+					continue;
+				}
 				if (do_sum)
 					*(ulonglong2 *) &acc.sum[2 * gi] = ulonglong2{s_lo[wv][k], s_hi[wv][k]};
 				acc.cnt[gi] = s_c[wv][k];
@@ -1067,6 +1148,35 @@ k_gaggr_sorted(const void *base, oid off, const oid *gids, oid gseq, oid gmin, B
 	}
 	if (lane == 0 && mxa)
 		publish_max(maxabs, mxa);
+	if (so.on) {
+		for (int o = 32; o > 0; o >>= 1)
+			sof |= __shfl_xor(sof, o);
+		if (lane == 0 && sof)
+			publish_or(so.flags, sof);
+	}
+}
+
+// the shared groups' partials summed (a group's entries are consecutive)
+__global__ __launch_bounds__(256) void
+k_gedge_sum(const GEdge *e, BUN ne, oid gmin, BUN ngrp, SOut so)
+{
+	uint32_t f = 0;
+	for (BUN j = (BUN) blockIdx.x * blockDim.x + threadIdx.x; j < ne; j += (BUN) gridDim.x * blockDim.x) {
+		const oid g = e[j].g;
+		if ((j > 0 && e[j - 1].g == g) || g < gmin || g - gmin >= ngrp)
+			continue;
+		uhge s = 0;
+		unsigned long long c = 0;
+		for (BUN q = j; q < ne && e[q].g == g; q++) {
+			s += ((uhge) e[q].hi << 64) | e[q].lo;
+			c += e[q].c;
+		}
+		f |= sout_put(so, g - gmin, s, c);
+	}
+	for (int o = 32; o > 0; o >>= 1)
+		f |= __shfl_xor(f, o);
+	if (__lane_id() == 0 && f)
+		publish_or(so.flags, f);
 }
 
 __global__ void
@@ -1293,7 +1403,7 @@ gaggr_device(const AggrInit &a, mgdk_bat *b, int what, bool count_all, GAcc &acc
 			// 16-byte loads when a lane's rows start 16-byte aligned
 			const bool vec = ((uintptr_t) a.gids & 15) == 0 &&
 				(!vb || (((uintptr_t) vb + (uintptr_t) off * b->twidth) & 15) == 0);
-#define GS3(VW_, MM_, POS_) hipLaunchKernelGGL((k_gaggr_sorted<VW_, MM_, POS_>), gs, blk, 0, st, vb, off, a.gids, a.gseq, a.min, ng, a.ci.n, sum, count_all, vec, gapinit, stage, acc, maxabs)
+#define GS3(VW_, MM_, POS_) hipLaunchKernelGGL((k_gaggr_sorted<VW_, MM_, POS_>), gs, blk, 0, st, vb, off, a.gids, a.gseq, a.min, ng, a.ci.n, sum, count_all, vec, gapinit, stage, acc, maxabs, SOut{}, nullptr)
 #define GS2(VW_) do { if (what & AGG_MINMAX) GS3(VW_, true, false); \
 			else if (what & AGG_POS) GS3(VW_, false, true); \
 			else GS3(VW_, false, false); } while (0)
@@ -1705,6 +1815,47 @@ k_avg3c_terms(const T *avg, const long long *rem, const long long *cnt, oid off,
 		atomicOr(flags, 1u);
 }
 
+// BATgroupsum over sorted group ids straight into bn (see SOut); false
+// when the case does not apply
+bool
+gsum_sorted_direct(const AggrInit &a, mgdk_bat *b, mgdk_bat *bn, int tp, bool skip_nils, uint32_t *flags, uint32_t *hf,
+		   int *rc)
+{
+	static const bool on = getenv("MGDK_GSUM_DIRECT") ? atoi(getenv("MGDK_GSUM_DIRECT")) != 0 : true;
+	const BUN ng = a.ngrp;
+	if (!on || !a.gsorted || ng <= 8 || a.ci.n == 0 || !(skip_nils || b->tnonil))
+		return false;
+	*rc = -1;
+	hipStream_t st = stream();
+	const BUN rw = 64 * GS_US, nr = (a.ci.n + rw - 1) / rw;
+	DevBuf eb(nr * 2 * sizeof(GEdge) + 64), mx(64);
+	if (!eb.p || !mx.p || !hip_ok(hipMemsetAsync(mx.p, 0, 8, st), "memset"))
+		return true;
+	const oid off = a.ci.seq - b->hseqbase;
+	const bool vec = ((uintptr_t) a.gids & 15) == 0 && (((uintptr_t) b->theap + (uintptr_t) off * b->twidth) & 15) == 0;
+	static const bool stage = getenv("MGDK_GS_STAGE") ? atoi(getenv("MGDK_GS_STAGE")) != 0 : true;
+	SOut so{bn->theap, basetype(tp), tmax(tp), flags, true};
+	const dim3 gs(grid_for(nr, 4, 65535u * 16u)), blk(256);
+	GAcc acc{};
+	GEdge *e = eb.as<GEdge>();
+	unsigned long long *m = mx.as<unsigned long long>();
+#define GSD(VW_) hipLaunchKernelGGL((k_gaggr_sorted<VW_, false, false>), gs, blk, 0, st, b->theap, off, a.gids, a.gseq, a.min, ng, a.ci.n, true, false, vec, true, stage, acc, m, so, e)
+	switch (b->twidth) {
+	case 1: GSD(1); break;
+	case 2: GSD(2); break;
+	case 4: GSD(4); break;
+	case 8: GSD(8); break;
+	default: GSD(16); break;
+	}
+#undef GSD
+	hipLaunchKernelGGL(k_gedge_sum, dim3(grid_for(2 * nr, 1024, 4096)), blk, 0, st, e, 2 * nr, a.min, ng, so);
+	// the flags read waits for the stream: eb goes back to the shared cache
+	// only after the kernels are done
+	if (read_flags(flags, hf))
+		*rc = 0;
+	return true;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1749,15 +1900,25 @@ mgdk_BATgroupsum(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, boo
 	}
 	uint32_t hf = 0;
 	if (ng) {
-		GAcc acc;
-		unsigned long long *mx;
-		if (gaggr_device(a, b, AGG_SUM | (skip_nils ? 0 : AGG_POS), false, acc, mx) < 0) {
-			mgdk_BBPunfix(bn);
-			return nullptr;
+		int rc = 0;
+		bool read = false;
+		if (gsum_sorted_direct(a, b, bn, tp, skip_nils, fl.as<uint32_t>(), &hf, &rc)) {
+			if (rc < 0) {
+				mgdk_BBPunfix(bn);
+				return nullptr;
+			}
+			read = true;
+		} else {
+			GAcc acc;
+			unsigned long long *mx;
+			if (gaggr_device(a, b, AGG_SUM | (skip_nils ? 0 : AGG_POS), false, acc, mx) < 0) {
+				mgdk_BBPunfix(bn);
+				return nullptr;
+			}
+			hipLaunchKernelGGL(k_gsum_out, dim3(grid_for(ng, 1024, 8192)), dim3(256), 0, stream(), acc, ng,
+					   a.ci.n == 0, basetype(tp), skip_nils, tmax(tp), bn->theap, fl.as<uint32_t>());
 		}
-		hipLaunchKernelGGL(k_gsum_out, dim3(grid_for(ng, 1024, 8192)), dim3(256), 0, stream(), acc, ng, a.ci.n == 0,
-				   basetype(tp), skip_nils, tmax(tp), bn->theap, fl.as<uint32_t>());
-		if (!read_flags(fl.p, &hf)) {
+		if (!read && !read_flags(fl.p, &hf)) {
 			mgdk_BBPunfix(bn);
 			return nullptr;
 		}
