@@ -1836,7 +1836,9 @@ gsum_sorted_direct(const AggrInit &a, mgdk_bat *b, mgdk_bat *bn, int tp, bool sk
 		return false;
 	*rc = -1;
 	hipStream_t st = stream();
-	const BUN rw = 64 * GS_U, nr = (a.ci.n + rw - 1) / rw;
+	// 16-byte values: 8 rows per lane (register budget), else 16
+	const int u = b->twidth >= 16 ? GS_UA : GS_U;
+	const BUN rw = 64 * (BUN) u, nr = (a.ci.n + rw - 1) / rw;
 	DevBuf eb(nr * 2 * sizeof(GEdge) + 64), mx(64);
 	if (!eb.p || !mx.p || !hip_ok(hipMemsetAsync(mx.p, 0, 8, st), "memset"))
 		return true;
@@ -1850,7 +1852,7 @@ gsum_sorted_direct(const AggrInit &a, mgdk_bat *b, mgdk_bat *bn, int tp, bool sk
 	// results of 8 bytes or more stored from the lanes that finish the
 	// groups measured faster than staged in LDS (2.80 vs 3.07 ms for 600M
 	// rows): no LDS, full occupancy
-#define GSD(VW_) hipLaunchKernelGGL((k_gaggr_sorted<VW_, false, false, GS_U>), gs, blk, 0, st, b->theap, off, a.gids, a.gseq, a.min, ng, a.ci.n, true, false, vec, true, false, acc, m, so, e)
+#define GSD(VW_) hipLaunchKernelGGL((k_gaggr_sorted<VW_, false, false, (VW_ >= 16 ? GS_UA : GS_U)>), gs, blk, 0, st, b->theap, off, a.gids, a.gseq, a.min, ng, a.ci.n, true, false, vec, true, false, acc, m, so, e)
 	switch (b->twidth) {
 	case 1: GSD(1); break;
 	case 2: GSD(2); break;
@@ -2340,6 +2342,268 @@ mgdk_BATgroupavg3(mgdk_bat **avgp, mgdk_bat **remp, mgdk_bat **cntp, mgdk_bat *b
 	return 0;
 }
 
+}  // extern "C"
+
+namespace {
+
+// ---- BATgroupmin / max over SORTED group ids in one pass: the segmented
+// reduction of k_gaggr_sorted with (has a candidate, is nil, best value,
+// candidate index) per run -- the first nil wins without skip_nils, else the
+// first row holding the extreme; runs combine in row order, so ties keep
+// the earlier row.  Results (oids) are stored by the lanes that finish the
+// groups, empty groups get oid_nil, the groups a range shares with its
+// neighbours go through per-range edge entries (k_gminpos_edges).
+struct MRun {
+	long long best;
+	unsigned long long idx;    // candidate index, ~0: none
+	bool isn;
+	__device__ void clear()
+	{
+		best = 0;
+		idx = ~0ull;
+		isn = false;
+	}
+	template <bool DOMAX>
+	__device__ void add(const MRun &r)    // *this = (*this) followed by r
+	{
+		if (r.idx == ~0ull || isn)
+			return;
+		if (idx == ~0ull || r.isn || (DOMAX ? r.best > best : r.best < best))
+			*this = r;
+	}
+	__device__ MRun shfl_up(int d) const
+	{
+		MRun t;
+		t.best = __shfl_up(best, d);
+		t.idx = __shfl_up(idx, d);
+		t.isn = __shfl_up((int) isn, d) != 0;
+		return t;
+	}
+};
+
+struct MEdge {
+	oid g;
+	long long best;
+	unsigned long long idx;
+	unsigned long long isn;
+};
+
+struct MOut {
+	oid *out;
+	bool cdense;
+	oid cseq;
+	const oid *coids;
+	uint32_t *flags;
+};
+
+__device__ __forceinline__ uint32_t
+mout_put(const MOut &mo, BUN gi, const MRun &r)
+{
+	const bool nil = r.idx == ~0ull;
+	mo.out[gi] = nil ? MGDK_OID_NIL : mo.cdense ? mo.cseq + r.idx : mo.coids[r.idx];
+	return nil ? 2u : 0u;
+}
+
+template <int VW, bool DOMAX>
+__global__ __launch_bounds__(256) void
+k_gminpos_sorted(const void *base, oid off, const oid *gids, oid gseq, oid gmin, BUN ngrp, BUN n, bool skip_nils,
+		 bool vec, MOut mo, MEdge *edges)
+{
+	typedef typename VTy<VW>::T T;
+	constexpr int U = GS_U;
+	constexpr BUN RW = 64 * U;
+	const int lane = __lane_id();
+	const BUN nwaves = (BUN) gridDim.x * (blockDim.x / 64);
+	const BUN wid = (BUN) blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+	uint32_t f = 0;
+	auto valid = [&](oid g) { return g >= gmin && g - gmin < ngrp; };
+	auto gap = [&](oid prev, oid hi) {   // groups strictly between prev and hi
+		if (prev >= gmin + ngrp)
+			return;
+		oid lo = prev + 1;
+		lo = lo > gmin ? lo : gmin;
+		hi = hi < gmin + ngrp ? hi : gmin + ngrp;
+		MRun e;
+		e.clear();
+		for (oid h = lo; h < hi; h++)
+			f |= mout_put(mo, h - gmin, e);
+	};
+	for (BUN r0 = wid * RW; r0 < n; r0 += nwaves * RW) {
+		const BUN r1 = r0 + RW < n ? r0 + RW : n;
+		const BUN l0 = r0 + (BUN) lane * U;
+		oid g[U];
+		T x[U];
+		if (vec && l0 + U <= r1) {
+			if (gids) {
+				const uint4 *p = (const uint4 *) (gids + l0);
+				uint4 q[U / 2];
+#pragma unroll
+				for (int u = 0; u < U / 2; u++)
+					q[u] = p[u];
+				__builtin_memcpy(g, q, sizeof g);
+			} else {
+#pragma unroll
+				for (int u = 0; u < U; u++)
+					g[u] = gseq + l0 + u;
+			}
+			constexpr int NQ = U * VW / 16;
+			const uint4 *p = (const uint4 *) ((const T *) base + off + l0);
+			uint4 q[NQ];
+#pragma unroll
+			for (int u = 0; u < NQ; u++)
+				q[u] = p[u];
+			__builtin_memcpy(x, q, sizeof x);
+		} else {
+#pragma unroll
+			for (int u = 0; u < U; u++) {
+				const BUN ic = l0 + u < r1 ? l0 + u : r1 - 1;
+				g[u] = gids ? gids[ic] : gseq + ic;
+				x[u] = ((const T *) base)[off + ic];
+			}
+		}
+		MRun P, cur;
+		P.clear();
+		cur.clear();
+		bool single = true;
+		const oid gF = g[0];
+		oid cg = g[0];
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			if (g[u] != cg) {
+				if (single)
+					P = cur;
+				else if (valid(cg))
+					f |= mout_put(mo, cg - gmin, cur);
+				if (g[u] > cg + 1)
+					gap(cg, g[u]);
+				single = false;
+				cur.clear();
+				cg = g[u];
+			}
+			const BUN i = l0 + u;
+			if (i < r1 && valid(g[u])) {
+				const bool vn = is_nil(x[u]);
+				if (!(skip_nils && vn)) {
+					MRun r;
+					r.best = (long long) x[u];
+					r.idx = i;
+					r.isn = vn;
+					cur.add<DOMAX>(r);
+				}
+			}
+		}
+		const oid gL = cg;
+		const oid gLprev = __shfl_up(gL, 1), gFnext = __shfl_down(gF, 1);
+		const bool connects = lane > 0 && gLprev == gF;
+		const bool nextconn = lane < 63 && gFnext == gL;
+		const unsigned long long chain = __ballot(single && (lane == 0 || connects));
+		const bool rfirst = lane == 0 || (connects && (~chain & ((1ull << lane) - 1)) == 0);
+		// segmented scan of the last runs (a run's earlier part is on the left)
+		MRun t = cur;
+		bool hd = !(single && connects);
+#pragma unroll
+		for (int d = 1; d < 64; d <<= 1) {
+			const MRun o = t.shfl_up(d);
+			const bool th = __shfl_up((int) hd, d) != 0;
+			if (lane >= d) {
+				if (!hd) {
+					MRun c = o;
+					c.add<DOMAX>(t);
+					t = c;
+				}
+				hd |= th;
+			}
+		}
+		const MRun cin = t.shfl_up(1);
+		if (lane < 63 && gFnext > gL + 1)
+			gap(gL, gFnext);
+		if (lane == 0) {
+			if (r0 == 0) {
+				MRun e;
+				e.clear();
+				for (oid h = gmin; h < gF && h < gmin + ngrp; h++)
+					f |= mout_put(mo, h - gmin, e);
+			} else {
+				const oid gp = gids ? gids[r0 - 1] : gseq + r0 - 1;
+				if (gF > gp + 1)
+					gap(gp, gF);
+			}
+		}
+		if (lane == 63 && r1 == n)
+			gap(gL, gmin + ngrp);
+		bool e0 = false;
+		MRun e0run;
+		e0run.clear();
+		if (!single) {
+			if (connects) {
+				MRun c = cin;
+				c.add<DOMAX>(P);
+				P = c;
+			}
+			if (valid(gF)) {
+				if (rfirst) {
+					e0 = true;
+					e0run = P;
+				} else {
+					f |= mout_put(mo, gF - gmin, P);
+				}
+			}
+			if (!nextconn && valid(gL) && lane < 63)
+				f |= mout_put(mo, gL - gmin, cur);
+		} else if (!nextconn && valid(gL) && lane < 63) {
+			if (rfirst) {
+				e0 = true;
+				e0run = t;
+			} else {
+				f |= mout_put(mo, gL - gmin, t);
+			}
+		}
+		const BUN rk = r0 / RW;
+		if (e0 || (__ballot(e0) == 0 && lane == 0))
+			edges[2 * rk] = MEdge{gF, e0run.best, e0run.idx, e0run.isn};
+		if (lane == 63) {
+			MRun r = single ? t : cur;
+			if (!valid(gL))
+				r.clear();
+			edges[2 * rk + 1] = MEdge{gL, r.best, r.idx, r.isn};
+		}
+	}
+	for (int o = 32; o > 0; o >>= 1)
+		f |= __shfl_xor(f, o);
+	if (lane == 0 && f)
+		publish_or(mo.flags, f);
+}
+
+template <bool DOMAX>
+__global__ __launch_bounds__(256) void
+k_gminpos_edges(const MEdge *e, BUN ne, oid gmin, BUN ngrp, MOut mo)
+{
+	uint32_t f = 0;
+	for (BUN j = (BUN) blockIdx.x * blockDim.x + threadIdx.x; j < ne; j += (BUN) gridDim.x * blockDim.x) {
+		const oid g = e[j].g;
+		if ((j > 0 && e[j - 1].g == g) || g < gmin || g - gmin >= ngrp)
+			continue;
+		MRun acc;
+		acc.clear();
+		for (BUN q = j; q < ne && e[q].g == g; q++) {
+			MRun r;
+			r.best = e[q].best;
+			r.idx = e[q].idx;
+			r.isn = e[q].isn != 0;
+			acc.add<DOMAX>(r);
+		}
+		f |= mout_put(mo, g - gmin, acc);
+	}
+	for (int o = 32; o > 0; o >>= 1)
+		f |= __shfl_xor(f, o);
+	if (__lane_id() == 0 && f)
+		publish_or(mo.flags, f);
+}
+
+}  // namespace
+
+extern "C" {
+
 // the rows holding each group's extreme value (target) and its first nil:
 // smallest candidate index of each (atomicMin, skipped when not smaller)
 __global__ __launch_bounds__(256) void
@@ -2410,13 +2674,53 @@ groupminmax(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, bool skip_nils, 
 		bn->tnonil = ng == 0;
 		return bn;
 	}
+	hipStream_t st = stream();
+	static const bool direct = getenv("MGDK_GMINPOS_DIRECT") ? atoi(getenv("MGDK_GMINPOS_DIRECT")) != 0 : true;
+	if (direct && a.gsorted && ng > 8 && b->twidth <= 8) {
+		// sorted ids: one pass straight into the result (k_gminpos_sorted)
+		const BUN rw = 64 * GS_U, nr = (a.ci.n + rw - 1) / rw;
+		DevBuf eb(nr * 2 * sizeof(MEdge) + 64), fl(16);
+		if (!eb.p || !fl.p || !hip_ok(hipMemsetAsync(fl.p, 0, 16, st), "memset")) {
+			mgdk_BBPunfix(bn);
+			return nullptr;
+		}
+		const oid off = a.ci.seq - b->hseqbase;
+		const bool vec = ((uintptr_t) a.gids & 15) == 0 &&
+			(((uintptr_t) b->theap + (uintptr_t) off * b->twidth) & 15) == 0;
+		MOut mo{(oid *) bn->theap, c0.dense, c0.seq, c0.oids, fl.as<uint32_t>()};
+		const dim3 gs(grid_for(nr, 4, 65535u * 16u)), blk(256);
+		MEdge *ep = eb.as<MEdge>();
+#define GMP(VW_, D_) hipLaunchKernelGGL((k_gminpos_sorted<VW_, D_>), gs, blk, 0, st, b->theap, off, a.gids, a.gseq, a.min, ng, a.ci.n, skip_nils, vec, mo, ep)
+#define GMP2(VW_) do { if (domax) GMP(VW_, true); else GMP(VW_, false); } while (0)
+		switch (b->twidth) {
+		case 1: GMP2(1); break;
+		case 2: GMP2(2); break;
+		case 4: GMP2(4); break;
+		default: GMP2(8); break;
+		}
+#undef GMP2
+#undef GMP
+		if (domax)
+			hipLaunchKernelGGL(k_gminpos_edges<true>, dim3(grid_for(2 * nr, 1024, 4096)), blk, 0, st, ep, 2 * nr,
+					   a.min, ng, mo);
+		else
+			hipLaunchKernelGGL(k_gminpos_edges<false>, dim3(grid_for(2 * nr, 1024, 4096)), blk, 0, st, ep, 2 * nr,
+					   a.min, ng, mo);
+		uint32_t hf = 0;
+		if (!read_flags(fl.p, &hf)) {
+			mgdk_BBPunfix(bn);
+			return nullptr;
+		}
+		bn->tnil = (hf & 2) != 0;
+		bn->tnonil = !bn->tnil;
+		return bn;
+	}
 	GAcc acc;
 	unsigned long long *mxa;
 	if (gaggr_device(a, b, AGG_MINMAX, false, acc, mxa) < 0) {
 		mgdk_BBPunfix(bn);
 		return nullptr;
 	}
-	hipStream_t st = stream();
 	DevBuf fn(ng * 8 + 8), fb(ng * 8 + 8), fl(16);
 	const long long *tgt = domax ? acc.mx : acc.mn;     // each group's extreme value
 	if (!fn.p || !fb.p || !fl.p || !hip_ok(hipMemsetAsync(fl.p, 0, 16, st), "memset") ||

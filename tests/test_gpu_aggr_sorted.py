@@ -129,7 +129,32 @@ def test_sorted_groupsum_empty_groups(gdk, ora):
     for skip in (True, False):
         _eq(gdk.BATgroupsum(V, G, E, gdk.TYPE_lng, skip), ora.BATgroupsum(OV, OG, OE, ora.TYPE_lng, skip))
         _eq(gdk.BATgroupcount(V, G, E, skip), ora.BATgroupcount(OV, OG, OE, skip))
+        _eq(gdk.BATgroupmin(V, G, E, skip), ora.BATgroupminmax(OV, OG, OE, False, skip))
+        _eq(gdk.BATgroupmax(V, G, E, skip), ora.BATgroupminmax(OV, OG, OE, True, skip))
         a, rm, c = gdk.BATgroupavg3(V, G, E, skip)
         oa, orm, oc = ora.BATgroupavg3(OV, OG, OE, skip)
         for d, o in ((a, oa), (rm, orm), (c, oc)):
             assert np.array_equal(np.asarray(d.values()), np.asarray(o.values()))
+
+
+@pytest.mark.parametrize("tname", ["bte", "int", "lng"])
+def test_sorted_groupminmax_ties_nils_cands(gdk, ora, tname):
+    """first row of the extreme on ties, the first nil without skip_nils,
+    candidate oids in the result, groups spanning lanes and ranges"""
+    r = rng(840)
+    n = 250_001
+    gids = _runs(r, n, 300)
+    vals = r.integers(-3, 4, n).astype({"bte": np.int8, "int": np.int32, "lng": np.int64}[tname])
+    nil = {"bte": -128, "int": -(1 << 31), "lng": NIL64}[tname]
+    vals[r.random(n) < 0.001] = nil
+    (V, OV), _ = _cols(gdk, ora, tname, vals, gids)
+    cand = np.sort(r.choice(n, 200_000, replace=False)).astype(np.uint64)
+    S = gdk.BAT.from_numpy(gdk.TYPE_oid, cand, sorted_=True, revsorted=False, key=True, nonil=True)
+    OS = ora.Bat.from_array(ora.TYPE_oid, cand, sorted_=True, key=True, nonil=True)
+    gs = gids[cand.astype(np.int64)]
+    Gs = gdk.BAT.from_numpy(gdk.TYPE_oid, gs, hseqbase=int(cand[0]), sorted_=True, revsorted=False, key=False,
+                            nonil=True)
+    OGs = ora.Bat.from_array(ora.TYPE_oid, gs, hseqbase=int(cand[0]), sorted_=True, nonil=True)
+    for skip in (True, False):
+        _eq(gdk.BATgroupmin(V, Gs, None, skip, s=S), ora.BATgroupminmax(OV, OGs, None, False, skip, s=OS))
+        _eq(gdk.BATgroupmax(V, Gs, None, skip, s=S), ora.BATgroupminmax(OV, OGs, None, True, skip, s=OS))
