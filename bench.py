@@ -75,7 +75,10 @@ def main():
         if args.dist_backend == "nccl":
             torch.cuda.set_device(local)
             dev = "cuda:%d" % local
-        dist.init_process_group(args.dist_backend)
+        import datetime
+        # a rank stuck in a collective (another rank failed) ends the job
+        # instead of waiting for the default 10 minutes
+        dist.init_process_group(args.dist_backend, timeout=datetime.timedelta(seconds=240))
 
     from monetdb_amd import gdk
     gdk.init(local)
@@ -195,11 +198,19 @@ def main():
                                     "grows_per_s": round(rows / op1_ms / 1e6, 2)}
 
     if not args.no_dist_legs:
-        extra["config4_orderkey_group"] = leg_orderkey_group(args, gdk, D, dist, dev, cols, rows, row0, world,
-                                                             barrier)
+        # a leg that fails (the same way on every rank) is reported in the
+        # line instead of losing the headline measurement
+        try:
+            extra["config4_orderkey_group"] = leg_orderkey_group(args, gdk, D, dist, dev, cols, rows, row0, world,
+                                                                 barrier)
+        except Exception as ex:  # noqa: BLE001
+            extra["config4_orderkey_group"] = {"error": str(ex)[:300]}
         del cols, qargs
         gdk.lib().mgdk_mem_release_cache()
-        extra["config5_window_bounds"] = leg_window(args, gdk, D, dist, dev, rank, world, barrier)
+        try:
+            extra["config5_window_bounds"] = leg_window(args, gdk, D, dist, dev, rank, world, barrier)
+        except Exception as ex:  # noqa: BLE001
+            extra["config5_window_bounds"] = {"error": str(ex)[:300]}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
