@@ -1296,6 +1296,15 @@ group_core(mgdk_bat **groups, mgdk_bat **extents, mgdk_bat **histo, mgdk_bat *b,
 			goto fail;
 		goto done;
 	}
+	// the order of b is established first (gdk_group.c:764-765), so a
+	// sorted column whose property is not set yet (e.g. the concatenation of
+	// the ranks' sorted partial keys after an exchange) takes the
+	// consecutive-comparison path below; str order is by content, which the
+	// offsets do not show
+	if (b->ttype != MGDK_str) {
+		(void) mgdk_BATordered(b);
+		(void) mgdk_BATordered_rev(b);
+	}
 	// all values equal and no (or a constant) prior grouping: one group
 	// (gdk_group.c:768-770 evaluates BATordered / BATordered_rev on g)
 	if (b->tsorted && b->trevsorted && (!g || (mgdk_BATordered(g) && mgdk_BATordered_rev(g)))) {

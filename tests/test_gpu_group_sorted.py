@@ -61,3 +61,18 @@ def test_group_ordered(gdk, ora, tname, dt, rev):
     _same(g, og, extra=True)
     _same(e, oe)
     _same(h, oh)
+
+
+def test_group_establishes_order(gdk, ora):
+    """BATgroup computes b's order first (gdk_group.c:764-765): a sorted
+    column without the property set groups like the oracle and comes back
+    with tsorted known"""
+    r = np.random.default_rng(77)
+    vals = np.sort(r.integers(-10**6, 10**6, 300_001)).astype(np.int64)
+    b = gdk.BAT.from_numpy(gdk.TYPE_lng, vals, sorted_=False, revsorted=False, key=False, nonil=True)
+    g, e, h = gdk.BATgroup(b)
+    og, oe, oh = ora.BATgroup(ora.Bat.from_array(ora.TYPE_lng, vals))
+    assert np.array_equal(g.to_numpy(), og.values())
+    assert np.array_equal(e.to_numpy(), oe.values())
+    assert np.array_equal(h.to_numpy(), oh.values())
+    assert b.s.tsorted == 1
