@@ -153,6 +153,77 @@ k_order_flags(Col c, BUN n, unsigned long long *first)
 	}
 }
 
+// the same with the value width a template parameter: a lane's 8 rows (and
+// their predecessors, mostly the same lines) loaded before any compare, one
+// workgroup minimum per flag published only when smaller than the visible
+// one (a same-word atomic per workgroup of a large grid serialises)
+template <typename T>
+__global__ void __launch_bounds__(256)
+k_order_flags_t(const T *v, BUN n, unsigned long long *first)
+{
+	// a wave owns 64 * V * U consecutive values, a lane V consecutive ones
+	// per step read with one 16-byte load (the heap is 16-byte aligned: the
+	// host checks); a value's predecessor is the one before it in the lane,
+	// or the previous lane's last (lane 63 of the previous step for lane 0),
+	// so each value is loaded once
+	constexpr int V = 16 / (int) sizeof(T), U = 4;
+	typedef T vt __attribute__((ext_vector_type(V)));
+	const unsigned lane = __lane_id(), w = threadIdx.x >> 6;
+	constexpr BUN STEP = 64 * V * U;
+	unsigned long long fd = NONE, fa = NONE, fe = NONE;
+	for (BUN t0 = ((BUN) blockIdx.x * 4 + w) * STEP; t0 < n; t0 += (BUN) gridDim.x * 4 * STEP) {
+		vt y[U];
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const BUN e0 = t0 + ((BUN) u * 64 + lane) * V;
+			if (e0 + V <= n) {
+				y[u] = __builtin_nontemporal_load((const vt *) (v + e0));
+			} else {
+#pragma unroll
+				for (int k = 0; k < V; k++)
+					y[u][k] = v[e0 + k < n ? e0 + k : n - 1];
+			}
+		}
+		T carry = v[t0 ? t0 - 1 : 0];      // the value before the wave's first
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const BUN e0 = t0 + ((BUN) u * 64 + lane) * V;
+			const T up = __shfl_up((T) y[u][V - 1], 1);
+			T x = lane == 0 ? carry : up;
+			carry = __shfl((T) y[u][V - 1], 63);
+#pragma unroll
+			for (int k = 0; k < V; k++) {
+				const BUN p = e0 + k;
+				const T yk = y[u][k];
+				if (p > 0 && p < n) {
+					if (x > yk)
+						fd = p < fd ? p : fd;
+					else if (x < yk)
+						fa = p < fa ? p : fa;
+					else
+						fe = p < fe ? p : fe;
+				}
+				x = yk;
+			}
+		}
+		// later rows cannot lower the minima once every lane has all three
+		// (wave-uniform: the shuffles need the whole wave)
+		if (__all(fd != NONE && fa != NONE && fe != NONE))
+			break;
+	}
+	auto mn = [](unsigned long long a, unsigned long long b) { return a < b ? a : b; };
+	fd = block_reduce(fd, mn);
+	fa = block_reduce(fa, mn);
+	fe = block_reduce(fe, mn);
+	if (threadIdx.x == 0) {
+		unsigned long long *f[3] = {&first[0], &first[1], &first[2]};
+		const unsigned long long val[3] = {fd, fa, fe};
+		for (int k = 0; k < 3; k++)
+			if (val[k] < __hip_atomic_load(f[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+				atomicMin(f[k], val[k]);
+	}
+}
+
 // neighbour relations of an oid result column: bit 0 some v[i-1] < v[i],
 // bit 1 some >, bit 2 some ==, bit 3 some v[i] != v[i-1] + 1
 __global__ void __launch_bounds__(256)
@@ -310,8 +381,22 @@ scan_order(const mgdk_bat *b, Ord &o)
 	hipStream_t st = stream();
 	if (!hip_ok(hipMemsetAsync(m, 0xff, 24, st), "memset"))
 		return -1;
-	if (b->count > 1)
-		hipLaunchKernelGGL(k_order_flags, dim3(grid256(b->count)), dim3(256), 0, st, col_of(b), b->count, m);
+	{
+		const Col c = col_of(b);
+		const dim3 gt(grid_for(b->count, 4 * 64 * 64, 8192));     // 4 waves x 64 lanes x 64 B per step
+		if (b->count > 1) {
+			if (c.base == nullptr || ((uintptr_t) c.base & 15) != 0)
+				hipLaunchKernelGGL(k_order_flags, dim3(grid256(b->count)), dim3(256), 0, st, c, b->count, m);
+			else if (c.w == 1)
+				hipLaunchKernelGGL(k_order_flags_t<int8_t>, gt, dim3(256), 0, st, (const int8_t *) c.base, b->count, m);
+			else if (c.w == 2)
+				hipLaunchKernelGGL(k_order_flags_t<int16_t>, gt, dim3(256), 0, st, (const int16_t *) c.base, b->count, m);
+			else if (c.w == 4)
+				hipLaunchKernelGGL(k_order_flags_t<int32_t>, gt, dim3(256), 0, st, (const int32_t *) c.base, b->count, m);
+			else
+				hipLaunchKernelGGL(k_order_flags_t<int64_t>, gt, dim3(256), 0, st, (const int64_t *) c.base, b->count, m);
+		}
+	}
 	if (!hip_ok(hipMemcpyAsync(h, m, 24, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
 		return -1;
 	o.have = true;
@@ -322,12 +407,22 @@ scan_order(const mgdk_bat *b, Ord &o)
 }
 
 // BATordered (gdk/gdk_batop.c:2002-2179): 1 / 0, -1 on error
+// the scan compares values as signed 64-bit integers: flt / dbl / hge / str
+// columns are not scanned (reported not ordered unless their property says
+// so); none of this library's users of the order passes them
+static bool
+order_scannable(const mgdk_bat *b)
+{
+	const int t = b->ttype;
+	return t != MGDK_flt && t != MGDK_dbl && t != MGDK_str && b->twidth <= 8;
+}
+
 int
 ordered(mgdk_bat *b, Ord &o)
 {
 	if (b->ttype == MGDK_void || b->tsorted || b->count == 0)
 		return 1;
-	if (b->tnosorted > 0)
+	if (b->tnosorted > 0 || !order_scannable(b))
 		return 0;
 	if (scan_order(b, o) < 0)
 		return -1;
@@ -357,7 +452,7 @@ ordered_rev(mgdk_bat *b, Ord &o)
 		return 1;
 	if (b->ttype == MGDK_void)
 		return b->tseqbase == MGDK_OID_NIL;
-	if (tdense(b) || b->tnorevsorted > 0)
+	if (tdense(b) || b->tnorevsorted > 0 || !order_scannable(b))
 		return 0;
 	if (scan_order(b, o) < 0)
 		return -1;
