@@ -314,8 +314,12 @@ k_andor(const K *keys, BUN n, unsigned long long *out)
 	a = block_reduce(a, [](unsigned long long x, unsigned long long y) { return x & y; });
 	o = block_reduce(o, [](unsigned long long x, unsigned long long y) { return x | y; });
 	if (threadIdx.x == 0) {
-		atomicAnd(&out[0], a);
-		atomicOr(&out[1], o);
+		const unsigned long long ca = __hip_atomic_load(&out[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		const unsigned long long co = __hip_atomic_load(&out[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		if ((ca & a) != ca)
+			atomicAnd(&out[0], a);
+		if ((co | o) != co)
+			atomicOr(&out[1], o);
 	}
 }
 
@@ -380,15 +384,30 @@ k_keys(const T *col, BUN n, bool reverse, bool nilslast, K *keys, unsigned long 
 		__syncthreads();
 	}
 	unsigned long long a = ~0ull, o = 0;
-	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
-		const K k = keyimg<T, K>(col[i], reverse, nilslast);
-		keys[i] = k;
-		a &= (unsigned long long) k;
-		o |= (unsigned long long) k;
-		if (dh)
+	// 8 values per thread per step, all loaded before the first is used
+	constexpr int KU = 8;
+	const BUN stride = (BUN) gridDim.x * blockDim.x;
+	for (BUN i0 = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += KU * stride) {
+		T x[KU];
 #pragma unroll
-			for (int q = 0; q < NBYTES; q++)
-				atomicAdd(&h[q][(uint32_t) (k >> (8 * q)) & 255], 1u);
+		for (int u = 0; u < KU; u++) {
+			const BUN i = i0 + u * stride;
+			x[u] = col[i < n ? i : n - 1];
+		}
+#pragma unroll
+		for (int u = 0; u < KU; u++) {
+			const BUN i = i0 + u * stride;
+			if (i >= n)
+				break;
+			const K k = keyimg<T, K>(x[u], reverse, nilslast);
+			keys[i] = k;
+			a &= (unsigned long long) k;
+			o |= (unsigned long long) k;
+			if (dh)
+#pragma unroll
+				for (int q = 0; q < NBYTES; q++)
+					atomicAdd(&h[q][(uint32_t) (k >> (8 * q)) & 255], 1u);
+		}
 	}
 	if (dh) {
 		__syncthreads();
@@ -399,8 +418,14 @@ k_keys(const T *col, BUN n, bool reverse, bool nilslast, K *keys, unsigned long 
 	a = block_reduce(a, [](unsigned long long x, unsigned long long y) { return x & y; });
 	o = block_reduce(o, [](unsigned long long x, unsigned long long y) { return x | y; });
 	if (threadIdx.x == 0) {
-		atomicAnd(&andor[0], a);
-		atomicOr(&andor[1], o);
+		// only when it changes the visible value: a same-word atomic from
+		// every workgroup serialises
+		const unsigned long long ca = __hip_atomic_load(&andor[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		const unsigned long long co = __hip_atomic_load(&andor[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		if ((ca & a) != ca)
+			atomicAnd(&andor[0], a);
+		if ((co | o) != co)
+			atomicOr(&andor[1], o);
 	}
 }
 
@@ -649,7 +674,7 @@ sort_typed(const mgdk_bat *b, bool reverse, bool nilslast, mgdk_bat *sn, mgdk_ba
 	DevBuf dh(8 * 256 * 4);
 	if (!dh.p || !hip_ok(hipMemsetAsync(dh.p, 0, 8 * 256 * 4, st), "memset"))
 		return -1;
-	hipLaunchKernelGGL((k_keys<T, K>), dim3(grid_for(n, 2048, 4096)), dim3(256), 0, st, (const T *) b->theap, n,
+	hipLaunchKernelGGL((k_keys<T, K>), dim3(grid_for(n, 8192, 1024)), dim3(256), 0, st, (const T *) b->theap, n,
 			   reverse, nilslast, k0.as<K>(), ao, dh.as<uint32_t>());
 	FinalOut fo{};
 	fo.vw = b->twidth;
