@@ -731,6 +731,7 @@ struct AggrInit {
 	const uint8_t *g8; // 1-byte image of gids kept by BATgroup (or NULL)
 	oid gseq;
 	bool gsorted;      // g non-decreasing: every group a run of rows
+	bool gkey;         // g strictly increasing (or dense): at most one row per group
 };
 
 // ---- many groups, g sorted (every group a run of consecutive rows, as
@@ -1258,6 +1259,7 @@ aggr_init(AggrInit *a, mgdk_bat **bp, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s)
 	a->g8 = a->gids ? img8_get(g) : nullptr;
 	a->gseq = g->tseqbase;
 	a->gsorted = g->ttype == MGDK_void || g->tsorted;
+	a->gkey = g->ttype == MGDK_void ? g->tseqbase != MGDK_OID_NIL : (g->tkey && g->tsorted);
 	if (e) {
 		a->ngrp = e->count;
 		a->min = e->hseqbase;
@@ -1824,6 +1826,60 @@ k_avg3c_terms(const T *avg, const long long *rem, const long long *cnt, oid off,
 		atomicOr(flags, 1u);
 }
 
+// one row per group, row i in group min + i (g strictly increasing over
+// exactly the group range): a grouped aggregate is then element-wise
+bool
+one_row_groups(const AggrInit &a)
+{
+	const BUN ng = a.ngrp;
+	if (!a.gkey || a.ci.n != ng || ng == 0)
+		return false;
+	if (a.gids == nullptr)
+		return a.gseq == a.min;
+	// strictly increasing ids, as many as groups: they are the range iff
+	// the first is its start and the last its end
+	oid *d = (oid *) meta_buf() + 8;
+	oid *h = (oid *) pinned(16);
+	hipStream_t st = stream();
+	if (!hip_ok(hipMemcpyAsync(d, a.gids, 8, hipMemcpyDeviceToDevice, st), "memcpy") ||
+	    !hip_ok(hipMemcpyAsync(d + 1, a.gids + ng - 1, 8, hipMemcpyDeviceToDevice, st), "memcpy") ||
+	    !hip_ok(hipMemcpyAsync(h, d, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+		return false;
+	return h[0] == a.min && h[1] == a.min + ng - 1;
+}
+
+// BATgroupsum with one row per group: each group's sum is its row's value
+// (nil: no value, so nil; a value beyond the result type overflows)
+template <int VW>
+__global__ __launch_bounds__(256) void
+k_gsum_rows(const void *base, oid off, BUN n, SOut so)
+{
+	typedef typename VTy<VW>::T T;
+	constexpr int U = 8;
+	uint32_t f = 0;
+	const BUN stride = (BUN) gridDim.x * blockDim.x;
+	for (BUN i0 = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += U * stride) {
+		T x[U];
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const BUN i = i0 + u * stride;
+			x[u] = ((const T *) base)[off + (i < n ? i : n - 1)];
+		}
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const BUN i = i0 + u * stride;
+			if (i >= n)
+				break;
+			const bool nil = is_nil(x[u]);
+			f |= sout_put(so, i, nil ? 0 : (uhge) (hge) x[u], nil ? 0 : 1);
+		}
+	}
+	for (int o = 32; o > 0; o >>= 1)
+		f |= __shfl_xor(f, o);
+	if (__lane_id() == 0 && f)
+		publish_or(so.flags, f);
+}
+
 // BATgroupsum over sorted group ids straight into bn (see SOut); false
 // when the case does not apply
 bool
@@ -1836,6 +1892,21 @@ gsum_sorted_direct(const AggrInit &a, mgdk_bat *b, mgdk_bat *bn, int tp, bool sk
 		return false;
 	*rc = -1;
 	hipStream_t st = stream();
+	if (one_row_groups(a)) {
+		SOut so1{bn->theap, basetype(tp), tmax(tp), flags, true};
+		const oid off1 = a.ci.seq - b->hseqbase;
+		const dim3 g1(grid_for(a.ci.n, 256 * 8, 8192)), b1(256);
+		switch (b->twidth) {
+		case 1: hipLaunchKernelGGL(k_gsum_rows<1>, g1, b1, 0, st, b->theap, off1, a.ci.n, so1); break;
+		case 2: hipLaunchKernelGGL(k_gsum_rows<2>, g1, b1, 0, st, b->theap, off1, a.ci.n, so1); break;
+		case 4: hipLaunchKernelGGL(k_gsum_rows<4>, g1, b1, 0, st, b->theap, off1, a.ci.n, so1); break;
+		case 8: hipLaunchKernelGGL(k_gsum_rows<8>, g1, b1, 0, st, b->theap, off1, a.ci.n, so1); break;
+		default: hipLaunchKernelGGL(k_gsum_rows<16>, g1, b1, 0, st, b->theap, off1, a.ci.n, so1); break;
+		}
+		if (read_flags(flags, hf))
+			*rc = 0;
+		return true;
+	}
 	// 16-byte values: 8 rows per lane (register budget), else 16
 	const int u = b->twidth >= 16 ? GS_UA : GS_U;
 	const BUN rw = 64 * (BUN) u, nr = (a.ci.n + rw - 1) / rw;
@@ -2574,6 +2645,31 @@ k_gminpos_sorted(const void *base, oid off, const oid *gids, oid gseq, oid gmin,
 		publish_or(mo.flags, f);
 }
 
+// BATgroupmin / max with one row per group: the row itself, unless its
+// value is nil and nils are skipped (then the group has no value)
+template <int VW>
+__global__ __launch_bounds__(256) void
+k_gminpos_rows(const void *base, oid off, BUN n, bool skip_nils, MOut mo)
+{
+	typedef typename VTy<VW>::T T;
+	uint32_t f = 0;
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		MRun r;
+		r.clear();
+		const T x = ((const T *) base)[off + i];
+		if (!(skip_nils && is_nil(x))) {
+			r.idx = i;
+			r.best = (long long) x;
+			r.isn = is_nil(x);
+		}
+		f |= mout_put(mo, i, r);
+	}
+	for (int o = 32; o > 0; o >>= 1)
+		f |= __shfl_xor(f, o);
+	if (__lane_id() == 0 && f)
+		publish_or(mo.flags, f);
+}
+
 template <bool DOMAX>
 __global__ __launch_bounds__(256) void
 k_gminpos_edges(const MEdge *e, BUN ne, oid gmin, BUN ngrp, MOut mo)
@@ -2690,6 +2786,23 @@ groupminmax(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, bool skip_nils, 
 		MOut mo{(oid *) bn->theap, c0.dense, c0.seq, c0.oids, fl.as<uint32_t>()};
 		const dim3 gs(grid_for(nr, 4, 65535u * 16u)), blk(256);
 		MEdge *ep = eb.as<MEdge>();
+		if (one_row_groups(a)) {
+			const dim3 g1(grid_for(a.ci.n, 256 * 8, 8192));
+			switch (b->twidth) {
+			case 1: hipLaunchKernelGGL(k_gminpos_rows<1>, g1, blk, 0, st, b->theap, off, a.ci.n, skip_nils, mo); break;
+			case 2: hipLaunchKernelGGL(k_gminpos_rows<2>, g1, blk, 0, st, b->theap, off, a.ci.n, skip_nils, mo); break;
+			case 4: hipLaunchKernelGGL(k_gminpos_rows<4>, g1, blk, 0, st, b->theap, off, a.ci.n, skip_nils, mo); break;
+			default: hipLaunchKernelGGL(k_gminpos_rows<8>, g1, blk, 0, st, b->theap, off, a.ci.n, skip_nils, mo); break;
+			}
+			uint32_t hf1 = 0;
+			if (!read_flags(fl.p, &hf1)) {
+				mgdk_BBPunfix(bn);
+				return nullptr;
+			}
+			bn->tnil = (hf1 & 2) != 0;
+			bn->tnonil = !bn->tnil;
+			return bn;
+		}
 #define GMP(VW_, D_) hipLaunchKernelGGL((k_gminpos_sorted<VW_, D_>), gs, blk, 0, st, b->theap, off, a.gids, a.gseq, a.min, ng, a.ci.n, skip_nils, vec, mo, ep)
 #define GMP2(VW_) do { if (domax) GMP(VW_, true); else GMP(VW_, false); } while (0)
 		switch (b->twidth) {

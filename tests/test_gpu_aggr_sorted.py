@@ -158,3 +158,34 @@ def test_sorted_groupminmax_ties_nils_cands(gdk, ora, tname):
     for skip in (True, False):
         _eq(gdk.BATgroupmin(V, Gs, None, skip, s=S), ora.BATgroupminmax(OV, OGs, None, False, skip, s=OS))
         _eq(gdk.BATgroupmax(V, Gs, None, skip, s=S), ora.BATgroupminmax(OV, OGs, None, True, skip, s=OS))
+
+
+@pytest.mark.parametrize("tname", ["int", "lng"])
+def test_one_row_groups(gdk, ora, tname):
+    """strictly increasing group ids covering the group range (one row per
+    group: what the owner of a distributed GROUP BY sees for clustered keys):
+    sums, counts, min / max positions with nils, with and without extents,
+    and ids that skip a group (not one row per group)"""
+    r = rng(850)
+    n = 200_003
+    vals = r.integers(-10**6, 10**6, n).astype(np.int32 if tname == "int" else np.int64)
+    nil = np.iinfo(vals.dtype).min
+    vals[r.random(n) < 0.01] = nil
+    tp, otp = getattr(gdk, "TYPE_" + tname), getattr(ora, "TYPE_" + tname)
+    V = gdk.BAT.from_numpy(tp, vals, sorted_=False, revsorted=False, key=False, nonil=False)
+    OV = ora.Bat.from_array(otp, vals)
+    for gids, ext in ((np.arange(n, dtype=np.uint64), False), (np.arange(n, dtype=np.uint64), True),
+                      (np.arange(n, dtype=np.uint64) + (np.arange(n) > n // 2), False)):
+        G = gdk.BAT.from_numpy(gdk.TYPE_oid, gids, sorted_=True, revsorted=False, key=True, nonil=True)
+        OG = ora.Bat.from_array(ora.TYPE_oid, gids, sorted_=True, key=True, nonil=True)
+        E, OE = (gdk.BAT.dense(0, n), ora.Bat.dense(0, n)) if ext else (None, None)
+        for skip in (True, False):
+            _eq(gdk.BATgroupsum(V, G, E, gdk.TYPE_hge, skip), ora.BATgroupsum(OV, OG, OE, ora.TYPE_hge, skip))
+            _eq(gdk.BATgroupmin(V, G, E, skip), ora.BATgroupminmax(OV, OG, OE, False, skip))
+            _eq(gdk.BATgroupmax(V, G, E, skip), ora.BATgroupminmax(OV, OG, OE, True, skip))
+    big = np.full(n, 1 << 40, np.int64)
+    B = gdk.BAT.from_numpy(gdk.TYPE_lng, big, sorted_=False, revsorted=False, key=False, nonil=True)
+    G = gdk.BAT.from_numpy(gdk.TYPE_oid, np.arange(n, dtype=np.uint64), sorted_=True, revsorted=False, key=True,
+                           nonil=True)
+    with pytest.raises(gdk.GDKError, match="22003!overflow in sum aggregate"):
+        gdk.BATgroupsum(B, G, None, gdk.TYPE_int, True)
