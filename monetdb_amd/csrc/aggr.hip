@@ -1908,7 +1908,9 @@ gsum_sorted_direct(const AggrInit &a, mgdk_bat *b, mgdk_bat *bn, int tp, bool sk
 		return true;
 	}
 	// 16-byte values: 8 rows per lane (register budget), else 16
-	const int u = b->twidth >= 16 ? GS_UA : GS_U;
+	// rows per lane: 8 (2.44 ms for 600M rows / 150M groups; 16: 2.75, 32: 3.05)
+	static const int ud = getenv("MGDK_GS_DIRECT_U") ? atoi(getenv("MGDK_GS_DIRECT_U")) : GS_UA;
+	const int u = b->twidth >= 16 ? GS_UA : (ud == 8 || ud == 32) ? ud : GS_U;
 	const BUN rw = 64 * (BUN) u, nr = (a.ci.n + rw - 1) / rw;
 	DevBuf eb(nr * 2 * sizeof(GEdge) + 64), mx(64);
 	if (!eb.p || !mx.p || !hip_ok(hipMemsetAsync(mx.p, 0, 8, st), "memset"))
@@ -1922,8 +1924,9 @@ gsum_sorted_direct(const AggrInit &a, mgdk_bat *b, mgdk_bat *bn, int tp, bool sk
 	unsigned long long *m = mx.as<unsigned long long>();
 	// results of 8 bytes or more stored from the lanes that finish the
 	// groups measured faster than staged in LDS (2.80 vs 3.07 ms for 600M
-	// rows): no LDS, full occupancy
-#define GSD(VW_) hipLaunchKernelGGL((k_gaggr_sorted<VW_, false, false, (VW_ >= 16 ? GS_UA : GS_U)>), gs, blk, 0, st, b->theap, off, a.gids, a.gseq, a.min, ng, a.ci.n, true, false, vec, true, false, acc, m, so, e)
+	// rows at 16 rows per lane): no LDS, full occupancy
+#define GSD_U(VW_, U_) hipLaunchKernelGGL((k_gaggr_sorted<VW_, false, false, U_>), gs, blk, 0, st, b->theap, off, a.gids, a.gseq, a.min, ng, a.ci.n, true, false, vec, true, false, acc, m, so, e)
+#define GSD(VW_) do { if (VW_ >= 16 || u == GS_UA) GSD_U(VW_, GS_UA); else if (u == 32) GSD_U(VW_, 32); else GSD_U(VW_, GS_U); } while (0)
 	switch (b->twidth) {
 	case 1: GSD(1); break;
 	case 2: GSD(2); break;
@@ -1932,6 +1935,7 @@ gsum_sorted_direct(const AggrInit &a, mgdk_bat *b, mgdk_bat *bn, int tp, bool sk
 	default: GSD(16); break;
 	}
 #undef GSD
+#undef GSD_U
 	hipLaunchKernelGGL(k_gedge_sum, dim3(grid_for(2 * nr, 1024, 4096)), blk, 0, st, e, 2 * nr, a.min, ng, so);
 	// the flags read waits for the stream: eb goes back to the shared cache
 	// only after the kernels are done
