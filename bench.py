@@ -460,6 +460,31 @@ def cpu_baselines_other(args):
     out["config5_rangebounds"] = {"value": round(n5 / med / 1e9, 5), "unit": "Grows/s", "cores": 1,
                                   "kind": "port", "ms": round(med * 1e3, 1),
                                   "sample": "%d rows, 20 partitions, limit 100, one run" % n5}
+    # the same on the box's CPU share: whole partitions per thread (the
+    # bounds never cross a partition), the oracle's C walk releases the GIL
+    try:
+        from concurrent.futures import ThreadPoolExecutor
+        nparts = 8 * share
+        n5m = nparts * 100_000
+        vm = np.cumsum(r.integers(0, 5, n5m)).astype(np.int64)
+        chunks = []
+        per = nparts // share
+        for k in range(share):
+            lo, hi = k * per * 100_000, (k + 1) * per * 100_000
+            pk = np.zeros(hi - lo, np.int8)
+            pk[::100_000] = 1
+            chunks.append((ora.Bat.from_array(ora.TYPE_lng, vm[lo:hi], nonil=True, sorted_=True),
+                           ora.Bat.from_array(ora.TYPE_bit, pk)))
+        with ThreadPoolExecutor(max_workers=share) as ex:
+            t = time.perf_counter()
+            list(ex.map(lambda c: ora.rangebounds(c[0], c[1], 100, True), chunks))
+            med = time.perf_counter() - t
+        out["config5_rangebounds_mt"] = {"value": round(n5m / med / 1e9, 5), "unit": "Grows/s", "cores": share,
+                                         "kind": "port", "ms": round(med * 1e3, 1),
+                                         "sample": "%d rows, %d partitions over %d threads, limit 100, one run"
+                                                   % (n5m, nparts, share)}
+    except Exception as e:  # noqa: BLE001
+        out["config5_rangebounds_mt"] = {"error": str(e)[:200]}
     return out
 
 
