@@ -1003,10 +1003,13 @@ mgdk_tpch_lineitem(uint64_t seed, uint64_t row0, uint64_t n, uint64_t sf_parts, 
 // tuning hooks: atomics, so a concurrent set/launch never tears (dataflow
 // workers call the library concurrently, SURVEY §8 b)
 // round 2: the predicate cascade k_q6s with buffer loads (variant 19: 2
-// chunks in flight, 16 WG/CU; profiles/r02/q6_cascade/tune_buf*.log: 1.79 ms
-// at SF100 against 1.89 with zero-region loads (variant 17) and 2.57-2.81 ms
-// for the full-read k_q6c)
-static std::atomic<int> q6_variant{19}, q6_bpc{16};
+// chunks in flight; profiles/r02/q6_cascade/tune_buf*.log: 1.79 ms at SF100
+// against 1.89 with zero-region loads (variant 17) and 2.57-2.81 ms for the
+// full-read k_q6c).  Round 3 (profiles/r03/q6_tune/): 128 WG/CU instead of
+// 16 -- 1.61 vs 1.83 ms on the same box; more, shorter-lived workgroups
+// balance the cascade's uneven per-chunk work across the CUs (64: 1.67,
+// 160-192: 1.68, 512: 1.79 with more chunks left to the scalar tail loop)
+static std::atomic<int> q6_variant{19}, q6_bpc{128};
 static thread_local unsigned long long q6_lines = 0;
 // fused Q1 main pass (tools/q1_tune.py, profiles/r01/q1_tune.log)
 static std::atomic<int> q1_layout{MGDK_Q1_LAYOUT}, q1_blocks{MGDK_Q1_BLOCKS};
