@@ -84,22 +84,27 @@ def test_join_unique_build(gdk, ora, tname, dt):
 
 
 @pytest.mark.parametrize("nil_matches", [False, True])
-@pytest.mark.parametrize("case", ["plain", "cands", "dups", "date", "skew", "big"])
+@pytest.mark.parametrize("case", ["plain", "cands", "dups", "date", "skew", "big", "big_cands", "big_dups",
+                                  "big_skew"])
 def test_join_partitioned(gdk, ora, nil_matches, case):
     """4-byte keys, >= 64 Ki unique build rows: the global-table path (build
     side cut into per-partition LDS tables stored as one table, one ordered
     probe pass), nils on both sides, candidate lists, a duplicate build key
     (falls back), and a skewed build side whose largest partition overflows
-    its global-table region (-> the radix-partitioned path)."""
+    its global-table region (-> the radix-partitioned path).  The "big"
+    cases (more than 2M build rows) take the radix-partitioned path, with
+    candidates, a duplicate build key, and 9000 build keys in one of its
+    512 partitions."""
     r = rng(85)
-    # "big": more than 2M build rows take the radix-partitioned path
-    nr, nl = (2_100_003, 3_000_001) if case == "big" else (700_001, 2_500_003)
+    big = case.startswith("big")
+    nr, nl = (2_100_003, 3_000_001) if big else (700_001, 2_500_003)
     rv = r.choice(np.arange(-(1 << 30), 1 << 30, 7), nr, replace=False).astype(np.int32)
-    if case == "skew":
-        # 9000 keys whose multiplicative hash (key * 0x9E3779B1, top 7 bits =
-        # partition of 700K build rows) lands in partition 0
+    if case.endswith("skew"):
+        # 9000 keys whose multiplicative hash (key * 0x9E3779B1; top 7 bits =
+        # partition of 700K build rows, top 9 bits of 2.1M) lands in
+        # partition 0
         cinv = pow(0x9E3779B1, -1, 1 << 32)
-        t = r.choice(1 << 25, 9000, replace=False).astype(np.uint64)
+        t = r.choice(1 << (23 if big else 25), 9000, replace=False).astype(np.uint64)
         sk = ((t * np.uint64(cinv)) & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.int32)
         sk = sk[(sk != -(1 << 31)) & ~np.isin(sk, rv)]
         rv[: sk.size] = sk
@@ -109,10 +114,10 @@ def test_join_partitioned(gdk, ora, nil_matches, case):
     lv[::997] = -(1 << 31)
     tp = gdk.TYPE_date if case == "date" else gdk.TYPE_int
     otp = ora.TYPE_date if case == "date" else ora.TYPE_int
-    if case == "dups":
+    if case.endswith("dups"):
         rv[5] = rv[6]
     kw, okw = {}, {}
-    if case == "cands":
+    if case.endswith("cands"):
         sl = np.sort(r.choice(nl, nl // 2, replace=False)).astype(np.uint64) + 11
         sr = np.sort(r.choice(nr, nr - 1000, replace=False)).astype(np.uint64) + 4
         kw = dict(sl=mk(gdk, gdk.TYPE_oid, sl), sr=mk(gdk, gdk.TYPE_oid, sr))
