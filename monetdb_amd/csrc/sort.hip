@@ -33,11 +33,17 @@ using namespace mgdk;
 
 namespace {
 
+#ifndef MGDK_SORT_WAVES
+#define MGDK_SORT_WAVES 4
+#endif
 #ifndef MGDK_SORT_ROWS
 #define MGDK_SORT_ROWS 32
 #endif
+constexpr int SWAVES = MGDK_SORT_WAVES;    // waves per scatter workgroup
 constexpr int SROWS = MGDK_SORT_ROWS;      // rows of 64 keys per wave
-constexpr int STILE = 256 * SROWS;         // keys per tile
+constexpr int STHREADS = 64 * SWAVES;
+constexpr int STILE = STHREADS * SROWS;    // keys per tile
+static_assert(SWAVES >= 4 && STILE % 256 == 0, "the digit steps need 256 threads");
 
 template <typename K>
 __global__ __launch_bounds__(256) void
@@ -47,14 +53,15 @@ k_rs_hist(const K *keys, BUN n, int shift, uint32_t *hist, uint32_t nblocks)
 	h[threadIdx.x] = 0;
 	__syncthreads();
 	const BUN base = (BUN) blockIdx.x * STILE;
-	K k[SROWS];
+	constexpr int HR = STILE / 256;
+	K k[HR];
 #pragma unroll
-	for (int r = 0; r < SROWS; r++) {
+	for (int r = 0; r < HR; r++) {
 		const BUN i = base + r * 256 + threadIdx.x;
 		k[r] = i < n ? keys[i] : 0;
 	}
 #pragma unroll
-	for (int r = 0; r < SROWS; r++) {
+	for (int r = 0; r < HR; r++) {
 		const BUN i = base + r * 256 + threadIdx.x;
 		if (i < n)
 			atomicAdd(&h[(uint32_t) (k[r] >> shift) & 255], 1u);
@@ -156,19 +163,21 @@ emit_final(const FinalOut &fo, BUN g, K key, uint32_t v)
 // per-pass histogram pass and scan.  Otherwise offs holds the digit-major
 // exclusive scan of k_rs_hist's counts.
 template <typename K, bool FINAL, bool IDV, bool LB>
-__global__ __launch_bounds__(256) void
+__global__ __launch_bounds__(STHREADS) void
 k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32_t *offs, uint32_t nblocks,
 	     K *kout, uint32_t *vout, FinalOut fo, uint32_t *ticket, uint64_t *status, const uint32_t *gdig,
 	     uint32_t *err)
 {
 	__shared__ K sk[STILE];
 	__shared__ uint32_t sv[STILE];
-	__shared__ uint32_t wcnt[4][256];     // per-wave running digit counts, then per-wave bases
+	__shared__ uint32_t wcnt[SWAVES][256]; // per-wave running digit counts, then per-wave bases
 	__shared__ uint32_t tstart[256];      // digit start inside the reordered tile
 	__shared__ uint32_t gbase[256];       // digit start of this tile in the output
 	__shared__ uint32_t s_wt[4];
 	__shared__ uint32_t s_tile;
+	// threads 0..255 (waves 0-3) own one digit each in the per-digit steps
 	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+	const bool dig = tid < 256;
 	if (LB) {
 		if (tid == 0)
 			s_tile = atomicAdd(ticket, 1u);
@@ -176,10 +185,11 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 	}
 	const uint32_t blk = LB ? s_tile : blockIdx.x;
 	__shared__ uint32_t lh[256];          // LB: the tile's digit counts, published before ranking
-	if (LB)
+	if (LB && dig)
 		lh[tid] = 0;
-	wcnt[0][tid] = wcnt[1][tid] = wcnt[2][tid] = wcnt[3][tid] = 0;
-	if (!LB)
+	for (unsigned q = tid; q < SWAVES * 256; q += STHREADS)
+		(&wcnt[0][0])[q] = 0;
+	if (!LB && dig)
 		gbase[tid] = offs[(BUN) tid * nblocks + blk];
 	const BUN tbase = (BUN) blk * STILE;
 	const BUN base = tbase + (BUN) w * (64 * SROWS);
@@ -200,7 +210,9 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 			if (base + r * 64 + lane < n)
 				atomicAdd(&lh[(uint32_t) (k[r] >> shift) & 255], 1u);
 		__syncthreads();
-		mgdk_lb::lb_store(status + (size_t) blk * 256 + tid, (blk == 0 ? mgdk_lb::ST_PRE : mgdk_lb::ST_AGG) | lh[tid]);
+		if (dig)
+			mgdk_lb::lb_store(status + (size_t) blk * 256 + tid,
+					  (blk == 0 ? mgdk_lb::ST_PRE : mgdk_lb::ST_AGG) | lh[tid]);
 	}
 	const uint64_t lt = lanemask_lt();
 	uint32_t rk[SROWS];
@@ -221,11 +233,17 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 			wcnt[w][d] = before + (uint32_t) __popcll(peer);
 	}
 	__syncthreads();
-	{
-		// digit d = tid: per-wave bases and the tile's digit prefix
-		const uint32_t c0 = wcnt[0][tid], c1 = wcnt[1][tid], c2 = wcnt[2][tid], c3 = wcnt[3][tid];
-		const uint32_t tot = c0 + c1 + c2 + c3;
-		uint32_t incl = tot;
+	// digit d = tid: per-wave bases and the tile's digit prefix
+	uint32_t tot = 0, incl = 0;
+	if (dig) {
+		uint32_t run = 0;
+#pragma unroll
+		for (int q = 0; q < SWAVES; q++) {
+			const uint32_t c = wcnt[q][tid];
+			wcnt[q][tid] = run;
+			run += c;
+		}
+		tot = incl = run;
 #pragma unroll
 		for (int o = 1; o < 64; o <<= 1) {
 			const uint32_t u = __shfl_up(incl, o);
@@ -234,11 +252,9 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 		}
 		if (lane == 63)
 			s_wt[w] = incl;
-		wcnt[0][tid] = 0;
-		wcnt[1][tid] = c0;
-		wcnt[2][tid] = c0 + c1;
-		wcnt[3][tid] = c0 + c1 + c2;
-		__syncthreads();
+	}
+	__syncthreads();
+	if (dig) {
 		uint32_t ex = incl - tot;
 		for (unsigned q = 0; q < w; q++)
 			ex += s_wt[q];
@@ -287,7 +303,7 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 	const uint32_t nt = (uint32_t) (n - tbase < (BUN) STILE ? n - tbase : (BUN) STILE);
 #pragma unroll
 	for (int u = 0; u < SROWS; u++) {
-		const uint32_t i = tid + u * 256;
+		const uint32_t i = tid + u * STHREADS;
 		if (i < nt) {
 			const K key = sk[i];
 			const uint32_t d = (uint32_t) (key >> shift) & 255;
@@ -607,7 +623,7 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 			f2.keys = kout;
 		uint32_t *tk = lbm.as<uint32_t>(), *er = lbm.as<uint32_t>() + 4;
 		const uint32_t *gd = gdig + s * 256;
-#define SCAT(F, I, L) hipLaunchKernelGGL((k_rs_scatter<K, F, I, L>), dim3(nblocks), dim3(256), 0, st, kin, vin, n, \
+#define SCAT(F, I, L) hipLaunchKernelGGL((k_rs_scatter<K, F, I, L>), dim3(nblocks), dim3(STHREADS), 0, st, kin, vin, n, \
 					 shift, offs.as<uint32_t>(), nblocks, kout, vout, f2, tk, status.as<uint64_t>(), gd, er)
 		if (lb) {
 			if (fin) {
