@@ -24,6 +24,7 @@
 //   runs leave as contiguous stores;
 //   the LAST pass writes the result columns directly: integer values decoded
 //   from the key image (no gather) and the order oids (hseqbase + position).
+#include <type_traits>
 #include <vector>
 
 #include "lookback.h"
@@ -698,10 +699,13 @@ sort_typed(const mgdk_bat *b, bool reverse, bool nilslast, mgdk_bat *sn, mgdk_ba
 	fo.is64 = sizeof(K) == 8;
 	fo.uns = basetype(b->ttype) == MGDK_oid;
 	fo.hseq = b->hseqbase;
-	fo.want_keys = gn != nullptr;
 	// floats (and reverse != nilslast images) are not decodable: gather by order
 	const bool decodable = !is_float && reverse == nilslast;
 	fo.sorted = decodable && sn ? sn->theap : nullptr;
+	// groups: from the decoded sorted values when those are written (equal
+	// values <=> equal images), so the last pass writes no key images
+	const bool gid_vals = gn != nullptr && fo.sorted != nullptr;
+	fo.want_keys = gn != nullptr && !gid_vals;
 	fo.order = on ? (oid *) on->theap : otmp.as<oid>();
 	K *ks;
 	uint32_t *vs;
@@ -724,12 +728,23 @@ sort_typed(const mgdk_bat *b, bool reverse, bool nilslast, mgdk_bat *sn, mgdk_ba
 		if (!cnt.p || !pre.p)
 			return -1;
 		if (nt > 0) {
-			hipLaunchKernelGGL((k_gid_count<K>), dim3((unsigned) nt), dim3(256), 0, st, ks, n,
-					   cnt.as<uint32_t>());
-			if (exclusive_scan(cnt.as<uint32_t>(), pre.as<uint64_t>(), nt, &tot) < 0)
+			auto gids = [&](auto *src) {
+				using KT = std::remove_const_t<std::remove_pointer_t<decltype(src)>>;
+				hipLaunchKernelGGL((k_gid_count<KT>), dim3((unsigned) nt), dim3(256), 0, st, src, n,
+						   cnt.as<uint32_t>());
+				if (exclusive_scan(cnt.as<uint32_t>(), pre.as<uint64_t>(), nt, &tot) < 0)
+					return -1;
+				hipLaunchKernelGGL((k_gid_write<KT>), dim3((unsigned) nt), dim3(256), 0, st, src, n,
+						   pre.as<uint64_t>(), (oid *) gn->theap);
+				return 0;
+			};
+			int rc;
+			if constexpr (!is_float)
+				rc = gid_vals ? gids((const T *) sn->theap) : gids((const K *) ks);
+			else
+				rc = gids((const K *) ks);
+			if (rc < 0)
 				return -1;
-			hipLaunchKernelGGL((k_gid_write<K>), dim3((unsigned) nt), dim3(256), 0, st, ks, n,
-					   pre.as<uint64_t>(), (oid *) gn->theap);
 		}
 		if (!sync())
 			return -1;

@@ -214,7 +214,7 @@ def test_join_duplicates_descending(gdk):
 
 # ---- sort -----------------------------------------------------------------------
 
-@pytest.mark.parametrize("tname,dt", [("bte", np.int8), ("int", np.int32), ("lng", np.int64)])
+@pytest.mark.parametrize("tname,dt", [("bte", np.int8), ("sht", np.int16), ("int", np.int32), ("lng", np.int64)])
 @pytest.mark.parametrize("reverse", [False, True])
 def test_sort_int(gdk, ora, tname, dt, reverse):
     r = rng(91)
