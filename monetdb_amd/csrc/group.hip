@@ -996,6 +996,15 @@ k_grp_seq_ext(BUN ngrp, BUN n, const uint64_t *spos, bool cdense, oid cseq, cons
 	}
 }
 
+// histogram from extents that hold the group starts as oids (dense
+// candidates: the write pass stored cseq + start row straight into them)
+__global__ __launch_bounds__(256) void
+k_grp_seq_hist(BUN ngrp, oid end, const oid *en, int64_t *hn)
+{
+	for (BUN k = (BUN) blockIdx.x * blockDim.x + threadIdx.x; k < ngrp; k += (BUN) gridDim.x * blockDim.x)
+		hn[k] = (int64_t) ((k + 1 < ngrp ? en[k + 1] : end) - en[k]);
+}
+
 // Dense candidates: the same starts in two passes over the keys instead of
 // flags -> 8-byte scan -> ids (three passes and 8 B of scan per row): a
 // count of the starts per 2048-row tile, a scan of the tile counts, then
@@ -1091,7 +1100,7 @@ k_sq_count(KeySrc s, BUN n, uint32_t *tcnt)
 
 template <int W, bool FL, int GK>
 __global__ __launch_bounds__(256) void
-k_sq_write(KeySrc s, BUN n, const uint64_t *tpre, oid *gid, uint64_t *spos)
+k_sq_write(KeySrc s, BUN n, const uint64_t *tpre, oid *gid, uint64_t *spos, uint64_t soff)
 {
 	__shared__ uint32_t tab[SQU * 4];
 	const int lane = __lane_id(), w = threadIdx.x >> 6;
@@ -1129,14 +1138,15 @@ k_sq_write(KeySrc s, BUN n, const uint64_t *tpre, oid *gid, uint64_t *spos)
 			const uint64_t k = base + tab[u * 4 + w] + (uint64_t) __popcll(bal[u] & lt) + st[u] - 1;
 			gid[i] = k;
 			if (st[u])
-				spos[k] = i;
+				spos[k] = soff + i;
 		}
 	}
 }
 
 template <int W, bool FL, int GK>
 static int
-sq_ids(const KeySrc &ks, BUN n, DevBuf &tc, DevBuf &tp, oid *gid, uint64_t *spos, uint64_t *ngrp, bool write)
+sq_ids(const KeySrc &ks, BUN n, DevBuf &tc, DevBuf &tp, oid *gid, uint64_t *spos, uint64_t *ngrp, bool write,
+       uint64_t soff)
 {
 	hipStream_t st = stream();
 	const BUN nt = (n + SQT - 1) / SQT;
@@ -1144,45 +1154,52 @@ sq_ids(const KeySrc &ks, BUN n, DevBuf &tc, DevBuf &tp, oid *gid, uint64_t *spos
 		hipLaunchKernelGGL((k_sq_count<W, FL, GK>), dim3(nt), dim3(256), 0, st, ks, n, tc.as<uint32_t>());
 		return exclusive_scan(tc.as<uint32_t>(), tp.as<uint64_t>(), nt, ngrp);
 	}
-	hipLaunchKernelGGL((k_sq_write<W, FL, GK>), dim3(nt), dim3(256), 0, st, ks, n, tp.as<uint64_t>(), gid, spos);
+	hipLaunchKernelGGL((k_sq_write<W, FL, GK>), dim3(nt), dim3(256), 0, st, ks, n, tp.as<uint64_t>(), gid, spos, soff);
 	return 0;
 }
 
 template <int W, bool FL>
 static int
-sq_ids_g(const KeySrc &ks, BUN n, DevBuf &tc, DevBuf &tp, oid *gid, uint64_t *spos, uint64_t *ngrp, bool write)
+sq_ids_g(const KeySrc &ks, BUN n, DevBuf &tc, DevBuf &tp, oid *gid, uint64_t *spos, uint64_t *ngrp, bool write,
+	 uint64_t soff)
 {
 	if (!ks.has_g)
-		return sq_ids<W, FL, 0>(ks, n, tc, tp, gid, spos, ngrp, write);
+		return sq_ids<W, FL, 0>(ks, n, tc, tp, gid, spos, ngrp, write, soff);
 	if (ks.g8)
-		return sq_ids<W, FL, 1>(ks, n, tc, tp, gid, spos, ngrp, write);
+		return sq_ids<W, FL, 1>(ks, n, tc, tp, gid, spos, ngrp, write, soff);
 	if (ks.g)
-		return sq_ids<W, FL, 2>(ks, n, tc, tp, gid, spos, ngrp, write);
-	return sq_ids<W, FL, 3>(ks, n, tc, tp, gid, spos, ngrp, write);
+		return sq_ids<W, FL, 2>(ks, n, tc, tp, gid, spos, ngrp, write, soff);
+	return sq_ids<W, FL, 3>(ks, n, tc, tp, gid, spos, ngrp, write, soff);
 }
 
 static int
-sq_dispatch(const KeySrc &ks, BUN n, DevBuf &tc, DevBuf &tp, oid *gid, uint64_t *spos, uint64_t *ngrp, bool write)
+sq_dispatch(const KeySrc &ks, BUN n, DevBuf &tc, DevBuf &tp, oid *gid, uint64_t *spos, uint64_t *ngrp, bool write,
+	    uint64_t soff = 0)
 {
 	switch (ks.w) {
-	case 1: return sq_ids_g<1, false>(ks, n, tc, tp, gid, spos, ngrp, write);
-	case 2: return sq_ids_g<2, false>(ks, n, tc, tp, gid, spos, ngrp, write);
-	case 4: return ks.kind == 2 ? sq_ids_g<4, true>(ks, n, tc, tp, gid, spos, ngrp, write)
-				    : sq_ids_g<4, false>(ks, n, tc, tp, gid, spos, ngrp, write);
-	case 8: return ks.kind == 3 ? sq_ids_g<8, true>(ks, n, tc, tp, gid, spos, ngrp, write)
-				    : sq_ids_g<8, false>(ks, n, tc, tp, gid, spos, ngrp, write);
-	default: return sq_ids_g<16, false>(ks, n, tc, tp, gid, spos, ngrp, write);
+	case 1: return sq_ids_g<1, false>(ks, n, tc, tp, gid, spos, ngrp, write, soff);
+	case 2: return sq_ids_g<2, false>(ks, n, tc, tp, gid, spos, ngrp, write, soff);
+	case 4: return ks.kind == 2 ? sq_ids_g<4, true>(ks, n, tc, tp, gid, spos, ngrp, write, soff)
+				    : sq_ids_g<4, false>(ks, n, tc, tp, gid, spos, ngrp, write, soff);
+	case 8: return ks.kind == 3 ? sq_ids_g<8, true>(ks, n, tc, tp, gid, spos, ngrp, write, soff)
+				    : sq_ids_g<8, false>(ks, n, tc, tp, gid, spos, ngrp, write, soff);
+	default: return sq_ids_g<16, false>(ks, n, tc, tp, gid, spos, ngrp, write, soff);
 	}
 }
 
 int
 group_ordered(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mgdk_bat **enp,
-	      mgdk_bat **hnp)
+	      mgdk_bat **hnp, bool want_h)
 {
 	hipStream_t st = stream();
 	const dim3 grd(grid_for(n, 1024, 8192)), blk(256);
 	static const bool two = getenv("MGDK_GROUP_SEQ2") ? atoi(getenv("MGDK_GROUP_SEQ2")) != 0 : true;
 	const bool fast = two && ks.dense && n > 0;
+	// dense candidates: the write pass stores each group's start (cseq +
+	// row) straight into the extents; the histogram, when wanted, is the
+	// difference of neighbouring extents (no start-row array, no pass that
+	// reads it to write the extents)
+	const bool direct = fast && ci.dense;
 	const BUN nt = (n + SQT - 1) / SQT;
 	DevBuf fl(fast ? 0 : n + 8), ex(fast ? 0 : n * 8 + 8), tc(fast ? nt * 4 + 8 : 0), tp(fast ? nt * 8 + 8 : 0);
 	if ((!fast && (!fl.p || !ex.p)) || (fast && (!tc.p || !tp.p)))
@@ -1196,24 +1213,43 @@ group_ordered(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp
 		if (exclusive_scan(fl.as<uint8_t>(), ex.as<uint64_t>(), n, &ngrp) < 0)
 			return -1;
 	}
-	DevBuf spos(ngrp * 8 + 8);
-	mgdk_bat *gn = newbat(hseqb, MGDK_oid, n), *en = newbat(0, MGDK_oid, ngrp), *hn = newbat(0, MGDK_lng, ngrp);
-	if (!gn || !en || !hn || !spos.p) {
+	DevBuf spos(direct ? 8 : ngrp * 8 + 8);
+	mgdk_bat *gn = newbat(hseqb, MGDK_oid, n), *en = newbat(0, MGDK_oid, ngrp);
+	mgdk_bat *hn = want_h ? newbat(0, MGDK_lng, ngrp) : nullptr;
+	if (!gn || !en || (want_h && !hn) || !spos.p) {
 		mgdk_BBPunfix(gn);
 		mgdk_BBPunfix(en);
 		mgdk_BBPunfix(hn);
 		return -1;
 	}
+	uint64_t *starts = direct ? (uint64_t *) en->theap : spos.as<uint64_t>();
 	if (fast)
-		sq_dispatch(ks, n, tc, tp, (oid *) gn->theap, spos.as<uint64_t>(), nullptr, true);
+		sq_dispatch(ks, n, tc, tp, (oid *) gn->theap, starts, nullptr, true, direct ? ci.seq : 0);
 	else
 		hipLaunchKernelGGL(k_grp_seq_ids, grd, blk, 0, st, n, fl.as<uint8_t>(), ex.as<uint64_t>(), (oid *) gn->theap,
 				   spos.as<uint64_t>());
-	hipLaunchKernelGGL(k_grp_seq_ext, dim3(grid_for(ngrp, 1024, 8192)), blk, 0, st, ngrp, n, spos.as<uint64_t>(),
-			   ci.dense, ci.seq, ci.oids, (oid *) en->theap, (int64_t *) hn->theap);
+	if (direct) {
+		if (want_h && ngrp)
+			hipLaunchKernelGGL(k_grp_seq_hist, dim3(grid_for(ngrp, 1024, 8192)), blk, 0, st, ngrp,
+					   (oid) (ci.seq + n), (const oid *) en->theap, (int64_t *) hn->theap);
+	} else {
+		DevBuf hdummy(want_h ? 0 : ngrp * 8 + 8);
+		if (!want_h && !hdummy.p) {
+			mgdk_BBPunfix(gn);
+			mgdk_BBPunfix(en);
+			return -1;
+		}
+		hipLaunchKernelGGL(k_grp_seq_ext, dim3(grid_for(ngrp, 1024, 8192)), blk, 0, st, ngrp, n, spos.as<uint64_t>(),
+				   ci.dense, ci.seq, ci.oids, (oid *) en->theap,
+				   want_h ? (int64_t *) hn->theap : hdummy.as<int64_t>());
+		if (!want_h && !sync()) {       // hdummy goes back to the cache after the kernel
+			mgdk_BBPunfix(gn);
+			mgdk_BBPunfix(en);
+			return -1;
+		}
+	}
 	uint64_t *hl = (uint64_t *) pinned(16);
-	if (!hip_ok(hipMemcpyAsync(hl, spos.as<uint64_t>() + ngrp - 1, 8, hipMemcpyDeviceToHost, st), "memcpy") ||
-	    !sync()) {
+	if (!hip_ok(hipMemcpyAsync(hl, starts + ngrp - 1, 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
 		mgdk_BBPunfix(gn);
 		mgdk_BBPunfix(en);
 		mgdk_BBPunfix(hn);
@@ -1224,13 +1260,16 @@ group_ordered(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp
 	gn->trevsorted = ngrp == 1 || n <= 1;
 	gn->tkey = ngrp == n;
 	gn->tnonil = 1;
-	gn->tmaxpos = hl[0];
-	en->count = hn->count = ngrp;
+	gn->tmaxpos = direct ? hl[0] - ci.seq : hl[0];
+	en->count = ngrp;
 	en->tsorted = en->tkey = en->tnonil = 1;
 	en->trevsorted = ngrp == 1;
-	hn->tkey = ngrp == 1;
-	hn->tsorted = hn->trevsorted = ngrp == n || ngrp == 1;
-	hn->tnonil = 1;
+	if (hn) {
+		hn->count = ngrp;
+		hn->tkey = ngrp == 1;
+		hn->tsorted = hn->trevsorted = ngrp == n || ngrp == 1;
+		hn->tnonil = 1;
+	}
 	oid fl2[2];
 	if (oid_at(en, 0, &fl2[0]) < 0 || oid_at(en, ngrp - 1, &fl2[1]) < 0) {
 		mgdk_BBPunfix(gn);
@@ -1362,7 +1401,7 @@ group_core(mgdk_bat **groups, mgdk_bat **extents, mgdk_bat **histo, mgdk_bat *b,
 		// (gdk_group.c:940-975); 1- and 2-byte keys keep the table paths
 		if (ks.w >= 4 && (b->tsorted || b->trevsorted) &&
 		    (!g || mgdk_BATordered(g) || mgdk_BATordered_rev(g))) {
-			if (group_ordered(ks, n, ci, hseqb, &gn, &en, &hn) < 0)
+			if (group_ordered(ks, n, ci, hseqb, &gn, &en, &hn, histo != nullptr) < 0)
 				goto fail;
 			goto done;
 		}

@@ -202,8 +202,8 @@ class GdkBackend:
     def project(self, order, c):
         return self.gdk.BATproject(order, c)
 
-    def group(self, c):
-        return self.gdk.BATgroup(c)
+    def group(self, c, histo=True):
+        return self.gdk.BATgroup(c, want_histo=histo)
 
     def groupsum(self, c, g, e, tp):
         return self.gdk.BATgroupsum(c, g, e, tp)
@@ -511,7 +511,7 @@ def dist_group_aggr(be, dist, keys, vals):
     if be.n(rk) == 0:
         mk, mf, mc, ms = rk, rfirst, rcount, list(rsums)
     else:
-        g2, e2, _ = be.group(rk)
+        g2, e2, _ = be.group(rk, histo=False)
         mk = be.project(e2, rk)
         mf = be.groupmin(rfirst, g2, e2)
         mc = be.groupsum(rcount, g2, e2, TL)
@@ -539,7 +539,7 @@ def dist_group_avg(be, dist, keys, vals):
     TL, TO, TH = _types(be)
     world, rank = _world(dist)
     row0s = [_s64(x[0]) for x in _gather_int64(dist, be.device, [keys.hseqbase])] if world > 1 else [0]
-    g, e, _ = be.group(keys)
+    g, e, _ = be.group(keys, histo=False)
     a, r, c = be.groupavg3(vals, g, e)
     parts = [be.widen(be.project(e, keys)), e, a, r, c]
     if world > 1:
@@ -550,7 +550,7 @@ def dist_group_avg(be, dist, keys, vals):
     if be.n(rk) == 0:
         mk, mf, ma = rk, rfirst, ra
     else:
-        g2, e2, _ = be.group(rk)
+        g2, e2, _ = be.group(rk, histo=False)
         mk = be.project(e2, rk)
         mf = be.groupmin(rfirst, g2, e2)
         ma = be.groupavg3combine(ra, rr, rc, g2, e2)

@@ -550,11 +550,13 @@ def BATgroupavg3(b, g, e, skip_nils=True, s=None):
     return BAT(a), BAT(r), BAT(c)
 
 
-def BATgroup(b, s=None, g=None, e=None, h=None):
+def BATgroup(b, s=None, g=None, e=None, h=None, want_histo=True):
+    """(groups, extents, histo) -- gdk_group.c:1359; histo is None (and not
+    computed) when want_histo is False, as BATgroup(&g, &e, NULL, ...)."""
     gp, ep, hp = P(), P(), P()
-    _chk(lib().mgdk_BATgroup(C.byref(gp), C.byref(ep), C.byref(hp), b.ptr, _p(s), _p(g), _p(e),
-                             _p(h)))
-    return BAT(gp), BAT(ep), BAT(hp)
+    _chk(lib().mgdk_BATgroup(C.byref(gp), C.byref(ep), C.byref(hp) if want_histo else None, b.ptr, _p(s),
+                             _p(g), _p(e), _p(h)))
+    return BAT(gp), BAT(ep), (BAT(hp) if want_histo else None)
 
 
 def BATjoin(l, r, sl=None, sr=None, nil_matches=False, estimate=0):

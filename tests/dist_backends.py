@@ -92,9 +92,9 @@ class OracleBackend:
         idx = order.arr.astype(np.int64) - c.hseqbase
         return Col(c.tp, c.arr[idx], order.hseqbase)
 
-    def group(self, c):
+    def group(self, c, histo=True):
         g, e, h = ora.BATgroup(c.ora())
-        return _from_ora(g, c.hseqbase), _from_ora(e), _from_ora(h)
+        return _from_ora(g, c.hseqbase), _from_ora(e), (_from_ora(h) if histo else None)
 
     def groupsum(self, c, g, e, tp):
         return _from_ora(ora.BATgroupsum(c.ora(), g.ora(), e.ora(), tp))

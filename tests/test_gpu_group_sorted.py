@@ -53,6 +53,17 @@ def test_group_ordered(gdk, ora, tname, dt, rev):
     _same(g, og, extra=True)
     _same(e, oe)
     _same(h, oh)
+    # a dense candidate slice (extents = its seqbase + start rows, stored by
+    # the write pass itself) and no histogram wanted: BATgroup(&g, &e, NULL, ...)
+    for want_h in (True, False):
+        g, e, h = gdk.BATgroup(D, gdk.BAT.dense(1005, 150_000), want_histo=want_h)
+        og, oe, oh = ora.BATgroup(O, ora.Bat.dense(1005, 150_000))
+        _same(g, og, extra=True)
+        _same(e, oe)
+        if want_h:
+            _same(h, oh)
+        else:
+            assert h is None
     prior = (np.arange(n) // 7000).astype(np.uint64)
     G = (gdk.BAT.from_numpy(gdk.TYPE_oid, prior, sorted_=True, revsorted=False, key=False, nonil=True),
          ora.Bat.from_array(ora.TYPE_oid, prior, sorted_=True, nonil=True))
