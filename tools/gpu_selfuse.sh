@@ -1,4 +1,6 @@
-# select: scan fused into the write pass (default) vs the separate scan kernel
+# select: scan fused into the write pass vs the separate scan kernel (the
+# round-3 experiment behind profiles/r03/select_fuse; the fused variant was
+# dropped, so both legs now run the same library unless a variant is rebuilt)
 set -e
 out=gpurun_out/selfuse
 mkdir -p $out
