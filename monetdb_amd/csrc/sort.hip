@@ -18,8 +18,10 @@
 //   tiles' digit counts (each tile publishes its counts before ranking, so
 //   the walk back is short; MGDK_SORT_LB=0 restores the per-pass histogram
 //   + scan); in the tile each wave
-//   ranks its 16 rows of 64 keys with 8 bit-sliced ballots against per-wave
-//   running digit counters (no workgroup barrier per row), the tile is
+//   ranks its 32 rows of 64 keys against per-wave running digit counters
+//   (no workgroup barrier per row), a row's same-digit lanes found through
+//   a per-wave LDS lane mask per digit (one OR, one read, one clear;
+//   MGDK_SORT_LDSMATCH=0 restores 8 bit-sliced ballots), the tile is
 //   reordered by digit in LDS and written out in that order, so equal-digit
 //   runs leave as contiguous stores;
 //   the LAST pass writes the result columns directly: integer values decoded
@@ -45,6 +47,11 @@ constexpr int SROWS = MGDK_SORT_ROWS;      // rows of 64 keys per wave
 constexpr int STHREADS = 64 * SWAVES;
 constexpr int STILE = STHREADS * SROWS;    // keys per tile
 static_assert(SWAVES >= 4 && STILE % 256 == 0, "the digit steps need 256 threads");
+// 1: a row's peer lanes (same digit) come from a per-wave LDS lane mask per
+// digit (one OR, one read, one clear) instead of 8 bit-sliced ballots
+#ifndef MGDK_SORT_LDSMATCH
+#define MGDK_SORT_LDSMATCH 1
+#endif
 
 template <typename K>
 __global__ __launch_bounds__(256) void
@@ -170,7 +177,7 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 	     uint32_t *err)
 {
 	__shared__ K sk[STILE];
-	__shared__ uint32_t sv[STILE];
+	__shared__ __attribute__((aligned(16))) uint32_t sv[STILE];
 	__shared__ uint32_t wcnt[SWAVES][256]; // per-wave running digit counts, then per-wave bases
 	__shared__ uint32_t tstart[256];      // digit start inside the reordered tile
 	__shared__ uint32_t gbase[256];       // digit start of this tile in the output
@@ -194,6 +201,14 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 		gbase[tid] = offs[(BUN) tid * nblocks + blk];
 	const BUN tbase = (BUN) blk * STILE;
 	const BUN base = tbase + (BUN) w * (64 * SROWS);
+#if MGDK_SORT_LDSMATCH
+	// the wave's 256 digit lane masks live in sv until the tile is placed
+	static_assert(SWAVES * 256 * 2 <= STILE, "lane masks fit in sv");
+	unsigned long long *wm = (unsigned long long *) sv + (size_t) w * 256;
+#pragma unroll
+	for (int q = 0; q < 4; q++)
+		wm[lane + 64 * q] = 0ull;
+#endif
 	K k[SROWS];
 	uint32_t v[SROWS];
 #pragma unroll
@@ -222,12 +237,25 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 		const BUN i = base + r * 64 + lane;
 		const bool valid = i < n;
 		const uint32_t d = (uint32_t) (k[r] >> shift) & 255;
+#if MGDK_SORT_LDSMATCH
+		// the wave's lanes OR their bit into their digit's mask, read it
+		// back whole (a wave's LDS operations complete in order), clear it
+		if (valid)
+			__hip_atomic_fetch_or(&wm[d], 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+		__builtin_amdgcn_wave_barrier();
+		const uint64_t peer = valid ? __hip_atomic_load(&wm[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) : 0ull;
+		__builtin_amdgcn_wave_barrier();
+		if (valid)
+			__hip_atomic_store(&wm[d], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+		__builtin_amdgcn_wave_barrier();
+#else
 		uint64_t peer = __ballot(valid);
 #pragma unroll
 		for (int b = 0; b < 8; b++) {
 			const uint64_t bal = __ballot((d >> b) & 1);
 			peer &= ((d >> b) & 1) ? bal : ~bal;
 		}
+#endif
 		const uint32_t before = wcnt[w][d];
 		rk[r] = ((before + (uint32_t) __popcll(peer & lt)) << 8) | d;
 		if (valid && (peer >> lane) == 1)    // highest lane of its peer group
