@@ -440,6 +440,18 @@ def _allgather_col(be, dist, c, tp):
     return col, sum(sizes[:rank])
 
 
+def _row0s(be, dist, keys):
+    """Every rank's first global row (its shard's hseqbase).  The home-rank
+    numbering (_home_ids) needs the shards to be contiguous row ranges in rank
+    order -- mitosis slices, opt_mitosis.c:150-230 -- so that the row ranges
+    cut the ascending first rows; anything else is refused loudly."""
+    row0s = [_s64(x[0]) for x in _gather_int64(dist, be.device, [keys.hseqbase])]
+    if any(a > b for a, b in zip(row0s, row0s[1:])):
+        raise ValueError("dist_group: shards must be row ranges in rank order (hseqbase per rank %s)"
+                         % row0s)
+    return row0s
+
+
 def _global_ids(be, dist, firsts):
     """Group ids in global first-occurrence order (what BATgroup over all
     rows numbers them): the rank of each owned group's first row among the
@@ -500,13 +512,18 @@ def dist_group_aggr(be, dist, keys, vals):
     """
     TL, TO, TH = _types(be)
     world, rank = _world(dist)
-    row0s = [_s64(x[0]) for x in _gather_int64(dist, be.device, [keys.hseqbase])] if world > 1 else [0]
     g, e, h = be.group(keys)
+    if world == 1:
+        # one piece: mergetable leaves the plan's BATgroup + BATgroupsum as
+        # they are (opt_mergetable.c:1496-1670); their ids are already the
+        # first-occurrence numbering, extents the first rows, histo the counts
+        return {"gid": be.dense(0, be.n(e)), "key": be.widen(be.project(e, keys)), "first_row": e,
+                "count": h, "sums": [be.groupsum(v, g, e, TH) for v in vals]}
+    row0s = _row0s(be, dist, keys)
     parts = [be.widen(be.project(e, keys)), e, h] + [be.groupsum(v, g, e, TH) for v in vals]
-    if world > 1:
-        order, counts = be.hashpartition(parts[0], world)
-        parts = [be.project(order, c) for c in parts]
-        parts = exchange(be, dist, parts, [TL, TO, TL] + [TH] * len(vals), counts)
+    order, counts = be.hashpartition(parts[0], world)
+    parts = [be.project(order, c) for c in parts]
+    parts = exchange(be, dist, parts, [TL, TO, TL] + [TH] * len(vals), counts)
     rk, rfirst, rcount, rsums = parts[0], parts[1], parts[2], parts[3:]
     if be.n(rk) == 0:
         mk, mf, mc, ms = rk, rfirst, rcount, list(rsums)
@@ -516,10 +533,7 @@ def dist_group_aggr(be, dist, keys, vals):
         mf = be.groupmin(rfirst, g2, e2)
         mc = be.groupsum(rcount, g2, e2, TL)
         ms = [be.groupsum(s, g2, e2, TH) for s in rsums]
-    if world > 1:
-        gid, cols = _home_ids(be, dist, mf, row0s, [mk, mf, mc] + ms)
-    else:
-        gid, cols = _by_gid(be, _global_ids(be, dist, mf), [mk, mf, mc] + ms)
+    gid, cols = _home_ids(be, dist, mf, row0s, [mk, mf, mc] + ms)
     return {"gid": gid, "key": cols[0], "first_row": cols[1], "count": cols[2], "sums": cols[3:]}
 
 
@@ -538,7 +552,7 @@ def dist_group_avg(be, dist, keys, vals):
     order: {"gid", "key", "first_row", "avg"}."""
     TL, TO, TH = _types(be)
     world, rank = _world(dist)
-    row0s = [_s64(x[0]) for x in _gather_int64(dist, be.device, [keys.hseqbase])] if world > 1 else [0]
+    row0s = _row0s(be, dist, keys) if world > 1 else [0]
     g, e, _ = be.group(keys, histo=False)
     a, r, c = be.groupavg3(vals, g, e)
     parts = [be.widen(be.project(e, keys)), e, a, r, c]

@@ -1,6 +1,9 @@
 """Summarise rocprofv3 PMC passes into profiles/pmc_traffic.json.
 
-    python tools/pmc_summary.py FETCH_CSV WRITE_CSV ROWS_PER_LAUNCH [KERNEL ...]
+    python tools/pmc_summary.py [--src KERNEL_SOURCE] FETCH_CSV WRITE_CSV ROWS_PER_LAUNCH [KERNEL ...]
+
+--src names the .hip file holding the kernels; its sha256 is recorded, and
+bench.py reports `traffic` only while that file is unchanged.
 
 FETCH_SIZE / WRITE_SIZE are KiB per dispatch.  On gfx950 FETCH_SIZE counts
 exactly half of the bytes of a wide (16 B/lane) coalesced streaming read
@@ -9,6 +12,7 @@ exact for 16-B stores and atomics.
 """
 import collections
 import csv
+import hashlib
 import json
 import os
 import re
@@ -30,8 +34,13 @@ def per_kernel(path, counter):
 
 
 def main():
-    fetch, write, rows = sys.argv[1], sys.argv[2], int(sys.argv[3])
-    kernels = sys.argv[4:] or None
+    argv = sys.argv[1:]
+    src = None
+    if argv and argv[0] == "--src":
+        src, argv = argv[1], argv[2:]
+    fetch, write, rows = argv[0], argv[1], int(argv[2])
+    kernels = argv[3:] or None
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     f = per_kernel(fetch, "FETCH_SIZE")
     w = per_kernel(write, "WRITE_SIZE")
     out_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
@@ -46,6 +55,9 @@ def main():
                   "hbm_bytes_per_launch": int(fb + wb), "rows_per_launch": rows,
                   "hbm_bytes_per_row": (fb + wb) / rows,
                   "source": [os.path.relpath(fetch), os.path.relpath(write)]}
+        if src:
+            out[k]["kernel_source"] = os.path.relpath(os.path.abspath(src), root)
+            out[k]["kernel_source_sha16"] = hashlib.sha256(open(src, "rb").read()).hexdigest()[:16]
     json.dump(out, open(out_path, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
