@@ -111,6 +111,12 @@ int mgdk_BATupload(mgdk_bat *b, const void *host, mgdk_BUN n);
 int mgdk_BATdownload(const mgdk_bat *b, void *host);
 int mgdk_BATsetvheap(mgdk_bat *b, const void *host, uint64_t size);
 int mgdk_BATdownload_vheap(const mgdk_bat *b, void *host);
+/* BATmaskedcands (gdk/gdk_cand.h:232; gdk/gdk_cand.c:1366): a cand_mask
+ * candidate list over [hseq, hseq + nr) from a msk BAT's bits (selected) or
+ * their complement; rows past masked's end are candidates.  msk BATs (tail
+ * = 32-bit words of bits, count = bits) are accepted wherever a candidate
+ * list is: they stand for the oid list BATunmask makes of them */
+mgdk_bat *mgdk_BATmaskedcands(mgdk_oid hseq, mgdk_BUN nr, mgdk_bat *masked, bool selected);
 
 /* ---- select (gdk/gdk.h:2245-2246; gdk/gdk_select.c:1342, :2103) ------- */
 mgdk_bat *mgdk_BATselect(mgdk_bat *b, mgdk_bat *s, const void *tl, const void *th,

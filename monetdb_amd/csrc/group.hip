@@ -992,7 +992,8 @@ k_grp_seq_ext(BUN ngrp, BUN n, const uint64_t *spos, bool cdense, oid cseq, cons
 	for (BUN k = (BUN) blockIdx.x * blockDim.x + threadIdx.x; k < ngrp; k += (BUN) gridDim.x * blockDim.x) {
 		const uint64_t p = spos[k];
 		en[k] = cdense ? cseq + p : coids[p];
-		hn[k] = (int64_t) ((k + 1 < ngrp ? spos[k + 1] : n) - p);
+		if (hn)                         // (uniform: no histogram asked for)
+			hn[k] = (int64_t) ((k + 1 < ngrp ? spos[k + 1] : n) - p);
 	}
 }
 
@@ -1233,20 +1234,8 @@ group_ordered(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp
 			hipLaunchKernelGGL(k_grp_seq_hist, dim3(grid_for(ngrp, 1024, 8192)), blk, 0, st, ngrp,
 					   (oid) (ci.seq + n), (const oid *) en->theap, (int64_t *) hn->theap);
 	} else {
-		DevBuf hdummy(want_h ? 0 : ngrp * 8 + 8);
-		if (!want_h && !hdummy.p) {
-			mgdk_BBPunfix(gn);
-			mgdk_BBPunfix(en);
-			return -1;
-		}
 		hipLaunchKernelGGL(k_grp_seq_ext, dim3(grid_for(ngrp, 1024, 8192)), blk, 0, st, ngrp, n, spos.as<uint64_t>(),
-				   ci.dense, ci.seq, ci.oids, (oid *) en->theap,
-				   want_h ? (int64_t *) hn->theap : hdummy.as<int64_t>());
-		if (!want_h && !sync()) {       // hdummy goes back to the cache after the kernel
-			mgdk_BBPunfix(gn);
-			mgdk_BBPunfix(en);
-			return -1;
-		}
+				   ci.dense, ci.seq, ci.oids, (oid *) en->theap, want_h ? (int64_t *) hn->theap : nullptr);
 	}
 	uint64_t *hl = (uint64_t *) pinned(16);
 	if (!hip_ok(hipMemcpyAsync(hl, starts + ngrp - 1, 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {

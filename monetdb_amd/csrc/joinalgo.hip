@@ -224,6 +224,51 @@ k_order_flags_t(const T *v, BUN n, unsigned long long *first)
 	}
 }
 
+// three-way compare of BATordered's scans: BAT_ORDERED for integers,
+// BAT_ORDERED_FP for flt / dbl (nil = NaN below every value, two nils equal;
+// gdk/gdk_batop.c:1950-1995)
+template <typename T>
+__device__ __forceinline__ int
+ord_cmp(T x, T y)
+{
+	if constexpr (std::is_floating_point<T>::value) {
+		const bool xn = x != x, yn = y != y;
+		if (xn || yn)
+			return xn ? -(int) !yn : 1;
+	}
+	return (x > y) - (x < y);
+}
+
+// the first-pair positions for the types the vector scan does not cover
+// (flt, dbl, hge): one row per lane per step
+template <typename T>
+__global__ void __launch_bounds__(256)
+k_order_flags_g(const T *v, BUN n, unsigned long long *first)
+{
+	unsigned long long fd = NONE, fa = NONE, fe = NONE;
+	const BUN stride = (BUN) gridDim.x * blockDim.x;
+	for (BUN p = (BUN) blockIdx.x * blockDim.x + threadIdx.x + 1; p < n; p += stride) {
+		const int c = ord_cmp(v[p - 1], v[p]);
+		if (c > 0)
+			fd = p < fd ? p : fd;
+		else if (c < 0)
+			fa = p < fa ? p : fa;
+		else
+			fe = p < fe ? p : fe;
+	}
+	auto mn = [](unsigned long long a, unsigned long long b) { return a < b ? a : b; };
+	fd = block_reduce(fd, mn);
+	fa = block_reduce(fa, mn);
+	fe = block_reduce(fe, mn);
+	if (threadIdx.x == 0) {
+		unsigned long long *f[3] = {&first[0], &first[1], &first[2]};
+		const unsigned long long val[3] = {fd, fa, fe};
+		for (int k = 0; k < 3; k++)
+			if (val[k] < __hip_atomic_load(f[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+				atomicMin(f[k], val[k]);
+	}
+}
+
 // neighbour relations of an oid result column: bit 0 some v[i-1] < v[i],
 // bit 1 some >, bit 2 some ==, bit 3 some v[i] != v[i-1] + 1
 __global__ void __launch_bounds__(256)
@@ -385,7 +430,17 @@ scan_order(const mgdk_bat *b, Ord &o)
 		const Col c = col_of(b);
 		const dim3 gt(grid_for(b->count, 4 * 64 * 64, 8192));     // 4 waves x 64 lanes x 64 B per step
 		if (b->count > 1) {
-			if (c.base == nullptr || ((uintptr_t) c.base & 15) != 0)
+			const int bt = basetype(b->ttype);
+			if (bt == MGDK_flt)
+				hipLaunchKernelGGL(k_order_flags_g<float>, dim3(grid256(b->count)), dim3(256), 0, st,
+						   (const float *) b->theap, b->count, m);
+			else if (bt == MGDK_dbl)
+				hipLaunchKernelGGL(k_order_flags_g<double>, dim3(grid256(b->count)), dim3(256), 0, st,
+						   (const double *) b->theap, b->count, m);
+			else if (bt == MGDK_hge)
+				hipLaunchKernelGGL(k_order_flags_g<hge>, dim3(grid256(b->count)), dim3(256), 0, st,
+						   (const hge *) b->theap, b->count, m);
+			else if (c.base == nullptr || ((uintptr_t) c.base & 15) != 0)
 				hipLaunchKernelGGL(k_order_flags, dim3(grid256(b->count)), dim3(256), 0, st, c, b->count, m);
 			else if (c.w == 1)
 				hipLaunchKernelGGL(k_order_flags_t<int8_t>, gt, dim3(256), 0, st, (const int8_t *) c.base, b->count, m);
@@ -407,14 +462,14 @@ scan_order(const mgdk_bat *b, Ord &o)
 }
 
 // BATordered (gdk/gdk_batop.c:2002-2179): 1 / 0, -1 on error
-// the scan compares values as signed 64-bit integers: flt / dbl / hge / str
-// columns are not scanned (reported not ordered unless their property says
-// so); none of this library's users of the order passes them
+// integers compare as signed 64-bit images (oid as lng, its nil smallest, as
+// BAT_ORDERED(lng) does), flt / dbl as BAT_ORDERED_FP (NaN nil smallest), hge
+// as 128-bit integers; str columns are not scanned (reported not ordered
+// unless their property says so)
 static bool
 order_scannable(const mgdk_bat *b)
 {
-	const int t = b->ttype;
-	return t != MGDK_flt && t != MGDK_dbl && t != MGDK_str && b->twidth <= 8;
+	return b->ttype != MGDK_str && b->ttype != MGDK_msk;
 }
 
 int
@@ -842,7 +897,8 @@ int
 cand_kind(const mgdk_bat *s, CandKind *k)
 {
 	*k = CandKind{};
-	if (s == nullptr || !is_complex_cand(s))
+	// a msk BAT counts as the oid list it unmasks to (runtime.hip unmask_cand)
+	if (s == nullptr || !is_complex_cand(s) || s->ttype == MGDK_msk)
 		return 0;
 	uint64_t *hdr = (uint64_t *) pinned(64);
 	if (!hip_ok(hipMemcpyAsync(hdr, s->tvheap, 8, hipMemcpyDeviceToHost, stream()), "memcpy") || !sync())
@@ -1050,6 +1106,23 @@ mgdk_BATjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk_bat 
 	*r1p = nullptr;
 	if (r2p)
 		*r2p = nullptr;
+	if (l->ttype == MGDK_msk || r->ttype == MGDK_msk) {
+		// msk inputs are joined as the oid lists BATunmask makes of them
+		// (gdk_join.c:4500-4517)
+		mgdk_bat *lm = l->ttype == MGDK_msk ? unmask_cand(l) : nullptr;
+		mgdk_bat *rm = r->ttype == MGDK_msk ? unmask_cand(r) : nullptr;
+		int rc = -1;
+		if ((l->ttype != MGDK_msk || lm) && (r->ttype != MGDK_msk || rm)) {
+			if (lm)
+				lm->hseqbase = l->hseqbase;
+			if (rm)
+				rm->hseqbase = r->hseqbase;
+			rc = mgdk_BATjoin(r1p, r2p, lm ? lm : l, rm ? rm : r, sl, sr, nil_matches, estimate);
+		}
+		mgdk_BBPunfix(lm);
+		mgdk_BBPunfix(rm);
+		return rc;
+	}
 	if (basetype(atomtype(l->ttype)) != basetype(atomtype(r->ttype))) {
 		seterr("42000!BATjoin: inputs not compatible.");
 		return -1;

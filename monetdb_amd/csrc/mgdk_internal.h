@@ -131,7 +131,14 @@ int oid_at(const mgdk_bat *b, BUN p, oid *v);
 // a cand_except / cand_mask list (void BAT + ccand_t vheap) as a new ordered
 // oid list (BATunmask, gdk_cand.c); the caller owns the result
 mgdk_bat *unmask_cand(const mgdk_bat *s);
-inline bool is_complex_cand(const mgdk_bat *s) { return s->ttype == MGDK_void && s->tvheap && s->tvheapsize > 8; }
+// a candidate list that is not a dense range or a sorted oid array: the
+// cand_except / cand_mask forms (void + ccand_t vheap) and msk bit BATs
+inline bool is_complex_cand(const mgdk_bat *s)
+{
+	return (s->ttype == MGDK_void && s->tvheap && s->tvheapsize > 8) || s->ttype == MGDK_msk;
+}
+// bytes of the first n values of b's tail (msk: 32-bit words of bits)
+size_t tail_bytes(const mgdk_bat *b, BUN n);
 
 // ordered compaction (select.hip): sorted positions base+i with flags[i]==1;
 // the result may be a dense (void) BAT.  Uses the thread's scratch buffer.

@@ -516,12 +516,13 @@ mgdk_BATproject(mgdk_bat *l, mgdk_bat *r)
 		seterr("BATproject: NULL argument");
 		return nullptr;
 	}
-	if (l->ttype != MGDK_void && l->ttype != MGDK_oid) {
+	if (l->ttype != MGDK_void && l->ttype != MGDK_oid && l->ttype != MGDK_msk) {
 		seterr("BATproject: left must be oid");
 		return nullptr;
 	}
 	if (is_complex_cand(l)) {
-		// candidate list with exceptions or a bitmask (gdk_project.c:656-670)
+		// candidate list with exceptions, a bitmask, or a msk BAT
+		// (gdk_project.c:645-660: BATunmask)
 		mgdk_bat *m = unmask_cand(l);
 		if (m == nullptr)
 			return nullptr;
@@ -669,7 +670,7 @@ mgdk_BATproject2(mgdk_bat *l, mgdk_bat *r1, mgdk_bat *r2)
 			return nullptr;
 		}
 	}
-	if (l->ttype != MGDK_void && l->ttype != MGDK_oid) {
+	if (l->ttype != MGDK_void && l->ttype != MGDK_oid && l->ttype != MGDK_msk) {
 		seterr("BATproject2: left must be oid");
 		return nullptr;
 	}
@@ -765,7 +766,7 @@ mgdk_BATprojectchain(mgdk_bat **bats)
 	}
 	c.nl = 0;
 	for (int i = 1; i + 1 < k; i++) {
-		if (keep[i]->ttype != MGDK_void && keep[i]->ttype != MGDK_oid) {
+		if (keep[i]->ttype != MGDK_void && keep[i]->ttype != MGDK_oid && keep[i]->ttype != MGDK_msk) {
 			cleanup();
 			seterr("BATprojectchain: all but the last BAT must be oid");
 			return nullptr;

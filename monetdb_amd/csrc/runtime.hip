@@ -390,10 +390,16 @@ heap_decref(Heap *h)
 	}
 }
 
+size_t
+tail_bytes(const mgdk_bat *b, BUN n)
+{
+	return b->ttype == MGDK_msk ? (size_t) ((n + 31) / 32) * 4 : n * (size_t) b->twidth;
+}
+
 mgdk_bat *
 newbat(oid hseq, int tt, BUN cap)
 {
-	int w = width_of(tt);
+	int w = tt == MGDK_msk ? 0 : width_of(tt);
 	if (w < 0) {
 		seterr("42000!type %d not supported", tt);
 		return nullptr;
@@ -408,7 +414,18 @@ newbat(oid hseq, int tt, BUN cap)
 	b->tsorted = b->trevsorted = b->tkey = 1;
 	b->tnonil = 1;
 	b->tminpos = b->tmaxpos = MGDK_BUN_NONE;
-	if (w > 0) {
+	if (tt == MGDK_msk) {
+		// bits packed into 32-bit words (gdk_atoms.c msk); count = bits
+		b->twidth = 4;
+		b->tseqbase = MGDK_OID_NIL;
+		p->theap = heap_new(((cap ? cap : 1) + 31) / 32 * 4);
+		if (p->theap == nullptr) {
+			delete p;
+			free(b);
+			return nullptr;
+		}
+		b->theap = p->theap->base;
+	} else if (w > 0) {
 		p->theap = heap_new((cap ? cap : 1) * (size_t) w);
 		if (p->theap == nullptr) {
 			delete p;
@@ -581,6 +598,21 @@ static thread_local unsigned cand_ring_next;
 mgdk_bat *
 unmask_cand(const mgdk_bat *s)
 {
+	if (s->ttype == MGDK_msk) {
+		// a bit BAT: candidate hseqbase + i for every set bit i < count,
+		// the positive list BATunmask makes of it (gdk_cand.c:1464-1490,
+		// :1560-1600); the reference's canditer_init has no working branch
+		// for a msk-typed s (gdk_cand.c:468-473 asserts), and its callers
+		// (BATjoin gdk_join.c:4500-4517, BATproject2 gdk_project.c:652-660)
+		// unmask msk BATs first -- so the device takes every msk s that way
+		const BUN R = s->count;
+		DevBuf f(R + 1);
+		if (!f.p)
+			return nullptr;
+		hipLaunchKernelGGL(k_cand_mask, dim3(grid_for(R, 1024, 8192)), dim3(256), 0, stream(), f.as<int8_t>(),
+				   R, (const uint32_t *) s->theap);
+		return compact_flags(f.as<int8_t>(), R, s->hseqbase);
+	}
 	uint64_t *hdr = (uint64_t *) pinned(64);
 	if (hdr == nullptr ||
 	    !hip_ok(hipMemcpyAsync(hdr, s->tvheap, 8, hipMemcpyDeviceToHost, stream()), "hipMemcpyAsync") || !sync())
@@ -615,6 +647,41 @@ unmask_cand(const mgdk_bat *s)
 		hipLaunchKernelGGL(k_cand_negoid_clear, dim3(grid_for(nexc, 1024, 8192)), dim3(256), 0, st,
 				   f.as<int8_t>(), R, seq, (const oid *) payload, nexc);
 	return compact_flags(f.as<int8_t>(), R, seq);
+}
+
+// BATmaskedcands (gdk_cand.c:1366-1460): the words of the cand_mask list --
+// masked's bits (or their complement), rows past masked's end selected, the
+// bits past nr cleared -- with the number of set bits (meta[0]) and the
+// lowest set bit (meta[1], a minimum kept as ~max of the complement)
+__global__ __launch_bounds__(256) void
+k_masked_words(uint32_t *r, const uint32_t *src, BUN bcount, BUN nr, bool selected, unsigned long long *meta)
+{
+	const BUN nmask = (nr + 31) / 32, nsrc = (bcount + 31) / 32;
+	const uint32_t rest = (uint32_t) (bcount & 31);
+	unsigned long long ones = 0, lowest = ~0ull;
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < nmask; i += (BUN) gridDim.x * blockDim.x) {
+		uint32_t w;
+		if (i < nsrc) {
+			w = selected ? src[i] : ~src[i];
+			if (nr > bcount && rest > 0 && i == nsrc - 1)
+				w |= ~0u << rest;
+		} else {
+			w = ~0u;
+		}
+		if (i == nmask - 1 && (nr & 31))
+			w &= (1u << (nr & 31)) - 1;
+		r[i] = w;
+		ones += __popc(w);
+		if (w && lowest == ~0ull)
+			lowest = i * 32 + __ffs(w) - 1;
+	}
+	ones = block_reduce(ones, [](unsigned long long a, unsigned long long b) { return a + b; });
+	lowest = block_reduce(lowest, [](unsigned long long a, unsigned long long b) { return a < b ? a : b; });
+	if (threadIdx.x == 0) {
+		if (ones)
+			atomicAdd(&meta[0], ones);
+		publish_max(&meta[1], ~lowest);
+	}
 }
 
 __global__ void
@@ -675,7 +742,7 @@ cand_init(Cand *ci, const mgdk_bat *b, const mgdk_bat *s)
 	}
 	if (s->count == 0 || (b && b->count == 0))
 		return 0;
-	if (s->ttype == MGDK_void && s->tvheap != nullptr && s->tvheapsize > 8) {
+	if (is_complex_cand(s)) {
 		mgdk_bat *m = unmask_cand(s);
 		if (m == nullptr)
 			return -1;
@@ -698,10 +765,6 @@ cand_init(Cand *ci, const mgdk_bat *b, const mgdk_bat *s)
 			ci->last = e - 1;
 		}
 		return 0;
-	}
-	if (s->ttype == MGDK_msk) {
-		seterr("42000!mask candidate lists are not supported on the device path");
-		return -1;
 	}
 	if (s->ttype != MGDK_oid) {
 		seterr("candidate list must have type oid");
@@ -926,6 +989,10 @@ mgdk_BATslice(mgdk_bat *b, mgdk_BUN lo, mgdk_BUN hi)
 		hi = b->count;
 	if (lo > hi)
 		lo = hi;
+	if (b->ttype == MGDK_msk && (lo & 31)) {
+		seterr("42000!BATslice: a msk view must start at a multiple of 32 rows");
+		return nullptr;
+	}
 	mgdk_bat *v = (mgdk_bat *) calloc(1, sizeof(mgdk_bat));
 	Priv *p = new Priv{}, *bp = (Priv *) b->priv;
 	*v = *b;
@@ -939,7 +1006,7 @@ mgdk_BATslice(mgdk_bat *b, mgdk_BUN lo, mgdk_BUN hi)
 		p->theap = bp->theap;
 		if (p->theap)
 			__atomic_add_fetch(&p->theap->refs, 1, __ATOMIC_ACQ_REL);
-		v->theap = (char *) b->theap + lo * (size_t) b->twidth;
+		v->theap = (char *) b->theap + tail_bytes(b, lo);
 	}
 	if (bp->tvheap) {
 		p->tvheap = bp->tvheap;
@@ -978,7 +1045,7 @@ mgdk_BATupload(mgdk_bat *b, const void *host, mgdk_BUN n)
 		return -1;
 	}
 	Priv *p = (Priv *) b->priv;
-	size_t bytes = n * (size_t) b->twidth;
+	size_t bytes = tail_bytes(b, n);
 	img8_drop(b);
 	// a heap shared with views (refs > 1) is never written in place
 	if (p->theap == nullptr || p->theap->refs != 1 ||
@@ -1011,11 +1078,66 @@ mgdk_BATdownload(const mgdk_bat *b, void *host)
 			o[i] = b->tseqbase == MGDK_OID_NIL ? MGDK_OID_NIL : b->tseqbase + i;
 		return 0;
 	}
-	size_t bytes = b->count * (size_t) b->twidth;
+	size_t bytes = tail_bytes(b, b->count);
 	if (bytes && !hip_ok(hipMemcpyAsync(host, b->theap, bytes, hipMemcpyDeviceToHost, stream()),
 			     "hipMemcpyAsync D2H"))
 		return -1;
 	return sync_data() ? 0 : -1;
+}
+
+mgdk_bat *
+mgdk_BATmaskedcands(oid hseq, BUN nr, mgdk_bat *masked, bool selected)
+{
+	if (masked == nullptr || masked->ttype != MGDK_msk) {
+		seterr("BATmaskedcands: masked must be a msk BAT");
+		return nullptr;
+	}
+	mgdk_bat *bn = newbat(hseq, MGDK_void, 0);
+	if (bn == nullptr)
+		return nullptr;
+	bn->tseqbase = hseq;
+	bn->count = 0;
+	if (masked->count == 0 || nr == 0)
+		return bn;
+	const BUN nmask = (nr + 31) / 32;
+	Heap *h = heap_new(8 + nmask * 4);
+	unsigned long long *meta = (unsigned long long *) meta_buf();
+	unsigned long long *hm = (unsigned long long *) pinned(64);
+	hipStream_t st = stream();
+	if (h == nullptr || meta == nullptr || hm == nullptr || !hip_ok(hipMemsetAsync(meta, 0, 16, st), "memset")) {
+		heap_decref(h);
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	hipLaunchKernelGGL(k_masked_words, dim3(grid_for(nmask, 256 * 8, 2048)), dim3(256), 0, st,
+			   (uint32_t *) ((char *) h->base + 8), (const uint32_t *) masked->theap, masked->count, nr,
+			   selected, meta);
+	if (!hip_ok(hipMemcpyAsync(hm, meta, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
+		heap_decref(h);
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	const BUN cnt = hm[0];
+	if (cnt == 0) {                 // no point having a mask if it's empty
+		heap_decref(h);
+		return bn;
+	}
+	const unsigned long long firstbit = ~hm[1];
+	// ccand_t {type = CAND_MSK (bit 0), firstbit (bits 1..48)} (gdk_cand.h:23-38)
+	hm[2] = 1ull | (firstbit << 1);
+	if (!hip_ok(hipMemcpyAsync(h->base, &hm[2], 8, hipMemcpyHostToDevice, st), "memcpy") || !sync()) {
+		heap_decref(h);
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	Priv *p = (Priv *) bn->priv;
+	p->tvheap = h;
+	bn->tvheap = h->base;
+	bn->tvheapsize = 8 + nmask * 4;
+	bn->tseqbase = hseq + firstbit;
+	bn->count = cnt;
+	bn->trevsorted = cnt <= 1;
+	return bn;
 }
 
 int

@@ -1578,10 +1578,6 @@ mgdk_BATsort(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b
 		seterr("no place to put the result.\n");
 		return -1;
 	}
-	if (n >= ((BUN) 1 << 32)) {
-		seterr("42000!BATsort: more than 2^32 rows");
-		return -1;
-	}
 	if (g == nullptr && !stable)
 		o = nullptr;        // pre-ordering is meaningless for an unstable full sort (:2410-2414)
 	if (b->tnonil)
@@ -1627,6 +1623,13 @@ mgdk_BATsort(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b
 				goto fail;
 		}
 		goto done;
+	}
+	// positions and ranks of the sorts below are 32-bit: a column of 2^32 or
+	// more rows is only sorted through the shortcuts above (a documented
+	// difference from the reference, which has no such limit)
+	if (n >= ((BUN) 1 << 32)) {
+		seterr("42000!BATsort: more than 2^32 rows");
+		goto fail;
 	}
 	{
 		// the runs do_sort sorts with GDKqsort

@@ -89,6 +89,7 @@ _SIGS = {
     "mgdk_BATdownload": (C.c_int, [P, C.c_void_p]),
     "mgdk_BATsetvheap": (C.c_int, [P, C.c_void_p, C.c_uint64]),
     "mgdk_BATdownload_vheap": (C.c_int, [P, C.c_void_p]),
+    "mgdk_BATmaskedcands": (P, [C.c_uint64, C.c_uint64, P, C.c_bool]),
     "mgdk_BATselect": (P, [P, P, C.c_void_p, C.c_void_p, C.c_bool, C.c_bool, C.c_bool, C.c_bool]),
     "mgdk_BATthetaselect": (P, [P, P, C.c_void_p, C.c_char_p]),
     "mgdk_BATproject": (P, [P, P]),
@@ -310,6 +311,20 @@ class BAT:
         _chk(lib().mgdk_BATsetvheap(b.ptr, buf, len(buf)))
         return b
 
+    @classmethod
+    def msk(cls, bits, hseqbase=0):
+        """A msk BAT (TYPE_msk): one bit per row packed into 32-bit words,
+        count = len(bits)."""
+        init()
+        bits = np.asarray(bits, bool)
+        n = bits.size
+        words = np.packbits(np.concatenate([bits, np.zeros((-n) % 32, bool)]),
+                            bitorder="little").view(np.uint32)
+        b = BAT(lib().mgdk_COLnew(hseqbase, TYPE_msk, max(1, n)))
+        _chk(lib().mgdk_BATupload(b.ptr, words.ctypes.data, n))
+        b.ptr.contents.count = n
+        return b
+
     # -- properties --
     @property
     def s(self):
@@ -379,6 +394,11 @@ def _valptr(tp, v, keep):
 
 
 # ---- operators (same names as GDK) ------------------------------------------
+
+def BATmaskedcands(hseq, nr, masked, selected=True):
+    """gdk/gdk_cand.c:1366: a cand_mask candidate list from a msk BAT."""
+    return BAT(lib().mgdk_BATmaskedcands(hseq, nr, masked.ptr, selected))
+
 
 def BATselect(b, s, tl, th, li, hi, anti, nil_matches=False):
     keep = []

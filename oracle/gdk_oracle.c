@@ -133,6 +133,27 @@ ora_ci_init(ora_ci *ci, const ora_bat *b, const ora_bat *s)
 		}
 		return 0;
 	}
+	if (s->type == ORA_msk) {
+		/* a bit BAT stands for the oid list BATunmask makes of it
+		 * (gdk_cand.c:1549-1590: hseqbase + i for every set bit i <
+		 * count); kept in a per-thread ring of 4 lists */
+		static __thread ora_oid *ring[4];
+		static __thread unsigned next;
+		const uint32_t *w = s->base;
+		ora_oid *o = malloc((s->count + 1) * sizeof(ora_oid));
+		uint64_t k = 0;
+		if (o == NULL) {
+			ora_seterr("malloc");
+			return -1;
+		}
+		for (uint64_t i = 0; i < s->count; i++)
+			if ((w[i >> 5] >> (i & 31)) & 1)
+				o[k++] = s->hseqbase + i;
+		free(ring[next & 3]);
+		ring[next++ & 3] = o;
+		ora_bat tmp = {.type = ORA_oid, .width = 8, .count = k, .base = o};
+		return ora_ci_init(ci, b, &tmp);
+	}
 	if (s->type != ORA_oid) {
 		ora_seterr("candidate list must be oid");
 		return -1;
@@ -553,9 +574,73 @@ ora_thetaselect(const ora_bat *b, const ora_bat *s, const void *val, const char 
 /* ---------------------------------------------------------------------- */
 /* BATproject (gdk/gdk_project.c:590-857): out[i] = r[l[i] - r.hseqbase];
  * a nil oid in l yields nil; out-of-range oids are an error. */
+/* BATunmask of a msk BAT (gdk_cand.c:1464, its positive-list branch
+ * :1549-1599): hseqbase + i for every set bit i < count, virtualised */
+ora_bat *
+ora_unmask(const ora_bat *b)
+{
+	if (b->type != ORA_msk) {
+		ora_seterr("BATunmask: not a msk BAT");
+		return NULL;
+	}
+	const uint32_t *w = b->base;
+	uint64_t k = 0;
+	for (uint64_t i = 0; i < b->count; i++)
+		k += (w[i >> 5] >> (i & 31)) & 1;
+	ora_bat *bn = ora_new(ORA_oid, k, b->hseqbase);
+	if (bn == NULL)
+		return NULL;
+	ora_oid *o = bn->base;
+	k = 0;
+	for (uint64_t i = 0; i < b->count; i++)
+		if ((w[i >> 5] >> (i & 31)) & 1)
+			o[k++] = b->hseqbase + i;
+	bn->count = k;
+	bn->sorted = bn->key = bn->nonil = 1;
+	bn->revsorted = k <= 1;
+	return ora_virtualize(bn);
+}
+
+/* BATmaskedcands (gdk_cand.c:1366-1460) as the oid list it stands for: the
+ * mask words of [hseq, hseq + nr) from masked's bits (or their complement),
+ * rows past masked's end selected -- returned unmasked (materialised) */
+ora_bat *
+ora_maskedcands(ora_oid hseq, uint64_t nr, const ora_bat *masked, bool selected)
+{
+	if (masked->type != ORA_msk) {
+		ora_seterr("BATmaskedcands: not a msk BAT");
+		return NULL;
+	}
+	const uint32_t *w = masked->base;
+	ora_bat *bn = ora_new(ORA_oid, nr, hseq);
+	if (bn == NULL)
+		return NULL;
+	ora_oid *o = bn->base;
+	uint64_t k = 0;
+	if (masked->count > 0)
+		for (uint64_t i = 0; i < nr; i++) {
+			bool bit = i < masked->count ? (((w[i >> 5] >> (i & 31)) & 1) != 0) == selected : true;
+			if (bit)
+				o[k++] = hseq + i;
+		}
+	bn->count = k;
+	bn->sorted = bn->key = bn->nonil = 1;
+	bn->revsorted = k <= 1;
+	return ora_virtualize(bn);
+}
+
 ora_bat *
 ora_project(const ora_bat *l, const ora_bat *r)
 {
+	if (l->type == ORA_msk) {
+		/* gdk_project.c:652-660 */
+		ora_bat *m = ora_unmask(l);
+		if (m == NULL)
+			return NULL;
+		ora_bat *bn = ora_project(m, r);
+		ora_free(m);
+		return bn;
+	}
 	ora_ci ci;
 	if (ora_ci_init(&ci, NULL, l) < 0)
 		return NULL;

@@ -83,6 +83,11 @@ ora_bat *ora_select(const ora_bat *b, const ora_bat *s, const void *tl,
 ora_bat *ora_thetaselect(const ora_bat *b, const ora_bat *s, const void *val,
 			 const char *op);
 ora_bat *ora_project(const ora_bat *l, const ora_bat *r);
+/* msk BATs (tail = 32-bit words of bits, count = bits): BATunmask
+ * (gdk/gdk_cand.c:1464) and BATmaskedcands (:1366) as materialised lists;
+ * a msk candidate list anywhere = its BATunmask */
+ora_bat *ora_unmask(const ora_bat *b);
+ora_bat *ora_maskedcands(ora_oid hseq, uint64_t nr, const ora_bat *masked, bool selected);
 /* op: '+', '-', '*'; b1/b2 may be NULL when a constant is given */
 ora_bat *ora_calc(char op, const ora_bat *b1, const void *c1, int t1,
 		  const ora_bat *b2, const void *c2, int t2,

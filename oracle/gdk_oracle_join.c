@@ -714,6 +714,19 @@ int
 ora_join(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r,
 	 const ora_bat *sl, const ora_bat *sr, bool nil_matches)
 {
+	if (l->type == ORA_msk || r->type == ORA_msk) {
+		/* msk inputs joined as their BATunmask (gdk_join.c:4500-4517) */
+		ora_bat *lm = l->type == ORA_msk ? ora_unmask(l) : NULL;
+		ora_bat *rm = r->type == ORA_msk ? ora_unmask(r) : NULL;
+		int rc = -1;
+		if ((l->type != ORA_msk || lm) && (r->type != ORA_msk || rm))
+			rc = ora_join(r1p, r2p, lm ? lm : l, rm ? rm : r, sl, sr, nil_matches);
+		if (lm)
+			ora_free(lm);
+		if (rm)
+			ora_free(rm);
+		return rc;
+	}
 	if (atomtype(l->type) != atomtype(r->type)) {
 		ora_seterr("BATjoin: inputs not compatible.");
 		return -1;

@@ -14,6 +14,7 @@ LIB_PATH = os.path.join(HERE, "liboracle.so")
 TYPE_void, TYPE_bit, TYPE_bte, TYPE_sht, TYPE_int, TYPE_oid = 0, 2, 3, 4, 5, 6
 TYPE_flt, TYPE_dbl, TYPE_lng, TYPE_hge, TYPE_date, TYPE_str = 8, 9, 10, 11, 12, 16
 TYPE_daytime, TYPE_timestamp = 13, 14
+TYPE_msk = 1
 OID_NIL = 1 << 63
 
 NP = {TYPE_bit: np.int8, TYPE_bte: np.int8, TYPE_sht: np.int16, TYPE_int: np.int32,
@@ -71,6 +72,10 @@ def lib():
         L.ora_thetaselect.restype = P
         L.ora_thetaselect.argtypes = [P, P, C.c_void_p, C.c_char_p]
         L.ora_project.restype = P
+        L.ora_unmask.restype = P
+        L.ora_unmask.argtypes = [P]
+        L.ora_maskedcands.restype = P
+        L.ora_maskedcands.argtypes = [C.c_uint64, C.c_uint64, P, C.c_bool]
         L.ora_project.argtypes = [P, P]
         L.ora_calc.restype = P
         L.ora_calc.argtypes = [C.c_char, P, C.c_void_p, C.c_int, P, C.c_void_p, C.c_int, P, C.c_int]
@@ -178,6 +183,23 @@ class Bat:
         return cls(C.pointer(b), keep)
 
     @classmethod
+    def msk(cls, bits, hseqbase=0):
+        """A msk BAT: one bit per row in 32-bit words, count = len(bits)."""
+        bits = np.asarray(bits, bool)
+        n = bits.size
+        a = np.packbits(np.concatenate([bits, np.zeros((-n) % 32 + 32, bool)]),
+                        bitorder="little").view(np.uint32).copy()
+        b = OraBat()
+        b.type = TYPE_msk
+        b.width = 4
+        b.count = n
+        b.hseqbase = hseqbase
+        b.tseqbase = OID_NIL
+        b.base = a.ctypes.data
+        b.minpos = b.maxpos = (1 << 63) - 1
+        return cls(C.pointer(b), [a, b])
+
+    @classmethod
     def dense(cls, tseq, n, hseqbase=0):
         b = OraBat()
         b.type = TYPE_void
@@ -239,6 +261,14 @@ def BATselect(b, s, tl, th, li, hi, anti, nil_matches=False):
     tp = b.s.type
     return _ret(lib().ora_select(b.ptr, s.ptr if s else None, _valptr(tp, tl, keep),
                                  _valptr(tp, th, keep), li, hi, anti, nil_matches))
+
+
+def unmask(b):
+    return _ret(lib().ora_unmask(b.ptr))
+
+
+def maskedcands(hseq, nr, masked, selected=True):
+    return _ret(lib().ora_maskedcands(hseq, nr, masked.ptr, selected))
 
 
 def BATthetaselect(b, s, val, op):

@@ -137,3 +137,56 @@ def test_gpu_join_swap_example(gdk):
     a, b = gdk.BATjoin(l, r)
     assert a.to_numpy().tolist() == [2, 0, 2, 0, 2, 0]
     assert b.to_numpy().tolist() == [0, 0, 1, 1, 3, 3]
+
+
+def _ordered_model(vals, isnil):
+    """BAT_ORDERED / BAT_ORDERED_FP (gdk/gdk_batop.c:1950-1995): nil below
+    every value, two nils equal; returns (sorted, revsorted)."""
+    def cmp(i):
+        a, b = isnil[i - 1], isnil[i]
+        if a or b:
+            return -int(not b) if a else 1
+        return (vals[i - 1] > vals[i]) - (vals[i - 1] < vals[i])
+    cs = [cmp(i) for i in range(1, len(vals))]
+    return all(c <= 0 for c in cs), all(c >= 0 for c in cs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tp", ["flt", "dbl", "hge"])
+@pytest.mark.parametrize("shape", ["asc", "desc", "asc_nils", "desc_nils_end", "mixed", "const", "negzero"])
+def test_gpu_ordered_fp_hge(gdk, tp, shape):
+    """BATordered / BATordered_rev scan flt / dbl (NaN nil smallest) and hge
+    columns as the reference does instead of answering 'not ordered'."""
+    r = np.random.default_rng(hash((tp, shape)) & 0xffff)
+    n = 5000
+    v = np.sort(r.integers(-10**6, 10**6, n)).astype(np.float64) / 7
+    isnil = np.zeros(n, bool)
+    if shape == "desc":
+        v = v[::-1].copy()
+    elif shape == "asc_nils":
+        isnil[:40] = True
+    elif shape == "desc_nils_end":
+        v = v[::-1].copy()
+        isnil[-40:] = True
+    elif shape == "mixed":
+        v[100], v[101] = v[101], v[100] - 1
+    elif shape == "const":
+        v[:] = -3.5
+    elif shape == "negzero":
+        v = np.array([-1.0, -0.0, 0.0, -0.0, 2.0] * 1, np.float64)
+        isnil = np.zeros(v.size, bool)
+    if tp == "hge":
+        iv = [int(x * 7) * (1 << 70) + 5 for x in v]
+        words = [gdk.int_to_hge_words(gdk.NIL[gdk.TYPE_hge] if isnil[i] else iv[i]) for i in range(v.size)]
+        arr = np.array(words, np.uint64)
+        mv = iv
+        b = gdk.BAT.from_numpy(gdk.TYPE_hge, arr, sorted_=False, revsorted=False, key=False)
+    else:
+        dt = np.float32 if tp == "flt" else np.float64
+        arr = v.astype(dt)
+        arr[isnil] = np.nan
+        mv = arr.tolist()
+        b = gdk.BAT.from_numpy(gdk.TYPE_flt if tp == "flt" else gdk.TYPE_dbl, arr, sorted_=False,
+                               revsorted=False, key=False)
+    want = _ordered_model(mv, isnil)
+    assert (gdk.BATordered(b), gdk.BATordered_rev(b)) == want
