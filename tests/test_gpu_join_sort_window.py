@@ -487,3 +487,36 @@ def test_sort_maltest_fixture(gdk):
             assert [int(v) for v in srt.to_numpy()] == c["sorted"]
             if c["order"]:
                 assert [int(v) for v in order.to_numpy()] == c["order_oids"]
+
+
+@pytest.mark.parametrize("case", ["fk", "probe_skew", "lng_cands", "sparse_hits"])
+def test_join_region_partitioned(gdk, ora, case):
+    """More than 2M unique build rows: the region-partitioned path (build side
+    as the global bucketed table, probe side cut into 128 coarse partitions
+    probed from one XCD's L2, restored by subtile).  An FK-shaped join of
+    12M x 3M (every row matches), a probe side with 60 % of its rows on one
+    key (its coarse partition overflows its capacity -> the radix-partitioned
+    path), 8-byte keys with candidate lists on both sides, and 1 % hits --
+    all bit-exact with the oracle."""
+    r = rng(88)
+    nr, nl = 3_000_017, 12_000_029
+    dt, tp, otp = np.int32, gdk.TYPE_int, ora.TYPE_int
+    if case == "lng_cands":
+        dt, tp, otp = np.int64, gdk.TYPE_lng, ora.TYPE_lng
+    rv = r.permutation(np.arange(1, 4 * nr + 1, 4))[:nr].astype(dt)
+    lv = r.choice(rv, nl).astype(dt)
+    if case == "probe_skew":
+        lv[r.random(nl) < 0.6] = rv[1000]
+    if case == "sparse_hits":
+        lv[r.random(nl) < 0.99] += 2                               # off the 4-grid: no match
+    kw, okw = {}, {}
+    if case == "lng_cands":
+        lv[::1001] = np.iinfo(np.int64).min
+        sl = np.sort(r.choice(nl, nl - nl // 3, replace=False)).astype(np.uint64) + 7
+        sr = np.sort(r.choice(nr, nr - 5000, replace=False)).astype(np.uint64) + 2
+        kw = dict(sl=mk(gdk, gdk.TYPE_oid, sl), sr=mk(gdk, gdk.TYPE_oid, sr))
+        okw = dict(sl=omk(ora, ora.TYPE_oid, sl, sorted_=True), sr=omk(ora, ora.TYPE_oid, sr, sorted_=True))
+    a, b = gdk.BATjoin(mk(gdk, tp, lv, hseqbase=7), mk(gdk, tp, rv, hseqbase=2), **kw)
+    oa, ob = ora.BATjoin(omk(ora, otp, lv, hseqbase=7), omk(ora, otp, rv, hseqbase=2), **okw)
+    assert np.array_equal(a.to_numpy(), oa.values())
+    assert np.array_equal(b.to_numpy(), ob.values())

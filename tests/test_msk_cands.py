@@ -71,13 +71,18 @@ def test_msk_cand_operators(gdk, ora, hseq, n):
     assert np.array_equal(got, want)
     assert gdk.BATsum(gdk.TYPE_lng, B, s=S) == ora.BATsum(ora.TYPE_lng, OB, s=OS)
     # groupsum with the msk as candidates
-    gk = (np.arange(v.size) % 17).astype(np.int32)
-    G = gdk.BAT.from_numpy(gdk.TYPE_int, gk, hseqbase=100)
-    g, e, _ = gdk.BATgroup(G)
-    og, oe, _ = ora.BATgroup(ora.Bat.from_array(ora.TYPE_int, gk, hseqbase=100))
-    got = gdk.BATgroupsum(B, g, e, gdk.TYPE_lng, s=S).values()
-    want = ora.BATgroupsum(OB, og, oe, ora.TYPE_lng, s=OS).values()
-    assert list(got) == list(want)
+    # (g holds one id per candidate, its head at the first candidate:
+    # BATgroupaggrinit, gdk_aggr.c:76-80)
+    cands = hseq + np.flatnonzero(bits)
+    cands = cands[(cands >= 100) & (cands < 100 + v.size)]
+    if cands.size:
+        gk = (cands % 17).astype(np.int32)
+        G = gdk.BAT.from_numpy(gdk.TYPE_int, gk, hseqbase=int(cands[0]))
+        g, e, _ = gdk.BATgroup(G)
+        og, oe, _ = ora.BATgroup(ora.Bat.from_array(ora.TYPE_int, gk, hseqbase=int(cands[0])))
+        got = gdk.BATgroupsum(B, g, e, gdk.TYPE_lng, s=S).values()
+        want = ora.BATgroupsum(OB, og, oe, ora.TYPE_lng, s=OS).values()
+        assert list(got) == list(want)
     # join with the msk as left candidates, and a msk joined as a value column
     rk = r.permutation(2000).astype(np.int32) - 1000
     R = gdk.BAT.from_numpy(gdk.TYPE_int, rk)
