@@ -711,7 +711,7 @@ pj_part32(uint32_t key, int pbits)
 __device__ __forceinline__ uint32_t
 pj_home(uint32_t key, int pbits)
 {
-	return (pj_hash(key) >> (32 - pbits - 14)) & (PJ_SLOTS - 1);
+	return (pj_hash(key) >> (32 - pbits - 14)) & 16383;
 }
 
 // home bucket of a key in a table of nbp buckets: the hash bits below the
@@ -1309,8 +1309,11 @@ join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_b
 	int pbits = 6;
 	while (pbits < PJ_MAXPBITS && ((BUN) 8192 << pbits) < nr)
 		pbits++;
+	// the expected largest partition (mean + 6 sigma) must fit the LDS table
+	while (pbits < PJ_MAXPBITS && (double) nr / (1u << pbits) + 6.0 * sqrt((double) nr / (1u << pbits)) > PJ_MAXFILL)
+		pbits++;
 	const uint32_t P = 1u << pbits;
-	if (nr / P > PJ_MAXFILL * 3 / 4)
+	if ((double) nr / P + 6.0 * sqrt((double) nr / P) > PJ_MAXFILL)
 		return 1;
 	hipStream_t st = stream();
 	uint32_t *meta32 = (uint32_t *) meta_buf();
@@ -1351,10 +1354,10 @@ join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_b
 	if (2 * nbp <= h[0])
 		nbp = h[0] / 2 + 1;
 	nbp = nbp < PJ_SLOTS / 2 ? nbp : PJ_SLOTS / 2;    // (h[0] <= PJ_MAXFILL keeps load < 3/4)
-	const bool ldsd = Pr.nsub <= PJ_LDS_SUBS;
+	const bool ldsd = Pr.nsub <= PJ_LDS_SUBS && (size_t) nbp * 16 + (size_t) Pr.nsub * 4 <= 160 * 1024;
 	const size_t lds = (size_t) nbp * 16 + (ldsd ? (size_t) Pr.nsub * 4 : 0);
 	static const bool lds_attr = hipFuncSetAttribute((const void *) k_pj_probe,
-							 hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) == hipSuccess;
+							 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
 	(void) lds_attr;
 	(void) hipGetLastError();
 	hipLaunchKernelGGL(k_pj_probe, dim3(P), dim3(1024), lds, st, B.ent->as<uint2>(), B.base->as<uint32_t>(),
@@ -1683,369 +1686,6 @@ join_gt(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_bat
 }
 
 // ---------------------------------------------------------------------------
-// Region-partitioned path (4-byte keys, or 8-byte keys by their 4-byte images;
-// unique build side of 2M..~20M rows).  The build side becomes the global
-// table of the global-table path (pj_cut + k_gt_build: P fine regions of nbp
-// 16-byte buckets).  The probe side is cut only COARSELY, into C = 2^cbits
-// partitions by the top bits of the same hash, so coarse partition c owns the
-// 2^(pbits - cbits) consecutive fine regions of the table (~1.4 MB at 15M
-// build rows) and its probes are answered from ONE XCD's L2: partition c is
-// probed only by workgroups dealt to XCD c % 8, partitions in order.
-//   scatter  one workgroup per 8 Ki-row subtile: keys counted per coarse
-//            partition in LDS, the runs allocated in the partitions by ONE
-//            global atomic per (subtile, partition) -- no histogram pass, no
-//            column scan -- and stored as (4-byte key, 2-byte local row) SoA
-//            through an LDS stage, each run contiguous; the run table
-//            (position, count) per (subtile, partition) is kept
-//   probe    per 2048 entries of a partition: the key, ONE 16-byte bucket
-//            load from the L2-resident region (a chain step rarely), the
-//            match position + 1 stored over... a 4-byte result array
-//   restore  one workgroup per subtile (ticketed): its C runs read in place
-//            (local row + result), matches dropped into an LDS row array,
-//            compacted in row order, output offset by decoupled look-back
-// Partitions are allocated with a capacity (mean + margin); an overflow, a
-// duplicate build key, an overfull region or a build value without a 4-byte
-// image is flagged on the device and checked at the ONE host round trip at
-// the end, after which the caller falls back.  Probe-side bytes per row: 4
-// key + 4 + 2 scattered + 4 + 4 probed + 2 + 4 + 16 restored = 40 B.
-// ---------------------------------------------------------------------------
-
-constexpr uint32_t RP_SUB = 8192;                  // rows per subtile (local rows in 13 bits)
-constexpr uint32_t RP_CHUNK = 2048;                // probe entries per workgroup
-constexpr int RP_MAXCBITS = 8;
-
-// exclusive scan of v over the 256 threads of a workgroup; *total = sum
-__device__ __forceinline__ uint32_t
-rp_scan256(uint32_t v, uint32_t *wsum4, uint32_t *total)
-{
-	const unsigned lane = __lane_id(), w = threadIdx.x >> 6;
-	uint32_t x = v;
-#pragma unroll
-	for (int o = 1; o < 64; o <<= 1) {
-		const uint32_t u = __shfl_up(x, o);
-		if (lane >= (unsigned) o)
-			x += u;
-	}
-	if (lane == 63)
-		wsum4[w] = x;
-	__syncthreads();
-	uint32_t pre = 0, t = 0;
-#pragma unroll
-	for (unsigned q = 0; q < 4; q++) {
-		pre += q < w ? wsum4[q] : 0;
-		t += wsum4[q];
-	}
-	*total = t;
-	return pre + x - v;
-}
-
-__global__ __launch_bounds__(256) void
-k_rp_scatter(Side s, BUN n, int cbits, bool skipnil, uint32_t cap, uint32_t *fill, uint32_t *runpos,
-	     uint32_t *runcnt, uint32_t *pkeys, uint16_t *prow, uint32_t *oflow)
-{
-	__shared__ uint32_t skey[RP_SUB];
-	__shared__ uint16_t srow[RP_SUB];
-	__shared__ uint32_t hist[256], start[256], gpos[256], wsum4[4];
-	const unsigned tid = threadIdx.x;
-	const uint32_t C = 1u << cbits;
-	const uint32_t sub = blockIdx.x;
-	const BUN a0 = (BUN) sub * RP_SUB;
-	hist[tid] = 0;
-	// 32 rows per thread: [q * 4096 + 16 tid, + 16) for q = 0, 1, all loads
-	// issued before the first is ranked
-	uint32_t k[2][16];
-	bool ok[2][16];
-#pragma unroll
-	for (int q = 0; q < 2; q++)
-		pj_keys16(s, a0 + (BUN) q * 4096 + (BUN) tid * 16, n, skipnil, k[q], ok[q]);
-	__syncthreads();
-	uint32_t rk[2][16];
-#pragma unroll
-	for (int q = 0; q < 2; q++)
-#pragma unroll
-		for (int j = 0; j < 16; j++)
-			if (ok[q][j])
-				rk[q][j] = atomicAdd(&hist[pj_hash(k[q][j]) >> (32 - cbits)], 1u);
-	__syncthreads();
-	const uint32_t v = tid < C ? hist[tid] : 0;
-	uint32_t total;
-	const uint32_t pre = rp_scan256(v, wsum4, &total);
-	if (tid < C) {
-		start[tid] = pre;
-		uint32_t gp = 0;
-		if (v) {
-			gp = atomicAdd(&fill[tid], v);
-			if (gp + v > cap)
-				atomicOr(oflow, 1u);
-		}
-		gpos[tid] = gp;
-		runpos[(size_t) sub * C + tid] = gp;
-		runcnt[(size_t) sub * C + tid] = v;
-	}
-	__syncthreads();
-#pragma unroll
-	for (int q = 0; q < 2; q++)
-#pragma unroll
-		for (int j = 0; j < 16; j++)
-			if (ok[q][j]) {
-				const uint32_t c = pj_hash(k[q][j]) >> (32 - cbits);
-				const uint32_t d = start[c] + rk[q][j];
-				skey[d] = k[q][j];
-				srow[d] = (uint16_t) (q * 4096 + tid * 16 + j);
-			}
-	__syncthreads();
-	for (uint32_t j = tid; j < total; j += 256) {
-		const uint32_t key = skey[j];
-		const uint32_t c = pj_hash(key) >> (32 - cbits);
-		const uint32_t d = gpos[c] + (j - start[c]);
-		if (d < cap) {
-			const size_t e = (size_t) c * cap + d;
-			__builtin_nontemporal_store(key, &pkeys[e]);
-			__builtin_nontemporal_store(srow[j], &prow[e]);
-		}
-	}
-}
-
-// per XCD x, the probe chunks of its partitions c = x + 8 j in order:
-// xpre[x][j] = first chunk of partition j of x, xpre[x][per] = total
-__global__ void
-k_rp_plan(const uint32_t *fill, uint32_t cap, int cbits, uint32_t *xpre)
-{
-	const uint32_t x = threadIdx.x, per = (1u << cbits) >> 3;
-	if (x >= 8)
-		return;
-	uint32_t acc = 0;
-	for (uint32_t j = 0; j < per; j++) {
-		xpre[x * (per + 1) + j] = acc;
-		const uint32_t f = min(fill[x + 8 * j], cap);
-		acc += (f + RP_CHUNK - 1) / RP_CHUNK;
-	}
-	xpre[x * (per + 1) + per] = acc;
-}
-
-// probe: workgroup b runs on XCD b % 8 (round-robin dispatch) and takes the
-// (b / 8)-th chunk of that XCD's list
-__global__ __launch_bounds__(256) void
-k_rp_probe(const uint32_t *pkeys, uint32_t *pm, const uint32_t *fill, uint32_t cap, const uint32_t *xpre, int cbits,
-	   int pbits, uint32_t nbp, const ulonglong2 *t)
-{
-	constexpr int U = RP_CHUNK / 256;
-	const uint32_t x = blockIdx.x & 7, kk = blockIdx.x >> 3, per = (1u << cbits) >> 3;
-	const uint32_t *xp = xpre + x * (per + 1);
-	if (kk >= xp[per])
-		return;
-	uint32_t j = 0;
-	while (j + 1 < per && xp[j + 1] <= kk)
-		j++;
-	const uint32_t c = x + 8 * j;
-	const uint32_t f = min(fill[c], cap);
-	const uint32_t e0 = (kk - xp[j]) * RP_CHUNK + threadIdx.x;
-	const size_t base = (size_t) c * cap;
-	uint32_t key[U];
-#pragma unroll
-	for (int u = 0; u < U; u++) {
-		const uint32_t e = e0 + u * 256;
-		key[u] = __builtin_nontemporal_load(&pkeys[base + (e < f ? e : 0)]);
-	}
-	uint32_t reg[U], bk[U];
-	ulonglong2 sv[U];
-#pragma unroll
-	for (int u = 0; u < U; u++) {
-		const uint32_t h = pj_hash(key[u]);
-		reg[u] = h >> (32 - pbits);
-		bk[u] = gt_home(h, pbits, nbp);
-		sv[u] = t[(size_t) reg[u] * nbp + bk[u]];
-	}
-#pragma unroll
-	for (int u = 0; u < U; u++) {
-		const uint32_t e = e0 + u * 256;
-		const uint32_t m = gt_find(t, key[u], sv[u], reg[u], bk[u], nbp);
-		if (e < f)
-			__builtin_nontemporal_store(m, &pm[base + e]);
-	}
-}
-
-__global__ __launch_bounds__(256) void
-k_rp_restore(const uint16_t *prow, const uint32_t *pm, const uint32_t *runpos, const uint32_t *runcnt, int cbits,
-	     uint32_t cap, uint32_t nsub, BUN n, Side L, Side R, uint32_t *ticket, uint64_t *status, uint64_t *meta,
-	     oid *r1, oid *r2)
-{
-	// res[row + row / 32]: one pad word per 32 rows (the 32-row runs of
-	// consecutive threads in different banks)
-	__shared__ uint32_t res[RP_SUB + RP_SUB / 32];
-	__shared__ uint32_t rpre[257], rpos[256];
-	__shared__ uint32_t wsum4[4], rmask[256], rbase[256];
-	__shared__ uint32_t s_sub;
-	__shared__ uint64_t s_pre;
-	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
-	const uint32_t C = 1u << cbits;
-	if (tid == 0)
-		s_sub = atomicAdd(ticket, 1u);
-	for (uint32_t i = tid; i < RP_SUB + RP_SUB / 32; i += 256)
-		res[i] = 0;
-	__syncthreads();
-	const uint32_t sub = s_sub;
-	const BUN a = (BUN) sub * RP_SUB;
-	const uint32_t rows = (uint32_t) min((BUN) RP_SUB, n - a);
-	const uint32_t v = tid < C ? runcnt[(size_t) sub * C + tid] : 0;
-	const uint32_t p = tid < C ? runpos[(size_t) sub * C + tid] : 0;
-	uint32_t total;
-	const uint32_t pre = rp_scan256(v, wsum4, &total);
-	if (tid < C) {
-		rpre[tid] = pre;
-		rpos[tid] = p;
-	}
-	if (tid == 0)
-		rpre[C] = total;
-	__syncthreads();
-	constexpr int U = 8;
-	for (uint32_t j0 = tid; j0 < total; j0 += U * 256) {
-		uint32_t r[U], m[U];
-#pragma unroll
-		for (int u = 0; u < U; u++) {
-			const uint32_t j = j0 + u * 256;
-			// the run holding flat index j: largest c with rpre[c] <= j
-			uint32_t lo = 0;
-#pragma unroll
-			for (int b = RP_MAXCBITS - 1; b >= 0; b--) {
-				const uint32_t c2 = lo + (1u << b);
-				if (b < cbits && c2 < C && rpre[c2] <= j)
-					lo = c2;
-			}
-			const uint32_t d = rpos[lo] + (j - rpre[lo]);
-			const bool in = j < total && d < cap;
-			const size_t e = (size_t) lo * cap + (in ? d : 0);
-			r[u] = prow[e];
-			m[u] = in ? pm[e] : 0;
-		}
-#pragma unroll
-		for (int u = 0; u < U; u++)
-			if (m[u])
-				res[r[u] + (r[u] >> 5)] = m[u];
-	}
-	__syncthreads();
-	// thread tid counts rows [32 tid, 32 tid + 32): match mask + offset
-	static_assert(RP_SUB == 32 * 256, "32 rows per thread");
-	const uint32_t r0 = tid * 32, rb = tid * 33;
-	uint32_t msk = 0;
-#pragma unroll
-	for (int k = 0; k < 32; k++)
-		msk |= (uint32_t) ((r0 + k < rows) && res[rb + k] != 0) << k;
-	const uint32_t cn = __popc(msk);
-	uint32_t tot;
-	const uint32_t ex = rp_scan256(cn, wsum4, &tot);
-	rmask[tid] = msk;
-	rbase[tid] = ex;
-	if (w == 0) {
-		const uint64_t pr = lookback(status, sub, tot, (uint32_t *) &meta[1]);
-		if (lane == 0) {
-			s_pre = pr;
-			if (sub == nsub - 1)
-				meta[0] = pr + tot;
-		}
-	}
-	__syncthreads();
-	const uint64_t base = s_pre;
-	for (uint32_t r = tid; r < rows; r += 256) {
-		const uint32_t run = r >> 5, bit = r & 31;
-		const uint32_t mk = rmask[run];
-		if ((mk >> bit) & 1) {
-			const uint64_t o = base + rbase[run] + __popc(mk & ((1u << bit) - 1));
-			__builtin_nontemporal_store(oid_of(L, a + r), &r1[o]);
-			__builtin_nontemporal_store(oid_of(R, res[r + run] - 1), &r2[o]);
-		}
-	}
-}
-
-// returns 1 when not applicable (caller tries the next path)
-int
-join_rp(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_bat **ap, mgdk_bat **bp, bool *ukey)
-{
-	static const int mode = getenv("MGDK_JOIN_RP") ? atoi(getenv("MGDK_JOIN_RP")) : 1;
-	static const int cb_env = getenv("MGDK_JOIN_RP_CBITS") ? atoi(getenv("MGDK_JOIN_RP_CBITS")) : 7;
-	const bool w4 = L.w == 4 && R.w == 4, w8 = L.w == 8 && R.w == 8 && L.base && R.base;
-	if (mode == 0 || !(w4 || w8) || nr < 65536 || nl < RP_SUB || (mode == 1 && nr <= 2000000))
-		return 1;
-	int pbits = 6;
-	while (pbits < PJ_MAXPBITS && ((BUN) 8192 << pbits) < nr)
-		pbits++;
-	const uint32_t P = 1u << pbits;
-	const int cbits = std::min(std::max(cb_env, 3), std::min(pbits, RP_MAXCBITS));
-	const uint32_t C = 1u << cbits;
-	// build regions as the global-table path sizes them
-	const double mean = (double) nr / P;
-	const double mx = mean + 6.0 * sqrt(mean) + 64.0;
-	const uint64_t nbp = (uint64_t) (mx * 100.0 / (2.0 * 72)) + 1;
-	if (nbp > GT_MAXB)
-		return 1;
-	// probe partitions: mean + 8 sigma + 6 % + 4096 entries
-	const double pmean = (double) nl / C;
-	const uint64_t cap64 = ((uint64_t) (pmean * 1.06 + 8.0 * sqrt(pmean)) + 4096 + 63) & ~63ull;
-	if (cap64 * C >= (1ull << 32))
-		return 1;
-	const uint32_t cap = (uint32_t) cap64;
-	const uint32_t nsub = (uint32_t) ((nl + RP_SUB - 1) / RP_SUB);
-	const uint32_t per = C / 8;
-	const uint64_t grid_probe = 8ull * per * ((cap + RP_CHUNK - 1) / RP_CHUNK);
-	hipStream_t st = stream();
-	uint32_t *meta32 = (uint32_t *) meta_buf();
-	uint64_t *meta = (uint64_t *) meta32 + 4;          // [0] pairs, [1] look-back error
-	// meta32: [0] duplicate build key, [1] region overflow, [2] build value
-	// without a 4-byte image, [3] probe partition overflow, [4] build maxtot
-	PjSide B;
-	DevBuf gtab((size_t) P * nbp * 16 + 64);
-	DevBuf pkeys((size_t) C * cap * 4 + 64), prow((size_t) C * cap * 2 + 64), pm((size_t) C * cap * 4 + 64);
-	DevBuf runs((size_t) nsub * C * 8 + 64), small((size_t) C * 4 + 8 * (per + 1) * 4 + 256);
-	mgdk_bat *ra = newbat(0, MGDK_oid, nl), *rb = newbat(0, MGDK_oid, nl);
-	const size_t sbytes = (nsub + 8) * sizeof(uint64_t);
-	char *sc = (char *) scratch(sbytes);
-	if (!gtab.p || !pkeys.p || !prow.p || !pm.p || !runs.p || !small.p || !ra || !rb || !sc ||
-	    !hip_ok(hipMemsetAsync(meta32, 0, 64, st), "memset") || !hip_ok(hipMemsetAsync(sc, 0, sbytes, st), "memset") ||
-	    !hip_ok(hipMemsetAsync(small.p, 0, C * 4, st), "memset")) {
-		unfix2(ra, rb);
-		return sync_fail();
-	}
-	uint32_t *fill = small.as<uint32_t>(), *xpre = fill + C;
-	uint32_t *runpos = runs.as<uint32_t>(), *runcnt = runpos + (size_t) nsub * C;
-	Side Rn = R;
-	Rn.nofit = &meta32[2];
-	if (pj_cut(Rn, nr, pbits, !nil_matches, B, &meta32[4]) < 0) {
-		unfix2(ra, rb);
-		return sync_fail();
-	}
-	hipLaunchKernelGGL(k_gt_build, dim3(P), dim3(1024), 0, st, B.ent->as<uint2>(), B.base->as<uint32_t>(), pbits,
-			   (uint32_t) nbp, gtab.as<ulonglong2>(), &meta32[0]);
-	hipLaunchKernelGGL(k_rp_scatter, dim3(nsub), dim3(256), 0, st, L, nl, cbits, !nil_matches, cap, fill, runpos,
-			   runcnt, pkeys.as<uint32_t>(), prow.as<uint16_t>(), &meta32[3]);
-	hipLaunchKernelGGL(k_rp_plan, dim3(1), dim3(64), 0, st, fill, cap, cbits, xpre);
-	hipLaunchKernelGGL(k_rp_probe, dim3((unsigned) grid_probe), dim3(256), 0, st, pkeys.as<uint32_t>(),
-			   pm.as<uint32_t>(), fill, cap, xpre, cbits, pbits, (uint32_t) nbp, gtab.as<ulonglong2>());
-	hipLaunchKernelGGL(k_rp_restore, dim3(nsub), dim3(256), 0, st, prow.as<uint16_t>(), pm.as<uint32_t>(), runpos,
-			   runcnt, cbits, cap, nsub, nl, L, R, (uint32_t *) sc, (uint64_t *) sc + 8, meta, (oid *) ra->theap,
-			   (oid *) rb->theap);
-	uint32_t *h = (uint32_t *) pinned(64);
-	if (!hip_ok(hipMemcpyAsync(h, meta32, 64, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
-		unfix2(ra, rb);
-		return -1;
-	}
-	if (h[0] || h[1] || h[2] || h[3]) {
-		unfix2(ra, rb);
-		return 1;
-	}
-	const uint64_t *h64 = (const uint64_t *) h + 4;   // = meta
-	if (h64[1] & 1) {
-		seterr("HY013!BATjoin: look-back did not complete");
-		unfix2(ra, rb);
-		return -1;
-	}
-	ra->count = rb->count = h64[0];
-	*ukey = true;
-	*ap = ra;
-	*bp = rb;
-	return 0;
-}
-
-// ---------------------------------------------------------------------------
 // Broadcast path (small unique build side, <= BJ_MAXR rows; 4-byte keys or
 // 8-byte keys with 4-byte images): every workgroup builds the whole build
 // side's table in its LDS (the build column stays in L2) and then claims
@@ -2279,8 +1919,6 @@ hash_join(const mgdk_bat *l, const mgdk_bat *r, const Cand &lc, const Cand &rc, 
 	int rc_ = w == 4 || w == 8 ? join_bj(L, nl, R, nr, nil_matches, ap, bp, ukey) : 1;
 	if (rc_ > 0 && (w == 4 || w == 8))
 		rc_ = join_gt(L, nl, R, nr, nil_matches, ap, bp, ukey);
-	if (rc_ > 0 && (w == 4 || w == 8))
-		rc_ = join_rp(L, nl, R, nr, nil_matches, ap, bp, ukey);
 	if (rc_ > 0 && (w == 4 || w == 8))
 		rc_ = join_part(L, nl, R, nr, nil_matches, ap, bp, ukey);
 	if (rc_ > 0)
