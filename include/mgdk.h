@@ -246,6 +246,18 @@ int mgdk_GDKanalyticalwindowbounds(mgdk_bat *r, mgdk_bat *b, mgdk_bat *p, mgdk_b
 
 /* ---- fused MAL pipelines (one pass over the lineitem columns; same
  *      results as the op-at-a-time plans of SURVEY.md §3.2/§3.3) --------- */
+/* GROUP BY an ordered key with exact sums: the results of
+ * BATgroup(&g, &e, &h, b, NULL, NULL, NULL, NULL) (gdk/gdk_group.c:940-975),
+ * BATgroupsum(vals[v], g, e, NULL, TYPE_hge, true) for each value column
+ * (gdk/gdk_aggr.c:1009) and BATproject(e, b) widened to lng, without the
+ * group-id column: *extents (oid), *histo (lng), *keys (lng), sums[v] (hge).
+ * b: int / lng / oid / date / timestamp keys, sorted or reverse sorted (its
+ * order is looked up as BATordered does); vals: 1..4 int or lng columns of
+ * one width aligned with b.  Returns 0, 1 when not applicable (the caller
+ * runs the GDK operators), -1 on error.  The local step of the mergetable
+ * GROUP BY plan (opt_mergetable.c:1496-1670) in dist_group_aggr. */
+int mgdk_group_sums_ordered(mgdk_bat **extents, mgdk_bat **histo, mgdk_bat **keys, mgdk_bat **sums, mgdk_bat *b,
+			    mgdk_bat **vals, int nvals);
 /* Q6: sum(price*disc) over rows with d0 <= shipdate < d1, dlo <= disc <= dhi,
  * qty < qmax; result hge written to *revenue (16 bytes). */
 int mgdk_q6_fused(mgdk_bat *shipdate, mgdk_bat *discount, mgdk_bat *quantity,
@@ -303,6 +315,25 @@ int mgdk_GDKanalyticalsum(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mg
 			  int tp1, int tp2, int frame_type);
 int mgdk_GDKanalyticalcount(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e,
 			    bool ignore_nils, int tpe, int frame_type);
+/* gdk_analytic_func.c :124 GDKanalyticalntile, :230 GDKanalyticalfirst,
+ * :312 GDKanalyticallast, :421 GDKanalyticalnthvalue, :671 GDKanalyticallag,
+ * :823 GDKanalyticallead, :1264 GDKanalyticalmin / max (gdk_analytic.h:
+ * 23-37): r is caller-allocated (count(b) slots of type tpe); p: bit BAT of
+ * partition starts (NULL: one partition), o: peer-group starts, s / e:
+ * frame bounds.  ntile: exactly one of n (per-row tile counts of type tpe)
+ * and ntile (one value of tpe); nth_value: t (lng per row) or *pnth; lag /
+ * lead: BUN_NONE (INT64_MAX) gives all nils. */
+int mgdk_GDKanalyticalntile(mgdk_bat *r, mgdk_bat *b, mgdk_bat *p, mgdk_bat *n, int tpe, const void *ntile);
+int mgdk_GDKanalyticalfirst(mgdk_bat *r, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e, int tpe);
+int mgdk_GDKanalyticallast(mgdk_bat *r, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e, int tpe);
+int mgdk_GDKanalyticalnthvalue(mgdk_bat *r, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e, mgdk_bat *t, const int64_t *pnth,
+			       int tpe);
+int mgdk_GDKanalyticallag(mgdk_bat *r, mgdk_bat *b, mgdk_bat *p, mgdk_BUN lag, const void *default_value, int tpe);
+int mgdk_GDKanalyticallead(mgdk_bat *r, mgdk_bat *b, mgdk_bat *p, mgdk_BUN lead, const void *default_value, int tpe);
+int mgdk_GDKanalyticalmin(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e, int tpe,
+			  int frame_type);
+int mgdk_GDKanalyticalmax(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e, int tpe,
+			  int frame_type);
 /* gdk_analytic_statistics.c:364 GDKanalyticalavg (gdk_analytic.h:41): dbl
  * average per row over its frame, frame kinds as above; r is a
  * caller-allocated dbl BAT; tpe = type of b (bte..lng, flt, dbl) */

@@ -30,6 +30,7 @@
 #include <cstdio>
 
 #include "mgdk_internal.h"
+#include "segments.h"
 
 using namespace mgdk;
 
@@ -263,52 +264,6 @@ k_or_flags(const int8_t *p, const int8_t *o, BUN n, int8_t *f)
 	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
 		f[i] = i == 0 || (p && p[i]) || (o && o[i]);
 }
-
-// sorted list of segment starts (row 0 always first)
-struct Starts {
-	const oid *L;        // NULL: dense Lseq + k
-	oid Lseq;
-	BUN m;               // entries, including a virtual row 0 when lead
-	bool lead;
-	BUN n;
-	__device__ __forceinline__ oid at(BUN k) const
-	{
-		if (lead) {
-			if (k == 0)
-				return 0;
-			k--;
-		}
-		return L ? L[k] : Lseq + k;
-	}
-	// index of the segment holding row i
-	__device__ __forceinline__ BUN idx(BUN i) const
-	{
-		BUN lo = 0, hi = m;
-		while (hi - lo > 1) {
-			const BUN mid = (lo + hi) / 2;
-			if (at(mid) <= i)
-				lo = mid;
-			else
-				hi = mid;
-		}
-		return lo;
-	}
-	__device__ __forceinline__ BUN end_of(BUN k) const { return k + 1 < m ? at(k + 1) : n; }
-	// [start, end) of the segment holding row i
-	__device__ __forceinline__ void seg(BUN i, BUN &s, BUN &e) const
-	{
-		BUN lo = 0, hi = m;
-		while (hi - lo > 1) {
-			const BUN mid = (lo + hi) / 2;
-			if (at(mid) <= i)
-				lo = mid;
-			else
-				hi = mid;
-		}
-		s = at(lo);
-		e = lo + 1 < m ? at(lo + 1) : n;
-	}
-};
 
 struct FArgs {
 	BUN n;
@@ -592,6 +547,10 @@ k_first(const oid *L, oid *out)
 	*out = L[0];
 }
 
+}  // namespace
+
+namespace mgdk {
+
 // starts list from flags (nonzero = start); row 0 is always a start
 int
 make_starts(const int8_t *flags, BUN n, Starts &st, mgdk_bat **keep)
@@ -628,6 +587,10 @@ make_starts(const int8_t *flags, BUN n, Starts &st, mgdk_bat **keep)
 	st.m = S->count + (st.lead ? 1 : 0);
 	return 0;
 }
+
+}  // namespace mgdk
+
+namespace {
 
 bool
 sum_in_type(int t)

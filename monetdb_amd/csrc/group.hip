@@ -260,7 +260,7 @@ gl_hash(uint64_t k)
 
 template <int W, int G>
 __global__ __launch_bounds__(1024) void
-k_gl_first(KeySrc s, BUN n, unsigned long long *gkey, unsigned long long *gmin, uint32_t *err)
+k_gl_first(KeySrc s, BUN n, BUN tile0, unsigned long long *gkey, unsigned long long *gmin, uint32_t *err)
 {
 	__shared__ unsigned long long lkey[GL_SLOTS];
 	__shared__ uint32_t lmin[GL_SLOTS + 1];
@@ -272,7 +272,7 @@ k_gl_first(KeySrc s, BUN n, unsigned long long *gkey, unsigned long long *gmin, 
 	if (tid == 0)
 		lmin[GL_SLOTS] = ~0u;
 	__syncthreads();
-	const BUN a = (BUN) blockIdx.x * GL_TILE, e = min(n, a + GL_TILE);
+	const BUN a = ((BUN) blockIdx.x + tile0) * GL_TILE, e = min(n, a + GL_TILE);
 	bool ovf = false;
 	for (BUN i0 = a + tid; i0 < e; i0 += (BUN) GL_U * blockDim.x) {
 		uint64_t kk[GL_U];
@@ -380,15 +380,20 @@ gl_lookup(const unsigned long long *lkey, const uint32_t *lmap, uint64_t k)
 	if (k == GL_EMPTY)
 		return lmap[GL_SLOTS];
 	uint32_t h = gl_hash(k);
-	while (lkey[h] != k)
+	for (;;) {
+		const unsigned long long o = lkey[h];
+		if (o == k)
+			return lmap[h];
+		if (o == GL_EMPTY)
+			return ~0u;             // not in the table (the table keeps an empty slot)
 		h = (h + 1) & (GL_SLOTS - 1);
-	return lmap[h];
+	}
 }
 
 template <int W, int G>
 __global__ __launch_bounds__(1024) void
 k_gl_assign(KeySrc s, BUN n, const unsigned long long *gkey, const uint32_t *gmap, uint32_t ngrp, oid *gid,
-	    uint8_t *img, unsigned long long *histo, uint32_t *unsorted)
+	    uint8_t *img, unsigned long long *histo, uint32_t *unsorted, uint32_t *miss)
 {
 	__shared__ unsigned long long lkey[GL_SLOTS];
 	__shared__ uint32_t lmap[GL_SLOTS + 1];
@@ -405,14 +410,17 @@ k_gl_assign(KeySrc s, BUN n, const unsigned long long *gkey, const uint32_t *gma
 	__syncthreads();
 	const BUN a = (BUN) blockIdx.x * GL_TILE, e = min(n, a + GL_TILE);
 	uint32_t uns = 0;
+	bool mis = false;
 	for (BUN i0 = a + tid; i0 < e; i0 += (BUN) GL_U * blockDim.x) {
 		uint64_t kk[GL_U], kp[GL_U];
 #pragma unroll
 		for (int u = 0; u < GL_U; u++) {
 			const BUN i = i0 + (BUN) u * blockDim.x, ic = i < e ? i : e - 1;
 			kk[u] = gl_key_t<W, G>(s, ic);
-			// lane 0's predecessor lies in the previous wave's rows
-			kp[u] = lane == 0 && ic > 0 ? gl_key_t<W, G>(s, ic - 1) : 0;
+			// lane 0's predecessor lies in the previous wave's rows; loaded
+			// by every lane (the same lines): a load under a lane-0 branch
+			// would be waited for before the branch joins, one row at a time
+			kp[u] = gl_key_t<W, G>(s, ic > 0 ? ic - 1 : 0);
 		}
 #pragma unroll
 		for (int u = 0; u < GL_U; u++) {
@@ -420,10 +428,15 @@ k_gl_assign(KeySrc s, BUN n, const unsigned long long *gkey, const uint32_t *gma
 			uint32_t g = 0;
 			if (i < e) {
 				g = gl_lookup(lkey, lmap, kk[u]);
-				gid[i] = g;
-				if (img)
-					img[i] = (uint8_t) g;
-				atomicAdd(&lh[g], 1u);
+				if (g == ~0u) {
+					mis = true;         // first seen past the scanned prefix
+					g = 0;
+				} else {
+					gid[i] = g;
+					if (img)
+						img[i] = (uint8_t) g;
+					atomicAdd(&lh[g], 1u);
+				}
 			}
 			uint32_t gp = __shfl_up(g, 1);
 			if (lane == 0 && i > 0 && i < e)
@@ -434,13 +447,23 @@ k_gl_assign(KeySrc s, BUN n, const unsigned long long *gkey, const uint32_t *gma
 	}
 	if (__any(uns) && lane == 0)
 		publish_or(unsorted, 1u);
+	if (__any(mis) && lane == 0)
+		publish_or(miss, 1u);
 	__syncthreads();
 	for (uint32_t q = tid; q < ngrp; q += blockDim.x)
 		if (lh[q])
 			atomicAdd(&histo[q], (unsigned long long) lh[q]);
 }
 
-// returns 1 when the path does not apply (too many groups)
+// returns 1 when the path does not apply (too many groups).  The first
+// pass reads only a prefix of GL_PREFIX tiles first: the groups it finds
+// are numbered, and they are ALL the groups unless the assign pass meets a
+// key the prefix did not hold (flagged) -- then the first pass reads every
+// tile and the assign runs again.  A prefix group's first row lies inside
+// the prefix, before any later group's, so the ids are the first-occurrence
+// numbering either way (gdk_group.c:1118-1282).
+constexpr unsigned GL_PREFIX = 4;
+
 int
 group_lds(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mgdk_bat **enp, mgdk_bat **hnp)
 {
@@ -455,6 +478,7 @@ group_lds(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mg
 	    !hip_ok(hipMemsetAsync(m, 0, 16, st), "memset"))
 		return -1;
 	const unsigned tiles = (unsigned) ((n + GL_TILE - 1) / GL_TILE);
+	static const unsigned prefix = getenv("MGDK_GROUP_PREFIX") ? (unsigned) atoi(getenv("MGDK_GROUP_PREFIX")) : GL_PREFIX;
 	// typed fast path: dense candidates, integer keys of 1-8 bytes
 	const int fw = ks.dense && ks.kind <= 1 && ks.w <= 8 ? ks.w : 0;
 	const int fg = !ks.has_g ? 0 : ks.g8 ? 1 : ks.g ? 2 : 3;
@@ -478,66 +502,81 @@ group_lds(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mg
 		case 35: hipLaunchKernelGGL((K<8, 3>), __VA_ARGS__); break; \
 		default: hipLaunchKernelGGL((K<0, 0>), __VA_ARGS__); break; \
 		} } while (0)
-	GL_LAUNCH(k_gl_first, dim3(tiles), dim3(1024), 0, st, ks, n, gkey.as<unsigned long long>(),
-		  gmin.as<unsigned long long>(), &m[0]);
-	hipLaunchKernelGGL(k_gl_order, dim3(1), dim3(1024), 0, st, gmin.as<unsigned long long>(), gmap.as<uint32_t>(),
-			   ci.dense, ci.seq, ci.oids, ext.as<oid>(), &m[1]);
-	if (!hip_ok(hipMemcpyAsync(h, m, 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
-		return -1;
-	if (h[0] || h[1] > GL_MAXG)
-		return 1;
-	const uint32_t ngrp = h[1];
-	mgdk_bat *en = newbat(0, MGDK_oid, ngrp), *hn = newbat(0, MGDK_lng, ngrp), *gn = newbat(hseqb, MGDK_oid, n);
-	if (!en || !hn || !gn || !hip_ok(hipMemsetAsync(hn->theap, 0, ngrp * 8 + 8, st), "memset") ||
-	    !hip_ok(hipMemcpyAsync(en->theap, ext.p, ngrp * 8, hipMemcpyDeviceToDevice, st), "memcpy")) {
-		mgdk_BBPunfix(en);
-		mgdk_BBPunfix(hn);
-		mgdk_BBPunfix(gn);
-		return -1;
+	unsigned done = 0;          // tiles the first pass has read
+	unsigned upto = prefix > 0 && prefix < tiles ? prefix : tiles;
+	for (;;) {
+		GL_LAUNCH(k_gl_first, dim3(upto - done), dim3(1024), 0, st, ks, n, (BUN) done, gkey.as<unsigned long long>(),
+			  gmin.as<unsigned long long>(), &m[0]);
+		done = upto;
+		hipLaunchKernelGGL(k_gl_order, dim3(1), dim3(1024), 0, st, gmin.as<unsigned long long>(), gmap.as<uint32_t>(),
+				   ci.dense, ci.seq, ci.oids, ext.as<oid>(), &m[1]);
+		if (!hip_ok(hipMemcpyAsync(h, m, 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+			return -1;
+		if (h[0] || h[1] > GL_MAXG)
+			return 1;
+		const uint32_t ngrp = h[1];
+		mgdk_bat *en = newbat(0, MGDK_oid, ngrp), *hn = newbat(0, MGDK_lng, ngrp), *gn = newbat(hseqb, MGDK_oid, n);
+		auto unfix3 = [&]() {
+			mgdk_BBPunfix(en);
+			mgdk_BBPunfix(hn);
+			mgdk_BBPunfix(gn);
+		};
+		if (!en || !hn || !gn || !hip_ok(hipMemsetAsync(hn->theap, 0, ngrp * 8 + 8, st), "memset") ||
+		    !hip_ok(hipMemsetAsync(&m[2], 0, 8, st), "memset") ||
+		    !hip_ok(hipMemcpyAsync(en->theap, ext.p, ngrp * 8, hipMemcpyDeviceToDevice, st), "memcpy")) {
+			unfix3();
+			return -1;
+		}
+		uint8_t *img = nullptr;
+		gn->count = n;
+		if (ngrp <= 255 && (img = img8_new(gn)) == nullptr) {
+			unfix3();
+			return -1;
+		}
+		GL_LAUNCH(k_gl_assign, dim3(tiles), dim3(1024), 0, st, ks, n, gkey.as<unsigned long long>(),
+			  gmap.as<uint32_t>(), ngrp, (oid *) gn->theap, img, (unsigned long long *) hn->theap, &m[2], &m[3]);
+		oid fl[2] = {0, 0};
+		if (!hip_ok(hipMemcpyAsync(h, m, 16, hipMemcpyDeviceToHost, st), "memcpy") ||
+		    (ngrp > 0 && (!hip_ok(hipMemcpyAsync(&fl[0], ext.p, 8, hipMemcpyDeviceToHost, st), "memcpy") ||
+				  !hip_ok(hipMemcpyAsync(&fl[1], ext.as<oid>() + ngrp - 1, 8, hipMemcpyDeviceToHost, st),
+					  "memcpy"))) ||
+		    !sync()) {
+			unfix3();
+			return -1;
+		}
+		if (h[3]) {
+			// a key the prefix did not hold: read the remaining tiles too
+			unfix3();
+			if (done == tiles) {
+				seterr("BATgroup: a key missing from the complete table");
+				return -1;
+			}
+			upto = tiles;
+			continue;
+		}
+		gn->count = n;
+		en->count = ngrp;
+		hn->count = ngrp;
+		gn->tsorted = h[2] == 0;
+		gn->trevsorted = ngrp == 1 || n <= 1;
+		gn->tkey = ngrp == n;
+		gn->tnonil = 1;
+		en->tsorted = en->tkey = en->tnonil = 1;
+		en->trevsorted = ngrp == 1;
+		hn->tkey = ngrp == 1;
+		hn->tsorted = hn->trevsorted = ngrp == n || ngrp == 1;
+		hn->tnonil = 1;
+		// tmaxpos: the row that started the last group (maxgrppos,
+		// gdk_group.c:99,1313)
+		gn->tmaxpos = ngrp > 0 ? cand_index(ci, fl[1]) : MGDK_BUN_NONE;
+		if (ngrp > 0 && fl[1] - fl[0] == ngrp - 1)
+			setdense(en, fl[0], ngrp);
+		*gnp = gn;
+		*enp = en;
+		*hnp = hn;
+		return 0;
 	}
-	uint8_t *img = nullptr;
-	gn->count = n;
-	if (ngrp <= 255 && (img = img8_new(gn)) == nullptr) {
-		mgdk_BBPunfix(en);
-		mgdk_BBPunfix(hn);
-		mgdk_BBPunfix(gn);
-		return -1;
-	}
-	GL_LAUNCH(k_gl_assign, dim3(tiles), dim3(1024), 0, st, ks, n, gkey.as<unsigned long long>(),
-		  gmap.as<uint32_t>(), ngrp, (oid *) gn->theap, img, (unsigned long long *) hn->theap, &m[2]);
 #undef GL_LAUNCH
-	oid fl[2] = {0, 0};
-	if (!hip_ok(hipMemcpyAsync(h, m, 12, hipMemcpyDeviceToHost, st), "memcpy") ||
-	    (ngrp > 0 && (!hip_ok(hipMemcpyAsync(&fl[0], ext.p, 8, hipMemcpyDeviceToHost, st), "memcpy") ||
-			  !hip_ok(hipMemcpyAsync(&fl[1], ext.as<oid>() + ngrp - 1, 8, hipMemcpyDeviceToHost, st),
-				  "memcpy"))) ||
-	    !sync()) {
-		mgdk_BBPunfix(en);
-		mgdk_BBPunfix(hn);
-		mgdk_BBPunfix(gn);
-		return -1;
-	}
-	gn->count = n;
-	en->count = ngrp;
-	hn->count = ngrp;
-	gn->tsorted = h[2] == 0;
-	gn->trevsorted = ngrp == 1 || n <= 1;
-	gn->tkey = ngrp == n;
-	gn->tnonil = 1;
-	en->tsorted = en->tkey = en->tnonil = 1;
-	en->trevsorted = ngrp == 1;
-	hn->tkey = ngrp == 1;
-	hn->tsorted = hn->trevsorted = ngrp == n || ngrp == 1;
-	hn->tnonil = 1;
-	// tmaxpos: the row that started the last group (maxgrppos,
-	// gdk_group.c:99,1313)
-	gn->tmaxpos = ngrp > 0 ? cand_index(ci, fl[1]) : MGDK_BUN_NONE;
-	if (ngrp > 0 && fl[1] - fl[0] == ngrp - 1)
-		setdense(en, fl[0], ngrp);
-	*gnp = gn;
-	*enp = en;
-	*hnp = hn;
-	return 0;
 }
 
 // ---------------------------------------------------------------------------

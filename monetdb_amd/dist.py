@@ -208,6 +208,19 @@ class GdkBackend:
     def groupsum(self, c, g, e, tp):
         return self.gdk.BATgroupsum(c, g, e, tp)
 
+    def group_sums(self, keys, vals, tp):
+        """(extents, histo, keys widened to lng, [sums]) of GROUP BY keys
+        with exact sums: ONE fused pass when the keys are ordered and the
+        sums are hge (mgdk_group_sums_ordered), else BATgroup + BATgroupsum
+        + BATproject -- the same columns either way."""
+        g = self.gdk
+        if tp == g.TYPE_hge and 1 <= len(vals) <= 4:
+            r = g.group_sums_ordered(keys, vals)
+            if r is not None:
+                return r
+        gi, e, h = self.group(keys)
+        return e, h, self.widen(self.project(e, keys)), [self.groupsum(v, gi, e, tp) for v in vals]
+
     def groupmin(self, c, g, e):
         # MAL aggr.min: the positions of BATgroupmin projected (aggr.c:321-333)
         return self.gdk.BATproject(self.gdk.BATgroupmin(c, g, e), c)
@@ -512,15 +525,16 @@ def dist_group_aggr(be, dist, keys, vals):
     """
     TL, TO, TH = _types(be)
     world, rank = _world(dist)
-    g, e, h = be.group(keys)
+    # the piece's BATgroup + BATgroupsum (+ the group keys): fused into one
+    # pass over the values when the keys are ordered (be.group_sums)
+    e, h, gk, gs = be.group_sums(keys, vals, TH)
     if world == 1:
         # one piece: mergetable leaves the plan's BATgroup + BATgroupsum as
         # they are (opt_mergetable.c:1496-1670); their ids are already the
         # first-occurrence numbering, extents the first rows, histo the counts
-        return {"gid": be.dense(0, be.n(e)), "key": be.widen(be.project(e, keys)), "first_row": e,
-                "count": h, "sums": [be.groupsum(v, g, e, TH) for v in vals]}
+        return {"gid": be.dense(0, be.n(e)), "key": gk, "first_row": e, "count": h, "sums": gs}
     row0s = _row0s(be, dist, keys)
-    parts = [be.widen(be.project(e, keys)), e, h] + [be.groupsum(v, g, e, TH) for v in vals]
+    parts = [gk, e, h] + gs
     order, counts = be.hashpartition(parts[0], world)
     parts = [be.project(order, c) for c in parts]
     parts = exchange(be, dist, parts, [TL, TO, TL] + [TH] * len(vals), counts)

@@ -132,6 +132,8 @@ _SIGS = {
     "mgdk_BATsort": (C.c_int, [PP, PP, PP, P, P, P, C.c_bool, C.c_bool, C.c_bool]),
     "mgdk_GDKanalyticalwindowbounds": (C.c_int, [P, P, P, P, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                                  C.c_bool, C.c_uint64]),
+    "mgdk_group_sums_ordered": (C.c_int, [C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(P), P,
+                                           C.POINTER(P), C.c_int]),
     "mgdk_q6_fused": (C.c_int, [P, P, P, P, C.c_int32, C.c_int32, C.c_int64, C.c_int64, C.c_int64,
                                 C.c_void_p]),
     "mgdk_q1_fused": (C.c_int, [P, P, P, P, P, P, P, C.c_int32, C.POINTER(Q1Row), C.c_int,
@@ -158,6 +160,14 @@ _SIGS = {
     "mgdk_GDKanalyticalsum": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_int, C.c_int]),
     "mgdk_GDKanalyticalcount": (C.c_int, [C.c_void_p] * 6 + [C.c_bool, C.c_int, C.c_int]),
     "mgdk_GDKanalyticalavg": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_int]),
+    "mgdk_GDKanalyticalntile": (C.c_int, [C.c_void_p] * 4 + [C.c_int, C.c_void_p]),
+    "mgdk_GDKanalyticalfirst": (C.c_int, [C.c_void_p] * 4 + [C.c_int]),
+    "mgdk_GDKanalyticallast": (C.c_int, [C.c_void_p] * 4 + [C.c_int]),
+    "mgdk_GDKanalyticalnthvalue": (C.c_int, [C.c_void_p] * 6 + [C.c_int]),
+    "mgdk_GDKanalyticallag": (C.c_int, [C.c_void_p] * 3 + [C.c_uint64, C.c_void_p, C.c_int]),
+    "mgdk_GDKanalyticallead": (C.c_int, [C.c_void_p] * 3 + [C.c_uint64, C.c_void_p, C.c_int]),
+    "mgdk_GDKanalyticalmin": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_int]),
+    "mgdk_GDKanalyticalmax": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_int]),
     "mgdk_GDKanalyticalavginteger": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_int]),
     "mgdk_BATlowerbound2": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
                                       C.c_void_p]),
@@ -684,6 +694,79 @@ def GDKanalyticalsum(b, p, o, s, e, tp2, frame_type):
     return r
 
 
+BUN_NONE = (1 << 63) - 1
+
+
+def _wres(tp, n):
+    return BAT(lib().mgdk_COLnew(0, tp, max(1, n)))
+
+
+def GDKanalyticalntile(b, p, n=None, ntile=None, tpe=None):
+    """gdk_analytic_func.c:124: the tile number of every row in its
+    partition; n a BAT of per-row tile counts or ntile one value of tpe."""
+    keep = []
+    tpe = tpe if tpe is not None else n.ttype
+    r = _wres(tpe, b.count())
+    _chk(lib().mgdk_GDKanalyticalntile(r.ptr, b.ptr, _p(p), _p(n), tpe,
+                                       _valptr(tpe, ntile, keep) if n is None else None))
+    return r
+
+
+def GDKanalyticalfirst(b, s, e):
+    """gdk_analytic_func.c:230: the first value of every row's frame."""
+    r = _wres(b.ttype, b.count())
+    _chk(lib().mgdk_GDKanalyticalfirst(r.ptr, b.ptr, s.ptr, e.ptr, b.ttype))
+    return r
+
+
+def GDKanalyticallast(b, s, e):
+    """gdk_analytic_func.c:312: the last value of every row's frame."""
+    r = _wres(b.ttype, b.count())
+    _chk(lib().mgdk_GDKanalyticallast(r.ptr, b.ptr, s.ptr, e.ptr, b.ttype))
+    return r
+
+
+def GDKanalyticalnthvalue(b, s, e, t=None, nth=None):
+    """gdk_analytic_func.c:421: the nth value of every row's frame (t: lng
+    BAT of per-row n, or nth one value)."""
+    r = _wres(b.ttype, b.count())
+    ref = C.c_int64(nth) if t is None else None
+    _chk(lib().mgdk_GDKanalyticalnthvalue(r.ptr, b.ptr, s.ptr, e.ptr, _p(t),
+                                          C.cast(C.pointer(ref), C.c_void_p) if ref is not None else None,
+                                          b.ttype))
+    return r
+
+
+def GDKanalyticallag(b, p, lag, default):
+    """gdk_analytic_func.c:671: the value `lag` rows back in the partition."""
+    keep = []
+    r = _wres(b.ttype, b.count())
+    _chk(lib().mgdk_GDKanalyticallag(r.ptr, b.ptr, _p(p), lag, _valptr(b.ttype, default, keep), b.ttype))
+    return r
+
+
+def GDKanalyticallead(b, p, lead, default):
+    """gdk_analytic_func.c:823: the value `lead` rows ahead in the partition."""
+    keep = []
+    r = _wres(b.ttype, b.count())
+    _chk(lib().mgdk_GDKanalyticallead(r.ptr, b.ptr, _p(p), lead, _valptr(b.ttype, default, keep), b.ttype))
+    return r
+
+
+def GDKanalyticalmin(b, p, o, s, e, frame_type):
+    """gdk_analytic_func.c:1264: windowed min per row over its frame."""
+    r = _wres(b.ttype, b.count())
+    _chk(lib().mgdk_GDKanalyticalmin(r.ptr, _p(p), _p(o), b.ptr, _p(s), _p(e), b.ttype, frame_type))
+    return r
+
+
+def GDKanalyticalmax(b, p, o, s, e, frame_type):
+    """gdk_analytic_func.c:1264: windowed max per row over its frame."""
+    r = _wres(b.ttype, b.count())
+    _chk(lib().mgdk_GDKanalyticalmax(r.ptr, _p(p), _p(o), b.ptr, _p(s), _p(e), b.ttype, frame_type))
+    return r
+
+
 def GDKanalyticalcount(b, p, o, s, e, ignore_nils, frame_type):
     """Windowed count per row over its frame (gdk_analytic_func.c:1626)."""
     r = BAT(lib().mgdk_COLnew(0, TYPE_lng, max(1, b.count())))
@@ -705,6 +788,22 @@ def GDKanalyticalavginteger(b, p, o, s, e, frame_type):
     r = BAT(lib().mgdk_COLnew(0, b.ttype, max(1, b.count())))
     _chk(lib().mgdk_GDKanalyticalavginteger(r.ptr, _p(p), _p(o), b.ptr, _p(s), _p(e), b.ttype, frame_type))
     return r
+
+
+def group_sums_ordered(b, vals):
+    """(extents, histo, keys-as-lng, [hge sums]) of GROUP BY an ordered b with
+    exact sums of vals (mgdk_group_sums_ordered), or None when b's order or
+    the types do not allow it (the caller runs BATgroup + BATgroupsum)."""
+    e, h, k = P(), P(), P()
+    nv = len(vals)
+    sums = (P * nv)()
+    vv = (P * nv)(*[v.ptr for v in vals])
+    rc = lib().mgdk_group_sums_ordered(C.byref(e), C.byref(h), C.byref(k), sums, b.ptr, vv, nv)
+    if rc < 0:
+        raise _err()
+    if rc > 0:
+        return None
+    return BAT(e), BAT(h), BAT(k), [BAT(sums[i]) for i in range(nv)]
 
 
 def q6_fused(shipdate, discount, quantity, price, d0, d1, dlo, dhi, qmax):

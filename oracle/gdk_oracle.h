@@ -28,6 +28,8 @@
  *               gdk/gdk_analytic_statistics.c:364 (avg), :428-700 (avginteger), segment
  *               tree gdk/gdk_analytic.h:52-130
  *   firstn      gdk/gdk_firstn.c:71-97 (heap), :211-1020, :1280
+ *   window fns  gdk/gdk_analytic_func.c:124-1300 ntile, first, last,
+ *               nth_value, lag, lead, min, max (gdk_oracle_window.c)
  *
  * Parity pinning: see tests/golden/ (fixtures extracted from the reference's
  * own MAL known-answer tests) and DESIGN.md §Oracle.
@@ -184,6 +186,21 @@ int ora_analyticalavg(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_
 		      const ora_bat *s, const ora_bat *e, int tpe, int frame_type);
 int ora_analyticalavginteger(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_bat *b,
 			     const ora_bat *s, const ora_bat *e, int tpe, int frame_type);
+/* gdk_analytic_func.c :124 ntile, :230 first, :312 last, :421 nth_value,
+ * :671 lag, :823 lead, :1264 min / max (gdk_oracle_window.c); r is a
+ * caller-allocated BAT of count(b) slots of type tpe */
+int ora_analyticalntile(ora_bat *r, const ora_bat *b, const ora_bat *p, const ora_bat *n, int tpe,
+			const void *ntile);
+int ora_analyticalfirst(ora_bat *r, const ora_bat *b, const ora_bat *s, const ora_bat *e, int tpe);
+int ora_analyticallast(ora_bat *r, const ora_bat *b, const ora_bat *s, const ora_bat *e, int tpe);
+int ora_analyticalnthvalue(ora_bat *r, const ora_bat *b, const ora_bat *s, const ora_bat *e, const ora_bat *t,
+			   const int64_t *pnth, int tpe);
+int ora_analyticallag(ora_bat *r, const ora_bat *b, const ora_bat *p, uint64_t lag, const void *def, int tpe);
+int ora_analyticallead(ora_bat *r, const ora_bat *b, const ora_bat *p, uint64_t lead, const void *def, int tpe);
+int ora_analyticalmin(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_bat *b, const ora_bat *s,
+		      const ora_bat *e, int tpe, int frame_type);
+int ora_analyticalmax(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_bat *b, const ora_bat *s,
+		      const ora_bat *e, int tpe, int frame_type);
 int ora_analyticalcount(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_bat *b,
 			const ora_bat *s, const ora_bat *e, bool ignore_nils, int frame_type);
 

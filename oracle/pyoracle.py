@@ -115,6 +115,14 @@ def lib():
         L.ora_analyticalavg.argtypes = [P, P, P, P, P, P, C.c_int, C.c_int]
         L.ora_analyticalavginteger.argtypes = [P, P, P, P, P, P, C.c_int, C.c_int]
         L.ora_analyticalcount.argtypes = [P, P, P, P, P, P, C.c_bool, C.c_int]
+        L.ora_analyticalntile.argtypes = [P, P, P, P, C.c_int, C.c_void_p]
+        L.ora_analyticalfirst.argtypes = [P, P, P, P, C.c_int]
+        L.ora_analyticallast.argtypes = [P, P, P, P, C.c_int]
+        L.ora_analyticalnthvalue.argtypes = [P, P, P, P, P, C.c_void_p, C.c_int]
+        L.ora_analyticallag.argtypes = [P, P, P, C.c_uint64, C.c_void_p, C.c_int]
+        L.ora_analyticallead.argtypes = [P, P, P, C.c_uint64, C.c_void_p, C.c_int]
+        L.ora_analyticalmin.argtypes = [P, P, P, P, P, P, C.c_int, C.c_int]
+        L.ora_analyticalmax.argtypes = [P, P, P, P, P, P, C.c_int, C.c_int]
         L.ora_tpch_lineitem.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64] + [C.c_void_p] * 7
         L.ora_mkdate.restype = C.c_int32
         L.ora_mkdate.argtypes = [C.c_int, C.c_int, C.c_int]
@@ -556,3 +564,63 @@ def q1(cols, nthreads=1):
                         rem_qty=r.rem_qty, rem_price=r.rem_price, rem_disc=r.rem_disc,
                         count_order=r.count_order))
     return res
+
+
+# ---- window functions (gdk_oracle_window.c) --------------------------------
+BUN_NONE = (1 << 63) - 1
+
+
+def _wrun(tp, n, fn, *args):
+    r = lib().ora_new(tp, n, 0)
+    if fn(r, *args) < 0:
+        lib().ora_free(r)
+        raise _err()
+    return Bat(r)
+
+
+def _pp(b):
+    return b.ptr if b is not None else None
+
+
+def analyticalntile(b, p, n=None, ntile=None, tpe=None):
+    """GDKanalyticalntile: n a BAT of per-row tile counts, or ntile a scalar of tpe."""
+    keep = []
+    tpe = tpe if tpe is not None else n.s.type
+    return _wrun(tpe, b.count(), lib().ora_analyticalntile, b.ptr, _pp(p), _pp(n), tpe,
+                 _valptr(tpe, ntile, keep) if n is None else None)
+
+
+def analyticalfirst(b, s, e):
+    return _wrun(b.s.type, b.count(), lib().ora_analyticalfirst, b.ptr, s.ptr, e.ptr, b.s.type)
+
+
+def analyticallast(b, s, e):
+    return _wrun(b.s.type, b.count(), lib().ora_analyticallast, b.ptr, s.ptr, e.ptr, b.s.type)
+
+
+def analyticalnthvalue(b, s, e, t=None, nth=None):
+    ref = C.c_int64(nth) if t is None else None
+    return _wrun(b.s.type, b.count(), lib().ora_analyticalnthvalue, b.ptr, s.ptr, e.ptr, _pp(t),
+                 C.cast(C.pointer(ref), C.c_void_p) if ref is not None else None, b.s.type)
+
+
+def analyticallag(b, p, lag, default):
+    keep = []
+    return _wrun(b.s.type, b.count(), lib().ora_analyticallag, b.ptr, _pp(p), lag,
+                 _valptr(b.s.type, default, keep), b.s.type)
+
+
+def analyticallead(b, p, lead, default):
+    keep = []
+    return _wrun(b.s.type, b.count(), lib().ora_analyticallead, b.ptr, _pp(p), lead,
+                 _valptr(b.s.type, default, keep), b.s.type)
+
+
+def analyticalmin(b, p, o, s, e, frame_type):
+    return _wrun(b.s.type, b.count(), lib().ora_analyticalmin, _pp(p), _pp(o), b.ptr, _pp(s), _pp(e),
+                 b.s.type, frame_type)
+
+
+def analyticalmax(b, p, o, s, e, frame_type):
+    return _wrun(b.s.type, b.count(), lib().ora_analyticalmax, _pp(p), _pp(o), b.ptr, _pp(s), _pp(e),
+                 b.s.type, frame_type)

@@ -99,6 +99,10 @@ class OracleBackend:
     def groupsum(self, c, g, e, tp):
         return _from_ora(ora.BATgroupsum(c.ora(), g.ora(), e.ora(), tp))
 
+    def group_sums(self, keys, vals, tp):
+        gi, e, h = self.group(keys)
+        return e, h, self.widen(self.project(e, keys)), [self.groupsum(v, gi, e, tp) for v in vals]
+
     def groupmin(self, c, g, e):
         co = c.ora()
         return _from_ora(ora.BATproject(ora.BATgroupminmax(co, g.ora(), e.ora(), False), co))

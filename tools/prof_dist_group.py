@@ -53,7 +53,7 @@ def main():
     D.dist_group_aggr(be, None, okey, vals)
     tot = time.perf_counter() - t0
     ops = {}
-    for k in ("group", "groupsum", "groupcount", "project", "sort", "calc", "convert", "BATsort", "groupmin"):
+    for k in ("group_sums_ordered", "group", "groupsum", "groupcount", "project", "sort", "calc", "convert", "BATsort", "groupmin"):
         ms, n = gdk.prof_get(k)
         if n:
             ops[k] = [round(ms, 3), n]
