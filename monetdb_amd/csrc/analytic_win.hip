@@ -442,7 +442,11 @@ fl_run(int mode, mgdk_bat *r, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e, mgdk_bat *t
 		}
 		nth0 = *pnth == INT64_MIN ? -1 : *pnth - 1;
 	}
-	uint32_t *fl = (uint32_t *) meta_buf();
+	// flags in a buffer of their own: make_starts uses meta_buf()
+	DevBuf flb(64);
+	uint32_t *fl = flb.as<uint32_t>();
+	if (fl == nullptr)
+		return -1;
 	hipStream_t st = stream();
 	if (!hip_ok(hipMemsetAsync(fl, 0, 8, st), "memset"))
 		return -1;
@@ -480,7 +484,11 @@ lag_run(bool lead, mgdk_bat *r, mgdk_bat *b, mgdk_bat *p, BUN off, const void *d
 	}
 	if (!bits_ok(p, n))
 		return -1;
-	uint32_t *fl = (uint32_t *) meta_buf();
+	// flags in a buffer of their own: make_starts uses meta_buf()
+	DevBuf flb(64);
+	uint32_t *fl = flb.as<uint32_t>();
+	if (fl == nullptr)
+		return -1;
 	hipStream_t st = stream();
 	if (!hip_ok(hipMemsetAsync(fl, 0, 8, st), "memset"))
 		return -1;
@@ -586,7 +594,11 @@ minmax_run(bool ismax, mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_
 		return -1;
 	}
 	hipStream_t st = stream();
-	uint32_t *fl = (uint32_t *) meta_buf();
+	// flags in a buffer of their own: make_starts uses meta_buf()
+	DevBuf flb(64);
+	uint32_t *fl = flb.as<uint32_t>();
+	if (fl == nullptr)
+		return -1;
 	if (!hip_ok(hipMemsetAsync(fl, 0, 8, st), "memset"))
 		return -1;
 	const int cls = wclass(tpe);
@@ -716,7 +728,11 @@ mgdk_GDKanalyticalntile(mgdk_bat *r, mgdk_bat *b, mgdk_bat *p, mgdk_bat *n, int 
 	if (make_starts(p ? (const int8_t *) p->theap : nullptr, cnt, part, &keep) < 0)
 		return -1;
 	hipStream_t st = stream();
-	uint32_t *fl = (uint32_t *) meta_buf();
+	// flags in a buffer of their own: make_starts uses meta_buf()
+	DevBuf flb(64);
+	uint32_t *fl = flb.as<uint32_t>();
+	if (fl == nullptr)
+		return -1;
 	if (!hip_ok(hipMemsetAsync(fl, 0, 8, st), "memset")) {
 		mgdk_BBPunfix(keep);
 		return -1;

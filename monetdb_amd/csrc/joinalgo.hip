@@ -1092,6 +1092,62 @@ joincost(mgdk_bat *r, Ord &o, BUN lcount, const Cand &rc, const mgdk_bat *sr, co
 	return 0;
 }
 
+// flt / dbl join keys as integer images that keep both equality and order
+// under the reference's compare (dbl_cmp: -0.0 == +0.0; nil = NaN below
+// every value): -0.0 -> +0.0, the sign-magnitude bits turned into two's
+// complement order, NaN -> the integer nil (no float maps there).  BATjoin
+// over the images takes the reference's algorithm choices and result order
+// for the floats (hash path gdk_join.c:2900 with the value's hash, merge
+// paths for ordered inputs) and returns the same oids.
+template <typename F, typename I, typename U>
+__global__ __launch_bounds__(256) void
+k_float_image(const F *in, BUN n, I *out)
+{
+	constexpr U SIGN = (U) 1 << (sizeof(U) * 8 - 1);
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		F v = in[i];
+		I r;
+		if (v != v) {
+			r = (I) SIGN;                // the integer nil
+		} else {
+			if (v == (F) 0)
+				v = (F) 0;              // -0.0 -> +0.0
+			U u;
+			__builtin_memcpy(&u, &v, sizeof u);
+			u = (u & SIGN) ? ~u : (u | SIGN);
+			r = (I) (u ^ SIGN);
+		}
+		out[i] = r;
+	}
+}
+
+mgdk_bat *
+float_image(const mgdk_bat *b)
+{
+	const bool dbl = basetype(b->ttype) == MGDK_dbl;
+	mgdk_bat *m = newbat(b->hseqbase, dbl ? MGDK_lng : MGDK_int, b->count);
+	if (m == nullptr)
+		return nullptr;
+	if (b->count) {
+		if (dbl)
+			hipLaunchKernelGGL((k_float_image<double, int64_t, uint64_t>), dim3(grid_for(b->count, 1024, 16384)),
+					   dim3(256), 0, stream(), (const double *) b->theap, b->count, (int64_t *) m->theap);
+		else
+			hipLaunchKernelGGL((k_float_image<float, int32_t, uint32_t>), dim3(grid_for(b->count, 1024, 16384)),
+					   dim3(256), 0, stream(), (const float *) b->theap, b->count, (int32_t *) m->theap);
+	}
+	m->count = b->count;
+	m->tsorted = b->tsorted;
+	m->trevsorted = b->trevsorted;
+	m->tkey = b->tkey;
+	m->tnonil = b->tnonil;
+	m->tnil = b->tnil;
+	m->tnosorted = b->tnosorted;
+	m->tnorevsorted = b->tnorevsorted;
+	m->tseqbase = MGDK_OID_NIL;
+	return m;
+}
+
 }  // namespace
 
 extern "C" int
@@ -1126,6 +1182,31 @@ mgdk_BATjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk_bat 
 	if (basetype(atomtype(l->ttype)) != basetype(atomtype(r->ttype))) {
 		seterr("42000!BATjoin: inputs not compatible.");
 		return -1;
+	}
+	if (basetype(l->ttype) == MGDK_flt || basetype(l->ttype) == MGDK_dbl) {
+		mgdk_bat *li = float_image(l), *ri = li ? float_image(r) : nullptr;
+		int rc = -1;
+		if (li && ri) {
+			rc = mgdk_BATjoin(r1p, r2p, li, ri, sl, sr, nil_matches, estimate);
+			// the order the scans found on the images holds for the floats
+			l->tsorted |= li->tsorted;
+			l->trevsorted |= li->trevsorted;
+			l->tkey |= li->tkey;
+			r->tsorted |= ri->tsorted;
+			r->trevsorted |= ri->trevsorted;
+			r->tkey |= ri->tkey;
+			if (!l->tnosorted)
+				l->tnosorted = li->tnosorted;
+			if (!l->tnorevsorted)
+				l->tnorevsorted = li->tnorevsorted;
+			if (!r->tnosorted)
+				r->tnosorted = ri->tnosorted;
+			if (!r->tnorevsorted)
+				r->tnorevsorted = ri->tnorevsorted;
+		}
+		mgdk_BBPunfix(li);
+		mgdk_BBPunfix(ri);
+		return rc;
 	}
 	if (!join_type_ok(l->ttype) || !join_type_ok(r->ttype)) {
 		seterr("42000!BATjoin: type %s not supported on the device path", atomname(l->ttype));

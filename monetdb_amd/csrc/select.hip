@@ -1095,6 +1095,186 @@ compact_flags(const int8_t *flags, BUN n, oid base, bool nonzero)
 }
 }  // namespace mgdk
 
+namespace {
+
+// ---- str columns: BATselect's generic part with strCmp, then the
+// fullscan_any predicate (gdk/gdk_select.c:449-605) per candidate.
+// fullscan_str's string-elimination path (:608-760) compares heap offsets
+// instead of bytes when doubles are eliminated -- the same oids.
+
+constexpr char SEL_STR_NIL[2] = {'\x80', 0};
+
+__device__ __forceinline__ const uint8_t *
+sel_str_at(const void *offs, int w, const char *vh, BUN p)
+{
+	size_t o;
+	switch (w) {
+	case 1: o = (size_t) ((const uint8_t *) offs)[p] + 8192; break;     // GDK_VAROFFSET
+	case 2: o = (size_t) ((const uint16_t *) offs)[p] + 8192; break;
+	case 4: o = (size_t) ((const uint32_t *) offs)[p]; break;
+	default: o = (size_t) ((const uint64_t *) offs)[p]; break;
+	}
+	return (const uint8_t *) vh + o;
+}
+
+__device__ __forceinline__ bool
+dstr_isnil(const uint8_t *a)
+{
+	return a[0] == 0x80 && a[1] == 0;
+}
+
+// strCmp (gdk_atoms.c): nil before every string, then strcmp's unsigned bytes
+__device__ __forceinline__ int
+dstr_cmp(const uint8_t *a, const uint8_t *b)
+{
+	const bool an = dstr_isnil(a), bn = dstr_isnil(b);
+	if (an || bn)
+		return an ? -(int) !bn : 1;
+	for (;; a++, b++) {
+		const int x = *a, y = *b;
+		if (x != y)
+			return x < y ? -1 : 1;
+		if (x == 0)
+			return 0;
+	}
+}
+
+struct StrSel {
+	const void *offs;
+	int w;
+	const char *vh;
+	oid hseq;
+	const uint8_t *tl, *th;     // device copies
+	bool li, hi, equi, anti, nil_matches, lval, hval, all_but_nil;
+};
+
+// flags over rows [first, first + m): 1 where a candidate row qualifies
+__global__ __launch_bounds__(256) void
+k_sel_str(StrSel a, bool dense, oid cseq, const oid *coids, BUN ncand, oid first, int8_t *flags)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < ncand; i += (BUN) gridDim.x * blockDim.x) {
+		const oid o = dense ? cseq + i : coids[i];
+		const uint8_t *v = sel_str_at(a.offs, a.w, a.vh, o - a.hseq);
+		const bool isnil = dstr_isnil(v);
+		bool ok;
+		int c;
+		if (a.all_but_nil)
+			ok = !isnil;
+		else if (a.equi)
+			ok = dstr_cmp(a.tl, v) == 0;
+		else if (a.anti)
+			ok = (a.nil_matches && isnil) ||
+			     (!isnil && ((a.lval && ((c = dstr_cmp(a.tl, v)) > 0 || (!a.li && c == 0))) ||
+					 (a.hval && ((c = dstr_cmp(a.th, v)) < 0 || (!a.hi && c == 0)))));
+		else
+			ok = !isnil && (!a.lval || (c = dstr_cmp(a.tl, v)) < 0 || (a.li && c == 0)) &&
+			     (!a.hval || (c = dstr_cmp(a.th, v)) > 0 || (a.hi && c == 0));
+		flags[o - first] = ok;
+	}
+}
+
+int
+host_str_cmp(const char *a, const char *b)
+{
+	const bool an = (unsigned char) a[0] == 0x80 && a[1] == 0, bn = (unsigned char) b[0] == 0x80 && b[1] == 0;
+	if (an || bn)
+		return an ? -(int) !bn : 1;
+	const int c = strcmp(a, b);
+	return (c > 0) - (c < 0);
+}
+
+mgdk_bat *
+select_str(mgdk_bat *b, const Cand &ci, const char *tl, const char *th, bool li, bool hi, bool anti,
+	   bool nil_matches)
+{
+	if (b->tvheap == nullptr) {
+		seterr("42000!BATselect: str column without a string heap");
+		return nullptr;
+	}
+	const char *nil = SEL_STR_NIL;
+	bool lnil = host_str_cmp(tl, nil) == 0;
+	bool lval = !lnil || th == nullptr;
+	bool equi = th == nullptr || (lval && host_str_cmp(tl, th) == 0);
+	bool hval;
+	if (lnil && nil_matches && (th == nullptr || host_str_cmp(th, nil) == 0)) {
+		equi = true;
+		lval = true;
+	}
+	if (equi) {
+		if (th == nullptr)
+			hi = li;
+		th = tl;
+		hval = true;
+		if (!anti && (!li || !hi))
+			return empty_result();
+	} else {
+		nil_matches = false;
+		hval = host_str_cmp(th, nil) != 0;
+	}
+	bool all_but_nil = false;
+	if (anti) {
+		if (lval != hval) {
+			const char *tv = tl;
+			bool ti = li;
+			li = !hi;
+			hi = !ti;
+			tl = th;
+			th = tv;
+			ti = lval;
+			lval = hval;
+			hval = ti;
+			lnil = host_str_cmp(tl, nil) == 0;
+			anti = false;
+		} else if (!lval && !hval) {
+			return empty_result();
+		} else if ((equi && (lnil || !(li && hi))) || host_str_cmp(tl, th) > 0) {
+			// everything except nil (:1482-1509)
+			if (equi && !lnil && nil_matches && !(li && hi))
+				return cand_slice(ci);
+			if (b->tnonil)
+				return cand_slice(ci);
+			all_but_nil = true;
+		} else {
+			equi = false;
+		}
+	}
+	if (!all_but_nil && hval && (equi ? !li || !hi : host_str_cmp(tl, th) > 0))
+		return empty_result();
+	if (equi && lnil && b->tnonil)
+		return empty_result();
+	const size_t ll = strlen(tl) + 1, hl = strlen(th) + 1;
+	const BUN m = ci.last - ci.first + 1;
+	DevBuf vals(ll + hl + 16), flags(m + 8);
+	hipStream_t st = stream();
+	if (!vals.p || !flags.p || !hip_ok(hipMemsetAsync(flags.p, 0, m, st), "memset"))
+		return nullptr;
+	char *hv = (char *) stage_host(tl, ll);
+	char *hv2 = (char *) stage_host(th, hl);
+	if (!hip_ok(hipMemcpyAsync(vals.p, hv, ll, hipMemcpyHostToDevice, st), "memcpy") ||
+	    !hip_ok(hipMemcpyAsync((char *) vals.p + ll, hv2, hl, hipMemcpyHostToDevice, st), "memcpy"))
+		return nullptr;
+	StrSel a{};
+	a.offs = b->theap;
+	a.w = b->twidth;
+	a.vh = (const char *) b->tvheap;
+	a.hseq = b->hseqbase;
+	a.tl = (const uint8_t *) vals.p;
+	a.th = (const uint8_t *) vals.p + ll;
+	a.li = li;
+	a.hi = hi;
+	a.equi = equi;
+	a.anti = anti;
+	a.nil_matches = nil_matches;
+	a.lval = lval;
+	a.hval = hval;
+	a.all_but_nil = all_but_nil;
+	hipLaunchKernelGGL(k_sel_str, dim3(grid_for(ci.n, 1024, 16384)), dim3(256), 0, st, a, ci.dense, ci.seq, ci.oids,
+			   ci.n, ci.first, flags.as<int8_t>());
+	return compact_flags(flags.as<int8_t>(), m, ci.first);
+}
+
+}  // namespace
+
 extern "C" {
 
 mgdk_bat *
@@ -1137,6 +1317,8 @@ mgdk_BATselect(mgdk_bat *b, mgdk_bat *s, const void *tl, const void *th, bool li
 		return select_typed<float>(b, ci, (const float *) tl, (const float *) th, li, hi, anti, nil_matches);
 	case MGDK_dbl:
 		return select_typed<double>(b, ci, (const double *) tl, (const double *) th, li, hi, anti, nil_matches);
+	case MGDK_str:
+		return select_str(b, ci, (const char *) tl, (const char *) th, li, hi, anti, nil_matches);
 	default:
 		seterr("42000!BATselect: type %s not supported on the device path", atomname(b->ttype));
 		return nullptr;
@@ -1158,6 +1340,11 @@ mgdk_BATthetaselect(mgdk_bat *b, mgdk_bat *s, const void *val, const char *op)
 	alignas(16) unsigned char nilv[16];
 	bool isnil = false;
 	switch (basetype(b->ttype)) {
+	case MGDK_str:
+		nilv[0] = 0x80;
+		nilv[1] = 0;
+		isnil = ((const unsigned char *) val)[0] == 0x80 && ((const unsigned char *) val)[1] == 0;
+		break;
 	case MGDK_bte: *(int8_t *) nilv = INT8_MIN; isnil = *(const int8_t *) val == INT8_MIN; break;
 	case MGDK_sht: *(int16_t *) nilv = INT16_MIN; isnil = *(const int16_t *) val == INT16_MIN; break;
 	case MGDK_int: *(int32_t *) nilv = INT32_MIN; isnil = *(const int32_t *) val == INT32_MIN; break;

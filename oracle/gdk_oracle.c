@@ -423,6 +423,121 @@ basetype(int t)
 	return t == ORA_date ? ORA_int : t == ORA_bit ? ORA_bte : t;
 }
 
+/* ---- str select: BATselect's generic part (gdk_select.c:1342-1520) with
+ * strCmp (nil "\200" before every string, then strcmp), then
+ * fullscan_any (:449-605; fullscan_str's string-elimination fast path,
+ * :608-760, returns the same oids by comparing heap offsets) */
+static const char ora_str_nil[2] = {'\200', 0};
+
+static const char *
+sel_str_at(const ora_bat *b, uint64_t p)
+{
+	const char *x = (const char *) b->base + p * b->width;
+	uint64_t o;
+	switch (b->width) {
+	case 1: o = *(const uint8_t *) x + 8192u; break;      /* GDK_VAROFFSET */
+	case 2: o = *(const uint16_t *) x + 8192u; break;
+	case 4: o = *(const uint32_t *) x; break;
+	default: o = *(const uint64_t *) x; break;
+	}
+	return b->vheap + o;
+}
+
+static bool
+str_isnil(const char *a)
+{
+	return (unsigned char) a[0] == 0x80 && a[1] == 0;
+}
+
+static int
+str_cmp(const char *a, const char *b)
+{
+	bool an = str_isnil(a), bn = str_isnil(b);
+	if (an || bn)
+		return an ? -!bn : 1;
+	int c = strcmp(a, b);
+	return (c > 0) - (c < 0);
+}
+
+static ora_bat *
+select_str(const ora_bat *b, const ora_ci *ci, const char *tl, const char *th, bool li, bool hi, bool anti,
+	   bool nil_matches)
+{
+	const char *nil = ora_str_nil;
+	bool lnil = str_cmp(tl, nil) == 0;
+	bool lval = !lnil || th == NULL;
+	bool equi = th == NULL || (lval && str_cmp(tl, th) == 0);
+	bool hval;
+	if (lnil && nil_matches && (th == NULL || str_cmp(th, nil) == 0)) {
+		equi = true;
+		lval = true;
+	}
+	if (equi) {
+		if (th == NULL)
+			hi = li;
+		th = tl;
+		hval = true;
+		if (!anti && (!li || !hi))
+			return ora_dense(0, 0, 0);
+	} else {
+		nil_matches = false;
+		hval = str_cmp(th, nil) != 0;
+	}
+	bool all_but_nil = false;
+	if (anti) {
+		if (lval != hval) {
+			const char *tv = tl;
+			bool ti = li;
+			li = !hi;
+			hi = !ti;
+			tl = th;
+			th = tv;
+			ti = lval;
+			lval = hval;
+			hval = ti;
+			lnil = str_cmp(tl, nil) == 0;
+			anti = false;
+		} else if (!lval && !hval) {
+			return ora_dense(0, 0, 0);
+		} else if ((equi && (lnil || !(li && hi))) || str_cmp(tl, th) > 0) {
+			if (equi && !lnil && nil_matches && !(li && hi))
+				return ci_slice(ci);
+			all_but_nil = true;
+		} else {
+			equi = false;
+		}
+	}
+	if (!all_but_nil && hval && (equi ? !li || !hi : str_cmp(tl, th) > 0))
+		return ora_dense(0, 0, 0);
+	ora_bat *bn = ora_new(ORA_oid, ci->n, 0);
+	if (bn == NULL)
+		return NULL;
+	ora_oid *dst = bn->base;
+	uint64_t cnt = 0;
+	for (uint64_t i = 0; i < ci->n; i++) {
+		const ora_oid o = ci_get(ci, i);
+		const char *v = sel_str_at(b, o - b->hseqbase);
+		const bool isnil = str_isnil(v);
+		bool ok;
+		int c;
+		if (all_but_nil)
+			ok = !isnil;
+		else if (equi)
+			ok = str_cmp(tl, v) == 0;
+		else if (anti)
+			ok = (nil_matches && isnil) ||
+			     (!isnil && ((lval && ((c = str_cmp(tl, v)) > 0 || (!li && c == 0))) ||
+					 (hval && ((c = str_cmp(th, v)) < 0 || (!hi && c == 0)))));
+		else
+			ok = !isnil && (!lval || (c = str_cmp(tl, v)) < 0 || (li && c == 0)) &&
+			     (!hval || (c = str_cmp(th, v)) > 0 || (hi && c == 0));
+		if (ok)
+			dst[cnt++] = o;
+	}
+	bn->count = cnt;
+	return ora_virtualize(bn);
+}
+
 ora_bat *
 ora_select(const ora_bat *b, const ora_bat *s, const void *tl, const void *th,
 	   bool li, bool hi, bool anti, bool nil_matches)
@@ -440,6 +555,8 @@ ora_select(const ora_bat *b, const ora_bat *s, const void *tl, const void *th,
 		return NULL;
 	if (ci.n == 0)
 		return ora_dense(0, 0, 0);
+	if (b->type == ORA_str)
+		return select_str(b, &ci, tl, th, li, hi, anti, nil_matches);
 
 	int t = basetype(b->type);
 	if (b->type == ORA_void) {
@@ -538,7 +655,7 @@ ora_bat *
 ora_thetaselect(const ora_bat *b, const ora_bat *s, const void *val, const char *op)
 {
 	int t = b->type == ORA_void ? ORA_oid : basetype(b->type);
-	const void *nil = nilptr(t);
+	const void *nil = b->type == ORA_str ? (const void *) ora_str_nil : nilptr(t);
 	if (val == NULL || op == NULL) {
 		ora_seterr("thetaselect: NULL argument");
 		return NULL;
@@ -547,7 +664,7 @@ ora_thetaselect(const ora_bat *b, const ora_bat *s, const void *val, const char 
 		return ora_select(b, s, val, NULL, true, true, false, true);
 	if (strcmp(op, "ne") == 0)
 		return ora_select(b, s, val, NULL, true, true, true, true);
-	if (cmp_val(t, val, nil) == 0)
+	if (b->type == ORA_str ? str_isnil(val) : cmp_val(t, val, nil) == 0)
 		return ora_dense(0, 0, 0);
 	if (op[0] == '=' && ((op[1] == '=' && op[2] == 0) || op[1] == 0))
 		return ora_select(b, s, val, NULL, true, true, false, false);

@@ -62,10 +62,29 @@ ci_get(const ora_ci *ci, uint64_t i)
 /* value of position p sign-extended to 64 bits: every join type compares
  * as a signed integer with its nil (the type minimum) smallest; oid
  * compares like lng (its storage type, gdk/gdk_atoms.c:1720-1737) */
+/* a flt / dbl value as an int64 that compares as dbl_cmp does (nil = NaN
+ * below everything, -0.0 == +0.0): the bits of a non-negative double as
+ * they are, a negative one's low 63 bits flipped (a flt widens exactly to
+ * dbl); equal images <=> equal values, so the hash path's buckets
+ * (dblHash hashes -0.0 as 0, gdk_atoms.c:138-145) agree too */
+static int64_t
+fimage(double x)
+{
+	if (isnan(x))
+		return INT64_MIN;
+	if (x == 0)
+		return 0;
+	int64_t s;
+	memcpy(&s, &x, 8);
+	return s < 0 ? s ^ INT64_MAX : s;
+}
+
 static int64_t
 jv(const ora_bat *b, uint64_t p)
 {
 	switch (b->type) {
+	case ORA_flt: return fimage(((const float *) b->base)[p]);
+	case ORA_dbl: return fimage(((const double *) b->base)[p]);
 	case ORA_void:
 		return b->tseqbase == ORA_OID_NIL ? INT64_MIN : (int64_t) (b->tseqbase + p);
 	case ORA_bte: case ORA_bit: return ((const int8_t *) b->base)[p];
@@ -92,6 +111,7 @@ join_type_ok(int t)
 	switch (t) {
 	case ORA_void: case ORA_bte: case ORA_sht: case ORA_int: case ORA_date:
 	case ORA_lng: case ORA_oid: case ORA_daytime: case ORA_timestamp:
+	case ORA_flt: case ORA_dbl:
 		return true;
 	}
 	return false;
@@ -291,12 +311,17 @@ selectjoin(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r, const ora_ci *l
 			((int64_t *) tmp->base)[p] = jv(r, p);
 		rr = tmp;
 	}
-	union { int8_t b; int16_t s; int32_t i; int64_t l; } val;
-	switch (rr->width) {
-	case 1: val.b = (int8_t) v; break;
-	case 2: val.s = (int16_t) v; break;
-	case 4: val.i = (int32_t) v; break;
-	default: val.l = v; break;
+	union { int8_t b; int16_t s; int32_t i; int64_t l; float f; double d; } val;
+	if (l->type == ORA_flt || l->type == ORA_dbl) {
+		/* the point select takes the value itself */
+		memcpy(&val, (const char *) l->base + (o - l->hseqbase) * l->width, l->width);
+	} else {
+		switch (rr->width) {
+		case 1: val.b = (int8_t) v; break;
+		case 2: val.s = (int16_t) v; break;
+		case 4: val.i = (int32_t) v; break;
+		default: val.l = v; break;
+		}
 	}
 	ora_bat *bn = ora_select(rr, sr, &val, NULL, true, true, false, false);
 	ora_free(tmp);

@@ -248,6 +248,11 @@ class Bat:
 def _valptr(tp, v, keep):
     if v is None:
         return None
+    if tp == TYPE_str:
+        # a C string (bytes or str); b"\x80" is str nil
+        buf = C.create_string_buffer(v if isinstance(v, bytes) else v.encode())
+        keep.append(buf)
+        return C.cast(buf, C.c_void_p)
     if tp == TYPE_hge:
         buf = (C.c_uint64 * 2)(*int_to_hge_words(v))
     elif tp == TYPE_void:

@@ -190,3 +190,53 @@ def test_gpu_ordered_fp_hge(gdk, tp, shape):
                                revsorted=False, key=False)
     want = _ordered_model(mv, isnil)
     assert (gdk.BATordered(b), gdk.BATordered_rev(b)) == want
+
+
+def _fl_cases():
+    r = np.random.default_rng(77)
+    out = []
+    for dt in (np.float32, np.float64):
+        lv = (r.integers(-50, 50, 3000) / 4).astype(dt)
+        rv = (r.integers(-50, 50, 700) / 4).astype(dt)
+        lv[::37] = np.nan
+        rv[::41] = np.nan
+        lv[5], rv[9] = -0.0, 0.0
+        lv[6], rv[10] = 0.0, -0.0
+        out.append((dt, lv, rv, "shuffled"))
+        out.append((dt, np.sort(lv), np.sort(rv), "sorted"))
+        uq = np.unique(rv[~np.isnan(rv)])
+        out.append((dt, lv, r.permutation(uq).astype(dt), "unique_build"))
+    return out
+
+
+@pytest.mark.parametrize("case", range(6))
+@pytest.mark.parametrize("nil_matches", [False, True])
+def test_oracle_float_join_pairs(ora, case, nil_matches):
+    """Float keys join by dbl_cmp equality (-0.0 == +0.0, NaN nil matches
+    only with nil_matches): the oracle's pairs equal a brute-force model."""
+    dt, lv, rv, _ = _fl_cases()[case]
+    tp = ora.TYPE_flt if dt == np.float32 else ora.TYPE_dbl
+    a, b = ora.BATjoin(ora.Bat.from_array(tp, lv), ora.Bat.from_array(tp, rv), nil_matches=nil_matches)
+    got = sorted(zip(np.asarray(a.values()).tolist(), np.asarray(b.values()).tolist()))
+    want = sorted((i, j) for i, x in enumerate(lv) for j, y in enumerate(rv)
+                  if (x == y) or (nil_matches and np.isnan(x) and np.isnan(y)))
+    assert got == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(6))
+@pytest.mark.parametrize("nil_matches", [False, True])
+def test_gpu_float_join(gdk, ora, case, nil_matches):
+    """BATjoin on flt / dbl keys: the device (integer images that keep
+    equality and order) gives the oracle's pairs in the oracle's order, and
+    both cache the same order properties."""
+    dt, lv, rv, _ = _fl_cases()[case]
+    tg = gdk.TYPE_flt if dt == np.float32 else gdk.TYPE_dbl
+    to = ora.TYPE_flt if dt == np.float32 else ora.TYPE_dbl
+    L = gdk.BAT.from_numpy(tg, lv, hseqbase=3, sorted_=False, revsorted=False, key=False)
+    R = gdk.BAT.from_numpy(tg, rv, hseqbase=5, sorted_=False, revsorted=False, key=False)
+    a, b = gdk.BATjoin(L, R, nil_matches=nil_matches)
+    oa, ob = ora.BATjoin(ora.Bat.from_array(to, lv, hseqbase=3), ora.Bat.from_array(to, rv, hseqbase=5),
+                         nil_matches=nil_matches)
+    assert np.array_equal(a.to_numpy(), oa.values())
+    assert np.array_equal(b.to_numpy(), ob.values())
