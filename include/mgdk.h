@@ -323,6 +323,11 @@ int mgdk_GDKanalyticalcount(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, 
  * frame bounds.  ntile: exactly one of n (per-row tile counts of type tpe)
  * and ntile (one value of tpe); nth_value: t (lng per row) or *pnth; lag /
  * lead: BUN_NONE (INT64_MAX) gives all nils. */
+/* gdk_analytic_bounds.c:95 GDKanalyticaldiff (gdk_analytic.h:21): r (a
+ * caller-allocated bit BAT) marks the rows whose value differs from the row
+ * before (the partition / peer starts of a sorted column), else p[i] /
+ * *npbit / 0; fixed-width types and str */
+int mgdk_GDKanalyticaldiff(mgdk_bat *r, mgdk_bat *b, mgdk_bat *p, const int8_t *npbit, int tpe);
 int mgdk_GDKanalyticalntile(mgdk_bat *r, mgdk_bat *b, mgdk_bat *p, mgdk_bat *n, int tpe, const void *ntile);
 int mgdk_GDKanalyticalfirst(mgdk_bat *r, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e, int tpe);
 int mgdk_GDKanalyticallast(mgdk_bat *r, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e, int tpe);

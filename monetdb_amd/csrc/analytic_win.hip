@@ -314,6 +314,67 @@ k_win_copy(const T *b, BUN n, T *r, uint32_t *flags)
 		publish_or(&flags[0], hasnil);
 }
 
+// ---- GDKanalyticaldiff (gdk_analytic_bounds.c:95) -------------------------
+// The reference compares each value with the last value that differed;
+// equality is transitive here (-0.0 == +0.0, two NaNs the same when b has
+// nils), so that value always equals the row before: one compare per row.
+template <typename T>
+__global__ __launch_bounds__(256) void
+k_win_diff(const T *b, BUN n, const int8_t *np, int8_t npb, bool nanaware, int8_t *r)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		bool d = false;
+		if (i > 0) {
+			const T x = b[i - 1], y = b[i];
+			d = x != y;
+			if constexpr (std::is_floating_point<T>::value)
+				d = d && (!nanaware || x == x || y == y);
+		}
+		r[i] = d ? 1 : np ? np[i] : npb;
+	}
+}
+
+__device__ __forceinline__ const uint8_t *
+wstr_at(const void *offs, int w, const char *vh, BUN p)
+{
+	size_t o;
+	switch (w) {
+	case 1: o = (size_t) ((const uint8_t *) offs)[p] + 8192; break;     // GDK_VAROFFSET
+	case 2: o = (size_t) ((const uint16_t *) offs)[p] + 8192; break;
+	case 4: o = (size_t) ((const uint32_t *) offs)[p]; break;
+	default: o = (size_t) ((const uint64_t *) offs)[p]; break;
+	}
+	return (const uint8_t *) vh + o;
+}
+
+// strCmp != 0: nil ("\200") equals only nil, otherwise bytewise
+__global__ __launch_bounds__(256) void
+k_win_diff_str(const void *offs, int w, const char *vh, BUN n, const int8_t *np, int8_t npb, int8_t *r)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		bool d = false;
+		if (i > 0) {
+			const uint8_t *a = wstr_at(offs, w, vh, i - 1), *c = wstr_at(offs, w, vh, i);
+			if (a != c) {
+				const bool an = a[0] == 0x80 && a[1] == 0, cn = c[0] == 0x80 && c[1] == 0;
+				if (an || cn) {
+					d = an != cn;
+				} else {
+					for (;; a++, c++) {
+						if (*a != *c) {
+							d = true;
+							break;
+						}
+						if (*a == 0)
+							break;
+					}
+				}
+			}
+		}
+		r[i] = d ? 1 : np ? np[i] : npb;
+	}
+}
+
 // ---- host side -----------------------------------------------------------
 
 // the storage class of a window function's values: 1 bte, 2 sht, 4 int,
@@ -768,4 +829,46 @@ mgdk_GDKanalyticalmax(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_b
 {
 	ProfScope prof("analyticalmax");
 	return minmax_run(true, r, p, o, b, s, e, tpe, frame_type, "GDKanalyticalmax");
+}
+
+extern "C" int
+mgdk_GDKanalyticaldiff(mgdk_bat *r, mgdk_bat *b, mgdk_bat *p, const int8_t *npbit, int tpe)
+{
+	ProfScope prof("analyticaldiff");
+	if (r == nullptr || b == nullptr) {
+		seterr("GDKanalyticaldiff: NULL argument");
+		return -1;
+	}
+	const BUN n = b->count;
+	const bool str = basetype(tpe) == MGDK_str;
+	const int cls = str ? 0 : wclass(tpe);
+	if ((!str && cls == 0) || (str && b->tvheap == nullptr) || width_of(r->ttype) != 1) {
+		seterr("42000!GDKanalyticaldiff: type %s not supported on the device path", atomname(tpe));
+		return -1;
+	}
+	if (n > 0 && (!bits_ok(p, n) || r->theap == nullptr))
+		return -1;
+	const int8_t *np = p ? (const int8_t *) p->theap : nullptr;
+	const int8_t npb = npbit ? *npbit : 0;
+	if (n > 0) {
+		const dim3 g(grid_for(n, 1024, 16384)), blk(256);
+		hipStream_t st = stream();
+		int8_t *rb = (int8_t *) r->theap;
+		if (str) {
+			hipLaunchKernelGGL(k_win_diff_str, g, blk, 0, st, b->theap, (int) b->twidth, (const char *) b->tvheap, n, np,
+					   npb, rb);
+		} else {
+			const bool nanaware = !b->tnonil;
+#define DF(T) hipLaunchKernelGGL((k_win_diff<T>), g, blk, 0, st, (const T *) b->theap, n, np, npb, nanaware, rb)
+			WDISPATCH(cls, DF)
+#undef DF
+		}
+		if (!sync())
+			return -1;
+	}
+	r->count = n;
+	r->tnonil = 1;
+	r->tnil = 0;
+	r->tsorted = r->trevsorted = r->tkey = n <= 1;
+	return 0;
 }

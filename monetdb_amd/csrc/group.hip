@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <vector>
 
+#include <type_traits>
 #include "mgdk_internal.h"
 
 using namespace mgdk;
@@ -455,6 +456,105 @@ k_gl_assign(KeySrc s, BUN n, const unsigned long long *gkey, const uint32_t *gma
 			atomicAdd(&histo[q], (unsigned long long) lh[q]);
 }
 
+// the assign pass for dense integer keys of W = 4 or 8 bytes without prior
+// groups: a lane takes V = 16 / W CONSECUTIVE rows per step (one 16-byte
+// key load; every wave instruction covers 1 KiB of keys) and stores their
+// ids as 16-byte pieces; the order flag compares each row with the one
+// before it (the lane's previous row, or the key before the lane's first)
+template <int W>
+__global__ __launch_bounds__(1024) void
+k_gl_assign_v(KeySrc s, BUN n, const unsigned long long *gkey, const uint32_t *gmap, uint32_t ngrp, oid *gid,
+	      uint8_t *img, unsigned long long *histo, uint32_t *unsorted, uint32_t *miss)
+{
+	typedef typename std::conditional<W == 4, uint32_t, uint64_t>::type K;
+	constexpr int V = 16 / W;
+	__shared__ unsigned long long lkey[GL_SLOTS];
+	__shared__ uint32_t lmap[GL_SLOTS + 1];
+	__shared__ uint32_t lh[GL_MAXG];
+	const unsigned tid = threadIdx.x;
+	for (uint32_t q = tid; q < GL_SLOTS; q += blockDim.x) {
+		lkey[q] = gkey[q];
+		lmap[q] = gmap[q];
+	}
+	if (tid == 0)
+		lmap[GL_SLOTS] = gmap[GL_SLOTS];
+	for (uint32_t q = tid; q < ngrp; q += blockDim.x)
+		lh[q] = 0;
+	__syncthreads();
+	const BUN a = (BUN) blockIdx.x * GL_TILE, e = min(n, a + GL_TILE);
+	const K *kb = (const K *) s.base + s.off;
+	uint32_t uns = 0;
+	bool mis = false;
+	typedef K kv __attribute__((ext_vector_type(V)));
+	constexpr BUN STEP = 1024 * V;
+	for (BUN r0 = a + (BUN) tid * V; r0 < e; r0 += STEP) {
+		K k[V];
+		if (r0 + V <= e) {
+			const kv x = __builtin_nontemporal_load((const kv *) (kb + r0));
+#pragma unroll
+			for (int u = 0; u < V; u++)
+				k[u] = x[u];
+		} else {
+#pragma unroll
+			for (int u = 0; u < V; u++)
+				k[u] = kb[r0 + u < e ? r0 + u : e - 1];
+		}
+		const K before = kb[r0 > 0 ? r0 - 1 : 0];
+		uint32_t g[V], gp = 0;
+#pragma unroll
+		for (int u = 0; u < V; u++) {
+			g[u] = gl_lookup(lkey, lmap, (uint64_t) k[u]);
+			if (g[u] == ~0u) {
+				mis = true;
+				g[u] = 0;
+			}
+		}
+		if (r0 > 0)
+			gp = gl_lookup(lkey, lmap, (uint64_t) before);
+		mis |= gp == ~0u && r0 > 0;
+#pragma unroll
+		for (int u = 0; u < V; u++) {
+			const BUN i = r0 + u;
+			if (i < e) {
+				atomicAdd(&lh[g[u]], 1u);
+				const uint32_t prev = u == 0 ? gp : g[u - 1];
+				if (i > 0 && prev > g[u])
+					uns = 1;
+			}
+		}
+		if (r0 + V <= e) {
+			typedef unsigned long long o2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+			for (int u = 0; u < V; u += 2)
+				__builtin_nontemporal_store((o2){g[u], g[u + 1]}, (o2 *) (gid + r0 + u));
+			if (img) {
+				if constexpr (V == 4) {
+					const uint32_t w4 = g[0] | (g[1] << 8) | (g[2] << 16) | (g[3] << 24);
+					*(uint32_t *) (img + r0) = w4;
+				} else {
+					*(uint16_t *) (img + r0) = (uint16_t) (g[0] | (g[1] << 8));
+				}
+			}
+		} else {
+#pragma unroll
+			for (int u = 0; u < V; u++)
+				if (r0 + u < e) {
+					gid[r0 + u] = g[u];
+					if (img)
+						img[r0 + u] = (uint8_t) g[u];
+				}
+		}
+	}
+	if (__any(uns) && __lane_id() == 0)
+		publish_or(unsorted, 1u);
+	if (__any(mis) && __lane_id() == 0)
+		publish_or(miss, 1u);
+	__syncthreads();
+	for (uint32_t q = tid; q < ngrp; q += blockDim.x)
+		if (lh[q])
+			atomicAdd(&histo[q], (unsigned long long) lh[q]);
+}
+
 // returns 1 when the path does not apply (too many groups).  The first
 // pass reads only a prefix of GL_PREFIX tiles first: the groups it finds
 // are numbered, and they are ALL the groups unless the assign pass meets a
@@ -533,8 +633,20 @@ group_lds(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mg
 			unfix3();
 			return -1;
 		}
-		GL_LAUNCH(k_gl_assign, dim3(tiles), dim3(1024), 0, st, ks, n, gkey.as<unsigned long long>(),
-			  gmap.as<uint32_t>(), ngrp, (oid *) gn->theap, img, (unsigned long long *) hn->theap, &m[2], &m[3]);
+		// the vector form needs 16-byte aligned keys and ids
+		const bool vec = fg == 0 && (fw == 4 || fw == 8) && (((uintptr_t) ks.base + ks.off * fw) & 15) == 0 &&
+				 ((uintptr_t) gn->theap & 15) == 0 && (!img || ((uintptr_t) img & 3) == 0);
+		if (vec && fw == 4)
+			hipLaunchKernelGGL(k_gl_assign_v<4>, dim3(tiles), dim3(1024), 0, st, ks, n, gkey.as<unsigned long long>(),
+					   gmap.as<uint32_t>(), ngrp, (oid *) gn->theap, img, (unsigned long long *) hn->theap,
+					   &m[2], &m[3]);
+		else if (vec)
+			hipLaunchKernelGGL(k_gl_assign_v<8>, dim3(tiles), dim3(1024), 0, st, ks, n, gkey.as<unsigned long long>(),
+					   gmap.as<uint32_t>(), ngrp, (oid *) gn->theap, img, (unsigned long long *) hn->theap,
+					   &m[2], &m[3]);
+		else
+			GL_LAUNCH(k_gl_assign, dim3(tiles), dim3(1024), 0, st, ks, n, gkey.as<unsigned long long>(),
+				  gmap.as<uint32_t>(), ngrp, (oid *) gn->theap, img, (unsigned long long *) hn->theap, &m[2], &m[3]);
 		oid fl[2] = {0, 0};
 		if (!hip_ok(hipMemcpyAsync(h, m, 16, hipMemcpyDeviceToHost, st), "memcpy") ||
 		    (ngrp > 0 && (!hip_ok(hipMemcpyAsync(&fl[0], ext.p, 8, hipMemcpyDeviceToHost, st), "memcpy") ||

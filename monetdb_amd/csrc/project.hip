@@ -21,7 +21,7 @@ __global__ __launch_bounds__(256) void
 k_project(const oid *__restrict__ l, BUN n, const T *__restrict__ r, oid rseq, BUN rcnt, T nilv,
 	  T *__restrict__ out, uint32_t *__restrict__ flags)
 {
-	constexpr int U = 8;
+	constexpr int U = 16;
 	constexpr BUN CH = 64 * U;
 	uint32_t bad = 0, nil = 0;
 	const unsigned lane = __lane_id();

@@ -161,6 +161,7 @@ _SIGS = {
     "mgdk_GDKanalyticalcount": (C.c_int, [C.c_void_p] * 6 + [C.c_bool, C.c_int, C.c_int]),
     "mgdk_GDKanalyticalavg": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_int]),
     "mgdk_GDKanalyticalntile": (C.c_int, [C.c_void_p] * 4 + [C.c_int, C.c_void_p]),
+    "mgdk_GDKanalyticaldiff": (C.c_int, [C.c_void_p] * 4 + [C.c_int]),
     "mgdk_GDKanalyticalfirst": (C.c_int, [C.c_void_p] * 4 + [C.c_int]),
     "mgdk_GDKanalyticallast": (C.c_int, [C.c_void_p] * 4 + [C.c_int]),
     "mgdk_GDKanalyticalnthvalue": (C.c_int, [C.c_void_p] * 6 + [C.c_int]),
@@ -704,6 +705,16 @@ BUN_NONE = (1 << 63) - 1
 
 def _wres(tp, n):
     return BAT(lib().mgdk_COLnew(0, tp, max(1, n)))
+
+
+def GDKanalyticaldiff(b, p=None, npbit=None):
+    """gdk_analytic_bounds.c:95: bit column of the rows whose value differs
+    from the row before (else p[i] / npbit / 0)."""
+    r = _wres(TYPE_bit, b.count())
+    ref = C.c_int8(npbit) if npbit is not None else None
+    _chk(lib().mgdk_GDKanalyticaldiff(r.ptr, b.ptr, _p(p), C.cast(C.pointer(ref), C.c_void_p) if ref is not None
+                                      else None, b.ttype))
+    return r
 
 
 def GDKanalyticalntile(b, p, n=None, ntile=None, tpe=None):

@@ -189,6 +189,9 @@ int ora_analyticalavginteger(ora_bat *r, const ora_bat *p, const ora_bat *o, con
 /* gdk_analytic_func.c :124 ntile, :230 first, :312 last, :421 nth_value,
  * :671 lag, :823 lead, :1264 min / max (gdk_oracle_window.c); r is a
  * caller-allocated BAT of count(b) slots of type tpe */
+/* gdk_analytic_bounds.c:95 GDKanalyticaldiff: r (bit) marks the rows whose
+ * value differs from the previous distinct one, or np[i] / *npbit */
+int ora_analyticaldiff(ora_bat *r, const ora_bat *b, const ora_bat *p, const int8_t *npbit, int tpe);
 int ora_analyticalntile(ora_bat *r, const ora_bat *b, const ora_bat *p, const ora_bat *n, int tpe,
 			const void *ntile);
 int ora_analyticalfirst(ora_bat *r, const ora_bat *b, const ora_bat *s, const ora_bat *e, int tpe);

@@ -2,7 +2,9 @@
  * gdk_oracle_window.c -- window functions beyond the frame aggregates
  * (TEST INFRASTRUCTURE ONLY; see gdk_oracle.h).
  *
- * Restates gdk/gdk_analytic_func.c:
+ * Restates gdk/gdk_analytic_bounds.c:95 GDKanalyticaldiff (ANALYTICAL_DIFF_IMP
+ * :19-51, the NaN-aware ANALYTICAL_DIFF_FLOAT_IMP :54-92, atomcmp for str
+ * :135-170) and gdk/gdk_analytic_func.c:
  *   GDKanalyticalntile    :124 (NTILE_CALC :64-90, partition walk :92-112)
  *   GDKanalyticalfirst    :230 (ANALYTICAL_FIRST_FIXED :215-227)
  *   GDKanalyticallast     :312 (ANALYTICAL_LAST_FIXED :297-309)
@@ -581,4 +583,66 @@ ora_analyticalmax(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_bat 
 		  const ora_bat *e, int tpe, int frame_type)
 {
 	return minmax(r, p, o, b, s, e, tpe, frame_type, true);
+}
+
+/* ---- diff ---------------------------------------------------------------- */
+
+static const char *
+wstr_at(const ora_bat *b, uint64_t p)
+{
+	const char *x = (const char *) b->base + p * b->width;
+	uint64_t o;
+	switch (b->width) {
+	case 1: o = *(const uint8_t *) x + 8192u; break;
+	case 2: o = *(const uint16_t *) x + 8192u; break;
+	case 4: o = *(const uint32_t *) x; break;
+	default: o = *(const uint64_t *) x; break;
+	}
+	return b->vheap + o;
+}
+
+static int
+wstr_cmp(const char *a, const char *b)
+{
+	bool an = (unsigned char) a[0] == 0x80 && a[1] == 0, bn = (unsigned char) b[0] == 0x80 && b[1] == 0;
+	if (an || bn)
+		return an ? -!bn : 1;
+	return strcmp(a, b);
+}
+
+/* r[i] = the value differs from the last value that differed (TRUE), else
+ * np[i] / *npbit / FALSE; floats: two NaNs are the same (when b has nils) */
+int
+ora_analyticaldiff(ora_bat *r, const ora_bat *b, const ora_bat *p, const int8_t *npbit, int tpe)
+{
+	const uint64_t cnt = b->count;
+	const int8_t *np = p ? p->base : NULL;
+	int8_t *rb = r->base;
+	const int8_t npb = npbit ? *npbit : 0;
+	const int t = tpe == ORA_str ? ORA_str : wbase(tpe);
+	uint64_t prev = 0;            /* position of the last differing value */
+	for (uint64_t i = 0; i < cnt; i++) {
+		bool diff;
+		if (t == ORA_str) {
+			diff = wstr_cmp(wstr_at(b, prev), wstr_at(b, i)) != 0;
+		} else if (t == ORA_flt || t == ORA_dbl) {
+			double x = t == ORA_flt ? ((const float *) b->base)[prev] : ((const double *) b->base)[prev];
+			double y = t == ORA_flt ? ((const float *) b->base)[i] : ((const double *) b->base)[i];
+			diff = x != y && (!b->nonil ? (x == x || y == y) : true);
+		} else {
+			const int w = wwidth(t);
+			diff = memcmp((const char *) b->base + prev * w, (const char *) b->base + i * w, w) != 0;
+		}
+		if (diff) {
+			rb[i] = 1;
+			prev = i;
+		} else {
+			rb[i] = np ? np[i] : npbit ? npb : 0;
+		}
+	}
+	r->count = cnt;
+	r->nonil = 1;
+	r->nil = 0;
+	r->sorted = r->revsorted = r->key = cnt <= 1;
+	return 0;
 }

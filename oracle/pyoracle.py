@@ -122,6 +122,7 @@ def lib():
         L.ora_analyticallag.argtypes = [P, P, P, C.c_uint64, C.c_void_p, C.c_int]
         L.ora_analyticallead.argtypes = [P, P, P, C.c_uint64, C.c_void_p, C.c_int]
         L.ora_analyticalmin.argtypes = [P, P, P, P, P, P, C.c_int, C.c_int]
+        L.ora_analyticaldiff.argtypes = [P, P, P, C.c_void_p, C.c_int]
         L.ora_analyticalmax.argtypes = [P, P, P, P, P, P, C.c_int, C.c_int]
         L.ora_tpch_lineitem.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64] + [C.c_void_p] * 7
         L.ora_mkdate.restype = C.c_int32
@@ -629,3 +630,9 @@ def analyticalmin(b, p, o, s, e, frame_type):
 def analyticalmax(b, p, o, s, e, frame_type):
     return _wrun(b.s.type, b.count(), lib().ora_analyticalmax, _pp(p), _pp(o), b.ptr, _pp(s), _pp(e),
                  b.s.type, frame_type)
+
+
+def analyticaldiff(b, p=None, npbit=None):
+    ref = C.c_int8(npbit) if npbit is not None else None
+    return _wrun(TYPE_bit, b.count(), lib().ora_analyticaldiff, b.ptr, _pp(p),
+                 C.cast(C.pointer(ref), C.c_void_p) if ref is not None else None, b.s.type)

@@ -222,3 +222,43 @@ def test_oracle_window_small_cases(ora):
     assert list(ora.analyticalnthvalue(b, s, e, nth=2).values()) == [np.iinfo(np.int32).min, 3, 7,
                                                                    np.iinfo(np.int32).min, 9, 2]
     assert list(ora.analyticalmin(b, p, None, s, e, 0).values()) == [5, 3, 3, 1, 1, 2]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tname,dt", TYPES + [("str", None)])
+@pytest.mark.parametrize("mode", ["none", "p", "npbit"])
+def test_diff(gdk, ora, tname, dt, mode):
+    """GDKanalyticaldiff over sorted runs with nils (NaN runs for floats,
+    -0.0 next to +0.0), with a partition column, a constant npbit or neither."""
+    r = rng(len(tname) * 5 + len(mode))
+    n = 30_007
+    if tname == "str":
+        from strheap import sample
+        t, heap, _ = sample(r, n, 4)
+        t = np.sort(t)
+        b = gdk.BAT.from_numpy(gdk.TYPE_str, t, vheap=heap, sorted_=False, revsorted=False, key=False, nonil=False)
+        ob = ora.Bat.from_array(ora.TYPE_str, t, vheap=heap)
+    else:
+        v = _vals(r, tname, dt, n, nils=0.0)
+        if tname == "hge":
+            v = sorted(v)
+            v[:50] = [-(1 << 127)] * 50
+        else:
+            v = np.sort(v)
+            if tname in ("flt", "dbl"):
+                v[:50] = np.nan
+                v[100:103] = [-0.0, 0.0, -0.0]
+            else:
+                v[:50] = np.iinfo(dt).min
+        b, ob = _pair(gdk, ora, tname, v)
+        b.s.tnonil = 0
+        ob.s.nonil = 0
+    pf, _ = _layout(r, n, "small")
+    p, op = _bits(gdk, ora, pf)
+    if mode == "p":
+        got, want = gdk.GDKanalyticaldiff(b, p=p), ora.analyticaldiff(ob, p=op)
+    elif mode == "npbit":
+        got, want = gdk.GDKanalyticaldiff(b, npbit=1), ora.analyticaldiff(ob, npbit=1)
+    else:
+        got, want = gdk.GDKanalyticaldiff(b), ora.analyticaldiff(ob)
+    assert np.array_equal(got.to_numpy(), np.asarray(want.values()))
