@@ -1148,6 +1148,189 @@ float_image(const mgdk_bat *b)
 	return m;
 }
 
+// str join keys: BATjoin compares strings with strCmp (nil first, then
+// strcmp's unsigned bytes) and hashes them with strHash; its choices, scans
+// and result order only see that order and equality, so a str pair joins
+// exactly as the pair of lng columns holding each string's rank among the
+// distinct strings of both sides (nil -> lng nil).  The ranks: BATgroup of
+// each side (never merges different strings), the groups' representative
+// strings of both sides as one str column over the two heaps laid end to
+// end (8-byte absolute offsets), its chunked BATsort's group ids.
+__device__ __forceinline__ uint64_t
+jstr_off(const void *offs, int w, BUN p)
+{
+	switch (w) {
+	case 1: return (uint64_t) ((const uint8_t *) offs)[p] + 8192;      // GDK_VAROFFSET
+	case 2: return (uint64_t) ((const uint16_t *) offs)[p] + 8192;
+	case 4: return ((const uint32_t *) offs)[p];
+	default: return ((const uint64_t *) offs)[p];
+	}
+}
+
+__device__ __forceinline__ oid
+oid_at(const oid *p, oid seq, BUN i)
+{
+	return p ? p[i] : seq + i;
+}
+
+__global__ __launch_bounds__(256) void
+k_str_rep_offs(const oid *ext, oid eseq, BUN ne, oid hseq, const void *offs, int w, uint64_t add, uint64_t *out)
+{
+	for (BUN j = (BUN) blockIdx.x * blockDim.x + threadIdx.x; j < ne; j += (BUN) gridDim.x * blockDim.x)
+		out[j] = jstr_off(offs, w, oid_at(ext, eseq, j) - hseq) + add;
+}
+
+__global__ __launch_bounds__(256) void
+k_str_ranks(const oid *ord, oid oseq, const oid *grp, oid gseq, BUN n, const uint64_t *coffs, const char *vh,
+	    int64_t *rank)
+{
+	for (BUN j = (BUN) blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (BUN) gridDim.x * blockDim.x) {
+		const BUN p = oid_at(ord, oseq, j);
+		const uint8_t *s = (const uint8_t *) vh + coffs[p];
+		rank[p] = s[0] == 0x80 && s[1] == 0 ? INT64_MIN : (int64_t) oid_at(grp, gseq, j);
+	}
+}
+
+__global__ __launch_bounds__(256) void
+k_str_img(const oid *g, oid gseq, BUN n, const int64_t *rank, BUN base, int64_t *out)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
+		out[i] = rank[base + oid_at(g, gseq, i)];
+}
+
+const oid *
+oid_col(const mgdk_bat *b, oid *seq)
+{
+	if (b->ttype == MGDK_void) {
+		*seq = b->tseqbase;
+		return nullptr;
+	}
+	*seq = 0;
+	return (const oid *) b->theap;
+}
+
+mgdk_bat *
+str_img(const mgdk_bat *b, const mgdk_bat *g, const int64_t *rank, BUN base)
+{
+	mgdk_bat *m = newbat(b->hseqbase, MGDK_lng, b->count);
+	if (m == nullptr)
+		return nullptr;
+	oid gs;
+	const oid *gp = oid_col(g, &gs);
+	if (b->count)
+		hipLaunchKernelGGL(k_str_img, dim3(grid_for(b->count, 1024, 16384)), dim3(256), 0, stream(), gp, gs,
+				   b->count, rank, base, (int64_t *) m->theap);
+	m->count = b->count;
+	m->tsorted = b->tsorted;
+	m->trevsorted = b->trevsorted;
+	m->tkey = b->tkey;
+	m->tnonil = b->tnonil;
+	m->tnil = b->tnil;
+	m->tnosorted = b->tnosorted;
+	m->tnorevsorted = b->tnorevsorted;
+	m->tseqbase = MGDK_OID_NIL;
+	return m;
+}
+
+int
+str_images(mgdk_bat *l, mgdk_bat *r, mgdk_bat **lip, mgdk_bat **rip)
+{
+	*lip = *rip = nullptr;
+	mgdk_bat *gl = nullptr, *el = nullptr, *gr = nullptr, *er = nullptr, *C = nullptr, *ord = nullptr,
+		 *grp = nullptr, *rk = nullptr;
+	int rc = -1;
+	hipStream_t st = stream();
+	if (mgdk_BATgroup(&gl, &el, nullptr, l, nullptr, nullptr, nullptr, nullptr) != 0 ||
+	    mgdk_BATgroup(&gr, &er, nullptr, r, nullptr, nullptr, nullptr, nullptr) != 0)
+		goto out;
+	{
+		const BUN nl = el->count, nr = er->count, A = nl + nr;
+		const size_t lsz = l->tvheapsize, rsz = r->tvheapsize;
+		C = newbat(0, MGDK_lng, A);
+		rk = newbat(0, MGDK_lng, A);
+		Heap *vh = heap_new(lsz + rsz + 8);
+		if (C == nullptr || rk == nullptr || vh == nullptr) {
+			heap_decref(vh);
+			goto out;
+		}
+		Priv *p = (Priv *) C->priv;
+		heap_decref(p->tvheap);
+		p->tvheap = vh;
+		C->ttype = MGDK_str;
+		C->twidth = 8;
+		C->tvheap = vh->base;
+		C->tvheapsize = lsz + rsz;
+		if ((lsz && !hip_ok(hipMemcpyAsync(vh->base, l->tvheap, lsz, hipMemcpyDeviceToDevice, st), "memcpy")) ||
+		    (rsz && !hip_ok(hipMemcpyAsync((char *) vh->base + lsz, r->tvheap, rsz, hipMemcpyDeviceToDevice, st),
+				    "memcpy")))
+			goto out;
+		oid es;
+		const oid *ep = oid_col(el, &es);
+		if (nl)
+			hipLaunchKernelGGL(k_str_rep_offs, dim3(grid_for(nl, 1024, 16384)), dim3(256), 0, st, ep, es, nl,
+					   l->hseqbase, (const void *) l->theap, (int) l->twidth, (uint64_t) 0,
+					   (uint64_t *) C->theap);
+		ep = oid_col(er, &es);
+		if (nr)
+			hipLaunchKernelGGL(k_str_rep_offs, dim3(grid_for(nr, 1024, 16384)), dim3(256), 0, st, ep, es, nr,
+					   r->hseqbase, (const void *) r->theap, (int) r->twidth, (uint64_t) lsz,
+					   (uint64_t *) C->theap + nl);
+		C->count = A;
+		C->tsorted = C->trevsorted = C->tkey = A <= 1;
+		C->tnosorted = C->tnorevsorted = 0;
+		C->tnonil = l->tnonil && r->tnonil;
+		C->tnil = 0;
+		if (A) {
+			if (mgdk_BATsort(nullptr, &ord, &grp, C, nullptr, nullptr, false, false, false) != 0)
+				goto out;
+			oid os, gs;
+			const oid *op = oid_col(ord, &os), *gp = oid_col(grp, &gs);
+			hipLaunchKernelGGL(k_str_ranks, dim3(grid_for(A, 1024, 16384)), dim3(256), 0, st, op, os, gp, gs, A,
+					   (const uint64_t *) C->theap, (const char *) C->tvheap, (int64_t *) rk->theap);
+		}
+		*lip = str_img(l, gl, (const int64_t *) rk->theap, 0);
+		*rip = *lip ? str_img(r, gr, (const int64_t *) rk->theap, nl) : nullptr;
+		if (*rip == nullptr || !sync())
+			goto out;
+		rc = 0;
+	}
+out:
+	if (rc != 0) {
+		mgdk_BBPunfix(*lip);
+		mgdk_BBPunfix(*rip);
+		*lip = *rip = nullptr;
+	}
+	mgdk_BBPunfix(gl);
+	mgdk_BBPunfix(el);
+	mgdk_BBPunfix(gr);
+	mgdk_BBPunfix(er);
+	mgdk_BBPunfix(C);
+	mgdk_BBPunfix(ord);
+	mgdk_BBPunfix(grp);
+	mgdk_BBPunfix(rk);
+	return rc;
+}
+
+// the order the scans found on the images holds for the keys they stand for
+void
+image_flags_back(mgdk_bat *l, mgdk_bat *r, const mgdk_bat *li, const mgdk_bat *ri)
+{
+	l->tsorted |= li->tsorted;
+	l->trevsorted |= li->trevsorted;
+	l->tkey |= li->tkey;
+	r->tsorted |= ri->tsorted;
+	r->trevsorted |= ri->trevsorted;
+	r->tkey |= ri->tkey;
+	if (!l->tnosorted)
+		l->tnosorted = li->tnosorted;
+	if (!l->tnorevsorted)
+		l->tnorevsorted = li->tnorevsorted;
+	if (!r->tnosorted)
+		r->tnosorted = ri->tnosorted;
+	if (!r->tnorevsorted)
+		r->tnorevsorted = ri->tnorevsorted;
+}
+
 }  // namespace
 
 extern "C" int
@@ -1183,26 +1366,20 @@ mgdk_BATjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk_bat 
 		seterr("42000!BATjoin: inputs not compatible.");
 		return -1;
 	}
-	if (basetype(l->ttype) == MGDK_flt || basetype(l->ttype) == MGDK_dbl) {
-		mgdk_bat *li = float_image(l), *ri = li ? float_image(r) : nullptr;
+	if (basetype(l->ttype) == MGDK_flt || basetype(l->ttype) == MGDK_dbl || l->ttype == MGDK_str) {
+		mgdk_bat *li = nullptr, *ri = nullptr;
+		if (l->ttype == MGDK_str) {
+			ProfScope prof("join_str_images");
+			if (str_images(l, r, &li, &ri) != 0)
+				return -1;
+		} else {
+			li = float_image(l);
+			ri = li ? float_image(r) : nullptr;
+		}
 		int rc = -1;
 		if (li && ri) {
 			rc = mgdk_BATjoin(r1p, r2p, li, ri, sl, sr, nil_matches, estimate);
-			// the order the scans found on the images holds for the floats
-			l->tsorted |= li->tsorted;
-			l->trevsorted |= li->trevsorted;
-			l->tkey |= li->tkey;
-			r->tsorted |= ri->tsorted;
-			r->trevsorted |= ri->trevsorted;
-			r->tkey |= ri->tkey;
-			if (!l->tnosorted)
-				l->tnosorted = li->tnosorted;
-			if (!l->tnorevsorted)
-				l->tnorevsorted = li->tnorevsorted;
-			if (!r->tnosorted)
-				r->tnosorted = ri->tnosorted;
-			if (!r->tnorevsorted)
-				r->tnorevsorted = ri->tnorevsorted;
+			image_flags_back(l, r, li, ri);
 		}
 		mgdk_BBPunfix(li);
 		mgdk_BBPunfix(ri);

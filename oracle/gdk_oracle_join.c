@@ -733,6 +733,122 @@ joincost(ora_bat *r, uint64_t lcount, const ora_ci *rci, const ora_bat *sr)
 	return rcost;
 }
 
+/* ---- str keys: BATjoin compares with strCmp (nil "\200" first, then
+ * strcmp's unsigned bytes) and hashes the string (strHash); every algorithm
+ * choice, scan and result order only depends on that order and equality,
+ * so the pair of str columns joins exactly as the pair of lng columns that
+ * hold each string's rank among the distinct strings of both sides (nil ->
+ * lng nil).  The ranks come from a qsort of all strings here. */
+static const char *
+jstr_at(const ora_bat *b, uint64_t p)
+{
+	const char *x = (const char *) b->base + p * b->width;
+	uint64_t o;
+	switch (b->width) {
+	case 1: o = *(const uint8_t *) x + 8192u; break;      /* GDK_VAROFFSET */
+	case 2: o = *(const uint16_t *) x + 8192u; break;
+	case 4: o = *(const uint32_t *) x; break;
+	default: o = *(const uint64_t *) x; break;
+	}
+	return b->vheap + o;
+}
+
+static bool
+jstr_nil(const char *s)
+{
+	return (unsigned char) s[0] == 0x80 && s[1] == 0;
+}
+
+static int
+jstr_qcmp(const void *a, const void *b)
+{
+	return strcmp(*(const char *const *) a, *(const char *const *) b);
+}
+
+static ora_bat *
+jstr_image(const ora_bat *b, const char **dict, uint64_t nd)
+{
+	ora_bat *m = ora_new(ORA_lng, b->count, b->hseqbase);
+	if (m == NULL)
+		return NULL;
+	int64_t *o = m->base;
+	for (uint64_t i = 0; i < b->count; i++) {
+		const char *s = jstr_at(b, i);
+		if (jstr_nil(s)) {
+			o[i] = INT64_MIN;
+			continue;
+		}
+		uint64_t lo = 0, hi = nd;
+		while (lo < hi) {
+			uint64_t mid = (lo + hi) / 2;
+			if (strcmp(dict[mid], s) < 0)
+				lo = mid + 1;
+			else
+				hi = mid;
+		}
+		o[i] = (int64_t) lo;
+	}
+	m->sorted = b->sorted;
+	m->revsorted = b->revsorted;
+	m->key = b->key;
+	m->nonil = b->nonil;
+	m->nil = b->nil;
+	m->unique_est = b->unique_est;
+	return m;
+}
+
+static int
+str_images(const ora_bat *l, const ora_bat *r, ora_bat **lip, ora_bat **rip)
+{
+	*lip = *rip = NULL;
+	const uint64_t n = l->count + r->count;
+	const char **dict = malloc((n ? n : 1) * sizeof(char *));
+	if (dict == NULL) {
+		ora_seterr("malloc");
+		return -1;
+	}
+	uint64_t nd = 0;
+	for (int side = 0; side < 2; side++) {
+		const ora_bat *b = side ? r : l;
+		for (uint64_t i = 0; i < b->count; i++) {
+			const char *s = jstr_at(b, i);
+			if (!jstr_nil(s))
+				dict[nd++] = s;
+		}
+	}
+	qsort(dict, nd, sizeof(char *), jstr_qcmp);
+	uint64_t k = 0;
+	for (uint64_t i = 0; i < nd; i++)
+		if (k == 0 || strcmp(dict[k - 1], dict[i]) != 0)
+			dict[k++] = dict[i];
+	*lip = jstr_image(l, dict, k);
+	*rip = *lip ? jstr_image(r, dict, k) : NULL;
+	free(dict);
+	if (*rip == NULL) {
+		if (*lip)
+			ora_free(*lip);
+		*lip = NULL;
+		return -1;
+	}
+	return 0;
+}
+
+/* what the scans found on the images holds for the strings */
+static void
+str_flags_back(ora_bat *l, ora_bat *r, ora_bat *li, ora_bat *ri)
+{
+	l->sorted = li->sorted;
+	l->revsorted = li->revsorted;
+	l->key = li->key;
+	l->unique_est = li->unique_est;
+	r->sorted = ri->sorted;
+	r->revsorted = ri->revsorted;
+	r->key = ri->key;
+	r->unique_est = ri->unique_est;
+	ora_free(li);
+	ora_free(ri);
+}
+
 /* ---- BATjoin (gdk_join.c:4451-4623) ---------------------------------------- */
 
 int
@@ -755,6 +871,14 @@ ora_join(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r,
 	if (atomtype(l->type) != atomtype(r->type)) {
 		ora_seterr("BATjoin: inputs not compatible.");
 		return -1;
+	}
+	if (l->type == ORA_str) {
+		ora_bat *li, *ri;
+		if (str_images(l, r, &li, &ri) < 0)
+			return -1;
+		int rc = ora_join(r1p, r2p, li, ri, sl, sr, nil_matches);
+		str_flags_back(l, r, li, ri);
+		return rc;
 	}
 	if (!join_type_ok(l->type) || !join_type_ok(r->type)) {
 		ora_seterr("BATjoin: type not restated");
@@ -798,6 +922,14 @@ ora_join(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r,
 int
 ora_join_algo(ora_bat *l, ora_bat *r, const ora_bat *sl, const ora_bat *sr)
 {
+	if (l->type == ORA_str && r->type == ORA_str) {
+		ora_bat *li, *ri;
+		if (str_images(l, r, &li, &ri) < 0)
+			return -1;
+		int a = ora_join_algo(li, ri, sl, sr);
+		str_flags_back(l, r, li, ri);
+		return a;
+	}
 	ora_ci lci, rci;
 	if (ora_ci_init(&lci, l, sl) < 0 || ora_ci_init(&rci, r, sr) < 0)
 		return -1;
