@@ -42,11 +42,22 @@ namespace {
 #ifndef MGDK_SORT_ROWS
 #define MGDK_SORT_ROWS 32
 #endif
-constexpr int SWAVES = MGDK_SORT_WAVES;    // waves per scatter workgroup
-constexpr int SROWS = MGDK_SORT_ROWS;      // rows of 64 keys per wave
-constexpr int STHREADS = 64 * SWAVES;
-constexpr int STILE = STHREADS * SROWS;    // keys per tile
-static_assert(SWAVES >= 4 && STILE % 256 == 0, "the digit steps need 256 threads");
+#ifndef MGDK_SORT_WAVES8
+#define MGDK_SORT_WAVES8 4
+#endif
+#ifndef MGDK_SORT_ROWS8
+#define MGDK_SORT_ROWS8 32
+#endif
+// scatter tile shape per key width: waves per workgroup x rows of 64 keys
+// per wave (the tile's keys and values are staged in LDS)
+template <typename K>
+struct Tile {
+	static constexpr int W = sizeof(K) == 4 ? MGDK_SORT_WAVES : MGDK_SORT_WAVES8;
+	static constexpr int R = sizeof(K) == 4 ? MGDK_SORT_ROWS : MGDK_SORT_ROWS8;
+	static constexpr int THREADS = 64 * W;
+	static constexpr int N = THREADS * R;
+	static_assert(W >= 4 && N % 256 == 0, "the digit steps need 256 threads");
+};
 // 1: a row's peer lanes (same digit) come from a per-wave LDS lane mask per
 // digit (one OR, one read, one clear) instead of 8 bit-sliced ballots
 #ifndef MGDK_SORT_LDSMATCH
@@ -60,8 +71,8 @@ k_rs_hist(const K *keys, BUN n, int shift, uint32_t *hist, uint32_t nblocks)
 	__shared__ uint32_t h[256];
 	h[threadIdx.x] = 0;
 	__syncthreads();
-	const BUN base = (BUN) blockIdx.x * STILE;
-	constexpr int HR = STILE / 256;
+	const BUN base = (BUN) blockIdx.x * Tile<K>::N;
+	constexpr int HR = Tile<K>::N / 256;
 	K k[HR];
 #pragma unroll
 	for (int r = 0; r < HR; r++) {
@@ -127,6 +138,15 @@ k_rs_dscan(const uint32_t *cnt, Shifts sh, uint32_t *gdig)
 	gdig[blockIdx.x * 256 + threadIdx.x] = x - v;
 }
 
+// the tiles of a pass that sorts inside the buckets of the previous (MSD)
+// pass: desc[t] = {first row, rows, first tile of the bucket, tiles of the
+// bucket}; the counts / offsets of tile t live at 256 * first + d * tiles +
+// (t - first), so one exclusive scan gives every (bucket, digit) its start
+struct SegTiles {
+	const uint4 *desc;
+	const uint32_t *count;      // number of tiles
+};
+
 // final pass outputs: decoded value column and order oids
 struct FinalOut {
 	void *sorted;       // NULL: not requested (or gathered separately)
@@ -170,12 +190,13 @@ emit_final(const FinalOut &fo, BUN g, K key, uint32_t v)
 // predecessor is resident) plus the pass's global digit start gdig -- no
 // per-pass histogram pass and scan.  Otherwise offs holds the digit-major
 // exclusive scan of k_rs_hist's counts.
-template <typename K, bool FINAL, bool IDV, bool LB>
-__global__ __launch_bounds__(STHREADS) void
+template <typename K, bool FINAL, bool IDV, bool LB, bool SEG>
+__global__ __launch_bounds__(Tile<K>::THREADS) void
 k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32_t *offs, uint32_t nblocks,
 	     K *kout, uint32_t *vout, FinalOut fo, uint32_t *ticket, uint64_t *status, const uint32_t *gdig,
-	     uint32_t *err)
+	     uint32_t *err, SegTiles sg)
 {
+	constexpr int SWAVES = Tile<K>::W, SROWS = Tile<K>::R, STHREADS = Tile<K>::THREADS, STILE = Tile<K>::N;
 	__shared__ K sk[STILE];
 	__shared__ __attribute__((aligned(16))) uint32_t sv[STILE];
 	__shared__ uint32_t wcnt[SWAVES][256]; // per-wave running digit counts, then per-wave bases
@@ -192,14 +213,22 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 		__syncthreads();
 	}
 	const uint32_t blk = LB ? s_tile : blockIdx.x;
+	// SEG: the tile is a piece of one bucket of the previous (MSD) pass
+	uint4 sd = {0, 0, 0, 0};
+	if (SEG) {
+		if (blk >= *sg.count)
+			return;
+		sd = sg.desc[blk];
+	}
+	const BUN tbase = SEG ? (BUN) sd.x : (BUN) blk * STILE;
+	const BUN tend = SEG ? tbase + sd.y : n;
 	__shared__ uint32_t lh[256];          // LB: the tile's digit counts, published before ranking
 	if (LB && dig)
 		lh[tid] = 0;
 	for (unsigned q = tid; q < SWAVES * 256; q += STHREADS)
 		(&wcnt[0][0])[q] = 0;
 	if (!LB && dig)
-		gbase[tid] = offs[(BUN) tid * nblocks + blk];
-	const BUN tbase = (BUN) blk * STILE;
+		gbase[tid] = SEG ? offs[(BUN) 256 * sd.z + (BUN) tid * sd.w + (blk - sd.z)] : offs[(BUN) tid * nblocks + blk];
 	const BUN base = tbase + (BUN) w * (64 * SROWS);
 #if MGDK_SORT_LDSMATCH
 	// the wave's 256 digit lane masks live in sv until the tile is placed
@@ -214,8 +243,8 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 #pragma unroll
 	for (int r = 0; r < SROWS; r++) {
 		const BUN i = base + r * 64 + lane;
-		k[r] = i < n ? keys[i] : 0;
-		v[r] = IDV ? (uint32_t) i : (i < n ? vals[i] : 0);   // first pass: positions
+		k[r] = i < tend ? keys[i] : 0;
+		v[r] = IDV ? (uint32_t) i : (i < tend ? vals[i] : 0);   // first pass: positions
 	}
 	__syncthreads();
 	if (LB) {
@@ -223,7 +252,7 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 		// look-back of later tiles rarely has to walk far
 #pragma unroll
 		for (int r = 0; r < SROWS; r++)
-			if (base + r * 64 + lane < n)
+			if (base + r * 64 + lane < tend)
 				atomicAdd(&lh[(uint32_t) (k[r] >> shift) & 255], 1u);
 		__syncthreads();
 		if (dig)
@@ -235,7 +264,7 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 #pragma unroll
 	for (int r = 0; r < SROWS; r++) {
 		const BUN i = base + r * 64 + lane;
-		const bool valid = i < n;
+		const bool valid = i < tend;
 		const uint32_t d = (uint32_t) (k[r] >> shift) & 255;
 #if MGDK_SORT_LDSMATCH
 		// the wave's lanes OR their bit into their digit's mask, read it
@@ -321,7 +350,7 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 #pragma unroll
 	for (int r = 0; r < SROWS; r++) {
 		const BUN i = base + r * 64 + lane;
-		if (i < n) {
+		if (i < tend) {
 			const uint32_t d = rk[r] & 255;
 			const uint32_t lpos = tstart[d] + wcnt[w][d] + (rk[r] >> 8);
 			sk[lpos] = k[r];
@@ -329,7 +358,7 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 		}
 	}
 	__syncthreads();
-	const uint32_t nt = (uint32_t) (n - tbase < (BUN) STILE ? n - tbase : (BUN) STILE);
+	const uint32_t nt = (uint32_t) (tend - tbase < (BUN) STILE ? tend - tbase : (BUN) STILE);
 #pragma unroll
 	for (int u = 0; u < SROWS; u++) {
 		const uint32_t i = tid + u * STHREADS;
@@ -575,6 +604,264 @@ k_gid(const uint64_t *excl, const uint8_t *flag, BUN n, oid *gid)
 		gid[i] = excl[i] + flag[i];
 }
 
+// ---- MSD-then-local variant for 4-byte keys with >= 3 varying digits -------
+// pass A scatters by the top varying digit d1 (the LSD scatter kernel, stable,
+// positions as values); pass B sorts every d1 bucket by the next digit d2
+// (tiles cut at bucket borders, one exclusive scan over (bucket, digit,
+// tile) counts); every (d1, d2) bucket -- ~n / 65536 rows -- is then sorted
+// by its remaining bits inside one workgroup's LDS (stable 4-bit counting
+// passes) and written out as the final columns.  Three passes over HBM
+// instead of four; the order is the stable one (each step is stable).
+
+// the tiles of pass B: bucket b's rows cut into pieces of `tile` rows
+__global__ __launch_bounds__(256) void
+k_seg_tiles(const uint32_t *cnt, const uint32_t *start, uint32_t tile, uint4 *desc, uint32_t *count,
+	    uint32_t *bfirst, uint32_t *bnt)
+{
+	__shared__ uint32_t ws[4];
+	const unsigned b = threadIdx.x, lane = __lane_id(), w = b >> 6;
+	const uint32_t c = cnt[b], t = (c + tile - 1) / tile;
+	uint32_t x = t;
+#pragma unroll
+	for (int o = 1; o < 64; o <<= 1) {
+		const uint32_t u = __shfl_up(x, o);
+		if (lane >= (unsigned) o)
+			x += u;
+	}
+	if (lane == 63)
+		ws[w] = x;
+	__syncthreads();
+	for (unsigned q = 0; q < w; q++)
+		x += ws[q];
+	const uint32_t first = x - t;
+	bfirst[b] = first;
+	bnt[b] = t;
+	for (uint32_t j = 0; j < t; j++)
+		desc[first + j] = make_uint4(start[b] + j * tile, c - j * tile < tile ? c - j * tile : tile, first, t);
+	if (b == 255)
+		*count = x;
+}
+
+// pass B's per-tile digit counts at 256 * first + d * tiles + (t - first)
+template <typename K>
+__global__ __launch_bounds__(256) void
+k_seg_hist(const K *keys, int shift, SegTiles sg, uint32_t *hist)
+{
+	__shared__ uint32_t h[256];
+	const uint32_t t = blockIdx.x;
+	if (t >= *sg.count)
+		return;
+	const uint4 d = sg.desc[t];
+	h[threadIdx.x] = 0;
+	__syncthreads();
+	constexpr int U = 8;
+	for (uint32_t i0 = threadIdx.x; i0 < d.y; i0 += U * 256) {
+		K k[U];
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const uint32_t i = i0 + u * 256;
+			k[u] = i < d.y ? keys[d.x + i] : 0;
+		}
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			if (i0 + u * 256 < d.y)
+				atomicAdd(&h[(uint32_t) (k[u] >> shift) & 255], 1u);
+	}
+	__syncthreads();
+	hist[(BUN) 256 * d.z + (BUN) threadIdx.x * d.w + (t - d.z)] = h[threadIdx.x];
+}
+
+// padded index of the counting table (one pad word per 16: the scan's
+// 16-entry runs per thread fall on different banks)
+__device__ __forceinline__ uint32_t
+lpad(uint32_t i)
+{
+	return i + (i >> 4);
+}
+
+// one (d1, d2) bucket per workgroup: load it into LDS, stable 4-bit
+// counting passes over the remaining bits (each thread owns a contiguous
+// chunk of rows and one counter per digit), write the final columns
+template <typename K, int CAP>
+__global__ __launch_bounds__(256) void
+k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *offs, const uint32_t *bfirst, const uint32_t *bnt,
+	   const uint32_t *bstart, const uint32_t *bcnt, Shifts ls, FinalOut fo, uint32_t *ovf)
+{
+	__shared__ K sk[2][CAP];
+	__shared__ uint32_t sv[2][CAP];
+	__shared__ uint16_t cnt[16 * 256 + 256];
+	__shared__ uint32_t ws[4];
+	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+	const uint32_t b = blockIdx.x >> 8, d = blockIdx.x & 255;
+	const uint32_t nt = bnt[b], f = bfirst[b];
+	if (nt == 0)
+		return;
+	const uint32_t s = offs[(BUN) 256 * f + (BUN) d * nt];
+	const uint32_t e = d < 255 ? offs[(BUN) 256 * f + (BUN) (d + 1) * nt] : bstart[b] + bcnt[b];
+	const uint32_t m = e - s;
+	if (m == 0)
+		return;
+	if (m > (uint32_t) CAP) {
+		// sorted by the host afterwards (rare: the gate expects <= CAP / 2)
+		if (tid == 0) {
+			const uint32_t q = atomicAdd(&ovf[0], 1u);
+			ovf[1 + 2 * q] = s;
+			ovf[2 + 2 * q] = m;
+		}
+		return;
+	}
+	for (uint32_t i = tid; i < m; i += 256) {
+		sk[0][i] = keys[s + i];
+		sv[0][i] = vals[s + i];
+	}
+	__syncthreads();
+	int cur = 0;
+	const uint32_t chunk = (m + 255) >> 8;
+	const uint32_t j0 = tid * chunk < m ? tid * chunk : m, j1 = j0 + chunk < m ? j0 + chunk : m;
+	for (int p = 0; p < ls.n && m > 1; p++) {
+		const int sh = ls.s[p];
+#pragma unroll
+		for (int q = 0; q < 16; q++)
+			cnt[lpad(q * 256 + tid)] = 0;
+		for (uint32_t j = j0; j < j1; j++)
+			cnt[lpad(((uint32_t) (sk[cur][j] >> sh) & 15) * 256 + tid)]++;
+		__syncthreads();
+		// exclusive scan of the table in (digit, thread) order
+		uint32_t loc[16], sum = 0;
+#pragma unroll
+		for (int q = 0; q < 16; q++) {
+			loc[q] = cnt[lpad(tid * 16 + q)];
+			sum += loc[q];
+		}
+		uint32_t x = sum;
+#pragma unroll
+		for (int o = 1; o < 64; o <<= 1) {
+			const uint32_t u = __shfl_up(x, o);
+			if (lane >= (unsigned) o)
+				x += u;
+		}
+		if (lane == 63)
+			ws[w] = x;
+		__syncthreads();
+		uint32_t ex = x - sum;
+		for (unsigned q = 0; q < w; q++)
+			ex += ws[q];
+#pragma unroll
+		for (int q = 0; q < 16; q++) {
+			cnt[lpad(tid * 16 + q)] = (uint16_t) ex;
+			ex += loc[q];
+		}
+		__syncthreads();
+		for (uint32_t j = j0; j < j1; j++) {
+			const K kk = sk[cur][j];
+			const uint32_t pos = cnt[lpad(((uint32_t) (kk >> sh) & 15) * 256 + tid)]++;
+			sk[cur ^ 1][pos] = kk;
+			sv[cur ^ 1][pos] = sv[cur][j];
+		}
+		__syncthreads();
+		cur ^= 1;
+	}
+	for (uint32_t i = tid; i < m; i += 256)
+		emit_final<K>(fo, (BUN) s + i, sk[cur][i], sv[cur][i]);
+}
+
+template <typename K>
+__global__ __launch_bounds__(256) void
+k_final_copy_at(const K *keys, const uint32_t *vals, BUN m, BUN s, FinalOut fo)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (BUN) gridDim.x * blockDim.x)
+		emit_final<K>(fo, s + i, keys[i], vals[i]);
+}
+
+template <typename K>
+int radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int bits, const FinalOut *fo,
+	       bool positions, bool andor, K **keys_out, uint32_t **vals_out, const uint32_t *digit_hist = nullptr);
+
+// passes A, B, C (see above); keys / vals hold the input images, the
+// alternates are free; cap: the largest (d1, d2) bucket sorted in LDS
+template <typename K>
+int
+radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, const std::vector<int> &shifts, uint64_t diff,
+	     const uint32_t *dh, const uint32_t *gdig, uint64_t *status, uint32_t *lbm, const FinalOut &fo0, int cap,
+	     K **keys_out, uint32_t **vals_out)
+{
+	hipStream_t st = stream();
+	const size_t ns = shifts.size();
+	const int s1 = shifts[ns - 1], s2 = shifts[ns - 2];
+	constexpr uint32_t TILE = (uint32_t) Tile<K>::N;
+	const uint32_t nblocks = (uint32_t) ((n + TILE - 1) / TILE);
+	const uint32_t tmax = nblocks + 256;
+	DevBuf desc((size_t) tmax * 16 + 64), meta(4 * 1024), hist((size_t) 256 * tmax * 4 + 64),
+		offs((size_t) 256 * tmax * 4 + 64), ovf((size_t) (1 + 2 * 65536) * 4);
+	if (!desc.p || !meta.p || !hist.p || !offs.p || !ovf.p)
+		return -1;
+	uint32_t *count = meta.as<uint32_t>(), *bfirst = count + 256, *bnt = count + 512;
+	FinalOut none{};
+	// pass A: by d1, positions as values
+	if (!hip_ok(hipMemsetAsync(status, 0, (size_t) 256 * nblocks * 8, st), "memset") ||
+	    !hip_ok(hipMemsetAsync(lbm, 0, 8, st), "memset") ||
+	    !hip_ok(hipMemsetAsync(hist.p, 0, (size_t) 256 * tmax * 4, st), "memset") ||
+	    !hip_ok(hipMemsetAsync(ovf.p, 0, 4, st), "memset"))
+		return -1;
+	const uint32_t *gd1 = gdig + (ns - 1) * 256, *cnt1 = dh + (s1 / 8) * 256;
+	hipLaunchKernelGGL((k_rs_scatter<K, false, true, true, false>), dim3(nblocks), dim3(Tile<K>::THREADS), 0, st, k0,
+			   v0, n, s1, nullptr, nblocks, k1, v1, none, lbm, status, gd1, lbm + 4, SegTiles{});
+	// pass B: by d2 inside the d1 buckets
+	hipLaunchKernelGGL(k_seg_tiles, dim3(1), dim3(256), 0, st, cnt1, gd1, TILE, desc.as<uint4>(), count, bfirst,
+			   bnt);
+	const SegTiles sg{desc.as<uint4>(), count};
+	hipLaunchKernelGGL((k_seg_hist<K>), dim3(tmax), dim3(256), 0, st, (const K *) k1, s2, sg, hist.as<uint32_t>());
+	if (exclusive_scan(hist.as<uint32_t>(), offs.as<uint32_t>(), (BUN) 256 * tmax, nullptr) < 0)
+		return -1;
+	hipLaunchKernelGGL((k_rs_scatter<K, false, false, false, true>), dim3(tmax), dim3(Tile<K>::THREADS), 0, st,
+			   (const K *) k1, (const uint32_t *) v1, n, s2, offs.as<uint32_t>(), tmax, k0, v0, none, lbm,
+			   status, gd1, lbm + 4, sg);
+	// pass C: the remaining varying bits, 4 at a time, inside each (d1, d2) bucket
+	Shifts ls{};
+	for (size_t q = 0; q + 2 < ns; q++)
+		for (int h = 0; h < 2; h++)
+			if ((diff >> (shifts[q] + 4 * h)) & 15)
+				ls.s[ls.n++] = shifts[q] + 4 * h;
+	FinalOut fo = fo0;
+	if (fo.want_keys)
+		fo.keys = k1;
+	if (cap <= 2048)
+		hipLaunchKernelGGL((k_rs_local<K, 2048>), dim3(65536), dim3(256), 0, st, (const K *) k0,
+				   (const uint32_t *) v0, offs.as<uint32_t>(), bfirst, bnt, gd1, cnt1, ls, fo, ovf.as<uint32_t>());
+	else
+		hipLaunchKernelGGL((k_rs_local<K, 4096>), dim3(65536), dim3(256), 0, st, (const K *) k0,
+				   (const uint32_t *) v0, offs.as<uint32_t>(), bfirst, bnt, gd1, cnt1, ls, fo, ovf.as<uint32_t>());
+	uint32_t *h = (uint32_t *) pinned(16);
+	if (!h || !hip_ok(hipMemcpyAsync(h, ovf.p, 4, hipMemcpyDeviceToHost, st), "memcpy") ||
+	    !hip_ok(hipMemcpyAsync(h + 1, lbm + 4, 4, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+		return -1;
+	if (h[1]) {
+		seterr("HY013!BATsort: radix look-back did not complete");
+		return -1;
+	}
+	const uint32_t nov = h[0];
+	if (nov) {
+		std::vector<uint32_t> ov((size_t) 2 * nov);
+		if (!hip_ok(hipMemcpyAsync(ov.data(), ovf.as<uint32_t>() + 1, (size_t) 8 * nov, hipMemcpyDeviceToHost, st),
+			    "memcpy") ||
+		    !sync_data())
+			return -1;
+		for (uint32_t q = 0; q < nov; q++) {
+			const BUN s = ov[2 * q], m = ov[2 * q + 1];
+			K *ks;
+			uint32_t *vs;
+			if (radix_sort<K>(k0 + s, v0 + s, k1 + s, v1 + s, m, 8 * (int) sizeof(K), nullptr, false, false, &ks,
+					  &vs) < 0)
+				return -1;
+			hipLaunchKernelGGL((k_final_copy_at<K>), dim3(grid_for(m, 1024, 8192)), dim3(256), 0, st,
+					   (const K *) ks, (const uint32_t *) vs, m, s, fo);
+		}
+	}
+	*keys_out = fo.want_keys ? k1 : k0;
+	*vals_out = v0;
+	return sync() ? 0 : -1;
+}
+
 // stable LSD radix sort of (key, position) pairs; the final pass (when fo
 // is given) writes the result columns instead of the pairs
 // positions: the values are 0..n-1 and `vals` is uninitialised (the first
@@ -583,7 +870,7 @@ k_gid(const uint64_t *excl, const uint8_t *flag, BUN n, oid *gid)
 template <typename K>
 int
 radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int bits, const FinalOut *fo,
-	   bool positions, bool andor, K **keys_out, uint32_t **vals_out, const uint32_t *digit_hist = nullptr)
+	   bool positions, bool andor, K **keys_out, uint32_t **vals_out, const uint32_t *digit_hist)
 {
 	*keys_out = keys;
 	*vals_out = vals;
@@ -597,15 +884,22 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 			return -1;
 		hipLaunchKernelGGL((k_andor<K>), dim3(grid_for(n, 8192, 1024)), dim3(256), 0, st, keys, n, ao);
 	}
-	unsigned long long *h = (unsigned long long *) pinned(16);
-	if (!hip_ok(hipMemcpyAsync(h, ao, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+	// the MSD-then-local variant needs the digit counts of d1 and d2 to
+	// choose its bucket capacity
+	static const bool use_hy = getenv("MGDK_SORT_HYBRID") ? atoi(getenv("MGDK_SORT_HYBRID")) != 0 : true;
+	const bool hy_try = use_hy && sizeof(K) == 4 && fo != nullptr && positions && digit_hist != nullptr &&
+			    n >= ((BUN) 1 << 22);
+	unsigned long long *h = (unsigned long long *) pinned(16 + 4 * 256 * 4);
+	if (!h || !hip_ok(hipMemcpyAsync(h, ao, 16, hipMemcpyDeviceToHost, st), "memcpy") ||
+	    (hy_try && !hip_ok(hipMemcpyAsync(h + 2, digit_hist, 4 * 256 * 4, hipMemcpyDeviceToHost, st), "memcpy")) ||
+	    !sync())
 		return -1;
 	const uint64_t diff = h[0] ^ h[1];
 	std::vector<int> shifts;
 	for (int shift = 0; shift < bits; shift += 8)
 		if ((diff >> shift) & 255)
 			shifts.push_back(shift);   // other digits are constant: identity passes
-	const uint32_t nblocks = (uint32_t) ((n + STILE - 1) / STILE);
+	const uint32_t nblocks = (uint32_t) ((n + Tile<K>::N - 1) / Tile<K>::N);
 	static const bool use_lb = getenv("MGDK_SORT_LB") ? atoi(getenv("MGDK_SORT_LB")) != 0 : true;
 	const bool lb = use_lb && !shifts.empty() && shifts.size() <= (size_t) RS_MAXP;
 	DevBuf hist(lb ? 64 : (size_t) 256 * nblocks * 4), offs(lb ? 64 : (size_t) 256 * nblocks * 4);
@@ -629,6 +923,21 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 			dh = dcnt.as<uint32_t>();
 		}
 		hipLaunchKernelGGL(k_rs_dscan, dim3(sh.n), dim3(256), 0, st, dh, sh, gdig);
+		if (hy_try && shifts.size() >= 3) {
+			// expected largest (d1, d2) bucket if the two digits were independent
+			const uint32_t *hc = (const uint32_t *) (h + 2);
+			const int s1 = shifts.back(), s2 = shifts[shifts.size() - 2];
+			uint32_t m1 = 0, m2 = 0;
+			for (int b = 0; b < 256; b++) {
+				m1 = hc[(s1 / 8) * 256 + b] > m1 ? hc[(s1 / 8) * 256 + b] : m1;
+				m2 = hc[(s2 / 8) * 256 + b] > m2 ? hc[(s2 / 8) * 256 + b] : m2;
+			}
+			const double est = (double) m1 * (double) m2 / (double) n;
+			const int cap = est <= 1024 ? 2048 : est <= 2048 ? 4096 : 0;
+			if (cap)
+				return radix_hybrid<K>(keys, vals, keys_alt, vals_alt, n, shifts, diff, dh, gdig,
+						       status.as<uint64_t>(), lbm.as<uint32_t>(), *fo, cap, keys_out, vals_out);
+		}
 	}
 	K *kin = keys, *kout = keys_alt;
 	uint32_t *vin = vals, *vout = vals_alt;
@@ -652,8 +961,9 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 			f2.keys = kout;
 		uint32_t *tk = lbm.as<uint32_t>(), *er = lbm.as<uint32_t>() + 4;
 		const uint32_t *gd = gdig + s * 256;
-#define SCAT(F, I, L) hipLaunchKernelGGL((k_rs_scatter<K, F, I, L>), dim3(nblocks), dim3(STHREADS), 0, st, kin, vin, n, \
-					 shift, offs.as<uint32_t>(), nblocks, kout, vout, f2, tk, status.as<uint64_t>(), gd, er)
+#define SCAT(F, I, L) hipLaunchKernelGGL((k_rs_scatter<K, F, I, L, false>), dim3(nblocks), dim3(Tile<K>::THREADS), 0, st, kin, \
+					 vin, n, shift, offs.as<uint32_t>(), nblocks, kout, vout, f2, tk, status.as<uint64_t>(), gd, er, \
+					 SegTiles{})
 		if (lb) {
 			if (fin) {
 				if (idv) SCAT(true, true, true); else SCAT(true, false, true);
