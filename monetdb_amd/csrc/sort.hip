@@ -158,6 +158,8 @@ struct FinalOut {
 	bool uns;           // oid
 	oid *order;
 	oid hseq;
+	oid *gid;           // hybrid pass C: group ids written with the rows (NULL: not)
+	bool *gid_done;     // set when it did
 };
 
 template <typename K>
@@ -681,32 +683,50 @@ lpad(uint32_t i)
 
 // one (d1, d2) bucket per workgroup: load it into LDS, stable 4-bit
 // counting passes over the remaining bits (each thread owns a contiguous
-// chunk of rows and one counter per digit), write the final columns
-template <typename K, int CAP>
+// chunk of rows and one counter per digit), write the final columns.
+// GID: buckets taken in ticket order; each counts its group starts (its
+// first row always starts a group: consecutive buckets hold different
+// leading digits) and a decoupled look-back over the buckets gives the ids
+// (every bucket fits: the host checked the largest one first)
+template <typename K, int CAP, bool GID>
 __global__ __launch_bounds__(256) void
 k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *offs, const uint32_t *bfirst, const uint32_t *bnt,
-	   const uint32_t *bstart, const uint32_t *bcnt, Shifts ls, FinalOut fo, uint32_t *ovf)
+	   const uint32_t *bstart, const uint32_t *bcnt, Shifts ls, FinalOut fo, uint32_t *ovf, uint32_t *ticket,
+	   uint64_t *status, uint32_t *err)
 {
 	__shared__ K sk[2][CAP];
 	__shared__ uint32_t sv[2][CAP];
 	__shared__ uint16_t cnt[16 * 256 + 256];
 	__shared__ uint32_t ws[4];
+	__shared__ uint32_t s_q;
+	__shared__ uint64_t s_excl;
 	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
-	const uint32_t b = blockIdx.x >> 8, d = blockIdx.x & 255;
+	uint32_t q = blockIdx.x;
+	if (GID) {
+		if (tid == 0)
+			s_q = atomicAdd(ticket, 1u);
+		__syncthreads();
+		q = s_q;
+	}
+	const uint32_t b = q >> 8, d = q & 255;
 	const uint32_t nt = bnt[b], f = bfirst[b];
-	if (nt == 0)
+	uint32_t s = 0, m = 0;
+	if (nt != 0) {
+		s = offs[(BUN) 256 * f + (BUN) d * nt];
+		const uint32_t e = d < 255 ? offs[(BUN) 256 * f + (BUN) (d + 1) * nt] : bstart[b] + bcnt[b];
+		m = e - s;
+	}
+	if (m == 0) {
+		if (GID && w == 0)
+			(void) mgdk_lb::lookback(status, q, 0, err);
 		return;
-	const uint32_t s = offs[(BUN) 256 * f + (BUN) d * nt];
-	const uint32_t e = d < 255 ? offs[(BUN) 256 * f + (BUN) (d + 1) * nt] : bstart[b] + bcnt[b];
-	const uint32_t m = e - s;
-	if (m == 0)
-		return;
+	}
 	if (m > (uint32_t) CAP) {
 		// sorted by the host afterwards (rare: the gate expects <= CAP / 2)
 		if (tid == 0) {
-			const uint32_t q = atomicAdd(&ovf[0], 1u);
-			ovf[1 + 2 * q] = s;
-			ovf[2 + 2 * q] = m;
+			const uint32_t o = atomicAdd(&ovf[0], 1u);
+			ovf[1 + 2 * o] = s;
+			ovf[2 + 2 * o] = m;
 		}
 		return;
 	}
@@ -718,22 +738,8 @@ k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *offs, const uint
 	int cur = 0;
 	const uint32_t chunk = (m + 255) >> 8;
 	const uint32_t j0 = tid * chunk < m ? tid * chunk : m, j1 = j0 + chunk < m ? j0 + chunk : m;
-	for (int p = 0; p < ls.n && m > 1; p++) {
-		const int sh = ls.s[p];
-#pragma unroll
-		for (int q = 0; q < 16; q++)
-			cnt[lpad(q * 256 + tid)] = 0;
-		for (uint32_t j = j0; j < j1; j++)
-			cnt[lpad(((uint32_t) (sk[cur][j] >> sh) & 15) * 256 + tid)]++;
-		__syncthreads();
-		// exclusive scan of the table in (digit, thread) order
-		uint32_t loc[16], sum = 0;
-#pragma unroll
-		for (int q = 0; q < 16; q++) {
-			loc[q] = cnt[lpad(tid * 16 + q)];
-			sum += loc[q];
-		}
-		uint32_t x = sum;
+	auto block_excl = [&](uint32_t v, uint32_t &total) -> uint32_t {
+		uint32_t x = v;
 #pragma unroll
 		for (int o = 1; o < 64; o <<= 1) {
 			const uint32_t u = __shfl_up(x, o);
@@ -743,13 +749,34 @@ k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *offs, const uint
 		if (lane == 63)
 			ws[w] = x;
 		__syncthreads();
-		uint32_t ex = x - sum;
-		for (unsigned q = 0; q < w; q++)
-			ex += ws[q];
+		uint32_t ex = x - v;
+		for (unsigned k = 0; k < w; k++)
+			ex += ws[k];
+		total = ws[0] + ws[1] + ws[2] + ws[3];
+		__syncthreads();
+		return ex;
+	};
+	for (int p = 0; p < ls.n && m > 1; p++) {
+		const int sh = ls.s[p];
 #pragma unroll
-		for (int q = 0; q < 16; q++) {
-			cnt[lpad(tid * 16 + q)] = (uint16_t) ex;
-			ex += loc[q];
+		for (int k = 0; k < 16; k++)
+			cnt[lpad(k * 256 + tid)] = 0;
+		for (uint32_t j = j0; j < j1; j++)
+			cnt[lpad(((uint32_t) (sk[cur][j] >> sh) & 15) * 256 + tid)]++;
+		__syncthreads();
+		// exclusive scan of the table in (digit, thread) order
+		uint32_t loc[16], sum = 0;
+#pragma unroll
+		for (int k = 0; k < 16; k++) {
+			loc[k] = cnt[lpad(tid * 16 + k)];
+			sum += loc[k];
+		}
+		uint32_t tot;
+		uint32_t ex = block_excl(sum, tot);
+#pragma unroll
+		for (int k = 0; k < 16; k++) {
+			cnt[lpad(tid * 16 + k)] = (uint16_t) ex;
+			ex += loc[k];
 		}
 		__syncthreads();
 		for (uint32_t j = j0; j < j1; j++) {
@@ -761,8 +788,49 @@ k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *offs, const uint
 		__syncthreads();
 		cur ^= 1;
 	}
-	for (uint32_t i = tid; i < m; i += 256)
+	uint64_t excl = 0;
+	uint16_t *pre = cnt;     // GID: inclusive group-start count per row
+	if (GID) {
+		uint32_t c = 0;
+		for (uint32_t j = j0; j < j1; j++)
+			c += j > 0 ? sk[cur][j] != sk[cur][j - 1] : s > 0;
+		uint32_t tot;
+		uint32_t run = block_excl(c, tot);
+		if (w == 0) {
+			const uint64_t e = mgdk_lb::lookback(status, q, tot, err);
+			if (lane == 0)
+				s_excl = e;
+		}
+		for (uint32_t j = j0; j < j1; j++) {
+			run += j > 0 ? sk[cur][j] != sk[cur][j - 1] : s > 0;
+			pre[j] = (uint16_t) run;
+		}
+		__syncthreads();
+		excl = s_excl;
+	}
+	for (uint32_t i = tid; i < m; i += 256) {
 		emit_final<K>(fo, (BUN) s + i, sk[cur][i], sv[cur][i]);
+		if (GID)
+			fo.gid[(BUN) s + i] = excl + pre[i];
+	}
+}
+
+// the largest (d1, d2) bucket (decides the LDS capacity / the GID variant)
+__global__ __launch_bounds__(256) void
+k_bucket_max(const uint32_t *offs, const uint32_t *bfirst, const uint32_t *bnt, const uint32_t *bstart,
+	     const uint32_t *bcnt, uint32_t *mx)
+{
+	const uint32_t q = blockIdx.x * 256 + threadIdx.x, b = q >> 8, d = q & 255;
+	const uint32_t nt = bnt[b], f = bfirst[b];
+	uint32_t m = 0;
+	if (nt != 0) {
+		const uint32_t s = offs[(BUN) 256 * f + (BUN) d * nt];
+		const uint32_t e = d < 255 ? offs[(BUN) 256 * f + (BUN) (d + 1) * nt] : bstart[b] + bcnt[b];
+		m = e - s;
+	}
+	m = block_reduce(m, [](uint32_t x, uint32_t y) { return x > y ? x : y; });
+	if (threadIdx.x == 0)
+		atomicMax(mx, m);
 }
 
 template <typename K>
@@ -825,17 +893,45 @@ radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, const std::vector<
 	FinalOut fo = fo0;
 	if (fo.want_keys)
 		fo.keys = k1;
-	if (cap <= 2048)
-		hipLaunchKernelGGL((k_rs_local<K, 2048>), dim3(65536), dim3(256), 0, st, (const K *) k0,
-				   (const uint32_t *) v0, offs.as<uint32_t>(), bfirst, bnt, gd1, cnt1, ls, fo, ovf.as<uint32_t>());
-	else
-		hipLaunchKernelGGL((k_rs_local<K, 4096>), dim3(65536), dim3(256), 0, st, (const K *) k0,
-				   (const uint32_t *) v0, offs.as<uint32_t>(), bfirst, bnt, gd1, cnt1, ls, fo, ovf.as<uint32_t>());
+	bool gid = false;
+	if (fo.gid != nullptr) {
+		// group ids with the rows need every bucket in LDS: the largest first
+		static const bool use_fg = getenv("MGDK_SORT_FUSEGID") ? atoi(getenv("MGDK_SORT_FUSEGID")) != 0 : true;
+		uint32_t *mx = count + 768, *hm = (uint32_t *) pinned(16);
+		if (use_fg) {
+			if (!hm || !hip_ok(hipMemsetAsync(mx, 0, 4, st), "memset"))
+				return -1;
+			hipLaunchKernelGGL(k_bucket_max, dim3(256), dim3(256), 0, st, (const uint32_t *) offs.as<uint32_t>(),
+					   (const uint32_t *) bfirst, (const uint32_t *) bnt, gd1, cnt1, mx);
+			if (!hip_ok(hipMemcpyAsync(hm, mx, 4, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+				return -1;
+			if (hm[0] <= 4096) {
+				gid = true;
+				cap = hm[0] <= 2048 ? 2048 : 4096;
+			}
+		}
+		if (!gid)
+			fo.gid = nullptr;
+	}
+	DevBuf gst(gid ? (size_t) 65536 * 8 + 64 : 64);
+	if (!gst.p || (gid && !hip_ok(hipMemsetAsync(gst.p, 0, (size_t) 65536 * 8 + 64, st), "memset")))
+		return -1;
+	uint32_t *gtk = (uint32_t *) (gst.as<uint64_t>() + 65536), *ger = gtk + 4;
+#define LOCAL(C, G) hipLaunchKernelGGL((k_rs_local<K, C, G>), dim3(65536), dim3(256), 0, st, (const K *) k0, \
+				       (const uint32_t *) v0, offs.as<uint32_t>(), bfirst, bnt, gd1, cnt1, ls, fo, \
+				       ovf.as<uint32_t>(), gtk, gst.as<uint64_t>(), ger)
+	if (cap <= 2048) {
+		if (gid) LOCAL(2048, true); else LOCAL(2048, false);
+	} else {
+		if (gid) LOCAL(4096, true); else LOCAL(4096, false);
+	}
+#undef LOCAL
 	uint32_t *h = (uint32_t *) pinned(16);
 	if (!h || !hip_ok(hipMemcpyAsync(h, ovf.p, 4, hipMemcpyDeviceToHost, st), "memcpy") ||
-	    !hip_ok(hipMemcpyAsync(h + 1, lbm + 4, 4, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+	    !hip_ok(hipMemcpyAsync(h + 1, lbm + 4, 4, hipMemcpyDeviceToHost, st), "memcpy") ||
+	    !hip_ok(hipMemcpyAsync(h + 2, ger, 4, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
 		return -1;
-	if (h[1]) {
+	if (h[1] || (gid && h[2])) {
 		seterr("HY013!BATsort: radix look-back did not complete");
 		return -1;
 	}
@@ -857,6 +953,8 @@ radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, const std::vector<
 					   (const K *) ks, (const uint32_t *) vs, m, s, fo);
 		}
 	}
+	if (gid && fo0.gid_done)
+		*fo0.gid_done = true;
 	*keys_out = fo.want_keys ? k1 : k0;
 	*vals_out = v0;
 	return sync() ? 0 : -1;
@@ -1045,6 +1143,10 @@ sort_typed(const mgdk_bat *b, bool reverse, bool nilslast, mgdk_bat *sn, mgdk_ba
 	const bool gid_vals = gn != nullptr && fo.sorted != nullptr;
 	fo.want_keys = gn != nullptr && !gid_vals;
 	fo.order = on ? (oid *) on->theap : otmp.as<oid>();
+	// the MSD-then-local path may write the group ids with the rows
+	bool gid_done = false;
+	fo.gid = gn ? (oid *) gn->theap : nullptr;
+	fo.gid_done = &gid_done;
 	K *ks;
 	uint32_t *vs;
 	if (radix_sort<K>(k0.as<K>(), v0.as<uint32_t>(), k1.as<K>(), v1.as<uint32_t>(), n, 8 * (int) sizeof(K), &fo,
@@ -1065,7 +1167,13 @@ sort_typed(const mgdk_bat *b, bool reverse, bool nilslast, mgdk_bat *sn, mgdk_ba
 		uint64_t tot = 0;
 		if (!cnt.p || !pre.p)
 			return -1;
-		if (nt > 0) {
+		if (gid_done) {
+			uint64_t *hl = (uint64_t *) pinned(16);
+			if (!hl || !hip_ok(hipMemcpyAsync(hl, (const oid *) gn->theap + n - 1, 8, hipMemcpyDeviceToHost, st),
+					   "memcpy") || !sync())
+				return -1;
+			tot = hl[0];
+		} else if (nt > 0) {
 			auto gids = [&](auto *src) {
 				using KT = std::remove_const_t<std::remove_pointer_t<decltype(src)>>;
 				hipLaunchKernelGGL((k_gid_count<KT>), dim3((unsigned) nt), dim3(256), 0, st, src, n,
