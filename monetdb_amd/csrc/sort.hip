@@ -192,11 +192,32 @@ emit_final(const FinalOut &fo, BUN g, K key, uint32_t v)
 // predecessor is resident) plus the pass's global digit start gdig -- no
 // per-pass histogram pass and scan.  Otherwise offs holds the digit-major
 // exclusive scan of k_rs_hist's counts.
+// XCD-grouped tile order (xg > 0): the tiles are dealt to the XCDs in
+// groups of xg consecutive tiles, each XCD claiming its own tiles in order
+// (a per-XCD ticket; an XCD whose tiles are all claimed takes the next ones
+// of another XCD), so neighbouring tiles -- whose runs of a digit are
+// adjacent in the output -- complete their shared lines in one L2.  Every
+// tile's predecessors were claimed before it or are claimed in order by
+// some XCD, so the look-back still progresses.
+__device__ __forceinline__ uint32_t
+claim_tile(uint32_t *xtk, uint32_t ntiles, uint32_t xg)
+{
+	const uint32_t x = (uint32_t) __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7;   // HW_REG_XCC_ID
+	for (uint32_t k = 0; k < 8; k++) {
+		const uint32_t y = (x + k) & 7;
+		const uint32_t j = atomicAdd(&xtk[y], 1u);
+		const uint32_t t = (j / xg) * 8 * xg + y * xg + j % xg;
+		if (t < ntiles)
+			return t;
+	}
+	return ~0u;
+}
+
 template <typename K, bool FINAL, bool IDV, bool LB, bool SEG>
 __global__ __launch_bounds__(Tile<K>::THREADS) void
 k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32_t *offs, uint32_t nblocks,
 	     K *kout, uint32_t *vout, FinalOut fo, uint32_t *ticket, uint64_t *status, const uint32_t *gdig,
-	     uint32_t *err, SegTiles sg)
+	     uint32_t *err, SegTiles sg, uint32_t xg)
 {
 	constexpr int SWAVES = Tile<K>::W, SROWS = Tile<K>::R, STHREADS = Tile<K>::THREADS, STILE = Tile<K>::N;
 	__shared__ K sk[STILE];
@@ -209,12 +230,12 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 	// threads 0..255 (waves 0-3) own one digit each in the per-digit steps
 	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
 	const bool dig = tid < 256;
-	if (LB) {
+	if (LB || (SEG && xg)) {
 		if (tid == 0)
-			s_tile = atomicAdd(ticket, 1u);
+			s_tile = xg ? claim_tile(ticket + 8, SEG ? *sg.count : nblocks, xg) : atomicAdd(ticket, 1u);
 		__syncthreads();
 	}
-	const uint32_t blk = LB ? s_tile : blockIdx.x;
+	const uint32_t blk = LB || (SEG && xg) ? s_tile : blockIdx.x;
 	// SEG: the tile is a piece of one bucket of the previous (MSD) pass
 	uint4 sd = {0, 0, 0, 0};
 	if (SEG) {
@@ -222,6 +243,8 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 			return;
 		sd = sg.desc[blk];
 	}
+	if (LB && blk == ~0u)
+		return;     // cannot happen: one tile per workgroup
 	const BUN tbase = SEG ? (BUN) sd.x : (BUN) blk * STILE;
 	const BUN tend = SEG ? tbase + sd.y : n;
 	__shared__ uint32_t lh[256];          // LB: the tile's digit counts, published before ranking
@@ -841,6 +864,14 @@ k_final_copy_at(const K *keys, const uint32_t *vals, BUN m, BUN s, FinalOut fo)
 		emit_final<K>(fo, s + i, keys[i], vals[i]);
 }
 
+// tiles per XCD group of the scatter passes (0: plain ticket order)
+static uint32_t
+sort_xg()
+{
+	static const uint32_t g = getenv("MGDK_SORT_XCDG") ? (uint32_t) atoi(getenv("MGDK_SORT_XCDG")) : 0u;
+	return g;
+}
+
 template <typename K>
 int radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int bits, const FinalOut *fo,
 	       bool positions, bool andor, K **keys_out, uint32_t **vals_out, const uint32_t *digit_hist = nullptr);
@@ -867,23 +898,24 @@ radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, const std::vector<
 	FinalOut none{};
 	// pass A: by d1, positions as values
 	if (!hip_ok(hipMemsetAsync(status, 0, (size_t) 256 * nblocks * 8, st), "memset") ||
-	    !hip_ok(hipMemsetAsync(lbm, 0, 8, st), "memset") ||
+	    !hip_ok(hipMemsetAsync(lbm, 0, 8, st), "memset") || !hip_ok(hipMemsetAsync(lbm + 8, 0, 32, st), "memset") ||
 	    !hip_ok(hipMemsetAsync(hist.p, 0, (size_t) 256 * tmax * 4, st), "memset") ||
 	    !hip_ok(hipMemsetAsync(ovf.p, 0, 4, st), "memset"))
 		return -1;
 	const uint32_t *gd1 = gdig + (ns - 1) * 256, *cnt1 = dh + (s1 / 8) * 256;
 	hipLaunchKernelGGL((k_rs_scatter<K, false, true, true, false>), dim3(nblocks), dim3(Tile<K>::THREADS), 0, st, k0,
-			   v0, n, s1, nullptr, nblocks, k1, v1, none, lbm, status, gd1, lbm + 4, SegTiles{});
+			   v0, n, s1, nullptr, nblocks, k1, v1, none, lbm, status, gd1, lbm + 4, SegTiles{}, sort_xg());
 	// pass B: by d2 inside the d1 buckets
 	hipLaunchKernelGGL(k_seg_tiles, dim3(1), dim3(256), 0, st, cnt1, gd1, TILE, desc.as<uint4>(), count, bfirst,
 			   bnt);
 	const SegTiles sg{desc.as<uint4>(), count};
 	hipLaunchKernelGGL((k_seg_hist<K>), dim3(tmax), dim3(256), 0, st, (const K *) k1, s2, sg, hist.as<uint32_t>());
-	if (exclusive_scan(hist.as<uint32_t>(), offs.as<uint32_t>(), (BUN) 256 * tmax, nullptr) < 0)
+	if (exclusive_scan(hist.as<uint32_t>(), offs.as<uint32_t>(), (BUN) 256 * tmax, nullptr) < 0 ||
+	    !hip_ok(hipMemsetAsync(lbm + 8, 0, 32, st), "memset"))
 		return -1;
 	hipLaunchKernelGGL((k_rs_scatter<K, false, false, false, true>), dim3(tmax), dim3(Tile<K>::THREADS), 0, st,
 			   (const K *) k1, (const uint32_t *) v1, n, s2, offs.as<uint32_t>(), tmax, k0, v0, none, lbm,
-			   status, gd1, lbm + 4, sg);
+			   status, gd1, lbm + 4, sg, sort_xg());
 	// pass C: the remaining varying bits, 4 at a time, inside each (d1, d2) bucket
 	Shifts ls{};
 	for (size_t q = 0; q + 2 < ns; q++)
@@ -1046,7 +1078,8 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 		const bool idv = positions && s == 0;
 		if (lb) {
 			if (!hip_ok(hipMemsetAsync(status.p, 0, (size_t) 256 * nblocks * 8, st), "memset") ||
-			    !hip_ok(hipMemsetAsync(lbm.p, 0, 8, st), "memset"))
+			    !hip_ok(hipMemsetAsync(lbm.p, 0, 8, st), "memset") ||
+			    !hip_ok(hipMemsetAsync(lbm.as<uint32_t>() + 8, 0, 32, st), "memset"))
 				return -1;
 		} else {
 			hipLaunchKernelGGL((k_rs_hist<K>), dim3(nblocks), dim3(256), 0, st, kin, n, shift,
@@ -1061,7 +1094,7 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 		const uint32_t *gd = gdig + s * 256;
 #define SCAT(F, I, L) hipLaunchKernelGGL((k_rs_scatter<K, F, I, L, false>), dim3(nblocks), dim3(Tile<K>::THREADS), 0, st, kin, \
 					 vin, n, shift, offs.as<uint32_t>(), nblocks, kout, vout, f2, tk, status.as<uint64_t>(), gd, er, \
-					 SegTiles{})
+					 SegTiles{}, sort_xg())
 		if (lb) {
 			if (fin) {
 				if (idv) SCAT(true, true, true); else SCAT(true, false, true);
