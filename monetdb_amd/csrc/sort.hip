@@ -160,6 +160,7 @@ struct FinalOut {
 	oid hseq;
 	oid *gid;           // hybrid pass C: group ids written with the rows (NULL: not)
 	bool *gid_done;     // set when it did
+	uint64_t *gid_last; // ... and the last row's group id
 };
 
 template <typename K>
@@ -961,7 +962,8 @@ radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, const std::vector<
 	uint32_t *h = (uint32_t *) pinned(16);
 	if (!h || !hip_ok(hipMemcpyAsync(h, ovf.p, 4, hipMemcpyDeviceToHost, st), "memcpy") ||
 	    !hip_ok(hipMemcpyAsync(h + 1, lbm + 4, 4, hipMemcpyDeviceToHost, st), "memcpy") ||
-	    !hip_ok(hipMemcpyAsync(h + 2, ger, 4, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+	    !hip_ok(hipMemcpyAsync(h + 2, ger, 4, hipMemcpyDeviceToHost, st), "memcpy") ||
+	    (gid && !hip_ok(hipMemcpyAsync(h + 4, fo.gid + n - 1, 8, hipMemcpyDeviceToHost, st), "memcpy")) || !sync())
 		return -1;
 	if (h[1] || (gid && h[2])) {
 		seterr("HY013!BATsort: radix look-back did not complete");
@@ -985,8 +987,11 @@ radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, const std::vector<
 					   (const K *) ks, (const uint32_t *) vs, m, s, fo);
 		}
 	}
-	if (gid && fo0.gid_done)
+	if (gid && fo0.gid_done) {
 		*fo0.gid_done = true;
+		if (fo0.gid_last)
+			*fo0.gid_last = *(const uint64_t *) (h + 4);
+	}
 	*keys_out = fo.want_keys ? k1 : k0;
 	*vals_out = v0;
 	return sync() ? 0 : -1;
@@ -1178,8 +1183,10 @@ sort_typed(const mgdk_bat *b, bool reverse, bool nilslast, mgdk_bat *sn, mgdk_ba
 	fo.order = on ? (oid *) on->theap : otmp.as<oid>();
 	// the MSD-then-local path may write the group ids with the rows
 	bool gid_done = false;
+	uint64_t gid_last = 0;
 	fo.gid = gn ? (oid *) gn->theap : nullptr;
 	fo.gid_done = &gid_done;
+	fo.gid_last = &gid_last;
 	K *ks;
 	uint32_t *vs;
 	if (radix_sort<K>(k0.as<K>(), v0.as<uint32_t>(), k1.as<K>(), v1.as<uint32_t>(), n, 8 * (int) sizeof(K), &fo,
@@ -1201,11 +1208,7 @@ sort_typed(const mgdk_bat *b, bool reverse, bool nilslast, mgdk_bat *sn, mgdk_ba
 		if (!cnt.p || !pre.p)
 			return -1;
 		if (gid_done) {
-			uint64_t *hl = (uint64_t *) pinned(16);
-			if (!hl || !hip_ok(hipMemcpyAsync(hl, (const oid *) gn->theap + n - 1, 8, hipMemcpyDeviceToHost, st),
-					   "memcpy") || !sync())
-				return -1;
-			tot = hl[0];
+			tot = gid_last;
 		} else if (nt > 0) {
 			auto gids = [&](auto *src) {
 				using KT = std::remove_const_t<std::remove_pointer_t<decltype(src)>>;
