@@ -881,13 +881,11 @@ int radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, 
 // alternates are free; cap: the largest (d1, d2) bucket sorted in LDS
 template <typename K>
 int
-radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, const std::vector<int> &shifts, uint64_t diff,
-	     const uint32_t *dh, const uint32_t *gdig, uint64_t *status, uint32_t *lbm, const FinalOut &fo0, int cap,
-	     K **keys_out, uint32_t **vals_out)
+radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, int s1, int s2, uint64_t diff, const uint32_t *cnt1,
+	     const uint32_t *gd1, uint64_t *status, uint32_t *lbm, const FinalOut &fo0, int cap, K **keys_out,
+	     uint32_t **vals_out)
 {
 	hipStream_t st = stream();
-	const size_t ns = shifts.size();
-	const int s1 = shifts[ns - 1], s2 = shifts[ns - 2];
 	constexpr uint32_t TILE = (uint32_t) Tile<K>::N;
 	const uint32_t nblocks = (uint32_t) ((n + TILE - 1) / TILE);
 	const uint32_t tmax = nblocks + 256;
@@ -903,7 +901,6 @@ radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, const std::vector<
 	    !hip_ok(hipMemsetAsync(hist.p, 0, (size_t) 256 * tmax * 4, st), "memset") ||
 	    !hip_ok(hipMemsetAsync(ovf.p, 0, 4, st), "memset"))
 		return -1;
-	const uint32_t *gd1 = gdig + (ns - 1) * 256, *cnt1 = dh + (s1 / 8) * 256;
 	hipLaunchKernelGGL((k_rs_scatter<K, false, true, true, false>), dim3(nblocks), dim3(Tile<K>::THREADS), 0, st, k0,
 			   v0, n, s1, nullptr, nblocks, k1, v1, none, lbm, status, gd1, lbm + 4, SegTiles{}, sort_xg());
 	// pass B: by d2 inside the d1 buckets
@@ -919,10 +916,9 @@ radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, const std::vector<
 			   status, gd1, lbm + 4, sg, sort_xg());
 	// pass C: the remaining varying bits, 4 at a time, inside each (d1, d2) bucket
 	Shifts ls{};
-	for (size_t q = 0; q + 2 < ns; q++)
-		for (int h = 0; h < 2; h++)
-			if ((diff >> (shifts[q] + 4 * h)) & 15)
-				ls.s[ls.n++] = shifts[q] + 4 * h;
+	for (int q = 0; q < s2; q += 4)
+		if ((diff >> q) & 15)
+			ls.s[ls.n++] = q;
 	FinalOut fo = fo0;
 	if (fo.want_keys)
 		fo.keys = k1;
@@ -1058,19 +1054,54 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 			dh = dcnt.as<uint32_t>();
 		}
 		hipLaunchKernelGGL(k_rs_dscan, dim3(sh.n), dim3(256), 0, st, dh, sh, gdig);
-		if (hy_try && shifts.size() >= 3) {
+		const int hi = diff ? 63 - __builtin_clzll(diff) : -1;
+		if (hy_try && hi >= 16) {
+			// d1: the top 8 varying bits, d2: the 8 below them; their counts
+			// from the key-image pass when they are whole bytes, else one
+			// more read of the keys
+			const int s1 = hi - 7, s2 = s1 - 8;
+			const uint32_t *hc1, *hc2, *cnt1, *gd1;
+			DevBuf hcnt(RS_MAXP * 256 * 4 * 2 + 64);
+			if (!hcnt.p)
+				return -1;
+			if (s1 % 8 == 0) {
+				const uint32_t *hc = (const uint32_t *) (h + 2);
+				hc1 = hc + (s1 / 8) * 256;
+				hc2 = hc + (s2 / 8) * 256;
+				cnt1 = dh + (s1 / 8) * 256;
+				size_t q = 0;
+				while (shifts[q] != s1)
+					q++;
+				gd1 = gdig + q * 256;
+			} else {
+				Shifts s12{};
+				s12.n = 2;
+				s12.s[0] = s2;
+				s12.s[1] = s1;
+				uint32_t *c = hcnt.as<uint32_t>(), *g = c + RS_MAXP * 256;
+				uint32_t *hh = (uint32_t *) (h + 2);
+				if (!hip_ok(hipMemsetAsync(c, 0, RS_MAXP * 256 * 4, st), "memset"))
+					return -1;
+				hipLaunchKernelGGL((k_rs_dhist<K>), dim3(grid_for(n, 16384, 2048)), dim3(256), 0, st, keys, n, s12, c);
+				hipLaunchKernelGGL(k_rs_dscan, dim3(2), dim3(256), 0, st, (const uint32_t *) c, s12, g);
+				if (!hip_ok(hipMemcpyAsync(hh, c, (size_t) 4 * 256 * 4, hipMemcpyDeviceToHost, st), "memcpy") ||
+				    !sync())
+					return -1;
+				hc1 = hh + (s1 / 8) * 256;
+				hc2 = hh + (s2 / 8) * 256;
+				cnt1 = c + (s1 / 8) * 256;
+				gd1 = g + 256;
+			}
 			// expected largest (d1, d2) bucket if the two digits were independent
-			const uint32_t *hc = (const uint32_t *) (h + 2);
-			const int s1 = shifts.back(), s2 = shifts[shifts.size() - 2];
 			uint32_t m1 = 0, m2 = 0;
 			for (int b = 0; b < 256; b++) {
-				m1 = hc[(s1 / 8) * 256 + b] > m1 ? hc[(s1 / 8) * 256 + b] : m1;
-				m2 = hc[(s2 / 8) * 256 + b] > m2 ? hc[(s2 / 8) * 256 + b] : m2;
+				m1 = hc1[b] > m1 ? hc1[b] : m1;
+				m2 = hc2[b] > m2 ? hc2[b] : m2;
 			}
 			const double est = (double) m1 * (double) m2 / (double) n;
 			const int cap = est <= 1024 ? 2048 : est <= 2048 ? 4096 : 0;
 			if (cap)
-				return radix_hybrid<K>(keys, vals, keys_alt, vals_alt, n, shifts, diff, dh, gdig,
+				return radix_hybrid<K>(keys, vals, keys_alt, vals_alt, n, s1, s2, diff, cnt1, gd1,
 						       status.as<uint64_t>(), lbm.as<uint32_t>(), *fo, cap, keys_out, vals_out);
 		}
 	}

@@ -53,6 +53,14 @@ def test_hybrid_three_digits(gdk, ora):
     _check_int(gdk, ora, r.integers(0, 1 << 24, N, dtype=np.int64).astype(np.int32))
 
 
+@pytest.mark.parametrize("lo,hi", [(0, 1 << 19), (-(1 << 20), 1 << 20), (5, (1 << 27) + 5)])
+def test_hybrid_unaligned_digits(gdk, ora, lo, hi):
+    """the MSD digits are the top 8 + 8 VARYING bits, not whole bytes (an
+    extra count pass); ranges straddling the sign flip fall back to LSD"""
+    r = rng(507)
+    _check_int(gdk, ora, r.integers(lo, hi, N, dtype=np.int64).astype(np.int32))
+
+
 def test_hybrid_overflowing_buckets(gdk, ora):
     """d1 == d2 on every row: the marginals look uniform but each (x, x)
     bucket holds n / 256 rows, far above the LDS capacity"""
