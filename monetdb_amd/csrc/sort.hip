@@ -60,6 +60,9 @@ struct Tile {
 };
 // 1: a row's peer lanes (same digit) come from a per-wave LDS lane mask per
 // digit (one OR, one read, one clear) instead of 8 bit-sliced ballots
+#ifndef MGDK_SORT_LOCAL_NOPASS
+#define MGDK_SORT_LOCAL_NOPASS 0     // diagnostic builds only: pass C without its LDS passes
+#endif
 #ifndef MGDK_SORT_LDSMATCH
 #define MGDK_SORT_LDSMATCH 1
 #endif
@@ -716,7 +719,7 @@ template <typename K, int CAP, bool GID>
 __global__ __launch_bounds__(256) void
 k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *offs, const uint32_t *bfirst, const uint32_t *bnt,
 	   const uint32_t *bstart, const uint32_t *bcnt, Shifts ls, FinalOut fo, uint32_t *ovf, uint32_t *ticket,
-	   uint64_t *status, uint32_t *err)
+	   uint64_t *status, uint32_t *err, uint32_t xg)
 {
 	__shared__ K sk[2][CAP];
 	__shared__ uint32_t sv[2][CAP];
@@ -727,8 +730,9 @@ k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *offs, const uint
 	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
 	uint32_t q = blockIdx.x;
 	if (GID) {
+		// one ticket word saturates near 88 claims / us: claim per XCD
 		if (tid == 0)
-			s_q = atomicAdd(ticket, 1u);
+			s_q = xg ? claim_tile(ticket + 8, 65536, xg) : atomicAdd(ticket, 1u);
 		__syncthreads();
 		q = s_q;
 	}
@@ -780,7 +784,7 @@ k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *offs, const uint
 		__syncthreads();
 		return ex;
 	};
-	for (int p = 0; p < ls.n && m > 1; p++) {
+	for (int p = 0; p < ls.n && m > 1 && !MGDK_SORT_LOCAL_NOPASS; p++) {
 		const int sh = ls.s[p];
 #pragma unroll
 		for (int k = 0; k < 16; k++)
@@ -873,6 +877,14 @@ sort_xg()
 	return g;
 }
 
+// buckets per XCD group of the local pass's claims (0: one ticket word)
+static uint32_t
+local_xg()
+{
+	static const uint32_t g = getenv("MGDK_SORT_LOCALXG") ? (uint32_t) atoi(getenv("MGDK_SORT_LOCALXG")) : 16u;
+	return g;
+}
+
 template <typename K>
 int radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int bits, const FinalOut *fo,
 	       bool positions, bool andor, K **keys_out, uint32_t **vals_out, const uint32_t *digit_hist = nullptr);
@@ -948,7 +960,7 @@ radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, int s1, int s2, ui
 	uint32_t *gtk = (uint32_t *) (gst.as<uint64_t>() + 65536), *ger = gtk + 4;
 #define LOCAL(C, G) hipLaunchKernelGGL((k_rs_local<K, C, G>), dim3(65536), dim3(256), 0, st, (const K *) k0, \
 				       (const uint32_t *) v0, offs.as<uint32_t>(), bfirst, bnt, gd1, cnt1, ls, fo, \
-				       ovf.as<uint32_t>(), gtk, gst.as<uint64_t>(), ger)
+				       ovf.as<uint32_t>(), gtk, gst.as<uint64_t>(), ger, local_xg())
 	if (cap <= 2048) {
 		if (gid) LOCAL(2048, true); else LOCAL(2048, false);
 	} else {
