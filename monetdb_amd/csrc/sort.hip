@@ -108,10 +108,21 @@ k_rs_dhist(const K *keys, BUN n, Shifts sh, uint32_t *out)
 	for (int p = 0; p < sh.n; p++)
 		h[p][threadIdx.x] = 0;
 	__syncthreads();
-	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
-		const K k = keys[i];
-		for (int p = 0; p < sh.n; p++)
-			atomicAdd(&h[p][(uint32_t) (k >> sh.s[p]) & 255], 1u);
+	// 8 keys per thread per step, all loaded before the first is counted
+	constexpr int KU = 8;
+	const BUN stride = (BUN) gridDim.x * blockDim.x;
+	for (BUN i0 = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += KU * stride) {
+		K k[KU];
+#pragma unroll
+		for (int u = 0; u < KU; u++) {
+			const BUN i = i0 + u * stride;
+			k[u] = keys[i < n ? i : n - 1];
+		}
+#pragma unroll
+		for (int u = 0; u < KU; u++)
+			if (i0 + u * stride < n)
+				for (int p = 0; p < sh.n; p++)
+					atomicAdd(&h[p][(uint32_t) (k[u] >> sh.s[p]) & 255], 1u);
 	}
 	__syncthreads();
 	for (int p = 0; p < sh.n; p++)
@@ -708,33 +719,43 @@ lpad(uint32_t i)
 	return i + (i >> 4);
 }
 
-// one (d1, d2) bucket per workgroup: load it into LDS, stable 4-bit
-// counting passes over the remaining bits (each thread owns a contiguous
-// chunk of rows and one counter per digit), write the final columns.
-// GID: buckets taken in ticket order; each counts its group starts (its
-// first row always starts a group: consecutive buckets hold different
-// leading digits) and a decoupled look-back over the buckets gives the ids
-// (every bucket fits: the host checked the largest one first)
-template <typename K, int CAP, bool GID>
-__global__ __launch_bounds__(256) void
+// one (d1, d2) bucket per one-wave workgroup (no workgroup barriers, many
+// buckets per CU): the bucket's rows are loaded into LDS with all loads in
+// flight, each lane takes C consecutive rows into registers, and stable 4-bit
+// counting passes sort them by the remaining bits: a lane's ranks come from
+// returning LDS adds on its own (digit, lane) counter (issued back to back,
+// answered in order), one scan over the 16 x 64 counters in (digit, lane)
+// order gives the bases, the rows are placed in LDS and every lane reads its
+// next chunk back.  The sorted bucket is written out in coalesced order.
+// GID: buckets claimed per XCD; each counts its group starts (its first row
+// always starts one: consecutive buckets hold different leading digits) by
+// ballots, and a decoupled look-back over the buckets numbers them (every
+// bucket fits: the host checked the largest one first)
+__device__ __forceinline__ void
+wave_sync()
+{
+	__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+}
+
+template <typename K, int C, bool GID>
+__global__ __launch_bounds__(64) void
 k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *offs, const uint32_t *bfirst, const uint32_t *bnt,
 	   const uint32_t *bstart, const uint32_t *bcnt, Shifts ls, FinalOut fo, uint32_t *ovf, uint32_t *ticket,
 	   uint64_t *status, uint32_t *err, uint32_t xg)
 {
-	__shared__ K sk[2][CAP];
-	__shared__ uint32_t sv[2][CAP];
-	__shared__ uint16_t cnt[16 * 256 + 256];
-	__shared__ uint32_t ws[4];
-	__shared__ uint32_t s_q;
-	__shared__ uint64_t s_excl;
-	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+	constexpr int CAP = 64 * C;
+	__shared__ K wk[CAP];
+	__shared__ uint32_t wv[CAP];
+	__shared__ uint32_t wc[16 * 64 + 64];
+	const unsigned lane = __lane_id();
 	uint32_t q = blockIdx.x;
 	if (GID) {
 		// one ticket word saturates near 88 claims / us: claim per XCD
-		if (tid == 0)
-			s_q = xg ? claim_tile(ticket + 8, 65536, xg) : atomicAdd(ticket, 1u);
-		__syncthreads();
-		q = s_q;
+		uint32_t t = 0;
+		if (lane == 0)
+			t = xg ? claim_tile(ticket + 8, 65536, xg) : atomicAdd(ticket, 1u);
+		q = __shfl(t, 0);
 	}
 	const uint32_t b = q >> 8, d = q & 255;
 	const uint32_t nt = bnt[b], f = bfirst[b];
@@ -745,101 +766,127 @@ k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *offs, const uint
 		m = e - s;
 	}
 	if (m == 0) {
-		if (GID && w == 0)
+		if (GID)
 			(void) mgdk_lb::lookback(status, q, 0, err);
 		return;
 	}
 	if (m > (uint32_t) CAP) {
 		// sorted by the host afterwards (rare: the gate expects <= CAP / 2)
-		if (tid == 0) {
+		if (lane == 0) {
 			const uint32_t o = atomicAdd(&ovf[0], 1u);
 			ovf[1 + 2 * o] = s;
 			ovf[2 + 2 * o] = m;
 		}
 		return;
 	}
-	for (uint32_t i = tid; i < m; i += 256) {
-		sk[0][i] = keys[s + i];
-		sv[0][i] = vals[s + i];
+	{
+		K x[C];
+		uint32_t y[C];
+#pragma unroll
+		for (int u = 0; u < C; u++) {
+			const uint32_t i = lane + 64 * u, ic = i < m ? i : m - 1;
+			x[u] = keys[s + ic];
+			y[u] = vals[s + ic];
+		}
+#pragma unroll
+		for (int u = 0; u < C; u++) {
+			const uint32_t i = lane + 64 * u;
+			if (i < m) {
+				wk[i] = x[u];
+				wv[i] = y[u];
+			}
+		}
 	}
-	__syncthreads();
-	int cur = 0;
-	const uint32_t chunk = (m + 255) >> 8;
-	const uint32_t j0 = tid * chunk < m ? tid * chunk : m, j1 = j0 + chunk < m ? j0 + chunk : m;
-	auto block_excl = [&](uint32_t v, uint32_t &total) -> uint32_t {
-		uint32_t x = v;
+	wave_sync();
+	if (m > 1 && ls.n > 0 && !MGDK_SORT_LOCAL_NOPASS) {
+		const uint32_t j0 = lane * C;
+		K k[C];
+		uint32_t v[C];
 #pragma unroll
-		for (int o = 1; o < 64; o <<= 1) {
-			const uint32_t u = __shfl_up(x, o);
-			if (lane >= (unsigned) o)
-				x += u;
+		for (int u = 0; u < C; u++) {
+			k[u] = wk[j0 + u < CAP ? j0 + u : 0];
+			v[u] = wv[j0 + u < CAP ? j0 + u : 0];
 		}
-		if (lane == 63)
-			ws[w] = x;
-		__syncthreads();
-		uint32_t ex = x - v;
-		for (unsigned k = 0; k < w; k++)
-			ex += ws[k];
-		total = ws[0] + ws[1] + ws[2] + ws[3];
-		__syncthreads();
-		return ex;
-	};
-	for (int p = 0; p < ls.n && m > 1 && !MGDK_SORT_LOCAL_NOPASS; p++) {
-		const int sh = ls.s[p];
+		for (int p = 0; p < ls.n; p++) {
+			const int sh = ls.s[p];
 #pragma unroll
-		for (int k = 0; k < 16; k++)
-			cnt[lpad(k * 256 + tid)] = 0;
-		for (uint32_t j = j0; j < j1; j++)
-			cnt[lpad(((uint32_t) (sk[cur][j] >> sh) & 15) * 256 + tid)]++;
-		__syncthreads();
-		// exclusive scan of the table in (digit, thread) order
-		uint32_t loc[16], sum = 0;
+			for (int x = 0; x < 16; x++)
+				wc[lpad(x * 64 + lane)] = 0;
+			wave_sync();
+			uint32_t rk[C];
 #pragma unroll
-		for (int k = 0; k < 16; k++) {
-			loc[k] = cnt[lpad(tid * 16 + k)];
-			sum += loc[k];
-		}
-		uint32_t tot;
-		uint32_t ex = block_excl(sum, tot);
+			for (int u = 0; u < C; u++) {
+				const uint32_t dg = (uint32_t) (k[u] >> sh) & 15;
+				rk[u] = j0 + u < m ? atomicAdd(&wc[lpad(dg * 64 + lane)], 1u) : 0;
+			}
+			wave_sync();
+			// exclusive scan of the counters in (digit, lane) order: lane l
+			// owns the 16 entries from 16 l
+			uint32_t loc[16], sum = 0;
 #pragma unroll
-		for (int k = 0; k < 16; k++) {
-			cnt[lpad(tid * 16 + k)] = (uint16_t) ex;
-			ex += loc[k];
+			for (int x = 0; x < 16; x++) {
+				loc[x] = wc[lpad(16 * lane + x)];
+				sum += loc[x];
+			}
+			uint32_t inc = sum;
+#pragma unroll
+			for (int o = 1; o < 64; o <<= 1) {
+				const uint32_t t = __shfl_up(inc, o);
+				if (lane >= (unsigned) o)
+					inc += t;
+			}
+			uint32_t ex = inc - sum;
+#pragma unroll
+			for (int x = 0; x < 16; x++) {
+				wc[lpad(16 * lane + x)] = ex;
+				ex += loc[x];
+			}
+			wave_sync();
+#pragma unroll
+			for (int u = 0; u < C; u++) {
+				if (j0 + u < m) {
+					const uint32_t dg = (uint32_t) (k[u] >> sh) & 15;
+					const uint32_t pos = wc[lpad(dg * 64 + lane)] + rk[u];
+					wk[pos] = k[u];
+					wv[pos] = v[u];
+				}
+			}
+			wave_sync();
+			if (p + 1 < ls.n) {
+#pragma unroll
+				for (int u = 0; u < C; u++) {
+					k[u] = wk[j0 + u < CAP ? j0 + u : 0];
+					v[u] = wv[j0 + u < CAP ? j0 + u : 0];
+				}
+			}
 		}
-		__syncthreads();
-		for (uint32_t j = j0; j < j1; j++) {
-			const K kk = sk[cur][j];
-			const uint32_t pos = cnt[lpad(((uint32_t) (kk >> sh) & 15) * 256 + tid)]++;
-			sk[cur ^ 1][pos] = kk;
-			sv[cur ^ 1][pos] = sv[cur][j];
-		}
-		__syncthreads();
-		cur ^= 1;
 	}
-	uint64_t excl = 0;
-	uint16_t *pre = cnt;     // GID: inclusive group-start count per row
+	uint64_t run = 0;
 	if (GID) {
+		// group starts in this bucket, counted by ballots
 		uint32_t c = 0;
-		for (uint32_t j = j0; j < j1; j++)
-			c += j > 0 ? sk[cur][j] != sk[cur][j - 1] : s > 0;
-		uint32_t tot;
-		uint32_t run = block_excl(c, tot);
-		if (w == 0) {
-			const uint64_t e = mgdk_lb::lookback(status, q, tot, err);
-			if (lane == 0)
-				s_excl = e;
+#pragma unroll
+		for (int u = 0; u < C; u++) {
+			const uint32_t i = lane + 64 * u;
+			const bool st = i < m && (i > 0 ? wk[i] != wk[i - 1] : s > 0);
+			c += (uint32_t) __popcll(__ballot(st));
 		}
-		for (uint32_t j = j0; j < j1; j++) {
-			run += j > 0 ? sk[cur][j] != sk[cur][j - 1] : s > 0;
-			pre[j] = (uint16_t) run;
-		}
-		__syncthreads();
-		excl = s_excl;
+		run = mgdk_lb::lookback(status, q, c, err);
 	}
-	for (uint32_t i = tid; i < m; i += 256) {
-		emit_final<K>(fo, (BUN) s + i, sk[cur][i], sv[cur][i]);
+	const uint64_t le = (2ull << lane) - 1;     // lanes <= this one
+#pragma unroll
+	for (int u = 0; u < C; u++) {
+		const uint32_t i = lane + 64 * u;
+		uint64_t bal = 0;
 		if (GID)
-			fo.gid[(BUN) s + i] = excl + pre[i];
+			bal = __ballot(i < m && (i > 0 ? wk[i] != wk[i - 1] : s > 0));
+		if (i < m) {
+			emit_final<K>(fo, (BUN) s + i, wk[i], wv[i]);
+			if (GID)
+				fo.gid[(BUN) s + i] = run + (uint64_t) __popcll(bal & le);
+		}
+		if (GID)
+			run += (uint64_t) __popcll(bal);
 	}
 }
 
@@ -948,7 +995,7 @@ radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, int s1, int s2, ui
 				return -1;
 			if (hm[0] <= 4096) {
 				gid = true;
-				cap = hm[0] <= 2048 ? 2048 : 4096;
+				cap = hm[0] <= 1024 ? 1024 : hm[0] <= 2048 ? 2048 : 4096;
 			}
 		}
 		if (!gid)
@@ -958,13 +1005,15 @@ radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, int s1, int s2, ui
 	if (!gst.p || (gid && !hip_ok(hipMemsetAsync(gst.p, 0, (size_t) 65536 * 8 + 64, st), "memset")))
 		return -1;
 	uint32_t *gtk = (uint32_t *) (gst.as<uint64_t>() + 65536), *ger = gtk + 4;
-#define LOCAL(C, G) hipLaunchKernelGGL((k_rs_local<K, C, G>), dim3(65536), dim3(256), 0, st, (const K *) k0, \
+#define LOCAL(C, G) hipLaunchKernelGGL((k_rs_local<K, C, G>), dim3(65536), dim3(64), 0, st, (const K *) k0, \
 				       (const uint32_t *) v0, offs.as<uint32_t>(), bfirst, bnt, gd1, cnt1, ls, fo, \
 				       ovf.as<uint32_t>(), gtk, gst.as<uint64_t>(), ger, local_xg())
-	if (cap <= 2048) {
-		if (gid) LOCAL(2048, true); else LOCAL(2048, false);
+	if (cap <= 1024) {
+		if (gid) LOCAL(16, true); else LOCAL(16, false);
+	} else if (cap <= 2048) {
+		if (gid) LOCAL(32, true); else LOCAL(32, false);
 	} else {
-		if (gid) LOCAL(4096, true); else LOCAL(4096, false);
+		if (gid) LOCAL(64, true); else LOCAL(64, false);
 	}
 #undef LOCAL
 	uint32_t *h = (uint32_t *) pinned(16);
