@@ -745,8 +745,11 @@ k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *offs, const uint
 	   uint64_t *status, uint32_t *err, uint32_t xg)
 {
 	constexpr int CAP = 64 * C;
-	__shared__ K wk[CAP];
-	__shared__ uint32_t wv[CAP];
+	// row i lives at i + i / C: a lane's C consecutive rows (stride C) fall
+	// on different banks
+	__shared__ K wk[CAP + 64];
+	__shared__ uint32_t wv[CAP + 64];
+	auto sw = [](uint32_t i) { return i + i / C; };
 	__shared__ uint32_t wc[16 * 64 + 64];
 	const unsigned lane = __lane_id();
 	uint32_t q = blockIdx.x;
@@ -792,8 +795,8 @@ k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *offs, const uint
 		for (int u = 0; u < C; u++) {
 			const uint32_t i = lane + 64 * u;
 			if (i < m) {
-				wk[i] = x[u];
-				wv[i] = y[u];
+				wk[sw(i)] = x[u];
+				wv[sw(i)] = y[u];
 			}
 		}
 	}
@@ -804,8 +807,8 @@ k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *offs, const uint
 		uint32_t v[C];
 #pragma unroll
 		for (int u = 0; u < C; u++) {
-			k[u] = wk[j0 + u < CAP ? j0 + u : 0];
-			v[u] = wv[j0 + u < CAP ? j0 + u : 0];
+			k[u] = wk[sw(j0 + u)];
+			v[u] = wv[sw(j0 + u)];
 		}
 		for (int p = 0; p < ls.n; p++) {
 			const int sh = ls.s[p];
@@ -846,7 +849,7 @@ k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *offs, const uint
 			for (int u = 0; u < C; u++) {
 				if (j0 + u < m) {
 					const uint32_t dg = (uint32_t) (k[u] >> sh) & 15;
-					const uint32_t pos = wc[lpad(dg * 64 + lane)] + rk[u];
+					const uint32_t pos = sw(wc[lpad(dg * 64 + lane)] + rk[u]);
 					wk[pos] = k[u];
 					wv[pos] = v[u];
 				}
@@ -855,8 +858,8 @@ k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *offs, const uint
 			if (p + 1 < ls.n) {
 #pragma unroll
 				for (int u = 0; u < C; u++) {
-					k[u] = wk[j0 + u < CAP ? j0 + u : 0];
-					v[u] = wv[j0 + u < CAP ? j0 + u : 0];
+					k[u] = wk[sw(j0 + u)];
+					v[u] = wv[sw(j0 + u)];
 				}
 			}
 		}
@@ -868,7 +871,7 @@ k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *offs, const uint
 #pragma unroll
 		for (int u = 0; u < C; u++) {
 			const uint32_t i = lane + 64 * u;
-			const bool st = i < m && (i > 0 ? wk[i] != wk[i - 1] : s > 0);
+			const bool st = i < m && (i > 0 ? wk[sw(i)] != wk[sw(i - 1)] : s > 0);
 			c += (uint32_t) __popcll(__ballot(st));
 		}
 		run = mgdk_lb::lookback(status, q, c, err);
@@ -879,9 +882,9 @@ k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *offs, const uint
 		const uint32_t i = lane + 64 * u;
 		uint64_t bal = 0;
 		if (GID)
-			bal = __ballot(i < m && (i > 0 ? wk[i] != wk[i - 1] : s > 0));
+			bal = __ballot(i < m && (i > 0 ? wk[sw(i)] != wk[sw(i - 1)] : s > 0));
 		if (i < m) {
-			emit_final<K>(fo, (BUN) s + i, wk[i], wv[i]);
+			emit_final<K>(fo, (BUN) s + i, wk[sw(i)], wv[sw(i)]);
 			if (GID)
 				fo.gid[(BUN) s + i] = run + (uint64_t) __popcll(bal & le);
 		}
