@@ -720,17 +720,17 @@ lpad(uint32_t i)
 }
 
 // one (d1, d2) bucket per one-wave workgroup (no workgroup barriers, many
-// buckets per CU): the bucket's rows are loaded into LDS with all loads in
-// flight, each lane takes C consecutive rows into registers, and stable 4-bit
-// counting passes sort them by the remaining bits: a lane's ranks come from
-// returning LDS adds on its own (digit, lane) counter (issued back to back,
-// answered in order), one scan over the 16 x 64 counters in (digit, lane)
-// order gives the bases, the rows are placed in LDS and every lane reads its
-// next chunk back.  The sorted bucket is written out in coalesced order.
-// GID: buckets claimed per XCD; each counts its group starts (its first row
-// always starts one: consecutive buckets hold different leading digits) by
-// ballots, and a decoupled look-back over the buckets numbers them (every
-// bucket fits: the host checked the largest one first)
+// buckets per CU): the bucket's rows (R rows of 64 keys at most) are loaded
+// with all loads in flight and sorted by their remaining bits in 8-bit
+// stable LSD passes, ranked row by row as the scatter passes rank: a row's
+// same-digit lanes from a per-digit LDS lane mask (one OR, one read, one
+// clear), its rank = the digit's running count + the peers before it; one
+// scan of the 256 counts gives the bases, the rows are placed in LDS and read
+// back as rows for the next pass.  The sorted bucket leaves in coalesced
+// rows.  GID: buckets claimed per XCD; each counts its group starts (its
+// first row always starts one: consecutive buckets hold different leading
+// digits) by ballots, and a decoupled look-back over the buckets numbers
+// them (every bucket fits: the host checked the largest one first)
 __device__ __forceinline__ void
 wave_sync()
 {
@@ -738,19 +738,17 @@ wave_sync()
 	__builtin_amdgcn_wave_barrier();
 }
 
-template <typename K, int C, bool GID>
+template <typename K, int R, bool GID>
 __global__ __launch_bounds__(64) void
 k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *offs, const uint32_t *bfirst, const uint32_t *bnt,
 	   const uint32_t *bstart, const uint32_t *bcnt, Shifts ls, FinalOut fo, uint32_t *ovf, uint32_t *ticket,
 	   uint64_t *status, uint32_t *err, uint32_t xg)
 {
-	constexpr int CAP = 64 * C;
-	// row i lives at i + i / C: a lane's C consecutive rows (stride C) fall
-	// on different banks
-	__shared__ K wk[CAP + 64];
-	__shared__ uint32_t wv[CAP + 64];
-	auto sw = [](uint32_t i) { return i + i / C; };
-	__shared__ uint32_t wc[16 * 64 + 64];
+	constexpr int CAP = 64 * R;
+	__shared__ K wk[CAP];
+	__shared__ uint32_t wv[CAP];
+	__shared__ unsigned long long msk[256];
+	__shared__ uint32_t dc[256];
 	const unsigned lane = __lane_id();
 	uint32_t q = blockIdx.x;
 	if (GID) {
@@ -782,114 +780,128 @@ k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *offs, const uint
 		}
 		return;
 	}
-	{
-		K x[C];
-		uint32_t y[C];
+	const uint32_t rows = (m + 63) >> 6;
+	K k[R];
+	uint32_t v[R];
 #pragma unroll
-		for (int u = 0; u < C; u++) {
-			const uint32_t i = lane + 64 * u, ic = i < m ? i : m - 1;
-			x[u] = keys[s + ic];
-			y[u] = vals[s + ic];
+	for (int r = 0; r < R; r++) {
+		const uint32_t i = lane + 64 * r, ic = i < m ? i : m - 1;
+		k[r] = keys[s + ic];
+		v[r] = vals[s + ic];
+	}
+	const uint64_t lt = (1ull << lane) - 1;
+	bool sorted_in_lds = false;
+	for (int p = 0; p < ls.n && m > 1; p++) {
+		const int sh = ls.s[p];
+#pragma unroll
+		for (int x = 0; x < 4; x++) {
+			msk[lane + 64 * x] = 0ull;
+			dc[lane + 64 * x] = 0;
 		}
+		wave_sync();
+		uint32_t rk[R];
 #pragma unroll
-		for (int u = 0; u < C; u++) {
-			const uint32_t i = lane + 64 * u;
-			if (i < m) {
-				wk[sw(i)] = x[u];
-				wv[sw(i)] = y[u];
+		for (int r = 0; r < R; r++) {
+			rk[r] = 0;
+			if ((uint32_t) r < rows) {
+				const bool valid = lane + 64 * r < m;
+				const uint32_t dg = (uint32_t) (k[r] >> sh) & 255;
+				if (valid)
+					__hip_atomic_fetch_or(&msk[dg], 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+				wave_sync();
+				const uint64_t peer = valid ? msk[dg] : 0ull;
+				const uint32_t before = valid ? dc[dg] : 0;
+				wave_sync();
+				if (valid) {
+					msk[dg] = 0ull;
+					if ((peer >> lane) == 1)      // highest lane of its peer group
+						dc[dg] = before + (uint32_t) __popcll(peer);
+				}
+				wave_sync();
+				rk[r] = before + (uint32_t) __popcll(peer & lt);
+			}
+		}
+		// exclusive scan of the 256 digit counts (4 per lane)
+		uint32_t c4[4], sum = 0;
+#pragma unroll
+		for (int x = 0; x < 4; x++) {
+			c4[x] = dc[4 * lane + x];
+			sum += c4[x];
+		}
+		uint32_t inc = sum;
+#pragma unroll
+		for (int o = 1; o < 64; o <<= 1) {
+			const uint32_t t = __shfl_up(inc, o);
+			if (lane >= (unsigned) o)
+				inc += t;
+		}
+		uint32_t ex = inc - sum;
+		wave_sync();
+#pragma unroll
+		for (int x = 0; x < 4; x++) {
+			dc[4 * lane + x] = ex;
+			ex += c4[x];
+		}
+		wave_sync();
+#pragma unroll
+		for (int r = 0; r < R; r++) {
+			if ((uint32_t) r < rows && lane + 64 * r < m) {
+				const uint32_t pos = dc[(uint32_t) (k[r] >> sh) & 255] + rk[r];
+				wk[pos] = k[r];
+				wv[pos] = v[r];
+			}
+		}
+		wave_sync();
+		sorted_in_lds = true;
+		if (p + 1 < ls.n) {
+#pragma unroll
+			for (int r = 0; r < R; r++) {
+				if ((uint32_t) r < rows) {
+					k[r] = wk[lane + 64 * r];
+					v[r] = wv[lane + 64 * r];
+				}
 			}
 		}
 	}
-	wave_sync();
-	if (m > 1 && ls.n > 0 && !MGDK_SORT_LOCAL_NOPASS) {
-		const uint32_t j0 = lane * C;
-		K k[C];
-		uint32_t v[C];
+	if (!sorted_in_lds) {
 #pragma unroll
-		for (int u = 0; u < C; u++) {
-			k[u] = wk[sw(j0 + u)];
-			v[u] = wv[sw(j0 + u)];
-		}
-		for (int p = 0; p < ls.n; p++) {
-			const int sh = ls.s[p];
-#pragma unroll
-			for (int x = 0; x < 16; x++)
-				wc[lpad(x * 64 + lane)] = 0;
-			wave_sync();
-			uint32_t rk[C];
-#pragma unroll
-			for (int u = 0; u < C; u++) {
-				const uint32_t dg = (uint32_t) (k[u] >> sh) & 15;
-				rk[u] = j0 + u < m ? atomicAdd(&wc[lpad(dg * 64 + lane)], 1u) : 0;
+		for (int r = 0; r < R; r++)
+			if (lane + 64 * r < m) {
+				wk[lane + 64 * r] = k[r];
+				wv[lane + 64 * r] = v[r];
 			}
-			wave_sync();
-			// exclusive scan of the counters in (digit, lane) order: lane l
-			// owns the 16 entries from 16 l
-			uint32_t loc[16], sum = 0;
-#pragma unroll
-			for (int x = 0; x < 16; x++) {
-				loc[x] = wc[lpad(16 * lane + x)];
-				sum += loc[x];
-			}
-			uint32_t inc = sum;
-#pragma unroll
-			for (int o = 1; o < 64; o <<= 1) {
-				const uint32_t t = __shfl_up(inc, o);
-				if (lane >= (unsigned) o)
-					inc += t;
-			}
-			uint32_t ex = inc - sum;
-#pragma unroll
-			for (int x = 0; x < 16; x++) {
-				wc[lpad(16 * lane + x)] = ex;
-				ex += loc[x];
-			}
-			wave_sync();
-#pragma unroll
-			for (int u = 0; u < C; u++) {
-				if (j0 + u < m) {
-					const uint32_t dg = (uint32_t) (k[u] >> sh) & 15;
-					const uint32_t pos = sw(wc[lpad(dg * 64 + lane)] + rk[u]);
-					wk[pos] = k[u];
-					wv[pos] = v[u];
-				}
-			}
-			wave_sync();
-			if (p + 1 < ls.n) {
-#pragma unroll
-				for (int u = 0; u < C; u++) {
-					k[u] = wk[sw(j0 + u)];
-					v[u] = wv[sw(j0 + u)];
-				}
-			}
-		}
+		wave_sync();
 	}
 	uint64_t run = 0;
 	if (GID) {
 		// group starts in this bucket, counted by ballots
 		uint32_t c = 0;
 #pragma unroll
-		for (int u = 0; u < C; u++) {
-			const uint32_t i = lane + 64 * u;
-			const bool st = i < m && (i > 0 ? wk[sw(i)] != wk[sw(i - 1)] : s > 0);
-			c += (uint32_t) __popcll(__ballot(st));
+		for (int r = 0; r < R; r++) {
+			if ((uint32_t) r < rows) {
+				const uint32_t i = lane + 64 * r;
+				const bool st = i < m && (i > 0 ? wk[i] != wk[i - 1] : s > 0);
+				c += (uint32_t) __popcll(__ballot(st));
+			}
 		}
 		run = mgdk_lb::lookback(status, q, c, err);
 	}
 	const uint64_t le = (2ull << lane) - 1;     // lanes <= this one
 #pragma unroll
-	for (int u = 0; u < C; u++) {
-		const uint32_t i = lane + 64 * u;
-		uint64_t bal = 0;
-		if (GID)
-			bal = __ballot(i < m && (i > 0 ? wk[sw(i)] != wk[sw(i - 1)] : s > 0));
-		if (i < m) {
-			emit_final<K>(fo, (BUN) s + i, wk[sw(i)], wv[sw(i)]);
+	for (int r = 0; r < R; r++) {
+		if ((uint32_t) r < rows) {
+			const uint32_t i = lane + 64 * r;
+			uint64_t bal = 0;
 			if (GID)
-				fo.gid[(BUN) s + i] = run + (uint64_t) __popcll(bal & le);
+				bal = __ballot(i < m && (i > 0 ? wk[i] != wk[i - 1] : s > 0));
+			if (i < m) {
+				emit_final<K>(fo, (BUN) s + i, wk[i], wv[i]);
+				if (GID)
+					fo.gid[(BUN) s + i] = run + (uint64_t) __popcll(bal & le);
+			}
+			if (GID)
+				run += (uint64_t) __popcll(bal);
 		}
-		if (GID)
-			run += (uint64_t) __popcll(bal);
 	}
 }
 
@@ -977,9 +989,11 @@ radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, int s1, int s2, ui
 			   (const K *) k1, (const uint32_t *) v1, n, s2, offs.as<uint32_t>(), tmax, k0, v0, none, lbm,
 			   status, gd1, lbm + 4, sg, sort_xg());
 	// pass C: the remaining varying bits, 4 at a time, inside each (d1, d2) bucket
+	// the remaining bits in 8-bit LSD digits (the top one may reach into d2,
+	// constant inside a bucket)
 	Shifts ls{};
-	for (int q = 0; q < s2; q += 4)
-		if ((diff >> q) & 15)
+	for (int q = 0; q < s2; q += 8)
+		if ((diff >> q) & 255)
 			ls.s[ls.n++] = q;
 	FinalOut fo = fo0;
 	if (fo.want_keys)
@@ -1008,7 +1022,7 @@ radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, int s1, int s2, ui
 	if (!gst.p || (gid && !hip_ok(hipMemsetAsync(gst.p, 0, (size_t) 65536 * 8 + 64, st), "memset")))
 		return -1;
 	uint32_t *gtk = (uint32_t *) (gst.as<uint64_t>() + 65536), *ger = gtk + 4;
-#define LOCAL(C, G) hipLaunchKernelGGL((k_rs_local<K, C, G>), dim3(65536), dim3(64), 0, st, (const K *) k0, \
+#define LOCAL(R, G) hipLaunchKernelGGL((k_rs_local<K, R, G>), dim3(65536), dim3(64), 0, st, (const K *) k0, \
 				       (const uint32_t *) v0, offs.as<uint32_t>(), bfirst, bnt, gd1, cnt1, ls, fo, \
 				       ovf.as<uint32_t>(), gtk, gst.as<uint64_t>(), ger, local_xg())
 	if (cap <= 1024) {
