@@ -740,9 +740,8 @@ wave_sync()
 
 template <typename K, int R, bool GID>
 __global__ __launch_bounds__(64) void
-k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *offs, const uint32_t *bfirst, const uint32_t *bnt,
-	   const uint32_t *bstart, const uint32_t *bcnt, Shifts ls, FinalOut fo, uint32_t *ovf, uint32_t *ticket,
-	   uint64_t *status, uint32_t *err, uint32_t xg)
+k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *bs, Shifts ls, FinalOut fo, uint32_t *ovf,
+	   uint32_t *ticket, uint64_t *status, uint32_t *err, uint32_t xg)
 {
 	constexpr int CAP = 64 * R;
 	__shared__ K wk[CAP];
@@ -758,14 +757,7 @@ k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *offs, const uint
 			t = xg ? claim_tile(ticket + 8, 65536, xg) : atomicAdd(ticket, 1u);
 		q = __shfl(t, 0);
 	}
-	const uint32_t b = q >> 8, d = q & 255;
-	const uint32_t nt = bnt[b], f = bfirst[b];
-	uint32_t s = 0, m = 0;
-	if (nt != 0) {
-		s = offs[(BUN) 256 * f + (BUN) d * nt];
-		const uint32_t e = d < 255 ? offs[(BUN) 256 * f + (BUN) (d + 1) * nt] : bstart[b] + bcnt[b];
-		m = e - s;
-	}
+	const uint32_t s = bs[q], m = bs[q + 1] - s;
 	if (m == 0) {
 		if (GID)
 			(void) mgdk_lb::lookback(status, q, 0, err);
@@ -886,21 +878,53 @@ k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *offs, const uint
 		}
 		run = mgdk_lb::lookback(status, q, c, err);
 	}
-	const uint64_t le = (2ull << lane) - 1;     // lanes <= this one
+	// the bucket leaves in pairs of rows at even global positions (16-byte
+	// oid and group-id stores, 8-byte value stores where both are in the
+	// bucket)
+	const uint32_t a = s & 1;
+	const uint32_t prow = (m + a + 127) >> 7;
+	const bool fast = sizeof(K) == 4 && fo.vw == 4 && fo.sorted && fo.order && !fo.keys;
+	typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+	typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-	for (int r = 0; r < R; r++) {
-		if ((uint32_t) r < rows) {
-			const uint32_t i = lane + 64 * r;
-			uint64_t bal = 0;
-			if (GID)
-				bal = __ballot(i < m && (i > 0 ? wk[i] != wk[i - 1] : s > 0));
-			if (i < m) {
-				emit_final<K>(fo, (BUN) s + i, wk[i], wv[i]);
-				if (GID)
-					fo.gid[(BUN) s + i] = run + (uint64_t) __popcll(bal & le);
+	for (int r = 0; r < R / 2 + 1; r++) {
+		if ((uint32_t) r < prow) {
+			const int32_t i0 = (int32_t) (128 * r + 2 * lane) - (int32_t) a;   // local index of the pair
+			const bool v0 = i0 >= 0 && i0 < (int32_t) m, v1 = i0 + 1 < (int32_t) m;
+			const K k0 = v0 ? wk[i0] : (K) 0, k1 = v1 ? wk[i0 + 1] : (K) 0;
+			const uint32_t x0 = v0 ? wv[i0] : 0, x1 = v1 ? wv[i0 + 1] : 0;
+			uint64_t g0 = 0, g1 = 0;
+			if (GID) {
+				const bool f0 = v0 && (i0 > 0 ? k0 != wk[i0 - 1] : s > 0);
+				const bool f1 = v1 && (i0 + 1 > 0 ? k1 != (v0 ? k0 : wk[i0]) : s > 0);
+				const uint64_t b0 = __ballot(f0), b1 = __ballot(f1);
+				g0 = run + (uint64_t) (__popcll(b0 & lt) + __popcll(b1 & lt)) + f0;
+				g1 = g0 + f1;
+				run += (uint64_t) (__popcll(b0) + __popcll(b1));
 			}
-			if (GID)
-				run += (uint64_t) __popcll(bal);
+			const BUN g = (BUN) s + (BUN) i0;
+			if (fast && v0 && v1) {
+				uint32_t u0 = (uint32_t) k0, u1 = (uint32_t) k1;
+				if (fo.reverse) {
+					u0 = ~u0;
+					u1 = ~u1;
+				}
+				*(u32x2 *) ((int32_t *) fo.sorted + g) = (u32x2){u0 ^ 0x80000000u, u1 ^ 0x80000000u};
+				*(u64x2 *) (fo.order + g) = (u64x2){fo.hseq + x0, fo.hseq + x1};
+				if (GID)
+					*(u64x2 *) (fo.gid + g) = (u64x2){g0, g1};
+			} else {
+				if (v0) {
+					emit_final<K>(fo, g, k0, x0);
+					if (GID)
+						fo.gid[g] = g0;
+				}
+				if (v1) {
+					emit_final<K>(fo, g + 1, k1, x1);
+					if (GID)
+						fo.gid[g + 1] = g1;
+				}
+			}
 		}
 	}
 }
@@ -908,16 +932,19 @@ k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *offs, const uint
 // the largest (d1, d2) bucket (decides the LDS capacity / the GID variant)
 __global__ __launch_bounds__(256) void
 k_bucket_max(const uint32_t *offs, const uint32_t *bfirst, const uint32_t *bnt, const uint32_t *bstart,
-	     const uint32_t *bcnt, uint32_t *mx)
+	     const uint32_t *bcnt, uint32_t *mx, uint32_t *bs)
 {
 	const uint32_t q = blockIdx.x * 256 + threadIdx.x, b = q >> 8, d = q & 255;
 	const uint32_t nt = bnt[b], f = bfirst[b];
-	uint32_t m = 0;
+	uint32_t m = 0, s = bstart[b];
 	if (nt != 0) {
-		const uint32_t s = offs[(BUN) 256 * f + (BUN) d * nt];
+		s = offs[(BUN) 256 * f + (BUN) d * nt];
 		const uint32_t e = d < 255 ? offs[(BUN) 256 * f + (BUN) (d + 1) * nt] : bstart[b] + bcnt[b];
 		m = e - s;
 	}
+	bs[q] = s;
+	if (q == 65535)
+		bs[65536] = bstart[b] + bcnt[b];
 	m = block_reduce(m, [](uint32_t x, uint32_t y) { return x > y ? x : y; });
 	if (threadIdx.x == 0)
 		atomicMax(mx, m);
@@ -998,16 +1025,18 @@ radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, int s1, int s2, ui
 	FinalOut fo = fo0;
 	if (fo.want_keys)
 		fo.keys = k1;
+	// every (d1, d2) bucket's start, and the largest bucket (the group ids
+	// ride along only when every bucket fits in LDS)
+	DevBuf bsb((size_t) (65536 + 1) * 4 + 64);
+	uint32_t *mx = count + 768, *hm = (uint32_t *) pinned(16);
+	if (!bsb.p || !hm || !hip_ok(hipMemsetAsync(mx, 0, 4, st), "memset"))
+		return -1;
+	hipLaunchKernelGGL(k_bucket_max, dim3(256), dim3(256), 0, st, (const uint32_t *) offs.as<uint32_t>(),
+			   (const uint32_t *) bfirst, (const uint32_t *) bnt, gd1, cnt1, mx, bsb.as<uint32_t>());
 	bool gid = false;
 	if (fo.gid != nullptr) {
-		// group ids with the rows need every bucket in LDS: the largest first
 		static const bool use_fg = getenv("MGDK_SORT_FUSEGID") ? atoi(getenv("MGDK_SORT_FUSEGID")) != 0 : true;
-		uint32_t *mx = count + 768, *hm = (uint32_t *) pinned(16);
 		if (use_fg) {
-			if (!hm || !hip_ok(hipMemsetAsync(mx, 0, 4, st), "memset"))
-				return -1;
-			hipLaunchKernelGGL(k_bucket_max, dim3(256), dim3(256), 0, st, (const uint32_t *) offs.as<uint32_t>(),
-					   (const uint32_t *) bfirst, (const uint32_t *) bnt, gd1, cnt1, mx);
 			if (!hip_ok(hipMemcpyAsync(hm, mx, 4, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
 				return -1;
 			if (hm[0] <= 4096) {
@@ -1023,8 +1052,8 @@ radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, int s1, int s2, ui
 		return -1;
 	uint32_t *gtk = (uint32_t *) (gst.as<uint64_t>() + 65536), *ger = gtk + 4;
 #define LOCAL(R, G) hipLaunchKernelGGL((k_rs_local<K, R, G>), dim3(65536), dim3(64), 0, st, (const K *) k0, \
-				       (const uint32_t *) v0, offs.as<uint32_t>(), bfirst, bnt, gd1, cnt1, ls, fo, \
-				       ovf.as<uint32_t>(), gtk, gst.as<uint64_t>(), ger, local_xg())
+				       (const uint32_t *) v0, (const uint32_t *) bsb.as<uint32_t>(), ls, fo, ovf.as<uint32_t>(), gtk, \
+				       gst.as<uint64_t>(), ger, local_xg())
 	if (cap <= 1024) {
 		if (gid) LOCAL(16, true); else LOCAL(16, false);
 	} else if (cap <= 2048) {
