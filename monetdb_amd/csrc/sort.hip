@@ -738,50 +738,17 @@ wave_sync()
 	__builtin_amdgcn_wave_barrier();
 }
 
-template <typename K, int R, bool GID>
-__global__ __launch_bounds__(64) void
-k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *bs, Shifts ls, FinalOut fo, uint32_t *ovf,
-	   uint32_t *ticket, uint64_t *status, uint32_t *err, uint32_t xg)
+// sorts the rows held in k / v (row r = rows 64 r .. 64 r + 63 of the
+// bucket, m of them) by the bits of ls; the sorted bucket is left in wk / wv
+template <typename K, int R>
+__device__ __forceinline__ void
+local_sort(K (&k)[R], uint32_t (&v)[R], uint32_t m, const Shifts &ls, K *wk, uint32_t *wv,
+	   unsigned long long *msk, uint32_t *dc)
 {
-	constexpr int CAP = 64 * R;
-	__shared__ K wk[CAP];
-	__shared__ uint32_t wv[CAP];
-	__shared__ unsigned long long msk[256];
-	__shared__ uint32_t dc[256];
 	const unsigned lane = __lane_id();
-	uint32_t q = blockIdx.x;
-	if (GID) {
-		// one ticket word saturates near 88 claims / us: claim per XCD
-		uint32_t t = 0;
-		if (lane == 0)
-			t = xg ? claim_tile(ticket + 8, 65536, xg) : atomicAdd(ticket, 1u);
-		q = __shfl(t, 0);
-	}
-	const uint32_t s = bs[q], m = bs[q + 1] - s;
-	if (m == 0) {
-		if (GID)
-			(void) mgdk_lb::lookback(status, q, 0, err);
-		return;
-	}
-	if (m > (uint32_t) CAP) {
-		// sorted by the host afterwards (rare: the gate expects <= CAP / 2)
-		if (lane == 0) {
-			const uint32_t o = atomicAdd(&ovf[0], 1u);
-			ovf[1 + 2 * o] = s;
-			ovf[2 + 2 * o] = m;
-		}
-		return;
-	}
 	const uint32_t rows = (m + 63) >> 6;
-	K k[R];
-	uint32_t v[R];
-#pragma unroll
-	for (int r = 0; r < R; r++) {
-		const uint32_t i = lane + 64 * r, ic = i < m ? i : m - 1;
-		k[r] = keys[s + ic];
-		v[r] = vals[s + ic];
-	}
 	const uint64_t lt = (1ull << lane) - 1;
+	wave_sync();
 	bool sorted_in_lds = false;
 	for (int p = 0; p < ls.n && m > 1; p++) {
 		const int sh = ls.s[p];
@@ -864,23 +831,17 @@ k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *bs, Shifts ls, F
 			}
 		wave_sync();
 	}
-	uint64_t run = 0;
-	if (GID) {
-		// group starts in this bucket, counted by ballots
-		uint32_t c = 0;
-#pragma unroll
-		for (int r = 0; r < R; r++) {
-			if ((uint32_t) r < rows) {
-				const uint32_t i = lane + 64 * r;
-				const bool st = i < m && (i > 0 ? wk[i] != wk[i - 1] : s > 0);
-				c += (uint32_t) __popcll(__ballot(st));
-			}
-		}
-		run = mgdk_lb::lookback(status, q, c, err);
-	}
-	// the bucket leaves in pairs of rows at even global positions (16-byte
-	// oid and group-id stores, 8-byte value stores where both are in the
-	// bucket)
+}
+
+// the sorted bucket in wk / wv leaves in pairs of rows at even global
+// positions (16-byte oid and group-id stores, 8-byte value stores where both
+// are in the bucket); GID: run = the group id before the bucket's first row
+template <typename K, int R, bool GID>
+__device__ __forceinline__ void
+local_emit(uint32_t s, uint32_t m, const FinalOut &fo, uint64_t run, const K *wk, const uint32_t *wv)
+{
+	const unsigned lane = __lane_id();
+	const uint64_t lt = (1ull << lane) - 1;
 	const uint32_t a = s & 1;
 	const uint32_t prow = (m + a + 127) >> 7;
 	const bool fast = sizeof(K) == 4 && fo.vw == 4 && fo.sorted && fo.order && !fo.keys;
@@ -926,6 +887,120 @@ k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *bs, Shifts ls, F
 				}
 			}
 		}
+	}
+}
+
+template <typename K, int R>
+__device__ __forceinline__ void
+local_load(const K *keys, const uint32_t *vals, uint32_t s, uint32_t m, K (&k)[R], uint32_t (&v)[R])
+{
+	const unsigned lane = __lane_id();
+#pragma unroll
+	for (int r = 0; r < R; r++) {
+		const uint32_t i = lane + 64 * r, ic = i < m ? i : (m ? m - 1 : 0);
+		k[r] = keys[s + ic];
+		v[r] = vals[s + ic];
+	}
+}
+
+template <typename K, int R, bool GID>
+__global__ __launch_bounds__(64) void
+k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *bs, Shifts ls, FinalOut fo, uint32_t *ovf,
+	   uint32_t *ticket, uint64_t *status, uint32_t *err, uint32_t xg)
+{
+	constexpr int CAP = 64 * R;
+	__shared__ K wk[CAP];
+	__shared__ uint32_t wv[CAP];
+	__shared__ unsigned long long msk[256];
+	__shared__ uint32_t dc[256];
+	const unsigned lane = __lane_id();
+	uint32_t q = blockIdx.x;
+	if (GID) {
+		// one ticket word saturates near 88 claims / us: claim per XCD
+		uint32_t t = 0;
+		if (lane == 0)
+			t = xg ? claim_tile(ticket + 8, 65536, xg) : atomicAdd(ticket, 1u);
+		q = __shfl(t, 0);
+	}
+	const uint32_t s = bs[q], m = bs[q + 1] - s;
+	if (m == 0) {
+		if (GID)
+			(void) mgdk_lb::lookback(status, q, 0, err);
+		return;
+	}
+	if (m > (uint32_t) CAP) {
+		// sorted by the host afterwards (rare: the gate expects <= CAP / 2)
+		if (lane == 0) {
+			const uint32_t o = atomicAdd(&ovf[0], 1u);
+			ovf[1 + 2 * o] = s;
+			ovf[2 + 2 * o] = m;
+		}
+		return;
+	}
+	K k[R];
+	uint32_t v[R];
+	local_load<K, R>(keys, vals, s, m, k, v);
+	local_sort<K, R>(k, v, m, ls, wk, wv, msk, dc);
+	uint64_t run = 0;
+	if (GID) {
+		// group starts in this bucket, counted by ballots
+		uint32_t c = 0;
+		const uint32_t rows = (m + 63) >> 6;
+#pragma unroll
+		for (int r = 0; r < R; r++) {
+			if ((uint32_t) r < rows) {
+				const uint32_t i = lane + 64 * r;
+				const bool st = i < m && (i > 0 ? wk[i] != wk[i - 1] : s > 0);
+				c += (uint32_t) __popcll(__ballot(st));
+			}
+		}
+		run = mgdk_lb::lookback(status, q, c, err);
+	}
+	local_emit<K, R, GID>(s, m, fo, run, wk, wv);
+}
+
+// BPW consecutive buckets per one-wave workgroup, the next bucket's rows
+// loaded while the current one is sorted (no group ids: those need every
+// bucket's predecessors, see k_rs_local<GID>)
+template <typename K, int R, int BPW>
+__global__ __launch_bounds__(64) void
+k_rs_local_mb(const K *keys, const uint32_t *vals, const uint32_t *bs, Shifts ls, FinalOut fo, uint32_t *ovf)
+{
+	constexpr int CAP = 64 * R;
+	__shared__ K wk[CAP];
+	__shared__ uint32_t wv[CAP];
+	__shared__ unsigned long long msk[256];
+	__shared__ uint32_t dc[256];
+	const unsigned lane = __lane_id();
+	const uint32_t q0 = blockIdx.x * BPW;
+	const uint32_t bl = lane <= (unsigned) BPW ? bs[q0 + lane] : 0;
+	K k[2][R];
+	uint32_t v[2][R];
+	{
+		const uint32_t s0 = __shfl(bl, 0), m0 = __shfl(bl, 1) - s0;
+		if (m0 <= (uint32_t) CAP)
+			local_load<K, R>(keys, vals, s0, m0, k[0], v[0]);
+	}
+#pragma unroll
+	for (int j = 0; j < BPW; j++) {
+		const uint32_t s = __shfl(bl, j), m = __shfl(bl, j + 1) - s;
+		if (j + 1 < BPW) {
+			const uint32_t s1 = __shfl(bl, j + 1), m1 = __shfl(bl, j + 2) - s1;
+			if (m1 <= (uint32_t) CAP)
+				local_load<K, R>(keys, vals, s1, m1, k[(j + 1) & 1], v[(j + 1) & 1]);
+		}
+		if (m == 0)
+			continue;
+		if (m > (uint32_t) CAP) {
+			if (lane == 0) {
+				const uint32_t o = atomicAdd(&ovf[0], 1u);
+				ovf[1 + 2 * o] = s;
+				ovf[2 + 2 * o] = m;
+			}
+			continue;
+		}
+		local_sort<K, R>(k[j & 1], v[j & 1], m, ls, wk, wv, msk, dc);
+		local_emit<K, R, false>(s, m, fo, 0, wk, wv);
 	}
 }
 
@@ -1033,39 +1108,38 @@ radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, int s1, int s2, ui
 		return -1;
 	hipLaunchKernelGGL(k_bucket_max, dim3(256), dim3(256), 0, st, (const uint32_t *) offs.as<uint32_t>(),
 			   (const uint32_t *) bfirst, (const uint32_t *) bnt, gd1, cnt1, mx, bsb.as<uint32_t>());
-	bool gid = false;
-	if (fo.gid != nullptr) {
-		static const bool use_fg = getenv("MGDK_SORT_FUSEGID") ? atoi(getenv("MGDK_SORT_FUSEGID")) != 0 : true;
-		if (use_fg) {
-			if (!hip_ok(hipMemcpyAsync(hm, mx, 4, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
-				return -1;
-			if (hm[0] <= 4096) {
-				gid = true;
-				cap = hm[0] <= 1024 ? 1024 : hm[0] <= 2048 ? 2048 : 4096;
-			}
-		}
-		if (!gid)
-			fo.gid = nullptr;
-	}
+	// the LDS capacity from the largest bucket
+	if (!hip_ok(hipMemcpyAsync(hm, mx, 4, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+		return -1;
+	if (hm[0] <= 4096)
+		cap = hm[0] <= 1024 ? 1024 : hm[0] <= 2048 ? 2048 : 4096;
+	static const bool use_fg = getenv("MGDK_SORT_FUSEGID") ? atoi(getenv("MGDK_SORT_FUSEGID")) != 0 : true;
+	const bool gid = fo.gid != nullptr && use_fg && hm[0] <= 4096;
+	if (!gid)
+		fo.gid = nullptr;
 	DevBuf gst(gid ? (size_t) 65536 * 8 + 64 : 64);
 	if (!gst.p || (gid && !hip_ok(hipMemsetAsync(gst.p, 0, (size_t) 65536 * 8 + 64, st), "memset")))
 		return -1;
-	uint32_t *gtk = (uint32_t *) (gst.as<uint64_t>() + 65536), *ger = gtk + 4;
+	// GID: the ticket words and the error flag follow the 65536 status words
+	uint32_t *gtk = gid ? (uint32_t *) (gst.as<uint64_t>() + 65536) : gst.as<uint32_t>(), *ger = gtk + 4;
 #define LOCAL(R, G) hipLaunchKernelGGL((k_rs_local<K, R, G>), dim3(65536), dim3(64), 0, st, (const K *) k0, \
 				       (const uint32_t *) v0, (const uint32_t *) bsb.as<uint32_t>(), ls, fo, ovf.as<uint32_t>(), gtk, \
 				       gst.as<uint64_t>(), ger, local_xg())
+#define LOCALMB(R) hipLaunchKernelGGL((k_rs_local_mb<K, R, 4>), dim3(65536 / 4), dim3(64), 0, st, (const K *) k0, \
+				      (const uint32_t *) v0, (const uint32_t *) bsb.as<uint32_t>(), ls, fo, ovf.as<uint32_t>())
 	if (cap <= 1024) {
-		if (gid) LOCAL(16, true); else LOCAL(16, false);
+		if (gid) LOCAL(16, true); else LOCALMB(16);
 	} else if (cap <= 2048) {
-		if (gid) LOCAL(32, true); else LOCAL(32, false);
+		if (gid) LOCAL(32, true); else LOCALMB(32);
 	} else {
-		if (gid) LOCAL(64, true); else LOCAL(64, false);
+		if (gid) LOCAL(64, true); else LOCALMB(64);
 	}
+#undef LOCALMB
 #undef LOCAL
 	uint32_t *h = (uint32_t *) pinned(16);
 	if (!h || !hip_ok(hipMemcpyAsync(h, ovf.p, 4, hipMemcpyDeviceToHost, st), "memcpy") ||
 	    !hip_ok(hipMemcpyAsync(h + 1, lbm + 4, 4, hipMemcpyDeviceToHost, st), "memcpy") ||
-	    !hip_ok(hipMemcpyAsync(h + 2, ger, 4, hipMemcpyDeviceToHost, st), "memcpy") ||
+	    (gid && !hip_ok(hipMemcpyAsync(h + 2, ger, 4, hipMemcpyDeviceToHost, st), "memcpy")) ||
 	    (gid && !hip_ok(hipMemcpyAsync(h + 4, fo.gid + n - 1, 8, hipMemcpyDeviceToHost, st), "memcpy")) || !sync())
 		return -1;
 	if (h[1] || (gid && h[2])) {
