@@ -14,6 +14,13 @@ from helpers import rng, with_nils
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def _hybrid_on(monkeypatch):
+    """the path is off by default (slower than the LSD passes at 100M int32,
+    DESIGN §9); the library reads the switch on every call"""
+    monkeypatch.setenv("MGDK_SORT_HYBRID", "1")
+
 N = (1 << 22) + 12_345
 
 
