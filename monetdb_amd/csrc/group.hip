@@ -209,6 +209,7 @@ constexpr uint32_t GL_SLOTS = 4096;
 constexpr uint32_t GL_MAXG = 3072;
 constexpr uint64_t GL_EMPTY = ~0ull;
 constexpr BUN GL_TILE = 65536;
+constexpr BUN GL_FTILE = 8192;            // rows per workgroup of the first-occurrence pass
 
 __device__ __forceinline__ uint64_t
 gl_key(const KeySrc &s, BUN i)
@@ -273,7 +274,9 @@ k_gl_first(KeySrc s, BUN n, BUN tile0, unsigned long long *gkey, unsigned long l
 	if (tid == 0)
 		lmin[GL_SLOTS] = ~0u;
 	__syncthreads();
-	const BUN a = ((BUN) blockIdx.x + tile0) * GL_TILE, e = min(n, a + GL_TILE);
+	// GL_FTILE rows per workgroup from tile tile0 on: many small tables
+	// fill the chip where one per 64 Ki-row tile left it idle
+	const BUN a = tile0 * GL_TILE + (BUN) blockIdx.x * GL_FTILE, e = min(n, a + GL_FTILE);
 	bool ovf = false;
 	for (BUN i0 = a + tid; i0 < e; i0 += (BUN) GL_U * blockDim.x) {
 		uint64_t kk[GL_U];
@@ -343,9 +346,12 @@ k_gl_first(KeySrc s, BUN n, BUN tile0, unsigned long long *gkey, unsigned long l
 	}
 }
 
-// one workgroup: occupied slots ranked by first row (counting ranks over
-// the compacted keys first << 13 | slot, all distinct) -> group ids, extents
-__global__ __launch_bounds__(1024) void
+// occupied slots ranked by first row (counting ranks over the compacted
+// keys first << 13 | slot, all distinct) -> group ids, extents.  Every
+// workgroup compacts the table (in its own order: the ranks compare values)
+// and ranks its share of the entries
+constexpr unsigned GL_ORDER_WG = (GL_MAXG + 255) / 256;
+__global__ __launch_bounds__(256) void
 k_gl_order(const unsigned long long *gmin, uint32_t *gmap, bool cdense, oid cseq, const oid *coids, oid *ext,
 	   uint32_t *ngrp)
 {
@@ -362,7 +368,7 @@ k_gl_order(const unsigned long long *gmin, uint32_t *gmap, bool cdense, oid cseq
 	}
 	__syncthreads();
 	const uint32_t c = s_cnt;
-	for (uint32_t i = tid; i < c; i += blockDim.x) {
+	for (uint32_t i = blockIdx.x * blockDim.x + tid; i < c; i += gridDim.x * blockDim.x) {
 		const unsigned long long v = sk[i];
 		uint32_t r = 0;
 		for (uint32_t j = 0; j < c; j++)
@@ -371,7 +377,7 @@ k_gl_order(const unsigned long long *gmin, uint32_t *gmap, bool cdense, oid cseq
 		gmap[slot] = r;
 		ext[r] = cdense ? cseq + (BUN) (v >> 13) : coids[v >> 13];
 	}
-	if (tid == 0)
+	if (tid == 0 && blockIdx.x == 0)
 		*ngrp = c;
 }
 
@@ -605,10 +611,11 @@ group_lds(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mg
 	unsigned done = 0;          // tiles the first pass has read
 	unsigned upto = prefix > 0 && prefix < tiles ? prefix : tiles;
 	for (;;) {
-		GL_LAUNCH(k_gl_first, dim3(upto - done), dim3(1024), 0, st, ks, n, (BUN) done, gkey.as<unsigned long long>(),
-			  gmin.as<unsigned long long>(), &m[0]);
+		const BUN frows = min(n, (BUN) upto * GL_TILE) - (BUN) done * GL_TILE;
+		GL_LAUNCH(k_gl_first, dim3((unsigned) ((frows + GL_FTILE - 1) / GL_FTILE)), dim3(1024), 0, st, ks, n, (BUN) done,
+			  gkey.as<unsigned long long>(), gmin.as<unsigned long long>(), &m[0]);
 		done = upto;
-		hipLaunchKernelGGL(k_gl_order, dim3(1), dim3(1024), 0, st, gmin.as<unsigned long long>(), gmap.as<uint32_t>(),
+		hipLaunchKernelGGL(k_gl_order, dim3(GL_ORDER_WG), dim3(256), 0, st, gmin.as<unsigned long long>(), gmap.as<uint32_t>(),
 				   ci.dense, ci.seq, ci.oids, ext.as<oid>(), &m[1]);
 		if (!hip_ok(hipMemcpyAsync(h, m, 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
 			return -1;
