@@ -227,7 +227,10 @@ pinned(size_t bytes)
 	if (tctx.pinned_size < bytes) {
 		if (tctx.pinned)
 			(void) hipHostFree(tctx.pinned);
-		size_t n = bytes < 4096 ? 4096 : bytes;
+		// 1 MiB at least: a caller may hold the buffer across an operator
+		// that asks for a few KiB more (a reallocation would leave it
+		// dangling)
+		size_t n = bytes < (1u << 20) ? (size_t) 1 << 20 : bytes;
 		if (hipHostMalloc(&tctx.pinned, n, hipHostMallocDefault) != hipSuccess) {
 			tctx.pinned = nullptr;
 			tctx.pinned_size = 0;
