@@ -348,26 +348,46 @@ k_gl_first(KeySrc s, BUN n, BUN tile0, unsigned long long *gkey, unsigned long l
 
 // occupied slots ranked by first row (counting ranks over the compacted
 // keys first << 13 | slot, all distinct) -> group ids, extents.  Every
-// workgroup compacts the table (in its own order: the ranks compare values)
-// and ranks its share of the entries
+// workgroup compacts the table in slot order (a scan, so all workgroups
+// hold the same list) and ranks its share of the entries
 constexpr unsigned GL_ORDER_WG = (GL_MAXG + 255) / 256;
 __global__ __launch_bounds__(256) void
 k_gl_order(const unsigned long long *gmin, uint32_t *gmap, bool cdense, oid cseq, const oid *coids, oid *ext,
 	   uint32_t *ngrp)
 {
 	__shared__ unsigned long long sk[GL_SLOTS + 1];
-	__shared__ uint32_t s_cnt;
-	const unsigned tid = threadIdx.x;
-	if (tid == 0)
-		s_cnt = 0;
-	__syncthreads();
-	for (uint32_t q = tid; q <= GL_SLOTS; q += blockDim.x) {
-		const unsigned long long f = gmin[q];
-		if (f != ~0ull)
-			sk[atomicAdd(&s_cnt, 1u)] = (f << 13) | q;
+	__shared__ uint32_t ws[4];
+	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+	// thread t holds slots 16 t .. 16 t + 15 (and thread 255 the extra slot GL_SLOTS)
+	constexpr uint32_t PER = GL_SLOTS / 256;
+	unsigned long long f[PER + 1];
+	uint32_t cnt = 0;
+#pragma unroll
+	for (uint32_t x = 0; x < PER; x++) {
+		f[x] = gmin[tid * PER + x];
+		cnt += f[x] != ~0ull;
 	}
+	f[PER] = tid == 255 ? gmin[GL_SLOTS] : ~0ull;
+	cnt += f[PER] != ~0ull;
+	uint32_t inc = cnt;
+#pragma unroll
+	for (int o = 1; o < 64; o <<= 1) {
+		const uint32_t t = __shfl_up(inc, o);
+		if (lane >= (unsigned) o)
+			inc += t;
+	}
+	if (lane == 63)
+		ws[w] = inc;
 	__syncthreads();
-	const uint32_t c = s_cnt;
+	uint32_t pos = inc - cnt;
+	for (unsigned k = 0; k < w; k++)
+		pos += ws[k];
+	const uint32_t c = ws[0] + ws[1] + ws[2] + ws[3];
+#pragma unroll
+	for (uint32_t x = 0; x <= PER; x++)
+		if (f[x] != ~0ull)
+			sk[pos++] = (f[x] << 13) | (x < PER ? tid * PER + x : GL_SLOTS);
+	__syncthreads();
 	for (uint32_t i = blockIdx.x * blockDim.x + tid; i < c; i += gridDim.x * blockDim.x) {
 		const unsigned long long v = sk[i];
 		uint32_t r = 0;
