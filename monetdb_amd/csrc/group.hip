@@ -581,6 +581,122 @@ k_gl_assign_v(KeySrc s, BUN n, const unsigned long long *gkey, const uint32_t *g
 			atomicAdd(&histo[q], (unsigned long long) lh[q]);
 }
 
+// the assign pass for dense 4-byte keys without prior groups: the table is
+// rebuilt per workgroup as ONE 8-byte LDS word per slot (key << 32 | id,
+// ~0 = empty) under a 32-bit hash, so a probe is one LDS read and one
+// 32-bit compare (the 8-byte key table + id map took two reads and 64-bit
+// arithmetic), and the smaller table leaves room for a third workgroup per CU
+__device__ __forceinline__ uint32_t
+gl_hash32(uint32_t k)
+{
+	return (k * 0x9E3779B1u) >> 20;
+}
+
+__global__ __launch_bounds__(1024) void
+k_gl_assign_v32(KeySrc s, BUN n, const unsigned long long *gkey, const uint32_t *gmap, uint32_t ngrp, oid *gid,
+		uint8_t *img, unsigned long long *histo, uint32_t *unsorted, uint32_t *miss)
+{
+	static_assert(GL_SLOTS == 4096, "12-bit hash");
+	constexpr int V = 4;
+	__shared__ unsigned long long tab[GL_SLOTS];
+	__shared__ uint32_t lh[GL_MAXG];
+	const unsigned tid = threadIdx.x;
+	for (uint32_t q = tid; q < GL_SLOTS; q += blockDim.x)
+		tab[q] = GL_EMPTY;
+	for (uint32_t q = tid; q < ngrp; q += blockDim.x)
+		lh[q] = 0;
+	__syncthreads();
+	for (uint32_t q = tid; q < GL_SLOTS; q += blockDim.x) {
+		const unsigned long long k = gkey[q];
+		if (k == GL_EMPTY)
+			continue;
+		const unsigned long long ent = (k << 32) | gmap[q];
+		uint32_t h = gl_hash32((uint32_t) k);
+		while (atomicCAS(&tab[h], GL_EMPTY, ent) != GL_EMPTY)
+			h = (h + 1) & (GL_SLOTS - 1);
+	}
+	__syncthreads();
+	auto look = [&](uint32_t k) -> uint32_t {
+		uint32_t h = gl_hash32(k);
+		for (;;) {
+			const unsigned long long e = tab[h];
+			if (e == GL_EMPTY)
+				return ~0u;
+			if ((uint32_t) (e >> 32) == k)
+				return (uint32_t) e;
+			h = (h + 1) & (GL_SLOTS - 1);
+		}
+	};
+	const BUN a = (BUN) blockIdx.x * GL_TILE, e = min(n, a + GL_TILE);
+	const uint32_t *kb = (const uint32_t *) s.base + s.off;
+	uint32_t uns = 0;
+	bool mis = false;
+	typedef uint32_t kv __attribute__((ext_vector_type(V)));
+	constexpr BUN STEP = 1024 * V;
+	for (BUN r0 = a + (BUN) tid * V; r0 < e; r0 += STEP) {
+		uint32_t k[V];
+		if (r0 + V <= e) {
+			const kv x = __builtin_nontemporal_load((const kv *) (kb + r0));
+#pragma unroll
+			for (int u = 0; u < V; u++)
+				k[u] = x[u];
+		} else {
+#pragma unroll
+			for (int u = 0; u < V; u++)
+				k[u] = kb[r0 + u < e ? r0 + u : e - 1];
+		}
+		const uint32_t before = kb[r0 > 0 ? r0 - 1 : 0];
+		uint32_t g[V], gp = 0;
+#pragma unroll
+		for (int u = 0; u < V; u++) {
+			g[u] = look(k[u]);
+			if (g[u] == ~0u) {
+				mis = true;
+				g[u] = 0;
+			}
+		}
+		if (r0 > 0)
+			gp = look(before);
+		mis |= gp == ~0u && r0 > 0;
+#pragma unroll
+		for (int u = 0; u < V; u++) {
+			const BUN i = r0 + u;
+			if (i < e) {
+				atomicAdd(&lh[g[u]], 1u);
+				const uint32_t prev = u == 0 ? gp : g[u - 1];
+				if (i > 0 && prev > g[u])
+					uns = 1;
+			}
+		}
+		if (r0 + V <= e) {
+			typedef unsigned long long o2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+			for (int u = 0; u < V; u += 2)
+				__builtin_nontemporal_store((o2){g[u], g[u + 1]}, (o2 *) (gid + r0 + u));
+			if (img) {
+				const uint32_t w4 = g[0] | (g[1] << 8) | (g[2] << 16) | (g[3] << 24);
+				*(uint32_t *) (img + r0) = w4;
+			}
+		} else {
+#pragma unroll
+			for (int u = 0; u < V; u++)
+				if (r0 + u < e) {
+					gid[r0 + u] = g[u];
+					if (img)
+						img[r0 + u] = (uint8_t) g[u];
+				}
+		}
+	}
+	if (__any(uns) && __lane_id() == 0)
+		publish_or(unsorted, 1u);
+	if (__any(mis) && __lane_id() == 0)
+		publish_or(miss, 1u);
+	__syncthreads();
+	for (uint32_t q = tid; q < ngrp; q += blockDim.x)
+		if (lh[q])
+			atomicAdd(&histo[q], (unsigned long long) lh[q]);
+}
+
 // returns 1 when the path does not apply (too many groups).  The first
 // pass reads only a prefix of GL_PREFIX tiles first: the groups it finds
 // are numbered, and they are ALL the groups unless the assign pass meets a
@@ -663,7 +779,12 @@ group_lds(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mg
 		// the vector form needs 16-byte aligned keys and ids
 		const bool vec = fg == 0 && (fw == 4 || fw == 8) && (((uintptr_t) ks.base + ks.off * fw) & 15) == 0 &&
 				 ((uintptr_t) gn->theap & 15) == 0 && (!img || ((uintptr_t) img & 3) == 0);
-		if (vec && fw == 4)
+		static const bool v32 = getenv("MGDK_GROUP_V32") ? atoi(getenv("MGDK_GROUP_V32")) != 0 : true;
+		if (vec && fw == 4 && v32)
+			hipLaunchKernelGGL(k_gl_assign_v32, dim3(tiles), dim3(1024), 0, st, ks, n, gkey.as<unsigned long long>(),
+					   gmap.as<uint32_t>(), ngrp, (oid *) gn->theap, img, (unsigned long long *) hn->theap,
+					   &m[2], &m[3]);
+		else if (vec && fw == 4)
 			hipLaunchKernelGGL(k_gl_assign_v<4>, dim3(tiles), dim3(1024), 0, st, ks, n, gkey.as<unsigned long long>(),
 					   gmap.as<uint32_t>(), ngrp, (oid *) gn->theap, img, (unsigned long long *) hn->theap,
 					   &m[2], &m[3]);
