@@ -1033,13 +1033,17 @@ k_final_copy_at(const K *keys, const uint32_t *vals, BUN m, BUN s, FinalOut fo)
 		emit_final<K>(fo, s + i, keys[i], vals[i]);
 }
 
-// tiles per XCD group of the scatter passes (0: plain ticket order); 64
-// measured best on 100M int32 (2.79 vs 3.00 ms)
+// tiles per XCD group of the scatter passes (0: plain ticket order).  A
+// group must not exceed the workgroups one XCD runs at once (32 CUs x
+// workgroups per CU): the first tile of the next XCD's group waits for the
+// whole group before it (128 / 256 measured 9.4 ms / look-back timeout on
+// 100M int32, 32 2.94, 64 2.79-2.84, 0 2.99 -- DESIGN §9).  4-byte keys run
+// two scatter workgroups per CU, 8-byte keys one
 static uint32_t
-sort_xg()
+sort_xg(int kw = 4)
 {
 	const char *e = getenv("MGDK_SORT_XCDG");
-	return e ? (uint32_t) atoi(e) : 64u;
+	return e ? (uint32_t) atoi(e) : kw == 4 ? 64u : 32u;
 }
 
 // buckets per XCD group of the local pass's claims (0: one ticket word)
@@ -1079,7 +1083,7 @@ radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, int s1, int s2, ui
 	    !hip_ok(hipMemsetAsync(ovf.p, 0, 4, st), "memset"))
 		return -1;
 	hipLaunchKernelGGL((k_rs_scatter<K, false, true, true, false>), dim3(nblocks), dim3(Tile<K>::THREADS), 0, st, k0,
-			   v0, n, s1, nullptr, nblocks, k1, v1, none, lbm, status, gd1, lbm + 4, SegTiles{}, sort_xg());
+			   v0, n, s1, nullptr, nblocks, k1, v1, none, lbm, status, gd1, lbm + 4, SegTiles{}, sort_xg((int) sizeof(K)));
 	// pass B: by d2 inside the d1 buckets
 	hipLaunchKernelGGL(k_seg_tiles, dim3(1), dim3(256), 0, st, cnt1, gd1, TILE, desc.as<uint4>(), count, bfirst,
 			   bnt);
@@ -1090,7 +1094,7 @@ radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, int s1, int s2, ui
 		return -1;
 	hipLaunchKernelGGL((k_rs_scatter<K, false, false, false, true>), dim3(tmax), dim3(Tile<K>::THREADS), 0, st,
 			   (const K *) k1, (const uint32_t *) v1, n, s2, offs.as<uint32_t>(), tmax, k0, v0, none, lbm,
-			   status, gd1, lbm + 4, sg, sort_xg());
+			   status, gd1, lbm + 4, sg, sort_xg((int) sizeof(K)));
 	// pass C: the remaining varying bits, 4 at a time, inside each (d1, d2) bucket
 	// the remaining bits in 8-bit LSD digits (the top one may reach into d2,
 	// constant inside a bucket)
@@ -1314,7 +1318,7 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 		const uint32_t *gd = gdig + s * 256;
 #define SCAT(F, I, L) hipLaunchKernelGGL((k_rs_scatter<K, F, I, L, false>), dim3(nblocks), dim3(Tile<K>::THREADS), 0, st, kin, \
 					 vin, n, shift, offs.as<uint32_t>(), nblocks, kout, vout, f2, tk, status.as<uint64_t>(), gd, er, \
-					 SegTiles{}, sort_xg())
+					 SegTiles{}, sort_xg((int) sizeof(K)))
 		if (lb) {
 			if (fin) {
 				if (idv) SCAT(true, true, true); else SCAT(true, false, true);
