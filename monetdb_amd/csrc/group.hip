@@ -209,7 +209,13 @@ constexpr uint32_t GL_SLOTS = 4096;
 constexpr uint32_t GL_MAXG = 3072;
 constexpr uint64_t GL_EMPTY = ~0ull;
 constexpr BUN GL_TILE = 65536;
-constexpr BUN GL_FTILE = 8192;            // rows per workgroup of the first-occurrence pass
+constexpr BUN GL_FTILE = 8192;
+#ifndef MGDK_GL_NT_STORE
+#define MGDK_GL_NT_STORE 1        // nontemporal id stores in the 4-byte assign pass
+#endif
+#ifndef MGDK_GL_NT_LOAD
+#define MGDK_GL_NT_LOAD 1
+#endif            // rows per workgroup of the first-occurrence pass
 
 __device__ __forceinline__ uint64_t
 gl_key(const KeySrc &s, BUN i)
@@ -636,7 +642,11 @@ k_gl_assign_v32(KeySrc s, BUN n, const unsigned long long *gkey, const uint32_t 
 	for (BUN r0 = a + (BUN) tid * V; r0 < e; r0 += STEP) {
 		uint32_t k[V];
 		if (r0 + V <= e) {
+#if MGDK_GL_NT_LOAD
 			const kv x = __builtin_nontemporal_load((const kv *) (kb + r0));
+#else
+			const kv x = *(const kv *) (kb + r0);
+#endif
 #pragma unroll
 			for (int u = 0; u < V; u++)
 				k[u] = x[u];
@@ -671,8 +681,13 @@ k_gl_assign_v32(KeySrc s, BUN n, const unsigned long long *gkey, const uint32_t 
 		if (r0 + V <= e) {
 			typedef unsigned long long o2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-			for (int u = 0; u < V; u += 2)
+			for (int u = 0; u < V; u += 2) {
+#if MGDK_GL_NT_STORE
 				__builtin_nontemporal_store((o2){g[u], g[u + 1]}, (o2 *) (gid + r0 + u));
+#else
+				*(o2 *) (gid + r0 + u) = (o2){g[u], g[u + 1]};
+#endif
+			}
 			if (img) {
 				const uint32_t w4 = g[0] | (g[1] << 8) | (g[2] << 16) | (g[3] << 24);
 				*(uint32_t *) (img + r0) = w4;
