@@ -208,7 +208,10 @@ k_max_oid(const oid *g, BUN n, unsigned long long *out)
 constexpr uint32_t GL_SLOTS = 4096;
 constexpr uint32_t GL_MAXG = 3072;
 constexpr uint64_t GL_EMPTY = ~0ull;
-constexpr BUN GL_TILE = 65536;
+#ifndef MGDK_GL_TILE
+#define MGDK_GL_TILE 65536
+#endif
+constexpr BUN GL_TILE = MGDK_GL_TILE;     // rows per assign workgroup (and per prefix tile)
 constexpr BUN GL_FTILE = 8192;
 #ifndef MGDK_GL_NT_STORE
 #define MGDK_GL_NT_STORE 1        // nontemporal id stores in the 4-byte assign pass
