@@ -359,7 +359,8 @@ k_gl_first(KeySrc s, BUN n, BUN tile0, unsigned long long *gkey, unsigned long l
 // keys first << 13 | slot, all distinct) -> group ids, extents.  Every
 // workgroup compacts the table in slot order (a scan, so all workgroups
 // hold the same list) and ranks its share of the entries
-constexpr unsigned GL_ORDER_WG = (GL_MAXG + 255) / 256;
+constexpr unsigned GL_ORDER_SPLIT = 4;
+constexpr unsigned GL_ORDER_WG = (GL_MAXG * GL_ORDER_SPLIT + 255) / 256;
 __global__ __launch_bounds__(256) void
 k_gl_order(const unsigned long long *gmin, uint32_t *gmap, bool cdense, oid cseq, const oid *coids, oid *ext,
 	   uint32_t *ngrp)
@@ -397,14 +398,24 @@ k_gl_order(const unsigned long long *gmin, uint32_t *gmap, bool cdense, oid cseq
 		if (f[x] != ~0ull)
 			sk[pos++] = (f[x] << 13) | (x < PER ? tid * PER + x : GL_SLOTS);
 	__syncthreads();
-	for (uint32_t i = blockIdx.x * blockDim.x + tid; i < c; i += gridDim.x * blockDim.x) {
+	// GL_ORDER_SPLIT consecutive lanes count one entry's rank over
+	// interleaved quarters of the list and add their counts
+	const uint32_t sub = tid % GL_ORDER_SPLIT;
+	for (uint32_t i0 = (blockIdx.x * blockDim.x + tid) / GL_ORDER_SPLIT; i0 < (c + 63) / 64 * 64;
+	     i0 += gridDim.x * blockDim.x / GL_ORDER_SPLIT) {
+		const uint32_t i = i0 < c ? i0 : 0;
 		const unsigned long long v = sk[i];
 		uint32_t r = 0;
-		for (uint32_t j = 0; j < c; j++)
+		for (uint32_t j = sub; j < c; j += GL_ORDER_SPLIT)
 			r += sk[j] < v;
-		const uint32_t slot = (uint32_t) (v & 8191);
-		gmap[slot] = r;
-		ext[r] = cdense ? cseq + (BUN) (v >> 13) : coids[v >> 13];
+#pragma unroll
+		for (int o = 1; o < (int) GL_ORDER_SPLIT; o <<= 1)
+			r += __shfl_xor(r, o);
+		if (sub == 0 && i0 < c) {
+			const uint32_t slot = (uint32_t) (v & 8191);
+			gmap[slot] = r;
+			ext[r] = cdense ? cseq + (BUN) (v >> 13) : coids[v >> 13];
+		}
 	}
 	if (tid == 0 && blockIdx.x == 0)
 		*ngrp = c;
