@@ -211,9 +211,11 @@ emit_final(const FinalOut &fo, BUN g, K key, uint32_t v)
 // groups of xg consecutive tiles, each XCD claiming its own tiles in order
 // (a per-XCD ticket; an XCD whose tiles are all claimed takes the next ones
 // of another XCD), so neighbouring tiles -- whose runs of a digit are
-// adjacent in the output -- complete their shared lines in one L2.  Every
-// tile's predecessors were claimed before it or are claimed in order by
-// some XCD, so the look-back still progresses.
+// adjacent in the output -- complete their shared lines in one L2.  A
+// tile's predecessor may then be unclaimed while the tile waits on it, and
+// whether it is ever claimed depends on what the dispatcher can place, so
+// the look-back counts a predecessor's digits itself after a bounded wait
+// (k_rs_scatter): no residency assumption, any group size is safe.
 __device__ __forceinline__ uint32_t
 claim_tile(uint32_t *xtk, uint32_t ntiles, uint32_t xg)
 {
@@ -357,34 +359,73 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 		for (unsigned q = 0; q < w; q++)
 			ex += s_wt[q];
 		tstart[tid] = ex;
-		if (LB) {
-			using namespace mgdk_lb;
-			uint64_t *me = status + (size_t) blk * 256 + tid;
-			if (blk == 0) {
-				gbase[tid] = gdig[tid];
-			} else {
-				uint64_t excl = 0;
-				int64_t t = (int64_t) blk - 1;
+	}
+	if (LB) {
+		// The walk back over the predecessors' digit counts, one step per
+		// predecessor for the whole workgroup.  A predecessor that has not
+		// published after a bounded wait may not even be claimed yet (XCD
+		// claims deal tiles out of order, and the dispatcher may have no
+		// room for the workgroup that would claim it), so the workgroup
+		// counts that tile's digits itself from its keys -- a pure function
+		// of the tile -- and walks on: every step makes progress whatever
+		// is resident, and any claim order is safe.
+		using namespace mgdk_lb;
+		uint64_t excl = 0;
+		bool done = blk == 0 || !dig;
+		int64_t t = (int64_t) blk - 1;
+		uint32_t limit = 4096;                 // spins before counting a tile ourselves
+		uint32_t *fh = (uint32_t *) sk;        // sk is free until the tile is placed
+		for (;;) {
+			bool miss = false;
+			if (!done) {
 				uint32_t spins = 0;
-				while (t >= 0) {
-					const uint64_t sv = lb_load(status + (size_t) t * 256 + tid);
-					if ((sv >> 62) == 0) {
-						if (++spins > (1u << 24)) {
-							atomicOr(err, 1u);
-							break;
-						}
-						__builtin_amdgcn_s_sleep(1);
-						continue;
-					}
-					excl += sv & ST_VAL;
-					if (sv & ST_PRE)
+				uint64_t s;
+				for (;;) {
+					s = lb_load(status + (size_t) t * 256 + tid);
+					if ((s >> 62) != 0)
 						break;
-					t--;
+					if (++spins > limit) {
+						miss = true;
+						break;
+					}
+					__builtin_amdgcn_s_sleep(1);
 				}
-				lb_store(me, ST_PRE | (excl + tot));
-				gbase[tid] = gdig[tid] + (uint32_t) excl;
+				if (!miss) {
+					excl += s & ST_VAL;
+					if (s & ST_PRE)
+						done = true;
+				}
 			}
+			if (__syncthreads_or(miss)) {
+				if (dig)
+					fh[tid] = 0;
+				__syncthreads();
+				const BUN fb = (BUN) t * STILE, fe = fb + STILE < n ? fb + STILE : n;
+				K fk[SROWS];
+#pragma unroll
+				for (int r = 0; r < SROWS; r++) {
+					const BUN i = fb + (BUN) r * STHREADS + tid;
+					fk[r] = keys[i < fe ? i : fe - 1];
+				}
+#pragma unroll
+				for (int r = 0; r < SROWS; r++)
+					if (fb + (BUN) r * STHREADS + tid < fe)
+						atomicAdd(&fh[(uint32_t) (fk[r] >> shift) & 255], 1u);
+				__syncthreads();
+				if (miss)
+					excl += fh[tid];
+				__syncthreads();
+				limit = 16;            // claims are behind: do not wait long again
+			}
+			if (!done && --t < 0)
+				done = true;
+			if (!__syncthreads_or(!done))
+				break;
 		}
+		if (dig && blk != 0)
+			lb_store(status + (size_t) blk * 256 + tid, ST_PRE | (excl + tot));
+		if (dig)
+			gbase[tid] = gdig[tid] + (uint32_t) excl;
 	}
 	__syncthreads();
 #pragma unroll
@@ -916,7 +957,11 @@ k_rs_local(const K *keys, const uint32_t *vals, const uint32_t *bs, Shifts ls, F
 	const unsigned lane = __lane_id();
 	uint32_t q = blockIdx.x;
 	if (GID) {
-		// one ticket word saturates near 88 claims / us: claim per XCD
+		// claimed in ticket order: the group ids' look-back needs every
+		// predecessor bucket claimed earlier (its distinct-key count is not
+		// something a waiting wave can recompute cheaply), so no per-XCD
+		// claims here (MGDK_SORT_LOCALXG, round 4, could leave a predecessor
+		// unclaimed behind a spinning wave)
 		uint32_t t = 0;
 		if (lane == 0)
 			t = xg ? claim_tile(ticket + 8, 65536, xg) : atomicAdd(ticket, 1u);
@@ -1033,25 +1078,18 @@ k_final_copy_at(const K *keys, const uint32_t *vals, BUN m, BUN s, FinalOut fo)
 		emit_final<K>(fo, s + i, keys[i], vals[i]);
 }
 
-// tiles per XCD group of the scatter passes (0: plain ticket order).  A
-// group must not exceed the workgroups one XCD runs at once (32 CUs x
-// workgroups per CU): the first tile of the next XCD's group waits for the
-// whole group before it (128 / 256 measured 9.4 ms / look-back timeout on
-// 100M int32, 32 2.94, 64 2.79-2.84, 0 2.99 -- DESIGN §9).  4-byte keys run
-// two scatter workgroups per CU, 8-byte keys one
+// tiles per XCD group of the scatter passes (0: plain ticket order).  The
+// first tile of an XCD's group waits on the previous XCD's whole group;
+// when that group is larger than what one XCD runs at once the waiting
+// tile counts the unclaimed predecessors' digits itself (k_rs_scatter), so
+// large groups are correct but slow (before that fallback 128 / 256 took
+// 9.4 ms / never completed on 100M int32; 32 2.94, 64 2.79-2.84, 0 2.99 --
+// DESIGN §9).  4-byte keys run two scatter workgroups per CU, 8-byte keys one
 static uint32_t
 sort_xg(int kw = 4)
 {
 	const char *e = getenv("MGDK_SORT_XCDG");
 	return e ? (uint32_t) atoi(e) : kw == 4 ? 64u : 32u;
-}
-
-// buckets per XCD group of the local pass's claims (0: one ticket word)
-static uint32_t
-local_xg()
-{
-	const char *e = getenv("MGDK_SORT_LOCALXG");
-	return e ? (uint32_t) atoi(e) : 16u;
 }
 
 template <typename K>
@@ -1129,7 +1167,7 @@ radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, int s1, int s2, ui
 	uint32_t *gtk = gid ? (uint32_t *) (gst.as<uint64_t>() + 65536) : gst.as<uint32_t>(), *ger = gtk + 4;
 #define LOCAL(R, G) hipLaunchKernelGGL((k_rs_local<K, R, G>), dim3(65536), dim3(64), 0, st, (const K *) k0, \
 				       (const uint32_t *) v0, (const uint32_t *) bsb.as<uint32_t>(), ls, fo, ovf.as<uint32_t>(), gtk, \
-				       gst.as<uint64_t>(), ger, local_xg())
+				       gst.as<uint64_t>(), ger, 0u)
 #define LOCALMB(R) hipLaunchKernelGGL((k_rs_local_mb<K, R, 4>), dim3(65536 / 4), dim3(64), 0, st, (const K *) k0, \
 				      (const uint32_t *) v0, (const uint32_t *) bsb.as<uint32_t>(), ls, fo, ovf.as<uint32_t>())
 	if (cap <= 1024) {

@@ -438,6 +438,165 @@ def analytics07_fixture():
     return {"source": rel, "tables": tables, "cases": cases, "errors": errors}
 
 
+# ---- window functions of analytics00 / 01 / 02.test ------------------------
+WIN_FUNCS = ("ntile", "first_value", "last_value", "nth_value", "lag", "lead", "min", "max", "sum", "count",
+             "avg")
+SQL_TYPES = {"int": "int", "bigint": "lng", "real": "flt", "double": "dbl"}
+
+
+def _split_top(s, sep=","):
+    """split s at top-level separators (outside parentheses / quotes)"""
+    out, depth, cur, q = [], 0, "", False
+    for ch in s:
+        if ch == "'":
+            q = not q
+        if not q and ch == "(":
+            depth += 1
+        elif not q and ch == ")":
+            depth -= 1
+        if ch == sep and depth == 0 and not q:
+            out.append(cur.strip())
+            cur = ""
+        else:
+            cur += ch
+    out.append(cur.strip())
+    return out
+
+
+def _sql_literal(t):
+    t = t.strip()
+    if t == "null":
+        return None
+    if t.startswith("'"):
+        return t.strip("'")
+    try:
+        return float(t) if "." in t else int(t)
+    except ValueError:
+        return t                  # e.g. a date literal: the table is not replayed
+
+
+def _frame_bound(t):
+    t = t.strip()
+    if t == "current row":
+        return ["CURRENT", 0]
+    if t.startswith("unbounded"):
+        return ["UNBOUNDED", None]
+    n, kind = t.split()
+    return [kind.upper(), int(n)]
+
+
+def _window_spec(spec):
+    """partition / order column, direction and ROWS frame of an OVER clause
+    (None when outside what the replay models)"""
+    m = re.fullmatch(r"\s*(?:partition by (\w+))?\s*(?:order by (\w+)(?:\s+(asc|desc))?)?\s*(rows .*)?\s*", spec)
+    if not m:
+        return None
+    part, order, direction, rows = m.groups()
+    frame = None
+    if rows:
+        fm = re.fullmatch(r"rows between (.*) and (.*)", rows.strip())
+        if fm:
+            frame = [_frame_bound(fm.group(1)), _frame_bound(fm.group(2))]
+        else:
+            frame = [_frame_bound(rows[5:]), ["CURRENT", 0]]
+    return dict(part=part, order=order, desc=direction == "desc", rows=frame)
+
+
+def _window_item(item, cols):
+    """a select-list item: a table column, or FUNC(args) OVER (spec) with an
+    optional cast(... as bigint) / floor(...) around it"""
+    wrap = None
+    m = re.fullmatch(r"cast\((.*) as bigint\)", item)
+    if m:
+        item, wrap = m.group(1), "cast"
+    m = re.fullmatch(r"floor\((.*)\)", item)
+    if m:
+        item, wrap = m.group(1), "floor"
+    if item in cols:
+        return dict(kind="col", col=item)
+    m = re.fullmatch(r"(\w+)\((.*?)\) over \((.*)\)", item)
+    if not m or m.group(1) not in WIN_FUNCS:
+        return None
+    func, args, spec = m.group(1), _split_top(m.group(2)) if m.group(2) else [], _window_spec(m.group(3))
+    if spec is None:
+        return None
+    for c in (spec["part"], spec["order"]):
+        if c is not None and c not in cols:
+            return None
+    val = args[0] if args else None
+    rest = []
+    if func == "ntile":
+        if val in cols:
+            rest = [dict(col=val)]
+        else:
+            rest = [dict(lit=_sql_literal(val))]
+        val = None
+    elif func == "count" and val == "*":
+        val = None
+    else:
+        if val not in cols or cols[val] not in SQL_TYPES.values():
+            return None               # literal / str values: not GDK window calls on the device
+        for a in args[1:]:
+            rest.append(dict(col=a) if a in cols else dict(lit=_sql_literal(a)))
+    if func in ("first_value", "last_value", "nth_value", "ntile", "lag", "lead") and spec["rows"]:
+        return None
+    return dict(kind="win", func=func, val=val, args=rest, spec=spec, wrap=wrap)
+
+
+def analytics_window_fixture():
+    """sql/test/analytics/Tests/analytics00 / 01 / 02.test: window functions
+    (ntile, first_value, last_value, nth_value, lag, lead, min, max, sum,
+    count, avg) over PARTITION BY / ORDER BY / ROWS frames of small tables
+    with NULLs.  Each case keeps the tables as inserted (the SQL front end's
+    window sort is stable, so rows keep their insertion order among peers)
+    and the expected rows as printed (rowsort: compared as multisets)."""
+    out = []
+    for name in ("analytics00", "analytics01", "analytics02"):
+        rel = "sql/test/analytics/Tests/%s.test" % name
+        text = open(os.path.join(REF, rel)).read()
+        tables, cases = {}, []
+        for kind, body, exp in parse_blocks(text):
+            stmt = " ".join(body).strip()
+            low = stmt.lower()
+            m = re.match(r"create table (\w+) \((.*)\)$", low)
+            if m:
+                cols = {}
+                for cd in _split_top(m.group(2)):
+                    cn, ct = cd.split()[:2]
+                    cols[cn] = SQL_TYPES.get(ct, "str" if ct.startswith("varchar") else None)
+                tables[m.group(1)] = dict(cols=cols, names=list(cols), rows=[])
+                continue
+            m = re.match(r"insert into (\w+) values (.*)$", low)
+            if m and m.group(1) in tables:
+                for t in re.findall(r"\(([^()]*)\)", stmt[stmt.lower().index(" values ") + 8:]):
+                    tables[m.group(1)]["rows"].append([_sql_literal(x.lower() if "'" not in x else x)
+                                                       for x in _split_top(t)])
+                continue
+            if not kind.startswith("query"):
+                continue
+            m = re.fullmatch(r"select (.*) from (\w+)", low)
+            if not m or m.group(2) not in tables:
+                continue
+            tb = tables[m.group(2)]
+            items = [_window_item(it, tb["cols"]) for it in _split_top(m.group(1))]
+            wins = [it for it in items if it and it["kind"] == "win"]
+            if not wins or any(it is None for it in items) or any(w["spec"] != wins[0]["spec"] for w in wins):
+                continue
+            types, sortmode = kind.split()[1], kind.split()[2]
+            if "T" in types:
+                continue
+            width = len(types)
+            if len(exp) % width:
+                continue
+            rows = [[None if x == "NULL" else (float(x) if t == "R" else int(x))
+                     for x, t in zip(exp[i:i + width], types)] for i in range(0, len(exp), width)]
+            cases.append(dict(table=m.group(2), items=items, spec=wins[0]["spec"], types=types,
+                              sortmode=sortmode, expected=rows))
+        out.append(dict(source=rel, tables={k: dict(cols=v["cols"], names=v["names"], rows=v["rows"])
+                                            for k, v in tables.items()}, cases=cases))
+    return out
+
+
 # ---- batcalc (tst901 / tst906 / tst908) -------------------------------------
 def batcalc_fixture():
     """monetdb5/mal/Tests/tst901.maltest, tst906.maltest: io.print of the BATs
@@ -476,7 +635,8 @@ def main():
                    for f in ("orderidx00", "orderidx04")],
           "window_bounds_employee": window_functions_fixture(),
           "window_bounds_intervals": analytics07_fixture(),
-          "batcalc": batcalc_fixture()}
+          "batcalc": batcalc_fixture(),
+          "window_sqltests": analytics_window_fixture()}
     fx["project"] = []
     for rel in ("monetdb5/mal/Tests/tst033.maltest", "monetdb5/mal/Tests/tst034.maltest",
                 "monetdb5/modules/mal/Tests/orderidx02.maltest"):
@@ -488,6 +648,7 @@ def main():
         json.dump(fx, f, indent=1)
     print("select cases:", len(fx["select"]["cases"]))
     print("firstn cases:", [len(f["cases"]) for f in fx["firstn"]])
+    print("window sqltest cases:", [(f["source"], len(f["cases"])) for f in fx["window_sqltests"]])
 
 
 if __name__ == "__main__":

@@ -262,3 +262,14 @@ def test_diff(gdk, ora, tname, dt, mode):
     else:
         got, want = gdk.GDKanalyticaldiff(b), ora.analyticaldiff(ob)
     assert np.array_equal(got.to_numpy(), np.asarray(want.values()))
+
+
+@pytest.mark.gpu
+def test_window_sqltests(gdk):
+    """analytics00 / 01 / 02.test (the reference's own answers) on the
+    device: the same 295 window queries the oracle replays
+    (tests/test_oracle.py::test_window_sqltests_oracle)."""
+    from helpers import replay_window_sqltests, sqlwin_api_gdk
+    ran, bad = replay_window_sqltests(sqlwin_api_gdk(gdk))
+    assert ran >= 290
+    assert not bad, bad[:3]

@@ -538,3 +538,14 @@ def test_project_maltest(ora):
     assert sum(len(f["cases"]) for f in FIX["project"]) == 20
     bad = replay_project(ora, mk, ora.TYPE_int, ora.NIL[ora.TYPE_int])
     assert not bad, bad[:3]
+
+
+def test_window_sqltests_oracle(ora):
+    """analytics00 / 01 / 02.test (the reference's own answers): ntile,
+    first_value, last_value, nth_value, lag, lead, min, max, sum, count and
+    avg over PARTITION BY / ORDER BY / ROWS frames, replayed through the
+    oracle's restatement of gdk_analytic_func.c / gdk_analytic_bounds.c."""
+    from helpers import replay_window_sqltests, sqlwin_api_ora
+    ran, bad = replay_window_sqltests(sqlwin_api_ora(ora))
+    assert ran >= 290
+    assert not bad, bad[:3]

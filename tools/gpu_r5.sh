@@ -1,0 +1,36 @@
+# round-5 GPU steps: bash tools/gpu_r5.sh <step> [...]; each step writes under
+# gpurun_out/r5/<step>/ and runs under its own time limit; the first failing
+# step ends the call
+set -e
+export TMPDIR=/tmp
+T="python -u -m pytest -q --timeout 120 --timeout-method thread -m gpu"
+for step in "$@"; do
+O=gpurun_out/r5/$step
+mkdir -p $O
+case $step in
+sort)
+	timeout -k 10 600 $T tests/test_gpu_sort_progress.py tests/test_gpu_join_sort_window.py -k "sort" > $O/tests.log 2>&1
+	for xg in 0 32 64 128 256; do
+		MGDK_SORT_XCDG=$xg timeout -k 10 200 python tools/opbench.py --only other_ops > $O/opbench_xg$xg.json 2> $O/opbench_xg$xg.err
+	done
+	;;
+sortsuite)
+	timeout -k 10 900 $T tests/test_gpu_join_sort_window.py tests/test_gpu_sort_qsort.py tests/test_gpu_str_sort.py tests/test_gpu_sort_hybrid.py tests/test_gpu_firstn.py tests/test_gpu_group_str.py tests/test_gpu_sort_progress.py > $O/tests.log 2>&1
+	;;
+all)
+	timeout -k 10 1100 $T tests > $O/tests.log 2>&1
+	;;
+smoke)
+	timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+	;;
+bench)
+	timeout -k 10 900 python bench.py > $O/bench.json 2> $O/bench.err
+	;;
+opbench)
+	timeout -k 10 600 python tools/opbench.py > $O/opbench.json 2> $O/opbench.err
+	;;
+*)
+	echo "unknown step $step"; exit 2
+	;;
+esac
+done
