@@ -214,8 +214,9 @@ emit_final(const FinalOut &fo, BUN g, K key, uint32_t v)
 // adjacent in the output -- complete their shared lines in one L2.  A
 // tile's predecessor may then be unclaimed while the tile waits on it, and
 // whether it is ever claimed depends on what the dispatcher can place, so
-// the look-back counts a predecessor's digits itself after a bounded wait
-// (k_rs_scatter): no residency assumption, any group size is safe.
+// the look-back counts an unclaimed predecessor's digits itself instead of
+// waiting for it (k_rs_scatter): no residency assumption, any group size is
+// safe.
 __device__ __forceinline__ uint32_t
 claim_tile(uint32_t *xtk, uint32_t ntiles, uint32_t xg)
 {
@@ -360,21 +361,37 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 			ex += s_wt[q];
 		tstart[tid] = ex;
 	}
+	__syncthreads();
+	// the tile reordered by digit in LDS before the look-back: the rows'
+	// registers are free while the walk waits
+#pragma unroll
+	for (int r = 0; r < SROWS; r++) {
+		const BUN i = base + r * 64 + lane;
+		if (i < tend) {
+			const uint32_t d = rk[r] & 255;
+			const uint32_t lpos = tstart[d] + wcnt[w][d] + (rk[r] >> 8);
+			sk[lpos] = k[r];
+			sv[lpos] = v[r];
+		}
+	}
 	if (LB) {
 		// The walk back over the predecessors' digit counts, one step per
-		// predecessor for the whole workgroup.  A predecessor that has not
-		// published after a bounded wait may not even be claimed yet (XCD
-		// claims deal tiles out of order, and the dispatcher may have no
-		// room for the workgroup that would claim it), so the workgroup
-		// counts that tile's digits itself from its keys -- a pure function
-		// of the tile -- and walks on: every step makes progress whatever
-		// is resident, and any claim order is safe.
+		// predecessor for the whole workgroup.  A claimed predecessor is
+		// running and publishes its counts before anything it waits for, so
+		// waiting on it is safe.  An UNCLAIMED one (XCD claims deal tiles
+		// out of order) may never be claimed while we wait -- the
+		// dispatcher may have no room for the workgroup that would claim it
+		// -- so the workgroup counts that tile's digits itself from its keys
+		// (a pure function of the tile) and walks on: every step makes
+		// progress whatever is resident, and any claim order is safe.
+		// Claimed <=> its XCD's ticket has passed it (every claim of a tile
+		// is an atomicAdd on its owner's ticket, claim_tile).
 		using namespace mgdk_lb;
 		uint64_t excl = 0;
 		bool done = blk == 0 || !dig;
 		int64_t t = (int64_t) blk - 1;
-		uint32_t limit = 4096;                 // spins before counting a tile ourselves
-		uint32_t *fh = (uint32_t *) sk;        // sk is free until the tile is placed
+		__shared__ uint32_t fh[256];           // a predecessor's digit counts, counted here
+		const uint32_t *xtk = ticket + 8;
 		for (;;) {
 			bool miss = false;
 			if (!done) {
@@ -384,8 +401,17 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 					s = lb_load(status + (size_t) t * 256 + tid);
 					if ((s >> 62) != 0)
 						break;
-					if (++spins > limit) {
-						miss = true;
+					if (xg && (spins & 15) == 0) {
+						const uint32_t y = (uint32_t) (t / xg) & 7;
+						const uint32_t j = (uint32_t) (t / (8 * (int64_t) xg)) * xg + (uint32_t) (t % xg);
+						if (__hip_atomic_load(&xtk[y], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= j) {
+							miss = true;
+							break;
+						}
+					}
+					if (++spins > (1u << 26)) {
+						atomicOr(err, 1u);     // cannot happen: claimed tiles publish
+						s = ST_PRE;
 						break;
 					}
 					__builtin_amdgcn_s_sleep(1);
@@ -401,21 +427,23 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 					fh[tid] = 0;
 				__syncthreads();
 				const BUN fb = (BUN) t * STILE, fe = fb + STILE < n ? fb + STILE : n;
-				K fk[SROWS];
+#pragma unroll 1
+				for (int r = 0; r < SROWS; r += 4) {
+					K fk[4];
 #pragma unroll
-				for (int r = 0; r < SROWS; r++) {
-					const BUN i = fb + (BUN) r * STHREADS + tid;
-					fk[r] = keys[i < fe ? i : fe - 1];
+					for (int u = 0; u < 4; u++) {
+						const BUN i = fb + (BUN) (r + u) * STHREADS + tid;
+						fk[u] = keys[i < fe ? i : fe - 1];
+					}
+#pragma unroll
+					for (int u = 0; u < 4; u++)
+						if (fb + (BUN) (r + u) * STHREADS + tid < fe)
+							atomicAdd(&fh[(uint32_t) (fk[u] >> shift) & 255], 1u);
 				}
-#pragma unroll
-				for (int r = 0; r < SROWS; r++)
-					if (fb + (BUN) r * STHREADS + tid < fe)
-						atomicAdd(&fh[(uint32_t) (fk[r] >> shift) & 255], 1u);
 				__syncthreads();
 				if (miss)
 					excl += fh[tid];
 				__syncthreads();
-				limit = 16;            // claims are behind: do not wait long again
 			}
 			if (!done && --t < 0)
 				done = true;
@@ -426,17 +454,6 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 			lb_store(status + (size_t) blk * 256 + tid, ST_PRE | (excl + tot));
 		if (dig)
 			gbase[tid] = gdig[tid] + (uint32_t) excl;
-	}
-	__syncthreads();
-#pragma unroll
-	for (int r = 0; r < SROWS; r++) {
-		const BUN i = base + r * 64 + lane;
-		if (i < tend) {
-			const uint32_t d = rk[r] & 255;
-			const uint32_t lpos = tstart[d] + wcnt[w][d] + (rk[r] >> 8);
-			sk[lpos] = k[r];
-			sv[lpos] = v[r];
-		}
 	}
 	__syncthreads();
 	const uint32_t nt = (uint32_t) (tend - tbase < (BUN) STILE ? tend - tbase : (BUN) STILE);
@@ -1079,12 +1096,12 @@ k_final_copy_at(const K *keys, const uint32_t *vals, BUN m, BUN s, FinalOut fo)
 }
 
 // tiles per XCD group of the scatter passes (0: plain ticket order).  The
-// first tile of an XCD's group waits on the previous XCD's whole group;
-// when that group is larger than what one XCD runs at once the waiting
-// tile counts the unclaimed predecessors' digits itself (k_rs_scatter), so
-// large groups are correct but slow (before that fallback 128 / 256 took
-// 9.4 ms / never completed on 100M int32; 32 2.94, 64 2.79-2.84, 0 2.99 --
-// DESIGN §9).  4-byte keys run two scatter workgroups per CU, 8-byte keys one
+// first tile of an XCD's group depends on the previous XCD's whole group;
+// the tiles of it that are not claimed yet are counted by the waiting tile
+// itself (k_rs_scatter), so any group size completes (before that fallback
+// 128 / 256 took 9.4 ms / never completed on 100M int32; 32 2.94, 64
+// 2.79-2.84, 0 2.99 -- DESIGN §9).  4-byte keys run two scatter workgroups
+// per CU, 8-byte keys one
 static uint32_t
 sort_xg(int kw = 4)
 {

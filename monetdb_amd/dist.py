@@ -10,7 +10,10 @@ results are combined the way mergetable re-aggregates packed partials
   * group + aggregates: local BATgroup + BATgroupsum per rank, the partial
     (key, first row, count, sums) rows hash-partitioned by key and shuffled
     with ONE all_to_all, merged by a second BATgroup on the owner, and group
-    ids renumbered in global first-occurrence order (dist_group_aggr);
+    ids renumbered in global first-occurrence order (dist_group_aggr); when
+    the shards' keys are ordered and their ranges meet only at the shard
+    edges (an ordered column cut into row ranges) only the groups shared
+    across an edge are merged, from two small all_gathers (_ordered_merge);
   * join: both sides hash-partitioned by key and shuffled, joined on the
     owner, the (l, r) pairs shuffled back to the home rank of their driving
     row and put in the order of the algorithm single-node BATjoin would take
@@ -300,7 +303,13 @@ class GdkBackend:
         dist.all_to_all_single(rc, sc)
         recv = [int(x) for x in rc.cpu().tolist()]
         tot = sum(recv)
-        g.sync()                              # the library stream wrote the sources
+        # stream order instead of host waits: torch's stream (on which the
+        # collectives are ordered) waits for the library stream that wrote
+        # the sources, and the library stream -- where every later operator
+        # on the received BATs runs -- waits for the collectives
+        cur = torch.cuda.current_stream(torch.device(self.device))
+        lib = torch.cuda.ExternalStream(g.lib().mgdk_stream(), device=torch.device(self.device))
+        cur.wait_stream(lib)
         out, keep = [], []
         for c, tp in zip(cols, types):
             b = g.BAT(g.lib().mgdk_COLnew(0, tp, max(1, tot)))
@@ -313,7 +322,10 @@ class GdkBackend:
             keep += [src, c]
             dist.all_to_all_single(dst, src, recv, list(send_counts))
             out.append(b)
-        torch.cuda.current_stream(torch.device(self.device)).synchronize()
+        lib.wait_stream(cur)
+        # the sources may be released by the caller now: their heaps are
+        # reused only by later work on the library stream, which is ordered
+        # after the collectives
         return out, recv
 
     # -- packing -------------------------------------------------------------
@@ -512,6 +524,82 @@ def _home_ids(be, dist, firsts, row0s, cols):
     return gid, [be.project(o, c) for c in cols]
 
 
+def _hge_column(be, vals):
+    import numpy as np
+    TL, TO, TH = _types(be)
+    return be.column(TH, np.array([_words(int(v)) for v in vals], dtype=np.uint64).reshape(-1, 2))
+
+
+def _ordered_merge(be, dist, keys, e, h, gk, gs):
+    """dist_group_aggr when every rank's keys are in ascending order and the
+    ranks' key ranges follow each other in rank order (max of rank r <= min
+    of the next non-empty rank), as an ordered column cut into row ranges
+    (mitosis over l_orderkey) is: a group then lives on ONE rank, except a
+    key shared across a shard boundary, which is the first group of the
+    later rank(s) and the last group of the earlier one.  The earliest rank
+    holding a key owns its group (its first row is the group's first row);
+    a later rank's first group is folded into it -- count and exact sums
+    added -- and dropped there.  Group ids in global first-occurrence order
+    are then the owned groups numbered rank by rank.  The exchange is two
+    all_gathers of a few words per rank instead of the hash all_to_all of
+    every partial group.  Returns None (caller takes the hash path) when the
+    shards are not ordered that way."""
+    TL, TO, TH = _types(be)
+    world, rank = _world(dist)
+    n, ng = be.n(keys), be.n(e)
+    srt, first, last = 1, 0, 0
+    if n:
+        s_, _, _, first, last = be.order_info(be.widen(keys))
+        srt = int(bool(s_))
+    info = _gather_int64(dist, be.device, [srt, ng, first, last])
+    info = [[int(q[0]), int(q[1]), _s64(q[2]), _s64(q[3])] for q in info]
+    live = [q for q in range(world) if info[q][1]]
+    if not all(info[q][0] for q in live) or any(info[a][3] > info[b][2] for a, b in zip(live, live[1:])):
+        return None
+    STATS["ordered_merge"] = STATS.get("ordered_merge", 0) + 1
+    # the first group's partial (count, sums) of every rank, for its owner
+    nv = len(gs)
+    mine = [0] * (1 + 2 * nv)
+    if ng:
+        mine[0] = int(be.values(be.slice(h, 0, 1))[0])
+        for j, c in enumerate(gs):
+            mine[1 + 2 * j:3 + 2 * j] = _words(int(be.values(be.slice(c, 0, 1))[0]))
+    parts = _gather_int64(dist, be.device, mine)
+    # owner of each live rank's first group: the earliest live rank holding its key
+    owner = {}
+    for q in live:
+        o = q
+        for p in live:
+            if p < q and info[p][3] == info[q][2]:
+                o = p
+                break
+        owner[q] = o
+    kept = {q: info[q][1] - (1 if owner[q] != q else 0) for q in live}
+    off = sum(kept.get(q, 0) for q in range(rank))
+    if rank not in kept:
+        return {"gid": be.dense(off, 0), "key": gk, "first_row": e, "count": h, "sums": gs}
+    lo = 1 if owner[rank] != rank else 0
+    add = [q for q in live if q != rank and owner[q] == rank and info[q][2] == info[rank][3]]
+    cols = [gk, e, h] + list(gs)
+    if lo:
+        cols = [be.slice(c, 1, ng) for c in cols]
+    if add:
+        m = be.n(cols[0])
+        cnt = int(be.values(be.slice(cols[2], m - 1, m))[0]) + sum(_s64(parts[q][0]) for q in add)
+        sums = []
+        for j in range(nv):
+            c = cols[3 + j]
+            v = int(be.values(be.slice(c, m - 1, m))[0])
+            v += sum(_from_words(parts[q][1 + 2 * j], parts[q][2 + 2 * j]) for q in add)
+            sums.append(v)
+        head = [be.copy(be.slice(c, 0, m - 1)) for c in cols]
+        cols[2] = be.append(head[2], be.column(TL, [cnt]))
+        for j in range(nv):
+            cols[3 + j] = be.append(head[3 + j], _hge_column(be, [sums[j]]))
+    return {"gid": be.dense(off, kept[rank]), "key": cols[0], "first_row": cols[1], "count": cols[2],
+            "sums": cols[3:]}
+
+
 def dist_group_aggr(be, dist, keys, vals):
     """GROUP BY keys with exact sums of `vals` (lng columns) and counts.
 
@@ -534,6 +622,9 @@ def dist_group_aggr(be, dist, keys, vals):
         # first-occurrence numbering, extents the first rows, histo the counts
         return {"gid": be.dense(0, be.n(e)), "key": gk, "first_row": e, "count": h, "sums": gs}
     row0s = _row0s(be, dist, keys)
+    got = _ordered_merge(be, dist, keys, e, h, gk, gs)
+    if got is not None:
+        return got
     parts = [gk, e, h] + gs
     order, counts = be.hashpartition(parts[0], world)
     parts = [be.project(order, c) for c in parts]

@@ -46,6 +46,8 @@ class OracleBackend:
     TYPE_lng, TYPE_oid, TYPE_hge, TYPE_bit = ora.TYPE_lng, ora.TYPE_oid, ora.TYPE_hge, ora.TYPE_bit
 
     def column(self, tp, arr, hseq=0):
+        if tp == ora.TYPE_hge:                  # (n, 2) words
+            return Col(tp, np.asarray(arr, dtype=np.uint64).reshape(-1, 2), hseq)
         return Col(tp, np.asarray(arr).astype(NP[tp]), hseq)
 
     def n(self, c):
@@ -124,9 +126,9 @@ class OracleBackend:
 
     def order_info(self, c):
         a = c.arr.astype(np.int64)
-        d = np.diff(a)
-        srt, rev = bool((d >= 0).all()), bool((d <= 0).all())
-        return srt, rev, srt and bool((d > 0).all()), int(a[0]), int(a[-1])
+        # compare neighbours (a difference would overflow next to the nil)
+        srt, rev = bool((a[1:] >= a[:-1]).all()), bool((a[1:] <= a[:-1]).all())
+        return srt, rev, srt and bool((a[1:] > a[:-1]).all()), int(a[0]), int(a[-1])
 
     def values_at(self, c, positions):
         return [int(v) for v in c.arr.astype(np.int64)[np.asarray(positions, np.int64)]]

@@ -144,6 +144,39 @@ def _exchange_worker(rank, world, port, out_dir, backend="oracle"):
     if int(tot) != len(ev):
         errs.append("groups %d != %d" % (int(tot), len(ev)))
 
+    # group + sums over ORDERED shards whose key ranges meet at the shard
+    # edges (l_orderkey-like): the ordered merge, no hash shuffle.  Rank 1
+    # (of 3) holds one key only, shared with both neighbours (a chain).
+    ok_ = np.sort(r.integers(0, 40, N)).astype(np.int64)
+    if world == 3:
+        ok_[per - 200:2 * per + 300] = ok_[per - 200]
+    ok_[:3] = np.iinfo(np.int64).min                                   # nils first
+    before = D.STATS.get("ordered_merge", 0)
+    got = D.dist_group_aggr(be, dist, Col(ora.TYPE_lng, ok_[lo:hi], lo),
+                            [Col(ora.TYPE_lng, v1[lo:hi], lo), Col(ora.TYPE_lng, v2[lo:hi], lo)])
+    if D.STATS.get("ordered_merge", 0) != before + 1:
+        errs.append("ordered shards did not take the ordered merge")
+    g, e, h = ora.BATgroup(ora.Bat.from_array(ora.TYPE_lng, ok_))
+    ev, hv = e.values().astype(np.int64), h.values()
+    s1 = ora.BATgroupsum(ora.Bat.from_array(ora.TYPE_lng, v1), g, e, ora.TYPE_hge).values()
+    s2 = ora.BATgroupsum(ora.Bat.from_array(ora.TYPE_lng, v2), g, e, ora.TYPE_hge).values()
+    gid = V(got["gid"]).astype(np.int64)
+    if len(gid) and not (np.diff(gid) > 0).all():
+        errs.append("ordered: gids not ascending")
+    if len(gid):
+        for name, have, want in (("key", V(got["key"]), ok_[ev[gid]]), ("first", V(got["first_row"]), ev[gid]),
+                                 ("count", V(got["count"]), hv[gid]),
+                                 ("sum1", V(got["sums"][0]), np.asarray(s1, dtype=object)[gid]),
+                                 ("sum2", V(got["sums"][1]), np.asarray(s2, dtype=object)[gid])):
+            if [int(x) for x in have] != [int(x) for x in want]:
+                errs.append("ordered: group column %s mismatch" % name)
+    tot = torch.tensor([len(gid)])
+    dist.all_reduce(tot)
+    if int(tot) != len(ev):
+        errs.append("ordered: groups %d != %d" % (int(tot), len(ev)))
+    g, e, h = ora.BATgroup(ora.Bat.from_array(ora.TYPE_int, keys))
+    ev, hv = e.values().astype(np.int64), h.values()
+
     # group + AVG: per-shard BATgroupavg3 partials, one shuffle, BATgroupavg3combine
     v3 = v1.copy()
     v3[r.random(N) < 0.03] = np.iinfo(np.int64).min

@@ -14,6 +14,14 @@ sort)
 		MGDK_SORT_XCDG=$xg timeout -k 10 200 python tools/opbench.py --only other_ops > $O/opbench_xg$xg.json 2> $O/opbench_xg$xg.err
 	done
 	;;
+join)
+	timeout -k 10 600 $T tests/test_gpu_join_sort_window.py tests/test_join_algo.py tests/test_join_str.py tests/test_msk_cands.py -k "join" > $O/tests.log 2>&1
+	for v in 0 1; do
+		MGDK_JOIN_PROBE4=$v timeout -k 10 200 python tools/opbench.py --only config3 > $O/opbench_v$v.json 2> $O/opbench_v$v.err
+	done
+	cd /tmp && cd $GRAFT_REPO_ROOT
+	timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 tools/opbench.py --only config3 > $O/prof.log 2>&1
+	;;
 sortsuite)
 	timeout -k 10 900 $T tests/test_gpu_join_sort_window.py tests/test_gpu_sort_qsort.py tests/test_gpu_str_sort.py tests/test_gpu_sort_hybrid.py tests/test_gpu_firstn.py tests/test_gpu_group_str.py tests/test_gpu_sort_progress.py > $O/tests.log 2>&1
 	;;
