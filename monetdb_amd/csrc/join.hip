@@ -1259,453 +1259,6 @@ k_pj_restore(const uint2 *flat, const uint32_t *offT, uint32_t P, uint64_t total
 	}
 }
 
-// ---------------------------------------------------------------------------
-// Probe side without row indices (round 5).  The probe side's entries are
-// the 4-byte key images alone, and the probe answers each with a 4-byte
-// match (build position + 1, or 0); no row index travels through the
-// partitions.  Instead every half-subtile's piece of a (subtile, partition)
-// run is stored in ascending key order (equal keys in slot order), which is
-// a function of the keys alone: the restore recomputes, from the subtile's
-// own keys, where each row's answer sits -- the number of keys of its run
-// piece below its own key.  Equal keys get equal answers, so which of
-// several equal keys is met first does not matter.  Per probe row this
-// moves 4 + 4 bytes through the scatter and the probe where (key, row) and
-// (match + 1, row) moved 8 + 8, and the restore reads 4 bytes of keys
-// again and 4 bytes of answers instead of 8.
-// ---------------------------------------------------------------------------
-
-// exclusive scan of cnt[0..P) into start[0..P) by a 1024-thread workgroup;
-// returns the total (P <= 4096)
-__device__ __forceinline__ uint32_t
-pj_lds_scan(const uint32_t *cnt, uint32_t *start, uint32_t P, uint32_t *wsum)
-{
-	const unsigned tid = threadIdx.x;
-	uint32_t loc[4], t = 0;
-	const uint32_t per = (P + 1023) / 1024;
-	for (uint32_t q = 0; q < per; q++) {
-		const uint32_t p = tid * per + q;
-		loc[q] = p < P ? cnt[p] : 0;
-		t += loc[q];
-	}
-	uint32_t x = t;
-#pragma unroll
-	for (int o = 1; o < 64; o <<= 1) {
-		const uint32_t u = __shfl_up(x, o);
-		if (__lane_id() >= (unsigned) o)
-			x += u;
-	}
-	if (__lane_id() == 63)
-		wsum[tid >> 6] = x;
-	__syncthreads();
-	uint32_t pre = x - t, total = 0;
-	for (uint32_t w = 0; w < 16; w++) {
-		pre += w < (tid >> 6) ? wsum[w] : 0;
-		total += wsum[w];
-	}
-	for (uint32_t q = 0; q < per; q++) {
-		const uint32_t p = tid * per + q;
-		if (p < P)
-			start[p] = pre;
-		pre += loc[q];
-	}
-	__syncthreads();
-	return total;
-}
-
-// 16 consecutive keys of a half-subtile, rows i0 .. i0 + 15 (FULL: a whole
-// aligned dense 4-byte subtile, straight-line vector loads); bit q of the
-// result: row i0 + q exists and takes part
-template <bool FULL>
-__device__ __forceinline__ uint32_t
-pj_load16(const Side &s, BUN i0, BUN e, bool skipnil, uint32_t k[16])
-{
-	uint32_t okm = 0;
-	if constexpr (FULL) {
-		typedef int32_t i4 __attribute__((ext_vector_type(4)));
-		const i4 *src = (const i4 *) ((const int32_t *) s.base + s.off + i0);
-#pragma unroll
-		for (int q = 0; q < 4; q++) {
-			const i4 v = __builtin_nontemporal_load(src + q);
-			k[4 * q] = (uint32_t) v.x;
-			k[4 * q + 1] = (uint32_t) v.y;
-			k[4 * q + 2] = (uint32_t) v.z;
-			k[4 * q + 3] = (uint32_t) v.w;
-		}
-#pragma unroll
-		for (int q = 0; q < 16; q++)
-			okm |= (uint32_t) !(skipnil && k[q] == 0x80000000u) << q;
-	} else {
-		bool ok[16];
-		pj_keys16(s, i0, e, skipnil, k, ok);
-#pragma unroll
-		for (int q = 0; q < 16; q++)
-			okm |= (uint32_t) ok[q] << q;
-	}
-	return okm;
-}
-
-// a half-subtile's keys placed by partition in LDS (unordered inside a
-// partition): stage[start[p] + rank] = key, hist / start of the half;
-// rslot (restore): the slot of each of the half's rows (rows row0 + q)
-__device__ __forceinline__ uint32_t
-pj_stage_half(const uint32_t kk[16], uint32_t okm, int pbits, uint32_t *stage, uint32_t *hist, uint32_t *start,
-	      uint32_t *wsum, uint16_t *rslot, uint32_t row0)
-{
-	const uint32_t P = 1u << pbits;
-	for (uint32_t p = threadIdx.x; p < P; p += blockDim.x)
-		hist[p] = 0;
-	__syncthreads();
-	uint32_t pr[16];
-#pragma unroll
-	for (int q = 0; q < 16; q++) {
-		pr[q] = ~0u;
-		if ((okm >> q) & 1) {
-			const uint32_t p = pj_part32(kk[q], pbits);
-			pr[q] = (p << 16) | atomicAdd(&hist[p], 1u);
-		}
-	}
-	__syncthreads();
-	const uint32_t total = pj_lds_scan(hist, start, P, wsum);
-#pragma unroll
-	for (int q = 0; q < 16; q++) {
-		const uint32_t slot = pr[q] != ~0u ? start[pr[q] >> 16] + (pr[q] & 0xffff) : 0xffffu;
-		if (pr[q] != ~0u)
-			stage[slot] = kk[q];
-		if (rslot)
-			rslot[row0 + q] = (uint16_t) slot;
-	}
-	__syncthreads();
-	return total;
-}
-
-// keys of the run piece [s0, s0 + len) below x, and (eqb) equal to x in
-// slots before j
-__device__ __forceinline__ uint32_t
-pj_rank(const uint32_t *stage, uint32_t s0, uint32_t len, uint32_t x, uint32_t j, uint32_t *eqb)
-{
-	uint32_t lt = 0, eq = 0;
-	for (uint32_t i = 0; i < len; i++) {
-		const uint32_t v = stage[s0 + i];
-		lt += v < x;
-		eq += (v == x) & (s0 + i < j);
-	}
-	if (eqb)
-		*eqb = eq;
-	return lt;
-}
-
-// one half of the scatter: stage, then each key to its run piece's
-// ascending-key place straight from the stage (consecutive slots are
-// mostly one run, so the stores of a wave land in one or two pieces).  A
-// key's place costs a pass over its piece, so a piece longer than
-// PJ_MAXPIECE (a heavily repeated probe key) flags the cut instead: the
-// caller then cuts the probe side with row indices (k_pj_scatter)
-constexpr uint32_t PJ_MAXPIECE = 192;
-
-__device__ __forceinline__ void
-pj_scatter4_half(const uint32_t kk[16], uint32_t okm, int pbits, uint32_t *ent, uint32_t *stage, uint32_t *hist,
-		 uint32_t *start, uint32_t *gcur, uint32_t *wsum, uint32_t *longp)
-{
-	const uint32_t P = 1u << pbits;
-	const uint32_t total = pj_stage_half(kk, okm, pbits, stage, hist, start, wsum, nullptr, 0);
-	bool lng = false;
-	for (uint32_t p = threadIdx.x; p < P; p += blockDim.x)
-		lng |= hist[p] > PJ_MAXPIECE;
-	if (__syncthreads_or(lng)) {
-		if (threadIdx.x == 0)
-			atomicOr(longp, 1u);
-		return;
-	}
-	for (uint32_t j = threadIdx.x; j < total; j += blockDim.x) {
-		const uint32_t x = stage[j];
-		const uint32_t p = pj_part32(x, pbits), s0 = start[p];
-		uint32_t eq;
-		const uint32_t lt = pj_rank(stage, s0, hist[p], x, j, &eq);
-		ent[gcur[p] + lt + eq] = x;
-	}
-	__syncthreads();
-	for (uint32_t p = threadIdx.x; p < P; p += blockDim.x)
-		gcur[p] += hist[p];
-	__syncthreads();
-}
-
-template <bool FULL>
-__device__ __forceinline__ void
-pj_scatter4_sub(const Side &s, BUN n, int pbits, bool skipnil, BUN a0, uint32_t *ent, uint32_t *stage,
-		uint32_t *hist, uint32_t *start, uint32_t *gcur, uint32_t *wsum, uint32_t *longp)
-{
-	const unsigned tid = threadIdx.x;
-	// both halves' keys are loaded before the first is ranked
-	uint32_t k0[16], k1[16];
-	const BUN e0 = min(n, a0 + (BUN) PJ_HALF), e1 = min(n, a0 + (BUN) PJ_SUBROWS);
-	const uint32_t m0 = pj_load16<FULL>(s, a0 + (BUN) tid * 16, e0, skipnil, k0);
-	const uint32_t m1 = FULL || a0 + PJ_HALF < n ? pj_load16<FULL>(s, a0 + PJ_HALF + (BUN) tid * 16, e1, skipnil, k1) : 0u;
-	pj_scatter4_half(k0, m0, pbits, ent, stage, hist, start, gcur, wsum, longp);
-	if (FULL || a0 + PJ_HALF < n)
-		pj_scatter4_half(k1, m1, pbits, ent, stage, hist, start, gcur, wsum, longp);
-}
-
-__global__ __launch_bounds__(1024) void
-k_pj_scatter4(Side s, BUN n, int pbits, bool skipnil, const uint32_t *off, const uint32_t *base, uint32_t *ent,
-	      uint32_t *longp)
-{
-	__shared__ uint32_t stage[PJ_HALF];
-	__shared__ uint32_t hist[1u << PJ_MAXPBITS], start[1u << PJ_MAXPBITS], gcur[1u << PJ_MAXPBITS];
-	__shared__ uint32_t wsum[16];
-	const uint32_t P = 1u << pbits;
-	const BUN sub = xcd_block(blockIdx.x, gridDim.x);
-	const BUN a0 = sub * PJ_SUBROWS;
-	for (uint32_t p = threadIdx.x; p < P; p += blockDim.x)
-		gcur[p] = base[p] + off[sub * P + p];
-	if (s.w == 4 && s.dense && a0 + PJ_SUBROWS <= n && ((s.off + a0) & 3) == 0)
-		pj_scatter4_sub<true>(s, n, pbits, skipnil, a0, ent, stage, hist, start, gcur, wsum, longp);
-	else
-		pj_scatter4_sub<false>(s, n, pbits, skipnil, a0, ent, stage, hist, start, gcur, wsum, longp);
-}
-
-// rdT[p][sub] = (start of the (sub, p) run inside partition p, the delta
-// that moves it to its subtile-major place), 64 x 64 tiles through LDS
-__global__ __launch_bounds__(256) void
-k_pj_rd(const uint32_t *offT, const uint32_t *poff, const uint32_t *pbase, uint32_t nsub, uint32_t P, uint2 *rdT)
-{
-	__shared__ uint2 t[64][65];
-	const uint32_t s0 = blockIdx.x * 64, p0 = blockIdx.y * 64;
-	for (uint32_t k = threadIdx.x; k < 64 * 64; k += blockDim.x) {
-		const uint32_t r = k / 64, c = k % 64, sub = s0 + r, p = p0 + c;
-		if (sub < nsub && p < P) {
-			const uint32_t o = poff[(size_t) sub * P + p];
-			t[r][c] = make_uint2(o, offT[(size_t) sub * P + p] - pbase[p] - o);
-		}
-	}
-	__syncthreads();
-	for (uint32_t k = threadIdx.x; k < 64 * 64; k += blockDim.x) {
-		const uint32_t r = k / 64, c = k % 64, p = p0 + r, sub = s0 + c;
-		if (sub < nsub && p < P)
-			rdT[(size_t) p * nsub + sub] = t[c][r];
-	}
-}
-
-// one workgroup per partition: the LDS table of the build entries as in
-// k_pj_probe; each 4-byte probe key's answer (build position + 1, or 0) is
-// stored at its subtile-major place, its subtile found by a binary search
-// over the partition's run starts (staged in LDS with the deltas)
-__global__ __launch_bounds__(1024) void
-k_pj_probe4(const uint2 *bent, const uint32_t *bbase, const uint32_t *pent, const uint32_t *pbase, int pbits,
-	    uint32_t nbp, const uint2 *rdT, uint32_t nsub, uint32_t *flat, uint32_t *dupflag)
-{
-	extern __shared__ __attribute__((aligned(16))) unsigned long long dyn[];
-	unsigned long long *tab = dyn;
-	uint2 *srd = (uint2 *) (dyn + 2 * nbp);
-	const uint32_t p = xcd_block(blockIdx.x, gridDim.x), ns = 2 * nbp;
-	for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x)
-		tab[i] = 0ull;
-	const uint2 *rcol = rdT + (size_t) p * nsub;
-	for (uint32_t i = threadIdx.x; i < nsub; i += blockDim.x)
-		srd[i] = rcol[i];
-	__syncthreads();
-	constexpr int U = 8;
-	const uint32_t q0 = pbase[p], q1 = pbase[p + 1];
-	uint32_t cur[U];
-#pragma unroll
-	for (int u = 0; u < U; u++) {
-		const uint32_t e = q0 + threadIdx.x + u * blockDim.x;
-		cur[u] = pent[e < q1 ? e : q0];
-	}
-	const uint32_t b0 = bbase[p], b1 = bbase[p + 1];
-	bool dup = false;
-	for (uint32_t e = b0 + threadIdx.x; e < b1; e += blockDim.x) {
-		const uint2 en = bent[e];
-		const unsigned long long v = ((unsigned long long) (en.y + 1) << 32) | en.x;
-		uint32_t h = 2 * gt_home(pj_hash(en.x), pbits, nbp);
-		for (;;) {
-			const unsigned long long o = atomicCAS(&tab[h], 0ull, v);
-			if (o == 0ull)
-				break;
-			if ((uint32_t) o == en.x) {
-				dup = true;
-				break;
-			}
-			h = h + 1 == ns ? 0 : h + 1;
-		}
-	}
-	if (__any(dup) && __lane_id() == 0)
-		atomicOr(dupflag, 1u);
-	__syncthreads();
-	const ulonglong2 *bk = (const ulonglong2 *) tab;
-	for (uint32_t e0 = q0 + threadIdx.x; e0 < q1; e0 += U * blockDim.x) {
-		uint32_t key[U], m[U];
-#pragma unroll
-		for (int u = 0; u < U; u++) {
-			key[u] = cur[u];
-			const uint32_t e = e0 + (U + u) * blockDim.x;
-			cur[u] = pent[e < q1 ? e : q0];
-		}
-#pragma unroll
-		for (int u = 0; u < U; u++) {
-			uint32_t b = gt_home(pj_hash(key[u]), pbits, nbp);
-			m[u] = 0;
-			for (;;) {
-				const ulonglong2 sl = bk[b];
-				if (sl.x == 0ull)
-					break;
-				if ((uint32_t) sl.x == key[u]) {
-					m[u] = (uint32_t) (sl.x >> 32);
-					break;
-				}
-				if (sl.y == 0ull)
-					break;
-				if ((uint32_t) sl.y == key[u]) {
-					m[u] = (uint32_t) (sl.y >> 32);
-					break;
-				}
-				b = b + 1 == nbp ? 0 : b + 1;
-			}
-		}
-#pragma unroll
-		for (int u = 0; u < U; u++) {
-			const uint32_t e = e0 + u * blockDim.x;
-			if (e < q1) {
-				// the last subtile whose run starts at or before e
-				const uint32_t x = e - q0;
-				uint32_t lo = 0, hi = nsub - 1;
-				while (lo < hi) {
-					const uint32_t mid = (lo + hi + 1) >> 1;
-					if (srd[mid].x <= x)
-						lo = mid;
-					else
-						hi = mid - 1;
-				}
-				flat[e + srd[lo].y] = m[u];
-			}
-		}
-	}
-}
-
-// one workgroup per subtile (ticketed), half by half: the half's keys are
-// staged by partition again (rslot: each row's slot); each slot's answer is
-// read from the subtile's contiguous range of the flat answers at (its
-// partition's run start in the subtile) + (half 0's piece of the run, for
-// half 1) + (keys of its piece below its key) and kept in the stage by
-// slot; the half's matches are then written in row order (decoupled
-// look-back over half-subtiles)
-template <bool FULL>
-__device__ __forceinline__ void
-pj_restore4_half(const uint32_t *flat, uint32_t f0, BUN n, BUN ah, uint32_t hrows, int half, int pbits,
-		 bool skipnil, const Side &L, const Side &R, uint32_t unit, uint32_t nunits, uint64_t *status,
-		 uint64_t *meta, oid *r1, oid *r2, uint32_t *stage, uint16_t *rslot, uint32_t *hist, uint32_t *start,
-		 uint32_t *h0, const uint32_t *sofs, uint32_t *wsum, uint32_t *rmask, uint32_t *rbase, uint64_t *s_pre)
-{
-	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
-	uint32_t kk[16];
-	const uint32_t okm = hrows ? pj_load16<FULL>(L, ah + (BUN) tid * 16, ah + hrows, skipnil, kk) : 0u;
-	const uint32_t total = pj_stage_half(kk, okm, pbits, stage, hist, start, wsum, rslot, tid * 16);
-	// (partition, rank) of each of this thread's slots, then (after every
-	// rank is taken) the answers over the keys
-	uint32_t pl[16];
-#pragma unroll
-	for (int k = 0; k < 16; k++) {
-		const uint32_t j = tid + k * blockDim.x;
-		pl[k] = ~0u;
-		if (j < total) {
-			const uint32_t x = stage[j];
-			const uint32_t p = pj_part32(x, pbits);
-			pl[k] = (p << 16) | pj_rank(stage, start[p], hist[p], x, j, nullptr);
-		}
-	}
-	__syncthreads();
-#pragma unroll
-	for (int k = 0; k < 16; k++)
-		if (pl[k] != ~0u) {
-			const uint32_t p = pl[k] >> 16;
-			stage[tid + k * blockDim.x] = flat[(size_t) f0 + sofs[p] + (half ? h0[p] : 0) + (pl[k] & 0xffff)];
-		}
-	if (half == 0)
-		for (uint32_t p = tid; p < (1u << pbits); p += blockDim.x)
-			h0[p] = hist[p];
-	__syncthreads();
-	// thread tid: rows [16 tid, 16 tid + 16) of the half
-	uint32_t msk = 0;
-#pragma unroll
-	for (int k = 0; k < 16; k++) {
-		const uint32_t r = tid * 16 + k, sl = rslot[r];
-		msk |= (uint32_t) (r < hrows && sl != 0xffffu && stage[sl] != 0) << k;
-	}
-	const uint32_t c = __popc(msk);
-	uint32_t x = c;
-#pragma unroll
-	for (int o = 1; o < 64; o <<= 1) {
-		const uint32_t u = __shfl_up(x, o);
-		if (lane >= (unsigned) o)
-			x += u;
-	}
-	if (lane == 63)
-		wsum[w] = x;
-	__syncthreads();
-	uint32_t wpre = 0, tot = 0;
-	for (uint32_t q = 0; q < 16; q++) {
-		wpre += q < w ? wsum[q] : 0;
-		tot += wsum[q];
-	}
-	rmask[tid] = msk;
-	rbase[tid] = wpre + x - c;
-	if (w == 0) {
-		const uint64_t pre = lookback(status, unit, tot, (uint32_t *) &meta[1]);
-		if (lane == 0) {
-			*s_pre = pre;
-			if (unit == nunits - 1)
-				meta[0] = pre + tot;
-		}
-	}
-	__syncthreads();
-	const uint64_t pre = *s_pre;
-	for (uint32_t r = tid; r < hrows; r += blockDim.x) {
-		const uint32_t run = r >> 4, bit = r & 15;
-		const uint32_t mk = rmask[run];
-		if ((mk >> bit) & 1) {
-			const uint64_t o = pre + rbase[run] + __popc(mk & ((1u << bit) - 1));
-			r1[o] = oid_of(L, ah + r);
-			r2[o] = oid_of(R, stage[rslot[r]] - 1);
-		}
-	}
-	__syncthreads();
-}
-
-__global__ __launch_bounds__(1024) void
-k_pj_restore4(const uint32_t *flat, const uint32_t *offT, uint32_t P, BUN n, uint32_t nsub, int pbits, bool skipnil,
-	      Side L, Side R, uint32_t *ticket, uint64_t *status, uint64_t *meta, oid *r1, oid *r2)
-{
-	__shared__ uint32_t stage[PJ_HALF];
-	__shared__ uint16_t rslot[PJ_HALF];
-	__shared__ uint32_t hist[1u << PJ_MAXPBITS], start[1u << PJ_MAXPBITS], h0[1u << PJ_MAXPBITS],
-		sofs[1u << PJ_MAXPBITS];
-	__shared__ uint32_t wsum[16];
-	__shared__ uint32_t rmask[1024], rbase[1024];
-	__shared__ uint32_t s_sub;
-	__shared__ uint64_t s_pre;
-	const unsigned tid = threadIdx.x;
-	if (tid == 0)
-		s_sub = atomicAdd(ticket, 1u);
-	__syncthreads();
-	const uint32_t sub = s_sub;
-	const BUN a = (BUN) sub * PJ_SUBROWS;
-	const uint32_t f0 = offT[(size_t) sub * P];
-	for (uint32_t p = tid; p < P; p += blockDim.x)
-		sofs[p] = offT[(size_t) sub * P + p] - f0;
-	const bool full = L.w == 4 && L.dense && a + PJ_SUBROWS <= n && ((L.off + a) & 3) == 0;
-	for (int half = 0; half < 2; half++) {
-		const BUN ah = a + (BUN) half * PJ_HALF;
-		const uint32_t hrows = ah < n ? (uint32_t) min((BUN) PJ_HALF, n - ah) : 0;
-		if (full)
-			pj_restore4_half<true>(flat, f0, n, ah, hrows, half, pbits, skipnil, L, R, 2 * sub + half, 2 * nsub,
-					       status, meta, r1, r2, stage, rslot, hist, start, h0, sofs, wsum, rmask, rbase,
-					       &s_pre);
-		else
-			pj_restore4_half<false>(flat, f0, n, ah, hrows, half, pbits, skipnil, L, R, 2 * sub + half, 2 * nsub,
-						status, meta, r1, r2, stage, rslot, hist, start, h0, sofs, wsum, rmask, rbase,
-						&s_pre);
-	}
-}
-
 // one side cut into partitions: cnt/off matrices, partition bases, entries
 struct PjSide {
 	uint32_t nsub = 0;
@@ -1721,9 +1274,8 @@ struct PjSide {
 };
 
 int
-pj_cut(const Side &S, BUN n, int pbits, bool skipnil, PjSide &o, uint32_t *maxtot_dev, uint32_t *longp = nullptr)
+pj_cut(const Side &S, BUN n, int pbits, bool skipnil, PjSide &o, uint32_t *maxtot_dev)
 {
-	const bool keys4 = longp != nullptr;
 	hipStream_t st = stream();
 	const uint32_t P = 1u << pbits;
 	o.nsub = (uint32_t) ((n + PJ_SUBROWS - 1) / PJ_SUBROWS);
@@ -1732,7 +1284,7 @@ pj_cut(const Side &S, BUN n, int pbits, bool skipnil, PjSide &o, uint32_t *maxto
 	o.off = new DevBuf(m);
 	o.tot = new DevBuf(P * 4 + 64);
 	o.base = new DevBuf(P * 4 + 64);
-	o.ent = new DevBuf(n * (keys4 ? 4 : 8) + 64);
+	o.ent = new DevBuf(n * 8 + 64);
 	if (!o.cnt->p || !o.off->p || !o.tot->p || !o.base->p || !o.ent->p)
 		return -1;
 	const unsigned grid = (o.nsub + PJ_SUBS - 1) / PJ_SUBS;
@@ -1741,69 +1293,8 @@ pj_cut(const Side &S, BUN n, int pbits, bool skipnil, PjSide &o, uint32_t *maxto
 			   o.off->as<uint32_t>(), o.tot->as<uint32_t>());
 	hipLaunchKernelGGL(k_pj_base, dim3(1), dim3(1024), 0, st, o.tot->as<uint32_t>(), P, o.base->as<uint32_t>(),
 			   maxtot_dev);
-	if (keys4)
-		hipLaunchKernelGGL(k_pj_scatter4, dim3(o.nsub), dim3(1024), 0, st, S, n, pbits, skipnil,
-				   o.off->as<uint32_t>(), o.base->as<uint32_t>(), o.ent->as<uint32_t>(), longp);
-	else
-		hipLaunchKernelGGL(k_pj_scatter, dim3(o.nsub), dim3(1024), 0, st, S, n, pbits, skipnil,
-				   o.off->as<uint32_t>(), o.base->as<uint32_t>(), o.ent->as<uint2>());
-	return 0;
-}
-
-// probe, answers and restore of the 4-byte probe entries (k_pj_probe4 /
-// k_pj_restore4); both sides are cut, offT holds the probe side's
-// subtile-major run offsets.  Returns 1 when the build side has duplicate keys
-int
-join_probe4(const Side &L, BUN nl, const Side &R, int pbits, PjSide &B, PjSide &Pr, DevBuf &offT, uint64_t total,
-	    uint32_t nbp, bool skipnil, mgdk_bat **ap, mgdk_bat **bp, bool *ukey)
-{
-	hipStream_t st = stream();
-	const uint32_t P = 1u << pbits;
-	uint32_t *meta32 = (uint32_t *) meta_buf();
-	uint64_t *meta = (uint64_t *) meta32 + 4;          // [0] pairs, [1] look-back error
-	uint32_t *h = (uint32_t *) pinned(64);
-	DevBuf rdT((size_t) Pr.nsub * P * 8 + 64), flat((size_t) nl * 4 + 64);
-	if (!rdT.p || !flat.p)
-		return sync_fail();
-	hipLaunchKernelGGL(k_pj_rd, dim3((Pr.nsub + 63) / 64, (P + 63) / 64), dim3(256), 0, st, offT.as<uint32_t>(),
-			   Pr.off->as<uint32_t>(), Pr.base->as<uint32_t>(), Pr.nsub, P, rdT.as<uint2>());
-	const size_t lds = (size_t) nbp * 16 + (size_t) Pr.nsub * 8;
-	static const bool lds_attr = hipFuncSetAttribute((const void *) k_pj_probe4,
-							 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
-	(void) lds_attr;
-	(void) hipGetLastError();
-	hipLaunchKernelGGL(k_pj_probe4, dim3(P), dim3(1024), lds, st, B.ent->as<uint2>(), B.base->as<uint32_t>(),
-			   Pr.ent->as<uint32_t>(), Pr.base->as<uint32_t>(), pbits, nbp, rdT.as<uint2>(), Pr.nsub,
-			   flat.as<uint32_t>(), &meta32[2]);
-	if (!hip_ok(hipMemcpyAsync(h, meta32, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
-		return -1;
-	if (h[2])
-		return 1;                                   // duplicate build keys
-	mgdk_bat *ra = newbat(0, MGDK_oid, nl), *rb = newbat(0, MGDK_oid, nl);
-	const size_t sbytes = (2 * (size_t) Pr.nsub + 8) * sizeof(uint64_t);
-	char *sc = (char *) scratch(sbytes);
-	if (!ra || !rb || !sc || !hip_ok(hipMemsetAsync(sc, 0, sbytes, st), "memset")) {
-		unfix2(ra, rb);
-		return sync_fail();
-	}
-	hipLaunchKernelGGL(k_pj_restore4, dim3(Pr.nsub), dim3(1024), 0, st, flat.as<uint32_t>(), offT.as<uint32_t>(), P,
-			   nl, Pr.nsub, pbits, skipnil, L, R, (uint32_t *) sc, (uint64_t *) sc + 8, meta,
-			   (oid *) ra->theap, (oid *) rb->theap);
-	uint64_t *h64 = (uint64_t *) pinned(64);
-	if (!hip_ok(hipMemcpyAsync(h64, meta, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
-		unfix2(ra, rb);
-		return -1;
-	}
-	if (h64[1] & 1) {
-		seterr("HY013!BATjoin: look-back did not complete");
-		unfix2(ra, rb);
-		return -1;
-	}
-	(void) total;
-	ra->count = rb->count = h64[0];
-	*ukey = true;                                       // unique build keys: one match per row
-	*ap = ra;
-	*bp = rb;
+	hipLaunchKernelGGL(k_pj_scatter, dim3(o.nsub), dim3(1024), 0, st, S, n, pbits, skipnil, o.off->as<uint32_t>(),
+			   o.base->as<uint32_t>(), o.ent->as<uint2>());
 	return 0;
 }
 
@@ -1836,12 +1327,8 @@ join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_b
 	PjSide B, Pr;
 	Side Rn = R;
 	Rn.nofit = &meta32[5];
-	// round 5: 4-byte probe entries and answers, no row index (k_pj_scatter4)
-	static const bool v4env = getenv("MGDK_JOIN_PROBE4") ? atoi(getenv("MGDK_JOIN_PROBE4")) != 0 : true;
-	// (pieces of a half-subtile's runs average 16 Ki / P keys: at most 64)
-	bool v4 = v4env && pbits >= 8 && (nl + PJ_SUBROWS - 1) / PJ_SUBROWS <= PJ_LDS_SUBS;
 	if (pj_cut(Rn, nr, pbits, !nil_matches, B, &meta32[0]) < 0 ||
-	    pj_cut(L, nl, pbits, !nil_matches, Pr, &meta32[1], v4 ? &meta32[6] : nullptr) < 0) {
+	    pj_cut(L, nl, pbits, !nil_matches, Pr, &meta32[1]) < 0) {
 		(void) sync();                              // launched cuts still use the buffers
 		return -1;
 	}
@@ -1849,34 +1336,12 @@ join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_b
 		return -1;
 	if (h[0] > PJ_MAXFILL || h[5])
 		return 1;                                   // oversized partition / build value without a 4-byte image
-	if (v4 && h[6]) {
-		// a heavily repeated probe key: cut the probe side again with row indices
-		v4 = false;
-		PjSide P8;
-		if (pj_cut(L, nl, pbits, !nil_matches, P8, &meta32[1]) < 0) {
-			(void) sync();
-			return -1;
-		}
-		std::swap(Pr.nsub, P8.nsub);
-		std::swap(Pr.cnt, P8.cnt);
-		std::swap(Pr.off, P8.off);
-		std::swap(Pr.tot, P8.tot);
-		std::swap(Pr.base, P8.base);
-		std::swap(Pr.ent, P8.ent);
-	}
 	// subtile-major offsets of the probe results
 	DevBuf offT((size_t) Pr.nsub * P * 4 + 64);
 	uint64_t total = 0;
 	if (!offT.p ||
 	    exclusive_scan(Pr.cnt->as<uint32_t>(), offT.as<uint32_t>(), (BUN) Pr.nsub * P, &total) < 0)
 		return sync_fail();
-	static const int lfpct = getenv("MGDK_PJ_LF") ? atoi(getenv("MGDK_PJ_LF")) : 80;
-	uint32_t nbp = (uint32_t) ((uint64_t) h[0] * 100 / (2 * (uint64_t) (lfpct < 40 ? 40 : lfpct > 95 ? 95 : lfpct))) + 1;
-	if (2 * nbp <= h[0])
-		nbp = h[0] / 2 + 1;
-	nbp = nbp < PJ_SLOTS / 2 ? nbp : PJ_SLOTS / 2;    // (h[0] <= PJ_MAXFILL keeps load < 3/4)
-	if (v4)
-		return join_probe4(L, nl, R, pbits, B, Pr, offT, total, nbp, !nil_matches, ap, bp, ukey);
 	DevBuf deltaT((size_t) Pr.nsub * P * 4 + 64), flat((size_t) nl * 8 + 64);
 	if (!deltaT.p || !flat.p)
 		return sync_fail();
@@ -1884,6 +1349,11 @@ join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_b
 			   Pr.off->as<uint32_t>(), Pr.base->as<uint32_t>(), Pr.nsub, P, deltaT.as<uint32_t>());
 	// table: ~80 % load on the largest build partition (an empty slot always
 	// remains); LDS = table + the probe's offsets column when it fits
+	static const int lfpct = getenv("MGDK_PJ_LF") ? atoi(getenv("MGDK_PJ_LF")) : 80;
+	uint32_t nbp = (uint32_t) ((uint64_t) h[0] * 100 / (2 * (uint64_t) (lfpct < 40 ? 40 : lfpct > 95 ? 95 : lfpct))) + 1;
+	if (2 * nbp <= h[0])
+		nbp = h[0] / 2 + 1;
+	nbp = nbp < PJ_SLOTS / 2 ? nbp : PJ_SLOTS / 2;    // (h[0] <= PJ_MAXFILL keeps load < 3/4)
 	const bool ldsd = Pr.nsub <= PJ_LDS_SUBS && (size_t) nbp * 16 + (size_t) Pr.nsub * 4 <= 160 * 1024;
 	const size_t lds = (size_t) nbp * 16 + (ldsd ? (size_t) Pr.nsub * 4 : 0);
 	static const bool lds_attr = hipFuncSetAttribute((const void *) k_pj_probe,
