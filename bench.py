@@ -481,16 +481,18 @@ def leg_orderkey_group(cx, cols, rows, row0):
     exch = D.STATS["exchange_s"] / cx.args.leg_steps
     tot, exch, comp = cx.max_over_ranks([tot, exch, tot - exch])
     ng = cx.sum_over_ranks(ngroups_local)
-    # byte floor of the one-GPU plan: key 8 B + two lng values read per row,
-    # group ids 8 B written and read back by the two sums; per group the
-    # extents 8 B, histogram 8 B, two hge sums 32 B written
-    floor = rows * (8 + 16 + 8 + 16) + ng // cx.world * (8 + 8 + 32)
+    # byte floor of the plan that runs (the fused ordered GROUP BY + sums,
+    # mgdk_group_sums_ordered): key 8 B + two lng values read per row; per
+    # group the extent 8 B, key 8 B, histogram 8 B and two hge sums 32 B
+    # written (no group-id column is written or read back)
+    floor = rows * (8 + 16) + ng // cx.world * (8 + 8 + 8 + 32)
     return {"ms_per_step": round(tot * 1e3, 3), "grows_per_s": round(rows * cx.world / tot / 1e9, 3),
             "unit": "Grows/s", "exchange_ms": round(exch * 1e3, 3), "local_ms": round(comp * 1e3, 3),
             "groups": ng, "rows_per_gpu": rows, "scaling": "weak",
             "byte_floor_per_gpu": floor, "floor_frac": round(floor / tot / 1e9 / HBM_PEAK_GBS, 4),
             "workload": "GROUP BY l_orderkey (4 lines/order) SUM(l_quantity), SUM(l_extendedprice): "
-                        "dist_group_aggr, one all_to_all per partial column"}
+                        "dist_group_aggr (fused ordered group + sums per rank; ordered shards merge "
+                        "their edge groups, else one all_to_all per partial column)"}
 
 
 def _int32_column(n, seed):

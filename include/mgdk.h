@@ -117,6 +117,16 @@ int mgdk_BATdownload_vheap(const mgdk_bat *b, void *host);
  * = 32-bit words of bits, count = bits) are accepted wherever a candidate
  * list is: they stand for the oid list BATunmask makes of them */
 mgdk_bat *mgdk_BATmaskedcands(mgdk_oid hseq, mgdk_BUN nr, mgdk_bat *masked, bool selected);
+/* candidate-list algebra (gdk/gdk_cand.h:160-170): BATmergecand
+ * (gdk/gdk_cand.c:46) the union, BATintersectcand (:184) the intersection,
+ * BATdiffcand (:259) a minus b, of two candidate lists in any form; the
+ * result is a new list (void when dense), hseqbase 0.  BATnegcands (:1296):
+ * [tseq, tseq + nr) minus the sorted deletions odels, as a cand_except list
+ * (void BAT + ccand_t {CAND_NEGOID} vheap) when a deletion falls inside */
+mgdk_bat *mgdk_BATmergecand(mgdk_bat *a, mgdk_bat *b);
+mgdk_bat *mgdk_BATintersectcand(mgdk_bat *a, mgdk_bat *b);
+mgdk_bat *mgdk_BATdiffcand(mgdk_bat *a, mgdk_bat *b);
+mgdk_bat *mgdk_BATnegcands(mgdk_oid tseq, mgdk_BUN nr, mgdk_bat *odels);
 
 /* ---- select (gdk/gdk.h:2245-2246; gdk/gdk_select.c:1342, :2103) ------- */
 mgdk_bat *mgdk_BATselect(mgdk_bat *b, mgdk_bat *s, const void *tl, const void *th,

@@ -216,8 +216,12 @@ k_gs_sums(const typename KT<KW>::T *k, const void *const *vals, BUN n, oid hseq,
 	__shared__ GsPart<NV> s_wtot[4];
 	__shared__ int s_wflag[4];
 	__shared__ uint32_t s_wst[4];
-	__shared__ T s_k[4][512];
-	__shared__ V s_v[NV][4][512];
+	// one 512-row staging region per wave, reused column after column (every
+	// column's loads are in flight in registers before the first is staged):
+	// 16 KiB of LDS per workgroup instead of (1 + NV) x 16 KiB, so four
+	// workgroups fit a CU instead of three
+	constexpr int SW = KW > VW ? KW : VW;
+	__shared__ __attribute__((aligned(16))) char s_st[4][512 * SW];
 	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
 	const BUN t = blockIdx.x, t0 = t * GST, l0 = t0 + (BUN) tid * GSU, r0 = t0 + (BUN) w * 512;
 	const bool live = l0 < n;
@@ -236,14 +240,15 @@ k_gs_sums(const typename KT<KW>::T *k, const void *const *vals, BUN n, oid hseq,
 		stage_ld<KW>(k, r0, n, sk);
 		const T before = r0 > 0 ? k[r0 - 1] : 0;
 #pragma unroll
-		for (int v = 0; v < NV; v++)
-			stage_st<VW>((const V *) vals[v], r0, n, sv[v], s_v[v][w]);
-		stage_st<KW>(k, r0, n, sk, s_k[w]);
+		for (int v = 0; v < NV; v++) {
+			stage_st<VW>((const V *) vals[v], r0, n, sv[v], (V *) s_st[w]);
+			stage_sync();
+			stage_rd<VW>((const V *) s_st[w], y[v]);
+			stage_sync();
+		}
+		stage_st<KW>(k, r0, n, sk, (T *) s_st[w]);
 		stage_sync();
-#pragma unroll
-		for (int v = 0; v < NV; v++)
-			stage_rd<VW>(s_v[v][w], y[v]);
-		stage_rd<KW>(s_k[w], x);
+		stage_rd<KW>((const T *) s_st[w], x);
 		T prev = stage_pred<T>(x, before, r0);
 #pragma unroll
 		for (int u = 0; u < GSU; u++) {

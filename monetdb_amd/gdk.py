@@ -90,6 +90,10 @@ _SIGS = {
     "mgdk_BATsetvheap": (C.c_int, [P, C.c_void_p, C.c_uint64]),
     "mgdk_BATdownload_vheap": (C.c_int, [P, C.c_void_p]),
     "mgdk_BATmaskedcands": (P, [C.c_uint64, C.c_uint64, P, C.c_bool]),
+    "mgdk_BATmergecand": (P, [P, P]),
+    "mgdk_BATintersectcand": (P, [P, P]),
+    "mgdk_BATdiffcand": (P, [P, P]),
+    "mgdk_BATnegcands": (P, [C.c_uint64, C.c_uint64, P]),
     "mgdk_BATselect": (P, [P, P, C.c_void_p, C.c_void_p, C.c_bool, C.c_bool, C.c_bool, C.c_bool]),
     "mgdk_BATthetaselect": (P, [P, P, C.c_void_p, C.c_char_p]),
     "mgdk_BATproject": (P, [P, P]),
@@ -414,6 +418,33 @@ def _valptr(tp, v, keep):
 def BATmaskedcands(hseq, nr, masked, selected=True):
     """gdk/gdk_cand.c:1366: a cand_mask candidate list from a msk BAT."""
     return BAT(lib().mgdk_BATmaskedcands(hseq, nr, masked.ptr, selected))
+
+
+def BATmergecand(a, b):
+    """gdk/gdk_cand.c:46: the union of two candidate lists."""
+    return BAT(lib().mgdk_BATmergecand(a.ptr, b.ptr))
+
+
+def BATintersectcand(a, b):
+    """gdk/gdk_cand.c:184: the intersection of two candidate lists."""
+    return BAT(lib().mgdk_BATintersectcand(a.ptr, b.ptr))
+
+
+def BATdiffcand(a, b):
+    """gdk/gdk_cand.c:259: the candidates of a that are not in b."""
+    return BAT(lib().mgdk_BATdiffcand(a.ptr, b.ptr))
+
+
+def BATnegcands(tseq, nr, odels):
+    """gdk/gdk_cand.c:1296: [tseq, tseq + nr) minus the sorted deletions odels
+    (a cand_except list when a deletion falls inside)."""
+    return BAT(lib().mgdk_BATnegcands(tseq, nr, odels.ptr))
+
+
+def cand_oids(c):
+    """The oids a candidate list of any form stands for (numpy uint64), read
+    back through BATmergecand with an empty list (canditer_slice)."""
+    return BATmergecand(c, BAT.dense(0, 0)).to_numpy().astype(np.uint64)
 
 
 def BATselect(b, s, tl, th, li, hi, anti, nil_matches=False):

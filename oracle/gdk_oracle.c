@@ -746,6 +746,166 @@ ora_maskedcands(ora_oid hseq, uint64_t nr, const ora_bat *masked, bool selected)
 	return ora_virtualize(bn);
 }
 
+/* ---------------------------------------------------------------------- */
+/* candidate-list algebra (gdk/gdk_cand.c:46-355, :1296-1363).  A list's
+ * candidates are its own values (canditer_init(&ci, NULL, b)): a void BAT
+ * the range [tseqbase, tseqbase + count), an oid BAT its sorted values. */
+
+static void
+cand_list(const ora_bat *b, ora_ci *ci)
+{
+	ci->dense = b->type == ORA_void;
+	ci->seq = b->tseqbase;
+	ci->oids = b->type == ORA_void ? NULL : (const ora_oid *) b->base;
+	ci->n = b->count;
+}
+
+/* a new oid list from `o` with `n` values: properties as the reference
+ * sets them, then virtualize (gdk_select.c:31) */
+static ora_bat *
+cand_result(ora_oid *o, uint64_t n)
+{
+	ora_bat *bn = ora_new(ORA_oid, n, 0);
+	if (bn == NULL)
+		return NULL;
+	if (n)
+		memcpy(bn->base, o, n * sizeof(ora_oid));
+	bn->count = n;
+	bn->sorted = bn->key = bn->nonil = 1;
+	bn->revsorted = n <= 1;
+	bn->nil = 0;
+	return ora_virtualize(bn);
+}
+
+/* BATmergecand (gdk_cand.c:46-166): the two-pointer merge of :131-153;
+ * the reference's dense shortcuts (:66-95) give the same sequence */
+ora_bat *
+ora_mergecand(const ora_bat *a, const ora_bat *b)
+{
+	ora_ci ca, cb;
+	cand_list(a, &ca);
+	cand_list(b, &cb);
+	ora_oid *o = malloc((ca.n + cb.n + 1) * sizeof(ora_oid));
+	if (o == NULL) {
+		ora_seterr("malloc");
+		return NULL;
+	}
+	uint64_t i = 0, j = 0, k = 0;
+	while (i < ca.n && j < cb.n) {
+		const ora_oid x = ci_get(&ca, i), y = ci_get(&cb, j);
+		if (x < y) {
+			o[k++] = x;
+			i++;
+		} else if (y < x) {
+			o[k++] = y;
+			j++;
+		} else {
+			o[k++] = x;
+			i++;
+			j++;
+		}
+	}
+	while (i < ca.n)
+		o[k++] = ci_get(&ca, i++);
+	while (j < cb.n)
+		o[k++] = ci_get(&cb, j++);
+	ora_bat *bn = cand_result(o, k);
+	free(o);
+	return bn;
+}
+
+/* BATintersectcand (gdk_cand.c:184-252), the loop of :228-240 */
+ora_bat *
+ora_intersectcand(const ora_bat *a, const ora_bat *b)
+{
+	ora_ci ca, cb;
+	cand_list(a, &ca);
+	cand_list(b, &cb);
+	ora_oid *o = malloc(((ca.n < cb.n ? ca.n : cb.n) + 1) * sizeof(ora_oid));
+	if (o == NULL) {
+		ora_seterr("malloc");
+		return NULL;
+	}
+	uint64_t i = 0, j = 0, k = 0;
+	while (i < ca.n && j < cb.n) {
+		const ora_oid x = ci_get(&ca, i), y = ci_get(&cb, j);
+		if (x < y)
+			i++;
+		else if (y < x)
+			j++;
+		else {
+			o[k++] = x;
+			i++;
+			j++;
+		}
+	}
+	ora_bat *bn = cand_result(o, k);
+	free(o);
+	return bn;
+}
+
+/* BATdiffcand (gdk_cand.c:259-355), the loop of :331-339 */
+ora_bat *
+ora_diffcand(const ora_bat *a, const ora_bat *b)
+{
+	ora_ci ca, cb;
+	cand_list(a, &ca);
+	cand_list(b, &cb);
+	ora_oid *o = malloc((ca.n + 1) * sizeof(ora_oid));
+	if (o == NULL) {
+		ora_seterr("malloc");
+		return NULL;
+	}
+	uint64_t j = 0, k = 0;
+	for (uint64_t i = 0; i < ca.n; i++) {
+		const ora_oid x = ci_get(&ca, i);
+		while (j < cb.n && ci_get(&cb, j) < x)
+			j++;
+		if (j == cb.n || x < ci_get(&cb, j))
+			o[k++] = x;
+	}
+	ora_bat *bn = cand_result(o, k);
+	free(o);
+	return bn;
+}
+
+/* BATnegcands (gdk_cand.c:1296-1363): [tseq, tseq + nr) minus the
+ * deletions odels[lo, hi) that fall inside it (SORTfndfirst bounds); the
+ * reference keeps them as a cand_except vheap -- returned here as the oid
+ * list that stands for */
+ora_bat *
+ora_negcands(ora_oid tseq, uint64_t nr, const ora_bat *odels)
+{
+	ora_ci cd;
+	cand_list(odels, &cd);
+	uint64_t lo = 0, hi;
+	while (lo < cd.n && ci_get(&cd, lo) < tseq)
+		lo++;
+	hi = lo;
+	while (hi < cd.n && ci_get(&cd, hi) < tseq + nr)
+		hi++;
+	if (lo == hi || cd.n == 0)
+		return ora_dense(0, tseq, nr);
+	if (hi - lo == nr)
+		return ora_dense(0, tseq, 0);
+	ora_oid *o = malloc((nr + 1) * sizeof(ora_oid));
+	if (o == NULL) {
+		ora_seterr("malloc");
+		return NULL;
+	}
+	uint64_t k = 0, d = lo;
+	for (ora_oid x = tseq; x < tseq + nr; x++) {
+		if (d < hi && ci_get(&cd, d) == x) {
+			d++;
+			continue;
+		}
+		o[k++] = x;
+	}
+	ora_bat *bn = cand_result(o, k);
+	free(o);
+	return bn;
+}
+
 ora_bat *
 ora_project(const ora_bat *l, const ora_bat *r)
 {

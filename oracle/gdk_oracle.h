@@ -90,6 +90,12 @@ ora_bat *ora_project(const ora_bat *l, const ora_bat *r);
  * a msk candidate list anywhere = its BATunmask */
 ora_bat *ora_unmask(const ora_bat *b);
 ora_bat *ora_maskedcands(ora_oid hseq, uint64_t nr, const ora_bat *masked, bool selected);
+/* candidate-list algebra (gdk/gdk_cand.c:46, :184, :259, :1296); the
+ * negcands result as the oid list its cand_except form stands for */
+ora_bat *ora_mergecand(const ora_bat *a, const ora_bat *b);
+ora_bat *ora_intersectcand(const ora_bat *a, const ora_bat *b);
+ora_bat *ora_diffcand(const ora_bat *a, const ora_bat *b);
+ora_bat *ora_negcands(ora_oid tseq, uint64_t nr, const ora_bat *odels);
 /* op: '+', '-', '*'; b1/b2 may be NULL when a constant is given */
 ora_bat *ora_calc(char op, const ora_bat *b1, const void *c1, int t1,
 		  const ora_bat *b2, const void *c2, int t2,

@@ -76,6 +76,11 @@ def lib():
         L.ora_unmask.argtypes = [P]
         L.ora_maskedcands.restype = P
         L.ora_maskedcands.argtypes = [C.c_uint64, C.c_uint64, P, C.c_bool]
+        for f in ("ora_mergecand", "ora_intersectcand", "ora_diffcand"):
+            getattr(L, f).restype = P
+            getattr(L, f).argtypes = [P, P]
+        L.ora_negcands.restype = P
+        L.ora_negcands.argtypes = [C.c_uint64, C.c_uint64, P]
         L.ora_project.argtypes = [P, P]
         L.ora_calc.restype = P
         L.ora_calc.argtypes = [C.c_char, P, C.c_void_p, C.c_int, P, C.c_void_p, C.c_int, P, C.c_int]
@@ -283,6 +288,22 @@ def unmask(b):
 
 def maskedcands(hseq, nr, masked, selected=True):
     return _ret(lib().ora_maskedcands(hseq, nr, masked.ptr, selected))
+
+
+def mergecand(a, b):
+    return _ret(lib().ora_mergecand(a.ptr, b.ptr))
+
+
+def intersectcand(a, b):
+    return _ret(lib().ora_intersectcand(a.ptr, b.ptr))
+
+
+def diffcand(a, b):
+    return _ret(lib().ora_diffcand(a.ptr, b.ptr))
+
+
+def negcands(tseq, nr, odels):
+    return _ret(lib().ora_negcands(tseq, nr, odels.ptr))
 
 
 def BATthetaselect(b, s, val, op):

@@ -22,6 +22,17 @@ join)
 	cd /tmp && cd $GRAFT_REPO_ROOT
 	timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 tools/opbench.py --only config3 > $O/prof.log 2>&1
 	;;
+gsums)
+	timeout -k 10 600 $T tests/test_gpu_group_sums.py > $O/tests.log 2>&1
+	timeout -k 10 200 python tools/opbench.py --only config4_group_sums > $O/opbench.json 2> $O/opbench.err
+	cd /tmp && cd $GRAFT_REPO_ROOT
+	timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 tools/opbench.py --only config4_group_sums > $O/prof.log 2>&1
+	timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f -o run -- python3 tools/opbench.py --only config4_group_sums > $O/pmc_f.log 2>&1
+	timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_w -o run -- python3 tools/opbench.py --only config4_group_sums > $O/pmc_w.log 2>&1
+	;;
+cand)
+	timeout -k 10 600 $T tests/test_cand_algebra.py tests/test_gpu_window_funcs.py > $O/tests.log 2>&1
+	;;
 sortsuite)
 	timeout -k 10 900 $T tests/test_gpu_join_sort_window.py tests/test_gpu_sort_qsort.py tests/test_gpu_str_sort.py tests/test_gpu_sort_hybrid.py tests/test_gpu_firstn.py tests/test_gpu_group_str.py tests/test_gpu_sort_progress.py > $O/tests.log 2>&1
 	;;

@@ -114,6 +114,22 @@ def config4_q1(sf=100):
     return out
 
 
+def config4_group_sums(sf=100):
+    """the config-4 leg's local step: GROUP BY an l_orderkey-shaped key (4
+    rows per key, ordered) with exact sums of l_quantity and
+    l_extendedprice (mgdk_group_sums_ordered); bytes: 24 per row read, 56
+    per group written"""
+    rows = int(round(sf * 6_001_215))
+    cols = gdk.tpch_lineitem(7, 0, rows, int(sf * 200_000))
+    okey = gdk.BATconvert(gdk.BAT.dense(0, rows), None, gdk.TYPE_lng)
+    okey = gdk.BATcalcdivmod("/", okey, None, gdk.TYPE_lng, c2=4, t2=gdk.TYPE_lng)
+    okey.s.tsorted, okey.s.trevsorted, okey.s.tkey, okey.s.tnonil = 1, 0, 0, 1
+    vals = [cols["quantity"], cols["extendedprice"]]
+    res, wall, kms = timed(lambda: gdk.group_sums_ordered(okey, vals), reps=5, kernels=("group_sums_ordered",))
+    ng = res[0].count()
+    return entry(rows, rows * 24 + ng * 56, wall, kms, groups=ng)
+
+
 def config5_window(n=1_000_000_000, plen=100_000, limit=100):
     v, p = gdk.gen_window_column(5, n, plen)
     res, wall, kms = timed(lambda: gdk.GDKanalyticalwindowbounds(v, p, limit, True), reps=3,
@@ -153,6 +169,7 @@ def run(quick=False, only=None):
                      ("config2_q6_sf10", config2_q6),
                      ("config3_hashjoin_sf10", config3_hashjoin),
                      ("config4_q1_sf100", config4_q1),
+                     ("config4_group_sums_sf100", config4_group_sums),
                      ("config5_window_range_1B", (lambda: config5_window(200_000_000)) if quick
                       else config5_window),
                      ("other_ops", other_ops)):
