@@ -216,6 +216,45 @@ mgdk_bat *mgdk_BATgroupavg3combine(mgdk_bat *avg, mgdk_bat *rem, mgdk_bat *cnt, 
 				   bool skip_nils);
 int mgdk_BATgroupavg3(mgdk_bat **avgp, mgdk_bat **remp, mgdk_bat **cntp,
 		      mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, bool skip_nils);
+/* grouped statistics (gdk_calc.h:156-167): Welford moments per group in
+ * candidate order (dogroupstdev gdk_aggr.c:4612, BATgroupstdev_sample :4778,
+ * _population :4785, BATgroupvariance_sample :4793, _population :4801;
+ * dogroupcovariance :4851, BATgroupcovariance_sample :5000, _population
+ * :5007; BATgroupcorrelation :5057); dbl results, tp is not read */
+mgdk_bat *mgdk_BATgroupstdev_sample(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils);
+mgdk_bat *mgdk_BATgroupstdev_population(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp,
+					bool skip_nils);
+mgdk_bat *mgdk_BATgroupvariance_sample(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils);
+mgdk_bat *mgdk_BATgroupvariance_population(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp,
+					   bool skip_nils);
+mgdk_bat *mgdk_BATgroupcovariance_sample(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp,
+					 bool skip_nils);
+mgdk_bat *mgdk_BATgroupcovariance_population(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s,
+					     int tp, bool skip_nils);
+mgdk_bat *mgdk_BATgroupcorrelation(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp,
+				   bool skip_nils);
+/* whole-column forms (gdk_calc.h:154-164; calcvariance gdk_aggr.c:4276,
+ * BATcalcstdev_population :4327, _sample :4341, BATcalcvariance_population
+ * :4355, _sample :4369; calccovariance :4404, BATcalccovariance_population
+ * :4449, _sample :4464; BATcalccorrelation :4503): nil (NaN) results when
+ * undefined; errors (overflow, type) leave a message in mgdk_GDKerrbuf */
+double mgdk_BATcalcstdev_population(double *avgp, mgdk_bat *b);
+double mgdk_BATcalcstdev_sample(double *avgp, mgdk_bat *b);
+double mgdk_BATcalcvariance_population(double *avgp, mgdk_bat *b);
+double mgdk_BATcalcvariance_sample(double *avgp, mgdk_bat *b);
+double mgdk_BATcalccovariance_population(mgdk_bat *b1, mgdk_bat *b2);
+double mgdk_BATcalccovariance_sample(mgdk_bat *b1, mgdk_bat *b2);
+double mgdk_BATcalccorrelation(mgdk_bat *b1, mgdk_bat *b2);
+/* quantiles (gdk_calc.h:135-138; doBATgroupquantile gdk_aggr.c:3881,
+ * BATgroupmedian :4225, BATgroupquantile :4233, BATgroupmedian_avg :4241,
+ * BATgroupquantile_avg :4247): g may be NULL (one result); _avg
+ * interpolates and returns dbl */
+mgdk_bat *mgdk_BATgroupmedian(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils);
+mgdk_bat *mgdk_BATgroupquantile(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, double quantile,
+				bool skip_nils);
+mgdk_bat *mgdk_BATgroupmedian_avg(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils);
+mgdk_bat *mgdk_BATgroupquantile_avg(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, double quantile,
+				    bool skip_nils);
 mgdk_bat *mgdk_BATgroupmin(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils);
 mgdk_bat *mgdk_BATgroupmax(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils);
 
@@ -228,6 +267,24 @@ int mgdk_BATgroup(mgdk_bat **groups, mgdk_bat **extents, mgdk_bat **histo,
  * which fixes the result order and properties ---------------------------- */
 int mgdk_BATjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r,
 		 mgdk_bat *sl, mgdk_bat *sr, bool nil_matches, mgdk_BUN estimate);
+/* the left-output join family (gdk/gdk.h:2264-2272; gdk_join.c:4320-4407,
+ * through leftjoin :4049): BATintersect / BATsemijoin (r2p must be NULL:
+ * which of several matches a semi join returns depends on the algorithm)
+ * the left candidates with a match, BATdiff those without (not_in: SQL NOT
+ * IN), as candidate lists; BATleftjoin / BATouterjoin the (left, match)
+ * pairs in left order (outer: a miss pairs with nil) -- refused when a left
+ * candidate matches twice (unless match_one asks for the reference's
+ * "more than one match").  Integer-like key types */
+mgdk_bat *mgdk_BATintersect(mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, bool nil_matches,
+			    bool max_one, mgdk_BUN estimate);
+mgdk_bat *mgdk_BATdiff(mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, bool nil_matches, bool not_in,
+		       mgdk_BUN estimate);
+int mgdk_BATsemijoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr,
+		     bool nil_matches, bool max_one, mgdk_BUN estimate);
+int mgdk_BATleftjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr,
+		     bool nil_matches, mgdk_BUN estimate);
+int mgdk_BATouterjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr,
+		      bool nil_matches, bool match_one, mgdk_BUN estimate);
 /* gdk/gdk.h:1524-1525 (gdk_batop.c:2002, :2181): whether b is sorted /
  * reverse sorted; what is found is recorded in b (tsorted, trevsorted,
  * tkey, tnosorted, tnorevsorted) as the reference does */
@@ -357,6 +414,30 @@ int mgdk_GDKanalyticalavg(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mg
 /* gdk_analytic_statistics.c:631 GDKanalyticalavginteger (gdk_analytic.h:42):
  * the average in b's integer type (bte..lng), rounded half away from zero;
  * r is a caller-allocated BAT of that type */
+/* gdk_analytic_statistics.c:897-965 GDK_ANALYTICAL_STDEV_VARIANCE
+ * (gdk_analytic.h:44-47), :1120-1188 GDK_ANALYTICAL_COVARIANCE (:48-49),
+ * :1379 GDKanalytical_correlation (:50): dbl per row over its frame (frame
+ * kinds as GDKanalyticalsum; others through the reference's segment tree);
+ * r is a caller-allocated dbl BAT; tpe = type of b (bte..hge, flt, dbl) */
+int mgdk_GDKanalytical_stddev_samp(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e,
+				   int tpe, int frame_type);
+int mgdk_GDKanalytical_stddev_pop(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e,
+				  int tpe, int frame_type);
+int mgdk_GDKanalytical_variance_samp(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e,
+				     int tpe, int frame_type);
+int mgdk_GDKanalytical_variance_pop(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e,
+				    int tpe, int frame_type);
+int mgdk_GDKanalytical_covariance_samp(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b1, mgdk_bat *b2,
+				       mgdk_bat *s, mgdk_bat *e, int tpe, int frame_type);
+int mgdk_GDKanalytical_covariance_pop(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s,
+				      mgdk_bat *e, int tpe, int frame_type);
+int mgdk_GDKanalytical_correlation(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s,
+				   mgdk_bat *e, int tpe, int frame_type);
+/* gdk_analytic_func.c:2479 GDKanalyticalprod (gdk_analytic.h:40): the
+ * product in tp2 (bte..hge from narrower or equal integers, flt from flt,
+ * dbl from flt / dbl) with the reference's overflow checks */
+int mgdk_GDKanalyticalprod(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e, int tp1,
+			   int tp2, int frame_type);
 int mgdk_GDKanalyticalavginteger(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e,
 				 int tpe, int frame_type);
 

@@ -723,17 +723,6 @@ k_gaggr_fin(const GPart *parts, BUN nwaves, int K, BUN ngrp, GAcc acc, unsigned 
 	}
 }
 
-struct AggrInit {
-	Cand ci;
-	oid min, max;
-	BUN ngrp;
-	const oid *gids;   // NULL: dense g
-	const uint8_t *g8; // 1-byte image of gids kept by BATgroup (or NULL)
-	oid gseq;
-	bool gsorted;      // g non-decreasing: every group a run of rows
-	bool gkey;         // g strictly increasing (or dense): at most one row per group
-};
-
 // ---- many groups, g sorted (every group a run of consecutive rows, as
 // BATgroup numbers ordered keys, a sub-grouping of them or a clustered
 // column): a wave owns a range of 64 * GS_U rows and a lane GS_U CONSECUTIVE
@@ -1946,6 +1935,66 @@ gsum_sorted_direct(const AggrInit &a, mgdk_bat *b, mgdk_bat *bn, int tp, bool sk
 
 }  // namespace
 
+namespace mgdk {
+
+int
+group_init(AggrInit *a, mgdk_bat **bp, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s)
+{
+	return aggr_init(a, bp, g, e, s);
+}
+
+GroupRows::GroupRows(BUN n, BUN ng)
+	: key(n * 4 + 4), key2(n * 4 + 4), v0(n * 4 + 4), v1(n * 4 + 4), cnt((ng + 1) * 4), start((ng + 1) * 8)
+{
+}
+
+bool
+GroupRows::ok() const
+{
+	return key.p && key2.p && v0.p && v1.p && cnt.p && start.p;
+}
+
+// a stable counting sort of the candidate rows by group (k_avg_keys' keys,
+// the exclusive scan of the group sizes, LSD radix passes over the keys)
+int
+group_rows(const AggrInit &a, GroupRows &gr)
+{
+	const BUN ng = a.ngrp;
+	gr.perm = nullptr;
+	gr.start_p = nullptr;
+	if (a.ci.n >= 0xffffffffull || ng >= 0xffffffffull) {
+		seterr("42000!more than 2^32-1 rows on the device path\n");
+		return -1;
+	}
+	if (ng <= 1)
+		return 0;
+	hipStream_t st = stream();
+	if (!hip_ok(hipMemsetAsync(gr.cnt.p, 0, (ng + 1) * 4, st), "memset"))
+		return -1;
+	hipLaunchKernelGGL(k_avg_keys, dim3(grid_for(a.ci.n, 2048, 1024)), dim3(256),
+			   ng < AVG_LDS_BINS ? (ng + 1) * 4 : 0, st, a.gids, a.gseq, a.min, ng, a.ci.n,
+			   gr.key.as<uint32_t>(), gr.cnt.as<uint32_t>());
+	int bits = 0;
+	while (bits < 32 && (ng >> bits))
+		bits++;
+	uint32_t *pm = nullptr;
+	if (exclusive_scan(gr.cnt.as<uint32_t>(), gr.start.as<uint64_t>(), ng + 1, nullptr) != 0 ||
+	    radix_sort_positions32(gr.key.as<uint32_t>(), gr.v0.as<uint32_t>(), gr.key2.as<uint32_t>(),
+				   gr.v1.as<uint32_t>(), a.ci.n, bits, &pm) != 0)
+		return -1;
+	gr.perm = pm;
+	gr.start_p = gr.start.as<uint64_t>();
+	return 0;
+}
+
+mgdk_bat *
+cand_values_at(mgdk_bat *b, const Cand &ci)
+{
+	return cand_values(b, ci);
+}
+
+}  // namespace mgdk
+
 extern "C" {
 
 // BATgroupsum (gdk/gdk_aggr.c:900)
@@ -2158,33 +2207,15 @@ mgdk_BATgroupavg(mgdk_bat **bnp, mgdk_bat **cntsp, mgdk_bat *b, mgdk_bat *g, mgd
 		}
 		bn = newbat(hb, MGDK_dbl, ng);
 		cn = newbat(hb, MGDK_lng, ng);
-		DevBuf key(a.ci.n * 4 + 4), key2(a.ci.n * 4 + 4), v0(a.ci.n * 4 + 4), v1(a.ci.n * 4 + 4),
-			cnt((ng + 1) * 4), start((ng + 1) * 8);
-		if (!bn || !cn || !key.p || !key2.p || !v0.p || !v1.p || !cnt.p || !start.p) {
+		GroupRows gr(a.ci.n, ng);
+		if (!bn || !cn || !gr.ok()) {
 			mgdk_BBPunfix(bn);
 			mgdk_BBPunfix(cn);
 			return -1;
 		}
-		const uint32_t *perm = nullptr;
-		const uint64_t *sp = nullptr;
-		bool ok = true;
-		if (ng > 1) {
-			ok = hip_ok(hipMemsetAsync(cnt.p, 0, (ng + 1) * 4, st), "memset");
-			if (ok) {
-				hipLaunchKernelGGL(k_avg_keys, dim3(grid_for(a.ci.n, 2048, 1024)), dim3(256),
-						   ng < AVG_LDS_BINS ? (ng + 1) * 4 : 0, st, a.gids,
-						   a.gseq, a.min, ng, a.ci.n, key.as<uint32_t>(), cnt.as<uint32_t>());
-				int bits = 0;
-				while (bits < 32 && (ng >> bits))
-					bits++;
-				uint32_t *pm = nullptr;
-				ok = exclusive_scan(cnt.as<uint32_t>(), start.as<uint64_t>(), ng + 1, nullptr) == 0 &&
-				     radix_sort_positions32(key.as<uint32_t>(), v0.as<uint32_t>(), key2.as<uint32_t>(),
-							    v1.as<uint32_t>(), a.ci.n, bits, &pm) == 0;
-				perm = pm;     // NULL: identity, rows already in group order
-				sp = start.as<uint64_t>();
-			}
-		}
+		bool ok = group_rows(a, gr) == 0;
+		const uint32_t *perm = gr.perm;
+		const uint64_t *sp = gr.start_p;
 		if (ok) {
 			const dim3 grid((unsigned) ((ng + 63) / 64)), blk(64);
 			if (bt == MGDK_flt)

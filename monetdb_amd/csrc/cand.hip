@@ -137,10 +137,12 @@ cl_of(const mgdk_bat *b, CL *c, mgdk_bat **own)
 	return 0;
 }
 
+}  // namespace
+
 // a sorted, duplicate-free oid BAT of n values: properties, and void when
 // dense (virtualize, gdk_select.c:31)
 mgdk_bat *
-finish(mgdk_bat *bn, BUN n)
+mgdk::cand_finish(mgdk_bat *bn, BUN n)
 {
 	bn->count = n;
 	bn->tsorted = 1;
@@ -167,6 +169,8 @@ finish(mgdk_bat *bn, BUN n)
 	bn->tmaxpos = n - 1;
 	return bn;
 }
+
+namespace {
 
 // the candidates of a that are (keep_in) or are not in b, as a new list
 mgdk_bat *
@@ -195,7 +199,7 @@ member(const CL &a, const CL &b, bool keep_in)
 				   pos->ttype == MGDK_void ? nullptr : (const oid *) pos->theap, pos->tseqbase, n, a.o,
 				   (oid *) bn->theap);
 	mgdk_BBPunfix(pos);
-	return finish(bn, n);
+	return cand_finish(bn, n);
 }
 
 struct Owned {
@@ -298,7 +302,7 @@ mgdk_BATmergecand(mgdk_bat *a, mgdk_bat *b)
 	if (cd.n)
 		hipLaunchKernelGGL(k_cand_place, dim3(grid_for(cd.n, 256 * 8, 8192)), dim3(256), 0, st, cd, ca,
 				   (oid *) bn->theap);
-	bn = finish(bn, n);
+	bn = cand_finish(bn, n);
 	mgdk_BBPunfix(d);
 	return bn;
 }

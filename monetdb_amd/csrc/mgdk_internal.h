@@ -143,6 +143,9 @@ size_t tail_bytes(const mgdk_bat *b, BUN n);
 // ordered compaction (select.hip): sorted positions base+i with flags[i]==1;
 // the result may be a dense (void) BAT.  Uses the thread's scratch buffer.
 mgdk_bat *compact_flags(const int8_t *flags, BUN n, oid base, bool nonzero = false);
+// a new sorted, duplicate-free oid BAT of n values (cand.hip): candidate-list
+// properties, and void when the values are dense (virtualize)
+mgdk_bat *cand_finish(mgdk_bat *bn, BUN n);
 
 // device-wide exclusive prefix sums (scan.hip); *total = sum of all inputs
 int exclusive_scan(const uint32_t *in, uint32_t *out, BUN n, uint64_t *total);
@@ -205,6 +208,36 @@ struct DevBuf {
 	DevBuf &operator=(const DevBuf &) = delete;
 	template <typename T> T *as() const { return (T *) p; }
 };
+
+// BATgroupaggrinit (gdk/gdk_aggr.c:65; aggr.hip): candidates, group id range
+// and the form of g.  group_init replaces *bp by b's values gathered at a
+// materialised candidate list (then ci is dense over them)
+struct AggrInit {
+	Cand ci;
+	oid min, max;
+	BUN ngrp;
+	const oid *gids;   // NULL: dense g
+	const uint8_t *g8; // 1-byte image of gids kept by BATgroup (or NULL)
+	oid gseq;
+	bool gsorted;      // g non-decreasing: every group a run of rows
+	bool gkey;         // g strictly increasing (or dense): at most one row per group
+};
+int group_init(AggrInit *a, mgdk_bat **bp, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s);
+// b's values at a materialised candidate list, head at the first candidate
+// (kept alive by a small per-thread ring: use before the next few calls)
+mgdk_bat *cand_values_at(mgdk_bat *b, const Cand &ci);
+// the candidate rows grouped by group id, candidate order kept within a
+// group (aggr.hip): rows perm[start[k]] .. perm[start[k+1] - 1] of group k;
+// perm NULL: the identity; start_p NULL (one group): every row, whose ids
+// the reader range-checks.  Rows outside the group range sort behind.
+struct GroupRows {
+	DevBuf key, key2, v0, v1, cnt, start;
+	const uint32_t *perm = nullptr;
+	const uint64_t *start_p = nullptr;
+	GroupRows(BUN n, BUN ng);
+	bool ok() const;
+};
+int group_rows(const AggrInit &a, GroupRows &gr);
 
 }  // namespace mgdk
 

@@ -128,9 +128,32 @@ _SIGS = {
     "mgdk_BATgroupavg3combine": (P, [P, P, P, P, P, C.c_bool]),
     "mgdk_BATgroupavg3": (C.c_int, [PP, PP, PP, P, P, P, P, C.c_bool]),
     "mgdk_BATgroupmin": (P, [P, P, P, P, C.c_int, C.c_bool]),
+    "mgdk_BATgroupstdev_sample": (P, [P, P, P, P, C.c_int, C.c_bool]),
+    "mgdk_BATgroupstdev_population": (P, [P, P, P, P, C.c_int, C.c_bool]),
+    "mgdk_BATgroupvariance_sample": (P, [P, P, P, P, C.c_int, C.c_bool]),
+    "mgdk_BATgroupvariance_population": (P, [P, P, P, P, C.c_int, C.c_bool]),
+    "mgdk_BATgroupmedian": (P, [P, P, P, P, C.c_int, C.c_bool]),
+    "mgdk_BATgroupmedian_avg": (P, [P, P, P, P, C.c_int, C.c_bool]),
+    "mgdk_BATgroupcovariance_sample": (P, [P, P, P, P, P, C.c_int, C.c_bool]),
+    "mgdk_BATgroupcovariance_population": (P, [P, P, P, P, P, C.c_int, C.c_bool]),
+    "mgdk_BATgroupcorrelation": (P, [P, P, P, P, P, C.c_int, C.c_bool]),
+    "mgdk_BATgroupquantile": (P, [P, P, P, P, C.c_int, C.c_double, C.c_bool]),
+    "mgdk_BATgroupquantile_avg": (P, [P, P, P, P, C.c_int, C.c_double, C.c_bool]),
+    "mgdk_BATcalcstdev_population": (C.c_double, [C.POINTER(C.c_double), P]),
+    "mgdk_BATcalcstdev_sample": (C.c_double, [C.POINTER(C.c_double), P]),
+    "mgdk_BATcalcvariance_population": (C.c_double, [C.POINTER(C.c_double), P]),
+    "mgdk_BATcalcvariance_sample": (C.c_double, [C.POINTER(C.c_double), P]),
+    "mgdk_BATcalccovariance_population": (C.c_double, [P, P]),
+    "mgdk_BATcalccovariance_sample": (C.c_double, [P, P]),
+    "mgdk_BATcalccorrelation": (C.c_double, [P, P]),
     "mgdk_BATgroupmax": (P, [P, P, P, P, C.c_int, C.c_bool]),
     "mgdk_BATgroup": (C.c_int, [PP, PP, PP, P, P, P, P, P]),
     "mgdk_BATjoin": (C.c_int, [PP, PP, P, P, P, P, C.c_bool, C.c_uint64]),
+    "mgdk_BATintersect": (P, [P, P, P, P, C.c_bool, C.c_bool, C.c_uint64]),
+    "mgdk_BATdiff": (P, [P, P, P, P, C.c_bool, C.c_bool, C.c_uint64]),
+    "mgdk_BATsemijoin": (C.c_int, [PP, PP, P, P, P, P, C.c_bool, C.c_bool, C.c_uint64]),
+    "mgdk_BATleftjoin": (C.c_int, [PP, PP, P, P, P, P, C.c_bool, C.c_uint64]),
+    "mgdk_BATouterjoin": (C.c_int, [PP, PP, P, P, P, P, C.c_bool, C.c_bool, C.c_uint64]),
     "mgdk_BATordered": (C.c_bool, [P]),
     "mgdk_BATordered_rev": (C.c_bool, [P]),
     "mgdk_BATsort": (C.c_int, [PP, PP, PP, P, P, P, C.c_bool, C.c_bool, C.c_bool]),
@@ -174,6 +197,14 @@ _SIGS = {
     "mgdk_GDKanalyticalmin": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_int]),
     "mgdk_GDKanalyticalmax": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_int]),
     "mgdk_GDKanalyticalavginteger": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_int]),
+    "mgdk_GDKanalytical_stddev_samp": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_int]),
+    "mgdk_GDKanalytical_stddev_pop": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_int]),
+    "mgdk_GDKanalytical_variance_samp": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_int]),
+    "mgdk_GDKanalytical_variance_pop": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_int]),
+    "mgdk_GDKanalytical_covariance_samp": (C.c_int, [C.c_void_p] * 7 + [C.c_int, C.c_int]),
+    "mgdk_GDKanalytical_covariance_pop": (C.c_int, [C.c_void_p] * 7 + [C.c_int, C.c_int]),
+    "mgdk_GDKanalytical_correlation": (C.c_int, [C.c_void_p] * 7 + [C.c_int, C.c_int]),
+    "mgdk_GDKanalyticalprod": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_int, C.c_int]),
     "mgdk_BATlowerbound2": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
                                       C.c_void_p]),
     "mgdk_BATupload_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
@@ -595,6 +626,91 @@ def BATgroupmax(b, g, e, skip_nils=True, s=None):
     return BAT(lib().mgdk_BATgroupmax(b.ptr, g.ptr, _p(e), _p(s), b.ttype, skip_nils))
 
 
+def _stat1(name, b, g, e, skip_nils, s):
+    return BAT(getattr(lib(), "mgdk_BATgroup" + name)(b.ptr, _p(g), _p(e), _p(s), TYPE_dbl, skip_nils))
+
+
+def _stat2(name, b1, b2, g, e, skip_nils, s):
+    return BAT(getattr(lib(), "mgdk_BATgroup" + name)(b1.ptr, b2.ptr, _p(g), _p(e), _p(s), TYPE_dbl, skip_nils))
+
+
+def BATgroupstdev_sample(b, g, e, skip_nils=True, s=None):
+    """gdk_aggr.c:4778 (dogroupstdev :4612): Welford per group, dbl"""
+    return _stat1("stdev_sample", b, g, e, skip_nils, s)
+
+
+def BATgroupstdev_population(b, g, e, skip_nils=True, s=None):
+    """gdk_aggr.c:4785"""
+    return _stat1("stdev_population", b, g, e, skip_nils, s)
+
+
+def BATgroupvariance_sample(b, g, e, skip_nils=True, s=None):
+    """gdk_aggr.c:4793"""
+    return _stat1("variance_sample", b, g, e, skip_nils, s)
+
+
+def BATgroupvariance_population(b, g, e, skip_nils=True, s=None):
+    """gdk_aggr.c:4801"""
+    return _stat1("variance_population", b, g, e, skip_nils, s)
+
+
+def BATgroupcovariance_sample(b1, b2, g, e, skip_nils=True, s=None):
+    """gdk_aggr.c:5000 (dogroupcovariance :4851)"""
+    return _stat2("covariance_sample", b1, b2, g, e, skip_nils, s)
+
+
+def BATgroupcovariance_population(b1, b2, g, e, skip_nils=True, s=None):
+    """gdk_aggr.c:5007"""
+    return _stat2("covariance_population", b1, b2, g, e, skip_nils, s)
+
+
+def BATgroupcorrelation(b1, b2, g, e, skip_nils=True, s=None):
+    """gdk_aggr.c:5057"""
+    return _stat2("correlation", b1, b2, g, e, skip_nils, s)
+
+
+def _calc(fn, *args):
+    lib().mgdk_GDKclrerr()
+    v = fn(*args)
+    msg = lib().mgdk_GDKerrbuf().decode()
+    if msg:
+        raise GDKError(msg)
+    return v
+
+
+def BATcalcvariance(b, sample, stdev=False):
+    """BATcalc{stdev,variance}_{sample,population}(&avg, b) (gdk_aggr.c:4327-4380):
+    returns (value, average); nil is NaN"""
+    avg = C.c_double()
+    name = "mgdk_BATcalc%s_%s" % ("stdev" if stdev else "variance", "sample" if sample else "population")
+    v = _calc(getattr(lib(), name), C.byref(avg), b.ptr)
+    return v, avg.value
+
+
+def BATcalccovariance(b1, b2, sample):
+    """BATcalccovariance_{sample,population} (gdk_aggr.c:4449-4476)"""
+    name = "mgdk_BATcalccovariance_%s" % ("sample" if sample else "population")
+    return _calc(getattr(lib(), name), b1.ptr, b2.ptr)
+
+
+def BATcalccorrelation(b1, b2):
+    """gdk_aggr.c:4503"""
+    return _calc(lib().mgdk_BATcalccorrelation, b1.ptr, b2.ptr)
+
+
+def BATgroupquantile(b, g, e, quantile, skip_nils=True, s=None, average=False):
+    """doBATgroupquantile (gdk_aggr.c:3881) through BATgroupquantile (:4233) or
+    BATgroupquantile_avg (:4247); g may be None"""
+    f = lib().mgdk_BATgroupquantile_avg if average else lib().mgdk_BATgroupquantile
+    return BAT(f(b.ptr, _p(g), _p(e), _p(s), b.ttype, quantile, skip_nils))
+
+
+def BATgroupmedian(b, g, e, skip_nils=True, s=None, average=False):
+    """BATgroupmedian (gdk_aggr.c:4225) / BATgroupmedian_avg (:4241)"""
+    f = lib().mgdk_BATgroupmedian_avg if average else lib().mgdk_BATgroupmedian
+    return BAT(f(b.ptr, _p(g), _p(e), _p(s), b.ttype, skip_nils))
+
+
 def BATgroupavg(b, g, e, skip_nils=True, s=None, scale=0, want_counts=True):
     """BATgroupavg(&bn, &cnts, b, g, e, s, TYPE_dbl, skip_nils, scale)
     (gdk/gdk_aggr.c:1801); returns (averages, counts or None)."""
@@ -630,6 +746,38 @@ def BATjoin(l, r, sl=None, sr=None, nil_matches=False, estimate=0):
     a, b = P(), P()
     _chk(lib().mgdk_BATjoin(C.byref(a), C.byref(b), l.ptr, r.ptr, _p(sl), _p(sr), nil_matches,
                             estimate))
+    return BAT(a), BAT(b)
+
+
+def BATintersect(l, r, sl=None, sr=None, nil_matches=False, max_one=False, estimate=0):
+    """gdk_join.c:4366: the left candidates whose value occurs on the right."""
+    return BAT(lib().mgdk_BATintersect(l.ptr, r.ptr, _p(sl), _p(sr), nil_matches, max_one, estimate))
+
+
+def BATdiff(l, r, sl=None, sr=None, nil_matches=False, not_in=False, estimate=0):
+    """gdk_join.c:4388: the left candidates whose value does not occur on the right."""
+    return BAT(lib().mgdk_BATdiff(l.ptr, r.ptr, _p(sl), _p(sr), nil_matches, not_in, estimate))
+
+
+def BATsemijoin(l, r, sl=None, sr=None, nil_matches=False, max_one=False, estimate=0):
+    """gdk_join.c:4346 with r2p = NULL: the left output (a candidate list)."""
+    a = P()
+    _chk(lib().mgdk_BATsemijoin(C.byref(a), None, l.ptr, r.ptr, _p(sl), _p(sr), nil_matches, max_one, estimate))
+    return BAT(a)
+
+
+def BATleftjoin(l, r, sl=None, sr=None, nil_matches=False, estimate=0):
+    """gdk_join.c:4320: (left, match) pairs in left order."""
+    a, b = P(), P()
+    _chk(lib().mgdk_BATleftjoin(C.byref(a), C.byref(b), l.ptr, r.ptr, _p(sl), _p(sr), nil_matches, estimate))
+    return BAT(a), BAT(b)
+
+
+def BATouterjoin(l, r, sl=None, sr=None, nil_matches=False, match_one=False, estimate=0):
+    """gdk_join.c:4334: (left, match or nil) pairs in left order."""
+    a, b = P(), P()
+    _chk(lib().mgdk_BATouterjoin(C.byref(a), C.byref(b), l.ptr, r.ptr, _p(sl), _p(sr), nil_matches, match_one,
+                                 estimate))
     return BAT(a), BAT(b)
 
 
@@ -827,6 +975,26 @@ def GDKanalyticalavg(b, p, o, s, e, frame_type):
     (gdk/gdk_analytic_statistics.c:364)."""
     r = BAT(lib().mgdk_COLnew(0, TYPE_dbl, max(1, b.count())))
     _chk(lib().mgdk_GDKanalyticalavg(r.ptr, _p(p), _p(o), b.ptr, _p(s), _p(e), b.ttype, frame_type))
+    return r
+
+
+def GDKanalytical_stat(name, b1, b2, p, o, s, e, frame_type):
+    """GDKanalytical_<name> (gdk_analytic_statistics.c:962-1443): name one of
+    stddev_samp, stddev_pop, variance_samp, variance_pop (b2 None),
+    covariance_samp, covariance_pop, correlation; dbl per row"""
+    r = BAT(lib().mgdk_COLnew(0, TYPE_dbl, max(1, b1.count())))
+    f = getattr(lib(), "mgdk_GDKanalytical_" + name)
+    if b2 is None:
+        _chk(f(r.ptr, _p(p), _p(o), b1.ptr, _p(s), _p(e), b1.ttype, frame_type))
+    else:
+        _chk(f(r.ptr, _p(p), _p(o), b1.ptr, b2.ptr, _p(s), _p(e), b1.ttype, frame_type))
+    return r
+
+
+def GDKanalyticalprod(b, p, o, s, e, tp2, frame_type):
+    """Windowed product per row over its frame (gdk_analytic_func.c:2479)."""
+    r = BAT(lib().mgdk_COLnew(0, tp2, max(1, b.count())))
+    _chk(lib().mgdk_GDKanalyticalprod(r.ptr, _p(p), _p(o), b.ptr, _p(s), _p(e), b.ttype, tp2, frame_type))
     return r
 
 

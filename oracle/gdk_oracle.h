@@ -139,6 +139,22 @@ ora_bat *ora_groupminmax(const ora_bat *b, const ora_bat *g, const ora_bat *e,
 			 const ora_bat *s, bool skip_nils, bool domax);
 /* BATjoin with its algorithm choice (gdk_oracle_join.c); l and r receive
  * the ordering / key flags the reference caches on them */
+/* BATintersect / BATsemijoin's left output (only_misses false) and BATdiff
+ * (true) (gdk_join.c:4343-4407, leftjoin :4049); BATleftjoin / BATouterjoin
+ * for at most one match per left candidate (-2: several, not restated) */
+/* statistics (gdk/gdk_aggr.c:4255-5202): kind 0 stdev / variance, 1
+ * covariance, 2 correlation (gdk_oracle_grp.c) */
+ora_bat *ora_groupmoments(int kind, const ora_bat *b1, const ora_bat *b2, const ora_bat *g, const ora_bat *e,
+			  const ora_bat *s, bool skip_nils, bool issample, bool variance);
+int ora_calcmoments(double *res, double *avgp, int kind, const ora_bat *b1, const ora_bat *b2, bool issample,
+		    bool variance);
+/* doBATgroupquantile (gdk/gdk_aggr.c:3881); g may be NULL */
+ora_bat *ora_groupquantile(const ora_bat *b, const ora_bat *g, const ora_bat *e, const ora_bat *s, double quantile,
+			   bool skip_nils, bool average);
+ora_bat *ora_semijoin_cands(ora_bat *l, ora_bat *r, const ora_bat *sl, const ora_bat *sr, bool nil_matches,
+			    bool max_one, bool only_misses, bool not_in);
+int ora_leftjoin(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r, const ora_bat *sl, const ora_bat *sr,
+		 bool nil_matches, bool outer, bool match_one);
 int ora_join(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r,
 	     const ora_bat *sl, const ora_bat *sr, bool nil_matches);
 int ora_join_algo(ora_bat *l, ora_bat *r, const ora_bat *sl, const ora_bat *sr);
@@ -190,6 +206,14 @@ int ora_analyticalsum(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_
 		      const ora_bat *s, const ora_bat *e, int tp1, int tp2, int frame_type);
 int ora_analyticalavg(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_bat *b,
 		      const ora_bat *s, const ora_bat *e, int tpe, int frame_type);
+/* gdk_analytic_statistics.c:897-1443 (kind 0 stddev / variance, op 0
+ * stddev_samp 1 stddev_pop 2 variance_samp 3 variance_pop; kind 1
+ * covariance, op 0 samp 1 pop; kind 2 correlation) and
+ * gdk_analytic_func.c:2479 GDKanalyticalprod (gdk_oracle_winstats.c) */
+int ora_analyticalstat(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_bat *b1, const ora_bat *b2,
+		       const ora_bat *s, const ora_bat *e, int kind, int op, int frame_type);
+int ora_analyticalprod(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_bat *b, const ora_bat *s,
+		       const ora_bat *e, int tp2, int frame_type);
 int ora_analyticalavginteger(ora_bat *r, const ora_bat *p, const ora_bat *o, const ora_bat *b,
 			     const ora_bat *s, const ora_bat *e, int tpe, int frame_type);
 /* gdk_analytic_func.c :124 ntile, :230 first, :312 last, :421 nth_value,

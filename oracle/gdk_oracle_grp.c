@@ -929,3 +929,404 @@ ora_groupminmax(const ora_bat *b, const ora_bat *g, const ora_bat *e,
  * forward and gives one past the last row; a nil row's frame is its run of
  * nils; a limit of GDK_lng_max is "unbounded".  Results are absolute row
  * numbers.  Supports lng values with a lng limit. */
+
+/* ---------------------------------------------------------------------- */
+/* statistics (gdk/gdk_aggr.c:4255-5202): Welford updates per group in
+ * candidate order.  AGGR_STDEV (:4561-4601) for dogroupstdev (:4612-4775),
+ * AGGR_COVARIANCE (:4808-4848) for dogroupcovariance (:4851-4997),
+ * AGGR_CORRELATION (:5013-5054) for BATgroupcorrelation (:5057-5202); the
+ * _SINGLE loops (:4257, :4382, :4478) for calcvariance (:4276),
+ * calccovariance (:4404) and BATcalccorrelation (:4503).  A nil value makes
+ * its group nil for good unless skip_nils (cnts = BUN_NONE); the whole-column
+ * forms skip nils and stop with an overflow error at the first infinite
+ * accumulator, the grouped ones check the final accumulators. */
+
+#define ST_VAR 0
+#define ST_COV 1
+#define ST_COR 2
+#define CNT_NONE (~(uint64_t) 0)
+
+/* (dbl) of row p; true when nil */
+static bool
+dbl_at(const ora_bat *b, uint64_t p, double *d)
+{
+	if (b->type == ORA_flt) {
+		*d = ((const float *) b->base)[p];
+		return isnan(*d);
+	}
+	if (b->type == ORA_dbl) {
+		*d = ((const double *) b->base)[p];
+		return isnan(*d);
+	}
+	ora_hge v;
+	const bool nil = val_at(b, p, &v);
+	*d = (double) v;
+	return nil;
+}
+
+static bool
+moment_type(int tp)
+{
+	return tp == ORA_bte || tp == ORA_sht || tp == ORA_int || tp == ORA_lng || tp == ORA_hge ||
+	       tp == ORA_flt || tp == ORA_dbl;
+}
+
+static ora_bat *
+const_dbl(ora_oid hseq, double v, uint64_t n)
+{
+	ora_bat *bn = ora_new(ORA_dbl, n, hseq);
+	for (uint64_t k = 0; k < n; k++)
+		((double *) bn->base)[k] = v;
+	bn->sorted = bn->revsorted = 1;
+	bn->key = n <= 1;
+	bn->nil = n > 0 && isnan(v);
+	bn->nonil = !bn->nil;
+	return bn;
+}
+
+struct moments {
+	uint64_t cnt;
+	double mean1, mean2, m2, up, down1, down2;
+};
+
+/* one Welford step; returns true when the whole-column form overflows */
+static bool
+moment_step(struct moments *m, int kind, double x, double y, bool single)
+{
+	m->cnt++;
+	const double n = (double) m->cnt;
+	const double delta1 = x - m->mean1;
+	m->mean1 += delta1 / n;
+	if (kind == ST_VAR) {
+		m->m2 += delta1 * (x - m->mean1);
+		return single && isinf(m->m2);
+	}
+	const double delta2 = y - m->mean2;
+	m->mean2 += delta2 / n;
+	if (kind == ST_COV) {
+		m->m2 += delta1 * (y - m->mean2);
+		return single && isinf(m->m2);
+	}
+	const double aux = y - m->mean2;
+	m->up += delta1 * aux;
+	m->down1 += delta1 * (x - m->mean1);
+	m->down2 += delta2 * aux;
+	return single && (isinf(m->up) || isinf(m->down1) || isinf(m->down2));
+}
+
+ora_bat *
+ora_groupmoments(int kind, const ora_bat *b1, const ora_bat *b2, const ora_bat *g, const ora_bat *e,
+		 const ora_bat *s, bool skip_nils, bool issample, bool variance)
+{
+	aggr_ctx a;
+	if (g == NULL) {
+		ora_seterr("b and g must be aligned\n");
+		return NULL;
+	}
+	if (kind != ST_VAR && (b2 == NULL || b1->count != b2->count || b1->type != b2->type)) {
+		ora_seterr("b1 and b2 must be aligned\n");
+		return NULL;
+	}
+	if (aggr_init(&a, b1, g, e, s) < 0)
+		return NULL;
+	const uint64_t ng = a.ngrp;
+	if (b1->count == 0 || ng == 0)
+		return const_dbl(ng ? a.min : 0, nan(""), ng);
+	const bool singles = g->tseqbase != ORA_OID_NIL || (g->key && g->nonil);
+	if (kind == ST_VAR) {
+		/* :4652-4661 */
+		if ((e == NULL || (e->count == a.ci.n && e->hseqbase == b1->hseqbase)) && singles &&
+		    (issample || b1->nonil))
+			return const_dbl(a.min, issample ? nan("") : 0.0, ng);
+	} else if ((e == NULL || (e->count == b1->count &&
+				  (e->hseqbase == b1->hseqbase || e->hseqbase == b2->hseqbase))) && singles) {
+		/* :4887-4896, :5091-5097 */
+		if (kind == ST_COR)
+			return const_dbl(a.min, nan(""), ng);
+		if (issample || (b1->nonil && b2->nonil))
+			return const_dbl(a.min, issample ? nan("") : 0.0, ng);
+	}
+	if (!moment_type(b1->type)) {
+		ora_seterr("type (%d) not supported.\n", b1->type);
+		return NULL;
+	}
+	struct moments *m = calloc(ng, sizeof(*m));
+	for (uint64_t i = 0; i < a.ci.n; i++) {
+		ora_oid gid;
+		if (!aggr_gid(&a, i, &gid))
+			continue;
+		const uint64_t p = ci_get(&a.ci, i) - b1->hseqbase;
+		double x, y = 0;
+		bool nil = dbl_at(b1, p, &x);
+		if (kind != ST_VAR)
+			nil |= dbl_at(b2, p, &y);
+		if (nil) {
+			if (!skip_nils)
+				m[gid].cnt = CNT_NONE;
+		} else if (m[gid].cnt != CNT_NONE) {
+			moment_step(&m[gid], kind, x, y, false);
+		}
+	}
+	ora_bat *bn = ora_new(ORA_dbl, ng, a.min);
+	double *dbls = bn->base;
+	uint64_t nils = 0;
+	for (uint64_t k = 0; k < ng; k++) {
+		const struct moments *q = &m[k];
+		if (kind == ST_COR) {
+			if (q->cnt <= 1 || q->cnt == CNT_NONE || q->down1 == 0 || q->down2 == 0) {
+				dbls[k] = nan("");
+				nils++;
+			} else if (isinf(q->up) || isinf(q->down1) || isinf(q->down2)) {
+				goto overflow;
+			} else {
+				const double n = (double) q->cnt;
+				dbls[k] = (q->up / n) / (sqrt(q->down1 / n) * sqrt(q->down2 / n));
+			}
+		} else if (q->cnt == 0 || q->cnt == CNT_NONE) {
+			dbls[k] = nan("");
+			nils++;
+		} else if (q->cnt == 1) {
+			dbls[k] = issample ? nan("") : 0;
+			nils += issample;
+		} else if (isinf(q->m2)) {
+			goto overflow;
+		} else {
+			dbls[k] = q->m2 / (double) (q->cnt - issample);
+			if (kind == ST_VAR && !variance)
+				dbls[k] = sqrt(dbls[k]);
+		}
+	}
+	free(m);
+	bn->sorted = bn->revsorted = bn->key = ng <= 1;
+	bn->nil = nils != 0;
+	bn->nonil = nils == 0;
+	return bn;
+overflow:
+	free(m);
+	ora_free(bn);
+	ora_seterr("22003!overflow in calculation.\n");
+	return NULL;
+}
+
+int
+ora_calcmoments(double *res, double *avgp, int kind, const ora_bat *b1, const ora_bat *b2, bool issample,
+		bool variance)
+{
+	*res = nan("");
+	if (avgp)
+		*avgp = nan("");
+	if (!moment_type(b1->type)) {
+		ora_seterr("type (%d) not supported.\n", b1->type);
+		return -1;
+	}
+	if (kind != ST_VAR && (b2 == NULL || b1->count != b2->count || b1->type != b2->type)) {
+		ora_seterr("b1 and b2 must be aligned\n");
+		return -1;
+	}
+	struct moments m = {0};
+	for (uint64_t i = 0; i < b1->count; i++) {
+		double x, y = 0;
+		bool nil = dbl_at(b1, i, &x);
+		if (kind != ST_VAR)
+			nil |= dbl_at(b2, i, &y);
+		if (nil)
+			continue;
+		if (moment_step(&m, kind, x, y, true)) {
+			ora_seterr("22003!overflow in calculation.\n");
+			return -1;
+		}
+	}
+	if (kind == ST_COR) {
+		const double n = (double) m.cnt;
+		if (m.cnt != 0 && m.down1 != 0 && m.down2 != 0)
+			*res = (m.up / n) / (sqrt(m.down1 / n) * sqrt(m.down2 / n));
+		return 0;
+	}
+	if (m.cnt <= (uint64_t) issample)
+		return 0;
+	if (avgp)
+		*avgp = m.mean1;
+	*res = m.m2 / (double) (m.cnt - issample);
+	if (kind == ST_VAR && !variance)
+		*res = sqrt(*res);   /* BATcalcstdev_*: is_dbl_nil(v) ? dbl_nil : sqrt(v) */
+	return 0;
+}
+
+/* ---------------------------------------------------------------------- */
+/* doBATgroupquantile (gdk/gdk_aggr.c:3881-4222): b (and g) at the candidates
+ * (BATproject(s, .)), g sorted, b sorted within the groups (BATsort twice);
+ * per run of equal group ids (in sorted order) the value at
+ * r + p - (BUN) (p + 0.5 - f), f = (p - r - 1) * quantile, r past the nils
+ * with skip_nils; the _avg forms interpolate the two neighbours in dbl
+ * (DO_QUANTILE_AVG :3860).  Results go to consecutive positions, nil padded
+ * to ngrp (:4073-4077); dense g: a copy of b (:3968-3981). */
+
+static bool
+nil_at(const ora_bat *b, uint64_t p)
+{
+	double d;
+	if (b->type == ORA_flt || b->type == ORA_dbl)
+		return dbl_at(b, p, &d);
+	const char *x = (const char *) b->base + p * b->width;
+	switch (b->type) {
+	case ORA_daytime: case ORA_timestamp: return *(const int64_t *) x == INT64_MIN;
+	default: { ora_hge v; return val_at(b, p, &v); }
+	}
+}
+
+static void
+set_nil(ora_bat *bn, uint64_t k)
+{
+	char *x = (char *) bn->base + k * bn->width;
+	switch (bn->type) {
+	case ORA_flt: ((float *) bn->base)[k] = nanf(""); break;
+	case ORA_dbl: ((double *) bn->base)[k] = nan(""); break;
+	case ORA_bit: case ORA_bte: *(int8_t *) x = INT8_MIN; break;
+	case ORA_sht: *(int16_t *) x = INT16_MIN; break;
+	case ORA_int: case ORA_date: *(int32_t *) x = INT32_MIN; break;
+	case ORA_hge: *(ora_hge *) x = HGE_NIL; break;
+	default: *(int64_t *) x = INT64_MIN; break;   /* lng, oid, daytime, timestamp */
+	}
+}
+
+/* the quantile of the sorted run [r, p) of v into bn[k]; true when nil */
+static bool
+quantile_of(ora_bat *bn, uint64_t k, const ora_bat *v, uint64_t r, uint64_t p, double quantile, bool skip_nils,
+	    bool average)
+{
+	if (skip_nils)
+		while (r < p && nil_at(v, r))
+			r++;
+	if (r == p) {
+		set_nil(bn, k);
+		return true;
+	}
+	const double f = (double) (p - r - 1) * quantile;
+	if (average) {
+		const double lo = floor(f), hi = ceil(f);
+		double low, high;
+		/* DO_QUANTILE_AVG: low from idxhi, high from idxlo */
+		const bool n1 = dbl_at(v, r + (uint64_t) hi, &low), n2 = dbl_at(v, r + (uint64_t) lo, &high);
+		if (n1 || n2) {
+			set_nil(bn, k);
+			return true;
+		}
+		((double *) bn->base)[k] = (f - lo) * low + (lo + 1 - f) * high;
+		return false;
+	}
+	const uint64_t qi = r + p - (uint64_t) ((double) p + 0.5 - f);
+	memcpy((char *) bn->base + k * bn->width, (const char *) v->base + qi * v->width, v->width);
+	return nil_at(v, qi);
+}
+
+ora_bat *
+ora_groupquantile(const ora_bat *b, const ora_bat *g, const ora_bat *e, const ora_bat *s, double quantile,
+		  bool skip_nils, bool average)
+{
+	if (average && !moment_type(b->type)) {
+		ora_seterr("incompatible type\n");
+		return NULL;
+	}
+	ora_oid min = 0;
+	uint64_t ngrp = 1;
+	aggr_ctx a;
+	ora_ci ci;
+	if (ora_ci_init(&ci, b, s) < 0)
+		return NULL;
+	if (g) {
+		if (aggr_init(&a, b, g, e, s) < 0)
+			return NULL;
+		min = a.min;
+		ngrp = a.ngrp;
+	}
+	if (quantile < 0 || quantile > 1) {
+		ora_seterr("cannot determine quantile for p=%f (p has to be in [0,1])\n", quantile);
+		return NULL;
+	}
+	const int rt = average ? ORA_dbl : b->type;
+	if (b->count == 0 || ngrp == 0 || isnan(quantile)) {
+		ora_bat *bn = ora_new(rt, ngrp, ngrp == 0 ? 0 : min);
+		for (uint64_t k = 0; k < ngrp; k++)
+			set_nil(bn, k);
+		bn->sorted = bn->revsorted = 1;
+		bn->key = ngrp <= 1;
+		bn->nil = ngrp > 0;
+		bn->nonil = ngrp == 0;
+		return bn;
+	}
+	/* BATproject(s, g): g is aligned with the candidates */
+	if (g && !ci.dense && ci.n && ci_get(&ci, ci.n - 1) - ci_get(&ci, 0) + 1 != ci.n) {
+		ora_seterr("BATproject: does not match always\n");
+		return NULL;
+	}
+	/* b at the candidates, head aligned with g */
+	ora_bat *bv = ora_new(b->type, ci.n, g ? g->hseqbase : 0);
+	for (uint64_t i = 0; i < ci.n; i++)
+		memcpy((char *) bv->base + i * bv->width,
+		       (const char *) b->base + (ci_get(&ci, i) - b->hseqbase) * b->width, b->width);
+	if (g && g->tseqbase != ORA_OID_NIL) {
+		ora_bat *bn = ora_new(rt, ci.n, g->tseqbase);
+		for (uint64_t i = 0; i < ci.n; i++) {
+			if (average) {
+				double d;
+				if (dbl_at(bv, i, &d))
+					d = nan("");
+				((double *) bn->base)[i] = d;
+			} else {
+				memcpy((char *) bn->base + i * bn->width, (const char *) bv->base + i * bv->width, bv->width);
+			}
+		}
+		ora_free(bv);
+		return bn;
+	}
+	ora_bat *sv = NULL, *gs = NULL, *go = NULL;
+	if (g) {
+		ora_bat *gp = (ora_bat *) g;
+		if (ora_BATsort(&gs, &go, NULL, gp, NULL, NULL, false, false, false) < 0 ||
+		    ora_BATsort(&sv, NULL, NULL, bv, go, gs, false, false, false) < 0) {
+			ora_free(bv);
+			ora_free(gs);
+			ora_free(go);
+			return NULL;
+		}
+	} else if (ora_BATsort(&sv, NULL, NULL, bv, NULL, NULL, false, false, false) < 0) {
+		ora_free(bv);
+		return NULL;
+	}
+	ora_bat *bn = ora_new(rt, ngrp, g ? min : 0);
+	uint64_t nils = 0, k = 0;
+	if (g) {
+		for (uint64_t r = 0, p; r < ci.n; r = p, k++) {
+			ora_hge gr, gq;
+			val_at(gs, r, &gr);
+			for (p = r + 1; p < ci.n; p++) {
+				val_at(gs, p, &gq);
+				if (gq != gr)
+					break;
+			}
+			if (k >= ngrp) {
+				ora_seterr("BATgroupquantile: more group ids than groups\n");
+				ora_free(bn);
+				bn = NULL;
+				goto done;
+			}
+			nils += quantile_of(bn, k, sv, r, p, quantile, skip_nils, average);
+		}
+	} else {
+		nils += quantile_of(bn, 0, sv, 0, ci.n, quantile, skip_nils, average);
+		k = 1;
+	}
+	for (; k < ngrp; k++) {
+		set_nil(bn, k);
+		nils++;
+	}
+	bn->sorted = bn->revsorted = bn->key = ngrp <= 1;
+	bn->nil = nils != 0;
+	bn->nonil = nils == 0;
+done:
+	ora_free(bv);
+	ora_free(sv);
+	ora_free(gs);
+	ora_free(go);
+	return bn;
+}

@@ -957,3 +957,224 @@ ora_join_algo(ora_bat *l, ora_bat *r, const ora_bat *sl, const ora_bat *sr)
 		return 7;
 	return swap ? 8 : 9;
 }
+
+/* ---- semi / anti / outer joins (gdk_join.c:4049 leftjoin, :4320-4407) ----
+ * BATintersect / BATsemijoin's r1 (semi), BATdiff (only_misses, not_in) and
+ * BATleftjoin / BATouterjoin (nil_on_miss, match_one) restated by their
+ * result definitions, which every path of leftjoin shares:
+ *   a left candidate's matches are the right candidates with an equal value;
+ *   a nil never matches unless nil_matches (gdk_join.c:3127, :2338);
+ *   semi: the left candidates with a match, once each, in order (virtualized);
+ *     max_one: "more than one match" when a candidate has two (:2760);
+ *   only_misses: the left candidates without a match; not_in additionally
+ *     drops nil left values and returns nothing when a right candidate is nil
+ *     (:3027-3060, :2038) -- except on the dense-right path, mergejoin_void
+ *     (:4096-4101), which has no not_in and no nil on the right;
+ *   empty left or right side: nomatch (:301-360), the misses being every
+ *   left candidate;
+ *   left / outer join: the matched pairs in left order (outer: a miss gives
+ *   (l, nil)); a left candidate with several matches orders them by the
+ *   algorithm leftjoin picks, which this restatement does not model, so it is
+ *   refused (-2) unless match_one asks for the reference's error. */
+typedef struct {
+	int64_t v;
+	ora_oid o;
+} vpair;
+
+static int
+vpair_cmp(const void *a, const void *b)
+{
+	const vpair *x = a, *y = b;
+	if (x->v != y->v)
+		return x->v < y->v ? -1 : 1;
+	return x->o < y->o ? -1 : x->o > y->o;
+}
+
+/* the right candidates' (value, oid), sorted; *rnil: some value is nil */
+static vpair *
+rpairs(const ora_bat *r, const ora_ci *rci, bool *rnil)
+{
+	vpair *p = malloc((rci->n + 1) * sizeof(vpair));
+	if (p == NULL)
+		return NULL;
+	*rnil = false;
+	const int64_t nil = jnilv(r->type);
+	for (uint64_t i = 0; i < rci->n; i++) {
+		const ora_oid o = ci_get(rci, i);
+		p[i].v = jv(r, o - r->hseqbase);
+		p[i].o = o;
+		if (r->type != ORA_void && p[i].v == nil)
+			*rnil = true;
+		if (r->type == ORA_void && r->tseqbase == ORA_OID_NIL)
+			*rnil = true;
+	}
+	qsort(p, rci->n, sizeof(vpair), vpair_cmp);
+	return p;
+}
+
+static uint64_t
+vlower(const vpair *p, uint64_t n, int64_t v)
+{
+	uint64_t lo = 0, hi = n;
+	while (lo < hi) {
+		uint64_t m = (lo + hi) / 2;
+		if (p[m].v < v)
+			lo = m + 1;
+		else
+			hi = m;
+	}
+	return lo;
+}
+
+static bool
+lnil(const ora_bat *l, int64_t v)
+{
+	if (l->type == ORA_void)
+		return l->tseqbase == ORA_OID_NIL;
+	return v == jnilv(l->type);
+}
+
+/* semi (only_misses = false) or anti (true) join's left output */
+ora_bat *
+ora_semijoin_cands(ora_bat *l, ora_bat *r, const ora_bat *sl, const ora_bat *sr, bool nil_matches,
+		   bool max_one, bool only_misses, bool not_in)
+{
+	if (atomtype(l->type) != atomtype(r->type) || !join_type_ok(l->type) || l->type == ORA_flt ||
+	    l->type == ORA_dbl) {
+		ora_seterr("leftjoin: type not restated");
+		return NULL;
+	}
+	ora_ci lci, rci;
+	if (ora_ci_init(&lci, l, sl) < 0 || ora_ci_init(&rci, r, sr) < 0)
+		return NULL;
+	ora_oid *o = malloc((lci.n + 1) * sizeof(ora_oid));
+	if (o == NULL) {
+		ora_seterr("malloc");
+		return NULL;
+	}
+	uint64_t k = 0;
+	if (lci.n == 0 || rci.n == 0) {
+		if (only_misses)
+			for (uint64_t i = 0; i < lci.n; i++)
+				o[k++] = ci_get(&lci, i);
+	} else {
+		if (tdense(r) && rci.dense)
+			not_in = false;             /* mergejoin_void */
+		bool rnil;
+		vpair *p = rpairs(r, &rci, &rnil);
+		if (p == NULL) {
+			free(o);
+			ora_seterr("malloc");
+			return NULL;
+		}
+		if (!(not_in && rnil)) {
+			for (uint64_t i = 0; i < lci.n; i++) {
+				const ora_oid lo = ci_get(&lci, i);
+				const int64_t v = jv(l, lo - l->hseqbase);
+				uint64_t cnt = 0;
+				if (lnil(l, v) && (!nil_matches || not_in)) {
+					if (not_in)
+						continue;
+				} else {
+					const uint64_t a = vlower(p, rci.n, v);
+					uint64_t b = a;
+					while (b < rci.n && p[b].v == v)
+						b++;
+					cnt = b - a;
+				}
+				if (cnt > 1 && max_one && !only_misses) {
+					free(p);
+					free(o);
+					ora_seterr("more than one match");
+					return NULL;
+				}
+				if ((cnt > 0) != only_misses)
+					o[k++] = lo;
+			}
+		}
+		free(p);
+	}
+	ora_bat *bn = oidbat(o, k);
+	free(o);
+	if (bn == NULL)
+		return NULL;
+	bn->sorted = bn->key = 1;
+	bn->revsorted = k <= 1;
+	virtualize(bn);
+	return bn;
+}
+
+/* BATleftjoin (outer = false) / BATouterjoin (outer = true) for right
+ * candidates whose values match at most once per left candidate: returns
+ * -2 when a left candidate matches twice and match_one is not set */
+int
+ora_leftjoin(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r, const ora_bat *sl, const ora_bat *sr,
+	     bool nil_matches, bool outer, bool match_one)
+{
+	if (atomtype(l->type) != atomtype(r->type) || !join_type_ok(l->type) || l->type == ORA_flt ||
+	    l->type == ORA_dbl) {
+		ora_seterr("leftjoin: type not restated");
+		return -1;
+	}
+	ora_ci lci, rci;
+	if (ora_ci_init(&lci, l, sl) < 0 || ora_ci_init(&rci, r, sr) < 0)
+		return -1;
+	ora_oid *a = malloc((lci.n + 1) * sizeof(ora_oid)), *b = malloc((lci.n + 1) * sizeof(ora_oid));
+	bool rnil;
+	vpair *p = rci.n ? rpairs(r, &rci, &rnil) : NULL;
+	if (a == NULL || b == NULL || (rci.n && p == NULL)) {
+		free(a);
+		free(b);
+		free(p);
+		ora_seterr("malloc");
+		return -1;
+	}
+	uint64_t k = 0;
+	bool anynil = false;
+	for (uint64_t i = 0; i < lci.n; i++) {
+		const ora_oid lo = ci_get(&lci, i);
+		const int64_t v = jv(l, lo - l->hseqbase);
+		uint64_t cnt = 0, at = 0;
+		if (rci.n && !(lnil(l, v) && !nil_matches)) {
+			at = vlower(p, rci.n, v);
+			uint64_t e = at;
+			while (e < rci.n && p[e].v == v)
+				e++;
+			cnt = e - at;
+		}
+		if (cnt > 1) {
+			free(a);
+			free(b);
+			free(p);
+			if (match_one) {
+				ora_seterr("more than one match");
+				return -1;
+			}
+			return -2;
+		}
+		if (cnt == 1) {
+			a[k] = lo;
+			b[k++] = p[at].o;
+		} else if (outer) {
+			a[k] = lo;
+			b[k++] = ORA_OID_NIL;
+			anynil = true;
+		}
+	}
+	free(p);
+	ora_bat *x = oidbat(a, k), *y = oidbat(b, k);
+	free(a);
+	free(b);
+	if (x == NULL || y == NULL) {
+		ora_free(x);
+		ora_free(y);
+		return -1;
+	}
+	x->sorted = x->key = 1;
+	x->revsorted = k <= 1;
+	y->nil = anynil;
+	y->nonil = !anynil;
+	*r1p = x;
+	*r2p = y;
+	return 0;
+}

@@ -108,6 +108,15 @@ def lib():
         L.ora_groupavg3combine.argtypes = [P, P, P, P, P, C.c_bool]
         L.ora_groupavg3.argtypes = [C.POINTER(P), C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool]
         L.ora_join.argtypes = [C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool]
+        L.ora_groupmoments.restype = P
+        L.ora_groupmoments.argtypes = [C.c_int, P, P, P, P, P, C.c_bool, C.c_bool, C.c_bool]
+        L.ora_calcmoments.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int, P, P, C.c_bool,
+                                      C.c_bool]
+        L.ora_groupquantile.restype = P
+        L.ora_groupquantile.argtypes = [P, P, P, P, C.c_double, C.c_bool, C.c_bool]
+        L.ora_semijoin_cands.restype = P
+        L.ora_semijoin_cands.argtypes = [P, P, P, P, C.c_bool, C.c_bool, C.c_bool, C.c_bool]
+        L.ora_leftjoin.argtypes = [C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool, C.c_bool, C.c_bool]
         L.ora_join_algo.argtypes = [P, P, P, P]
         L.ora_BATsort.argtypes = [C.POINTER(P), C.POINTER(P), C.POINTER(P), P, P, P, C.c_bool, C.c_bool,
                                   C.c_bool]
@@ -119,6 +128,8 @@ def lib():
         L.ora_analyticalsum.argtypes = [P, P, P, P, P, P, C.c_int, C.c_int, C.c_int]
         L.ora_analyticalavg.argtypes = [P, P, P, P, P, P, C.c_int, C.c_int]
         L.ora_analyticalavginteger.argtypes = [P, P, P, P, P, P, C.c_int, C.c_int]
+        L.ora_analyticalstat.argtypes = [P, P, P, P, P, P, P, C.c_int, C.c_int, C.c_int]
+        L.ora_analyticalprod.argtypes = [P, P, P, P, P, P, C.c_int, C.c_int]
         L.ora_analyticalcount.argtypes = [P, P, P, P, P, P, C.c_bool, C.c_int]
         L.ora_analyticalntile.argtypes = [P, P, P, P, C.c_int, C.c_void_p]
         L.ora_analyticalfirst.argtypes = [P, P, P, P, C.c_int]
@@ -394,6 +405,33 @@ def BATgroupminmax(b, g, e, domax, skip_nils=True, s=None):
                                       s.ptr if s else None, skip_nils, domax))
 
 
+_ST = {"stdev": 0, "variance": 0, "covariance": 1, "correlation": 2}
+
+
+def BATgroupstat(name, b1, b2, g, e, skip_nils=True, s=None, sample=True):
+    """the grouped statistics of gdk_aggr.c:4612-5202: name one of stdev,
+    variance, covariance, correlation (b2 for the two-column ones)"""
+    return _ret(lib().ora_groupmoments(_ST[name], b1.ptr, b2.ptr if b2 else None, g.ptr if g else None,
+                                       e.ptr if e else None, s.ptr if s else None, skip_nils,
+                                       sample and name != "correlation", name == "variance"))
+
+
+def BATcalcstat(name, b1, b2=None, sample=True):
+    """calcvariance / calccovariance / BATcalccorrelation (gdk_aggr.c:4276-4559):
+    (value, average) -- NaN is nil"""
+    r, a = C.c_double(), C.c_double()
+    if lib().ora_calcmoments(C.byref(r), C.byref(a), _ST[name], b1.ptr, b2.ptr if b2 else None,
+                             sample and name != "correlation", name == "variance") < 0:
+        raise _err()
+    return r.value, a.value
+
+
+def BATgroupquantile(b, g, e, quantile, skip_nils=True, s=None, average=False):
+    """doBATgroupquantile (gdk_aggr.c:3881); g may be None"""
+    return _ret(lib().ora_groupquantile(b.ptr, g.ptr if g else None, e.ptr if e else None,
+                                        s.ptr if s else None, quantile, skip_nils, average))
+
+
 def BATgroupavg(b, g, e, skip_nils=True, s=None, scale=0, want_counts=True):
     a, c = P(), P()
     if lib().ora_groupavg(C.byref(a), C.byref(c) if want_counts else None, b.ptr, g.ptr,
@@ -419,6 +457,31 @@ def BATjoin(l, r, sl=None, sr=None, nil_matches=False):
     a, b = P(), P()
     if lib().ora_join(C.byref(a), C.byref(b), l.ptr, r.ptr, sl.ptr if sl else None,
                       sr.ptr if sr else None, nil_matches) < 0:
+        raise _err()
+    return Bat(a), Bat(b)
+
+
+def BATintersect(l, r, sl=None, sr=None, nil_matches=False, max_one=False):
+    """gdk_join.c:4366: the left candidates whose value occurs on the right"""
+    return _ret(lib().ora_semijoin_cands(l.ptr, r.ptr, sl.ptr if sl else None, sr.ptr if sr else None,
+                                         nil_matches, max_one, False, False))
+
+
+def BATdiff(l, r, sl=None, sr=None, nil_matches=False, not_in=False):
+    """gdk_join.c:4388: the left candidates whose value does not occur on the right"""
+    return _ret(lib().ora_semijoin_cands(l.ptr, r.ptr, sl.ptr if sl else None, sr.ptr if sr else None,
+                                         nil_matches, False, True, not_in))
+
+
+def BATleftjoin(l, r, sl=None, sr=None, nil_matches=False, outer=False, match_one=False):
+    """BATleftjoin / BATouterjoin (gdk_join.c:4320, :4334) with at most one
+    match per left candidate; None when a candidate matches twice"""
+    a, b = P(), P()
+    rc = lib().ora_leftjoin(C.byref(a), C.byref(b), l.ptr, r.ptr, sl.ptr if sl else None,
+                            sr.ptr if sr else None, nil_matches, outer, match_one)
+    if rc == -2:
+        return None
+    if rc < 0:
         raise _err()
     return Bat(a), Bat(b)
 
@@ -515,6 +578,30 @@ def analyticalavg(b, p, o, s, e, frame_type):
     if lib().ora_analyticalavg(r, p.ptr if p else None, o.ptr if o else None, b.ptr,
                                s.ptr if s else None, e.ptr if e else None, b.s.type,
                                frame_type) < 0:
+        lib().ora_free(r)
+        raise _err()
+    return Bat(r)
+
+
+# GDKanalytical_<name> (gdk_analytic_statistics.c:962-1443): (kind, op)
+WIN_STATS = {"stddev_samp": (0, 0), "stddev_pop": (0, 1), "variance_samp": (0, 2), "variance_pop": (0, 3),
+             "covariance_samp": (1, 0), "covariance_pop": (1, 1), "correlation": (2, 0)}
+
+
+def analyticalstat(name, b1, b2, p, o, s, e, frame_type):
+    kind, op = WIN_STATS[name]
+    r = lib().ora_new(TYPE_dbl, b1.count(), 0)
+    if lib().ora_analyticalstat(r, p.ptr if p else None, o.ptr if o else None, b1.ptr, b2.ptr if b2 else None,
+                                s.ptr if s else None, e.ptr if e else None, kind, op, frame_type) < 0:
+        lib().ora_free(r)
+        raise _err()
+    return Bat(r)
+
+
+def analyticalprod(b, p, o, s, e, tp2, frame_type):
+    r = lib().ora_new(tp2, b.count(), 0)
+    if lib().ora_analyticalprod(r, p.ptr if p else None, o.ptr if o else None, b.ptr,
+                                s.ptr if s else None, e.ptr if e else None, tp2, frame_type) < 0:
         lib().ora_free(r)
         raise _err()
     return Bat(r)

@@ -34,6 +34,10 @@ Sources (reference paths, relative to /root/reference):
       algebra.select results (every li/hi/anti combination, nil bounds, a
       slice view): the printed (head, value) / (head, oid, value) rows; and
       orderidx02's bat.orderidx order (a stable sort's order oids)
+  sql/test/quantiles/Tests/quantiles.test, sql/test/Tests/median_stdev.test,
+  sql/test/BugTracker-2013/Tests/stddev-group.Bug-3257.test,
+  median-null.Bug-3280.test -- quantile / median / stddev_pop / var_pop
+      data and expected printed results (stats_fixtures.json)
 """
 import json
 import os
@@ -440,7 +444,7 @@ def analytics07_fixture():
 
 # ---- window functions of analytics00 / 01 / 02.test ------------------------
 WIN_FUNCS = ("ntile", "first_value", "last_value", "nth_value", "lag", "lead", "min", "max", "sum", "count",
-             "avg")
+             "avg", "prod", "stddev_samp", "stddev_pop", "var_samp", "var_pop", "covar_samp", "covar_pop", "corr")
 SQL_TYPES = {"int": "int", "bigint": "lng", "real": "flt", "double": "dbl"}
 
 
@@ -544,14 +548,17 @@ def _window_item(item, cols):
 
 
 def analytics_window_fixture():
-    """sql/test/analytics/Tests/analytics00 / 01 / 02.test: window functions
-    (ntile, first_value, last_value, nth_value, lag, lead, min, max, sum,
-    count, avg) over PARTITION BY / ORDER BY / ROWS frames of small tables
-    with NULLs.  Each case keeps the tables as inserted (the SQL front end's
+    """sql/test/analytics/Tests/analytics00 / 01 / 02 / 14 / 15 / 16.test:
+    window functions (ntile, first_value, last_value, nth_value, lag, lead,
+    min, max, sum, count, avg, prod, stddev_samp / _pop, var_samp / _pop,
+    covar_samp / _pop, corr) over PARTITION BY / ORDER BY / ROWS frames of
+    small tables with NULLs; a query may mix OVER clauses (spec None: each
+    item is evaluated in its own order and the rows compare as a multiset,
+    whatever the sort mode).  Each case keeps the tables as inserted (the SQL front end's
     window sort is stable, so rows keep their insertion order among peers)
     and the expected rows as printed (rowsort: compared as multisets)."""
     out = []
-    for name in ("analytics00", "analytics01", "analytics02"):
+    for name in ("analytics00", "analytics01", "analytics02", "analytics14", "analytics15", "analytics16"):
         rel = "sql/test/analytics/Tests/%s.test" % name
         text = open(os.path.join(REF, rel)).read()
         tables, cases = {}, []
@@ -580,9 +587,10 @@ def analytics_window_fixture():
             tb = tables[m.group(2)]
             items = [_window_item(it, tb["cols"]) for it in _split_top(m.group(1))]
             wins = [it for it in items if it and it["kind"] == "win"]
-            if not wins or any(it is None for it in items) or any(w["spec"] != wins[0]["spec"] for w in wins):
+            if not wins or any(it is None for it in items):
                 continue
             types, sortmode = kind.split()[1], kind.split()[2]
+            mixed = any(w["spec"] != wins[0]["spec"] for w in wins)
             if "T" in types:
                 continue
             width = len(types)
@@ -590,7 +598,7 @@ def analytics_window_fixture():
                 continue
             rows = [[None if x == "NULL" else (float(x) if t == "R" else int(x))
                      for x, t in zip(exp[i:i + width], types)] for i in range(0, len(exp), width)]
-            cases.append(dict(table=m.group(2), items=items, spec=wins[0]["spec"], types=types,
+            cases.append(dict(table=m.group(2), items=items, spec=None if mixed else wins[0]["spec"], types=types,
                               sortmode=sortmode, expected=rows))
         out.append(dict(source=rel, tables={k: dict(cols=v["cols"], names=v["names"], rows=v["rows"])
                                             for k, v in tables.items()}, cases=cases))
@@ -620,6 +628,87 @@ def batcalc_fixture():
     return out
 
 
+# ---- statistics (median / quantile / stddev / var SQL tests) ----------------
+def _copy_rows(text):
+    """the data rows of the first COPY ... FROM stdin block"""
+    i = text.index("<COPY_INTO_DATA>")
+    rows = []
+    for ln in text[i:].split("\n")[1:]:
+        if not ln.strip():
+            break
+        rows.append(ln)
+    return rows
+
+
+def _inserts(text):
+    return [tuple(int(x) for x in m.group(1).split(","))
+            for m in re.finditer(r"INSERT INTO \w+ VALUES \(([-\d, ]+)\)", text)] + \
+        [tuple(int(x) for x in t.split(","))
+         for m in re.finditer(r"insert into \w+ values ((?:\([-\d, ]+\),? ?)+)", text)
+         for t in re.findall(r"\(([-\d, ]+)\)", m.group(1))]
+
+
+def stats_fixture():
+    """sql/test/quantiles/Tests/quantiles.test (quantile / median of a
+    DECIMAL(15,2) column over 10000 rows, whole and per l_returnflag, p out of
+    [0,1] an error), sql/test/Tests/median_stdev.test (median of int columns,
+    whole and grouped), sql/test/BugTracker-2013/Tests/stddev-group.Bug-3257.test
+    (stddev_pop / var_pop, whole and grouped), median-null.Bug-3280.test
+    (median of a DOUBLE column with NULLs).  Kept: the data and the queries'
+    (function, p, grouped) with their expected printed results."""
+    out = {}
+    rel = "sql/test/quantiles/Tests/quantiles.test"
+    text = open(os.path.join(REF, rel)).read()
+    price, flag = [], []
+    for ln in _copy_rows(text):
+        a, b = ln.split("\t")
+        whole, frac = a.split(".")
+        price.append(int(whole) * 100 + int(frac.ljust(2, "0")))
+        flag.append(b.strip('"'))
+    queries = []
+    for kind, body, exp in parse_blocks(text):
+        sql = " ".join(body)
+        if "l_extendedprice" not in sql or not sql.lower().startswith("select"):
+            continue
+        items = []
+        for m in re.finditer(r"(quantile|median)\(l_extendedprice(?:,\s*([-\d.]+))?\)", sql):
+            items.append([m.group(1), float(m.group(2)) if m.group(2) else 0.5])
+        queries.append({"items": items, "grouped": "group by" in sql.lower(),
+                        "error": kind.startswith("statement error"), "rowsort": "rowsort" in kind,
+                        "expected": exp})
+    out["quantiles"] = {"source": rel, "price_cents": price, "flag": flag, "queries": queries}
+    rel = "sql/test/Tests/median_stdev.test"
+    text = open(os.path.join(REF, rel)).read()
+    rows = _inserts(text)
+    qs = []
+    for kind, body, exp in parse_blocks(text):
+        sql = " ".join(body)
+        m = re.match(r"SELECT (groupID, )?median\((\w+)\) FROM sampleData( GROUP BY groupID)?", sql)
+        if m:
+            qs.append({"column": m.group(2), "grouped": bool(m.group(3)), "expected": exp})
+    out["median_stdev"] = {"source": rel, "groupID": [r[0] for r in rows], "numValue": [r[1] for r in rows],
+                           "queries": qs}
+    rel = "sql/test/BugTracker-2013/Tests/stddev-group.Bug-3257.test"
+    text = open(os.path.join(REF, rel)).read()
+    rows = _inserts(text)
+    qs = []
+    for kind, body, exp in parse_blocks(text):
+        sql = " ".join(body)
+        m = re.match(r"select (stddev_pop|var_pop)\(i\) from t3257( group by j)?", sql)
+        if m:
+            qs.append({"func": m.group(1), "grouped": bool(m.group(2)), "expected": exp})
+    out["stddev_group"] = {"source": rel, "i": [r[0] for r in rows], "j": [r[1] for r in rows], "queries": qs}
+    rel = "sql/test/BugTracker-2013/Tests/median-null.Bug-3280.test"
+    text = open(os.path.join(REF, rel)).read()
+    rows = [ln.split(",") for ln in _copy_rows(text)[1:]]
+    # UPDATE mtcars SET mpg = NULL WHERE cyl = 6
+    assert "UPDATE mtcars SET mpg = NULL WHERE cyl = 6" in text
+    mpg = [None if float(r[2]) == 6 else float(r[1]) for r in rows]
+    exp = [e for k, b, e in parse_blocks(text) if k.startswith("query") and "median" in " ".join(b)][0]
+    out["median_null"] = {"source": rel, "mpg": mpg, "expected": exp}
+    return out
+
+
 def main():
     if not os.path.isdir(REF):
         sys.exit("reference not present; fixtures are already committed")
@@ -646,6 +735,8 @@ def main():
             fx["sort"].append({"source": rel, "cases": sorts})
     with open(os.path.join(OUT, "maltest_fixtures.json"), "w") as f:
         json.dump(fx, f, indent=1)
+    with open(os.path.join(OUT, "stats_fixtures.json"), "w") as f:
+        json.dump(stats_fixture(), f, indent=0)
     print("select cases:", len(fx["select"]["cases"]))
     print("firstn cases:", [len(f["cases"]) for f in fx["firstn"]])
     print("window sqltest cases:", [(f["source"], len(f["cases"])) for f in fx["window_sqltests"]])

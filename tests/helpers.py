@@ -412,7 +412,8 @@ def sqlwin_api_gdk(gdk):
         nth_value=lambda b, s, e, t, nth: gdk.GDKanalyticalnthvalue(b, s, e, t=t, nth=nth),
         lag=gdk.GDKanalyticallag, lead=gdk.GDKanalyticallead,
         min=gdk.GDKanalyticalmin, max=gdk.GDKanalyticalmax, sum=gdk.GDKanalyticalsum,
-        count=gdk.GDKanalyticalcount, avg=gdk.GDKanalyticalavg, BUN_NONE=gdk.BUN_NONE)
+        count=gdk.GDKanalyticalcount, avg=gdk.GDKanalyticalavg, prod=gdk.GDKanalyticalprod,
+        stat=gdk.GDKanalytical_stat, BUN_NONE=gdk.BUN_NONE)
 
 
 def sqlwin_api_ora(ora):
@@ -426,7 +427,8 @@ def sqlwin_api_ora(ora):
         nth_value=lambda b, s, e, t, nth: ora.analyticalnthvalue(b, s, e, t=t, nth=nth),
         lag=ora.analyticallag, lead=ora.analyticallead,
         min=ora.analyticalmin, max=ora.analyticalmax, sum=ora.analyticalsum,
-        count=ora.analyticalcount, avg=ora.analyticalavg, BUN_NONE=ora.BUN_NONE)
+        count=ora.analyticalcount, avg=ora.analyticalavg, prod=ora.analyticalprod,
+        stat=ora.analyticalstat, BUN_NONE=ora.BUN_NONE)
 
 
 def _sqlwin_perm(tb, spec):
@@ -464,9 +466,38 @@ def _sqlwin_out(bat, tp):
     return out
 
 
+SQL_STATS = {"stddev_samp": "stddev_samp", "stddev_pop": "stddev_pop", "var_samp": "variance_samp",
+             "var_pop": "variance_pop", "covar_samp": "covariance_samp", "covar_pop": "covariance_pop",
+             "corr": "correlation"}
+
+
 def sqlwin_eval(api, tb, c):
-    """the window query's result rows in evaluation (sorted) order"""
+    """the window query's result rows in evaluation (sorted) order; a query
+    mixing OVER clauses (spec None): each item in its own order, the rows in
+    table order"""
     spec = c["spec"]
+    if spec is None:
+        # the plan sorts the relation by the first OVER clause that orders
+        # anything; a window without PARTITION / ORDER sees that order
+        n = len(tb["rows"])
+        first = next((it["spec"] for it in c["items"] if it["kind"] == "win" and
+                      (it["spec"]["part"] or it["spec"]["order"])), None)
+        base = _sqlwin_perm(tb, first)[1] if first else list(range(n))
+        tbb = dict(tb, rows=[tb["rows"][i] for i in base])
+        cols = []
+        for it in c["items"]:
+            if it["kind"] == "col":
+                cols.append([r[tb["names"].index(it["col"])] for r in tb["rows"]])
+                continue
+            plain = not (it["spec"]["part"] or it["spec"]["order"])
+            tbx, bx = (tbb, base) if plain else (tb, list(range(n)))
+            vals = [r[0] for r in sqlwin_eval(api, tbx, dict(items=[it], spec=it["spec"]))]
+            _, perm = _sqlwin_perm(tbx, it["spec"])
+            back = [None] * n
+            for k, i in enumerate(perm):
+                back[bx[i]] = vals[k]
+            cols.append(back)
+        return [list(r) for r in zip(*cols)]
     cols, perm = _sqlwin_perm(tb, spec)
     n = len(perm)
     types = tb["cols"]
@@ -557,6 +588,16 @@ def sqlwin_eval(api, tb, c):
             elif f == "sum":
                 rtp = btp if btp in (8, 9) else TYPE_LNG
                 r = api["sum"](b, P, O, s, e, rtp, ft)
+            elif f in SQL_STATS:
+                b2 = None
+                if f in ("covar_samp", "covar_pop", "corr"):
+                    if "col" not in it["args"][0]:
+                        raise NotImplementedError("a literal second argument")
+                    b2, _ = _sqlwin_col(api, types[it["args"][0]["col"]], sc[it["args"][0]["col"]])
+                r, rtp = api["stat"](SQL_STATS[f], b, b2, P, O, s, e, ft), 9
+            elif f == "prod":
+                rtp = btp if btp in (8, 9) else TYPE_LNG
+                r = api["prod"](b, P, O, s, e, rtp, ft)
             elif f == "count":
                 if b is None:
                     b = api["mk"](TYPE_INT, np.zeros(n, np.int32))
@@ -588,7 +629,7 @@ def replay_window_sqltests(api):
             ran += 1
             g = [_sqlwin_fmt(r, c["types"]) for r in got]
             w = [_sqlwin_fmt(r, c["types"]) for r in c["expected"]]
-            if c["sortmode"] == "rowsort":
+            if c["sortmode"] == "rowsort" or c["spec"] is None:
                 g, w = sorted(g), sorted(w)
             if g != w:
                 bad.append((fx["source"], c["table"], c["items"], c["spec"], w, g))

@@ -266,10 +266,10 @@ def test_diff(gdk, ora, tname, dt, mode):
 
 @pytest.mark.gpu
 def test_window_sqltests(gdk):
-    """analytics00 / 01 / 02.test (the reference's own answers) on the
-    device: the same 295 window queries the oracle replays
+    """analytics00 / 01 / 02 / 14 / 15.test (the reference's own answers) on
+    the device: the same 346 window queries the oracle replays
     (tests/test_oracle.py::test_window_sqltests_oracle)."""
     from helpers import replay_window_sqltests, sqlwin_api_gdk
     ran, bad = replay_window_sqltests(sqlwin_api_gdk(gdk))
-    assert ran >= 290
+    assert ran >= 346
     assert not bad, bad[:3]

@@ -541,11 +541,13 @@ def test_project_maltest(ora):
 
 
 def test_window_sqltests_oracle(ora):
-    """analytics00 / 01 / 02.test (the reference's own answers): ntile,
-    first_value, last_value, nth_value, lag, lead, min, max, sum, count and
-    avg over PARTITION BY / ORDER BY / ROWS frames, replayed through the
-    oracle's restatement of gdk_analytic_func.c / gdk_analytic_bounds.c."""
+    """analytics00 / 01 / 02 / 14 / 15.test (the reference's own answers):
+    ntile, first_value, last_value, nth_value, lag, lead, min, max, sum,
+    count, avg, prod, stddev / variance / covariance (samp, pop) and corr over
+    PARTITION BY / ORDER BY / ROWS frames, replayed through the oracle's
+    restatement of gdk_analytic_func.c / gdk_analytic_statistics.c /
+    gdk_analytic_bounds.c."""
     from helpers import replay_window_sqltests, sqlwin_api_ora
     ran, bad = replay_window_sqltests(sqlwin_api_ora(ora))
-    assert ran >= 290
+    assert ran >= 346
     assert not bad, bad[:3]

@@ -20,15 +20,21 @@ join)
 		MGDK_JOIN_PROBE4=$v timeout -k 10 200 python tools/opbench.py --only config3 > $O/opbench_v$v.json 2> $O/opbench_v$v.err
 	done
 	cd /tmp && cd $GRAFT_REPO_ROOT
-	timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 tools/opbench.py --only config3 > $O/prof.log 2>&1
+	timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 tools/opbench.py --only config3 > $O/prof.log 2>&1
 	;;
 gsums)
 	timeout -k 10 600 $T tests/test_gpu_group_sums.py > $O/tests.log 2>&1
 	timeout -k 10 200 python tools/opbench.py --only config4_group_sums > $O/opbench.json 2> $O/opbench.err
 	cd /tmp && cd $GRAFT_REPO_ROOT
-	timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 tools/opbench.py --only config4_group_sums > $O/prof.log 2>&1
+	timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 tools/opbench.py --only config4_group_sums > $O/prof.log 2>&1
 	timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f -o run -- python3 tools/opbench.py --only config4_group_sums > $O/pmc_f.log 2>&1
 	timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_w -o run -- python3 tools/opbench.py --only config4_group_sums > $O/pmc_w.log 2>&1
+	;;
+jk)
+	timeout -k 10 600 $T tests/test_join_kinds.py tests/test_cand_algebra.py > $O/tests.log 2>&1
+	;;
+stats)
+	timeout -k 10 600 $T tests/test_group_stats.py tests/test_window_stats.py tests/test_gpu_window_funcs.py > $O/tests.log 2>&1
 	;;
 cand)
 	timeout -k 10 600 $T tests/test_cand_algebra.py tests/test_gpu_window_funcs.py > $O/tests.log 2>&1
