@@ -285,6 +285,22 @@ int mgdk_BATleftjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, m
 		     bool nil_matches, mgdk_BUN estimate);
 int mgdk_BATouterjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr,
 		      bool nil_matches, bool match_one, mgdk_BUN estimate);
+/* BATthetajoin (gdk/gdk.h; gdk_join.c:4409, nested loop thetajoin :3699):
+ * op JOIN_EQ 0 (= BATjoin), JOIN_LT -1, JOIN_LE -2, JOIN_GT 1, JOIN_GE 2,
+ * JOIN_NE -3 (gdk.h:2237-2243); the pairs in left-candidate order, each left
+ * candidate's matches in right-candidate order.  BATbandjoin (gdk_join.c:
+ * 4626): r - c1 <= l <= r + c2 (linc / hinc: the ends included), c1 / c2
+ * point at values of the columns' type */
+int mgdk_BATthetajoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, int op,
+		      bool nil_matches, mgdk_BUN estimate);
+int mgdk_BATbandjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr,
+		     const void *c1, const void *c2, bool linc, bool hinc, mgdk_BUN estimate);
+/* BATrangejoin (gdk_join.c:5422, rangejoin :5067): l within [rl, rh] of each
+ * right candidate (rl, rh aligned); not anti / symmetric and l ordered:
+ * right-major pairs by binary search, otherwise the nested loop's
+ * left-major pairs with BETWEEN's three-valued logic */
+int mgdk_BATrangejoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *rl, mgdk_bat *rh, mgdk_bat *sl,
+		      mgdk_bat *sr, bool linc, bool hinc, bool anti, bool symmetric, mgdk_BUN estimate);
 /* gdk/gdk.h:1524-1525 (gdk_batop.c:2002, :2181): whether b is sorted /
  * reverse sorted; what is found is recorded in b (tsorted, trevsorted,
  * tkey, tnosorted, tnorevsorted) as the reference does */

@@ -22,6 +22,7 @@
 //          the tile's first and last groups leave (group, partial) records
 //          that k_gs_edges combines in order (no atomics).
 #include "mgdk_internal.h"
+#include "lookback.h"
 
 using namespace mgdk;
 
@@ -206,24 +207,124 @@ k_gs_count(const typename KT<KW>::T *k, BUN n, uint32_t *tcnt)
 		tcnt[blockIdx.x] = c;
 }
 
-template <int KW, int VW, int NV>
+// the fused variant's tile claims and look-back state (LB)
+struct GsLb {
+	uint32_t *xtk;         // 8 per-XCD tickets
+	uint64_t *status;      // per tile: {flag:2, starts:62}, zero before the launch
+	uint32_t *err;
+	uint32_t xg;
+	BUN nt;
+};
+
+// group starts in tile tp (one wave): the look-back's count of a
+// predecessor that no XCD has claimed yet
+template <typename T>
+__device__ uint64_t
+gs_wave_starts(const T *k, BUN n, BUN tp)
+{
+	const unsigned lane = __lane_id();
+	const BUN a = tp * GST, e = a + GST < n ? a + GST : n;
+	uint64_t c = 0;
+	for (BUN i = a + lane; i < e; i += 64)
+		c += i == 0 || k[i] != k[i - 1];
+	for (int d = 32; d > 0; d >>= 1)
+		c += __shfl_xor(c, d);
+	return c;
+}
+
+// decoupled look-back over the tiles' group-start counts (mgdk_lb::lookback,
+// 64 predecessors per step), run by one wave; a predecessor no XCD has
+// claimed is counted from its keys instead of waited for
+template <typename T>
+__device__ uint64_t
+gs_lookback(const GsLb &lb, BUN t, uint64_t agg, const T *k, BUN n)
+{
+	using namespace mgdk_lb;
+	const unsigned lane = __lane_id();
+	if (t == 0) {
+		if (lane == 0)
+			lb_store(&lb.status[0], ST_PRE | agg);
+		return 0;
+	}
+	if (lane == 0)
+		lb_store(&lb.status[t], ST_AGG | agg);
+	uint64_t excl = 0;
+	int64_t base = (int64_t) t - 1;
+	for (;;) {
+		const int64_t idx = base - (int64_t) lane;
+		uint64_t val = 0;
+		bool pre = true, miss = false;
+		if (idx >= 0) {
+			pre = false;
+			for (uint32_t spins = 0;; spins++) {
+				const uint64_t sv = lb_load(&lb.status[idx]);
+				if ((sv >> 62) != 0) {
+					val = sv & ST_VAL;
+					pre = (sv >> 62) == 2;
+					break;
+				}
+				if ((spins & 15) == 0 && !xcd_claimed(lb.xtk, (uint64_t) idx, lb.xg)) {
+					miss = true;
+					break;
+				}
+				if (spins > (1u << 26)) {
+					atomicOr(lb.err, 1u);      // cannot happen: claimed tiles publish
+					pre = true;
+					break;
+				}
+				__builtin_amdgcn_s_sleep(1);
+			}
+		}
+		const uint64_t pmask = __ballot(pre);
+		const int first = pmask ? __ffsll((long long) pmask) - 1 : 64;
+		uint64_t mm = __ballot(miss && (int) lane <= first);
+		while (mm) {
+			const int q = __ffsll((long long) mm) - 1;
+			const uint64_t c = gs_wave_starts<T>(k, n, (BUN) (base - q));
+			if ((int) lane == q)
+				val = c;
+			mm &= mm - 1;
+		}
+		uint64_t v = (int) lane <= first ? val : 0;
+		for (int d = 32; d > 0; d >>= 1)
+			v += __shfl_xor(v, d);
+		excl += v;
+		if (pmask)
+			break;
+		base -= 64;
+	}
+	if (lane == 0)
+		lb_store(&lb.status[t], ST_PRE | (excl + agg));
+	return excl;
+}
+
+template <int KW, int VW, int NV, bool LB>
 __global__ __launch_bounds__(256) void
 k_gs_sums(const typename KT<KW>::T *k, const void *const *vals, BUN n, oid hseq, const uint64_t *tpre, GsOut o,
-	  GsEdge<NV> *edges)
+	  GsEdge<NV> *edges, GsLb lb)
 {
 	typedef typename KT<KW>::T T;
 	typedef typename KT<VW>::T V;
 	__shared__ GsPart<NV> s_wtot[4];
 	__shared__ int s_wflag[4];
 	__shared__ uint32_t s_wst[4];
-	// one 512-row staging region per wave, reused column after column (every
-	// column's loads are in flight in registers before the first is staged):
-	// 16 KiB of LDS per workgroup instead of (1 + NV) x 16 KiB, so four
-	// workgroups fit a CU instead of three
-	constexpr int SW = KW > VW ? KW : VW;
-	__shared__ __attribute__((aligned(16))) char s_st[4][512 * SW];
+	__shared__ T s_k[4][512];
+	__shared__ V s_v[NV][4][512];
+	__shared__ uint32_t s_tile;
+	__shared__ uint64_t s_tbase;
 	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
-	const BUN t = blockIdx.x, t0 = t * GST, l0 = t0 + (BUN) tid * GSU, r0 = t0 + (BUN) w * 512;
+	BUN t = blockIdx.x;
+	if (LB) {
+		// tiles in per-XCD claim order (claim_xcd_tile), so the look-back
+		// below only ever waits on running tiles
+		if (tid == 0)
+			s_tile = mgdk_lb::claim_xcd_tile(lb.xtk, (uint32_t) lb.nt, lb.xg);
+		__syncthreads();
+		if (s_tile == ~0u)
+			return;     // cannot happen: one tile per workgroup
+		t = s_tile;
+	}
+	const BUN t0 = t * GST, l0 = t0 + (BUN) tid * GSU, r0 = t0 + (BUN) w * 512;
 	const bool live = l0 < n;
 	T x[GSU];
 	V y[NV][GSU];
@@ -240,15 +341,14 @@ k_gs_sums(const typename KT<KW>::T *k, const void *const *vals, BUN n, oid hseq,
 		stage_ld<KW>(k, r0, n, sk);
 		const T before = r0 > 0 ? k[r0 - 1] : 0;
 #pragma unroll
-		for (int v = 0; v < NV; v++) {
-			stage_st<VW>((const V *) vals[v], r0, n, sv[v], (V *) s_st[w]);
-			stage_sync();
-			stage_rd<VW>((const V *) s_st[w], y[v]);
-			stage_sync();
-		}
-		stage_st<KW>(k, r0, n, sk, (T *) s_st[w]);
+		for (int v = 0; v < NV; v++)
+			stage_st<VW>((const V *) vals[v], r0, n, sv[v], s_v[v][w]);
+		stage_st<KW>(k, r0, n, sk, s_k[w]);
 		stage_sync();
-		stage_rd<KW>((const T *) s_st[w], x);
+#pragma unroll
+		for (int v = 0; v < NV; v++)
+			stage_rd<VW>(s_v[v][w], y[v]);
+		stage_rd<KW>(s_k[w], x);
 		T prev = stage_pred<T>(x, before, r0);
 #pragma unroll
 		for (int u = 0; u < GSU; u++) {
@@ -273,13 +373,26 @@ k_gs_sums(const typename KT<KW>::T *k, const void *const *vals, BUN n, oid hseq,
 		s_wst[w] = xs;
 	// the lane's runs: pre = rows before its first start, post = from its
 	// last start to its end; runs between two of its starts are complete
-	const uint64_t tbase = tpre[t];
 	GsPart<NV> pre, cur;
 	pre.clear();
 	cur.clear();
 	bool seen = false;
 	uint32_t of = 0;
 	__syncthreads();
+	uint64_t tbase;
+	if (LB) {
+		// the tile's first group id: the starts of every tile before it
+		if (w == 0) {
+			const uint64_t agg = s_wst[0] + s_wst[1] + s_wst[2] + s_wst[3];
+			const uint64_t ex = gs_lookback<T>(lb, t, agg, k, n);
+			if (lane == 0)
+				s_tbase = ex;
+		}
+		__syncthreads();
+		tbase = s_tbase;
+	} else {
+		tbase = tpre[t];
+	}
 	uint32_t lpre = xs - ns;
 	for (unsigned q = 0; q < w; q++)
 		lpre += s_wst[q];
@@ -387,10 +500,15 @@ k_gs_sums(const typename KT<KW>::T *k, const void *const *vals, BUN n, oid hseq,
 }
 
 // the tile edge records in order: a group's records are consecutive; the
-// first record of each group sums them and stores the group
+// first record of each group sums them and stores the group.  A group over
+// more than GS_ECAP records (a key spanning that many tiles) is left to
+// k_gs_edges_long: its first record goes to a list instead of one thread
+// walking it
+constexpr BUN GS_ECAP = 256;
+
 template <int NV>
 __global__ __launch_bounds__(256) void
-k_gs_edges(const GsEdge<NV> *e, BUN ne, BUN ngrp, GsOut o)
+k_gs_edges(const GsEdge<NV> *e, BUN ne, BUN ngrp, GsOut o, uint32_t *longs)
 {
 	uint32_t f = 0;
 	for (BUN j = (BUN) blockIdx.x * blockDim.x + threadIdx.x; j < ne; j += (BUN) gridDim.x * blockDim.x) {
@@ -398,8 +516,13 @@ k_gs_edges(const GsEdge<NV> *e, BUN ne, BUN ngrp, GsOut o)
 		if (g >= ngrp || (j > 0 && e[j - 1].g == g))
 			continue;
 		GsPart<NV> p = e[j].p;
-		for (BUN q = j + 1; q < ne && e[q].g == g; q++)
+		BUN q = j + 1;
+		for (; q < ne && q < j + GS_ECAP && e[q].g == g; q++)
 			p.add(e[q].p);
+		if (q < ne && q == j + GS_ECAP && e[q].g == g) {
+			longs[1 + atomicAdd(&longs[0], 1u)] = (uint32_t) j;
+			continue;
+		}
 		f |= gs_put<NV>(o, g, p);
 	}
 	for (int q = 32; q > 0; q >>= 1)
@@ -408,29 +531,88 @@ k_gs_edges(const GsEdge<NV> *e, BUN ne, BUN ngrp, GsOut o)
 		publish_or(o.flags, f);
 }
 
+// the long groups: one workgroup sums a group's records 256 at a time (a
+// group's records are consecutive and its key never comes back, so the
+// first chunk that holds another key ends it)
+template <int NV>
+__global__ __launch_bounds__(256) void
+k_gs_edges_long(const GsEdge<NV> *e, BUN ne, BUN ngrp, GsOut o, const uint32_t *longs)
+{
+	__shared__ GsPart<NV> s_p[4];
+	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+	const uint32_t nl = longs[0];
+	for (uint32_t k = blockIdx.x; k < nl; k += gridDim.x) {
+		const BUN j = longs[1 + k];
+		const unsigned long long g = e[j].g;
+		GsPart<NV> p;
+		p.clear();
+		for (BUN c = j;; c += 256) {
+			const BUN q = c + tid;
+			const bool in = q < ne && e[q].g == g;
+			if (in)
+				p.add(e[q].p);
+			if (__syncthreads_or(!in))
+				break;
+		}
+		for (int d = 32; d > 0; d >>= 1) {
+			GsPart<NV> t;
+			t.cnt = __shfl_xor(p.cnt, d);
+#pragma unroll
+			for (int v = 0; v < NV; v++) {
+				t.nn[v] = __shfl_xor(p.nn[v], d);
+				const unsigned long long lo = __shfl_xor((unsigned long long) p.s[v], d);
+				const unsigned long long hi = __shfl_xor((unsigned long long) ((uhge) p.s[v] >> 64), d);
+				t.s[v] = (hge) (((uhge) hi << 64) | lo);
+			}
+			p.add(t);
+		}
+		if (lane == 0)
+			s_p[w] = p;
+		__syncthreads();
+		if (tid == 0) {
+			GsPart<NV> tot = s_p[0];
+			for (int q = 1; q < 4; q++)
+				tot.add(s_p[q]);
+			const uint32_t f = gs_put<NV>(o, g, tot);
+			if (f)
+				publish_or(o.flags, f);
+		}
+		__syncthreads();
+	}
+}
+
 template <int KW, int VW, int NV>
 int
 gs_run(const void *kb, const void *const *vals_dev, BUN n, oid hseq, const uint64_t *tpre, BUN nt, BUN ngrp,
-       GsOut o, void *edges)
+       GsOut o, void *edges, uint32_t *longs, const GsLb *lb)
 {
 	hipStream_t st = stream();
-	hipLaunchKernelGGL((k_gs_sums<KW, VW, NV>), dim3((unsigned) nt), dim3(256), 0, st, (const typename KT<KW>::T *) kb,
-			   vals_dev, n, hseq, tpre, o, (GsEdge<NV> *) edges);
-	hipLaunchKernelGGL(k_gs_edges<NV>, dim3(grid_for(2 * nt, 1024, 4096)), dim3(256), 0, st,
-			   (const GsEdge<NV> *) edges, 2 * nt, ngrp, o);
+	if (lb)
+		hipLaunchKernelGGL((k_gs_sums<KW, VW, NV, true>), dim3((unsigned) nt), dim3(256), 0, st,
+				   (const typename KT<KW>::T *) kb, vals_dev, n, hseq, tpre, o, (GsEdge<NV> *) edges, *lb);
+	else
+		hipLaunchKernelGGL((k_gs_sums<KW, VW, NV, false>), dim3((unsigned) nt), dim3(256), 0, st,
+				   (const typename KT<KW>::T *) kb, vals_dev, n, hseq, tpre, o, (GsEdge<NV> *) edges, GsLb{});
+	const BUN ne = 2 * nt;
+	if (!hip_ok(hipMemsetAsync(longs, 0, 4, st), "memset"))
+		return -1;
+	hipLaunchKernelGGL(k_gs_edges<NV>, dim3(grid_for(ne, 1024, 4096)), dim3(256), 0, st, (const GsEdge<NV> *) edges,
+			   ne, ngrp, o, longs);
+	hipLaunchKernelGGL(k_gs_edges_long<NV>, dim3(256), dim3(256), 0, st, (const GsEdge<NV> *) edges, ne, ngrp, o,
+			   (const uint32_t *) longs);
 	return 0;
 }
 
 template <int KW, int VW>
 int
 gs_nv(int nv, const void *kb, const void *const *vals_dev, BUN n, oid hseq, const uint64_t *tpre, BUN nt, BUN ngrp,
-      GsOut o, void *edges)
+      GsOut o, void *edges, uint32_t *longs, const GsLb *lb)
 {
 	switch (nv) {
-	case 1: return gs_run<KW, VW, 1>(kb, vals_dev, n, hseq, tpre, nt, ngrp, o, edges);
-	case 2: return gs_run<KW, VW, 2>(kb, vals_dev, n, hseq, tpre, nt, ngrp, o, edges);
-	case 3: return gs_run<KW, VW, 3>(kb, vals_dev, n, hseq, tpre, nt, ngrp, o, edges);
-	default: return gs_run<KW, VW, 4>(kb, vals_dev, n, hseq, tpre, nt, ngrp, o, edges);
+	case 1: return gs_run<KW, VW, 1>(kb, vals_dev, n, hseq, tpre, nt, ngrp, o, edges, longs, lb);
+	case 2: return gs_run<KW, VW, 2>(kb, vals_dev, n, hseq, tpre, nt, ngrp, o, edges, longs, lb);
+	case 3: return gs_run<KW, VW, 3>(kb, vals_dev, n, hseq, tpre, nt, ngrp, o, edges, longs, lb);
+	default: return gs_run<KW, VW, 4>(kb, vals_dev, n, hseq, tpre, nt, ngrp, o, edges, longs, lb);
 	}
 }
 
@@ -484,25 +666,54 @@ mgdk_group_sums_ordered(mgdk_bat **extents, mgdk_bat **histo, mgdk_bat **keys, m
 	hipStream_t st = stream();
 	const int kw = b->twidth, vw = vals[0]->twidth;
 	const BUN nt = (n + GST - 1) / GST;
-	DevBuf tc(nt * 4 + 8), tp(nt * 8 + 8), vp(64);
-	if (!tc.p || !tp.p || !vp.p)
+	// fused (default): the group ids come from a look-back over the tiles'
+	// start counts inside the sums pass, so the keys are read once; the
+	// outputs are then sized for n groups (56 B x n at two sums) and the
+	// count is read back at the end.  Two-pass (MGDK_GS_FUSED=0, or when
+	// that bound is large): a count pass + scan first, outputs sized exactly
+	static const bool fused_on = !getenv("MGDK_GS_FUSED") || atoi(getenv("MGDK_GS_FUSED")) != 0;
+	const bool fused = fused_on && nt < 0xffffffffull &&
+			   n * (24 + 16 * (BUN) nvals) <= ((BUN) 48 << 30);
+	DevBuf tc(fused ? 8 : nt * 4 + 8), tp(fused ? 8 : nt * 8 + 8), vp(64), lbs(fused ? nt * 8 + 256 : 8);
+	if (!tc.p || !tp.p || !vp.p || !lbs.p)
 		return -1;
-	if (kw == 4)
-		hipLaunchKernelGGL(k_gs_count<4>, dim3((unsigned) nt), dim3(256), 0, st, (const int32_t *) b->theap, n,
-				   tc.as<uint32_t>());
-	else
-		hipLaunchKernelGGL(k_gs_count<8>, dim3((unsigned) nt), dim3(256), 0, st, (const int64_t *) b->theap, n,
-				   tc.as<uint32_t>());
-	uint64_t ngrp = 0;
-	if (exclusive_scan(tc.as<uint32_t>(), tp.as<uint64_t>(), nt, &ngrp) < 0)
-		return -1;
-	mgdk_bat *en = newbat(0, MGDK_oid, ngrp), *hn = newbat(0, MGDK_lng, ngrp), *kn = newbat(0, MGDK_lng, ngrp);
+	uint64_t ngrp = 0, cap;
+	GsLb lb{};
+	const GsLb *lbp = nullptr;
+	if (fused) {
+		lb.status = lbs.as<uint64_t>();
+		lb.xtk = (uint32_t *) (lb.status + nt);
+		lb.err = lb.xtk + 16;
+		lb.xg = getenv("MGDK_GS_XCDG") ? (uint32_t) atoi(getenv("MGDK_GS_XCDG")) : 16u;
+		if (lb.xg == 0)
+			lb.xg = 1;
+		lb.nt = nt;
+		lbp = &lb;
+		if (!hip_ok(hipMemsetAsync(lbs.p, 0, nt * 8 + 256, st), "memset"))
+			return -1;
+		cap = n;
+	} else {
+		if (kw == 4)
+			hipLaunchKernelGGL(k_gs_count<4>, dim3((unsigned) nt), dim3(256), 0, st, (const int32_t *) b->theap,
+					   n, tc.as<uint32_t>());
+		else
+			hipLaunchKernelGGL(k_gs_count<8>, dim3((unsigned) nt), dim3(256), 0, st, (const int64_t *) b->theap,
+					   n, tc.as<uint32_t>());
+		if (exclusive_scan(tc.as<uint32_t>(), tp.as<uint64_t>(), nt, &ngrp) < 0)
+			return -1;
+		cap = ngrp;
+	}
+	mgdk_bat *en = newbat(0, MGDK_oid, cap), *hn = newbat(0, MGDK_lng, cap), *kn = newbat(0, MGDK_lng, cap);
 	mgdk_bat *sn[GS_MAXV] = {};
 	bool ok = en && hn && kn;
 	for (int v = 0; v < nvals && ok; v++)
-		ok = (sn[v] = newbat(0, MGDK_hge, ngrp)) != nullptr;
+		ok = (sn[v] = newbat(0, MGDK_hge, cap)) != nullptr;
 	const size_t esz = sizeof(GsEdge<GS_MAXV>);
-	DevBuf edges(2 * nt * esz + 64);
+	// the tiles' edge records, then the list of groups over more than
+	// GS_ECAP records (k_gs_edges_long)
+	const size_t lgoff = (2 * nt * esz + 255) & ~(size_t) 255;
+	DevBuf edges(lgoff + (2 * nt / GS_ECAP + 2) * 4);
+	uint32_t *longs = (uint32_t *) ((char *) edges.p + lgoff);
 	uint32_t *flags = (uint32_t *) meta_buf();
 	const void *hv[GS_MAXV] = {};
 	for (int v = 0; v < nvals; v++)
@@ -527,16 +738,28 @@ mgdk_group_sums_ordered(mgdk_bat **extents, mgdk_bat **histo, mgdk_bat **keys, m
 	o.flags = flags;
 	const void *const *vd = vp.as<const void *const>();
 	if (kw == 4 && vw == 4)
-		gs_nv<4, 4>(nvals, b->theap, vd, n, b->hseqbase, tp.as<uint64_t>(), nt, ngrp, o, edges.p);
+		gs_nv<4, 4>(nvals, b->theap, vd, n, b->hseqbase, tp.as<uint64_t>(), nt, cap, o, edges.p, longs, lbp);
 	else if (kw == 4)
-		gs_nv<4, 8>(nvals, b->theap, vd, n, b->hseqbase, tp.as<uint64_t>(), nt, ngrp, o, edges.p);
+		gs_nv<4, 8>(nvals, b->theap, vd, n, b->hseqbase, tp.as<uint64_t>(), nt, cap, o, edges.p, longs, lbp);
 	else if (vw == 4)
-		gs_nv<8, 4>(nvals, b->theap, vd, n, b->hseqbase, tp.as<uint64_t>(), nt, ngrp, o, edges.p);
+		gs_nv<8, 4>(nvals, b->theap, vd, n, b->hseqbase, tp.as<uint64_t>(), nt, cap, o, edges.p, longs, lbp);
 	else
-		gs_nv<8, 8>(nvals, b->theap, vd, n, b->hseqbase, tp.as<uint64_t>(), nt, ngrp, o, edges.p);
-	uint32_t *hf = (uint32_t *) pinned(16);
-	if (!hip_ok(hipMemcpyAsync(hf, flags, 4, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+		gs_nv<8, 8>(nvals, b->theap, vd, n, b->hseqbase, tp.as<uint64_t>(), nt, cap, o, edges.p, longs, lbp);
+	uint32_t *hf = (uint32_t *) pinned(32);
+	if (!hip_ok(hipMemcpyAsync(hf, flags, 4, hipMemcpyDeviceToHost, st), "memcpy") ||
+	    (fused && (!hip_ok(hipMemcpyAsync(hf + 2, lb.status + (nt - 1), 8, hipMemcpyDeviceToHost, st), "memcpy") ||
+		       !hip_ok(hipMemcpyAsync(hf + 4, lb.err, 4, hipMemcpyDeviceToHost, st), "memcpy"))) ||
+	    !sync())
 		return fail();
+	if (fused) {
+		uint64_t last;
+		memcpy(&last, hf + 2, 8);
+		if (hf[4] || (last >> 62) != 2) {
+			seterr("HY013!group_sums_ordered: look-back did not complete");
+			return fail();
+		}
+		ngrp = last & mgdk_lb::ST_VAL;
+	}
 	const bool anynil = (hf[0] & 2) != 0;
 	// properties as BATgroup / BATgroupsum leave them (extents ascending and
 	// key, the histogram and sums unknown, keys ordered as b)

@@ -388,6 +388,634 @@ jk_run(const char *fn, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, boo
 	return 0;
 }
 
+// ---- BATthetajoin / BATbandjoin (gdk_join.c:3699 thetajoin, :4626) -----
+// The reference runs nested loops: the pairs in left-candidate order, each
+// left candidate's matches in right-candidate order.  On the device the
+// right candidates' values are sorted once (their candidate index along);
+// a left value's matches are one range of that order (two for <>), found by
+// binary search -- the predicate is monotone in the right value -- then the
+// counts give the offsets, each left candidate writes its (left, right)
+// index pairs, and a sort of the pairs restores the right-candidate order
+// inside each left candidate (skipped when the right side is already in
+// value order).  bandjoin over flt / dbl evaluates the reference's
+// floating-point expression (and its overflow rules) pair by pair instead:
+// a brute-force nested loop, right values streamed through LDS.
+
+#pragma clang fp contract(off)
+
+// signed 64-bit key ordered as ATOMcompare: nil the smallest (and equal to
+// itself), -0.0 == +0.0 for flt / dbl
+__device__ __forceinline__ int64_t
+th_key(const JSide &s, int fk, BUN p)
+{
+	if (fk == 0) {
+		bool isnil;
+		const int64_t v = js_val(s, p, isnil);
+		return isnil ? INT64_MIN : v;
+	}
+	double d = fk == 1 ? (double) ((const float *) s.base)[p] : ((const double *) s.base)[p];
+	if (d != d)
+		return INT64_MIN;
+	if (d == 0)
+		d = 0;
+	uint64_t b = (uint64_t) __double_as_longlong(d);
+	b = (b >> 63) ? ~b : (b | (1ull << 63));
+	return (int64_t) (b ^ (1ull << 63));
+}
+
+__global__ __launch_bounds__(256) void
+k_th_rkeys(JSide r, int fk, int64_t *key)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < r.n; i += (BUN) gridDim.x * blockDim.x)
+		key[i] = th_key(r, fk, js_oid(r, i) - r.hseq);
+}
+
+// first index in [a, b) with v[i] >= x (ge) or v[i] > x (!ge)
+__device__ __forceinline__ BUN
+th_bound(const int64_t *v, BUN a, BUN b, int64_t x, bool gt)
+{
+	while (a < b) {
+		const BUN m = a + (b - a) / 2;
+		if (gt ? v[m] <= x : v[m] < x)
+			a = m + 1;
+		else
+			b = m;
+	}
+	return a;
+}
+
+struct ThArgs {
+	int mode;          // 0 theta, 1 band (integers)
+	int mask;          // theta: MASK_EQ 1 | MASK_LT 2 | MASK_GT 4
+	bool nil_matches;
+	hge c1, c2;        // band
+	bool linc, hinc;
+};
+
+// per left candidate: its ranges [r0, r1) and [r2, r3) of the sorted right
+// values and their total
+__global__ __launch_bounds__(256) void
+k_th_ranges(JSide L, int fk, const int64_t *sk, BUN nr, ThArgs t, uint32_t *rg, uint32_t *cnt)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < L.n; i += (BUN) gridDim.x * blockDim.x) {
+		const int64_t x = th_key(L, fk, js_oid(L, i) - L.hseq);
+		const BUN nnil = th_bound(sk, 0, nr, INT64_MIN, true);
+		BUN a = 0, b = 0, c = 0, d = 0;
+		if (t.mode == 0) {
+			if (x != INT64_MIN || t.nil_matches) {
+				// the right values below / equal to / above x are three
+				// consecutive parts; vl op vr keeps some of them: GT the
+				// part below, EQ the equal one, LT the part above
+				const BUN s0 = t.nil_matches ? 0 : nnil;
+				const BUN lo = th_bound(sk, s0, nr, x, false), hi = th_bound(sk, s0, nr, x, true);
+				const BUN pa[3] = {s0, lo, hi}, pb[3] = {lo, hi, nr};
+				const bool inc[3] = {(t.mask & 4) != 0, (t.mask & 1) != 0, (t.mask & 2) != 0};
+				int nrg = 0;
+				BUN ra[2] = {0, 0}, rb[2] = {0, 0};
+				for (int q = 0; q < 3; q++) {
+					if (!inc[q] || pa[q] == pb[q])
+						continue;
+					if (nrg && rb[nrg - 1] == pa[q])
+						rb[nrg - 1] = pb[q];
+					else {
+						ra[nrg] = pa[q];
+						rb[nrg] = pb[q];
+						nrg++;
+					}
+				}
+				a = ra[0];
+				b = rb[0];
+				c = ra[1];
+				d = rb[1];
+			}
+		} else if (x != INT64_MIN) {
+			// band: vr - c1 <= vl <= vr + c2 (exact): vl - c2 <= vr <= vl + c1
+			const hge lo = (hge) x - t.c2, hi = (hge) x + t.c1;
+			const int64_t lo64 = lo < (hge) INT64_MIN ? INT64_MIN : (int64_t) lo;
+			const int64_t hi64 = hi > (hge) INT64_MAX ? INT64_MAX : (int64_t) hi;
+			if (hi >= (hge) INT64_MIN && lo <= (hge) INT64_MAX) {
+				a = lo < (hge) INT64_MIN ? nnil : th_bound(sk, nnil, nr, lo64, !t.hinc);
+				b = hi > (hge) INT64_MAX ? nr : th_bound(sk, nnil, nr, hi64, t.linc);
+				if (b < a)
+					b = a;
+			}
+		}
+		rg[4 * i] = (uint32_t) a;
+		rg[4 * i + 1] = (uint32_t) b;
+		rg[4 * i + 2] = (uint32_t) c;
+		rg[4 * i + 3] = (uint32_t) d;
+		cnt[i] = (uint32_t) ((b - a) + (d - c));
+	}
+}
+
+// the pairs of each left candidate: key (left index << rb) | right index
+// (sorted order's payload), or straight into r1 / r2 when the right side
+// is in value order
+__global__ __launch_bounds__(256) void
+k_th_emit(JSide L, JSide R, const uint32_t *rg, const uint64_t *off, const oid *sidx, int rb, int64_t *keys,
+	  oid *r1, oid *r2)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < L.n; i += (BUN) gridDim.x * blockDim.x) {
+		BUN o = off[i];
+		const oid lo = js_oid(L, i);
+		for (int q = 0; q < 2; q++) {
+			const BUN a = rg[4 * i + 2 * q], b = rg[4 * i + 2 * q + 1];
+			for (BUN k = a; k < b; k++, o++) {
+				const BUN ri = sidx ? sidx[k] : k;
+				if (keys) {
+					keys[o] = (int64_t) (((uint64_t) i << rb) | ri);
+				} else {
+					r1[o] = lo;
+					r2[o] = js_oid(R, ri);
+				}
+			}
+		}
+	}
+}
+
+__global__ __launch_bounds__(256) void
+k_th_decode(const int64_t *keys, BUN n, int rb, JSide L, JSide R, oid *r1, oid *r2)
+{
+	const uint64_t m = ((uint64_t) 1 << rb) - 1;
+	for (BUN k = (BUN) blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (BUN) gridDim.x * blockDim.x) {
+		const uint64_t x = (uint64_t) keys[k];
+		r1[k] = js_oid(L, x >> rb);
+		r2[k] = js_oid(R, x & m);
+	}
+}
+
+// bandjoin's pair test for flt (in dbl) and dbl (SUBF / ADDF_WITH_CHECK),
+// gdk_join.c:4923-4966
+template <typename T>
+__device__ __forceinline__ bool
+band_fp(T vl, T vr, T c1, T c2, bool linc, bool hinc)
+{
+	if constexpr (sizeof(T) == 4) {
+		double v1 = (double) vr, v2 = v1;
+		v1 -= c1;
+		if (vl <= v1 && (!linc || vl != v1))
+			return false;
+		v2 += c2;
+		if (vl >= v2 && (!hinc || vl != v2))
+			return false;
+		return true;
+	} else {
+		const double mx = 1.7976931348623157e308;
+		bool skip1 = false;
+		double v1 = 0, v2 = 0;
+		if (c1 < 1 ? mx + c1 < vr : -mx + c1 > vr) {
+			if (c1 < 0)
+				return false;
+			skip1 = true;
+		} else {
+			v1 = vr - c1;
+		}
+		if (!skip1 && vl <= v1 && (!linc || vl != v1))
+			return false;
+		if (c2 < 1 ? -mx - c2 > vr : mx - c2 < vr) {
+			if (c2 > 0)
+				return false;
+			return true;
+		}
+		v2 = vr + c2;
+		if (vl >= v2 && (!hinc || vl != v2))
+			return false;
+		return true;
+	}
+}
+
+// brute force over the right candidates (streamed through LDS, 1024 at a
+// time): pass 0 counts per left candidate, pass 1 writes the pairs in
+// right-candidate order
+template <typename T>
+__global__ __launch_bounds__(256) void
+k_band_fp(JSide L, JSide R, T c1, T c2, bool linc, bool hinc, int pass, uint32_t *cnt, const uint64_t *off,
+	  oid *r1, oid *r2)
+{
+	__shared__ T sv[1024];
+	__shared__ oid so[1024];
+	__shared__ uint8_t sn[1024];
+	const BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x;
+	const bool live = i < L.n;
+	oid lo = 0;
+	T vl = 0;
+	bool lnil = true;
+	if (live) {
+		lo = js_oid(L, i);
+		vl = ((const T *) L.base)[lo - L.hseq];
+		lnil = vl != vl;
+	}
+	uint32_t c = 0;
+	BUN o = pass && live ? off[i] : 0;
+	for (BUN c0 = 0; c0 < R.n; c0 += 1024) {
+		__syncthreads();
+		for (unsigned q = threadIdx.x; q < 1024; q += blockDim.x) {
+			const BUN k = c0 + q;
+			if (k < R.n) {
+				const oid ro = js_oid(R, k);
+				const T v = ((const T *) R.base)[ro - R.hseq];
+				sv[q] = v;
+				so[q] = ro;
+				sn[q] = v != v;
+			}
+		}
+		__syncthreads();
+		if (!live || lnil)
+			continue;
+		const unsigned m = (unsigned) min((BUN) 1024, R.n - c0);
+		for (unsigned q = 0; q < m; q++) {
+			if (sn[q] || !band_fp<T>(vl, sv[q], c1, c2, linc, hinc))
+				continue;
+			if (pass) {
+				r1[o] = lo;
+				r2[o] = so[q];
+				o++;
+			} else {
+				c++;
+			}
+		}
+	}
+	if (live && !pass)
+		cnt[i] = c;
+}
+
+int
+th_fk(int t)
+{
+	return t == MGDK_flt ? 1 : t == MGDK_dbl ? 2 : 0;
+}
+
+bool
+th_type_ok(int t)
+{
+	return jk_type_ok(t) || t == MGDK_flt || t == MGDK_dbl;
+}
+
+// the shared driver: mode 0 theta (mask), 1 band (c1, c2 as the column's
+// type, already checked non-nil and non-empty)
+int
+th_run(const char *fn, mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, ThArgs t,
+       const void *c1, const void *c2)
+{
+	*r1p = nullptr;
+	if (r2p)
+		*r2p = nullptr;
+	Held held;
+	JSide L, R;
+	mgdk_bat *lb, *rb;
+	if (jside(fn, l, sl, &L, held, &lb) < 0 || jside(fn, r, sr, &R, held, &rb) < 0)
+		return -1;
+	const int tt = atomtype(lb->ttype);
+	if (tt != atomtype(rb->ttype)) {
+		seterr("%s: inputs not compatible.\n", fn);
+		return -1;
+	}
+	if (!th_type_ok(lb->ttype) || !th_type_ok(rb->ttype)) {
+		seterr("%s: type %s is not on the device path", fn, atomname(lb->ttype));
+		return -1;
+	}
+	// void with a nil sequence: every value nil (thetajoin :3738-3763)
+	const bool lallnil = lb->ttype == MGDK_void && lb->tseqbase == MGDK_OID_NIL;
+	const bool rallnil = rb->ttype == MGDK_void && rb->tseqbase == MGDK_OID_NIL;
+	ProfScope prof("thetajoin");
+	hipStream_t st = stream();
+	auto result = [&](BUN n, mgdk_bat **a, mgdk_bat **b) -> bool {
+		*a = newbat(0, MGDK_oid, n);
+		*b = newbat(0, MGDK_oid, n);
+		if (*a == nullptr || *b == nullptr) {
+			mgdk_BBPunfix(*a);
+			mgdk_BBPunfix(*b);
+			return false;
+		}
+		return true;
+	};
+	auto finish = [&](mgdk_bat *a, mgdk_bat *b, BUN n, bool onekey) {
+		a->count = b->count = n;
+		a->tsorted = a->tnonil = b->tnonil = 1;
+		a->tkey = onekey || n <= 1;
+		a->trevsorted = n <= 1;
+		b->tsorted = b->trevsorted = b->tkey = n <= 1;
+		*r1p = a;
+		if (r2p)
+			*r2p = b;
+		else
+			mgdk_BBPunfix(b);
+	};
+	if (L.n == 0 || R.n == 0 || ((lallnil || rallnil) && (t.mode == 1 || !t.nil_matches))) {
+		mgdk_bat *a, *b;
+		if (!result(0, &a, &b))
+			return -1;
+		finish(a, b, 0, true);
+		return 0;
+	}
+	const int fk = th_fk(tt);
+	if (t.mode == 1 && fk) {
+		// bandjoin over flt / dbl: the reference's expression pair by pair
+		DevBuf cnt(L.n * 4 + 4), off(L.n * 8 + 8);
+		if (!cnt.p || !off.p)
+			return -1;
+		const dim3 g((unsigned) ((L.n + 255) / 256));
+		if (fk == 1)
+			hipLaunchKernelGGL(k_band_fp<float>, g, dim3(256), 0, st, L, R, *(const float *) c1,
+					   *(const float *) c2, t.linc, t.hinc, 0, cnt.as<uint32_t>(), (const uint64_t *) nullptr,
+					   (oid *) nullptr, (oid *) nullptr);
+		else
+			hipLaunchKernelGGL(k_band_fp<double>, g, dim3(256), 0, st, L, R, *(const double *) c1,
+					   *(const double *) c2, t.linc, t.hinc, 0, cnt.as<uint32_t>(), (const uint64_t *) nullptr,
+					   (oid *) nullptr, (oid *) nullptr);
+		uint64_t tot = 0;
+		if (exclusive_scan(cnt.as<uint32_t>(), off.as<uint64_t>(), L.n, &tot) != 0)
+			return -1;
+		mgdk_bat *a, *b;
+		if (!result(tot, &a, &b))
+			return -1;
+		if (tot) {
+			if (fk == 1)
+				hipLaunchKernelGGL(k_band_fp<float>, g, dim3(256), 0, st, L, R, *(const float *) c1,
+						   *(const float *) c2, t.linc, t.hinc, 1, (uint32_t *) nullptr,
+						   off.as<uint64_t>(), (oid *) a->theap, (oid *) b->theap);
+			else
+				hipLaunchKernelGGL(k_band_fp<double>, g, dim3(256), 0, st, L, R, *(const double *) c1,
+						   *(const double *) c2, t.linc, t.hinc, 1, (uint32_t *) nullptr,
+						   off.as<uint64_t>(), (oid *) a->theap, (oid *) b->theap);
+		}
+		if (!sync()) {
+			mgdk_BBPunfix(a);
+			mgdk_BBPunfix(b);
+			return -1;
+		}
+		finish(a, b, tot, tot <= L.n && false);
+		return 0;
+	}
+	if (R.n >= 0xffffffffull || L.n >= 0xffffffffull) {
+		seterr("%s: more than 2^32-1 candidates on the device path", fn);
+		return -1;
+	}
+	// the right values sorted, their candidate index along
+	mgdk_bat *kb = held.keep(newbat(0, MGDK_lng, R.n));
+	if (kb == nullptr)
+		return -1;
+	hipLaunchKernelGGL(k_th_rkeys, dim3(grid_for(R.n, 256 * 8, 8192)), dim3(256), 0, st, R, fk, (int64_t *) kb->theap);
+	kb->count = R.n;
+	kb->tsorted = kb->trevsorted = kb->tkey = 0;
+	kb->tnonil = 0;
+	mgdk_bat *sv = nullptr, *so = nullptr;
+	if (mgdk_BATsort(&sv, &so, nullptr, kb, nullptr, nullptr, false, false, true) != 0)
+		return -1;
+	held.keep(sv);
+	held.keep(so);
+	const oid *sidx = so->ttype == MGDK_void ? nullptr : (const oid *) so->theap;
+	DevBuf rg(L.n * 16 + 16), cnt(L.n * 4 + 4), off(L.n * 8 + 8);
+	if (!rg.p || !cnt.p || !off.p)
+		return -1;
+	hipLaunchKernelGGL(k_th_ranges, dim3(grid_for(L.n, 256 * 4, 8192)), dim3(256), 0, st, L, fk,
+			   (const int64_t *) sv->theap, R.n, t, rg.as<uint32_t>(), cnt.as<uint32_t>());
+	uint64_t tot = 0;
+	if (exclusive_scan(cnt.as<uint32_t>(), off.as<uint64_t>(), L.n, &tot) != 0)
+		return -1;
+	int rbits = 1;
+	while (rbits < 63 && (R.n >> rbits))
+		rbits++;
+	if (sidx && (L.n >> (63 - rbits))) {
+		seterr("%s: result too large for the device path", fn);
+		return -1;
+	}
+	mgdk_bat *a, *b;
+	if (!result(tot, &a, &b))
+		return -1;
+	if (tot) {
+		if (sidx == nullptr) {
+			hipLaunchKernelGGL(k_th_emit, dim3(grid_for(L.n, 256 * 4, 8192)), dim3(256), 0, st, L, R,
+					   (const uint32_t *) rg.p, off.as<uint64_t>(), (const oid *) nullptr, rbits,
+					   (int64_t *) nullptr, (oid *) a->theap, (oid *) b->theap);
+		} else {
+			mgdk_bat *pk = held.keep(newbat(0, MGDK_lng, tot));
+			if (pk == nullptr) {
+				mgdk_BBPunfix(a);
+				mgdk_BBPunfix(b);
+				return -1;
+			}
+			hipLaunchKernelGGL(k_th_emit, dim3(grid_for(L.n, 256 * 4, 8192)), dim3(256), 0, st, L, R,
+					   (const uint32_t *) rg.p, off.as<uint64_t>(), sidx, rbits, (int64_t *) pk->theap,
+					   (oid *) nullptr, (oid *) nullptr);
+			pk->count = tot;
+			pk->tsorted = pk->trevsorted = pk->tkey = 0;
+			pk->tnonil = 1;
+			mgdk_bat *ps = nullptr;
+			if (mgdk_BATsort(&ps, nullptr, nullptr, pk, nullptr, nullptr, false, false, false) != 0) {
+				mgdk_BBPunfix(a);
+				mgdk_BBPunfix(b);
+				return -1;
+			}
+			held.keep(ps);
+			hipLaunchKernelGGL(k_th_decode, dim3(grid_for(tot, 256 * 8, 16384)), dim3(256), 0, st,
+					   (const int64_t *) ps->theap, tot, rbits, L, R, (oid *) a->theap, (oid *) b->theap);
+		}
+	}
+	if (!sync()) {
+		mgdk_BBPunfix(a);
+		mgdk_BBPunfix(b);
+		return -1;
+	}
+	finish(a, b, tot, false);
+	return 0;
+}
+
+// bandjoin's trivial cases (gdk_join.c:4667-4729): a nil bound, -c1 > c2,
+// or -c1 == c2 with an open end
+template <typename T>
+bool
+band_empty(const void *c1p, const void *c2p, bool linc, bool hinc)
+{
+	const T c1 = *(const T *) c1p, c2 = *(const T *) c2p;
+	if (is_nil(c1) || is_nil(c2))
+		return true;
+	return -c1 > c2 || ((!hinc || !linc) && -c1 == c2);
+}
+
+// ---- BATrangejoin (gdk_join.c:5422, rangejoin :5067) ---------------------
+// Not anti, not symmetric, l sorted or reverse sorted: per right candidate
+// (one lane each) the l positions of [rl, rh] by binary search
+// (SORTfndfirst / SORTfndlast), mapped to the left candidates in between;
+// right-major output placed by a scan of the counts.  Otherwise the nested
+// loop (left-major, BETWEEN's three-valued logic), brute force with the
+// right bounds streamed through LDS.  The result properties are the
+// reference's extra scan over the result (k_oid_props).
+
+// first position p of l (asc: value >= v / > v with last; desc: <= v / < v)
+__device__ __forceinline__ BUN
+rj_fnd(const JSide &l, int fk, BUN cnt, bool rev, int64_t v, bool last)
+{
+	BUN a = 0, b = cnt;
+	while (a < b) {
+		const BUN m = a + (b - a) / 2;
+		const int64_t x = th_key(l, fk, m);
+		const bool before = rev ? (last ? x >= v : x > v) : (last ? x <= v : x < v);
+		if (before)
+			a = m + 1;
+		else
+			b = m;
+	}
+	return a;
+}
+
+// index of the first candidate >= o (canditer_search(.., next = true))
+__device__ __forceinline__ BUN
+cand_lower(const JSide &c, oid o)
+{
+	if (c.dense)
+		return o <= c.seq ? 0 : (o - c.seq < c.n ? o - c.seq : c.n);
+	BUN a = 0, b = c.n;
+	while (a < b) {
+		const BUN m = a + (b - a) / 2;
+		if (c.oids[m] < o)
+			a = m + 1;
+		else
+			b = m;
+	}
+	return a;
+}
+
+__global__ __launch_bounds__(256) void
+k_rj_sorted(JSide L, BUN lcnt, JSide RL, JSide RH, int fk, bool rev, bool linc, bool hinc, uint32_t *rg,
+	    uint32_t *cnt)
+{
+	for (BUN j = (BUN) blockIdx.x * blockDim.x + threadIdx.x; j < RL.n; j += (BUN) gridDim.x * blockDim.x) {
+		const oid ro = js_oid(RL, j);
+		const int64_t vlo = th_key(RL, fk, ro - RL.hseq), vhi = th_key(RH, fk, ro - RH.hseq);
+		BUN cl = 0, ch = 0;
+		if (vlo != INT64_MIN && vhi != INT64_MIN) {
+			BUN low, high;
+			if (!rev) {
+				low = rj_fnd(L, fk, lcnt, false, vlo, !linc);
+				high = rj_fnd(L, fk, lcnt, false, vhi, hinc);
+			} else {
+				low = rj_fnd(L, fk, lcnt, true, vhi, !hinc);
+				high = rj_fnd(L, fk, lcnt, true, vlo, linc);
+			}
+			if (high > low) {
+				cl = cand_lower(L, low + L.hseq);
+				ch = cand_lower(L, high + L.hseq);
+			}
+		}
+		rg[2 * j] = (uint32_t) cl;
+		rg[2 * j + 1] = (uint32_t) (ch > cl ? ch : cl);
+		cnt[j] = (uint32_t) (ch > cl ? ch - cl : 0);
+	}
+}
+
+__global__ __launch_bounds__(256) void
+k_rj_sorted_emit(JSide L, JSide RL, const uint32_t *rg, const uint64_t *off, oid *r1, oid *r2)
+{
+	for (BUN j = (BUN) blockIdx.x * blockDim.x + threadIdx.x; j < RL.n; j += (BUN) gridDim.x * blockDim.x) {
+		const oid ro = js_oid(RL, j);
+		BUN o = off[j];
+		for (BUN q = rg[2 * j]; q < rg[2 * j + 1]; q++, o++) {
+			r1[o] = js_oid(L, q);
+			r2[o] = ro;
+		}
+	}
+}
+
+// BETWEEN (gdk_join.c:5040-5064): 1 true, 0 false, -1 nil
+__device__ __forceinline__ int
+rj_between3(int64_t v, int64_t lo, bool linc, int64_t hi, bool hinc)
+{
+	const int g = lo == INT64_MIN ? -1 : (lo < v || (linc && v == lo));
+	const int l = hi == INT64_MIN ? -1 : (v < hi || (hinc && v == hi));
+	if (g == 0 || l == 0)
+		return 0;
+	return g < 0 || l < 0 ? -1 : 1;
+}
+
+// the nested loop: pass 0 counts per left candidate, pass 1 writes
+__global__ __launch_bounds__(256) void
+k_rj_nested(JSide L, JSide RL, JSide RH, int fk, bool linc, bool hinc, bool anti, bool symmetric, int pass,
+	    uint32_t *cnt, const uint64_t *off, oid *r1, oid *r2)
+{
+	__shared__ int64_t slo[1024], shi[1024];
+	__shared__ oid so[1024];
+	const BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x;
+	const bool live = i < L.n;
+	oid lo = 0;
+	int64_t v = INT64_MIN;
+	if (live) {
+		lo = js_oid(L, i);
+		v = th_key(L, fk, lo - L.hseq);
+	}
+	const bool vn = v == INT64_MIN && L.base != nullptr;
+	uint32_t c = 0;
+	BUN o = pass && live ? off[i] : 0;
+	for (BUN c0 = 0; c0 < RL.n; c0 += 1024) {
+		__syncthreads();
+		for (unsigned q = threadIdx.x; q < 1024; q += blockDim.x) {
+			const BUN k = c0 + q;
+			if (k < RL.n) {
+				const oid ro = js_oid(RL, k);
+				slo[q] = th_key(RL, fk, ro - RL.hseq);
+				shi[q] = th_key(RH, fk, ro - RH.hseq);
+				so[q] = ro;
+			}
+		}
+		__syncthreads();
+		if (!live || vn)
+			continue;
+		const unsigned m = (unsigned) min((BUN) 1024, RL.n - c0);
+		for (unsigned q = 0; q < m; q++) {
+			int r = rj_between3(v, slo[q], linc, shi[q], hinc);
+			if (symmetric) {
+				const int r2v = rj_between3(v, shi[q], hinc, slo[q], linc);
+				r = r == 1 || r2v == 1 ? 1 : (r < 0 || r2v < 0 ? -1 : 0);
+			}
+			if (anti)
+				r = r < 0 ? -1 : !r;
+			if (r != 1)
+				continue;
+			if (pass) {
+				r1[o] = lo;
+				r2[o] = so[q];
+				o++;
+			} else {
+				c++;
+			}
+		}
+	}
+	if (live && !pass)
+		cnt[i] = c;
+}
+
+// the reference's property scan of an oid result: bit 0 equal neighbours,
+// 1 an ascent, 2 a descent, 3 an ascent by more than one
+__global__ __launch_bounds__(256) void
+k_oid_props(const oid *d, BUN n, uint32_t *flags)
+{
+	uint32_t f = 0;
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x + 1; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		const oid a = d[i - 1], b = d[i];
+		if (a == b)
+			f |= 1;
+		else if (a < b)
+			f |= 2 | (a + 1 != b ? 8u : 0u);
+		else
+			f |= 4;
+	}
+	f = block_reduce(f, [](uint32_t x, uint32_t y) { return x | y; });
+	if (threadIdx.x == 0 && f)
+		atomicOr(flags, f);
+}
+
+// r's properties from k_oid_props' bits (gdk_join.c:5351-5410)
+void
+rj_props(mgdk_bat *r, uint32_t f, oid first)
+{
+	r->tkey = !(f & 1) && !(f & 4);
+	r->tsorted = !(f & 4);
+	r->trevsorted = !(f & 2);
+	r->tnil = 0;
+	r->tnonil = 1;
+	r->tseqbase = (!(f & 1) && !(f & 4) && !(f & 8)) ? (r->count ? first : 0) : MGDK_OID_NIL;
+}
+
 }  // namespace
 
 extern "C" mgdk_bat *
@@ -435,4 +1063,216 @@ mgdk_BATouterjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk
 {
 	(void) estimate;
 	return jk_run("BATouterjoin", l, r, sl, sr, nil_matches, false, match_one, 3, r1p, r2p);
+}
+
+// BATthetajoin (gdk_join.c:4409): op JOIN_EQ 0 (BATjoin), JOIN_LT -1,
+// JOIN_LE -2, JOIN_GT 1, JOIN_GE 2, JOIN_NE -3
+extern "C" int
+mgdk_BATthetajoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, int op,
+		  bool nil_matches, mgdk_BUN estimate)
+{
+	ThArgs t{};
+	switch (op) {
+	case 0:
+		return mgdk_BATjoin(r1p, r2p, l, r, sl, sr, nil_matches, estimate);
+	case -3: t.mask = 2 | 4; break;
+	case -1: t.mask = 2; break;
+	case -2: t.mask = 2 | 1; break;
+	case 1: t.mask = 4; break;
+	case 2: t.mask = 4 | 1; break;
+	default:
+		seterr("unknown operator %d.\n", op);
+		return -1;
+	}
+	if (l == nullptr || r == nullptr) {
+		seterr("BATthetajoin: inputs must not be NULL");
+		return -1;
+	}
+	t.mode = 0;
+	t.nil_matches = nil_matches;
+	return th_run("BATthetajoin", r1p, r2p, l, r, sl, sr, t, nullptr, nullptr);
+}
+
+// BATbandjoin (gdk_join.c:4626): l within [r - c1, r + c2] (linc / hinc
+// include the ends); c1, c2 point at values of the columns' type
+extern "C" int
+mgdk_BATbandjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, const void *c1,
+		 const void *c2, bool linc, bool hinc, mgdk_BUN estimate)
+{
+	(void) estimate;
+	*r1p = nullptr;
+	if (r2p)
+		*r2p = nullptr;
+	if (l == nullptr || r == nullptr || c1 == nullptr || c2 == nullptr) {
+		seterr("BATbandjoin: inputs must not be NULL");
+		return -1;
+	}
+	if (atomtype(l->ttype) != atomtype(r->ttype)) {
+		seterr("BATbandjoin: inputs not compatible.\n");
+		return -1;
+	}
+	const int bt = basetype(l->ttype);
+	bool empty;
+	ThArgs t{};
+	t.mode = 1;
+	t.linc = linc;
+	t.hinc = hinc;
+	switch (bt) {
+	case MGDK_bte: empty = band_empty<int8_t>(c1, c2, linc, hinc); t.c1 = *(const int8_t *) c1; t.c2 = *(const int8_t *) c2; break;
+	case MGDK_sht: empty = band_empty<int16_t>(c1, c2, linc, hinc); t.c1 = *(const int16_t *) c1; t.c2 = *(const int16_t *) c2; break;
+	case MGDK_int: empty = band_empty<int32_t>(c1, c2, linc, hinc); t.c1 = *(const int32_t *) c1; t.c2 = *(const int32_t *) c2; break;
+	case MGDK_lng: empty = band_empty<int64_t>(c1, c2, linc, hinc); t.c1 = *(const int64_t *) c1; t.c2 = *(const int64_t *) c2; break;
+	case MGDK_flt: empty = band_empty<float>(c1, c2, linc, hinc); break;
+	case MGDK_dbl: empty = band_empty<double>(c1, c2, linc, hinc); break;
+	default:
+		seterr("unsupported type\n");
+		return -1;
+	}
+	if (empty) {
+		mgdk_bat *a = newbat(0, MGDK_oid, 0), *b = newbat(0, MGDK_oid, 0);
+		if (a == nullptr || b == nullptr) {
+			mgdk_BBPunfix(a);
+			mgdk_BBPunfix(b);
+			return -1;
+		}
+		a->tsorted = a->trevsorted = a->tkey = a->tnonil = 1;
+		b->tsorted = b->trevsorted = b->tkey = b->tnonil = 1;
+		*r1p = a;
+		if (r2p)
+			*r2p = b;
+		else
+			mgdk_BBPunfix(b);
+		return 0;
+	}
+	return th_run("BATbandjoin", r1p, r2p, l, r, sl, sr, t, c1, c2);
+}
+
+// BATrangejoin (gdk_join.c:5422): l within [rl, rh] of each right candidate
+extern "C" int
+mgdk_BATrangejoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *rl, mgdk_bat *rh, mgdk_bat *sl, mgdk_bat *sr,
+		  bool linc, bool hinc, bool anti, bool symmetric, mgdk_BUN estimate)
+{
+	(void) estimate;
+	*r1p = nullptr;
+	if (r2p)
+		*r2p = nullptr;
+	if (l == nullptr || rl == nullptr || rh == nullptr) {
+		seterr("BATrangejoin: inputs must not be NULL");
+		return -1;
+	}
+	if (atomtype(l->ttype) != atomtype(rl->ttype) || atomtype(l->ttype) != atomtype(rh->ttype)) {
+		seterr("BATrangejoin: inputs not compatible.\n");
+		return -1;
+	}
+	if (rl->count != rh->count || rl->hseqbase != rh->hseqbase) {
+		seterr("BATrangejoin: right inputs not aligned.\n");
+		return -1;
+	}
+	Held held;
+	JSide L, RL, RH;
+	mgdk_bat *lb, *rlb, *rhb;
+	if (jside("BATrangejoin", l, sl, &L, held, &lb) < 0 || jside("BATrangejoin", rl, sr, &RL, held, &rlb) < 0 ||
+	    jside("BATrangejoin", rh, sr, &RH, held, &rhb) < 0)
+		return -1;
+	if (!th_type_ok(lb->ttype) || !th_type_ok(rlb->ttype) || !th_type_ok(rhb->ttype)) {
+		seterr("BATrangejoin: type %s is not on the device path", atomname(lb->ttype));
+		return -1;
+	}
+	const bool lnilall = lb->ttype == MGDK_void && lb->tseqbase == MGDK_OID_NIL;
+	const bool rlnil = rlb->ttype == MGDK_void && rlb->tseqbase == MGDK_OID_NIL;
+	const bool rhnil = rhb->ttype == MGDK_void && rhb->tseqbase == MGDK_OID_NIL;
+	hipStream_t st = stream();
+	ProfScope prof("rangejoin");
+	const int fk = th_fk(atomtype(lb->ttype));
+	mgdk_bat *a = nullptr, *b = nullptr;
+	uint64_t tot = 0;
+	auto alloc = [&](BUN n) {
+		a = newbat(0, MGDK_oid, n);
+		b = newbat(0, MGDK_oid, n);
+		if (a == nullptr || b == nullptr) {
+			mgdk_BBPunfix(a);
+			mgdk_BBPunfix(b);
+			return false;
+		}
+		return true;
+	};
+	if (L.n == 0 || RL.n == 0 || lnilall || (rlnil && rhnil) || ((rlnil || rhnil) && !anti)) {
+		if (!alloc(0))
+			return -1;
+	} else if (rlnil || rhnil) {
+		// anti with a nil bound column: thetajoin l > rh (or l < rl), :5448-5460
+		ThArgs t{};
+		t.mode = 0;
+		t.mask = rlnil ? 4 : 2;
+		t.nil_matches = false;
+		return th_run("BATrangejoin", r1p, r2p, l, rlnil ? rh : rl, sl, sr, t, nullptr, nullptr);
+	} else if (RL.n >= 0xffffffffull || L.n >= 0xffffffffull) {
+		seterr("BATrangejoin: more than 2^32-1 candidates on the device path");
+		return -1;
+	} else {
+		// the reference computes both orders first (:5071-5075)
+		bool asc = false, desc = false;
+		if (!anti && !symmetric) {
+			asc = mgdk_BATordered(lb);
+			desc = mgdk_BATordered_rev(lb);
+		}
+		if (asc || desc) {
+			DevBuf rg(RL.n * 8 + 8), cnt(RL.n * 4 + 4), off(RL.n * 8 + 8);
+			if (!rg.p || !cnt.p || !off.p)
+				return -1;
+			hipLaunchKernelGGL(k_rj_sorted, dim3(grid_for(RL.n, 256 * 4, 8192)), dim3(256), 0, st, L, lb->count, RL,
+					   RH, fk, !asc, linc, hinc, rg.as<uint32_t>(), cnt.as<uint32_t>());
+			if (exclusive_scan(cnt.as<uint32_t>(), off.as<uint64_t>(), RL.n, &tot) != 0 || !alloc(tot))
+				return -1;
+			if (tot)
+				hipLaunchKernelGGL(k_rj_sorted_emit, dim3(grid_for(RL.n, 256 * 4, 8192)), dim3(256), 0, st, L, RL,
+						   (const uint32_t *) rg.p, off.as<uint64_t>(), (oid *) a->theap, (oid *) b->theap);
+		} else {
+			DevBuf cnt(L.n * 4 + 4), off(L.n * 8 + 8);
+			if (!cnt.p || !off.p)
+				return -1;
+			const dim3 g((unsigned) ((L.n + 255) / 256));
+			hipLaunchKernelGGL(k_rj_nested, g, dim3(256), 0, st, L, RL, RH, fk, linc, hinc, anti, symmetric, 0,
+					   cnt.as<uint32_t>(), (const uint64_t *) nullptr, (oid *) nullptr, (oid *) nullptr);
+			if (exclusive_scan(cnt.as<uint32_t>(), off.as<uint64_t>(), L.n, &tot) != 0 || !alloc(tot))
+				return -1;
+			if (tot)
+				hipLaunchKernelGGL(k_rj_nested, g, dim3(256), 0, st, L, RL, RH, fk, linc, hinc, anti, symmetric,
+						   1, (uint32_t *) nullptr, off.as<uint64_t>(), (oid *) a->theap, (oid *) b->theap);
+		}
+	}
+	DevBuf fl(16);
+	uint32_t *h = (uint32_t *) pinned(32);
+	if (!fl.p || !hip_ok(hipMemsetAsync(fl.p, 0, 16, st), "memset")) {
+		mgdk_BBPunfix(a);
+		mgdk_BBPunfix(b);
+		return -1;
+	}
+	if (tot > 1) {
+		hipLaunchKernelGGL(k_oid_props, dim3(grid_for(tot, 256 * 8, 4096)), dim3(256), 0, st, (const oid *) a->theap,
+				   tot, fl.as<uint32_t>());
+		hipLaunchKernelGGL(k_oid_props, dim3(grid_for(tot, 256 * 8, 4096)), dim3(256), 0, st, (const oid *) b->theap,
+				   tot, fl.as<uint32_t>() + 1);
+	}
+	bool ok = hip_ok(hipMemcpyAsync(h, fl.p, 8, hipMemcpyDeviceToHost, st), "memcpy");
+	if (ok && tot)
+		ok = hip_ok(hipMemcpyAsync(h + 2, a->theap, 8, hipMemcpyDeviceToHost, st), "memcpy") &&
+		     hip_ok(hipMemcpyAsync(h + 4, b->theap, 8, hipMemcpyDeviceToHost, st), "memcpy");
+	if (!ok || !sync()) {
+		mgdk_BBPunfix(a);
+		mgdk_BBPunfix(b);
+		return -1;
+	}
+	oid f1 = 0, f2 = 0;
+	memcpy(&f1, h + 2, 8);
+	memcpy(&f2, h + 4, 8);
+	a->count = b->count = tot;
+	rj_props(a, h[0], f1);
+	rj_props(b, h[1], f2);
+	*r1p = a;
+	if (r2p)
+		*r2p = b;
+	else
+		mgdk_BBPunfix(b);
+	return 0;
 }

@@ -75,4 +75,36 @@ lookback(uint64_t *status, uint32_t tile, uint64_t agg, uint32_t *err)
 	return excl;
 }
 
+
+// XCD-grouped tile claims (sort.hip's claim_tile): the tiles are dealt to
+// the XCDs in groups of xg consecutive tiles; each XCD claims its own tiles
+// in order through its ticket xtk[xcd] and takes another XCD's when its own
+// are gone.  A tile's predecessor may then be unclaimed while the tile
+// waits on it (and stay so while the dispatcher has no room for the
+// workgroup that would claim it), so a look-back over such claims must not
+// wait for an unclaimed predecessor: xcd_claimed tells.
+__device__ __forceinline__ uint32_t
+claim_xcd_tile(uint32_t *xtk, uint32_t ntiles, uint32_t xg)
+{
+	const uint32_t x = (uint32_t) __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7;   // HW_REG_XCC_ID
+	for (uint32_t k = 0; k < 8; k++) {
+		const uint32_t y = (x + k) & 7;
+		const uint32_t j = atomicAdd(&xtk[y], 1u);
+		const uint32_t t = (j / xg) * 8 * xg + y * xg + j % xg;
+		if (t < ntiles)
+			return t;
+	}
+	return ~0u;
+}
+
+// tile t has been claimed (every claim of it is an atomicAdd on its owner's
+// ticket that passed it)
+__device__ __forceinline__ bool
+xcd_claimed(const uint32_t *xtk, uint64_t t, uint32_t xg)
+{
+	const uint32_t y = (uint32_t) (t / xg) & 7;
+	const uint32_t j = (uint32_t) (t / (8 * (uint64_t) xg)) * xg + (uint32_t) (t % xg);
+	return __hip_atomic_load(&xtk[y], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > j;
+}
+
 }  // namespace mgdk_lb

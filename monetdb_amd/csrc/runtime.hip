@@ -47,6 +47,7 @@ struct ThreadCtx {
 	size_t scratch_size = 0;
 	void *pinned = nullptr;
 	size_t pinned_size = 0;
+	std::vector<void *> pinned_retired;   // outgrown pinned buffers (see pinned())
 	void *meta = nullptr;
 	void *stage = nullptr;          // pinned upload arena, reclaimed at sync()
 	size_t stage_size = 0, stage_used = 0;
@@ -59,6 +60,8 @@ struct ThreadCtx {
 			dfree(scratch);
 		if (pinned)
 			(void) hipHostFree(pinned);
+		for (void *q : pinned_retired)
+			(void) hipHostFree(q);
 		if (s)
 			(void) hipStreamDestroy(s);
 	}
@@ -225,12 +228,15 @@ void *
 pinned(size_t bytes)
 {
 	if (tctx.pinned_size < bytes) {
+		// an outgrown buffer is retired, not freed: a caller may hold it
+		// across a nested operator that asks for more (it stays valid until
+		// the thread ends; sizes at least double, so the retired buffers
+		// together are never larger than the live one)
 		if (tctx.pinned)
-			(void) hipHostFree(tctx.pinned);
-		// 1 MiB at least: a caller may hold the buffer across an operator
-		// that asks for a few KiB more (a reallocation would leave it
-		// dangling)
+			tctx.pinned_retired.push_back(tctx.pinned);
 		size_t n = bytes < (1u << 20) ? (size_t) 1 << 20 : bytes;
+		if (n < 2 * tctx.pinned_size)
+			n = 2 * tctx.pinned_size;
 		if (hipHostMalloc(&tctx.pinned, n, hipHostMallocDefault) != hipSuccess) {
 			tctx.pinned = nullptr;
 			tctx.pinned_size = 0;

@@ -1248,10 +1248,10 @@ select_str(mgdk_bat *b, const Cand &ci, const char *tl, const char *th, bool li,
 	hipStream_t st = stream();
 	if (!vals.p || !flags.p || !hip_ok(hipMemsetAsync(flags.p, 0, m, st), "memset"))
 		return nullptr;
-	char *hv = (char *) stage_host(tl, ll);
-	char *hv2 = (char *) stage_host(th, hl);
-	if (!hip_ok(hipMemcpyAsync(vals.p, hv, ll, hipMemcpyHostToDevice, st), "memcpy") ||
-	    !hip_ok(hipMemcpyAsync((char *) vals.p + ll, hv2, hl, hipMemcpyHostToDevice, st), "memcpy"))
+	// each bound's copy is queued right after it is staged: a second
+	// stage_host may wrap the arena (sync + reuse from offset 0)
+	if (!hip_ok(hipMemcpyAsync(vals.p, stage_host(tl, ll), ll, hipMemcpyHostToDevice, st), "memcpy") ||
+	    !hip_ok(hipMemcpyAsync((char *) vals.p + ll, stage_host(th, hl), hl, hipMemcpyHostToDevice, st), "memcpy"))
 		return nullptr;
 	StrSel a{};
 	a.offs = b->theap;

@@ -36,11 +36,16 @@ using namespace mgdk;
 
 namespace {
 
+// 4-byte keys: 8 waves x 16 rows (122 VGPRs, 4 waves per SIMD) measured
+// 2.80-2.84 ms for 100M int32 against 3.05-3.07 for 4 x 32 (243 VGPRs, 2
+// waves per SIMD) on the same boxes with the per-thread look-back
+// (profiles/r05/sort); in round 3, with the walk waiting on residency, it
+// was the other way round
 #ifndef MGDK_SORT_WAVES
-#define MGDK_SORT_WAVES 4
+#define MGDK_SORT_WAVES 8
 #endif
 #ifndef MGDK_SORT_ROWS
-#define MGDK_SORT_ROWS 32
+#define MGDK_SORT_ROWS 16
 #endif
 #ifndef MGDK_SORT_WAVES8
 #define MGDK_SORT_WAVES8 4
@@ -375,32 +380,32 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 		}
 	}
 	if (LB) {
-		// The walk back over the predecessors' digit counts, one step per
-		// predecessor for the whole workgroup.  A claimed predecessor is
-		// running and publishes its counts before anything it waits for, so
-		// waiting on it is safe.  An UNCLAIMED one (XCD claims deal tiles
-		// out of order) may never be claimed while we wait -- the
-		// dispatcher may have no room for the workgroup that would claim it
-		// -- so the workgroup counts that tile's digits itself from its keys
-		// (a pure function of the tile) and walks on: every step makes
-		// progress whatever is resident, and any claim order is safe.
-		// Claimed <=> its XCD's ticket has passed it (every claim of a tile
-		// is an atomicAdd on its owner's ticket, claim_tile).
+		// The walk back over the predecessors' digit counts: every thread
+		// (digit) walks on its own, as the classic decoupled look-back.  A
+		// claimed predecessor is running and publishes its counts before
+		// anything it waits for, so waiting on it is safe.  An UNCLAIMED one
+		// (XCD claims deal tiles out of order) may never be claimed while we
+		// wait -- the dispatcher may have no room for the workgroup that
+		// would claim it -- so a thread that finds its predecessor unclaimed
+		// stops, and the workgroup then counts that tile's digits itself
+		// from its keys (a pure function of the tile) and the thread walks
+		// on: every round makes progress whatever is resident, and any claim
+		// order is safe.  Claimed <=> its XCD's ticket has passed it (every
+		// claim of a tile is an atomicAdd on its owner's ticket,
+		// claim_tile).  Without a miss the walk costs one barrier.
 		using namespace mgdk_lb;
 		uint64_t excl = 0;
 		bool done = blk == 0 || !dig;
 		int64_t t = (int64_t) blk - 1;
 		__shared__ uint32_t fh[256];           // a predecessor's digit counts, counted here
+		__shared__ uint32_t s_miss;
 		const uint32_t *xtk = ticket + 8;
 		for (;;) {
 			bool miss = false;
-			if (!done) {
-				uint32_t spins = 0;
-				uint64_t s;
-				for (;;) {
-					s = lb_load(status + (size_t) t * 256 + tid);
-					if ((s >> 62) != 0)
-						break;
+			uint32_t spins = 0;
+			while (!done) {
+				const uint64_t sv = lb_load(status + (size_t) t * 256 + tid);
+				if ((sv >> 62) == 0) {
 					if (xg && (spins & 15) == 0) {
 						const uint32_t y = (uint32_t) (t / xg) & 7;
 						const uint32_t j = (uint32_t) (t / (8 * (int64_t) xg)) * xg + (uint32_t) (t % xg);
@@ -411,44 +416,52 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 					}
 					if (++spins > (1u << 26)) {
 						atomicOr(err, 1u);     // cannot happen: claimed tiles publish
-						s = ST_PRE;
+						done = true;
 						break;
 					}
 					__builtin_amdgcn_s_sleep(1);
+					continue;
 				}
-				if (!miss) {
-					excl += s & ST_VAL;
-					if (s & ST_PRE)
-						done = true;
-				}
+				spins = 0;
+				excl += sv & ST_VAL;
+				if ((sv & ST_PRE) || --t < 0)
+					done = true;
 			}
-			if (__syncthreads_or(miss)) {
-				if (dig)
-					fh[tid] = 0;
-				__syncthreads();
-				const BUN fb = (BUN) t * STILE, fe = fb + STILE < n ? fb + STILE : n;
-#pragma unroll 1
-				for (int r = 0; r < SROWS; r += 4) {
-					K fk[4];
-#pragma unroll
-					for (int u = 0; u < 4; u++) {
-						const BUN i = fb + (BUN) (r + u) * STHREADS + tid;
-						fk[u] = keys[i < fe ? i : fe - 1];
-					}
-#pragma unroll
-					for (int u = 0; u < 4; u++)
-						if (fb + (BUN) (r + u) * STHREADS + tid < fe)
-							atomicAdd(&fh[(uint32_t) (fk[u] >> shift) & 255], 1u);
-				}
-				__syncthreads();
-				if (miss)
-					excl += fh[tid];
-				__syncthreads();
-			}
-			if (!done && --t < 0)
-				done = true;
-			if (!__syncthreads_or(!done))
+			if (!__syncthreads_or(miss))
 				break;
+			// the latest tile some thread is missing: count it here
+			if (tid == 0)
+				s_miss = 0;
+			if (dig)
+				fh[tid] = 0;
+			__syncthreads();
+			if (miss)
+				atomicMax(&s_miss, (uint32_t) t + 1);
+			__syncthreads();
+			const int64_t ft = (int64_t) s_miss - 1;
+			const BUN fb = (BUN) ft * STILE, fe = fb + STILE < n ? fb + STILE : n;
+#pragma unroll 1
+			for (int r = 0; r < SROWS; r += 4) {
+				K fk[4];
+#pragma unroll
+				for (int u = 0; u < 4; u++) {
+					const BUN i = fb + (BUN) (r + u) * STHREADS + tid;
+					fk[u] = keys[i < fe ? i : fe - 1];
+				}
+#pragma unroll
+				for (int u = 0; u < 4; u++)
+					if (fb + (BUN) (r + u) * STHREADS + tid < fe)
+						atomicAdd(&fh[(uint32_t) (fk[u] >> shift) & 255], 1u);
+			}
+			__syncthreads();
+			if (miss && t == ft) {
+				excl += fh[tid];
+				if (--t < 0)
+					done = true;
+			}
+			// a thread missing an earlier tile looks at it again (it may
+			// be claimed by now, or is counted in a later round)
+			__syncthreads();
 		}
 		if (dig && blk != 0)
 			lb_store(status + (size_t) blk * 256 + tid, ST_PRE | (excl + tot));
@@ -1099,14 +1112,14 @@ k_final_copy_at(const K *keys, const uint32_t *vals, BUN m, BUN s, FinalOut fo)
 // first tile of an XCD's group depends on the previous XCD's whole group;
 // the tiles of it that are not claimed yet are counted by the waiting tile
 // itself (k_rs_scatter), so any group size completes (before that fallback
-// 128 / 256 took 9.4 ms / never completed on 100M int32; 32 2.94, 64
-// 2.79-2.84, 0 2.99 -- DESIGN §9).  4-byte keys run two scatter workgroups
-// per CU, 8-byte keys one
+// 128 / 256 took 9.4 ms / never completed on 100M int32).  Measured with
+// the 8 x 16 tile (profiles/r05/sort): 16 2.87, 24 3.06, 32 2.80, 48 3.54,
+// 64 3.24, 128 8.0 ms; 8-byte keys keep round 4's 32
 static uint32_t
 sort_xg(int kw = 4)
 {
 	const char *e = getenv("MGDK_SORT_XCDG");
-	return e ? (uint32_t) atoi(e) : kw == 4 ? 64u : 32u;
+	return e ? (uint32_t) atoi(e) : 32u;
 }
 
 template <typename K>

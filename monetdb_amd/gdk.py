@@ -153,6 +153,9 @@ _SIGS = {
     "mgdk_BATdiff": (P, [P, P, P, P, C.c_bool, C.c_bool, C.c_uint64]),
     "mgdk_BATsemijoin": (C.c_int, [PP, PP, P, P, P, P, C.c_bool, C.c_bool, C.c_uint64]),
     "mgdk_BATleftjoin": (C.c_int, [PP, PP, P, P, P, P, C.c_bool, C.c_uint64]),
+    "mgdk_BATthetajoin": (C.c_int, [PP, PP, P, P, P, P, C.c_int, C.c_bool, C.c_uint64]),
+    "mgdk_BATbandjoin": (C.c_int, [PP, PP, P, P, P, P, C.c_void_p, C.c_void_p, C.c_bool, C.c_bool, C.c_uint64]),
+    "mgdk_BATrangejoin": (C.c_int, [PP, PP, P, P, P, P, P, C.c_bool, C.c_bool, C.c_bool, C.c_bool, C.c_uint64]),
     "mgdk_BATouterjoin": (C.c_int, [PP, PP, P, P, P, P, C.c_bool, C.c_bool, C.c_uint64]),
     "mgdk_BATordered": (C.c_bool, [P]),
     "mgdk_BATordered_rev": (C.c_bool, [P]),
@@ -770,6 +773,34 @@ def BATleftjoin(l, r, sl=None, sr=None, nil_matches=False, estimate=0):
     """gdk_join.c:4320: (left, match) pairs in left order."""
     a, b = P(), P()
     _chk(lib().mgdk_BATleftjoin(C.byref(a), C.byref(b), l.ptr, r.ptr, _p(sl), _p(sr), nil_matches, estimate))
+    return BAT(a), BAT(b)
+
+
+JOIN_EQ, JOIN_LT, JOIN_LE, JOIN_GT, JOIN_GE, JOIN_NE = 0, -1, -2, 1, 2, -3
+
+
+def BATthetajoin(l, r, sl=None, sr=None, op=JOIN_LT, nil_matches=False, estimate=0):
+    """BATthetajoin (gdk_join.c:4409): (r1, r2) pairs with l op r"""
+    a, b = P(), P()
+    _chk(lib().mgdk_BATthetajoin(C.byref(a), C.byref(b), l.ptr, r.ptr, _p(sl), _p(sr), op, nil_matches,
+                                 estimate))
+    return BAT(a), BAT(b)
+
+
+def BATbandjoin(l, r, c1, c2, sl=None, sr=None, linc=True, hinc=True, estimate=0):
+    """BATbandjoin (gdk_join.c:4626): r - c1 <= l <= r + c2"""
+    keep = []
+    a, b = P(), P()
+    _chk(lib().mgdk_BATbandjoin(C.byref(a), C.byref(b), l.ptr, r.ptr, _p(sl), _p(sr), _valptr(l.ttype, c1, keep),
+                                _valptr(l.ttype, c2, keep), linc, hinc, estimate))
+    return BAT(a), BAT(b)
+
+
+def BATrangejoin(l, rl, rh, sl=None, sr=None, linc=True, hinc=True, anti=False, symmetric=False, estimate=0):
+    """BATrangejoin (gdk_join.c:5422): rl <= l <= rh per right candidate"""
+    a, b = P(), P()
+    _chk(lib().mgdk_BATrangejoin(C.byref(a), C.byref(b), l.ptr, rl.ptr, rh.ptr, _p(sl), _p(sr), linc, hinc, anti,
+                                 symmetric, estimate))
     return BAT(a), BAT(b)
 
 

@@ -155,6 +155,15 @@ ora_bat *ora_semijoin_cands(ora_bat *l, ora_bat *r, const ora_bat *sl, const ora
 			    bool max_one, bool only_misses, bool not_in);
 int ora_leftjoin(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r, const ora_bat *sl, const ora_bat *sr,
 		 bool nil_matches, bool outer, bool match_one);
+/* gdk_join.c:3699 thetajoin (mask: 1 EQ, 2 LT, 4 GT of vl op vr), :4626
+ * BATbandjoin (c1 / c2 of the columns' type) */
+int ora_thetajoin(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r, const ora_bat *sl, const ora_bat *sr,
+		  int mask, bool nil_matches);
+int ora_bandjoin(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r, const ora_bat *sl, const ora_bat *sr,
+		 const void *c1, const void *c2, bool linc, bool hinc);
+/* gdk_join.c:5422 BATrangejoin (rangejoin :5067) */
+int ora_rangejoin(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *rl, ora_bat *rh, const ora_bat *sl,
+		  const ora_bat *sr, bool linc, bool hinc, bool anti, bool symmetric);
 int ora_join(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r,
 	     const ora_bat *sl, const ora_bat *sr, bool nil_matches);
 int ora_join_algo(ora_bat *l, ora_bat *r, const ora_bat *sl, const ora_bat *sr);

@@ -36,6 +36,7 @@
  */
 #include "gdk_oracle.h"
 
+#include <float.h>
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -1176,5 +1177,363 @@ ora_leftjoin(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r, const ora_bat
 	y->nonil = !anynil;
 	*r1p = x;
 	*r2p = y;
+	return 0;
+}
+
+/* ---- BATthetajoin / BATbandjoin (gdk/gdk_join.c:3699-3889 thetajoin,
+ * :4626-5000 BATbandjoin): the nested loops as the reference runs them --
+ * left candidates in order, each one's matches in right-candidate order.
+ * theta compares with ATOMcompare (jv's images: nil the smallest, -0.0 ==
+ * +0.0); mask 1 EQ, 2 LT, 4 GT (vl op vr).  band: vr - c1 <= vl <= vr + c2
+ * in the reference's arithmetic per type (integers widened, flt in dbl, dbl
+ * with SUBF / ADDF_WITH_CHECK and their goto rules), nils never match. */
+
+static int
+pair_out(ora_bat **r1p, ora_bat **r2p, ora_oid *a, ora_oid *b, uint64_t n)
+{
+	ora_bat *x = ora_new(ORA_oid, n, 0), *y = ora_new(ORA_oid, n, 0);
+	memcpy(x->base, a, n * sizeof(ora_oid));
+	memcpy(y->base, b, n * sizeof(ora_oid));
+	x->sorted = 1;
+	x->nonil = y->nonil = 1;
+	*r1p = x;
+	*r2p = y;
+	return 0;
+}
+
+int
+ora_thetajoin(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r, const ora_bat *sl, const ora_bat *sr, int mask,
+	      bool nil_matches)
+{
+	if (atomtype(l->type) != atomtype(r->type)) {
+		ora_seterr("BATthetajoin: inputs not compatible.\n");
+		return -1;
+	}
+	ora_ci lci, rci;
+	if (ora_ci_init(&lci, l, sl) < 0 || ora_ci_init(&rci, r, sr) < 0)
+		return -1;
+	const bool lall = l->type == ORA_void && l->tseqbase == ORA_OID_NIL;
+	const bool rall = r->type == ORA_void && r->tseqbase == ORA_OID_NIL;
+	uint64_t cap = 1024, n = 0;
+	ora_oid *a = malloc(cap * sizeof(ora_oid)), *b = malloc(cap * sizeof(ora_oid));
+	if ((lall || rall) && !nil_matches)
+		goto done;     /* nomatch (:3738-3763) */
+	for (uint64_t i = 0; i < lci.n; i++) {
+		const ora_oid lo = ci_get(&lci, i);
+		const int64_t vl = jv(l, lo - l->hseqbase);
+		if (!nil_matches && lnil(l, vl))
+			continue;
+		for (uint64_t j = 0; j < rci.n; j++) {
+			const ora_oid ro = ci_get(&rci, j);
+			const int64_t vr = jv(r, ro - r->hseqbase);
+			if (!nil_matches && lnil(r, vr))
+				continue;
+			const int c = (vl > vr) - (vl < vr);
+			if (!((mask & 2 && c < 0) || (mask & 4 && c > 0) || (mask & 1 && c == 0)))
+				continue;
+			if (n == cap) {
+				cap *= 2;
+				a = realloc(a, cap * sizeof(ora_oid));
+				b = realloc(b, cap * sizeof(ora_oid));
+			}
+			a[n] = lo;
+			b[n++] = ro;
+		}
+	}
+done:
+	pair_out(r1p, r2p, a, b, n);
+	free(a);
+	free(b);
+	return 0;
+}
+
+static bool
+band_match(const ora_bat *l, const ora_bat *r, uint64_t pl, uint64_t pr, const void *c1p, const void *c2p,
+	   bool linc, bool hinc)
+{
+	switch (l->type) {
+	case ORA_flt: {
+		const float vl = ((const float *) l->base)[pl], vr = ((const float *) r->base)[pr];
+		const float c1 = *(const float *) c1p, c2 = *(const float *) c2p;
+		if (isnan(vr))
+			return false;
+		double v1 = (double) vr, v2 = v1;
+		v1 -= c1;
+		if (vl <= v1 && (!linc || vl != v1))
+			return false;
+		v2 += c2;
+		if (vl >= v2 && (!hinc || vl != v2))
+			return false;
+		return true;
+	}
+	case ORA_dbl: {
+		const double vl = ((const double *) l->base)[pl], vr = ((const double *) r->base)[pr];
+		const double c1 = *(const double *) c1p, c2 = *(const double *) c2p;
+		if (isnan(vr))
+			return false;
+		double v1, v2;
+		if (c1 < 1 ? DBL_MAX + c1 < vr : -DBL_MAX + c1 > vr) {
+			if (c1 < 0)
+				return false;
+		} else {
+			v1 = vr - c1;
+			if (vl <= v1 && (!linc || vl != v1))
+				return false;
+		}
+		if (c2 < 1 ? -DBL_MAX - c2 > vr : DBL_MAX - c2 < vr)
+			return !(c2 > 0);
+		v2 = vr + c2;
+		if (vl >= v2 && (!hinc || vl != v2))
+			return false;
+		return true;
+	}
+	default: {
+		const int64_t vl = jv(l, pl), vr = jv(r, pr);
+		if (vr == jnilv(r->type))
+			return false;
+		ora_hge c1, c2;
+		switch (l->type) {
+		case ORA_bte: c1 = *(const int8_t *) c1p; c2 = *(const int8_t *) c2p; break;
+		case ORA_sht: c1 = *(const int16_t *) c1p; c2 = *(const int16_t *) c2p; break;
+		case ORA_int: case ORA_date: c1 = *(const int32_t *) c1p; c2 = *(const int32_t *) c2p; break;
+		default: c1 = *(const int64_t *) c1p; c2 = *(const int64_t *) c2p; break;
+		}
+		const ora_hge v1 = (ora_hge) vr - c1, v2 = (ora_hge) vr + c2;
+		if (vl <= v1 && (!linc || vl != v1))
+			return false;
+		if (vl >= v2 && (!hinc || vl != v2))
+			return false;
+		return true;
+	}
+	}
+}
+
+int
+ora_bandjoin(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r, const ora_bat *sl, const ora_bat *sr,
+	     const void *c1p, const void *c2p, bool linc, bool hinc)
+{
+	if (atomtype(l->type) != atomtype(r->type)) {
+		ora_seterr("BATbandjoin: inputs not compatible.\n");
+		return -1;
+	}
+	ora_ci lci, rci;
+	if (ora_ci_init(&lci, l, sl) < 0 || ora_ci_init(&rci, r, sr) < 0)
+		return -1;
+	uint64_t cap = 1024, n = 0;
+	ora_oid *a = malloc(cap * sizeof(ora_oid)), *b = malloc(cap * sizeof(ora_oid));
+	bool empty;
+	switch (l->type) {
+#define BE(T, NILT) { const T c1 = *(const T *) c1p, c2 = *(const T *) c2p; \
+		empty = NILT || -c1 > c2 || ((!hinc || !linc) && -c1 == c2); }
+	case ORA_bte: BE(int8_t, (c1 == INT8_MIN || c2 == INT8_MIN)) break;
+	case ORA_sht: BE(int16_t, (c1 == INT16_MIN || c2 == INT16_MIN)) break;
+	case ORA_int: case ORA_date: BE(int32_t, (c1 == INT32_MIN || c2 == INT32_MIN)) break;
+	case ORA_lng: BE(int64_t, (c1 == INT64_MIN || c2 == INT64_MIN)) break;
+	case ORA_flt: BE(float, (isnan(c1) || isnan(c2))) break;
+	case ORA_dbl: BE(double, (isnan(c1) || isnan(c2))) break;
+#undef BE
+	default:
+		free(a);
+		free(b);
+		ora_seterr("unsupported type\n");
+		return -1;
+	}
+	if (lci.n == 0 || rci.n == 0 || empty)
+		goto done;
+	for (uint64_t i = 0; i < lci.n; i++) {
+		const ora_oid lo = ci_get(&lci, i);
+		const uint64_t pl = lo - l->hseqbase;
+		bool ln;
+		if (l->type == ORA_flt)
+			ln = isnan(((const float *) l->base)[pl]);
+		else if (l->type == ORA_dbl)
+			ln = isnan(((const double *) l->base)[pl]);
+		else
+			ln = jv(l, pl) == jnilv(l->type);
+		if (ln)
+			continue;
+		for (uint64_t j = 0; j < rci.n; j++) {
+			const ora_oid ro = ci_get(&rci, j);
+			if (!band_match(l, r, pl, ro - r->hseqbase, c1p, c2p, linc, hinc))
+				continue;
+			if (n == cap) {
+				cap *= 2;
+				a = realloc(a, cap * sizeof(ora_oid));
+				b = realloc(b, cap * sizeof(ora_oid));
+			}
+			a[n] = lo;
+			b[n++] = ro;
+		}
+	}
+done:
+	pair_out(r1p, r2p, a, b, n);
+	free(a);
+	free(b);
+	return 0;
+}
+
+/* ---- BATrangejoin (gdk/gdk_join.c:5422-5471, rangejoin :5067-5420) -----
+ * l within [rl, rh] per right candidate (linc / hinc: the ends included).
+ * Not anti, not symmetric and l sorted or reverse sorted (BATordered /
+ * BATordered_rev are computed first, :5071-5075): for each right candidate
+ * in order, the l positions of the range by binary search (SORTfndfirst /
+ * SORTfndlast), mapped to the left candidates in between -- right-major
+ * output.  Otherwise the nested loop: left-major, BETWEEN's three-valued
+ * logic (:5040-5064; a nil bound gives nil, which never matches, but its
+ * negation under anti is nil too).  An order index would take the first
+ * path through it; the oracle (like the device) keeps no order indexes.
+ * The result properties come from the reference's extra scan (:5351-5410),
+ * restated over the whole result (the scan only stops once nothing can
+ * change). */
+
+static uint64_t
+ci_lower(const ora_ci *ci, ora_oid o)
+{
+	if (ci->dense)
+		return o <= ci->seq ? 0 : (o - ci->seq < ci->n ? o - ci->seq : ci->n);
+	uint64_t a = 0, b = ci->n;
+	while (a < b) {
+		const uint64_t m = (a + b) / 2;
+		if (ci->oids[m] < o)
+			a = m + 1;
+		else
+			b = m;
+	}
+	return a;
+}
+
+/* first position of l (sorted: value >= v / > v; reverse sorted: <= v / < v) */
+static uint64_t
+sortfnd(const ora_bat *l, bool rev, int64_t v, bool last)
+{
+	uint64_t a = 0, b = l->count;
+	while (a < b) {
+		const uint64_t m = (a + b) / 2;
+		const int64_t x = jv(l, m);
+		const bool before = rev ? (last ? x >= v : x > v) : (last ? x <= v : x < v);
+		if (before)
+			a = m + 1;
+		else
+			b = m;
+	}
+	return a;
+}
+
+static int
+between3(int64_t v, bool vn, int64_t lo, bool lon, bool linc, int64_t hi, bool hin, bool hinc)
+{
+	/* 1 true, 0 false, -1 nil */
+	const int g = vn || lon ? -1 : (lo < v || (linc && v == lo));
+	const int l = vn || hin ? -1 : (v < hi || (hinc && v == hi));
+	if (g == 0 || l == 0)
+		return 0;
+	if (g < 0 || l < 0)
+		return -1;
+	return 1;
+}
+
+static void
+oid_props(ora_bat *b)
+{
+	const ora_oid *d = b->base;
+	bool eq = false, lt = false, gt = false, gap = false;
+	for (uint64_t i = 1; i < b->count; i++) {
+		if (d[i - 1] == d[i])
+			eq = true;
+		else if (d[i - 1] < d[i]) {
+			lt = true;
+			gap |= d[i - 1] + 1 != d[i];
+		} else
+			gt = true;
+	}
+	b->key = !eq && !gt;
+	b->sorted = !gt;
+	b->revsorted = !lt;
+	b->nil = false;
+	b->nonil = true;
+	b->tseqbase = !eq && !gt && !gap ? (b->count ? d[0] : 0) : ORA_OID_NIL;
+}
+
+int
+ora_rangejoin(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *rl, ora_bat *rh, const ora_bat *sl,
+	      const ora_bat *sr, bool linc, bool hinc, bool anti, bool symmetric)
+{
+	if (atomtype(l->type) != atomtype(rl->type) || atomtype(l->type) != atomtype(rh->type)) {
+		ora_seterr("BATrangejoin: inputs not compatible.\n");
+		return -1;
+	}
+	if (rl->count != rh->count || rl->hseqbase != rh->hseqbase) {
+		ora_seterr("BATrangejoin: right inputs not aligned.\n");
+		return -1;
+	}
+	ora_ci lci, rci;
+	if (ora_ci_init(&lci, l, sl) < 0 || ora_ci_init(&rci, rl, sr) < 0)
+		return -1;
+	const bool lnilall = l->type == ORA_void && l->tseqbase == ORA_OID_NIL;
+	const bool rlnil = rl->type == ORA_void && rl->tseqbase == ORA_OID_NIL;
+	const bool rhnil = rh->type == ORA_void && rh->tseqbase == ORA_OID_NIL;
+	uint64_t cap = 1024, n = 0;
+	ora_oid *a = malloc(cap * sizeof(ora_oid)), *b = malloc(cap * sizeof(ora_oid));
+	if (lci.n == 0 || rci.n == 0 || lnilall || (rlnil && rhnil) || ((rlnil || rhnil) && !anti))
+		goto done;
+	if (rlnil || rhnil) {
+		free(a);
+		free(b);
+		/* anti with a nil bound column: l > rh (or l < rl), gdk_join.c:5448-5460 */
+		return ora_thetajoin(r1p, r2p, l, rlnil ? rh : rl, sl, sr, rlnil ? 4 : 2, false);
+	}
+#define ADD(x, y) do { if (n == cap) { cap *= 2; a = realloc(a, cap * sizeof(ora_oid)); \
+			b = realloc(b, cap * sizeof(ora_oid)); } a[n] = (x); b[n++] = (y); } while (0)
+	if (!anti && !symmetric && (ordered(l) || ordered_rev(l))) {
+		const bool rev = !ordered(l);
+		for (uint64_t j = 0; j < rci.n; j++) {
+			const ora_oid ro = ci_get(&rci, j);
+			const int64_t vlo = jv(rl, ro - rl->hseqbase), vhi = jv(rh, ro - rh->hseqbase);
+			if (lnil(rl, vlo) || lnil(rh, vhi))
+				continue;
+			uint64_t low, high;
+			if (!rev) {
+				low = sortfnd(l, false, vlo, !linc);
+				high = sortfnd(l, false, vhi, hinc);
+			} else {
+				low = sortfnd(l, true, vhi, !hinc);
+				high = sortfnd(l, true, vlo, linc);
+			}
+			if (high <= low)
+				continue;
+			const uint64_t cl = ci_lower(&lci, low + l->hseqbase), ch = ci_lower(&lci, high + l->hseqbase);
+			for (uint64_t q = cl; q < ch; q++)
+				ADD(ci_get(&lci, q), ro);
+		}
+	} else {
+		for (uint64_t i = 0; i < lci.n; i++) {
+			const ora_oid lo = ci_get(&lci, i);
+			const int64_t v = jv(l, lo - l->hseqbase);
+			const bool vn = l->type != ORA_void && lnil(l, v);
+			if (vn)
+				continue;
+			for (uint64_t j = 0; j < rci.n; j++) {
+				const ora_oid ro = ci_get(&rci, j);
+				const int64_t vlo = jv(rl, ro - rl->hseqbase), vhi = jv(rh, ro - rh->hseqbase);
+				const bool ln = lnil(rl, vlo), hn = lnil(rh, vhi);
+				int m = between3(v, false, vlo, ln, linc, vhi, hn, hinc);
+				if (symmetric) {
+					const int m2 = between3(v, false, vhi, hn, hinc, vlo, ln, linc);
+					m = m == 1 || m2 == 1 ? 1 : (m < 0 || m2 < 0 ? -1 : 0);
+				}
+				if (anti)
+					m = m < 0 ? -1 : !m;
+				if (m == 1)
+					ADD(lo, ro);
+			}
+		}
+	}
+#undef ADD
+done:
+	pair_out(r1p, r2p, a, b, n);
+	free(a);
+	free(b);
+	oid_props(*r1p);
+	oid_props(*r2p);
 	return 0;
 }

@@ -114,6 +114,11 @@ def lib():
                                       C.c_bool]
         L.ora_groupquantile.restype = P
         L.ora_groupquantile.argtypes = [P, P, P, P, C.c_double, C.c_bool, C.c_bool]
+        L.ora_thetajoin.argtypes = [C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_int, C.c_bool]
+        L.ora_bandjoin.argtypes = [C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_void_p, C.c_void_p, C.c_bool,
+                                   C.c_bool]
+        L.ora_rangejoin.argtypes = [C.POINTER(P), C.POINTER(P), P, P, P, P, P, C.c_bool, C.c_bool, C.c_bool,
+                                    C.c_bool]
         L.ora_semijoin_cands.restype = P
         L.ora_semijoin_cands.argtypes = [P, P, P, P, C.c_bool, C.c_bool, C.c_bool, C.c_bool]
         L.ora_leftjoin.argtypes = [C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool, C.c_bool, C.c_bool]
@@ -457,6 +462,38 @@ def BATjoin(l, r, sl=None, sr=None, nil_matches=False):
     a, b = P(), P()
     if lib().ora_join(C.byref(a), C.byref(b), l.ptr, r.ptr, sl.ptr if sl else None,
                       sr.ptr if sr else None, nil_matches) < 0:
+        raise _err()
+    return Bat(a), Bat(b)
+
+
+_THETA_MASK = {-1: 2, -2: 3, 1: 4, 2: 5, -3: 6}
+
+
+def BATthetajoin(l, r, sl=None, sr=None, op=-1, nil_matches=False):
+    """gdk_join.c:4409 / thetajoin :3699 (op as JOIN_LT -1 ... JOIN_NE -3)"""
+    a, b = P(), P()
+    if lib().ora_thetajoin(C.byref(a), C.byref(b), l.ptr, r.ptr, sl.ptr if sl else None, sr.ptr if sr else None,
+                           _THETA_MASK[op], nil_matches) < 0:
+        raise _err()
+    return Bat(a), Bat(b)
+
+
+def BATbandjoin(l, r, c1, c2, sl=None, sr=None, linc=True, hinc=True):
+    """gdk_join.c:4626"""
+    ct = CT[l.s.type]
+    v1, v2 = ct(c1), ct(c2)
+    a, b = P(), P()
+    if lib().ora_bandjoin(C.byref(a), C.byref(b), l.ptr, r.ptr, sl.ptr if sl else None, sr.ptr if sr else None,
+                          C.cast(C.pointer(v1), C.c_void_p), C.cast(C.pointer(v2), C.c_void_p), linc, hinc) < 0:
+        raise _err()
+    return Bat(a), Bat(b)
+
+
+def BATrangejoin(l, rl, rh, sl=None, sr=None, linc=True, hinc=True, anti=False, symmetric=False):
+    """gdk_join.c:5422 / rangejoin :5067"""
+    a, b = P(), P()
+    if lib().ora_rangejoin(C.byref(a), C.byref(b), l.ptr, rl.ptr, rh.ptr, sl.ptr if sl else None,
+                           sr.ptr if sr else None, linc, hinc, anti, symmetric) < 0:
         raise _err()
     return Bat(a), Bat(b)
 

@@ -132,3 +132,24 @@ def test_group_prefix_then_all(gdk, ora, case):
     assert np.array_equal(g.to_numpy(), og.values())
     assert np.array_equal(e.to_numpy(), oe.values())
     assert np.array_equal(h.to_numpy(), oh.values())
+
+
+@pytest.mark.parametrize("glen", [20_000_000, 3_000_017, 40_000])
+def test_group_sums_long_runs(gdk, ora, glen):
+    """groups spanning thousands of tiles: the edge records combine over
+    several fold levels (k_gs_edges_fold) instead of one serial walk"""
+    n = 20_000_000
+    r = rng(glen)
+    k = (np.arange(n, dtype=np.int64) // glen) * 7 - 3
+    v = r.integers(-10**12, 10**12, n).astype(np.int64)
+    v[r.random(n) < 0.01] = np.iinfo(np.int64).min
+    kb = gdk.BAT.from_numpy(gdk.TYPE_lng, k)
+    kb.s.tsorted, kb.s.trevsorted = 1, int(glen >= n)
+    res = gdk.group_sums_ordered(kb, [gdk.BAT.from_numpy(gdk.TYPE_lng, v)])
+    assert res is not None
+    e, h, gk, sums = res
+    oe, oh, ogk, osums = _model(ora, ora.Bat.from_array(ora.TYPE_lng, k, sorted_=True),
+                                [ora.Bat.from_array(ora.TYPE_lng, v)])
+    assert np.array_equal(h.to_numpy(), oh.values())
+    assert np.array_equal(gk.to_numpy(), ogk.values())
+    assert sums[0].values() == list(osums[0].values())

@@ -14,6 +14,14 @@ sort)
 		MGDK_SORT_XCDG=$xg timeout -k 10 200 python tools/opbench.py --only other_ops > $O/opbench_xg$xg.json 2> $O/opbench_xg$xg.err
 	done
 	;;
+sortvar)
+	# sort tile variants (tools/variant_build.py): opbench other_ops per variant x XCD group
+	for v in $SORTVARS; do
+		for xg in ${XGS:-32 64 128}; do
+			MGDK_LIB=$PWD/tools/variants/libmgdk_$v.so MGDK_SORT_XCDG=$xg timeout -k 10 200 python tools/opbench.py --only other_ops > $O/opbench_${v}_xg$xg.json 2> $O/opbench_${v}_xg$xg.err
+		done
+	done
+	;;
 join)
 	timeout -k 10 600 $T tests/test_gpu_join_sort_window.py tests/test_join_algo.py tests/test_join_str.py tests/test_msk_cands.py -k "join" > $O/tests.log 2>&1
 	for v in 0 1; do
@@ -31,7 +39,7 @@ gsums)
 	timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_w -o run -- python3 tools/opbench.py --only config4_group_sums > $O/pmc_w.log 2>&1
 	;;
 jk)
-	timeout -k 10 600 $T tests/test_join_kinds.py tests/test_cand_algebra.py > $O/tests.log 2>&1
+	timeout -k 10 600 $T tests/test_join_kinds.py tests/test_cand_algebra.py tests/test_theta_join.py > $O/tests.log 2>&1
 	;;
 stats)
 	timeout -k 10 600 $T tests/test_group_stats.py tests/test_window_stats.py tests/test_gpu_window_funcs.py > $O/tests.log 2>&1
