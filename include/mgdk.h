@@ -285,6 +285,13 @@ int mgdk_BATleftjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, m
 		     bool nil_matches, mgdk_BUN estimate);
 int mgdk_BATouterjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr,
 		      bool nil_matches, bool match_one, mgdk_BUN estimate);
+/* BATmarkjoin (gdk/gdk.h; gdk_join.c:4367, leftjoin with nil_on_miss): every
+ * left candidate once (r2p NULL: semi) or with its match (nil on a miss), and
+ * the mark column r3 (bit): TRUE on a match; on a miss nil when the left value
+ * is nil or a right candidate is nil, else FALSE; no right candidates: FALSE.
+ * With r2p, refused when a left candidate matches twice, as BATleftjoin */
+int mgdk_BATmarkjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat **r3p, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl,
+		     mgdk_bat *sr, mgdk_BUN estimate);
 /* BATthetajoin (gdk/gdk.h; gdk_join.c:4409, nested loop thetajoin :3699):
  * op JOIN_EQ 0 (= BATjoin), JOIN_LT -1, JOIN_LE -2, JOIN_GT 1, JOIN_GE 2,
  * JOIN_NE -3 (gdk.h:2237-2243); the pairs in left-candidate order, each left

@@ -1,7 +1,7 @@
 // joinkinds.hip -- the left-output join family of gdk_join.c on the MI355X:
 // BATintersect / BATsemijoin's candidate output (semi), BATdiff (anti, with
 // SQL NOT IN semantics), BATleftjoin and BATouterjoin (gdk_join.c:4320-4407,
-// all through leftjoin :4049).
+// all through leftjoin :4049), and BATmarkjoin (:4367).
 //
 // What these return does not depend on which of leftjoin's algorithms runs
 // (selectjoin, mergejoin_void, fetchjoin, bitmaskjoin, mergejoin, hashjoin):
@@ -83,13 +83,17 @@ k_jk_gather(const oid *order, BUN n, const oid *ro, oid *dst)
 		dst[i] = ro[order[i]];
 }
 
-// mode 0 semi, 1 anti, 2 left, 3 outer; flags[i] = keep the candidate;
-// match[i] = its first match (nil: none); err |= 1: two matches, 2: a miss
+// mode 0 semi, 1 anti, 2 left, 3 outer, 4 mark; flags[i] = keep the
+// candidate; match[i] = its first match (nil: none); mark[i] (mode 4): TRUE on
+// a match, on a miss nil when the left value or a right candidate (*rnil) is
+// nil, else FALSE (gdk_join.c:3026-3076, :3127-3133); err |= 1: two matches,
+// 2: a miss, 4: a nil mark
 __global__ __launch_bounds__(256) void
 k_jk_probe(JSide l, const int64_t *rv, const oid *ro, BUN nr, bool nil_matches, bool not_in, int mode,
-	   int8_t *flags, oid *match, uint32_t *err)
+	   int8_t *flags, oid *match, int8_t *mark, const uint32_t *rnil, uint32_t *err)
 {
-	bool two = false, miss = false;
+	bool two = false, miss = false, mnil = false;
+	const bool rhasnil = mark && *rnil != 0;
 	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < l.n; i += (BUN) gridDim.x * blockDim.x) {
 		const oid lo = js_oid(l, i);
 		bool isnil;
@@ -122,8 +126,13 @@ k_jk_probe(JSide l, const int64_t *rv, const oid *ro, BUN nr, bool nil_matches, 
 		flags[i] = keep;
 		if (match)
 			match[i] = cnt ? ro[at] : MGDK_OID_NIL;
+		if (mark) {
+			const int8_t m = cnt ? 1 : (isnil || rhasnil) ? INT8_MIN : 0;
+			mark[i] = m;
+			mnil |= m == INT8_MIN;
+		}
 	}
-	const uint32_t f = (__any(two) ? 1u : 0u) | (__any(miss) ? 2u : 0u);
+	const uint32_t f = (__any(two) ? 1u : 0u) | (__any(miss) ? 2u : 0u) | (__any(mnil) ? 4u : 0u);
 	if (f && __lane_id() == 0)
 		atomicOr(err, f);
 }
@@ -192,14 +201,29 @@ jside(const char *fn, mgdk_bat *b, mgdk_bat *s, JSide *j, Held &held, mgdk_bat *
 	return 0;
 }
 
-// the shared plan; mode as k_jk_probe.  r1 (and r2) out
+// a result column released to the caller or, on an error return, freed
+struct Own {
+	mgdk_bat *b = nullptr;
+	~Own() { mgdk_BBPunfix(b); }
+	mgdk_bat *release()
+	{
+		mgdk_bat *x = b;
+		b = nullptr;
+		return x;
+	}
+};
+
+// the shared plan; mode as k_jk_probe.  r1 (and r2, and for mode 4 the
+// mark column r3) out
 int
 jk_run(const char *fn, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, bool nil_matches, bool not_in,
-       bool max_one, int mode, mgdk_bat **r1p, mgdk_bat **r2p)
+       bool max_one, int mode, mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat **r3p = nullptr)
 {
 	*r1p = nullptr;
 	if (r2p)
 		*r2p = nullptr;
+	if (r3p)
+		*r3p = nullptr;
 	if (l == nullptr || r == nullptr) {
 		seterr("%s: inputs must not be NULL", fn);
 		return -1;
@@ -219,12 +243,19 @@ jk_run(const char *fn, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, boo
 	}
 	ProfScope prof("joinkinds");
 	hipStream_t st = stream();
-	const bool want_r2 = mode >= 2;
-	// nomatch (gdk_join.c:301-360): semi / left -> empty; anti / outer -> every
-	// left candidate (outer: with nil matches)
+	const bool want_r2 = mode == 4 ? r2p != nullptr : mode >= 2;
+	Own mk;
+	// nomatch (gdk_join.c:301-360): semi / left -> empty; anti / outer / mark
+	// -> every left candidate (outer, mark: with nil matches; mark: FALSE,
+	// leftjoin :4144 passes defmark 0)
 	if (L.n == 0 || R.n == 0) {
-		const bool all = mode == 1 || mode == 3;
+		const bool all = mode == 1 || mode >= 3;
 		const BUN n = all ? L.n : 0;
+		if (mode == 4) {
+			const int8_t f = 0;
+			if ((mk.b = mgdk_BATconstant(0, MGDK_bit, &f, n)) == nullptr)
+				return -1;
+		}
 		if (mode <= 1 && L.dense) {
 			*r1p = mgdk_BATdense(0, n ? L.seq : 0, n);
 			return *r1p ? 0 : -1;
@@ -271,8 +302,12 @@ jk_run(const char *fn, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, boo
 			*r2p = b;
 		else
 			mgdk_BBPunfix(b);
+		if (r3p)
+			*r3p = mk.release();
 		return 0;
 	}
+	if (mode == 4 && (mk.b = newbat(0, MGDK_bit, L.n)) == nullptr)
+		return -1;
 	// the dense-right path (mergejoin_void) has no not_in
 	const bool rtdense = rb->ttype == MGDK_void ? rb->tseqbase != MGDK_OID_NIL
 						    : (rb->ttype == MGDK_oid && rb->tseqbase != MGDK_OID_NIL);
@@ -311,7 +346,8 @@ jk_run(const char *fn, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, boo
 		return -1;
 	}
 	hipLaunchKernelGGL(k_jk_probe, dim3(grid_for(L.n, 256 * 8, 8192)), dim3(256), 0, st, L, rvs, so.as<oid>(), R.n,
-			   nil_matches, not_in, mode, fl.as<int8_t>(), want_r2 ? mt.as<oid>() : (oid *) nullptr, meta + 1);
+			   nil_matches, not_in, mode, fl.as<int8_t>(), want_r2 ? mt.as<oid>() : (oid *) nullptr,
+			   mk.b ? (int8_t *) mk.b->theap : (int8_t *) nullptr, (const uint32_t *) meta, meta + 1);
 	if (!hip_ok(hipMemcpyAsync(h, meta, 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
 		return -1;
 	// copies: compact_flags below reuses the pinned buffer
@@ -320,7 +356,7 @@ jk_run(const char *fn, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, boo
 		seterr("more than one match");
 		return -1;
 	}
-	if ((perr & 1) && mode >= 2) {
+	if ((perr & 1) && mode >= 2 && want_r2) {
 		seterr("%s: a left row with several matches is not on the device path", fn);
 		return -1;
 	}
@@ -376,11 +412,24 @@ jk_run(const char *fn, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, boo
 		*r1p = cand_finish(a, n);
 		return *r1p ? 0 : -1;
 	}
+	if (mode == 4) {
+		// every left candidate is kept: the marks are in candidate order
+		mk.b->count = n;
+		mk.b->tnil = (perr & 4) != 0;
+		mk.b->tnonil = !mk.b->tnil;
+		mk.b->tsorted = mk.b->trevsorted = n <= 1;
+		mk.b->tkey = n <= 1;
+		*r3p = mk.release();
+	}
+	if (!want_r2) {
+		*r1p = a;
+		return 0;
+	}
 	b->count = n;
 	b->tsorted = b->trevsorted = n <= 1;
 	b->tkey = n <= 1;
 	// an outer join's miss leaves a nil match (k_jk_probe: meta bit 2)
-	const bool anynil = mode == 3 && (perr & 2) != 0;
+	const bool anynil = mode >= 3 && (perr & 2) != 0;
 	b->tnil = anynil;
 	b->tnonil = !anynil;
 	*r1p = a;
@@ -1063,6 +1112,21 @@ mgdk_BATouterjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk
 {
 	(void) estimate;
 	return jk_run("BATouterjoin", l, r, sl, sr, nil_matches, false, match_one, 3, r1p, r2p);
+}
+
+// BATmarkjoin (gdk_join.c:4367): leftjoin with nil_on_miss, semi when r2p is
+// NULL; a left candidate with two matches and r2p set is refused (see the
+// head of this file)
+extern "C" int
+mgdk_BATmarkjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat **r3p, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl,
+		 mgdk_bat *sr, mgdk_BUN estimate)
+{
+	(void) estimate;
+	if (r3p == nullptr) {
+		seterr("BATmarkjoin: the mark output must not be NULL");
+		return -1;
+	}
+	return jk_run("BATmarkjoin", l, r, sl, sr, false, false, false, 4, r1p, r2p, r3p);
 }
 
 // BATthetajoin (gdk_join.c:4409): op JOIN_EQ 0 (BATjoin), JOIN_LT -1,

@@ -157,6 +157,7 @@ _SIGS = {
     "mgdk_BATbandjoin": (C.c_int, [PP, PP, P, P, P, P, C.c_void_p, C.c_void_p, C.c_bool, C.c_bool, C.c_uint64]),
     "mgdk_BATrangejoin": (C.c_int, [PP, PP, P, P, P, P, P, C.c_bool, C.c_bool, C.c_bool, C.c_bool, C.c_uint64]),
     "mgdk_BATouterjoin": (C.c_int, [PP, PP, P, P, P, P, C.c_bool, C.c_bool, C.c_uint64]),
+    "mgdk_BATmarkjoin": (C.c_int, [PP, PP, PP, P, P, P, P, C.c_uint64]),
     "mgdk_BATordered": (C.c_bool, [P]),
     "mgdk_BATordered_rev": (C.c_bool, [P]),
     "mgdk_BATsort": (C.c_int, [PP, PP, PP, P, P, P, C.c_bool, C.c_bool, C.c_bool]),
@@ -810,6 +811,15 @@ def BATouterjoin(l, r, sl=None, sr=None, nil_matches=False, match_one=False, est
     _chk(lib().mgdk_BATouterjoin(C.byref(a), C.byref(b), l.ptr, r.ptr, _p(sl), _p(sr), nil_matches, match_one,
                                  estimate))
     return BAT(a), BAT(b)
+
+
+def BATmarkjoin(l, r, sl=None, sr=None, want_r2=True, estimate=0):
+    """gdk_join.c:4367: (r1, r2, r3) -- every left candidate, its match or
+    nil, the mark (TRUE / FALSE / nil); without r2 (semi) (r1, r3)."""
+    a, b, c = P(), P(), P()
+    _chk(lib().mgdk_BATmarkjoin(C.byref(a), C.byref(b) if want_r2 else None, C.byref(c), l.ptr, r.ptr, _p(sl), _p(sr),
+                                estimate))
+    return (BAT(a), BAT(b), BAT(c)) if want_r2 else (BAT(a), BAT(c))
 
 
 def BATordered(b):

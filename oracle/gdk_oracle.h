@@ -155,6 +155,9 @@ ora_bat *ora_semijoin_cands(ora_bat *l, ora_bat *r, const ora_bat *sl, const ora
 			    bool max_one, bool only_misses, bool not_in);
 int ora_leftjoin(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r, const ora_bat *sl, const ora_bat *sr,
 		 bool nil_matches, bool outer, bool match_one);
+/* gdk_join.c:4367 BATmarkjoin; r2p may be NULL (semi) */
+int ora_markjoin(ora_bat **r1p, ora_bat **r2p, ora_bat **r3p, ora_bat *l, ora_bat *r, const ora_bat *sl,
+		 const ora_bat *sr);
 /* gdk_join.c:3699 thetajoin (mask: 1 EQ, 2 LT, 4 GT of vl op vr), :4626
  * BATbandjoin (c1 / c2 of the columns' type) */
 int ora_thetajoin(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r, const ora_bat *sl, const ora_bat *sr,

@@ -1180,6 +1180,97 @@ ora_leftjoin(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r, const ora_bat
 	return 0;
 }
 
+/* BATmarkjoin (gdk_join.c:4367: leftjoin with nil_on_miss, semi when r2p is
+ * NULL): every left candidate once, its match (nil on a miss) and a mark:
+ * TRUE on a match; on a miss nil when the left value is nil (hashjoin
+ * :3127-3133, selectjoin :386-391, mergejoin_void :3100) or a right candidate
+ * is nil (defmark, hashjoin :3026-3076, selectjoin :513-527, mergejoin
+ * :2033-2036), else FALSE; no right candidates: FALSE everywhere (leftjoin
+ * :4144 nomatch with defmark 0).  With r2p, -2 when a left candidate matches
+ * twice (the order of several matches is the algorithm's). */
+int
+ora_markjoin(ora_bat **r1p, ora_bat **r2p, ora_bat **r3p, ora_bat *l, ora_bat *r, const ora_bat *sl,
+	     const ora_bat *sr)
+{
+	if (atomtype(l->type) != atomtype(r->type) || !join_type_ok(l->type) || l->type == ORA_flt ||
+	    l->type == ORA_dbl) {
+		ora_seterr("markjoin: type not restated");
+		return -1;
+	}
+	ora_ci lci, rci;
+	if (ora_ci_init(&lci, l, sl) < 0 || ora_ci_init(&rci, r, sr) < 0)
+		return -1;
+	ora_oid *a = malloc((lci.n + 1) * sizeof(ora_oid)), *b = malloc((lci.n + 1) * sizeof(ora_oid));
+	int8_t *m = malloc(lci.n + 1);
+	bool rnil = false;
+	vpair *p = rci.n ? rpairs(r, &rci, &rnil) : NULL;
+	if (a == NULL || b == NULL || m == NULL || (rci.n && p == NULL)) {
+		free(a);
+		free(b);
+		free(m);
+		free(p);
+		ora_seterr("malloc");
+		return -1;
+	}
+	bool anynil = false, mnil = false;
+	for (uint64_t i = 0; i < lci.n; i++) {
+		const ora_oid lo = ci_get(&lci, i);
+		const int64_t v = jv(l, lo - l->hseqbase);
+		uint64_t cnt = 0, at = 0;
+		int8_t mk = 0;
+		if (rci.n) {
+			if (lnil(l, v)) {
+				mk = INT8_MIN;
+			} else {
+				at = vlower(p, rci.n, v);
+				uint64_t e = at;
+				while (e < rci.n && p[e].v == v)
+					e++;
+				cnt = e - at;
+				mk = cnt ? 1 : rnil ? INT8_MIN : 0;
+			}
+		}
+		if (cnt > 1 && r2p) {
+			free(a);
+			free(b);
+			free(m);
+			free(p);
+			return -2;
+		}
+		a[i] = lo;
+		b[i] = cnt ? p[at].o : ORA_OID_NIL;
+		m[i] = mk;
+		anynil |= cnt == 0;
+		mnil |= mk == INT8_MIN;
+	}
+	free(p);
+	const uint64_t n = lci.n;
+	ora_bat *x = oidbat(a, n), *y = r2p ? oidbat(b, n) : NULL, *z = ora_new(ORA_bit, n, 0);
+	free(a);
+	free(b);
+	if (x == NULL || (r2p && y == NULL) || z == NULL) {
+		free(m);
+		ora_free(x);
+		ora_free(y);
+		ora_free(z);
+		return -1;
+	}
+	memcpy(z->base, m, n);
+	free(m);
+	z->nil = mnil;
+	z->nonil = !mnil;
+	x->sorted = x->key = 1;
+	x->revsorted = n <= 1;
+	*r1p = x;
+	if (r2p) {
+		y->nil = anynil;
+		y->nonil = !anynil;
+		*r2p = y;
+	}
+	*r3p = z;
+	return 0;
+}
+
 /* ---- BATthetajoin / BATbandjoin (gdk/gdk_join.c:3699-3889 thetajoin,
  * :4626-5000 BATbandjoin): the nested loops as the reference runs them --
  * left candidates in order, each one's matches in right-candidate order.

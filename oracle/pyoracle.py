@@ -122,6 +122,7 @@ def lib():
         L.ora_semijoin_cands.restype = P
         L.ora_semijoin_cands.argtypes = [P, P, P, P, C.c_bool, C.c_bool, C.c_bool, C.c_bool]
         L.ora_leftjoin.argtypes = [C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool, C.c_bool, C.c_bool]
+        L.ora_markjoin.argtypes = [C.POINTER(P), C.POINTER(P), C.POINTER(P), P, P, P, P]
         L.ora_join_algo.argtypes = [P, P, P, P]
         L.ora_BATsort.argtypes = [C.POINTER(P), C.POINTER(P), C.POINTER(P), P, P, P, C.c_bool, C.c_bool,
                                   C.c_bool]
@@ -464,6 +465,19 @@ def BATjoin(l, r, sl=None, sr=None, nil_matches=False):
                       sr.ptr if sr else None, nil_matches) < 0:
         raise _err()
     return Bat(a), Bat(b)
+
+
+def BATmarkjoin(l, r, sl=None, sr=None, want_r2=True):
+    """BATmarkjoin (gdk_join.c:4367): (r1, r2, r3) or, without r2 (semi),
+    (r1, r3); None when r2 is wanted and a left candidate matches twice"""
+    a, b, c = P(), P(), P()
+    rc = lib().ora_markjoin(C.byref(a), C.byref(b) if want_r2 else None, C.byref(c), l.ptr, r.ptr,
+                            sl.ptr if sl else None, sr.ptr if sr else None)
+    if rc == -2:
+        return None
+    if rc < 0:
+        raise _err()
+    return (Bat(a), Bat(b), Bat(c)) if want_r2 else (Bat(a), Bat(c))
 
 
 _THETA_MASK = {-1: 2, -2: 3, 1: 4, 2: 5, -3: 6}

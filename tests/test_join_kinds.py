@@ -180,3 +180,79 @@ def test_gpu_not_in_dense_right(gdk, ora):
     got = gdk.BATdiff(L, gdk.BAT.dense(seq, n), None, None, False, True).to_numpy()
     want = ora.BATdiff(ora.Bat.from_array(ora.TYPE_oid, lv), ora.Bat.dense(seq, n), None, None, False, True)
     assert np.array_equal(got.astype(np.uint64), np.asarray(want.values(), np.uint64))
+
+
+def _mark_model(lv, rv, lc, rc, nilv):
+    """BATmarkjoin's mark per left candidate -- SQL's three-valued IN: TRUE on
+    a match; else nil when the left value or a right candidate is nil; FALSE;
+    no right candidates at all: FALSE (gdk_join.c:4144, nomatch defmark 0)"""
+    m = _model(lv, rv, lc, rc, False, nilv)
+    if len(rc) == 0:
+        return [0] * len(m)
+    rnil = any(rv[o] == nilv for o in rc)
+    return [1 if ms else (-128 if (lv[o] == nilv or rnil) else 0) for o, ms in m]
+
+
+@pytest.mark.parametrize("name,tname,lv,rv,kw", list(_shapes()))
+def test_oracle_markjoin_model(ora, name, tname, lv, rv, kw):
+    r = rng(1305)
+    tp = getattr(ora, "TYPE_" + tname)
+    nilv = {"int": NI, "lng": NL, "sht": -(1 << 15)}[tname]
+    lcs = _cands(r, len(lv), "oids") if kw.get("cands") else None
+    rcs = _cands(r, len(rv), "dense") if kw.get("cands") else None
+    L, R = ora.Bat.from_array(tp, lv), ora.Bat.from_array(tp, rv)
+    lc, rc = _oids(lcs, len(lv)), _oids(rcs, len(rv))
+    m = _model(lv, rv, lc, rc, False, nilv)
+    marks = _mark_model(lv, rv, lc, rc, nilv)
+    a, c = ora.BATmarkjoin(L, R, _ora_c(ora, lcs), _ora_c(ora, rcs), want_r2=False)
+    assert [int(x) for x in a.values()] == [int(o) for o in lc]
+    assert [int(x) for x in c.values()] == marks
+    assert bool(c.s.nil) == (-128 in marks)
+    res = ora.BATmarkjoin(L, R, _ora_c(ora, lcs), _ora_c(ora, rcs))
+    if any(len(ms) > 1 for _, ms in m):
+        assert res is None
+    else:
+        a, b, c = res
+        assert [int(x) for x in b.values()] == [ms[0] if ms else ONIL for _, ms in m]
+        assert [int(x) for x in c.values()] == marks
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,tname,lv,rv,kw", list(_shapes()))
+@pytest.mark.parametrize("cform", ["plain", "except"])
+def test_gpu_markjoin(gdk, ora, name, tname, lv, rv, kw, cform):
+    r = rng(1306)
+    tg, to = getattr(gdk, "TYPE_" + tname), getattr(ora, "TYPE_" + tname)
+    lcs = _cands(r, len(lv), "oids") if kw.get("cands") else None
+    rcs = _cands(r, len(rv), "dense") if kw.get("cands") else None
+    mk = lambda v: gdk.BAT.from_numpy(tg, v, sorted_=False, revsorted=False, key=False)   # noqa: E731
+    L, R = mk(lv), mk(rv)
+    OL, OR = ora.Bat.from_array(to, lv), ora.Bat.from_array(to, rv)
+    gl, gr, ol, orr = _gdk_c(gdk, lcs, cform), _gdk_c(gdk, rcs, cform), _ora_c(ora, lcs), _ora_c(ora, rcs)
+
+    def eq(g, o, dt=np.uint64):
+        return np.array_equal(g.to_numpy().astype(dt), np.asarray(o.values()).astype(dt))
+
+    a, c = gdk.BATmarkjoin(L, R, gl, gr, want_r2=False)
+    wa, wc = ora.BATmarkjoin(OL, OR, ol, orr, want_r2=False)
+    assert eq(a, wa) and eq(c, wc, np.int8)
+    assert bool(c.tnil) == bool(wc.s.nil)
+    res = ora.BATmarkjoin(OL, OR, ol, orr)
+    if res is None:
+        with pytest.raises(gdk.GDKError, match="not on the device path"):
+            gdk.BATmarkjoin(L, R, gl, gr)
+    else:
+        a, b, c = gdk.BATmarkjoin(L, R, gl, gr)
+        assert eq(a, res[0]) and eq(b, res[1]) and eq(c, res[2], np.int8)
+
+
+@pytest.mark.gpu
+def test_gpu_markjoin_dense_right(gdk, ora):
+    """oid keys against a dense right side (mergejoin_void): nil left values
+    give a nil mark, the rest TRUE / FALSE"""
+    lv, (seq, n) = _dense_right_shape()
+    L = gdk.BAT.from_numpy(gdk.TYPE_oid, lv, sorted_=False, revsorted=False, key=False)
+    a, b, c = gdk.BATmarkjoin(L, gdk.BAT.dense(seq, n))
+    wa, wb, wc = ora.BATmarkjoin(ora.Bat.from_array(ora.TYPE_oid, lv), ora.Bat.dense(seq, n))
+    assert np.array_equal(b.to_numpy().astype(np.uint64), np.asarray(wb.values(), np.uint64))
+    assert np.array_equal(c.to_numpy().astype(np.int8), np.asarray(wc.values()).astype(np.int8))
