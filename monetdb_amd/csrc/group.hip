@@ -437,11 +437,29 @@ gl_lookup(const unsigned long long *lkey, const uint32_t *lmap, uint64_t k)
 	}
 }
 
+// The assign kernels are queued right behind the order pass, before the host
+// knows the group count: they read it (gm[1]) and the first pass's overflow
+// flag (gm[0]) themselves, return at once when the table overflowed (the
+// host then takes the global path), write the 1-byte image only for <= 255
+// groups and copy the first / last extent for the host's virtualisation test
+// -- one host round trip per BATgroup instead of two
+#define GL_ASSIGN_PROLOGUE \
+	const uint32_t ngrp = gm[1]; \
+	if (gm[0] != 0 || ngrp > GL_MAXG) \
+		return; \
+	if (ngrp > 255) \
+		img = nullptr; \
+	if (blockIdx.x == 0 && threadIdx.x == 0 && ngrp > 0) { \
+		flo[0] = ext[0]; \
+		flo[1] = ext[ngrp - 1]; \
+	}
+
 template <int W, int G>
 __global__ __launch_bounds__(1024) void
-k_gl_assign(KeySrc s, BUN n, const unsigned long long *gkey, const uint32_t *gmap, uint32_t ngrp, oid *gid,
-	    uint8_t *img, unsigned long long *histo, uint32_t *unsorted, uint32_t *miss)
+k_gl_assign(KeySrc s, BUN n, const unsigned long long *gkey, const uint32_t *gmap, const uint32_t *gm, oid *gid,
+	    uint8_t *img, unsigned long long *histo, uint32_t *unsorted, uint32_t *miss, const oid *ext, oid *flo)
 {
+	GL_ASSIGN_PROLOGUE;
 	__shared__ unsigned long long lkey[GL_SLOTS];
 	__shared__ uint32_t lmap[GL_SLOTS + 1];
 	__shared__ uint32_t lh[GL_MAXG];
@@ -509,9 +527,10 @@ k_gl_assign(KeySrc s, BUN n, const unsigned long long *gkey, const uint32_t *gma
 // before it (the lane's previous row, or the key before the lane's first)
 template <int W>
 __global__ __launch_bounds__(1024) void
-k_gl_assign_v(KeySrc s, BUN n, const unsigned long long *gkey, const uint32_t *gmap, uint32_t ngrp, oid *gid,
-	      uint8_t *img, unsigned long long *histo, uint32_t *unsorted, uint32_t *miss)
+k_gl_assign_v(KeySrc s, BUN n, const unsigned long long *gkey, const uint32_t *gmap, const uint32_t *gm, oid *gid,
+	      uint8_t *img, unsigned long long *histo, uint32_t *unsorted, uint32_t *miss, const oid *ext, oid *flo)
 {
+	GL_ASSIGN_PROLOGUE;
 	typedef typename std::conditional<W == 4, uint32_t, uint64_t>::type K;
 	constexpr int V = 16 / W;
 	__shared__ unsigned long long lkey[GL_SLOTS];
@@ -613,9 +632,10 @@ gl_hash32(uint32_t k)
 }
 
 __global__ __launch_bounds__(1024) void
-k_gl_assign_v32(KeySrc s, BUN n, const unsigned long long *gkey, const uint32_t *gmap, uint32_t ngrp, oid *gid,
-		uint8_t *img, unsigned long long *histo, uint32_t *unsorted, uint32_t *miss)
+k_gl_assign_v32(KeySrc s, BUN n, const unsigned long long *gkey, const uint32_t *gmap, const uint32_t *gm, oid *gid,
+		uint8_t *img, unsigned long long *histo, uint32_t *unsorted, uint32_t *miss, const oid *ext, oid *flo)
 {
+	GL_ASSIGN_PROLOGUE;
 	static_assert(GL_SLOTS == 4096, "12-bit hash");
 	constexpr int V = 4;
 	__shared__ unsigned long long tab[GL_SLOTS];
@@ -739,10 +759,10 @@ int
 group_lds(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mgdk_bat **enp, mgdk_bat **hnp)
 {
 	hipStream_t st = stream();
-	DevBuf gkey((GL_SLOTS + 1) * 8), gmin((GL_SLOTS + 1) * 8), gmap((GL_SLOTS + 1) * 4), ext((GL_SLOTS + 1) * 8);
+	DevBuf gkey((GL_SLOTS + 1) * 8), gmin((GL_SLOTS + 1) * 8), gmap((GL_SLOTS + 1) * 4), ext((GL_SLOTS + 1) * 8), fl(16);
 	uint32_t *m = (uint32_t *) meta_buf();
-	uint32_t *h = (uint32_t *) pinned(16);
-	if (!gkey.p || !gmin.p || !gmap.p || !ext.p)
+	uint32_t *h = (uint32_t *) pinned(64);
+	if (!gkey.p || !gmin.p || !gmap.p || !ext.p || !fl.p || m == nullptr || h == nullptr)
 		return -1;
 	if (!hip_ok(hipMemsetAsync(gkey.p, 0xff, (GL_SLOTS + 1) * 8, st), "memset") ||
 	    !hip_ok(hipMemsetAsync(gmin.p, 0xff, (GL_SLOTS + 1) * 8, st), "memset") ||
@@ -782,57 +802,62 @@ group_lds(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mg
 		done = upto;
 		hipLaunchKernelGGL(k_gl_order, dim3(GL_ORDER_WG), dim3(256), 0, st, gmin.as<unsigned long long>(), gmap.as<uint32_t>(),
 				   ci.dense, ci.seq, ci.oids, ext.as<oid>(), &m[1]);
-		if (!hip_ok(hipMemcpyAsync(h, m, 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
-			return -1;
-		if (h[0] || h[1] > GL_MAXG)
-			return 1;
-		const uint32_t ngrp = h[1];
-		mgdk_bat *en = newbat(0, MGDK_oid, ngrp), *hn = newbat(0, MGDK_lng, ngrp), *gn = newbat(hseqb, MGDK_oid, n);
+		// group count not known yet: ids, extents and histogram sized for
+		// the largest count this path takes
+		mgdk_bat *en = newbat(0, MGDK_oid, GL_MAXG), *hn = newbat(0, MGDK_lng, GL_MAXG + 1), *gn = newbat(hseqb, MGDK_oid, n);
 		auto unfix3 = [&]() {
 			mgdk_BBPunfix(en);
 			mgdk_BBPunfix(hn);
 			mgdk_BBPunfix(gn);
 		};
-		if (!en || !hn || !gn || !hip_ok(hipMemsetAsync(hn->theap, 0, ngrp * 8 + 8, st), "memset") ||
+		if (!en || !hn || !gn || !hip_ok(hipMemsetAsync(hn->theap, 0, GL_MAXG * 8 + 8, st), "memset") ||
 		    !hip_ok(hipMemsetAsync(&m[2], 0, 8, st), "memset") ||
-		    !hip_ok(hipMemcpyAsync(en->theap, ext.p, ngrp * 8, hipMemcpyDeviceToDevice, st), "memcpy")) {
+		    !hip_ok(hipMemcpyAsync(en->theap, ext.p, GL_MAXG * 8, hipMemcpyDeviceToDevice, st), "memcpy")) {
 			unfix3();
 			return -1;
 		}
-		uint8_t *img = nullptr;
 		gn->count = n;
-		if (ngrp <= 255 && (img = img8_new(gn)) == nullptr) {
+		uint8_t *img = img8_new(gn);   // dropped below unless <= 255 groups
+		if (img == nullptr) {
 			unfix3();
 			return -1;
 		}
 		// the vector form needs 16-byte aligned keys and ids
 		const bool vec = fg == 0 && (fw == 4 || fw == 8) && (((uintptr_t) ks.base + ks.off * fw) & 15) == 0 &&
-				 ((uintptr_t) gn->theap & 15) == 0 && (!img || ((uintptr_t) img & 3) == 0);
+				 ((uintptr_t) gn->theap & 15) == 0 && ((uintptr_t) img & 3) == 0;
 		static const bool v32 = getenv("MGDK_GROUP_V32") ? atoi(getenv("MGDK_GROUP_V32")) != 0 : true;
+		const oid *extp = ext.as<oid>();
+		oid *flo = fl.as<oid>();
 		if (vec && fw == 4 && v32)
 			hipLaunchKernelGGL(k_gl_assign_v32, dim3(tiles), dim3(1024), 0, st, ks, n, gkey.as<unsigned long long>(),
-					   gmap.as<uint32_t>(), ngrp, (oid *) gn->theap, img, (unsigned long long *) hn->theap,
-					   &m[2], &m[3]);
+					   gmap.as<uint32_t>(), (const uint32_t *) m, (oid *) gn->theap, img,
+					   (unsigned long long *) hn->theap, &m[2], &m[3], extp, flo);
 		else if (vec && fw == 4)
 			hipLaunchKernelGGL(k_gl_assign_v<4>, dim3(tiles), dim3(1024), 0, st, ks, n, gkey.as<unsigned long long>(),
-					   gmap.as<uint32_t>(), ngrp, (oid *) gn->theap, img, (unsigned long long *) hn->theap,
-					   &m[2], &m[3]);
+					   gmap.as<uint32_t>(), (const uint32_t *) m, (oid *) gn->theap, img,
+					   (unsigned long long *) hn->theap, &m[2], &m[3], extp, flo);
 		else if (vec)
 			hipLaunchKernelGGL(k_gl_assign_v<8>, dim3(tiles), dim3(1024), 0, st, ks, n, gkey.as<unsigned long long>(),
-					   gmap.as<uint32_t>(), ngrp, (oid *) gn->theap, img, (unsigned long long *) hn->theap,
-					   &m[2], &m[3]);
+					   gmap.as<uint32_t>(), (const uint32_t *) m, (oid *) gn->theap, img,
+					   (unsigned long long *) hn->theap, &m[2], &m[3], extp, flo);
 		else
 			GL_LAUNCH(k_gl_assign, dim3(tiles), dim3(1024), 0, st, ks, n, gkey.as<unsigned long long>(),
-				  gmap.as<uint32_t>(), ngrp, (oid *) gn->theap, img, (unsigned long long *) hn->theap, &m[2], &m[3]);
-		oid fl[2] = {0, 0};
+				  gmap.as<uint32_t>(), (const uint32_t *) m, (oid *) gn->theap, img,
+				  (unsigned long long *) hn->theap, &m[2], &m[3], extp, flo);
 		if (!hip_ok(hipMemcpyAsync(h, m, 16, hipMemcpyDeviceToHost, st), "memcpy") ||
-		    (ngrp > 0 && (!hip_ok(hipMemcpyAsync(&fl[0], ext.p, 8, hipMemcpyDeviceToHost, st), "memcpy") ||
-				  !hip_ok(hipMemcpyAsync(&fl[1], ext.as<oid>() + ngrp - 1, 8, hipMemcpyDeviceToHost, st),
-					  "memcpy"))) ||
-		    !sync()) {
+		    !hip_ok(hipMemcpyAsync(h + 4, flo, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
 			unfix3();
 			return -1;
 		}
+		if (h[0] || h[1] > GL_MAXG) {
+			unfix3();
+			return 1;
+		}
+		const uint32_t ngrp = h[1];
+		oid fl2[2];
+		memcpy(fl2, h + 4, 16);
+		if (ngrp > 255)
+			img8_drop(gn);
 		if (h[3]) {
 			// a key the prefix did not hold: read the remaining tiles too
 			unfix3();
@@ -857,9 +882,9 @@ group_lds(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mg
 		hn->tnonil = 1;
 		// tmaxpos: the row that started the last group (maxgrppos,
 		// gdk_group.c:99,1313)
-		gn->tmaxpos = ngrp > 0 ? cand_index(ci, fl[1]) : MGDK_BUN_NONE;
-		if (ngrp > 0 && fl[1] - fl[0] == ngrp - 1)
-			setdense(en, fl[0], ngrp);
+		gn->tmaxpos = ngrp > 0 ? cand_index(ci, fl2[1]) : MGDK_BUN_NONE;
+		if (ngrp > 0 && fl2[1] - fl2[0] == ngrp - 1)
+			setdense(en, fl2[0], ngrp);
 		*gnp = gn;
 		*enp = en;
 		*hnp = hn;

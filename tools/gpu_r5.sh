@@ -44,6 +44,17 @@ jk)
 stats)
 	timeout -k 10 600 $T tests/test_group_stats.py tests/test_window_stats.py tests/test_gpu_window_funcs.py > $O/tests.log 2>&1
 	;;
+grp)
+	timeout -k 10 600 $T tests/test_gpu_ops.py tests/test_gpu_group_sorted.py tests/test_gpu_group_str.py tests/test_gpu_props.py tests/test_msk_cands.py > $O/tests.log 2>&1
+	;;
+selgrp)
+	timeout -k 10 200 python tools/selgrp_trace.py > $O/plain.json 2> $O/plain.err
+	cd /tmp && cd $GRAFT_REPO_ROOT
+	timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/prof -o run -- python3 tools/selgrp_trace.py > $O/prof.log 2>&1
+	;;
+markjoin)
+	timeout -k 10 300 $T tests/test_join_kinds.py -k markjoin > $O/tests.log 2>&1
+	;;
 cand)
 	timeout -k 10 600 $T tests/test_cand_algebra.py tests/test_gpu_window_funcs.py > $O/tests.log 2>&1
 	;;
