@@ -667,73 +667,76 @@ k_gl_assign_v32(KeySrc s, BUN n, const unsigned long long *gkey, const uint32_t 
 			h = (h + 1) & (GL_SLOTS - 1);
 		}
 	};
-	const BUN a = (BUN) blockIdx.x * GL_TILE, e = min(n, a + GL_TILE);
 	const uint32_t *kb = (const uint32_t *) s.base + s.off;
 	uint32_t uns = 0;
 	bool mis = false;
 	typedef uint32_t kv __attribute__((ext_vector_type(V)));
 	constexpr BUN STEP = 1024 * V;
-	for (BUN r0 = a + (BUN) tid * V; r0 < e; r0 += STEP) {
-		uint32_t k[V];
-		if (r0 + V <= e) {
+	// a grid smaller than the tile count keeps its table for several tiles
+	for (BUN a = (BUN) blockIdx.x * GL_TILE; a < n; a += (BUN) gridDim.x * GL_TILE) {
+		const BUN e = min(n, a + GL_TILE);
+		for (BUN r0 = a + (BUN) tid * V; r0 < e; r0 += STEP) {
+			uint32_t k[V];
+			if (r0 + V <= e) {
 #if MGDK_GL_NT_LOAD
-			const kv x = __builtin_nontemporal_load((const kv *) (kb + r0));
+				const kv x = __builtin_nontemporal_load((const kv *) (kb + r0));
 #else
-			const kv x = *(const kv *) (kb + r0);
+				const kv x = *(const kv *) (kb + r0);
 #endif
 #pragma unroll
-			for (int u = 0; u < V; u++)
-				k[u] = x[u];
-		} else {
+				for (int u = 0; u < V; u++)
+					k[u] = x[u];
+			} else {
 #pragma unroll
-			for (int u = 0; u < V; u++)
-				k[u] = kb[r0 + u < e ? r0 + u : e - 1];
-		}
-		const uint32_t before = kb[r0 > 0 ? r0 - 1 : 0];
-		uint32_t g[V], gp = 0;
-#pragma unroll
-		for (int u = 0; u < V; u++) {
-			g[u] = look(k[u]);
-			if (g[u] == ~0u) {
-				mis = true;
-				g[u] = 0;
+				for (int u = 0; u < V; u++)
+					k[u] = kb[r0 + u < e ? r0 + u : e - 1];
 			}
-		}
-		if (r0 > 0)
-			gp = look(before);
-		mis |= gp == ~0u && r0 > 0;
+			const uint32_t before = kb[r0 > 0 ? r0 - 1 : 0];
+			uint32_t g[V], gp = 0;
 #pragma unroll
-		for (int u = 0; u < V; u++) {
-			const BUN i = r0 + u;
-			if (i < e) {
-				atomicAdd(&lh[g[u]], 1u);
-				const uint32_t prev = u == 0 ? gp : g[u - 1];
-				if (i > 0 && prev > g[u])
-					uns = 1;
-			}
-		}
-		if (r0 + V <= e) {
-			typedef unsigned long long o2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-			for (int u = 0; u < V; u += 2) {
-#if MGDK_GL_NT_STORE
-				__builtin_nontemporal_store((o2){g[u], g[u + 1]}, (o2 *) (gid + r0 + u));
-#else
-				*(o2 *) (gid + r0 + u) = (o2){g[u], g[u + 1]};
-#endif
-			}
-			if (img) {
-				const uint32_t w4 = g[0] | (g[1] << 8) | (g[2] << 16) | (g[3] << 24);
-				*(uint32_t *) (img + r0) = w4;
-			}
-		} else {
-#pragma unroll
-			for (int u = 0; u < V; u++)
-				if (r0 + u < e) {
-					gid[r0 + u] = g[u];
-					if (img)
-						img[r0 + u] = (uint8_t) g[u];
+			for (int u = 0; u < V; u++) {
+				g[u] = look(k[u]);
+				if (g[u] == ~0u) {
+					mis = true;
+					g[u] = 0;
 				}
+			}
+			if (r0 > 0)
+				gp = look(before);
+			mis |= gp == ~0u && r0 > 0;
+#pragma unroll
+			for (int u = 0; u < V; u++) {
+				const BUN i = r0 + u;
+				if (i < e) {
+					atomicAdd(&lh[g[u]], 1u);
+					const uint32_t prev = u == 0 ? gp : g[u - 1];
+					if (i > 0 && prev > g[u])
+						uns = 1;
+				}
+			}
+			if (r0 + V <= e) {
+				typedef unsigned long long o2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+				for (int u = 0; u < V; u += 2) {
+#if MGDK_GL_NT_STORE
+					__builtin_nontemporal_store((o2){g[u], g[u + 1]}, (o2 *) (gid + r0 + u));
+#else
+					*(o2 *) (gid + r0 + u) = (o2){g[u], g[u + 1]};
+#endif
+				}
+				if (img) {
+					const uint32_t w4 = g[0] | (g[1] << 8) | (g[2] << 16) | (g[3] << 24);
+					*(uint32_t *) (img + r0) = w4;
+				}
+			} else {
+#pragma unroll
+				for (int u = 0; u < V; u++)
+					if (r0 + u < e) {
+						gid[r0 + u] = g[u];
+						if (img)
+							img[r0 + u] = (uint8_t) g[u];
+					}
+			}
 		}
 	}
 	if (__any(uns) && __lane_id() == 0)
@@ -828,8 +831,11 @@ group_lds(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mg
 		static const bool v32 = getenv("MGDK_GROUP_V32") ? atoi(getenv("MGDK_GROUP_V32")) != 0 : true;
 		const oid *extp = ext.as<oid>();
 		oid *flo = fl.as<oid>();
+		// MGDK_GROUP_GRID: workgroups of the 4-byte assign pass (each keeps its
+		// LDS table over grid-strided tiles); 0 = one per tile
+		static const unsigned agrid = getenv("MGDK_GROUP_GRID") ? (unsigned) atoi(getenv("MGDK_GROUP_GRID")) : 0;
 		if (vec && fw == 4 && v32)
-			hipLaunchKernelGGL(k_gl_assign_v32, dim3(tiles), dim3(1024), 0, st, ks, n, gkey.as<unsigned long long>(),
+			hipLaunchKernelGGL(k_gl_assign_v32, dim3(agrid && agrid < tiles ? agrid : tiles), dim3(1024), 0, st, ks, n, gkey.as<unsigned long long>(),
 					   gmap.as<uint32_t>(), (const uint32_t *) m, (oid *) gn->theap, img,
 					   (unsigned long long *) hn->theap, &m[2], &m[3], extp, flo);
 		else if (vec && fw == 4)
