@@ -481,116 +481,120 @@ k_sel_write(SelArgs<T> a, const uint32_t *bits, const uint64_t *pre)
 	__shared__ uint32_t s_words[WPT];
 	__shared__ uint32_t s_wave[4];
 	const unsigned tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-	const uint32_t t = blockIdx.x;
-	const uint64_t slot0 = (uint64_t) t * WPT * 32;
-	const bool active = tid * WPL < WPT;
-	uint32_t w[WPL], cnt = 0;
-#pragma unroll
-	for (int q = 0; q < WPL; q++) {
-		w[q] = active ? bits[(uint64_t) t * WPT + tid * WPL + q] : 0u;
-		cnt += __popc(w[q]);
-	}
-	// workgroup exclusive scan of the per-lane counts
-	uint32_t x = cnt;
-#pragma unroll
-	for (int o = 1; o < 64; o <<= 1) {
-		const uint32_t y = __shfl_up(x, o);
-		if ((int) lane >= o)
-			x += y;
-	}
-	if (lane == 63)
-		s_wave[wave] = x;
-	__syncthreads();
-	uint32_t ex = x - cnt;
-	for (unsigned q = 0; q < wave; q++)
-		ex += s_wave[q];
-	const uint32_t hits = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
-	if (hits == 0)
-		return;
-	const uint64_t prefix = pre[t];
-	const oid base = a.cseq + slot0 - a.shift;
-	// first / last oid of the whole result (virtualisation test on the host)
-	if (cnt > 0 && (ex == 0 ? prefix == 0 : false)) {
-		int q = 0;
-		while (w[q] == 0)
-			q++;
-		a.meta[2] = base + ((uint64_t) (tid * WPL + q) * 32 + __ffs(w[q]) - 1);
-	}
-	if (cnt > 0 && ex + cnt == hits && prefix + hits == a.meta[0]) {
-		int q = WPL - 1;
-		while (w[q] == 0)
-			q--;
-		a.meta[3] = base + ((uint64_t) (tid * WPL + q) * 32 + 31 - __clz(w[q]));
-	}
-	if (hits < 1024) {
-		// sparse: the owning lane stores its hits
-		uint64_t pos = prefix + ex;
+	// a grid smaller than the tile count strides over the tiles (fewer,
+	// longer workgroups for sparse results)
+	for (uint32_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+		__syncthreads();   // the previous tile's s_wave / s_stage / s_words are consumed
+		const uint64_t slot0 = (uint64_t) t * WPT * 32;
+		const bool active = tid * WPL < WPT;
+		uint32_t w[WPL], cnt = 0;
 #pragma unroll
 		for (int q = 0; q < WPL; q++) {
-			uint32_t m = w[q];
-			while (m) {
-				const int b = __ffs(m) - 1;
-				m &= m - 1;
-				a.out[pos++] = base + ((uint64_t) (tid * WPL + q) * 32 + b);
-			}
+			w[q] = active ? bits[(uint64_t) t * WPT + tid * WPL + q] : 0u;
+			cnt += __popc(w[q]);
 		}
-		return;
-	}
-	if (hits <= (uint32_t) SCH) {
-		// all of the tile's hits fit the LDS stage: each lane places its
-		// own, then one contiguous store
-		uint32_t pos = ex;
-#pragma unroll
-		for (int q = 0; q < WPL; q++) {
-			uint32_t m = w[q];
-			while (m) {
-				const int b = __ffs(m) - 1;
-				m &= m - 1;
-				s_stage[pos++] = base + ((uint64_t) (tid * WPL + q) * 32 + b);
-			}
-		}
-		__syncthreads();
-		for (uint32_t i = tid; i < hits; i += 256)
-			a.out[prefix + i] = s_stage[i];
-		return;
-	}
-	// very dense: rounds of 4096 slots, lane i taking the 16 slots
-	// [16i, 16i+16) of the round; the round's hits are ranked by a workgroup
-	// scan, placed in LDS in order and stored as one run
-#pragma unroll
-	for (int q = 0; q < WPL; q++)
-		if (active)
-			s_words[tid * WPL + q] = w[q];
-	uint64_t obase = prefix;
-	for (int rd = 0; rd < WPT * 32 / SCH; rd++) {
-		__syncthreads();   // s_words written / previous round's s_wave, s_stage consumed
-		const uint32_t piece = (s_words[rd * (SCH / 32) + tid / 2] >> (16 * (tid & 1))) & 0xffffu;
-		const uint32_t pc = __popc(piece);
-		uint32_t y = pc;
+		// workgroup exclusive scan of the per-lane counts
+		uint32_t x = cnt;
 #pragma unroll
 		for (int o = 1; o < 64; o <<= 1) {
-			const uint32_t z = __shfl_up(y, o);
+			const uint32_t y = __shfl_up(x, o);
 			if ((int) lane >= o)
-				y += z;
+				x += y;
 		}
 		if (lane == 63)
-			s_wave[wave] = y;
+			s_wave[wave] = x;
 		__syncthreads();
-		uint32_t pos = y - pc;
+		uint32_t ex = x - cnt;
 		for (unsigned q = 0; q < wave; q++)
-			pos += s_wave[q];
-		const uint32_t rhits = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
-		uint32_t mm = piece;
-		const oid rb = base + (uint64_t) rd * SCH + tid * 16;
-		while (mm) {
-			const int bb = __ffs(mm) - 1;
-			mm &= mm - 1;
-			s_stage[pos++] = rb + bb;
+			ex += s_wave[q];
+		const uint32_t hits = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+		if (hits == 0)
+			continue;
+		const uint64_t prefix = pre[t];
+		const oid base = a.cseq + slot0 - a.shift;
+		// first / last oid of the whole result (virtualisation test on the host)
+		if (cnt > 0 && (ex == 0 ? prefix == 0 : false)) {
+			int q = 0;
+			while (w[q] == 0)
+				q++;
+			a.meta[2] = base + ((uint64_t) (tid * WPL + q) * 32 + __ffs(w[q]) - 1);
 		}
-		__syncthreads();
-		for (uint32_t i = tid; i < rhits; i += 256)
-			a.out[obase + i] = s_stage[i];
-		obase += rhits;
+		if (cnt > 0 && ex + cnt == hits && prefix + hits == a.meta[0]) {
+			int q = WPL - 1;
+			while (w[q] == 0)
+				q--;
+			a.meta[3] = base + ((uint64_t) (tid * WPL + q) * 32 + 31 - __clz(w[q]));
+		}
+		if (hits < 1024) {
+			// sparse: the owning lane stores its hits
+			uint64_t pos = prefix + ex;
+#pragma unroll
+			for (int q = 0; q < WPL; q++) {
+				uint32_t m = w[q];
+				while (m) {
+					const int b = __ffs(m) - 1;
+					m &= m - 1;
+					a.out[pos++] = base + ((uint64_t) (tid * WPL + q) * 32 + b);
+				}
+			}
+			continue;
+		}
+		if (hits <= (uint32_t) SCH) {
+			// all of the tile's hits fit the LDS stage: each lane places its
+			// own, then one contiguous store
+			uint32_t pos = ex;
+#pragma unroll
+			for (int q = 0; q < WPL; q++) {
+				uint32_t m = w[q];
+				while (m) {
+					const int b = __ffs(m) - 1;
+					m &= m - 1;
+					s_stage[pos++] = base + ((uint64_t) (tid * WPL + q) * 32 + b);
+				}
+			}
+			__syncthreads();
+			for (uint32_t i = tid; i < hits; i += 256)
+				a.out[prefix + i] = s_stage[i];
+			continue;
+		}
+		// very dense: rounds of 4096 slots, lane i taking the 16 slots
+		// [16i, 16i+16) of the round; the round's hits are ranked by a workgroup
+		// scan, placed in LDS in order and stored as one run
+#pragma unroll
+		for (int q = 0; q < WPL; q++)
+			if (active)
+				s_words[tid * WPL + q] = w[q];
+		uint64_t obase = prefix;
+		for (int rd = 0; rd < WPT * 32 / SCH; rd++) {
+			__syncthreads();   // s_words written / previous round's s_wave, s_stage consumed
+			const uint32_t piece = (s_words[rd * (SCH / 32) + tid / 2] >> (16 * (tid & 1))) & 0xffffu;
+			const uint32_t pc = __popc(piece);
+			uint32_t y = pc;
+#pragma unroll
+			for (int o = 1; o < 64; o <<= 1) {
+				const uint32_t z = __shfl_up(y, o);
+				if ((int) lane >= o)
+					y += z;
+			}
+			if (lane == 63)
+				s_wave[wave] = y;
+			__syncthreads();
+			uint32_t pos = y - pc;
+			for (unsigned q = 0; q < wave; q++)
+				pos += s_wave[q];
+			const uint32_t rhits = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+			uint32_t mm = piece;
+			const oid rb = base + (uint64_t) rd * SCH + tid * 16;
+			while (mm) {
+				const int bb = __ffs(mm) - 1;
+				mm &= mm - 1;
+				s_stage[pos++] = rb + bb;
+			}
+			__syncthreads();
+			for (uint32_t i = tid; i < rhits; i += 256)
+				a.out[obase + i] = s_stage[i];
+			obase += rhits;
+		}
 	}
 }
 
@@ -600,6 +604,14 @@ k_select_fin(const oid *out, uint64_t *meta)
 	uint64_t n = meta[0];
 	meta[2] = n ? out[0] : 0;
 	meta[3] = n ? out[n - 1] : 0;
+}
+
+// workgroups of k_sel_write: MGDK_SEL_WGRID (0 = one per tile)
+static unsigned
+sel_wgrid(uint64_t ntiles)
+{
+	static const unsigned g = getenv("MGDK_SEL_WGRID") ? (unsigned) atoi(getenv("MGDK_SEL_WGRID")) : 0;
+	return g && g < ntiles ? g : (unsigned) ntiles;
 }
 
 // ---- host-side normalisation -------------------------------------------------
@@ -761,7 +773,7 @@ run_scan(const mgdk_bat *b, const Cand &ci, const SelPred<T> &pred)
 	struct { void *p; } sb{sbh.h ? sbh.h->base : nullptr};
 	uint32_t *smap_bits = nullptr;
 	{
-		const dim3 g((unsigned) ntiles), blk(256);
+		const dim3 g((unsigned) ntiles), blk(256), gw(sel_wgrid(ntiles));
 		uint32_t *bits = nullptr, *counts = nullptr;
 		uint64_t *pre = nullptr;
 		if (streamed) {
@@ -776,7 +788,7 @@ run_scan(const mgdk_bat *b, const Cand &ci, const SelPred<T> &pred)
 		}
 #define SELS(MODE) do { hipLaunchKernelGGL((k_sel_count<T, MODE>), g, blk, 0, st, a, bits, counts); \
 			hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(1024), 0, st, counts, pre, (uint32_t) ntiles, a.meta); \
-			hipLaunchKernelGGL(k_sel_write<T>, g, blk, 0, st, a, bits, pre); } while (0)
+			hipLaunchKernelGGL(k_sel_write<T>, gw, blk, 0, st, a, bits, pre); } while (0)
 #define SELL(MAT, MODE) do { if (!(MAT) && MGDK_SEL_STREAM) SELS(MODE); \
 			     else hipLaunchKernelGGL((k_select<T, MAT, MODE>), g, blk, 0, st, a); } while (0)
 #define SELM(MAT) switch (pred.mode) { \
@@ -873,10 +885,10 @@ run_scan_bits(const mgdk_bat *b, const Cand &ci, const SelPred<T> &pred, const S
 	uint32_t *counts = (uint32_t *) (pre + ntiles);
 	uint32_t *bits = counts + ntiles + (ntiles & 1);
 	hipStream_t st = stream();
-	const dim3 g((unsigned) ntiles), blk(256);
+	const dim3 g((unsigned) ntiles), blk(256), gw(sel_wgrid(ntiles));
 #define SELC(MODE) do { hipLaunchKernelGGL((k_sel_count_c<T, MODE>), g, blk, 0, st, a, cm.bits, zero, bits, counts); \
 			hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(1024), 0, st, counts, pre, (uint32_t) ntiles, a.meta); \
-			hipLaunchKernelGGL(k_sel_write<T>, g, blk, 0, st, a, bits, pre); } while (0)
+			hipLaunchKernelGGL(k_sel_write<T>, gw, blk, 0, st, a, bits, pre); } while (0)
 	switch (pred.mode) {
 	case SEL_RANGE: SELC(SEL_RANGE); break;
 	case SEL_ANTI: SELC(SEL_ANTI); break;

@@ -50,7 +50,7 @@ grp)
 selgrp)
 	timeout -k 10 200 python tools/selgrp_trace.py > $O/plain.json 2> $O/plain.err
 	for gg in 256 512 1024; do
-		MGDK_GROUP_GRID=$gg timeout -k 10 200 python tools/selgrp_trace.py > $O/grid$gg.json 2> $O/grid$gg.err
+		MGDK_GROUP_GRID=$gg MGDK_SEL_WGRID=$((gg * 2)) timeout -k 10 200 python tools/selgrp_trace.py > $O/grid$gg.json 2> $O/grid$gg.err
 	done
 	cd /tmp && cd $GRAFT_REPO_ROOT
 	timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/prof -o run -- python3 tools/selgrp_trace.py > $O/prof.log 2>&1
