@@ -361,10 +361,29 @@ k_gl_first(KeySrc s, BUN n, BUN tile0, unsigned long long *gkey, unsigned long l
 // hold the same list) and ranks its share of the entries
 constexpr unsigned GL_ORDER_SPLIT = 4;
 constexpr unsigned GL_ORDER_WG = (GL_MAXG * GL_ORDER_SPLIT + 255) / 256;
+// the tables' and flags' initial state in ONE launch (three memsets cost
+// ~10 us of blit launches on a 0.4 ms call)
+__global__ __launch_bounds__(256) void
+k_gl_init(unsigned long long *gkey, unsigned long long *gmin, uint32_t *m)
+{
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i <= GL_SLOTS; i += gridDim.x * blockDim.x) {
+		gkey[i] = ~0ull;
+		gmin[i] = ~0ull;
+	}
+	if (blockIdx.x == 0 && threadIdx.x < 4)
+		m[threadIdx.x] = 0;
+}
+
+// also clears the histogram (GL_MAXG + 1 words) and the assign pass's two
+// flags m[2], m[3], which the assign pass that follows accumulates into
 __global__ __launch_bounds__(256) void
 k_gl_order(const unsigned long long *gmin, uint32_t *gmap, bool cdense, oid cseq, const oid *coids, oid *ext,
-	   uint32_t *ngrp)
+	   uint32_t *ngrp, unsigned long long *histo)
 {
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i <= GL_MAXG; i += gridDim.x * blockDim.x)
+		histo[i] = 0ull;
+	if (blockIdx.x == 0 && threadIdx.x < 2)
+		ngrp[1 + threadIdx.x] = 0;
 	__shared__ unsigned long long sk[GL_SLOTS + 1];
 	__shared__ uint32_t ws[4];
 	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
@@ -414,7 +433,8 @@ k_gl_order(const unsigned long long *gmin, uint32_t *gmap, bool cdense, oid cseq
 		if (sub == 0 && i0 < c) {
 			const uint32_t slot = (uint32_t) (v & 8191);
 			gmap[slot] = r;
-			ext[r] = cdense ? cseq + (BUN) (v >> 13) : coids[v >> 13];
+			if (r < GL_MAXG)     // more groups: the path does not apply
+				ext[r] = cdense ? cseq + (BUN) (v >> 13) : coids[v >> 13];
 		}
 	}
 	if (tid == 0 && blockIdx.x == 0)
@@ -762,15 +782,13 @@ int
 group_lds(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mgdk_bat **enp, mgdk_bat **hnp)
 {
 	hipStream_t st = stream();
-	DevBuf gkey((GL_SLOTS + 1) * 8), gmin((GL_SLOTS + 1) * 8), gmap((GL_SLOTS + 1) * 4), ext((GL_SLOTS + 1) * 8), fl(16);
+	DevBuf gkey((GL_SLOTS + 1) * 8), gmin((GL_SLOTS + 1) * 8), gmap((GL_SLOTS + 1) * 4), fl(16);
 	uint32_t *m = (uint32_t *) meta_buf();
 	uint32_t *h = (uint32_t *) pinned(64);
-	if (!gkey.p || !gmin.p || !gmap.p || !ext.p || !fl.p || m == nullptr || h == nullptr)
+	if (!gkey.p || !gmin.p || !gmap.p || !fl.p || m == nullptr || h == nullptr)
 		return -1;
-	if (!hip_ok(hipMemsetAsync(gkey.p, 0xff, (GL_SLOTS + 1) * 8, st), "memset") ||
-	    !hip_ok(hipMemsetAsync(gmin.p, 0xff, (GL_SLOTS + 1) * 8, st), "memset") ||
-	    !hip_ok(hipMemsetAsync(m, 0, 16, st), "memset"))
-		return -1;
+	hipLaunchKernelGGL(k_gl_init, dim3((GL_SLOTS + 256) / 256), dim3(256), 0, st, gkey.as<unsigned long long>(),
+			   gmin.as<unsigned long long>(), m);
 	const unsigned tiles = (unsigned) ((n + GL_TILE - 1) / GL_TILE);
 	static const unsigned prefix = getenv("MGDK_GROUP_PREFIX") ? (unsigned) atoi(getenv("MGDK_GROUP_PREFIX")) : GL_PREFIX;
 	// typed fast path: dense candidates, integer keys of 1-8 bytes
@@ -803,22 +821,21 @@ group_lds(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mg
 		GL_LAUNCH(k_gl_first, dim3((unsigned) ((frows + GL_FTILE - 1) / GL_FTILE)), dim3(1024), 0, st, ks, n, (BUN) done,
 			  gkey.as<unsigned long long>(), gmin.as<unsigned long long>(), &m[0]);
 		done = upto;
-		hipLaunchKernelGGL(k_gl_order, dim3(GL_ORDER_WG), dim3(256), 0, st, gmin.as<unsigned long long>(), gmap.as<uint32_t>(),
-				   ci.dense, ci.seq, ci.oids, ext.as<oid>(), &m[1]);
 		// group count not known yet: ids, extents and histogram sized for
-		// the largest count this path takes
+		// the largest count this path takes; the ordering pass writes the
+		// extents in place and clears the histogram
 		mgdk_bat *en = newbat(0, MGDK_oid, GL_MAXG), *hn = newbat(0, MGDK_lng, GL_MAXG + 1), *gn = newbat(hseqb, MGDK_oid, n);
 		auto unfix3 = [&]() {
 			mgdk_BBPunfix(en);
 			mgdk_BBPunfix(hn);
 			mgdk_BBPunfix(gn);
 		};
-		if (!en || !hn || !gn || !hip_ok(hipMemsetAsync(hn->theap, 0, GL_MAXG * 8 + 8, st), "memset") ||
-		    !hip_ok(hipMemsetAsync(&m[2], 0, 8, st), "memset") ||
-		    !hip_ok(hipMemcpyAsync(en->theap, ext.p, GL_MAXG * 8, hipMemcpyDeviceToDevice, st), "memcpy")) {
+		if (!en || !hn || !gn) {
 			unfix3();
 			return -1;
 		}
+		hipLaunchKernelGGL(k_gl_order, dim3(GL_ORDER_WG), dim3(256), 0, st, gmin.as<unsigned long long>(), gmap.as<uint32_t>(),
+				   ci.dense, ci.seq, ci.oids, (oid *) en->theap, &m[1], (unsigned long long *) hn->theap);
 		gn->count = n;
 		uint8_t *img = img8_new(gn);   // dropped below unless <= 255 groups
 		if (img == nullptr) {
@@ -829,7 +846,7 @@ group_lds(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mg
 		const bool vec = fg == 0 && (fw == 4 || fw == 8) && (((uintptr_t) ks.base + ks.off * fw) & 15) == 0 &&
 				 ((uintptr_t) gn->theap & 15) == 0 && ((uintptr_t) img & 3) == 0;
 		static const bool v32 = getenv("MGDK_GROUP_V32") ? atoi(getenv("MGDK_GROUP_V32")) != 0 : true;
-		const oid *extp = ext.as<oid>();
+		const oid *extp = (const oid *) en->theap;
 		oid *flo = fl.as<oid>();
 		// MGDK_GROUP_GRID: workgroups of the 4-byte assign pass (each keeps its
 		// LDS table over grid-strided tiles); 0 = one per tile

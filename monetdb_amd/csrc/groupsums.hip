@@ -22,7 +22,6 @@
 //          the tile's first and last groups leave (group, partial) records
 //          that k_gs_edges combines in order (no atomics).
 #include "mgdk_internal.h"
-#include "lookback.h"
 
 using namespace mgdk;
 
@@ -207,101 +206,10 @@ k_gs_count(const typename KT<KW>::T *k, BUN n, uint32_t *tcnt)
 		tcnt[blockIdx.x] = c;
 }
 
-// the fused variant's tile claims and look-back state (LB)
-struct GsLb {
-	uint32_t *xtk;         // 8 per-XCD tickets
-	uint64_t *status;      // per tile: {flag:2, starts:62}, zero before the launch
-	uint32_t *err;
-	uint32_t xg;
-	BUN nt;
-};
-
-// group starts in tile tp (one wave): the look-back's count of a
-// predecessor that no XCD has claimed yet
-template <typename T>
-__device__ uint64_t
-gs_wave_starts(const T *k, BUN n, BUN tp)
-{
-	const unsigned lane = __lane_id();
-	const BUN a = tp * GST, e = a + GST < n ? a + GST : n;
-	uint64_t c = 0;
-	for (BUN i = a + lane; i < e; i += 64)
-		c += i == 0 || k[i] != k[i - 1];
-	for (int d = 32; d > 0; d >>= 1)
-		c += __shfl_xor(c, d);
-	return c;
-}
-
-// decoupled look-back over the tiles' group-start counts (mgdk_lb::lookback,
-// 64 predecessors per step), run by one wave; a predecessor no XCD has
-// claimed is counted from its keys instead of waited for
-template <typename T>
-__device__ uint64_t
-gs_lookback(const GsLb &lb, BUN t, uint64_t agg, const T *k, BUN n)
-{
-	using namespace mgdk_lb;
-	const unsigned lane = __lane_id();
-	if (t == 0) {
-		if (lane == 0)
-			lb_store(&lb.status[0], ST_PRE | agg);
-		return 0;
-	}
-	if (lane == 0)
-		lb_store(&lb.status[t], ST_AGG | agg);
-	uint64_t excl = 0;
-	int64_t base = (int64_t) t - 1;
-	for (;;) {
-		const int64_t idx = base - (int64_t) lane;
-		uint64_t val = 0;
-		bool pre = true, miss = false;
-		if (idx >= 0) {
-			pre = false;
-			for (uint32_t spins = 0;; spins++) {
-				const uint64_t sv = lb_load(&lb.status[idx]);
-				if ((sv >> 62) != 0) {
-					val = sv & ST_VAL;
-					pre = (sv >> 62) == 2;
-					break;
-				}
-				if ((spins & 15) == 0 && !xcd_claimed(lb.xtk, (uint64_t) idx, lb.xg)) {
-					miss = true;
-					break;
-				}
-				if (spins > (1u << 26)) {
-					atomicOr(lb.err, 1u);      // cannot happen: claimed tiles publish
-					pre = true;
-					break;
-				}
-				__builtin_amdgcn_s_sleep(1);
-			}
-		}
-		const uint64_t pmask = __ballot(pre);
-		const int first = pmask ? __ffsll((long long) pmask) - 1 : 64;
-		uint64_t mm = __ballot(miss && (int) lane <= first);
-		while (mm) {
-			const int q = __ffsll((long long) mm) - 1;
-			const uint64_t c = gs_wave_starts<T>(k, n, (BUN) (base - q));
-			if ((int) lane == q)
-				val = c;
-			mm &= mm - 1;
-		}
-		uint64_t v = (int) lane <= first ? val : 0;
-		for (int d = 32; d > 0; d >>= 1)
-			v += __shfl_xor(v, d);
-		excl += v;
-		if (pmask)
-			break;
-		base -= 64;
-	}
-	if (lane == 0)
-		lb_store(&lb.status[t], ST_PRE | (excl + agg));
-	return excl;
-}
-
-template <int KW, int VW, int NV, bool LB>
+template <int KW, int VW, int NV>
 __global__ __launch_bounds__(256) void
 k_gs_sums(const typename KT<KW>::T *k, const void *const *vals, BUN n, oid hseq, const uint64_t *tpre, GsOut o,
-	  GsEdge<NV> *edges, GsLb lb)
+	  GsEdge<NV> *edges)
 {
 	typedef typename KT<KW>::T T;
 	typedef typename KT<VW>::T V;
@@ -310,20 +218,8 @@ k_gs_sums(const typename KT<KW>::T *k, const void *const *vals, BUN n, oid hseq,
 	__shared__ uint32_t s_wst[4];
 	__shared__ T s_k[4][512];
 	__shared__ V s_v[NV][4][512];
-	__shared__ uint32_t s_tile;
-	__shared__ uint64_t s_tbase;
 	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
-	BUN t = blockIdx.x;
-	if (LB) {
-		// tiles in per-XCD claim order (claim_xcd_tile), so the look-back
-		// below only ever waits on running tiles
-		if (tid == 0)
-			s_tile = mgdk_lb::claim_xcd_tile(lb.xtk, (uint32_t) lb.nt, lb.xg);
-		__syncthreads();
-		if (s_tile == ~0u)
-			return;     // cannot happen: one tile per workgroup
-		t = s_tile;
-	}
+	const BUN t = blockIdx.x;
 	const BUN t0 = t * GST, l0 = t0 + (BUN) tid * GSU, r0 = t0 + (BUN) w * 512;
 	const bool live = l0 < n;
 	T x[GSU];
@@ -379,20 +275,7 @@ k_gs_sums(const typename KT<KW>::T *k, const void *const *vals, BUN n, oid hseq,
 	bool seen = false;
 	uint32_t of = 0;
 	__syncthreads();
-	uint64_t tbase;
-	if (LB) {
-		// the tile's first group id: the starts of every tile before it
-		if (w == 0) {
-			const uint64_t agg = s_wst[0] + s_wst[1] + s_wst[2] + s_wst[3];
-			const uint64_t ex = gs_lookback<T>(lb, t, agg, k, n);
-			if (lane == 0)
-				s_tbase = ex;
-		}
-		__syncthreads();
-		tbase = s_tbase;
-	} else {
-		tbase = tpre[t];
-	}
+	const uint64_t tbase = tpre[t];
 	uint32_t lpre = xs - ns;
 	for (unsigned q = 0; q < w; q++)
 		lpre += s_wst[q];
@@ -584,15 +467,11 @@ k_gs_edges_long(const GsEdge<NV> *e, BUN ne, BUN ngrp, GsOut o, const uint32_t *
 template <int KW, int VW, int NV>
 int
 gs_run(const void *kb, const void *const *vals_dev, BUN n, oid hseq, const uint64_t *tpre, BUN nt, BUN ngrp,
-       GsOut o, void *edges, uint32_t *longs, const GsLb *lb)
+       GsOut o, void *edges, uint32_t *longs)
 {
 	hipStream_t st = stream();
-	if (lb)
-		hipLaunchKernelGGL((k_gs_sums<KW, VW, NV, true>), dim3((unsigned) nt), dim3(256), 0, st,
-				   (const typename KT<KW>::T *) kb, vals_dev, n, hseq, tpre, o, (GsEdge<NV> *) edges, *lb);
-	else
-		hipLaunchKernelGGL((k_gs_sums<KW, VW, NV, false>), dim3((unsigned) nt), dim3(256), 0, st,
-				   (const typename KT<KW>::T *) kb, vals_dev, n, hseq, tpre, o, (GsEdge<NV> *) edges, GsLb{});
+	hipLaunchKernelGGL((k_gs_sums<KW, VW, NV>), dim3((unsigned) nt), dim3(256), 0, st, (const typename KT<KW>::T *) kb,
+			   vals_dev, n, hseq, tpre, o, (GsEdge<NV> *) edges);
 	const BUN ne = 2 * nt;
 	if (!hip_ok(hipMemsetAsync(longs, 0, 4, st), "memset"))
 		return -1;
@@ -606,13 +485,13 @@ gs_run(const void *kb, const void *const *vals_dev, BUN n, oid hseq, const uint6
 template <int KW, int VW>
 int
 gs_nv(int nv, const void *kb, const void *const *vals_dev, BUN n, oid hseq, const uint64_t *tpre, BUN nt, BUN ngrp,
-      GsOut o, void *edges, uint32_t *longs, const GsLb *lb)
+      GsOut o, void *edges, uint32_t *longs)
 {
 	switch (nv) {
-	case 1: return gs_run<KW, VW, 1>(kb, vals_dev, n, hseq, tpre, nt, ngrp, o, edges, longs, lb);
-	case 2: return gs_run<KW, VW, 2>(kb, vals_dev, n, hseq, tpre, nt, ngrp, o, edges, longs, lb);
-	case 3: return gs_run<KW, VW, 3>(kb, vals_dev, n, hseq, tpre, nt, ngrp, o, edges, longs, lb);
-	default: return gs_run<KW, VW, 4>(kb, vals_dev, n, hseq, tpre, nt, ngrp, o, edges, longs, lb);
+	case 1: return gs_run<KW, VW, 1>(kb, vals_dev, n, hseq, tpre, nt, ngrp, o, edges, longs);
+	case 2: return gs_run<KW, VW, 2>(kb, vals_dev, n, hseq, tpre, nt, ngrp, o, edges, longs);
+	case 3: return gs_run<KW, VW, 3>(kb, vals_dev, n, hseq, tpre, nt, ngrp, o, edges, longs);
+	default: return gs_run<KW, VW, 4>(kb, vals_dev, n, hseq, tpre, nt, ngrp, o, edges, longs);
 	}
 }
 
@@ -666,43 +545,24 @@ mgdk_group_sums_ordered(mgdk_bat **extents, mgdk_bat **histo, mgdk_bat **keys, m
 	hipStream_t st = stream();
 	const int kw = b->twidth, vw = vals[0]->twidth;
 	const BUN nt = (n + GST - 1) / GST;
-	// fused (default): the group ids come from a look-back over the tiles'
-	// start counts inside the sums pass, so the keys are read once; the
-	// outputs are then sized for n groups (56 B x n at two sums) and the
-	// count is read back at the end.  Two-pass (MGDK_GS_FUSED=0, or when
-	// that bound is large): a count pass + scan first, outputs sized exactly
-	static const bool fused_on = !getenv("MGDK_GS_FUSED") || atoi(getenv("MGDK_GS_FUSED")) != 0;
-	const bool fused = fused_on && nt < 0xffffffffull &&
-			   n * (24 + 16 * (BUN) nvals) <= ((BUN) 48 << 30);
-	DevBuf tc(fused ? 8 : nt * 4 + 8), tp(fused ? 8 : nt * 8 + 8), vp(64), lbs(fused ? nt * 8 + 256 : 8);
-	if (!tc.p || !tp.p || !vp.p || !lbs.p)
+	// a count pass + scan first, so the outputs are sized exactly.  (Fusing
+	// the count into the sums pass by a decoupled look-back over the tiles'
+	// start counts was measured slower and dropped, profiles/r05/gsums/:
+	// 6.47 ms at SF100 with a plain ticket -- 293K same-word ticket atomics --
+	// and 101-112 ms with per-XCD claim groups, against 5.40 two-pass.)
+	DevBuf tc(nt * 4 + 8), tp(nt * 8 + 8), vp(64);
+	if (!tc.p || !tp.p || !vp.p)
 		return -1;
-	uint64_t ngrp = 0, cap;
-	GsLb lb{};
-	const GsLb *lbp = nullptr;
-	if (fused) {
-		lb.status = lbs.as<uint64_t>();
-		lb.xtk = (uint32_t *) (lb.status + nt);
-		lb.err = lb.xtk + 16;
-		lb.xg = getenv("MGDK_GS_XCDG") ? (uint32_t) atoi(getenv("MGDK_GS_XCDG")) : 16u;
-		if (lb.xg == 0)
-			lb.xg = 1;
-		lb.nt = nt;
-		lbp = &lb;
-		if (!hip_ok(hipMemsetAsync(lbs.p, 0, nt * 8 + 256, st), "memset"))
-			return -1;
-		cap = n;
-	} else {
-		if (kw == 4)
-			hipLaunchKernelGGL(k_gs_count<4>, dim3((unsigned) nt), dim3(256), 0, st, (const int32_t *) b->theap,
-					   n, tc.as<uint32_t>());
-		else
-			hipLaunchKernelGGL(k_gs_count<8>, dim3((unsigned) nt), dim3(256), 0, st, (const int64_t *) b->theap,
-					   n, tc.as<uint32_t>());
-		if (exclusive_scan(tc.as<uint32_t>(), tp.as<uint64_t>(), nt, &ngrp) < 0)
-			return -1;
-		cap = ngrp;
-	}
+	if (kw == 4)
+		hipLaunchKernelGGL(k_gs_count<4>, dim3((unsigned) nt), dim3(256), 0, st, (const int32_t *) b->theap, n,
+				   tc.as<uint32_t>());
+	else
+		hipLaunchKernelGGL(k_gs_count<8>, dim3((unsigned) nt), dim3(256), 0, st, (const int64_t *) b->theap, n,
+				   tc.as<uint32_t>());
+	uint64_t ngrp = 0;
+	if (exclusive_scan(tc.as<uint32_t>(), tp.as<uint64_t>(), nt, &ngrp) < 0)
+		return -1;
+	const uint64_t cap = ngrp;
 	mgdk_bat *en = newbat(0, MGDK_oid, cap), *hn = newbat(0, MGDK_lng, cap), *kn = newbat(0, MGDK_lng, cap);
 	mgdk_bat *sn[GS_MAXV] = {};
 	bool ok = en && hn && kn;
@@ -738,28 +598,16 @@ mgdk_group_sums_ordered(mgdk_bat **extents, mgdk_bat **histo, mgdk_bat **keys, m
 	o.flags = flags;
 	const void *const *vd = vp.as<const void *const>();
 	if (kw == 4 && vw == 4)
-		gs_nv<4, 4>(nvals, b->theap, vd, n, b->hseqbase, tp.as<uint64_t>(), nt, cap, o, edges.p, longs, lbp);
+		gs_nv<4, 4>(nvals, b->theap, vd, n, b->hseqbase, tp.as<uint64_t>(), nt, cap, o, edges.p, longs);
 	else if (kw == 4)
-		gs_nv<4, 8>(nvals, b->theap, vd, n, b->hseqbase, tp.as<uint64_t>(), nt, cap, o, edges.p, longs, lbp);
+		gs_nv<4, 8>(nvals, b->theap, vd, n, b->hseqbase, tp.as<uint64_t>(), nt, cap, o, edges.p, longs);
 	else if (vw == 4)
-		gs_nv<8, 4>(nvals, b->theap, vd, n, b->hseqbase, tp.as<uint64_t>(), nt, cap, o, edges.p, longs, lbp);
+		gs_nv<8, 4>(nvals, b->theap, vd, n, b->hseqbase, tp.as<uint64_t>(), nt, cap, o, edges.p, longs);
 	else
-		gs_nv<8, 8>(nvals, b->theap, vd, n, b->hseqbase, tp.as<uint64_t>(), nt, cap, o, edges.p, longs, lbp);
+		gs_nv<8, 8>(nvals, b->theap, vd, n, b->hseqbase, tp.as<uint64_t>(), nt, cap, o, edges.p, longs);
 	uint32_t *hf = (uint32_t *) pinned(32);
-	if (!hip_ok(hipMemcpyAsync(hf, flags, 4, hipMemcpyDeviceToHost, st), "memcpy") ||
-	    (fused && (!hip_ok(hipMemcpyAsync(hf + 2, lb.status + (nt - 1), 8, hipMemcpyDeviceToHost, st), "memcpy") ||
-		       !hip_ok(hipMemcpyAsync(hf + 4, lb.err, 4, hipMemcpyDeviceToHost, st), "memcpy"))) ||
-	    !sync())
+	if (!hip_ok(hipMemcpyAsync(hf, flags, 4, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
 		return fail();
-	if (fused) {
-		uint64_t last;
-		memcpy(&last, hf + 2, 8);
-		if (hf[4] || (last >> 62) != 2) {
-			seterr("HY013!group_sums_ordered: look-back did not complete");
-			return fail();
-		}
-		ngrp = last & mgdk_lb::ST_VAL;
-	}
 	const bool anynil = (hf[0] & 2) != 0;
 	// properties as BATgroup / BATgroupsum leave them (extents ascending and
 	// key, the histogram and sums unknown, keys ordered as b)

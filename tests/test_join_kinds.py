@@ -236,7 +236,7 @@ def test_gpu_markjoin(gdk, ora, name, tname, lv, rv, kw, cform):
     a, c = gdk.BATmarkjoin(L, R, gl, gr, want_r2=False)
     wa, wc = ora.BATmarkjoin(OL, OR, ol, orr, want_r2=False)
     assert eq(a, wa) and eq(c, wc, np.int8)
-    assert bool(c.tnil) == bool(wc.s.nil)
+    assert bool(c.s.tnil) == bool(wc.s.nil)
     res = ora.BATmarkjoin(OL, OR, ol, orr)
     if res is None:
         with pytest.raises(gdk.GDKError, match="not on the device path"):

@@ -32,7 +32,10 @@ join)
 	;;
 gsums)
 	timeout -k 10 600 $T tests/test_gpu_group_sums.py > $O/tests.log 2>&1
-	timeout -k 10 200 python tools/opbench.py --only config4_group_sums > $O/opbench.json 2> $O/opbench.err
+	MGDK_GS_FUSED=0 timeout -k 10 200 python tools/opbench.py --only config4_group_sums > $O/opbench_f0.json 2> $O/opbench_f0.err
+	for xg in ${GSXG:-0 16}; do
+		MGDK_GS_XCDG=$xg timeout -k 10 200 python tools/opbench.py --only config4_group_sums > $O/opbench_xg$xg.json 2> $O/opbench_xg$xg.err
+	done
 	cd /tmp && cd $GRAFT_REPO_ROOT
 	timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 tools/opbench.py --only config4_group_sums > $O/prof.log 2>&1
 	timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f -o run -- python3 tools/opbench.py --only config4_group_sums > $O/pmc_f.log 2>&1
@@ -75,6 +78,11 @@ bench)
 	;;
 opbench)
 	timeout -k 10 600 python tools/opbench.py > $O/opbench.json 2> $O/opbench.err
+	;;
+place)
+	for p in 1024 2048 4096; do
+		timeout -k 10 120 tools/probes/place_probe $p >> $O/place.log 2>&1
+	done
 	;;
 *)
 	echo "unknown step $step"; exit 2
