@@ -21,6 +21,7 @@
 //          segmented scan over the 256 lanes carries a group across lanes);
 //          the tile's first and last groups leave (group, partial) records
 //          that k_gs_edges combines in order (no atomics).
+#include "lookback.h"
 #include "mgdk_internal.h"
 
 using namespace mgdk;
@@ -206,11 +207,20 @@ k_gs_count(const typename KT<KW>::T *k, BUN n, uint32_t *tcnt)
 		tcnt[blockIdx.x] = c;
 }
 
-template <int KW, int VW, int NV>
+// LB: the tile's first group id comes from a decoupled look-back over the
+// tiles' start counts (mgdk_lb::lookback on lbst, zero before the launch)
+// instead of the count pass's prefix tpre.  Tiles are numbered by blockIdx,
+// no ticket (293K same-word ticket atomics cost more than the count pass):
+// each XCD dispatches its share of the grid in blockIdx order, so the lowest
+// unfinished tile is always resident or next on its XCD and the walk always
+// ends; a walk that exceeds the spin limit sets lberr and the host reruns
+// the two-pass form
+template <int KW, int VW, int NV, bool LB>
 __global__ __launch_bounds__(256) void
 k_gs_sums(const typename KT<KW>::T *k, const void *const *vals, BUN n, oid hseq, const uint64_t *tpre, GsOut o,
-	  GsEdge<NV> *edges)
+	  GsEdge<NV> *edges, uint64_t *lbst, uint32_t *lberr)
 {
+	__shared__ uint64_t s_tbase;
 	typedef typename KT<KW>::T T;
 	typedef typename KT<VW>::T V;
 	__shared__ GsPart<NV> s_wtot[4];
@@ -275,7 +285,21 @@ k_gs_sums(const typename KT<KW>::T *k, const void *const *vals, BUN n, oid hseq,
 	bool seen = false;
 	uint32_t of = 0;
 	__syncthreads();
-	const uint64_t tbase = tpre[t];
+	uint64_t tbase;
+	if constexpr (LB) {
+		if (w == 0) {
+			// a predecessor's wait is microseconds; 2^20 spins (~1 s) means the
+			// dispatch order assumption failed: give up, the host reruns
+			const uint64_t ex = mgdk_lb::lookback(lbst, (uint32_t) t, s_wst[0] + s_wst[1] + s_wst[2] + s_wst[3],
+							      lberr, 1u << 20);
+			if (lane == 0)
+				s_tbase = ex;
+		}
+		__syncthreads();
+		tbase = s_tbase;
+	} else {
+		tbase = tpre[t];
+	}
 	uint32_t lpre = xs - ns;
 	for (unsigned q = 0; q < w; q++)
 		lpre += s_wst[q];
@@ -467,11 +491,15 @@ k_gs_edges_long(const GsEdge<NV> *e, BUN ne, BUN ngrp, GsOut o, const uint32_t *
 template <int KW, int VW, int NV>
 int
 gs_run(const void *kb, const void *const *vals_dev, BUN n, oid hseq, const uint64_t *tpre, BUN nt, BUN ngrp,
-       GsOut o, void *edges, uint32_t *longs)
+       GsOut o, void *edges, uint32_t *longs, uint64_t *lbst, uint32_t *lberr)
 {
 	hipStream_t st = stream();
-	hipLaunchKernelGGL((k_gs_sums<KW, VW, NV>), dim3((unsigned) nt), dim3(256), 0, st, (const typename KT<KW>::T *) kb,
-			   vals_dev, n, hseq, tpre, o, (GsEdge<NV> *) edges);
+	if (lbst)
+		hipLaunchKernelGGL((k_gs_sums<KW, VW, NV, true>), dim3((unsigned) nt), dim3(256), 0, st,
+				   (const typename KT<KW>::T *) kb, vals_dev, n, hseq, tpre, o, (GsEdge<NV> *) edges, lbst, lberr);
+	else
+		hipLaunchKernelGGL((k_gs_sums<KW, VW, NV, false>), dim3((unsigned) nt), dim3(256), 0, st,
+				   (const typename KT<KW>::T *) kb, vals_dev, n, hseq, tpre, o, (GsEdge<NV> *) edges, lbst, lberr);
 	const BUN ne = 2 * nt;
 	if (!hip_ok(hipMemsetAsync(longs, 0, 4, st), "memset"))
 		return -1;
@@ -485,13 +513,13 @@ gs_run(const void *kb, const void *const *vals_dev, BUN n, oid hseq, const uint6
 template <int KW, int VW>
 int
 gs_nv(int nv, const void *kb, const void *const *vals_dev, BUN n, oid hseq, const uint64_t *tpre, BUN nt, BUN ngrp,
-      GsOut o, void *edges, uint32_t *longs)
+      GsOut o, void *edges, uint32_t *longs, uint64_t *lbst, uint32_t *lberr)
 {
 	switch (nv) {
-	case 1: return gs_run<KW, VW, 1>(kb, vals_dev, n, hseq, tpre, nt, ngrp, o, edges, longs);
-	case 2: return gs_run<KW, VW, 2>(kb, vals_dev, n, hseq, tpre, nt, ngrp, o, edges, longs);
-	case 3: return gs_run<KW, VW, 3>(kb, vals_dev, n, hseq, tpre, nt, ngrp, o, edges, longs);
-	default: return gs_run<KW, VW, 4>(kb, vals_dev, n, hseq, tpre, nt, ngrp, o, edges, longs);
+	case 1: return gs_run<KW, VW, 1>(kb, vals_dev, n, hseq, tpre, nt, ngrp, o, edges, longs, lbst, lberr);
+	case 2: return gs_run<KW, VW, 2>(kb, vals_dev, n, hseq, tpre, nt, ngrp, o, edges, longs, lbst, lberr);
+	case 3: return gs_run<KW, VW, 3>(kb, vals_dev, n, hseq, tpre, nt, ngrp, o, edges, longs, lbst, lberr);
+	default: return gs_run<KW, VW, 4>(kb, vals_dev, n, hseq, tpre, nt, ngrp, o, edges, longs, lbst, lberr);
 	}
 }
 
@@ -545,69 +573,111 @@ mgdk_group_sums_ordered(mgdk_bat **extents, mgdk_bat **histo, mgdk_bat **keys, m
 	hipStream_t st = stream();
 	const int kw = b->twidth, vw = vals[0]->twidth;
 	const BUN nt = (n + GST - 1) / GST;
-	// a count pass + scan first, so the outputs are sized exactly.  (Fusing
-	// the count into the sums pass by a decoupled look-back over the tiles'
-	// start counts was measured slower and dropped, profiles/r05/gsums/:
-	// 6.47 ms at SF100 with a plain ticket -- 293K same-word ticket atomics --
-	// and 101-112 ms with per-XCD claim groups, against 5.40 two-pass.)
-	DevBuf tc(nt * 4 + 8), tp(nt * 8 + 8), vp(64);
-	if (!tc.p || !tp.p || !vp.p)
-		return -1;
-	if (kw == 4)
-		hipLaunchKernelGGL(k_gs_count<4>, dim3((unsigned) nt), dim3(256), 0, st, (const int32_t *) b->theap, n,
-				   tc.as<uint32_t>());
-	else
-		hipLaunchKernelGGL(k_gs_count<8>, dim3((unsigned) nt), dim3(256), 0, st, (const int64_t *) b->theap, n,
-				   tc.as<uint32_t>());
-	uint64_t ngrp = 0;
-	if (exclusive_scan(tc.as<uint32_t>(), tp.as<uint64_t>(), nt, &ngrp) < 0)
-		return -1;
-	const uint64_t cap = ngrp;
-	mgdk_bat *en = newbat(0, MGDK_oid, cap), *hn = newbat(0, MGDK_lng, cap), *kn = newbat(0, MGDK_lng, cap);
-	mgdk_bat *sn[GS_MAXV] = {};
-	bool ok = en && hn && kn;
-	for (int v = 0; v < nvals && ok; v++)
-		ok = (sn[v] = newbat(0, MGDK_hge, cap)) != nullptr;
+	// fused (default): the tile's first group id comes from the look-back
+	// inside the sums pass, so the keys are read once; the outputs are sized
+	// for n groups (56 B per row at two sums, capped at 48 GiB) and the count
+	// is the last tile's inclusive prefix.  Two-pass (MGDK_GS_FUSED=0, above
+	// the cap, or when a look-back did not complete): a count pass + scan
+	// first, outputs sized exactly.  (Fused with a tile ticket was slower than
+	// two-pass: 6.47 vs 5.40 ms at SF100, profiles/r05/gsums/.)
+	const bool fused_on = !getenv("MGDK_GS_FUSED") || atoi(getenv("MGDK_GS_FUSED")) != 0;   // read per call (tests)
+	bool fused = fused_on && nt < 0xffffffffull && n * (24 + 16 * (BUN) nvals) <= ((BUN) 48 << 30);
+	DevBuf vp(64);
 	const size_t esz = sizeof(GsEdge<GS_MAXV>);
 	// the tiles' edge records, then the list of groups over more than
 	// GS_ECAP records (k_gs_edges_long)
 	const size_t lgoff = (2 * nt * esz + 255) & ~(size_t) 255;
 	DevBuf edges(lgoff + (2 * nt / GS_ECAP + 2) * 4);
+	if (!vp.p || !edges.p)
+		return -1;
 	uint32_t *longs = (uint32_t *) ((char *) edges.p + lgoff);
 	uint32_t *flags = (uint32_t *) meta_buf();
 	const void *hv[GS_MAXV] = {};
 	for (int v = 0; v < nvals; v++)
 		hv[v] = vals[v]->theap;
-	auto fail = [&]() {
+	if (!hip_ok(hipMemcpyAsync(vp.p, stage_host(hv, sizeof hv), sizeof hv, hipMemcpyHostToDevice, st), "memcpy"))
+		return -1;
+	const void *const *vd = vp.as<const void *const>();
+	mgdk_bat *en = nullptr, *hn = nullptr, *kn = nullptr;
+	mgdk_bat *sn[GS_MAXV] = {};
+	auto drop = [&]() {
 		mgdk_BBPunfix(en);
 		mgdk_BBPunfix(hn);
 		mgdk_BBPunfix(kn);
-		for (int v = 0; v < nvals; v++)
+		en = hn = kn = nullptr;
+		for (int v = 0; v < nvals; v++) {
 			mgdk_BBPunfix(sn[v]);
+			sn[v] = nullptr;
+		}
 		return -1;
 	};
-	if (!ok || !edges.p || !hip_ok(hipMemsetAsync(flags, 0, 8, st), "memset") ||
-	    !hip_ok(hipMemcpyAsync(vp.p, stage_host(hv, sizeof hv), sizeof hv, hipMemcpyHostToDevice, st), "memcpy"))
-		return fail();
-	GsOut o{};
-	o.ext = (oid *) en->theap;
-	o.hist = (int64_t *) hn->theap;
-	o.key = (int64_t *) kn->theap;
-	for (int v = 0; v < nvals; v++)
-		o.sum[v] = (hge *) sn[v]->theap;
-	o.flags = flags;
-	const void *const *vd = vp.as<const void *const>();
-	if (kw == 4 && vw == 4)
-		gs_nv<4, 4>(nvals, b->theap, vd, n, b->hseqbase, tp.as<uint64_t>(), nt, cap, o, edges.p, longs);
-	else if (kw == 4)
-		gs_nv<4, 8>(nvals, b->theap, vd, n, b->hseqbase, tp.as<uint64_t>(), nt, cap, o, edges.p, longs);
-	else if (vw == 4)
-		gs_nv<8, 4>(nvals, b->theap, vd, n, b->hseqbase, tp.as<uint64_t>(), nt, cap, o, edges.p, longs);
-	else
-		gs_nv<8, 8>(nvals, b->theap, vd, n, b->hseqbase, tp.as<uint64_t>(), nt, cap, o, edges.p, longs);
+	uint64_t ngrp = 0;
 	uint32_t *hf = (uint32_t *) pinned(32);
-	if (!hip_ok(hipMemcpyAsync(hf, flags, 4, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
-		return fail();
+	if (hf == nullptr)
+		return -1;
+	for (;;) {
+		DevBuf tc(fused ? 8 : nt * 4 + 8), tp(fused ? 8 : nt * 8 + 8), lbs(fused ? nt * 8 + 64 : 8);
+		if (!tc.p || !tp.p || !lbs.p)
+			return -1;
+		uint64_t *lbst = fused ? lbs.as<uint64_t>() : nullptr;
+		uint32_t *lberr = fused ? (uint32_t *) (lbst + nt) : nullptr;
+		uint64_t cap;
+		if (fused) {
+			if (!hip_ok(hipMemsetAsync(lbs.p, 0, nt * 8 + 64, st), "memset"))
+				return -1;
+			cap = n;
+		} else {
+			if (kw == 4)
+				hipLaunchKernelGGL(k_gs_count<4>, dim3((unsigned) nt), dim3(256), 0, st, (const int32_t *) b->theap,
+						   n, tc.as<uint32_t>());
+			else
+				hipLaunchKernelGGL(k_gs_count<8>, dim3((unsigned) nt), dim3(256), 0, st, (const int64_t *) b->theap,
+						   n, tc.as<uint32_t>());
+			if (exclusive_scan(tc.as<uint32_t>(), tp.as<uint64_t>(), nt, &ngrp) < 0)
+				return -1;
+			cap = ngrp;
+		}
+		en = newbat(0, MGDK_oid, cap);
+		hn = newbat(0, MGDK_lng, cap);
+		kn = newbat(0, MGDK_lng, cap);
+		bool ok = en && hn && kn;
+		for (int v = 0; v < nvals && ok; v++)
+			ok = (sn[v] = newbat(0, MGDK_hge, cap)) != nullptr;
+		if (!ok || !hip_ok(hipMemsetAsync(flags, 0, 8, st), "memset"))
+			return drop();
+		GsOut o{};
+		o.ext = (oid *) en->theap;
+		o.hist = (int64_t *) hn->theap;
+		o.key = (int64_t *) kn->theap;
+		for (int v = 0; v < nvals; v++)
+			o.sum[v] = (hge *) sn[v]->theap;
+		o.flags = flags;
+		const uint64_t *tpre = tp.as<uint64_t>();
+		if (kw == 4 && vw == 4)
+			gs_nv<4, 4>(nvals, b->theap, vd, n, b->hseqbase, tpre, nt, cap, o, edges.p, longs, lbst, lberr);
+		else if (kw == 4)
+			gs_nv<4, 8>(nvals, b->theap, vd, n, b->hseqbase, tpre, nt, cap, o, edges.p, longs, lbst, lberr);
+		else if (vw == 4)
+			gs_nv<8, 4>(nvals, b->theap, vd, n, b->hseqbase, tpre, nt, cap, o, edges.p, longs, lbst, lberr);
+		else
+			gs_nv<8, 8>(nvals, b->theap, vd, n, b->hseqbase, tpre, nt, cap, o, edges.p, longs, lbst, lberr);
+		if (!hip_ok(hipMemcpyAsync(hf, flags, 4, hipMemcpyDeviceToHost, st), "memcpy") ||
+		    (fused && (!hip_ok(hipMemcpyAsync(hf + 2, lbst + (nt - 1), 8, hipMemcpyDeviceToHost, st), "memcpy") ||
+			       !hip_ok(hipMemcpyAsync(hf + 4, lberr, 4, hipMemcpyDeviceToHost, st), "memcpy"))) ||
+		    !sync())
+			return drop();
+		if (!fused)
+			break;
+		uint64_t last;
+		memcpy(&last, hf + 2, 8);
+		if (hf[4] == 0 && (last >> 62) == 2) {
+			ngrp = last & mgdk_lb::ST_VAL;
+			break;
+		}
+		// a look-back that did not complete: the two-pass form
+		drop();
+		fused = false;
+	}
 	const bool anynil = (hf[0] & 2) != 0;
 	// properties as BATgroup / BATgroupsum leave them (extents ascending and
 	// key, the histogram and sums unknown, keys ordered as b)

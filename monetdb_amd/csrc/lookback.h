@@ -30,7 +30,7 @@ lb_store(uint64_t *p, uint64_t v)
 // status[] must be zero before the launch.  A predecessor that never
 // publishes (cannot happen with ticketed tiles) sets *err instead of hanging.
 __device__ inline uint64_t
-lookback(uint64_t *status, uint32_t tile, uint64_t agg, uint32_t *err)
+lookback(uint64_t *status, uint32_t tile, uint64_t agg, uint32_t *err, uint32_t maxspins = 1u << 26)
 {
 	const unsigned lane = __lane_id();
 	if (tile == 0) {
@@ -51,7 +51,7 @@ lookback(uint64_t *status, uint32_t tile, uint64_t agg, uint32_t *err)
 				s = lb_load(&status[idx]);
 				if ((s >> 62) != 0)
 					break;
-				if (++spins > (1u << 26)) {
+				if (++spins > maxspins) {
 					atomicOr(err, 1u);
 					s = ST_PRE;
 					break;

@@ -36,9 +36,13 @@ def _model(ora, okeys, ovals):
     return e, h, ora.BATproject(e, okeys), sums
 
 
+@pytest.mark.parametrize("fused", ["1", "0"])
 @pytest.mark.parametrize("n", [1, 7, 8, 2047, 2049, 1_000_003])
 @pytest.mark.parametrize("shape", ["orders", "long", "one", "singles", "mixed"])
-def test_group_sums_ordered(gdk, ora, n, shape):
+def test_group_sums_ordered(gdk, ora, n, shape, fused, monkeypatch):
+    # fused: group ids by the look-back inside the sums pass (default);
+    # "0": the count pass + scan first (MGDK_GS_FUSED, read per call)
+    monkeypatch.setenv("MGDK_GS_FUSED", fused)
     r = rng(n + len(shape))
     k = _keys(r, n, shape, np.int64)
     vals = [r.integers(-10**12, 10**12, n).astype(np.int64) for _ in range(2)]

@@ -23,9 +23,9 @@ sortvar)
 	done
 	;;
 join)
-	timeout -k 10 600 $T tests/test_gpu_join_sort_window.py tests/test_join_algo.py tests/test_join_str.py tests/test_msk_cands.py -k "join" > $O/tests.log 2>&1
-	for v in 0 1; do
-		MGDK_JOIN_PROBE4=$v timeout -k 10 200 python tools/opbench.py --only config3 > $O/opbench_v$v.json 2> $O/opbench_v$v.err
+	timeout -k 10 600 $T -x tests/test_gpu_join_sort_window.py tests/test_join_algo.py tests/test_join_str.py tests/test_msk_cands.py -k "join" > $O/tests.log 2>&1
+	for v in 1 3; do
+		MGDK_JOIN_PART=$v timeout -k 10 200 python tools/opbench.py --only config3 > $O/opbench_part$v.json 2> $O/opbench_part$v.err
 	done
 	cd /tmp && cd $GRAFT_REPO_ROOT
 	timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 tools/opbench.py --only config3 > $O/prof.log 2>&1
@@ -33,9 +33,7 @@ join)
 gsums)
 	timeout -k 10 600 $T tests/test_gpu_group_sums.py > $O/tests.log 2>&1
 	MGDK_GS_FUSED=0 timeout -k 10 200 python tools/opbench.py --only config4_group_sums > $O/opbench_f0.json 2> $O/opbench_f0.err
-	for xg in ${GSXG:-0 16}; do
-		MGDK_GS_XCDG=$xg timeout -k 10 200 python tools/opbench.py --only config4_group_sums > $O/opbench_xg$xg.json 2> $O/opbench_xg$xg.err
-	done
+	timeout -k 10 200 python tools/opbench.py --only config4_group_sums > $O/opbench_fused.json 2> $O/opbench_fused.err
 	cd /tmp && cd $GRAFT_REPO_ROOT
 	timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 tools/opbench.py --only config4_group_sums > $O/prof.log 2>&1
 	timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f -o run -- python3 tools/opbench.py --only config4_group_sums > $O/pmc_f.log 2>&1
@@ -78,6 +76,11 @@ bench)
 	;;
 opbench)
 	timeout -k 10 600 python tools/opbench.py > $O/opbench.json 2> $O/opbench.err
+	;;
+soa)
+	for p in 10 11; do
+		timeout -k 10 120 tools/probes/join_soa_probe $p >> $O/soa.log 2>&1
+	done
 	;;
 place)
 	for p in 1024 2048 4096; do
