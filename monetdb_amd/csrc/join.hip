@@ -1173,43 +1173,16 @@ k_pj_delta(const uint32_t *offT, const uint32_t *poff, const uint32_t *pbase, ui
 // one workgroup per subtile (ticketed): matches back into row order; the
 // subtile's probe results are the contiguous range [offT[sub][0],
 // offT[sub + 1][0]) of the flat array
-__global__ __launch_bounds__(1024) void
-k_pj_restore(const uint2 *flat, const uint32_t *offT, uint32_t P, uint64_t total, BUN n, uint32_t nsub, Side L,
-	     Side R, uint32_t *ticket, uint64_t *status, uint64_t *meta, oid *r1, oid *r2)
+// the subtile's matches back in row order (shared by both restores):
+// res[r + r / 32] = match position + 1 of row r (0: none); output offset by
+// decoupled look-back over the subtiles (numbered by ticket)
+__device__ __forceinline__ void
+pj_emit(const uint32_t *res, uint32_t sub, BUN a, uint32_t rows, uint32_t nsub, const Side &L, const Side &R,
+	uint64_t *status, uint64_t *meta, oid *r1, oid *r2)
 {
-	// res[row + row / 32]: one pad word per 32 rows, so the 32-row runs of
-	// consecutive threads fall in different banks
-	__shared__ uint32_t res[PJ_SUBROWS + PJ_SUBROWS / 32];
 	__shared__ uint32_t wsum[16];
-	__shared__ uint32_t s_sub;
 	__shared__ uint64_t s_pre;
 	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
-	if (tid == 0)
-		s_sub = atomicAdd(ticket, 1u);
-	for (uint32_t i = tid; i < PJ_SUBROWS + PJ_SUBROWS / 32; i += blockDim.x)
-		res[i] = 0;
-	__syncthreads();
-	const uint32_t sub = s_sub;
-	const BUN a = (BUN) sub * PJ_SUBROWS;
-	const uint32_t rows = (uint32_t) min((BUN) PJ_SUBROWS, n - a);
-	const uint32_t f0 = offT[(size_t) sub * P];
-	const uint32_t f1 = sub + 1 < nsub ? offT[(size_t) (sub + 1) * P] : (uint32_t) total;
-	constexpr int U = 8;
-	for (uint32_t j0 = f0 + tid; j0 < f1; j0 += U * blockDim.x) {
-		uint2 en[U];
-#pragma unroll
-		for (int u = 0; u < U; u++) {
-			const uint32_t j = j0 + u * blockDim.x;
-			en[u] = j < f1 ? flat[j] : make_uint2(0, (uint32_t) a);
-		}
-#pragma unroll
-		for (int u = 0; u < U; u++) {
-			const uint32_t r = en[u].y - (uint32_t) a;
-			if (en[u].x)
-				res[r + (r >> 5)] = en[u].x;
-		}
-	}
-	__syncthreads();
 	// thread tid counts the rows [32 tid, 32 tid + 32): a match mask and the
 	// run's exclusive offset, so the output pass below can walk the rows in
 	// order (consecutive lanes -> consecutive positions) without barriers
@@ -1259,6 +1232,335 @@ k_pj_restore(const uint2 *flat, const uint32_t *offT, uint32_t P, uint64_t total
 	}
 }
 
+__global__ __launch_bounds__(1024) void
+k_pj_restore(const uint2 *flat, const uint32_t *offT, uint32_t P, uint64_t total, BUN n, uint32_t nsub, Side L,
+	     Side R, uint32_t *ticket, uint64_t *status, uint64_t *meta, oid *r1, oid *r2)
+{
+	// res[row + row / 32]: one pad word per 32 rows, so the 32-row runs of
+	// consecutive threads fall in different banks
+	__shared__ uint32_t res[PJ_SUBROWS + PJ_SUBROWS / 32];
+	__shared__ uint32_t s_sub;
+	const unsigned tid = threadIdx.x;
+	if (tid == 0)
+		s_sub = atomicAdd(ticket, 1u);
+	for (uint32_t i = tid; i < PJ_SUBROWS + PJ_SUBROWS / 32; i += blockDim.x)
+		res[i] = 0;
+	__syncthreads();
+	const uint32_t sub = s_sub;
+	const BUN a = (BUN) sub * PJ_SUBROWS;
+	const uint32_t rows = (uint32_t) min((BUN) PJ_SUBROWS, n - a);
+	const uint32_t f0 = offT[(size_t) sub * P];
+	const uint32_t f1 = sub + 1 < nsub ? offT[(size_t) (sub + 1) * P] : (uint32_t) total;
+	constexpr int U = 8;
+	for (uint32_t j0 = f0 + tid; j0 < f1; j0 += U * blockDim.x) {
+		uint2 en[U];
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const uint32_t j = j0 + u * blockDim.x;
+			en[u] = j < f1 ? flat[j] : make_uint2(0, (uint32_t) a);
+		}
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const uint32_t r = en[u].y - (uint32_t) a;
+			if (en[u].x)
+				res[r + (r >> 5)] = en[u].x;
+		}
+	}
+	__syncthreads();
+	pj_emit(res, sub, a, rows, nsub, L, R, status, meta, r1, r2);
+}
+
+// ---------------------------------------------------------------------------
+// Probe side with subtile-local runs (round 5, default; MGDK_JOIN_PART=3 runs
+// the cut / probe / restore above).  The cut above stores each (subtile,
+// partition) run at its partition-major place: ~8 entries of 8 B per run,
+// written as 64-B pieces by different workgroups (1.9 TB/s), after a
+// histogram pass over the keys.  Here every subtile keeps its own region:
+//   k_pj2_cut     one pass, no histogram: the subtile's keys counting-sorted
+//                 by partition in LDS and stored contiguously (4-B key images
+//                 in pkey, the 2-B row inside the subtile in prow, split so
+//                 the probe reads keys only) + the run starts poff[s][0..P]
+//                 (uint16; poff[s][P] = the subtile's entries);
+//   k_pj2_offt    the run starts transposed (partition-major);
+//   k_pj2_probe   one workgroup per partition builds its LDS table and answers
+//                 its run of every subtile: a wave takes the runs of 64
+//                 subtiles at once, numbers their entries by a wave scan of
+//                 the run lengths and lets lane l take entries l, l + 64, ...
+//                 (a binary search over the 64 run starts finds an entry's
+//                 run), so the key loads of a run are consecutive lanes; the
+//                 4-B answer (match + 1, 0 = none) goes to the key's own index
+//                 in pans;
+//   k_pj2_restore per subtile: the answers dropped into the LDS row array
+//                 through prow, then pj_emit.
+// Probe-side bytes per row: 4 read + 6 written, 4 + 4, 6 + 16 (40 B) against
+// 4, 4 + 8, 8 + 8, 8 + 16 (56 B) for the plan above.
+// ---------------------------------------------------------------------------
+
+constexpr size_t PJ2_CUT_LDS = ((size_t) (1u << PJ_MAXPBITS) + PJ_SUBROWS) * 4;
+
+__global__ __launch_bounds__(1024) void
+k_pj2_cut(Side s, BUN n, int pbits, bool skipnil, uint32_t *pkey, uint16_t *prow, uint16_t *poff)
+{
+	extern __shared__ __attribute__((aligned(16))) uint32_t sm2[];
+	uint32_t *hist = sm2;                          // counters, then run starts
+	uint32_t *stk = sm2 + (1u << PJ_MAXPBITS);     // the run-ordered keys, then rows
+	__shared__ uint32_t wsum[16];
+	const uint32_t P = 1u << pbits;
+	const unsigned tid = threadIdx.x, lane = __lane_id();
+	const uint32_t sub = blockIdx.x;
+	const BUN a = (BUN) sub * PJ_SUBROWS;
+	for (uint32_t p = tid; p < P; p += blockDim.x)
+		hist[p] = 0;
+	uint32_t kk[2][16], rk[2][16];
+	bool ok[2][16];
+	// a full, aligned dense 4-byte subtile: lane-consecutive 16-B loads (one
+	// 1-KiB piece per wave instruction), key (half, q) = row
+	// (half * 4 + q / 4) * 4096 + tid * 4 + q % 4; otherwise 16 consecutive
+	// rows per thread and half, key (half, q) = row half * 16384 + tid * 16 + q
+	const bool fast = s.w == 4 && s.dense && a + PJ_SUBROWS <= n && ((s.off + a) & 3) == 0;
+	if (fast) {
+		typedef int32_t i4 __attribute__((ext_vector_type(4)));
+		const i4 *src = (const i4 *) ((const int32_t *) s.base + s.off + a);
+#pragma unroll
+		for (int half = 0; half < 2; half++)
+#pragma unroll
+			for (int q4 = 0; q4 < 4; q4++) {
+				const i4 v = __builtin_nontemporal_load(src + (half * 4 + q4) * 1024 + tid);
+				kk[half][4 * q4] = (uint32_t) v.x;
+				kk[half][4 * q4 + 1] = (uint32_t) v.y;
+				kk[half][4 * q4 + 2] = (uint32_t) v.z;
+				kk[half][4 * q4 + 3] = (uint32_t) v.w;
+			}
+#pragma unroll
+		for (int half = 0; half < 2; half++)
+#pragma unroll
+			for (int q = 0; q < 16; q++)
+				ok[half][q] = !(skipnil && kk[half][q] == 0x80000000u);
+	} else {
+#pragma unroll
+		for (int half = 0; half < 2; half++)
+			pj_keys16(s, a + (BUN) half * PJ_HALF + (BUN) tid * 16, n, skipnil, kk[half], ok[half]);
+	}
+	__syncthreads();
+#pragma unroll
+	for (int half = 0; half < 2; half++)
+#pragma unroll
+		for (int q = 0; q < 16; q++)
+			if (ok[half][q])
+				rk[half][q] = atomicAdd(&hist[pj_part32(kk[half][q], pbits)], 1u);
+	__syncthreads();
+	// exclusive scan of the counters in place (P <= 2048: two per thread)
+	static_assert((1u << PJ_MAXPBITS) <= 2048, "two counters per thread");
+	const uint32_t p0 = 2 * tid;
+	const uint32_t c0 = p0 < P ? hist[p0] : 0, c1 = p0 + 1 < P ? hist[p0 + 1] : 0;
+	uint32_t x = c0 + c1;
+#pragma unroll
+	for (int o = 1; o < 64; o <<= 1) {
+		const uint32_t u = __shfl_up(x, o);
+		if (lane >= (unsigned) o)
+			x += u;
+	}
+	if (lane == 63)
+		wsum[tid >> 6] = x;
+	__syncthreads();
+	uint32_t pre = x - c0 - c1, total = 0;
+	for (uint32_t w = 0; w < 16; w++) {
+		pre += w < (tid >> 6) ? wsum[w] : 0;
+		total += wsum[w];
+	}
+	uint16_t *po = poff + (size_t) sub * (P + 1);
+	if (p0 < P) {
+		hist[p0] = pre;
+		po[p0] = (uint16_t) pre;
+	}
+	if (p0 + 1 < P) {
+		hist[p0 + 1] = pre + c0;
+		po[p0 + 1] = (uint16_t) (pre + c0);
+	}
+	if (tid == 0)
+		po[P] = (uint16_t) total;      // <= PJ_SUBROWS = 32768 fits
+	__syncthreads();
+#pragma unroll
+	for (int half = 0; half < 2; half++)
+#pragma unroll
+		for (int q = 0; q < 16; q++)
+			if (ok[half][q]) {
+				rk[half][q] += hist[pj_part32(kk[half][q], pbits)];
+				stk[rk[half][q]] = kk[half][q];
+			}
+	__syncthreads();
+	// whole 16-B pieces: the region holds PJ_SUBROWS entries, so rounding
+	// the count up to a multiple of 4 (8 for the rows) stays inside it
+	typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+	u4 *dk = (u4 *) (pkey + a);
+	for (uint32_t j = tid; 4 * j < total; j += blockDim.x)
+		__builtin_nontemporal_store(((const u4 *) stk)[j], dk + j);
+	__syncthreads();
+	uint16_t *str = (uint16_t *) stk;
+#pragma unroll
+	for (int half = 0; half < 2; half++)
+#pragma unroll
+		for (int q = 0; q < 16; q++)
+			if (ok[half][q])
+				str[rk[half][q]] = (uint16_t) (fast ? (half * 4 + q / 4) * 4096 + tid * 4 + q % 4
+								 : half * PJ_HALF + tid * 16 + q);
+	__syncthreads();
+	u4 *dr = (u4 *) (prow + a);
+	for (uint32_t j = tid; 8 * j < total; j += blockDim.x)
+		__builtin_nontemporal_store(((const u4 *) stk)[j], dr + j);
+}
+
+// poffT[p][s] = poff[s][p] for p in [0, P]: 64 x 64 tiles through LDS
+__global__ __launch_bounds__(256) void
+k_pj2_offt(const uint16_t *poff, uint32_t nsub, uint32_t P, uint16_t *poffT)
+{
+	__shared__ uint16_t t[64][65];
+	const uint32_t s0 = blockIdx.x * 64, q0 = blockIdx.y * 64;
+	for (uint32_t k = threadIdx.x; k < 64 * 64; k += blockDim.x) {
+		const uint32_t r = k / 64, c = k % 64;
+		if (s0 + r < nsub && q0 + c <= P)
+			t[r][c] = poff[(size_t) (s0 + r) * (P + 1) + q0 + c];
+	}
+	__syncthreads();
+	for (uint32_t k = threadIdx.x; k < 64 * 64; k += blockDim.x) {
+		const uint32_t r = k / 64, c = k % 64;
+		if (s0 + c < nsub && q0 + r <= P)
+			poffT[(size_t) (q0 + r) * nsub + s0 + c] = t[c][r];
+	}
+}
+
+constexpr int PJ2_U = 16;       // entries per lane in flight in the probe (a batch of 64 runs ~ 1000 entries)
+
+__global__ __launch_bounds__(1024) void
+k_pj2_probe(const uint2 *bent, const uint32_t *bbase, const uint32_t *pkey, const uint16_t *poffT, int pbits,
+	    uint32_t nbp, uint32_t nsub, uint32_t *pans, uint32_t *dupflag)
+{
+	extern __shared__ __attribute__((aligned(16))) unsigned long long dyn2[];
+	unsigned long long *tab = dyn2;
+	uint32_t *wst = (uint32_t *) (dyn2 + 2 * nbp);            // [16][64] run starts in the wave's entry list
+	uint32_t *wbs = wst + 16 * 64;                            // [16][64] first index of each run (< 2^32)
+	const uint32_t p = xcd_block(blockIdx.x, gridDim.x), ns = 2 * nbp;
+	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+	for (uint32_t i = tid; i < ns; i += blockDim.x)
+		tab[i] = 0ull;
+	__syncthreads();
+	const uint32_t b0 = bbase[p], b1 = bbase[p + 1];
+	bool dup = false;
+	for (uint32_t e = b0 + tid; e < b1; e += blockDim.x) {
+		const uint2 en = bent[e];
+		const unsigned long long v = ((unsigned long long) (en.y + 1) << 32) | en.x;
+		uint32_t h = 2 * gt_home(pj_hash(en.x), pbits, nbp);
+		for (;;) {
+			const unsigned long long o = atomicCAS(&tab[h], 0ull, v);
+			if (o == 0ull)
+				break;
+			if ((uint32_t) o == en.x) {
+				dup = true;
+				break;
+			}
+			h = h + 1 == ns ? 0 : h + 1;
+		}
+	}
+	if (__any(dup) && lane == 0)
+		atomicOr(dupflag, 1u);
+	__syncthreads();
+	const ulonglong2 *bk = (const ulonglong2 *) tab;
+	const uint16_t *o0 = poffT + (size_t) p * nsub, *o1 = poffT + (size_t) (p + 1) * nsub;
+	uint32_t *ws = wst + w * 64, *wb = wbs + w * 64;
+	for (uint32_t s0 = w * 64; s0 < nsub; s0 += 16 * 64) {
+		const uint32_t sb = s0 + lane;
+		uint32_t b = 0, len = 0;
+		if (sb < nsub) {
+			b = o0[sb];
+			len = o1[sb] - b;
+		}
+		uint32_t inc = len;
+#pragma unroll
+		for (int o = 1; o < 64; o <<= 1) {
+			const uint32_t u = __shfl_up(inc, o);
+			if (lane >= (unsigned) o)
+				inc += u;
+		}
+		const uint32_t tot = __shfl(inc, 63);
+		ws[lane] = inc - len;
+		wb[lane] = sb * PJ_SUBROWS + b;
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+		__builtin_amdgcn_wave_barrier();
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+		for (uint32_t i0 = 0; i0 < tot; i0 += 64 * PJ2_U) {
+			uint32_t idx[PJ2_U], key[PJ2_U];
+#pragma unroll
+			for (int u = 0; u < PJ2_U; u++) {
+				const uint32_t t = i0 + u * 64 + lane;
+				// the run holding entry t: the last run starting at or before it
+				uint32_t r = 0;
+#pragma unroll
+				for (uint32_t st = 32; st > 0; st >>= 1)
+					r += ws[r + st] <= t ? st : 0;
+				idx[u] = t < tot ? wb[r] + (t - ws[r]) : ~0u;
+				key[u] = t < tot ? pkey[idx[u]] : 0u;
+			}
+#pragma unroll
+			for (int u = 0; u < PJ2_U; u++) {
+				uint32_t bb = gt_home(pj_hash(key[u]), pbits, nbp), m = 0;
+				for (;;) {
+					const ulonglong2 sl = bk[bb];
+					if (sl.x == 0ull)
+						break;
+					if ((uint32_t) sl.x == key[u]) {
+						m = (uint32_t) (sl.x >> 32);
+						break;
+					}
+					if (sl.y == 0ull)
+						break;
+					if ((uint32_t) sl.y == key[u]) {
+						m = (uint32_t) (sl.y >> 32);
+						break;
+					}
+					bb = bb + 1 == nbp ? 0 : bb + 1;
+				}
+				if (idx[u] != ~0u)
+					pans[idx[u]] = m;
+			}
+		}
+		__builtin_amdgcn_wave_barrier();      // ws / wb read before the next batch writes them
+	}
+}
+
+__global__ __launch_bounds__(1024) void
+k_pj2_restore(const uint16_t *prow, const uint32_t *pans, const uint16_t *poff, uint32_t P, BUN n, uint32_t nsub,
+	      Side L, Side R, uint32_t *ticket, uint64_t *status, uint64_t *meta, oid *r1, oid *r2)
+{
+	__shared__ uint32_t res[PJ_SUBROWS + PJ_SUBROWS / 32];
+	__shared__ uint32_t s_sub;
+	const unsigned tid = threadIdx.x;
+	if (tid == 0)
+		s_sub = atomicAdd(ticket, 1u);
+	for (uint32_t i = tid; i < PJ_SUBROWS + PJ_SUBROWS / 32; i += blockDim.x)
+		res[i] = 0;
+	__syncthreads();
+	const uint32_t sub = s_sub;
+	const BUN a = (BUN) sub * PJ_SUBROWS;
+	const uint32_t rows = (uint32_t) min((BUN) PJ_SUBROWS, n - a);
+	const uint32_t cnt = poff[(size_t) sub * (P + 1) + P];
+	constexpr int U = 8;
+	for (uint32_t j0 = tid; j0 < cnt; j0 += U * blockDim.x) {
+		uint32_t m[U], r[U];
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			const uint32_t j = j0 + u * blockDim.x;
+			m[u] = j < cnt ? pans[a + j] : 0u;
+			r[u] = j < cnt ? prow[a + j] : 0u;
+		}
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			if (m[u])
+				res[r[u] + (r[u] >> 5)] = m[u];
+	}
+	__syncthreads();
+	pj_emit(res, sub, a, rows, nsub, L, R, status, meta, r1, r2);
+}
+
 // one side cut into partitions: cnt/off matrices, partition bases, entries
 struct PjSide {
 	uint32_t nsub = 0;
@@ -1298,11 +1600,90 @@ pj_cut(const Side &S, BUN n, int pbits, bool skipnil, PjSide &o, uint32_t *maxto
 	return 0;
 }
 
+// the probe side of join_part with subtile-local runs (k_pj2_*); B = the
+// build side already cut (its largest partition in meta32[0], its nofit flag
+// in meta32[5], both checked here after the probe side's cut is queued)
+int
+join_part2(const Side &L, BUN nl, const Side &R, const PjSide &B, int pbits, bool nil_matches, mgdk_bat **ap,
+	   mgdk_bat **bp, bool *ukey)
+{
+	hipStream_t st = stream();
+	const uint32_t P = 1u << pbits;
+	uint32_t *meta32 = (uint32_t *) meta_buf();
+	uint64_t *meta = (uint64_t *) meta32 + 4;          // [0] pairs, [1] look-back error
+	uint32_t *h = (uint32_t *) pinned(64);
+	const uint32_t nsub = (uint32_t) ((nl + PJ_SUBROWS - 1) / PJ_SUBROWS);
+	const size_t rsz = (size_t) nsub * PJ_SUBROWS;
+	if (rsz >= ((size_t) 1 << 32))
+		return 1;                                   // entry indexes are 32-bit
+	DevBuf pkey(rsz * 4 + 64), prow(rsz * 2 + 64), pans(rsz * 4 + 64), poff((size_t) nsub * (P + 1) * 2 + 64),
+		poffT((size_t) nsub * (P + 1) * 2 + 64);
+	if (!pkey.p || !prow.p || !pans.p || !poff.p || !poffT.p)
+		return sync_fail();
+	static const bool cut_attr = hipFuncSetAttribute((const void *) k_pj2_cut,
+							 hipFuncAttributeMaxDynamicSharedMemorySize, (int) PJ2_CUT_LDS) == hipSuccess;
+	static const bool probe_attr = hipFuncSetAttribute((const void *) k_pj2_probe,
+							   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+	(void) cut_attr;
+	(void) probe_attr;
+	(void) hipGetLastError();
+	hipLaunchKernelGGL(k_pj2_cut, dim3(nsub), dim3(1024), PJ2_CUT_LDS, st, L, nl, pbits, !nil_matches,
+			   pkey.as<uint32_t>(), prow.as<uint16_t>(), poff.as<uint16_t>());
+	hipLaunchKernelGGL(k_pj2_offt, dim3((nsub + 63) / 64, (P + 1 + 63) / 64), dim3(256), 0, st, poff.as<uint16_t>(),
+			   nsub, P, poffT.as<uint16_t>());
+	if (!hip_ok(hipMemcpyAsync(h, meta32, 32, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+		return -1;
+	if (h[0] > PJ_MAXFILL || h[5])
+		return 1;                                   // oversized partition / build value without a 4-byte image
+	static const int lfpct = getenv("MGDK_PJ_LF") ? atoi(getenv("MGDK_PJ_LF")) : 80;
+	uint32_t nbp = (uint32_t) ((uint64_t) h[0] * 100 / (2 * (uint64_t) (lfpct < 40 ? 40 : lfpct > 95 ? 95 : lfpct))) + 1;
+	if (2 * nbp <= h[0])
+		nbp = h[0] / 2 + 1;
+	nbp = nbp < PJ_SLOTS / 2 ? nbp : PJ_SLOTS / 2;    // (h[0] <= PJ_MAXFILL keeps load < 3/4)
+	// two workgroups per CU when the table fits 80 KiB at <= 90 % load
+	constexpr uint32_t NBP2 = (80 * 1024 - 16 * 64 * 8) / 16;
+	static const bool occ2 = !getenv("MGDK_PJ2_OCC") || atoi(getenv("MGDK_PJ2_OCC")) != 0;
+	if (occ2 && nbp > NBP2 && (uint64_t) h[0] * 10 <= (uint64_t) 2 * NBP2 * 9)
+		nbp = NBP2;
+	const size_t lds = (size_t) nbp * 16 + 16 * 64 * 8;
+	hipLaunchKernelGGL(k_pj2_probe, dim3(P), dim3(1024), lds, st, B.ent->as<uint2>(), B.base->as<uint32_t>(),
+			   pkey.as<uint32_t>(), poffT.as<uint16_t>(), pbits, nbp, nsub, pans.as<uint32_t>(), &meta32[2]);
+	if (!hip_ok(hipMemcpyAsync(h, meta32, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+		return -1;
+	if (h[2])
+		return 1;                                   // duplicate build keys
+	mgdk_bat *ra = newbat(0, MGDK_oid, nl), *rb = newbat(0, MGDK_oid, nl);
+	const size_t sbytes = (nsub + 8) * sizeof(uint64_t);
+	char *sc = (char *) scratch(sbytes);
+	if (!ra || !rb || !sc || !hip_ok(hipMemsetAsync(sc, 0, sbytes, st), "memset")) {
+		unfix2(ra, rb);
+		return sync_fail();
+	}
+	hipLaunchKernelGGL(k_pj2_restore, dim3(nsub), dim3(1024), 0, st, prow.as<uint16_t>(), pans.as<uint32_t>(),
+			   poff.as<uint16_t>(), P, nl, nsub, L, R, (uint32_t *) sc, (uint64_t *) sc + 8, meta,
+			   (oid *) ra->theap, (oid *) rb->theap);
+	uint64_t *h64 = (uint64_t *) pinned(64);
+	if (!hip_ok(hipMemcpyAsync(h64, meta, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
+		unfix2(ra, rb);
+		return -1;
+	}
+	if (h64[1] & 1) {
+		seterr("HY013!BATjoin: look-back did not complete");
+		unfix2(ra, rb);
+		return -1;
+	}
+	ra->count = rb->count = h64[0];
+	*ukey = true;                                       // unique build keys: one match per row
+	*ap = ra;
+	*bp = rb;
+	return 0;
+}
+
 // returns 1 when not applicable (caller uses the open-addressing path)
 int
 join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_bat **ap, mgdk_bat **bp, bool *ukey)
 {
-	static const int mode = getenv("MGDK_JOIN_PART") ? atoi(getenv("MGDK_JOIN_PART")) : 1;
+	const int mode = getenv("MGDK_JOIN_PART") ? atoi(getenv("MGDK_JOIN_PART")) : 1;   // per call (tests)
 	const bool w4 = L.w == 4 && R.w == 4, w8 = L.w == 8 && R.w == 8 && L.base && R.base;
 	if (mode == 0 || !(w4 || w8) || nr < 65536)
 		return 1;
@@ -1327,9 +1708,14 @@ join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_b
 	PjSide B, Pr;
 	Side Rn = R;
 	Rn.nofit = &meta32[5];
-	if (pj_cut(Rn, nr, pbits, !nil_matches, B, &meta32[0]) < 0 ||
-	    pj_cut(L, nl, pbits, !nil_matches, Pr, &meta32[1]) < 0) {
+	if (pj_cut(Rn, nr, pbits, !nil_matches, B, &meta32[0]) < 0) {
 		(void) sync();                              // launched cuts still use the buffers
+		return -1;
+	}
+	if (mode != 3)
+		return join_part2(L, nl, R, B, pbits, nil_matches, ap, bp, ukey);
+	if (pj_cut(L, nl, pbits, !nil_matches, Pr, &meta32[1]) < 0) {
+		(void) sync();
 		return -1;
 	}
 	if (!hip_ok(hipMemcpyAsync(h, meta32, 32, hipMemcpyDeviceToHost, st), "memcpy") || !sync())

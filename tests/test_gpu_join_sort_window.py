@@ -83,10 +83,12 @@ def test_join_unique_build(gdk, ora, tname, dt):
     assert np.array_equal(b.to_numpy(), ob.values())
 
 
+@pytest.mark.parametrize("part", ["1", "3"])
 @pytest.mark.parametrize("nil_matches", [False, True])
 @pytest.mark.parametrize("case", ["plain", "cands", "dups", "date", "skew", "big", "big_cands", "big_dups",
                                   "big_skew"])
-def test_join_partitioned(gdk, ora, nil_matches, case):
+def test_join_partitioned(gdk, ora, nil_matches, case, part, monkeypatch):
+    monkeypatch.setenv("MGDK_JOIN_PART", part)     # the big cases: probe-side cut (see below)
     """4-byte keys, >= 64 Ki unique build rows: the global-table path (build
     side cut into per-partition LDS tables stored as one table, one ordered
     probe pass), nils on both sides, candidate lists, a duplicate build key
@@ -489,15 +491,16 @@ def test_sort_maltest_fixture(gdk):
                 assert [int(v) for v in order.to_numpy()] == c["order_oids"]
 
 
+@pytest.mark.parametrize("part", ["1", "3"])
 @pytest.mark.parametrize("case", ["fk", "probe_skew", "lng_cands", "sparse_hits"])
-def test_join_region_partitioned(gdk, ora, case):
-    """More than 2M unique build rows: the region-partitioned path (build side
-    as the global bucketed table, probe side cut into 128 coarse partitions
-    probed from one XCD's L2, restored by subtile).  An FK-shaped join of
-    12M x 3M (every row matches), a probe side with 60 % of its rows on one
-    key (its coarse partition overflows its capacity -> the radix-partitioned
-    path), 8-byte keys with candidate lists on both sides, and 1 % hits --
-    all bit-exact with the oracle."""
+def test_join_region_partitioned(gdk, ora, case, part, monkeypatch):
+    """More than 2M unique build rows: the radix-partitioned path, with the
+    probe side cut into subtile-local runs (MGDK_JOIN_PART=1, the default) or
+    into partition-major runs after a histogram pass ("3").  An FK-shaped
+    join of 12M x 3M (every row matches), a probe side with 60 % of its rows
+    on one key, 8-byte keys with candidate lists on both sides, and 1 % hits
+    -- all bit-exact with the oracle."""
+    monkeypatch.setenv("MGDK_JOIN_PART", part)
     r = rng(88)
     nr, nl = 3_000_017, 12_000_029
     dt, tp, otp = np.int32, gdk.TYPE_int, ora.TYPE_int

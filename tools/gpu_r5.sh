@@ -87,6 +87,14 @@ place)
 		timeout -k 10 120 tools/probes/place_probe $p >> $O/place.log 2>&1
 	done
 	;;
+joinlf)
+	for v in "80 1" "80 0" "65 0" "50 0"; do
+		set -- $v
+		MGDK_PJ_LF=$1 MGDK_PJ2_OCC=$2 timeout -k 10 200 python tools/opbench.py --only config3 > $O/opbench_lf$1_occ$2.json 2> $O/opbench_lf$1_occ$2.err
+	done
+	cd /tmp && cd $GRAFT_REPO_ROOT
+	MGDK_PJ_LF=50 MGDK_PJ2_OCC=0 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof50 -o run -- python3 tools/opbench.py --only config3 > $O/prof50.log 2>&1
+	;;
 *)
 	echo "unknown step $step"; exit 2
 	;;
