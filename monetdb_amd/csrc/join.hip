@@ -1297,6 +1297,9 @@ k_pj_restore(const uint2 *flat, const uint32_t *offT, uint32_t P, uint64_t total
 // ---------------------------------------------------------------------------
 
 constexpr size_t PJ2_CUT_LDS = ((size_t) (1u << PJ_MAXPBITS) + PJ_SUBROWS) * 4;
+// the probe's LDS: table buckets + the waves' run lists (16 x 64 x 8 B)
+constexpr uint32_t PJ2_MAXB = (160 * 1024 - 16 * 64 * 8) / 16;
+constexpr uint32_t PJ2_MAXFILL = PJ2_MAXB * 2 * 4 / 5;       // <= 80 % load
 
 __global__ __launch_bounds__(1024) void
 k_pj2_cut(Side s, BUN n, int pbits, bool skipnil, uint32_t *pkey, uint16_t *prow, uint16_t *poff)
@@ -1429,45 +1432,31 @@ k_pj2_offt(const uint16_t *poff, uint32_t nsub, uint32_t P, uint16_t *poffT)
 	}
 }
 
-constexpr int PJ2_U = 16;       // entries per lane in flight in the probe (a batch of 64 runs ~ 1000 entries)
+#ifndef PJ2_UV
+#define PJ2_UV 4
+#endif
+#ifndef PJ2_BUV
+#define PJ2_BUV 4
+#endif
+constexpr int PJ2_U = PJ2_UV;   // entries per lane in flight in the probe
 
-__global__ __launch_bounds__(1024) void
-k_pj2_probe(const uint2 *bent, const uint32_t *bbase, const uint32_t *pkey, const uint16_t *poffT, int pbits,
-	    uint32_t nbp, uint32_t nsub, uint32_t *pans, uint32_t *dupflag)
+// one batch of a wave: the runs of subtiles [s0, s0 + 64) in partition p.
+// Lane l loads the run bounds of subtile s0 + l; a wave scan of the run
+// lengths numbers the batch's entries, and lane l takes entries l, l + 64,
+// ... (the run holding entry t: a binary search over the 64 run starts in
+// LDS), so the key loads of one run are consecutive lanes.  All PJ2_U key
+// loads of a lane are issued here; idx = ~0 marks no entry.
+struct Pj2Batch {
+	uint32_t tot;
+	uint32_t idx[PJ2_U], key[PJ2_U];
+};
+
+__device__ __forceinline__ void
+pj2_issue(const uint32_t *pkey, const uint16_t *o0, const uint16_t *o1, uint32_t nsub, uint32_t s0, uint32_t *ws,
+	  uint32_t *wb, uint32_t i0, Pj2Batch &bt, bool scan)
 {
-	extern __shared__ __attribute__((aligned(16))) unsigned long long dyn2[];
-	unsigned long long *tab = dyn2;
-	uint32_t *wst = (uint32_t *) (dyn2 + 2 * nbp);            // [16][64] run starts in the wave's entry list
-	uint32_t *wbs = wst + 16 * 64;                            // [16][64] first index of each run (< 2^32)
-	const uint32_t p = xcd_block(blockIdx.x, gridDim.x), ns = 2 * nbp;
-	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
-	for (uint32_t i = tid; i < ns; i += blockDim.x)
-		tab[i] = 0ull;
-	__syncthreads();
-	const uint32_t b0 = bbase[p], b1 = bbase[p + 1];
-	bool dup = false;
-	for (uint32_t e = b0 + tid; e < b1; e += blockDim.x) {
-		const uint2 en = bent[e];
-		const unsigned long long v = ((unsigned long long) (en.y + 1) << 32) | en.x;
-		uint32_t h = 2 * gt_home(pj_hash(en.x), pbits, nbp);
-		for (;;) {
-			const unsigned long long o = atomicCAS(&tab[h], 0ull, v);
-			if (o == 0ull)
-				break;
-			if ((uint32_t) o == en.x) {
-				dup = true;
-				break;
-			}
-			h = h + 1 == ns ? 0 : h + 1;
-		}
-	}
-	if (__any(dup) && lane == 0)
-		atomicOr(dupflag, 1u);
-	__syncthreads();
-	const ulonglong2 *bk = (const ulonglong2 *) tab;
-	const uint16_t *o0 = poffT + (size_t) p * nsub, *o1 = poffT + (size_t) (p + 1) * nsub;
-	uint32_t *ws = wst + w * 64, *wb = wbs + w * 64;
-	for (uint32_t s0 = w * 64; s0 < nsub; s0 += 16 * 64) {
+	const unsigned lane = __lane_id();
+	if (scan) {
 		const uint32_t sb = s0 + lane;
 		uint32_t b = 0, len = 0;
 		if (sb < nsub) {
@@ -1481,49 +1470,139 @@ k_pj2_probe(const uint2 *bent, const uint32_t *bbase, const uint32_t *pkey, cons
 			if (lane >= (unsigned) o)
 				inc += u;
 		}
-		const uint32_t tot = __shfl(inc, 63);
+		bt.tot = __shfl(inc, 63);
+		__builtin_amdgcn_wave_barrier();      // the previous batch's reads of ws / wb are done
 		ws[lane] = inc - len;
 		wb[lane] = sb * PJ_SUBROWS + b;
 		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 		__builtin_amdgcn_wave_barrier();
 		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-		for (uint32_t i0 = 0; i0 < tot; i0 += 64 * PJ2_U) {
-			uint32_t idx[PJ2_U], key[PJ2_U];
+	}
 #pragma unroll
-			for (int u = 0; u < PJ2_U; u++) {
-				const uint32_t t = i0 + u * 64 + lane;
-				// the run holding entry t: the last run starting at or before it
-				uint32_t r = 0;
+	for (int u = 0; u < PJ2_U; u++) {
+		const uint32_t t = i0 + u * 64 + lane;
+		uint32_t r = 0;
 #pragma unroll
-				for (uint32_t st = 32; st > 0; st >>= 1)
-					r += ws[r + st] <= t ? st : 0;
-				idx[u] = t < tot ? wb[r] + (t - ws[r]) : ~0u;
-				key[u] = t < tot ? pkey[idx[u]] : 0u;
+		for (uint32_t st = 32; st > 0; st >>= 1)
+			r += ws[r + st] <= t ? st : 0;
+		bt.idx[u] = t < bt.tot ? wb[r] + (t - ws[r]) : ~0u;
+		bt.key[u] = t < bt.tot ? pkey[bt.idx[u]] : 0u;
+	}
+}
+
+__device__ __forceinline__ void
+pj2_answer(const ulonglong2 *bk, int pbits, uint32_t nbp, const Pj2Batch &bt, uint32_t *pans)
+{
+#pragma unroll
+	for (int u = 0; u < PJ2_U; u++) {
+		const uint32_t k = bt.key[u];
+		uint32_t bb = gt_home(pj_hash(k), pbits, nbp), m = 0;
+		for (;;) {
+			const ulonglong2 sl = bk[bb];
+			if (sl.x == 0ull)
+				break;
+			if ((uint32_t) sl.x == k) {
+				m = (uint32_t) (sl.x >> 32);
+				break;
 			}
+			if (sl.y == 0ull)
+				break;
+			if ((uint32_t) sl.y == k) {
+				m = (uint32_t) (sl.y >> 32);
+				break;
+			}
+			bb = bb + 1 == nbp ? 0 : bb + 1;
+		}
+		if (bt.idx[u] != ~0u)
+			pans[bt.idx[u]] = m;
+	}
+}
+
+constexpr int PJ2_BU = PJ2_BUV;  // build entries per thread per round, all loaded before any insert
+
+__global__ __launch_bounds__(1024) void
+k_pj2_probe(const uint2 *bent, const uint32_t *bbase, const uint32_t *pkey, const uint16_t *poffT, int pbits,
+	    uint32_t nbp, uint32_t nsub, uint32_t *pans, uint32_t *dupflag)
+{
+	extern __shared__ __attribute__((aligned(16))) unsigned long long dyn2[];
+	unsigned long long *tab = dyn2;
+	uint32_t *wst = (uint32_t *) (dyn2 + 2 * nbp);            // [16][64] run starts in the wave's entry list
+	uint32_t *wbs = wst + 16 * 64;                            // [16][64] first index of each run (< 2^32)
+	const uint32_t p = xcd_block(blockIdx.x, gridDim.x), ns = 2 * nbp;
+	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+	const uint16_t *o0 = poffT + (size_t) p * nsub, *o1 = poffT + (size_t) (p + 1) * nsub;
+	uint32_t *ws = wst + w * 64, *wb = wbs + w * 64;
+	for (uint32_t i = tid; i < ns; i += blockDim.x)
+		tab[i] = 0ull;
+	// the first batch's run bounds and key loads go out before the table is
+	// built, so their latency hides behind the build
+	Pj2Batch bt;
+	uint32_t s0 = w * 64;
+	if (s0 < nsub)
+		pj2_issue(pkey, o0, o1, nsub, s0, ws, wb, 0, bt, true);
+	// a build partition above 90 % of the table (the host sized it for the
+	// expected largest one) is flagged and not built: its runs are answered
+	// "no match" and the host falls back after the restore
+	const uint32_t b0 = bbase[p], over = (bbase[p + 1] - b0) * 10 > ns * 9;
+	const uint32_t b1 = over ? b0 : bbase[p + 1];
+	if (over && tid == 0)
+		atomicOr(dupflag, 2u);
+	bool dup = false;
+	uint2 en[PJ2_BU];
+	uint32_t e0 = b0 + tid;
 #pragma unroll
-			for (int u = 0; u < PJ2_U; u++) {
-				uint32_t bb = gt_home(pj_hash(key[u]), pbits, nbp), m = 0;
-				for (;;) {
-					const ulonglong2 sl = bk[bb];
-					if (sl.x == 0ull)
-						break;
-					if ((uint32_t) sl.x == key[u]) {
-						m = (uint32_t) (sl.x >> 32);
-						break;
-					}
-					if (sl.y == 0ull)
-						break;
-					if ((uint32_t) sl.y == key[u]) {
-						m = (uint32_t) (sl.y >> 32);
-						break;
-					}
-					bb = bb + 1 == nbp ? 0 : bb + 1;
+	for (int u = 0; u < PJ2_BU; u++) {
+		const uint32_t e = e0 + u * blockDim.x;
+		en[u] = e < b1 ? bent[e] : make_uint2(0, 0);
+	}
+	__syncthreads();                              // the table is zeroed
+	while (e0 < b1) {
+#pragma unroll
+		for (int u = 0; u < PJ2_BU; u++) {
+			if (e0 + u * blockDim.x >= b1)
+				continue;
+			const unsigned long long v = ((unsigned long long) (en[u].y + 1) << 32) | en[u].x;
+			uint32_t h = 2 * gt_home(pj_hash(en[u].x), pbits, nbp);
+			for (;;) {
+				const unsigned long long o = atomicCAS(&tab[h], 0ull, v);
+				if (o == 0ull)
+					break;
+				if ((uint32_t) o == en[u].x) {
+					dup = true;
+					break;
 				}
-				if (idx[u] != ~0u)
-					pans[idx[u]] = m;
+				h = h + 1 == ns ? 0 : h + 1;
 			}
 		}
-		__builtin_amdgcn_wave_barrier();      // ws / wb read before the next batch writes them
+		e0 += PJ2_BU * blockDim.x;
+#pragma unroll
+		for (int u = 0; u < PJ2_BU; u++) {
+			const uint32_t e = e0 + u * blockDim.x;
+			en[u] = e < b1 ? bent[e] : make_uint2(0, 0);
+		}
+	}
+	if (__any(dup) && lane == 0)
+		atomicOr(dupflag, 1u);
+	__syncthreads();
+	const ulonglong2 *bk = (const ulonglong2 *) tab;     // (an empty table when over)
+	// software pipeline: the next chunk's key loads (and, at a batch
+	// boundary, the next batch's run bounds) are issued before the current
+	// chunk is answered
+	uint32_t ci0 = 0;
+	while (s0 < nsub) {
+		uint32_t ns0 = s0, ni0 = ci0 + 64 * PJ2_U;
+		if (ni0 >= bt.tot) {
+			ns0 = s0 + 16 * 64;
+			ni0 = 0;
+		}
+		Pj2Batch nx;
+		nx.tot = bt.tot;
+		if (ns0 < nsub)
+			pj2_issue(pkey, o0, o1, nsub, ns0, ws, wb, ni0, nx, ni0 == 0);
+		pj2_answer(bk, pbits, nbp, bt, pans);
+		bt = nx;
+		s0 = ns0;
+		ci0 = ni0;
 	}
 }
 
@@ -1604,7 +1683,7 @@ pj_cut(const Side &S, BUN n, int pbits, bool skipnil, PjSide &o, uint32_t *maxto
 // build side already cut (its largest partition in meta32[0], its nofit flag
 // in meta32[5], both checked here after the probe side's cut is queued)
 int
-join_part2(const Side &L, BUN nl, const Side &R, const PjSide &B, int pbits, bool nil_matches, mgdk_bat **ap,
+join_part2(const Side &L, BUN nl, const Side &R, BUN nr, const PjSide &B, int pbits, bool nil_matches, mgdk_bat **ap,
 	   mgdk_bat **bp, bool *ukey)
 {
 	hipStream_t st = stream();
@@ -1631,27 +1710,30 @@ join_part2(const Side &L, BUN nl, const Side &R, const PjSide &B, int pbits, boo
 			   pkey.as<uint32_t>(), prow.as<uint16_t>(), poff.as<uint16_t>());
 	hipLaunchKernelGGL(k_pj2_offt, dim3((nsub + 63) / 64, (P + 1 + 63) / 64), dim3(256), 0, st, poff.as<uint16_t>(),
 			   nsub, P, poffT.as<uint16_t>());
-	if (!hip_ok(hipMemcpyAsync(h, meta32, 32, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
-		return -1;
-	if (h[0] > PJ_MAXFILL || h[5])
-		return 1;                                   // oversized partition / build value without a 4-byte image
+	// the table is sized for the expected largest build partition (mean + 6
+	// sigma) instead of the measured one, so no round trip is needed between
+	// the passes: a larger partition, a duplicate build key or a build value
+	// without a 4-byte image is flagged on the device, read back once after
+	// the restore, and sends the join to the fallback
+	const double mean = (double) nr / P;
+	const uint32_t est = (uint32_t) (mean + 6.0 * sqrt(mean)) + 1;
+	if (est > PJ2_MAXFILL) {
+		(void) sync();                              // the cuts still use the buffers
+		return 1;
+	}
 	static const int lfpct = getenv("MGDK_PJ_LF") ? atoi(getenv("MGDK_PJ_LF")) : 80;
-	uint32_t nbp = (uint32_t) ((uint64_t) h[0] * 100 / (2 * (uint64_t) (lfpct < 40 ? 40 : lfpct > 95 ? 95 : lfpct))) + 1;
-	if (2 * nbp <= h[0])
-		nbp = h[0] / 2 + 1;
-	nbp = nbp < PJ_SLOTS / 2 ? nbp : PJ_SLOTS / 2;    // (h[0] <= PJ_MAXFILL keeps load < 3/4)
+	uint32_t nbp = (uint32_t) ((uint64_t) est * 100 / (2 * (uint64_t) (lfpct < 40 ? 40 : lfpct > 95 ? 95 : lfpct))) + 1;
+	if (2 * nbp <= est)
+		nbp = est / 2 + 1;
+	nbp = nbp < PJ2_MAXB ? nbp : PJ2_MAXB;             // (est <= PJ2_MAXFILL keeps load <= 4/5)
 	// two workgroups per CU when the table fits 80 KiB at <= 90 % load
 	constexpr uint32_t NBP2 = (80 * 1024 - 16 * 64 * 8) / 16;
 	static const bool occ2 = !getenv("MGDK_PJ2_OCC") || atoi(getenv("MGDK_PJ2_OCC")) != 0;
-	if (occ2 && nbp > NBP2 && (uint64_t) h[0] * 10 <= (uint64_t) 2 * NBP2 * 9)
+	if (occ2 && nbp > NBP2 && (uint64_t) est * 10 <= (uint64_t) 2 * NBP2 * 9)
 		nbp = NBP2;
 	const size_t lds = (size_t) nbp * 16 + 16 * 64 * 8;
 	hipLaunchKernelGGL(k_pj2_probe, dim3(P), dim3(1024), lds, st, B.ent->as<uint2>(), B.base->as<uint32_t>(),
 			   pkey.as<uint32_t>(), poffT.as<uint16_t>(), pbits, nbp, nsub, pans.as<uint32_t>(), &meta32[2]);
-	if (!hip_ok(hipMemcpyAsync(h, meta32, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
-		return -1;
-	if (h[2])
-		return 1;                                   // duplicate build keys
 	mgdk_bat *ra = newbat(0, MGDK_oid, nl), *rb = newbat(0, MGDK_oid, nl);
 	const size_t sbytes = (nsub + 8) * sizeof(uint64_t);
 	char *sc = (char *) scratch(sbytes);
@@ -1662,10 +1744,17 @@ join_part2(const Side &L, BUN nl, const Side &R, const PjSide &B, int pbits, boo
 	hipLaunchKernelGGL(k_pj2_restore, dim3(nsub), dim3(1024), 0, st, prow.as<uint16_t>(), pans.as<uint32_t>(),
 			   poff.as<uint16_t>(), P, nl, nsub, L, R, (uint32_t *) sc, (uint64_t *) sc + 8, meta,
 			   (oid *) ra->theap, (oid *) rb->theap);
-	uint64_t *h64 = (uint64_t *) pinned(64);
-	if (!hip_ok(hipMemcpyAsync(h64, meta, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
+	// meta32[2]: duplicate build key (1) / oversized partition (2);
+	// meta32[5]: build value without a 4-byte image; meta = meta32 + 8
+	if (!hip_ok(hipMemcpyAsync(h, meta32, 48, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
 		unfix2(ra, rb);
 		return -1;
+	}
+	uint64_t h64[2];
+	memcpy(h64, h + 8, 16);
+	if (h[2] || h[5]) {
+		unfix2(ra, rb);
+		return 1;
 	}
 	if (h64[1] & 1) {
 		seterr("HY013!BATjoin: look-back did not complete");
@@ -1693,9 +1782,19 @@ join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_b
 	// the expected largest partition (mean + 6 sigma) must fit the LDS table
 	while (pbits < PJ_MAXPBITS && (double) nr / (1u << pbits) + 6.0 * sqrt((double) nr / (1u << pbits)) > PJ_MAXFILL)
 		pbits++;
-	const uint32_t P = 1u << pbits;
-	if ((double) nr / P + 6.0 * sqrt((double) nr / P) > PJ_MAXFILL)
+	if ((double) nr / (1u << pbits) + 6.0 * sqrt((double) nr / (1u << pbits)) > PJ_MAXFILL)
 		return 1;
+	// the subtile-local probe side (mode != 3) can take partitions up to
+	// PJ2_MAXFILL: MGDK_PJ2_PB = partition bits below the default
+	// (halving the partitions doubles the probe's runs)
+	const int pbd = mode != 3 && getenv("MGDK_PJ2_PB") ? atoi(getenv("MGDK_PJ2_PB")) : 0;
+	for (int k = 0; k < pbd && pbits > 6; k++) {
+		const double m = (double) nr / (1u << (pbits - 1));
+		if (m + 6.0 * sqrt(m) > PJ2_MAXFILL)
+			break;
+		pbits--;
+	}
+	const uint32_t P = 1u << pbits;
 	hipStream_t st = stream();
 	uint32_t *meta32 = (uint32_t *) meta_buf();
 	uint64_t *meta = (uint64_t *) meta32 + 4;          // [0] pairs, [1] look-back error
@@ -1713,7 +1812,7 @@ join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_b
 		return -1;
 	}
 	if (mode != 3)
-		return join_part2(L, nl, R, B, pbits, nil_matches, ap, bp, ukey);
+		return join_part2(L, nl, R, nr, B, pbits, nil_matches, ap, bp, ukey);
 	if (pj_cut(L, nl, pbits, !nil_matches, Pr, &meta32[1]) < 0) {
 		(void) sync();
 		return -1;

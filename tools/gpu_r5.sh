@@ -95,6 +95,27 @@ joinlf)
 	cd /tmp && cd $GRAFT_REPO_ROOT
 	MGDK_PJ_LF=50 MGDK_PJ2_OCC=0 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof50 -o run -- python3 tools/opbench.py --only config3 > $O/prof50.log 2>&1
 	;;
+joinpb)
+	timeout -k 10 600 $T -x tests/test_gpu_join_sort_window.py -k "partitioned" > $O/tests.log 2>&1
+	for v in ${PBV:-"0 80" "1 80" "1 70"}; do
+		set -- $v
+		MGDK_PJ2_PB=$1 MGDK_PJ_LF=$2 timeout -k 10 200 python tools/opbench.py --only config3 > $O/opbench_pb$1_lf$2.json 2> $O/opbench_pb$1_lf$2.err
+	done
+	cd /tmp && cd $GRAFT_REPO_ROOT
+	MGDK_PJ2_PB=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 tools/opbench.py --only config3 > $O/prof.log 2>&1
+	;;
+joinpmc)
+	cd /tmp && cd $GRAFT_REPO_ROOT
+	timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD --output-format csv -d $O/pmc_sq -o run -- python3 tools/opbench.py --only config3 > $O/pmc_sq.log 2>&1
+	timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f -o run -- python3 tools/opbench.py --only config3 > $O/pmc_f.log 2>&1
+	timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_w -o run -- python3 tools/opbench.py --only config3 > $O/pmc_w.log 2>&1
+	;;
+joinvar)
+	# join variants (tools/variant_build.py): opbench config3 per variant
+	for v in $JVARS; do
+		MGDK_LIB=$PWD/tools/variants/libmgdk_$v.so timeout -k 10 200 python tools/opbench.py --only config3 > $O/opbench_$v.json 2> $O/opbench_$v.err
+	done
+	;;
 *)
 	echo "unknown step $step"; exit 2
 	;;
