@@ -218,6 +218,9 @@ constexpr BUN GL_FTILE = 8192;
 #endif
 #ifndef MGDK_GL_NT_LOAD
 #define MGDK_GL_NT_LOAD 1
+#endif
+#ifndef MGDK_GL_CSTORE
+#define MGDK_GL_CSTORE 1          // ids stored as whole 1-KiB pieces per wave instruction
 #endif            // rows per workgroup of the first-occurrence pass
 
 __device__ __forceinline__ uint64_t
@@ -736,6 +739,29 @@ k_gl_assign_v32(KeySrc s, BUN n, const unsigned long long *gkey, const uint32_t 
 			}
 			if (r0 + V <= e) {
 				typedef unsigned long long o2 __attribute__((ext_vector_type(2)));
+#if MGDK_GL_CSTORE
+				// the wave's 256 ids as two 1-KiB pieces: store q takes rows
+				// 128 q + 2 l, 2 l + 1 of the wave, held by lane 32 q + l / 2
+				// (elements 2 (l & 1), + 1) -- one contiguous run per store
+				// instruction instead of 16-B pieces at a 32-B stride
+				const BUN wbase = r0 - (BUN) (tid & 63) * V;
+				if (wbase + 256 <= e) {
+					const unsigned l = tid & 63;
+#pragma unroll
+					for (int q = 0; q < 2; q++) {
+						const int src = 32 * q + (int) (l >> 1);
+						const uint32_t a0 = __shfl(g[0], src), a1 = __shfl(g[1], src);
+						const uint32_t a2 = __shfl(g[2], src), a3 = __shfl(g[3], src);
+						const bool odd = l & 1;
+						const o2 val = (o2){odd ? a2 : a0, odd ? a3 : a1};
+#if MGDK_GL_NT_STORE
+						__builtin_nontemporal_store(val, (o2 *) (gid + wbase + 128 * q + 2 * l));
+#else
+						*(o2 *) (gid + wbase + 128 * q + 2 * l) = val;
+#endif
+					}
+				} else
+#endif
 #pragma unroll
 				for (int u = 0; u < V; u += 2) {
 #if MGDK_GL_NT_STORE

@@ -116,6 +116,11 @@ joinvar)
 		MGDK_LIB=$PWD/tools/variants/libmgdk_$v.so timeout -k 10 200 python tools/opbench.py --only config3 > $O/opbench_$v.json 2> $O/opbench_$v.err
 	done
 	;;
+grpvar)
+	for v in $GVARS; do
+		MGDK_LIB=$PWD/tools/variants/libmgdk_$v.so timeout -k 10 200 python tools/selgrp_trace.py > $O/selgrp_$v.json 2> $O/selgrp_$v.err
+	done
+	;;
 *)
 	echo "unknown step $step"; exit 2
 	;;
