@@ -31,6 +31,9 @@ namespace {
 constexpr int GSU = 8;                 // rows per lane
 constexpr BUN GST = 256 * GSU;         // rows per tile
 constexpr int GS_MAXV = 4;
+#ifndef GS_STAGE
+#define GS_STAGE 1       // group outputs staged in LDS and stored as runs (0: per-lane stores)
+#endif
 
 template <int NV>
 struct GsPart {
@@ -226,8 +229,12 @@ k_gs_sums(const typename KT<KW>::T *k, const void *const *vals, BUN n, oid hseq,
 	__shared__ GsPart<NV> s_wtot[4];
 	__shared__ int s_wflag[4];
 	__shared__ uint32_t s_wst[4];
-	__shared__ T s_k[4][512];
-	__shared__ V s_v[NV][4][512];
+	// the rows' staging area (s_k, s_v), reused once the rows are in
+	// registers for the tile's group outputs
+	constexpr size_t KBY = 4 * 512 * sizeof(T), VBY = (size_t) NV * 4 * 512 * sizeof(V);
+	__shared__ __attribute__((aligned(16))) unsigned char s_raw[KBY + VBY];
+	T (*s_k)[512] = (T (*)[512]) s_raw;
+	V (*s_v)[4][512] = (V (*)[4][512]) (s_raw + KBY);
 	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
 	const BUN t = blockIdx.x;
 	const BUN t0 = t * GST, l0 = t0 + (BUN) tid * GSU, r0 = t0 + (BUN) w * 512;
@@ -303,7 +310,32 @@ k_gs_sums(const typename KT<KW>::T *k, const void *const *vals, BUN n, oid hseq,
 	uint32_t lpre = xs - ns;
 	for (unsigned q = 0; q < w; q++)
 		lpre += s_wst[q];
-	const bool tile_has_start = (s_wst[0] + s_wst[1] + s_wst[2] + s_wst[3]) != 0;
+	const uint32_t tst = s_wst[0] + s_wst[1] + s_wst[2] + s_wst[3];
+	const bool tile_has_start = tst != 0;
+	// the groups starting in the tile, [tbase, tbase + tst), are written by
+	// this tile only (ext / key all of them, hist / sums all but the last,
+	// which the tail edge record carries): staged in LDS (the rows are in
+	// registers since the barrier above) and stored as contiguous runs
+	// after the tile, when they fit
+	constexpr uint32_t GCAP = (uint32_t) ((KBY + VBY) / (24 + 16 * NV)) & ~1u;
+	const bool stg = GS_STAGE && tst <= GCAP;
+	oid *l_ext = (oid *) s_raw;
+	int64_t *l_key = (int64_t *) (s_raw + 8 * GCAP), *l_hist = (int64_t *) (s_raw + 16 * GCAP);
+	hge *l_sum = (hge *) (s_raw + 24 * GCAP);     // [NV][GCAP]
+	auto put = [&](unsigned long long g, const GsPart<NV> &p) -> uint32_t {
+		const uint64_t j = g - tbase;
+		if (!stg || j >= tst)
+			return gs_put<NV>(o, g, p);
+		uint32_t f = 0;
+		l_hist[j] = (int64_t) p.cnt;
+#pragma unroll
+		for (int v = 0; v < NV; v++) {
+			const bool nil = p.nn[v] == 0;
+			l_sum[(size_t) v * GCAP + j] = nil ? NilOf<hge>::v() : p.s[v];
+			f |= nil ? 2u : 0u;
+		}
+		return f;
+	};
 	// group id of the lane's rows: tbase + (starts in the tile up to the row) - 1
 	uint64_t gcur = tbase + lpre - 1;
 	if (live) {
@@ -312,15 +344,21 @@ k_gs_sums(const typename KT<KW>::T *k, const void *const *vals, BUN n, oid hseq,
 			const BUN i = l0 + u;
 			if (st[u]) {
 				if (seen)
-					of |= gs_put<NV>(o, gcur, cur);   // a run inside the lane
+					of |= put(gcur, cur);             // a run inside the lane
 				else
 					pre = cur;
 				seen = true;
 				cur.clear();
 				gcur++;
-				o.ext[gcur] = hseq + i;
 				// the key widened to lng (nil stays nil), as dist_group_aggr's widen
-				o.key[gcur] = KW == 4 && is_nil((int32_t) x[u]) ? INT64_MIN : (int64_t) x[u];
+				const int64_t kw = KW == 4 && is_nil((int32_t) x[u]) ? INT64_MIN : (int64_t) x[u];
+				if (stg) {
+					l_ext[gcur - tbase] = hseq + i;
+					l_key[gcur - tbase] = kw;
+				} else {
+					o.ext[gcur] = hseq + i;
+					o.key[gcur] = kw;
+				}
 			}
 			if (i < n) {
 				cur.cnt++;
@@ -385,7 +423,7 @@ k_gs_sums(const typename KT<KW>::T *k, const void *const *vals, BUN n, oid hseq,
 		GsPart<NV> tot = Sin;
 		tot.add(pre);
 		if (before)
-			of |= gs_put<NV>(o, tbase + lpre - 1, tot);
+			of |= put(tbase + lpre - 1, tot);
 		else
 			edges[2 * t] = GsEdge<NV>{tbase - 1, tot};      // the tile's head group
 	}
@@ -398,6 +436,19 @@ k_gs_sums(const typename KT<KW>::T *k, const void *const *vals, BUN n, oid hseq,
 			edges[2 * t + 1] = GsEdge<NV>{tbase - 1, z};
 		} else {
 			edges[2 * t + 1] = GsEdge<NV>{tbase + lpre + ns - 1, S};   // the tile's last group
+		}
+	}
+	if (stg) {
+		__syncthreads();
+		for (uint32_t j = tid; j < tst; j += 256) {
+			o.ext[tbase + j] = l_ext[j];
+			o.key[tbase + j] = l_key[j];
+		}
+		for (uint32_t j = tid; j + 1 < tst; j += 256) {
+			o.hist[tbase + j] = l_hist[j];
+#pragma unroll
+			for (int v = 0; v < NV; v++)
+				o.sum[v][tbase + j] = l_sum[(size_t) v * GCAP + j];
 		}
 	}
 	for (int q = 32; q > 0; q >>= 1)
@@ -573,14 +624,15 @@ mgdk_group_sums_ordered(mgdk_bat **extents, mgdk_bat **histo, mgdk_bat **keys, m
 	hipStream_t st = stream();
 	const int kw = b->twidth, vw = vals[0]->twidth;
 	const BUN nt = (n + GST - 1) / GST;
-	// fused (default): the tile's first group id comes from the look-back
-	// inside the sums pass, so the keys are read once; the outputs are sized
-	// for n groups (56 B per row at two sums, capped at 48 GiB) and the count
-	// is the last tile's inclusive prefix.  Two-pass (MGDK_GS_FUSED=0, above
-	// the cap, or when a look-back did not complete): a count pass + scan
-	// first, outputs sized exactly.  (Fused with a tile ticket was slower than
-	// two-pass: 6.47 vs 5.40 ms at SF100, profiles/r05/gsums/.)
-	const bool fused_on = !getenv("MGDK_GS_FUSED") || atoi(getenv("MGDK_GS_FUSED")) != 0;   // read per call (tests)
+	// two-pass (default): a count pass + scan first, outputs sized exactly.
+	// Fused (MGDK_GS_FUSED=1): the tile's first group id comes from the
+	// look-back inside the sums pass, so the keys are read once; the outputs
+	// are sized for n groups (56 B per row at two sums, capped at 48 GiB) and
+	// the count is the last tile's inclusive prefix; a look-back that did not
+	// complete reruns two-pass.  With the outputs staged in LDS the fused form
+	// is the slower one (5.67 vs 4.65 ms at SF100, profiles/r05/gsums/: the
+	// tiles' stores wait on the look-back); before staging it was 6.09 vs 6.30.
+	const bool fused_on = getenv("MGDK_GS_FUSED") && atoi(getenv("MGDK_GS_FUSED")) != 0;   // read per call (tests)
 	bool fused = fused_on && nt < 0xffffffffull && n * (24 + 16 * (BUN) nvals) <= ((BUN) 48 << 30);
 	DevBuf vp(64);
 	const size_t esz = sizeof(GsEdge<GS_MAXV>);
