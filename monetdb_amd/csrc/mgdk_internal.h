@@ -151,6 +151,11 @@ mgdk_bat *cand_finish(mgdk_bat *bn, BUN n);
 int exclusive_scan(const uint32_t *in, uint32_t *out, BUN n, uint64_t *total);
 int exclusive_scan(const uint32_t *in, uint64_t *out, BUN n, uint64_t *total);
 int exclusive_scan(const uint8_t *in, uint64_t *out, BUN n, uint64_t *total);
+// the same without waiting for the stream: ws (scan_ws_words(n) words, owned
+// by the caller until its next sync) receives the total at ws[2] and the
+// look-back error flag at ws[3] (low 32 bits)
+BUN scan_ws_words(BUN n);
+int exclusive_scan_nosync(const uint32_t *in, uint64_t *out, BUN n, uint64_t *ws);
 
 // stable LSD radix sort of (key, payload) pairs in place (sort.hip); keys
 // are order-preserving unsigned images; `bits` = significant key bits.

@@ -144,6 +144,22 @@ k_scan(const TI *in, TO *out, BUN n, uint64_t *status, uint32_t *ticket, uint32_
 
 template <typename TI, typename TO>
 int
+scan_launch(const TI *in, TO *out, BUN n, uint64_t *ws)
+{
+	const uint64_t per = 256 * ITEMS;
+	const uint64_t ntiles = (n + per - 1) / per;
+	uint32_t *ticket = (uint32_t *) ws;
+	uint64_t *status = ws + 8;
+	hipStream_t s = stream();
+	if (!hip_ok(hipMemsetAsync(ws, 0, (ntiles + 16) * 8, s), "memset"))
+		return -1;
+	hipLaunchKernelGGL((k_scan<TI, TO>), dim3((unsigned) ntiles), dim3(256), 0, s, in, out, n, status, ticket,
+			   (uint32_t) ntiles, ws + 2, (uint32_t *) (ws + 3));
+	return 0;
+}
+
+template <typename TI, typename TO>
+int
 scan_impl(const TI *in, TO *out, BUN n, uint64_t *total_host)
 {
 	if (n == 0) {
@@ -180,6 +196,20 @@ scan_impl(const TI *in, TO *out, BUN n, uint64_t *total_host)
 }  // namespace
 
 namespace mgdk {
+
+BUN
+scan_ws_words(BUN n)
+{
+	return (n + 256 * ITEMS - 1) / (256 * ITEMS) + 16;
+}
+
+int
+exclusive_scan_nosync(const uint32_t *in, uint64_t *out, BUN n, uint64_t *ws)
+{
+	if (n == 0)
+		return hip_ok(hipMemsetAsync(ws, 0, 32, stream()), "memset") ? 0 : -1;
+	return scan_launch<uint32_t, uint64_t>(in, out, n, ws);
+}
 
 int
 exclusive_scan(const uint32_t *in, uint32_t *out, BUN n, uint64_t *total)

@@ -240,7 +240,7 @@ template <typename K, bool FINAL, bool IDV, bool LB, bool SEG>
 __global__ __launch_bounds__(Tile<K>::THREADS) void
 k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32_t *offs, uint32_t nblocks,
 	     K *kout, uint32_t *vout, FinalOut fo, uint32_t *ticket, uint64_t *status, const uint32_t *gdig,
-	     uint32_t *err, SegTiles sg, uint32_t xg)
+	     uint32_t *err, SegTiles sg, uint32_t xg, uint64_t *znext)
 {
 	constexpr int SWAVES = Tile<K>::W, SROWS = Tile<K>::R, STHREADS = Tile<K>::THREADS, STILE = Tile<K>::N;
 	__shared__ K sk[STILE];
@@ -268,6 +268,10 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 	}
 	if (LB && blk == ~0u)
 		return;     // cannot happen: one tile per workgroup
+	// the next LSD pass's look-back status of this tile, zeroed here (the
+	// passes alternate between two status arrays: no memset between them)
+	if (LB && znext != nullptr && dig)
+		znext[(size_t) blk * 256 + tid] = 0ull;
 	const BUN tbase = SEG ? (BUN) sd.x : (BUN) blk * STILE;
 	const BUN tend = SEG ? tbase + sd.y : n;
 	__shared__ uint32_t lh[256];          // LB: the tile's digit counts, published before ranking
@@ -1151,7 +1155,8 @@ radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, int s1, int s2, ui
 	    !hip_ok(hipMemsetAsync(ovf.p, 0, 4, st), "memset"))
 		return -1;
 	hipLaunchKernelGGL((k_rs_scatter<K, false, true, true, false>), dim3(nblocks), dim3(Tile<K>::THREADS), 0, st, k0,
-			   v0, n, s1, nullptr, nblocks, k1, v1, none, lbm, status, gd1, lbm + 4, SegTiles{}, sort_xg((int) sizeof(K)));
+			   v0, n, s1, nullptr, nblocks, k1, v1, none, lbm, status, gd1, lbm + 4, SegTiles{}, sort_xg((int) sizeof(K)),
+			   nullptr);
 	// pass B: by d2 inside the d1 buckets
 	hipLaunchKernelGGL(k_seg_tiles, dim3(1), dim3(256), 0, st, cnt1, gd1, TILE, desc.as<uint4>(), count, bfirst,
 			   bnt);
@@ -1162,7 +1167,7 @@ radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, int s1, int s2, ui
 		return -1;
 	hipLaunchKernelGGL((k_rs_scatter<K, false, false, false, true>), dim3(tmax), dim3(Tile<K>::THREADS), 0, st,
 			   (const K *) k1, (const uint32_t *) v1, n, s2, offs.as<uint32_t>(), tmax, k0, v0, none, lbm,
-			   status, gd1, lbm + 4, sg, sort_xg((int) sizeof(K)));
+			   status, gd1, lbm + 4, sg, sort_xg((int) sizeof(K)), nullptr);
 	// pass C: the remaining varying bits, 4 at a time, inside each (d1, d2) bucket
 	// the remaining bits in 8-bit LSD digits (the top one may reach into d2,
 	// constant inside a bucket)
@@ -1290,16 +1295,23 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 	static const bool use_lb = getenv("MGDK_SORT_LB") ? atoi(getenv("MGDK_SORT_LB")) != 0 : true;
 	const bool lb = use_lb && !shifts.empty() && shifts.size() <= (size_t) RS_MAXP;
 	DevBuf hist(lb ? 64 : (size_t) 256 * nblocks * 4), offs(lb ? 64 : (size_t) 256 * nblocks * 4);
-	DevBuf status(lb ? (size_t) 256 * nblocks * 8 : 64), dcnt(RS_MAXP * 256 * 4 * 2 + 64), lbm(64);
-	if (!hist.p || !offs.p || !status.p || !dcnt.p || !lbm.p)
+	// look-back state: two status arrays (pass s uses status[s % 2] and
+	// zeroes status[(s + 1) % 2] for the next pass), ticket words per pass
+	// (16 words each: ticket, -, -, -, -, ..., 8 XCD tickets), the error flag
+	// after them -- zeroed once, not per pass
+	DevBuf status(lb ? (size_t) 256 * nblocks * 8 : 64), status2(lb && shifts.size() > 1 ? (size_t) 256 * nblocks * 8 : 64),
+		dcnt(RS_MAXP * 256 * 4 * 2 + 64), lbm(64 * (RS_MAXP + 1));
+	if (!hist.p || !offs.p || !status.p || !status2.p || !dcnt.p || !lbm.p)
 		return -1;
+	uint32_t *lb_err = lbm.as<uint32_t>() + 16 * RS_MAXP + 4;
 	uint32_t *gdig = dcnt.as<uint32_t>() + RS_MAXP * 256;
 	if (lb) {
 		Shifts sh{};
 		sh.n = (int) shifts.size();
 		for (int q = 0; q < sh.n; q++)
 			sh.s[q] = shifts[q];
-		if (!hip_ok(hipMemsetAsync(lbm.p, 0, 64, st), "memset"))
+		if (!hip_ok(hipMemsetAsync(lbm.p, 0, 64 * (RS_MAXP + 1), st), "memset") ||
+		    !hip_ok(hipMemsetAsync(status.p, 0, (size_t) 256 * nblocks * 8, st), "memset"))
 			return -1;
 		const uint32_t *dh = digit_hist;
 		if (dh == nullptr) {
@@ -1368,12 +1380,9 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 		const int shift = shifts[s];
 		const bool fin = fo != nullptr && s + 1 == shifts.size();
 		const bool idv = positions && s == 0;
-		if (lb) {
-			if (!hip_ok(hipMemsetAsync(status.p, 0, (size_t) 256 * nblocks * 8, st), "memset") ||
-			    !hip_ok(hipMemsetAsync(lbm.p, 0, 8, st), "memset") ||
-			    !hip_ok(hipMemsetAsync(lbm.as<uint32_t>() + 8, 0, 32, st), "memset"))
-				return -1;
-		} else {
+		uint64_t *sts = (s & 1 ? status2 : status).as<uint64_t>();
+		uint64_t *znx = lb && s + 1 < shifts.size() ? (s & 1 ? status : status2).as<uint64_t>() : nullptr;
+		if (!lb) {
 			hipLaunchKernelGGL((k_rs_hist<K>), dim3(nblocks), dim3(256), 0, st, kin, n, shift,
 					   hist.as<uint32_t>(), nblocks);
 			if (exclusive_scan(hist.as<uint32_t>(), offs.as<uint32_t>(), (BUN) 256 * nblocks, nullptr) < 0)
@@ -1382,11 +1391,11 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 		FinalOut f2 = fin ? *fo : none;
 		if (fin && f2.want_keys)
 			f2.keys = kout;
-		uint32_t *tk = lbm.as<uint32_t>(), *er = lbm.as<uint32_t>() + 4;
+		uint32_t *tk = lbm.as<uint32_t>() + 16 * s, *er = lb_err;
 		const uint32_t *gd = gdig + s * 256;
 #define SCAT(F, I, L) hipLaunchKernelGGL((k_rs_scatter<K, F, I, L, false>), dim3(nblocks), dim3(Tile<K>::THREADS), 0, st, kin, \
-					 vin, n, shift, offs.as<uint32_t>(), nblocks, kout, vout, f2, tk, status.as<uint64_t>(), gd, er, \
-					 SegTiles{}, sort_xg((int) sizeof(K)))
+					 vin, n, shift, offs.as<uint32_t>(), nblocks, kout, vout, f2, tk, sts, gd, er, \
+					 SegTiles{}, sort_xg((int) sizeof(K)), znx)
 		if (lb) {
 			if (fin) {
 				if (idv) SCAT(true, true, true); else SCAT(true, false, true);
@@ -1410,12 +1419,12 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 		hipLaunchKernelGGL((k_final_copy<K>), dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st, kin,
 				   positions ? nullptr : vin, n, f2);
 	}
+	uint32_t *he = (uint32_t *) pinned(16);
+	if (lb && !hip_ok(hipMemcpyAsync(he, lb_err, 4, hipMemcpyDeviceToHost, st), "memcpy"))
+		return -1;
 	if (!sync())
 		return -1;
 	if (lb) {
-		uint32_t *he = (uint32_t *) pinned(16);
-		if (!hip_ok(hipMemcpyAsync(he, lbm.as<uint32_t>() + 4, 4, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
-			return -1;
 		if (he[0]) {
 			seterr("HY013!BATsort: radix look-back did not complete");
 			return -1;
@@ -1490,9 +1499,12 @@ sort_typed(const mgdk_bat *b, bool reverse, bool nilslast, mgdk_bat *sn, mgdk_ba
 	if (gn) {
 		// groups: a new group wherever the sorted key image changes
 		const BUN nt = (n + GTILE - 1) / GTILE;
-		DevBuf cnt(nt * 4 + 4), pre(nt * 8 + 8);
+		// the scan's total and error flag are read with the final sync (no
+		// round trip between the count and the write pass)
+		DevBuf cnt(nt * 4 + 4), pre(nt * 8 + 8), sws(scan_ws_words(nt) * 8);
 		uint64_t tot = 0;
-		if (!cnt.p || !pre.p)
+		bool tot_dev = false;
+		if (!cnt.p || !pre.p || !sws.p)
 			return -1;
 		if (gid_done) {
 			tot = gid_last;
@@ -1501,8 +1513,9 @@ sort_typed(const mgdk_bat *b, bool reverse, bool nilslast, mgdk_bat *sn, mgdk_ba
 				using KT = std::remove_const_t<std::remove_pointer_t<decltype(src)>>;
 				hipLaunchKernelGGL((k_gid_count<KT>), dim3((unsigned) nt), dim3(256), 0, st, src, n,
 						   cnt.as<uint32_t>());
-				if (exclusive_scan(cnt.as<uint32_t>(), pre.as<uint64_t>(), nt, &tot) < 0)
+				if (exclusive_scan_nosync(cnt.as<uint32_t>(), pre.as<uint64_t>(), nt, sws.as<uint64_t>()) < 0)
 					return -1;
+				tot_dev = true;
 				hipLaunchKernelGGL((k_gid_write<KT>), dim3((unsigned) nt), dim3(256), 0, st, src, n,
 						   pre.as<uint64_t>(), (oid *) gn->theap);
 				return 0;
@@ -1515,8 +1528,18 @@ sort_typed(const mgdk_bat *b, bool reverse, bool nilslast, mgdk_bat *sn, mgdk_ba
 			if (rc < 0)
 				return -1;
 		}
+		uint64_t *ht = (uint64_t *) pinned(16);
+		if (tot_dev && !hip_ok(hipMemcpyAsync(ht, sws.as<uint64_t>() + 2, 16, hipMemcpyDeviceToHost, st), "memcpy"))
+			return (void) sync(), -1;
 		if (!sync())
 			return -1;
+		if (tot_dev) {
+			if ((uint32_t) ht[1]) {
+				seterr("HY013!scan: look-back did not complete");
+				return -1;
+			}
+			tot = ht[0];
+		}
 		gn->count = n;
 		gn->tsorted = 1;
 		gn->trevsorted = tot == 0;

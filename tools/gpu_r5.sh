@@ -121,6 +121,11 @@ grpvar)
 		MGDK_LIB=$PWD/tools/variants/libmgdk_$v.so timeout -k 10 200 python tools/selgrp_trace.py > $O/selgrp_$v.json 2> $O/selgrp_$v.err
 	done
 	;;
+sortprof)
+	timeout -k 10 200 python tools/opbench.py --only other_ops > $O/opbench.json 2> $O/opbench.err
+	cd /tmp && cd $GRAFT_REPO_ROOT
+	timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 tools/opbench.py --only other_ops > $O/prof.log 2>&1
+	;;
 *)
 	echo "unknown step $step"; exit 2
 	;;
