@@ -100,6 +100,9 @@ k_rs_hist(const K *keys, BUN n, int shift, uint32_t *hist, uint32_t nblocks)
 // digit histograms of every pass at once: LSD passes permute the keys, so
 // each pass's global digit counts are those of the input (one read)
 constexpr int RS_MAXP = 8;
+#ifndef MGDK_SORT_NTLOAD
+#define MGDK_SORT_NTLOAD 1      // nontemporal key / value loads in the scatter passes (0: plain; 2.84 vs 2.74 ms)
+#endif
 struct Shifts {
 	int s[RS_MAXP];
 	int n;
@@ -295,8 +298,13 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 #pragma unroll
 	for (int r = 0; r < SROWS; r++) {
 		const BUN i = base + r * 64 + lane;
+#if MGDK_SORT_NTLOAD
+		k[r] = i < tend ? __builtin_nontemporal_load(keys + i) : 0;
+		v[r] = IDV ? (uint32_t) i : (i < tend ? __builtin_nontemporal_load(vals + i) : 0);
+#else
 		k[r] = i < tend ? keys[i] : 0;
 		v[r] = IDV ? (uint32_t) i : (i < tend ? vals[i] : 0);   // first pass: positions
+#endif
 	}
 	__syncthreads();
 	if (LB) {

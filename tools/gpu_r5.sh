@@ -17,7 +17,7 @@ sort)
 sortvar)
 	# sort tile variants (tools/variant_build.py): opbench other_ops per variant x XCD group
 	for v in $SORTVARS; do
-		for xg in ${XGS:-32 64 128}; do
+		for xg in ${XGS:-32}; do
 			MGDK_LIB=$PWD/tools/variants/libmgdk_$v.so MGDK_SORT_XCDG=$xg timeout -k 10 200 python tools/opbench.py --only other_ops > $O/opbench_${v}_xg$xg.json 2> $O/opbench_${v}_xg$xg.err
 		done
 	done
