@@ -1432,6 +1432,9 @@ k_pj2_offt(const uint16_t *poff, uint32_t nsub, uint32_t P, uint16_t *poffT)
 	}
 }
 
+#ifndef PJ2_NT
+#define PJ2_NT 0        // nontemporal loads of the probe's keys and the restore's answers / rows (A/B)
+#endif
 #ifndef PJ2_UV
 #define PJ2_UV 4
 #endif
@@ -1486,7 +1489,11 @@ pj2_issue(const uint32_t *pkey, const uint16_t *o0, const uint16_t *o1, uint32_t
 		for (uint32_t st = 32; st > 0; st >>= 1)
 			r += ws[r + st] <= t ? st : 0;
 		bt.idx[u] = t < bt.tot ? wb[r] + (t - ws[r]) : ~0u;
+#if PJ2_NT
+		bt.key[u] = t < bt.tot ? __builtin_nontemporal_load(pkey + bt.idx[u]) : 0u;
+#else
 		bt.key[u] = t < bt.tot ? pkey[bt.idx[u]] : 0u;
+#endif
 	}
 }
 
@@ -1628,8 +1635,13 @@ k_pj2_restore(const uint16_t *prow, const uint32_t *pans, const uint16_t *poff, 
 #pragma unroll
 		for (int u = 0; u < U; u++) {
 			const uint32_t j = j0 + u * blockDim.x;
+#if PJ2_NT
+			m[u] = j < cnt ? __builtin_nontemporal_load(pans + a + j) : 0u;
+			r[u] = j < cnt ? __builtin_nontemporal_load(prow + a + j) : 0u;
+#else
 			m[u] = j < cnt ? pans[a + j] : 0u;
 			r[u] = j < cnt ? prow[a + j] : 0u;
+#endif
 		}
 #pragma unroll
 		for (int u = 0; u < U; u++)

@@ -589,7 +589,11 @@ k_keys(const T *col, BUN n, bool reverse, bool nilslast, K *keys, unsigned long 
 #pragma unroll
 		for (int u = 0; u < KU; u++) {
 			const BUN i = i0 + u * stride;
+#if MGDK_SORT_NTLOAD
+			x[u] = __builtin_nontemporal_load(col + (i < n ? i : n - 1));
+#else
 			x[u] = col[i < n ? i : n - 1];
+#endif
 		}
 #pragma unroll
 		for (int u = 0; u < KU; u++) {
