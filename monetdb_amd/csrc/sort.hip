@@ -243,7 +243,7 @@ template <typename K, bool FINAL, bool IDV, bool LB, bool SEG>
 __global__ __launch_bounds__(Tile<K>::THREADS) void
 k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32_t *offs, uint32_t nblocks,
 	     K *kout, uint32_t *vout, FinalOut fo, uint32_t *ticket, uint64_t *status, const uint32_t *gdig,
-	     uint32_t *err, SegTiles sg, uint32_t xg, uint64_t *znext)
+	     uint32_t *err, SegTiles sg, uint32_t xg, uint64_t *znext, K kx)
 {
 	constexpr int SWAVES = Tile<K>::W, SROWS = Tile<K>::R, STHREADS = Tile<K>::THREADS, STILE = Tile<K>::N;
 	__shared__ K sk[STILE];
@@ -299,10 +299,10 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 	for (int r = 0; r < SROWS; r++) {
 		const BUN i = base + r * 64 + lane;
 #if MGDK_SORT_NTLOAD
-		k[r] = i < tend ? __builtin_nontemporal_load(keys + i) : 0;
+		k[r] = i < tend ? __builtin_nontemporal_load(keys + i) ^ kx : 0;
 		v[r] = IDV ? (uint32_t) i : (i < tend ? __builtin_nontemporal_load(vals + i) : 0);
 #else
-		k[r] = i < tend ? keys[i] : 0;
+		k[r] = i < tend ? keys[i] ^ kx : 0;
 		v[r] = IDV ? (uint32_t) i : (i < tend ? vals[i] : 0);   // first pass: positions
 #endif
 	}
@@ -458,7 +458,7 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 #pragma unroll
 				for (int u = 0; u < 4; u++) {
 					const BUN i = fb + (BUN) (r + u) * STHREADS + tid;
-					fk[u] = keys[i < fe ? i : fe - 1];
+					fk[u] = keys[i < fe ? i : fe - 1] ^ kx;
 				}
 #pragma unroll
 				for (int u = 0; u < 4; u++)
@@ -601,7 +601,8 @@ k_keys(const T *col, BUN n, bool reverse, bool nilslast, K *keys, unsigned long 
 			if (i >= n)
 				break;
 			const K k = keyimg<T, K>(x[u], reverse, nilslast);
-			keys[i] = k;
+			if (keys)
+				keys[i] = k;
 			a &= (unsigned long long) k;
 			o |= (unsigned long long) k;
 			if (dh)
@@ -1138,9 +1139,22 @@ sort_xg(int kw = 4)
 	return e ? (uint32_t) atoi(e) : 32u;
 }
 
+// src0: when set, `keys` was NOT filled; the first pass reads the column
+// src0 and takes src0[i] ^ kx0 as the image (4-byte integers: the sign flip,
+// or its complement for a reverse sort); any other use of the images
+// materialises them first
 template <typename K>
 int radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int bits, const FinalOut *fo,
-	       bool positions, bool andor, K **keys_out, uint32_t **vals_out, const uint32_t *digit_hist = nullptr);
+	       bool positions, bool andor, K **keys_out, uint32_t **vals_out, const uint32_t *digit_hist = nullptr,
+	       const K *src0 = nullptr, K kx0 = 0);
+
+template <typename K>
+__global__ __launch_bounds__(256) void
+k_img_xor(const K *src, BUN n, K kx, K *keys)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
+		keys[i] = src[i] ^ kx;
+}
 
 // passes A, B, C (see above); keys / vals hold the input images, the
 // alternates are free; cap: the largest (d1, d2) bucket sorted in LDS
@@ -1168,7 +1182,7 @@ radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, int s1, int s2, ui
 		return -1;
 	hipLaunchKernelGGL((k_rs_scatter<K, false, true, true, false>), dim3(nblocks), dim3(Tile<K>::THREADS), 0, st, k0,
 			   v0, n, s1, nullptr, nblocks, k1, v1, none, lbm, status, gd1, lbm + 4, SegTiles{}, sort_xg((int) sizeof(K)),
-			   nullptr);
+			   nullptr, (K) 0);
 	// pass B: by d2 inside the d1 buckets
 	hipLaunchKernelGGL(k_seg_tiles, dim3(1), dim3(256), 0, st, cnt1, gd1, TILE, desc.as<uint4>(), count, bfirst,
 			   bnt);
@@ -1179,7 +1193,7 @@ radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, int s1, int s2, ui
 		return -1;
 	hipLaunchKernelGGL((k_rs_scatter<K, false, false, false, true>), dim3(tmax), dim3(Tile<K>::THREADS), 0, st,
 			   (const K *) k1, (const uint32_t *) v1, n, s2, offs.as<uint32_t>(), tmax, k0, v0, none, lbm,
-			   status, gd1, lbm + 4, sg, sort_xg((int) sizeof(K)), nullptr);
+			   status, gd1, lbm + 4, sg, sort_xg((int) sizeof(K)), nullptr, (K) 0);
 	// pass C: the remaining varying bits, 4 at a time, inside each (d1, d2) bucket
 	// the remaining bits in 8-bit LSD digits (the top one may reach into d2,
 	// constant inside a bucket)
@@ -1272,7 +1286,8 @@ radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, int s1, int s2, ui
 template <typename K>
 int
 radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int bits, const FinalOut *fo,
-	   bool positions, bool andor, K **keys_out, uint32_t **vals_out, const uint32_t *digit_hist)
+	   bool positions, bool andor, K **keys_out, uint32_t **vals_out, const uint32_t *digit_hist, const K *src0,
+	   K kx0)
 {
 	*keys_out = keys;
 	*vals_out = vals;
@@ -1280,6 +1295,10 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 	if (n == 0)
 		return 0;
 	unsigned long long *ao = (unsigned long long *) meta_buf();
+	if (src0 != nullptr && !andor) {
+		hipLaunchKernelGGL((k_img_xor<K>), dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st, src0, n, kx0, keys);
+		src0 = nullptr;
+	}
 	if (!andor) {
 		unsigned long long init[2] = {~0ull, 0ull};
 		if (!hip_ok(hipMemcpyAsync(ao, init, 16, hipMemcpyHostToDevice, st), "memcpy"))
@@ -1306,6 +1325,11 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 	const uint32_t nblocks = (uint32_t) ((n + Tile<K>::N - 1) / Tile<K>::N);
 	static const bool use_lb = getenv("MGDK_SORT_LB") ? atoi(getenv("MGDK_SORT_LB")) != 0 : true;
 	const bool lb = use_lb && !shifts.empty() && shifts.size() <= (size_t) RS_MAXP;
+	if (src0 != nullptr && (shifts.empty() || hy_try || !positions || !lb || !andor || digit_hist == nullptr)) {
+		// paths that read the images themselves: materialise them
+		hipLaunchKernelGGL((k_img_xor<K>), dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st, src0, n, kx0, keys);
+		src0 = nullptr;
+	}
 	DevBuf hist(lb ? 64 : (size_t) 256 * nblocks * 4), offs(lb ? 64 : (size_t) 256 * nblocks * 4);
 	// look-back state: two status arrays (pass s uses status[s % 2] and
 	// zeroes status[(s + 1) % 2] for the next pass), ticket words per pass
@@ -1388,6 +1412,7 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 	K *kin = keys, *kout = keys_alt;
 	uint32_t *vin = vals, *vout = vals_alt;
 	FinalOut none{};
+	// the first pass reads the column itself (src0, kx0) when given
 	for (size_t s = 0; s < shifts.size(); s++) {
 		const int shift = shifts[s];
 		const bool fin = fo != nullptr && s + 1 == shifts.size();
@@ -1405,9 +1430,11 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 			f2.keys = kout;
 		uint32_t *tk = lbm.as<uint32_t>() + 16 * s, *er = lb_err;
 		const uint32_t *gd = gdig + s * 256;
-#define SCAT(F, I, L) hipLaunchKernelGGL((k_rs_scatter<K, F, I, L, false>), dim3(nblocks), dim3(Tile<K>::THREADS), 0, st, kin, \
+		const K *kfrom = s == 0 && src0 ? src0 : kin;
+		const K kx = s == 0 && src0 ? kx0 : (K) 0;
+#define SCAT(F, I, L) hipLaunchKernelGGL((k_rs_scatter<K, F, I, L, false>), dim3(nblocks), dim3(Tile<K>::THREADS), 0, st, kfrom, \
 					 vin, n, shift, offs.as<uint32_t>(), nblocks, kout, vout, f2, tk, sts, gd, er, \
-					 SegTiles{}, sort_xg((int) sizeof(K)), znx)
+					 SegTiles{}, sort_xg((int) sizeof(K)), znx, kx)
 		if (lb) {
 			if (fin) {
 				if (idv) SCAT(true, true, true); else SCAT(true, false, true);
@@ -1473,8 +1500,15 @@ sort_typed(const mgdk_bat *b, bool reverse, bool nilslast, mgdk_bat *sn, mgdk_ba
 	DevBuf dh(8 * 256 * 4);
 	if (!dh.p || !hip_ok(hipMemsetAsync(dh.p, 0, 8 * 256 * 4, st), "memset"))
 		return -1;
+	// 4-byte signed integers whose image is a plain XOR (no nil, or nils
+	// where their natural image puts them): the key-image pass only counts
+	// digits, and the first radix pass reads the column itself
+	constexpr bool sint4 = sizeof(T) == 4 && sizeof(K) == 4 && !is_float && (T) -1 < (T) 0;
+	static const bool direct_on = !getenv("MGDK_SORT_DIRECT") || atoi(getenv("MGDK_SORT_DIRECT")) != 0;
+	const bool direct = sint4 && direct_on && (reverse == nilslast || b->tnonil) && ((uintptr_t) b->theap & 3) == 0;
+	const K kx0 = (K) (reverse ? 0x7fffffffu : 0x80000000u);
 	hipLaunchKernelGGL((k_keys<T, K>), dim3(grid_for(n, 8192, 1024)), dim3(256), 0, st, (const T *) b->theap, n,
-			   reverse, nilslast, k0.as<K>(), ao, dh.as<uint32_t>());
+			   reverse, nilslast, direct ? (K *) nullptr : k0.as<K>(), ao, dh.as<uint32_t>());
 	FinalOut fo{};
 	fo.vw = b->twidth;
 	fo.reverse = reverse;
@@ -1498,7 +1532,8 @@ sort_typed(const mgdk_bat *b, bool reverse, bool nilslast, mgdk_bat *sn, mgdk_ba
 	K *ks;
 	uint32_t *vs;
 	if (radix_sort<K>(k0.as<K>(), v0.as<uint32_t>(), k1.as<K>(), v1.as<uint32_t>(), n, 8 * (int) sizeof(K), &fo,
-			  true, true, &ks, &vs, dh.as<uint32_t>()) < 0)
+			  true, true, &ks, &vs, dh.as<uint32_t>(), direct ? (const K *) b->theap : nullptr,
+			  direct ? kx0 : (K) 0) < 0)
 		return -1;
 	if (sn && !decodable) {
 		switch (b->twidth) {
