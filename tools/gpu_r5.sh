@@ -139,6 +139,12 @@ final)
 	timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_jw -o run -- python3 tools/opbench.py --only config3 config4_group_sums > $O/pmc_jw.log 2>&1
 	timeout -k 10 300 python tools/opbench.py > $O/opbench.json 2> $O/opbench.err
 	;;
+sortlb)
+	for v in 1 0 1 0; do
+		MGDK_SORT_LB=$v timeout -k 10 200 python tools/opbench.py --only other_ops > $O/opbench_lb$v.json 2> $O/opbench_lb$v.err
+		echo "lb=$v $(grep -h '"kernel_ms"' $O/opbench_lb$v.json | head -1)" >> $O/summary.txt
+	done
+	;;
 sortdirect)
 	for v in 0 1 0 1; do
 		MGDK_SORT_DIRECT=$v timeout -k 10 200 python tools/opbench.py --only other_ops > $O/opbench_d$v.json 2> $O/opbench_d$v.err
