@@ -1432,6 +1432,9 @@ k_pj2_offt(const uint16_t *poff, uint32_t nsub, uint32_t P, uint16_t *poffT)
 	}
 }
 
+#ifndef PJ2_RALL
+#define PJ2_RALL 1      // the restore loads all of a subtile's entries at once (0: four rounds of 8 per thread)
+#endif
 #ifndef PJ2_NT
 #define PJ2_NT 0        // nontemporal loads of the probe's keys and the restore's answers / rows (A/B)
 #endif
@@ -1629,6 +1632,33 @@ k_pj2_restore(const uint16_t *prow, const uint32_t *pans, const uint16_t *poff, 
 	const BUN a = (BUN) sub * PJ_SUBROWS;
 	const uint32_t rows = (uint32_t) min((BUN) PJ_SUBROWS, n - a);
 	const uint32_t cnt = poff[(size_t) sub * (P + 1) + P];
+#if PJ2_RALL
+	// every entry of the subtile loaded at once (the region holds PJ_SUBROWS
+	// entries, so whole 16-B pieces past cnt stay inside it): thread tid
+	// takes entries 4 (tid + 1024 q) .. + 3, q < 8 -- one latency instead of
+	// four dependent rounds
+	static_assert(PJ_SUBROWS == 32 * 1024, "32 entries per thread");
+	typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+	typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+	u4 am[8];
+	u2 ar[8];
+#pragma unroll
+	for (int q = 0; q < 8; q++) {
+		const uint32_t j = 4 * (tid + 1024 * q);
+		am[q] = j < cnt ? __builtin_nontemporal_load((const u4 *) (pans + a + j)) : (u4) {0, 0, 0, 0};
+		ar[q] = j < cnt ? __builtin_nontemporal_load((const u2 *) (prow + a + j)) : (u2) {0, 0};
+	}
+#pragma unroll
+	for (int q = 0; q < 8; q++) {
+		const uint32_t j = 4 * (tid + 1024 * q);
+#pragma unroll
+		for (int c = 0; c < 4; c++) {
+			const uint32_t m = am[q][c], r = (ar[q][c >> 1] >> (16 * (c & 1))) & 0xffffu;
+			if (j + c < cnt && m)
+				res[r + (r >> 5)] = m;
+		}
+	}
+#else
 	constexpr int U = 8;
 	for (uint32_t j0 = tid; j0 < cnt; j0 += U * blockDim.x) {
 		uint32_t m[U], r[U];
@@ -1648,6 +1678,7 @@ k_pj2_restore(const uint16_t *prow, const uint32_t *pans, const uint16_t *poff, 
 			if (m[u])
 				res[r[u] + (r[u] >> 5)] = m[u];
 	}
+#endif
 	__syncthreads();
 	pj_emit(res, sub, a, rows, nsub, L, R, status, meta, r1, r2);
 }
