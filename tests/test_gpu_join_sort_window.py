@@ -132,15 +132,15 @@ def test_join_partitioned(gdk, ora, nil_matches, case, part, monkeypatch):
 
 
 @pytest.mark.parametrize("tname", ["lng", "oid"])
-@pytest.mark.parametrize("case", ["gt", "part", "probe_wide", "build_wide"])
+@pytest.mark.parametrize("case", ["gt", "part", "probe_wide", "build_wide", "part_build_wide"])
 def test_join_8byte_keys(gdk, ora, tname, case):
     """8-byte keys run the global-table / partitioned paths by their 4-byte
     images when every build value has one: nils (nil_matches both ways),
     probe values beyond 32 bits (no match), and a build value beyond 32 bits
-    (falls back to the open-addressing path) -- all bit-exact with the
-    oracle."""
+    (falls back to the open-addressing path; on the partitioned path the
+    flag is read after the restore) -- all bit-exact with the oracle."""
     r = rng(86)
-    nr, nl = (2_100_003, 3_000_001) if case == "part" else (700_001, 2_500_003)
+    nr, nl = (2_100_003, 3_000_001) if case.startswith("part") else (700_001, 2_500_003)
     tp = getattr(gdk, "TYPE_" + tname)
     otp = getattr(ora, "TYPE_" + tname)
     if tname == "lng":
@@ -154,7 +154,7 @@ def test_join_8byte_keys(gdk, ora, tname, case):
     lv[::997] = nil
     if case == "probe_wide":
         lv[5::1013] = (1 << 40) + 3 if tname == "oid" else -(1 << 40) - 3
-    if case == "build_wide":
+    if case.endswith("build_wide"):
         rv[77] = (1 << 33) + 5
     for nm in (False, True):
         a, b = gdk.BATjoin(mk(gdk, tp, lv, hseqbase=11), mk(gdk, tp, rv, hseqbase=4), nil_matches=nm)
