@@ -1736,8 +1736,10 @@ join_part2(const Side &L, BUN nl, const Side &R, BUN nr, const PjSide &B, int pb
 	uint32_t *h = (uint32_t *) pinned(64);
 	const uint32_t nsub = (uint32_t) ((nl + PJ_SUBROWS - 1) / PJ_SUBROWS);
 	const size_t rsz = (size_t) nsub * PJ_SUBROWS;
-	if (rsz >= ((size_t) 1 << 32))
-		return 1;                                   // entry indexes are 32-bit
+	if (nl == 0 || rsz >= ((size_t) 1 << 32)) {
+		(void) sync();                              // the build side's cut still uses its buffers
+		return 1;                                   // (entry indexes are 32-bit)
+	}
 	DevBuf pkey(rsz * 4 + 64), prow(rsz * 2 + 64), pans(rsz * 4 + 64), poff((size_t) nsub * (P + 1) * 2 + 64),
 		poffT((size_t) nsub * (P + 1) * 2 + 64);
 	if (!pkey.p || !prow.p || !pans.p || !poff.p || !poffT.p)
