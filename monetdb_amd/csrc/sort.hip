@@ -100,6 +100,9 @@ k_rs_hist(const K *keys, BUN n, int shift, uint32_t *hist, uint32_t nblocks)
 // digit histograms of every pass at once: LSD passes permute the keys, so
 // each pass's global digit counts are those of the input (one read)
 constexpr int RS_MAXP = 8;
+#ifndef MGDK_SORT_GIDV
+#define MGDK_SORT_GIDV 1        // group-start count pass with 16-B loads (0: 4-B loads at a 256-row stride)
+#endif
 #ifndef MGDK_SORT_NTLOAD
 #define MGDK_SORT_NTLOAD 1      // nontemporal key / value loads in the scatter passes (0: plain; 2.84 vs 2.74 ms)
 #endif
@@ -651,6 +654,54 @@ k_newgrp(const K *keys, BUN n, uint8_t *flag)
 // keys[i'] != keys[i'-1].  Two passes over 4096-key tiles (count, then
 // write with a workgroup scan) around a scan of the tile counts: 16 B/row.
 constexpr int GTILE = 4096;
+
+// k_gid_count with whole 16-B loads (1 KiB per wave instruction): thread
+// tid holds elements t0 + j * 256 V + tid V .. + V - 1 (V per 16 B); the
+// element before a lane's first comes from the lane before (shfl) or, for
+// lane 0, one scalar load.  keys must be 16-B aligned (the host checks)
+template <typename K>
+__global__ __launch_bounds__(256) void
+k_gid_count_v(const K *keys, BUN n, uint32_t *cnt)
+{
+	constexpr int V = 16 / (int) sizeof(K), J = GTILE / 256 / V;
+	static_assert(J >= 1 && GTILE % (256 * V) == 0, "whole 16-B pieces per thread");
+	typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+	const BUN t0 = (BUN) blockIdx.x * GTILE;
+	const unsigned tid = threadIdx.x, lane = __lane_id();
+	const BUN nv = n / V;                  // whole 16-B pieces in the column
+	u4 raw[J];
+	K before[J];
+#pragma unroll
+	for (int j = 0; j < J; j++) {
+		const BUN e0 = t0 + (BUN) j * 256 * V + (BUN) tid * V, pv = e0 / V;
+		raw[j] = __builtin_nontemporal_load((const u4 *) keys + (pv < nv ? pv : (nv ? nv - 1 : 0)));
+		before[j] = lane == 0 && e0 > 0 && e0 <= n ? keys[e0 - 1] : (K) 0;
+	}
+	uint32_t c = 0;
+#pragma unroll
+	for (int j = 0; j < J; j++) {
+		K x[V];
+		__builtin_memcpy(x, &raw[j], 16);
+		const BUN e0 = t0 + (BUN) j * 256 * V + (BUN) tid * V;
+		// a piece past the last whole one: its elements by scalar loads
+		if (e0 / V >= nv)
+#pragma unroll
+			for (int v = 0; v < V; v++)
+				x[v] = e0 + v < n ? keys[e0 + v] : (K) 0;
+		K prev = __shfl_up(x[V - 1], 1);
+		if (lane == 0)
+			prev = before[j];
+#pragma unroll
+		for (int v = 0; v < V; v++) {
+			const BUN i = e0 + v;
+			c += i > 0 && i < n && x[v] != prev;
+			prev = x[v];
+		}
+	}
+	c = block_reduce(c, [](uint32_t a, uint32_t b) { return a + b; });
+	if (threadIdx.x == 0)
+		cnt[blockIdx.x] = c;
+}
 
 template <typename K>
 __global__ __launch_bounds__(256) void
@@ -1558,8 +1609,12 @@ sort_typed(const mgdk_bat *b, bool reverse, bool nilslast, mgdk_bat *sn, mgdk_ba
 		} else if (nt > 0) {
 			auto gids = [&](auto *src) {
 				using KT = std::remove_const_t<std::remove_pointer_t<decltype(src)>>;
-				hipLaunchKernelGGL((k_gid_count<KT>), dim3((unsigned) nt), dim3(256), 0, st, src, n,
-						   cnt.as<uint32_t>());
+				if (MGDK_SORT_GIDV && n >= (BUN) GTILE && ((uintptr_t) src & 15) == 0)
+					hipLaunchKernelGGL((k_gid_count_v<KT>), dim3((unsigned) nt), dim3(256), 0, st, src, n,
+							   cnt.as<uint32_t>());
+				else
+					hipLaunchKernelGGL((k_gid_count<KT>), dim3((unsigned) nt), dim3(256), 0, st, src, n,
+							   cnt.as<uint32_t>());
 				if (exclusive_scan_nosync(cnt.as<uint32_t>(), pre.as<uint64_t>(), nt, sws.as<uint64_t>()) < 0)
 					return -1;
 				tot_dev = true;
