@@ -292,33 +292,45 @@ k_gs_sums(const typename KT<KW>::T *k, const void *const *vals, BUN n, oid hseq,
 	bool seen = false;
 	uint32_t of = 0;
 	__syncthreads();
-	uint64_t tbase;
-	if constexpr (LB) {
-		if (w == 0) {
-			// a predecessor's wait is microseconds; 2^20 spins (~1 s) means the
-			// dispatch order assumption failed: give up, the host reruns
-			const uint64_t ex = mgdk_lb::lookback(lbst, (uint32_t) t, s_wst[0] + s_wst[1] + s_wst[2] + s_wst[3],
-							      lberr, 1u << 20);
-			if (lane == 0)
-				s_tbase = ex;
-		}
-		__syncthreads();
-		tbase = s_tbase;
-	} else {
-		tbase = tpre[t];
-	}
 	uint32_t lpre = xs - ns;
 	for (unsigned q = 0; q < w; q++)
 		lpre += s_wst[q];
 	const uint32_t tst = s_wst[0] + s_wst[1] + s_wst[2] + s_wst[3];
 	const bool tile_has_start = tst != 0;
+	constexpr uint32_t GCAP = (uint32_t) ((KBY + VBY) / (24 + 16 * NV)) & ~1u;
+	const bool stg = GS_STAGE && tst <= GCAP;
+	// LB with staged outputs: the tile publishes its start count now and
+	// numbers its groups from 0 while it reduces and stages them; the
+	// look-back runs at the end, when its predecessors have long published
+	// (a look-back before the work made every tile wait on the one before
+	// it), and only the copy-out and the edge records need the real base
+	const bool late = LB && stg;
+	uint64_t tbase;
+	if constexpr (LB) {
+		if (late) {
+			// tile 0's base is 0: its inclusive count is known already
+			if (tid == 0)
+				mgdk_lb::lb_store(&lbst[t], (t == 0 ? mgdk_lb::ST_PRE : mgdk_lb::ST_AGG) | tst);
+			tbase = 0;
+		} else {
+			if (w == 0) {
+				// a predecessor's wait is microseconds; 2^20 spins (~1 s) means
+				// the dispatch order assumption failed: give up, the host reruns
+				const uint64_t ex = mgdk_lb::lookback(lbst, (uint32_t) t, tst, lberr, 1u << 20);
+				if (lane == 0)
+					s_tbase = ex;
+			}
+			__syncthreads();
+			tbase = s_tbase;
+		}
+	} else {
+		tbase = tpre[t];
+	}
 	// the groups starting in the tile, [tbase, tbase + tst), are written by
 	// this tile only (ext / key all of them, hist / sums all but the last,
 	// which the tail edge record carries): staged in LDS (the rows are in
 	// registers since the barrier above) and stored as contiguous runs
 	// after the tile, when they fit
-	constexpr uint32_t GCAP = (uint32_t) ((KBY + VBY) / (24 + 16 * NV)) & ~1u;
-	const bool stg = GS_STAGE && tst <= GCAP;
 	oid *l_ext = (oid *) s_raw;
 	int64_t *l_key = (int64_t *) (s_raw + 8 * GCAP), *l_hist = (int64_t *) (s_raw + 16 * GCAP);
 	hge *l_sum = (hge *) (s_raw + 24 * GCAP);     // [NV][GCAP]
@@ -418,15 +430,24 @@ k_gs_sums(const typename KT<KW>::T *k, const void *const *vals, BUN n, oid hseq,
 	}
 	// some start in the tile before this lane
 	const bool before = (lane == 0 ? cflag : (fin || cflag));
-	if (seen) {
-		// the group of the lane's first rows ends before its first start
-		GsPart<NV> tot = Sin;
-		tot.add(pre);
-		if (before)
-			of |= put(tbase + lpre - 1, tot);
-		else
-			edges[2 * t] = GsEdge<NV>{tbase - 1, tot};      // the tile's head group
+	// the group of the lane's first rows ends before its first start
+	GsPart<NV> tot = Sin;
+	tot.add(pre);
+	if (seen && before)
+		of |= put(tbase + lpre - 1, tot);
+	if constexpr (LB) {
+		if (late && w == 0) {
+			const uint64_t ex = mgdk_lb::lookback(lbst, (uint32_t) t, tst, lberr, 1u << 20);
+			if (lane == 0)
+				s_tbase = ex;
+		}
 	}
+	if (stg)
+		__syncthreads();
+	if (late)
+		tbase = s_tbase;
+	if (seen && !before)
+		edges[2 * t] = GsEdge<NV>{tbase - 1, tot};      // the tile's head group
 	if (tid == 255) {
 		if (!tile_has_start) {
 			// one group over the whole tile: head = everything, tail = empty
@@ -439,7 +460,6 @@ k_gs_sums(const typename KT<KW>::T *k, const void *const *vals, BUN n, oid hseq,
 		}
 	}
 	if (stg) {
-		__syncthreads();
 		for (uint32_t j = tid; j < tst; j += 256) {
 			o.ext[tbase + j] = l_ext[j];
 			o.key[tbase + j] = l_key[j];

@@ -32,10 +32,14 @@ join)
 	;;
 gsums)
 	timeout -k 10 600 $T tests/test_gpu_group_sums.py > $O/tests.log 2>&1
-	MGDK_GS_FUSED=0 timeout -k 10 200 python tools/opbench.py --only config4_group_sums > $O/opbench_f0.json 2> $O/opbench_f0.err
-	timeout -k 10 200 python tools/opbench.py --only config4_group_sums > $O/opbench_fused.json 2> $O/opbench_fused.err
+	for r in a b; do
+		for f in 0 1; do
+			MGDK_GS_FUSED=$f timeout -k 10 200 python tools/opbench.py --only config4_group_sums > $O/opbench_f$f$r.json 2> $O/opbench_f$f$r.err
+		done
+	done
 	cd /tmp && cd $GRAFT_REPO_ROOT
 	timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 tools/opbench.py --only config4_group_sums > $O/prof.log 2>&1
+	MGDK_GS_FUSED=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_fused -o run -- python3 tools/opbench.py --only config4_group_sums > $O/prof_fused.log 2>&1
 	timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f -o run -- python3 tools/opbench.py --only config4_group_sums > $O/pmc_f.log 2>&1
 	timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_w -o run -- python3 tools/opbench.py --only config4_group_sums > $O/pmc_w.log 2>&1
 	;;
