@@ -649,9 +649,12 @@ mgdk_group_sums_ordered(mgdk_bat **extents, mgdk_bat **histo, mgdk_bat **keys, m
 	// look-back inside the sums pass, so the keys are read once; the outputs
 	// are sized for n groups (56 B per row at two sums, capped at 48 GiB) and
 	// the count is the last tile's inclusive prefix; a look-back that did not
-	// complete reruns two-pass.  With the outputs staged in LDS the fused form
-	// is the slower one (5.67 vs 4.65 ms at SF100, profiles/r05/gsums/: the
-	// tiles' stores wait on the look-back); before staging it was 6.09 vs 6.30.
+	// complete reruns two-pass.  With the look-back after the staging the
+	// fused form is 1.4 % faster at SF100 (5.20 vs 5.27 ms,
+	// profiles/r05/gsums_late/): the look-back's round trips cost about what
+	// the count pass does, so the exact two-pass form stays the default.  A
+	// persistent fused form (next tile's rows fetched during the look-back)
+	// needed 240 VGPRs in its tile loop, against 98 for one tile per block.
 	const bool fused_on = getenv("MGDK_GS_FUSED") && atoi(getenv("MGDK_GS_FUSED")) != 0;   // read per call (tests)
 	bool fused = fused_on && nt < 0xffffffffull && n * (24 + 16 * (BUN) nvals) <= ((BUN) 48 << 30);
 	DevBuf vp(64);
