@@ -93,6 +93,7 @@ struct SelArgs {
 	uint64_t *status;         // [ntiles] look-back granules
 	uint32_t *ticket;         // dynamic tile numbering
 	uint64_t *meta;           // [0] total count, [1] error flags
+	uint64_t *hmeta;          // streamed: meta[0..3] also stored to this pinned host copy (or null)
 };
 
 // rows of 256 lanes x 16 B per tile: 32 for a dense scan (128 KiB of input per
@@ -110,6 +111,11 @@ struct SelArgs {
 #endif
 #ifndef MGDK_SEL_BATCH
 #define MGDK_SEL_BATCH 8
+#endif
+// the streamed scan's result words go straight to pinned host memory (no
+// device-to-host copy after the write pass)
+#ifndef MGDK_SEL_HMETA
+#define MGDK_SEL_HMETA 1
 #endif
 template <bool MAT> constexpr int sel_rows() { return MAT ? 16 : MGDK_SEL_ROWS; }
 constexpr int BATCH = MGDK_SEL_BATCH;
@@ -421,7 +427,7 @@ k_sel_count_c(SelArgs<T> a, const uint32_t *cbits, const void *zero, uint32_t *b
 // (A thread owning one long run serialised ~70 dependent loads and wrote
 // its run with a stride: 0.13 ms for 73 K tiles.)
 __global__ __launch_bounds__(1024) void
-k_sel_scan(const uint32_t *counts, uint64_t *pre, uint32_t n, uint64_t *meta)
+k_sel_scan(const uint32_t *counts, uint64_t *pre, uint32_t n, uint64_t *meta, uint64_t *hmeta)
 {
 	__shared__ uint64_t s_wave[16];
 	__shared__ uint64_t s_carry;
@@ -468,6 +474,10 @@ k_sel_scan(const uint32_t *counts, uint64_t *pre, uint32_t n, uint64_t *meta)
 	if (tid == 0) {
 		meta[0] = s_carry;
 		meta[1] = 0;   // no look-back errors on this path
+		if (hmeta) {
+			hmeta[0] = s_carry;
+			hmeta[1] = 0;
+		}
 	}
 }
 
@@ -518,12 +528,16 @@ k_sel_write(SelArgs<T> a, const uint32_t *bits, const uint64_t *pre)
 			while (w[q] == 0)
 				q++;
 			a.meta[2] = base + ((uint64_t) (tid * WPL + q) * 32 + __ffs(w[q]) - 1);
+			if (a.hmeta)
+				a.hmeta[2] = a.meta[2];
 		}
 		if (cnt > 0 && ex + cnt == hits && prefix + hits == a.meta[0]) {
 			int q = WPL - 1;
 			while (w[q] == 0)
 				q--;
 			a.meta[3] = base + ((uint64_t) (tid * WPL + q) * 32 + 31 - __clz(w[q]));
+			if (a.hmeta)
+				a.hmeta[3] = a.meta[3];
 		}
 		if (hits < 1024) {
 			// sparse: the owning lane stores its hits
@@ -759,6 +773,12 @@ run_scan(const mgdk_bat *b, const Cand &ci, const SelPred<T> &pred)
 	a.meta = meta;
 	hipStream_t st = stream();
 	const bool streamed = ci.dense && MGDK_SEL_STREAM;   // count / scan / write, no look-back
+	uint64_t *h = (uint64_t *) pinned(64);
+	if (h == nullptr) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	a.hmeta = streamed && MGDK_SEL_HMETA ? h : nullptr;
 	if (!streamed && (!hip_ok(hipMemsetAsync(sc, 0, sbytes, st), "hipMemsetAsync") ||
 			  !hip_ok(hipMemsetAsync(meta, 0, 64, st), "hipMemsetAsync"))) {
 		mgdk_BBPunfix(bn);
@@ -787,7 +807,7 @@ run_scan(const mgdk_bat *b, const Cand &ci, const SelPred<T> &pred)
 			smap_bits = bits;
 		}
 #define SELS(MODE) do { hipLaunchKernelGGL((k_sel_count<T, MODE>), g, blk, 0, st, a, bits, counts); \
-			hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(1024), 0, st, counts, pre, (uint32_t) ntiles, a.meta); \
+			hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(1024), 0, st, counts, pre, (uint32_t) ntiles, a.meta, a.hmeta); \
 			hipLaunchKernelGGL(k_sel_write<T>, gw, blk, 0, st, a, bits, pre); } while (0)
 #define SELL(MAT, MODE) do { if (!(MAT) && MGDK_SEL_STREAM) SELS(MODE); \
 			     else hipLaunchKernelGGL((k_select<T, MAT, MODE>), g, blk, 0, st, a); } while (0)
@@ -808,8 +828,7 @@ run_scan(const mgdk_bat *b, const Cand &ci, const SelPred<T> &pred)
 	}
 	if (!streamed)
 		hipLaunchKernelGGL(k_select_fin, dim3(1), dim3(1), 0, st, (const oid *) bn->theap, meta);
-	uint64_t *h = (uint64_t *) pinned(64);
-	if (h == nullptr || !hip_ok(hipMemcpyAsync(h, meta, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, st), "memcpy") ||
+	if ((a.hmeta == nullptr && !hip_ok(hipMemcpyAsync(h, meta, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, st), "memcpy")) ||
 	    !sync()) {
 		mgdk_BBPunfix(bn);
 		return nullptr;
@@ -872,12 +891,14 @@ run_scan_bits(const mgdk_bat *b, const Cand &ci, const SelPred<T> &pred, const S
 	}
 	a.ntiles = (uint32_t) ntiles;
 	uint64_t *meta = (uint64_t *) meta_buf();
+	uint64_t *h = (uint64_t *) pinned(64);
 	a.meta = meta;
+	a.hmeta = MGDK_SEL_HMETA ? h : nullptr;
 	struct HeapRef {
 		Heap *h;
 		~HeapRef() { heap_decref(h); }
 	} sbh{heap_new(ntiles * (4 * (size_t) sel_wpt<T>() + 4 + 8) + 64)};
-	if (sbh.h == nullptr || meta == nullptr) {
+	if (sbh.h == nullptr || meta == nullptr || h == nullptr) {
 		mgdk_BBPunfix(bn);
 		return nullptr;
 	}
@@ -887,7 +908,7 @@ run_scan_bits(const mgdk_bat *b, const Cand &ci, const SelPred<T> &pred, const S
 	hipStream_t st = stream();
 	const dim3 g((unsigned) ntiles), blk(256), gw(sel_wgrid(ntiles));
 #define SELC(MODE) do { hipLaunchKernelGGL((k_sel_count_c<T, MODE>), g, blk, 0, st, a, cm.bits, zero, bits, counts); \
-			hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(1024), 0, st, counts, pre, (uint32_t) ntiles, a.meta); \
+			hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(1024), 0, st, counts, pre, (uint32_t) ntiles, a.meta, a.hmeta); \
 			hipLaunchKernelGGL(k_sel_write<T>, gw, blk, 0, st, a, bits, pre); } while (0)
 	switch (pred.mode) {
 	case SEL_RANGE: SELC(SEL_RANGE); break;
@@ -897,8 +918,7 @@ run_scan_bits(const mgdk_bat *b, const Cand &ci, const SelPred<T> &pred, const S
 	default: SELC(SEL_NOTNIL); break;
 	}
 #undef SELC
-	uint64_t *h = (uint64_t *) pinned(64);
-	if (h == nullptr || !hip_ok(hipMemcpyAsync(h, meta, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, st), "memcpy") ||
+	if ((a.hmeta == nullptr && !hip_ok(hipMemcpyAsync(h, meta, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, st), "memcpy")) ||
 	    !sync()) {
 		mgdk_BBPunfix(bn);
 		return nullptr;

@@ -52,6 +52,19 @@ stats)
 grp)
 	timeout -k 10 600 $T tests/test_gpu_ops.py tests/test_gpu_group_sorted.py tests/test_gpu_group_str.py tests/test_gpu_props.py tests/test_msk_cands.py > $O/tests.log 2>&1
 	;;
+selvar)
+	# select variants (tools/variant_build.py): the select suites on the default build, then
+	# selgrp_trace alternating default / variants twice, then a kernel trace of the default
+	timeout -k 10 600 $T -x tests/test_gpu_ops.py tests/test_gpu_props.py tests/test_msk_cands.py tests/test_cand_algebra.py tests/test_gpu_threads.py tests/test_c_abi.py > $O/tests.log 2>&1
+	for r in a b; do
+		timeout -k 10 200 python tools/selgrp_trace.py > $O/default_$r.json 2> $O/default_$r.err
+		for v in $SELVARS; do
+			MGDK_LIB=$PWD/tools/variants/libmgdk_$v.so timeout -k 10 200 python tools/selgrp_trace.py > $O/${v}_$r.json 2> $O/${v}_$r.err
+		done
+	done
+	cd /tmp && cd $GRAFT_REPO_ROOT
+	timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/prof -o run -- python3 tools/selgrp_trace.py > $O/prof.log 2>&1
+	;;
 selgrp)
 	timeout -k 10 200 python tools/selgrp_trace.py > $O/plain.json 2> $O/plain.err
 	for gg in 256 512 1024; do
