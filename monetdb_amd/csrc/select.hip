@@ -112,6 +112,11 @@ struct SelArgs {
 #ifndef MGDK_SEL_BATCH
 #define MGDK_SEL_BATCH 8
 #endif
+// oids staged in LDS per dense round of the write pass (LDS per workgroup:
+// 8 B per slot, so 2048 leaves room for 8 workgroups per CU)
+#ifndef MGDK_SEL_SCH
+#define MGDK_SEL_SCH 2048
+#endif
 // the streamed scan's result words go straight to pinned host memory (no
 // device-to-host copy after the write pass)
 #ifndef MGDK_SEL_HMETA
@@ -486,7 +491,10 @@ __global__ __launch_bounds__(256) void
 k_sel_write(SelArgs<T> a, const uint32_t *bits, const uint64_t *pre)
 {
 	constexpr int WPT = sel_wpt<T>(), WPL = sel_wpl<T>();
-	constexpr int SCH = 4096;   // slots per dense round (>= one tile of hge)
+	// slots per dense round (a tile holds a whole number of rounds), SPL per lane
+	constexpr int SCH = MGDK_SEL_SCH, SPL = SCH / 256;
+	static_assert(SPL == 4 || SPL == 8 || SPL == 16, "4 to 16 slots per lane");
+	static_assert((WPT * 32) % SCH == 0, "whole rounds per tile");
 	__shared__ oid s_stage[SCH];
 	__shared__ uint32_t s_words[WPT];
 	__shared__ uint32_t s_wave[4];
@@ -571,8 +579,8 @@ k_sel_write(SelArgs<T> a, const uint32_t *bits, const uint64_t *pre)
 				a.out[prefix + i] = s_stage[i];
 			continue;
 		}
-		// very dense: rounds of 4096 slots, lane i taking the 16 slots
-		// [16i, 16i+16) of the round; the round's hits are ranked by a workgroup
+		// very dense: rounds of SCH slots, lane i taking the SPL slots
+		// [SPL i, SPL i + SPL) of the round; the round's hits are ranked by a workgroup
 		// scan, placed in LDS in order and stored as one run
 #pragma unroll
 		for (int q = 0; q < WPL; q++)
@@ -581,7 +589,8 @@ k_sel_write(SelArgs<T> a, const uint32_t *bits, const uint64_t *pre)
 		uint64_t obase = prefix;
 		for (int rd = 0; rd < WPT * 32 / SCH; rd++) {
 			__syncthreads();   // s_words written / previous round's s_wave, s_stage consumed
-			const uint32_t piece = (s_words[rd * (SCH / 32) + tid / 2] >> (16 * (tid & 1))) & 0xffffu;
+			const uint32_t sl = (uint32_t) rd * SCH + tid * SPL;
+			const uint32_t piece = (s_words[sl / 32] >> (sl % 32)) & ((1u << SPL) - 1);
 			const uint32_t pc = __popc(piece);
 			uint32_t y = pc;
 #pragma unroll
@@ -598,7 +607,7 @@ k_sel_write(SelArgs<T> a, const uint32_t *bits, const uint64_t *pre)
 				pos += s_wave[q];
 			const uint32_t rhits = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
 			uint32_t mm = piece;
-			const oid rb = base + (uint64_t) rd * SCH + tid * 16;
+			const oid rb = base + sl;
 			while (mm) {
 				const int bb = __ffs(mm) - 1;
 				mm &= mm - 1;

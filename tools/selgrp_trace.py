@@ -24,7 +24,7 @@ def main():
     b = gdk.BAT.from_numpy(gdk.TYPE_int, r.integers(0, 1000, n, dtype=np.int32), sorted_=False, revsorted=False,
                            key=False, nonil=True)
     out = {}
-    for thr, reps in ((10, 20), (100, 10)):
+    for thr, reps in ((10, 20), (100, 10), (500, 10)):
         gdk.BATthetaselect(b, None, thr, "<")
         gdk.prof_reset()
         gdk.prof_enable(True)
