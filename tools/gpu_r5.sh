@@ -43,6 +43,17 @@ gsums)
 	timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f -o run -- python3 tools/opbench.py --only config4_group_sums > $O/pmc_f.log 2>&1
 	timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_w -o run -- python3 tools/opbench.py --only config4_group_sums > $O/pmc_w.log 2>&1
 	;;
+gsvar)
+	# group-sums variants (tools/variant_build.py): tests on the default build, then opbench
+	# config4_group_sums alternating default / variants twice
+	timeout -k 10 600 $T -x tests/test_gpu_group_sums.py > $O/tests.log 2>&1
+	for r in a b; do
+		timeout -k 10 200 python tools/opbench.py --only config4_group_sums > $O/default_$r.json 2> $O/default_$r.err
+		for v in $GSVARS; do
+			MGDK_LIB=$PWD/tools/variants/libmgdk_$v.so timeout -k 10 200 python tools/opbench.py --only config4_group_sums > $O/${v}_$r.json 2> $O/${v}_$r.err
+		done
+	done
+	;;
 jk)
 	timeout -k 10 600 $T tests/test_join_kinds.py tests/test_cand_algebra.py tests/test_theta_join.py > $O/tests.log 2>&1
 	;;
