@@ -808,10 +808,10 @@ int
 group_lds(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mgdk_bat **enp, mgdk_bat **hnp)
 {
 	hipStream_t st = stream();
-	DevBuf gkey((GL_SLOTS + 1) * 8), gmin((GL_SLOTS + 1) * 8), gmap((GL_SLOTS + 1) * 4), fl(16);
+	DevBuf gkey((GL_SLOTS + 1) * 8), gmin((GL_SLOTS + 1) * 8), gmap((GL_SLOTS + 1) * 4);
 	uint32_t *m = (uint32_t *) meta_buf();
 	uint32_t *h = (uint32_t *) pinned(64);
-	if (!gkey.p || !gmin.p || !gmap.p || !fl.p || m == nullptr || h == nullptr)
+	if (!gkey.p || !gmin.p || !gmap.p || m == nullptr || h == nullptr)
 		return -1;
 	hipLaunchKernelGGL(k_gl_init, dim3((GL_SLOTS + 256) / 256), dim3(256), 0, st, gkey.as<unsigned long long>(),
 			   gmin.as<unsigned long long>(), m);
@@ -873,7 +873,7 @@ group_lds(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mg
 				 ((uintptr_t) gn->theap & 15) == 0 && ((uintptr_t) img & 3) == 0;
 		static const bool v32 = getenv("MGDK_GROUP_V32") ? atoi(getenv("MGDK_GROUP_V32")) != 0 : true;
 		const oid *extp = (const oid *) en->theap;
-		oid *flo = fl.as<oid>();
+		oid *flo = (oid *) (m + 4);       // after the flags: one 32-B download
 		// MGDK_GROUP_GRID: workgroups of the 4-byte assign pass (each keeps its
 		// LDS table over grid-strided tiles); 0 = one per tile
 		static const unsigned agrid = getenv("MGDK_GROUP_GRID") ? (unsigned) atoi(getenv("MGDK_GROUP_GRID")) : 0;
@@ -893,8 +893,7 @@ group_lds(const KeySrc &ks, BUN n, const Cand &ci, oid hseqb, mgdk_bat **gnp, mg
 			GL_LAUNCH(k_gl_assign, dim3(tiles), dim3(1024), 0, st, ks, n, gkey.as<unsigned long long>(),
 				  gmap.as<uint32_t>(), (const uint32_t *) m, (oid *) gn->theap, img,
 				  (unsigned long long *) hn->theap, &m[2], &m[3], extp, flo);
-		if (!hip_ok(hipMemcpyAsync(h, m, 16, hipMemcpyDeviceToHost, st), "memcpy") ||
-		    !hip_ok(hipMemcpyAsync(h + 4, flo, 16, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
+		if (!hip_ok(hipMemcpyAsync(h, m, 32, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
 			unfix3();
 			return -1;
 		}
