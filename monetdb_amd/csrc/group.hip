@@ -1250,7 +1250,7 @@ group_small(const KeySrc &ks, BUN n, uint32_t nslots, const Cand &ci, oid hseqb,
 	hipStream_t st = stream();
 	DevBuf gmin(GS_MAXSLOTS * 8), gmap(GS_MAXSLOTS * 4), ext(GS_MAXSLOTS * 8);
 	uint32_t *m = (uint32_t *) meta_buf();
-	uint32_t *h = (uint32_t *) pinned(16);
+	uint32_t *h = (uint32_t *) pinned(32);
 	if (!gmin.p || !gmap.p || !ext.p)
 		return -1;
 	if (!hip_ok(hipMemsetAsync(gmin.p, 0xff, nslots * 8, st), "memset") || !hip_ok(hipMemsetAsync(m, 0, 16, st), "memset"))
@@ -1310,10 +1310,11 @@ group_small(const KeySrc &ks, BUN n, uint32_t nslots, const Cand &ci, oid hseqb,
 	if (ngrp <= 8 && ngrp > 0)
 		hipLaunchKernelGGL(k_gs_hist, dim3(kk), dim3(256), 0, st, hpart.as<unsigned long long>(), (BUN) tiles, kk, (BUN) ngrp,
 				   (unsigned long long *) hn->theap);
+	// the first / last extent into the pinned buffer too (not pageable stack memory)
 	oid fl[2] = {0, 0};
 	if (!hip_ok(hipMemcpyAsync(h, m, 12, hipMemcpyDeviceToHost, st), "memcpy") ||
-	    (ngrp > 0 && (!hip_ok(hipMemcpyAsync(&fl[0], ext.p, 8, hipMemcpyDeviceToHost, st), "memcpy") ||
-			  !hip_ok(hipMemcpyAsync(&fl[1], ext.as<oid>() + ngrp - 1, 8, hipMemcpyDeviceToHost, st), "memcpy"))) ||
+	    (ngrp > 0 && (!hip_ok(hipMemcpyAsync(h + 4, ext.p, 8, hipMemcpyDeviceToHost, st), "memcpy") ||
+			  !hip_ok(hipMemcpyAsync(h + 6, ext.as<oid>() + ngrp - 1, 8, hipMemcpyDeviceToHost, st), "memcpy"))) ||
 	    !sync()) {
 		mgdk_BBPunfix(en);
 		mgdk_BBPunfix(hn);
@@ -1322,6 +1323,8 @@ group_small(const KeySrc &ks, BUN n, uint32_t nslots, const Cand &ci, oid hseqb,
 	}
 	en->count = ngrp;
 	hn->count = ngrp;
+	if (ngrp > 0)
+		memcpy(fl, h + 4, 16);
 	gn->tsorted = h[2] == 0;
 	gn->trevsorted = ngrp == 1 || n <= 1;
 	gn->tkey = ngrp == n;
