@@ -1553,7 +1553,8 @@ k_pj2_probe(const uint2 *bent, const uint32_t *bbase, const uint32_t *pkey, cons
 	// a build partition above 90 % of the table (the host sized it for the
 	// expected largest one) is flagged and not built: its runs are answered
 	// "no match" and the host falls back after the restore
-	const uint32_t b0 = bbase[p], over = (bbase[p + 1] - b0) * 10 > ns * 9;
+	// (64-bit: a partition of more than ~429M entries must not wrap past the test)
+	const uint32_t b0 = bbase[p], over = (uint64_t) (bbase[p + 1] - b0) * 10 > (uint64_t) ns * 9;
 	const uint32_t b1 = over ? b0 : bbase[p + 1];
 	if (over && tid == 0)
 		atomicOr(dupflag, 2u);
@@ -1748,9 +1749,11 @@ join_part2(const Side &L, BUN nl, const Side &R, BUN nr, const PjSide &B, int pb
 							 hipFuncAttributeMaxDynamicSharedMemorySize, (int) PJ2_CUT_LDS) == hipSuccess;
 	static const bool probe_attr = hipFuncSetAttribute((const void *) k_pj2_probe,
 							   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
-	(void) cut_attr;
-	(void) probe_attr;
 	(void) hipGetLastError();
+	if (!cut_attr || !probe_attr) {
+		(void) sync();                              // the build side's cut still uses its buffers
+		return 1;                                   // the kernels cannot get their LDS: fallback
+	}
 	hipLaunchKernelGGL(k_pj2_cut, dim3(nsub), dim3(1024), PJ2_CUT_LDS, st, L, nl, pbits, !nil_matches,
 			   pkey.as<uint32_t>(), prow.as<uint16_t>(), poff.as<uint16_t>());
 	hipLaunchKernelGGL(k_pj2_offt, dim3((nsub + 63) / 64, (P + 1 + 63) / 64), dim3(256), 0, st, poff.as<uint16_t>(),
@@ -1789,6 +1792,11 @@ join_part2(const Side &L, BUN nl, const Side &R, BUN nr, const PjSide &B, int pb
 	hipLaunchKernelGGL(k_pj2_restore, dim3(nsub), dim3(1024), 0, st, prow.as<uint16_t>(), pans.as<uint32_t>(),
 			   poff.as<uint16_t>(), P, nl, nsub, L, R, (uint32_t *) sc, (uint64_t *) sc + 8, meta,
 			   (oid *) ra->theap, (oid *) rb->theap);
+	// a failed launch leaves pkey / pans / the results unwritten: fail the call
+	if (!hip_ok(hipGetLastError(), "join probe launch")) {
+		unfix2(ra, rb);
+		return sync_fail();
+	}
 	// meta32[2]: duplicate build key (1) / oversized partition (2);
 	// meta32[5]: build value without a 4-byte image; meta = meta32 + 8
 	if (!hip_ok(hipMemcpyAsync(h, meta32, 48, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {

@@ -149,6 +149,20 @@ class GdkBackend:
         from monetdb_amd import gdk
         self.gdk = gdk
         self.device = device
+        # (event on torch's stream after an exchange's collectives, the source
+        # tensors and BATs they read): held until the event has completed
+        self._pending = []
+
+    def drain(self, wait=False):
+        """release the sources of finished exchanges (all of them, after
+        waiting, with wait=True)"""
+        left = []
+        for ev, keep in self._pending:
+            if wait:
+                ev.synchronize()
+            elif not ev.query():
+                left.append((ev, keep))
+        self._pending = left
 
     # -- columns -------------------------------------------------------------
     def n(self, c):
@@ -323,9 +337,16 @@ class GdkBackend:
             dist.all_to_all_single(dst, src, recv, list(send_counts))
             out.append(b)
         lib.wait_stream(cur)
-        # the sources may be released by the caller now: their heaps are
-        # reused only by later work on the library stream, which is ordered
-        # after the collectives
+        # the collectives may still be reading the sources on torch's stream.
+        # This thread's later operators run on the library stream, ordered
+        # after them, but a heap the caller releases goes back to the shared
+        # caching allocator, whose next user may be another thread's stream
+        # (MAL dataflow workers): the sources are held until an event
+        # recorded after the collectives has completed
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        self._pending.append((ev, keep))
+        self.drain()
         return out, recv
 
     # -- packing -------------------------------------------------------------
@@ -604,8 +625,13 @@ def dist_group_aggr(be, dist, keys, vals):
     """GROUP BY keys with exact sums of `vals` (lng columns) and counts.
 
     keys/vals: this rank's shard, hseqbase = the shard's first global row.
-    Returns the groups OWNED by this rank (hash of the key) as columns of the
-    backend (device BATs with GdkBackend), in ascending gid order:
+    Returns the groups OWNED by this rank as columns of the backend (device
+    BATs with GdkBackend), in ascending gid order.  Ownership: by the hash of
+    the key when the shards' key ranges overlap (one all_to_all of the
+    partial rows); when the ranges meet only at neighbours (ordered input,
+    `_ordered_merge`, `STATS["ordered_merge"]`) a group belongs to the
+    earliest rank holding its key instead -- a consumer that co-partitions
+    other data by `hashpartition` must not assume hash placement then:
     {"gid", "key" (lng), "first_row" (oid), "count" (lng), "sums" [hge]},
     gid = the group's number in global first-occurrence order (what BATgroup
     over all rows would give).  No per-group host objects: the merge, the

@@ -199,3 +199,64 @@ def test_gdk_backend_rccl_exchange_cols_world1():
         assert not errs, errs
     finally:
         dist.destroy_process_group()
+
+
+def test_gdk_backend_exchange_sources_outlive_collectives():
+    """exchange_cols releases nothing the collectives may still read: the
+    caller drops its source BATs right after the call while another thread
+    (its own library stream, the same caching allocator) allocates and fills
+    BATs of the same size; every received column must still equal what was
+    sent (dist.py: the sources are held until an event recorded after the
+    collectives completes)."""
+    import os
+    import threading
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from monetdb_amd import dist as D
+    from monetdb_amd import gdk
+    from test_distributed import _free_port
+    gdk.init(0)
+    torch.cuda.set_device(0)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    stop = threading.Event()
+    errs = []
+
+    def churn():
+        try:
+            k = 0
+            while not stop.is_set():
+                b = gdk.BATconstant(gdk.TYPE_lng, -7 - k, n)
+                assert b.count() == n
+                del b
+                k += 1
+        except Exception as e:      # surfaced below
+            errs.append(e)
+
+    try:
+        be = D.GdkBackend("cuda:0")
+        r = np.random.default_rng(5)
+        n = 4_000_000
+        th = threading.Thread(target=churn)
+        th.start()
+        try:
+            for it in range(6):
+                vals = [r.integers(-2**62, 2**62, n, dtype=np.int64) for _ in range(3)]
+                cols = [gdk.BAT.from_numpy(gdk.TYPE_lng, v) for v in vals]
+                out, recv = be.exchange_cols(dist, cols, [gdk.TYPE_lng] * 3, [n])
+                del cols                     # the caller lets go at once
+                assert recv == [n]
+                for o, v in zip(out, vals):
+                    assert np.array_equal(o.to_numpy(), v), it
+        finally:
+            stop.set()
+            th.join()
+        assert not errs, errs
+        be.drain(wait=True)
+        assert be._pending == []
+    finally:
+        dist.destroy_process_group()

@@ -1,0 +1,52 @@
+# round-6 GPU steps: bash tools/gpu_r6.sh <step> [...]; each step writes under
+# gpurun_out/r6/<step>/ and runs under its own time limit; the first failing
+# step ends the call
+set -e
+export TMPDIR=/tmp
+T="python -u -m pytest -q --timeout 120 --timeout-method thread -m gpu"
+for step in "$@"; do
+O=gpurun_out/r6/$step
+mkdir -p $O
+case $step in
+gputests)
+	timeout -k 10 900 $T -x tests > $O/tests.log 2>&1
+	;;
+dist)
+	timeout -k 10 300 $T -x tests/test_gpu_distributed.py > $O/tests.log 2>&1
+	;;
+jk)
+	timeout -k 10 600 $T -x tests/test_join_kinds.py tests/test_cand_algebra.py tests/test_theta_join.py tests/test_leftjoin_multi.py > $O/tests.log 2>&1
+	;;
+tests_*)
+	timeout -k 10 600 $T -x ${TESTS} > $O/tests.log 2>&1
+	;;
+bench)
+	timeout -k 10 420 python bench.py > $O/bench.json 2> $O/bench.err
+	;;
+benchprof)
+	cd /tmp && cd $GRAFT_REPO_ROOT
+	timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --no-cpu --no-parity > $O/bench.json 2> $O/bench.err
+	;;
+join)
+	timeout -k 10 200 python tools/opbench.py --only config3 > $O/opbench.json 2> $O/opbench.err
+	cd /tmp && cd $GRAFT_REPO_ROOT
+	timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 tools/opbench.py --only config3 > $O/prof.log 2>&1
+	;;
+joinpmc)
+	cd /tmp && cd $GRAFT_REPO_ROOT
+	timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_VALU --output-format csv -d $O/pmc_sq -o run -- python3 tools/opbench.py --only config3 > $O/pmc_sq.log 2>&1
+	timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $O/pmc_tcc -o run -- python3 tools/opbench.py --only config3 > $O/pmc_tcc.log 2>&1
+	timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f -o run -- python3 tools/opbench.py --only config3 > $O/pmc_f.log 2>&1
+	timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_w -o run -- python3 tools/opbench.py --only config3 > $O/pmc_w.log 2>&1
+	;;
+sort)
+	timeout -k 10 200 python tools/opbench.py --only other_ops > $O/opbench.json 2> $O/opbench.err
+	cd /tmp && cd $GRAFT_REPO_ROOT
+	timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 tools/opbench.py --only other_ops > $O/prof.log 2>&1
+	;;
+*)
+	echo "unknown step $step"; exit 2
+	;;
+esac
+echo "step $step done"
+done
