@@ -268,13 +268,15 @@ int mgdk_BATgroup(mgdk_bat **groups, mgdk_bat **extents, mgdk_bat **histo,
 int mgdk_BATjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r,
 		 mgdk_bat *sl, mgdk_bat *sr, bool nil_matches, mgdk_BUN estimate);
 /* the left-output join family (gdk/gdk.h:2264-2272; gdk_join.c:4320-4407,
- * through leftjoin :4049): BATintersect / BATsemijoin (r2p must be NULL:
- * which of several matches a semi join returns depends on the algorithm)
- * the left candidates with a match, BATdiff those without (not_in: SQL NOT
- * IN), as candidate lists; BATleftjoin / BATouterjoin the (left, match)
- * pairs in left order (outer: a miss pairs with nil) -- refused when a left
- * candidate matches twice (unless match_one asks for the reference's
- * "more than one match").  Integer-like key types */
+ * through leftjoin :4049): BATintersect / BATsemijoin the left candidates
+ * with a match (BATsemijoin's r2p, as algebra.semijoin binds it,
+ * algebra.c:1792: the match kept for each, the one leftjoin's algorithm
+ * keeps), BATdiff those without (not_in: SQL NOT IN), as candidate lists;
+ * BATleftjoin / BATouterjoin the (left, match) pairs in left order (outer: a
+ * miss pairs with nil), a left candidate's several matches in the order
+ * leftjoin's algorithm choice gives them (joinkinds.hip; match_one raises
+ * "more than one match").  Keys of every join type: integers, oid, temporal,
+ * flt / dbl and str (as BATjoin's order-preserving images) */
 mgdk_bat *mgdk_BATintersect(mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, bool nil_matches,
 			    bool max_one, mgdk_BUN estimate);
 mgdk_bat *mgdk_BATdiff(mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, bool nil_matches, bool not_in,
@@ -289,7 +291,7 @@ int mgdk_BATouterjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, 
  * left candidate once (r2p NULL: semi) or with its match (nil on a miss), and
  * the mark column r3 (bit): TRUE on a match; on a miss nil when the left value
  * is nil or a right candidate is nil, else FALSE; no right candidates: FALSE.
- * With r2p, refused when a left candidate matches twice, as BATleftjoin */
+ * With r2p, one row per match in leftjoin's order, as BATouterjoin */
 int mgdk_BATmarkjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat **r3p, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl,
 		     mgdk_bat *sr, mgdk_BUN estimate);
 /* BATthetajoin (gdk/gdk.h; gdk_join.c:4409, nested loop thetajoin :3699):

@@ -1333,6 +1333,104 @@ image_flags_back(mgdk_bat *l, mgdk_bat *r, const mgdk_bat *li, const mgdk_bat *r
 
 }  // namespace
 
+namespace mgdk {
+
+// leftjoin's algorithm choice (gdk/gdk_join.c:4049-4300), for the left-output
+// join family (joinkinds.hip): the branch decides the order of several
+// matches of a left candidate, which match a semi join with a right output
+// keeps, and two quirks (fetchjoin's right-position order, mergejoin's
+// skipped nils).  BATordered / BATordered_rev are evaluated in the
+// reference's order (their findings cached in l and r as it caches them);
+// mergejoin's memory-pressure term (:4185) depends on the host and is taken
+// as false.  *equal_order: mergejoin scans l and r the same way
+// (:2091-2107).  Returns LJ_* or -1.
+int
+leftjoin_algo(mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, const Cand &lc, const Cand &rc,
+	      bool nil_matches, bool nil_on_miss, bool semi, bool only_misses, bool not_in, bool max_one,
+	      bool min_one, bool want_r2, bool *equal_order)
+{
+	*equal_order = true;
+	if (lc.n == 0 || rc.n == 0)
+		return LJ_NOMATCH;
+	Ord lo, ro;
+	int t1, t2;
+#define ORD(x) do { if ((x) < 0) return -1; } while (0)
+	if (!only_misses && !not_in) {
+		if (lc.n == 1)
+			return LJ_SELECT;
+		ORD(t1 = ordered(l, lo));
+		if (t1) {
+			ORD(t2 = ordered_rev(l, lo));
+			if (t2)
+				return LJ_SELECT;
+		}
+		if (l->ttype == MGDK_void && l->tseqbase == MGDK_OID_NIL)
+			return LJ_SELECT;
+	}
+	CandKind lk, rk;
+	if (cand_kind(sl, &lk) < 0 || cand_kind(sr, &rk) < 0)
+		return -1;
+	const bool ldense = lc.dense && !lk.mask && !lk.except, rdense = rc.dense && !rk.mask && !rk.except;
+	if (tdense(r) && rdense)
+		return LJ_MJVOID;
+	if (tdense(l) && ldense && rdense && !semi && !max_one && !min_one && !nil_matches && !only_misses && !not_in) {
+		ORD(t1 = ordered(r, ro));
+		if (!t1)
+			ORD(t1 = ordered_rev(r, ro));
+		if (t1)
+			return LJ_FETCH;
+	}
+	if (tdense(l) && ldense && !want_r2 && (semi || only_misses) && !nil_on_miss && !not_in && !max_one && !min_one)
+		return LJ_BITMASK;
+	ORD(t1 = ordered(r, ro));
+	if (!t1)
+		ORD(t1 = ordered_rev(r, ro));
+	if (t1) {
+		ORD(t2 = ordered(l, lo));
+		if (!t2)
+			ORD(t2 = ordered_rev(l, lo));
+		if (t2 || tdense(r) || lc.n < 1024) {
+			if (l->tsorted || l->trevsorted) {
+				const bool lv = tdense(l) || l->ttype == MGDK_void, rv = tdense(r) || r->ttype == MGDK_void;
+				*equal_order = (l->tsorted && r->tsorted) || (l->trevsorted && r->trevsorted && !lv && !rv);
+			}
+			return LJ_MERGE;
+		}
+	}
+	if (!nil_on_miss && !only_misses && !not_in && !max_one && !min_one) {
+		double lcost, rcost;
+		if (joincost(r, ro, lc.n, rc, sr, rk, &rcost) < 0 || joincost(l, lo, rc.n, lc, sl, lk, &lcost) < 0)
+			return -1;
+		if (semi && !r->tkey)
+			lcost += rc.n;                  // BATunique(r)
+		lcost += rc.n * log((double) rc.n);     // the sort of the swapped result
+		if (lcost < rcost)
+			return LJ_SWAP;
+	}
+	return LJ_HASH;
+#undef ORD
+}
+
+mgdk_bat *
+join_float_image(const mgdk_bat *b)
+{
+	return float_image(b);
+}
+
+int
+join_str_images(mgdk_bat *l, mgdk_bat *r, mgdk_bat **lip, mgdk_bat **rip)
+{
+	return str_images(l, r, lip, rip);
+}
+
+void
+join_image_flags_back(mgdk_bat *l, mgdk_bat *r, const mgdk_bat *li, const mgdk_bat *ri)
+{
+	image_flags_back(l, r, li, ri);
+}
+
+}  // namespace mgdk
+
 extern "C" int
 mgdk_BATjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr,
 	     bool nil_matches, mgdk_BUN estimate)

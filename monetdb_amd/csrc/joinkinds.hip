@@ -3,25 +3,36 @@
 // SQL NOT IN semantics), BATleftjoin and BATouterjoin (gdk_join.c:4320-4407,
 // all through leftjoin :4049), and BATmarkjoin (:4367).
 //
-// What these return does not depend on which of leftjoin's algorithms runs
-// (selectjoin, mergejoin_void, fetchjoin, bitmaskjoin, mergejoin, hashjoin):
-// it is the left candidates, in order, with or without a match among the
-// right candidates (and, for left / outer joins, that match).  So the device
-// runs one plan for all of them:
+// A left candidate's matches do not depend on which of leftjoin's algorithms
+// runs (selectjoin, mergejoin_void, fetchjoin, bitmaskjoin, mergejoin,
+// hashjoin, the swapped hashjoin); their order, which one a semi join with a
+// right output keeps, and two quirks do.  So the device runs one plan and
+// asks the reference's algorithm choice (joinalgo.hip leftjoin_algo) only
+// when the answer depends on it:
 //   the right candidates' values as sign-extended 64-bit images with their
-//   oids, sorted by value (BATsort, stable: ties by oid);
-//   per left candidate one binary search: its match count (capped at 2) and
-//   first match;
-//   flags -> the select path's ordered compaction -> the left oids (and the
-//   matches) of the kept candidates.
+//   candidate indexes, sorted by value (BATsort, stable: ties by index);
+//   per left candidate two binary searches: its match range and count;
+//   one match per candidate (or only the left output): flags -> the select
+//   path's ordered compaction -> the left oids (and the matches);
+//   several matches with a right output: per candidate its row count, an
+//   exclusive scan, and each candidate writes its rows in the algorithm's
+//   order -- ascending (selectjoin, mergejoin), descending (hashjoin: the
+//   hash chains), the first / last match for semi (selectjoin, the swapped
+//   hash join's BATunique; hashjoin, mergejoin in equal order), the swapped
+//   hash join's pairs in hashjoin(r, l) order put through the GDKqsort
+//   replay (qsort.hip) as the reference sorts them (gdk_join.c:4236);
+//   fetchjoin (dense l): the rows in right position order, i.e. the left
+//   candidates descending when r is reverse sorted, and no rows for misses
+//   (the reference reaches it without checking nil_on_miss, :4156-4168).
 // The reference's nil rules are kept: a nil matches only with nil_matches
 // (gdk_join.c:3127, :2338); NOT IN drops nil left values and gives nothing
 // when a right candidate is nil (:3027-3060, :2038), except on the dense-
-// right path mergejoin_void (:4096-4101), which has no not_in argument;
-// empty sides give nomatch (:301-360); max_one / match_one raise "more than
-// one match" (:2760).  A left / outer join where a left candidate matches
-// twice is refused loudly: the order of several matches depends on the
-// algorithm, which this plan does not replay.
+// right path mergejoin_void (:4096-4101), which has no not_in; mergejoin
+// over an ordered l skips l's nils before its scan, so BATdiff does not list
+// them there (:2093-2100); empty sides give nomatch (:301-360); max_one /
+// match_one raise "more than one match" (:2760), selectjoin's min_one "not
+// enough matches" (:399-404).  flt / dbl / str keys join as BATjoin's order-
+// and equality-preserving integer images (joinalgo.hip).
 #include "mgdk_internal.h"
 
 using namespace mgdk;
@@ -77,6 +88,13 @@ k_jk_rvals(JSide r, int64_t *rv, oid *ro, uint32_t *anynil)
 }
 
 __global__ __launch_bounds__(256) void
+k_jk_iota(BUN n, oid *dst)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
+		dst[i] = i;
+}
+
+__global__ __launch_bounds__(256) void
 k_jk_gather(const oid *order, BUN n, const oid *ro, oid *dst)
 {
 	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
@@ -86,13 +104,15 @@ k_jk_gather(const oid *order, BUN n, const oid *ro, oid *dst)
 // mode 0 semi, 1 anti, 2 left, 3 outer, 4 mark; flags[i] = keep the
 // candidate; match[i] = its first match (nil: none); mark[i] (mode 4): TRUE on
 // a match, on a miss nil when the left value or a right candidate (*rnil) is
-// nil, else FALSE (gdk_join.c:3026-3076, :3127-3133); err |= 1: two matches,
-// 2: a miss, 4: a nil mark
+// nil, else FALSE (gdk_join.c:3026-3076, :3127-3133); lob[i] / cnt[i]: its
+// match range in the sorted right images (optional).  err bits: 1 two
+// matches, 2 a miss, 4 a nil mark, 8 a nil left value, 16 a miss of a left
+// value that can match, 32 a count of 2^32 or more
 __global__ __launch_bounds__(256) void
 k_jk_probe(JSide l, const int64_t *rv, const oid *ro, BUN nr, bool nil_matches, bool not_in, int mode,
-	   int8_t *flags, oid *match, int8_t *mark, const uint32_t *rnil, uint32_t *err)
+	   int8_t *flags, oid *match, int8_t *mark, const uint32_t *rnil, uint64_t *lob, uint32_t *cntb, uint32_t *err)
 {
-	bool two = false, miss = false, mnil = false;
+	uint32_t f = 0;
 	const bool rhasnil = mark && *rnil != 0;
 	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < l.n; i += (BUN) gridDim.x * blockDim.x) {
 		const oid lo = js_oid(l, i);
@@ -112,10 +132,18 @@ k_jk_probe(JSide l, const int64_t *rv, const oid *ro, BUN nr, bool nil_matches, 
 					b = m;
 			}
 			at = a;
-			cnt = (a < nr && rv[a] == v) + (a + 1 < nr && rv[a + 1] == v);
+			BUN c = a, d = nr;
+			while (c < d) {
+				const BUN m = (c + d) >> 1;
+				if (rv[m] <= v)
+					c = m + 1;
+				else
+					d = m;
+			}
+			cnt = c - a;
+			f |= cnt == 0 ? 16u : 0u;
 		}
-		two |= cnt > 1;
-		miss |= cnt == 0;
+		f |= (cnt > 1 ? 1u : 0u) | (cnt == 0 ? 2u : 0u) | (isnil ? 8u : 0u) | (cnt >> 32 ? 32u : 0u);
 		int8_t keep;
 		switch (mode) {
 		case 0: keep = cnt > 0; break;
@@ -129,12 +157,109 @@ k_jk_probe(JSide l, const int64_t *rv, const oid *ro, BUN nr, bool nil_matches, 
 		if (mark) {
 			const int8_t m = cnt ? 1 : (isnil || rhasnil) ? INT8_MIN : 0;
 			mark[i] = m;
-			mnil |= m == INT8_MIN;
+			f |= m == INT8_MIN ? 4u : 0u;
+		}
+		if (lob) {
+			lob[i] = at;
+			cntb[i] = (uint32_t) (cnt >> 32 ? 0xffffffffu : cnt);
 		}
 	}
-	const uint32_t f = (__any(two) ? 1u : 0u) | (__any(miss) ? 2u : 0u) | (__any(mnil) ? 4u : 0u);
+	for (int o = 32; o > 0; o >>= 1)
+		f |= __shfl_xor(f, o);
 	if (f && __lane_id() == 0)
 		atomicOr(err, f);
+}
+
+// mergejoin over an ordered l skips l's nil values (gdk_join.c:2093-2100):
+// BATdiff's flags of nil left values cleared
+__global__ __launch_bounds__(256) void
+k_jk_dropnil(JSide l, int8_t *flags)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < l.n; i += (BUN) gridDim.x * blockDim.x) {
+		bool isnil;
+		(void) js_val(l, js_oid(l, i) - l.hseq, isnil);
+		if (isnil)
+			flags[i] = 0;
+	}
+}
+
+// the rows each left candidate puts out when it may have several matches:
+// semi one per match found, left one per match, outer / mark one per match
+// or one nil row (fetchjoin: no nil rows)
+__global__ __launch_bounds__(256) void
+k_jk_ocnt(BUN n, const uint32_t *cnt, int mode, bool fetch, uint32_t *ocnt)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		const uint32_t c = cnt[i];
+		ocnt[i] = mode == 0 ? (c > 0) : (mode == 2 || fetch) ? c : (c > 0 ? c : 1u);
+	}
+}
+
+// the order a left candidate's matches leave in (see the head of this file)
+enum { JK_ASC = 0, JK_DESC = 1, JK_FIRST = 2, JK_LAST = 3 };
+
+// each left candidate writes its rows at its offset (rev: the candidates'
+// blocks in reverse order, fetchjoin over a reverse-sorted r); sidx: the
+// right candidate index of each sorted image; mk: the probe's per-candidate
+// mark (for a miss); pairs (optional): (right index << 32 | ~left index)
+// keys of the swapped hash join instead of the result columns
+__global__ __launch_bounds__(256) void
+k_jk_emit(JSide L, JSide R, const uint64_t *lob, const uint32_t *cnt, const uint32_t *ocnt, const uint64_t *off,
+	  uint64_t tot, bool rev, int kind, const oid *sidx, const int8_t *mk, oid *r1, oid *r2, int8_t *r3,
+	  int64_t *pairs)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < L.n; i += (BUN) gridDim.x * blockDim.x) {
+		const uint32_t q = ocnt[i], c = cnt[i];
+		if (q == 0)
+			continue;
+		const uint64_t o = rev ? tot - off[i] - q : off[i];
+		const oid lo = js_oid(L, i);
+		if (c == 0) {
+			r1[o] = lo;
+			if (r2)
+				r2[o] = MGDK_OID_NIL;
+			if (r3)
+				r3[o] = mk[i];
+			continue;
+		}
+		const uint64_t a = lob[i];
+		for (uint32_t k = 0; k < q; k++) {
+			const uint64_t p = kind == JK_ASC ? a + k : kind == JK_DESC ? a + c - 1 - k
+					   : kind == JK_FIRST ? a : a + c - 1;
+			const oid ri = sidx[p];
+			if (pairs) {
+				pairs[o + k] = (int64_t) ((ri << 32) | (0xffffffffull - i));
+				continue;
+			}
+			r1[o + k] = lo;
+			if (r2)
+				r2[o + k] = js_oid(R, ri);
+			if (r3)
+				r3[o + k] = 1;
+		}
+	}
+}
+
+// the swapped hash join's sorted pair keys -> GDKqsort replay input
+// (rank = left candidate index, payload = right candidate index)
+__global__ __launch_bounds__(256) void
+k_jk_swkeys(const int64_t *keys, uint64_t n, uint32_t *rank, uint64_t *pay)
+{
+	for (BUN k = (BUN) blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (BUN) gridDim.x * blockDim.x) {
+		const uint64_t x = (uint64_t) keys[k];
+		rank[k] = 0xffffffffu - (uint32_t) x;
+		pay[k] = x >> 32;
+	}
+}
+
+__global__ __launch_bounds__(256) void
+k_jk_swout(const uint32_t *rank, const uint64_t *pay, uint64_t n, JSide L, JSide R, oid *r1, oid *r2)
+{
+	for (BUN k = (BUN) blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (BUN) gridDim.x * blockDim.x) {
+		r1[k] = js_oid(L, rank[k]);
+		if (r2)
+			r2[k] = js_oid(R, pay[k]);
+	}
 }
 
 __global__ __launch_bounds__(256) void
@@ -183,7 +308,7 @@ atomtype(int t)
 
 // b (msk / mask forms unmasked, as leftjoin does) and its candidates as a JSide
 int
-jside(const char *fn, mgdk_bat *b, mgdk_bat *s, JSide *j, Held &held, mgdk_bat **bout)
+jside(const char *fn, mgdk_bat *b, mgdk_bat *s, JSide *j, Held &held, mgdk_bat **bout, Cand *cout = nullptr)
 {
 	if (b->ttype == MGDK_msk || is_complex_cand(b)) {
 		if ((b = held.keep(unmask_cand(b))) == nullptr)
@@ -197,6 +322,8 @@ jside(const char *fn, mgdk_bat *b, mgdk_bat *s, JSide *j, Held &held, mgdk_bat *
 	*j = JSide{b->ttype == MGDK_void ? nullptr : b->theap, b->twidth, b->tseqbase, b->hseqbase, ci.dense, ci.seq,
 		   ci.oids, ci.n};
 	*bout = b;
+	if (cout)
+		*cout = ci;
 	(void) fn;
 	return 0;
 }
@@ -214,10 +341,10 @@ struct Own {
 };
 
 // the shared plan; mode as k_jk_probe.  r1 (and r2, and for mode 4 the
-// mark column r3) out
+// mark column r3) out; semi (mode 0) with r2p: BATsemijoin's right output
 int
 jk_run(const char *fn, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, bool nil_matches, bool not_in,
-       bool max_one, int mode, mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat **r3p = nullptr)
+       bool max_one, int mode, mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat **r3p = nullptr, bool min_one = false)
 {
 	*r1p = nullptr;
 	if (r2p)
@@ -228,10 +355,34 @@ jk_run(const char *fn, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, boo
 		seterr("%s: inputs must not be NULL", fn);
 		return -1;
 	}
+	// flt / dbl / str keys: BATjoin's integer images keep equality, order
+	// and nil, so every choice and result below is the keys' own
+	{
+		const int lt = basetype(l->ttype), rt = basetype(r->ttype);
+		if ((lt == MGDK_flt || lt == MGDK_dbl || l->ttype == MGDK_str) && lt == rt && l->ttype == r->ttype) {
+			mgdk_bat *li = nullptr, *ri = nullptr;
+			if (l->ttype == MGDK_str) {
+				if (join_str_images(l, r, &li, &ri) != 0)
+					return -1;
+			} else {
+				li = join_float_image(l);
+				ri = li ? join_float_image(r) : nullptr;
+			}
+			int rc = -1;
+			if (li && ri) {
+				rc = jk_run(fn, li, ri, sl, sr, nil_matches, not_in, max_one, mode, r1p, r2p, r3p, min_one);
+				join_image_flags_back(l, r, li, ri);
+			}
+			mgdk_BBPunfix(li);
+			mgdk_BBPunfix(ri);
+			return rc;
+		}
+	}
 	Held held;
 	JSide L, R;
+	Cand LC, RC;
 	mgdk_bat *lb, *rb;
-	if (jside(fn, l, sl, &L, held, &lb) < 0 || jside(fn, r, sr, &R, held, &rb) < 0)
+	if (jside(fn, l, sl, &L, held, &lb, &LC) < 0 || jside(fn, r, sr, &R, held, &rb, &RC) < 0)
 		return -1;
 	if (atomtype(lb->ttype) != atomtype(rb->ttype)) {
 		seterr("%s: inputs not compatible.", fn);
@@ -243,7 +394,9 @@ jk_run(const char *fn, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, boo
 	}
 	ProfScope prof("joinkinds");
 	hipStream_t st = stream();
-	const bool want_r2 = mode == 4 ? r2p != nullptr : mode >= 2;
+	const bool want_r2 = mode == 4 || mode == 0 ? r2p != nullptr : mode >= 2;
+	const bool nil_on_miss = mode >= 3;
+	const bool semi = mode == 0 || (mode == 4 && r2p == nullptr);
 	Own mk;
 	// nomatch (gdk_join.c:301-360): semi / left -> empty; anti / outer / mark
 	// -> every left candidate (outer, mark: with nil matches; mark: FALSE,
@@ -256,7 +409,7 @@ jk_run(const char *fn, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, boo
 			if ((mk.b = mgdk_BATconstant(0, MGDK_bit, &f, n)) == nullptr)
 				return -1;
 		}
-		if (mode <= 1 && L.dense) {
+		if (mode <= 1 && L.dense && !want_r2) {
 			*r1p = mgdk_BATdense(0, n ? L.seq : 0, n);
 			return *r1p ? 0 : -1;
 		}
@@ -297,14 +450,14 @@ jk_run(const char *fn, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, boo
 			b->tsorted = b->trevsorted = 1;
 			b->tkey = n <= 1;
 		}
-		*r1p = a;
+		*r1p = mode == 0 ? cand_finish(a, n) : a;
 		if (r2p)
 			*r2p = b;
 		else
 			mgdk_BBPunfix(b);
 		if (r3p)
 			*r3p = mk.release();
-		return 0;
+		return *r1p ? 0 : -1;
 	}
 	if (mode == 4 && (mk.b = newbat(0, MGDK_bit, L.n)) == nullptr)
 		return -1;
@@ -313,13 +466,16 @@ jk_run(const char *fn, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, boo
 						    : (rb->ttype == MGDK_oid && rb->tseqbase != MGDK_OID_NIL);
 	if (rtdense && R.dense)
 		not_in = false;
-	// right candidates' images sorted, with their oids
+	// right candidates' images sorted, with their candidate indexes (the
+	// sort's order) and oids
 	mgdk_bat *rvb = held.keep(newbat(0, MGDK_lng, R.n));
 	// flags in a buffer of their own: BATsort below uses meta_buf()
 	DevBuf ro(R.n * 8 + 8), so(R.n * 8 + 8), fl(L.n + 8), mt(want_r2 ? L.n * 8 + 8 : 8), mb(16);
+	DevBuf lob(L.n * 8 + 8), cnt(L.n * 4 + 8);
 	uint32_t *meta = mb.as<uint32_t>();
 	uint32_t *h = (uint32_t *) pinned(16);
-	if (rvb == nullptr || !ro.p || !so.p || !fl.p || !mt.p || !mb.p || !hip_ok(hipMemsetAsync(meta, 0, 8, st), "memset"))
+	if (rvb == nullptr || !ro.p || !so.p || !fl.p || !mt.p || !mb.p || !lob.p || !cnt.p ||
+	    !hip_ok(hipMemsetAsync(meta, 0, 8, st), "memset"))
 		return -1;
 	hipLaunchKernelGGL(k_jk_rvals, dim3(grid_for(R.n, 256 * 8, 8192)), dim3(256), 0, st, R,
 			   (int64_t *) rvb->theap, ro.as<oid>(), meta);
@@ -331,15 +487,14 @@ jk_run(const char *fn, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, boo
 		return -1;
 	held.keep(sv);
 	held.keep(sord);
-	// sorted right oids
-	{
-		const oid *ord = sord->ttype == MGDK_void ? nullptr : (const oid *) sord->theap;
-		if (ord)
-			hipLaunchKernelGGL(k_jk_gather, dim3(grid_for(R.n, 256 * 8, 8192)), dim3(256), 0, st, ord, R.n,
-					   (const oid *) ro.p, so.as<oid>());
-		else if (!hip_ok(hipMemcpyAsync(so.p, ro.p, R.n * 8, hipMemcpyDeviceToDevice, st), "memcpy"))
-			return -1;
-	}
+	// sorted right oids; the sort's order = the candidate indexes
+	const oid *ord = sord->ttype == MGDK_void ? nullptr : (const oid *) sord->theap;
+	DevBuf sidxb(ord ? 8 : R.n * 8 + 8);
+	if (ord)
+		hipLaunchKernelGGL(k_jk_gather, dim3(grid_for(R.n, 256 * 8, 8192)), dim3(256), 0, st, ord, R.n,
+				   (const oid *) ro.p, so.as<oid>());
+	else if (!sidxb.p || !hip_ok(hipMemcpyAsync(so.p, ro.p, R.n * 8, hipMemcpyDeviceToDevice, st), "memcpy"))
+		return -1;
 	const int64_t *rvs = sv->ttype == MGDK_void ? nullptr : (const int64_t *) sv->theap;
 	if (rvs == nullptr) {
 		seterr("%s: sorted right values", fn);
@@ -347,7 +502,8 @@ jk_run(const char *fn, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, boo
 	}
 	hipLaunchKernelGGL(k_jk_probe, dim3(grid_for(L.n, 256 * 8, 8192)), dim3(256), 0, st, L, rvs, so.as<oid>(), R.n,
 			   nil_matches, not_in, mode, fl.as<int8_t>(), want_r2 ? mt.as<oid>() : (oid *) nullptr,
-			   mk.b ? (int8_t *) mk.b->theap : (int8_t *) nullptr, (const uint32_t *) meta, meta + 1);
+			   mk.b ? (int8_t *) mk.b->theap : (int8_t *) nullptr, (const uint32_t *) meta, lob.as<uint64_t>(),
+			   cnt.as<uint32_t>(), meta + 1);
 	if (!hip_ok(hipMemcpyAsync(h, meta, 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
 		return -1;
 	// copies: compact_flags below reuses the pinned buffer
@@ -356,14 +512,145 @@ jk_run(const char *fn, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, boo
 		seterr("more than one match");
 		return -1;
 	}
-	if ((perr & 1) && mode >= 2 && want_r2) {
-		seterr("%s: a left row with several matches is not on the device path", fn);
-		return -1;
-	}
 	if (not_in && rnil) {
 		// NOT IN a set holding a nil: nothing qualifies
 		*r1p = mgdk_BATdense(0, 0, 0);
 		return *r1p ? 0 : -1;
+	}
+	// the reference's algorithm choice, where the answer depends on it
+	int algo = -1;
+	bool eqo = true;
+	const bool ltdense = lb->ttype == MGDK_void ? lb->tseqbase != MGDK_OID_NIL
+						    : (lb->ttype == MGDK_oid && lb->tseqbase != MGDK_OID_NIL);
+	const bool multi = (perr & 1) && want_r2;
+	const bool need = multi || (mode == 1 && !not_in && !nil_matches && (perr & 8)) ||
+			  (mode >= 2 && want_r2 && ltdense && !nil_matches) || (min_one && (perr & 16));
+	if (need) {
+		algo = leftjoin_algo(lb, rb, sl, sr, LC, RC,
+				     nil_matches, nil_on_miss, semi, mode == 1, not_in, max_one, min_one, want_r2, &eqo);
+		if (algo < 0)
+			return -1;
+	}
+	if (min_one && (perr & 16) && algo == LJ_SELECT) {
+		seterr("not enough matches");
+		return -1;
+	}
+	if (mode == 1 && algo == LJ_MERGE && (lb->tsorted || lb->trevsorted))
+		hipLaunchKernelGGL(k_jk_dropnil, dim3(grid_for(L.n, 256 * 8, 8192)), dim3(256), 0, st, L, fl.as<int8_t>());
+	if (multi || algo == LJ_FETCH) {
+		if (perr & 32) {
+			seterr("%s: a left value with 2^32 or more matches is not on the device path", fn);
+			return -1;
+		}
+		const bool fetch = algo == LJ_FETCH;
+		const bool rev = fetch && !rb->tsorted;
+		DevBuf ocnt(L.n * 4 + 8), off(L.n * 8 + 8);
+		if (!ocnt.p || !off.p)
+			return -1;
+		hipLaunchKernelGGL(k_jk_ocnt, dim3(grid_for(L.n, 256 * 8, 8192)), dim3(256), 0, st, L.n,
+				   cnt.as<const uint32_t>(), mode, fetch, ocnt.as<uint32_t>());
+		uint64_t tot = 0;
+		if (exclusive_scan(ocnt.as<const uint32_t>(), off.as<uint64_t>(), L.n, &tot) != 0)
+			return -1;
+		int kind = JK_ASC;
+		if (semi)
+			kind = algo == LJ_HASH || (algo == LJ_MERGE && eqo) ? JK_LAST : JK_FIRST;
+		else if (algo == LJ_HASH)
+			kind = JK_DESC;
+		const oid *sidx = ord ? ord : nullptr;
+		if (sidx == nullptr) {
+			// the right images were already in order: index i is i
+			hipLaunchKernelGGL(k_jk_iota, dim3(grid_for(R.n, 256 * 8, 8192)), dim3(256), 0, st, R.n,
+					   sidxb.as<oid>());
+			sidx = sidxb.as<const oid>();
+		}
+		Own A, B;
+		if ((A.b = newbat(0, MGDK_oid, tot)) == nullptr || (want_r2 && (B.b = newbat(0, MGDK_oid, tot)) == nullptr))
+			return -1;
+		Own M;
+		if (mode == 4 && (M.b = newbat(0, MGDK_bit, tot)) == nullptr)
+			return -1;
+		const bool swap = algo == LJ_SWAP && !semi;
+		if (swap) {
+			// hashjoin(r, l)'s pairs -- right candidates in order, each
+			// one's left matches descending -- then GDKqsort on the left
+			// oids (gdk_join.c:4203-4251)
+			if (R.n >= ((BUN) 1 << 31) || L.n >= ((BUN) 1 << 32) || tot >= ((uint64_t) 1 << 32)) {
+				seterr("%s: swapped hash join of more than 2^31 rows is not on the device path", fn);
+				return -1;
+			}
+			mgdk_bat *pk = held.keep(newbat(0, MGDK_lng, tot));
+			if (pk == nullptr)
+				return -1;
+			if (tot)
+				hipLaunchKernelGGL(k_jk_emit, dim3(grid_for(L.n, 256 * 4, 8192)), dim3(256), 0, st, L, R,
+						   lob.as<const uint64_t>(), cnt.as<const uint32_t>(), ocnt.as<const uint32_t>(),
+						   off.as<const uint64_t>(), tot, false, (int) JK_ASC, sidx, (const int8_t *) nullptr,
+						   (oid *) nullptr, (oid *) nullptr, (int8_t *) nullptr, (int64_t *) pk->theap);
+			pk->count = tot;
+			pk->tsorted = pk->trevsorted = pk->tkey = tot <= 1;
+			pk->tnonil = 1;
+			mgdk_bat *ps = nullptr;
+			if (tot > 1) {
+				if (mgdk_BATsort(&ps, nullptr, nullptr, pk, nullptr, nullptr, false, false, false) != 0)
+					return -1;
+				held.keep(ps);
+			}
+			DevBuf rank(tot * 4 + 8), pay(tot * 8 + 8);
+			if (!rank.p || !pay.p)
+				return -1;
+			if (tot)
+				hipLaunchKernelGGL(k_jk_swkeys, dim3(grid_for(tot, 256 * 8, 8192)), dim3(256), 0, st,
+						   (const int64_t *) (ps ? ps->theap : pk->theap), tot, rank.as<uint32_t>(),
+						   pay.as<uint64_t>());
+			if (tot > 1) {
+				std::vector<std::pair<uint64_t, uint32_t>> segs{{0, (uint32_t) tot}};
+				if (qsort_replay(rank.as<uint32_t>(), pay.as<uint64_t>(), tot, segs) < 0)
+					return -1;
+			}
+			if (tot)
+				hipLaunchKernelGGL(k_jk_swout, dim3(grid_for(tot, 256 * 8, 8192)), dim3(256), 0, st,
+						   rank.as<const uint32_t>(), pay.as<const uint64_t>(), tot, L, R, (oid *) A.b->theap,
+						   B.b ? (oid *) B.b->theap : (oid *) nullptr);
+		} else if (tot) {
+			hipLaunchKernelGGL(k_jk_emit, dim3(grid_for(L.n, 256 * 4, 8192)), dim3(256), 0, st, L, R,
+					   lob.as<const uint64_t>(), cnt.as<const uint32_t>(), ocnt.as<const uint32_t>(),
+					   off.as<const uint64_t>(), tot, rev, kind, sidx,
+					   mk.b ? (const int8_t *) mk.b->theap : (const int8_t *) nullptr, (oid *) A.b->theap,
+					   B.b ? (oid *) B.b->theap : (oid *) nullptr, M.b ? (int8_t *) M.b->theap : (int8_t *) nullptr,
+					   (int64_t *) nullptr);
+		}
+		if (!sync())
+			return -1;
+		mgdk_bat *a = A.release();
+		a->count = tot;
+		const bool onekey = semi || !(perr & 1);
+		a->tsorted = !rev || tot <= 1;
+		a->trevsorted = rev || tot <= 1;
+		a->tkey = onekey || tot <= 1;
+		a->tnonil = 1;
+		a->tnil = 0;
+		const bool misses = nil_on_miss && !fetch && (perr & 2);
+		if (B.b) {
+			B.b->count = tot;
+			B.b->tsorted = B.b->trevsorted = B.b->tkey = tot <= 1;
+			B.b->tnil = misses;
+			B.b->tnonil = !misses;
+		}
+		if (M.b) {
+			M.b->count = tot;
+			M.b->tnil = misses && (perr & 4);
+			M.b->tnonil = !M.b->tnil;
+			M.b->tsorted = M.b->trevsorted = M.b->tkey = tot <= 1;
+		}
+		*r1p = semi ? cand_finish(a, tot) : a;
+		if (*r1p == nullptr)
+			return -1;
+		if (r2p)
+			*r2p = B.release();
+		if (r3p)
+			*r3p = M.release();
+		return 0;
 	}
 	// the kept candidates
 	mgdk_bat *pos = held.keep(compact_flags(fl.as<int8_t>(), L.n, 0));
@@ -372,7 +659,7 @@ jk_run(const char *fn, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, boo
 	const BUN n = pos->count;
 	const oid *idx = pos->ttype == MGDK_void ? nullptr : (const oid *) pos->theap;
 	const oid i0 = pos->ttype == MGDK_void ? pos->tseqbase : 0;
-	if (mode <= 1 && L.dense) {
+	if (mode <= 1 && L.dense && !want_r2) {
 		// dense candidates: the positions are the oids shifted
 		mgdk_bat *a = newbat(0, MGDK_oid, n);
 		if (a == nullptr)
@@ -409,8 +696,21 @@ jk_run(const char *fn, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, boo
 	a->tsorted = a->tkey = a->tnonil = 1;
 	a->trevsorted = n <= 1;
 	if (mode <= 1) {
+		if (b) {
+			// BATsemijoin's right output: one match per kept candidate
+			b->count = n;
+			b->tsorted = b->trevsorted = b->tkey = n <= 1;
+			b->tnil = 0;
+			b->tnonil = 1;
+		}
 		*r1p = cand_finish(a, n);
-		return *r1p ? 0 : -1;
+		if (*r1p == nullptr) {
+			mgdk_BBPunfix(b);
+			return -1;
+		}
+		if (r2p)
+			*r2p = b;
+		return 0;
 	}
 	if (mode == 4) {
 		// every left candidate is kept: the marks are in candidate order
@@ -1090,12 +1390,7 @@ mgdk_BATsemijoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk_
 		 bool nil_matches, bool max_one, mgdk_BUN estimate)
 {
 	(void) estimate;
-	if (r2p != nullptr) {
-		*r2p = nullptr;
-		seterr("BATsemijoin: the right output (which match of several) is not on the device path");
-		return -1;
-	}
-	return jk_run("BATsemijoin", l, r, sl, sr, nil_matches, false, max_one, 0, r1p, nullptr);
+	return jk_run("BATsemijoin", l, r, sl, sr, nil_matches, false, max_one, 0, r1p, r2p);
 }
 
 extern "C" int
@@ -1111,12 +1406,11 @@ mgdk_BATouterjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk
 		  bool nil_matches, bool match_one, mgdk_BUN estimate)
 {
 	(void) estimate;
-	return jk_run("BATouterjoin", l, r, sl, sr, nil_matches, false, match_one, 3, r1p, r2p);
+	return jk_run("BATouterjoin", l, r, sl, sr, nil_matches, false, match_one, 3, r1p, r2p, nullptr, match_one);
 }
 
 // BATmarkjoin (gdk_join.c:4367): leftjoin with nil_on_miss, semi when r2p is
-// NULL; a left candidate with two matches and r2p set is refused (see the
-// head of this file)
+// NULL
 extern "C" int
 mgdk_BATmarkjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat **r3p, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl,
 		 mgdk_bat *sr, mgdk_BUN estimate)

@@ -163,6 +163,16 @@ int exclusive_scan_nosync(const uint32_t *in, uint64_t *out, BUN n, uint64_t *ws
 int radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32_t *vals_alt,
 		     BUN n, int bits, uint64_t **keys_out, uint32_t **vals_out);
 
+// leftjoin's algorithm choice (joinalgo.hip; gdk_join.c:4049-4300)
+enum { LJ_NOMATCH = 0, LJ_SELECT = 1, LJ_MJVOID = 2, LJ_FETCH = 3, LJ_BITMASK = 4, LJ_MERGE = 5, LJ_SWAP = 6,
+       LJ_HASH = 7 };
+int leftjoin_algo(mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, const Cand &lc, const Cand &rc,
+		  bool nil_matches, bool nil_on_miss, bool semi, bool only_misses, bool not_in, bool max_one,
+		  bool min_one, bool want_r2, bool *equal_order);
+// BATjoin's key images for flt / dbl and str (joinalgo.hip)
+mgdk_bat *join_float_image(const mgdk_bat *b);
+int join_str_images(mgdk_bat *l, mgdk_bat *r, mgdk_bat **lip, mgdk_bat **rip);
+void join_image_flags_back(mgdk_bat *l, mgdk_bat *r, const mgdk_bat *li, const mgdk_bat *ri);
 // GDKqsort's permutation (qsort.hip) of every segment (start, len) of the
 // rows (rank, pay): ranks are the rows' dense ranks in the requested order
 int qsort_replay(uint32_t *rank, uint64_t *pay, BUN n, const std::vector<std::pair<uint64_t, uint32_t>> &segs);

@@ -763,11 +763,14 @@ def BATdiff(l, r, sl=None, sr=None, nil_matches=False, not_in=False, estimate=0)
     return BAT(lib().mgdk_BATdiff(l.ptr, r.ptr, _p(sl), _p(sr), nil_matches, not_in, estimate))
 
 
-def BATsemijoin(l, r, sl=None, sr=None, nil_matches=False, max_one=False, estimate=0):
-    """gdk_join.c:4346 with r2p = NULL: the left output (a candidate list)."""
-    a = P()
-    _chk(lib().mgdk_BATsemijoin(C.byref(a), None, l.ptr, r.ptr, _p(sl), _p(sr), nil_matches, max_one, estimate))
-    return BAT(a)
+def BATsemijoin(l, r, sl=None, sr=None, nil_matches=False, max_one=False, estimate=0, want_r2=False):
+    """gdk_join.c:4346: the left output (a candidate list); with want_r2 also
+    the right output, one match per kept left candidate (algebra.semijoin,
+    algebra.c:1792), as (r1, r2)."""
+    a, b = P(), P()
+    _chk(lib().mgdk_BATsemijoin(C.byref(a), C.byref(b) if want_r2 else None, l.ptr, r.ptr, _p(sl), _p(sr),
+                                nil_matches, max_one, estimate))
+    return (BAT(a), BAT(b)) if want_r2 else BAT(a)
 
 
 def BATleftjoin(l, r, sl=None, sr=None, nil_matches=False, estimate=0):

@@ -155,6 +155,12 @@ ora_bat *ora_semijoin_cands(ora_bat *l, ora_bat *r, const ora_bat *sl, const ora
 			    bool max_one, bool only_misses, bool not_in);
 int ora_leftjoin(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r, const ora_bat *sl, const ora_bat *sr,
 		 bool nil_matches, bool outer, bool match_one);
+/* leftjoin (gdk_join.c:4049) with its algorithm choice, for several matches
+ * per left candidate: BATleftjoin / BATouterjoin / BATsemijoin with r2p /
+ * BATmarkjoin (r3p); *algo = the branch taken (gdk_oracle_join.c LJ_*) */
+int ora_leftjoin_ex(ora_bat **r1p, ora_bat **r2p, ora_bat **r3p, ora_bat *l, ora_bat *r, const ora_bat *sl,
+		    const ora_bat *sr, bool nil_matches, bool nil_on_miss, bool semi, bool max_one, bool min_one,
+		    int *algo);
 /* gdk_join.c:4367 BATmarkjoin; r2p may be NULL (semi) */
 int ora_markjoin(ora_bat **r1p, ora_bat **r2p, ora_bat **r3p, ora_bat *l, ora_bat *r, const ora_bat *sl,
 		 const ora_bat *sr);

@@ -991,6 +991,13 @@ vpair_cmp(const void *a, const void *b)
 	return x->o < y->o ? -1 : x->o > y->o;
 }
 
+/* leftjoin's algorithms (gdk_join.c:4049-4300; lj_algo below) */
+enum { LJ_NOMATCH = 0, LJ_SELECT = 1, LJ_MJVOID = 2, LJ_FETCH = 3, LJ_BITMASK = 4, LJ_MERGE = 5, LJ_SWAP = 6,
+       LJ_HASH = 7 };
+static int lj_algo(ora_bat *l, ora_bat *r, const ora_bat *sl, const ora_bat *sr, const ora_ci *lci,
+		   const ora_ci *rci, bool nil_matches, bool nil_on_miss, bool semi, bool only_misses, bool not_in,
+		   bool max_one, bool min_one, bool want_r2, bool *equal_order);
+
 /* the right candidates' (value, oid), sorted; *rnil: some value is nil */
 static vpair *
 rpairs(const ora_bat *r, const ora_ci *rci, bool *rnil)
@@ -1061,6 +1068,15 @@ ora_semijoin_cands(ora_bat *l, ora_bat *r, const ora_bat *sl, const ora_bat *sr,
 	} else {
 		if (tdense(r) && rci.dense)
 			not_in = false;             /* mergejoin_void */
+		/* mergejoin with an ordered l skips l's nils before its scan when
+		 * neither nil_matches nor nil_on_miss is set (gdk_join.c:2093-2100):
+		 * BATdiff then does not list them (the other paths do) */
+		bool skipnil = false;
+		if (only_misses && !not_in && !nil_matches) {
+			bool eqo;
+			skipnil = lj_algo(l, r, sl, sr, &lci, &rci, nil_matches, false, false, true, false, false, false,
+					  false, &eqo) == LJ_MERGE && (l->sorted || l->revsorted);
+		}
 		bool rnil;
 		vpair *p = rpairs(r, &rci, &rnil);
 		if (p == NULL) {
@@ -1074,7 +1090,7 @@ ora_semijoin_cands(ora_bat *l, ora_bat *r, const ora_bat *sl, const ora_bat *sr,
 				const int64_t v = jv(l, lo - l->hseqbase);
 				uint64_t cnt = 0;
 				if (lnil(l, v) && (!nil_matches || not_in)) {
-					if (not_in)
+					if (not_in || skipnil)
 						continue;
 				} else {
 					const uint64_t a = vlower(p, rci.n, v);
@@ -1626,5 +1642,363 @@ done:
 	free(b);
 	oid_props(*r1p);
 	oid_props(*r2p);
+	return 0;
+}
+
+/* ---- leftjoin's algorithm choice and the order of several matches --------
+ * (gdk/gdk_join.c:4049-4300).  What a left candidate's matches are does not
+ * depend on the algorithm; their ORDER, which one a semi join with a right
+ * output keeps, and a few quirks do:
+ *   selectjoin (:363-563; one left candidate or all left values equal): the
+ *     matches ascending (a point BATselect), semi keeps the first; max_one ->
+ *     "more than one match", min_one (BATouterjoin's match_one) -> "not enough
+ *     matches" on a miss (:399-404, the only path that raises it);
+ *   mergejoin_void (:571), fetchjoin (:3893), bitmaskjoin (:3956): at most one
+ *     match per left candidate; fetchjoin returns the pairs in RIGHT position
+ *     order (r1 descends when r is reverse sorted) and, reached without a
+ *     check of nil_on_miss (:4156-4168), no nil rows for misses;
+ *   mergejoin (:1941-2780): the matches ascending (:2651-2683 emits a run
+ *     forwards in both scan directions); semi keeps the LAST of the run when
+ *     l and r are scanned in the same order (equal_order, :2091-2107: also
+ *     when l is not ordered) -- rci already points past the run and the copy
+ *     steps back by nr = 1 (:2661-2668) -- else the first; a sorted l's nil
+ *     values are skipped before the scan when neither nil_matches nor
+ *     nil_on_miss is set (:2093-2100), so BATdiff does not list them;
+ *   hashjoin (:2900-3335): the matches in hash-chain order, DESCENDING
+ *     position (chains are built by prepending); semi keeps the first of the
+ *     chain, i.e. the last position;
+ *   swapped hashjoin (:4203-4295; leftjoin / semi without max_one when
+ *     joincost prefers hashing l): the pairs of hashjoin(r, l) -- right
+ *     candidates in order, each one's left matches descending -- then r1 / r2
+ *     sorted by GDKqsort on r1 (unstable, :4236-4251); semi first reduces the
+ *     right side to BATunique (first occurrence of each value, gdk_unique.c),
+ *     so every left candidate keeps its FIRST match.
+ * mergejoin's memory-pressure term (:4185, BATcount(r) * width >
+ * GDK_mem_maxsize / nthreads) depends on the host and is taken as false.
+ * BATmarkjoin's reference quirks (the mark column of selectjoin has one row
+ * per left candidate whatever the match count, :513-527; fetchjoin returns no
+ * mark column) are not reproduced: the marks are one per result row. */
+
+/* BATtvoid (gdk.h): dense or void */
+static bool
+tvoid(const ora_bat *b)
+{
+	return tdense(b) || b->type == ORA_void;
+}
+
+static int
+lj_algo(ora_bat *l, ora_bat *r, const ora_bat *sl, const ora_bat *sr, const ora_ci *lci, const ora_ci *rci,
+	bool nil_matches, bool nil_on_miss, bool semi, bool only_misses, bool not_in, bool max_one, bool min_one,
+	bool want_r2, bool *equal_order)
+{
+	*equal_order = true;
+	if (lci->n == 0 || rci->n == 0)
+		return LJ_NOMATCH;
+	if (!only_misses && !not_in &&
+	    (lci->n == 1 || (ordered(l) && ordered_rev(l)) || (l->type == ORA_void && l->tseqbase == ORA_OID_NIL)))
+		return LJ_SELECT;
+	if (tdense(r) && rci->dense)
+		return LJ_MJVOID;
+	if (tdense(l) && lci->dense && rci->dense && !semi && !max_one && !min_one && !nil_matches && !only_misses &&
+	    !not_in && (ordered(r) || ordered_rev(r)))
+		return LJ_FETCH;
+	if (tdense(l) && lci->dense && !want_r2 && (semi || only_misses) && !nil_on_miss && !not_in && !max_one &&
+	    !min_one)
+		return LJ_BITMASK;
+	if ((ordered(r) || ordered_rev(r)) && (ordered(l) || ordered_rev(l) || tdense(r) || lci->n < 1024)) {
+		if (l->sorted || l->revsorted)
+			*equal_order = (l->sorted && r->sorted) ||
+				(l->revsorted && r->revsorted && !tvoid(l) && !tvoid(r));
+		return LJ_MERGE;
+	}
+	const double rcost = joincost(r, lci->n, rci, sr);
+	if (!nil_on_miss && !only_misses && !not_in && !max_one && !min_one) {
+		double lcost = joincost(l, rci->n, lci, sl);
+		if (semi && !r->key)
+			lcost += rci->n;
+		lcost += rci->n * log((double) rci->n);
+		if (lcost < rcost)
+			return LJ_SWAP;
+	}
+	return LJ_HASH;
+}
+
+typedef struct {
+	ora_oid *a, *b;
+	int8_t *m;
+	uint64_t n, cap;
+} ljrows;
+
+static int
+ljrows_add(ljrows *R, ora_oid x, ora_oid y, int8_t m)
+{
+	if (R->n == R->cap) {
+		uint64_t c = R->cap ? R->cap * 2 : 1024;
+		ora_oid *na = realloc(R->a, c * 8), *nb = realloc(R->b, c * 8);
+		int8_t *nm = realloc(R->m, c);
+		if (na)
+			R->a = na;
+		if (nb)
+			R->b = nb;
+		if (nm)
+			R->m = nm;
+		if (!na || !nb || !nm) {
+			ora_seterr("out of memory");
+			return -1;
+		}
+		R->cap = c;
+	}
+	R->a[R->n] = x;
+	R->b[R->n] = y;
+	R->m[R->n] = m;
+	R->n++;
+	return 0;
+}
+
+/* the swapped hash join's rows (see above): r1 / r2 of the pairs in
+ * hashjoin(r, l)'s order, then GDKqsort on r1 with r2 as payload */
+static int
+lj_swapped(ljrows *R, ora_bat *l, ora_bat *r, const ora_ci *lci, const ora_ci *rci, bool nil_matches, bool semi)
+{
+	bool lnil_any;
+	vpair *lp = rpairs(l, lci, &lnil_any);          /* l's candidates by (value, oid) */
+	if (lp == NULL)
+		return -1;
+	/* semi and r not known key: BATunique(r, sr), the first candidate of
+	 * every distinct value */
+	int64_t *seen = NULL;
+	uint64_t nseen = 0;
+	if (semi && !r->key) {
+		seen = malloc((rci->n + 1) * sizeof(int64_t));
+		if (seen == NULL) {
+			free(lp);
+			ora_seterr("malloc");
+			return -1;
+		}
+	}
+	pairs P = {0};
+	const int64_t rn = jnilv(r->type);
+	for (uint64_t j = 0; j < rci->n; j++) {
+		const ora_oid ro = ci_get(rci, j);
+		const int64_t v = jv(r, ro - r->hseqbase);
+		if (seen) {
+			/* a value seen before is not in BATunique's list */
+			uint64_t a = 0, b = nseen;
+			while (a < b) {
+				uint64_t m = (a + b) / 2;
+				if (seen[m] < v)
+					a = m + 1;
+				else
+					b = m;
+			}
+			if (a < nseen && seen[a] == v)
+				continue;
+			memmove(seen + a + 1, seen + a, (nseen - a) * sizeof(int64_t));
+			seen[a] = v;
+			nseen++;
+		}
+		const bool isnil = r->type == ORA_void ? r->tseqbase == ORA_OID_NIL : v == rn;
+		if (isnil && !nil_matches)
+			continue;
+		uint64_t a = vlower(lp, lci->n, v), b = a;
+		while (b < lci->n && lp[b].v == v)
+			b++;
+		for (uint64_t k = b; k > a; k--)          /* descending left position */
+			if (pairs_add(&P, lp[k - 1].o, ro) < 0) {
+				free(lp);
+				free(seen);
+				free(P.a);
+				free(P.b);
+				return -1;
+			}
+	}
+	free(lp);
+	free(seen);
+	if (P.n > 1) {
+		ora_bat *v = ora_new(ORA_oid, P.n, 0);
+		uint64_t *h = malloc(P.n * sizeof(uint64_t));
+		if (v == NULL || h == NULL) {
+			ora_free(v);
+			free(h);
+			free(P.a);
+			free(P.b);
+			ora_seterr("malloc");
+			return -1;
+		}
+		memcpy(v->base, P.a, P.n * 8);
+		for (uint64_t k = 0; k < P.n; k++)
+			h[k] = k;
+		ora_GDKqsort(v, h, P.b, P.n, false, false);
+		for (uint64_t k = 0; k < P.n; k++)
+			P.a[k] = ((const ora_oid *) v->base)[h[k]];
+		ora_free(v);
+		free(h);
+	}
+	int rc = 0;
+	for (uint64_t k = 0; k < P.n && rc == 0; k++)
+		rc = ljrows_add(R, P.a[k], P.b[k], 1);
+	free(P.a);
+	free(P.b);
+	return rc;
+}
+
+/* leftjoin (gdk_join.c:4049) for the outputs with a right (or mark) column:
+ * BATleftjoin (nil_on_miss false, semi false), BATouterjoin (nil_on_miss,
+ * match_one = max_one = min_one), BATsemijoin with r2p (semi, max_one),
+ * BATmarkjoin (nil_on_miss; semi when r2p is NULL; r3p set).  *algo: the
+ * LJ_* branch taken (tests check the shapes they mean to cover). */
+int
+ora_leftjoin_ex(ora_bat **r1p, ora_bat **r2p, ora_bat **r3p, ora_bat *l, ora_bat *r, const ora_bat *sl,
+		const ora_bat *sr, bool nil_matches, bool nil_on_miss, bool semi, bool max_one, bool min_one,
+		int *algo)
+{
+	*r1p = NULL;
+	if (r2p)
+		*r2p = NULL;
+	if (r3p)
+		*r3p = NULL;
+	if (l->type == ORA_msk || r->type == ORA_msk) {
+		ora_bat *lm = l->type == ORA_msk ? ora_unmask(l) : NULL;
+		ora_bat *rm = r->type == ORA_msk ? ora_unmask(r) : NULL;
+		int rc = -1;
+		if ((l->type != ORA_msk || lm) && (r->type != ORA_msk || rm))
+			rc = ora_leftjoin_ex(r1p, r2p, r3p, lm ? lm : l, rm ? rm : r, sl, sr, nil_matches, nil_on_miss, semi,
+					     max_one, min_one, algo);
+		ora_free(lm);
+		ora_free(rm);
+		return rc;
+	}
+	if (atomtype(l->type) != atomtype(r->type)) {
+		ora_seterr("leftjoin: inputs not compatible.");
+		return -1;
+	}
+	if (l->type == ORA_str) {
+		ora_bat *li, *ri;
+		if (str_images(l, r, &li, &ri) < 0)
+			return -1;
+		int rc = ora_leftjoin_ex(r1p, r2p, r3p, li, ri, sl, sr, nil_matches, nil_on_miss, semi, max_one,
+					 min_one, algo);
+		str_flags_back(l, r, li, ri);
+		return rc;
+	}
+	if (!join_type_ok(l->type) || !join_type_ok(r->type)) {
+		ora_seterr("leftjoin: type not restated");
+		return -1;
+	}
+	ora_ci lci, rci;
+	if (ora_ci_init(&lci, l, sl) < 0 || ora_ci_init(&rci, r, sr) < 0)
+		return -1;
+	const bool want_r2 = r2p != NULL;
+	bool eqo;
+	const int a = lj_algo(l, r, sl, sr, &lci, &rci, nil_matches, nil_on_miss, semi, false, false, max_one, min_one,
+			      want_r2, &eqo);
+	if (algo)
+		*algo = a;
+	ljrows R = {0};
+	bool rnil = false;
+	vpair *p = rci.n ? rpairs(r, &rci, &rnil) : NULL;
+	if (rci.n && p == NULL) {
+		ora_seterr("malloc");
+		return -1;
+	}
+	int rc = 0;
+	if (a == LJ_NOMATCH) {
+		/* nomatch (:301-360): the misses with nil (defmark 0, leftjoin :4144) */
+		for (uint64_t i = 0; nil_on_miss && i < lci.n && rc == 0; i++)
+			rc = ljrows_add(&R, ci_get(&lci, i), ORA_OID_NIL, 0);
+	} else if (a == LJ_SWAP) {
+		rc = lj_swapped(&R, l, r, &lci, &rci, nil_matches, semi);
+	} else {
+		/* fetchjoin's rows leave in right position order: with r reverse
+		 * sorted the left candidates come out descending */
+		const bool rev = a == LJ_FETCH && !r->sorted;
+		for (uint64_t ii = 0; ii < lci.n && rc == 0; ii++) {
+			const uint64_t i = rev ? lci.n - 1 - ii : ii;
+			const ora_oid lo = ci_get(&lci, i);
+			const int64_t v = jv(l, lo - l->hseqbase);
+			const bool isnil = lnil(l, v);
+			uint64_t lo_ = 0, hi_ = 0;
+			if (!(isnil && !nil_matches)) {
+				lo_ = vlower(p, rci.n, v);
+				hi_ = lo_;
+				while (hi_ < rci.n && p[hi_].v == v)
+					hi_++;
+			}
+			const uint64_t cnt = hi_ - lo_;
+			if (cnt > 1 && max_one) {
+				ora_seterr("more than one match");
+				rc = -1;
+				break;
+			}
+			if (cnt == 0) {
+				if (a == LJ_SELECT && min_one && !(isnil && !nil_matches)) {
+					ora_seterr("not enough matches");
+					rc = -1;
+					break;
+				}
+				if (nil_on_miss && a != LJ_FETCH)
+					rc = ljrows_add(&R, lo, ORA_OID_NIL, (int8_t) (isnil || rnil ? INT8_MIN : 0));
+				continue;
+			}
+			if (semi) {
+				const bool last = a == LJ_HASH || (a == LJ_MERGE && eqo);
+				rc = ljrows_add(&R, lo, p[last ? hi_ - 1 : lo_].o, 1);
+				continue;
+			}
+			if (a == LJ_HASH) {
+				for (uint64_t k = hi_; k > lo_ && rc == 0; k--)
+					rc = ljrows_add(&R, lo, p[k - 1].o, 1);
+			} else {
+				for (uint64_t k = lo_; k < hi_ && rc == 0; k++)
+					rc = ljrows_add(&R, lo, p[k].o, 1);
+			}
+		}
+	}
+	free(p);
+	if (rc < 0) {
+		free(R.a);
+		free(R.b);
+		free(R.m);
+		return -1;
+	}
+	ora_bat *x = oidbat(R.a, R.n), *y = oidbat(R.b, R.n), *z = r3p ? ora_new(ORA_bit, R.n, 0) : NULL;
+	if (x == NULL || y == NULL || (r3p && z == NULL)) {
+		ora_free(x);
+		ora_free(y);
+		ora_free(z);
+		free(R.a);
+		free(R.b);
+		free(R.m);
+		return -1;
+	}
+	bool ynil = false, znil = false;
+	for (uint64_t k = 0; k < R.n; k++) {
+		ynil |= R.b[k] == ORA_OID_NIL;
+		znil |= R.m[k] == INT8_MIN;
+	}
+	if (z) {
+		memcpy(z->base, R.m, R.n);
+		z->nil = znil;
+		z->nonil = !znil;
+	}
+	adj a1 = adjacent(R.a, R.n);
+	free(R.a);
+	free(R.b);
+	free(R.m);
+	x->sorted = !a1.desc;
+	x->revsorted = !a1.asc;
+	x->key = !a1.eq;
+	y->nil = ynil;
+	y->nonil = !ynil;
+	y->sorted = y->revsorted = y->key = R.n <= 1;
+	if (semi && x->sorted && x->key)
+		virtualize(x);
+	*r1p = x;
+	if (r2p)
+		*r2p = y;
+	else
+		ora_free(y);
+	if (r3p)
+		*r3p = z;
 	return 0;
 }

@@ -123,6 +123,8 @@ def lib():
         L.ora_semijoin_cands.argtypes = [P, P, P, P, C.c_bool, C.c_bool, C.c_bool, C.c_bool]
         L.ora_leftjoin.argtypes = [C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool, C.c_bool, C.c_bool]
         L.ora_markjoin.argtypes = [C.POINTER(P), C.POINTER(P), C.POINTER(P), P, P, P, P]
+        L.ora_leftjoin_ex.argtypes = [C.POINTER(P), C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool, C.c_bool,
+                                      C.c_bool, C.c_bool, C.c_bool, C.POINTER(C.c_int)]
         L.ora_join_algo.argtypes = [P, P, P, P]
         L.ora_BATsort.argtypes = [C.POINTER(P), C.POINTER(P), C.POINTER(P), P, P, P, C.c_bool, C.c_bool,
                                   C.c_bool]
@@ -535,6 +537,24 @@ def BATleftjoin(l, r, sl=None, sr=None, nil_matches=False, outer=False, match_on
     if rc < 0:
         raise _err()
     return Bat(a), Bat(b)
+
+
+LJ_ALGOS = ["nomatch", "selectjoin", "mergejoin_void", "fetchjoin", "bitmaskjoin", "mergejoin",
+            "hashjoin_swapped", "hashjoin"]
+
+
+def leftjoin_ex(l, r, sl=None, sr=None, nil_matches=False, nil_on_miss=False, semi=False, max_one=False,
+                min_one=False, want_r2=True, want_r3=False):
+    """leftjoin (gdk_join.c:4049) with the reference's algorithm choice and
+    the order of several matches per left candidate (gdk_oracle_join.c):
+    (r1, r2 or None, r3 or None, algorithm name)"""
+    a, b, c = P(), P(), P()
+    al = C.c_int(-1)
+    if lib().ora_leftjoin_ex(C.byref(a), C.byref(b) if want_r2 else None, C.byref(c) if want_r3 else None,
+                             l.ptr, r.ptr, sl.ptr if sl else None, sr.ptr if sr else None, nil_matches,
+                             nil_on_miss, semi, max_one, min_one, C.byref(al)) < 0:
+        raise _err()
+    return Bat(a), (Bat(b) if want_r2 else None), (Bat(c) if want_r3 else None), LJ_ALGOS[al.value]
 
 
 JOIN_ALGOS = ["nomatch", "selectjoin", "selectjoin_swapped", "mergejoin_void", "mergejoin_void_swapped",
