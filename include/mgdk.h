@@ -127,6 +127,11 @@ mgdk_bat *mgdk_BATmergecand(mgdk_bat *a, mgdk_bat *b);
 mgdk_bat *mgdk_BATintersectcand(mgdk_bat *a, mgdk_bat *b);
 mgdk_bat *mgdk_BATdiffcand(mgdk_bat *a, mgdk_bat *b);
 mgdk_bat *mgdk_BATnegcands(mgdk_oid tseq, mgdk_BUN nr, mgdk_bat *odels);
+/* BATunmask (gdk/gdk_cand.h; gdk_cand.c:1464): a msk BAT or a cand_mask list
+ * as the candidate list of its set bits -- a sorted oid list (virtualized
+ * when dense), or for a mask list with more than half its bits set the
+ * negative (cand_except) list of the unset ones, as the reference returns */
+mgdk_bat *mgdk_BATunmask(mgdk_bat *b);
 
 /* ---- select (gdk/gdk.h:2245-2246; gdk/gdk_select.c:1342, :2103) ------- */
 mgdk_bat *mgdk_BATselect(mgdk_bat *b, mgdk_bat *s, const void *tl, const void *th,
@@ -257,6 +262,25 @@ mgdk_bat *mgdk_BATgroupquantile_avg(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_
 				    bool skip_nils);
 mgdk_bat *mgdk_BATgroupmin(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils);
 mgdk_bat *mgdk_BATgroupmax(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils);
+/* BATmin / BATmax / BATmin_skipnil / BATmax_skipnil (gdk/gdk.h;
+ * gdk_aggr.c:3570-3844): the column's smallest / largest value as the
+ * reference finds it -- a cached tminpos / tmaxpos, an ordered column's end,
+ * else the first row holding the extreme (without skipnil the first nil) --
+ * nil for an empty or all-nil column; the position found is cached in b.
+ * aggr: a buffer of the value's width, or NULL for a copy from malloc (str:
+ * the NUL-terminated string; release it with mgdk_free).  NULL on error
+ * ("non-linear type" for msk). */
+void *mgdk_BATmin(mgdk_bat *b, void *aggr);
+void *mgdk_BATmax(mgdk_bat *b, void *aggr);
+void *mgdk_BATmin_skipnil(mgdk_bat *b, void *aggr, bool skipnil);
+void *mgdk_BATmax_skipnil(mgdk_bat *b, void *aggr, bool skipnil);
+void mgdk_free(void *p);
+/* BATprod (gdk/gdk.h; gdk_aggr.c:1650): the product of b's candidates into
+ * *res of type tp (bte..hge, flt, dbl; doprod's type table), "22003!overflow
+ * in product aggregate." as the reference raises it; BATgroupprod (:1575)
+ * the product per group (nil for an empty group) */
+int mgdk_BATprod(void *res, int tp, mgdk_bat *b, mgdk_bat *s, bool skip_nils, bool nil_if_empty);
+mgdk_bat *mgdk_BATgroupprod(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils);
 
 /* ---- group (gdk/gdk.h:1447; gdk/gdk_group.c:1347) --------------------- */
 int mgdk_BATgroup(mgdk_bat **groups, mgdk_bat **extents, mgdk_bat **histo,

@@ -128,6 +128,14 @@ _SIGS = {
     "mgdk_BATgroupavg3combine": (P, [P, P, P, P, P, C.c_bool]),
     "mgdk_BATgroupavg3": (C.c_int, [PP, PP, PP, P, P, P, P, C.c_bool]),
     "mgdk_BATgroupmin": (P, [P, P, P, P, C.c_int, C.c_bool]),
+    "mgdk_BATmin_skipnil": (C.c_void_p, [P, C.c_void_p, C.c_bool]),
+    "mgdk_BATmax_skipnil": (C.c_void_p, [P, C.c_void_p, C.c_bool]),
+    "mgdk_BATmin": (C.c_void_p, [P, C.c_void_p]),
+    "mgdk_BATmax": (C.c_void_p, [P, C.c_void_p]),
+    "mgdk_free": (None, [C.c_void_p]),
+    "mgdk_BATprod": (C.c_int, [C.c_void_p, C.c_int, P, P, C.c_bool, C.c_bool]),
+    "mgdk_BATgroupprod": (P, [P, P, P, P, C.c_int, C.c_bool]),
+    "mgdk_BATunmask": (P, [P]),
     "mgdk_BATgroupstdev_sample": (P, [P, P, P, P, C.c_int, C.c_bool]),
     "mgdk_BATgroupstdev_population": (P, [P, P, P, P, C.c_int, C.c_bool]),
     "mgdk_BATgroupvariance_sample": (P, [P, P, P, P, C.c_int, C.c_bool]),
@@ -620,6 +628,56 @@ def BATgroupsum(b, g, e, tp, skip_nils=True, s=None):
 
 def BATgroupcount(b, g, e, skip_nils=True, s=None):
     return BAT(lib().mgdk_BATgroupcount(b.ptr, g.ptr, _p(e), _p(s), TYPE_lng, skip_nils))
+
+
+def _scalar(tp, buf):
+    """a value of type tp from a raw buffer (hge as an int)"""
+    if tp == TYPE_hge:
+        return hge_to_int(C.cast(buf, C.POINTER(C.c_uint64 * 2))[0])
+    return C.cast(buf, C.POINTER(CT[tp]))[0]
+
+
+def _minmax(fn, b, skipnil):
+    if b.ttype == TYPE_str:
+        p = fn(b.ptr, None, skipnil)
+        if not p:
+            _chk(-1)
+        try:
+            return C.string_at(p)
+        finally:
+            lib().mgdk_free(p)
+    buf = (C.c_uint64 * 2)()
+    if not fn(b.ptr, C.cast(buf, C.c_void_p), skipnil):
+        _chk(-1)
+    return _scalar(TYPE_oid if b.ttype == TYPE_void else b.ttype, buf)
+
+
+def BATmin(b, skipnil=True):
+    """BATmin_skipnil (gdk_aggr.c:3570): the smallest value (nil when none;
+    str as bytes)"""
+    return _minmax(lib().mgdk_BATmin_skipnil, b, skipnil)
+
+
+def BATmax(b, skipnil=True):
+    """BATmax_skipnil (gdk_aggr.c:3727)"""
+    return _minmax(lib().mgdk_BATmax_skipnil, b, skipnil)
+
+
+def BATprod(tp, b, s=None, skip_nils=True, nil_if_empty=True):
+    """BATprod (gdk_aggr.c:1650)"""
+    buf = (C.c_uint64 * 2)()
+    _chk(lib().mgdk_BATprod(C.cast(buf, C.c_void_p), tp, b.ptr, _p(s), skip_nils, nil_if_empty))
+    return _scalar(tp, buf)
+
+
+def BATgroupprod(b, g, e, tp, skip_nils=True, s=None):
+    """BATgroupprod (gdk_aggr.c:1575)"""
+    return BAT(lib().mgdk_BATgroupprod(b.ptr, g.ptr, _p(e), _p(s), tp, skip_nils))
+
+
+def BATunmask(b):
+    """BATunmask (gdk_cand.c:1464)"""
+    return BAT(lib().mgdk_BATunmask(b.ptr))
 
 
 def BATgroupmin(b, g, e, skip_nils=True, s=None):

@@ -135,6 +135,13 @@ ora_bat *ora_groupavg3combine(const ora_bat *avg, const ora_bat *rem, const ora_
 			       const ora_bat *g, const ora_bat *e, bool skip_nils);
 int ora_groupavg(ora_bat **bnp, ora_bat **cntp, const ora_bat *b, const ora_bat *g,
 		 const ora_bat *e, const ora_bat *s, bool skip_nils, int scale);
+/* gdk_aggr.c:3570 BATmin_skipnil / :3727 BATmax_skipnil: the value into res
+ * (a buffer of the width), str: *sres = the string */
+int ora_minmax(ora_bat *b, bool skipnil, bool domax, void *res, const char **sres);
+/* gdk_aggr.c:1650 BATprod (res of type tp), :1575 BATgroupprod */
+int ora_prod(void *res, int tp, const ora_bat *b, const ora_bat *s, bool skip_nils, bool nil_if_empty);
+ora_bat *ora_groupprod(const ora_bat *b, const ora_bat *g, const ora_bat *e, const ora_bat *s, int tp,
+		       bool skip_nils);
 ora_bat *ora_groupminmax(const ora_bat *b, const ora_bat *g, const ora_bat *e,
 			 const ora_bat *s, bool skip_nils, bool domax);
 /* BATjoin with its algorithm choice (gdk_oracle_join.c); l and r receive

@@ -5,6 +5,7 @@
  */
 #include "gdk_oracle.h"
 
+#include <float.h>
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -1328,5 +1329,340 @@ done:
 	ora_free(sv);
 	ora_free(gs);
 	ora_free(go);
+	return bn;
+}
+
+/* ---------------------------------------------------------------------- */
+/* BATmin_skipnil / BATmax_skipnil (gdk/gdk_aggr.c:3570-3844): a cached
+ * minpos / maxpos first; an ordered column (BATordered / BATordered_rev,
+ * nil the smallest value) answers from its end -- min: the first non-nil
+ * row of a sorted column (skipnil) or its first row, the row before the
+ * first nil of a reverse-sorted one (skipnil) or its last row; max: the last
+ * row of a sorted column, the first of a reverse-sorted one, nil when that
+ * row is nil and skipnil -- else do_groupmin / do_groupmax over all rows:
+ * the first row holding the extreme, without skipnil the first nil.  The
+ * value at that row is copied to res (str: *sres points at the string);
+ * the row is cached in the descriptor.  Returns 0, -1 on error. */
+
+/* val_at with the 8-byte temporal types */
+static bool
+mm_val(const ora_bat *b, uint64_t p, ora_hge *v)
+{
+	if (b->type == ORA_daytime || b->type == ORA_timestamp) {
+		const int64_t x = ((const int64_t *) b->base)[p];
+		*v = x;
+		return x == INT64_MIN;
+	}
+	return val_at(b, p, v);
+}
+
+/* three-way compare of rows p, q (nil the smallest; flt / dbl compare as
+ * doubles, -0.0 == +0.0; str by strcmp) */
+static int
+mm_cmp(const ora_bat *b, uint64_t p, uint64_t q)
+{
+	if (b->type == ORA_str) {
+		const char *x = str_of(b, p), *y = str_of(b, q);
+		const bool nx = (unsigned char) x[0] == 0x80 && x[1] == 0, ny = (unsigned char) y[0] == 0x80 && y[1] == 0;
+		if (nx || ny)
+			return ny - nx;
+		int r = strcmp(x, y);
+		return (r > 0) - (r < 0);
+	}
+	if (b->type == ORA_flt || b->type == ORA_dbl) {
+		double x, y;
+		const bool nx = dbl_at(b, p, &x), ny = dbl_at(b, q, &y);
+		if (nx || ny)
+			return ny - nx;
+		return (x > y) - (x < y);
+	}
+	ora_hge x, y;
+	const bool nx = mm_val(b, p, &x), ny = mm_val(b, q, &y);
+	if (nx || ny)
+		return ny - nx;
+	return (x > y) - (x < y);
+}
+
+static bool
+mm_nil(const ora_bat *b, uint64_t p)
+{
+	if (b->type == ORA_str) {
+		const char *x = str_of(b, p);
+		return (unsigned char) x[0] == 0x80 && x[1] == 0;
+	}
+	if (b->type == ORA_flt || b->type == ORA_dbl) {
+		double d;
+		return dbl_at(b, p, &d);
+	}
+	ora_hge v;
+	return mm_val(b, p, &v);
+}
+
+static bool
+mm_ordered(ora_bat *b, bool rev)
+{
+	if (rev ? b->revsorted : b->sorted)
+		return true;
+	for (uint64_t p = 1; p < b->count; p++) {
+		const int c = mm_cmp(b, p - 1, p);
+		if (rev ? c < 0 : c > 0)
+			return false;
+	}
+	if (rev)
+		b->revsorted = 1;
+	else
+		b->sorted = 1;
+	return true;
+}
+
+int
+ora_minmax(ora_bat *b, bool skipnil, bool domax, void *res, const char **sres)
+{
+	const uint64_t n = b->count;
+	uint64_t pos = ORA_BUN_NONE;
+	const uint64_t cached = domax ? b->maxpos : b->minpos;
+	if (b->type == ORA_msk) {
+		ora_seterr("non-linear type");
+		return -1;
+	}
+	if (n == 0) {
+		pos = ORA_BUN_NONE;
+	} else if (b->type == ORA_void) {
+		const ora_oid v = b->tseqbase == ORA_OID_NIL ? ORA_OID_NIL : b->tseqbase + (domax ? n - 1 : 0);
+		memcpy(res, &v, 8);
+		return 0;
+	} else if (cached != ORA_BUN_NONE && cached < n) {
+		pos = cached;
+	} else {
+		const bool asc = mm_ordered(b, false), desc = !asc && mm_ordered(b, true);
+		if (asc || desc) {
+			if (!domax) {
+				if (skipnil && !b->nonil) {
+					uint64_t q = 0;
+					if (asc) {
+						while (q < n && mm_nil(b, q))
+							q++;
+						pos = q == n ? ORA_BUN_NONE : q;
+					} else {
+						while (q < n && !mm_nil(b, q))
+							q++;
+						pos = q == 0 ? ORA_BUN_NONE : q - 1;
+					}
+				} else {
+					pos = asc ? 0 : n - 1;
+				}
+			} else {
+				pos = asc ? n - 1 : 0;
+				if (skipnil && !b->nonil && mm_nil(b, pos))
+					pos = ORA_BUN_NONE;
+			}
+		} else {
+			/* do_groupmin / do_groupmax over all rows */
+			uint64_t best = ORA_BUN_NONE;
+			bool bnil = false;
+			for (uint64_t p = 0; p < n; p++) {
+				const bool vn = mm_nil(b, p);
+				if (skipnil && vn)
+					continue;
+				if (best == ORA_BUN_NONE) {
+					best = p;
+					bnil = vn;
+				} else if (!bnil && (vn || (domax ? mm_cmp(b, p, best) > 0 : mm_cmp(b, p, best) < 0))) {
+					best = p;
+					bnil = vn;
+				}
+			}
+			pos = best;
+		}
+		if (pos != ORA_BUN_NONE) {
+			if (domax)
+				b->maxpos = pos;
+			else
+				b->minpos = pos;
+		}
+	}
+	if (b->type == ORA_str) {
+		*sres = pos == ORA_BUN_NONE ? "\200" : str_of(b, pos);
+		return 0;
+	}
+	if (pos == ORA_BUN_NONE) {
+		switch (b->type) {
+		case ORA_flt: { const float f = NAN; memcpy(res, &f, 4); break; }
+		case ORA_dbl: { const double f = NAN; memcpy(res, &f, 8); break; }
+		default: put(b->type == ORA_date ? ORA_int : b->type == ORA_daytime || b->type == ORA_timestamp ? ORA_lng : b->type,
+			     res, 0, 0, true); break;
+		}
+		return 0;
+	}
+	memcpy(res, (const char *) b->base + pos * b->width, b->width);
+	return 0;
+}
+
+/* ---------------------------------------------------------------------- */
+/* BATprod (gdk/gdk_aggr.c:1650) / BATgroupprod (:1575) through doprod
+ * (:1340-1548): per group, in candidate order, the macro doprod picks for
+ * the result type -- AGGR_PROD (integer results up to lng: a nil value makes
+ * the product nil unless skip_nils, a group's first value resets it to 1
+ * when nil_if_empty, so nils before it are forgotten; multiply with the
+ * overflow check |p| <= max of MULI4_WITH_CHECK), AGGR_PROD_HGE (hge: any row
+ * marks the group seen, HGEMUL_CHECK), AGGR_PROD_FLOAT (flt / dbl: as
+ * AGGR_PROD with "|v| > 1 && max / |v| < |p|" as the overflow test).  An
+ * overflow is "22003!overflow in product aggregate." */
+
+static int
+prod_kind(int tp1, int tp2)
+{
+	switch (tp2) {
+	case ORA_bte: return tp1 == ORA_bte ? 0 : -1;
+	case ORA_sht: return tp1 == ORA_bte || tp1 == ORA_sht ? 0 : -1;
+	case ORA_int: return tp1 == ORA_bte || tp1 == ORA_sht || tp1 == ORA_int ? 0 : -1;
+	case ORA_lng: return tp1 == ORA_bte || tp1 == ORA_sht || tp1 == ORA_int || tp1 == ORA_lng ? 0 : -1;
+	case ORA_hge:
+		return tp1 == ORA_bte || tp1 == ORA_sht || tp1 == ORA_int || tp1 == ORA_lng || tp1 == ORA_hge ? 1 : -1;
+	case ORA_flt:
+		return tp1 == ORA_bte || tp1 == ORA_sht || tp1 == ORA_int || tp1 == ORA_lng || tp1 == ORA_hge ||
+			tp1 == ORA_flt ? 2 : -1;
+	case ORA_dbl:
+		return tp1 == ORA_bte || tp1 == ORA_sht || tp1 == ORA_int || tp1 == ORA_lng || tp1 == ORA_hge ||
+			tp1 == ORA_flt || tp1 == ORA_dbl ? 2 : -1;
+	}
+	return -1;
+}
+
+/* the running state of one group */
+typedef struct {
+	ora_hge ip;        /* integer product */
+	double fp;         /* float product (flt results rounded to float each step) */
+	bool nil, seen;
+} pstate;
+
+/* one row; false on overflow */
+static bool
+prod_step(pstate *s, int kind, int tp1, int tp2, const ora_bat *b, uint64_t p, bool skip_nils, bool nil_if_empty)
+{
+	bool vn;
+	ora_hge iv = 0;
+	double fv = 0;
+	if (tp1 == ORA_flt || tp1 == ORA_dbl)
+		vn = dbl_at(b, p, &fv);
+	else
+		vn = val_at(b, p, &iv);
+	if (kind == 1 && nil_if_empty && !s->seen) {
+		s->seen = true;
+		s->nil = false;
+		s->ip = 1;
+	}
+	if (vn) {
+		if (!skip_nils)
+			s->nil = true;
+		return true;
+	}
+	if (kind != 1 && nil_if_empty && !s->seen) {
+		s->seen = true;
+		s->nil = false;
+		s->ip = 1;
+		s->fp = 1;
+	}
+	if (s->nil)
+		return true;
+	if (kind == 2) {
+		/* C's arithmetic: the value converted to the result type */
+		if (tp2 == ORA_flt) {
+			const float x = tp1 == ORA_flt ? (float) fv : (float) iv;
+			const float ax = x < 0 ? -x : x, ap = (float) s->fp < 0 ? -(float) s->fp : (float) s->fp;
+			if (ax > 1 && FLT_MAX / ax < ap)
+				return false;
+			s->fp = (float) ((float) s->fp * x);
+		} else {
+			const double x = tp1 == ORA_flt || tp1 == ORA_dbl ? fv : (double) iv;
+			const double ax = x < 0 ? -x : x, ap = s->fp < 0 ? -s->fp : s->fp;
+			if (ax > 1 && DBL_MAX / ax < ap)
+				return false;
+			s->fp = s->fp * x;
+		}
+		return true;
+	}
+	ora_hge r;
+	if (__builtin_mul_overflow(iv, s->ip, &r))
+		return false;
+	const ora_hge mx = tmax(tp2);
+	if (r > mx || r < -mx)
+		return false;
+	s->ip = r;
+	return true;
+}
+
+static void
+prod_put(int tp2, void *base, uint64_t i, const pstate *s)
+{
+	if (tp2 == ORA_flt)
+		((float *) base)[i] = s->nil ? NAN : (float) s->fp;
+	else if (tp2 == ORA_dbl)
+		((double *) base)[i] = s->nil ? NAN : s->fp;
+	else
+		put(tp2, base, i, s->ip, s->nil);
+}
+
+int
+ora_prod(void *res, int tp, const ora_bat *b, const ora_bat *s, bool skip_nils, bool nil_if_empty)
+{
+	const int kind = prod_kind(b->type, tp);
+	if (kind < 0) {
+		ora_seterr("type combination (prod) not supported");
+		return -1;
+	}
+	ora_ci ci;
+	if (ora_ci_init(&ci, b, s) < 0)
+		return -1;
+	pstate st = {.ip = 1, .fp = 1, .nil = nil_if_empty, .seen = false};
+	for (uint64_t i = 0; i < ci.n; i++)
+		if (!prod_step(&st, kind, b->type, tp, b, ci_get(&ci, i) - b->hseqbase, skip_nils, nil_if_empty)) {
+			ora_seterr("22003!overflow in product aggregate.\n");
+			return -1;
+		}
+	prod_put(tp, res, 0, &st);
+	return 0;
+}
+
+ora_bat *
+ora_groupprod(const ora_bat *b, const ora_bat *g, const ora_bat *e, const ora_bat *s, int tp, bool skip_nils)
+{
+	aggr_ctx a;
+	if (aggr_init(&a, b, g, e, s) < 0)
+		return NULL;
+	const int kind = prod_kind(b->type, tp);
+	if (kind < 0 && a.ci.n && a.ngrp) {
+		ora_seterr("type combination (prod) not supported");
+		return NULL;
+	}
+	ora_bat *bn = ora_new(tp, a.ngrp, a.ngrp ? a.min : 0);
+	pstate *st = malloc((a.ngrp + 1) * sizeof(pstate));
+	if (!bn || !st) {
+		ora_free(bn);
+		free(st);
+		return NULL;
+	}
+	for (uint64_t k = 0; k < a.ngrp; k++)
+		st[k] = (pstate) {.ip = 1, .fp = 1, .nil = true, .seen = false};
+	for (uint64_t i = 0; i < a.ci.n; i++) {
+		ora_oid gid;
+		if (!aggr_gid(&a, i, &gid))
+			continue;
+		if (!prod_step(&st[gid], kind, b->type, tp, b, ci_get(&a.ci, i) - b->hseqbase, skip_nils, true)) {
+			ora_free(bn);
+			free(st);
+			ora_seterr("22003!overflow in product aggregate.\n");
+			return NULL;
+		}
+	}
+	uint64_t nils = 0;
+	for (uint64_t k = 0; k < a.ngrp; k++) {
+		prod_put(tp, bn->base, k, &st[k]);
+		nils += st[k].nil;
+	}
+	free(st);
+	bn->sorted = bn->revsorted = bn->key = a.ngrp <= 1;
+	bn->nil = nils != 0;
+	bn->nonil = nils == 0;
 	return bn;
 }

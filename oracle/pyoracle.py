@@ -123,6 +123,10 @@ def lib():
         L.ora_semijoin_cands.argtypes = [P, P, P, P, C.c_bool, C.c_bool, C.c_bool, C.c_bool]
         L.ora_leftjoin.argtypes = [C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool, C.c_bool, C.c_bool]
         L.ora_markjoin.argtypes = [C.POINTER(P), C.POINTER(P), C.POINTER(P), P, P, P, P]
+        L.ora_minmax.argtypes = [P, C.c_bool, C.c_bool, C.c_void_p, C.POINTER(C.c_char_p)]
+        L.ora_prod.argtypes = [C.c_void_p, C.c_int, P, P, C.c_bool, C.c_bool]
+        L.ora_groupprod.restype = P
+        L.ora_groupprod.argtypes = [P, P, P, P, C.c_int, C.c_bool]
         L.ora_leftjoin_ex.argtypes = [C.POINTER(P), C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool, C.c_bool,
                                       C.c_bool, C.c_bool, C.c_bool, C.POINTER(C.c_int)]
         L.ora_join_algo.argtypes = [P, P, P, P]
@@ -388,6 +392,36 @@ def BATsum(tp, b, s=None, skip_nils=True, nil_if_empty=True):
     if tp == TYPE_dbl:
         return C.cast(buf, C.POINTER(C.c_double))[0]
     return C.cast(buf, C.POINTER(CT[tp]))[0]
+
+
+def _scalar(tp, buf):
+    if tp == TYPE_hge:
+        return hge_to_int(buf)
+    return C.cast(buf, C.POINTER(CT[TYPE_oid if tp == TYPE_void else tp]))[0]
+
+
+def BATminmax(b, skipnil=True, domax=False):
+    """BATmin_skipnil / BATmax_skipnil (gdk_aggr.c:3570, :3727); str as bytes"""
+    buf = (C.c_uint64 * 2)()
+    sp = C.c_char_p()
+    if lib().ora_minmax(b.ptr, skipnil, domax, C.cast(buf, C.c_void_p), C.byref(sp)) < 0:
+        raise _err()
+    if b.s.type == TYPE_str:
+        return sp.value
+    return _scalar(b.s.type, buf)
+
+
+def BATprod(tp, b, s=None, skip_nils=True, nil_if_empty=True):
+    """BATprod (gdk_aggr.c:1650)"""
+    buf = (C.c_uint64 * 2)()
+    if lib().ora_prod(C.cast(buf, C.c_void_p), tp, b.ptr, s.ptr if s else None, skip_nils, nil_if_empty) < 0:
+        raise _err()
+    return _scalar(tp, buf)
+
+
+def BATgroupprod(b, g, e, tp, skip_nils=True, s=None):
+    """BATgroupprod (gdk_aggr.c:1575)"""
+    return _ret(lib().ora_groupprod(b.ptr, g.ptr, e.ptr if e else None, s.ptr if s else None, tp, skip_nils))
 
 
 def BATgroup(b, s=None, g=None):
