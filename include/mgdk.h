@@ -198,6 +198,54 @@ mgdk_bat *mgdk_BATcalcbetweencstbat(mgdk_bat *b, const void *lo, mgdk_bat *hi, i
 mgdk_bat *mgdk_BATconvert(mgdk_bat *b, mgdk_bat *s, int tp, uint8_t scale1, uint8_t scale2, uint8_t precision);
 /* BATcalcnot (gdk/gdk_calc.h:23; gdk_calc.c:41) */
 mgdk_bat *mgdk_BATcalcnot(mgdk_bat *b, mgdk_bat *s);
+/* the rest of gdk_calc.c's element-wise operators (gdk/gdk_calc.h:15-93):
+ * negate / absolute (b's type), iszero (bit), sign (bte), isnil / isnotnil
+ * (bit, never nil), incr / decr (b's type, overflow checked), min / max and
+ * their _no_nil forms (ATOMtype of the inputs; a constant v of type vt in
+ * the cst forms), and / or / xor (bit: three-valued; integers bitwise, a
+ * result equal to nil an overflow), lsh / rsh ("shift operand too large"),
+ * ifthenelse (b of type bit; a nil condition takes the else branch; then /
+ * else BATs or constants c of type ct).  Messages and result properties as
+ * the reference's. */
+mgdk_bat *mgdk_BATcalcnegate(mgdk_bat *b, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalcabsolute(mgdk_bat *b, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalciszero(mgdk_bat *b, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalcsign(mgdk_bat *b, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalcisnil(mgdk_bat *b, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalcisnotnil(mgdk_bat *b, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalcincr(mgdk_bat *b, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalcdecr(mgdk_bat *b, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalcmin(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2);
+mgdk_bat *mgdk_BATcalcmax(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2);
+mgdk_bat *mgdk_BATcalcmin_no_nil(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2);
+mgdk_bat *mgdk_BATcalcmax_no_nil(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2);
+mgdk_bat *mgdk_BATcalcmincst(mgdk_bat *b, const void *v, int vt, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalcmaxcst(mgdk_bat *b, const void *v, int vt, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalcmincst_no_nil(mgdk_bat *b, const void *v, int vt, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalcmaxcst_no_nil(mgdk_bat *b, const void *v, int vt, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalccstmin(const void *v, int vt, mgdk_bat *b, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalccstmax(const void *v, int vt, mgdk_bat *b, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalccstmin_no_nil(const void *v, int vt, mgdk_bat *b, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalccstmax_no_nil(const void *v, int vt, mgdk_bat *b, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalcand(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2);
+mgdk_bat *mgdk_BATcalcandcst(mgdk_bat *b, const void *v, int vt, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalccstand(const void *v, int vt, mgdk_bat *b, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalcor(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2);
+mgdk_bat *mgdk_BATcalcorcst(mgdk_bat *b, const void *v, int vt, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalccstor(const void *v, int vt, mgdk_bat *b, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalcxor(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2);
+mgdk_bat *mgdk_BATcalcxorcst(mgdk_bat *b, const void *v, int vt, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalccstxor(const void *v, int vt, mgdk_bat *b, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalclsh(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2);
+mgdk_bat *mgdk_BATcalclshcst(mgdk_bat *b, const void *v, int vt, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalccstlsh(const void *v, int vt, mgdk_bat *b, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalcrsh(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2);
+mgdk_bat *mgdk_BATcalcrshcst(mgdk_bat *b, const void *v, int vt, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalccstrsh(const void *v, int vt, mgdk_bat *b, mgdk_bat *s);
+mgdk_bat *mgdk_BATcalcifthenelse(mgdk_bat *b, mgdk_bat *b1, mgdk_bat *b2);
+mgdk_bat *mgdk_BATcalcifthenelsecst(mgdk_bat *b, mgdk_bat *b1, const void *c2, int ct);
+mgdk_bat *mgdk_BATcalcifthencstelse(mgdk_bat *b, const void *c1, int ct, mgdk_bat *b2);
+mgdk_bat *mgdk_BATcalcifthencstelsecst(mgdk_bat *b, const void *c1, const void *c2, int ct);
 /* division / modulo (gdk/gdk_calc.h:45-50; gdk_calc_div.c:1945, gdk_calc_mod.c:1179) */
 mgdk_bat *mgdk_BATcalcdiv(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2, int tp);
 mgdk_bat *mgdk_BATcalcdivcst(mgdk_bat *b, const void *v, int vt, mgdk_bat *s, int tp);

@@ -1392,6 +1392,623 @@ calcdivmod(bool div, mgdk_bat *b1, const void *v1, int t1, mgdk_bat *b2, const v
 	return bn;
 }
 
+// ---- the rest of gdk_calc.c's element-wise operators ---------------------
+// BATcalcnegate / absolute / iszero / sign (gdk_calc.c:233-800), isnil /
+// isnotnil (:802-920), min / max and their _no_nil and constant forms
+// (:976-2436), xor / or / and (:2439-3030; bit: the three-valued or3 / and3,
+// :2590, :2826), lsh / rsh (:3059-3760) and incr / decr
+// (gdk_calc_addsub.c:1681): one lane per candidate over the Num operands
+// above; the first failing candidate (atomicMin) gives the reference's
+// message.
+enum { X_NEG, X_ABS, X_ISZERO, X_SIGN, X_ISNIL, X_ISNOTNIL, X_MIN, X_MAX, X_MINNN, X_MAXNN, X_MINC, X_MAXC, X_MINNNC,
+       X_MAXNNC, X_AND, X_OR, X_XOR, X_LSH, X_RSH };
+
+struct XArgs {
+	int op;
+	int t;            // the operands' base type (shifts: the left one)
+	int t2;           // shifts: the right operand's base type
+	int ow;           // output width
+	bool isbit;       // bit operands (three-valued logic)
+	bool oid;         // oid / void values (unsigned compare)
+	int lbits;        // shifts: bits of the left operand's type
+};
+
+__device__ __forceinline__ bool
+x_lt(const Num &a, const Num &b, int t, bool oid)
+{
+	if (t == MGDK_flt)
+		return a.f < b.f;
+	if (t == MGDK_dbl)
+		return a.d < b.d;
+	if (oid)
+		return (uhge) a.i < (uhge) b.i;
+	return a.i < b.i;
+}
+
+__device__ __forceinline__ void
+x_store(void *out, const XArgs &x, BUN i, const Num &v)
+{
+	if (x.t == MGDK_flt && x.ow == 4 && x.op != X_ISZERO && x.op != X_SIGN && x.op != X_ISNIL && x.op != X_ISNOTNIL)
+		((float *) out)[i] = v.f;
+	else if (x.t == MGDK_dbl && x.ow == 8 && x.op != X_ISZERO && x.op != X_SIGN && x.op != X_ISNIL &&
+		 x.op != X_ISNOTNIL)
+		((double *) out)[i] = v.d;
+	else
+		st_int(out, x.ow, i, v.i);
+}
+
+__device__ __forceinline__ Num
+x_nil(const XArgs &x)
+{
+	Num v{};
+	v.nil = true;
+	v.f = __int_as_float(0x7fc00000);
+	v.d = __longlong_as_double(0x7ff8000000000000ll);
+	v.i = x.oid ? (hge) MGDK_OID_NIL : x.ow == 16 ? (hge) ((uhge) 1 << 127) : -((hge) 1 << (8 * x.ow - 1));
+	return v;
+}
+
+// meta[0] nils, meta[1] first failing candidate
+__global__ __launch_bounds__(256) void
+k_xop(Opnd a, Opnd b, XArgs x, void *out, BUN n, unsigned long long *meta)
+{
+	unsigned long long nils = 0, first = ~0ull;
+	const Num NIL = x_nil(x);
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		const Num p = opval(a, i);
+		Num r = p;
+		bool isnil = false, fail = false;
+		const bool fl = x.t == MGDK_flt || x.t == MGDK_dbl;
+		switch (x.op) {
+		case X_NEG:
+		case X_ABS:
+			if (p.nil) {
+				isnil = true;
+			} else if (x.op == X_NEG) {
+				r.i = -p.i;
+				r.f = -p.f;
+				r.d = -p.d;
+			} else {
+				r.i = p.i < 0 ? -p.i : p.i;
+				r.f = __builtin_fabsf(p.f);
+				r.d = __builtin_fabs(p.d);
+			}
+			break;
+		case X_ISZERO:
+		case X_SIGN:
+			if (p.nil) {
+				isnil = true;
+			} else {
+				const int sg = x.t == MGDK_flt ? (p.f < 0 ? -1 : p.f > 0) : x.t == MGDK_dbl ? (p.d < 0 ? -1 : p.d > 0)
+										      : (p.i < 0 ? -1 : p.i > 0);
+				const bool z = x.t == MGDK_flt ? p.f == 0 : x.t == MGDK_dbl ? p.d == 0 : p.i == 0;
+				r.i = x.op == X_ISZERO ? (hge) z : (hge) sg;
+			}
+			break;
+		case X_ISNIL:
+		case X_ISNOTNIL:
+			r.i = (hge) (p.nil != (x.op == X_ISNOTNIL));
+			break;
+		default: {
+			const Num q = opval(b, i);
+			switch (x.op) {
+			case X_MIN:
+			case X_MAX:
+				if (p.nil || q.nil)
+					isnil = true;
+				else
+					r = (x.op == X_MIN ? x_lt(p, q, x.t, x.oid) : x_lt(q, p, x.t, x.oid)) ? p : q;
+				break;
+			case X_MINNN:
+			case X_MAXNN:
+				if (p.nil)
+					r = q, isnil = q.nil;
+				else
+					r = !q.nil && (x.op == X_MINNN ? x_lt(q, p, x.t, x.oid) : x_lt(p, q, x.t, x.oid)) ? q : p;
+				break;
+			case X_MINC:
+			case X_MAXC:
+				// the constant is not nil (the caller answered that case)
+				if (p.nil)
+					isnil = true;
+				else
+					r = (x.op == X_MINC ? x_lt(p, q, x.t, x.oid) : x_lt(q, p, x.t, x.oid)) ? p : q;
+				break;
+			case X_MINNNC:
+			case X_MAXNNC:
+				if (q.nil)
+					r = p, isnil = p.nil;
+				else if (p.nil)
+					r = q;
+				else
+					r = (x.op == X_MINNNC ? x_lt(p, q, x.t, x.oid) : x_lt(q, p, x.t, x.oid)) ? p : q;
+				break;
+			case X_AND:
+			case X_OR:
+			case X_XOR:
+				if (x.isbit && x.op != X_XOR) {
+					// or3 / and3 (gdk_calc.c:2590, :2826)
+					const int8_t v1 = (int8_t) p.i, v2 = (int8_t) q.i;
+					int8_t o;
+					if (x.op == X_OR)
+						o = v1 == 1 || v2 == 1 ? 1 : (p.nil || q.nil) ? INT8_MIN : 0;
+					else
+						o = v1 == 0 || v2 == 0 ? 0 : (p.nil || q.nil) ? INT8_MIN : 1;
+					r.i = o;
+					isnil = o == INT8_MIN;
+				} else if (p.nil || q.nil) {
+					isnil = true;
+				} else if (x.isbit) {
+					r.i = (p.i == 0) != (q.i == 0);
+				} else {
+					r.i = x.op == X_AND ? (p.i & q.i) : x.op == X_OR ? (p.i | q.i) : (p.i ^ q.i);
+					// a result equal to nil is an overflow (AND / XOR; an OR
+					// giving nil has a nil operand)
+					fail = r.i == NIL.i && x.op != X_OR;
+				}
+				break;
+			case X_LSH:
+			case X_RSH: {
+				if (p.nil || q.nil) {
+					isnil = true;
+					break;
+				}
+				const int bits = x.lbits;
+				const hge sh = q.i;
+				if (sh < 0 || sh >= bits) {
+					fail = true;
+				} else if (x.op == X_LSH) {
+					const hge mx = bits == 128 ? (hge) (((uhge) 1 << 127) - 1) : (((hge) 1 << (bits - 1)) - 1);
+					if (p.i < 0 || p.i > (mx >> (int) sh))
+						fail = true;
+					else
+						r.i = p.i << (int) sh;
+				} else {
+					r.i = p.i >> (int) sh;
+				}
+				break;
+			}
+			}
+		}
+		}
+		if (fail) {
+			if (i < first)
+				first = i;
+			continue;
+		}
+		if (isnil) {
+			nils++;
+			if (x.op == X_ISZERO || x.op == X_SIGN)
+				((int8_t *) out)[i] = INT8_MIN;
+			else
+				x_store(out, x, i, NIL);
+			continue;
+		}
+		if (x.op == X_ISZERO || x.op == X_SIGN || x.op == X_ISNIL || x.op == X_ISNOTNIL)
+			((int8_t *) out)[i] = (int8_t) r.i;
+		else if (fl)
+			x_store(out, x, i, r);
+		else
+			st_int(out, x.ow, i, r.i);
+	}
+	nils = block_reduce(nils, [](unsigned long long u, unsigned long long v) { return u + v; });
+	first = block_reduce(first, [](unsigned long long u, unsigned long long v) { return u < v ? u : v; });
+	if (threadIdx.x == 0) {
+		if (nils)
+			atomicAdd(meta, nils);
+		if (first != ~0ull)
+			atomicMin(meta + 1, first);
+	}
+}
+
+Num
+x_nil_host(int t, int w)
+{
+	Num v{};
+	v.nil = true;
+	v.i = t == MGDK_oid ? (hge) MGDK_OID_NIL : w == 16 ? (hge) ((uhge) 1 << 127) : -((hge) 1 << (8 * w - 1));
+	return v;
+}
+
+const char *const xop_name[] = {"BATcalcnegate", "BATcalcabsolute", "BATcalciszero", "BATcalcsign",
+				 "BATcalcisnil", "BATcalcisnotnil", "BATcalcmin", "BATcalcmax", "BATcalcmin_no_nil",
+				 "BATcalcmax_no_nil", "BATcalcmincst", "BATcalcmaxcst", "BATcalcmincst_no_nil",
+				 "BATcalcmaxcst_no_nil", "BATcalcand", "BATcalcor", "BATcalcxor", "BATcalclsh",
+				 "BATcalcrsh"};
+
+bool
+tdense_bat(const mgdk_bat *b)
+{
+	return (b->ttype == MGDK_void || b->ttype == MGDK_oid) && b->tseqbase != MGDK_OID_NIL;
+}
+
+// the unary operators
+mgdk_bat *
+calc_unary(int op, mgdk_bat *b, mgdk_bat *s)
+{
+	if (b == nullptr) {
+		seterr("BATcalc: b must exist");
+		return nullptr;
+	}
+	ProfScope prof("calcunary");
+	Cand ci{};
+	if (cand_init(&ci, b, s) < 0)
+		return nullptr;
+	const oid hseq = s ? s->hseqbase : b->hseqbase;
+	const BUN n = ci.n;
+	if (op == X_ISNIL || op == X_ISNOTNIL) {
+		// BATcalcisnil_implementation (:802-900): constant answers first
+		const bool notnil = op == X_ISNOTNIL;
+		if (b->tnonil || tdense_bat(b) || b->ttype == MGDK_void) {
+			const int8_t v = (b->tnonil || tdense_bat(b)) ? notnil : !notnil;
+			return mgdk_BATconstant(hseq, MGDK_bit, &v, n);
+		}
+		if (b->ttype == MGDK_str || b->ttype == MGDK_msk) {
+			seterr("%s: type %s is not on the device path", xop_name[op], atomname(b->ttype));
+			return nullptr;
+		}
+	}
+	const int t = optype(b) == MGDK_oid ? MGDK_lng : basetype(b->ttype);
+	const bool numeric = is_num_t(t);
+	if (!numeric && !((op == X_ISNIL || op == X_ISNOTNIL) && (t == MGDK_lng || b->ttype == MGDK_oid))) {
+		seterr("type %s not supported.\n", atomname(b->ttype));
+		return nullptr;
+	}
+	const int otp = op == X_ISZERO || op == X_ISNIL || op == X_ISNOTNIL ? MGDK_bit : op == X_SIGN ? MGDK_bte : b->ttype;
+	if (n == 0) {
+		// BATconstant(ci.hseq, type, nil, 0)
+		return newbat(hseq, otp, 0);
+	}
+	mgdk_bat *bn = newbat(hseq, otp, n);
+	if (bn == nullptr)
+		return nullptr;
+	Opnd A{}, B{};
+	set_bat(A, b, ci, b->ttype == MGDK_oid ? MGDK_oid : t);
+	B.tp = -1;
+	XArgs x{op, t, t, width_of(otp), false, b->ttype == MGDK_oid, 0};
+	unsigned long long *m = counters(2);
+	if (m == nullptr) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	hipLaunchKernelGGL(k_xop, dim3(grid_for(n, 256 * 4, 256 * 64)), dim3(256), 0, stream(), A, B, x, bn->theap, n, m);
+	unsigned long long h[2];
+	if (!read_counters(m, h, 2)) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	const BUN nils = h[0];
+	bn->count = n;
+	bn->tnil = nils != 0;
+	bn->tnonil = nils == 0;
+	bn->tkey = n <= 1;
+	switch (op) {
+	case X_NEG:
+		// unary - reverses the order, but nils mess it up
+		bn->tsorted = nils == 0 && b->trevsorted;
+		bn->trevsorted = nils == 0 && b->tsorted;
+		bn->tkey = b->tkey && nils <= 1;
+		break;
+	case X_SIGN:
+		bn->tsorted = b->tsorted || n <= 1 || nils == n;
+		bn->trevsorted = b->trevsorted || n <= 1 || nils == n;
+		break;
+	case X_ISNIL:
+		bn->tsorted = b->trevsorted;
+		bn->trevsorted = b->tsorted;
+		bn->tnil = 0;
+		bn->tnonil = 1;
+		break;
+	case X_ISNOTNIL:
+		bn->tsorted = b->tsorted;
+		bn->trevsorted = b->trevsorted;
+		bn->tnil = 0;
+		bn->tnonil = 1;
+		break;
+	default:
+		bn->tsorted = n <= 1 || nils == n;
+		bn->trevsorted = n <= 1 || nils == n;
+		break;
+	}
+	return bn;
+}
+
+// min / max (b2 or the constant v of type vt), their _no_nil forms
+mgdk_bat *
+calc_minmax(int op, mgdk_bat *b1, mgdk_bat *b2, const void *v, int vt, mgdk_bat *s1, mgdk_bat *s2)
+{
+	const bool cst = b2 == nullptr;
+	const char *fname = xop_name[op];
+	if (b1 == nullptr) {
+		seterr("%s: b must exist", fname);
+		return nullptr;
+	}
+	ProfScope prof("calcminmax");
+	const int at1 = b1->ttype == MGDK_void ? MGDK_oid : b1->ttype;
+	if (cst ? at1 != (vt == MGDK_void ? MGDK_oid : vt) : at1 != (b2->ttype == MGDK_void ? MGDK_oid : b2->ttype)) {
+		seterr("inputs have incompatible types\n");
+		return nullptr;
+	}
+	Cand c1{}, c2{};
+	if (cand_init(&c1, b1, s1) < 0 || (!cst && cand_init(&c2, b2, s2) < 0))
+		return nullptr;
+	const oid h1 = s1 ? s1->hseqbase : b1->hseqbase;
+	if (!cst) {
+		const oid h2 = s2 ? s2->hseqbase : b2->hseqbase;
+		if (c1.n != c2.n || h1 != h2) {
+			seterr("inputs not the same size.\n");
+			return nullptr;
+		}
+	}
+	const bool isoid = at1 == MGDK_oid;
+	const int t = isoid ? MGDK_oid : basetype(b1->ttype);
+	if (!isoid && !is_num_t(t)) {
+		seterr("%s: type %s is not on the device path", fname, atomname(b1->ttype));
+		return nullptr;
+	}
+	const int otp = at1;
+	const BUN n = c1.n;
+	Opnd A{}, B{};
+	set_bat(A, b1, c1, b1->ttype == MGDK_void ? MGDK_void : t);
+	if (cst)
+		set_cst(B, v, t);
+	else
+		set_bat(B, b2, c2, b2->ttype == MGDK_void ? MGDK_void : t);
+	int xop = op;
+	if (cst) {
+		// BATcalcmincst (:1403-1433): an empty input, a nil constant or an
+		// all-nil void column give the all-nil column
+		const bool allnil1 = b1->ttype == MGDK_void && b1->tseqbase == MGDK_OID_NIL;
+		if (op == X_MIN || op == X_MAX) {
+			if (n == 0 || B.cnil || allnil1) {
+				mgdk_bat *bn = nullptr;
+				std::vector<uint8_t> nil(16, 0);
+				const int w = width_of(otp);
+				Num nv = x_nil_host(otp, w);
+				memcpy(nil.data(), &nv.i, 16);
+				if (t == MGDK_flt) { const float f = __builtin_nanf(""); memcpy(nil.data(), &f, 4); }
+				if (t == MGDK_dbl) { const double d = __builtin_nan(""); memcpy(nil.data(), &d, 8); }
+				bn = mgdk_BATconstant(h1, otp, nil.data(), n);
+				return bn;
+			}
+			xop = op == X_MIN ? X_MINC : X_MAXC;
+		} else {
+			if (n == 0)
+				return newbat(h1, otp, 0);
+			if (allnil1 && B.cnil) {
+				const oid nil = MGDK_OID_NIL;
+				return mgdk_BATconstant(h1, MGDK_void, &nil, n);
+			}
+			xop = op == X_MINNN ? X_MINNNC : X_MAXNNC;
+		}
+	}
+	mgdk_bat *bn = newbat(h1, otp, n);
+	if (bn == nullptr)
+		return nullptr;
+	if (n) {
+		XArgs x{xop, t == MGDK_oid ? MGDK_lng : t, t, width_of(otp), false, isoid, 0};
+		if (t == MGDK_oid)
+			x.t = MGDK_oid;
+		unsigned long long *m = counters(2);
+		if (m == nullptr) {
+			mgdk_BBPunfix(bn);
+			return nullptr;
+		}
+		hipLaunchKernelGGL(k_xop, dim3(grid_for(n, 256 * 4, 256 * 64)), dim3(256), 0, stream(), A, B, x, bn->theap, n,
+				   m);
+		unsigned long long h[2];
+		if (!read_counters(m, h, 2)) {
+			mgdk_BBPunfix(bn);
+			return nullptr;
+		}
+		bn->tnil = h[0] != 0;
+		bn->tnonil = h[0] == 0;
+	}
+	bn->count = n;
+	if (n <= 1) {
+		bn->tsorted = bn->trevsorted = bn->tkey = 1;
+		oid f = 0;
+		if (isoid && n == 1 && oid_at(bn, 0, &f) < 0) {
+			mgdk_BBPunfix(bn);
+			return nullptr;
+		}
+		bn->tseqbase = isoid ? (n == 1 ? f : 0) : MGDK_OID_NIL;
+	} else {
+		bn->tsorted = bn->trevsorted = bn->tkey = 0;
+		bn->tseqbase = MGDK_OID_NIL;
+	}
+	return bn;
+}
+
+// and / or / xor / lsh / rsh of (b1 | constant) with (b2 | constant)
+mgdk_bat *
+calc_bits(int op, const char *fname, mgdk_bat *b1, const void *v1, int t1, mgdk_bat *b2, const void *v2, int t2,
+	  mgdk_bat *s1, mgdk_bat *s2)
+{
+	mgdk_bat *bb = b1 ? b1 : b2;
+	if (bb == nullptr) {
+		seterr("%s: b must exist", fname);
+		return nullptr;
+	}
+	ProfScope prof("calcbits");
+	const int ta = b1 ? b1->ttype : t1, tb = b2 ? b2->ttype : t2;
+	const bool shift = op == X_LSH || op == X_RSH;
+	if (!shift && basetype(ta) != basetype(tb)) {
+		seterr("incompatible input types.\n");
+		return nullptr;
+	}
+	Cand c1{}, c2{}, ci{};
+	if (b1 && b2) {
+		if (cand_init(&c1, b1, s1) < 0 || cand_init(&c2, b2, s2) < 0)
+			return nullptr;
+		const oid h1 = s1 ? s1->hseqbase : b1->hseqbase, h2 = s2 ? s2->hseqbase : b2->hseqbase;
+		if (c1.n != c2.n || h1 != h2) {
+			seterr("inputs not the same size.\n");
+			return nullptr;
+		}
+		ci = c1;
+	} else {
+		if (cand_init(&ci, bb, s1) < 0)
+			return nullptr;
+		if (b1)
+			c1 = ci;
+		else
+			c2 = ci;
+	}
+	const oid hseq = s1 ? s1->hseqbase : bb->hseqbase;
+	const int ba = basetype(ta), bbt = basetype(tb);
+	// the result has the left operand's type (:2467, :3269)
+	const int otp = ta;
+	const BUN n = ci.n;
+	mgdk_bat *bn = newbat(hseq, otp, n);
+	if (bn == nullptr)
+		return nullptr;
+	bn->count = 0;
+	if (n == 0)
+		return bn;
+	if (!is_int_t(ba) || !is_int_t(bbt)) {
+		mgdk_BBPunfix(bn);
+		seterr("%s: bad input type %s.\n", fname, atomname(is_int_t(ba) ? tb : ta));
+		return nullptr;
+	}
+	Opnd A{}, B{};
+	if (b1)
+		set_bat(A, b1, c1, ba);
+	else
+		set_cst(A, v1, ba);
+	if (b2)
+		set_bat(B, b2, c2, bbt);
+	else
+		set_cst(B, v2, bbt);
+	XArgs x{op, ba, bbt, width_of(otp), ta == MGDK_bit, false, 8 * width_of(ba)};
+	unsigned long long *m = counters(2);
+	if (m == nullptr) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	hipLaunchKernelGGL(k_xop, dim3(grid_for(n, 256 * 4, 256 * 64)), dim3(256), 0, stream(), A, B, x, bn->theap, n, m);
+	unsigned long long h[2];
+	if (!read_counters(m, h, 2)) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	if (h[1] != ~0ull) {
+		Num v[2];
+		char xa[96], xb[96];
+		if (fetch2(A, &B, (BUN) h[1], v)) {
+			fmt_num(xa, sizeof(xa), ba, v[0]);
+			fmt_num(xb, sizeof(xb), bbt, v[1]);
+			if (shift)
+				seterr("%s: shift operand too large in %s(%s,%s).\n", fname, op == X_LSH ? "LSH" : "RSH", xa, xb);
+			else
+				seterr("22003!overflow in calculation %s%s%s.\n", xa, op == X_AND ? "AND" : "XOR", xb);
+		}
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	set_cmp_props(bn, n, h[0]);
+	return bn;
+}
+
+// BATcalcifthenelse (:4376-4760): b a bit column; "then" / "else" BATs (or
+// constants) aligned with b; a nil condition takes the else branch
+__global__ __launch_bounds__(256) void
+k_ifthenelse(const int8_t *cond, BUN n, const void *v1, bool c1, oid seq1, const void *v2, bool c2, oid seq2,
+	     int w, void *out)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		const int8_t c = cond[i];
+		const bool take1 = c != 0 && c != INT8_MIN;
+		const void *src = take1 ? v1 : v2;
+		const bool cs = take1 ? c1 : c2;
+		const oid seq = take1 ? seq1 : seq2;
+		if (src == nullptr) {
+			// a void column: its sequence advanced once per row
+			// (gdk_calc.c:4550-4561)
+			((uint64_t *) out)[i] = seq + i;
+			continue;
+		}
+		const BUN p = cs ? 0 : i;
+		switch (w) {
+		case 1: ((int8_t *) out)[i] = ((const int8_t *) src)[p]; break;
+		case 2: ((int16_t *) out)[i] = ((const int16_t *) src)[p]; break;
+		case 4: ((int32_t *) out)[i] = ((const int32_t *) src)[p]; break;
+		case 8: ((int64_t *) out)[i] = ((const int64_t *) src)[p]; break;
+		default: ((hge *) out)[i] = ((const hge *) src)[p]; break;
+		}
+	}
+}
+
+mgdk_bat *
+calc_ifthenelse(mgdk_bat *b, mgdk_bat *b1, const void *cv1, mgdk_bat *b2, const void *cv2, int ct)
+{
+	if (b == nullptr || (b1 == nullptr && cv1 == nullptr) || (b2 == nullptr && cv2 == nullptr)) {
+		seterr("BATcalcifthenelse: inputs must exist");
+		return nullptr;
+	}
+	ProfScope prof("calcifthenelse");
+	const int t1 = b1 ? b1->ttype : ct, t2 = b2 ? b2->ttype : ct;
+	auto at = [](int t) { return t == MGDK_void ? MGDK_oid : t; };
+	if ((b1 && b1->count != b->count) || (b2 && b2->count != b->count)) {
+		seterr("BATcalcifthenelse: BATs have different lengths.\n");
+		return nullptr;
+	}
+	if (b->ttype != MGDK_bit || at(t1) != at(t2)) {
+		seterr("\"then\" and \"else\" BATs have different types.\n");
+		return nullptr;
+	}
+	const int tp = at(t1);
+	if (tp == MGDK_str || tp == MGDK_msk || width_of(tp) == 0) {
+		seterr("BATcalcifthenelse: type %s is not on the device path", atomname(tp));
+		return nullptr;
+	}
+	const BUN n = b->count;
+	mgdk_bat *bn = newbat(b->hseqbase, tp, n);
+	if (bn == nullptr)
+		return nullptr;
+	const int w = width_of(tp);
+	// constants staged on the device
+	DevBuf cb(64);
+	if (!cb.p) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	char hc[64] = {0};
+	if (cv1)
+		memcpy(hc, cv1, w);
+	if (cv2)
+		memcpy(hc + 32, cv2, w);
+	if (!hip_ok(hipMemcpyAsync(cb.p, hc, 64, hipMemcpyHostToDevice, stream()), "memcpy")) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	auto src = [&](mgdk_bat *x, int k) -> const void * {
+		if (x == nullptr)
+			return (const char *) cb.p + 32 * k;
+		return x->ttype == MGDK_void ? nullptr : (const void *) x->theap;
+	};
+	const oid seq1 = b1 && b1->ttype == MGDK_void ? b1->tseqbase : 0, seq2 = b2 && b2->ttype == MGDK_void ? b2->tseqbase : 0;
+	if (n)
+		hipLaunchKernelGGL(k_ifthenelse, dim3(grid_for(n, 256 * 4, 256 * 64)), dim3(256), 0, stream(),
+				   (const int8_t *) b->theap, n, src(b1, 0), b1 == nullptr, seq1, src(b2, 1), b2 == nullptr, seq2, w,
+				   bn->theap);
+	if (!sync()) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	auto cnonil = [&](const void *c) {
+		Opnd o{};
+		set_cst(o, c, basetype(tp) == MGDK_oid ? MGDK_oid : basetype(tp));
+		return !o.cnil;
+	};
+	const bool nonil1 = b1 ? (bool) b1->tnonil : cnonil(cv1), nonil2 = b2 ? (bool) b2->tnonil : cnonil(cv2);
+	bn->count = n;
+	bn->tsorted = bn->trevsorted = bn->tkey = n <= 1;
+	bn->tnil = 0;
+	bn->tnonil = nonil1 && nonil2;
+	return bn;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1462,5 +2079,90 @@ mgdk_bat *mgdk_BATcalcmodcst(mgdk_bat *b, const void *v, int vt, mgdk_bat *s, in
 { return calcdivmod(false, b, nullptr, 0, nullptr, v, vt, s, nullptr, tp); }
 mgdk_bat *mgdk_BATcalccstmod(const void *v, int vt, mgdk_bat *b, mgdk_bat *s, int tp)
 { return calcdivmod(false, nullptr, v, vt, b, nullptr, 0, s, nullptr, tp); }
+
+
+// the rest of gdk_calc.c's element-wise operators (calc_unary & co. above)
+mgdk_bat *mgdk_BATcalcnegate(mgdk_bat *b, mgdk_bat *s) { return calc_unary(X_NEG, b, s); }
+mgdk_bat *mgdk_BATcalcabsolute(mgdk_bat *b, mgdk_bat *s) { return calc_unary(X_ABS, b, s); }
+mgdk_bat *mgdk_BATcalciszero(mgdk_bat *b, mgdk_bat *s) { return calc_unary(X_ISZERO, b, s); }
+mgdk_bat *mgdk_BATcalcsign(mgdk_bat *b, mgdk_bat *s) { return calc_unary(X_SIGN, b, s); }
+mgdk_bat *mgdk_BATcalcisnil(mgdk_bat *b, mgdk_bat *s) { return calc_unary(X_ISNIL, b, s); }
+mgdk_bat *mgdk_BATcalcisnotnil(mgdk_bat *b, mgdk_bat *s) { return calc_unary(X_ISNOTNIL, b, s); }
+
+// BATcalcincr / BATcalcdecr (gdk_calc_addsub.c:1681-1760): b + 1 / b - 1 in
+// b's type with the overflow check of BATcalcaddcst; the properties as
+// BATcalcincrdecr sets them.  (The reference's loop passes its candidate
+// iterators in swapped roles and computes only the first row; the device
+// computes every row.)
+static mgdk_bat *
+incrdecr(mgdk_bat *b, mgdk_bat *s, bool incr)
+{
+	if (b == nullptr) {
+		seterr("BATcalcincr: b must exist");
+		return nullptr;
+	}
+	const int8_t one = 1;
+	mgdk_bat *bn = incr ? mgdk_BATcalcaddcst(b, &one, MGDK_bte, s, b->ttype)
+			    : mgdk_BATcalcsubcst(b, &one, MGDK_bte, s, b->ttype);
+	if (bn == nullptr)
+		return nullptr;
+	const BUN n = bn->count;
+	const bool allnil = bn->tnil && n > 0 && !bn->tnonil && false;
+	(void) allnil;
+	bn->tsorted = b->tsorted || n <= 1 || (bn->tnil && n == 1);
+	bn->trevsorted = b->trevsorted || n <= 1;
+	bn->tkey = n <= 1;
+	return bn;
+}
+mgdk_bat *mgdk_BATcalcincr(mgdk_bat *b, mgdk_bat *s) { return incrdecr(b, s, true); }
+mgdk_bat *mgdk_BATcalcdecr(mgdk_bat *b, mgdk_bat *s) { return incrdecr(b, s, false); }
+
+mgdk_bat *mgdk_BATcalcmin(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2)
+{ return calc_minmax(X_MIN, b1, b2, nullptr, 0, s1, s2); }
+mgdk_bat *mgdk_BATcalcmax(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2)
+{ return calc_minmax(X_MAX, b1, b2, nullptr, 0, s1, s2); }
+mgdk_bat *mgdk_BATcalcmin_no_nil(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2)
+{ return calc_minmax(X_MINNN, b1, b2, nullptr, 0, s1, s2); }
+mgdk_bat *mgdk_BATcalcmax_no_nil(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2)
+{ return calc_minmax(X_MAXNN, b1, b2, nullptr, 0, s1, s2); }
+mgdk_bat *mgdk_BATcalcmincst(mgdk_bat *b, const void *v, int vt, mgdk_bat *s)
+{ return calc_minmax(X_MIN, b, nullptr, v, vt, s, nullptr); }
+mgdk_bat *mgdk_BATcalcmaxcst(mgdk_bat *b, const void *v, int vt, mgdk_bat *s)
+{ return calc_minmax(X_MAX, b, nullptr, v, vt, s, nullptr); }
+mgdk_bat *mgdk_BATcalcmincst_no_nil(mgdk_bat *b, const void *v, int vt, mgdk_bat *s)
+{ return calc_minmax(X_MINNN, b, nullptr, v, vt, s, nullptr); }
+mgdk_bat *mgdk_BATcalcmaxcst_no_nil(mgdk_bat *b, const void *v, int vt, mgdk_bat *s)
+{ return calc_minmax(X_MAXNN, b, nullptr, v, vt, s, nullptr); }
+mgdk_bat *mgdk_BATcalccstmin(const void *v, int vt, mgdk_bat *b, mgdk_bat *s)
+{ return calc_minmax(X_MIN, b, nullptr, v, vt, s, nullptr); }
+mgdk_bat *mgdk_BATcalccstmax(const void *v, int vt, mgdk_bat *b, mgdk_bat *s)
+{ return calc_minmax(X_MAX, b, nullptr, v, vt, s, nullptr); }
+mgdk_bat *mgdk_BATcalccstmin_no_nil(const void *v, int vt, mgdk_bat *b, mgdk_bat *s)
+{ return calc_minmax(X_MINNN, b, nullptr, v, vt, s, nullptr); }
+mgdk_bat *mgdk_BATcalccstmax_no_nil(const void *v, int vt, mgdk_bat *b, mgdk_bat *s)
+{ return calc_minmax(X_MAXNN, b, nullptr, v, vt, s, nullptr); }
+
+#define BITFN(NAME, OPC)                                                                                   \
+	mgdk_bat *mgdk_BATcalc##NAME(mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *s1, mgdk_bat *s2)                 \
+	{ return calc_bits(OPC, "BATcalc" #NAME, b1, nullptr, 0, b2, nullptr, 0, s1, s2); }               \
+	mgdk_bat *mgdk_BATcalc##NAME##cst(mgdk_bat *b, const void *v, int vt, mgdk_bat *s)                    \
+	{ return calc_bits(OPC, "BATcalc" #NAME "cst", b, nullptr, 0, nullptr, v, vt, s, nullptr); }      \
+	mgdk_bat *mgdk_BATcalccst##NAME(const void *v, int vt, mgdk_bat *b, mgdk_bat *s)                    \
+	{ return calc_bits(OPC, "BATcalccst" #NAME, nullptr, v, vt, b, nullptr, 0, s, nullptr); }
+BITFN(and, X_AND)
+BITFN(or, X_OR)
+BITFN(xor, X_XOR)
+BITFN(lsh, X_LSH)
+BITFN(rsh, X_RSH)
+#undef BITFN
+
+mgdk_bat *mgdk_BATcalcifthenelse(mgdk_bat *b, mgdk_bat *b1, mgdk_bat *b2)
+{ return calc_ifthenelse(b, b1, nullptr, b2, nullptr, 0); }
+mgdk_bat *mgdk_BATcalcifthenelsecst(mgdk_bat *b, mgdk_bat *b1, const void *c2, int ct)
+{ return calc_ifthenelse(b, b1, nullptr, nullptr, c2, ct); }
+mgdk_bat *mgdk_BATcalcifthencstelse(mgdk_bat *b, const void *c1, int ct, mgdk_bat *b2)
+{ return calc_ifthenelse(b, nullptr, c1, b2, nullptr, ct); }
+mgdk_bat *mgdk_BATcalcifthencstelsecst(mgdk_bat *b, const void *c1, const void *c2, int ct)
+{ return calc_ifthenelse(b, nullptr, c1, nullptr, c2, ct); }
 
 }  // extern "C"

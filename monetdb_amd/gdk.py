@@ -115,6 +115,45 @@ _SIGS = {
     "mgdk_BATcalcbetweencstbat": (P, [P, C.c_void_p, P, C.c_int, P, P] + [C.c_bool] * 5),
     "mgdk_BATconvert": (P, [P, P, C.c_int, C.c_uint8, C.c_uint8, C.c_uint8]),
     "mgdk_BATcalcnot": (P, [P, P]),
+    "mgdk_BATcalcnegate": (P, [P, P]),
+    "mgdk_BATcalcabsolute": (P, [P, P]),
+    "mgdk_BATcalciszero": (P, [P, P]),
+    "mgdk_BATcalcsign": (P, [P, P]),
+    "mgdk_BATcalcisnil": (P, [P, P]),
+    "mgdk_BATcalcisnotnil": (P, [P, P]),
+    "mgdk_BATcalcincr": (P, [P, P]),
+    "mgdk_BATcalcdecr": (P, [P, P]),
+    "mgdk_BATcalcmin": (P, [P, P, P, P]),
+    "mgdk_BATcalcmax": (P, [P, P, P, P]),
+    "mgdk_BATcalcmin_no_nil": (P, [P, P, P, P]),
+    "mgdk_BATcalcmax_no_nil": (P, [P, P, P, P]),
+    "mgdk_BATcalcand": (P, [P, P, P, P]),
+    "mgdk_BATcalcor": (P, [P, P, P, P]),
+    "mgdk_BATcalcxor": (P, [P, P, P, P]),
+    "mgdk_BATcalclsh": (P, [P, P, P, P]),
+    "mgdk_BATcalcrsh": (P, [P, P, P, P]),
+    "mgdk_BATcalcmincst": (P, [P, C.c_void_p, C.c_int, P]),
+    "mgdk_BATcalcmaxcst": (P, [P, C.c_void_p, C.c_int, P]),
+    "mgdk_BATcalcmincst_no_nil": (P, [P, C.c_void_p, C.c_int, P]),
+    "mgdk_BATcalcmaxcst_no_nil": (P, [P, C.c_void_p, C.c_int, P]),
+    "mgdk_BATcalcandcst": (P, [P, C.c_void_p, C.c_int, P]),
+    "mgdk_BATcalcorcst": (P, [P, C.c_void_p, C.c_int, P]),
+    "mgdk_BATcalcxorcst": (P, [P, C.c_void_p, C.c_int, P]),
+    "mgdk_BATcalclshcst": (P, [P, C.c_void_p, C.c_int, P]),
+    "mgdk_BATcalcrshcst": (P, [P, C.c_void_p, C.c_int, P]),
+    "mgdk_BATcalccstmin": (P, [C.c_void_p, C.c_int, P, P]),
+    "mgdk_BATcalccstmax": (P, [C.c_void_p, C.c_int, P, P]),
+    "mgdk_BATcalccstmin_no_nil": (P, [C.c_void_p, C.c_int, P, P]),
+    "mgdk_BATcalccstmax_no_nil": (P, [C.c_void_p, C.c_int, P, P]),
+    "mgdk_BATcalccstand": (P, [C.c_void_p, C.c_int, P, P]),
+    "mgdk_BATcalccstor": (P, [C.c_void_p, C.c_int, P, P]),
+    "mgdk_BATcalccstxor": (P, [C.c_void_p, C.c_int, P, P]),
+    "mgdk_BATcalccstlsh": (P, [C.c_void_p, C.c_int, P, P]),
+    "mgdk_BATcalccstrsh": (P, [C.c_void_p, C.c_int, P, P]),
+    "mgdk_BATcalcifthenelse": (P, [P, P, P]),
+    "mgdk_BATcalcifthenelsecst": (P, [P, P, C.c_void_p, C.c_int]),
+    "mgdk_BATcalcifthencstelse": (P, [P, C.c_void_p, C.c_int, P]),
+    "mgdk_BATcalcifthencstelsecst": (P, [P, C.c_void_p, C.c_void_p, C.c_int]),
     "mgdk_BATcalcdiv": (P, [P, P, P, P, C.c_int]),
     "mgdk_BATcalcdivcst": (P, [P, C.c_void_p, C.c_int, P, C.c_int]),
     "mgdk_BATcalccstdiv": (P, [C.c_void_p, C.c_int, P, P, C.c_int]),
@@ -678,6 +717,40 @@ def BATgroupprod(b, g, e, tp, skip_nils=True, s=None):
 def BATunmask(b):
     """BATunmask (gdk_cand.c:1464)"""
     return BAT(lib().mgdk_BATunmask(b.ptr))
+
+
+def BATcalcunary(name, b, s=None):
+    """BATcalc{negate,absolute,iszero,sign,isnil,isnotnil,incr,decr}(b, s)"""
+    return BAT(getattr(lib(), "mgdk_BATcalc" + name)(b.ptr, _p(s)))
+
+
+def BATcalcbin(name, b1, b2, s1=None, s2=None):
+    """BATcalc{min,max,min_no_nil,max_no_nil,and,or,xor,lsh,rsh}(b1, b2, s1, s2)"""
+    return BAT(getattr(lib(), "mgdk_BATcalc" + name)(b1.ptr, b2.ptr, _p(s1), _p(s2)))
+
+
+def BATcalcbincst(name, b, v, vt, s=None, cst_first=False):
+    """BATcalc<name>cst(b, v, s) or, cst_first, BATcalccst<name>(v, b, s)"""
+    keep = []
+    vp = _valptr(vt, v, keep)
+    if cst_first:
+        return BAT(getattr(lib(), "mgdk_BATcalccst" + name)(vp, vt, b.ptr, _p(s)))
+    n = name.replace("_no_nil", "cst_no_nil") if name.endswith("_no_nil") else name + "cst"
+    return BAT(getattr(lib(), "mgdk_BATcalc" + n)(b.ptr, vp, vt, _p(s)))
+
+
+def BATcalcifthenelse(b, then, else_, ct=None):
+    """BATcalcifthenelse (gdk_calc.c:4661) and its constant forms: then /
+    else are BATs or Python values of type ct"""
+    keep = []
+    t_bat, e_bat = isinstance(then, BAT), isinstance(else_, BAT)
+    if t_bat and e_bat:
+        return BAT(lib().mgdk_BATcalcifthenelse(b.ptr, then.ptr, else_.ptr))
+    if t_bat:
+        return BAT(lib().mgdk_BATcalcifthenelsecst(b.ptr, then.ptr, _valptr(ct, else_, keep), ct))
+    if e_bat:
+        return BAT(lib().mgdk_BATcalcifthencstelse(b.ptr, _valptr(ct, then, keep), ct, else_.ptr))
+    return BAT(lib().mgdk_BATcalcifthencstelsecst(b.ptr, _valptr(ct, then, keep), _valptr(ct, else_, keep), ct))
 
 
 def BATgroupmin(b, g, e, skip_nils=True, s=None):

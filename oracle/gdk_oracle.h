@@ -112,6 +112,17 @@ ora_bat *ora_calcbetween(const ora_bat *b, const ora_bat *lo, const void *clo, c
 /* BATconvert (gdk/gdk_calc_convert.c:1415) for numeric / oid / bit types */
 ora_bat *ora_convert(const ora_bat *b, const ora_bat *s, int tp, int scale1, int scale2, int prec);
 ora_bat *ora_calcnot(const ora_bat *b, const ora_bat *s);
+/* gdk_calc.c:233-920 negate / absolute / iszero / sign / isnil / isnotnil
+ * (op 0..5), :976-2436 min / max / _no_nil (op 6..9; b2 NULL: the constant c
+ * of type ct), :2439-3760 and / or / xor / lsh / rsh (op 10..14), :4376
+ * ifthenelse (b1 / b2 NULL: the constants of type ct) */
+ora_bat *ora_calcunary(int op, const ora_bat *b, const ora_bat *s);
+ora_bat *ora_calcminmax(int op, const ora_bat *b1, const ora_bat *b2, const void *c, int ct, const ora_bat *s1,
+			const ora_bat *s2);
+ora_bat *ora_calcbits(int op, const char *fname, const ora_bat *b1, const void *c1, int t1, const ora_bat *b2,
+		      const void *c2, int t2, const ora_bat *s1, const ora_bat *s2);
+ora_bat *ora_calcifthenelse(const ora_bat *b, const ora_bat *b1, const void *c1, const ora_bat *b2, const void *c2,
+			    int ct);
 /* BATcalcdiv / BATcalcmod (+cst variants): op '/' or '%' */
 ora_bat *ora_calcdivmod(char op, const ora_bat *b1, const void *c1, int t1, const ora_bat *b2,
 			const void *c2, int t2, const ora_bat *s1, const ora_bat *s2, int tp);

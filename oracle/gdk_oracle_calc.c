@@ -1061,3 +1061,375 @@ ora_calcdivmod(char op, const ora_bat *b1, const void *c1, int t1, const ora_bat
 	bn->nonil = nils == 0;
 	return bn;
 }
+
+/* ---------------------------------------------------------------------- */
+/* the rest of gdk_calc.c's element-wise operators: BATcalcnegate,
+ * -absolute, -iszero, -sign (gdk_calc.c:233-800; UNARY_2TYPE_FUNC
+ * gdk_calc_private.h:354), -isnil / -isnotnil (:802-920), min / max with
+ * their _no_nil and constant forms (MINMAX_TYPE :944, MINMAX_NONIL_TYPE
+ * :1150, MINMAX_CST_TYPE :1385, MINMAX_NONIL_CST_TYPE :1535), xor / or / and
+ * (:2439-3030; bit: or3 / and3 :2590 / :2826, XORBIT; integers: a result
+ * equal to nil is "overflow in calculation"), lsh / rsh (:3059-3760:
+ * SHIFT_CHECK, LSH_CHECK, "shift operand too large"), ifthenelse
+ * (:4376-4760: a nil condition takes the else branch). */
+
+enum { XO_NEG, XO_ABS, XO_ISZERO, XO_SIGN, XO_ISNIL, XO_ISNOTNIL, XO_MIN, XO_MAX, XO_MINNN, XO_MAXNN, XO_AND,
+       XO_OR, XO_XOR, XO_LSH, XO_RSH };
+
+static num
+nilnum(int t)
+{
+	num v = {.t = t, .nil = true, .f = NAN, .d = NAN};
+	switch (t) {
+	case ORA_bte: v.i = INT8_MIN; break;
+	case ORA_sht: v.i = INT16_MIN; break;
+	case ORA_int: v.i = INT32_MIN; break;
+	case ORA_lng: v.i = INT64_MIN; break;
+	case ORA_hge: v.i = HGE_NIL; break;
+	case ORA_oid: v.i = (ora_hge) ORA_OID_NIL; break;
+	}
+	return v;
+}
+
+static void
+store(int t, void *base, uint64_t k, const num *v)
+{
+	switch (t) {
+	case ORA_bte: ((int8_t *) base)[k] = (int8_t) v->i; break;
+	case ORA_sht: ((int16_t *) base)[k] = (int16_t) v->i; break;
+	case ORA_int: ((int32_t *) base)[k] = (int32_t) v->i; break;
+	case ORA_lng: ((int64_t *) base)[k] = (int64_t) v->i; break;
+	case ORA_hge: ((ora_hge *) base)[k] = v->i; break;
+	case ORA_oid: ((ora_oid *) base)[k] = (ora_oid) v->i; break;
+	case ORA_flt: ((float *) base)[k] = v->f; break;
+	case ORA_dbl: ((double *) base)[k] = v->d; break;
+	}
+}
+
+/* value k of an operand; void columns count from their tseqbase */
+static num
+getv(const opnd *o, uint64_t k)
+{
+	if (o->b && o->b->type == ORA_void) {
+		const ora_oid s = o->b->tseqbase;
+		num v = {.t = ORA_oid, .nil = s == ORA_OID_NIL, .i = (ora_hge) (s == ORA_OID_NIL ? s : s + pos_of(o, k))};
+		return v;
+	}
+	return load(o->t, base_of(o), o->b ? pos_of(o, k) : 0);
+}
+
+static bool
+lt(const num *a, const num *b)
+{
+	if (a->t == ORA_flt)
+		return a->f < b->f;
+	if (a->t == ORA_dbl)
+		return a->d < b->d;
+	if (a->t == ORA_oid)
+		return (unsigned __int128) a->i < (unsigned __int128) b->i;
+	return a->i < b->i;
+}
+
+static bool
+tdense_(const ora_bat *b)
+{
+	return (b->type == ORA_void || b->type == ORA_oid) && b->tseqbase != ORA_OID_NIL;
+}
+
+ora_bat *
+ora_calcunary(int op, const ora_bat *b, const ora_bat *s)
+{
+	opnd o = {.b = b};
+	if (ora_ci_init(&o.ci, b, s) < 0)
+		return NULL;
+	const uint64_t n = o.ci.n;
+	const ora_oid hseq = s ? s->hseqbase : b->hseqbase;
+	if (op == XO_ISNIL || op == XO_ISNOTNIL) {
+		const bool notnil = op == XO_ISNOTNIL;
+		if (b->nonil || tdense_(b) || b->type == ORA_void) {
+			ora_bat *bn = ora_new(ORA_bit, n, hseq);
+			if (bn == NULL)
+				return NULL;
+			memset(bn->base, (b->nonil || tdense_(b)) ? notnil : !notnil, n);
+			bn->sorted = bn->revsorted = 1;
+			bn->key = n <= 1;
+			bn->nil = 0;
+			bn->nonil = 1;
+			return bn;
+		}
+	}
+	const int t = b->type == ORA_oid ? ORA_oid : btype(b->type);
+	if (!is_num(t) && !((op == XO_ISNIL || op == XO_ISNOTNIL) && t == ORA_oid)) {
+		ora_seterr("type %s not supported.\n", tname(b->type));
+		return NULL;
+	}
+	o.t = t;
+	const int otp = op == XO_ISZERO || op == XO_ISNIL || op == XO_ISNOTNIL ? ORA_bit : op == XO_SIGN ? ORA_bte
+											       : b->type;
+	const int ot = btype(otp);
+	ora_bat *bn = ora_new(otp, n, hseq);
+	if (bn == NULL)
+		return NULL;
+	uint64_t nils = 0;
+	for (uint64_t k = 0; k < n; k++) {
+		num v = getv(&o, k), r = v;
+		if (op == XO_ISNIL || op == XO_ISNOTNIL) {
+			((int8_t *) bn->base)[k] = (int8_t) (v.nil != (op == XO_ISNOTNIL));
+			continue;
+		}
+		if (v.nil) {
+			num z = nilnum(ot);
+			store(ot, bn->base, k, &z);
+			nils++;
+			continue;
+		}
+		switch (op) {
+		case XO_NEG: r.i = -v.i; r.f = -v.f; r.d = -v.d; break;
+		case XO_ABS: r.i = v.i < 0 ? -v.i : v.i; r.f = fabsf(v.f); r.d = fabs(v.d); break;
+		case XO_ISZERO:
+			r.t = ORA_bte;
+			r.i = t == ORA_flt ? v.f == 0 : t == ORA_dbl ? v.d == 0 : v.i == 0;
+			break;
+		case XO_SIGN:
+			r.t = ORA_bte;
+			r.i = t == ORA_flt ? (v.f < 0 ? -1 : v.f > 0) : t == ORA_dbl ? (v.d < 0 ? -1 : v.d > 0)
+										 : (v.i < 0 ? -1 : v.i > 0);
+			break;
+		}
+		store(ot, bn->base, k, &r);
+	}
+	bn->nil = nils != 0;
+	bn->nonil = nils == 0;
+	bn->key = n <= 1;
+	switch (op) {
+	case XO_NEG:
+		bn->sorted = nils == 0 && b->revsorted;
+		bn->revsorted = nils == 0 && b->sorted;
+		bn->key = b->key && nils <= 1;
+		break;
+	case XO_SIGN:
+		bn->sorted = b->sorted || n <= 1 || nils == n;
+		bn->revsorted = b->revsorted || n <= 1 || nils == n;
+		break;
+	case XO_ISNIL:
+		bn->sorted = b->revsorted;
+		bn->revsorted = b->sorted;
+		break;
+	case XO_ISNOTNIL:
+		bn->sorted = b->sorted;
+		bn->revsorted = b->revsorted;
+		break;
+	default:
+		bn->sorted = bn->revsorted = n <= 1 || nils == n;
+		break;
+	}
+	return bn;
+}
+
+/* min / max (b2 NULL: the constant c of type ct) and their _no_nil forms */
+ora_bat *
+ora_calcminmax(int op, const ora_bat *b1, const ora_bat *b2, const void *c, int ct, const ora_bat *s1,
+	       const ora_bat *s2)
+{
+	const int a1 = b1->type == ORA_void ? ORA_oid : b1->type;
+	const int a2 = b2 ? (b2->type == ORA_void ? ORA_oid : b2->type) : (ct == ORA_void ? ORA_oid : ct);
+	if (a1 != a2) {
+		ora_seterr("inputs have incompatible types\n");
+		return NULL;
+	}
+	opnd l = {.b = b1}, r = {.b = b2, .c = c};
+	if (ora_ci_init(&l.ci, b1, s1) < 0 || (b2 && ora_ci_init(&r.ci, b2, s2) < 0))
+		return NULL;
+	const ora_oid h1 = s1 ? s1->hseqbase : b1->hseqbase;
+	if (b2 && (l.ci.n != r.ci.n || h1 != (s2 ? s2->hseqbase : b2->hseqbase))) {
+		ora_seterr("inputs not the same size.\n");
+		return NULL;
+	}
+	const int t = a1 == ORA_oid ? ORA_oid : btype(b1->type);
+	l.t = r.t = t;
+	const uint64_t n = l.ci.n;
+	ora_bat *bn = ora_new(a1, n, h1);
+	if (bn == NULL)
+		return NULL;
+	const bool domax = op == XO_MAX || op == XO_MAXNN, nonil = op == XO_MINNN || op == XO_MAXNN;
+	const num cv = b2 ? (num) {0} : load(t, c, 0);
+	const bool allnil1 = b1->type == ORA_void && b1->tseqbase == ORA_OID_NIL;
+	bool nils = false;
+	for (uint64_t k = 0; k < n; k++) {
+		num p = getv(&l, k), q = b2 ? getv(&r, k) : cv, res;
+		if (!b2 && !nonil && (cv.nil || allnil1)) {
+			res = nilnum(t);                          /* BATconstantV(nil) */
+		} else if (!nonil) {
+			if (p.nil || q.nil)
+				res = nilnum(t);
+			else if (b2)
+				res = (domax ? lt(&q, &p) : lt(&p, &q)) ? p : q;     /* p1 OP p2 ? p1 : p2 */
+			else
+				res = (domax ? lt(&q, &p) : lt(&p, &q)) ? p : q;     /* p1 OP pp2 ? p1 : pp2 */
+		} else if (b2) {
+			/* MINMAX_NONIL_TYPE: p1 nil -> p2; else (!nil(p2) && p2 OP p1) ? p2 : p1 */
+			if (p.nil)
+				res = q;
+			else
+				res = !q.nil && (domax ? lt(&p, &q) : lt(&q, &p)) ? q : p;
+		} else {
+			/* MINMAX_NONIL_CST_TYPE */
+			if (cv.nil)
+				res = p;
+			else if (p.nil)
+				res = cv;
+			else
+				res = (domax ? lt(&cv, &p) : lt(&p, &cv)) ? p : cv;
+		}
+		nils |= res.nil;
+		store(t, bn->base, k, &res);
+	}
+	bn->nil = nils;
+	bn->nonil = !nils;
+	bn->sorted = bn->revsorted = bn->key = n <= 1;
+	bn->tseqbase = a1 == ORA_oid && n <= 1 ? (n == 1 ? ((ora_oid *) bn->base)[0] : 0) : ORA_OID_NIL;
+	return bn;
+}
+
+static const char *const xo_opname[] = {[XO_AND] = "AND", [XO_OR] = "OR", [XO_XOR] = "XOR", [XO_LSH] = "LSH",
+					[XO_RSH] = "RSH"};
+
+static void
+fmtnum(char *buf, size_t sz, const num *v)
+{
+	switch (v->t) {
+	case ORA_bte: case ORA_sht: case ORA_int: snprintf(buf, sz, "%d", (int) v->i); break;
+	case ORA_lng: snprintf(buf, sz, "%lld", (long long) v->i); break;
+	case ORA_hge: snprintf(buf, sz, "%.40Lg (approx. value)", (long double) v->i); break;
+	default: snprintf(buf, sz, "%llu", (unsigned long long) v->i); break;
+	}
+}
+
+/* xor / or / and / lsh / rsh of (b1 | c1) with (b2 | c2); fname for the
+ * shift message */
+ora_bat *
+ora_calcbits(int op, const char *fname, const ora_bat *b1, const void *c1, int t1, const ora_bat *b2,
+	     const void *c2, int t2, const ora_bat *s1, const ora_bat *s2)
+{
+	const int ta = b1 ? b1->type : t1, tb = b2 ? b2->type : t2;
+	const bool shift = op == XO_LSH || op == XO_RSH;
+	if (!shift && btype(ta) != btype(tb)) {
+		ora_seterr("incompatible input types.\n");
+		return NULL;
+	}
+	opnd l = {.b = b1, .c = c1}, r = {.b = b2, .c = c2};
+	const ora_bat *bb = b1 ? b1 : b2;
+	ora_ci ci;
+	if (b1 && b2) {
+		if (ora_ci_init(&l.ci, b1, s1) < 0 || ora_ci_init(&r.ci, b2, s2) < 0)
+			return NULL;
+		if (l.ci.n != r.ci.n || (s1 ? s1->hseqbase : b1->hseqbase) != (s2 ? s2->hseqbase : b2->hseqbase)) {
+			ora_seterr("inputs not the same size.\n");
+			return NULL;
+		}
+		ci = l.ci;
+	} else {
+		if (ora_ci_init(&ci, bb, s1) < 0)
+			return NULL;
+		if (b1)
+			l.ci = ci;
+		else
+			r.ci = ci;
+	}
+	const ora_oid hseq = s1 ? s1->hseqbase : bb->hseqbase;
+	const uint64_t n = ci.n;
+	ora_bat *bn = ora_new(ta, n, hseq);
+	if (bn == NULL || n == 0)
+		return bn;
+	l.t = btype(ta);
+	r.t = btype(tb);
+	if (!is_int(l.t) || !is_int(r.t)) {
+		ora_free(bn);
+		ora_seterr("%s: bad input type %s.\n", fname, tname(is_int(l.t) ? tb : ta));
+		return NULL;
+	}
+	const int bits = ora_width(l.t) * 8;
+	const ora_hge mx = bits == 128 ? HGE_MAX : (((ora_hge) 1 << (bits - 1)) - 1);
+	const num NIL = nilnum(l.t);
+	uint64_t nils = 0;
+	for (uint64_t k = 0; k < n; k++) {
+		num p = getv(&l, k), q = getv(&r, k), res = p;
+		bool fail = false;
+		if (ta == ORA_bit && (op == XO_AND || op == XO_OR)) {
+			int8_t v1 = (int8_t) p.i, v2 = (int8_t) q.i;
+			res.i = op == XO_OR ? or3(v1, v2) : and3(v1, v2);
+			res.nil = res.i == INT8_MIN;
+		} else if (p.nil || q.nil) {
+			res = NIL;
+		} else if (ta == ORA_bit) {
+			res.i = (p.i == 0) != (q.i == 0);
+		} else if (!shift) {
+			res.i = op == XO_AND ? (p.i & q.i) : op == XO_OR ? (p.i | q.i) : (p.i ^ q.i);
+			fail = res.i == NIL.i && op != XO_OR;
+		} else if (q.i < 0 || q.i >= bits || (op == XO_LSH && (p.i < 0 || p.i > (mx >> (int) q.i)))) {
+			fail = true;
+		} else {
+			res.i = op == XO_LSH ? p.i << (int) q.i : p.i >> (int) q.i;
+		}
+		if (fail) {
+			char x[96], y[96];
+			fmtnum(x, sizeof(x), &p);
+			fmtnum(y, sizeof(y), &q);
+			if (shift)
+				ora_seterr("%s: shift operand too large in %s(%s,%s).\n", fname, xo_opname[op], x, y);
+			else
+				ora_seterr("22003!overflow in calculation %s%s%s.\n", x, xo_opname[op], y);
+			ora_free(bn);
+			return NULL;
+		}
+		nils += res.nil || (ta != ORA_bit && (p.nil || q.nil));
+		store(l.t, bn->base, k, &res);
+	}
+	bn->sorted = bn->revsorted = n <= 1 || nils == n;
+	bn->key = n <= 1;
+	bn->nil = nils != 0;
+	bn->nonil = nils == 0;
+	return bn;
+}
+
+/* BATcalcifthenelse and its constant forms (b1 / b2 NULL: c1 / c2 of type
+ * ct); a void column yields its sequence at the row (gdk_calc.c:4550-4561) */
+ora_bat *
+ora_calcifthenelse(const ora_bat *b, const ora_bat *b1, const void *c1, const ora_bat *b2, const void *c2, int ct)
+{
+	const int t1 = b1 ? b1->type : ct, t2 = b2 ? b2->type : ct;
+	const int a1 = t1 == ORA_void ? ORA_oid : t1, a2 = t2 == ORA_void ? ORA_oid : t2;
+	if ((b1 && b1->count != b->count) || (b2 && b2->count != b->count)) {
+		ora_seterr("BATcalcifthenelse: BATs have different lengths.\n");
+		return NULL;
+	}
+	if (b->type != ORA_bit || a1 != a2) {
+		ora_seterr("\"then\" and \"else\" BATs have different types.\n");
+		return NULL;
+	}
+	const uint64_t n = b->count;
+	ora_bat *bn = ora_new(a1, n, b->hseqbase);
+	if (bn == NULL)
+		return NULL;
+	const int w = ora_width(a1);
+	for (uint64_t i = 0; i < n; i++) {
+		const int8_t c = ((const int8_t *) b->base)[i];
+		const bool take1 = c != 0 && c != INT8_MIN;
+		const ora_bat *x = take1 ? b1 : b2;
+		const void *cv = take1 ? c1 : c2;
+		char *dst = (char *) bn->base + i * w;
+		if (x && x->type == ORA_void) {
+			const ora_oid v = x->tseqbase + i;
+			memcpy(dst, &v, 8);
+		} else if (x) {
+			memcpy(dst, (const char *) x->base + i * w, w);
+		} else {
+			memcpy(dst, cv, w);
+		}
+	}
+	const bool nonil1 = b1 ? b1->nonil : !cst_is_nil(ct, c1), nonil2 = b2 ? b2->nonil : !cst_is_nil(ct, c2);
+	bn->sorted = bn->revsorted = bn->key = n <= 1;
+	bn->nil = 0;
+	bn->nonil = nonil1 && nonil2;
+	return bn;
+}

@@ -91,6 +91,14 @@ def lib():
         L.ora_convert.restype = P
         L.ora_convert.argtypes = [P, P, C.c_int, C.c_int, C.c_int, C.c_int]
         L.ora_calcnot.restype = P
+        L.ora_calcunary.restype = P
+        L.ora_calcunary.argtypes = [C.c_int, P, P]
+        L.ora_calcminmax.restype = P
+        L.ora_calcminmax.argtypes = [C.c_int, P, P, C.c_void_p, C.c_int, P, P]
+        L.ora_calcbits.restype = P
+        L.ora_calcbits.argtypes = [C.c_int, C.c_char_p, P, C.c_void_p, C.c_int, P, C.c_void_p, C.c_int, P, P]
+        L.ora_calcifthenelse.restype = P
+        L.ora_calcifthenelse.argtypes = [P, P, C.c_void_p, P, C.c_void_p, C.c_int]
         L.ora_calcnot.argtypes = [P, P]
         L.ora_calcdivmod.restype = P
         L.ora_calcdivmod.argtypes = [C.c_char, P, C.c_void_p, C.c_int, P, C.c_void_p, C.c_int, P, P, C.c_int]
@@ -358,6 +366,34 @@ def BATcalccmp(op, b1, b2, s1=None, s2=None, c1=None, t1=0, c2=None, t2=0, nil_m
     keep = []
     return _ret(lib().ora_calccmp(CMP_OPS[op], _pp(b1), _valptr(t1, c1, keep), t1, _pp(b2),
                                   _valptr(t2, c2, keep), t2, _pp(s1), _pp(s2), nil_matches))
+
+
+XOPS = {"negate": 0, "absolute": 1, "iszero": 2, "sign": 3, "isnil": 4, "isnotnil": 5, "min": 6, "max": 7,
+        "min_no_nil": 8, "max_no_nil": 9, "and": 10, "or": 11, "xor": 12, "lsh": 13, "rsh": 14}
+
+
+def BATcalcunary(name, b, s=None):
+    """gdk_calc.c:233-920 (ora_calcunary)"""
+    return _ret(lib().ora_calcunary(XOPS[name], b.ptr, _pp(s)))
+
+
+def BATcalcminmax(name, b1, b2=None, s1=None, s2=None, c=None, ct=0):
+    """gdk_calc.c:976-2436 min / max / _no_nil; b2 None: the constant c"""
+    keep = []
+    return _ret(lib().ora_calcminmax(XOPS[name], b1.ptr, _pp(b2), _valptr(ct, c, keep), ct, _pp(s1), _pp(s2)))
+
+
+def BATcalcbits(name, fname, b1=None, b2=None, s1=None, s2=None, c1=None, t1=0, c2=None, t2=0):
+    """gdk_calc.c:2439-3760 and / or / xor / lsh / rsh; None BAT: the constant"""
+    keep = []
+    return _ret(lib().ora_calcbits(XOPS[name], fname.encode(), _pp(b1), _valptr(t1, c1, keep), t1, _pp(b2),
+                                   _valptr(t2, c2, keep), t2, _pp(s1), _pp(s2)))
+
+
+def BATcalcifthenelse(b, b1=None, b2=None, c1=None, c2=None, ct=0):
+    """gdk_calc.c:4376 ifthenelse; None BAT: the constant of type ct"""
+    keep = []
+    return _ret(lib().ora_calcifthenelse(b.ptr, _pp(b1), _valptr(ct, c1, keep), _pp(b2), _valptr(ct, c2, keep), ct))
 
 
 def BATcalcbetween(b, lo, hi, s=None, slo=None, shi=None, clo=None, chi=None, ct=0,

@@ -354,6 +354,9 @@ def test_gpu_groupprod(gdk, ora, tn, tp):
                 gdk.BATgroupprod(B, G, None, getattr(gdk, "TYPE_" + tp), skip)
             continue
         got = gdk.BATgroupprod(B, G, None, getattr(gdk, "TYPE_" + tp), skip)
+        if tp == "hge":
+            assert list(got.values()) == [int(x) for x in want.values()]
+            continue
         w, x = np.asarray(want.values()), got.to_numpy()
         if tp in ("flt", "dbl"):
             assert np.array_equal(w.view(np.uint8), x.view(np.uint8))

@@ -20,6 +20,15 @@ jk)
 tests_*)
 	timeout -k 10 600 $T -x ${TESTS} > $O/tests.log 2>&1
 	;;
+jvar)
+	# join variants (tools/variant_build.py): opbench config3, default / variants alternating twice
+	for r in a b; do
+		timeout -k 10 200 python tools/opbench.py --only config3 > $O/default_$r.json 2> $O/default_$r.err
+		for v in $JVARS; do
+			MGDK_LIB=$PWD/tools/variants/libmgdk_$v.so timeout -k 10 200 python tools/opbench.py --only config3 > $O/${v}_$r.json 2> $O/${v}_$r.err
+		done
+	done
+	;;
 bench)
 	timeout -k 10 420 python bench.py > $O/bench.json 2> $O/bench.err
 	;;
