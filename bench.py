@@ -686,8 +686,12 @@ def leg_sort_group(cx, parity, n=100_000_000, ngroups=1000):
     res = {}
     a = r.integers(-(2**31) + 1, 2**31 - 1, n, dtype=np.int64).astype(np.int32)
     b = gdk.BAT.from_numpy(gdk.TYPE_int, a, sorted_=False, revsorted=False, key=False, nonil=True)
+    # a sort that returns the order leaves it with b as b's order index (as
+    # the reference's BATsort does, gdk_batop.c:2717-2765) and the next sort
+    # of b would answer from it (:2510-2568): each step drops it first
     out = gdk.BATsort(b)
     del out
+    gdk.OIDXdestroy(b)
     cx.barrier()
     gdk.prof_reset()
     gdk.prof_enable(True)
@@ -696,6 +700,7 @@ def leg_sort_group(cx, parity, n=100_000_000, ngroups=1000):
     for _ in range(steps):
         out = gdk.BATsort(b)
         del out
+        gdk.OIDXdestroy(b)
     cx.barrier()
     wall = (time.perf_counter() - t) / steps
     kms, kn = gdk.prof_get("sort")

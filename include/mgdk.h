@@ -69,6 +69,15 @@ typedef struct mgdk_bat {
 
 /* ---- runtime ---------------------------------------------------------- */
 int mgdk_init(int device);                       /* select HIP device */
+/* Order-dependent floating-point folds (Welford moments, the running mean of
+ * a flt/dbl average, a running flt/dbl SUM) are replayed in the reference's
+ * order, bit for bit, one lane per group or partition.  A single group or
+ * partition of at least `rows` rows (default 2^20; MGDK_BUN_NONE: never)
+ * takes the parallel form instead -- blocked folds combined pairwise (Chan
+ * et al. for the moments) -- whose results differ from the sequential ones
+ * by rounding only, within the bounds DESIGN.md states (a few n ulp).
+ * Process-wide; returns the previous value. */
+mgdk_BUN mgdk_set_fp_parallel_min(mgdk_BUN rows);
 const char *mgdk_GDKerrbuf(void);                /* gdk.h:1947 GDKerrbuf */
 void mgdk_GDKclrerr(void);
 int mgdk_sync(void);                             /* drain calling thread's stream */
@@ -391,6 +400,18 @@ bool mgdk_BATordered_rev(mgdk_bat *b);
 /* ---- sort (gdk/gdk.h:1526; gdk/gdk_batop.c:2342) ---------------------- */
 int mgdk_BATsort(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups,
 		 mgdk_bat *b, mgdk_bat *o, mgdk_bat *g, bool reverse, bool nilslast, bool stable);
+/* order index (gdk/gdk.h:1590-1592; gdk_orderidx.c:184 BATorderidx, :74
+ * BATcheckorderidx, :534 OIDXdestroy): the oids of b in sorted order kept
+ * with b (stable: ties in oid order).  As in the reference, BATsort uses it
+ * (unstable sorts, and stable ones when it was built stable) and builds one
+ * when it returns an order of a column that is not a view; BATrangejoin
+ * probes an unsorted l through it (right-major pairs, the index's order per
+ * right candidate); a written tail drops it.  mgdk_BATorderidx_get: a copy
+ * of the index as an oid BAT (NULL without an error when b has none) */
+int mgdk_BATorderidx(mgdk_bat *b, bool stable);
+bool mgdk_BATcheckorderidx(mgdk_bat *b);
+void mgdk_OIDXdestroy(mgdk_bat *b);
+mgdk_bat *mgdk_BATorderidx_get(mgdk_bat *b, bool *stable);
 /* gdk_unique.c:30 BATunique: candidate list of the first occurrence of
  * every distinct value of b[s] */
 mgdk_bat *mgdk_BATunique(mgdk_bat *b, mgdk_bat *s);

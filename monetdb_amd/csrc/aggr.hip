@@ -1786,6 +1786,83 @@ k_favg_replay(const T *vals, oid off, const uint32_t *perm, const uint64_t *star
 	}
 }
 
+// The parallel form of one large group (fp_parallel_min): block b runs the
+// same recurrence over the rows l, l + 256, ... of its tile per lane, then
+// the lanes and blocks are merged in order, (a, c) + (b, d) -> a + (b - a) *
+// (d / (c + d)): the weighted mean of the partial means.  Only the rounding
+// differs from the sequential fold (DESIGN.md states the bound).
+struct FAvg {
+	double a;
+	double c;
+	int nil;
+};
+
+__device__ __forceinline__ FAvg
+favg_comb(const FAvg &x, const FAvg &y)
+{
+	FAvg r;
+	r.nil = x.nil | y.nil;
+	if (x.c == 0) {
+		r.a = y.a;
+		r.c = y.c;
+	} else if (y.c == 0) {
+		r.a = x.a;
+		r.c = x.c;
+	} else {
+		r.c = x.c + y.c;
+		r.a = x.a + (y.a - x.a) * (y.c / r.c);
+	}
+	return r;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void
+k_favg_par(const T *vals, oid off, const oid *gids, oid gseq, oid gmin, BUN n, BUN tile, bool skip_nils, FAvg *part)
+{
+	__shared__ FAvg lds[256];
+	const BUN b0 = (BUN) blockIdx.x * tile, b1 = min(n, b0 + tile);
+	FAvg s{0, 0, 0};
+	long long c = 0;
+	for (BUN r = b0 + threadIdx.x; r < b1; r += 256) {
+		const oid g = gids ? gids[r] : gseq + r;
+		if (g != gmin)
+			continue;
+		const double x = (double) vals[off + r];
+		if (__builtin_isnan(x)) {
+			s.nil |= !skip_nils;
+			continue;
+		}
+		const double nn = (double) ++c;
+		if ((s.a > 0) == (x > 0))
+			s.a += (x - s.a) / nn;
+		else
+			s.a = s.a - s.a / nn + x / nn;
+	}
+	s.c = (double) c;
+	s = block_tree(s, [](const FAvg &x, const FAvg &y) { return favg_comb(x, y); }, lds);
+	if (threadIdx.x == 0)
+		part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void
+k_favg_fin(const FAvg *part, unsigned nb, double fac, double *out, long long *cnt)
+{
+	__shared__ FAvg lds[256];
+	const unsigned per = (nb + 255) / 256, p0 = threadIdx.x * per, p1 = min(nb, p0 + per);
+	FAvg s{0, 0, 0};
+	for (unsigned p = p0; p < p1; p++)
+		s = favg_comb(s, part[p]);
+	s = block_tree(s, [](const FAvg &x, const FAvg &y) { return favg_comb(x, y); }, lds);
+	if (threadIdx.x != 0)
+		return;
+	if (s.nil || s.c == 0) {
+		out[0] = __builtin_nan("");
+		cnt[0] = 0;
+	} else {
+		out[0] = fac != 1.0 ? s.a / fac : s.a;
+		cnt[0] = (long long) s.c;
+	}
+}
 
 // BATgroupavg3combine terms: t = avg * cnt + rem (the row's exact total),
 // c = cnt; both nil where avg is nil.  flags[0]: |avg * cnt| beyond 2^126
@@ -2216,7 +2293,24 @@ mgdk_BATgroupavg(mgdk_bat **bnp, mgdk_bat **cntsp, mgdk_bat *b, mgdk_bat *g, mgd
 		bool ok = group_rows(a, gr) == 0;
 		const uint32_t *perm = gr.perm;
 		const uint64_t *sp = gr.start_p;
-		if (ok) {
+		if (ok && ng == 1 && a.ci.n >= fp_parallel_min()) {
+			unsigned nb = (unsigned) min((BUN) 2048, (a.ci.n + 4095) / 4096);
+			const BUN tile = (a.ci.n + nb - 1) / nb;
+			nb = (unsigned) ((a.ci.n + tile - 1) / tile);
+			DevBuf part((size_t) nb * sizeof(FAvg));
+			ok = part.p != nullptr;
+			if (ok) {
+				if (bt == MGDK_flt)
+					hipLaunchKernelGGL((k_favg_par<float>), dim3(nb), dim3(256), 0, st, (const float *) b->theap, off,
+							   a.gids, a.gseq, a.min, a.ci.n, tile, skip_nils, part.as<FAvg>());
+				else
+					hipLaunchKernelGGL((k_favg_par<double>), dim3(nb), dim3(256), 0, st, (const double *) b->theap,
+							   off, a.gids, a.gseq, a.min, a.ci.n, tile, skip_nils, part.as<FAvg>());
+				hipLaunchKernelGGL(k_favg_fin, dim3(1), dim3(256), 0, st, part.as<FAvg>(), nb, fac,
+						   (double *) bn->theap, (long long *) cn->theap);
+				ok = sync();
+			}
+		} else if (ok) {
 			const dim3 grid((unsigned) ((ng + 63) / 64)), blk(64);
 			if (bt == MGDK_flt)
 				hipLaunchKernelGGL((k_favg_replay<float>), grid, blk, 0, st, (const float *) b->theap, off, perm,

@@ -1397,6 +1397,226 @@ k_fsum_tree_query(const T1 *b, Starts part, const uint32_t *pidx, AvgTree t, con
 		publish_or(flags, fl);
 }
 
+// ---- the parallel form of frames 3 / 4 over one partition ----------------
+// (fp_parallel_min): the running sum as a blocked scan.  Positions q are
+// rows in fold order (frame 3: q = row; frame 4: q = n - 1 - row); a
+// position ends its peer run where the replay writes (frame 3: o[row + 1]
+// or the last row; frame 4: o[row] or row 0).  Pass 1 folds each 4096-
+// position tile (16 per lane, the lanes combined in order); pass 2 scans
+// the tile totals; pass 3 writes every position's running sum; pass 4 gives
+// every position the sum at the end of its run (end positions are never
+// rewritten, so it reads them in place).  FSum::fold keeps the replay's
+// overflow test and nil rule; only the rounding differs (DESIGN.md states
+// the bound).
+constexpr unsigned RS_PER = 16, RS_TILE = 256 * RS_PER;
+
+__device__ __forceinline__ BUN
+rs_row(BUN q, BUN n, bool fwd)
+{
+	return fwd ? q : n - 1 - q;
+}
+
+__device__ __forceinline__ bool
+rs_end(const int8_t *o, BUN q, BUN n, bool fwd)
+{
+	if (fwd)
+		return q + 1 == n || o[q + 1];
+	const BUN j = n - 1 - q;
+	return j == 0 || o[j];
+}
+
+template <typename T2>
+__device__ __forceinline__ FSum<T2>
+rs_comb(FSum<T2> a, const FSum<T2> &b, uint32_t &fl)
+{
+	if (!a.fold(b))
+		fl |= 2;
+	return a;
+}
+
+template <typename T1, typename T2>
+__global__ __launch_bounds__(256) void
+k_rs_tile(const T1 *b, const int8_t *o, BUN n, bool fwd, FSum<T2> *tot, BUN *fend, uint32_t *flags)
+{
+	__shared__ FSum<T2> lds[256];
+	__shared__ BUN sm[256];
+	const BUN q0 = (BUN) blockIdx.x * RS_TILE + threadIdx.x * RS_PER;
+	FSum<T2> acc;
+	acc.zero();
+	BUN fe = ~(BUN) 0;
+	uint32_t fl = 0;
+	for (unsigned k = 0; k < RS_PER; k++) {
+		const BUN q = q0 + k;
+		if (q >= n)
+			break;
+		FSum<T2> x;
+		x.leaf(b, rs_row(q, n, fwd));
+		acc = rs_comb(acc, x, fl);
+		if (fe == ~(BUN) 0 && rs_end(o, q, n, fwd))
+			fe = q;
+	}
+	acc = block_tree(acc, [&fl](const FSum<T2> &x, const FSum<T2> &y) { return rs_comb(x, y, fl); }, lds);
+	fe = block_tree(fe, [](BUN x, BUN y) { return x < y ? x : y; }, sm);
+	if (threadIdx.x == 0) {
+		tot[blockIdx.x] = acc;
+		fend[blockIdx.x] = fe;
+	}
+	if (fl)
+		atomicOr(flags, fl);
+}
+
+// one block: pre[t] = the fold of the tiles before t (in order); nxt[t] =
+// the first run end at or after tile t + 1's first position
+template <typename T2>
+__global__ __launch_bounds__(1024) void
+k_rs_tiles(const FSum<T2> *tot, const BUN *fend, BUN nt, FSum<T2> *pre, BUN *nxt, uint32_t *flags)
+{
+	__shared__ FSum<T2> ls[1024];
+	__shared__ BUN lm[1024];
+	const BUN per = (nt + 1023) / 1024, t0 = min(nt, (BUN) threadIdx.x * per), t1 = min(nt, t0 + per);
+	uint32_t fl = 0;
+	FSum<T2> acc;
+	acc.zero();
+	BUN mn = ~(BUN) 0;
+	for (BUN t = t0; t < t1; t++) {
+		acc = rs_comb(acc, tot[t], fl);
+		mn = min(mn, fend[t]);
+	}
+	// exclusive scan of the thread folds (in order) and suffix minimum
+	ls[threadIdx.x] = acc;
+	lm[threadIdx.x] = mn;
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		FSum<T2> run;
+		run.zero();
+		for (unsigned k = 0; k < 1024; k++) {
+			const FSum<T2> x = ls[k];
+			ls[k] = run;
+			run = rs_comb(run, x, fl);
+		}
+		BUN m = ~(BUN) 0;
+		for (int k = 1023; k >= 0; k--) {
+			const BUN x = lm[k];
+			lm[k] = m;          // minimum over the threads after k
+			m = min(m, x);
+		}
+	}
+	__syncthreads();
+	FSum<T2> run = ls[threadIdx.x];
+	for (BUN t = t0; t < t1; t++) {
+		pre[t] = run;
+		run = rs_comb(run, tot[t], fl);
+	}
+	BUN m = lm[threadIdx.x];
+	for (BUN t = t1; t-- > t0;) {
+		nxt[t] = m;
+		m = min(m, fend[t]);
+	}
+	if (fl)
+		atomicOr(flags, fl);
+}
+
+// pass 3 (write the running sums) and pass 4 (spread the run ends' sums)
+template <typename T1, typename T2>
+__global__ __launch_bounds__(256) void
+k_rs_write(const T1 *b, const int8_t *o, BUN n, bool fwd, const FSum<T2> *pre, const BUN *nxt, int pass, T2 *out,
+	   uint32_t *flags)
+{
+	__shared__ FSum<T2> ls[256];
+	__shared__ BUN lm[256];
+	const BUN q0 = (BUN) blockIdx.x * RS_TILE + threadIdx.x * RS_PER;
+	uint32_t fl = 0;
+	if (pass == 0) {
+		FSum<T2> acc;
+		acc.zero();
+		for (unsigned k = 0; k < RS_PER && q0 + k < n; k++) {
+			FSum<T2> x;
+			x.leaf(b, rs_row(q0 + k, n, fwd));
+			acc = rs_comb(acc, x, fl);
+		}
+		// exclusive scan of the lane folds in lane order (thread 0 walks them)
+		ls[threadIdx.x] = acc;
+		__syncthreads();
+		if (threadIdx.x == 0) {
+			FSum<T2> run = pre[blockIdx.x];
+			for (unsigned k = 0; k < 256; k++) {
+				const FSum<T2> x = ls[k];
+				ls[k] = run;
+				run = rs_comb(run, x, fl);
+			}
+		}
+		__syncthreads();
+		FSum<T2> run = ls[threadIdx.x];
+		for (unsigned k = 0; k < RS_PER && q0 + k < n; k++) {
+			const BUN q = q0 + k;
+			FSum<T2> x;
+			x.leaf(b, rs_row(q, n, fwd));
+			run = rs_comb(run, x, fl);
+			out[rs_row(q, n, fwd)] = run.nil ? (T2) __builtin_nan("") : run.v;
+			if (run.nil && rs_end(o, q, n, fwd))
+				fl |= 1;
+		}
+	} else {
+		// the first run end at or after each position: inside the lane,
+		// then the later lanes of the tile, then the later tiles
+		BUN fe = ~(BUN) 0;
+		for (unsigned k = 0; k < RS_PER && q0 + k < n; k++)
+			if (rs_end(o, q0 + k, n, fwd)) {
+				fe = q0 + k;
+				break;
+			}
+		lm[threadIdx.x] = fe;
+		__syncthreads();
+		if (threadIdx.x == 0) {
+			BUN m = nxt[blockIdx.x];
+			for (int k = 255; k >= 0; k--) {
+				const BUN x = lm[k];
+				lm[k] = m;      // first end after lane k
+				m = min(m, x);
+			}
+		}
+		__syncthreads();
+		BUN after = lm[threadIdx.x];
+		BUN endq = after;
+		for (int k = (int) RS_PER - 1; k >= 0; k--) {
+			const BUN q = q0 + k;
+			if (q >= n)
+				continue;
+			if (rs_end(o, q, n, fwd)) {
+				endq = q;
+				continue;
+			}
+			out[rs_row(q, n, fwd)] = out[rs_row(endq, n, fwd)];
+		}
+	}
+	if (fl)
+		atomicOr(flags, fl);
+}
+
+template <typename T1, typename T2>
+int
+run_fsum_par(const T1 *bv, const int8_t *o, BUN n, bool fwd, T2 *out, uint32_t *flags)
+{
+	hipStream_t st = stream();
+	const BUN nt = (n + RS_TILE - 1) / RS_TILE;
+	DevBuf tot(nt * sizeof(FSum<T2>)), pre(nt * sizeof(FSum<T2>)), fend(nt * sizeof(BUN)), nxt(nt * sizeof(BUN));
+	if (!tot.p || !pre.p || !fend.p || !nxt.p)
+		return -1;
+	if (nt > 0xffffffffull) {
+		seterr("42000!GDKanalyticalsum: too many rows on the device path\n");
+		return -1;
+	}
+	hipLaunchKernelGGL((k_rs_tile<T1, T2>), dim3((unsigned) nt), dim3(256), 0, st, bv, o, n, fwd,
+			   tot.as<FSum<T2>>(), fend.as<BUN>(), flags);
+	hipLaunchKernelGGL((k_rs_tiles<T2>), dim3(1), dim3(1024), 0, st, tot.as<FSum<T2>>(), fend.as<BUN>(), nt,
+			   pre.as<FSum<T2>>(), nxt.as<BUN>(), flags);
+	hipLaunchKernelGGL((k_rs_write<T1, T2>), dim3((unsigned) nt), dim3(256), 0, st, bv, o, n, fwd,
+			   pre.as<FSum<T2>>(), nxt.as<BUN>(), 0, out, flags);
+	hipLaunchKernelGGL((k_rs_write<T1, T2>), dim3((unsigned) nt), dim3(256), 0, st, bv, o, n, fwd,
+			   pre.as<FSum<T2>>(), nxt.as<BUN>(), 1, out, flags);
+	return sync() ? 0 : -1;
+}
+
 template <typename T1, typename T2>
 int
 run_fsum(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_bat *e, int frame_type)
@@ -1418,7 +1638,10 @@ run_fsum(mgdk_bat *r, mgdk_bat *p, mgdk_bat *o, mgdk_bat *b, mgdk_bat *s, mgdk_b
 		Starts part;
 		if (make_starts(p ? (const int8_t *) p->theap : nullptr, n, part, &Sp) < 0)
 			goto out;
-		if (frame_type == 3 || frame_type == 4) {
+		if ((frame_type == 3 || frame_type == 4) && part.m == 1 && n >= fp_parallel_min()) {
+			if (run_fsum_par<T1, T2>(bv, (const int8_t *) o->theap, n, frame_type == 3, out, fl.as<uint32_t>()) < 0)
+				goto out;
+		} else if (frame_type == 3 || frame_type == 4) {
 			hipLaunchKernelGGL((k_fsum_replay<T1, T2>), dim3((unsigned) ((part.m + 63) / 64)), dim3(64), 0, st, bv, part,
 					   (const int8_t *) o->theap, frame_type == 3, out, fl.as<uint32_t>());
 		} else {

@@ -873,6 +873,7 @@ mgdk_BATfirstn(mgdk_bat **topn, mgdk_bat **gids, mgdk_bat *b, mgdk_bat *s, mgdk_
 		mgdk_bat *vals = mgdk_BATproject(bn, b), *o4 = nullptr, *g5 = nullptr, *o6 = nullptr, *g7 = nullptr,
 			 *o8 = nullptr, *gp = nullptr;
 		bool ok = vals != nullptr;
+		SortInternal no_oidx;   // the reference sorts these temporaries too
 		if (ok && g) {
 			gp = mgdk_BATproject(pos, g);
 			ok = gp && mgdk_BATsort(nullptr, &o4, &g5, gp, nullptr, nullptr, false, false, false) == 0 &&

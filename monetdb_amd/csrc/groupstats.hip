@@ -396,6 +396,151 @@ group_moments(const char *fn, int kind, mgdk_bat *b1, mgdk_bat *b2, mgdk_bat *g,
 	return bn;
 }
 
+// ---- the parallel form of the whole-column moments (fp_parallel_min) ----
+// Block b folds the rows [b * tile, (b + 1) * tile) -- lane l the rows
+// l, l + 256, ... of it, each lane a Welford recurrence as AGGR_STDEV /
+// AGGR_COVARIANCE / AGGR_CORRELATION step it -- then the lanes and the
+// blocks are combined in order by the pairwise update of Chan, Golub and
+// LeVeque (n = na + nb, d = mean_b - mean_a: mean = mean_a + d nb / n,
+// M2 = M2a + M2b + d^2 na nb / n, the co-moments alike).  Only the rounding
+// differs from the sequential fold (DESIGN.md states the bound).
+struct MomState {
+	double n, mean1, mean2, m2, down1, down2;   // m2: the co-moment (up) for ST_COR
+};
+
+template <int KIND>
+__device__ __forceinline__ MomState
+mom_comb(const MomState &a, const MomState &b)
+{
+	if (a.n == 0)
+		return b;
+	if (b.n == 0)
+		return a;
+	MomState r;
+	r.n = a.n + b.n;
+	const double f = b.n / r.n, d1 = b.mean1 - a.mean1, w = a.n * f;
+	r.mean1 = a.mean1 + d1 * f;
+	r.mean2 = r.down1 = r.down2 = 0;
+	if (KIND == ST_VAR) {
+		r.m2 = a.m2 + b.m2 + d1 * d1 * w;
+	} else {
+		const double d2 = b.mean2 - a.mean2;
+		r.mean2 = a.mean2 + d2 * f;
+		r.m2 = a.m2 + b.m2 + d1 * d2 * w;
+		if (KIND == ST_COR) {
+			r.down1 = a.down1 + b.down1 + d1 * d1 * w;
+			r.down2 = a.down2 + b.down2 + d2 * d2 * w;
+		}
+	}
+	return r;
+}
+
+template <int KIND>
+__device__ __forceinline__ bool
+mom_inf(const MomState &s)
+{
+	return __builtin_isinf(s.m2) || (KIND == ST_COR && (__builtin_isinf(s.down1) || __builtin_isinf(s.down2)));
+}
+
+template <typename T, int KIND>
+__global__ __launch_bounds__(256) void
+k_mom_par(const T *v1, const T *v2, BUN n, BUN tile, MomState *part, uint32_t *flags)
+{
+	__shared__ MomState lds[256];
+	const BUN b0 = (BUN) blockIdx.x * tile, b1 = min(n, b0 + tile);
+	MomState s{0, 0, 0, 0, 0, 0};
+	unsigned long long cnt = 0;
+	for (BUN r = b0 + threadIdx.x; r < b1; r += 256) {
+		const T x = v1[r];
+		T y{};
+		if (KIND != ST_VAR)
+			y = v2[r];
+		if (is_nil(x) || (KIND != ST_VAR && is_nil(y)))
+			continue;
+		const double nn = (double) ++cnt;
+		const double xd = to_dbl(x);
+		const double delta1 = xd - s.mean1;
+		s.mean1 += delta1 / nn;
+		if (KIND == ST_VAR) {
+			s.m2 += delta1 * (xd - s.mean1);
+		} else {
+			const double yd = to_dbl(y);
+			const double delta2 = yd - s.mean2;
+			s.mean2 += delta2 / nn;
+			if (KIND == ST_COV) {
+				s.m2 += delta1 * (yd - s.mean2);
+			} else {
+				const double aux = yd - s.mean2;
+				s.m2 += delta1 * aux;
+				s.down1 += delta1 * (xd - s.mean1);
+				s.down2 += delta2 * aux;
+			}
+		}
+	}
+	s.n = (double) cnt;
+	const bool inf = mom_inf<KIND>(s);
+	if (inf)
+		atomicOr(flags, 1u);
+	s = block_tree(s, [](const MomState &a, const MomState &b) { return mom_comb<KIND>(a, b); }, lds);
+	if (threadIdx.x == 0)
+		part[blockIdx.x] = s;
+}
+
+// the blocks' states combined in block order (thread t: a contiguous run of
+// them, then the tree) and the result step of calcvariance /
+// calccovariance / BATcalccorrelation
+template <int KIND>
+__global__ __launch_bounds__(256) void
+k_mom_fin(const MomState *part, unsigned nb, bool issample, bool variance, double *res, double *avg,
+	  uint32_t *flags)
+{
+	__shared__ MomState lds[256];
+	const unsigned per = (nb + 255) / 256, p0 = threadIdx.x * per, p1 = min(nb, p0 + per);
+	MomState s{0, 0, 0, 0, 0, 0};
+	for (unsigned p = p0; p < p1; p++)
+		s = mom_comb<KIND>(s, part[p]);
+	s = block_tree(s, [](const MomState &a, const MomState &b) { return mom_comb<KIND>(a, b); }, lds);
+	if (threadIdx.x != 0)
+		return;
+	const double nil = __builtin_nan("");
+	const unsigned long long cnt = (unsigned long long) s.n;
+	double r, mean1 = s.mean1;
+	if (mom_inf<KIND>(s) || (*flags & 1)) {
+		r = nil;
+		atomicOr(flags, 1u);
+	} else if (KIND == ST_COR) {
+		const double nn = s.n;
+		r = (cnt != 0 && s.down1 != 0 && s.down2 != 0) ? (s.m2 / nn) / (sqrt(s.down1 / nn) * sqrt(s.down2 / nn)) : nil;
+	} else if (cnt <= (issample ? 1ull : 0ull)) {
+		r = nil;
+		mean1 = nil;
+	} else {
+		r = s.m2 / (double) (cnt - (issample ? 1 : 0));
+		if (KIND == ST_VAR && !variance)
+			r = sqrt(r);
+	}
+	*res = r;
+	*avg = cnt ? mean1 : nil;
+}
+
+template <int KIND>
+void
+launch_mom_par(int tt, const void *v1, const void *v2, BUN n, MomState *part, unsigned nb, BUN tile,
+	       uint32_t *flags)
+{
+	const dim3 grid(nb), blk(256);
+	hipStream_t st = stream();
+	switch (tt) {
+	case MGDK_bte: hipLaunchKernelGGL((k_mom_par<int8_t, KIND>), grid, blk, 0, st, (const int8_t *) v1, (const int8_t *) v2, n, tile, part, flags); break;
+	case MGDK_sht: hipLaunchKernelGGL((k_mom_par<int16_t, KIND>), grid, blk, 0, st, (const int16_t *) v1, (const int16_t *) v2, n, tile, part, flags); break;
+	case MGDK_int: hipLaunchKernelGGL((k_mom_par<int32_t, KIND>), grid, blk, 0, st, (const int32_t *) v1, (const int32_t *) v2, n, tile, part, flags); break;
+	case MGDK_lng: hipLaunchKernelGGL((k_mom_par<int64_t, KIND>), grid, blk, 0, st, (const int64_t *) v1, (const int64_t *) v2, n, tile, part, flags); break;
+	case MGDK_hge: hipLaunchKernelGGL((k_mom_par<hge, KIND>), grid, blk, 0, st, (const hge *) v1, (const hge *) v2, n, tile, part, flags); break;
+	case MGDK_flt: hipLaunchKernelGGL((k_mom_par<float, KIND>), grid, blk, 0, st, (const float *) v1, (const float *) v2, n, tile, part, flags); break;
+	default: hipLaunchKernelGGL((k_mom_par<double, KIND>), grid, blk, 0, st, (const double *) v1, (const double *) v2, n, tile, part, flags); break;
+	}
+}
+
 // calcvariance / calccovariance / BATcalccorrelation over the whole column
 double
 calc_moments(int kind, double *avgp, mgdk_bat *b1, mgdk_bat *b2, bool issample, bool variance)
@@ -430,7 +575,33 @@ calc_moments(int kind, double *avgp, mgdk_bat *b1, mgdk_bat *b2, bool issample, 
 	m.res = out.as<double>();
 	m.avg = out.as<double>() + 1;
 	m.flags = fl.as<uint32_t>();
-	if (kind == ST_VAR)
+	const BUN n = b1->count;
+	if (n >= fp_parallel_min() && n > 0) {
+		// the parallel form: ~16 rows per lane, at most 2048 blocks
+		unsigned nb = (unsigned) min((BUN) 2048, (n + 4095) / 4096);
+		const BUN tile = (n + nb - 1) / nb;
+		nb = (unsigned) ((n + tile - 1) / tile);
+		DevBuf part((size_t) nb * sizeof(MomState));
+		if (!part.p)
+			return nil;
+		MomState *pp = part.as<MomState>();
+		const void *p2 = kind != ST_VAR ? b2->theap : nullptr;
+		if (kind == ST_VAR) {
+			launch_mom_par<ST_VAR>(b1->ttype, b1->theap, p2, n, pp, nb, tile, m.flags);
+			hipLaunchKernelGGL((k_mom_fin<ST_VAR>), dim3(1), dim3(256), 0, stream(), pp, nb, issample, variance,
+					   m.res, m.avg, m.flags);
+		} else if (kind == ST_COV) {
+			launch_mom_par<ST_COV>(b1->ttype, b1->theap, p2, n, pp, nb, tile, m.flags);
+			hipLaunchKernelGGL((k_mom_fin<ST_COV>), dim3(1), dim3(256), 0, stream(), pp, nb, issample, variance,
+					   m.res, m.avg, m.flags);
+		} else {
+			launch_mom_par<ST_COR>(b1->ttype, b1->theap, p2, n, pp, nb, tile, m.flags);
+			hipLaunchKernelGGL((k_mom_fin<ST_COR>), dim3(1), dim3(256), 0, stream(), pp, nb, issample, variance,
+					   m.res, m.avg, m.flags);
+		}
+		if (!sync())
+			return nil;
+	} else if (kind == ST_VAR)
 		launch_moments<ST_VAR>(b1->ttype, b1->theap, nullptr, m);
 	else if (kind == ST_COV)
 		launch_moments<ST_COV>(b1->ttype, b1->theap, b2->theap, m);
@@ -715,8 +886,13 @@ group_quantile(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, doubl
 		fx.keep(go);
 		if (mgdk_BATsort(&sv, nullptr, nullptr, bv, go, gs, false, false, false) != 0)
 			return nullptr;
-	} else if (mgdk_BATsort(&sv, nullptr, nullptr, bv, nullptr, nullptr, false, false, false) != 0) {
-		return nullptr;
+	} else {
+		// with the order, as the reference asks for it (gdk_aggr.c:4121): a
+		// column that is not a view keeps it as its order index
+		mgdk_bat *so = nullptr;
+		if (mgdk_BATsort(&sv, &so, nullptr, bv, nullptr, nullptr, false, false, false) != 0)
+			return nullptr;
+		mgdk_BBPunfix(so);
 	}
 	fx.keep(sv);
 	// runs of equal group ids

@@ -1266,6 +1266,78 @@ k_rj_sorted_emit(JSide L, JSide RL, const uint32_t *rg, const uint64_t *off, oid
 	}
 }
 
+// l unsorted with an order index (gdk_join.c:5137-5273): the bounds are
+// found on the index (ORDERfndfirst / ORDERfndlast, gdk_search.c:423) and
+// the index entries in between that are left candidates are emitted in the
+// index's order.  The reference searches the index with offset 0
+// (vals[ord[i]]), right only for hseqbase 0; positions here are ord[i] -
+// hseqbase.
+__device__ __forceinline__ BUN
+rj_ofnd(const JSide &l, int fk, const oid *ord, BUN cnt, int64_t v, bool last)
+{
+	BUN a = 0, b = cnt;
+	while (a < b) {
+		const BUN m = a + (b - a) / 2;
+		const int64_t x = th_key(l, fk, ord[m] - l.hseq);
+		if (last ? x <= v : x < v)
+			a = m + 1;
+		else
+			b = m;
+	}
+	return a;
+}
+
+__device__ __forceinline__ bool
+js_contains(const JSide &c, oid o)
+{
+	if (c.dense)
+		return o >= c.seq && o - c.seq < c.n;
+	BUN a = 0, b = c.n;
+	while (a < b) {
+		const BUN m = a + (b - a) / 2;
+		if (c.oids[m] < o)
+			a = m + 1;
+		else
+			b = m;
+	}
+	return a < c.n && c.oids[a] == o;
+}
+
+// pass 0: per right candidate the index range and the number of left
+// candidates in it; pass 1: write them
+__global__ __launch_bounds__(256) void
+k_rj_oidx(JSide L, BUN lcnt, const oid *ord, JSide RL, JSide RH, int fk, bool linc, bool hinc, int pass,
+	  uint32_t *rg, uint32_t *cnt, const uint64_t *off, oid *r1, oid *r2)
+{
+	for (BUN j = (BUN) blockIdx.x * blockDim.x + threadIdx.x; j < RL.n; j += (BUN) gridDim.x * blockDim.x) {
+		const oid ro = js_oid(RL, j);
+		if (pass) {
+			BUN o = off[j];
+			for (BUN q = rg[2 * j]; q < rg[2 * j + 1]; q++) {
+				const oid lo = ord[q];
+				if (js_contains(L, lo)) {
+					r1[o] = lo;
+					r2[o] = ro;
+					o++;
+				}
+			}
+			continue;
+		}
+		const int64_t vlo = th_key(RL, fk, ro - RL.hseq), vhi = th_key(RH, fk, ro - RH.hseq);
+		BUN low = 0, high = 0;
+		uint32_t c = 0;
+		if (vlo != INT64_MIN && vhi != INT64_MIN) {
+			low = rj_ofnd(L, fk, ord, lcnt, vlo, !linc);
+			high = rj_ofnd(L, fk, ord, lcnt, vhi, hinc);
+			for (BUN q = low; q < high; q++)
+				c += js_contains(L, ord[q]);
+		}
+		rg[2 * j] = (uint32_t) low;
+		rg[2 * j + 1] = (uint32_t) (high > low ? high : low);
+		cnt[j] = c;
+	}
+}
+
 // BETWEEN (gdk_join.c:5040-5064): 1 true, 0 false, -1 nil
 __device__ __forceinline__ int
 rj_between3(int64_t v, int64_t lo, bool linc, int64_t hi, bool hinc)
@@ -1574,7 +1646,36 @@ mgdk_BATrangejoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *rl, mgd
 			asc = mgdk_BATordered(lb);
 			desc = mgdk_BATordered_rev(lb);
 		}
-		if (asc || desc) {
+		// an unsorted l's order index (gdk_join.c:5137-5156)
+		size_t ooff = 0;
+		Heap *oh = !anti && !symmetric && !asc && !desc && lb == l && lb->count < 0xffffffffull ?
+			oidx_get(l, nullptr, OIDX_OWN, &ooff) : nullptr;
+		if (oh) {
+			DevBuf rg(RL.n * 8 + 8), cnt(RL.n * 4 + 4), off(RL.n * 8 + 8);
+			const dim3 grd(grid_for(RL.n, 256 * 4, 8192));
+			const oid *ord = (const oid *) ((const char *) oh->base + ooff);
+			bool okk = rg.p && cnt.p && off.p;
+			if (okk) {
+				hipLaunchKernelGGL(k_rj_oidx, grd, dim3(256), 0, st, L, lb->count, ord, RL, RH, fk, linc, hinc, 0,
+						   rg.as<uint32_t>(), cnt.as<uint32_t>(), (const uint64_t *) nullptr, (oid *) nullptr,
+						   (oid *) nullptr);
+				okk = exclusive_scan(cnt.as<uint32_t>(), off.as<uint64_t>(), RL.n, &tot) == 0 && alloc(tot);
+			}
+			if (okk && tot)
+				hipLaunchKernelGGL(k_rj_oidx, grd, dim3(256), 0, st, L, lb->count, ord, RL, RH, fk, linc, hinc, 1,
+						   rg.as<uint32_t>(), cnt.as<uint32_t>(), off.as<uint64_t>(), (oid *) a->theap,
+						   (oid *) b->theap);
+			// the index stays referenced until the stream has drained
+			const bool drained = sync_data();
+			heap_decref(oh);
+			if (!okk || !drained) {
+				if (okk) {
+					mgdk_BBPunfix(a);
+					mgdk_BBPunfix(b);
+				}
+				return -1;
+			}
+		} else if (asc || desc) {
 			DevBuf rg(RL.n * 8 + 8), cnt(RL.n * 4 + 4), off(RL.n * 8 + 8);
 			if (!rg.p || !cnt.p || !off.p)
 				return -1;

@@ -71,6 +71,19 @@ struct Priv {
 	int64_t smap_base;       // oid of slot 0
 	size_t smap_bits_off;    // byte offset of the bitmap in the heap (the prefixes are at 0)
 	oid smap_lo, smap_hi;    // first / last oid of the list
+	// the order index (gdk_orderidx.c: b->torderidx): the oids of the column
+	// in sorted order.  A view over the whole column also holds its parent's
+	// slot (BATsort uses the parent's index for it, gdk_batop.c:2473-2509),
+	// so an index the parent gets later is seen; a written tail leaves both
+	struct OidxSlot *oidx, *poidx;
+	bool view;               // a BATslice view: BATsort builds no index for it
+};
+struct OidxSlot {
+	int refs;
+	Heap *idx;               // n oids at byte offset off, or NULL (the heap
+	size_t off;              // is shared with the order BAT it came from:
+	BUN n;                   // shared heaps are never written in place)
+	bool stable;
 };
 struct SelMap {
 	const uint32_t *bits;
@@ -92,8 +105,49 @@ uint8_t *img8_new(mgdk_bat *b);     // allocate an image for b->count values
 void img8_drop(mgdk_bat *b);        // drops every accelerator of the tail (img8, smap)
 bool smap_get(const mgdk_bat *b, SelMap *m);
 void smap_set(mgdk_bat *b, Heap *h, const SelMap &m);   // takes a reference on h
+// b's order index (a reference on its heap, release with heap_decref; the
+// oids start at *off bytes into it) or NULL: its own (OIDX_OWN), that of the
+// column a whole-column view shows (OIDX_PARENT), or either (OIDX_ANY)
+enum { OIDX_OWN = 1, OIDX_PARENT = 2, OIDX_ANY = 3 };
+Heap *oidx_get(const mgdk_bat *b, bool *stable, int which, size_t *off);
+// give b the order index `order` (an oid BAT of b->count rows, whose heap
+// is shared, not copied) unless it has one of its own
+int oidx_put(mgdk_bat *b, const mgdk_bat *order, bool stable);
+// a new oid BAT over an index heap (shares it)
+mgdk_bat *oidx_bat(Heap *h, size_t off, oid hseq, BUN n);
+void oidx_share(mgdk_bat *v, const mgdk_bat *b);   // v: a view over all of b
+// while one lives on a thread, mgdk_BATsort neither uses nor builds order
+// indexes: the sorts the device path runs where the reference runs none
+// (the reference's own BATsort calls sort temporaries or are mirrored as is)
+extern thread_local int sort_internal;
+struct SortInternal {
+	SortInternal() { ++sort_internal; }
+	~SortInternal() { --sort_internal; }
+};
+bool is_view(const mgdk_bat *b);
 int basetype(int tt);                            // date->int, bit->bte
 const char *atomname(int tt);
+
+// rows from which one group / partition of an order-dependent float fold
+// takes the parallel form (mgdk_set_fp_parallel_min)
+BUN fp_parallel_min();
+
+// ordered pairwise tree over one value per thread of the block (blockDim a
+// power of two <= 1024): thread 0 returns comb(v0, v1, ..., v_{n-1}) in
+// thread order, the same association for every launch (deterministic)
+template <typename S, typename F>
+__device__ __forceinline__ S
+block_tree(S v, F comb, S *lds)
+{
+	lds[threadIdx.x] = v;
+	__syncthreads();
+	for (unsigned st = 1; st < blockDim.x; st <<= 1) {
+		if ((threadIdx.x & (2 * st - 1)) == 0)
+			lds[threadIdx.x] = comb(lds[threadIdx.x], lds[threadIdx.x + st]);
+		__syncthreads();
+	}
+	return lds[0];
+}
 
 // ---- profiling ----------------------------------------------------------
 struct ProfScope {

@@ -119,6 +119,7 @@ q1_opatatime(mgdk_bat *shipdate, mgdk_bat *rf, mgdk_bat *ls, mgdk_bat *qty, mgdk
 	// projected through the final order (the plan's leftfetchjoins)
 	{
 		mgdk_bat *sa, *oa, *ga, *sb, *ob, *gb;
+		SortInternal no_oidx;   // the plan's sorts of projected temporaries
 		if (mgdk_BATsort(&sa, &oa, &ga, krf, nullptr, nullptr, false, false, false) < 0)
 			return -1;
 		t.add(sa), t.add(oa), t.add(ga);

@@ -6,6 +6,7 @@
 //   HEAPalloc / GDKmalloc + memory accounting     gdk/gdk_heap.c:141-225, gdk/gdk_utils.c:1636,1752
 //   COLnew / BATdense / BATslice / BBPunfix       gdk/gdk_bat.c:292,298, gdk/gdk_batop.c:1825, gdk/gdk_bbp.c:3149
 //   canditer_init clipping                         gdk/gdk_cand.c:407
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <map>
@@ -467,6 +468,8 @@ img8_new(mgdk_bat *b)
 	return (uint8_t *) p->img8->base;
 }
 
+static void oidx_leave(Priv *p);
+
 void
 img8_drop(mgdk_bat *b)
 {
@@ -481,6 +484,131 @@ img8_drop(mgdk_bat *b)
 		p->smap = nullptr;
 		p->smap_n = 0;
 	}
+	if (p && (p->oidx || p->poidx)) {
+		oidx_leave(p);
+		p->view = false;   // a written view holds a tail of its own
+	}
+}
+
+// ---- order index slots (gdk_orderidx.c) -----------------------------------
+static std::mutex oidx_mu;
+
+static void
+slot_decref(OidxSlot *s)
+{
+	if (s && --s->refs == 0) {
+		heap_decref(s->idx);
+		delete s;
+	}
+}
+
+static void
+oidx_leave(Priv *p)
+{
+	std::lock_guard<std::mutex> g(oidx_mu);
+	slot_decref(p->oidx);
+	slot_decref(p->poidx);
+	p->oidx = p->poidx = nullptr;
+}
+
+Heap *
+oidx_get(const mgdk_bat *b, bool *stable, int which, size_t *off)
+{
+	const Priv *p = (const Priv *) b->priv;
+	if (p == nullptr || b->ttype == MGDK_void)
+		return nullptr;
+	std::lock_guard<std::mutex> g(oidx_mu);
+	const OidxSlot *s = (which & OIDX_OWN) && p->oidx && p->oidx->idx && p->oidx->n == b->count ? p->oidx :
+		(which & OIDX_PARENT) && p->poidx && p->poidx->idx && p->poidx->n == b->count ? p->poidx : nullptr;
+	if (s == nullptr)
+		return nullptr;
+	__atomic_add_fetch(&s->idx->refs, 1, __ATOMIC_ACQ_REL);
+	if (stable)
+		*stable = s->stable;
+	if (off)
+		*off = s->off;
+	return s->idx;
+}
+
+int
+oidx_put(mgdk_bat *b, const mgdk_bat *order, bool stable)
+{
+	Priv *p = (Priv *) b->priv;
+	Heap *h = nullptr;
+	size_t off = 0;
+	if (order->ttype == MGDK_void || ((const Priv *) order->priv)->theap == nullptr) {
+		// a dense order materialised (BATorderidx never keeps one)
+		h = heap_new(b->count * sizeof(oid) + 8);
+		if (h == nullptr)
+			return -1;
+		std::vector<oid> seq(b->count);
+		for (BUN i = 0; i < b->count; i++)
+			seq[i] = order->tseqbase + i;
+		if (b->count && !(hip_ok(hipMemcpyAsync(h->base, seq.data(), b->count * sizeof(oid), hipMemcpyHostToDevice,
+							 stream()), "orderidx copy") && sync_data())) {
+			heap_decref(h);
+			return -1;
+		}
+	} else {
+		h = ((const Priv *) order->priv)->theap;
+		off = (size_t) ((const char *) order->theap - (const char *) h->base);
+		__atomic_add_fetch(&h->refs, 1, __ATOMIC_ACQ_REL);
+	}
+	std::lock_guard<std::mutex> g(oidx_mu);
+	if (p->oidx == nullptr)
+		p->oidx = new OidxSlot{1, nullptr, 0, 0, false};
+	if (p->oidx->idx && p->oidx->n == b->count) {
+		heap_decref(h);   // it has one (another thread was first)
+		return 0;
+	}
+	heap_decref(p->oidx->idx);
+	p->oidx->idx = h;
+	p->oidx->off = off;
+	p->oidx->n = b->count;
+	p->oidx->stable = stable;
+	return 0;
+}
+
+mgdk_bat *
+oidx_bat(Heap *h, size_t off, oid hseq, BUN n)
+{
+	mgdk_bat *o = (mgdk_bat *) calloc(1, sizeof(mgdk_bat));
+	Priv *p = new Priv{};
+	o->priv = p;
+	o->ttype = MGDK_oid;
+	o->twidth = 8;
+	o->hseqbase = hseq;
+	o->tseqbase = MGDK_OID_NIL;
+	o->tminpos = o->tmaxpos = MGDK_BUN_NONE;
+	__atomic_add_fetch(&h->refs, 1, __ATOMIC_ACQ_REL);
+	p->theap = h;
+	p->toff = off;
+	o->theap = (char *) h->base + off;
+	o->count = n;
+	o->tkey = o->tnonil = 1;
+	o->tnil = 0;
+	o->tsorted = o->trevsorted = n <= 1;
+	return o;
+}
+
+bool
+is_view(const mgdk_bat *b)
+{
+	const Priv *p = (const Priv *) b->priv;
+	return p && p->view;
+}
+
+// v, a view over all of b, sees b's index (the slot is created empty when b
+// has none, so one b gets later is seen too)
+void
+oidx_share(mgdk_bat *v, const mgdk_bat *b)
+{
+	Priv *vp = (Priv *) v->priv, *bp = (Priv *) b->priv;
+	std::lock_guard<std::mutex> g(oidx_mu);
+	if (bp->oidx == nullptr)
+		bp->oidx = new OidxSlot{1, nullptr, 0, 0, false};
+	bp->oidx->refs++;
+	vp->poidx = bp->oidx;
 }
 
 bool
@@ -1021,6 +1149,9 @@ mgdk_BATslice(mgdk_bat *b, mgdk_BUN lo, mgdk_BUN hi)
 		p->tvheap = bp->tvheap;
 		__atomic_add_fetch(&p->tvheap->refs, 1, __ATOMIC_ACQ_REL);
 	}
+	p->view = true;
+	if (lo == 0 && hi == b->count && b->ttype != MGDK_void)
+		oidx_share(v, b);
 	// what is known of the parent's order holds for a slice, positions do not
 	v->tnosorted = v->tnorevsorted = 0;
 	v->tminpos = v->tmaxpos = MGDK_BUN_NONE;
@@ -1041,6 +1172,7 @@ mgdk_BBPunfix(mgdk_bat *b)
 		heap_decref(p->tvheap);
 		heap_decref(p->img8);
 		heap_decref(p->smap);
+		oidx_leave(p);
 		delete p;
 	}
 	free(b);
@@ -1385,4 +1517,21 @@ out:
 	}
 	mgdk_BBPunfix(proj);
 	return rc;
+}
+
+// ---- order-dependent float folds: where the parallel form starts ---------
+static std::atomic<uint64_t> g_fp_par_min{(uint64_t) 1 << 20};
+
+namespace mgdk {
+BUN
+fp_parallel_min()
+{
+	return (BUN) g_fp_par_min.load(std::memory_order_relaxed);
+}
+}  // namespace mgdk
+
+extern "C" mgdk_BUN
+mgdk_set_fp_parallel_min(mgdk_BUN rows)
+{
+	return (mgdk_BUN) g_fp_par_min.exchange((uint64_t) rows);
 }

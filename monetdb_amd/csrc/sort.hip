@@ -1954,6 +1954,8 @@ radix_sort_positions32(uint32_t *keys, uint32_t *vals, uint32_t *keys_alt, uint3
 	return 0;
 }
 
+thread_local int sort_internal = 0;
+
 }  // namespace mgdk
 
 static int sort_core(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b, mgdk_bat *o,
@@ -2405,6 +2407,35 @@ out:
 	return rc;
 }
 
+// BATsort through an order index (gdk_batop.c:2510-2568): the order is the
+// index (its heap shared, where the reference copies it), the sorted column
+// its projection, the groups those of the sorted column
+int
+sort_by_oidx(mgdk_bat **sn, mgdk_bat **on, mgdk_bat **gn, mgdk_bat *b, Heap *oh, size_t ooff, bool want_sorted)
+{
+	mgdk_bat *o = oidx_bat(oh, ooff, b->hseqbase, b->count);
+	o->tsorted = o->trevsorted = 0;
+	*on = o;
+	if (want_sorted || gn) {
+		mgdk_bat *s = mgdk_BATproject(o, b);
+		if (s == nullptr)
+			return -1;
+		s->tsorted = 1;
+		*sn = s;
+		if (gn) {
+			if (mgdk_BATgroup(gn, nullptr, nullptr, s, nullptr, nullptr, nullptr, nullptr) < 0)
+				return -1;
+			if (want_sorted && (*gn)->tkey)
+				s->tkey = 1;
+		}
+		if (!want_sorted) {
+			mgdk_BBPunfix(s);
+			*sn = nullptr;
+		}
+	}
+	return 0;
+}
+
 }  // namespace
 
 extern "C" int
@@ -2450,6 +2481,7 @@ mgdk_BATsort(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b
 		nilslast = reverse;  // no nils: their placement does not matter (:2415-2420)
 	ProfScope prof("BATsort");
 	mgdk_bat *sn = nullptr, *on = nullptr, *gn = nullptr;
+	bool mk_oidx = false;
 	// trivially (sub)sorted (:2422-2472)
 	if (n <= 1 || (reverse == nilslast && (reverse ? b->trevsorted : b->tsorted) && o == nullptr && g == nullptr &&
 		       (groups == nullptr || b->tkey || (reverse ? b->tsorted : b->trevsorted)))) {
@@ -2489,6 +2521,29 @@ mgdk_BATsort(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b
 				goto fail;
 		}
 		goto done;
+	}
+	// the order index (gdk_batop.c:2488-2572): a column's own, or for a view
+	// over a whole column the parent's, serves an unstable sort and a stable
+	// one when it was built stable; BATsort builds one when it hands out an
+	// order of a column that is not a view (every device BAT is transient)
+	{
+		bool ostable = false;
+		size_t ooff = 0;
+		Heap *oh = g == nullptr && !reverse && !nilslast && sort_internal == 0 ?
+			oidx_get(b, &ostable, is_view(b) ? OIDX_PARENT : OIDX_OWN, &ooff) : nullptr;
+		mk_oidx = g == nullptr && !reverse && !nilslast && order != nullptr && !is_view(b) && oh == nullptr &&
+			  sort_internal == 0;
+		if (oh && (stable && !ostable))
+			heap_decref(oh), oh = nullptr;
+		if (oh && o == nullptr) {
+			const int rc = sort_by_oidx(&sn, &on, groups ? &gn : nullptr, b, oh, ooff, sorted != nullptr);
+			heap_decref(oh);
+			if (rc < 0)
+				goto fail;
+			goto done;
+		}
+		if (oh)
+			heap_decref(oh);
 	}
 	// positions and ranks of the sorts below are 32-bit: a column of 2^32 or
 	// more rows is only sorted through the shortcuts above (a documented
@@ -2533,6 +2588,9 @@ mgdk_BATsort(mgdk_bat **sorted, mgdk_bat **order, mgdk_bat **groups, mgdk_bat *b
 				on = nullptr;
 			}
 		}
+		// the order becomes b's order index (gdk_batop.c:2717-2765)
+		if (mk_oidx && on && oidx_put(b, on, stable) < 0)
+			goto fail;
 		if (sn) {
 			// gdk_batop.c:2712-2715, 2749-2750, 2772-2776
 			sn->tsorted = single_run && !reverse && !nilslast;
@@ -2558,4 +2616,73 @@ fail:
 	mgdk_BBPunfix(on);
 	mgdk_BBPunfix(gn);
 	return -1;
+}
+
+// ---- order index (gdk/gdk_orderidx.c) --------------------------------------
+
+// BATorderidx (gdk_orderidx.c:184): the column's sort order kept with it
+extern "C" int
+mgdk_BATorderidx(mgdk_bat *b, bool stable)
+{
+	if (b->ttype == MGDK_void) {
+		seterr("No order index on void type bats\n");
+		return -1;
+	}
+	if (mgdk_BATcheckorderidx(b))
+		return 0;
+	if (b->ttype == MGDK_oid && b->tseqbase != MGDK_OID_NIL)
+		return 0;   // BATtdense
+	mgdk_bat *on = nullptr;
+	if (mgdk_BATsort(nullptr, &on, nullptr, b, nullptr, nullptr, false, false, stable) < 0)
+		return -1;
+	int rc = 0;
+	if (on->ttype == MGDK_void) {
+		// a dense order: the input was sorted (:199-208)
+		b->tsorted = 1;
+		b->tnosorted = 0;
+	} else {
+		rc = oidx_put(b, on, stable);
+	}
+	mgdk_BBPunfix(on);
+	return rc;
+}
+
+// BATcheckorderidx (gdk_orderidx.c:74)
+extern "C" bool
+mgdk_BATcheckorderidx(mgdk_bat *b)
+{
+	if (b == nullptr)
+		return false;
+	Heap *h = oidx_get(b, nullptr, OIDX_OWN, nullptr);
+	heap_decref(h);
+	return h != nullptr;
+}
+
+// OIDXdestroy (gdk_orderidx.c:534)
+extern "C" void
+mgdk_OIDXdestroy(mgdk_bat *b)
+{
+	if (b == nullptr)
+		return;
+	Priv *p = (Priv *) b->priv;
+	const bool v = p->view;
+	img8_drop(b);   // drops every accelerator kept with the tail
+	p->view = v;
+}
+
+// the column's order index (b->torderidx + ORDERIDXOFF) as a new oid BAT, or
+// NULL without an error when it has none; stable: the index's stable flag
+extern "C" mgdk_bat *
+mgdk_BATorderidx_get(mgdk_bat *b, bool *stable)
+{
+	bool st = false;
+	size_t off = 0;
+	Heap *h = b ? oidx_get(b, &st, OIDX_OWN, &off) : nullptr;
+	if (h == nullptr)
+		return nullptr;
+	mgdk_bat *o = oidx_bat(h, off, b->hseqbase, b->count);
+	heap_decref(h);
+	if (stable)
+		*stable = st;
+	return o;
 }

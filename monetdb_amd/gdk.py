@@ -175,6 +175,11 @@ _SIGS = {
     "mgdk_BATprod": (C.c_int, [C.c_void_p, C.c_int, P, P, C.c_bool, C.c_bool]),
     "mgdk_BATgroupprod": (P, [P, P, P, P, C.c_int, C.c_bool]),
     "mgdk_BATunmask": (P, [P]),
+    "mgdk_BATorderidx": (C.c_int, [P, C.c_bool]),
+    "mgdk_set_fp_parallel_min": (C.c_uint64, [C.c_uint64]),
+    "mgdk_BATcheckorderidx": (C.c_bool, [P]),
+    "mgdk_OIDXdestroy": (None, [P]),
+    "mgdk_BATorderidx_get": (P, [P, C.POINTER(C.c_bool)]),
     "mgdk_BATgroupstdev_sample": (P, [P, P, P, P, C.c_int, C.c_bool]),
     "mgdk_BATgroupstdev_population": (P, [P, P, P, P, C.c_int, C.c_bool]),
     "mgdk_BATgroupvariance_sample": (P, [P, P, P, P, C.c_int, C.c_bool]),
@@ -717,6 +722,37 @@ def BATgroupprod(b, g, e, tp, skip_nils=True, s=None):
 def BATunmask(b):
     """BATunmask (gdk_cand.c:1464)"""
     return BAT(lib().mgdk_BATunmask(b.ptr))
+
+
+def set_fp_parallel_min(rows):
+    """rows from which one group / partition of an order-dependent float fold
+    takes the parallel form (None: never); returns the previous value"""
+    init()
+    return int(lib().mgdk_set_fp_parallel_min(BUN_NONE if rows is None else int(rows)))
+
+
+def BATorderidx(b, stable=False):
+    """BATorderidx (gdk_orderidx.c:184): keep b's sort order with b"""
+    _chk(lib().mgdk_BATorderidx(b.ptr, stable))
+
+
+def BATcheckorderidx(b):
+    """BATcheckorderidx (gdk_orderidx.c:74)"""
+    return bool(lib().mgdk_BATcheckorderidx(b.ptr))
+
+
+def OIDXdestroy(b):
+    """OIDXdestroy (gdk_orderidx.c:534)"""
+    lib().mgdk_OIDXdestroy(b.ptr)
+
+
+def BATorderidx_get(b):
+    """(index as an oid BAT, stable flag) of b's order index, or None"""
+    st = C.c_bool(False)
+    p = lib().mgdk_BATorderidx_get(b.ptr, C.byref(st))
+    if not p:
+        return None
+    return BAT(p), bool(st.value)
 
 
 def BATcalcunary(name, b, s=None):

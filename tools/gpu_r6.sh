@@ -1,24 +1,31 @@
 # round-6 GPU steps: bash tools/gpu_r6.sh <step> [...]; each step writes under
 # gpurun_out/r6/<step>/ and runs under its own time limit; the first failing
-# step ends the call
+# step ends the call, except that a test step whose pytest exits 1 (tests
+# failed, nothing crashed) lets the next steps run
 set -e
 export TMPDIR=/tmp
 T="python -u -m pytest -q --timeout 120 --timeout-method thread -m gpu"
+tests() {
+	local rc=0
+	timeout -k 10 "$@" || rc=$?
+	if [ $rc -eq 1 ]; then echo "tests failed (rc 1), continuing"; return 0; fi
+	return $rc
+}
 for step in "$@"; do
 O=gpurun_out/r6/$step
 mkdir -p $O
 case $step in
 gputests)
-	timeout -k 10 900 $T -x tests > $O/tests.log 2>&1
+	tests 900 $T -x tests > $O/tests.log 2>&1
 	;;
 dist)
-	timeout -k 10 300 $T -x tests/test_gpu_distributed.py > $O/tests.log 2>&1
+	tests 300 $T -x tests/test_gpu_distributed.py > $O/tests.log 2>&1
 	;;
 jk)
-	timeout -k 10 600 $T -x tests/test_join_kinds.py tests/test_cand_algebra.py tests/test_theta_join.py tests/test_leftjoin_multi.py > $O/tests.log 2>&1
+	tests 600 $T -x tests/test_join_kinds.py tests/test_cand_algebra.py tests/test_theta_join.py tests/test_leftjoin_multi.py > $O/tests.log 2>&1
 	;;
 tests_*)
-	timeout -k 10 600 $T -x ${TESTS} > $O/tests.log 2>&1
+	tests 600 $T -x ${TESTS} > $O/tests.log 2>&1
 	;;
 jvar)
 	# join variants (tools/variant_build.py): opbench config3, default / variants alternating twice

@@ -149,7 +149,11 @@ def other_ops(n=100_000_000):
     out = {}
     vals = r.integers(0, 1 << 30, n, dtype=np.int32)
     b = gdk.BAT.from_numpy(gdk.TYPE_int, vals, sorted_=False, revsorted=False, key=False, nonil=True)
-    _, wall, kms = timed(lambda: gdk.BATsort(b), reps=3, kernels=("sort",))
+    def sort_step():
+        # drop the order index the previous sort left (it would answer the next)
+        gdk.OIDXdestroy(b)
+        return gdk.BATsort(b)
+    _, wall, kms = timed(sort_step, reps=3, kernels=("sort",))
     out["sort_int32"] = entry(n, n * (4 + 4 + 8), wall, kms)
     g = r.integers(0, 1000, n, dtype=np.int32)
     gb = gdk.BAT.from_numpy(gdk.TYPE_int, g, sorted_=False, revsorted=False, key=False, nonil=True)

@@ -14,6 +14,7 @@ gdk.init(0)
 vals = np.random.default_rng(9).integers(0, 1 << 30, n, dtype=np.int32)
 b = gdk.BAT.from_numpy(gdk.TYPE_int, vals, sorted_=False, revsorted=False, key=False, nonil=True)
 for _ in range(reps):
+    gdk.OIDXdestroy(b)   # the previous sort's order index would answer
     r = gdk.BATsort(b)
     del r
 gdk.sync()
