@@ -1439,7 +1439,7 @@ k_pj2_offt(const uint16_t *poff, uint32_t nsub, uint32_t P, uint16_t *poffT)
 #define PJ2_NT 0        // nontemporal loads of the probe's keys and the restore's answers / rows (A/B)
 #endif
 #ifndef PJ2_UV
-#define PJ2_UV 4
+#define PJ2_UV 6
 #endif
 #ifndef PJ2_BUV
 #define PJ2_BUV 4
@@ -1454,8 +1454,98 @@ constexpr int PJ2_U = PJ2_UV;   // entries per lane in flight in the probe
 // loads of a lane are issued here; idx = ~0 marks no entry.
 struct Pj2Batch {
 	uint32_t tot;
+	uint32_t rs, rl, rb;      // PJ2_SRCH: this lane's run (start in the batch, length, index base)
 	uint32_t idx[PJ2_U], key[PJ2_U];
 };
+
+#ifndef PJ2_DIAG
+#define PJ2_DIAG 0      // timing diagnostics only (wrong answers): 1 no table build, 2 no key loads
+#endif
+#ifndef PJ2_SRCH
+#define PJ2_SRCH 1      // entries find their run by a wave max-scan of run marks (0: binary search over LDS)
+#endif
+
+// inclusive max-scan over the wave (every value >= -1): Hillis-Steele inside
+// the 16-lane rows by DPP row shifts, then the rows' last lanes broadcast
+// (row_bcast:15 / :31), no LDS
+__device__ __forceinline__ int
+wave_max_scan(int x)
+{
+	x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x111, 0xf, 0xf, false));   // row_shr:1
+	x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x112, 0xf, 0xf, false));   // row_shr:2
+	x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x114, 0xf, 0xf, false));   // row_shr:4
+	x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x118, 0xf, 0xf, false));   // row_shr:8
+	x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x142, 0xa, 0xf, false));   // row_bcast:15 -> rows 1, 3
+	x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x143, 0xc, 0xf, false));   // row_bcast:31 -> rows 2, 3
+	return x;
+}
+
+// PJ2_SRCH: the same batch numbering, but entry t's run is the last run that
+// starts at or before t: every non-empty run marks its first entry's place
+// among the call's 64 PJ2_U entries (a byte in the wave's LDS), each lane
+// reads its places and a wave max-scan carries the mark forward; the run
+// holding the call's first entry comes from a ballot.  The entry's index is
+// the run's base (read from its lane) + t.
+__device__ __forceinline__ void
+pj2_issue2(const uint32_t *pkey, const uint16_t *o0, const uint16_t *o1, uint32_t nsub, uint32_t s0, uint8_t *slot,
+	   uint32_t i0, Pj2Batch &bt, bool scan)
+{
+	const unsigned lane = __lane_id();
+	if (scan) {
+		const uint32_t sb = s0 + lane;
+		uint32_t b = 0, len = 0;
+		if (sb < nsub) {
+			b = o0[sb];
+			len = o1[sb] - b;
+		}
+		uint32_t inc = len;
+#pragma unroll
+		for (int o = 1; o < 64; o <<= 1) {
+			const uint32_t u = __shfl_up(inc, o);
+			if (lane >= (unsigned) o)
+				inc += u;
+		}
+		bt.tot = __shfl(inc, 63);
+		bt.rs = inc - len;
+		bt.rl = len;
+		bt.rb = sb * PJ_SUBROWS + b - bt.rs;
+	}
+	__builtin_amdgcn_wave_barrier();          // the previous call's reads of slot are done
+#pragma unroll
+	for (int u = 0; u < PJ2_U; u++)
+		slot[u * 64 + lane] = 0xff;
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+	if (bt.rl != 0 && bt.rs >= i0 && bt.rs - i0 < 64u * PJ2_U)
+		slot[bt.rs - i0] = (uint8_t) lane;
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+	const uint64_t before = __ballot(bt.rl != 0 && bt.rs < i0);
+	int carry = before ? 63 - __builtin_clzll(before) : 0;
+	int mk[PJ2_U];
+#pragma unroll
+	for (int u = 0; u < PJ2_U; u++) {
+		const uint32_t m = slot[u * 64 + lane];
+		mk[u] = m == 0xff ? -1 : (int) m;
+	}
+#pragma unroll
+	for (int u = 0; u < PJ2_U; u++) {
+		const int r = max(wave_max_scan(mk[u]), carry);
+		carry = __builtin_amdgcn_readlane(r, 63);
+		const uint32_t t = i0 + u * 64 + lane;
+		const uint32_t base = (uint32_t) __shfl((int) bt.rb, r);
+		bt.idx[u] = t < bt.tot ? base + t : ~0u;
+#if PJ2_DIAG & 2
+		bt.key[u] = bt.idx[u];     // timing diagnostic: no key loads
+#elif PJ2_NT
+		bt.key[u] = t < bt.tot ? __builtin_nontemporal_load(pkey + bt.idx[u]) : 0u;
+#else
+		bt.key[u] = t < bt.tot ? pkey[bt.idx[u]] : 0u;
+#endif
+	}
+}
 
 __device__ __forceinline__ void
 pj2_issue(const uint32_t *pkey, const uint16_t *o0, const uint16_t *o1, uint32_t nsub, uint32_t s0, uint32_t *ws,
@@ -1542,20 +1632,36 @@ k_pj2_probe(const uint2 *bent, const uint32_t *bbase, const uint32_t *pkey, cons
 	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
 	const uint16_t *o0 = poffT + (size_t) p * nsub, *o1 = poffT + (size_t) (p + 1) * nsub;
 	uint32_t *ws = wst + w * 64, *wb = wbs + w * 64;
+#if PJ2_SRCH
+	// the run marks: 64 PJ2_U bytes per wave in the 16 x 512 B of wst + wbs
+	static_assert(PJ2_U <= 8, "64 PJ2_U marks fit a wave's 512 B");
+	uint8_t *slot = (uint8_t *) wst + w * 512;
+	(void) ws;
+	(void) wb;
+#endif
 	for (uint32_t i = tid; i < ns; i += blockDim.x)
 		tab[i] = 0ull;
 	// the first batch's run bounds and key loads go out before the table is
 	// built, so their latency hides behind the build
 	Pj2Batch bt;
 	uint32_t s0 = w * 64;
-	if (s0 < nsub)
+	if (s0 < nsub) {
+#if PJ2_SRCH
+		pj2_issue2(pkey, o0, o1, nsub, s0, slot, 0, bt, true);
+#else
 		pj2_issue(pkey, o0, o1, nsub, s0, ws, wb, 0, bt, true);
+#endif
+	}
 	// a build partition above 90 % of the table (the host sized it for the
 	// expected largest one) is flagged and not built: its runs are answered
 	// "no match" and the host falls back after the restore
 	// (64-bit: a partition of more than ~429M entries must not wrap past the test)
 	const uint32_t b0 = bbase[p], over = (uint64_t) (bbase[p + 1] - b0) * 10 > (uint64_t) ns * 9;
+#if PJ2_DIAG & 1
+	const uint32_t b1 = b0;          // timing diagnostic: no table (every answer "no match")
+#else
 	const uint32_t b1 = over ? b0 : bbase[p + 1];
+#endif
 	if (over && tid == 0)
 		atomicOr(dupflag, 2u);
 	bool dup = false;
@@ -1608,8 +1714,16 @@ k_pj2_probe(const uint2 *bent, const uint32_t *bbase, const uint32_t *pkey, cons
 		}
 		Pj2Batch nx;
 		nx.tot = bt.tot;
-		if (ns0 < nsub)
+		nx.rs = bt.rs;
+		nx.rl = bt.rl;
+		nx.rb = bt.rb;
+		if (ns0 < nsub) {
+#if PJ2_SRCH
+			pj2_issue2(pkey, o0, o1, nsub, ns0, slot, ni0, nx, ni0 == 0);
+#else
 			pj2_issue(pkey, o0, o1, nsub, ns0, ws, wb, ni0, nx, ni0 == 0);
+#endif
+		}
 		pj2_answer(bk, pbits, nbp, bt, pans);
 		bt = nx;
 		s0 = ns0;

@@ -36,12 +36,29 @@ jvar)
 		done
 	done
 	;;
+svar)
+	# select variants: opbench config1, default / variants alternating twice
+	for r in a b; do
+		timeout -k 10 200 python tools/opbench.py --only config1 > $O/default_$r.json 2> $O/default_$r.err
+		for v in $SVARS; do
+			MGDK_LIB=$PWD/tools/variants/libmgdk_$v.so timeout -k 10 200 python tools/opbench.py --only config1 > $O/${v}_$r.json 2> $O/${v}_$r.err
+		done
+	done
+	;;
 bench)
 	timeout -k 10 420 python bench.py > $O/bench.json 2> $O/bench.err
 	;;
 benchprof)
 	cd /tmp && cd $GRAFT_REPO_ROOT
 	timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --no-cpu --no-parity > $O/bench.json 2> $O/bench.err
+	;;
+jprof)
+	# per-kernel times of opbench config3 for the default library and each of $JVARS
+	cd /tmp && cd $GRAFT_REPO_ROOT
+	timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/default -o run -- python3 tools/opbench.py --only config3 > $O/default.log 2>&1
+	for v in $JVARS; do
+		MGDK_LIB=$PWD/tools/variants/libmgdk_$v.so timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$v -o run -- python3 tools/opbench.py --only config3 > $O/$v.log 2>&1
+	done
 	;;
 join)
 	timeout -k 10 200 python tools/opbench.py --only config3 > $O/opbench.json 2> $O/opbench.err
@@ -54,6 +71,14 @@ joinpmc)
 	timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $O/pmc_tcc -o run -- python3 tools/opbench.py --only config3 > $O/pmc_tcc.log 2>&1
 	timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f -o run -- python3 tools/opbench.py --only config3 > $O/pmc_f.log 2>&1
 	timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_w -o run -- python3 tools/opbench.py --only config3 > $O/pmc_w.log 2>&1
+	;;
+sortenv)
+	# sort under environment switches, alternating: default, LB=0, HYBRID=1
+	for r in a b; do
+		timeout -k 10 200 python tools/opbench.py --only other_ops > $O/default_$r.json 2> $O/default_$r.err
+		MGDK_SORT_LB=0 timeout -k 10 200 python tools/opbench.py --only other_ops > $O/lb0_$r.json 2> $O/lb0_$r.err
+		MGDK_SORT_HYBRID=1 timeout -k 10 200 python tools/opbench.py --only other_ops > $O/hy_$r.json 2> $O/hy_$r.err
+	done
 	;;
 sort)
 	timeout -k 10 200 python tools/opbench.py --only other_ops > $O/opbench.json 2> $O/opbench.err
