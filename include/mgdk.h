@@ -270,6 +270,12 @@ mgdk_bat *mgdk_BATgroupsum(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, i
 mgdk_bat *mgdk_BATgroupcount(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils);
 /* BATgroupavg (gdk_calc.h:129, gdk_aggr.c:1801): dbl averages; tp must be
  * MGDK_dbl; cntsp may be NULL; scale divides by 10^scale */
+/* BATcalcavg (gdk_calc.h; gdk_aggr.c:2987): average of b[s] without nils into
+ * *avg (nil: NaN when there is none) and their number into *vals (may be
+ * NULL); integers (dbl) exact sum / n, flt / dbl the running mean in
+ * candidate order; divided by 10^scale.  An hge column whose sum leaves 128
+ * bits is refused (the reference continues with a remainder recurrence) */
+int mgdk_BATcalcavg(mgdk_bat *b, mgdk_bat *s, double *avg, mgdk_BUN *vals, int scale);
 int mgdk_BATgroupavg(mgdk_bat **bnp, mgdk_bat **cntsp, mgdk_bat *b, mgdk_bat *g, mgdk_bat *e,
 		     mgdk_bat *s, int tp, bool skip_nils, int scale);
 /* BATgroupavg3combine (gdk_calc.h, gdk_aggr.c:2634): combine per-row partial

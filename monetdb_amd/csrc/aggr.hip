@@ -1756,7 +1756,8 @@ k_favg_replay(const T *vals, oid off, const uint32_t *perm, const uint64_t *star
 			if (ok[u]) {
 				r = perm ? perm[jj] : jj;
 				if (!perm) {
-					const oid g = gids ? gids[r] : gseq + r;
+					// (gids NULL, gseq nil: every row is in the one group, BATcalcavg)
+					const oid g = gids ? gids[r] : gseq == MGDK_OID_NIL ? gmin : gseq + r;
 					ok[u] = g >= gmin && g - gmin < ngrp;
 				}
 			}
@@ -1824,7 +1825,7 @@ k_favg_par(const T *vals, oid off, const oid *gids, oid gseq, oid gmin, BUN n, B
 	FAvg s{0, 0, 0};
 	long long c = 0;
 	for (BUN r = b0 + threadIdx.x; r < b1; r += 256) {
-		const oid g = gids ? gids[r] : gseq + r;
+		const oid g = gids ? gids[r] : gseq == MGDK_OID_NIL ? gmin : gseq + r;
 		if (g != gmin)
 			continue;
 		const double x = (double) vals[off + r];
@@ -2198,6 +2199,146 @@ mgdk_BATgroupcount(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, b
 // BATgroupavg (gdk/gdk_aggr.c:1801-1984): trivial cases :1834-1873,
 // integers AGGR_AVG (:1717) as the exact floor average and remainder of the
 // group's 128-bit sum, flt/dbl AGGR_AVG_FLOAT (:1753) replayed per group
+// BATcalcavg (gdk/gdk_aggr.c:2987): the average of b[s] without nils and
+// their number.  Integers: the exact sum (the device's 128-bit reduction)
+// over the count, (dbl) sum / n as AVERAGE_TYPE_LNG_HGE computes it while the
+// sum fits (:2905-2924); an hge column whose sum leaves 128 bits -- where
+// the reference switches to its remainder recurrence (:2925-2958) -- is
+// refused.  flt / dbl: AVERAGE_FLOATTYPE's running mean (:2970-2984),
+// replayed in candidate order (the parallel form from fp_parallel_min rows).
+// scale: the result divided by 10^scale (:3036-3037).
+int
+mgdk_BATcalcavg(mgdk_bat *b, mgdk_bat *s, double *avg, mgdk_BUN *vals, int scale)
+{
+	const double nil = __builtin_nan("");
+	if (avg)
+		*avg = nil;
+	if (b == nullptr || avg == nullptr) {
+		seterr("BATcalcavg: NULL argument");
+		return -1;
+	}
+	const int bt = b->ttype;
+	if (!(int_type(bt) && bt != MGDK_oid) && bt != MGDK_flt && bt != MGDK_dbl) {
+		seterr("average of type %s unsupported.\n", atomname(bt));
+		return -1;
+	}
+	ProfScope prof("calcavg");
+	hipStream_t st = stream();
+	double a = nil;
+	unsigned long long n = 0;
+	if (bt == MGDK_flt || bt == MGDK_dbl) {
+		Cand ci;
+		if (cand_init(&ci, b, s) < 0)
+			return -1;
+		mgdk_bat *v = b;
+		if (!ci.dense) {
+			// the gathered values (owned by cand_values' per-thread ring)
+			v = cand_values(b, ci);
+			if (v == nullptr || cand_init(&ci, v, nullptr) < 0)
+				return -1;
+		}
+		const oid off = ci.n ? ci.seq - v->hseqbase : 0;
+		DevBuf out(16), cnt(16);
+		bool ok = out.p && cnt.p;
+		if (ok && ci.n >= fp_parallel_min() && ci.n > 0) {
+			unsigned nb = (unsigned) min((BUN) 2048, (ci.n + 4095) / 4096);
+			const BUN tile = (ci.n + nb - 1) / nb;
+			nb = (unsigned) ((ci.n + tile - 1) / tile);
+			DevBuf part((size_t) nb * sizeof(FAvg));
+			ok = part.p != nullptr;
+			if (ok) {
+				if (bt == MGDK_flt)
+					hipLaunchKernelGGL((k_favg_par<float>), dim3(nb), dim3(256), 0, st, (const float *) v->theap, off,
+							   (const oid *) nullptr, (oid) MGDK_OID_NIL, (oid) 0, ci.n, tile, true,
+							   part.as<FAvg>());
+				else
+					hipLaunchKernelGGL((k_favg_par<double>), dim3(nb), dim3(256), 0, st, (const double *) v->theap,
+							   off, (const oid *) nullptr, (oid) MGDK_OID_NIL, (oid) 0, ci.n, tile, true,
+							   part.as<FAvg>());
+				hipLaunchKernelGGL(k_favg_fin, dim3(1), dim3(256), 0, st, part.as<FAvg>(), nb, 1.0, out.as<double>(),
+						   cnt.as<long long>());
+				ok = sync();
+			}
+		} else if (ok && ci.n > 0) {
+			if (bt == MGDK_flt)
+				hipLaunchKernelGGL((k_favg_replay<float>), dim3(1), dim3(64), 0, st, (const float *) v->theap, off,
+						   (const uint32_t *) nullptr, (const uint64_t *) nullptr, (const oid *) nullptr,
+						   (oid) MGDK_OID_NIL, (oid) 0, (BUN) 1, ci.n, true, 1.0, out.as<double>(),
+						   cnt.as<long long>());
+			else
+				hipLaunchKernelGGL((k_favg_replay<double>), dim3(1), dim3(64), 0, st, (const double *) v->theap, off,
+						   (const uint32_t *) nullptr, (const uint64_t *) nullptr, (const oid *) nullptr,
+						   (oid) MGDK_OID_NIL, (oid) 0, (BUN) 1, ci.n, true, 1.0, out.as<double>(),
+						   cnt.as<long long>());
+			ok = sync();
+		}
+		double *h = (double *) pinned(16);
+		if (ok && ci.n > 0)
+			ok = h && hip_ok(hipMemcpyAsync(h, out.p, 8, hipMemcpyDeviceToHost, st), "memcpy") &&
+			     hip_ok(hipMemcpyAsync(h + 1, cnt.p, 8, hipMemcpyDeviceToHost, st), "memcpy") && sync_data();
+		if (!ok)
+			return -1;
+		if (ci.n > 0) {
+			long long c;
+			memcpy(&c, h + 1, 8);
+			n = (unsigned long long) c;
+			a = n > 0 ? h[0] : nil;
+		}
+	} else {
+		// the exact sum and count in one reduction; an hge column whose sum
+		// could leave 128 bits is checked in order
+		hge total = 0;
+		Cand ci;
+		if (cand_init(&ci, b, s) < 0)
+			return -1;
+		SumOut *o = (SumOut *) meta_buf();
+		if (ci.n) {
+			const oid off = ci.dense ? ci.seq - b->hseqbase : 0;
+			const unsigned g = grid_for(ci.n, 256 * 8, 2048);
+			SumPart *parts = (SumPart *) scratch((size_t) g * sizeof(SumPart));
+			if (parts == nullptr)
+				return -1;
+			const dim3 gd(g), blk(256);
+#define KS(W_) do { if (ci.dense) hipLaunchKernelGGL((k_sum<W_, true>), gd, blk, 0, st, b->theap, off, ci.oids, b->hseqbase, ci.n, parts); \
+		else hipLaunchKernelGGL((k_sum<W_, false>), gd, blk, 0, st, b->theap, off, ci.oids, b->hseqbase, ci.n, parts); } while (0)
+			switch (b->twidth) {
+			case 1: KS(1); break;
+			case 2: KS(2); break;
+			case 4: KS(4); break;
+			case 8: KS(8); break;
+			default: KS(16); break;
+			}
+#undef KS
+			hipLaunchKernelGGL(k_sum_fin, dim3(1), dim3(256), 0, st, parts, g, o);
+			SumOut *h = (SumOut *) pinned(sizeof(SumOut));
+			if (h == nullptr || !hip_ok(hipMemcpyAsync(h, o, sizeof(SumOut), hipMemcpyDeviceToHost, st), "memcpy") ||
+			    !sync())
+				return -1;
+			n = h->cnt;
+			total = (hge) (((uhge) h->sum[1] << 64) | h->sum[0]);
+			if (bt == MGDK_hge && mag_bound(h->maxabs) * (long double) n > (long double) tmax(MGDK_hge)) {
+				unsigned long long *ov = (unsigned long long *) o;
+				hipLaunchKernelGGL(k_sum_ordered, dim3(1), dim3(256), 0, st, b->theap, b->twidth, ci.dense,
+						   ci.dense ? ci.seq - b->hseqbase : 0, ci.oids, b->hseqbase, ci.n, tmax(MGDK_hge), ov);
+				unsigned long long *hv = (unsigned long long *) pinned(16);
+				if (!hip_ok(hipMemcpyAsync(hv, ov, 8, hipMemcpyDeviceToHost, st), "memcpy") || !sync())
+					return -1;
+				if (*hv) {
+					seterr("42000!BATcalcavg: hge sum exceeds the 128-bit device accumulator\n");
+					return -1;
+				}
+			}
+		}
+		a = n > 0 ? (double) total / (double) n : nil;
+	}
+	if (scale != 0 && a == a)
+		a /= pow(10.0, (double) scale);
+	*avg = a;
+	if (vals)
+		*vals = (mgdk_BUN) n;
+	return 0;
+}
+
 int
 mgdk_BATgroupavg(mgdk_bat **bnp, mgdk_bat **cntsp, mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp,
 		 bool skip_nils, int scale)

@@ -177,6 +177,7 @@ _SIGS = {
     "mgdk_BATunmask": (P, [P]),
     "mgdk_BATorderidx": (C.c_int, [P, C.c_bool]),
     "mgdk_set_fp_parallel_min": (C.c_uint64, [C.c_uint64]),
+    "mgdk_BATcalcavg": (C.c_int, [P, P, C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.c_int]),
     "mgdk_BATcheckorderidx": (C.c_bool, [P]),
     "mgdk_OIDXdestroy": (None, [P]),
     "mgdk_BATorderidx_get": (P, [P, C.POINTER(C.c_bool)]),
@@ -880,6 +881,13 @@ def BATgroupmedian(b, g, e, skip_nils=True, s=None, average=False):
     """BATgroupmedian (gdk_aggr.c:4225) / BATgroupmedian_avg (:4241)"""
     f = lib().mgdk_BATgroupmedian_avg if average else lib().mgdk_BATgroupmedian
     return BAT(f(b.ptr, _p(g), _p(e), _p(s), b.ttype, skip_nils))
+
+
+def BATcalcavg(b, s=None, scale=0):
+    """BATcalcavg (gdk_aggr.c:2987): (average, number of non-nil values); nil is NaN"""
+    a, n = C.c_double(), C.c_uint64()
+    _chk(lib().mgdk_BATcalcavg(b.ptr, _p(s), C.byref(a), C.byref(n), scale))
+    return a.value, n.value
 
 
 def BATgroupavg(b, g, e, skip_nils=True, s=None, scale=0, want_counts=True):

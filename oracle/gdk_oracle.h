@@ -151,6 +151,7 @@ int ora_groupavg(ora_bat **bnp, ora_bat **cntp, const ora_bat *b, const ora_bat 
 int ora_minmax(ora_bat *b, bool skipnil, bool domax, void *res, const char **sres);
 /* gdk_aggr.c:1650 BATprod (res of type tp), :1575 BATgroupprod */
 int ora_prod(void *res, int tp, const ora_bat *b, const ora_bat *s, bool skip_nils, bool nil_if_empty);
+int ora_calcavg(const ora_bat *b, const ora_bat *s, double *avg, uint64_t *vals, int scale);
 ora_bat *ora_groupprod(const ora_bat *b, const ora_bat *g, const ora_bat *e, const ora_bat *s, int tp,
 		       bool skip_nils);
 ora_bat *ora_groupminmax(const ora_bat *b, const ora_bat *g, const ora_bat *e,

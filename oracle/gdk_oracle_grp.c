@@ -1666,3 +1666,62 @@ ora_groupprod(const ora_bat *b, const ora_bat *g, const ora_bat *e, const ora_ba
 	bn->nonil = nils == 0;
 	return bn;
 }
+
+/* BATcalcavg (gdk/gdk_aggr.c:2987-3044): the average of b[s] without nils.
+ * Integers: the sum in hge (AVERAGE_TYPE_LNG_HGE :2905-2924), (dbl) sum / n;
+ * a sum that leaves hge -- only an hge column can -- is refused, as the
+ * device refuses it (the reference continues with its remainder recurrence,
+ * :2925-2958).  flt / dbl: AVERAGE_ITER_FLOAT in candidate order
+ * (AVERAGE_FLOATTYPE :2970-2984).  scale divides a non-nil result by
+ * 10^scale (:3036-3037); *vals = the number of non-nil values. */
+int
+ora_calcavg(const ora_bat *b, const ora_bat *s, double *avg, uint64_t *vals, int scale)
+{
+	const int tp = b->type;
+	*avg = nan("");
+	if (tp != ORA_bte && tp != ORA_sht && tp != ORA_int && tp != ORA_lng && tp != ORA_hge && tp != ORA_flt &&
+	    tp != ORA_dbl) {
+		ora_seterr("average of type %d unsupported.\n", tp);
+		return -1;
+	}
+	ora_ci ci;
+	if (ora_ci_init(&ci, b, s) < 0)
+		return -1;
+	uint64_t n = 0;
+	double a = 0;
+	if (tp == ORA_flt || tp == ORA_dbl) {
+		for (uint64_t i = 0; i < ci.n; i++) {
+			const uint64_t p = ci_get(&ci, i) - b->hseqbase;
+			const double x = tp == ORA_flt ? (double) ((const float *) b->base)[p] : ((const double *) b->base)[p];
+			if (isnan(x))
+				continue;
+			const double nn = (double) ++n;
+			if ((a > 0) == (x > 0))
+				a += (x - a) / nn;
+			else
+				a = a - a / nn + x / nn;
+		}
+		a = n > 0 ? a : nan("");
+	} else {
+		ora_hge sum = 0;
+		const ora_hge max = (ora_hge) (((unsigned __int128) 1 << 127) - 1);
+		for (uint64_t i = 0; i < ci.n; i++) {
+			ora_hge x;
+			if (val_at(b, ci_get(&ci, i) - b->hseqbase, &x))
+				continue;
+			if ((x > 0 && sum > max - x) || (x < 0 && sum < -max - x)) {
+				ora_seterr("42000!BATcalcavg: hge sum exceeds the 128-bit device accumulator\n");
+				return -1;
+			}
+			sum += x;
+			n++;
+		}
+		a = n > 0 ? (double) sum / (double) n : nan("");
+	}
+	if (scale != 0 && !isnan(a))
+		a /= pow(10.0, (double) scale);
+	*avg = a;
+	if (vals)
+		*vals = n;
+	return 0;
+}

@@ -135,6 +135,7 @@ def lib():
         L.ora_prod.argtypes = [C.c_void_p, C.c_int, P, P, C.c_bool, C.c_bool]
         L.ora_groupprod.restype = P
         L.ora_groupprod.argtypes = [P, P, P, P, C.c_int, C.c_bool]
+        L.ora_calcavg.argtypes = [P, P, C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.c_int]
         L.ora_leftjoin_ex.argtypes = [C.POINTER(P), C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool, C.c_bool,
                                       C.c_bool, C.c_bool, C.c_bool, C.POINTER(C.c_int)]
         L.ora_join_algo.argtypes = [P, P, P, P]
@@ -508,6 +509,14 @@ def BATgroupquantile(b, g, e, quantile, skip_nils=True, s=None, average=False):
     """doBATgroupquantile (gdk_aggr.c:3881); g may be None"""
     return _ret(lib().ora_groupquantile(b.ptr, g.ptr if g else None, e.ptr if e else None,
                                         s.ptr if s else None, quantile, skip_nils, average))
+
+
+def BATcalcavg(b, s=None, scale=0):
+    """gdk_aggr.c:2987: (average or NaN, number of non-nil values)"""
+    a, n = C.c_double(), C.c_uint64()
+    if lib().ora_calcavg(b.ptr, s.ptr if s else None, C.byref(a), C.byref(n), scale) < 0:
+        raise _err()
+    return a.value, n.value
 
 
 def BATgroupavg(b, g, e, skip_nils=True, s=None, scale=0, want_counts=True):

@@ -381,3 +381,72 @@ def test_gpu_unmask(gdk, ora):
         if m is not None:
             um = gdk.BATunmask(m)
             assert np.array_equal(np.asarray(gdk.cand_oids(um), np.uint64), 40 + np.flatnonzero(bits).astype(np.uint64))
+
+
+# ---- BATcalcavg (gdk_aggr.c:2987) -----------------------------------------
+
+
+def test_oracle_calcavg_model(ora):
+    r = rng(1520)
+    v = r.integers(-1000, 1000, 5000).astype(np.int32)
+    v[::7] = NI
+    a, n = ora.BATcalcavg(ora.Bat.from_array(ora.TYPE_int, v))
+    ok = v[v != NI].astype(np.int64)
+    assert n == len(ok) and a == float(ok.sum()) / len(ok)
+    a, n = ora.BATcalcavg(ora.Bat.from_array(ora.TYPE_int, v), scale=2)
+    assert a == float(ok.sum()) / len(ok) / 100.0
+    f = r.standard_normal(3000)
+    f[::11] = np.nan
+    a, n = ora.BATcalcavg(ora.Bat.from_array(ora.TYPE_dbl, f))
+    m = 0.0
+    k = 0
+    for x in f:
+        if np.isnan(x):
+            continue
+        k += 1
+        m = m + (x - m) / k if (m > 0) == (x > 0) else m - m / k + x / k
+    assert n == k and a == m
+    a, n = ora.BATcalcavg(ora.Bat.from_array(ora.TYPE_int, np.full(4, NI, np.int32)))
+    assert np.isnan(a) and n == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tp", ["bte", "int", "lng", "hge", "flt", "dbl"])
+@pytest.mark.parametrize("cands", [False, True])
+def test_gpu_calcavg(gdk, ora, tp, cands):
+    r = rng(1521)
+    n = 200_000
+    if tp in ("flt", "dbl"):
+        v = (r.standard_normal(n) * 50).astype(np.float32 if tp == "flt" else np.float64)
+        v[::13] = np.nan
+    elif tp == "hge":
+        vals = [int(x) << 70 if i % 17 else -(1 << 127) for i, x in enumerate(r.integers(-99, 99, n))]
+        v = np.array([[x & (2**64 - 1), (x >> 64) & (2**64 - 1)] for x in vals], np.uint64)
+    else:
+        dt = {"bte": np.int8, "int": np.int32, "lng": np.int64}[tp]
+        v = r.integers(np.iinfo(dt).min + 1, np.iinfo(dt).max, n).astype(dt)
+        v[::13] = np.iinfo(dt).min
+    G = gdk.BAT.from_numpy(getattr(gdk, "TYPE_" + tp), v)
+    O = ora.Bat.from_array(getattr(ora, "TYPE_" + tp), v)
+    s = os_ = None
+    if cands:
+        c = np.sort(r.choice(n, n // 3, replace=False)).astype(np.uint64)
+        s = gdk.BAT.from_numpy(gdk.TYPE_oid, c, sorted_=True, key=True, nonil=True)
+        os_ = ora.Bat.from_array(ora.TYPE_oid, c, sorted_=True, key=True, nonil=True)
+    for scale in (0, 3):
+        a, k = gdk.BATcalcavg(G, s, scale)
+        oa, ok_ = ora.BATcalcavg(O, os_, scale)
+        assert k == ok_
+        assert (np.isnan(a) and np.isnan(oa)) or a == oa, (a, oa)
+    prev = gdk.set_fp_parallel_min(1000)
+    try:
+        a, k = gdk.BATcalcavg(G, s)
+    finally:
+        gdk.set_fp_parallel_min(prev)
+    oa, ok_ = ora.BATcalcavg(O, os_)
+    assert k == ok_
+    if tp in ("flt", "dbl"):
+        xs = np.abs(np.asarray(v, np.float64))
+        assert abs(a - oa) <= 4 * k * 2.0 ** -53 * float(np.nanmax(xs))
+    else:
+        assert a == oa
