@@ -103,6 +103,9 @@ constexpr int RS_MAXP = 8;
 #ifndef MGDK_SORT_GIDV
 #define MGDK_SORT_GIDV 1        // group-start count pass with 16-B loads (0: 4-B loads at a 256-row stride)
 #endif
+#ifndef MGDK_SORT_LBW
+#define MGDK_SORT_LBW 8         // predecessors read per step of the scatter's look-back walk (1: one at a time)
+#endif
 #ifndef MGDK_SORT_NTLOAD
 #define MGDK_SORT_NTLOAD 1      // nontemporal key / value loads in the scatter passes (0: plain; 2.84 vs 2.74 ms)
 #endif
@@ -418,6 +421,53 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 		for (;;) {
 			bool miss = false;
 			uint32_t spins = 0;
+#if MGDK_SORT_LBW > 1
+			// the walk reads a window of LBW predecessors at once (their
+			// loads in flight together) and consumes it in order up to the
+			// first inclusive prefix or the first tile not yet published
+			while (!done) {
+				constexpr int LW = MGDK_SORT_LBW;
+				uint64_t win[LW];
+#pragma unroll
+				for (int q = 0; q < LW; q++)
+					win[q] = t - q >= 0 ? lb_load(status + (size_t) (t - q) * 256 + tid) : ST_PRE;
+				bool stop = false, notready = false;
+#pragma unroll
+				for (int q = 0; q < LW; q++) {
+					if (stop)
+						continue;
+					const uint64_t sv = win[q];
+					if ((sv >> 62) == 0) {
+						notready = true;
+						stop = true;
+						continue;
+					}
+					excl += sv & ST_VAL;
+					if ((sv & ST_PRE) || --t < 0) {
+						done = true;
+						stop = true;
+					}
+				}
+				if (!notready) {
+					spins = 0;
+					continue;
+				}
+				if (xg && (spins & 15) == 0) {
+					const uint32_t y = (uint32_t) (t / xg) & 7;
+					const uint32_t j = (uint32_t) (t / (8 * (int64_t) xg)) * xg + (uint32_t) (t % xg);
+					if (__hip_atomic_load(&xtk[y], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= j) {
+						miss = true;
+						break;
+					}
+				}
+				if (++spins > (1u << 26)) {
+					atomicOr(err, 1u);     // cannot happen: claimed tiles publish
+					done = true;
+					break;
+				}
+				__builtin_amdgcn_s_sleep(1);
+			}
+#else
 			while (!done) {
 				const uint64_t sv = lb_load(status + (size_t) t * 256 + tid);
 				if ((sv >> 62) == 0) {
@@ -442,6 +492,7 @@ k_rs_scatter(const K *keys, const uint32_t *vals, BUN n, int shift, const uint32
 				if ((sv & ST_PRE) || --t < 0)
 					done = true;
 			}
+#endif
 			if (!__syncthreads_or(miss))
 				break;
 			// the latest tile some thread is missing: count it here

@@ -80,6 +80,23 @@ sortenv)
 		MGDK_SORT_HYBRID=1 timeout -k 10 200 python tools/opbench.py --only other_ops > $O/hy_$r.json 2> $O/hy_$r.err
 	done
 	;;
+sortvar)
+	# sort variants (tools/variant_build.py): opbench other_ops, default / variants alternating twice
+	for r in a b; do
+		timeout -k 10 200 python tools/opbench.py --only other_ops > $O/default_$r.json 2> $O/default_$r.err
+		for v in $SVARS; do
+			MGDK_LIB=$PWD/tools/variants/libmgdk_$v.so timeout -k 10 200 python tools/opbench.py --only other_ops > $O/${v}_$r.json 2> $O/${v}_$r.err
+		done
+	done
+	;;
+sortpmc)
+	cd /tmp && cd $GRAFT_REPO_ROOT
+	timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_VALU --output-format csv -d $O/pmc_sq -o run -- python3 tools/run_sort.py 100000000 2 > $O/pmc_sq.log 2>&1
+	timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $O/pmc_tcc -o run -- python3 tools/run_sort.py 100000000 2 > $O/pmc_tcc.log 2>&1
+	timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f -o run -- python3 tools/run_sort.py 100000000 2 > $O/pmc_f.log 2>&1
+	timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_w -o run -- python3 tools/run_sort.py 100000000 2 > $O/pmc_w.log 2>&1
+	timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 tools/run_sort.py 100000000 2 > $O/prof.log 2>&1
+	;;
 sort)
 	timeout -k 10 200 python tools/opbench.py --only other_ops > $O/opbench.json 2> $O/opbench.err
 	cd /tmp && cd $GRAFT_REPO_ROOT
