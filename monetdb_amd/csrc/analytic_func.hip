@@ -1434,89 +1434,229 @@ rs_comb(FSum<T2> a, const FSum<T2> &b, uint32_t &fl)
 	return a;
 }
 
+// a lane's RS_PER positions q0 .. q0 + RS_PER - 1 of its tile: values (as
+// FSum leaves) and run-end flags.  The tile's values and end bytes are
+// loaded row-wise (consecutive lanes, consecutive addresses) into LDS and
+// each lane then reads its RS_PER consecutive positions (one pad slot per
+// RS_PER keeps those reads off a single bank)
+template <typename T1>
+struct RsStage {
+	T1 v[RS_TILE + RS_TILE / RS_PER];
+	int8_t f[RS_TILE];
+};
+
+template <typename T1, typename T2>
+__device__ __forceinline__ void
+rs_load(const T1 *b, const int8_t *o, BUN n, bool fwd, RsStage<T1> &sg, FSum<T2> (&x)[RS_PER], bool (&e)[RS_PER])
+{
+	const BUN t0 = (BUN) blockIdx.x * RS_TILE;
+#pragma unroll
+	for (unsigned k = 0; k < RS_PER; k++) {
+		const unsigned i = k * 256 + threadIdx.x;
+		const BUN q = t0 + i;
+		T1 v = (T1) 0;
+		int8_t f = 1;
+		if (q < n) {
+			v = b[rs_row(q, n, fwd)];
+			// the end flag's byte: o[q + 1] (frame 3) or o[n - 1 - q] (frame
+			// 4); the last position always ends its run
+			if (q + 1 < n)
+				f = o[fwd ? q + 1 : n - 1 - q];
+		}
+		sg.v[i + i / RS_PER] = v;
+		sg.f[i] = f;
+	}
+	__syncthreads();
+	const unsigned l0 = threadIdx.x * RS_PER;
+#pragma unroll
+	for (unsigned k = 0; k < RS_PER; k++) {
+		const unsigned i = l0 + k;
+		const BUN q = t0 + i;
+		const T1 v = sg.v[i + i / RS_PER];
+		x[k].nil = q >= n || v != v;
+		x[k].v = x[k].nil ? (T2) 0 : (T2) v;
+		e[k] = q < n && sg.f[i] != 0;
+	}
+}
+
+template <typename T2>
+__device__ __forceinline__ FSum<T2>
+rs_shfl_up(const FSum<T2> &v, int d)
+{
+	FSum<T2> y;
+	y.v = __shfl_up(v.v, d);
+	y.nil = __shfl_up(v.nil, d);
+	return y;
+}
+
+// ordered exclusive scan over the block's values (blockDim.x a multiple of
+// 64, at most 1024): a wave scan by shuffles, then the waves' totals through
+// LDS (one barrier); the same association every launch.  *total = the fold
+// of all of them
+template <typename T2>
+__device__ __forceinline__ FSum<T2>
+rs_block_excl(FSum<T2> v, FSum<T2> *wt, uint32_t &fl, FSum<T2> *total)
+{
+	const unsigned lane = __lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+	FSum<T2> inc = v;
+#pragma unroll
+	for (int d = 1; d < 64; d <<= 1) {
+		const FSum<T2> y = rs_shfl_up(inc, d);
+		if ((int) lane >= d)
+			inc = rs_comb(y, inc, fl);
+	}
+	FSum<T2> ex = rs_shfl_up(inc, 1);
+	if (lane == 0)
+		ex.zero();
+	if (lane == 63)
+		wt[w] = inc;
+	__syncthreads();
+	FSum<T2> wp, all;
+	wp.zero();
+	all.zero();
+	for (unsigned q = 0; q < nw; q++) {
+		if (q < w)
+			wp = rs_comb(wp, wt[q], fl);
+		all = rs_comb(all, wt[q], fl);
+	}
+	*total = all;
+	__syncthreads();            // wt may be reused by the caller
+	return rs_comb(wp, ex, fl);
+}
+
 template <typename T1, typename T2>
 __global__ __launch_bounds__(256) void
 k_rs_tile(const T1 *b, const int8_t *o, BUN n, bool fwd, FSum<T2> *tot, BUN *fend, uint32_t *flags)
 {
 	__shared__ FSum<T2> lds[256];
 	__shared__ BUN sm[256];
+	__shared__ RsStage<T1> sg;
 	const BUN q0 = (BUN) blockIdx.x * RS_TILE + threadIdx.x * RS_PER;
+	FSum<T2> x[RS_PER];
+	bool e[RS_PER];
+	rs_load<T1, T2>(b, o, n, fwd, sg, x, e);
 	FSum<T2> acc;
 	acc.zero();
 	BUN fe = ~(BUN) 0;
 	uint32_t fl = 0;
-	for (unsigned k = 0; k < RS_PER; k++) {
-		const BUN q = q0 + k;
-		if (q >= n)
-			break;
-		FSum<T2> x;
-		x.leaf(b, rs_row(q, n, fwd));
-		acc = rs_comb(acc, x, fl);
-		if (fe == ~(BUN) 0 && rs_end(o, q, n, fwd))
-			fe = q;
-	}
-	acc = block_tree(acc, [&fl](const FSum<T2> &x, const FSum<T2> &y) { return rs_comb(x, y, fl); }, lds);
-	fe = block_tree(fe, [](BUN x, BUN y) { return x < y ? x : y; }, sm);
+#pragma unroll
+	for (int k = (int) RS_PER - 1; k >= 0; k--)
+		if (e[k])
+			fe = q0 + k;
+#pragma unroll
+	for (unsigned k = 0; k < RS_PER; k++)
+		acc = rs_comb(acc, x[k], fl);
+	FSum<T2> total;
+	(void) rs_block_excl(acc, lds, fl, &total);
+#pragma unroll
+	for (int d = 32; d > 0; d >>= 1)
+		fe = min(fe, (BUN) __shfl_xor(fe, d));
+	if (__lane_id() == 0)
+		sm[threadIdx.x >> 6] = fe;
+	__syncthreads();
+	fe = min(min(sm[0], sm[1]), min(sm[2], sm[3]));
 	if (threadIdx.x == 0) {
-		tot[blockIdx.x] = acc;
+		tot[blockIdx.x] = total;
 		fend[blockIdx.x] = fe;
 	}
 	if (fl)
 		atomicOr(flags, fl);
 }
 
-// one block: pre[t] = the fold of the tiles before t (in order); nxt[t] =
-// the first run end at or after tile t + 1's first position
+// pre[t] = the fold of the tiles before t (in order); nxt[t] = the first run
+// end at or after tile t + 1's first position.  One workgroup of 1024
+// threads: thread t folds a contiguous run of tiles (its loads issued
+// together), one block scan of the runs, then each thread writes its run's
+// prefixes; the suffix minima alike
+constexpr unsigned RS_TPT = 32;     // tiles per thread per round (all loaded at once)
+
 template <typename T2>
 __global__ __launch_bounds__(1024) void
 k_rs_tiles(const FSum<T2> *tot, const BUN *fend, BUN nt, FSum<T2> *pre, BUN *nxt, uint32_t *flags)
 {
-	__shared__ FSum<T2> ls[1024];
-	__shared__ BUN lm[1024];
-	const BUN per = (nt + 1023) / 1024, t0 = min(nt, (BUN) threadIdx.x * per), t1 = min(nt, t0 + per);
+	__shared__ FSum<T2> wt[16];
+	__shared__ BUN wm[16];
 	uint32_t fl = 0;
-	FSum<T2> acc;
-	acc.zero();
-	BUN mn = ~(BUN) 0;
-	for (BUN t = t0; t < t1; t++) {
-		acc = rs_comb(acc, tot[t], fl);
-		mn = min(mn, fend[t]);
-	}
-	// exclusive scan of the thread folds (in order) and suffix minimum
-	ls[threadIdx.x] = acc;
-	lm[threadIdx.x] = mn;
-	__syncthreads();
-	if (threadIdx.x == 0) {
-		FSum<T2> run;
-		run.zero();
-		for (unsigned k = 0; k < 1024; k++) {
-			const FSum<T2> x = ls[k];
-			ls[k] = run;
-			run = rs_comb(run, x, fl);
+	FSum<T2> carry;
+	carry.zero();
+	const BUN round = (BUN) 1024 * RS_TPT;
+	for (BUN r0 = 0; r0 < nt; r0 += round) {
+		const BUN b0 = r0 + (BUN) threadIdx.x * RS_TPT;
+		FSum<T2> v[RS_TPT];
+#pragma unroll
+		for (unsigned k = 0; k < RS_TPT; k++) {
+			if (b0 + k < nt)
+				v[k] = tot[b0 + k];
+			else
+				v[k].zero();
 		}
-		BUN m = ~(BUN) 0;
-		for (int k = 1023; k >= 0; k--) {
-			const BUN x = lm[k];
-			lm[k] = m;          // minimum over the threads after k
-			m = min(m, x);
+		FSum<T2> acc;
+		acc.zero();
+#pragma unroll
+		for (unsigned k = 0; k < RS_TPT; k++)
+			acc = rs_comb(acc, v[k], fl);
+		FSum<T2> total;
+		FSum<T2> run = rs_comb(carry, rs_block_excl(acc, wt, fl, &total), fl);
+#pragma unroll
+		for (unsigned k = 0; k < RS_TPT; k++) {
+			if (b0 + k < nt)
+				pre[b0 + k] = run;
+			run = rs_comb(run, v[k], fl);
 		}
+		carry = rs_comb(carry, total, fl);
 	}
-	__syncthreads();
-	FSum<T2> run = ls[threadIdx.x];
-	for (BUN t = t0; t < t1; t++) {
-		pre[t] = run;
-		run = rs_comb(run, tot[t], fl);
-	}
-	BUN m = lm[threadIdx.x];
-	for (BUN t = t1; t-- > t0;) {
-		nxt[t] = m;
-		m = min(m, fend[t]);
+	// suffix minima of the first ends, rounds from the back
+	BUN m = ~(BUN) 0;
+	const BUN nr = (nt + round - 1) / round;
+	const unsigned lane = __lane_id(), w = threadIdx.x >> 6;
+	for (BUN rr = nr; rr-- > 0;) {
+		const BUN b0 = rr * round + (BUN) threadIdx.x * RS_TPT;
+		BUN f[RS_TPT];
+		BUN own = ~(BUN) 0;
+#pragma unroll
+		for (unsigned k = 0; k < RS_TPT; k++) {
+			f[k] = b0 + k < nt ? fend[b0 + k] : ~(BUN) 0;
+			own = min(own, f[k]);
+		}
+		// minimum over the threads after this one: wave suffix minimum,
+		// then the later waves
+		BUN suf = own;
+#pragma unroll
+		for (int d = 1; d < 64; d <<= 1) {
+			const BUN y = (BUN) __shfl_down(suf, d);
+			if ((int) lane + d < 64)
+				suf = min(suf, y);
+		}
+		if (lane == 0)
+			wm[w] = suf;
+		__syncthreads();
+		BUN later = m;
+		for (unsigned q = w + 1; q < 16; q++)
+			later = min(later, wm[q]);
+		const BUN nextin = (BUN) __shfl_down(suf, 1);
+		BUN after = lane + 1 < 64 ? min(nextin, later) : later;
+		const BUN rmin = min(min(min(wm[0], wm[1]), min(wm[2], wm[3])),
+				     min(min(min(wm[4], wm[5]), min(wm[6], wm[7])),
+					 min(min(min(wm[8], wm[9]), min(wm[10], wm[11])),
+					     min(min(wm[12], wm[13]), min(wm[14], wm[15])))));
+		__syncthreads();
+#pragma unroll
+		for (int k = (int) RS_TPT - 1; k >= 0; k--) {
+			if (b0 + k < nt)
+				nxt[b0 + k] = after;
+			after = min(after, f[k]);
+		}
+		m = min(m, rmin);
 	}
 	if (fl)
 		atomicOr(flags, fl);
 }
 
-// pass 3 (write the running sums) and pass 4 (spread the run ends' sums)
+// pass 3: every position's value -- the running sum at the end of its peer
+// run when that end lies inside the tile (read back from LDS), else its own
+// running sum for now -- stored row-wise; pass 4 gives the positions of the
+// tile's open last run (its end in a later tile) that end's value, read
+// from the output in place (end positions are never rewritten)
 template <typename T1, typename T2>
 __global__ __launch_bounds__(256) void
 k_rs_write(const T1 *b, const int8_t *o, BUN n, bool fwd, const FSum<T2> *pre, const BUN *nxt, int pass, T2 *out,
@@ -1524,70 +1664,87 @@ k_rs_write(const T1 *b, const int8_t *o, BUN n, bool fwd, const FSum<T2> *pre, c
 {
 	__shared__ FSum<T2> ls[256];
 	__shared__ BUN lm[256];
-	const BUN q0 = (BUN) blockIdx.x * RS_TILE + threadIdx.x * RS_PER;
+	__shared__ RsStage<T1> sg;
+	__shared__ T2 wo[RS_TILE + RS_TILE / RS_PER];
+	const BUN t0 = (BUN) blockIdx.x * RS_TILE;
+	const BUN q0 = t0 + threadIdx.x * RS_PER;
+	const BUN tend = t0 + RS_TILE < n ? t0 + RS_TILE : n;
 	uint32_t fl = 0;
-	if (pass == 0) {
-		FSum<T2> acc;
-		acc.zero();
-		for (unsigned k = 0; k < RS_PER && q0 + k < n; k++) {
-			FSum<T2> x;
-			x.leaf(b, rs_row(q0 + k, n, fwd));
-			acc = rs_comb(acc, x, fl);
-		}
-		// exclusive scan of the lane folds in lane order (thread 0 walks them)
-		ls[threadIdx.x] = acc;
+	FSum<T2> x[RS_PER];
+	bool e[RS_PER];
+	rs_load<T1, T2>(b, o, n, fwd, sg, x, e);
+	// the first run end at or after each lane's chunk, inside the tile
+	BUN fe = ~(BUN) 0;
+#pragma unroll
+	for (int k = (int) RS_PER - 1; k >= 0; k--)
+		if (e[k])
+			fe = q0 + k;
+	lm[threadIdx.x] = fe;
+	__syncthreads();
+	for (unsigned d = 1; d < 256; d <<= 1) {
+		BUN y = lm[threadIdx.x];
+		if (threadIdx.x + d < 256)
+			y = min(y, lm[threadIdx.x + d]);
 		__syncthreads();
-		if (threadIdx.x == 0) {
-			FSum<T2> run = pre[blockIdx.x];
-			for (unsigned k = 0; k < 256; k++) {
-				const FSum<T2> x = ls[k];
-				ls[k] = run;
-				run = rs_comb(run, x, fl);
-			}
-		}
+		lm[threadIdx.x] = y;
 		__syncthreads();
-		FSum<T2> run = ls[threadIdx.x];
-		for (unsigned k = 0; k < RS_PER && q0 + k < n; k++) {
-			const BUN q = q0 + k;
-			FSum<T2> x;
-			x.leaf(b, rs_row(q, n, fwd));
-			run = rs_comb(run, x, fl);
-			out[rs_row(q, n, fwd)] = run.nil ? (T2) __builtin_nan("") : run.v;
-			if (run.nil && rs_end(o, q, n, fwd))
-				fl |= 1;
-		}
-	} else {
-		// the first run end at or after each position: inside the lane,
-		// then the later lanes of the tile, then the later tiles
-		BUN fe = ~(BUN) 0;
-		for (unsigned k = 0; k < RS_PER && q0 + k < n; k++)
-			if (rs_end(o, q0 + k, n, fwd)) {
-				fe = q0 + k;
-				break;
-			}
-		lm[threadIdx.x] = fe;
-		__syncthreads();
-		if (threadIdx.x == 0) {
-			BUN m = nxt[blockIdx.x];
-			for (int k = 255; k >= 0; k--) {
-				const BUN x = lm[k];
-				lm[k] = m;      // first end after lane k
-				m = min(m, x);
-			}
-		}
-		__syncthreads();
-		BUN after = lm[threadIdx.x];
-		BUN endq = after;
+	}
+	const BUN after = threadIdx.x + 1 < 256 ? lm[threadIdx.x + 1] : ~(BUN) 0;
+	if (pass == 1) {
+		// the open last run: positions whose end is in a later tile
+		BUN endq = after != ~(BUN) 0 ? after : nxt[blockIdx.x];
+		if (after != ~(BUN) 0)
+			return;      // this lane's positions all end inside the tile
+#pragma unroll
 		for (int k = (int) RS_PER - 1; k >= 0; k--) {
 			const BUN q = q0 + k;
 			if (q >= n)
 				continue;
-			if (rs_end(o, q, n, fwd)) {
-				endq = q;
-				continue;
-			}
+			if (e[k])
+				return;      // this position and the ones before it end inside the tile
 			out[rs_row(q, n, fwd)] = out[rs_row(endq, n, fwd)];
 		}
+		return;
+	}
+	FSum<T2> acc;
+	acc.zero();
+#pragma unroll
+	for (unsigned k = 0; k < RS_PER; k++)
+		acc = rs_comb(acc, x[k], fl);
+	FSum<T2> total;
+	const FSum<T2> ex = rs_block_excl(acc, ls, fl, &total);
+	FSum<T2> run = rs_comb(pre[blockIdx.x], ex, fl);
+	const unsigned l0 = threadIdx.x * RS_PER;
+#pragma unroll
+	for (unsigned k = 0; k < RS_PER; k++) {
+		run = rs_comb(run, x[k], fl);
+		const unsigned i = l0 + k;
+		wo[i + i / RS_PER] = run.nil ? (T2) __builtin_nan("") : run.v;
+		if (run.nil && e[k])
+			fl |= 1;
+	}
+	__syncthreads();
+	// positions take their run end's value when it is in the tile (end
+	// positions keep their own: nothing they read is rewritten)
+	BUN endq = after;
+#pragma unroll
+	for (int k = (int) RS_PER - 1; k >= 0; k--) {
+		const BUN q = q0 + k;
+		if (e[k]) {
+			endq = q;
+			continue;
+		}
+		if (endq != ~(BUN) 0 && q < n) {
+			const unsigned j = (unsigned) (endq - t0), i = l0 + k;
+			wo[i + i / RS_PER] = wo[j + j / RS_PER];
+		}
+	}
+	__syncthreads();
+#pragma unroll
+	for (unsigned k = 0; k < RS_PER; k++) {
+		const unsigned i = k * 256 + threadIdx.x;
+		if (t0 + i < tend)
+			out[rs_row(t0 + i, n, fwd)] = wo[i + i / RS_PER];
 	}
 	if (fl)
 		atomicOr(flags, fl);

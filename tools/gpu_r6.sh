@@ -80,6 +80,13 @@ sortenv)
 		MGDK_SORT_HYBRID=1 timeout -k 10 200 python tools/opbench.py --only other_ops > $O/hy_$r.json 2> $O/hy_$r.err
 	done
 	;;
+fpcliff)
+	timeout -k 10 600 python tools/fp_cliff.py > $O/fp_cliff.json 2> $O/fp_cliff.err
+	;;
+fpprof)
+	cd /tmp && cd $GRAFT_REPO_ROOT
+	timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 tools/fp_cliff.py 100000000 par > $O/prof.log 2>&1
+	;;
 sortvar)
 	# sort variants (tools/variant_build.py): opbench other_ops, default / variants alternating twice
 	for r in a b; do
