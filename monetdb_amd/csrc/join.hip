@@ -1432,6 +1432,9 @@ k_pj2_offt(const uint16_t *poff, uint32_t nsub, uint32_t P, uint16_t *poffT)
 	}
 }
 
+#ifndef PJ2_SIDE
+#define PJ2_SIDE 1      // the probe side's cut on the thread's side stream, beside the build side's passes
+#endif
 #ifndef PJ2_RALL
 #define PJ2_RALL 1      // the restore loads all of a subtile's entries at once (0: four rounds of 8 per thread)
 #endif
@@ -1868,10 +1871,22 @@ join_part2(const Side &L, BUN nl, const Side &R, BUN nr, const PjSide &B, int pb
 		(void) sync();                              // the build side's cut still uses its buffers
 		return 1;                                   // the kernels cannot get their LDS: fallback
 	}
-	hipLaunchKernelGGL(k_pj2_cut, dim3(nsub), dim3(1024), PJ2_CUT_LDS, st, L, nl, pbits, !nil_matches,
+	// the probe side's cut depends on nothing the build side's (queued on st)
+	// writes: it runs on the side stream, beside the build side's passes,
+	// whose few workgroups leave CUs idle (PJ2_SIDE=0: one stream)
+	hipStream_t cs = st;
+#if PJ2_SIDE
+	if (stream2() != nullptr)
+		cs = stream2();
+#endif
+	hipLaunchKernelGGL(k_pj2_cut, dim3(nsub), dim3(1024), PJ2_CUT_LDS, cs, L, nl, pbits, !nil_matches,
 			   pkey.as<uint32_t>(), prow.as<uint16_t>(), poff.as<uint16_t>());
-	hipLaunchKernelGGL(k_pj2_offt, dim3((nsub + 63) / 64, (P + 1 + 63) / 64), dim3(256), 0, st, poff.as<uint16_t>(),
+	hipLaunchKernelGGL(k_pj2_offt, dim3((nsub + 63) / 64, (P + 1 + 63) / 64), dim3(256), 0, cs, poff.as<uint16_t>(),
 			   nsub, P, poffT.as<uint16_t>());
+	if (cs != st && !side_join()) {
+		(void) hipStreamSynchronize(cs);
+		return sync_fail();
+	}
 	// the table is sized for the expected largest build partition (mean + 6
 	// sigma) instead of the measured one, so no round trip is needed between
 	// the passes: a larger partition, a duplicate build key or a build value

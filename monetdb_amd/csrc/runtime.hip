@@ -44,6 +44,8 @@ hip_ok(hipError_t e, const char *what)
 // ---- streams ----------------------------------------------------------------
 struct ThreadCtx {
 	hipStream_t s = nullptr;
+	hipStream_t s2 = nullptr;       // a side stream for independent passes of one operator
+	hipEvent_t ev2 = nullptr;
 	void *scratch = nullptr;
 	size_t scratch_size = 0;
 	void *pinned = nullptr;
@@ -63,6 +65,10 @@ struct ThreadCtx {
 			(void) hipHostFree(pinned);
 		for (void *q : pinned_retired)
 			(void) hipHostFree(q);
+		if (ev2)
+			(void) hipEventDestroy(ev2);
+		if (s2)
+			(void) hipStreamDestroy(s2);
 		if (s)
 			(void) hipStreamDestroy(s);
 	}
@@ -78,6 +84,32 @@ stream()
 			tctx.s = nullptr;
 	}
 	return tctx.s;
+}
+
+// the thread's side stream; side_join() makes the main stream wait for what
+// was queued on it (so a sync of the main stream covers both)
+hipStream_t
+stream2()
+{
+	if (tctx.s2 == nullptr) {
+		(void) hipSetDevice(g_device);
+		if (hipStreamCreateWithFlags(&tctx.s2, hipStreamNonBlocking) != hipSuccess)
+			tctx.s2 = nullptr;
+	}
+	return tctx.s2;
+}
+
+bool
+side_join()
+{
+	if (tctx.s2 == nullptr)
+		return true;
+	if (tctx.ev2 == nullptr && hipEventCreateWithFlags(&tctx.ev2, hipEventDisableTiming) != hipSuccess) {
+		tctx.ev2 = nullptr;
+		return hip_ok(hipStreamSynchronize(tctx.s2), "side stream sync");
+	}
+	return hip_ok(hipEventRecord(tctx.ev2, tctx.s2), "side stream event") &&
+	       hip_ok(hipStreamWaitEvent(stream(), tctx.ev2, 0), "side stream wait");
 }
 
 // The calling thread's query context (MT_thread_set_qry_ctx,

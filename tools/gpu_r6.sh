@@ -87,6 +87,16 @@ fpprof)
 	cd /tmp && cd $GRAFT_REPO_ROOT
 	timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 tools/fp_cliff.py 100000000 par > $O/prof.log 2>&1
 	;;
+envvar)
+	# opbench legs under environment switches, alternating (ENVLEG: opbench --only key; ENVS: NAME=VAR=VALUE ...)
+	for r in a b; do
+		timeout -k 10 300 python tools/opbench.py --only $ENVLEG > $O/default_$r.json 2> $O/default_$r.err
+		for ev in $ENVS; do
+			nm=${ev%%=*}; kv=${ev#*=}
+			env $kv timeout -k 10 300 python tools/opbench.py --only $ENVLEG > $O/${nm}_$r.json 2> $O/${nm}_$r.err
+		done
+	done
+	;;
 sortvar)
 	# sort variants (tools/variant_build.py): opbench other_ops, default / variants alternating twice
 	for r in a b; do
