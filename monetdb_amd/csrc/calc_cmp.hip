@@ -31,6 +31,8 @@
 #include <cmath>
 #include <cstdio>
 
+#include <string>
+
 #include "mgdk_internal.h"
 
 using namespace mgdk;
@@ -1939,6 +1941,98 @@ k_ifthenelse(const int8_t *cond, BUN n, const void *v1, bool c1, oid seq1, const
 	}
 }
 
+// a str offset of width w (1 / 2: relative to GDK_VAROFFSET, gdk_atoms.h:421-436)
+__device__ __forceinline__ uint64_t
+str_off(const void *offs, int w, BUN p)
+{
+	switch (w) {
+	case 1: return (uint64_t) ((const uint8_t *) offs)[p] + 8192;
+	case 2: return (uint64_t) ((const uint16_t *) offs)[p] + 8192;
+	case 4: return ((const uint32_t *) offs)[p];
+	default: return ((const uint64_t *) offs)[p];
+	}
+}
+
+// str ifthenelse: 8-byte offsets into the result heap (then side: its own
+// offsets, else side: + base2; a constant: its place at the heap's end)
+__global__ __launch_bounds__(256) void
+k_ifte_str(const int8_t *cond, BUN n, const void *o1, int w1, uint64_t c1, const void *o2, int w2, uint64_t base2,
+	   uint64_t c2, uint64_t *out)
+{
+	for (BUN i = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x) {
+		const int8_t c = cond[i];
+		out[i] = c != 0 && c != INT8_MIN ? (o1 ? str_off(o1, w1, i) : c1) : (o2 ? base2 + str_off(o2, w2, i) : c2);
+	}
+}
+
+// BATcalcifthenelse of str (gdk_calc.c:4407-4459, the var-sized branch): the
+// strings are the then / else side's; the result's heap is the then side's
+// heap shared (both sides one heap, no constant) or the sides' heaps and the
+// constants copied after one another.  A copied heap may hold a string twice,
+// so it is kept at GDK_ELIMLIMIT (64 KiB) or more: grouping then compares
+// strings, never offsets (GDK_ELIMDOUBLES, gdk_atoms.h:373-375)
+mgdk_bat *
+ifthenelse_str(mgdk_bat *b, mgdk_bat *b1, const char *c1, mgdk_bat *b2, const char *c2)
+{
+	const BUN n = b->count;
+	hipStream_t st = stream();
+	mgdk_bat *bn = newbat(b->hseqbase, MGDK_lng, n);
+	if (bn == nullptr)
+		return nullptr;
+	Priv *p = (Priv *) bn->priv;
+	bn->ttype = MGDK_str;
+	bn->twidth = 8;
+	const bool shared = b1 && b2 && b1->tvheap == b2->tvheap;
+	const size_t s1 = b1 ? b1->tvheapsize : 0, s2 = b2 && !shared ? b2->tvheapsize : 0;
+	const size_t l1 = c1 ? strlen(c1) + 1 : 0, l2 = c2 ? strlen(c2) + 1 : 0;
+	const uint64_t base2 = shared ? 0 : s1, k1 = s1 + s2, k2 = s1 + s2 + l1;
+	bool ok = true;
+	if (shared) {
+		share_vheap(bn, b1);
+	} else {
+		size_t size = s1 + s2 + l1 + l2;
+		if (size < ((size_t) 1 << 16))
+			size = (size_t) 1 << 16;
+		Heap *vh = heap_new(size);
+		if (vh == nullptr) {
+			mgdk_BBPunfix(bn);
+			return nullptr;
+		}
+		heap_decref(p->tvheap);
+		p->tvheap = vh;
+		bn->tvheap = vh->base;
+		bn->tvheapsize = size;
+		char *d = (char *) vh->base;
+		ok = hip_ok(hipMemsetAsync(d, 0, size, st), "memset") &&
+		     (s1 == 0 || hip_ok(hipMemcpyAsync(d, b1->tvheap, s1, hipMemcpyDeviceToDevice, st), "memcpy")) &&
+		     (s2 == 0 || hip_ok(hipMemcpyAsync(d + s1, b2->tvheap, s2, hipMemcpyDeviceToDevice, st), "memcpy"));
+		if (ok && (l1 || l2)) {
+			std::string t;
+			if (c1)
+				t.append(c1, l1);
+			if (c2)
+				t.append(c2, l2);
+			const void *src = stage_host(t.data(), t.size());
+			ok = src && hip_ok(hipMemcpyAsync(d + k1, src, t.size(), hipMemcpyHostToDevice, st), "memcpy");
+		}
+	}
+	if (ok && n)
+		hipLaunchKernelGGL(k_ifte_str, dim3(grid_for(n, 256 * 4, 256 * 64)), dim3(256), 0, st, (const int8_t *) b->theap, n,
+				   b1 ? b1->theap : nullptr, b1 ? b1->twidth : 0, k1, b2 ? b2->theap : nullptr,
+				   b2 ? b2->twidth : 0, base2, k2, (uint64_t *) bn->theap);
+	if (!ok || !sync()) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	auto snonil = [](const char *c) { return !(c[0] == '\x80' && c[1] == 0); };
+	const bool nonil1 = b1 ? (bool) b1->tnonil : snonil(c1), nonil2 = b2 ? (bool) b2->tnonil : snonil(c2);
+	bn->count = n;
+	bn->tsorted = bn->trevsorted = bn->tkey = n <= 1;
+	bn->tnil = 0;
+	bn->tnonil = nonil1 && nonil2;
+	return bn;
+}
+
 mgdk_bat *
 calc_ifthenelse(mgdk_bat *b, mgdk_bat *b1, const void *cv1, mgdk_bat *b2, const void *cv2, int ct)
 {
@@ -1958,7 +2052,9 @@ calc_ifthenelse(mgdk_bat *b, mgdk_bat *b1, const void *cv1, mgdk_bat *b2, const 
 		return nullptr;
 	}
 	const int tp = at(t1);
-	if (tp == MGDK_str || tp == MGDK_msk || width_of(tp) == 0) {
+	if (tp == MGDK_str)
+		return ifthenelse_str(b, b1, (const char *) cv1, b2, (const char *) cv2);
+	if (tp == MGDK_msk || width_of(tp) == 0) {
 		seterr("BATcalcifthenelse: type %s is not on the device path", atomname(tp));
 		return nullptr;
 	}

@@ -305,3 +305,70 @@ def test_gpu_ifthenelse(gdk, ora):
                   ora.BATcalcifthenelse(OC, _ora(ora, f), None, c2=-0.0, ct=ora.TYPE_dbl))
     assert _eqbat(gdk.BATcalcifthenelse(C, gdk.BAT.dense(10, n), gdk.BAT.dense(7, n)),
                   ora.BATcalcifthenelse(OC, ora.Bat.dense(10, n), ora.Bat.dense(7, n)))
+
+
+# ---- ifthenelse on str (gdk_calc.c:4407-4459) ------------------------------
+
+
+def _strings(gdk, b):
+    """the strings of a device str BAT (its offsets and heap read back)"""
+    import ctypes as C
+    s = b.ptr.contents
+    heap = (C.c_uint8 * max(1, s.tvheapsize))()
+    assert gdk.lib().mgdk_BATdownload_vheap(b.ptr, C.cast(heap, C.c_void_p)) == 0
+    hb = bytes(heap)
+    offs = b.to_numpy().astype(np.uint64)
+    w = s.twidth
+    out = []
+    for o in offs:
+        o = int(o) + (8192 if w < 4 else 0)
+        out.append(hb[o:hb.index(b"\0", o)])
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("forms", ["bat_bat", "bat_cst", "cst_bat", "cst_cst", "same_heap"])
+def test_gpu_ifthenelse_str(gdk, forms):
+    from strheap import NIL, WORDS, sample, content_groups
+    r = rng(1609)
+    n = 20_000
+    c = r.integers(-1, 2, n).astype(np.int8)
+    c[c == -1] = -128
+    C_ = gdk.BAT.from_numpy(gdk.TYPE_bit, c)
+    t1, h1, w1 = sample(r, n, 2)
+    t2, h2, w2 = sample(r, n, 8, words=WORDS[::-1])
+    if forms == "same_heap":
+        t2, h2, w2 = sample(r, n, 4)
+        h2 = h1
+        w2 = [WORDS[i] for i in w2]
+        t2 = None
+    words1 = [WORDS[i] for i in w1]
+    words2 = [WORDS[::-1][i] for i in w2] if forms != "same_heap" else w2
+    B1 = gdk.BAT.from_numpy(gdk.TYPE_str, t1, vheap=h1, sorted_=False, revsorted=False, key=False, nonil=False)
+    if forms == "same_heap":
+        # the else side: other rows of the then side's column (a projection shares its heap)
+        perm = r.permutation(n).astype(np.uint64)
+        B2 = gdk.BATproject(gdk.BAT.from_numpy(gdk.TYPE_oid, perm), B1)
+        words2 = [words1[i] for i in perm]
+    else:
+        B2 = gdk.BAT.from_numpy(gdk.TYPE_str, t2, vheap=h2, sorted_=False, revsorted=False, key=False, nonil=False)
+    take = (c != 0) & (c != -128)
+    if forms in ("bat_bat", "same_heap"):
+        got = gdk.BATcalcifthenelse(C_, B1, B2)
+        want = [a if t else b for a, b, t in zip(words1, words2, take)]
+    elif forms == "bat_cst":
+        got = gdk.BATcalcifthenelse(C_, B1, b"other", gdk.TYPE_str)
+        want = [a if t else b"other" for a, t in zip(words1, take)]
+    elif forms == "cst_bat":
+        got = gdk.BATcalcifthenelse(C_, NIL, B2, gdk.TYPE_str)
+        want = [NIL if t else b for b, t in zip(words2, take)]
+    else:
+        got = gdk.BATcalcifthenelse(C_, b"yes", b"no", gdk.TYPE_str)
+        want = [b"yes" if t else b"no" for t in take]
+    assert _strings(gdk, got) == want
+    if forms == "same_heap":
+        assert got.ptr.contents.tvheap == B1.ptr.contents.tvheap      # shared, not copied
+    # grouping the result compares strings (a copied heap may repeat one)
+    g, e, h = gdk.BATgroup(got)
+    wg, we, wh = content_groups(want)
+    assert np.array_equal(g.to_numpy().astype(np.uint64), wg) and np.array_equal(e.to_numpy().astype(np.uint64), we)
