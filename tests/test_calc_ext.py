@@ -372,3 +372,62 @@ def test_gpu_ifthenelse_str(gdk, forms):
     g, e, h = gdk.BATgroup(got)
     wg, we, wh = content_groups(want)
     assert np.array_equal(g.to_numpy().astype(np.uint64), wg) and np.array_equal(e.to_numpy().astype(np.uint64), we)
+
+
+# ---- every value type through the device kernels ---------------------------
+
+
+def _typed(r, tn, n):
+    if tn in ("flt", "dbl"):
+        v = (r.integers(-60, 60, n) / 4).astype(np.float32 if tn == "flt" else np.float64)
+        v[::23] = np.nan
+        v[5] = -0.0
+        return v
+    if tn == "hge":
+        lo = r.integers(-1000, 1000, n, dtype=np.int64)
+        lo[::23] = 0
+        a = np.stack([lo.view(np.uint64), (lo >> 63).view(np.uint64)], axis=1)
+        a[::23] = [0, 1 << 63]      # hge nil
+        return a
+    dt = {"bte": np.int8, "sht": np.int16, "int": np.int32, "lng": np.int64}[tn]
+    v = r.integers(-100, 100, n).astype(dt)
+    v[::23] = np.iinfo(dt).min
+    return v
+
+
+def _eq_any(g, o, tn):
+    if tn == "hge":
+        return list(g.values()) == [int(x) for x in o.values()] if g.ttype == 11 else \
+            np.array_equal(g.to_numpy().astype(np.int64), np.asarray(o.values()).astype(np.int64))
+    return _eqbat(g, o)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tn", ["bte", "sht", "int", "lng", "hge", "flt", "dbl"])
+def test_gpu_calc_ext_types(gdk, ora, tn):
+    r = rng(1610)
+    n = 3000
+    a, b = _typed(r, tn, n), _typed(r, tn, n)
+    tg, to = getattr(gdk, "TYPE_" + tn), getattr(ora, "TYPE_" + tn)
+    G = lambda x: gdk.BAT.from_numpy(tg, x, sorted_=False, revsorted=False, key=False, nonil=False)   # noqa: E731
+    O = lambda x: ora.Bat.from_array(to, x)   # noqa: E731
+    for name in ("negate", "absolute", "iszero", "sign", "isnil", "isnotnil"):
+        assert _eq_any(gdk.BATcalcunary(name, G(a)), ora.BATcalcunary(name, O(a)), tn), name
+    for name in ("min", "max", "min_no_nil", "max_no_nil"):
+        assert _eq_any(gdk.BATcalcbin(name, G(a), G(b)), ora.BATcalcminmax(name, O(a), O(b)), tn), name
+    if tn in ("flt", "dbl"):
+        return
+    for name in ("and", "or", "xor"):
+        assert _eq_any(gdk.BATcalcbin(name, G(a), G(b)), ora.BATcalcbits(name, "BATcalc" + name, O(a), O(b)), tn), name
+    sh = np.abs(_typed(r, "bte", n).astype(np.int32)) % 5
+    sh[::23] = 1
+    S = gdk.BAT.from_numpy(gdk.TYPE_int, sh.astype(np.int32))
+    OS = ora.Bat.from_array(ora.TYPE_int, sh.astype(np.int32))
+    pos = a.copy()
+    if tn == "hge":
+        pos[:, 1] = 0
+        pos[:, 0] = pos[:, 0] % 1000
+    else:
+        pos = np.where(pos == np.iinfo(pos.dtype).min, pos, np.abs(pos) % 16).astype(a.dtype)
+    for name in ("lsh", "rsh"):
+        assert _eq_any(gdk.BATcalcbin(name, G(pos), S), ora.BATcalcbits(name, "BATcalc" + name, O(pos), OS), tn), name
