@@ -1623,9 +1623,74 @@ pj2_answer(const ulonglong2 *bk, int pbits, uint32_t nbp, const Pj2Batch &bt, ui
 
 constexpr int PJ2_BU = PJ2_BUV;  // build entries per thread per round, all loaded before any insert
 
+#ifndef PJ2_TB
+#define PJ2_TB 0        // 1: the LDS tables built by their own pass (beside the probe side's cut) and loaded by the
+                        // probe -- measured slower (0.89-0.90 against 0.86-0.87 ms: the cut shares the GPU with it)
+#endif
+
+// PJ2_TB: partition p's LDS table built as the probe would build it, then
+// stored to gtab[p] (2 nbp slots) for the probe to load with plain 16-B
+// loads; the build flags (duplicate key, oversized partition) are raised here
+__global__ __launch_bounds__(1024) void
+k_pj2_tbuild(const uint2 *bent, const uint32_t *bbase, int pbits, uint32_t nbp, unsigned long long *gtab,
+	     uint32_t *dupflag)
+{
+	extern __shared__ __attribute__((aligned(16))) unsigned long long dyn3[];
+	unsigned long long *tab = dyn3;
+	const uint32_t p = xcd_block(blockIdx.x, gridDim.x), ns = 2 * nbp;
+	const unsigned tid = threadIdx.x, lane = __lane_id();
+	for (uint32_t i = tid; i < ns; i += blockDim.x)
+		tab[i] = 0ull;
+	const uint32_t b0 = bbase[p], over = (uint64_t) (bbase[p + 1] - b0) * 10 > (uint64_t) ns * 9;
+	const uint32_t b1 = over ? b0 : bbase[p + 1];
+	if (over && tid == 0)
+		atomicOr(dupflag, 2u);
+	bool dup = false;
+	uint2 en[PJ2_BUV];
+	uint32_t e0 = b0 + tid;
+#pragma unroll
+	for (int u = 0; u < PJ2_BUV; u++) {
+		const uint32_t e = e0 + u * blockDim.x;
+		en[u] = e < b1 ? bent[e] : make_uint2(0, 0);
+	}
+	__syncthreads();                              // the table is zeroed
+	while (e0 < b1) {
+#pragma unroll
+		for (int u = 0; u < PJ2_BUV; u++) {
+			if (e0 + u * blockDim.x >= b1)
+				continue;
+			const unsigned long long v = ((unsigned long long) (en[u].y + 1) << 32) | en[u].x;
+			uint32_t h = 2 * gt_home(pj_hash(en[u].x), pbits, nbp);
+			for (;;) {
+				const unsigned long long o = atomicCAS(&tab[h], 0ull, v);
+				if (o == 0ull)
+					break;
+				if ((uint32_t) o == en[u].x) {
+					dup = true;
+					break;
+				}
+				h = h + 1 == ns ? 0 : h + 1;
+			}
+		}
+		e0 += PJ2_BUV * blockDim.x;
+#pragma unroll
+		for (int u = 0; u < PJ2_BUV; u++) {
+			const uint32_t e = e0 + u * blockDim.x;
+			en[u] = e < b1 ? bent[e] : make_uint2(0, 0);
+		}
+	}
+	if (__any(dup) && lane == 0)
+		atomicOr(dupflag, 1u);
+	__syncthreads();
+	typedef unsigned long long u2v __attribute__((ext_vector_type(2)));
+	u2v *dst = (u2v *) (gtab + (size_t) p * ns);
+	for (uint32_t i = tid; i < nbp; i += blockDim.x)
+		dst[i] = ((const u2v *) tab)[i];
+}
+
 __global__ __launch_bounds__(1024) void
 k_pj2_probe(const uint2 *bent, const uint32_t *bbase, const uint32_t *pkey, const uint16_t *poffT, int pbits,
-	    uint32_t nbp, uint32_t nsub, uint32_t *pans, uint32_t *dupflag)
+	    uint32_t nbp, uint32_t nsub, uint32_t *pans, uint32_t *dupflag, const unsigned long long *gtab)
 {
 	extern __shared__ __attribute__((aligned(16))) unsigned long long dyn2[];
 	unsigned long long *tab = dyn2;
@@ -1642,8 +1707,19 @@ k_pj2_probe(const uint2 *bent, const uint32_t *bbase, const uint32_t *pkey, cons
 	(void) ws;
 	(void) wb;
 #endif
+#if PJ2_TB
+	// the partition's table, built by k_pj2_tbuild
+	{
+		typedef unsigned long long u2v __attribute__((ext_vector_type(2)));
+		const u2v *src = (const u2v *) (gtab + (size_t) p * ns);
+		for (uint32_t i = tid; i < nbp; i += blockDim.x)
+			((u2v *) tab)[i] = src[i];
+	}
+#else
+	(void) gtab;
 	for (uint32_t i = tid; i < ns; i += blockDim.x)
 		tab[i] = 0ull;
+#endif
 	// the first batch's run bounds and key loads go out before the table is
 	// built, so their latency hides behind the build
 	Pj2Batch bt;
@@ -1655,6 +1731,12 @@ k_pj2_probe(const uint2 *bent, const uint32_t *bbase, const uint32_t *pkey, cons
 		pj2_issue(pkey, o0, o1, nsub, s0, ws, wb, 0, bt, true);
 #endif
 	}
+#if PJ2_TB
+	(void) bent;
+	(void) bbase;
+	(void) dupflag;
+	__syncthreads();                              // the table is loaded
+#else
 	// a build partition above 90 % of the table (the host sized it for the
 	// expected largest one) is flagged and not built: its runs are answered
 	// "no match" and the host falls back after the restore
@@ -1704,6 +1786,7 @@ k_pj2_probe(const uint2 *bent, const uint32_t *bbase, const uint32_t *pkey, cons
 	if (__any(dup) && lane == 0)
 		atomicOr(dupflag, 1u);
 	__syncthreads();
+#endif
 	const ulonglong2 *bk = (const ulonglong2 *) tab;     // (an empty table when over)
 	// software pipeline: the next chunk's key loads (and, at a batch
 	// boundary, the next batch's run bounds) are issued before the current
@@ -1871,22 +1954,6 @@ join_part2(const Side &L, BUN nl, const Side &R, BUN nr, const PjSide &B, int pb
 		(void) sync();                              // the build side's cut still uses its buffers
 		return 1;                                   // the kernels cannot get their LDS: fallback
 	}
-	// the probe side's cut depends on nothing the build side's (queued on st)
-	// writes: it runs on the side stream, beside the build side's passes,
-	// whose few workgroups leave CUs idle (PJ2_SIDE=0: one stream)
-	hipStream_t cs = st;
-#if PJ2_SIDE
-	if (stream2() != nullptr)
-		cs = stream2();
-#endif
-	hipLaunchKernelGGL(k_pj2_cut, dim3(nsub), dim3(1024), PJ2_CUT_LDS, cs, L, nl, pbits, !nil_matches,
-			   pkey.as<uint32_t>(), prow.as<uint16_t>(), poff.as<uint16_t>());
-	hipLaunchKernelGGL(k_pj2_offt, dim3((nsub + 63) / 64, (P + 1 + 63) / 64), dim3(256), 0, cs, poff.as<uint16_t>(),
-			   nsub, P, poffT.as<uint16_t>());
-	if (cs != st && !side_join()) {
-		(void) hipStreamSynchronize(cs);
-		return sync_fail();
-	}
 	// the table is sized for the expected largest build partition (mean + 6
 	// sigma) instead of the measured one, so no round trip is needed between
 	// the passes: a larger partition, a duplicate build key or a build value
@@ -1895,7 +1962,7 @@ join_part2(const Side &L, BUN nl, const Side &R, BUN nr, const PjSide &B, int pb
 	const double mean = (double) nr / P;
 	const uint32_t est = (uint32_t) (mean + 6.0 * sqrt(mean)) + 1;
 	if (est > PJ2_MAXFILL) {
-		(void) sync();                              // the cuts still use the buffers
+		(void) sync();                              // the build side's cut still uses its buffers
 		return 1;
 	}
 	static const int lfpct = getenv("MGDK_PJ_LF") ? atoi(getenv("MGDK_PJ_LF")) : 80;
@@ -1909,8 +1976,42 @@ join_part2(const Side &L, BUN nl, const Side &R, BUN nr, const PjSide &B, int pb
 	if (occ2 && nbp > NBP2 && (uint64_t) est * 10 <= (uint64_t) 2 * NBP2 * 9)
 		nbp = NBP2;
 	const size_t lds = (size_t) nbp * 16 + 16 * 64 * 8;
+#if PJ2_TB
+	// the build side's tables, built on st beside the probe side's cut
+	static const bool tb_attr = hipFuncSetAttribute((const void *) k_pj2_tbuild,
+							hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+	(void) hipGetLastError();
+	DevBuf gtab((size_t) P * 2 * nbp * 8 + 64);
+	if (!tb_attr || !gtab.p) {
+		(void) sync();                              // the build side's cut still uses its buffers
+		return tb_attr ? -1 : 1;
+	}
+	const unsigned long long *gtp = gtab.as<unsigned long long>();
+#else
+	const unsigned long long *gtp = nullptr;
+#endif
+	// the probe side's cut depends on nothing the build side's (queued on st)
+	// writes: it runs on the side stream, beside the build side's passes,
+	// whose few workgroups leave CUs idle (PJ2_SIDE=0: one stream)
+	hipStream_t cs = st;
+#if PJ2_SIDE
+	if (stream2() != nullptr)
+		cs = stream2();
+#endif
+	hipLaunchKernelGGL(k_pj2_cut, dim3(nsub), dim3(1024), PJ2_CUT_LDS, cs, L, nl, pbits, !nil_matches,
+			   pkey.as<uint32_t>(), prow.as<uint16_t>(), poff.as<uint16_t>());
+	hipLaunchKernelGGL(k_pj2_offt, dim3((nsub + 63) / 64, (P + 1 + 63) / 64), dim3(256), 0, cs, poff.as<uint16_t>(),
+			   nsub, P, poffT.as<uint16_t>());
+#if PJ2_TB
+	hipLaunchKernelGGL(k_pj2_tbuild, dim3(P), dim3(1024), (size_t) nbp * 16, st, B.ent->as<uint2>(),
+			   B.base->as<uint32_t>(), pbits, nbp, gtab.as<unsigned long long>(), &meta32[2]);
+#endif
+	if (cs != st && !side_join()) {
+		(void) hipStreamSynchronize(cs);
+		return sync_fail();
+	}
 	hipLaunchKernelGGL(k_pj2_probe, dim3(P), dim3(1024), lds, st, B.ent->as<uint2>(), B.base->as<uint32_t>(),
-			   pkey.as<uint32_t>(), poffT.as<uint16_t>(), pbits, nbp, nsub, pans.as<uint32_t>(), &meta32[2]);
+			   pkey.as<uint32_t>(), poffT.as<uint16_t>(), pbits, nbp, nsub, pans.as<uint32_t>(), &meta32[2], gtp);
 	mgdk_bat *ra = newbat(0, MGDK_oid, nl), *rb = newbat(0, MGDK_oid, nl);
 	const size_t sbytes = (nsub + 8) * sizeof(uint64_t);
 	char *sc = (char *) scratch(sbytes);
