@@ -345,6 +345,13 @@ void mgdk_free(void *p);
 int mgdk_BATprod(void *res, int tp, mgdk_bat *b, mgdk_bat *s, bool skip_nils, bool nil_if_empty);
 mgdk_bat *mgdk_BATgroupprod(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils);
 
+/* BATcount_no_nil (gdk/gdk.h; gdk_batop.c:3078): b's candidates whose
+ * value is not nil (tnonil / msk: every candidate; void: none when the
+ * sequence is nil); a count of every row sets b's tnonil.  0 for a NULL b;
+ * MGDK_BUN_NONE (message set) on a device error, which the reference has no
+ * way to report */
+mgdk_BUN mgdk_BATcount_no_nil(mgdk_bat *b, mgdk_bat *s);
+
 /* ---- group (gdk/gdk.h:1447; gdk/gdk_group.c:1347) --------------------- */
 int mgdk_BATgroup(mgdk_bat **groups, mgdk_bat **extents, mgdk_bat **histo,
 		  mgdk_bat *b, mgdk_bat *s, mgdk_bat *g, mgdk_bat *e, mgdk_bat *h);
@@ -397,6 +404,16 @@ int mgdk_BATbandjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, m
  * left-major pairs with BETWEEN's three-valued logic */
 int mgdk_BATrangejoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *rl, mgdk_bat *rh, mgdk_bat *sl,
 		      mgdk_bat *sr, bool linc, bool hinc, bool anti, bool symmetric, mgdk_BUN estimate);
+/* BATsubcross (gdk/gdk.h; gdk_cross.c:138, BATcrossci :22): every (left,
+ * right) candidate pair, left-major (r1 the left oid, r2 the right one); one
+ * candidate on a side gives a candidate slice and a constant column, none two
+ * empty dense columns.  BAToutercross (gdk_cross.c:153): no right candidate
+ * pairs each left candidate with nil (a void column of nil oids).  max_one:
+ * "more than one match" when a left candidate meets several right ones */
+int mgdk_BATsubcross(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr,
+		     bool max_one);
+int mgdk_BAToutercross(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr,
+		       bool max_one);
 /* gdk/gdk.h:1524-1525 (gdk_batop.c:2002, :2181): whether b is sorted /
  * reverse sorted; what is found is recorded in b (tsorted, trevsorted,
  * tkey, tnosorted, tnorevsorted) as the reference does */

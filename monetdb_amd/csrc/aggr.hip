@@ -3151,3 +3151,109 @@ mgdk_BATgroupmax(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, boo
 }
 
 }  // extern "C"
+
+// ---- BATcount_no_nil (gdk/gdk_batop.c:3078) ---------------------------------
+
+namespace {
+
+// non-nil values among the candidates, one atomic per workgroup
+template <typename T>
+__global__ void
+k_count_nonil(const T *__restrict__ v, oid hseq, bool dense, oid seq, const oid *__restrict__ oids, BUN n,
+	      unsigned long long *cnt)
+{
+	unsigned long long c = 0;
+	for (BUN i = blockIdx.x * (BUN) blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
+		c += !is_nil(v[(dense ? seq + i : oids[i]) - hseq]);
+	c = block_reduce(c, [](unsigned long long a, unsigned long long b) { return a + b; });
+	if (threadIdx.x == 0 && c)
+		atomicAdd(cnt, c);
+}
+
+// str: the first byte of the string at the offset (1- / 2-byte offsets
+// biased by GDK_VAROFFSET) is not the nil string's 0x80
+template <typename O>
+__global__ void
+k_count_nonil_str(const O *__restrict__ off, const char *__restrict__ heap, size_t bias, oid hseq, bool dense,
+		  oid seq, const oid *__restrict__ oids, BUN n, unsigned long long *cnt)
+{
+	unsigned long long c = 0;
+	for (BUN i = blockIdx.x * (BUN) blockDim.x + threadIdx.x; i < n; i += (BUN) gridDim.x * blockDim.x)
+		c += heap[(size_t) off[(dense ? seq + i : oids[i]) - hseq] + bias] != '\200';
+	c = block_reduce(c, [](unsigned long long a, unsigned long long b) { return a + b; });
+	if (threadIdx.x == 0 && c)
+		atomicAdd(cnt, c);
+}
+
+}  // namespace
+
+// the count of b's candidates whose value is not nil; every candidate when b
+// is known nil-free (tnonil), a msk BAT, or a void BAT with a sequence (none
+// when its sequence is nil).  A count of every row records tnonil in b, as
+// the reference does.  The reference cannot fail; here a device error gives
+// MGDK_BUN_NONE with the message set, a NULL b 0
+extern "C" mgdk_BUN
+mgdk_BATcount_no_nil(mgdk_bat *b, mgdk_bat *s)
+{
+	if (b == nullptr)
+		return 0;
+	mgdk_bat *held = nullptr;
+	if (s && is_complex_cand(s) && (s = held = unmask_cand(s)) == nullptr)
+		return MGDK_BUN_NONE;
+	struct Unfix {
+		mgdk_bat *b;
+		~Unfix() { mgdk_BBPunfix(b); }
+	} unfix{held};
+	Cand ci;
+	if (cand_init(&ci, b, s) < 0)
+		return MGDK_BUN_NONE;
+	if (b->tnonil || b->ttype == MGDK_msk)
+		return ci.n;
+	if (b->ttype == MGDK_void)
+		return b->tseqbase == MGDK_OID_NIL ? 0 : ci.n;
+	BUN cnt = 0;
+	if (ci.n > 0) {
+		DevBuf acc(8);
+		if (!acc.p)
+			return MGDK_BUN_NONE;
+		hipStream_t st = stream();
+		unsigned long long *d = acc.as<unsigned long long>();
+		if (!hip_ok(hipMemsetAsync(d, 0, 8, st), "hipMemsetAsync"))
+			return MGDK_BUN_NONE;
+		const dim3 g(grid_for(ci.n, BLOCK * 16, 256u * 32u)), blk(BLOCK);
+		const oid hs = b->hseqbase;
+		switch (b->ttype == MGDK_str ? MGDK_str : basetype(b->ttype)) {
+		case MGDK_bte: hipLaunchKernelGGL((k_count_nonil<int8_t>), g, blk, 0, st, (const int8_t *) b->theap, hs, ci.dense, ci.seq, ci.oids, ci.n, d); break;
+		case MGDK_sht: hipLaunchKernelGGL((k_count_nonil<int16_t>), g, blk, 0, st, (const int16_t *) b->theap, hs, ci.dense, ci.seq, ci.oids, ci.n, d); break;
+		case MGDK_int: hipLaunchKernelGGL((k_count_nonil<int32_t>), g, blk, 0, st, (const int32_t *) b->theap, hs, ci.dense, ci.seq, ci.oids, ci.n, d); break;
+		case MGDK_lng: hipLaunchKernelGGL((k_count_nonil<int64_t>), g, blk, 0, st, (const int64_t *) b->theap, hs, ci.dense, ci.seq, ci.oids, ci.n, d); break;
+		case MGDK_oid: hipLaunchKernelGGL((k_count_nonil<uint64_t>), g, blk, 0, st, (const uint64_t *) b->theap, hs, ci.dense, ci.seq, ci.oids, ci.n, d); break;
+		case MGDK_hge: hipLaunchKernelGGL((k_count_nonil<hge>), g, blk, 0, st, (const hge *) b->theap, hs, ci.dense, ci.seq, ci.oids, ci.n, d); break;
+		case MGDK_flt: hipLaunchKernelGGL((k_count_nonil<float>), g, blk, 0, st, (const float *) b->theap, hs, ci.dense, ci.seq, ci.oids, ci.n, d); break;
+		case MGDK_dbl: hipLaunchKernelGGL((k_count_nonil<double>), g, blk, 0, st, (const double *) b->theap, hs, ci.dense, ci.seq, ci.oids, ci.n, d); break;
+		case MGDK_str: {
+			const char *heap = (const char *) b->tvheap;
+			switch (b->twidth) {
+			case 1: hipLaunchKernelGGL((k_count_nonil_str<uint8_t>), g, blk, 0, st, (const uint8_t *) b->theap, heap, (size_t) 8192, hs, ci.dense, ci.seq, ci.oids, ci.n, d); break;
+			case 2: hipLaunchKernelGGL((k_count_nonil_str<uint16_t>), g, blk, 0, st, (const uint16_t *) b->theap, heap, (size_t) 8192, hs, ci.dense, ci.seq, ci.oids, ci.n, d); break;
+			case 4: hipLaunchKernelGGL((k_count_nonil_str<uint32_t>), g, blk, 0, st, (const uint32_t *) b->theap, heap, (size_t) 0, hs, ci.dense, ci.seq, ci.oids, ci.n, d); break;
+			default: hipLaunchKernelGGL((k_count_nonil_str<uint64_t>), g, blk, 0, st, (const uint64_t *) b->theap, heap, (size_t) 0, hs, ci.dense, ci.seq, ci.oids, ci.n, d); break;
+			}
+			break;
+		}
+		default:
+			seterr("BATcount_no_nil: type %s is not on the device path", atomname(b->ttype));
+			return MGDK_BUN_NONE;
+		}
+		unsigned long long h = 0;
+		if (!hip_ok(hipGetLastError(), "k_count_nonil") ||
+		    !hip_ok(hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, st), "hipMemcpyAsync") || !sync())
+			return MGDK_BUN_NONE;
+		cnt = (BUN) h;
+	}
+	if (cnt == b->count) {            // gdk_batop.c:3179 "we learned something"
+		b->tnonil = 1;
+		b->tnil = 0;
+	}
+	return cnt;
+}

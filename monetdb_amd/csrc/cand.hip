@@ -141,6 +141,26 @@ cl_of(const mgdk_bat *b, CL *c, mgdk_bat **own)
 
 // a sorted, duplicate-free oid BAT of n values: properties, and void when
 // dense (virtualize, gdk_select.c:31)
+// all candidates as a new candidate list (canditer_slice)
+mgdk_bat *
+mgdk::cand_slice(const Cand &ci)
+{
+	if (ci.dense)
+		return mgdk_BATdense(0, ci.seq, ci.n);
+	mgdk_bat *bn = newbat(0, MGDK_oid, ci.n);
+	if (bn == nullptr)
+		return nullptr;
+	if (!hip_ok(hipMemcpyAsync(bn->theap, ci.oids, ci.n * sizeof(oid), hipMemcpyDeviceToDevice, stream()),
+		    "hipMemcpyAsync") || !sync()) {
+		mgdk_BBPunfix(bn);
+		return nullptr;
+	}
+	bn->count = ci.n;
+	bn->tsorted = bn->tkey = bn->tnonil = 1;
+	bn->trevsorted = ci.n <= 1;
+	return bn;
+}
+
 mgdk_bat *
 mgdk::cand_finish(mgdk_bat *bn, BUN n)
 {

@@ -1735,3 +1735,168 @@ mgdk_BATrangejoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *rl, mgd
 		mgdk_BBPunfix(b);
 	return 0;
 }
+
+// ---- cross products (gdk/gdk_cross.c) ---------------------------------------
+
+namespace {
+
+__device__ __forceinline__ oid
+cross_oid(bool dense, oid seq, const oid *oids, BUN i)
+{
+	return dense ? seq + i : oids[i];
+}
+
+// pair p = i * n2 + j of the l-major product: r1[p] = left candidate i,
+// r2[p] = right candidate j (BATcrossci's two loops, gdk_cross.c:95-118).
+// 32-bit index arithmetic when the product fits
+template <typename I>
+__global__ void
+k_cross(oid *__restrict__ r1, oid *__restrict__ r2, bool d1, oid s1, const oid *o1, bool d2, oid s2, const oid *o2,
+	I n2, I total)
+{
+	for (I p = blockIdx.x * (I) blockDim.x + threadIdx.x; p < total; p += (I) gridDim.x * blockDim.x) {
+		const I i = p / n2, j = p - i * n2;
+		r1[p] = cross_oid(d1, s1, o1, i);
+		if (r2)
+			r2[p] = cross_oid(d2, s2, o2, j);
+	}
+}
+
+// a void column of n nil oids (BATtseqbase(bn, oid_nil), gdk_bat.c:2167)
+mgdk_bat *
+nil_void(BUN n)
+{
+	mgdk_bat *b = mgdk_BATdense(0, 0, 0);
+	if (b == nullptr)
+		return nullptr;
+	b->tseqbase = MGDK_OID_NIL;
+	b->count = n;
+	b->tsorted = b->trevsorted = 1;
+	b->tkey = n <= 1;
+	b->tnonil = n == 0;
+	b->tnil = n > 0;
+	return b;
+}
+
+// BATcrossci (gdk_cross.c:22): the special cases return candidate slices and
+// constants, the general case the l-major pairs
+int
+crossci(const Cand &c1, const Cand &c2, mgdk_bat **r1p, mgdk_bat **r2p)
+{
+	Own a, b;
+	if (c1.n == 0 || c2.n == 0) {
+		a.b = mgdk_BATdense(0, 0, 0);
+		if (a.b == nullptr || (r2p && (b.b = mgdk_BATdense(0, 0, 0)) == nullptr))
+			return -1;
+	} else if (c2.n == 1) {
+		if ((a.b = cand_slice(c1)) == nullptr)
+			return -1;
+		if (r2p) {
+			const oid v = c2.first;
+			b.b = c1.n == 1 ? cand_slice(c2) : mgdk_BATconstant(0, MGDK_oid, &v, c1.n);
+			if (b.b == nullptr)
+				return -1;
+		}
+	} else if (c1.n == 1) {
+		const oid v = c1.first;
+		if ((a.b = mgdk_BATconstant(0, MGDK_oid, &v, c2.n)) == nullptr ||
+		    (r2p && (b.b = cand_slice(c2)) == nullptr))
+			return -1;
+	} else {
+		if (c1.n > (BUN) MGDK_BUN_NONE / c2.n) {
+			seterr("BATsubcross: result too large");
+			return -1;
+		}
+		const BUN total = c1.n * c2.n;
+		if ((a.b = newbat(0, MGDK_oid, total)) == nullptr || (r2p && (b.b = newbat(0, MGDK_oid, total)) == nullptr))
+			return -1;
+		ProfScope prof("crossproduct");
+		oid *p1 = (oid *) a.b->theap, *p2 = r2p ? (oid *) b.b->theap : nullptr;
+		const unsigned grid = grid_for(total, BLOCK * 8, 256u * 64u);
+		if (total <= 0xffffffffu)
+			hipLaunchKernelGGL((k_cross<uint32_t>), dim3(grid), dim3(BLOCK), 0, stream(), p1, p2, c1.dense, c1.seq,
+					   c1.oids, c2.dense, c2.seq, c2.oids, (uint32_t) c2.n, (uint32_t) total);
+		else
+			hipLaunchKernelGGL((k_cross<uint64_t>), dim3(grid), dim3(BLOCK), 0, stream(), p1, p2, c1.dense, c1.seq,
+					   c1.oids, c2.dense, c2.seq, c2.oids, (uint64_t) c2.n, (uint64_t) total);
+		if (!hip_ok(hipGetLastError(), "k_cross") || !sync())
+			return -1;
+		a.b->count = total;
+		a.b->tsorted = a.b->tnonil = 1;
+		a.b->tnil = 0;
+		a.b->trevsorted = 0;     // c1.n > 1
+		a.b->tkey = 0;           // c2.n > 1
+		if (r2p) {
+			b.b->count = total;
+			b.b->tnonil = 1;
+			b.b->tnil = b.b->tsorted = b.b->trevsorted = b.b->tkey = 0;
+		}
+	}
+	*r1p = a.release();
+	if (r2p)
+		*r2p = b.release();
+	return 0;
+}
+
+// the candidates of b (complex lists unmasked first, as the joins do)
+int
+cross_cands(mgdk_bat *b, mgdk_bat *s, Cand *ci, Held &held)
+{
+	if (b == nullptr) {
+		seterr("BATsubcross: inputs must not be NULL");
+		return -1;
+	}
+	if (s && is_complex_cand(s) && (s = held.keep(unmask_cand(s))) == nullptr)
+		return -1;
+	return cand_init(ci, b, s);
+}
+
+}  // namespace
+
+// BATsubcross (gdk_cross.c:138): every (left, right) candidate pair, left-major;
+// max_one: at most one right candidate when there is a left one
+extern "C" int
+mgdk_BATsubcross(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, bool max_one)
+{
+	*r1p = nullptr;
+	if (r2p)
+		*r2p = nullptr;
+	Held held;
+	Cand c1, c2;
+	if (cross_cands(l, sl, &c1, held) < 0 || cross_cands(r, sr, &c2, held) < 0)
+		return -1;
+	if (max_one && c1.n > 0 && c2.n > 1) {
+		seterr("more than one match");
+		return -1;
+	}
+	return crossci(c1, c2, r1p, r2p);
+}
+
+// BAToutercross (gdk_cross.c:153): the left outer form; no right candidate
+// pairs every left one with nil
+extern "C" int
+mgdk_BAToutercross(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, mgdk_bat *sl, mgdk_bat *sr, bool max_one)
+{
+	*r1p = nullptr;
+	if (r2p)
+		*r2p = nullptr;
+	Held held;
+	Cand c1, c2;
+	if (cross_cands(l, sl, &c1, held) < 0 || cross_cands(r, sr, &c2, held) < 0)
+		return -1;
+	if (max_one && c1.n > 0 && c2.n > 1) {
+		seterr("more than one match");
+		return -1;
+	}
+	if (c1.n == 0 || c2.n == 0) {
+		Own a, b;
+		a.b = c1.n == 0 ? nil_void(0) : cand_slice(c1);
+		if (a.b == nullptr || (r2p && (b.b = nil_void(c1.n)) == nullptr))
+			return -1;
+		*r1p = a.release();
+		if (r2p)
+			*r2p = b.release();
+		return 0;
+	}
+	return crossci(c1, c2, r1p, r2p);
+}

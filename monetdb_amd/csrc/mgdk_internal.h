@@ -179,6 +179,9 @@ struct Cand {
 };
 // canditer_init (gdk/gdk_cand.c:407): clip s to b's [hseqbase, hseqbase+count)
 int cand_init(Cand *ci, const mgdk_bat *b, const mgdk_bat *s);
+// all of ci's candidates as a new candidate list, hseqbase 0 (canditer_slice,
+// gdk_cand.c; select.hip): void when dense
+mgdk_bat *cand_slice(const Cand &ci);
 // index of candidate oid o in ci (canditer_search); BUN NONE-like ~0 on error
 BUN cand_index(const Cand &ci, oid o);
 // one oid of an oid / void column (host read)

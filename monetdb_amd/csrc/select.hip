@@ -701,26 +701,6 @@ empty_result()
 	return mgdk_BATdense(0, 0, 0);
 }
 
-// all candidates as a new candidate list (canditer_slice)
-static mgdk_bat *
-cand_slice(const Cand &ci)
-{
-	if (ci.dense)
-		return mgdk_BATdense(0, ci.seq, ci.n);
-	mgdk_bat *bn = newbat(0, MGDK_oid, ci.n);
-	if (bn == nullptr)
-		return nullptr;
-	if (!hip_ok(hipMemcpyAsync(bn->theap, ci.oids, ci.n * sizeof(oid), hipMemcpyDeviceToDevice, stream()),
-		    "hipMemcpyAsync") || !sync()) {
-		mgdk_BBPunfix(bn);
-		return nullptr;
-	}
-	bn->count = ci.n;
-	bn->tsorted = bn->tkey = bn->tnonil = 1;
-	bn->trevsorted = ci.n <= 1;
-	return bn;
-}
-
 template <typename T>
 static mgdk_bat *run_scan_bits(const mgdk_bat *b, const Cand &ci, const SelPred<T> &pred, const SelMap &cm);
 

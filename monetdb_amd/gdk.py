@@ -207,6 +207,9 @@ _SIGS = {
     "mgdk_BATsemijoin": (C.c_int, [PP, PP, P, P, P, P, C.c_bool, C.c_bool, C.c_uint64]),
     "mgdk_BATleftjoin": (C.c_int, [PP, PP, P, P, P, P, C.c_bool, C.c_uint64]),
     "mgdk_BATthetajoin": (C.c_int, [PP, PP, P, P, P, P, C.c_int, C.c_bool, C.c_uint64]),
+    "mgdk_BATsubcross": (C.c_int, [PP, PP, P, P, P, P, C.c_bool]),
+    "mgdk_BATcount_no_nil": (C.c_uint64, [P, P]),
+    "mgdk_BAToutercross": (C.c_int, [PP, PP, P, P, P, P, C.c_bool]),
     "mgdk_BATbandjoin": (C.c_int, [PP, PP, P, P, P, P, C.c_void_p, C.c_void_p, C.c_bool, C.c_bool, C.c_uint64]),
     "mgdk_BATrangejoin": (C.c_int, [PP, PP, P, P, P, P, P, C.c_bool, C.c_bool, C.c_bool, C.c_bool, C.c_uint64]),
     "mgdk_BATouterjoin": (C.c_int, [PP, PP, P, P, P, P, C.c_bool, C.c_bool, C.c_uint64]),
@@ -964,6 +967,32 @@ def BATthetajoin(l, r, sl=None, sr=None, op=JOIN_LT, nil_matches=False, estimate
     _chk(lib().mgdk_BATthetajoin(C.byref(a), C.byref(b), l.ptr, r.ptr, _p(sl), _p(sr), op, nil_matches,
                                  estimate))
     return BAT(a), BAT(b)
+
+
+def BATcount_no_nil(b, s=None):
+    """BATcount_no_nil (gdk_batop.c:3078): candidates with a non-nil value"""
+    n = lib().mgdk_BATcount_no_nil(b.ptr, _p(s))
+    if n == BUN_NONE:
+        _chk(-1)
+    return n
+
+
+def BATsubcross(l, r, sl=None, sr=None, max_one=False, want_r2=True):
+    """BATsubcross (gdk_cross.c:138): every (left, right) candidate pair,
+    left-major; (r1, r2) or, without want_r2, r1"""
+    a, b = P(), P()
+    _chk(lib().mgdk_BATsubcross(C.byref(a), C.byref(b) if want_r2 else None, l.ptr, r.ptr, _p(sl), _p(sr),
+                                max_one))
+    return (BAT(a), BAT(b)) if want_r2 else BAT(a)
+
+
+def BAToutercross(l, r, sl=None, sr=None, max_one=False, want_r2=True):
+    """BAToutercross (gdk_cross.c:153): as BATsubcross; no right candidate
+    pairs every left one with nil"""
+    a, b = P(), P()
+    _chk(lib().mgdk_BAToutercross(C.byref(a), C.byref(b) if want_r2 else None, l.ptr, r.ptr, _p(sl), _p(sr),
+                                  max_one))
+    return (BAT(a), BAT(b)) if want_r2 else BAT(a)
 
 
 def BATbandjoin(l, r, c1, c2, sl=None, sr=None, linc=True, hinc=True, estimate=0):

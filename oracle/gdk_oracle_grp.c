@@ -1725,3 +1725,33 @@ ora_calcavg(const ora_bat *b, const ora_bat *s, double *avg, uint64_t *vals, int
 		*vals = n;
 	return 0;
 }
+
+/* BATcount_no_nil (gdk/gdk_batop.c:3078): candidates with a non-nil value;
+ * nonil / msk: every candidate, void: none when the sequence is nil */
+uint64_t
+ora_count_no_nil(const ora_bat *b, const ora_bat *s)
+{
+	ora_ci ci;
+	uint64_t cnt = 0;
+	if (ora_ci_init(&ci, b, s) < 0)
+		return 0;
+	if (b->nonil || b->type == ORA_msk)
+		return ci.n;
+	if (b->type == ORA_void)
+		return b->tseqbase == ORA_OID_NIL ? 0 : ci.n;
+	for (uint64_t i = 0; i < ci.n; i++) {
+		uint64_t p = ci_get(&ci, i) - b->hseqbase;
+		ora_hge v;
+		if (b->type == ORA_str)
+			cnt += (unsigned char) str_of(b, p)[0] != 0x80;
+		else if (b->type == ORA_flt)
+			cnt += ((const float *) b->base)[p] == ((const float *) b->base)[p];
+		else if (b->type == ORA_dbl)
+			cnt += ((const double *) b->base)[p] == ((const double *) b->base)[p];
+		else if (b->type == ORA_daytime || b->type == ORA_timestamp)
+			cnt += ((const int64_t *) b->base)[p] != INT64_MIN;
+		else
+			cnt += !val_at(b, p, &v);
+	}
+	return cnt;
+}

@@ -2002,3 +2002,126 @@ ora_leftjoin_ex(ora_bat **r1p, ora_bat **r2p, ora_bat **r3p, ora_bat *l, ora_bat
 		*r3p = z;
 	return 0;
 }
+
+/* ---- cross products (gdk/gdk_cross.c) ---------------------------------- */
+
+/* canditer_slice (gdk_cand.c): all candidates, hseqbase 0; void when dense */
+static ora_bat *
+cross_slice(const ora_ci *ci)
+{
+	if (ci->dense)
+		return ora_dense(0, ci->seq, ci->n);
+	ora_bat *b = ora_new(ORA_oid, ci->n, 0);
+	if (b == NULL)
+		return NULL;
+	for (uint64_t i = 0; i < ci->n; i++)
+		((ora_oid *) b->base)[i] = ci->oids[i];
+	b->sorted = b->key = b->nonil = 1;
+	b->revsorted = ci->n <= 1;
+	return b;
+}
+
+/* BATconstant (gdk_bat.c) of an oid */
+static ora_bat *
+cross_const(ora_oid v, uint64_t n)
+{
+	ora_bat *b = ora_new(ORA_oid, n, 0);
+	if (b == NULL)
+		return NULL;
+	for (uint64_t i = 0; i < n; i++)
+		((ora_oid *) b->base)[i] = v;
+	b->sorted = b->revsorted = b->nonil = 1;
+	b->key = n <= 1;
+	return b;
+}
+
+/* a void column of n nil oids (BATtseqbase(bn, oid_nil), gdk_bat.c:2167) */
+static ora_bat *
+cross_nilvoid(uint64_t n)
+{
+	ora_bat *b = ora_dense(0, ORA_OID_NIL, n);
+	if (b == NULL)
+		return NULL;
+	b->sorted = b->revsorted = 1;
+	b->key = n <= 1;
+	b->nonil = n == 0;
+	b->nil = n > 0;
+	return b;
+}
+
+/* BATcrossci (gdk_cross.c:22) */
+static int
+cross_ci(ora_bat **r1p, ora_bat **r2p, const ora_ci *c1, const ora_ci *c2)
+{
+	ora_bat *a = NULL, *b = NULL;
+	if (c1->n == 0 || c2->n == 0) {
+		a = ora_dense(0, 0, 0);
+		if (r2p)
+			b = ora_dense(0, 0, 0);
+	} else if (c2->n == 1) {
+		a = cross_slice(c1);
+		if (r2p)
+			b = c1->n == 1 ? cross_slice(c2) : cross_const(ci_get(c2, 0), c1->n);
+	} else if (c1->n == 1) {
+		a = cross_const(ci_get(c1, 0), c2->n);
+		if (r2p)
+			b = cross_slice(c2);
+	} else {
+		uint64_t n = c1->n * c2->n, p = 0;
+		a = ora_new(ORA_oid, n, 0);
+		if (r2p)
+			b = ora_new(ORA_oid, n, 0);
+		if (a && (b || !r2p)) {
+			/* :95-101 left oid repeated, :112-118 the right list again per left */
+			for (uint64_t i = 0; i < c1->n; i++)
+				for (uint64_t j = 0; j < c2->n; j++, p++) {
+					((ora_oid *) a->base)[p] = ci_get(c1, i);
+					if (b)
+						((ora_oid *) b->base)[p] = ci_get(c2, j);
+				}
+			a->sorted = a->nonil = 1;
+			a->revsorted = a->key = 0;
+			if (b) {
+				b->nonil = 1;
+				b->sorted = b->revsorted = b->key = 0;
+			}
+		}
+	}
+	if (a == NULL || (r2p && b == NULL)) {
+		ora_free(a);
+		ora_free(b);
+		ora_seterr("malloc");
+		return -1;
+	}
+	*r1p = a;
+	if (r2p)
+		*r2p = b;
+	return 0;
+}
+
+/* BATsubcross (gdk_cross.c:138); outer: BAToutercross (:153) */
+int
+ora_crossproduct(ora_bat **r1p, ora_bat **r2p, const ora_bat *l, const ora_bat *r, const ora_bat *sl,
+		 const ora_bat *sr, bool max_one, bool outer)
+{
+	ora_ci c1, c2;
+	if (ora_ci_init(&c1, l, sl) < 0 || ora_ci_init(&c2, r, sr) < 0)
+		return -1;
+	if (max_one && c1.n > 0 && c2.n > 1) {
+		ora_seterr("more than one match");
+		return -1;
+	}
+	if (outer && (c1.n == 0 || c2.n == 0)) {
+		ora_bat *a = c1.n == 0 ? cross_nilvoid(0) : cross_slice(&c1), *b = NULL;
+		if (a == NULL || (r2p && (b = cross_nilvoid(c1.n)) == NULL)) {
+			ora_free(a);
+			ora_seterr("malloc");
+			return -1;
+		}
+		*r1p = a;
+		if (r2p)
+			*r2p = b;
+		return 0;
+	}
+	return cross_ci(r1p, r2p, &c1, &c2);
+}

@@ -131,6 +131,9 @@ def lib():
         L.ora_semijoin_cands.argtypes = [P, P, P, P, C.c_bool, C.c_bool, C.c_bool, C.c_bool]
         L.ora_leftjoin.argtypes = [C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool, C.c_bool, C.c_bool]
         L.ora_markjoin.argtypes = [C.POINTER(P), C.POINTER(P), C.POINTER(P), P, P, P, P]
+        L.ora_count_no_nil.argtypes = [P, P]
+        L.ora_count_no_nil.restype = C.c_uint64
+        L.ora_crossproduct.argtypes = [C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool, C.c_bool]
         L.ora_minmax.argtypes = [P, C.c_bool, C.c_bool, C.c_void_p, C.POINTER(C.c_char_p)]
         L.ora_prod.argtypes = [C.c_void_p, C.c_int, P, P, C.c_bool, C.c_bool]
         L.ora_groupprod.restype = P
@@ -546,6 +549,20 @@ def BATjoin(l, r, sl=None, sr=None, nil_matches=False):
                       sr.ptr if sr else None, nil_matches) < 0:
         raise _err()
     return Bat(a), Bat(b)
+
+
+def BATcount_no_nil(b, s=None):
+    """gdk_batop.c:3078"""
+    return int(lib().ora_count_no_nil(b.ptr, s.ptr if s else None))
+
+
+def crossproduct(l, r, sl=None, sr=None, max_one=False, outer=False, want_r2=True):
+    """BATsubcross (gdk_cross.c:138) / BAToutercross (:153)"""
+    a, b = P(), P()
+    if lib().ora_crossproduct(C.byref(a), C.byref(b) if want_r2 else None, l.ptr, r.ptr,
+                              sl.ptr if sl else None, sr.ptr if sr else None, max_one, outer) < 0:
+        raise _err()
+    return (Bat(a), Bat(b)) if want_r2 else Bat(a)
 
 
 def BATmarkjoin(l, r, sl=None, sr=None, want_r2=True):
