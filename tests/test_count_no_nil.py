@@ -78,7 +78,7 @@ def test_gpu_count_no_nil_str(gdk, ora, width):
     from strheap import NIL, WORDS, sample
     r = rng(2613)
     n = 50_000
-    t, h, wi = sample(r, n, width)
+    t, h, wi = sample(r, n, width, copies=2 if width == 1 else 6)
     B = gdk.BAT.from_numpy(gdk.TYPE_str, t, vheap=h, sorted_=False, revsorted=False, key=False, nonil=False)
     O = ora.Bat.from_array(ora.TYPE_str, t, vheap=h)
     isnil = np.asarray([WORDS[k] == NIL for k in wi])
