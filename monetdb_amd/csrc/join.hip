@@ -478,6 +478,7 @@ side_init(Side &s, const mgdk_bat *b, const Cand &c)
 int
 sync_fail()
 {
+	(void) side_join();                 // work queued on the side stream too
 	(void) sync();
 	return -1;
 }
@@ -1170,24 +1171,23 @@ k_pj_delta(const uint32_t *offT, const uint32_t *poff, const uint32_t *pbase, ui
 	}
 }
 
-// one workgroup per subtile (ticketed): matches back into row order; the
-// subtile's probe results are the contiguous range [offT[sub][0],
-// offT[sub + 1][0]) of the flat array
-// the subtile's matches back in row order (shared by both restores):
-// res[r + r / 32] = match position + 1 of row r (0: none); output offset by
-// decoupled look-back over the subtiles (numbered by ticket)
+// the emit's LDS (per workgroup)
+struct EmitLds {
+	uint32_t rmask[1024], rbase[1024], wsum[16];
+	uint64_t pre;
+};
+
+// first half: thread tid counts the rows [32 tid, 32 tid + 32) -- a match
+// mask and the run's exclusive offset, so the write below can walk the rows
+// in order (consecutive lanes -> consecutive positions) without barriers --
+// and wave 0 takes the subtile's output offset by look-back (in e.pre after
+// the closing barrier)
 __device__ __forceinline__ void
-pj_emit(const uint32_t *res, uint32_t sub, BUN a, uint32_t rows, uint32_t nsub, const Side &L, const Side &R,
-	uint64_t *status, uint64_t *meta, oid *r1, oid *r2)
+pj_emit_scan(const uint32_t *res, uint32_t sub, uint32_t rows, uint32_t nsub, uint64_t *status, uint64_t *meta,
+	     EmitLds &e)
 {
-	__shared__ uint32_t wsum[16];
-	__shared__ uint64_t s_pre;
 	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
-	// thread tid counts the rows [32 tid, 32 tid + 32): a match mask and the
-	// run's exclusive offset, so the output pass below can walk the rows in
-	// order (consecutive lanes -> consecutive positions) without barriers
 	static_assert(PJ_SUBROWS == 32 * 1024, "32 rows per thread");
-	__shared__ uint32_t rmask[1024], rbase[1024];
 	const uint32_t r0 = tid * 32, rb = tid * 33;
 	uint32_t msk = 0;
 #pragma unroll
@@ -1202,36 +1202,58 @@ pj_emit(const uint32_t *res, uint32_t sub, BUN a, uint32_t rows, uint32_t nsub, 
 			x += u;
 	}
 	if (lane == 63)
-		wsum[w] = x;
+		e.wsum[w] = x;
 	__syncthreads();
 	uint32_t wpre = 0, tot = 0;
 	for (uint32_t q = 0; q < 16; q++) {
-		wpre += q < w ? wsum[q] : 0;
-		tot += wsum[q];
+		wpre += q < w ? e.wsum[q] : 0;
+		tot += e.wsum[q];
 	}
-	rmask[tid] = msk;
-	rbase[tid] = wpre + x - c;
+	e.rmask[tid] = msk;
+	e.rbase[tid] = wpre + x - c;
 	if (w == 0) {
 		const uint64_t pre = lookback(status, sub, tot, (uint32_t *) &meta[1]);
 		if (lane == 0) {
-			s_pre = pre;
+			e.pre = pre;
 			if (sub == nsub - 1)
 				meta[0] = pre + tot;
 		}
 	}
 	__syncthreads();
-	const uint64_t pre = s_pre;
-	for (uint32_t r = tid; r < rows; r += blockDim.x) {
+}
+
+// second half: the pairs of the matched rows at their output positions
+__device__ __forceinline__ void
+pj_emit_write(const uint32_t *res, BUN a, uint32_t rows, const Side &L, const Side &R, const EmitLds &e, oid *r1,
+	      oid *r2)
+{
+	const uint64_t pre = e.pre;
+	for (uint32_t r = threadIdx.x; r < rows; r += blockDim.x) {
 		const uint32_t run = r >> 5, bit = r & 31;
-		const uint32_t mk = rmask[run];
+		const uint32_t mk = e.rmask[run];
 		if ((mk >> bit) & 1) {
-			const uint64_t o = pre + rbase[run] + __popc(mk & ((1u << bit) - 1));
+			const uint64_t o = pre + e.rbase[run] + __popc(mk & ((1u << bit) - 1));
 			r1[o] = oid_of(L, a + r);
 			r2[o] = oid_of(R, res[r + run] - 1);
 		}
 	}
 }
 
+// the subtile's matches back in row order (shared by both restores):
+// res[r + r / 32] = match position + 1 of row r (0: none); output offset by
+// decoupled look-back over the subtiles (numbered by ticket)
+__device__ __forceinline__ void
+pj_emit(const uint32_t *res, uint32_t sub, BUN a, uint32_t rows, uint32_t nsub, const Side &L, const Side &R,
+	uint64_t *status, uint64_t *meta, oid *r1, oid *r2)
+{
+	__shared__ EmitLds e;
+	pj_emit_scan(res, sub, rows, nsub, status, meta, e);
+	pj_emit_write(res, a, rows, L, R, e, r1, r2);
+}
+
+// one workgroup per subtile (ticketed): matches back into row order; the
+// subtile's probe results are the contiguous range [offT[sub][0],
+// offT[sub + 1][0]) of the flat array
 __global__ __launch_bounds__(1024) void
 k_pj_restore(const uint2 *flat, const uint32_t *offT, uint32_t P, uint64_t total, BUN n, uint32_t nsub, Side L,
 	     Side R, uint32_t *ticket, uint64_t *status, uint64_t *meta, oid *r1, oid *r2)
@@ -1434,6 +1456,9 @@ k_pj2_offt(const uint16_t *poff, uint32_t nsub, uint32_t P, uint16_t *poffT)
 
 #ifndef PJ2_SIDE
 #define PJ2_SIDE 1      // the probe side's cut on the thread's side stream, beside the build side's passes
+#endif
+#ifndef PJ2_SWAP
+#define PJ2_SWAP 1      // 1: the build side's cut on the side stream, the probe side's on the main one
 #endif
 #ifndef PJ2_RALL
 #define PJ2_RALL 1      // the restore loads all of a subtile's entries at once (0: four rounds of 8 per thread)
@@ -1884,6 +1909,94 @@ k_pj2_restore(const uint16_t *prow, const uint32_t *pans, const uint16_t *poff, 
 	pj_emit(res, sub, a, rows, nsub, L, R, status, meta, r1, r2);
 }
 
+// persistent restore (PJ2_RP=1): one 1024-thread workgroup per CU (the
+// 143 KB of LDS allow no second) claims subtiles by ticket and loads the
+// next subtile's answers and rows while it writes the current one's pairs,
+// so a CU's reads and writes overlap instead of alternating.  The loads take
+// the whole 32K-entry region (in bounds: the region holds PJ_SUBROWS entries)
+// and the scatter masks entries past the subtile's count.  Claims in ticket
+// order keep the look-back deadlock-free: the lowest unpublished subtile's
+// owner waits on nothing unpublished.
+#ifndef PJ2_RP
+#define PJ2_RP 0
+#endif
+
+typedef uint32_t pj_u4 __attribute__((ext_vector_type(4)));
+typedef uint32_t pj_u2 __attribute__((ext_vector_type(2)));
+struct Pj2Ent {
+	pj_u4 am[8];
+	pj_u2 ar[8];
+	uint32_t cnt;
+};
+
+__device__ __forceinline__ void
+pj2_rload(const uint16_t *prow, const uint32_t *pans, const uint16_t *poff, uint32_t P, uint32_t sub, Pj2Ent &x)
+{
+	const BUN a = (BUN) sub * PJ_SUBROWS;
+	x.cnt = poff[(size_t) sub * (P + 1) + P];
+#pragma unroll
+	for (int q = 0; q < 8; q++) {
+		const uint32_t j = 4 * (threadIdx.x + 1024 * q);
+		x.am[q] = __builtin_nontemporal_load((const pj_u4 *) (pans + a + j));
+		x.ar[q] = __builtin_nontemporal_load((const pj_u2 *) (prow + a + j));
+	}
+}
+
+__device__ __forceinline__ void
+pj2_rscatter(const Pj2Ent &x, uint32_t *res)
+{
+#pragma unroll
+	for (int q = 0; q < 8; q++) {
+		const uint32_t j = 4 * (threadIdx.x + 1024 * q);
+#pragma unroll
+		for (int c = 0; c < 4; c++) {
+			const uint32_t m = x.am[q][c], r = (x.ar[q][c >> 1] >> (16 * (c & 1))) & 0xffffu;
+			if (j + c < x.cnt && m)
+				res[r + (r >> 5)] = m;
+		}
+	}
+}
+
+__global__ __launch_bounds__(1024) void
+k_pj2_restore_p(const uint16_t *prow, const uint32_t *pans, const uint16_t *poff, uint32_t P, BUN n, uint32_t nsub,
+		Side L, Side R, uint32_t *ticket, uint64_t *status, uint64_t *meta, oid *r1, oid *r2)
+{
+	__shared__ uint32_t res[PJ_SUBROWS + PJ_SUBROWS / 32];
+	__shared__ EmitLds e;
+	__shared__ uint32_t s_sub;
+	const unsigned tid = threadIdx.x;
+	if (tid == 0)
+		s_sub = atomicAdd(ticket, 1u);
+	for (uint32_t i = tid; i < PJ_SUBROWS + PJ_SUBROWS / 32; i += blockDim.x)
+		res[i] = 0;
+	__syncthreads();
+	uint32_t sub = s_sub;
+	Pj2Ent x;
+	if (sub < nsub)
+		pj2_rload(prow, pans, poff, P, sub, x);
+	while (sub < nsub) {
+		uint32_t nxt = 0;
+		if (tid == 0)
+			nxt = atomicAdd(ticket, 1u);
+		pj2_rscatter(x, res);
+		if (tid == 0)
+			s_sub = nxt;        // every read of the previous value is behind two barriers
+		__syncthreads();
+		const BUN a = (BUN) sub * PJ_SUBROWS;
+		const uint32_t rows = (uint32_t) min((BUN) PJ_SUBROWS, n - a);
+		pj_emit_scan(res, sub, rows, nsub, status, meta, e);
+		const uint32_t ns = s_sub;
+		if (ns < nsub)
+			pj2_rload(prow, pans, poff, P, ns, x);      // in flight during the writes
+		pj_emit_write(res, a, rows, L, R, e, r1, r2);
+		__syncthreads();
+		for (uint32_t i = tid; i < PJ_SUBROWS + PJ_SUBROWS / 32; i += blockDim.x)
+			res[i] = 0;
+		__syncthreads();
+		sub = ns;
+	}
+}
+
 // one side cut into partitions: cnt/off matrices, partition bases, entries
 struct PjSide {
 	uint32_t nsub = 0;
@@ -1899,9 +2012,10 @@ struct PjSide {
 };
 
 int
-pj_cut(const Side &S, BUN n, int pbits, bool skipnil, PjSide &o, uint32_t *maxtot_dev)
+pj_cut(const Side &S, BUN n, int pbits, bool skipnil, PjSide &o, uint32_t *maxtot_dev, hipStream_t st = nullptr)
 {
-	hipStream_t st = stream();
+	if (st == nullptr)
+		st = stream();
 	const uint32_t P = 1u << pbits;
 	o.nsub = (uint32_t) ((n + PJ_SUBROWS - 1) / PJ_SUBROWS);
 	const size_t m = (size_t) o.nsub * P * 4 + 64;
@@ -1938,7 +2052,8 @@ join_part2(const Side &L, BUN nl, const Side &R, BUN nr, const PjSide &B, int pb
 	const uint32_t nsub = (uint32_t) ((nl + PJ_SUBROWS - 1) / PJ_SUBROWS);
 	const size_t rsz = (size_t) nsub * PJ_SUBROWS;
 	if (nl == 0 || rsz >= ((size_t) 1 << 32)) {
-		(void) sync();                              // the build side's cut still uses its buffers
+		(void) side_join();                         // the build side's cut still uses its buffers
+		(void) sync();
 		return 1;                                   // (entry indexes are 32-bit)
 	}
 	DevBuf pkey(rsz * 4 + 64), prow(rsz * 2 + 64), pans(rsz * 4 + 64), poff((size_t) nsub * (P + 1) * 2 + 64),
@@ -1951,7 +2066,8 @@ join_part2(const Side &L, BUN nl, const Side &R, BUN nr, const PjSide &B, int pb
 							   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
 	(void) hipGetLastError();
 	if (!cut_attr || !probe_attr) {
-		(void) sync();                              // the build side's cut still uses its buffers
+		(void) side_join();                         // the build side's cut still uses its buffers
+		(void) sync();
 		return 1;                                   // the kernels cannot get their LDS: fallback
 	}
 	// the table is sized for the expected largest build partition (mean + 6
@@ -1962,7 +2078,8 @@ join_part2(const Side &L, BUN nl, const Side &R, BUN nr, const PjSide &B, int pb
 	const double mean = (double) nr / P;
 	const uint32_t est = (uint32_t) (mean + 6.0 * sqrt(mean)) + 1;
 	if (est > PJ2_MAXFILL) {
-		(void) sync();                              // the build side's cut still uses its buffers
+		(void) side_join();                         // the build side's cut still uses its buffers
+		(void) sync();
 		return 1;
 	}
 	static const int lfpct = getenv("MGDK_PJ_LF") ? atoi(getenv("MGDK_PJ_LF")) : 80;
@@ -1983,21 +2100,28 @@ join_part2(const Side &L, BUN nl, const Side &R, BUN nr, const PjSide &B, int pb
 	(void) hipGetLastError();
 	DevBuf gtab((size_t) P * 2 * nbp * 8 + 64);
 	if (!tb_attr || !gtab.p) {
-		(void) sync();                              // the build side's cut still uses its buffers
+		(void) side_join();                         // the build side's cut still uses its buffers
+		(void) sync();
 		return tb_attr ? -1 : 1;
 	}
 	const unsigned long long *gtp = gtab.as<unsigned long long>();
 #else
 	const unsigned long long *gtp = nullptr;
 #endif
-	// the probe side's cut depends on nothing the build side's (queued on st)
-	// writes: it runs on the side stream, beside the build side's passes,
-	// whose few workgroups leave CUs idle (PJ2_SIDE=0: one stream)
+	// the probe side's cut depends on nothing the build side's writes: it runs
+	// on the side stream, beside the build side's passes, whose few
+	// workgroups leave CUs idle (PJ2_SIDE=0: one stream; PJ2_SWAP: the build
+	// side is the one on the side stream).  join_part forked the side stream.
 	hipStream_t cs = st;
-#if PJ2_SIDE
+#if PJ2_SIDE && !PJ2_SWAP
 	if (stream2() != nullptr)
 		cs = stream2();
 #endif
+	// the restore's ticket and look-back words, cleared while the cuts run
+	const size_t sbytes = (nsub + 8) * sizeof(uint64_t);
+	char *sc = (char *) scratch(sbytes);
+	if (!sc || !hip_ok(hipMemsetAsync(sc, 0, sbytes, st), "memset"))
+		return sync_fail();
 	hipLaunchKernelGGL(k_pj2_cut, dim3(nsub), dim3(1024), PJ2_CUT_LDS, cs, L, nl, pbits, !nil_matches,
 			   pkey.as<uint32_t>(), prow.as<uint16_t>(), poff.as<uint16_t>());
 	hipLaunchKernelGGL(k_pj2_offt, dim3((nsub + 63) / 64, (P + 1 + 63) / 64), dim3(256), 0, cs, poff.as<uint16_t>(),
@@ -2006,22 +2130,34 @@ join_part2(const Side &L, BUN nl, const Side &R, BUN nr, const PjSide &B, int pb
 	hipLaunchKernelGGL(k_pj2_tbuild, dim3(P), dim3(1024), (size_t) nbp * 16, st, B.ent->as<uint2>(),
 			   B.base->as<uint32_t>(), pbits, nbp, gtab.as<unsigned long long>(), &meta32[2]);
 #endif
-	if (cs != st && !side_join()) {
-		(void) hipStreamSynchronize(cs);
+#if PJ2_SIDE
+	if (stream2() != nullptr && !side_join())
 		return sync_fail();
-	}
+#endif
 	hipLaunchKernelGGL(k_pj2_probe, dim3(P), dim3(1024), lds, st, B.ent->as<uint2>(), B.base->as<uint32_t>(),
 			   pkey.as<uint32_t>(), poffT.as<uint16_t>(), pbits, nbp, nsub, pans.as<uint32_t>(), &meta32[2], gtp);
 	mgdk_bat *ra = newbat(0, MGDK_oid, nl), *rb = newbat(0, MGDK_oid, nl);
-	const size_t sbytes = (nsub + 8) * sizeof(uint64_t);
-	char *sc = (char *) scratch(sbytes);
-	if (!ra || !rb || !sc || !hip_ok(hipMemsetAsync(sc, 0, sbytes, st), "memset")) {
+	if (!ra || !rb) {
 		unfix2(ra, rb);
 		return sync_fail();
 	}
+#if PJ2_RP
+	static const unsigned ncu = [] {
+		int v = 0, d = 0;
+		if (hipGetDevice(&d) != hipSuccess ||
+		    hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || v <= 0)
+			v = 256;
+		(void) hipGetLastError();
+		return (unsigned) v;
+	}();
+	hipLaunchKernelGGL(k_pj2_restore_p, dim3(min(ncu, nsub)), dim3(1024), 0, st, prow.as<uint16_t>(),
+			   pans.as<uint32_t>(), poff.as<uint16_t>(), P, nl, nsub, L, R, (uint32_t *) sc, (uint64_t *) sc + 8,
+			   meta, (oid *) ra->theap, (oid *) rb->theap);
+#else
 	hipLaunchKernelGGL(k_pj2_restore, dim3(nsub), dim3(1024), 0, st, prow.as<uint16_t>(), pans.as<uint32_t>(),
 			   poff.as<uint16_t>(), P, nl, nsub, L, R, (uint32_t *) sc, (uint64_t *) sc + 8, meta,
 			   (oid *) ra->theap, (oid *) rb->theap);
+#endif
 	// a failed launch leaves pkey / pans / the results unwritten: fail the call
 	if (!hip_ok(hipGetLastError(), "join probe launch")) {
 		unfix2(ra, rb);
@@ -2090,8 +2226,24 @@ join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_b
 	PjSide B, Pr;
 	Side Rn = R;
 	Rn.nofit = &meta32[5];
-	if (pj_cut(Rn, nr, pbits, !nil_matches, B, &meta32[0]) < 0) {
-		(void) sync();                              // launched cuts still use the buffers
+	// the side stream (PJ2_SIDE) first waits for everything queued so far on
+	// the main one (the inputs' producers, the memset above); PJ2_SWAP: the
+	// build side's cut goes there and the probe side's cut stays on the main
+	// stream, so the probe follows the probe side's transpose with no
+	// cross-stream wait on the longer chain
+	hipStream_t bs = st;
+#if PJ2_SIDE
+	if (mode != 3 && stream2() != nullptr) {
+		if (!side_fork())
+			return sync_fail();
+#if PJ2_SWAP
+		bs = stream2();
+#endif
+	}
+#endif
+	if (pj_cut(Rn, nr, pbits, !nil_matches, B, &meta32[0], bs) < 0) {
+		(void) side_join();                         // launched cuts still use the buffers
+		(void) sync();
 		return -1;
 	}
 	if (mode != 3)

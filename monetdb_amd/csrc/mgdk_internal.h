@@ -25,6 +25,7 @@ bool hip_ok(hipError_t e, const char *what);
 hipStream_t stream();                       // per calling thread
 hipStream_t stream2();                      // the thread's side stream (NULL if it cannot be made)
 bool side_join();                           // the main stream waits for the side stream's queued work
+bool side_fork();                           // the side stream waits for the main stream's queued work
 void *dalloc(size_t bytes);                 // HBM, cached, >= 256 B aligned
 void dfree(void *p);
 // per-thread scratch (grows; valid until the next scratch() on this thread)

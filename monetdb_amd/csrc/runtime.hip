@@ -45,7 +45,7 @@ hip_ok(hipError_t e, const char *what)
 struct ThreadCtx {
 	hipStream_t s = nullptr;
 	hipStream_t s2 = nullptr;       // a side stream for independent passes of one operator
-	hipEvent_t ev2 = nullptr;
+	hipEvent_t ev2 = nullptr, ev1 = nullptr;
 	void *scratch = nullptr;
 	size_t scratch_size = 0;
 	void *pinned = nullptr;
@@ -67,6 +67,8 @@ struct ThreadCtx {
 			(void) hipHostFree(q);
 		if (ev2)
 			(void) hipEventDestroy(ev2);
+		if (ev1)
+			(void) hipEventDestroy(ev1);
 		if (s2)
 			(void) hipStreamDestroy(s2);
 		if (s)
@@ -97,6 +99,19 @@ stream2()
 			tctx.s2 = nullptr;
 	}
 	return tctx.s2;
+}
+
+bool
+side_fork()
+{
+	if (tctx.s2 == nullptr)
+		return true;
+	if (tctx.ev1 == nullptr && hipEventCreateWithFlags(&tctx.ev1, hipEventDisableTiming) != hipSuccess) {
+		tctx.ev1 = nullptr;
+		return hip_ok(hipStreamSynchronize(stream()), "main stream sync");
+	}
+	return hip_ok(hipEventRecord(tctx.ev1, stream()), "main stream event") &&
+	       hip_ok(hipStreamWaitEvent(tctx.s2, tctx.ev1, 0), "main stream wait");
 }
 
 bool
