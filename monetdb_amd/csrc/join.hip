@@ -1324,8 +1324,14 @@ constexpr uint32_t PJ2_MAXB = (160 * 1024 - 16 * 64 * 8) / 16;
 constexpr uint32_t PJ2_MAXFILL = PJ2_MAXB * 2 * 4 / 5;       // <= 80 % load
 
 __global__ __launch_bounds__(1024) void
-k_pj2_cut(Side s, BUN n, int pbits, bool skipnil, uint32_t *pkey, uint16_t *prow, uint16_t *poff)
+k_pj2_cut(Side s, BUN n, int pbits, bool skipnil, uint32_t *pkey, uint16_t *prow, uint16_t *poff, uint64_t *rzero)
 {
+	// the restore's ticket words and look-back status, cleared here instead
+	// of by a memset of their own: 8 words, then one per subtile
+	if (rzero != nullptr && threadIdx.x < 8 && (blockIdx.x == 0 || threadIdx.x == 0))
+		rzero[blockIdx.x == 0 ? threadIdx.x : 8 + blockIdx.x] = 0;
+	if (rzero != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
+		rzero[8] = 0;
 	extern __shared__ __attribute__((aligned(16))) uint32_t sm2[];
 	uint32_t *hist = sm2;                          // counters, then run starts
 	uint32_t *stk = sm2 + (1u << PJ_MAXPBITS);     // the run-ordered keys, then rows
@@ -1456,6 +1462,10 @@ k_pj2_offt(const uint16_t *poff, uint32_t nsub, uint32_t P, uint16_t *poffT)
 
 #ifndef PJ2_SIDE
 #define PJ2_SIDE 1      // the probe side's cut on the thread's side stream, beside the build side's passes
+#endif
+#ifndef PJ2_BC
+#define PJ2_BC 0        // 1: the build side cut like the probe side (k_pj2_cut, subtile-local runs; measured slower: the
+                        // probe then gathers ~16-entry runs from every build subtile, 444 against 270 us)
 #endif
 #ifndef PJ2_SWAP
 #define PJ2_SWAP 1      // 1: the build side's cut on the side stream, the probe side's on the main one
@@ -1713,9 +1723,14 @@ k_pj2_tbuild(const uint2 *bent, const uint32_t *bbase, int pbits, uint32_t nbp, 
 		dst[i] = ((const u2v *) tab)[i];
 }
 
+#if PJ2_BC && (PJ2_TB || !PJ2_SRCH)
+#error "PJ2_BC needs PJ2_SRCH and not PJ2_TB"
+#endif
+
 __global__ __launch_bounds__(1024) void
 k_pj2_probe(const uint2 *bent, const uint32_t *bbase, const uint32_t *pkey, const uint16_t *poffT, int pbits,
-	    uint32_t nbp, uint32_t nsub, uint32_t *pans, uint32_t *dupflag, const unsigned long long *gtab)
+	    uint32_t nbp, uint32_t nsub, uint32_t *pans, uint32_t *dupflag, const unsigned long long *gtab,
+	    const uint32_t *bkey, const uint16_t *brow, const uint16_t *bpoffT, uint32_t nsubB)
 {
 	extern __shared__ __attribute__((aligned(16))) unsigned long long dyn2[];
 	unsigned long long *tab = dyn2;
@@ -1745,6 +1760,85 @@ k_pj2_probe(const uint2 *bent, const uint32_t *bbase, const uint32_t *pkey, cons
 	for (uint32_t i = tid; i < ns; i += blockDim.x)
 		tab[i] = 0ull;
 #endif
+#if PJ2_BC
+	// the partition's build entries are its run in every build subtile (the
+	// build side cut like the probe side, k_pj2_cut): counted first, then
+	// inserted a batch of 64 subtiles per wave as the probe takes its runs
+	// (pj2_issue2: consecutive lanes load a run's consecutive keys); the row
+	// of entry idx is its subtile's first row + brow[idx]
+	(void) bent;
+	(void) bbase;
+	(void) gtab;
+	Pj2Batch bt;
+	uint32_t s0 = w * 64;
+	{
+		const uint16_t *q0 = bpoffT + (size_t) p * nsubB, *q1 = bpoffT + (size_t) (p + 1) * nsubB;
+		// the waves' counts in their 512-B slot regions past the marks (no
+		// static LDS: the dynamic table may take all 160 KB)
+		static_assert(64 * PJ2_U + 4 <= 512, "a count word after the marks");
+		uint32_t bc = 0;
+		for (uint32_t sb = tid; sb < nsubB; sb += blockDim.x)
+			bc += (uint32_t) (q1[sb] - q0[sb]);
+#pragma unroll
+		for (int o = 32; o > 0; o >>= 1)
+			bc += __shfl_xor(bc, o);
+		if (lane == 0)
+			*(uint32_t *) ((uint8_t *) wst + w * 512 + 64 * PJ2_U) = bc;
+		__syncthreads();                          // (also: the table is zeroed)
+		uint64_t btot = 0;
+		for (int q = 0; q < 16; q++)
+			btot += *(const uint32_t *) ((const uint8_t *) wst + q * 512 + 64 * PJ2_U);
+		// a build partition above 90 % of the table (the host sized it for
+		// the expected largest one) is flagged and not built: its runs are
+		// answered "no match" and the host falls back after the restore
+		const bool over = btot * 10 > (uint64_t) ns * 9;
+		if (over && tid == 0)
+			atomicOr(dupflag, 2u);
+		bool dup = false;
+#if !(PJ2_DIAG & 1)
+		if (!over) {
+			for (uint32_t sb0 = w * 64; sb0 < nsubB; sb0 += 16 * 64) {
+				Pj2Batch bb;
+				pj2_issue2(bkey, q0, q1, nsubB, sb0, slot, 0, bb, true);
+				for (uint32_t i0 = 0;;) {
+					uint32_t rw[PJ2_U];
+#pragma unroll
+					for (int u = 0; u < PJ2_U; u++)
+						rw[u] = bb.idx[u] != ~0u ? brow[bb.idx[u]] : 0u;
+#pragma unroll
+					for (int u = 0; u < PJ2_U; u++) {
+						if (bb.idx[u] == ~0u)
+							continue;
+						const uint32_t row = (bb.idx[u] & ~(uint32_t) (PJ_SUBROWS - 1)) + rw[u];
+						const unsigned long long v = ((unsigned long long) (row + 1) << 32) | bb.key[u];
+						uint32_t h = 2 * gt_home(pj_hash(bb.key[u]), pbits, nbp);
+						for (;;) {
+							const unsigned long long o = atomicCAS(&tab[h], 0ull, v);
+							if (o == 0ull)
+								break;
+							if ((uint32_t) o == bb.key[u]) {
+								dup = true;
+								break;
+							}
+							h = h + 1 == ns ? 0 : h + 1;
+						}
+					}
+					i0 += 64 * PJ2_U;
+					if (i0 >= bb.tot)
+						break;
+					pj2_issue2(bkey, q0, q1, nsubB, sb0, slot, i0, bb, false);
+				}
+			}
+		}
+#endif
+		if (__any(dup) && lane == 0)
+			atomicOr(dupflag, 1u);
+	}
+	// the probe side's first batch, then the table complete
+	if (s0 < nsub)
+		pj2_issue2(pkey, o0, o1, nsub, s0, slot, 0, bt, true);
+	__syncthreads();
+#else
 	// the first batch's run bounds and key loads go out before the table is
 	// built, so their latency hides behind the build
 	Pj2Batch bt;
@@ -1811,6 +1905,7 @@ k_pj2_probe(const uint2 *bent, const uint32_t *bbase, const uint32_t *pkey, cons
 	if (__any(dup) && lane == 0)
 		atomicOr(dupflag, 1u);
 	__syncthreads();
+#endif
 #endif
 	const ulonglong2 *bk = (const ulonglong2 *) tab;     // (an empty table when over)
 	// software pipeline: the next chunk's key loads (and, at a batch
@@ -2037,39 +2132,66 @@ pj_cut(const Side &S, BUN n, int pbits, bool skipnil, PjSide &o, uint32_t *maxto
 	return 0;
 }
 
-// the probe side of join_part with subtile-local runs (k_pj2_*); B = the
-// build side already cut (its largest partition in meta32[0], its nofit flag
-// in meta32[5], both checked here after the probe side's cut is queued)
-int
-join_part2(const Side &L, BUN nl, const Side &R, BUN nr, const PjSide &B, int pbits, bool nil_matches, mgdk_bat **ap,
-	   mgdk_bat **bp, bool *ukey)
+// the join's 48 bytes of meta words and the first and last oid of both
+// result columns, stored straight into the thread's pinned host buffer (no
+// copy launch)
+__global__ void
+k_pj_ends(const uint32_t *meta32, const oid *r1, const oid *r2, uint32_t *h)
 {
+	if (threadIdx.x < 12)
+		h[threadIdx.x] = meta32[threadIdx.x];
+	if (threadIdx.x == 0) {
+		const uint64_t n = ((const uint64_t *) meta32)[4];
+		uint64_t *e = (uint64_t *) (h + 12);
+		if (n > 0) {
+			e[0] = r1[0];
+			e[1] = r1[n - 1];
+			e[2] = r2[0];
+			e[3] = r2[n - 1];
+		}
+	}
+}
+
+// the probe side of join_part with subtile-local runs (k_pj2_*).  The probe
+// side's cut is the longer chain (cut, transpose, probe, restore), so it is
+// queued first; the build side (Rn, its largest partition in meta32[0], its
+// nofit flag in meta32[5], read back after the restore) is cut after it, on
+// the side stream (PJ2_SIDE, PJ2_SWAP) forked from the main one before either
+int
+join_part2(const Side &L, BUN nl, const Side &Rn, BUN nr, int pbits, bool nil_matches, mgdk_bat **ap, mgdk_bat **bp,
+	   bool *ukey)
+{
+	PjSide B;
 	hipStream_t st = stream();
 	const uint32_t P = 1u << pbits;
 	uint32_t *meta32 = (uint32_t *) meta_buf();
 	uint64_t *meta = (uint64_t *) meta32 + 4;          // [0] pairs, [1] look-back error
-	uint32_t *h = (uint32_t *) pinned(64);
+	uint32_t *h = (uint32_t *) pinned(128);
 	const uint32_t nsub = (uint32_t) ((nl + PJ_SUBROWS - 1) / PJ_SUBROWS);
 	const size_t rsz = (size_t) nsub * PJ_SUBROWS;
-	if (nl == 0 || rsz >= ((size_t) 1 << 32)) {
-		(void) side_join();                         // the build side's cut still uses its buffers
-		(void) sync();
+	if (nl == 0 || rsz >= ((size_t) 1 << 32))
 		return 1;                                   // (entry indexes are 32-bit)
-	}
 	DevBuf pkey(rsz * 4 + 64), prow(rsz * 2 + 64), pans(rsz * 4 + 64), poff((size_t) nsub * (P + 1) * 2 + 64),
 		poffT((size_t) nsub * (P + 1) * 2 + 64);
 	if (!pkey.p || !prow.p || !pans.p || !poff.p || !poffT.p)
 		return sync_fail();
+	const uint32_t nsubB = (uint32_t) ((nr + PJ_SUBROWS - 1) / PJ_SUBROWS);
+	const size_t bsz = (size_t) nsubB * PJ_SUBROWS;
+	if (bsz >= ((size_t) 1 << 32) - PJ_SUBROWS)
+		return 1;                                   // (build rows + 1 are 32-bit)
+#if PJ2_BC
+	DevBuf bkey(bsz * 4 + 64), brow(bsz * 2 + 64), bpoff((size_t) nsubB * (P + 1) * 2 + 64),
+		bpoffT((size_t) nsubB * (P + 1) * 2 + 64);
+	if (!bkey.p || !brow.p || !bpoff.p || !bpoffT.p)
+		return sync_fail();
+#endif
 	static const bool cut_attr = hipFuncSetAttribute((const void *) k_pj2_cut,
 							 hipFuncAttributeMaxDynamicSharedMemorySize, (int) PJ2_CUT_LDS) == hipSuccess;
 	static const bool probe_attr = hipFuncSetAttribute((const void *) k_pj2_probe,
 							   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
 	(void) hipGetLastError();
-	if (!cut_attr || !probe_attr) {
-		(void) side_join();                         // the build side's cut still uses its buffers
-		(void) sync();
+	if (!cut_attr || !probe_attr)
 		return 1;                                   // the kernels cannot get their LDS: fallback
-	}
 	// the table is sized for the expected largest build partition (mean + 6
 	// sigma) instead of the measured one, so no round trip is needed between
 	// the passes: a larger partition, a duplicate build key or a build value
@@ -2077,11 +2199,8 @@ join_part2(const Side &L, BUN nl, const Side &R, BUN nr, const PjSide &B, int pb
 	// the restore, and sends the join to the fallback
 	const double mean = (double) nr / P;
 	const uint32_t est = (uint32_t) (mean + 6.0 * sqrt(mean)) + 1;
-	if (est > PJ2_MAXFILL) {
-		(void) side_join();                         // the build side's cut still uses its buffers
-		(void) sync();
+	if (est > PJ2_MAXFILL)
 		return 1;
-	}
 	static const int lfpct = getenv("MGDK_PJ_LF") ? atoi(getenv("MGDK_PJ_LF")) : 80;
 	uint32_t nbp = (uint32_t) ((uint64_t) est * 100 / (2 * (uint64_t) (lfpct < 40 ? 40 : lfpct > 95 ? 95 : lfpct))) + 1;
 	if (2 * nbp <= est)
@@ -2099,34 +2218,62 @@ join_part2(const Side &L, BUN nl, const Side &R, BUN nr, const PjSide &B, int pb
 							hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
 	(void) hipGetLastError();
 	DevBuf gtab((size_t) P * 2 * nbp * 8 + 64);
-	if (!tb_attr || !gtab.p) {
-		(void) side_join();                         // the build side's cut still uses its buffers
-		(void) sync();
+	if (!tb_attr || !gtab.p)
 		return tb_attr ? -1 : 1;
-	}
 	const unsigned long long *gtp = gtab.as<unsigned long long>();
 #else
 	const unsigned long long *gtp = nullptr;
 #endif
-	// the probe side's cut depends on nothing the build side's writes: it runs
-	// on the side stream, beside the build side's passes, whose few
-	// workgroups leave CUs idle (PJ2_SIDE=0: one stream; PJ2_SWAP: the build
-	// side is the one on the side stream).  join_part forked the side stream.
-	hipStream_t cs = st;
-#if PJ2_SIDE && !PJ2_SWAP
-	if (stream2() != nullptr)
+	// the two sides' cuts depend on nothing the other writes: one runs on the
+	// side stream, beside the other, whose few workgroups leave CUs idle
+	// (PJ2_SIDE=0: one stream; PJ2_SWAP: the build side is the one on the
+	// side stream).  The side stream first waits for what is queued on the
+	// main one (the inputs' producers, the meta words' memset).
+	hipStream_t cs = st, bs = st;
+#if PJ2_SIDE
+	if (stream2() != nullptr) {
+		if (!side_fork())
+			return sync_fail();
+#if PJ2_SWAP
+		bs = stream2();
+#else
 		cs = stream2();
 #endif
-	// the restore's ticket and look-back words, cleared while the cuts run
+	}
+#endif
+	// the restore's ticket and look-back words (cleared by the cut)
 	const size_t sbytes = (nsub + 8) * sizeof(uint64_t);
 	char *sc = (char *) scratch(sbytes);
-	if (!sc || !hip_ok(hipMemsetAsync(sc, 0, sbytes, st), "memset"))
+	if (!sc)
 		return sync_fail();
 	hipLaunchKernelGGL(k_pj2_cut, dim3(nsub), dim3(1024), PJ2_CUT_LDS, cs, L, nl, pbits, !nil_matches,
-			   pkey.as<uint32_t>(), prow.as<uint16_t>(), poff.as<uint16_t>());
+			   pkey.as<uint32_t>(), prow.as<uint16_t>(), poff.as<uint16_t>(), (uint64_t *) sc);
 	hipLaunchKernelGGL(k_pj2_offt, dim3((nsub + 63) / 64, (P + 1 + 63) / 64), dim3(256), 0, cs, poff.as<uint16_t>(),
 			   nsub, P, poffT.as<uint16_t>());
+#if PJ2_BC
+	// the build side cut into subtile-local runs the same way (the cut leaves
+	// the restore's words alone: rzero NULL)
+	hipLaunchKernelGGL(k_pj2_cut, dim3(nsubB), dim3(1024), PJ2_CUT_LDS, bs, Rn, nr, pbits, !nil_matches,
+			   bkey.as<uint32_t>(), brow.as<uint16_t>(), bpoff.as<uint16_t>(), (uint64_t *) nullptr);
+	hipLaunchKernelGGL(k_pj2_offt, dim3((nsubB + 63) / 64, (P + 1 + 63) / 64), dim3(256), 0, bs,
+			   bpoff.as<uint16_t>(), nsubB, P, bpoffT.as<uint16_t>());
+	if (!hip_ok(hipGetLastError(), "join build cut"))
+		return sync_fail();
+	const uint2 *bentp = nullptr;
+	const uint32_t *bbasep = nullptr;
+	const uint32_t *bkeyp = bkey.as<uint32_t>();
+	const uint16_t *browp = brow.as<uint16_t>(), *bpoffTp = bpoffT.as<uint16_t>();
+#else
+	const uint32_t *bkeyp = nullptr;
+	const uint16_t *browp = nullptr, *bpoffTp = nullptr;
+	if (pj_cut(Rn, nr, pbits, !nil_matches, B, &meta32[0], bs) < 0)
+		return sync_fail();
+	const uint2 *bentp = B.ent->as<uint2>();
+	const uint32_t *bbasep = B.base->as<uint32_t>();
+#endif
 #if PJ2_TB
+	if (!side_join())
+		return sync_fail();
 	hipLaunchKernelGGL(k_pj2_tbuild, dim3(P), dim3(1024), (size_t) nbp * 16, st, B.ent->as<uint2>(),
 			   B.base->as<uint32_t>(), pbits, nbp, gtab.as<unsigned long long>(), &meta32[2]);
 #endif
@@ -2134,8 +2281,9 @@ join_part2(const Side &L, BUN nl, const Side &R, BUN nr, const PjSide &B, int pb
 	if (stream2() != nullptr && !side_join())
 		return sync_fail();
 #endif
-	hipLaunchKernelGGL(k_pj2_probe, dim3(P), dim3(1024), lds, st, B.ent->as<uint2>(), B.base->as<uint32_t>(),
-			   pkey.as<uint32_t>(), poffT.as<uint16_t>(), pbits, nbp, nsub, pans.as<uint32_t>(), &meta32[2], gtp);
+	hipLaunchKernelGGL(k_pj2_probe, dim3(P), dim3(1024), lds, st, bentp, bbasep, pkey.as<uint32_t>(),
+			   poffT.as<uint16_t>(), pbits, nbp, nsub, pans.as<uint32_t>(), &meta32[2], gtp,
+			   bkeyp, browp, bpoffTp, nsubB);
 	mgdk_bat *ra = newbat(0, MGDK_oid, nl), *rb = newbat(0, MGDK_oid, nl);
 	if (!ra || !rb) {
 		unfix2(ra, rb);
@@ -2151,11 +2299,11 @@ join_part2(const Side &L, BUN nl, const Side &R, BUN nr, const PjSide &B, int pb
 		return (unsigned) v;
 	}();
 	hipLaunchKernelGGL(k_pj2_restore_p, dim3(min(ncu, nsub)), dim3(1024), 0, st, prow.as<uint16_t>(),
-			   pans.as<uint32_t>(), poff.as<uint16_t>(), P, nl, nsub, L, R, (uint32_t *) sc, (uint64_t *) sc + 8,
+			   pans.as<uint32_t>(), poff.as<uint16_t>(), P, nl, nsub, L, Rn, (uint32_t *) sc, (uint64_t *) sc + 8,
 			   meta, (oid *) ra->theap, (oid *) rb->theap);
 #else
 	hipLaunchKernelGGL(k_pj2_restore, dim3(nsub), dim3(1024), 0, st, prow.as<uint16_t>(), pans.as<uint32_t>(),
-			   poff.as<uint16_t>(), P, nl, nsub, L, R, (uint32_t *) sc, (uint64_t *) sc + 8, meta,
+			   poff.as<uint16_t>(), P, nl, nsub, L, Rn, (uint32_t *) sc, (uint64_t *) sc + 8, meta,
 			   (oid *) ra->theap, (oid *) rb->theap);
 #endif
 	// a failed launch leaves pkey / pans / the results unwritten: fail the call
@@ -2164,8 +2312,11 @@ join_part2(const Side &L, BUN nl, const Side &R, BUN nr, const PjSide &B, int pb
 		return sync_fail();
 	}
 	// meta32[2]: duplicate build key (1) / oversized partition (2);
-	// meta32[5]: build value without a 4-byte image; meta = meta32 + 8
-	if (!hip_ok(hipMemcpyAsync(h, meta32, 48, hipMemcpyDeviceToHost, st), "memcpy") || !sync()) {
+	// meta32[5]: build value without a 4-byte image; meta = meta32 + 8:
+	// pairs, look-back error, then the results' first / last oids
+	hipLaunchKernelGGL(k_pj_ends, dim3(1), dim3(64), 0, st, (const uint32_t *) meta32, (const oid *) ra->theap,
+			   (const oid *) rb->theap, h);
+	if (!hip_ok(hipGetLastError(), "k_pj_ends") || !sync()) {
 		unfix2(ra, rb);
 		return -1;
 	}
@@ -2181,6 +2332,11 @@ join_part2(const Side &L, BUN nl, const Side &R, BUN nr, const PjSide &B, int pb
 		return -1;
 	}
 	ra->count = rb->count = h64[0];
+	if (h64[0] > 0) {
+		uint64_t e[4];
+		memcpy(e, h + 12, 32);
+		join_ends = JoinEnds{ra, rb, e[0], e[1], e[2], e[3]};
+	}
 	*ukey = true;                                       // unique build keys: one match per row
 	*ap = ra;
 	*bp = rb;
@@ -2226,28 +2382,12 @@ join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_b
 	PjSide B, Pr;
 	Side Rn = R;
 	Rn.nofit = &meta32[5];
-	// the side stream (PJ2_SIDE) first waits for everything queued so far on
-	// the main one (the inputs' producers, the memset above); PJ2_SWAP: the
-	// build side's cut goes there and the probe side's cut stays on the main
-	// stream, so the probe follows the probe side's transpose with no
-	// cross-stream wait on the longer chain
-	hipStream_t bs = st;
-#if PJ2_SIDE
-	if (mode != 3 && stream2() != nullptr) {
-		if (!side_fork())
-			return sync_fail();
-#if PJ2_SWAP
-		bs = stream2();
-#endif
-	}
-#endif
-	if (pj_cut(Rn, nr, pbits, !nil_matches, B, &meta32[0], bs) < 0) {
-		(void) side_join();                         // launched cuts still use the buffers
-		(void) sync();
+	if (mode != 3)
+		return join_part2(L, nl, Rn, nr, pbits, nil_matches, ap, bp, ukey);
+	if (pj_cut(Rn, nr, pbits, !nil_matches, B, &meta32[0]) < 0) {
+		(void) sync();                              // launched cuts still use the buffers
 		return -1;
 	}
-	if (mode != 3)
-		return join_part2(L, nl, R, nr, B, pbits, nil_matches, ap, bp, ukey);
 	if (pj_cut(L, nl, pbits, !nil_matches, Pr, &meta32[1]) < 0) {
 		(void) sync();
 		return -1;
@@ -2816,6 +2956,8 @@ join_bj(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_bat
 }  // namespace
 
 namespace mgdk {
+
+thread_local JoinEnds join_ends;
 
 // hashjoin (gdk/gdk_join.c:2900-3335) over candidate lists already
 // initialised: per l candidate in order, the matches in r in DESCENDING

@@ -852,13 +852,23 @@ hashjoin(mgdk_bat **r1p, mgdk_bat **r2p, mgdk_bat *l, mgdk_bat *r, const Cand &l
 {
 	mgdk_bat *a = nullptr, *b = nullptr;
 	bool ukey = false;
+	join_ends = JoinEnds{};
 	if (hash_join(l, r, lc, rc, nil_matches, &a, &b, &ukey) < 0)
 		return -1;
 	const BUN n = a->count;
 	oid af, al, bf, bl;
 	uint32_t adj1 = 0;
+	// the ends come with the pair count when the partitioned join ran
+	const bool ends = join_ends.a == a && join_ends.b == b && n > 0;
+	if (ends) {
+		af = join_ends.af;
+		al = join_ends.al;
+		bf = join_ends.bf;
+		bl = join_ends.bl;
+	}
+	join_ends = JoinEnds{};
 	// with unique build keys r1 (ascending) cannot repeat an oid: no scan
-	if (first_last(a, &af, &al) < 0 || first_last(b, &bf, &bl) < 0 || (!ukey && oid_adj(a, &adj1) < 0)) {
+	if ((!ends && (first_last(a, &af, &al) < 0 || first_last(b, &bf, &bl) < 0)) || (!ukey && oid_adj(a, &adj1) < 0)) {
 		unfix2(a, b);
 		return -1;
 	}

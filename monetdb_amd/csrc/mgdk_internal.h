@@ -123,6 +123,14 @@ void oidx_share(mgdk_bat *v, const mgdk_bat *b);   // v: a view over all of b
 // indexes: the sorts the device path runs where the reference runs none
 // (the reference's own BATsort calls sort temporaries or are mirrored as is)
 extern thread_local int sort_internal;
+// the first / last oids of a join's two result columns, read back by the
+// partitioned hash join with its pair count (one round trip instead of
+// three); hashjoin (joinalgo.hip) takes them when a / b are its results
+struct JoinEnds {
+	const mgdk_bat *a = nullptr, *b = nullptr;
+	oid af = 0, al = 0, bf = 0, bl = 0;
+};
+extern thread_local JoinEnds join_ends;
 struct SortInternal {
 	SortInternal() { ++sort_internal; }
 	~SortInternal() { --sort_internal; }

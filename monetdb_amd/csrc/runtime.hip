@@ -95,8 +95,17 @@ stream2()
 {
 	if (tctx.s2 == nullptr) {
 		(void) hipSetDevice(g_device);
-		if (hipStreamCreateWithFlags(&tctx.s2, hipStreamNonBlocking) != hipSuccess)
+		// MGDK_S2_PRIO=1: the side stream at the device's greatest priority
+		// (its kernels' workgroups dispatched ahead of the main stream's)
+		static const int prio = getenv("MGDK_S2_PRIO") ? atoi(getenv("MGDK_S2_PRIO")) : 0;
+		int lo = 0, hi = 0;
+		if (prio != 0 && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo) {
+			if (hipStreamCreateWithPriority(&tctx.s2, hipStreamNonBlocking, hi) != hipSuccess)
+				tctx.s2 = nullptr;
+		} else if (hipStreamCreateWithFlags(&tctx.s2, hipStreamNonBlocking) != hipSuccess) {
 			tctx.s2 = nullptr;
+		}
+		(void) hipGetLastError();
 	}
 	return tctx.s2;
 }
