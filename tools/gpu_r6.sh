@@ -45,6 +45,22 @@ svar)
 		done
 	done
 	;;
+final_a)
+	# round-end evidence, part 1: the GPU suite and the smoke test
+	tests 1000 $T tests > $O/gpu_tests.log 2>&1
+	timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+	;;
+final_b)
+	# round-end evidence, part 2: the driver line, rocprof of it, PMC passes, the op legs
+	timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err
+	cd /tmp && cd $GRAFT_REPO_ROOT
+	timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 10 --no-cpu > $O/prof_bench.json 2> $O/prof_bench.err
+	timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f -o run -- python3 bench.py --no-dist-legs --no-op-legs --no-cpu --no-parity --steps 3 --warmup 1 > $O/pmc_f.log 2>&1
+	timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_w -o run -- python3 bench.py --no-dist-legs --no-op-legs --no-cpu --no-parity --steps 3 --warmup 1 > $O/pmc_w.log 2>&1
+	timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_jf -o run -- python3 tools/opbench.py --only config3 config4_group_sums > $O/pmc_jf.log 2>&1
+	timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_jw -o run -- python3 tools/opbench.py --only config3 config4_group_sums > $O/pmc_jw.log 2>&1
+	timeout -k 10 300 python tools/opbench.py > $O/opbench.json 2> $O/opbench.err
+	;;
 bench)
 	timeout -k 10 420 python bench.py > $O/bench.json 2> $O/bench.err
 	;;
