@@ -61,6 +61,11 @@ final_b)
 	timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_jw -o run -- python3 tools/opbench.py --only config3 config4_group_sums > $O/pmc_jw.log 2>&1
 	timeout -k 10 300 python tools/opbench.py > $O/opbench.json 2> $O/opbench.err
 	;;
+sprof)
+	# kernel trace of opbench config1 (the select legs)
+	cd /tmp && cd $GRAFT_REPO_ROOT
+	timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/default -o run -- python3 tools/opbench.py --only config1 > $O/default.log 2>&1
+	;;
 bench)
 	timeout -k 10 420 python bench.py > $O/bench.json 2> $O/bench.err
 	;;
