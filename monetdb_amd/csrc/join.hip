@@ -2004,6 +2004,147 @@ k_pj2_restore(const uint16_t *prow, const uint32_t *pans, const uint16_t *poff, 
 	pj_emit(res, sub, a, rows, nsub, L, R, status, meta, r1, r2);
 }
 
+// restore in 75 KB of LDS (PJ2_R2=1): two workgroups per CU, so one's LDS
+// and scan phases overlap the other's pair stores.  The answers stay in
+// registers (32 entries per thread, as PJ2_RALL loads them); the matched rows
+// become a 32K-bit mask by LDS atomics, which the emit's scan reads as its
+// run masks; then for each half of the subtile the entries of that half drop
+// their answers into a 16K-row stage and the half's pairs are stored in row
+// order.
+#ifndef PJ2_R2
+#define PJ2_R2 0        // measured slower (profiles/r06/join_r2): 1 (answers kept in registers, 28 VGPRs
+                        // spilled) 0.945-0.971 ms, 2 (the second half's entries read again) 0.881, 0: 0.851-0.853
+#endif
+constexpr uint32_t PJ2_R2H = PJ_SUBROWS / 2;       // rows per stage half
+
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void
+k_pj2_restore2(const uint16_t *prow, const uint32_t *pans, const uint16_t *poff, uint32_t P, BUN n, uint32_t nsub,
+	       Side L, Side R, uint32_t *ticket, uint64_t *status, uint64_t *meta, oid *r1, oid *r2)
+{
+	__shared__ uint32_t stage[PJ2_R2H + PJ2_R2H / 32];
+	__shared__ uint32_t rbase[1024], wsum[16];
+	__shared__ uint32_t rmask[1024];
+	__shared__ uint64_t s_pre;
+	__shared__ uint32_t s_sub;
+	const unsigned tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+	if (tid == 0)
+		s_sub = atomicAdd(ticket, 1u);
+	rmask[tid] = 0;
+	__syncthreads();
+	const uint32_t sub = s_sub;
+	const BUN a = (BUN) sub * PJ_SUBROWS;
+	const uint32_t rows = (uint32_t) min((BUN) PJ_SUBROWS, n - a);
+	const uint32_t cnt = poff[(size_t) sub * (P + 1) + P];
+	static_assert(PJ_SUBROWS == 32 * 1024, "32 entries per thread");
+	typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+	typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+	u4 am[8];
+	u2 ar[8];
+#pragma unroll
+	for (int q = 0; q < 8; q++) {
+		const uint32_t j = 4 * (tid + 1024 * q);
+#if PJ2_R2 == 2
+		am[q] = j < cnt ? *(const u4 *) (pans + a + j) : (u4) {0, 0, 0, 0};     // read again below: cached
+		ar[q] = j < cnt ? *(const u2 *) (prow + a + j) : (u2) {0, 0};
+#else
+		am[q] = j < cnt ? __builtin_nontemporal_load((const u4 *) (pans + a + j)) : (u4) {0, 0, 0, 0};
+		ar[q] = j < cnt ? __builtin_nontemporal_load((const u2 *) (prow + a + j)) : (u2) {0, 0};
+#endif
+	}
+	// the matched rows' bits, and the first half's answers into the stage
+#pragma unroll
+	for (int q = 0; q < 8; q++) {
+		const uint32_t j = 4 * (tid + 1024 * q);
+#pragma unroll
+		for (int c = 0; c < 4; c++) {
+			const uint32_t m = am[q][c], r = (ar[q][c >> 1] >> (16 * (c & 1))) & 0xffffu;
+			if (j + c < cnt && m) {
+				atomicOr(&rmask[r >> 5], 1u << (r & 31));
+#if PJ2_R2 == 2
+				if (r < PJ2_R2H)
+					stage[r + (r >> 5)] = m;
+#endif
+			}
+		}
+	}
+	__syncthreads();
+	// thread tid's 32 rows [32 tid, 32 tid + 32): count, wave and workgroup
+	// scans, the subtile's offset by look-back (as pj_emit_scan)
+	const uint32_t r0 = tid * 32;
+	const uint32_t msk = r0 >= rows ? 0u : rows - r0 >= 32 ? rmask[tid] : rmask[tid] & ((1u << (rows - r0)) - 1);
+	const uint32_t c = __popc(msk);
+	uint32_t x = c;
+#pragma unroll
+	for (int o = 1; o < 64; o <<= 1) {
+		const uint32_t u = __shfl_up(x, o);
+		if (lane >= (unsigned) o)
+			x += u;
+	}
+	if (lane == 63)
+		wsum[w] = x;
+	__syncthreads();
+	uint32_t wpre = 0, tot = 0;
+	for (uint32_t q = 0; q < 16; q++) {
+		wpre += q < w ? wsum[q] : 0;
+		tot += wsum[q];
+	}
+	rmask[tid] = msk;
+	rbase[tid] = wpre + x - c;
+	if (w == 0) {
+		const uint64_t pre = lookback(status, sub, tot, (uint32_t *) &meta[1]);
+		if (lane == 0) {
+			s_pre = pre;
+			if (sub == nsub - 1)
+				meta[0] = pre + tot;
+		}
+	}
+	__syncthreads();
+	const uint64_t pre = s_pre;
+	for (uint32_t h = 0; h < 2; h++) {
+		const uint32_t hb = h * PJ2_R2H;
+		if (hb >= rows)
+			break;
+#if PJ2_R2 == 2
+		// the second half's answers: the subtile's entries read again (the
+		// first read's registers are not kept through the scan and stores)
+		if (h == 1) {
+#pragma unroll
+			for (int q = 0; q < 8; q++) {
+				const uint32_t j = 4 * (tid + 1024 * q);
+				am[q] = j < cnt ? *(const u4 *) (pans + a + j) : (u4) {0, 0, 0, 0};
+				ar[q] = j < cnt ? *(const u2 *) (prow + a + j) : (u2) {0, 0};
+			}
+		}
+		if (h == 1)
+#endif
+#pragma unroll
+		for (int q = 0; q < 8; q++) {
+			const uint32_t j = 4 * (tid + 1024 * q);
+#pragma unroll
+			for (int c2 = 0; c2 < 4; c2++) {
+				const uint32_t m = am[q][c2], r = (ar[q][c2 >> 1] >> (16 * (c2 & 1))) & 0xffffu;
+				if (j + c2 < cnt && m && r - hb < PJ2_R2H) {
+					const uint32_t rl = r - hb;
+					stage[rl + (rl >> 5)] = m;
+				}
+			}
+		}
+		__syncthreads();
+		const uint32_t he = min(hb + PJ2_R2H, rows);
+		for (uint32_t r = hb + tid; r < he; r += blockDim.x) {
+			const uint32_t run = r >> 5, bit = r & 31;
+			const uint32_t mk = rmask[run];
+			if ((mk >> bit) & 1) {
+				const uint64_t o = pre + rbase[run] + __popc(mk & ((1u << bit) - 1));
+				const uint32_t rl = r - hb;
+				r1[o] = oid_of(L, a + r);
+				r2[o] = oid_of(R, stage[rl + (rl >> 5)] - 1);
+			}
+		}
+		__syncthreads();
+	}
+}
+
 // persistent restore (PJ2_RP=1): one 1024-thread workgroup per CU (the
 // 143 KB of LDS allow no second) claims subtiles by ticket and loads the
 // next subtile's answers and rows while it writes the current one's pairs,
@@ -2289,7 +2430,11 @@ join_part2(const Side &L, BUN nl, const Side &Rn, BUN nr, int pbits, bool nil_ma
 		unfix2(ra, rb);
 		return sync_fail();
 	}
-#if PJ2_RP
+#if PJ2_R2
+	hipLaunchKernelGGL(k_pj2_restore2, dim3(nsub), dim3(1024), 0, st, prow.as<uint16_t>(), pans.as<uint32_t>(),
+			   poff.as<uint16_t>(), P, nl, nsub, L, Rn, (uint32_t *) sc, (uint64_t *) sc + 8, meta,
+			   (oid *) ra->theap, (oid *) rb->theap);
+#elif PJ2_RP
 	static const unsigned ncu = [] {
 		int v = 0, d = 0;
 		if (hipGetDevice(&d) != hipSuccess ||
