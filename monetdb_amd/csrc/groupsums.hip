@@ -31,6 +31,9 @@ namespace {
 constexpr int GSU = 8;                 // rows per lane
 constexpr BUN GST = 256 * GSU;         // rows per tile
 constexpr int GS_MAXV = 4;
+#ifndef GS_FUSED_DEFAULT
+#define GS_FUSED_DEFAULT 1   // the tile base by look-back inside the sums pass (no count pass)
+#endif
 #ifndef GS_STAGE
 #define GS_STAGE 1       // group outputs staged in LDS and stored as runs (0: per-lane stores)
 #endif
@@ -655,7 +658,10 @@ mgdk_group_sums_ordered(mgdk_bat **extents, mgdk_bat **histo, mgdk_bat **keys, m
 	// the count pass does, so the exact two-pass form stays the default.  A
 	// persistent fused form (next tile's rows fetched during the look-back)
 	// needed 240 VGPRs in its tile loop, against 98 for one tile per block.
-	const bool fused_on = getenv("MGDK_GS_FUSED") && atoi(getenv("MGDK_GS_FUSED")) != 0;   // read per call (tests)
+	// Round 6: on this round's boxes (stores slower than round 5's) the fused
+	// form is 4 % faster at SF100 (5.24 vs 5.44-5.47 ms, profiles/r06/gsums_fused/)
+	// and is the default; MGDK_GS_FUSED=0 selects the two-pass form.
+	const bool fused_on = getenv("MGDK_GS_FUSED") ? atoi(getenv("MGDK_GS_FUSED")) != 0 : GS_FUSED_DEFAULT != 0;   // read per call (tests)
 	bool fused = fused_on && nt < 0xffffffffull && n * (24 + 16 * (BUN) nvals) <= ((BUN) 48 << 30);
 	DevBuf vp(64);
 	const size_t esz = sizeof(GsEdge<GS_MAXV>);
