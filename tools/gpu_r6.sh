@@ -66,6 +66,10 @@ sprof)
 	cd /tmp && cd $GRAFT_REPO_ROOT
 	timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/default -o run -- python3 tools/opbench.py --only config1 > $O/default.log 2>&1
 	;;
+q1prof)
+	cd /tmp && cd $GRAFT_REPO_ROOT
+	timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 tools/q1op_prof.py 3 > $O/q1.log 2>&1
+	;;
 bench)
 	timeout -k 10 420 python bench.py > $O/bench.json 2> $O/bench.err
 	;;
