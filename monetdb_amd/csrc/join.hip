@@ -2015,6 +2015,7 @@ k_pj2_restore(const uint16_t *prow, const uint32_t *pans, const uint16_t *poff, 
 #define PJ2_R2 0        // measured slower (profiles/r06/join_r2): 1 (answers kept in registers, 28 VGPRs
                         // spilled) 0.945-0.971 ms, 2 (the second half's entries read again) 0.881, 0: 0.851-0.853
 #endif
+#if PJ2_R2
 constexpr uint32_t PJ2_R2H = PJ_SUBROWS / 2;       // rows per stage half
 
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void
@@ -2145,6 +2146,8 @@ k_pj2_restore2(const uint16_t *prow, const uint32_t *pans, const uint16_t *poff,
 	}
 }
 
+#endif
+
 // persistent restore (PJ2_RP=1): one 1024-thread workgroup per CU (the
 // 143 KB of LDS allow no second) claims subtiles by ticket and loads the
 // next subtile's answers and rows while it writes the current one's pairs,
@@ -2157,6 +2160,7 @@ k_pj2_restore2(const uint16_t *prow, const uint32_t *pans, const uint16_t *poff,
 #define PJ2_RP 0
 #endif
 
+#if PJ2_RP
 typedef uint32_t pj_u4 __attribute__((ext_vector_type(4)));
 typedef uint32_t pj_u2 __attribute__((ext_vector_type(2)));
 struct Pj2Ent {
@@ -2232,6 +2236,7 @@ k_pj2_restore_p(const uint16_t *prow, const uint32_t *pans, const uint16_t *poff
 		sub = ns;
 	}
 }
+#endif
 
 // one side cut into partitions: cnt/off matrices, partition bases, entries
 struct PjSide {
@@ -2394,6 +2399,8 @@ join_part2(const Side &L, BUN nl, const Side &Rn, BUN nr, int pbits, bool nil_ma
 #if PJ2_BC
 	// the build side cut into subtile-local runs the same way (the cut leaves
 	// the restore's words alone: rzero NULL)
+	if (!hip_ok(hipMemsetAsync(meta32, 0, 64, bs), "memset"))
+		return sync_fail();
 	hipLaunchKernelGGL(k_pj2_cut, dim3(nsubB), dim3(1024), PJ2_CUT_LDS, bs, Rn, nr, pbits, !nil_matches,
 			   bkey.as<uint32_t>(), brow.as<uint16_t>(), bpoff.as<uint16_t>(), (uint64_t *) nullptr);
 	hipLaunchKernelGGL(k_pj2_offt, dim3((nsubB + 63) / 64, (P + 1 + 63) / 64), dim3(256), 0, bs,
@@ -2407,7 +2414,10 @@ join_part2(const Side &L, BUN nl, const Side &Rn, BUN nr, int pbits, bool nil_ma
 #else
 	const uint32_t *bkeyp = nullptr;
 	const uint16_t *browp = nullptr, *bpoffTp = nullptr;
-	if (pj_cut(Rn, nr, pbits, !nil_matches, B, &meta32[0], bs) < 0)
+	// the meta words: the build side's (largest partition, nofit) and the
+	// probe's / restore's flags and counts, which run after the side join
+	if (!hip_ok(hipMemsetAsync(meta32, 0, 64, bs), "memset") ||
+	    pj_cut(Rn, nr, pbits, !nil_matches, B, &meta32[0], bs) < 0)
 		return sync_fail();
 	const uint2 *bentp = B.ent->as<uint2>();
 	const uint32_t *bbasep = B.base->as<uint32_t>();
@@ -2519,7 +2529,9 @@ join_part(const Side &L, BUN nl, const Side &R, BUN nr, bool nil_matches, mgdk_b
 	uint32_t *meta32 = (uint32_t *) meta_buf();
 	uint64_t *meta = (uint64_t *) meta32 + 4;          // [0] pairs, [1] look-back error
 	uint32_t *h = (uint32_t *) pinned(64);
-	if (!hip_ok(hipMemsetAsync(meta32, 0, 64, st), "memset"))
+	// the subtile-local plan (mode != 3) clears the meta words itself, on
+	// the stream of the build side's cut, after the probe side's cut is queued
+	if (mode == 3 && !hip_ok(hipMemsetAsync(meta32, 0, 64, st), "memset"))
 		return -1;
 	// both sides are cut before the host looks at the build side's largest
 	// partition: one round trip instead of two (an oversized partition, rare,
