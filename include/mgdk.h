@@ -345,6 +345,12 @@ void mgdk_free(void *p);
 int mgdk_BATprod(void *res, int tp, mgdk_bat *b, mgdk_bat *s, bool skip_nils, bool nil_if_empty);
 mgdk_bat *mgdk_BATgroupprod(mgdk_bat *b, mgdk_bat *g, mgdk_bat *e, mgdk_bat *s, int tp, bool skip_nils);
 
+/* BATguess_uniques (gdk/gdk.h:2268; gdk_join.c:3572): the join cost model's
+ * estimate of distinct values among b's candidates s (NULL: all of b; the
+ * reference takes a struct canditer); a full column's estimate is cached in
+ * b->tunique_est.  The 1000-row sample is evenly spaced (the reference's
+ * BATsample is random).  MGDK_BUN_NONE on an error */
+mgdk_BUN mgdk_BATguess_uniques(mgdk_bat *b, mgdk_bat *s);
 /* BATcount_no_nil (gdk/gdk.h; gdk_batop.c:3078): b's candidates whose
  * value is not nil (tnonil / msk: every candidate; void: none when the
  * sequence is nil); a count of every row sets b's tnonil.  0 for a NULL b;

@@ -1583,3 +1583,28 @@ mgdk_BATordered_rev(mgdk_bat *b)
 	Ord o;
 	return b && ordered_rev(b, o) > 0;
 }
+
+// BATguess_uniques (gdk_join.c:3572): the join cost model's distinct-value
+// estimate over b's candidates s (NULL: all of b) -- b's count for a key
+// column, the cached tunique_est of a full column, else the two-point
+// extrapolation over a 1000-row sample (evenly spaced: the reference samples
+// at random) that a full column also caches in b
+extern "C" mgdk_BUN
+mgdk_BATguess_uniques(mgdk_bat *b, mgdk_bat *s)
+{
+	if (b == nullptr) {
+		seterr("BATguess_uniques: b must not be NULL");
+		return MGDK_BUN_NONE;
+	}
+	mgdk_bat *held = nullptr;
+	if (s && is_complex_cand(s) && (s = held = unmask_cand(s)) == nullptr)
+		return MGDK_BUN_NONE;
+	Cand ci;
+	Ord o;
+	double est = 0;
+	const int rc = cand_init(&ci, b, s) < 0 ? -1 : guess_uniques(b, o, ci, s, &est);
+	mgdk_BBPunfix(held);
+	if (rc < 0)
+		return MGDK_BUN_NONE;
+	return (mgdk_BUN) est;
+}

@@ -209,6 +209,7 @@ _SIGS = {
     "mgdk_BATthetajoin": (C.c_int, [PP, PP, P, P, P, P, C.c_int, C.c_bool, C.c_uint64]),
     "mgdk_BATsubcross": (C.c_int, [PP, PP, P, P, P, P, C.c_bool]),
     "mgdk_BATcount_no_nil": (C.c_uint64, [P, P]),
+    "mgdk_BATguess_uniques": (C.c_uint64, [P, P]),
     "mgdk_BAToutercross": (C.c_int, [PP, PP, P, P, P, P, C.c_bool]),
     "mgdk_BATbandjoin": (C.c_int, [PP, PP, P, P, P, P, C.c_void_p, C.c_void_p, C.c_bool, C.c_bool, C.c_uint64]),
     "mgdk_BATrangejoin": (C.c_int, [PP, PP, P, P, P, P, P, C.c_bool, C.c_bool, C.c_bool, C.c_bool, C.c_uint64]),
@@ -967,6 +968,14 @@ def BATthetajoin(l, r, sl=None, sr=None, op=JOIN_LT, nil_matches=False, estimate
     _chk(lib().mgdk_BATthetajoin(C.byref(a), C.byref(b), l.ptr, r.ptr, _p(sl), _p(sr), op, nil_matches,
                                  estimate))
     return BAT(a), BAT(b)
+
+
+def BATguess_uniques(b, s=None):
+    """BATguess_uniques (gdk_join.c:3572): distinct-value estimate"""
+    n = lib().mgdk_BATguess_uniques(b.ptr, _p(s))
+    if n == BUN_NONE:
+        _chk(-1)
+    return n
 
 
 def BATcount_no_nil(b, s=None):

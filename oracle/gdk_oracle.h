@@ -192,6 +192,8 @@ int ora_bandjoin(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *r, const ora
 /* gdk_join.c:5422 BATrangejoin (rangejoin :5067) */
 int ora_rangejoin(ora_bat **r1p, ora_bat **r2p, ora_bat *l, ora_bat *rl, ora_bat *rh, const ora_bat *sl,
 		  const ora_bat *sr, bool linc, bool hinc, bool anti, bool symmetric);
+/* gdk_join.c:3572 BATguess_uniques (s: the candidate BAT, NULL: all of b) */
+uint64_t ora_guess_uniques(ora_bat *b, const ora_bat *s);
 /* gdk_batop.c:3078 BATcount_no_nil */
 uint64_t ora_count_no_nil(const ora_bat *b, const ora_bat *s);
 /* gdk_cross.c:138 BATsubcross; outer: :153 BAToutercross (r2p may be NULL) */

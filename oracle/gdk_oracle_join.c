@@ -2125,3 +2125,14 @@ ora_crossproduct(ora_bat **r1p, ora_bat **r2p, const ora_bat *l, const ora_bat *
 	}
 	return cross_ci(r1p, r2p, &c1, &c2);
 }
+
+/* BATguess_uniques (gdk_join.c:3572): guess_uniques over b's candidates s
+ * (NULL: all of b) */
+uint64_t
+ora_guess_uniques(ora_bat *b, const ora_bat *s)
+{
+	ora_ci ci;
+	if (ora_ci_init(&ci, b, s) < 0)
+		return 0;
+	return (uint64_t) guess_uniques(b, &ci, s);
+}

@@ -132,6 +132,8 @@ def lib():
         L.ora_leftjoin.argtypes = [C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool, C.c_bool, C.c_bool]
         L.ora_markjoin.argtypes = [C.POINTER(P), C.POINTER(P), C.POINTER(P), P, P, P, P]
         L.ora_count_no_nil.argtypes = [P, P]
+        L.ora_guess_uniques.argtypes = [P, P]
+        L.ora_guess_uniques.restype = C.c_uint64
         L.ora_count_no_nil.restype = C.c_uint64
         L.ora_crossproduct.argtypes = [C.POINTER(P), C.POINTER(P), P, P, P, P, C.c_bool, C.c_bool]
         L.ora_minmax.argtypes = [P, C.c_bool, C.c_bool, C.c_void_p, C.POINTER(C.c_char_p)]
@@ -549,6 +551,11 @@ def BATjoin(l, r, sl=None, sr=None, nil_matches=False):
                       sr.ptr if sr else None, nil_matches) < 0:
         raise _err()
     return Bat(a), Bat(b)
+
+
+def BATguess_uniques(b, s=None):
+    """gdk_join.c:3572 (records tunique_est on b for a full column)"""
+    return int(lib().ora_guess_uniques(b.ptr, s.ptr if s else None))
 
 
 def BATcount_no_nil(b, s=None):
