@@ -303,7 +303,10 @@ k_select(SelArgs<T> a)
 //                dense tiles go in rounds of 4096 slots whose hits are
 //                placed in LDS in order and stored as one contiguous run.
 // The column is read once; extra traffic is the bitmap twice (2 bits/value).
-constexpr int SROWS = 16;
+#ifndef MGDK_SEL_SROWS
+#define MGDK_SEL_SROWS 16
+#endif
+constexpr int SROWS = MGDK_SEL_SROWS;
 // results of at least this many oids keep the scan's bitmap (Priv::smap)
 constexpr uint64_t SMAP_MIN = 1 << 20;
 // rows of 16-B loads per lane: 1- and 2-byte types unpack 16 / 8 values per
