@@ -70,6 +70,11 @@ q1prof)
 	cd /tmp && cd $GRAFT_REPO_ROOT
 	timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 tools/q1op_prof.py 3 > $O/q1.log 2>&1
 	;;
+benchrep)
+	# the driver line twice more on one box (run-to-run spread)
+	timeout -k 10 420 python bench.py > $O/bench_1.json 2> $O/bench_1.err
+	timeout -k 10 420 python bench.py > $O/bench_2.json 2> $O/bench_2.err
+	;;
 bench)
 	timeout -k 10 420 python bench.py > $O/bench.json 2> $O/bench.err
 	;;
