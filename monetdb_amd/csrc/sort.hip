@@ -1266,6 +1266,44 @@ k_img_xor(const K *src, BUN n, K kx, K *keys)
 		keys[i] = src[i] ^ kx;
 }
 
+// k_img_xor that also counts two digits of the images (the MSD-then-local
+// path's d1 / d2 when they are not whole bytes, which k_keys's byte counts do
+// not give): out[(s / 8) * 256 + digit] as k_rs_dhist lays them out, so the
+// keys are not read once more for them
+template <typename K>
+__global__ __launch_bounds__(256) void
+k_img_xor_h2(const K *src, BUN n, K kx, K *keys, int s1, int s2, uint32_t *out)
+{
+	__shared__ uint32_t h[2][256];
+	h[0][threadIdx.x] = 0;
+	h[1][threadIdx.x] = 0;
+	__syncthreads();
+	constexpr int KU = 8;
+	const BUN stride = (BUN) gridDim.x * blockDim.x;
+	for (BUN i0 = (BUN) blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += KU * stride) {
+		K k[KU];
+#pragma unroll
+		for (int u = 0; u < KU; u++) {
+			const BUN i = i0 + u * stride;
+			k[u] = src[i < n ? i : n - 1] ^ kx;
+		}
+#pragma unroll
+		for (int u = 0; u < KU; u++) {
+			const BUN i = i0 + u * stride;
+			if (i < n) {
+				keys[i] = k[u];
+				atomicAdd(&h[0][(uint32_t) (k[u] >> s1) & 255], 1u);
+				atomicAdd(&h[1][(uint32_t) (k[u] >> s2) & 255], 1u);
+			}
+		}
+	}
+	__syncthreads();
+	if (h[0][threadIdx.x])
+		atomicAdd(&out[(s1 / 8) * 256 + threadIdx.x], h[0][threadIdx.x]);
+	if (h[1][threadIdx.x])
+		atomicAdd(&out[(s2 / 8) * 256 + threadIdx.x], h[1][threadIdx.x]);
+}
+
 // passes A, B, C (see above); keys / vals hold the input images, the
 // alternates are free; cap: the largest (d1, d2) bucket sorted in LDS
 template <typename K>
@@ -1435,9 +1473,24 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 	const uint32_t nblocks = (uint32_t) ((n + Tile<K>::N - 1) / Tile<K>::N);
 	static const bool use_lb = getenv("MGDK_SORT_LB") ? atoi(getenv("MGDK_SORT_LB")) != 0 : true;
 	const bool lb = use_lb && !shifts.empty() && shifts.size() <= (size_t) RS_MAXP;
+	// the MSD-then-local path's top two varying digits; when they are not
+	// whole bytes their counts come with the images' materialisation below
+	const int hy_hi = diff ? 63 - __builtin_clzll(diff) : -1;
+	const bool hy_h2 = hy_try && hy_hi >= 16 && (hy_hi - 7) % 8 != 0 && src0 != nullptr &&
+			   !shifts.empty() && lb;
+	DevBuf h2c(hy_h2 ? RS_MAXP * 256 * 4 * 2 + 64 : 64);
+	if (!h2c.p)
+		return -1;
 	if (src0 != nullptr && (shifts.empty() || hy_try || !positions || !lb || !andor || digit_hist == nullptr)) {
 		// paths that read the images themselves: materialise them
-		hipLaunchKernelGGL((k_img_xor<K>), dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st, src0, n, kx0, keys);
+		if (hy_h2) {
+			if (!hip_ok(hipMemsetAsync(h2c.p, 0, RS_MAXP * 256 * 4, st), "memset"))
+				return -1;
+			hipLaunchKernelGGL((k_img_xor_h2<K>), dim3(grid_for(n, 16384, 2048)), dim3(256), 0, st, src0, n, kx0,
+					   keys, hy_hi - 7, hy_hi - 15, h2c.as<uint32_t>());
+		} else {
+			hipLaunchKernelGGL((k_img_xor<K>), dim3(grid_for(n, 1024, 8192)), dim3(256), 0, st, src0, n, kx0, keys);
+		}
 		src0 = nullptr;
 	}
 	DevBuf hist(lb ? 64 : (size_t) 256 * nblocks * 4), offs(lb ? 64 : (size_t) 256 * nblocks * 4);
@@ -1492,11 +1545,14 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 				s12.n = 2;
 				s12.s[0] = s2;
 				s12.s[1] = s1;
-				uint32_t *c = hcnt.as<uint32_t>(), *g = c + RS_MAXP * 256;
+				uint32_t *c = hy_h2 ? h2c.as<uint32_t>() : hcnt.as<uint32_t>(), *g = c + RS_MAXP * 256;
 				uint32_t *hh = (uint32_t *) (h + 2);
-				if (!hip_ok(hipMemsetAsync(c, 0, RS_MAXP * 256 * 4, st), "memset"))
-					return -1;
-				hipLaunchKernelGGL((k_rs_dhist<K>), dim3(grid_for(n, 16384, 2048)), dim3(256), 0, st, keys, n, s12, c);
+				if (!hy_h2) {
+					if (!hip_ok(hipMemsetAsync(c, 0, RS_MAXP * 256 * 4, st), "memset"))
+						return -1;
+					hipLaunchKernelGGL((k_rs_dhist<K>), dim3(grid_for(n, 16384, 2048)), dim3(256), 0, st, keys, n,
+							   s12, c);
+				}
 				hipLaunchKernelGGL(k_rs_dscan, dim3(2), dim3(256), 0, st, (const uint32_t *) c, s12, g);
 				if (!hip_ok(hipMemcpyAsync(hh, c, (size_t) 4 * 256 * 4, hipMemcpyDeviceToHost, st), "memcpy") ||
 				    !sync())
