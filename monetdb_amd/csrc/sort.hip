@@ -1322,10 +1322,9 @@ radix_hybrid(K *k0, uint32_t *v0, K *k1, uint32_t *v1, BUN n, int s1, int s2, ui
 		return -1;
 	uint32_t *count = meta.as<uint32_t>(), *bfirst = count + 256, *bnt = count + 512;
 	FinalOut none{};
-	// pass A: by d1, positions as values
-	if (!hip_ok(hipMemsetAsync(status, 0, (size_t) 256 * nblocks * 8, st), "memset") ||
-	    !hip_ok(hipMemsetAsync(lbm, 0, 8, st), "memset") || !hip_ok(hipMemsetAsync(lbm + 8, 0, 32, st), "memset") ||
-	    !hip_ok(hipMemsetAsync(hist.p, 0, (size_t) 256 * tmax * 4, st), "memset") ||
+	// pass A: by d1, positions as values (status and lbm arrive zeroed:
+	// radix_sort clears them before it chooses this path)
+	if (!hip_ok(hipMemsetAsync(hist.p, 0, (size_t) 256 * tmax * 4, st), "memset") ||
 	    !hip_ok(hipMemsetAsync(ovf.p, 0, 4, st), "memset"))
 		return -1;
 	hipLaunchKernelGGL((k_rs_scatter<K, false, true, true, false>), dim3(nblocks), dim3(Tile<K>::THREADS), 0, st, k0,
@@ -1570,7 +1569,7 @@ radix_sort(K *keys, uint32_t *vals, K *keys_alt, uint32_t *vals_alt, BUN n, int 
 			}
 			const double est = (double) m1 * (double) m2 / (double) n;
 			const int cap = est <= 1024 ? 2048 : est <= 2048 ? 4096 : 0;
-			if (cap)
+			if (cap)      // status and lbm as cleared above, untouched since
 				return radix_hybrid<K>(keys, vals, keys_alt, vals_alt, n, s1, s2, diff, cnt1, gd1,
 						       status.as<uint64_t>(), lbm.as<uint32_t>(), *fo, cap, keys_out, vals_out);
 		}
